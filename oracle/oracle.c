@@ -1,0 +1,1064 @@
+/*
+ * oracle.c — CPU restatement of the ruserf hot path.  TEST INFRASTRUCTURE:
+ * see the header of oracle.h.  Every function cites the reference file:line
+ * it restates (paths relative to the al8n/ruserf repository root).
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off, so that a*b+c is never
+ * contracted into an FMA: Rust does not contract either).
+ */
+#define _GNU_SOURCE
+#include "oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------ */
+/* Philox4x32-10 (Salmon et al., SC'11; Random123 constants)               */
+/* ------------------------------------------------------------------------ */
+void orc_philox4x32(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+  uint32_t k0 = key[0], k1 = key[1];
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c1 ^ k0;
+    uint32_t n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+  }
+  out[0] = c0;
+  out[1] = c1;
+  out[2] = c2;
+  out[3] = c3;
+}
+
+/* purpose tags in ctr[1] bits 24..31 */
+#define PURPOSE_UNIT 1u
+#define PURPOSE_PEER 2u
+#define PURPOSE_VPROBE 3u
+#define PURPOSE_NBR 5u
+#define PURPOSE_POS 6u
+
+static inline void seed_key(uint64_t seed, uint32_t key[2]) {
+  key[0] = (uint32_t)seed;
+  key[1] = (uint32_t)(seed >> 32);
+}
+static inline uint32_t mulhi32(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Rust std semantics                                                       */
+/* ------------------------------------------------------------------------ */
+/* Duration::as_secs_f64 = secs as f64 + nanos as f64 / 1e9 */
+double orc_as_secs_f64(uint64_t ns) {
+  uint64_t secs = ns / 1000000000ull;
+  uint32_t nanos = (uint32_t)(ns % 1000000000ull);
+  return (double)secs + (double)nanos / 1e9;
+}
+/* `f64 as u64`: truncate toward zero, saturate, NaN -> 0 */
+static inline uint64_t sat_u64(double x) {
+  if (!(x > 0.0)) return 0;
+  if (x >= 18446744073709551616.0) return UINT64_MAX;
+  return (uint64_t)x;
+}
+/* f64::max / f64::min: return the non-NaN operand (== C99 fmax/fmin) */
+static inline double rmax(double a, double b) { return fmax(a, b); }
+static inline double rmin(double a, double b) { return fmin(a, b); }
+
+/* ------------------------------------------------------------------------ */
+/* Vivaldi: Coordinate / helpers  (core/src/coordinate.rs)                  */
+/* ------------------------------------------------------------------------ */
+/* CoordinateOptions::new  coordinate.rs:200-213 */
+void orc_coord_opts_default(orc_coord_opts* o) {
+  memset(o, 0, sizeof(*o));
+  o->dimensionality = 8;
+  o->vivaldi_error_max = 1.5;
+  o->vivaldi_ce = 0.25;
+  o->vivaldi_cc = 0.25;
+  o->adjustment_window_size = 20;
+  o->height_min = 10.0e-6;
+  o->latency_filter_size = 3;
+  o->gravity_rho = 150.0;
+}
+
+/* Coordinate::with_options  coordinate.rs:568-577 */
+void orc_coord_with_options(const orc_coord_opts* o, orc_coord* c) {
+  memset(c, 0, sizeof(*c));
+  c->dim = o->dimensionality;
+  c->error = o->vivaldi_error_max;
+  c->adjustment = 0.0;
+  c->height = o->height_min;
+}
+
+/* Coordinate::is_valid  coordinate.rs:581-586 */
+int orc_coord_is_valid(const orc_coord* c) {
+  for (uint32_t i = 0; i < c->dim; ++i)
+    if (!isfinite(c->portion[i])) return 0;
+  return isfinite(c->error) && isfinite(c->adjustment) && isfinite(c->height);
+}
+
+/* magnitude_in_place  coordinate.rs:779-781: fold(0.0, acc + x*x).sqrt() */
+double orc_magnitude(const double* v, uint32_t n) {
+  double acc = 0.0;
+  for (uint32_t i = 0; i < n; ++i) acc = acc + v[i] * v[i];
+  return sqrt(acc);
+}
+
+/* raw_distance_to  coordinate.rs:647-649 */
+double orc_coord_raw_distance(const orc_coord* a, const orc_coord* b) {
+  double acc = 0.0;
+  for (uint32_t i = 0; i < a->dim; ++i) {
+    double d = a->portion[i] - b->portion[i];
+    acc = acc + d * d;
+  }
+  return sqrt(acc) + a->height + b->height;
+}
+
+/* distance_to  coordinate.rs:630-644 -> Duration nanoseconds */
+uint64_t orc_coord_distance_ns(const orc_coord* a, const orc_coord* b) {
+  double dist = orc_coord_raw_distance(a, b);
+  double adjusted = dist + a->adjustment + b->adjustment;
+  double d = adjusted > 0.0 ? adjusted : dist;
+  return sat_u64(d * 1.0e9);
+}
+
+/* rand_f64  coordinate.rs:812-821 (thread_rng replaced by Philox) */
+double orc_rand_f64(orc_rng* r) {
+  for (;;) {
+    uint32_t ctr[4] = {r->draw++, (PURPOSE_UNIT << 24) | (r->call & 0xFFFFFFu), r->member, r->round};
+    uint32_t o[4];
+    orc_philox4x32(ctr, r->key, o);
+    uint64_t u = (((uint64_t)o[1] << 32) | o[0]) & 0x7FFFFFFFFFFFFFFFull;
+    double f = (double)u / 9223372036854775808.0;
+    if (f == 1.0) continue;
+    return f;
+  }
+}
+
+/* unit_vector_at  coordinate.rs:786-810 */
+double orc_unit_vector_at(const double* v1, const double* v2, uint32_t n, double* ret, orc_rng* r) {
+  for (uint32_t i = 0; i < n; ++i) ret[i] = v1[i] - v2[i];
+  double mag = orc_magnitude(ret, n);
+  if (mag > 1.0e-6) {
+    double rc = 1.0 / mag;
+    for (uint32_t i = 0; i < n; ++i) ret[i] *= rc;
+    return mag;
+  }
+  for (uint32_t i = 0; i < n; ++i) ret[i] = orc_rand_f64(r) - 0.5;
+  mag = orc_magnitude(ret, n);
+  if (mag > 1.0e-6) {
+    double rc = 1.0 / mag;
+    for (uint32_t i = 0; i < n; ++i) ret[i] *= rc;
+    return 0.0;
+  }
+  for (uint32_t i = 0; i < n; ++i) ret[i] = 0.0;
+  ret[0] = 1.0;
+  return 0.0;
+}
+
+/* apply_force_in_place  coordinate.rs:614-626 */
+void orc_apply_force_in_place(orc_coord* self, double height_min, double force,
+                              const orc_coord* other, orc_rng* r) {
+  double unit[ORC_MAX_DIM];
+  double mag = orc_unit_vector_at(self->portion, other->portion, self->dim, unit, r);
+  for (uint32_t i = 0; i < self->dim; ++i) unit[i] *= force;        /* mul_in_place */
+  for (uint32_t i = 0; i < self->dim; ++i) self->portion[i] += unit[i]; /* add_in_place */
+  if (mag > 1.0e-6) {
+    self->height = (self->height + other->height) * force / mag + self->height;
+    self->height = rmax(self->height, height_min);
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* CoordinateClient  coordinate.rs:252-500                                  */
+/* ------------------------------------------------------------------------ */
+/* latency_filter  coordinate.rs:292-307: push, trim front, median of sorted copy */
+static double latency_filter_core(orc_filter* f, uint32_t fsize, double rtt_seconds) {
+  f->s[f->len++] = rtt_seconds;
+  if (f->len > fsize) {
+    memmove(&f->s[0], &f->s[1], sizeof(double) * (f->len - 1));
+    f->len--;
+  }
+  double tmp[ORC_MAX_FILTER + 1];
+  uint32_t n = f->len;
+  memcpy(tmp, f->s, sizeof(double) * n);
+  for (uint32_t i = 1; i < n; ++i) { /* any correct sort: equal keys are equal values */
+    double v = tmp[i];
+    uint32_t j = i;
+    while (j > 0 && tmp[j - 1] > v) {
+      tmp[j] = tmp[j - 1];
+      --j;
+    }
+    tmp[j] = v;
+  }
+  return tmp[n / 2];
+}
+
+typedef struct {
+  orc_coord* coord;
+  const orc_coord* origin;
+  const orc_coord_opts* opts;
+  double* adj_samples;
+  uint32_t* adj_index;
+  uint64_t* resets;
+} client_view;
+
+/* update_vivaldi  coordinate.rs:311-330 */
+static void update_vivaldi(client_view* c, const orc_coord* other, double rtt_seconds, orc_rng* r) {
+  orc_coord* me = c->coord;
+  double dist = orc_as_secs_f64(orc_coord_distance_ns(me, other));
+  rtt_seconds = rmax(rtt_seconds, 1.0e-6);
+  double wrongness = fabs((dist - rtt_seconds) / rtt_seconds);
+  double total_error = rmax(me->error + other->error, 1.0e-6);
+  double weight = me->error / total_error;
+  me->error = rmin((c->opts->vivaldi_ce * weight * wrongness) +
+                       (me->error * (1.0 - c->opts->vivaldi_ce * weight)),
+                   c->opts->vivaldi_error_max);
+  double force = c->opts->vivaldi_cc * weight * (rtt_seconds - dist);
+  r->call = 0;
+  r->draw = 0;
+  orc_apply_force_in_place(me, c->opts->height_min, force, other, r);
+}
+
+/* update_adjustment  coordinate.rs:334-346 */
+static void update_adjustment(client_view* c, const orc_coord* other, double rtt_seconds) {
+  uint32_t w = c->opts->adjustment_window_size;
+  if (w == 0) return;
+  double dist = orc_coord_raw_distance(c->coord, other);
+  c->adj_samples[*c->adj_index] = rtt_seconds - dist;
+  *c->adj_index = (*c->adj_index + 1) % w;
+  double sum = 0.0;
+  for (uint32_t i = 0; i < w; ++i) sum = sum + c->adj_samples[i];
+  c->coord->adjustment = sum / (2.0 * (double)w);
+}
+
+/* update_gravity  coordinate.rs:283-289 */
+static void update_gravity(client_view* c, orc_rng* r) {
+  uint64_t secs = orc_coord_distance_ns(c->origin, c->coord) / 1000000000ull; /* as_secs */
+  double x = (double)secs / c->opts->gravity_rho;
+  double force = -1.0 * (x * x); /* f64::powf(x, 2.0) == x*x (correctly rounded) */
+  r->call = 1;
+  r->draw = 0;
+  orc_apply_force_in_place(c->coord, c->opts->height_min, force, c->origin, r);
+}
+
+/* check_coordinate  coordinate.rs:436-446 */
+static int check_coordinate(const orc_coord* me, const orc_coord* other) {
+  if (me->dim != other->dim) return ORC_ERR_DIM_MISMATCH;
+  if (!orc_coord_is_valid(other)) return ORC_ERR_INVALID_COORD;
+  return ORC_OK;
+}
+
+/* CoordinateClient::update  coordinate.rs:462-499 */
+static int client_update_core(client_view* c, orc_filter* filt, const orc_coord* other,
+                              uint64_t rtt_ns, orc_rng* r) {
+  int e = check_coordinate(c->coord, other);
+  if (e) return e;
+  if (rtt_ns > 10000000000ull) return ORC_ERR_INVALID_RTT; /* rtt > MAX_RTT (10 s) */
+  double rtt_seconds = latency_filter_core(filt, c->opts->latency_filter_size, orc_as_secs_f64(rtt_ns));
+  update_vivaldi(c, other, rtt_seconds, r);
+  update_adjustment(c, other, rtt_seconds);
+  update_gravity(c, r);
+  if (!orc_coord_is_valid(c->coord)) {
+    (*c->resets)++;
+    orc_coord_with_options(c->opts, c->coord);
+  }
+  return ORC_OK;
+}
+
+/* CoordinateClient::with_options  coordinate.rs:388-402 */
+int orc_client_init(orc_client* c, const orc_coord_opts* o, uint32_t n_slots) {
+  if (o->dimensionality == 0 || o->dimensionality > ORC_MAX_DIM) return -1;
+  if (o->adjustment_window_size > ORC_MAX_WINDOW) return -1;
+  if (o->latency_filter_size == 0 || o->latency_filter_size > ORC_MAX_FILTER) return -1;
+  memset(c, 0, sizeof(*c));
+  c->opts = *o;
+  orc_coord_with_options(o, &c->coord);
+  orc_coord_with_options(o, &c->origin);
+  c->n_slots = n_slots;
+  c->filters = (orc_filter*)calloc(n_slots ? n_slots : 1, sizeof(orc_filter));
+  return c->filters ? 0 : -1;
+}
+void orc_client_free(orc_client* c) {
+  free(c->filters);
+  c->filters = NULL;
+}
+/* set_coordinate  coordinate.rs:412-415 */
+int orc_client_set_coordinate(orc_client* c, const orc_coord* coord) {
+  int e = check_coordinate(&c->coord, coord);
+  if (e) return e;
+  c->coord = *coord;
+  return ORC_OK;
+}
+/* forget_node  coordinate.rs:455-457 */
+void orc_client_forget_node(orc_client* c, uint32_t slot) {
+  if (slot < c->n_slots) c->filters[slot].len = 0;
+}
+double orc_client_latency_filter(orc_client* c, uint32_t slot, double rtt_seconds) {
+  return latency_filter_core(&c->filters[slot], c->opts.latency_filter_size, rtt_seconds);
+}
+int orc_client_update(orc_client* c, uint32_t slot, const orc_coord* other, uint64_t rtt_ns,
+                      orc_rng* rng, orc_coord* out) {
+  if (slot >= c->n_slots) return -1;
+  client_view v = {&c->coord, &c->origin, &c->opts, c->adjustment_samples, &c->adjustment_index, &c->resets};
+  int e = client_update_core(&v, &c->filters[slot], other, rtt_ns, rng);
+  if (!e && out) *out = c->coord;
+  return e;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Vivaldi population rounds (synthetic network of BASELINE configs 1 & 5)  */
+/* ------------------------------------------------------------------------ */
+uint32_t orc_row_stride(uint32_t dim) { return ((dim + 3 + 3) / 4) * 4; }
+
+static inline void row_to_coord(const double* row, uint32_t dim, orc_coord* c) {
+  memset(c, 0, sizeof(*c));
+  c->dim = dim;
+  for (uint32_t i = 0; i < dim; ++i) c->portion[i] = row[i];
+  c->error = row[dim];
+  c->adjustment = row[dim + 1];
+  c->height = row[dim + 2];
+}
+static inline void coord_to_row(const orc_coord* c, double* row) {
+  for (uint32_t i = 0; i < c->dim; ++i) row[i] = c->portion[i];
+  row[c->dim] = c->error;
+  row[c->dim + 1] = c->adjustment;
+  row[c->dim + 2] = c->height;
+}
+
+void orc_gen_neighbors(uint64_t seed, uint32_t n, uint32_t peers, uint32_t* nbr) {
+  uint32_t key[2];
+  seed_key(seed, key);
+  for (uint32_t m = 0; m < n; ++m)
+    for (uint32_t q = 0; q < peers; ++q) {
+      uint32_t ctr[4] = {q, PURPOSE_NBR << 24, m, 0}, o[4];
+      orc_philox4x32(ctr, key, o);
+      uint32_t p = mulhi32(o[0], n - 1);
+      if (p >= m) p++;
+      nbr[(size_t)m * peers + q] = p;
+    }
+}
+
+/* ground-truth position of member m: x,y ~ U[0,0.05) s, h ~ U[0,0.002) s */
+void orc_true_position(uint64_t seed, uint32_t m, double* x, double* y, double* h) {
+  uint32_t key[2];
+  seed_key(seed, key);
+  uint32_t ctr[4] = {0, PURPOSE_POS << 24, m, 0}, o[4];
+  orc_philox4x32(ctr, key, o);
+  const double s32 = 2.3283064365386963e-10; /* 2^-32 */
+  *x = ((double)o[0] * s32) * 0.05;
+  *y = ((double)o[1] * s32) * 0.05;
+  *h = ((double)o[2] * s32) * 0.002;
+}
+
+void orc_vivaldi_probe(uint64_t seed, uint32_t n, uint32_t peers, const uint32_t* nbr, uint32_t m,
+                       uint32_t round, uint32_t* slot_out, uint64_t* rtt_out) {
+  (void)n;
+  uint32_t key[2];
+  seed_key(seed, key);
+  uint32_t ctr[4] = {0, PURPOSE_VPROBE << 24, m, round}, o[4];
+  orc_philox4x32(ctr, key, o);
+  uint32_t q = mulhi32(o[0], peers);
+  uint32_t p = nbr[(size_t)m * peers + q];
+  double xm, ym, hm, xp, yp, hp;
+  orc_true_position(seed, m, &xm, &ym, &hm);
+  orc_true_position(seed, p, &xp, &yp, &hp);
+  double dx = xm - xp, dy = ym - yp;
+  double d = sqrt(dx * dx + dy * dy) + hm + hp;
+  double jit = 1.0 + 0.1 * ((double)o[1] * 2.3283064365386963e-10);
+  *slot_out = q;
+  *rtt_out = sat_u64((d * jit) * 1.0e9);
+}
+
+int orc_vivaldi_pop_init(orc_vivaldi_pop* p, uint32_t n, uint32_t peers, const orc_coord_opts* o,
+                         uint64_t seed) {
+  memset(p, 0, sizeof(*p));
+  if (n < 2 || peers == 0 || o->dimensionality == 0 || o->dimensionality > ORC_MAX_DIM) return -1;
+  if (o->adjustment_window_size > ORC_MAX_WINDOW) return -1;
+  if (o->latency_filter_size == 0 || o->latency_filter_size > ORC_MAX_FILTER) return -1;
+  p->n = n;
+  p->peers = peers;
+  p->opts = *o;
+  p->seed = seed;
+  p->row_stride = orc_row_stride(o->dimensionality);
+  size_t rows = (size_t)n * p->row_stride;
+  p->rows_cur = (double*)calloc(rows, sizeof(double));
+  p->rows_nxt = (double*)calloc(rows, sizeof(double));
+  p->adj = (double*)calloc((size_t)n * (o->adjustment_window_size ? o->adjustment_window_size : 1), sizeof(double));
+  p->adj_idx = (uint32_t*)calloc(n, sizeof(uint32_t));
+  p->filt = (double*)calloc((size_t)n * peers * o->latency_filter_size, sizeof(double));
+  p->filt_len = (uint32_t*)calloc((size_t)n * peers, sizeof(uint32_t));
+  p->nbr = (uint32_t*)calloc((size_t)n * peers, sizeof(uint32_t));
+  if (!p->rows_cur || !p->rows_nxt || !p->adj || !p->adj_idx || !p->filt || !p->filt_len || !p->nbr) {
+    orc_vivaldi_pop_free(p);
+    return -1;
+  }
+  orc_coord c;
+  orc_coord_with_options(o, &c);
+  for (uint32_t m = 0; m < n; ++m) coord_to_row(&c, p->rows_cur + (size_t)m * p->row_stride);
+  orc_gen_neighbors(seed, n, peers, p->nbr);
+  return 0;
+}
+
+void orc_vivaldi_pop_free(orc_vivaldi_pop* p) {
+  free(p->rows_cur);
+  free(p->rows_nxt);
+  free(p->adj);
+  free(p->adj_idx);
+  free(p->filt);
+  free(p->filt_len);
+  free(p->nbr);
+  memset(p, 0, sizeof(*p));
+}
+
+typedef struct {
+  orc_vivaldi_pop* p;
+  uint32_t round, lo, hi;
+  uint64_t resets;
+} viv_job;
+
+static void viv_member(orc_vivaldi_pop* p, uint32_t m, uint32_t round, uint64_t* resets) {
+  const uint32_t dim = p->opts.dimensionality, F = p->opts.latency_filter_size;
+  const uint32_t W = p->opts.adjustment_window_size;
+  uint32_t slot;
+  uint64_t rtt;
+  orc_vivaldi_probe(p->seed, p->n, p->peers, p->nbr, m, round, &slot, &rtt);
+  uint32_t peer = p->nbr[(size_t)m * p->peers + slot];
+  orc_coord me, other, origin;
+  row_to_coord(p->rows_cur + (size_t)m * p->row_stride, dim, &me);
+  row_to_coord(p->rows_cur + (size_t)peer * p->row_stride, dim, &other);
+  orc_coord_with_options(&p->opts, &origin);
+  /* filter (Vec semantics) over the flat [n][peers][F] store */
+  orc_filter f;
+  size_t fi = (size_t)m * p->peers + slot;
+  f.len = p->filt_len[fi];
+  memcpy(f.s, p->filt + fi * F, sizeof(double) * F);
+  double* adj = W ? p->adj + (size_t)m * W : NULL;
+  client_view v = {&me, &origin, &p->opts, adj, &p->adj_idx[m], resets};
+  orc_rng r;
+  seed_key(p->seed, r.key);
+  r.member = m;
+  r.round = round;
+  r.call = 0;
+  r.draw = 0;
+  client_update_core(&v, &f, &other, rtt, &r);
+  memcpy(p->filt + fi * F, f.s, sizeof(double) * F);
+  p->filt_len[fi] = f.len;
+  double* out = p->rows_nxt + (size_t)m * p->row_stride;
+  memset(out, 0, sizeof(double) * p->row_stride);
+  coord_to_row(&me, out);
+}
+
+static void* viv_worker(void* arg) {
+  viv_job* j = (viv_job*)arg;
+  for (uint32_t m = j->lo; m < j->hi; ++m) viv_member(j->p, m, j->round, &j->resets);
+  return NULL;
+}
+
+int orc_vivaldi_pop_rounds(orc_vivaldi_pop* p, uint32_t round0, uint32_t rounds, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  viv_job jobs[256];
+  for (uint32_t t = round0; t < round0 + rounds; ++t) {
+    uint32_t per = (p->n + nthreads - 1) / nthreads;
+    int launched = 0;
+    for (int i = 0; i < nthreads; ++i) {
+      uint32_t lo = (uint32_t)i * per, hi = lo + per;
+      if (hi > p->n) hi = p->n;
+      jobs[i].p = p;
+      jobs[i].round = t;
+      jobs[i].lo = lo < p->n ? lo : p->n;
+      jobs[i].hi = hi;
+      jobs[i].resets = 0;
+      if (nthreads == 1) {
+        viv_worker(&jobs[i]);
+      } else {
+        pthread_create(&th[i], NULL, viv_worker, &jobs[i]);
+        launched++;
+      }
+    }
+    for (int i = 0; i < launched; ++i) pthread_join(th[i], NULL);
+    for (int i = 0; i < nthreads; ++i) p->resets += jobs[i].resets;
+    double* tmp = p->rows_cur;
+    p->rows_cur = p->rows_nxt;
+    p->rows_nxt = tmp;
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Gossip world: member-state merge + dissemination                         */
+/* ------------------------------------------------------------------------ */
+#define EMPTY_RUMOR 0xFFFFFFFFu
+
+/* memberlist retransmitLimit: mult * ceil(log10(n+1))  (un-vendored; restated) */
+uint32_t orc_retransmit_limit(uint32_t mult, uint64_t n) {
+  uint64_t x = n + 1, p = 1;
+  uint32_t d = 0;
+  while (p < x) {
+    p *= 10;
+    d++;
+  }
+  return mult * d;
+}
+
+static uint32_t varint_len(uint64_t v) {
+  uint32_t n = 1;
+  while (v >= 0x80) {
+    v >>= 7;
+    n++;
+  }
+  return n;
+}
+
+/* Encoded message length model (types/src/{join,leave,user_event,query}.rs
+ * encoded_len: u32 length prefix + varint ltime + fields; +1 type byte).  A
+ * node id is modelled as a 12-byte encoded SmolStr. */
+uint32_t orc_msg_len(uint8_t type, uint64_t ltime, uint32_t name_len, uint32_t payload_len) {
+  uint32_t base = 1 + 4 + varint_len(ltime);
+  switch (type) {
+    case ORC_MSG_JOIN: return base + 12;
+    case ORC_MSG_LEAVE: return base + 12 + 1;
+    case ORC_MSG_USER_EVENT: return base + (4 + name_len) + (4 + payload_len) + 1;
+    case ORC_MSG_QUERY: return base + 4 + 28 + 4 + 1 + 8 + (4 + name_len) + (4 + payload_len);
+    default: return base;
+  }
+}
+
+uint64_t orc_digest_mix(uint64_t d, uint64_t x) {
+  d ^= x;
+  d *= 0x100000001B3ull;
+  d ^= d >> 29;
+  return d;
+}
+
+#define DIG_USER 0x1000000000000000ull
+#define DIG_QUERY 0x2000000000000000ull
+#define DIG_MEMBER 0x3000000000000000ull
+enum { EV_JOIN = 0, EV_LEAVE = 1, EV_FAILED = 2 };
+
+static inline void digest_member_event(orc_world* w, uint32_t m, uint32_t ev, uint32_t subj) {
+  w->digest[m] = orc_digest_mix(w->digest[m], DIG_MEMBER | ((uint64_t)ev << 32) | subj);
+}
+
+int orc_world_init(orc_world* w, const orc_world_cfg* c) {
+  memset(w, 0, sizeof(*w));
+  if (c->n < 2 || c->s == 0 || c->s > c->n || c->qcap == 0 || c->qcap > 64 || c->ebuf == 0 ||
+      c->qbuf == 0 || c->slot_k == 0 || c->fanout == 0 || c->fanout >= c->n || c->max_refute == 0)
+    return -1;
+  w->n = c->n;
+  w->s = c->s;
+  w->qcap = c->qcap;
+  w->ebuf = c->ebuf;
+  w->qbuf = c->qbuf;
+  w->slot_k = c->slot_k;
+  w->fanout = c->fanout;
+  w->limit = c->limit;
+  w->overhead = c->overhead;
+  w->tx_limit = orc_retransmit_limit(c->retransmit_mult, c->n);
+  w->max_refute = c->max_refute;
+  w->seed = c->seed;
+  size_t n = c->n, s = c->s;
+#define A(p, cnt) (w->p = calloc((cnt), sizeof(*w->p)), w->p == NULL)
+  if (A(clock, n) || A(eclock, n) || A(qclock, n) || A(emin, n) || A(qmin, n) || A(digest, n) ||
+      A(alive, n) || A(serf_state, n) || A(err, n) || A(subj_member, s) || A(member_subj, n) ||
+      A(refute_cnt, s) || A(refute_ltime, s * c->max_refute) || A(v_ltime, n * s) ||
+      A(v_status, n * s) || A(v_kind, n * s) || A(q_rumor, n * 3 * c->qcap) ||
+      A(q_seq, n * 3 * c->qcap) || A(q_tx, n * 3 * c->qcap) || A(q_len, n * 3 * c->qcap) ||
+      A(q_next_seq, n * 3) || A(eb_ltime, n * c->ebuf) || A(eb_cnt, n * c->ebuf) ||
+      A(eb_keys, n * c->ebuf * c->slot_k) || A(qb_ltime, n * c->qbuf) || A(qb_cnt, n * c->qbuf) ||
+      A(qb_ids, n * c->qbuf * c->slot_k) || A(rumors, c->cap_rumors ? c->cap_rumors : 1)) {
+    orc_world_free(w);
+    return -1;
+  }
+#undef A
+  w->cap_rumors = c->cap_rumors;
+  for (size_t m = 0; m < n; ++m) {
+    /* Serf::new: every clock incremented once (base.rs:195-199) */
+    w->clock[m] = 1;
+    w->eclock[m] = 1;
+    w->qclock[m] = 1;
+    w->alive[m] = 1;
+    w->serf_state[m] = ORC_SERF_ALIVE;
+    w->member_subj[m] = -1;
+  }
+  for (size_t i = 0; i < n * 3 * c->qcap; ++i) w->q_rumor[i] = EMPTY_RUMOR;
+  return 0;
+}
+
+void orc_world_free(orc_world* w) {
+  void* ptrs[] = {w->clock, w->eclock, w->qclock, w->emin, w->qmin, w->digest, w->alive,
+                  w->serf_state, w->err, w->subj_member, w->member_subj, w->refute_cnt,
+                  w->refute_ltime, w->v_ltime, w->v_status, w->v_kind, w->q_rumor, w->q_seq,
+                  w->q_tx, w->q_len, w->q_next_seq, w->eb_ltime, w->eb_cnt, w->eb_keys,
+                  w->qb_ltime, w->qb_cnt, w->qb_ids, w->rumors};
+  for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) free(ptrs[i]);
+  memset(w, 0, sizeof(*w));
+}
+
+/* upsert_intent  base.rs:1797-1828 (recent_intents: one entry per unknown node) */
+int orc_upsert_intent(orc_world* w, uint32_t m, uint32_t subj, uint8_t kind, uint64_t ltime) {
+  size_t e = (size_t)m * w->s + subj;
+  if (w->v_kind[e] == ORC_K_UNKNOWN) {
+    w->v_kind[e] = kind;
+    w->v_ltime[e] = ltime;
+    return 1;
+  }
+  if (ltime > w->v_ltime[e]) {
+    w->v_kind[e] = kind;
+    w->v_ltime[e] = ltime;
+    return 1;
+  }
+  return 0;
+}
+
+/* handle_node_join_intent  base.rs:1302-1337 */
+int orc_handle_join_intent(orc_world* w, uint32_t m, uint32_t subj, uint64_t ltime) {
+  orc_clock_witness(&w->clock[m], ltime);
+  size_t e = (size_t)m * w->s + subj;
+  if (w->v_kind[e] == ORC_K_KNOWN) {
+    if (ltime <= w->v_ltime[e]) return 0;
+    w->v_ltime[e] = ltime;
+    if (w->v_status[e] == ORC_ST_LEAVING) w->v_status[e] = ORC_ST_ALIVE;
+    return ORC_F_REBROADCAST;
+  }
+  return orc_upsert_intent(w, m, subj, ORC_K_INTENT_JOIN, ltime) ? ORC_F_REBROADCAST : 0;
+}
+
+/* handle_node_leave_intent  base.rs:1409-1528 */
+int orc_handle_leave_intent(orc_world* w, uint32_t m, uint32_t subj, uint64_t ltime, int prune,
+                            uint64_t* refute_ltime) {
+  uint8_t state = w->serf_state[m]; /* base.rs:1410 */
+  orc_clock_witness(&w->clock[m], ltime);
+  size_t e = (size_t)m * w->s + subj;
+  if (w->v_kind[e] != ORC_K_KNOWN)
+    return orc_upsert_intent(w, m, subj, ORC_K_INTENT_LEAVE, ltime) ? ORC_F_REBROADCAST : 0;
+  if (ltime <= w->v_ltime[e]) return 0;
+  if (w->member_subj[m] == (int32_t)subj && state == ORC_SERF_ALIVE) { /* refute (1437-1447) */
+    if (refute_ltime) *refute_ltime = w->clock[m];
+    return ORC_F_REFUTE;
+  }
+  w->v_ltime[e] = ltime; /* 1464 */
+  int pf = prune ? ORC_F_PRUNE : 0;
+  switch (w->v_status[e]) {
+    case ORC_ST_NONE: return 0;
+    case ORC_ST_ALIVE: w->v_status[e] = ORC_ST_LEAVING; return ORC_F_REBROADCAST | pf;
+    case ORC_ST_LEAVING:
+    case ORC_ST_LEFT: return ORC_F_REBROADCAST | pf;
+    case ORC_ST_FAILED:
+      w->v_status[e] = ORC_ST_LEFT;
+      digest_member_event(w, m, EV_LEAVE, subj);
+      return ORC_F_REBROADCAST | ORC_F_MEMBER_EVENT | pf;
+    default: return 0;
+  }
+}
+
+/* handle_node_join (memberlist NotifyJoin)  base.rs:1167-1298 */
+int orc_handle_node_join(orc_world* w, uint32_t m, uint32_t subj) {
+  size_t e = (size_t)m * w->s + subj;
+  if (w->v_kind[e] == ORC_K_KNOWN) {
+    w->v_status[e] = ORC_ST_ALIVE; /* status_time kept (1225) */
+  } else {
+    uint8_t status = ORC_ST_ALIVE;
+    uint64_t st = 0;
+    if (w->v_kind[e] == ORC_K_INTENT_JOIN) st = w->v_ltime[e];
+    if (w->v_kind[e] == ORC_K_INTENT_LEAVE) {
+      st = w->v_ltime[e];
+      status = ORC_ST_LEAVING;
+    }
+    w->v_kind[e] = ORC_K_KNOWN;
+    w->v_status[e] = status;
+    w->v_ltime[e] = st;
+  }
+  digest_member_event(w, m, EV_JOIN, subj);
+  return ORC_F_MEMBER_EVENT;
+}
+
+/* handle_node_leave (memberlist NotifyLeave)  base.rs:1339-1407 */
+int orc_handle_node_leave(orc_world* w, uint32_t m, uint32_t subj) {
+  size_t e = (size_t)m * w->s + subj;
+  if (w->v_kind[e] != ORC_K_KNOWN) return 0;
+  if (w->v_status[e] == ORC_ST_LEAVING) {
+    w->v_status[e] = ORC_ST_LEFT;
+    digest_member_event(w, m, EV_LEAVE, subj);
+  } else if (w->v_status[e] == ORC_ST_ALIVE) {
+    w->v_status[e] = ORC_ST_FAILED;
+    digest_member_event(w, m, EV_FAILED, subj);
+  } else {
+    return 0;
+  }
+  return ORC_F_MEMBER_EVENT;
+}
+
+/* handle_user_event  base.rs:770-837 */
+int orc_handle_user_event(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key) {
+  orc_clock_witness(&w->eclock[m], ltime);
+  if (ltime < w->emin[m]) return 0;
+  uint64_t B = w->ebuf, cur = w->eclock[m];
+  if (cur > B && ltime < cur - B) return 0;
+  size_t slot = (size_t)m * w->ebuf + (size_t)(ltime % B);
+  uint64_t* keys = w->eb_keys + slot * w->slot_k;
+  if (w->eb_cnt[slot]) {
+    for (uint32_t i = 0; i < w->eb_cnt[slot]; ++i)
+      if (keys[i] == key) return 0;
+    if (w->eb_cnt[slot] < w->slot_k) keys[w->eb_cnt[slot]++] = key;
+    else w->err[m] |= ORC_E_EVSLOT_FULL;
+  } else {
+    w->eb_ltime[slot] = ltime;
+    keys[0] = key;
+    w->eb_cnt[slot] = 1;
+  }
+  w->digest[m] = orc_digest_mix(orc_digest_mix(w->digest[m], DIG_USER ^ key), ltime);
+  return ORC_F_REBROADCAST | ORC_F_DELIVER;
+}
+
+/* handle_query  base.rs:981-1119 (dedup + rebroadcast decision; filters pass) */
+int orc_handle_query(orc_world* w, uint32_t m, uint64_t ltime, uint32_t id, int no_broadcast) {
+  orc_clock_witness(&w->qclock[m], ltime);
+  if (ltime < w->qmin[m]) return 0;
+  uint64_t cur = w->qclock[m], B = w->qbuf;
+  if (cur > B && B < cur - B) return 0; /* reference quirk base.rs:999 */
+  size_t slot = (size_t)m * w->qbuf + (size_t)(ltime % B);
+  uint32_t* ids = w->qb_ids + slot * w->slot_k;
+  if (w->qb_cnt[slot]) {
+    if (w->qb_ltime[slot] == ltime)
+      for (uint32_t i = 0; i < w->qb_cnt[slot]; ++i)
+        if (ids[i] == id) return 0;
+    if (w->qb_cnt[slot] < w->slot_k) ids[w->qb_cnt[slot]++] = id;
+    else w->err[m] |= ORC_E_QSLOT_FULL;
+  } else {
+    w->qb_ltime[slot] = ltime;
+    ids[0] = id;
+    w->qb_cnt[slot] = 1;
+  }
+  w->digest[m] = orc_digest_mix(orc_digest_mix(w->digest[m], DIG_QUERY ^ id), ltime);
+  return (no_broadcast ? 0 : ORC_F_REBROADCAST) | ORC_F_DELIVER;
+}
+
+/* ---- TransmitLimitedQueue model (memberlist; un-vendored, parity unpinned) */
+static inline uint64_t tlq_key(uint16_t tx, uint16_t len, uint32_t seq) {
+  return ((uint64_t)tx << 48) | ((uint64_t)(0xFFFFu - len) << 32) | (uint64_t)(0xFFFFFFFFu - seq);
+}
+
+void orc_queue_insert(orc_world* w, uint32_t m, uint32_t q, uint32_t rumor) {
+  size_t base = ((size_t)m * 3 + q) * w->qcap;
+  uint32_t seq = w->q_next_seq[(size_t)m * 3 + q]++;
+  uint16_t len = w->rumors[rumor].msg_len;
+  uint32_t slot = EMPTY_RUMOR;
+  for (uint32_t i = 0; i < w->qcap; ++i)
+    if (w->q_rumor[base + i] == EMPTY_RUMOR) {
+      slot = i;
+      break;
+    }
+  if (slot == EMPTY_RUMOR) { /* full: prune the last item in send order */
+    uint64_t kmax = 0;
+    for (uint32_t i = 0; i < w->qcap; ++i) {
+      uint64_t k = tlq_key(w->q_tx[base + i], w->q_len[base + i], w->q_seq[base + i]);
+      if (slot == EMPTY_RUMOR || k > kmax) {
+        kmax = k;
+        slot = i;
+      }
+    }
+    if (tlq_key(0, len, seq) > kmax) return; /* the new item itself is pruned */
+  }
+  w->q_rumor[base + slot] = rumor;
+  w->q_seq[base + slot] = seq;
+  w->q_tx[base + slot] = 0;
+  w->q_len[base + slot] = len;
+}
+
+/* get_broadcasts: lowest transmits first, then the largest message that fits,
+ * then the newest; picked items are re-inserted with transmits+1 or retired
+ * at the retransmit limit (memberlist queue.go GetBroadcasts, restated). */
+uint32_t orc_queue_get_broadcasts(orc_world* w, uint32_t m, uint32_t q, uint32_t limit,
+                                  uint32_t* out, uint32_t max_out, uint32_t* bytes_used) {
+  size_t base = ((size_t)m * 3 + q) * w->qcap;
+  uint64_t picked = 0;
+  int64_t used = 0;
+  uint32_t cnt = 0;
+  for (;;) {
+    int64_t free_b = (int64_t)limit - used - (int64_t)w->overhead;
+    if (free_b <= 0) break;
+    uint32_t best = EMPTY_RUMOR;
+    uint64_t kbest = UINT64_MAX;
+    for (uint32_t i = 0; i < w->qcap; ++i) {
+      if (w->q_rumor[base + i] == EMPTY_RUMOR || (picked >> i & 1)) continue;
+      if ((int64_t)w->q_len[base + i] > free_b) continue;
+      uint64_t k = tlq_key(w->q_tx[base + i], w->q_len[base + i], w->q_seq[base + i]);
+      if (k < kbest) {
+        kbest = k;
+        best = i;
+      }
+    }
+    if (best == EMPTY_RUMOR) break;
+    if (cnt < max_out) out[cnt] = w->q_rumor[base + best];
+    cnt++;
+    used += (int64_t)w->overhead + w->q_len[base + best];
+    picked |= 1ull << best;
+  }
+  for (uint32_t i = 0; i < w->qcap; ++i) {
+    if (!(picked >> i & 1)) continue;
+    if ((uint32_t)w->q_tx[base + i] + 1 >= w->tx_limit) w->q_rumor[base + i] = EMPTY_RUMOR;
+    else w->q_tx[base + i]++;
+  }
+  *bytes_used = (uint32_t)used;
+  return cnt;
+}
+
+/* kRandomNodes model: k distinct live peers != m, Philox-drawn (memberlist util.go; unpinned) */
+uint32_t orc_pick_peers(uint64_t seed, uint32_t n, const uint8_t* alive, uint32_t m, uint32_t round,
+                        uint32_t k, uint32_t* out) {
+  uint32_t key[2];
+  seed_key(seed, key);
+  uint32_t cnt = 0;
+  for (uint32_t a = 0; a < 64 * k && cnt < k; ++a) {
+    uint32_t ctr[4] = {a, PURPOSE_PEER << 24, m, round}, o[4];
+    orc_philox4x32(ctr, key, o);
+    uint32_t p = mulhi32(o[0], n - 1);
+    if (p >= m) p++;
+    if (!alive[p]) continue;
+    int dup = 0;
+    for (uint32_t j = 0; j < cnt; ++j) dup |= (out[j] == p);
+    if (dup) continue;
+    out[cnt++] = p;
+  }
+  return cnt;
+}
+
+static uint32_t queue_of(uint8_t type) {
+  return type == ORC_MSG_USER_EVENT ? ORC_Q_EVENT : (type == ORC_MSG_QUERY ? ORC_Q_QUERY : ORC_Q_INTENT);
+}
+
+static uint32_t new_rumor(orc_world* w, uint32_t id, uint8_t type, uint8_t flags, uint32_t subject,
+                          uint64_t ltime, uint64_t key, uint32_t name_len, uint32_t payload_len) {
+  orc_rumor* r = &w->rumors[id];
+  r->type = type;
+  r->flags = flags;
+  r->subject = subject;
+  r->ltime = ltime;
+  r->key = key;
+  r->msg_len = (uint16_t)orc_msg_len(type, ltime, name_len, payload_len);
+  return id;
+}
+
+static void push_refute(orc_world* w, uint32_t m, uint64_t ltime) {
+  int32_t s = w->member_subj[m];
+  if (s < 0) return;
+  if (w->refute_cnt[s] < w->max_refute) w->refute_ltime[(size_t)s * w->max_refute + w->refute_cnt[s]++] = ltime;
+  else w->err[m] |= ORC_E_REFUTE_FULL;
+}
+
+/* apply one received rumor at receiver r  (notify_message, delegate.rs:157-305) */
+static void merge_one(orc_world* w, uint32_t r, uint32_t rid) {
+  const orc_rumor* ru = &w->rumors[rid];
+  int f = 0;
+  uint64_t refute = 0;
+  switch (ru->type) {
+    case ORC_MSG_JOIN: f = orc_handle_join_intent(w, r, ru->subject, ru->ltime); break;
+    case ORC_MSG_LEAVE:
+      f = orc_handle_leave_intent(w, r, ru->subject, ru->ltime, ru->flags & 1, &refute);
+      break;
+    case ORC_MSG_USER_EVENT: f = orc_handle_user_event(w, r, ru->ltime, ru->key); break;
+    case ORC_MSG_QUERY: f = orc_handle_query(w, r, ru->ltime, (uint32_t)ru->key, ru->flags & 1); break;
+    default: return;
+  }
+  w->merges++;
+  if (f & ORC_F_REFUTE) push_refute(w, r, refute);
+  if (f & ORC_F_REBROADCAST) orc_queue_insert(w, r, queue_of(ru->type), rid);
+}
+
+/* broadcast_join  base.rs:396-412 */
+static void broadcast_join(orc_world* w, uint32_t m, uint64_t ltime, uint32_t rid) {
+  int32_t subj = w->member_subj[m];
+  orc_clock_witness(&w->clock[m], ltime);
+  orc_handle_join_intent(w, m, (uint32_t)subj, ltime);
+  new_rumor(w, rid, ORC_MSG_JOIN, 0, (uint32_t)subj, ltime, 0, 0, 0);
+  orc_queue_insert(w, m, ORC_Q_INTENT, rid);
+}
+
+int orc_world_round(orc_world* w, uint32_t round, const orc_ml_event* ml, uint32_t n_ml,
+                    const orc_action* acts, uint32_t n_acts) {
+  const uint32_t n = w->n, k = w->fanout;
+  /* rumor ids of this round: [refutes: s*max_refute][actions: n_acts] */
+  uint32_t base = w->n_rumors;
+  uint32_t need = w->s * w->max_refute + n_acts;
+  if (base + need > w->cap_rumors) return -1;
+  for (uint32_t i = 0; i < need; ++i) w->rumors[base + i].type = 0xFF;
+  w->n_rumors += need;
+
+  /* 1. memberlist-detected transitions (M6) at every live member but the subject */
+  for (uint32_t e = 0; e < n_ml; ++e) {
+    uint32_t subj = ml[e].subject, sm = w->subj_member[subj];
+    if (ml[e].set_alive == 1) {
+      w->alive[sm] = 1;
+      w->serf_state[sm] = ORC_SERF_ALIVE;
+    }
+    for (uint32_t m = 0; m < n; ++m) {
+      if (!w->alive[m] || m == sm) continue;
+      if (ml[e].kind == ORC_ML_JOIN) orc_handle_node_join(w, m, subj);
+      else orc_handle_node_leave(w, m, subj);
+    }
+    if (ml[e].set_alive == 0) w->alive[sm] = 0;
+  }
+
+  /* 2. refutations scheduled by the previous round's merges (spawn_detach) */
+  for (uint32_t s = 0; s < w->s; ++s) {
+    uint32_t m = w->subj_member[s];
+    for (uint32_t i = 0; i < w->refute_cnt[s]; ++i)
+      if (w->alive[m]) broadcast_join(w, m, w->refute_ltime[(size_t)s * w->max_refute + i],
+                                      base + s * w->max_refute + i);
+    w->refute_cnt[s] = 0;
+  }
+
+  /* 3. originations (api.rs / base.rs entry points) */
+  uint32_t abase = base + w->s * w->max_refute;
+  for (uint32_t a = 0; a < n_acts; ++a) {
+    const orc_action* x = &acts[a];
+    uint32_t m = x->member, rid = abase + a;
+    if (!w->alive[m]) continue;
+    switch (x->act) {
+      case ORC_ACT_JOIN_SELF: /* Serf::join -> broadcast_join(clock.time()) */
+        w->serf_state[m] = ORC_SERF_ALIVE;
+        broadcast_join(w, m, w->clock[m], rid);
+        break;
+      case ORC_ACT_LEAVE_SELF: { /* Serf::leave  api.rs:473-503 */
+        w->serf_state[m] = ORC_SERF_LEAVING;
+        uint64_t lt = w->clock[m];
+        orc_clock_increment(&w->clock[m]);
+        uint32_t subj = (uint32_t)w->member_subj[m];
+        orc_handle_leave_intent(w, m, subj, lt, 0, NULL);
+        new_rumor(w, rid, ORC_MSG_LEAVE, 0, subj, lt, 0, 0, 0);
+        orc_queue_insert(w, m, ORC_Q_INTENT, rid);
+        break;
+      }
+      case ORC_ACT_FORCE_LEAVE: { /* force_leave  base.rs:474-500 */
+        uint64_t lt = w->clock[m], ref = 0;
+        int f = orc_handle_leave_intent(w, m, x->subject, lt, x->flags & 1, &ref);
+        if (f & ORC_F_REFUTE) push_refute(w, m, ref);
+        new_rumor(w, rid, ORC_MSG_LEAVE, (uint8_t)(x->flags & 1), x->subject, lt, 0, 0, 0);
+        orc_queue_insert(w, m, ORC_Q_INTENT, rid);
+        break;
+      }
+      case ORC_ACT_USER_EVENT: { /* Serf::user_event  api.rs:247-315 */
+        uint64_t lt = w->eclock[m];
+        orc_clock_increment(&w->eclock[m]);
+        orc_handle_user_event(w, m, lt, x->key);
+        new_rumor(w, rid, ORC_MSG_USER_EVENT, 0, 0, lt, x->key, x->name_len, x->payload_len);
+        orc_queue_insert(w, m, ORC_Q_EVENT, rid);
+        break;
+      }
+      case ORC_ACT_QUERY: { /* query_in  base.rs:869-953 */
+        uint64_t lt = w->qclock[m];
+        orc_handle_query(w, m, lt, (uint32_t)x->key, x->flags & 1);
+        new_rumor(w, rid, ORC_MSG_QUERY, (uint8_t)(x->flags & 1), 0, lt, (uint32_t)x->key,
+                  x->name_len, x->payload_len);
+        orc_queue_insert(w, m, ORC_Q_QUERY, rid);
+        break;
+      }
+      default: break;
+    }
+  }
+
+  /* 4. emission: each live sender, k peers, broadcast_messages (delegate.rs:307-374) */
+  uint32_t cap_t = 3 * w->qcap;
+  size_t cap = (size_t)n * k * cap_t;
+  uint32_t* rec_recv = (uint32_t*)malloc(cap * sizeof(uint32_t));
+  uint32_t* rec_rumor = (uint32_t*)malloc(cap * sizeof(uint32_t));
+  if (!rec_recv || !rec_rumor) {
+    free(rec_recv);
+    free(rec_rumor);
+    return -1;
+  }
+  size_t nrec = 0;
+  uint32_t peers[64], buf[3 * 64];
+  for (uint32_t m = 0; m < n; ++m) {
+    if (!w->alive[m]) continue;
+    uint32_t np = orc_pick_peers(w->seed, n, w->alive, m, round, k, peers);
+    for (uint32_t j = 0; j < np; ++j) {
+      uint32_t used = 0, got = 0, b;
+      for (uint32_t q = 0; q < 3; ++q) {
+        got += orc_queue_get_broadcasts(w, m, q, w->limit - used, buf + got, cap_t - got, &b);
+        used += b;
+      }
+      for (uint32_t i = 0; i < got; ++i) {
+        rec_recv[nrec] = peers[j];
+        rec_rumor[nrec] = buf[i];
+        nrec++;
+      }
+      w->sends += got;
+    }
+  }
+
+  /* 5. merge in canonical (sender, position) order per receiver: stable
+   *    counting sort by receiver keeps the sender-major emission order. */
+  uint32_t* off = (uint32_t*)calloc((size_t)n + 1, sizeof(uint32_t));
+  uint32_t* order = (uint32_t*)malloc((nrec ? nrec : 1) * sizeof(uint32_t));
+  if (!off || !order) {
+    free(rec_recv);
+    free(rec_rumor);
+    free(off);
+    free(order);
+    return -1;
+  }
+  for (size_t i = 0; i < nrec; ++i) off[rec_recv[i] + 1]++;
+  for (uint32_t r = 0; r < n; ++r) off[r + 1] += off[r];
+  {
+    uint32_t* cur = (uint32_t*)malloc(((size_t)n + 1) * sizeof(uint32_t));
+    memcpy(cur, off, ((size_t)n + 1) * sizeof(uint32_t));
+    for (size_t i = 0; i < nrec; ++i) order[cur[rec_recv[i]]++] = rec_rumor[i];
+    free(cur);
+  }
+  for (uint32_t r = 0; r < n; ++r) {
+    if (!w->alive[r]) continue;
+    for (uint32_t i = off[r]; i < off[r + 1]; ++i) merge_one(w, r, order[i]);
+  }
+  free(off);
+  free(order);
+  free(rec_recv);
+  free(rec_rumor);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* UserEventCoalescer  core/src/coalesce/user.rs:52-97                      */
+/* ------------------------------------------------------------------------ */
+uint32_t orc_coalesce_user_events(const orc_uevent* in, uint32_t n, orc_uevent* out) {
+  /* IndexMap<name, LatestUserEvents>: names kept in first-insertion order.
+   * An event survives to the flush iff its ltime equals its name's final
+   * latest ltime (older ones are dropped or cleared, equal ones appended). */
+  uint32_t* names = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
+  uint64_t* lt = (uint64_t*)malloc((n ? n : 1) * sizeof(uint64_t));
+  uint32_t* grp = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
+  uint32_t nn = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t j = 0;
+    while (j < nn && names[j] != in[i].name) ++j;
+    grp[i] = j;
+    if (j == nn) {
+      names[nn] = in[i].name;
+      lt[nn++] = in[i].ltime;
+    } else if (lt[j] < in[i].ltime) {
+      lt[j] = in[i].ltime;
+    }
+  }
+  uint32_t o = 0;
+  for (uint32_t j = 0; j < nn; ++j)
+    for (uint32_t i = 0; i < n; ++i)
+      if (grp[i] == j && in[i].ltime == lt[j]) out[o++] = in[i];
+  free(names);
+  free(lt);
+  free(grp);
+  return o;
+}

@@ -1,0 +1,306 @@
+/*
+ * oracle.h — CPU restatement of the ruserf gossip-round hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing under ruserf_amd/ links, imports or
+ * executes this code; only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg load liboracle.so, and only as the checker / the timed
+ * CPU baseline.  The product path (HIP kernels behind include/ruserf_amd.h)
+ * never routes through it.
+ *
+ * Parity status (see DESIGN.md "Oracle"):
+ *   - Vivaldi (V1-V14), Lamport clock (M1), intent merge (M3-M6) and the
+ *     event/query dedup (D1, D2) and user-event coalescer (D8) are
+ *     line-for-line restatements of the Rust reference (cited per function in
+ *     oracle.c) and are PINNED by the reference's own unit-test known answers
+ *     (tests/golden/ fixtures, tests/test_oracle_kat.py).
+ *   - The TransmitLimitedQueue selection/prune model and peer selection live
+ *     in the un-vendored memberlist crate: PARITY UNPINNED (restated from the
+ *     published memberlist design; documented in DESIGN.md).
+ *
+ * The reference is Rust and cannot be compiled here (no cargo/rustc), so there
+ * is no oracle/_ref build.
+ */
+#ifndef RUSERF_ORACLE_H
+#define RUSERF_ORACLE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORC_MAX_DIM 16
+#define ORC_MAX_WINDOW 64
+#define ORC_MAX_FILTER 8
+
+/* ---- Philox4x32-10 (counter-based RNG shared, as a spec, with the kernels) */
+void orc_philox4x32(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
+/* ---- CoordinateError codes (coordinate.rs:29-40, variant order) ---------- */
+enum {
+  ORC_OK = 0,
+  ORC_ERR_DIM_MISMATCH = 1,
+  ORC_ERR_INVALID_COORD = 2,
+  ORC_ERR_INVALID_RTT = 3,
+};
+
+/* CoordinateOptions (coordinate.rs:62-213) */
+typedef struct {
+  uint32_t dimensionality;
+  uint32_t adjustment_window_size;
+  uint32_t latency_filter_size;
+  uint32_t _pad;
+  double vivaldi_error_max;
+  double vivaldi_ce;
+  double vivaldi_cc;
+  double height_min;
+  double gravity_rho;
+} orc_coord_opts;
+
+/* Coordinate (coordinate.rs:508-548) */
+typedef struct {
+  double portion[ORC_MAX_DIM];
+  uint32_t dim;
+  uint32_t _pad;
+  double error;
+  double adjustment;
+  double height;
+} orc_coord;
+
+/* RNG stream used by unit_vector_at's degenerate branch (rand_f64,
+ * coordinate.rs:812-821).  The reference uses thread_rng; the build replaces
+ * it with Philox keyed by (seed, round, member, call) so the kernel and the
+ * oracle draw identical values. */
+typedef struct {
+  uint32_t key[2];
+  uint32_t member;
+  uint32_t round;
+  uint32_t call;   /* which unit_vector_at call inside one update */
+  uint32_t draw;   /* draw counter inside the call */
+} orc_rng;
+
+void orc_coord_opts_default(orc_coord_opts* o);
+void orc_coord_with_options(const orc_coord_opts* o, orc_coord* c);
+int orc_coord_is_valid(const orc_coord* c);
+uint64_t orc_coord_distance_ns(const orc_coord* a, const orc_coord* b);
+double orc_coord_raw_distance(const orc_coord* a, const orc_coord* b);
+double orc_magnitude(const double* v, uint32_t n);
+double orc_rand_f64(orc_rng* r);
+double orc_unit_vector_at(const double* v1, const double* v2, uint32_t n, double* out, orc_rng* r);
+void orc_apply_force_in_place(orc_coord* self, double height_min, double force,
+                              const orc_coord* other, orc_rng* r);
+double orc_as_secs_f64(uint64_t ns);
+
+/* One CoordinateClient (coordinate.rs:252-500).  Latency-filter samples are
+ * kept per peer slot (the reference keys a HashMap by node id). */
+typedef struct {
+  double s[ORC_MAX_FILTER + 1];
+  uint32_t len;
+} orc_filter;
+
+typedef struct {
+  orc_coord coord;
+  orc_coord origin;
+  orc_coord_opts opts;
+  uint32_t adjustment_index;
+  uint32_t n_slots;
+  double adjustment_samples[ORC_MAX_WINDOW];
+  orc_filter* filters; /* n_slots entries */
+  uint64_t resets;
+} orc_client;
+
+int orc_client_init(orc_client* c, const orc_coord_opts* o, uint32_t n_slots);
+void orc_client_free(orc_client* c);
+int orc_client_set_coordinate(orc_client* c, const orc_coord* coord);
+void orc_client_forget_node(orc_client* c, uint32_t slot);
+double orc_client_latency_filter(orc_client* c, uint32_t slot, double rtt_seconds);
+int orc_client_update(orc_client* c, uint32_t slot, const orc_coord* other, uint64_t rtt_ns,
+                      orc_rng* rng, orc_coord* out);
+
+/* ---- Vivaldi population round (BASELINE configs 1 and 5) ----------------
+ * State in the same flat layout the kernels use so results compare directly:
+ *   rows  : [n][row_stride] doubles = portion[dim], error, adjustment, height
+ *   adj   : [window][n] doubles, adj_idx [n]
+ *   filt  : [n][peers][filter_size] doubles, filt_len [n][peers]
+ *   nbr   : [n][peers] member ids                                        */
+typedef struct {
+  uint32_t n, peers, row_stride;
+  orc_coord_opts opts;
+  uint64_t seed;
+  double* rows_cur;
+  double* rows_nxt;
+  double* adj;
+  uint32_t* adj_idx;
+  double* filt;
+  uint32_t* filt_len;
+  uint32_t* nbr;
+  uint64_t resets;
+} orc_vivaldi_pop;
+
+uint32_t orc_row_stride(uint32_t dim);
+int orc_vivaldi_pop_init(orc_vivaldi_pop* p, uint32_t n, uint32_t peers, const orc_coord_opts* o,
+                         uint64_t seed);
+void orc_vivaldi_pop_free(orc_vivaldi_pop* p);
+/* the synthetic probe of member m in round t: neighbour slot + rtt in ns */
+void orc_vivaldi_probe(uint64_t seed, uint32_t n, uint32_t peers, const uint32_t* nbr, uint32_t m,
+                       uint32_t round, uint32_t* slot_out, uint64_t* rtt_out);
+void orc_true_position(uint64_t seed, uint32_t m, double* x, double* y, double* h);
+/* Run rounds [round0, round0+rounds) over members [m_lo, m_hi) using nthreads threads.
+ * Every member probes once per round; peers are read from the previous-round table. */
+int orc_vivaldi_pop_rounds(orc_vivaldi_pop* p, uint32_t round0, uint32_t rounds, int nthreads);
+void orc_gen_neighbors(uint64_t seed, uint32_t n, uint32_t peers, uint32_t* nbr);
+
+/* ---- Lamport clock (types/src/clock.rs:142-182) ------------------------- */
+static inline void orc_clock_witness(uint64_t* clock, uint64_t t) {
+  if (t < *clock) return;
+  *clock = t + 1;
+}
+static inline uint64_t orc_clock_increment(uint64_t* clock) { return ++(*clock); }
+
+/* ---- Gossip world (member-state merge + dissemination) ------------------ */
+enum { ORC_ST_NONE = 0, ORC_ST_ALIVE = 1, ORC_ST_LEAVING = 2, ORC_ST_LEFT = 3, ORC_ST_FAILED = 4 };
+/* view entry kind: unknown member (no state), unknown + buffered intent, known */
+enum { ORC_K_UNKNOWN = 0, ORC_K_INTENT_JOIN = 1, ORC_K_INTENT_LEAVE = 2, ORC_K_KNOWN = 3 };
+/* serf state of a member process (SerfState) */
+enum { ORC_SERF_ALIVE = 0, ORC_SERF_LEAVING = 1, ORC_SERF_LEFT = 2, ORC_SERF_SHUTDOWN = 3 };
+/* rumor / message kinds (types/src/message.rs tags) */
+enum { ORC_MSG_LEAVE = 0, ORC_MSG_JOIN = 1, ORC_MSG_USER_EVENT = 3, ORC_MSG_QUERY = 4 };
+/* queue index: order in which broadcast_messages drains them (delegate.rs:307-374) */
+enum { ORC_Q_INTENT = 0, ORC_Q_QUERY = 1, ORC_Q_EVENT = 2 };
+/* merge result flags */
+enum {
+  ORC_F_REBROADCAST = 1,
+  ORC_F_REFUTE = 2,       /* leave intent about self while alive: broadcast_join(ltime) scheduled */
+  ORC_F_PRUNE = 4,        /* prune requested (handle_prune) */
+  ORC_F_DELIVER = 8,      /* event/query delivered to the application */
+  ORC_F_MEMBER_EVENT = 16 /* a MemberEvent was emitted */
+};
+/* world error bits */
+enum { ORC_E_EVSLOT_FULL = 1, ORC_E_QSLOT_FULL = 2, ORC_E_REFUTE_FULL = 4 };
+
+typedef struct {
+  uint8_t type;     /* ORC_MSG_* */
+  uint8_t flags;    /* leave: bit0 prune; query: bit0 no_broadcast */
+  uint16_t msg_len; /* encoded length used by the transmit-limited queue byte budget */
+  uint32_t subject; /* intents: subject slot */
+  uint64_t ltime;
+  uint64_t key;     /* events: (name_id<<32)|payload_id ; queries: id */
+} orc_rumor;
+
+typedef struct {
+  /* config */
+  uint32_t n, s, qcap, ebuf, qbuf, slot_k, fanout, limit, overhead, tx_limit, max_refute;
+  uint64_t seed;
+  /* per member */
+  uint64_t *clock, *eclock, *qclock, *emin, *qmin, *digest;
+  uint8_t *alive, *serf_state;
+  uint32_t* err;
+  /* subjects */
+  uint32_t* subj_member;     /* [s] */
+  int32_t* member_subj;      /* [n] */
+  uint32_t* refute_cnt;      /* [s] */
+  uint64_t* refute_ltime;    /* [s][max_refute] */
+  /* view [n][s] */
+  uint64_t* v_ltime;
+  uint8_t* v_status;
+  uint8_t* v_kind;
+  /* queues [n][3][qcap] */
+  uint32_t* q_rumor; /* 0xFFFFFFFF = empty */
+  uint32_t* q_seq;
+  uint16_t* q_tx;
+  uint16_t* q_len;
+  uint32_t* q_next_seq; /* [n][3] */
+  /* user-event dedup ring [n][ebuf]: ltime, count, keys[slot_k] */
+  uint64_t* eb_ltime;
+  uint32_t* eb_cnt; /* 0 = empty slot (reference Option::None) */
+  uint64_t* eb_keys;
+  /* query dedup ring [n][qbuf] */
+  uint64_t* qb_ltime;
+  uint32_t* qb_cnt;
+  uint32_t* qb_ids;
+  /* rumor table */
+  orc_rumor* rumors;
+  uint32_t n_rumors, cap_rumors;
+  /* stats */
+  uint64_t merges, sends, deliveries;
+} orc_world;
+
+typedef struct {
+  uint32_t n, s, qcap, ebuf, qbuf, slot_k, fanout, limit, overhead, retransmit_mult, max_refute;
+  uint32_t cap_rumors;
+  uint64_t seed;
+} orc_world_cfg;
+
+int orc_world_init(orc_world* w, const orc_world_cfg* cfg);
+void orc_world_free(orc_world* w);
+uint32_t orc_retransmit_limit(uint32_t mult, uint64_t n);
+
+/* handlers (one receiver) — return ORC_F_* flags */
+int orc_handle_join_intent(orc_world* w, uint32_t m, uint32_t subj, uint64_t ltime);
+int orc_handle_leave_intent(orc_world* w, uint32_t m, uint32_t subj, uint64_t ltime, int prune,
+                            uint64_t* refute_ltime);
+int orc_handle_node_join(orc_world* w, uint32_t m, uint32_t subj);
+int orc_handle_node_leave(orc_world* w, uint32_t m, uint32_t subj);
+int orc_handle_user_event(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key);
+int orc_handle_query(orc_world* w, uint32_t m, uint64_t ltime, uint32_t id, int no_broadcast);
+int orc_upsert_intent(orc_world* w, uint32_t m, uint32_t subj, uint8_t kind, uint64_t ltime);
+
+/* transmit-limited queue model */
+void orc_queue_insert(orc_world* w, uint32_t m, uint32_t q, uint32_t rumor);
+uint32_t orc_queue_get_broadcasts(orc_world* w, uint32_t m, uint32_t q, uint32_t limit,
+                                  uint32_t* out, uint32_t max_out, uint32_t* bytes_used);
+
+uint32_t orc_msg_len(uint8_t type, uint64_t ltime, uint32_t name_len, uint32_t payload_len);
+uint64_t orc_digest_mix(uint64_t d, uint64_t x);
+
+/* one origination (workload action) */
+enum {
+  ORC_ACT_JOIN_SELF = 1,
+  ORC_ACT_LEAVE_SELF = 2,
+  ORC_ACT_FORCE_LEAVE = 3,
+  ORC_ACT_USER_EVENT = 4,
+  ORC_ACT_QUERY = 5
+};
+typedef struct {
+  uint32_t member;
+  uint32_t act;
+  uint32_t subject;  /* FORCE_LEAVE target */
+  uint32_t name_len; /* events/queries */
+  uint32_t payload_len;
+  uint32_t flags;    /* query: no_broadcast */
+  uint64_t key;      /* events: content key; queries: id */
+} orc_action;
+
+/* memberlist-detected transitions (M6) applied at every live member */
+enum { ORC_ML_JOIN = 1, ORC_ML_LEAVE = 2 };
+typedef struct {
+  uint32_t subject;
+  uint32_t kind;     /* ORC_ML_* */
+  uint32_t set_alive;/* after applying: 1 subject's member becomes live, 0 dead, 2 unchanged */
+  uint32_t _pad;
+} orc_ml_event;
+
+/* One full gossip round (see DESIGN.md "Round model"):
+ *   1. memberlist transitions, 2. pending refutations, 3. originations,
+ *   4. emission (k peers x 3 queues under the byte budget), 5. merge at
+ *   receivers in canonical (sender, position) order. */
+int orc_world_round(orc_world* w, uint32_t round, const orc_ml_event* ml, uint32_t n_ml,
+                    const orc_action* acts, uint32_t n_acts);
+uint32_t orc_pick_peers(uint64_t seed, uint32_t n, const uint8_t* alive, uint32_t m, uint32_t round,
+                        uint32_t k, uint32_t* out);
+
+/* ---- user-event coalescer (core/src/coalesce/user.rs:52-97) ------------- */
+typedef struct {
+  uint32_t name;
+  uint64_t ltime;
+  uint64_t payload;
+} orc_uevent;
+/* Coalesce a batch of cc events, then flush; out receives flushed events in
+ * IndexMap insertion order.  Returns number written. */
+uint32_t orc_coalesce_user_events(const orc_uevent* in, uint32_t n, orc_uevent* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,415 @@
+"""Pins the CPU oracle (oracle/oracle.c) against the known answers held by
+al8n/ruserf's own unit tests (tests/golden/reference_kats.json, transcribed
+from the cited reference file:line).  CPU only."""
+import ctypes as C
+import math
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+
+L = O.lib()
+
+
+def test_philox_random123_kat():
+    # Random123 kat_vectors for philox4x32_10 (the counter-based RNG the build
+    # uses in place of the reference's thread_rng)
+    cases = [
+        ((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+        ((0xFFFFFFFF,) * 4, (0xFFFFFFFF,) * 2, (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+        ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0),
+         (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)),
+    ]
+    for ctr, key, exp in cases:
+        c = (C.c_uint32 * 4)(*ctr)
+        k = (C.c_uint32 * 2)(*key)
+        o = (C.c_uint32 * 4)()
+        L.orc_philox4x32(c, k, o)
+        assert tuple(o) == exp
+
+
+# ---------------------------------------------------------------- Vivaldi
+def test_opts_default(kats):
+    d = kats["coordinate"]["opts_default"]
+    o = O.default_opts()
+    for k in ["dimensionality", "vivaldi_error_max", "vivaldi_ce", "vivaldi_cc",
+              "adjustment_window_size", "height_min", "latency_filter_size", "gravity_rho"]:
+        assert getattr(o, k) == d[k], k
+
+
+def _client(opts, slots=4):
+    c = O.Client()
+    assert L.orc_client_init(C.byref(c), C.byref(opts), slots) == 0
+    return c
+
+
+def test_client_update(kats):
+    k = kats["coordinate"]["client_update"]
+    opts = O.default_opts(dimensionality=k["dim"])
+    cl = _client(opts)
+    assert list(cl.coord.portion[:3]) == [0.0, 0.0, 0.0]
+    other = O.coord(opts, k["other_portion"])
+    out = O.Coord()
+    r = O.rng()
+    assert L.orc_client_update(C.byref(cl), 0, C.byref(other), k["rtt_ns"], C.byref(r), C.byref(out)) == O.OK
+    assert out.portion[2] < 0.0
+    out.portion[2] = 99.0
+    assert L.orc_client_set_coordinate(C.byref(cl), C.byref(out)) == O.OK
+    assert cl.coord.portion[2] == 99.0
+    L.orc_client_free(C.byref(cl))
+
+
+def test_client_invalid_in_ping_values(kats):
+    k = kats["coordinate"]["client_invalid_in_ping_values"]
+    opts = O.default_opts(dimensionality=k["dim"])
+    cl = _client(opts)
+    other = O.coord(opts, k["other_portion"])
+    dist = L.orc_coord_distance_ns(C.byref(cl.coord), C.byref(other))
+    for ns in k["rtt_ns"]:
+        r = O.rng()
+        assert L.orc_client_update(C.byref(cl), 0, C.byref(other), ns, C.byref(r), None) == O.ERR_RTT
+        assert L.orc_coord_distance_ns(C.byref(cl.coord), C.byref(other)) == dist
+    L.orc_client_free(C.byref(cl))
+
+
+def test_client_distance_to(kats):
+    k = kats["coordinate"]["client_distance_to"]
+    opts = O.default_opts(dimensionality=k["dim"], height_min=k["height_min"])
+    cl = _client(opts)
+    other = O.coord(opts, k["other_portion"])
+    assert L.orc_coord_distance_ns(C.byref(cl.coord), C.byref(other)) == k["expect_ns"]
+    L.orc_client_free(C.byref(cl))
+
+
+def test_client_latency_filter(kats):
+    k = kats["coordinate"]["client_latency_filter"]
+    opts = O.default_opts(latency_filter_size=k["filter_size"])
+    cl = _client(opts, slots=2)
+    slot = {"alice": 0, "bob": 1}
+    for step in k["steps"]:
+        if step[0] == "forget":
+            L.orc_client_forget_node(C.byref(cl), slot[step[1]])
+            continue
+        got = L.orc_client_latency_filter(C.byref(cl), slot[step[0]], step[1])
+        assert got == step[2]  # the reference checks |d| <= 1e-6; the median is exact
+    L.orc_client_free(C.byref(cl))
+
+
+def test_client_nan_defense(kats):
+    k = kats["coordinate"]["client_nan_defense"]
+    opts = O.default_opts(dimensionality=k["dim"])
+    cl = _client(opts)
+    other = O.coord(opts, [math.nan, 0.0, 0.0])
+    assert not L.orc_coord_is_valid(C.byref(other))
+    r = O.rng()
+    assert L.orc_client_update(C.byref(cl), 0, C.byref(other), k["rtt_ns"], C.byref(r), None) == O.ERR_COORD
+    assert L.orc_coord_is_valid(C.byref(cl.coord))
+    wide = O.coord(opts, [math.nan, 0.0, 0.0, 0.0, 0.0, 0.0])
+    assert L.orc_client_set_coordinate(C.byref(cl), C.byref(wide)) == O.ERR_DIM
+    assert L.orc_coord_is_valid(C.byref(cl.coord))
+    cl.coord.portion[0] = math.nan
+    good = O.coord(opts)
+    out = O.Coord()
+    assert L.orc_client_update(C.byref(cl), 0, C.byref(good), k["rtt_ns"], C.byref(r), C.byref(out)) == O.OK
+    assert L.orc_coord_is_valid(C.byref(out))
+    assert cl.resets == 1
+    L.orc_client_free(C.byref(cl))
+
+
+def test_coordinate_apply_force(kats):
+    k = kats["coordinate"]["coordinate_apply_force"]
+    for case in k["cases"]:
+        opts = O.default_opts(dimensionality=k["dim"], height_min=case["height_min"])
+        me = O.coord(opts, case["self"], height=case["self_height"])
+        other = O.coord(opts, case["other"], height=case["other_height"])
+        r = O.rng()
+        L.orc_apply_force_in_place(C.byref(me), case["height_min"], case["force"], C.byref(other), C.byref(r))
+        for i in range(3):
+            assert abs(me.portion[i] - case["expect_portion"][i]) <= 1e-6
+            # exact where the arithmetic is exact
+        if "expect_height" in case:
+            assert abs(me.height - case["expect_height"]) <= 1e-6
+    rc = k["random_case"]
+    opts = O.default_opts(dimensionality=k["dim"], height_min=rc["height_min"])
+    origin = O.coord(opts)
+    me = O.coord(opts)
+    r = O.rng(member=7)
+    L.orc_apply_force_in_place(C.byref(me), rc["height_min"], rc["force"], C.byref(origin), C.byref(r))
+    d = L.orc_as_secs_f64(L.orc_coord_distance_ns(C.byref(origin), C.byref(me)))
+    assert abs(d - rc["expect_distance_secs"]) <= 1e-6
+
+
+def test_vector_helpers(kats):
+    k = kats["coordinate"]
+    v = (C.c_double * 3)(*k["coordinate_magnitude"]["v"])
+    assert L.orc_magnitude(v, 3) == k["coordinate_magnitude"]["expect"]
+    z = (C.c_double * 3)(0.0, 0.0, 0.0)
+    assert L.orc_magnitude(z, 3) == 0.0
+    u = k["coordinate_unit_vector_at"]
+    a = (C.c_double * 3)(*u["a"])
+    b = (C.c_double * 3)(*u["b"])
+    out = (C.c_double * 3)()
+    r = O.rng()
+    mag = L.orc_unit_vector_at(a, b, 3, out, C.byref(r))
+    for i in range(3):
+        assert abs(out[i] - u["expect"][i]) <= 1e-15
+    d = (C.c_double * 3)(*[x - y for x, y in zip(u["a"], u["b"])])
+    assert mag == L.orc_magnitude(d, 3)
+    assert abs(L.orc_magnitude(out, 3) - 1.0) <= 1e-6
+    mag = L.orc_unit_vector_at(a, a, 3, out, C.byref(r))
+    assert mag == 0.0 and abs(L.orc_magnitude(out, 3) - 1.0) <= 1e-6
+    # add / diff (coordinate.rs:1160-1197) are elementwise IEEE ops
+    ad, df = k["coordinate_add"], k["coordinate_diff"]
+    assert [x + y for x, y in zip(ad["a"], ad["b"])] == ad["expect"]
+    assert [x - y for x, y in zip(df["a"], df["b"])] == df["expect"]
+
+
+def test_as_secs_f64_and_saturating_cast():
+    # Duration::as_secs_f64 is secs + nanos/1e9, which differs from ns/1e9
+    diffs = 0
+    for ns in range(1_000_000_007, 1_000_000_007 + 20000 * 7919, 7919):
+        a = L.orc_as_secs_f64(ns)
+        assert a == (ns // 10**9) + (ns % 10**9) / 1e9
+        diffs += a != ns / 1e9
+    assert diffs > 0
+    opts = O.default_opts(dimensionality=3, height_min=0.0)
+    a = O.coord(opts)
+    b = O.coord(opts, [0.0, 0.0, 1e300])
+    assert L.orc_coord_distance_ns(C.byref(a), C.byref(b)) == 2**64 - 1
+
+
+# ------------------------------------------------------------ Lamport clock
+def test_lamport_clock(kats):
+    # LamportClock::{time, increment, witness} restated in oracle.h
+    clock = 0
+    for op in kats["clock"]["ops"]:
+        if op[0] == "time":
+            assert clock == op[1]
+        elif op[0] == "increment":
+            clock += 1
+            assert clock == op[1]
+        else:
+            if not op[1] < clock:
+                clock = op[1] + 1
+            assert clock == op[2]
+
+
+# ---------------------------------------------------------------- merge
+def make_world(n=2, s=1, **kw):
+    cfg = O.WorldCfg(n=n, s=s, qcap=8, ebuf=512, qbuf=512, slot_k=8, fanout=1, limit=1400,
+                     overhead=2, retransmit_mult=4, max_refute=2, cap_rumors=1024, seed=0x5EED5EED)
+    for k_, v in kw.items():
+        setattr(cfg, k_, v)
+    w = O.World()
+    assert L.orc_world_init(C.byref(w), C.byref(cfg)) == 0
+    for i in range(s):
+        w.subj_member[i] = n - s + i
+        w.member_subj[n - s + i] = i
+    return w
+
+
+def set_known(w, m, subj, status, st):
+    e = m * w.s + subj
+    w.v_kind[e] = O.K_KNOWN
+    w.v_status[e] = status
+    w.v_ltime[e] = st
+
+
+def intent(w, m, subj):
+    e = m * w.s + subj
+    return {O.K_JOIN: "join", O.K_LEAVE: "leave"}.get(w.v_kind[e]), w.v_ltime[e]
+
+
+STATUS = {"alive": O.ST_ALIVE, "leaving": O.ST_LEAVING, "left": O.ST_LEFT, "failed": O.ST_FAILED}
+
+
+@pytest.mark.parametrize("name", ["join_intent_buffer_early", "leave_intent_buffer_early"])
+def test_intent_buffer_early(kats, name):
+    k = kats["merge"][name]
+    w = make_world()
+    fn = (lambda: L.orc_handle_join_intent(C.byref(w), 0, 0, k["ltime"])) if name.startswith("join") \
+        else (lambda: L.orc_handle_leave_intent(C.byref(w), 0, 0, k["ltime"], 0, None))
+    assert [bool(fn() & O.F_REBROADCAST) for _ in range(2)] == k["expect"]
+    assert list(intent(w, 0, 0)) == k["buffered"]
+    L.orc_world_free(C.byref(w))
+
+
+@pytest.mark.parametrize("name", ["join_intent_old_message", "leave_intent_old_message"])
+def test_intent_old_message(kats, name):
+    k = kats["merge"][name]
+    w = make_world()
+    set_known(w, 0, 0, STATUS[k["subject"][0]], k["subject"][1])
+    if name.startswith("join"):
+        f = L.orc_handle_join_intent(C.byref(w), 0, 0, k["ltime"])
+    else:
+        f = L.orc_handle_leave_intent(C.byref(w), 0, 0, k["ltime"], 0, None)
+    assert bool(f & O.F_REBROADCAST) == k["expect"]
+    assert w.v_kind[0] == O.K_KNOWN  # nothing buffered
+    L.orc_world_free(C.byref(w))
+
+
+def test_join_intent_newer_and_reset_leaving(kats):
+    for name in ["join_intent_newer", "join_intent_reset_leaving"]:
+        k = kats["merge"][name]
+        w = make_world()
+        set_known(w, 0, 0, STATUS[k["subject"][0]], k["subject"][1])
+        assert bool(L.orc_handle_join_intent(C.byref(w), 0, 0, k["ltime"]) & O.F_REBROADCAST) == k["expect"]
+        assert w.v_ltime[0] == k["status_time"]
+        assert w.clock[0] == k["clock"]
+        if "status" in k:
+            assert w.v_status[0] == STATUS[k["status"]]
+        L.orc_world_free(C.byref(w))
+
+
+def test_leave_intent_newer(kats):
+    k = kats["merge"]["leave_intent_newer"]
+    w = make_world()
+    set_known(w, 0, 0, O.ST_ALIVE, 12)
+    assert bool(L.orc_handle_leave_intent(C.byref(w), 0, 0, k["ltime"], 0, None) & O.F_REBROADCAST)
+    assert w.v_status[0] == STATUS[k["status"]]
+    assert w.clock[0] == k["clock"]
+    L.orc_world_free(C.byref(w))
+
+
+def test_join_pending_intents(kats):
+    for name in ["join_pending_intent", "join_pending_intents"]:
+        k = kats["merge"][name]
+        w = make_world()
+        for ty, lt in k["intents"]:
+            L.orc_upsert_intent(C.byref(w), 0, 0, O.K_JOIN if ty == "join" else O.K_LEAVE, lt)
+        L.orc_handle_node_join(C.byref(w), 0, 0)
+        assert w.v_kind[0] == O.K_KNOWN
+        assert w.v_status[0] == STATUS[k["after_node_join"][0]]
+        assert w.v_ltime[0] == k["after_node_join"][1]
+        L.orc_world_free(C.byref(w))
+
+
+def test_leave_transitions_and_refute():
+    # base.rs:1466-1527 state table, plus the self-refute branch (1437-1447)
+    w = make_world(n=3, s=1)
+    for st, exp_st, exp_flags in [
+        (O.ST_ALIVE, O.ST_LEAVING, O.F_REBROADCAST),
+        (O.ST_LEAVING, O.ST_LEAVING, O.F_REBROADCAST),
+        (O.ST_LEFT, O.ST_LEFT, O.F_REBROADCAST),
+        (O.ST_FAILED, O.ST_LEFT, O.F_REBROADCAST | O.F_MEMBER_EVENT),
+        (O.ST_NONE, O.ST_NONE, 0),
+    ]:
+        set_known(w, 0, 0, st, 5)
+        f = L.orc_handle_leave_intent(C.byref(w), 0, 0, 9, 0, None)
+        assert f == exp_flags and w.v_status[0] == exp_st and w.v_ltime[0] == 9
+    # receiver == subject (member 2) and alive -> refute with clock.time()
+    set_known(w, 2, 0, O.ST_ALIVE, 5)
+    ref = C.c_uint64(0)
+    f = L.orc_handle_leave_intent(C.byref(w), 2, 0, 9, 0, C.byref(ref))
+    assert f == O.F_REFUTE and ref.value == w.clock[2] == 10 and w.v_ltime[2 * w.s] == 5
+    L.orc_world_free(C.byref(w))
+
+
+def test_delegate_merge_remote_state(kats):
+    """merge_remote_state (delegate.rs:422-554) driven through the oracle's handlers."""
+    k = kats["merge"]["delegate_merge_remote_state"]
+    pp = k["pp"]
+    # subjects: test=0, foo=1; receiver = member 0
+    w = make_world(n=3, s=2)
+    def witness(arr_, v):
+        if not v < arr_[0]:
+            arr_[0] = v + 1
+    if pp["ltime"] > 0:
+        witness(w.clock, pp["ltime"] - 1)
+    if pp["event_ltime"] > 0:
+        witness(w.eclock, pp["event_ltime"] - 1)
+    if pp["query_ltime"] > 0:
+        witness(w.qclock, pp["query_ltime"] - 1)
+    subj = {"test": 0, "foo": 1}
+    st = dict(pp["status_ltimes"])
+    for node in pp["left_members"]:
+        L.orc_handle_leave_intent(C.byref(w), 0, subj[node], st[node] + 1, 0, None)
+    for node, lt in pp["status_ltimes"]:
+        if node in pp["left_members"]:
+            continue
+        L.orc_handle_join_intent(C.byref(w), 0, subj[node], lt)
+    names = {"test": 1}
+    for ltime, evs in pp["events"]:
+        for name, payload in evs:
+            L.orc_handle_user_event(C.byref(w), 0, ltime, names[name] << 32)
+    e = k["expect"]
+    assert w.clock[0] == e["clock"]
+    assert list(intent(w, 0, 0)) == e["intent_test"]
+    assert list(intent(w, 0, 1)) == e["intent_foo"]
+    assert w.eclock[0] == e["event_clock"]
+    assert w.eb_cnt[45] == 1 and w.eb_keys[45 * w.slot_k] >> 32 == names[e["event_slot_45_name"]]
+    assert w.qclock[0] == e["query_clock"]
+    L.orc_world_free(C.byref(w))
+
+
+# ---------------------------------------------------------- dissemination
+def test_user_event_old_message(kats):
+    k = kats["dissemination"]["user_event_old_message"]
+    w = make_world()
+    if not k["witness"] < w.eclock[0]:
+        w.eclock[0] = k["witness"] + 1
+    assert L.orc_handle_user_event(C.byref(w), 0, k["ltime"], 7) == 0
+    L.orc_world_free(C.byref(w))
+
+
+def test_user_event_same_clock(kats):
+    k = kats["dissemination"]["user_event_same_clock"]
+    w = make_world()
+    names, payloads = {}, {}
+    keys = []
+    for lt, name, payload in k["events"]:
+        key = (names.setdefault(name, len(names) + 1) << 32) | payloads.setdefault(payload, len(payloads) + 1)
+        keys.append(key)
+        f = L.orc_handle_user_event(C.byref(w), 0, lt, key)
+        assert bool(f & O.F_REBROADCAST)
+        assert bool(f & O.F_DELIVER)
+    slot = 1 % 512
+    assert [w.eb_keys[slot * w.slot_k + i] for i in range(w.eb_cnt[slot])] == keys
+    # a repeat of an already-buffered (name, payload) is not delivered again
+    assert L.orc_handle_user_event(C.byref(w), 0, 1, keys[1]) == 0
+    L.orc_world_free(C.byref(w))
+
+
+def test_query_old_message_quirk(kats):
+    k = kats["dissemination"]["query_old_message"]
+    w = make_world()
+    if not k["witness"] < w.qclock[0]:
+        w.qclock[0] = k["witness"] + 1
+    assert L.orc_handle_query(C.byref(w), 0, k["ltime"], k["id"], 0) == 0
+    # quirk (base.rs:999): compares the buffer length, so even a CURRENT query is
+    # dropped once the clock exceeds 2*buffer
+    assert L.orc_handle_query(C.byref(w), 0, w.qclock[0], 99, 0) == 0
+    L.orc_world_free(C.byref(w))
+
+
+def test_query_same_clock(kats):
+    k = kats["dissemination"]["query_same_clock"]
+    w = make_world()
+    got = [bool(L.orc_handle_query(C.byref(w), 0, lt, qid, 0) & O.F_REBROADCAST) for lt, qid, _ in k["queries"]]
+    assert got == k["expect"]
+    slot = 1
+    assert [w.qb_ids[slot * w.slot_k + i] for i in range(w.qb_cnt[slot])] == [1, 2, 3]
+    L.orc_world_free(C.byref(w))
+
+
+def test_user_event_coalesce_basic(kats):
+    k = kats["dissemination"]["user_event_coalesce_basic"]
+    names, payloads = {}, {"": 0}
+    ev = (O.UEvent * len(k["events"]))()
+    for i, (name, lt, payload) in enumerate(k["events"]):
+        ev[i].name = names.setdefault(name, len(names) + 1)
+        ev[i].ltime = lt
+        ev[i].payload = payloads.setdefault(payload, len(payloads))
+    out = (O.UEvent * len(k["events"]))()
+    n = L.orc_coalesce_user_events(ev, len(k["events"]), out)
+    inv_n = {v: kk for kk, v in names.items()}
+    inv_p = {v: kk for kk, v in payloads.items()}
+    got = [[inv_n[out[i].name], out[i].ltime, inv_p[out[i].payload]] for i in range(n)]
+    assert got == k["expect_flushed"]
+
+
+def test_retransmit_limit():
+    # memberlist retransmitLimit = mult * ceil(log10(n+1)) (parity unpinned)
+    for n, exp in [(1, 4), (9, 4), (10, 8), (99, 8), (100, 12), (1_000_000, 28), (999_999, 24)]:
+        assert L.orc_retransmit_limit(4, n) == exp
