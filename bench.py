@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""bench.py — the driver's benchmark contract for ruserf_amd.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload gossip|vivaldi]
+
+One step = one pass of the hot path over one batch of synthetic input:
+  gossip  : one gossip round over the shard's members (BASELINE configs[1]:
+            1M members per GPU, fanout k=3, member-state merge + Lamport
+            clocks) -> metric "node-rounds/s"
+  vivaldi : one Vivaldi round (every member probes one neighbour and runs
+            CoordinateClient::update) (configs[4]) -> "Vivaldi updates/s"
+Multi-GPU: one process per GPU (torch.distributed over RCCL), members sharded
+by contiguous id range, weak scaling.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+SEED = 0x5EED5EED
+# algorithmic HBM bytes per Vivaldi update in rsf_vivaldi_round:
+# reads self 88 + peer 88 + adjustment window 160 + window index 4 + filter samples 24 + filter meta 4,
+# writes self 88 + window slot 8 + window index 4 + filter sample 8 + filter meta 4  (D=8, W=20, F=3)
+VIVALDI_BYTES = 480
+HBM_PEAK_GBS = 8000.0
+
+
+class CudaArray:
+    """Zero-copy view of engine-owned HBM as a torch tensor (for collectives)."""
+
+    def __init__(self, ptr, shape, typestr):
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr, "data": (int(ptr), False),
+                                         "version": 3, "strides": None}
+
+
+def env_rank():
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
+
+
+def cpu_info():
+    model = platform.processor() or "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model
+
+
+def cpu_threads():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", n))))
+
+
+def barrier(world):
+    if world > 1:
+        torch.distributed.barrier()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x, world):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    torch.distributed.all_reduce(t)
+    return float(t.item())
+
+
+# --------------------------------------------------------------------------- vivaldi
+def run_vivaldi(args, rank, world):
+    from ruserf_amd import CoordinateClients, CoordinateOptions
+    per = args.members // world if args.members_total else args.members
+    n = per * world
+    lo, hi = rank * per, (rank + 1) * per
+    stream = torch.cuda.current_stream()  # a non-default stream (set in main)
+    g = CoordinateClients(n, 16, CoordinateOptions(), seed=SEED, device=torch.cuda.current_device(),
+                          shard=(lo, hi))
+    g.set_stream(stream.cuda_stream)
+    table = None
+
+    def refresh():
+        # all-gather of the coordinate table (peers read last round's rows)
+        if world == 1:
+            return
+        ptr, stride = g.table_ptr()
+        full = torch.as_tensor(CudaArray(ptr, (n * stride,), "<f8"), device="cuda")
+        mine = full[lo * stride: hi * stride].clone()
+        torch.distributed.all_gather_into_tensor(full, mine)
+
+    step = [0]
+
+    def one_step():
+        g.round(step[0])
+        refresh()
+        step[0] += 1
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    barrier(world)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kernel_ms = []
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        g.round(step[0])
+        evs[i][1].record(stream)
+        refresh()
+        step[0] += 1
+    torch.cuda.synchronize()
+    barrier(world)
+    wall = time.perf_counter() - t0
+    kernel_ms = [a.elapsed_time(b) for a, b in evs]
+    wall = max_over_ranks(wall, world)
+    avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
+    updates = per * world * args.steps
+    value = updates / wall
+    achieved = VIVALDI_BYTES * per / avg_kernel_s / 1e9
+    g.close()
+    return {
+        "metric": "Vivaldi updates/s", "value": value, "unit": "updates/s",
+        "ms_per_step": wall / args.steps * 1e3, "dtype": "f64",
+        "config": {"workload": f"Vivaldi rounds (BASELINE configs[4] shape), {n} members, D=8 f64, height + "
+                               f"latency filter F=3, adjustment window W=20, 16 neighbours/member",
+                   "members": n, "members_per_gpu": per, "parallelism": f"members sharded x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "vivaldi_round_kernel<8,3>", "bytes_per_unit": VIVALDI_BYTES,
+                     "units_per_launch": per, "avg_launch_ms": avg_kernel_s * 1e3},
+    }
+
+
+def cpu_baseline_vivaldi(seconds_target=12.0):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O  # test infrastructure: the checker / CPU baseline only
+    L = O.lib()
+    th = cpu_threads()
+    n = 2_000_000
+    p = O.VivaldiPop()
+    oo = O.default_opts()
+    L.orc_vivaldi_pop_init(C.byref(p), n, 16, C.byref(oo), SEED)
+    L.orc_vivaldi_pop_rounds(C.byref(p), 0, 1, th)  # warm (page faults)
+    rounds, t_total, r = 0, 0.0, 1
+    while t_total < seconds_target and rounds < 200:
+        t = time.perf_counter()
+        L.orc_vivaldi_pop_rounds(C.byref(p), r, 1, th)
+        t_total += time.perf_counter() - t
+        rounds += 1
+        r += 1
+    L.orc_vivaldi_pop_free(C.byref(p))
+    return {"value": n * rounds / t_total, "unit": "updates/s", "cores": th, "kind": "port",
+            "sample": f"oracle Vivaldi rounds, {n} members x {rounds} rounds ({t_total:.1f}s) on {th} threads, "
+                      f"{cpu_info()}"}
+
+
+# --------------------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=["gossip", "vivaldi"], default=None)
+    ap.add_argument("--members", type=int, default=None, help="members per GPU")
+    ap.add_argument("--members-total", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    rank, world, local = env_rank()
+    if world != args.gpus and world == 1 and args.gpus > 1:
+        print("run multi-GPU through torch.distributed.run (one process per GPU)", file=sys.stderr)
+        sys.exit(2)
+    torch.cuda.set_device(local)
+    # every engine launch goes to this stream; torch's default stream handle is NULL,
+    # which the C ABI would read as "the context's own stream"
+    torch.cuda.set_stream(torch.cuda.Stream())
+    if world > 1:
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import ruserf_amd
+    try:
+        from ruserf_amd import gossip  # noqa: F401
+        have_gossip = True
+    except ImportError:
+        have_gossip = False
+    workload = args.workload or ("gossip" if have_gossip else "vivaldi")
+    if workload == "vivaldi":
+        args.members = args.members or 64_000_000 // max(1, world) * max(1, world) // world
+        res = run_vivaldi(args, rank, world)
+        cpu = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline_vivaldi()
+    else:
+        from bench_gossip import run_gossip, cpu_baseline_gossip
+        args.members = args.members or 1_000_000
+        res = run_gossip(args, rank, world)
+        cpu = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline_gossip(args)
+    if rank == 0:
+        line = {
+            "metric": res["metric"], "value": res["value"], "unit": res["unit"], "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": res["dtype"],
+            "data": "synthetic", "config": res["config"], "roofline": res["roofline"], "cpu_baseline": cpu,
+        }
+        for k in res:
+            if k not in line and k not in ("metric",):
+                line[k] = res[k]
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,153 @@
+"""Gossip-round leg of bench.py (metric: node-rounds/s, BASELINE configs[1]/[2]).
+
+A node-round = one member processing one gossip round: select
+k=3 live peers, drain its intent/query/event queues under the byte budget
+(b = 8 intents per target), emit, receive and merge its inbound records in
+canonical order, update its Lamport clocks.
+"""
+import ctypes as C
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+SEED = 0x5EED5EED
+SUBJECTS = 4096
+SETTLE_ROUNDS = 12   # setup: bring the cluster to gossip steady state (queues saturated) before timing
+HBM_PEAK_GBS = 8000.0
+
+
+def gossip_cfg(n_total, rounds_total, world, shard=None):
+    from ruserf_amd.gossip import GossipConfig
+    per_round = SUBJECTS * 4 + int(round(n_total * 0.01))
+    return GossipConfig(n_members=n_total, n_subjects=SUBJECTS, shard=shard, queue_cap=64, event_buffer_size=512,
+                        query_buffer_size=512, slot_k=1, fanout=3, gossip_limit=8 * 24, gossip_overhead=2,
+                        retransmit_mult=4, max_refute=4, max_rumors=per_round * rounds_total + 1024, seed=SEED)
+
+
+def kernel_bytes(qcap, senders, records):
+    """Algorithmic HBM bytes (roofline):
+    emit  : per live sender the three queues are scanned (rumor id, insertion seq,
+            transmits|len = 12 B per slot), picked slots' transmit words written
+            back (4 B) and records emitted (receiver + rumor id = 8 B)
+    merge : per received record B_merge = 64 B (record 16, view slot read 16 +
+            write 16, clock r/w 16) plus each receiver's queue
+            state read (12 B per slot)."""
+    emit = senders * 3 * qcap * 12 + records * (4 + 8)
+    merge = records * 64 + senders * 3 * qcap * 12
+    return emit, merge
+
+
+def run_gossip(args, rank, world):
+    from ruserf_amd import workload as W
+    from ruserf_amd.dist import ShardedGossip
+    from ruserf_amd.gossip import GossipEngine
+    per = args.members
+    n = per * world
+    rounds_total = SETTLE_ROUNDS + args.warmup + args.steps
+    cfg = gossip_cfg(n, rounds_total, world)
+    subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED)
+    views = W.initial_views(SUBJECTS)
+    stream = torch.cuda.current_stream()
+    if world == 1:
+        eng = GossipEngine(cfg, device=torch.cuda.current_device())
+        eng.set_stream(stream.cuda_stream)
+        step_fn = lambda t: eng.round(t, ml[t], acts[t])  # noqa: E731
+    else:
+        sg = ShardedGossip(cfg, rank, world, device=torch.cuda.current_device())
+        eng = sg.eng
+        step_fn = lambda t: sg.round(t, ml[t], acts[t])  # noqa: E731
+    eng.set_subjects(subj)
+    eng.init_views(*views)
+    t = 0
+    for _ in range(SETTLE_ROUNDS + args.warmup):
+        step_fn(t)
+        t += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    merged0 = eng.merged_total()
+    eng.set_profiling(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step_fn(t)
+        t += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    wall = time.perf_counter() - t0
+    phase_ms, nr = eng.phase_times()
+    merged = eng.merged_total() - merged0
+    st = eng.members()
+    err_members = int(np.count_nonzero(st["err"]))
+    eng.set_profiling(False)
+    if world > 1:
+        t_ = torch.tensor([wall, float(merged), float(err_members)], dtype=torch.float64, device="cuda")
+        mx = t_.clone()
+        torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX)
+        torch.distributed.all_reduce(t_)
+        wall, merged_all, err_all = float(mx[0]), float(t_[1]), float(t_[2])
+    else:
+        merged_all, err_all = float(merged), float(err_members)
+    node_rounds = n * args.steps
+    avg = [x / max(1, nr) for x in phase_ms]  # ms per round per phase
+    names = ["begin (memberlist+refute+originate)", "emit_kernel", "sort" + ("+exchange" if world > 1 else ""),
+             "segment+merge_kernel"]
+    senders = per
+    records = merged / max(1, args.steps)  # records per round on this shard
+    emit_b, merge_b = kernel_bytes(cfg.queue_cap, senders, records)
+    dom = 1 if avg[1] >= avg[3] else 3
+    dom_bytes = emit_b if dom == 1 else merge_b
+    achieved = dom_bytes / (avg[dom] / 1e3) / 1e9
+    return {
+        "metric": "gossip node-rounds/s", "value": node_rounds / wall, "unit": "node-rounds/s",
+        "ms_per_step": wall / args.steps * 1e3, "dtype": "u64",
+        "config": {"workload": f"gossip rounds, {n} members ({per}/GPU), fanout k=3, {SUBJECTS} tracked subjects, "
+                               f"1% of members originate a join/leave intent per round, member-state merge + "
+                               f"Lamport clocks (BASELINE configs[1]{'/[2]' if world > 1 else ''})",
+                   "members": n, "members_per_gpu": per, "fanout": 3, "items_per_target": 8,
+                   "queue_cap_per_queue": cfg.queue_cap, "subjects": SUBJECTS,
+                   "settle_rounds": SETTLE_ROUNDS, "parallelism": f"members sharded x{world}"},
+        "merges_per_s": merged_all / wall,
+        "records_per_round_per_gpu": records,
+        "error_members": err_all,
+        "phases_ms_per_round": dict(zip(names, avg)),
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": names[dom],
+                     "bytes_per_launch": dom_bytes, "avg_launch_ms": avg[dom]},
+    }
+
+
+def cpu_baseline_gossip(args, seconds_target=12.0):
+    """The oracle's round (a single-threaded restatement of the same path) on a
+    bounded sample: N members, same subject count, settled, then timed."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import gossip_harness as H  # test infrastructure: checker / CPU baseline only
+    from ruserf_amd import workload as W
+    n = 100_000
+    rounds_total = 40
+    cfg = gossip_cfg(n, rounds_total, 1)
+    subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED)
+    w = H.oracle_world(cfg, subj, W.initial_views(SUBJECTS))
+    t = 0
+    for _ in range(SETTLE_ROUNDS):
+        H.oracle_round(w, t, ml[t], acts[t])
+        t += 1
+    done, spent = 0, 0.0
+    while spent < seconds_target and t < rounds_total:
+        t0 = time.perf_counter()
+        H.oracle_round(w, t, ml[t], acts[t])
+        spent += time.perf_counter() - t0
+        done += 1
+        t += 1
+    H.L.orc_world_free(C.byref(w))
+    return {"value": n * done / spent, "unit": "node-rounds/s", "cores": 1, "kind": "port",
+            "sample": f"oracle gossip rounds, {n} members, {SUBJECTS} subjects, {done} settled rounds "
+                      f"({spent:.1f}s), single thread"}

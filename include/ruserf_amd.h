@@ -1,0 +1,309 @@
+/*
+ * ruserf_amd.h — C ABI of the MI355X-native engine for ruserf's data-parallel
+ * hot path (a batched gossip round over very large membership sets).
+ *
+ * Drop-in boundary.  Every entry point names the reference interface it
+ * replaces (al8n/ruserf @ v2, file:line).  Plain pointers and sizes only; no
+ * torch or HIP types in signatures (streams are passed as void*).  Errors are
+ * returned as int codes, never thrown or aborted across the boundary.  A
+ * context is NOT thread-safe: like the reference's RwLock write section the
+ * caller serialises calls on one context (coordinate.rs:356-360, 468).
+ *
+ * Pointer conventions: arguments documented "host" are host memory and are
+ * copied; "device" arguments are HBM pointers on the context's device.
+ * Calls are asynchronous on the context stream unless they return data to
+ * host memory, which synchronises that stream.
+ */
+#ifndef RUSERF_AMD_H
+#define RUSERF_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+/* 1..3 mirror CoordinateError in variant order (core/src/coordinate.rs:29-40) */
+#define RSF_OK 0
+#define RSF_ERR_DIM_MISMATCH 1   /* CoordinateError::DimensionalityMismatch */
+#define RSF_ERR_INVALID_COORD 2  /* CoordinateError::InvalidCoordinate */
+#define RSF_ERR_INVALID_RTT 3    /* CoordinateError::InvalidRTT(rtt > 10 s) */
+#define RSF_ERR_ARG (-1)         /* bad argument / precondition (reference would panic) */
+#define RSF_ERR_HIP (-2)         /* HIP runtime error; see rsf_last_error() */
+#define RSF_ERR_NOMEM (-3)       /* device allocation failed */
+#define RSF_ERR_OVERFLOW (-4)    /* a fixed-capacity device structure overflowed */
+
+/* Last error message of the calling thread (static storage, never NULL). */
+const char* rsf_last_error(void);
+/* Library version string. */
+const char* rsf_version(void);
+/* Number of visible devices (0 when no GPU): lets a caller probe without HIP headers. */
+int rsf_device_count(void);
+
+/* ======================================================================== */
+/* Vivaldi network coordinates                                              */
+/* ======================================================================== */
+
+/* = CoordinateOptions (core/src/coordinate.rs:62-188; defaults 200-213) */
+typedef struct rsf_coord_opts {
+  uint32_t dimensionality;         /* 1..16 (kernels specialised for 8) */
+  uint32_t adjustment_window_size; /* 0..64; 0 disables adjustment (coordinate.rs:335) */
+  uint32_t latency_filter_size;    /* 1..7 */
+  uint32_t _reserved;
+  double vivaldi_error_max;
+  double vivaldi_ce;
+  double vivaldi_cc;
+  double height_min;
+  double gravity_rho;
+} rsf_coord_opts;
+
+/* Fills CoordinateOptions::new() (coordinate.rs:200-213). */
+void rsf_coord_opts_default(rsf_coord_opts* opts);
+
+/* Row layout of one Coordinate in HBM and in host buffers:
+ *   row[0..dim) = portion, row[dim] = error, row[dim+1] = adjustment,
+ *   row[dim+2] = height, padded to rsf_coord_row_stride(dim) doubles. */
+uint32_t rsf_coord_row_stride(uint32_t dimensionality);
+
+/* A population of CoordinateClients, one per member (coordinate.rs:356-500;
+ * Serf builds one per node, core/src/serf/base.rs:166-173).  Each member keeps
+ * latency-filter samples for `peer_slots` peers (the reference keys them by
+ * node id in a HashMap, coordinate.rs:272). */
+typedef struct rsf_vivaldi rsf_vivaldi;
+
+/* n_members rows are allocated; this context updates members [shard_lo, shard_hi)
+ * (a full table is kept so peers on other shards can be read after an
+ * all-gather, see rsf_vivaldi_table).  seed keys the Philox streams that
+ * replace thread_rng (coordinate.rs:812-821). */
+int rsf_vivaldi_create(rsf_vivaldi** out, uint64_t n_members, uint64_t shard_lo, uint64_t shard_hi,
+                       uint32_t peer_slots, const rsf_coord_opts* opts, uint64_t seed, int device);
+int rsf_vivaldi_destroy(rsf_vivaldi* v);
+/* Use a caller-provided hipStream_t (NULL = the context's own stream). */
+int rsf_vivaldi_set_stream(rsf_vivaldi* v, void* hip_stream);
+int rsf_vivaldi_sync(rsf_vivaldi* v);
+
+/* = CoordinateClient::get_coordinate (coordinate.rs:406-408), for members
+ * [first, first+count); rows_out is host memory, count*row_stride doubles. */
+int rsf_vivaldi_get_coordinates(rsf_vivaldi* v, uint64_t first, uint64_t count, double* rows_out);
+/* = CoordinateClient::set_coordinate (coordinate.rs:412-415): returns
+ * RSF_ERR_DIM_MISMATCH / RSF_ERR_INVALID_COORD exactly as check_coordinate. */
+int rsf_vivaldi_set_coordinate(rsf_vivaldi* v, uint64_t member, const double* portion, uint32_t dim,
+                               double error, double adjustment, double height);
+/* = CoordinateClient::forget_node (coordinate.rs:455-457) */
+int rsf_vivaldi_forget_node(rsf_vivaldi* v, uint64_t member, uint32_t peer_slot);
+/* = CoordinateClient::stats().resets summed over the population (coordinate.rs:419-423) */
+int rsf_vivaldi_resets(rsf_vivaldi* v, uint64_t* resets_out);
+
+/* Batched CoordinateClient::update (coordinate.rs:462-499), one item per
+ * (member, peer observation).  All pointers are host memory.
+ *   member[i]     : the client being updated (members must be distinct in one batch)
+ *   peer_slot[i]  : latency-filter key of the observed node (< peer_slots)
+ *   other_rows    : n rows (row_stride doubles each) = the `other` Coordinate
+ *   other_dim     : n dims (NULL = all equal to the context's dimensionality)
+ *   rtt_ns[i]     : the observed rtt as Duration nanoseconds
+ *   round         : keys the Philox stream of unit_vector_at's random branch
+ *   status_out[i] : RSF_OK or the CoordinateError code of that item
+ *   rows_out      : optional; the updated coordinate (the reference returns a clone) */
+int rsf_vivaldi_update_batch(rsf_vivaldi* v, const uint32_t* member, const uint32_t* peer_slot,
+                             const double* other_rows, const uint32_t* other_dim,
+                             const uint64_t* rtt_ns, uint64_t n, uint32_t round,
+                             int32_t* status_out, double* rows_out);
+
+/* Batched Coordinate::distance_to = estimate_rtt (coordinate.rs:630-644).
+ * From member a[i]'s coordinate to member b[i]'s; ns_out[i] = Duration nanos.
+ * Host pointers. */
+int rsf_vivaldi_estimate_rtt_batch(rsf_vivaldi* v, const uint32_t* a, const uint32_t* b, uint64_t n,
+                                   uint64_t* ns_out);
+/* Same, device pointers, asynchronous (the throughput path). */
+int rsf_vivaldi_estimate_rtt_device(rsf_vivaldi* v, const uint32_t* a, const uint32_t* b, uint64_t n,
+                                    uint64_t* ns_out);
+
+/* One population round on the synthetic network of BASELINE configs 1/5:
+ * every member of the shard probes one Philox-chosen neighbour out of
+ * `peer_slots` fixed neighbours, observes rtt = true distance x (1 + U[0,0.1)),
+ * and runs CoordinateClient::update with the neighbour's coordinate as of the
+ * END OF THE PREVIOUS ROUND (the ack carries the peer's last coordinate,
+ * core/src/serf/delegate.rs:659-779).  Asynchronous; flips the table buffers. */
+int rsf_vivaldi_round(rsf_vivaldi* v, uint32_t round);
+
+/* Device pointer of the current full coordinate table (n_members rows) and of
+ * this shard's slice, for an all-gather between rounds on multi-GPU runs. */
+int rsf_vivaldi_table(rsf_vivaldi* v, double** table_out, uint64_t* row_stride_out);
+
+/* Ground truth of the synthetic network (for convergence reporting). */
+int rsf_vivaldi_true_rtt_ns(rsf_vivaldi* v, uint32_t a, uint32_t b, uint64_t* ns_out);
+
+/* ======================================================================== */
+/* Gossip round: Lamport-clock member-state merge + dissemination           */
+/* ======================================================================== */
+/* Model (DESIGN.md "Round model"): N members; S tracked subjects (members
+ * whose status churns).  Every member holds a view entry per subject
+ * (= members.states / recent_intents, core/src/types/member.rs:13-34), three
+ * Lamport clocks (types/src/clock.rs:134-182), three transmit-limited queues
+ * (core/src/serf/base.rs:178-189) and the user-event / query dedup rings
+ * (core/src/serf.rs:185-201). */
+
+/* view entry kind / member status / message type encodings */
+#define RSF_KIND_UNKNOWN 0      /* no state, no buffered intent */
+#define RSF_KIND_INTENT_JOIN 1  /* unknown member with a buffered join intent (upsert_intent) */
+#define RSF_KIND_INTENT_LEAVE 2 /* unknown member with a buffered leave intent */
+#define RSF_KIND_KNOWN 3        /* members.states entry exists */
+#define RSF_STATUS_NONE 0       /* MemberStatus (types/src/member.rs:16-27) */
+#define RSF_STATUS_ALIVE 1
+#define RSF_STATUS_LEAVING 2
+#define RSF_STATUS_LEFT 3
+#define RSF_STATUS_FAILED 4
+#define RSF_MSG_LEAVE 0         /* MessageType tags (types/src/message.rs:17-24) */
+#define RSF_MSG_JOIN 1
+#define RSF_MSG_USER_EVENT 3
+#define RSF_MSG_QUERY 4
+/* per-message result flags */
+#define RSF_F_REBROADCAST 1     /* handler returned true: notify_message re-queues (delegate.rs:297-304) */
+#define RSF_F_REFUTE 2          /* leave intent about self while alive: broadcast_join scheduled (base.rs:1437-1447) */
+#define RSF_F_PRUNE 4           /* prune requested (base.rs:1472-1523) */
+#define RSF_F_DELIVER 8         /* event/query delivered to the application (event_tx) */
+#define RSF_F_MEMBER_EVENT 16   /* a MemberEvent was emitted */
+
+typedef struct rsf_gossip_cfg {
+  uint64_t n_members;          /* N (global) */
+  uint64_t shard_lo, shard_hi; /* members owned by this context */
+  uint32_t n_subjects;         /* S */
+  uint32_t queue_cap;          /* slots per transmit-limited queue, 1..64 */
+  uint32_t event_buffer_size;  /* Options::event_buffer_size (default 512) */
+  uint32_t query_buffer_size;  /* Options::query_buffer_size (default 512) */
+  uint32_t slot_k;             /* events / query ids kept per dedup slot, 1..16 */
+  uint32_t fanout;             /* gossip targets per round (memberlist gossip_nodes), 1..8 */
+  uint32_t gossip_limit;       /* byte budget per gossip message (memberlist UDP budget) */
+  uint32_t gossip_overhead;    /* per-message compound overhead */
+  uint32_t retransmit_mult;    /* memberlist retransmit_mult (LAN: 4) */
+  uint32_t max_refute;         /* refutations buffered per subject per round, 1..4 */
+  uint32_t max_rumors;         /* rumor table capacity */
+  uint32_t _reserved;
+  uint64_t seed;               /* Philox key of peer selection */
+} rsf_gossip_cfg;
+
+/* One rumor (a broadcast message body; SerfBroadcast, core/src/broadcast.rs:153-183). 24 bytes. */
+typedef struct rsf_rumor {
+  uint64_t ltime;
+  uint64_t key;      /* user event: (name_id << 32) | payload_id; query: id */
+  uint32_t subject;  /* intents: subject slot */
+  uint8_t type;      /* RSF_MSG_* */
+  uint8_t flags;     /* leave: bit0 prune; query: bit0 no_broadcast */
+  uint16_t msg_len;  /* encoded length (queue byte budget); 0 = unused table entry */
+} rsf_rumor;
+
+/* Origination actions (api.rs / base.rs entry points) */
+#define RSF_ACT_JOIN_SELF 1   /* Serf::join -> broadcast_join(clock.time()) (base.rs:396-412) */
+#define RSF_ACT_LEAVE_SELF 2  /* Serf::leave (api.rs:473-503) */
+#define RSF_ACT_FORCE_LEAVE 3 /* force_leave / remove_failed_node (base.rs:474-500) */
+#define RSF_ACT_USER_EVENT 4  /* Serf::user_event (api.rs:247-315) */
+#define RSF_ACT_QUERY 5       /* query_in (base.rs:869-953) */
+typedef struct rsf_action {
+  uint32_t member, act, subject, name_len, payload_len, flags;
+  uint64_t key;
+} rsf_action;
+
+/* memberlist-detected transitions applied at every live member (NotifyJoin /
+ * NotifyLeave -> handle_node_join / handle_node_leave, base.rs:1167-1407) */
+#define RSF_ML_JOIN 1
+#define RSF_ML_LEAVE 2
+typedef struct rsf_ml_event {
+  uint32_t subject, kind;
+  uint32_t set_alive; /* 1: the subject's process becomes live first; 0: dead afterwards; 2: unchanged */
+  uint32_t _reserved;
+} rsf_ml_event;
+
+/* One received message for the direct-handler batch (notify_message dispatch). 32 bytes. */
+typedef struct rsf_msg {
+  uint32_t receiver; /* member id (must be in the shard) */
+  uint32_t subject;  /* intents: subject slot */
+  uint64_t ltime;
+  uint64_t key;
+  uint8_t type;      /* RSF_MSG_* */
+  uint8_t flags;     /* leave: prune; query: no_broadcast */
+  uint16_t _r0;
+  uint32_t _r1;
+} rsf_msg;
+
+typedef struct rsf_gossip rsf_gossip;
+
+int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device);
+int rsf_gossip_destroy(rsf_gossip* g);
+int rsf_gossip_set_stream(rsf_gossip* g, void* hip_stream);
+int rsf_gossip_sync(rsf_gossip* g);
+/* subject slot -> member id (S entries, host); defines which member a subject is */
+int rsf_gossip_set_subjects(rsf_gossip* g, const uint32_t* subject_member);
+/* initial view of every subject, replicated into every member's row (S entries each, host) */
+int rsf_gossip_init_views(rsf_gossip* g, const uint8_t* kind, const uint8_t* status, const uint64_t* ltime);
+/* one view entry (test / snapshot-restore hook) */
+int rsf_gossip_set_view(rsf_gossip* g, uint64_t member, uint32_t subject, uint8_t kind, uint8_t status,
+                        uint64_t ltime);
+/* process liveness of all N members (host, N bytes) */
+int rsf_gossip_set_alive(rsf_gossip* g, const uint8_t* alive);
+/* LamportClock values (e.g. restored from a snapshot, base.rs:195-204) */
+int rsf_gossip_set_clocks(rsf_gossip* g, uint64_t member, uint64_t clock, uint64_t event_clock,
+                          uint64_t query_clock);
+/* EventCore/QueryCore min_time (base.rs:777, 992) */
+int rsf_gossip_set_min_times(rsf_gossip* g, uint64_t member, uint64_t event_min, uint64_t query_min);
+/* SerfState of a member process (0 alive, 1 leaving, 2 left, 3 shutdown) */
+int rsf_gossip_set_serf_state(rsf_gossip* g, uint64_t member, uint8_t state);
+
+/* Direct handlers (notify_message, core/src/serf/delegate.rs:157-305):
+ * handle_node_join_intent / handle_node_leave_intent / handle_user_event /
+ * handle_query for n messages (host).  Messages of one receiver are applied in
+ * array order; receivers run in parallel.  flags_out[i] = RSF_F_*;
+ * refute_out[i] (optional) = the clock captured for a refuting broadcast_join.
+ * Re-queueing is left to the caller, as the reference's caller does it. */
+int rsf_gossip_apply_batch(rsf_gossip* g, const rsf_msg* msgs, uint64_t n, int32_t* flags_out,
+                           uint64_t* refute_out);
+
+/* One full round (single context): memberlist transitions, pending
+ * refutations, originations, emission (k peers x intent/query/event queues
+ * under the byte budget, broadcast_messages delegate.rs:307-374), exchange,
+ * and the canonical-order merge at every receiver.  ml/acts are host arrays;
+ * actions of one round must name distinct members. */
+int rsf_gossip_round(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml, uint32_t n_ml,
+                     const rsf_action* acts, uint32_t n_acts);
+
+/* Multi-GPU split of rsf_gossip_round (one context per GPU, members sharded):
+ *   begin : phases 1-3 for the shard; writes this round's rumor block, whose
+ *           entries are owned by exactly one shard (others zero) -> the caller
+ *           sums it across ranks (all-reduce over rsf_gossip_rumor_block)
+ *   emit  : emission + stable sort by global receiver; send_counts[w] records
+ *           go to shard w (shards are equal contiguous ranges); the packed
+ *           records ((receiver << 32) | rumor) are at rsf_gossip_send_buffer
+ *   merge : recv (device, n_recv packed records, concatenated in source-rank
+ *           order) -> stable sort by receiver -> canonical merge */
+int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml, uint32_t n_ml,
+                           const rsf_action* acts, uint32_t n_acts);
+int rsf_gossip_rumor_block(rsf_gossip* g, void** dev_ptr, uint64_t* bytes);
+int rsf_gossip_round_emit(rsf_gossip* g, uint32_t world, uint64_t* send_counts);
+int rsf_gossip_send_buffer(rsf_gossip* g, void** dev_ptr, uint64_t* capacity_records);
+int rsf_gossip_round_merge(rsf_gossip* g, const uint64_t* recv_dev, uint64_t n_recv);
+
+/* Inspection (host copies; synchronise).  Arrays are over the shard's members. */
+int rsf_gossip_dump_members(rsf_gossip* g, uint64_t* clock, uint64_t* event_clock, uint64_t* query_clock,
+                            uint64_t* digest, uint32_t* err, uint8_t* serf_state);
+int rsf_gossip_dump_view(rsf_gossip* g, uint64_t* ltime, uint8_t* status, uint8_t* kind);
+int rsf_gossip_dump_queues(rsf_gossip* g, uint32_t* rumor, uint32_t* seq, uint16_t* transmits, uint16_t* len,
+                           uint32_t* next_seq);
+int rsf_gossip_dump_buffers(rsf_gossip* g, uint64_t* eb_ltime, uint32_t* eb_cnt, uint64_t* eb_keys,
+                            uint64_t* qb_ltime, uint32_t* qb_cnt, uint32_t* qb_ids);
+int rsf_gossip_dump_rumors(rsf_gossip* g, uint32_t first, uint32_t count, rsf_rumor* out);
+int rsf_gossip_dump_refutes(rsf_gossip* g, uint32_t* count, uint64_t* ltimes);
+/* Phase profiling with HIP events on the context stream (no host sync while
+ * rounds run): ms_out[0..3] = summed device time of [memberlist + refute +
+ * originate], [emit kernel], [sort (+ exchange on multi-GPU)], [segment +
+ * merge kernel] over the rounds recorded since the last call. */
+int rsf_gossip_set_profiling(rsf_gossip* g, int on);
+int rsf_gossip_phase_times(rsf_gossip* g, double* ms_out, uint32_t* rounds_out);
+/* records merged by this shard since creation */
+int rsf_gossip_totals(rsf_gossip* g, uint64_t* merged_total);
+/* records emitted / merged by the last round (this shard) */
+int rsf_gossip_last_round_stats(rsf_gossip* g, uint64_t* records_sent, uint64_t* records_merged);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

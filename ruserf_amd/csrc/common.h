@@ -1,0 +1,69 @@
+// common.h — device/host helpers shared by the ruserf_amd HIP kernels.
+//
+// Philox4x32-10 is the counter-based generator that replaces the reference's
+// thread_rng (coordinate.rs:812-821) and memberlist's peer shuffles, so that a
+// run is a pure function of (seed, round, member, purpose, draw).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RSF_HD __host__ __device__ __forceinline__
+
+namespace rsf {
+
+// purpose tags (ctr[1] bits 24..31); the oracle uses the same numbering
+enum : uint32_t {
+  kPurposeUnit = 1,    // rand_f64 draws of unit_vector_at
+  kPurposePeer = 2,    // gossip peer selection (kRandomNodes model)
+  kPurposeVProbe = 3,  // Vivaldi synthetic probe: neighbour slot + jitter
+  kPurposeNbr = 5,     // Vivaldi fixed neighbour set
+  kPurposePos = 6,     // Vivaldi ground-truth positions
+};
+
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+
+RSF_HD u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                           uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+  }
+  return {c0, c1, c2, c3};
+}
+
+RSF_HD uint32_t mulhi32(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+}
+
+// `f64 as u64` in Rust: truncate toward zero, saturate, NaN -> 0
+RSF_HD uint64_t sat_u64(double x) {
+  if (!(x > 0.0)) return 0;
+  if (x >= 18446744073709551616.0) return UINT64_MAX;
+  return (uint64_t)x;
+}
+
+// Duration::as_secs_f64 = secs as f64 + nanos as f64 / 1e9
+RSF_HD double as_secs_f64(uint64_t ns) {
+  uint64_t secs = ns / 1000000000ull;
+  uint32_t nanos = (uint32_t)(ns - secs * 1000000000ull);
+  return (double)secs + (double)nanos / 1e9;
+}
+
+// f64::max / f64::min (non-NaN operand wins) == IEEE maxNum/minNum
+RSF_HD double rmax(double a, double b) { return fmax(a, b); }
+RSF_HD double rmin(double a, double b) { return fmin(a, b); }
+
+}  // namespace rsf

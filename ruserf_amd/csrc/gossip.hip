@@ -1,0 +1,1167 @@
+// gossip.hip — the batched gossip round on CDNA4 (gfx950): Lamport-clock
+// member-state merge + retransmit-limited dissemination.
+//
+// One round (see DESIGN.md "Round model"):
+//   ml_kernel        memberlist transitions at every live member (handle_node_join/leave)
+//   refute_kernel    broadcast_join for refutations spawned last round (base.rs:1437-1447)
+//   originate_kernel api entry points: join/leave/force_leave/user_event/query
+//   emit_kernel      ONE WAVE PER SENDER: the three queues live in registers (lane = queue slot);
+//                    k distinct live peers (Philox); per peer broadcast_messages drains
+//                    intent -> query -> event under the byte budget with wave argmin
+//                    selection (TransmitLimitedQueue::get_broadcasts model)
+//   radix sort       stable by receiver (hipCUB onesweep) -> canonical (sender, position) order
+//   segment_kernel   receiver segment bounds in the sorted record stream
+//   merge_kernel     ONE WAVE PER RECEIVER: lane 0 runs the handlers in canonical order, the
+//                    wave re-queues rebroadcasts (ballot for a free slot / wave max for the prune)
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/ruserf_amd.h"
+#include "common.h"
+#include "gossip_handlers.h"
+#include "rsf_internal.h"
+
+using namespace rsf;
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr uint32_t kSentinel = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    uint64_t t = __shfl_xor(v, o);
+    v = t < v ? t : v;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    uint64_t t = __shfl_xor(v, o);
+    v = t > v ? t : v;
+  }
+  return v;
+}
+
+// one transmit-limited queue held in registers: lane i owns slot i
+struct QRegs {
+  uint32_t r, sq, tl;  // rumor id (kEmpty = free), insertion seq, transmits | len << 16
+};
+
+__device__ __forceinline__ void q_load(const GCfg& c, const GState& s, uint64_t l, uint32_t q, uint32_t lane,
+                                       QRegs& Q) {
+  if (lane < c.qcap) {
+    uint64_t i = (l * 3 + q) * c.qcap + lane;
+    Q.r = s.q_rumor[i];
+    Q.sq = s.q_seq[i];
+    Q.tl = s.q_txlen[i];
+  } else {
+    Q.r = kEmpty;
+    Q.sq = 0;
+    Q.tl = 0;
+  }
+}
+__device__ __forceinline__ void q_store(const GCfg& c, const GState& s, uint64_t l, uint32_t q, uint32_t lane,
+                                        const QRegs& Q, bool with_seq) {
+  if (lane < c.qcap) {
+    uint64_t i = (l * 3 + q) * c.qcap + lane;
+    s.q_rumor[i] = Q.r;
+    s.q_txlen[i] = Q.tl;
+    if (with_seq) s.q_seq[i] = Q.sq;
+  }
+}
+
+// wave-parallel insert: identical slot choice to queue_insert_serial
+__device__ __forceinline__ void q_insert_wave(const GCfg& c, QRegs& Q, uint32_t lane, uint32_t rid, uint32_t len,
+                                              uint32_t seq) {
+  const bool valid = lane < c.qcap;
+  uint64_t empty = __ballot(valid && Q.r == kEmpty);
+  int slot;
+  if (empty) {
+    slot = __ffsll((long long)empty) - 1;
+  } else {
+    uint64_t k = valid ? tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq) : 0;
+    uint64_t kmax = wave_max_u64(k);
+    if (tlq_key(0, len, seq) > kmax) return;
+    slot = __ffsll((long long)__ballot(valid && k == kmax)) - 1;
+  }
+  if ((int)lane == slot) {
+    Q.r = rid;
+    Q.sq = seq;
+    Q.tl = len << 16;
+  }
+}
+
+// one get_broadcasts call on a register-resident queue; returns bytes used
+__device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uint32_t lane, int64_t limit,
+                                                    uint32_t recv, uint32_t* stage_key, uint32_t* stage_val,
+                                                    uint64_t out_base, uint32_t& nrec, uint32_t& err) {
+  bool picked = false;
+  int64_t used = 0;
+  const bool valid = lane < c.qcap;
+  for (;;) {
+    int64_t free_b = limit - used - (int64_t)c.overhead;
+    if (free_b <= 0) break;
+    uint32_t len = Q.tl >> 16;
+    bool elig = valid && Q.r != kEmpty && !picked && (int64_t)len <= free_b;
+    uint64_t key = elig ? tlq_key(Q.tl & 0xFFFF, len, Q.sq) : ~0ull;
+    uint64_t kmin = wave_min_u64(key);
+    if (kmin == ~0ull) break;
+    int win = __ffsll((long long)__ballot(key == kmin)) - 1;
+    uint32_t rid = __shfl(Q.r, win);
+    uint32_t ln = __shfl(len, win);
+    if ((int)lane == win) picked = true;
+    if (nrec < c.cap_t) {
+      if (lane == 0) {
+        stage_key[out_base + nrec] = recv;
+        stage_val[out_base + nrec] = rid;
+      }
+    } else {
+      err |= kErrStage;
+    }
+    nrec++;
+    used += (int64_t)c.overhead + ln;
+  }
+  if (picked) {
+    uint32_t tx = Q.tl & 0xFFFF;
+    if (tx + 1 >= c.tx_limit) Q.r = kEmpty;
+    else Q.tl = Q.tl + 1;
+  }
+  return used;
+}
+
+// ---------------------------------------------------------------- kernels
+__global__ void __launch_bounds__(256) ml_kernel(GCfg c, GState s, const rsf_ml_event* __restrict__ ml,
+                                                 uint32_t n_ml) {
+  uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= c.n_loc) return;
+  const uint32_t m = (uint32_t)(c.lo + l);
+  bool al = s.alive[m] != 0;
+  MRegs r;
+  load_regs(s, l, r);
+  bool touched = false;
+  for (uint32_t e = 0; e < n_ml; ++e) {
+    uint32_t subj = ml[e].subject, sm = s.subj_member[subj];
+    if (sm == m && ml[e].set_alive == 1) {
+      al = true;
+      r.serf_state = kSerfAlive;
+      touched = true;
+    }
+    if (al && m != sm) {
+      ViewE* v = s.view + l * c.S + subj;
+      if (ml[e].kind == RSF_ML_JOIN) h_node_join(v, r, subj);
+      else h_node_leave(v, r, subj);
+      touched = true;
+    }
+    if (sm == m && ml[e].set_alive == 0) al = false;
+  }
+  if (touched) store_regs(s, l, r);
+  s.alive[m] = al ? 1 : 0;
+}
+
+// liveness of every member (replicated array): last set_alive per subject wins
+__global__ void ml_alive_kernel(GState s, const rsf_ml_event* __restrict__ ml, uint32_t n_ml) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (uint32_t e = 0; e < n_ml; ++e) {
+    uint32_t sm = s.subj_member[ml[e].subject];
+    if (ml[e].set_alive == 1) s.alive[sm] = 1;
+    if (ml[e].set_alive == 0) s.alive[sm] = 0;
+  }
+}
+
+__device__ __forceinline__ void put_rumor(const GState& s, uint32_t rid, uint8_t type, uint8_t flags, uint32_t subj,
+                                          uint64_t L, uint64_t key, uint32_t len) {
+  rsf_rumor ru;
+  ru.ltime = L;
+  ru.key = key;
+  ru.subject = subj;
+  ru.type = type;
+  ru.flags = flags;
+  ru.msg_len = (uint16_t)len;
+  s.rumors[rid] = ru;
+}
+
+__device__ __forceinline__ void push_refute(const GCfg& c, const GState& s, MRegs& r, uint64_t ltime) {
+  if (r.subj < 0) return;
+  uint32_t cnt = s.refute_cnt[r.subj];
+  if (cnt < c.max_refute) {
+    s.refute_ltime[(uint64_t)r.subj * c.max_refute + cnt] = ltime;
+    s.refute_cnt[r.subj] = cnt + 1;
+  } else {
+    r.err |= kErrRefute;
+  }
+}
+
+// broadcast_join (base.rs:396-412)
+__device__ __forceinline__ void broadcast_join(const GCfg& c, const GState& s, uint64_t l, MRegs& r, uint64_t L,
+                                               uint32_t rid) {
+  uint32_t subj = (uint32_t)r.subj;
+  witness(r.clock, L);
+  h_join_intent(s.view + l * c.S + subj, r, L);
+  uint32_t len = msg_len(RSF_MSG_JOIN, L, 0, 0);
+  put_rumor(s, rid, RSF_MSG_JOIN, 0, subj, L, 0, len);
+  queue_insert_serial(c, s, l, kQIntent, rid, len);
+}
+
+__global__ void __launch_bounds__(256) refute_kernel(GCfg c, GState s, uint32_t base) {
+  uint32_t subj = blockIdx.x * blockDim.x + threadIdx.x;
+  if (subj >= c.S) return;
+  uint32_t m = s.subj_member[subj];
+  if (m < c.lo || m >= c.lo + c.n_loc) return;
+  uint32_t cnt = s.refute_cnt[subj];
+  if (!cnt) return;
+  s.refute_cnt[subj] = 0;
+  if (!s.alive[m]) return;
+  uint64_t l = m - c.lo;
+  MRegs r;
+  load_regs(s, l, r);
+  for (uint32_t i = 0; i < cnt; ++i)
+    broadcast_join(c, s, l, r, s.refute_ltime[(uint64_t)subj * c.max_refute + i], base + subj * c.max_refute + i);
+  store_regs(s, l, r);
+}
+
+__global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const rsf_action* __restrict__ acts,
+                                                        uint32_t n_acts, uint32_t abase) {
+  uint32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= n_acts) return;
+  rsf_action x = acts[a];
+  uint32_t m = x.member;
+  if (m < c.lo || m >= c.lo + c.n_loc || !s.alive[m]) return;
+  uint64_t l = m - c.lo;
+  uint32_t rid = abase + a;
+  MRegs r;
+  load_regs(s, l, r);
+  uint64_t ref = 0;
+  switch (x.act) {
+    case RSF_ACT_JOIN_SELF:
+      r.serf_state = kSerfAlive;
+      broadcast_join(c, s, l, r, r.clock, rid);
+      break;
+    case RSF_ACT_LEAVE_SELF: {
+      r.serf_state = kSerfLeaving;
+      uint64_t lt = r.clock;
+      r.clock++;
+      uint32_t subj = (uint32_t)r.subj;
+      h_leave_intent(s.view + l * c.S + subj, r, subj, lt, false, ref);
+      uint32_t len = msg_len(RSF_MSG_LEAVE, lt, 0, 0);
+      put_rumor(s, rid, RSF_MSG_LEAVE, 0, subj, lt, 0, len);
+      queue_insert_serial(c, s, l, kQIntent, rid, len);
+      break;
+    }
+    case RSF_ACT_FORCE_LEAVE: {
+      uint64_t lt = r.clock;
+      bool prune = x.flags & 1;
+      int f = h_leave_intent(s.view + l * c.S + x.subject, r, x.subject, lt, prune, ref);
+      if (f & RSF_F_REFUTE) push_refute(c, s, r, ref);
+      uint32_t len = msg_len(RSF_MSG_LEAVE, lt, 0, 0);
+      put_rumor(s, rid, RSF_MSG_LEAVE, prune ? 1 : 0, x.subject, lt, 0, len);
+      queue_insert_serial(c, s, l, kQIntent, rid, len);
+      break;
+    }
+    case RSF_ACT_USER_EVENT: {
+      uint64_t lt = r.eclock;
+      r.eclock++;
+      h_user_event(c, s, l, r, lt, x.key);
+      uint32_t len = msg_len(RSF_MSG_USER_EVENT, lt, x.name_len, x.payload_len);
+      put_rumor(s, rid, RSF_MSG_USER_EVENT, 0, 0, lt, x.key, len);
+      queue_insert_serial(c, s, l, kQEvent, rid, len);
+      break;
+    }
+    case RSF_ACT_QUERY: {
+      uint64_t lt = r.qclock;
+      bool nb = x.flags & 1;
+      h_query(c, s, l, r, lt, (uint32_t)x.key, nb);
+      uint32_t len = msg_len(RSF_MSG_QUERY, lt, x.name_len, x.payload_len);
+      put_rumor(s, rid, RSF_MSG_QUERY, nb ? 1 : 0, 0, lt, (uint32_t)x.key, len);
+      queue_insert_serial(c, s, l, kQQuery, rid, len);
+      break;
+    }
+    default: break;
+  }
+  store_regs(s, l, r);
+}
+
+__global__ void __launch_bounds__(256) emit_kernel(GCfg c, GState s, uint32_t round, uint32_t* __restrict__ stage_key,
+                                                   uint32_t* __restrict__ stage_val) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x / kWave);
+  if (l >= c.n_loc) return;
+  const uint32_t m = (uint32_t)(c.lo + l);
+  if (!s.alive[m]) return;
+  // kRandomNodes model: attempts a = 0,1,2,... in order, live, distinct, != m
+  uint32_t peers[8];
+  uint32_t np = 0;
+  const uint32_t attempts = 64 * c.fanout;
+  for (uint32_t b0 = 0; b0 < attempts && np < c.fanout; b0 += kWave) {
+    uint32_t a = b0 + lane;
+    uint32_t p = 0;
+    bool ok = false;
+    if (a < attempts) {
+      u32x4 o = philox4x32_10(a, kPurposePeer << 24, m, round, c.k0, c.k1);
+      p = mulhi32(o.x, (uint32_t)(c.N - 1));
+      if (p >= m) p++;
+      ok = s.alive[p] != 0;
+    }
+    uint64_t mask = __ballot(ok);
+    while (mask && np < c.fanout) {
+      int li = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      uint32_t cand = __shfl(p, li);
+      bool dup = false;
+      for (uint32_t j = 0; j < np; ++j) dup |= (peers[j] == cand);
+      if (!dup) peers[np++] = cand;
+    }
+  }
+  QRegs Q0, Q1, Q2;
+  q_load(c, s, l, 0, lane, Q0);
+  q_load(c, s, l, 1, lane, Q1);
+  q_load(c, s, l, 2, lane, Q2);
+  uint32_t err = 0;
+  for (uint32_t j = 0; j < np; ++j) {
+    uint32_t recv = peers[j];
+    uint64_t out_base = (l * c.fanout + j) * c.cap_t;
+    uint32_t nrec = 0;
+    int64_t used = 0;
+    used += q_get_broadcasts(c, Q0, lane, (int64_t)c.limit - used, recv, stage_key, stage_val, out_base, nrec, err);
+    used += q_get_broadcasts(c, Q1, lane, (int64_t)c.limit - used, recv, stage_key, stage_val, out_base, nrec, err);
+    used += q_get_broadcasts(c, Q2, lane, (int64_t)c.limit - used, recv, stage_key, stage_val, out_base, nrec, err);
+  }
+  q_store(c, s, l, 0, lane, Q0, false);
+  q_store(c, s, l, 1, lane, Q1, false);
+  q_store(c, s, l, 2, lane, Q2, false);
+  if (err && lane == 0) s.err[l] |= err;
+}
+
+__global__ void __launch_bounds__(256) segment_kernel(const uint32_t* __restrict__ keys, uint64_t n, uint64_t lo,
+                                                      uint32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_end,
+                                                      unsigned long long* /*unused*/) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k = keys[i];
+  if (k == kSentinel) return;
+  if (i == 0 || keys[i - 1] != k) seg_start[k - lo] = (uint32_t)i;
+  if (i + 1 == n || keys[i + 1] != k) seg_end[k - lo] = (uint32_t)(i + 1);
+}
+
+__global__ void __launch_bounds__(256) first_sentinel_kernel(const uint32_t* __restrict__ keys, uint64_t n,
+                                                             unsigned long long* n_valid) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (keys[i] == kSentinel && (i == 0 || keys[i - 1] != kSentinel)) *n_valid = i;
+}
+
+__global__ void __launch_bounds__(256) merge_kernel(GCfg c, GState s, const uint32_t* __restrict__ vals,
+                                                    const uint32_t* __restrict__ seg_start,
+                                                    const uint32_t* __restrict__ seg_end) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x / kWave);
+  if (l >= c.n_loc) return;
+  const uint32_t m = (uint32_t)(c.lo + l);
+  const uint32_t st = seg_start[l], en = seg_end[l];
+  if (st >= en || !s.alive[m]) return;
+  QRegs Q0, Q1, Q2;
+  q_load(c, s, l, 0, lane, Q0);
+  q_load(c, s, l, 1, lane, Q1);
+  q_load(c, s, l, 2, lane, Q2);
+  uint32_t nseq0 = s.q_next_seq[l * 3 + 0], nseq1 = s.q_next_seq[l * 3 + 1], nseq2 = s.q_next_seq[l * 3 + 2];
+  MRegs r;
+  load_regs(s, l, r);
+  ViewE* vrow = s.view + l * c.S;
+  for (uint32_t i = st; i < en; ++i) {
+    const uint32_t rid = vals[i];
+    const rsf_rumor ru = s.rumors[rid];
+    int f = 0;
+    if (lane == 0) {
+      uint64_t ref = 0;
+      switch (ru.type) {
+        case RSF_MSG_JOIN: f = h_join_intent(vrow + ru.subject, r, ru.ltime); break;
+        case RSF_MSG_LEAVE: f = h_leave_intent(vrow + ru.subject, r, ru.subject, ru.ltime, ru.flags & 1, ref); break;
+        case RSF_MSG_USER_EVENT: f = h_user_event(c, s, l, r, ru.ltime, ru.key); break;
+        case RSF_MSG_QUERY: f = h_query(c, s, l, r, ru.ltime, (uint32_t)ru.key, ru.flags & 1); break;
+        default: break;
+      }
+      if (f & RSF_F_REFUTE) push_refute(c, s, r, ref);
+    }
+    f = __shfl(f, 0);
+    if (f & RSF_F_REBROADCAST) {
+      uint32_t q = queue_of(ru.type);
+      if (q == kQIntent) q_insert_wave(c, Q0, lane, rid, ru.msg_len, nseq0++);
+      else if (q == kQQuery) q_insert_wave(c, Q1, lane, rid, ru.msg_len, nseq1++);
+      else q_insert_wave(c, Q2, lane, rid, ru.msg_len, nseq2++);
+    }
+  }
+  q_store(c, s, l, 0, lane, Q0, true);
+  q_store(c, s, l, 1, lane, Q1, true);
+  q_store(c, s, l, 2, lane, Q2, true);
+  if (lane == 0) {
+    store_regs(s, l, r);
+    s.q_next_seq[l * 3 + 0] = nseq0;
+    s.q_next_seq[l * 3 + 1] = nseq1;
+    s.q_next_seq[l * 3 + 2] = nseq2;
+  }
+}
+
+// direct-handler batch: one thread per receiver segment (array order within a receiver)
+__global__ void __launch_bounds__(256) apply_kernel(GCfg c, GState s, const rsf_msg* __restrict__ msgs,
+                                                    const uint32_t* __restrict__ order,
+                                                    const uint32_t* __restrict__ seg_start,
+                                                    const uint32_t* __restrict__ seg_end, int32_t* __restrict__ flags,
+                                                    uint64_t* __restrict__ refute) {
+  uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= c.n_loc) return;
+  uint32_t st = seg_start[l], en = seg_end[l];
+  if (st >= en) return;
+  MRegs r;
+  load_regs(s, l, r);
+  ViewE* vrow = s.view + l * c.S;
+  for (uint32_t i = st; i < en; ++i) {
+    uint32_t k = order[i];
+    rsf_msg x = msgs[k];
+    uint64_t ref = 0;
+    int f = 0;
+    switch (x.type) {
+      case RSF_MSG_JOIN: f = h_join_intent(vrow + x.subject, r, x.ltime); break;
+      case RSF_MSG_LEAVE: f = h_leave_intent(vrow + x.subject, r, x.subject, x.ltime, x.flags & 1, ref); break;
+      case RSF_MSG_USER_EVENT: f = h_user_event(c, s, l, r, x.ltime, x.key); break;
+      case RSF_MSG_QUERY: f = h_query(c, s, l, r, x.ltime, (uint32_t)x.key, x.flags & 1); break;
+      default: f = 0; break;
+    }
+    flags[k] = f;
+    refute[k] = ref;
+  }
+  store_regs(s, l, r);
+}
+
+__global__ void keys_from_msgs_kernel(const rsf_msg* __restrict__ msgs, uint64_t n, uint64_t lo,
+                                      uint32_t* __restrict__ keys, uint32_t* __restrict__ idx) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  keys[i] = (uint32_t)(msgs[i].receiver - lo);
+  idx[i] = (uint32_t)i;
+}
+
+__global__ void init_views_kernel(ViewE* view, uint64_t n_loc, uint32_t S, const uint8_t* kind,
+                                  const uint8_t* status, const uint64_t* ltime) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_loc * S) return;
+  uint32_t subj = (uint32_t)(i % S);
+  ViewE v;
+  v.ltime = ltime[subj];
+  v.meta = vmeta(status[subj], kind[subj]);
+  v._pad = 0;
+  view[i] = v;
+}
+
+__global__ void fill_u64_kernel(uint64_t* p, uint64_t n, uint64_t v) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+__global__ void shard_bounds_kernel(const uint32_t* __restrict__ keys, const unsigned long long* n_valid,
+                                    uint64_t per, uint32_t world, unsigned long long* __restrict__ bounds) {
+  uint32_t w = threadIdx.x;
+  if (w > world) return;
+  uint64_t nv = *n_valid;
+  uint64_t target = (uint64_t)w * per;  // first key >= target
+  uint64_t lo = 0, hi = nv;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) / 2;
+    if (keys[mid] < target) lo = mid + 1;
+    else hi = mid;
+  }
+  bounds[w] = (w == world) ? nv : lo;
+}
+
+__global__ void pack_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                            const unsigned long long* n_valid, uint64_t* __restrict__ out) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *n_valid) return;
+  out[i] = ((uint64_t)keys[i] << 32) | vals[i];
+}
+
+__global__ void unpack_kernel(const uint64_t* __restrict__ in, uint64_t n, uint32_t* __restrict__ keys,
+                              uint32_t* __restrict__ vals) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t x = in[i];
+  keys[i] = (uint32_t)(x >> 32);
+  vals[i] = (uint32_t)x;
+}
+
+__global__ void accumulate_kernel(unsigned long long* counters) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) counters[60] += counters[0];
+}
+
+inline unsigned grid1(uint64_t n, unsigned b = 256) { return (unsigned)((n + b - 1) / b); }
+inline int bits_for(uint64_t n) {
+  int b = 1;
+  while (b < 32 && ((1ull << b) <= n)) ++b;
+  return b;
+}
+
+}  // namespace
+
+struct rsf_gossip {
+  int device = 0;
+  hipStream_t own = nullptr, stream = nullptr;
+  GCfg c{};
+  GState s{};
+  uint32_t n_rumors = 0, max_rumors = 0;
+  uint32_t round_base = 0, round_abase = 0, round_need = 0;
+  // per-round device lists
+  rsf_ml_event* d_ml = nullptr;
+  rsf_action* d_acts = nullptr;
+  uint32_t cap_ml = 0, cap_acts = 0;
+  // record pipeline
+  uint64_t stage_cap = 0, recv_cap = 0;
+  uint32_t *stage_key = nullptr, *stage_val = nullptr, *sort_key = nullptr, *sort_val = nullptr;
+  uint32_t *seg_start = nullptr, *seg_end = nullptr;
+  uint64_t* send_buf = nullptr;
+  unsigned long long* d_counters = nullptr;  // [0] n_valid, [1..] shard bounds
+  void* sort_tmp = nullptr;
+  size_t sort_tmp_bytes = 0;
+  int end_bit = 32;
+  uint64_t last_sent = 0, last_merged = 0;
+  uint32_t cur_round = 0;
+  bool merged_from_stage = true;
+  uint64_t total_merged_host = 0;  // multi-GPU merges (n_recv known on host)
+  // phase profiling: marks per round [begin, after begin, after emit, after sort, after merge]
+  bool profiling = false;
+  static constexpr int kMarks = 5, kMaxProfRounds = 256;
+  hipEvent_t ev[kMaxProfRounds][kMarks] = {};
+  int prof_rounds = 0;
+  bool events_made = false;
+  DeviceScratch scratch;
+};
+
+static int gerr(const char* m) { return rsf::set_error(RSF_ERR_ARG, m); }
+
+static void mark(rsf_gossip* g, int k) {
+  if (!g->profiling || g->prof_rounds >= rsf_gossip::kMaxProfRounds) return;
+  hipEventRecord(g->ev[g->prof_rounds][k], g->stream);
+  if (k == rsf_gossip::kMarks - 1) g->prof_rounds++;
+}
+
+static int ensure_lists(rsf_gossip* g, uint32_t n_ml, uint32_t n_acts) {
+  int rc;
+  if (n_ml > g->cap_ml) {
+    hipFree(g->d_ml);
+    g->d_ml = nullptr;
+    uint32_t cap = std::max<uint32_t>(n_ml, 64);
+    if ((rc = dmalloc((void**)&g->d_ml, cap * sizeof(rsf_ml_event)))) return rc;
+    g->cap_ml = cap;
+  }
+  if (n_acts > g->cap_acts) {
+    hipFree(g->d_acts);
+    g->d_acts = nullptr;
+    uint32_t cap = std::max<uint32_t>(n_acts, 1024);
+    if ((rc = dmalloc((void**)&g->d_acts, (size_t)cap * sizeof(rsf_action)))) return rc;
+    g->cap_acts = cap;
+  }
+  return RSF_OK;
+}
+
+static int sort_pairs(rsf_gossip* g, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout,
+                      uint64_t n) {
+  size_t tmp = g->sort_tmp_bytes;
+  RSF_HIP(hipcub::DeviceRadixSort::SortPairs(g->sort_tmp, tmp, kin, kout, vin, vout, (int)n, 0, g->end_bit,
+                                             g->stream));
+  return RSF_OK;
+}
+
+extern "C" {
+
+int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
+  if (!out || !cfg) return gerr("null argument");
+  *out = nullptr;
+  const uint64_t N = cfg->n_members;
+  if (N < 2 || N >= 0xFFFFFFFFull) return gerr("n_members must be in [2, 2^32-1)");
+  if (cfg->shard_lo >= cfg->shard_hi || cfg->shard_hi > N) return gerr("bad shard range");
+  if (cfg->n_subjects == 0 || cfg->n_subjects > N) return gerr("n_subjects must be in [1, n_members]");
+  if (cfg->queue_cap == 0 || cfg->queue_cap > 64) return gerr("queue_cap must be 1..64");
+  if (cfg->event_buffer_size == 0 || cfg->query_buffer_size == 0) return gerr("dedup buffers must be non-empty");
+  if (cfg->slot_k == 0 || cfg->slot_k > 16) return gerr("slot_k must be 1..16");
+  if (cfg->fanout == 0 || cfg->fanout > 8 || cfg->fanout >= N) return gerr("fanout must be 1..8 and < n_members");
+  if (cfg->gossip_limit > 0xFFFFFF || cfg->gossip_overhead > 0xFFFF) return gerr("gossip budget too large");
+  if (cfg->max_refute == 0 || cfg->max_refute > 4) return gerr("max_refute must be 1..4");
+  if (cfg->max_rumors == 0) return gerr("max_rumors must be > 0");
+  RSF_HIP(hipSetDevice(device));
+  rsf_gossip* g = new (std::nothrow) rsf_gossip();
+  if (!g) return rsf::set_error(RSF_ERR_NOMEM, "host allocation failed");
+  g->device = device;
+  GCfg& c = g->c;
+  c.N = N;
+  c.lo = cfg->shard_lo;
+  c.n_loc = cfg->shard_hi - cfg->shard_lo;
+  c.S = cfg->n_subjects;
+  c.qcap = cfg->queue_cap;
+  c.ebuf = cfg->event_buffer_size;
+  c.qbuf = cfg->query_buffer_size;
+  c.slot_k = cfg->slot_k;
+  c.fanout = cfg->fanout;
+  c.limit = cfg->gossip_limit;
+  c.overhead = cfg->gossip_overhead;
+  {  // memberlist retransmitLimit = mult * ceil(log10(n+1))
+    uint64_t x = N + 1, p = 1;
+    uint32_t d = 0;
+    while (p < x) {
+      p *= 10;
+      d++;
+    }
+    c.tx_limit = cfg->retransmit_mult * d;
+  }
+  c.max_refute = cfg->max_refute;
+  {
+    uint64_t per = c.limit / (c.overhead + kMinMsgLen);
+    c.cap_t = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(3ull * c.qcap, per));
+  }
+  c.k0 = (uint32_t)cfg->seed;
+  c.k1 = (uint32_t)(cfg->seed >> 32);
+  g->max_rumors = cfg->max_rumors;
+  g->end_bit = bits_for(N);
+  auto fail = [&](int code) {
+    rsf_gossip_destroy(g);
+    return code;
+  };
+  if (hipStreamCreateWithFlags(&g->own, hipStreamNonBlocking) != hipSuccess)
+    return fail(rsf::set_error(RSF_ERR_HIP, "hipStreamCreate failed"));
+  g->stream = g->own;
+  GState& s = g->s;
+  const uint64_t n = c.n_loc, S = c.S;
+  int rc;
+#define GA(p, bytes) ((rc = dmalloc((void**)&(p), (bytes))) != 0)
+  if (GA(s.clock, n * 8) || GA(s.eclock, n * 8) || GA(s.qclock, n * 8) || GA(s.emin, n * 8) || GA(s.qmin, n * 8) ||
+      GA(s.digest, n * 8) || GA(s.err, n * 4) || GA(s.alive, N) || GA(s.serf_state, n) || GA(s.member_subj, n * 4) ||
+      GA(s.subj_member, S * 4) || GA(s.refute_cnt, S * 4) || GA(s.refute_ltime, S * c.max_refute * 8) ||
+      GA(s.view, n * S * sizeof(ViewE)) || GA(s.q_rumor, n * 3 * c.qcap * 4) || GA(s.q_seq, n * 3 * c.qcap * 4) ||
+      GA(s.q_txlen, n * 3 * c.qcap * 4) || GA(s.q_next_seq, n * 3 * 4) || GA(s.eb_ltime, n * c.ebuf * 8) ||
+      GA(s.eb_cnt, n * c.ebuf * 4) || GA(s.eb_keys, n * c.ebuf * c.slot_k * 8) || GA(s.qb_ltime, n * c.qbuf * 8) ||
+      GA(s.qb_cnt, n * c.qbuf * 4) || GA(s.qb_ids, n * c.qbuf * c.slot_k * 4) ||
+      GA(s.rumors, (size_t)cfg->max_rumors * sizeof(rsf_rumor)))
+    return fail(rc);
+  g->stage_cap = n * c.fanout * c.cap_t;
+  g->recv_cap = g->stage_cap + g->stage_cap / 2 + 4096;
+  const uint64_t pipe = std::max(g->stage_cap, g->recv_cap);
+  if (GA(g->stage_key, pipe * 4) || GA(g->stage_val, pipe * 4) || GA(g->sort_key, pipe * 4) ||
+      GA(g->sort_val, pipe * 4) || GA(g->seg_start, n * 4) || GA(g->seg_end, n * 4) || GA(g->send_buf, pipe * 8) ||
+      GA(g->d_counters, 64 * 8))
+    return fail(rc);
+#undef GA
+  size_t tmp = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, g->stage_key, g->sort_key, g->stage_val, g->sort_val,
+                                         (int)pipe, 0, g->end_bit, g->stream) != hipSuccess)
+    return fail(rsf::set_error(RSF_ERR_HIP, "hipcub sort sizing failed"));
+  g->sort_tmp_bytes = tmp;
+  if ((rc = dmalloc(&g->sort_tmp, tmp))) return fail(rc);
+  hipStream_t st = g->stream;
+  bool ok = true;
+  auto ms = [&](void* p, int v, size_t b) { ok = ok && hipMemsetAsync(p, v, b, st) == hipSuccess; };
+  ms(s.emin, 0, n * 8);
+  ms(s.qmin, 0, n * 8);
+  ms(s.digest, 0, n * 8);
+  ms(s.err, 0, n * 4);
+  ms(s.alive, 1, N);
+  ms(s.serf_state, 0, n);
+  ms(s.member_subj, 0xFF, n * 4);
+  ms(s.subj_member, 0, S * 4);
+  ms(s.refute_cnt, 0, S * 4);
+  ms(s.refute_ltime, 0, S * c.max_refute * 8);
+  ms(s.view, 0, n * S * sizeof(ViewE));
+  ms(s.q_rumor, 0xFF, n * 3 * c.qcap * 4);
+  ms(s.q_seq, 0, n * 3 * c.qcap * 4);
+  ms(s.q_txlen, 0, n * 3 * c.qcap * 4);
+  ms(s.q_next_seq, 0, n * 3 * 4);
+  ms(s.eb_ltime, 0, n * c.ebuf * 8);
+  ms(s.eb_cnt, 0, n * c.ebuf * 4);
+  ms(s.eb_keys, 0, n * c.ebuf * c.slot_k * 8);
+  ms(s.qb_ltime, 0, n * c.qbuf * 8);
+  ms(s.qb_cnt, 0, n * c.qbuf * 4);
+  ms(s.qb_ids, 0, n * c.qbuf * c.slot_k * 4);
+  ms(s.rumors, 0, (size_t)cfg->max_rumors * sizeof(rsf_rumor));
+  if (!ok) return fail(rsf::set_error(RSF_ERR_HIP, "context initialisation failed"));
+  // Serf::new increments every clock once (base.rs:195-199)
+  hipLaunchKernelGGL(fill_u64_kernel, dim3(grid1(n)), dim3(256), 0, st, s.clock, n, 1ull);
+  hipLaunchKernelGGL(fill_u64_kernel, dim3(grid1(n)), dim3(256), 0, st, s.eclock, n, 1ull);
+  hipLaunchKernelGGL(fill_u64_kernel, dim3(grid1(n)), dim3(256), 0, st, s.qclock, n, 1ull);
+  if (hipStreamSynchronize(st) != hipSuccess) return fail(rsf::set_error(RSF_ERR_HIP, "context init sync failed"));
+  *out = g;
+  return RSF_OK;
+}
+
+int rsf_gossip_destroy(rsf_gossip* g) {
+  if (!g) return RSF_OK;
+  hipSetDevice(g->device);
+  if (g->stream) hipStreamSynchronize(g->stream);
+  GState& s = g->s;
+  void* ptrs[] = {s.clock,  s.eclock,      s.qclock,       s.emin,        s.qmin,     s.digest,     s.err,
+                  s.alive,  s.serf_state,  s.member_subj,  s.subj_member, s.refute_cnt, s.refute_ltime, s.view,
+                  s.q_rumor, s.q_seq,      s.q_txlen,      s.q_next_seq,  s.eb_ltime, s.eb_cnt,     s.eb_keys,
+                  s.qb_ltime, s.qb_cnt,    s.qb_ids,       s.rumors,      g->d_ml,    g->d_acts,    g->stage_key,
+                  g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters,
+                  g->sort_tmp};
+  for (void* p : ptrs)
+    if (p) hipFree(p);
+  g->scratch.release();
+  if (g->events_made)
+    for (auto& row : g->ev)
+      for (auto& e : row) hipEventDestroy(e);
+  if (g->own) hipStreamDestroy(g->own);
+  delete g;
+  return RSF_OK;
+}
+
+int rsf_gossip_set_stream(rsf_gossip* g, void* st) {
+  if (!g) return gerr("null context");
+  g->stream = st ? (hipStream_t)st : g->own;
+  return RSF_OK;
+}
+
+int rsf_gossip_sync(rsf_gossip* g) {
+  if (!g) return gerr("null context");
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  return RSF_OK;
+}
+
+int rsf_gossip_set_subjects(rsf_gossip* g, const uint32_t* subj_member) {
+  if (!g || !subj_member) return gerr("null argument");
+  const GCfg& c = g->c;
+  std::vector<int32_t> ms(c.n_loc, -1);
+  std::vector<uint8_t> seen(c.N, 0);
+  for (uint32_t s = 0; s < c.S; ++s) {
+    uint32_t m = subj_member[s];
+    if (m >= c.N) return gerr("subject member out of range");
+    if (seen[m]++) return gerr("a member is the subject of two slots");
+    if (m >= c.lo && m < c.lo + c.n_loc) ms[m - c.lo] = (int32_t)s;
+  }
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemcpyAsync(g->s.subj_member, subj_member, c.S * 4, hipMemcpyHostToDevice, g->stream));
+  RSF_HIP(hipMemcpyAsync(g->s.member_subj, ms.data(), c.n_loc * 4, hipMemcpyHostToDevice, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  return RSF_OK;
+}
+
+int rsf_gossip_init_views(rsf_gossip* g, const uint8_t* kind, const uint8_t* status, const uint64_t* ltime) {
+  if (!g || !kind || !status || !ltime) return gerr("null argument");
+  const GCfg& c = g->c;
+  for (uint32_t i = 0; i < c.S; ++i)
+    if (kind[i] > RSF_KIND_KNOWN || status[i] > RSF_STATUS_FAILED) return gerr("bad view kind/status");
+  RSF_HIP(hipSetDevice(g->device));
+  size_t b[3] = {c.S, c.S, (size_t)c.S * 8};
+  void* d[3];
+  int rc = g->scratch.take(b, 3, d);
+  if (rc) return rc;
+  RSF_HIP(hipMemcpyAsync(d[0], kind, c.S, hipMemcpyHostToDevice, g->stream));
+  RSF_HIP(hipMemcpyAsync(d[1], status, c.S, hipMemcpyHostToDevice, g->stream));
+  RSF_HIP(hipMemcpyAsync(d[2], ltime, (size_t)c.S * 8, hipMemcpyHostToDevice, g->stream));
+  hipLaunchKernelGGL(init_views_kernel, dim3(grid1(c.n_loc * c.S)), dim3(256), 0, g->stream, g->s.view, c.n_loc, c.S,
+                     (const uint8_t*)d[0], (const uint8_t*)d[1], (const uint64_t*)d[2]);
+  RSF_HIP(hipGetLastError());
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  return RSF_OK;
+}
+
+int rsf_gossip_set_view(rsf_gossip* g, uint64_t m, uint32_t subj, uint8_t kind, uint8_t status, uint64_t ltime) {
+  if (!g) return gerr("null context");
+  const GCfg& c = g->c;
+  if (m < c.lo || m >= c.lo + c.n_loc || subj >= c.S) return gerr("member/subject out of range");
+  if (kind > RSF_KIND_KNOWN || status > RSF_STATUS_FAILED) return gerr("bad view kind/status");
+  ViewE v;
+  v.ltime = ltime;
+  v.meta = status | ((uint32_t)kind << 8);
+  v._pad = 0;
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemcpyAsync(g->s.view + (m - c.lo) * c.S + subj, &v, sizeof(v), hipMemcpyHostToDevice, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  return RSF_OK;
+}
+
+int rsf_gossip_set_alive(rsf_gossip* g, const uint8_t* alive) {
+  if (!g || !alive) return gerr("null argument");
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemcpyAsync(g->s.alive, alive, g->c.N, hipMemcpyHostToDevice, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  return RSF_OK;
+}
+
+static int set_u64(rsf_gossip* g, uint64_t* dst, uint64_t v) {
+  RSF_HIP(hipMemcpyAsync(dst, &v, 8, hipMemcpyHostToDevice, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  return RSF_OK;
+}
+
+int rsf_gossip_set_clocks(rsf_gossip* g, uint64_t m, uint64_t clock, uint64_t ec, uint64_t qc) {
+  if (!g) return gerr("null context");
+  if (m < g->c.lo || m >= g->c.lo + g->c.n_loc) return gerr("member out of shard");
+  uint64_t l = m - g->c.lo;
+  RSF_HIP(hipSetDevice(g->device));
+  int rc;
+  if ((rc = set_u64(g, g->s.clock + l, clock)) || (rc = set_u64(g, g->s.eclock + l, ec)) ||
+      (rc = set_u64(g, g->s.qclock + l, qc)))
+    return rc;
+  return RSF_OK;
+}
+
+int rsf_gossip_set_min_times(rsf_gossip* g, uint64_t m, uint64_t emin, uint64_t qmin) {
+  if (!g) return gerr("null context");
+  if (m < g->c.lo || m >= g->c.lo + g->c.n_loc) return gerr("member out of shard");
+  uint64_t l = m - g->c.lo;
+  RSF_HIP(hipSetDevice(g->device));
+  int rc;
+  if ((rc = set_u64(g, g->s.emin + l, emin)) || (rc = set_u64(g, g->s.qmin + l, qmin))) return rc;
+  return RSF_OK;
+}
+
+int rsf_gossip_set_serf_state(rsf_gossip* g, uint64_t m, uint8_t state) {
+  if (!g) return gerr("null context");
+  if (m < g->c.lo || m >= g->c.lo + g->c.n_loc || state > 3) return gerr("bad member/state");
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemcpyAsync(g->s.serf_state + (m - g->c.lo), &state, 1, hipMemcpyHostToDevice, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  return RSF_OK;
+}
+
+int rsf_gossip_apply_batch(rsf_gossip* g, const rsf_msg* msgs, uint64_t n, int32_t* flags_out, uint64_t* refute_out) {
+  if (!g || (n && (!msgs || !flags_out))) return gerr("null argument");
+  if (n == 0) return RSF_OK;
+  const GCfg& c = g->c;
+  if (n > 0xFFFFFFFFull) return gerr("batch too large");
+  for (uint64_t i = 0; i < n; ++i) {
+    if (msgs[i].receiver < c.lo || msgs[i].receiver >= c.lo + c.n_loc) return gerr("receiver outside shard");
+    uint8_t t = msgs[i].type;
+    if (t != RSF_MSG_JOIN && t != RSF_MSG_LEAVE && t != RSF_MSG_USER_EVENT && t != RSF_MSG_QUERY)
+      return gerr("unsupported message type");
+    if ((t == RSF_MSG_JOIN || t == RSF_MSG_LEAVE) && msgs[i].subject >= c.S) return gerr("subject out of range");
+  }
+  RSF_HIP(hipSetDevice(g->device));
+  size_t b[7] = {n * sizeof(rsf_msg), n * 4, n * 4, n * 4, n * 4, n * 4, n * 8};
+  void* d[7];
+  int rc = g->scratch.take(b, 7, d);
+  if (rc) return rc;
+  size_t tmp = 0;
+  RSF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (uint32_t*)d[1], (uint32_t*)d[2], (uint32_t*)d[3],
+                                             (uint32_t*)d[4], (int)n, 0, bits_for(c.n_loc), g->stream));
+  void* tmpbuf;
+  if ((rc = g->scratch.take_extra(tmp, &tmpbuf))) return rc;
+  RSF_HIP(hipMemcpyAsync(d[0], msgs, n * sizeof(rsf_msg), hipMemcpyHostToDevice, g->stream));
+  hipLaunchKernelGGL(keys_from_msgs_kernel, dim3(grid1(n)), dim3(256), 0, g->stream, (const rsf_msg*)d[0], n, c.lo,
+                     (uint32_t*)d[1], (uint32_t*)d[3]);
+  RSF_HIP(hipcub::DeviceRadixSort::SortPairs(tmpbuf, tmp, (uint32_t*)d[1], (uint32_t*)d[2], (uint32_t*)d[3],
+                                             (uint32_t*)d[4], (int)n, 0, bits_for(c.n_loc), g->stream));
+  RSF_HIP(hipMemsetAsync(g->seg_start, 0, c.n_loc * 4, g->stream));
+  RSF_HIP(hipMemsetAsync(g->seg_end, 0, c.n_loc * 4, g->stream));
+  hipLaunchKernelGGL(segment_kernel, dim3(grid1(n)), dim3(256), 0, g->stream, (const uint32_t*)d[2], n, 0ull,
+                     g->seg_start, g->seg_end, g->d_counters);
+  hipLaunchKernelGGL(apply_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, g->stream, c, g->s, (const rsf_msg*)d[0],
+                     (const uint32_t*)d[4], g->seg_start, g->seg_end, (int32_t*)d[5], (uint64_t*)d[6]);
+  RSF_HIP(hipGetLastError());
+  RSF_HIP(hipMemcpyAsync(flags_out, d[5], n * 4, hipMemcpyDeviceToHost, g->stream));
+  if (refute_out) RSF_HIP(hipMemcpyAsync(refute_out, d[6], n * 8, hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  return RSF_OK;
+}
+
+// phases 1-3 (everything before emission)
+int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml, uint32_t n_ml,
+                           const rsf_action* acts, uint32_t n_acts) {
+  if (!g || (n_ml && !ml) || (n_acts && !acts)) return gerr("null argument");
+  const GCfg& c = g->c;
+  for (uint32_t e = 0; e < n_ml; ++e)
+    if (ml[e].subject >= c.S || (ml[e].kind != RSF_ML_JOIN && ml[e].kind != RSF_ML_LEAVE) || ml[e].set_alive > 2)
+      return gerr("bad memberlist event");
+  // actions: known kinds, members in range, distinct members
+  {
+    std::vector<uint32_t> ms;
+    ms.reserve(n_acts);
+    for (uint32_t a = 0; a < n_acts; ++a) {
+      const rsf_action& x = acts[a];
+      if (x.member >= c.N || x.act < RSF_ACT_JOIN_SELF || x.act > RSF_ACT_QUERY) return gerr("bad action");
+      if (x.act == RSF_ACT_FORCE_LEAVE && x.subject >= c.S) return gerr("force_leave subject out of range");
+      ms.push_back(x.member);
+    }
+    std::sort(ms.begin(), ms.end());
+    if (std::adjacent_find(ms.begin(), ms.end()) != ms.end()) return gerr("actions of one round must name distinct members");
+  }
+  uint64_t need = (uint64_t)c.S * c.max_refute + n_acts;
+  if ((uint64_t)g->n_rumors + need > g->max_rumors) return rsf::set_error(RSF_ERR_OVERFLOW, "rumor table full");
+  RSF_HIP(hipSetDevice(g->device));
+  int rc = ensure_lists(g, n_ml, n_acts);
+  if (rc) return rc;
+  hipStream_t st = g->stream;
+  mark(g, 0);
+  g->cur_round = round;
+  g->round_base = g->n_rumors;
+  g->round_abase = g->round_base + c.S * c.max_refute;
+  g->round_need = (uint32_t)need;
+  g->n_rumors += (uint32_t)need;
+  RSF_HIP(hipMemsetAsync(g->s.rumors + g->round_base, 0, need * sizeof(rsf_rumor), st));
+  if (n_ml) {
+    RSF_HIP(hipMemcpyAsync(g->d_ml, ml, n_ml * sizeof(rsf_ml_event), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(ml_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, c, g->s, g->d_ml, n_ml);
+    hipLaunchKernelGGL(ml_alive_kernel, dim3(1), dim3(64), 0, st, g->s, g->d_ml, n_ml);
+  }
+  hipLaunchKernelGGL(refute_kernel, dim3(grid1(c.S)), dim3(256), 0, st, c, g->s, g->round_base);
+  if (n_acts) {
+    RSF_HIP(hipMemcpyAsync(g->d_acts, acts, n_acts * sizeof(rsf_action), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(originate_kernel, dim3(grid1(n_acts)), dim3(256), 0, st, c, g->s, g->d_acts, n_acts,
+                       g->round_abase);
+  }
+  RSF_HIP(hipGetLastError());
+  mark(g, 1);
+  return RSF_OK;
+}
+
+int rsf_gossip_rumor_block(rsf_gossip* g, void** p, uint64_t* bytes) {
+  if (!g || !p || !bytes) return gerr("null argument");
+  *p = g->s.rumors + g->round_base;
+  *bytes = (uint64_t)g->round_need * sizeof(rsf_rumor);
+  return RSF_OK;
+}
+
+}  // extern "C"
+
+static int emit_and_sort(rsf_gossip* g, uint32_t round) {
+  const GCfg& c = g->c;
+  hipStream_t st = g->stream;
+  RSF_HIP(hipMemsetAsync(g->stage_key, 0xFF, g->stage_cap * 4, st));
+  hipLaunchKernelGGL(emit_kernel, dim3(grid1(c.n_loc, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0, st, c, g->s,
+                     round, g->stage_key, g->stage_val);
+  RSF_HIP(hipGetLastError());
+  mark(g, 2);
+  int rc = sort_pairs(g, g->stage_key, g->sort_key, g->stage_val, g->sort_val, g->stage_cap);
+  if (rc) return rc;
+  // n_valid = index of the first sentinel (records of dead/absent slots sort last)
+  hipLaunchKernelGGL(fill_u64_kernel, dim3(1), dim3(64), 0, st, (uint64_t*)g->d_counters, 1ull,
+                     (uint64_t)g->stage_cap);
+  hipLaunchKernelGGL(first_sentinel_kernel, dim3(grid1(g->stage_cap)), dim3(256), 0, st, g->sort_key, g->stage_cap,
+                     g->d_counters);
+  RSF_HIP(hipGetLastError());
+  mark(g, 3);
+  return RSF_OK;
+}
+
+static int segment_and_merge(rsf_gossip* g, const uint32_t* keys, const uint32_t* vals, uint64_t n) {
+  const GCfg& c = g->c;
+  hipStream_t st = g->stream;
+  RSF_HIP(hipMemsetAsync(g->seg_start, 0, c.n_loc * 4, st));
+  RSF_HIP(hipMemsetAsync(g->seg_end, 0, c.n_loc * 4, st));
+  if (n) {
+    hipLaunchKernelGGL(segment_kernel, dim3(grid1(n)), dim3(256), 0, st, keys, n, c.lo, g->seg_start, g->seg_end,
+                       g->d_counters + 63);
+  }
+  hipLaunchKernelGGL(merge_kernel, dim3(grid1(c.n_loc, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0, st, c,
+                     g->s, vals, g->seg_start, g->seg_end);
+  RSF_HIP(hipGetLastError());
+  mark(g, 4);
+  return RSF_OK;
+}
+
+extern "C" {
+
+int rsf_gossip_round(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml, uint32_t n_ml, const rsf_action* acts,
+                     uint32_t n_acts) {
+  if (!g) return gerr("null context");
+  if (g->c.n_loc != g->c.N) return gerr("sharded context: use round_begin / round_emit / round_merge");
+  int rc = rsf_gossip_round_begin(g, round, ml, n_ml, acts, n_acts);
+  if (rc) return rc;
+  if ((rc = emit_and_sort(g, round))) return rc;
+  g->merged_from_stage = true;
+  hipLaunchKernelGGL(accumulate_kernel, dim3(1), dim3(64), 0, g->stream, g->d_counters);
+  return segment_and_merge(g, g->sort_key, g->sort_val, g->stage_cap);
+}
+
+int rsf_gossip_round_emit(rsf_gossip* g, uint32_t world, uint64_t* send_counts) {
+  if (!g || !send_counts || world == 0 || world > 62) return gerr("bad argument");
+  const GCfg& c = g->c;
+  if (c.N % world || c.n_loc != c.N / world) return gerr("shards must be equal contiguous ranges of n_members");
+  RSF_HIP(hipSetDevice(g->device));
+  int rc = emit_and_sort(g, g->cur_round);
+  if (rc) return rc;
+  hipStream_t st = g->stream;
+  hipLaunchKernelGGL(shard_bounds_kernel, dim3(1), dim3(64), 0, st, g->sort_key, g->d_counters, c.N / world, world,
+                     g->d_counters + 1);
+  hipLaunchKernelGGL(pack_kernel, dim3(grid1(g->stage_cap)), dim3(256), 0, st, g->sort_key, g->sort_val,
+                     g->d_counters, g->send_buf);
+  RSF_HIP(hipGetLastError());
+  unsigned long long b[64];
+  RSF_HIP(hipMemcpyAsync(b, g->d_counters, (world + 2) * 8, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipStreamSynchronize(st));
+  for (uint32_t w = 0; w < world; ++w) send_counts[w] = b[1 + w + 1] - b[1 + w];
+  g->merged_from_stage = false;
+  return RSF_OK;
+}
+
+int rsf_gossip_send_buffer(rsf_gossip* g, void** p, uint64_t* cap) {
+  if (!g || !p) return gerr("null argument");
+  *p = g->send_buf;
+  if (cap) *cap = std::max(g->stage_cap, g->recv_cap);
+  return RSF_OK;
+}
+
+int rsf_gossip_round_merge(rsf_gossip* g, const uint64_t* recv, uint64_t n_recv) {
+  if (!g || (n_recv && !recv)) return gerr("null argument");
+  if (n_recv > g->recv_cap) return rsf::set_error(RSF_ERR_OVERFLOW, "receive buffer capacity exceeded");
+  RSF_HIP(hipSetDevice(g->device));
+  hipStream_t st = g->stream;
+  if (n_recv) {
+    hipLaunchKernelGGL(unpack_kernel, dim3(grid1(n_recv)), dim3(256), 0, st, recv, n_recv, g->stage_key, g->stage_val);
+    int rc = sort_pairs(g, g->stage_key, g->sort_key, g->stage_val, g->sort_val, n_recv);
+    if (rc) return rc;
+  }
+  g->last_merged = n_recv;
+  g->total_merged_host += n_recv;
+  if (!g->profiling) {
+  } else if (g->prof_rounds < rsf_gossip::kMaxProfRounds) {
+    hipEventRecord(g->ev[g->prof_rounds][3], g->stream);  // exchange time lands in the sort slot
+  }
+  return segment_and_merge(g, g->sort_key, g->sort_val, n_recv);
+}
+
+int rsf_gossip_dump_members(rsf_gossip* g, uint64_t* clock, uint64_t* ec, uint64_t* qc, uint64_t* digest, uint32_t* err,
+                            uint8_t* serf_state) {
+  if (!g) return gerr("null context");
+  const uint64_t n = g->c.n_loc;
+  hipStream_t st = g->stream;
+  RSF_HIP(hipSetDevice(g->device));
+  if (clock) RSF_HIP(hipMemcpyAsync(clock, g->s.clock, n * 8, hipMemcpyDeviceToHost, st));
+  if (ec) RSF_HIP(hipMemcpyAsync(ec, g->s.eclock, n * 8, hipMemcpyDeviceToHost, st));
+  if (qc) RSF_HIP(hipMemcpyAsync(qc, g->s.qclock, n * 8, hipMemcpyDeviceToHost, st));
+  if (digest) RSF_HIP(hipMemcpyAsync(digest, g->s.digest, n * 8, hipMemcpyDeviceToHost, st));
+  if (err) RSF_HIP(hipMemcpyAsync(err, g->s.err, n * 4, hipMemcpyDeviceToHost, st));
+  if (serf_state) RSF_HIP(hipMemcpyAsync(serf_state, g->s.serf_state, n, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipStreamSynchronize(st));
+  return RSF_OK;
+}
+
+int rsf_gossip_dump_view(rsf_gossip* g, uint64_t* ltime, uint8_t* status, uint8_t* kind) {
+  if (!g || !ltime || !status || !kind) return gerr("null argument");
+  const uint64_t cnt = g->c.n_loc * g->c.S;
+  std::vector<ViewE> v(cnt);
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemcpyAsync(v.data(), g->s.view, cnt * sizeof(ViewE), hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  for (uint64_t i = 0; i < cnt; ++i) {
+    ltime[i] = v[i].ltime;
+    status[i] = (uint8_t)(v[i].meta & 0xFF);
+    kind[i] = (uint8_t)((v[i].meta >> 8) & 0xFF);
+  }
+  return RSF_OK;
+}
+
+int rsf_gossip_dump_queues(rsf_gossip* g, uint32_t* rumor, uint32_t* seq, uint16_t* tx, uint16_t* len,
+                           uint32_t* next_seq) {
+  if (!g || !rumor || !seq || !tx || !len || !next_seq) return gerr("null argument");
+  const uint64_t cnt = g->c.n_loc * 3 * g->c.qcap;
+  std::vector<uint32_t> tl(cnt);
+  hipStream_t st = g->stream;
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemcpyAsync(rumor, g->s.q_rumor, cnt * 4, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipMemcpyAsync(seq, g->s.q_seq, cnt * 4, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipMemcpyAsync(tl.data(), g->s.q_txlen, cnt * 4, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipMemcpyAsync(next_seq, g->s.q_next_seq, g->c.n_loc * 3 * 4, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipStreamSynchronize(st));
+  for (uint64_t i = 0; i < cnt; ++i) {
+    tx[i] = (uint16_t)(tl[i] & 0xFFFF);
+    len[i] = (uint16_t)(tl[i] >> 16);
+  }
+  return RSF_OK;
+}
+
+int rsf_gossip_dump_buffers(rsf_gossip* g, uint64_t* eb_ltime, uint32_t* eb_cnt, uint64_t* eb_keys, uint64_t* qb_ltime,
+                            uint32_t* qb_cnt, uint32_t* qb_ids) {
+  if (!g) return gerr("null context");
+  const GCfg& c = g->c;
+  hipStream_t st = g->stream;
+  RSF_HIP(hipSetDevice(g->device));
+  if (eb_ltime) RSF_HIP(hipMemcpyAsync(eb_ltime, g->s.eb_ltime, c.n_loc * c.ebuf * 8, hipMemcpyDeviceToHost, st));
+  if (eb_cnt) RSF_HIP(hipMemcpyAsync(eb_cnt, g->s.eb_cnt, c.n_loc * c.ebuf * 4, hipMemcpyDeviceToHost, st));
+  if (eb_keys)
+    RSF_HIP(hipMemcpyAsync(eb_keys, g->s.eb_keys, c.n_loc * c.ebuf * c.slot_k * 8, hipMemcpyDeviceToHost, st));
+  if (qb_ltime) RSF_HIP(hipMemcpyAsync(qb_ltime, g->s.qb_ltime, c.n_loc * c.qbuf * 8, hipMemcpyDeviceToHost, st));
+  if (qb_cnt) RSF_HIP(hipMemcpyAsync(qb_cnt, g->s.qb_cnt, c.n_loc * c.qbuf * 4, hipMemcpyDeviceToHost, st));
+  if (qb_ids)
+    RSF_HIP(hipMemcpyAsync(qb_ids, g->s.qb_ids, c.n_loc * c.qbuf * c.slot_k * 4, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipStreamSynchronize(st));
+  return RSF_OK;
+}
+
+int rsf_gossip_dump_rumors(rsf_gossip* g, uint32_t first, uint32_t count, rsf_rumor* out) {
+  if (!g || (count && !out)) return gerr("null argument");
+  if ((uint64_t)first + count > g->max_rumors) return gerr("rumor range out of bounds");
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemcpyAsync(out, g->s.rumors + first, (size_t)count * sizeof(rsf_rumor), hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  return RSF_OK;
+}
+
+int rsf_gossip_dump_refutes(rsf_gossip* g, uint32_t* count, uint64_t* ltimes) {
+  if (!g || !count || !ltimes) return gerr("null argument");
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemcpyAsync(count, g->s.refute_cnt, g->c.S * 4, hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipMemcpyAsync(ltimes, g->s.refute_ltime, (size_t)g->c.S * g->c.max_refute * 8, hipMemcpyDeviceToHost,
+                         g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  return RSF_OK;
+}
+
+int rsf_gossip_set_profiling(rsf_gossip* g, int on) {
+  if (!g) return gerr("null context");
+  RSF_HIP(hipSetDevice(g->device));
+  if (on && !g->events_made) {
+    for (auto& row : g->ev)
+      for (auto& e : row) RSF_HIP(hipEventCreate(&e));
+    g->events_made = true;
+  }
+  g->profiling = on != 0;
+  g->prof_rounds = 0;
+  return RSF_OK;
+}
+
+int rsf_gossip_phase_times(rsf_gossip* g, double* ms_out, uint32_t* rounds_out) {
+  if (!g || !ms_out) return gerr("null argument");
+  for (int k = 0; k < rsf_gossip::kMarks - 1; ++k) ms_out[k] = 0.0;
+  RSF_HIP(hipSetDevice(g->device));
+  for (int r = 0; r < g->prof_rounds; ++r) {
+    RSF_HIP(hipEventSynchronize(g->ev[r][rsf_gossip::kMarks - 1]));
+    for (int k = 0; k + 1 < rsf_gossip::kMarks; ++k) {
+      float ms = 0.f;
+      RSF_HIP(hipEventElapsedTime(&ms, g->ev[r][k], g->ev[r][k + 1]));
+      ms_out[k] += ms;
+    }
+  }
+  if (rounds_out) *rounds_out = (uint32_t)g->prof_rounds;
+  g->prof_rounds = 0;
+  return RSF_OK;
+}
+
+int rsf_gossip_totals(rsf_gossip* g, uint64_t* merged_total) {
+  if (!g || !merged_total) return gerr("null argument");
+  unsigned long long t = 0;
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemcpyAsync(&t, g->d_counters + 60, 8, hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  *merged_total = t + g->total_merged_host;
+  return RSF_OK;
+}
+
+int rsf_gossip_last_round_stats(rsf_gossip* g, uint64_t* sent, uint64_t* merged) {
+  if (!g) return gerr("null context");
+  unsigned long long nv = 0;
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemcpyAsync(&nv, g->d_counters, 8, hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  if (sent) *sent = nv;
+  if (merged) *merged = g->merged_from_stage ? nv : g->last_merged;
+  return RSF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,319 @@
+// gossip_handlers.h — device restatement of ruserf's member-state merge and
+// dissemination handlers.  Scalar (one lane) code; the kernels in gossip.hip
+// call it from thread-per-item or lane-0-of-a-wave contexts.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ruserf_amd.h"
+#include "common.h"
+
+namespace rsf {
+
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+constexpr uint32_t kMinMsgLen = 18;  // smallest encoded message of the length model
+constexpr uint64_t kDigUser = 0x1000000000000000ull;
+constexpr uint64_t kDigQuery = 0x2000000000000000ull;
+constexpr uint64_t kDigMember = 0x3000000000000000ull;
+enum : uint32_t { kEvJoin = 0, kEvLeave = 1, kEvFailed = 2 };
+enum : uint32_t { kQIntent = 0, kQQuery = 1, kQEvent = 2 };
+enum : uint32_t { kErrEvSlot = 1, kErrQSlot = 2, kErrRefute = 4, kErrStage = 8 };
+enum : uint8_t { kSerfAlive = 0, kSerfLeaving = 1, kSerfLeft = 2, kSerfShutdown = 3 };
+
+struct GCfg {
+  uint64_t N, lo, n_loc;
+  uint32_t S, qcap, ebuf, qbuf, slot_k, fanout, limit, overhead, tx_limit, max_refute, cap_t;
+  uint32_t k0, k1;
+};
+
+// view entry: members.states[subject] (status, status_time) or recent_intents[subject]
+struct __align__(16) ViewE {
+  uint64_t ltime;
+  uint32_t meta;  // status | kind << 8
+  uint32_t _pad;
+};
+
+struct GState {
+  uint64_t *clock, *eclock, *qclock, *emin, *qmin, *digest;
+  uint32_t* err;
+  uint8_t* alive;  // [N] global liveness
+  uint8_t* serf_state;
+  int32_t* member_subj;
+  uint32_t* subj_member;  // [S]
+  uint32_t* refute_cnt;   // [S]
+  uint64_t* refute_ltime; // [S][max_refute]
+  ViewE* view;            // [n_loc][S]
+  uint32_t *q_rumor, *q_seq, *q_txlen, *q_next_seq;  // [n_loc][3][qcap], next_seq [n_loc][3]
+  uint64_t* eb_ltime;
+  uint32_t* eb_cnt;
+  uint64_t* eb_keys;
+  uint64_t* qb_ltime;
+  uint32_t* qb_cnt;
+  uint32_t* qb_ids;
+  rsf_rumor* rumors;
+};
+
+// per-member scalar state held in registers while a kernel works on it
+struct MRegs {
+  uint64_t clock, eclock, qclock, emin, qmin, digest;
+  uint32_t err;
+  uint8_t serf_state;
+  int32_t subj;
+};
+
+__device__ __forceinline__ void load_regs(const GState& s, uint64_t l, MRegs& r) {
+  r.clock = s.clock[l];
+  r.eclock = s.eclock[l];
+  r.qclock = s.qclock[l];
+  r.emin = s.emin[l];
+  r.qmin = s.qmin[l];
+  r.digest = s.digest[l];
+  r.err = s.err[l];
+  r.serf_state = s.serf_state[l];
+  r.subj = s.member_subj[l];
+}
+__device__ __forceinline__ void store_regs(const GState& s, uint64_t l, const MRegs& r) {
+  s.clock[l] = r.clock;
+  s.eclock[l] = r.eclock;
+  s.qclock[l] = r.qclock;
+  s.digest[l] = r.digest;
+  s.err[l] = r.err;
+  s.serf_state[l] = r.serf_state;
+}
+
+// LamportClock::witness (types/src/clock.rs:164-181)
+RSF_HD void witness(uint64_t& c, uint64_t t) {
+  if (t < c) return;
+  c = t + 1;
+}
+
+RSF_HD uint64_t digest_mix(uint64_t d, uint64_t x) {
+  d ^= x;
+  d *= 0x100000001B3ull;
+  d ^= d >> 29;
+  return d;
+}
+
+RSF_HD uint32_t varint_len(uint64_t v) {
+  uint32_t n = 1;
+  while (v >= 0x80) {
+    v >>= 7;
+    n++;
+  }
+  return n;
+}
+
+// encoded length model (oracle orc_msg_len)
+RSF_HD uint32_t msg_len(uint8_t type, uint64_t ltime, uint32_t name_len, uint32_t payload_len) {
+  uint32_t base = 1 + 4 + varint_len(ltime);
+  switch (type) {
+    case RSF_MSG_JOIN: return base + 12;
+    case RSF_MSG_LEAVE: return base + 12 + 1;
+    case RSF_MSG_USER_EVENT: return base + (4 + name_len) + (4 + payload_len) + 1;
+    case RSF_MSG_QUERY: return base + 4 + 28 + 4 + 1 + 8 + (4 + name_len) + (4 + payload_len);
+    default: return base;
+  }
+}
+
+RSF_HD uint64_t tlq_key(uint32_t tx, uint32_t len, uint32_t seq) {
+  return ((uint64_t)tx << 48) | ((uint64_t)(0xFFFFu - len) << 32) | (uint64_t)(0xFFFFFFFFu - seq);
+}
+
+__device__ __forceinline__ uint32_t vstatus(uint32_t meta) { return meta & 0xFF; }
+__device__ __forceinline__ uint32_t vkind(uint32_t meta) { return (meta >> 8) & 0xFF; }
+__device__ __forceinline__ uint32_t vmeta(uint32_t status, uint32_t kind) { return status | (kind << 8); }
+
+// upsert_intent (base.rs:1797-1828)
+__device__ __forceinline__ bool upsert_intent(ViewE* e, uint32_t kind, uint64_t L) {
+  ViewE v = *e;
+  if (vkind(v.meta) == RSF_KIND_UNKNOWN || L > v.ltime) {
+    v.ltime = L;
+    v.meta = vmeta(vstatus(v.meta), kind);
+    *e = v;
+    return true;
+  }
+  return false;
+}
+
+// handle_node_join_intent (base.rs:1302-1337)
+__device__ __forceinline__ int h_join_intent(ViewE* e, MRegs& r, uint64_t L) {
+  witness(r.clock, L);
+  ViewE v = *e;
+  if (vkind(v.meta) == RSF_KIND_KNOWN) {
+    if (L <= v.ltime) return 0;
+    v.ltime = L;
+    uint32_t st = vstatus(v.meta);
+    if (st == RSF_STATUS_LEAVING) st = RSF_STATUS_ALIVE;
+    v.meta = vmeta(st, RSF_KIND_KNOWN);
+    *e = v;
+    return RSF_F_REBROADCAST;
+  }
+  return upsert_intent(e, RSF_KIND_INTENT_JOIN, L) ? RSF_F_REBROADCAST : 0;
+}
+
+// handle_node_leave_intent (base.rs:1409-1528)
+__device__ __forceinline__ int h_leave_intent(ViewE* e, MRegs& r, uint32_t subj, uint64_t L, bool prune,
+                                              uint64_t& refute) {
+  uint8_t state = r.serf_state;
+  witness(r.clock, L);
+  ViewE v = *e;
+  if (vkind(v.meta) != RSF_KIND_KNOWN) return upsert_intent(e, RSF_KIND_INTENT_LEAVE, L) ? RSF_F_REBROADCAST : 0;
+  if (L <= v.ltime) return 0;
+  if (r.subj == (int32_t)subj && state == kSerfAlive) {
+    refute = r.clock;
+    return RSF_F_REFUTE;
+  }
+  v.ltime = L;
+  int pf = prune ? RSF_F_PRUNE : 0;
+  uint32_t st = vstatus(v.meta);
+  int f;
+  switch (st) {
+    case RSF_STATUS_NONE: f = 0; break;
+    case RSF_STATUS_ALIVE: st = RSF_STATUS_LEAVING; f = RSF_F_REBROADCAST | pf; break;
+    case RSF_STATUS_LEAVING:
+    case RSF_STATUS_LEFT: f = RSF_F_REBROADCAST | pf; break;
+    case RSF_STATUS_FAILED:
+      st = RSF_STATUS_LEFT;
+      r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)kEvLeave << 32) | subj);
+      f = RSF_F_REBROADCAST | RSF_F_MEMBER_EVENT | pf;
+      break;
+    default: f = 0; break;
+  }
+  v.meta = vmeta(st, RSF_KIND_KNOWN);
+  *e = v;
+  return f;
+}
+
+// handle_node_join (base.rs:1167-1298)
+__device__ __forceinline__ int h_node_join(ViewE* e, MRegs& r, uint32_t subj) {
+  ViewE v = *e;
+  uint32_t kind = vkind(v.meta);
+  if (kind == RSF_KIND_KNOWN) {
+    v.meta = vmeta(RSF_STATUS_ALIVE, RSF_KIND_KNOWN);
+  } else {
+    uint32_t st = RSF_STATUS_ALIVE;
+    uint64_t t = 0;
+    if (kind == RSF_KIND_INTENT_JOIN) t = v.ltime;
+    if (kind == RSF_KIND_INTENT_LEAVE) {
+      t = v.ltime;
+      st = RSF_STATUS_LEAVING;
+    }
+    v.ltime = t;
+    v.meta = vmeta(st, RSF_KIND_KNOWN);
+  }
+  *e = v;
+  r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)kEvJoin << 32) | subj);
+  return RSF_F_MEMBER_EVENT;
+}
+
+// handle_node_leave (base.rs:1339-1407)
+__device__ __forceinline__ int h_node_leave(ViewE* e, MRegs& r, uint32_t subj) {
+  ViewE v = *e;
+  if (vkind(v.meta) != RSF_KIND_KNOWN) return 0;
+  uint32_t st = vstatus(v.meta), ev;
+  if (st == RSF_STATUS_LEAVING) {
+    st = RSF_STATUS_LEFT;
+    ev = kEvLeave;
+  } else if (st == RSF_STATUS_ALIVE) {
+    st = RSF_STATUS_FAILED;
+    ev = kEvFailed;
+  } else {
+    return 0;
+  }
+  v.meta = vmeta(st, RSF_KIND_KNOWN);
+  *e = v;
+  r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)ev << 32) | subj);
+  return RSF_F_MEMBER_EVENT;
+}
+
+// handle_user_event (base.rs:770-837)
+__device__ __forceinline__ int h_user_event(const GCfg& c, const GState& s, uint64_t l, MRegs& r, uint64_t L,
+                                            uint64_t key) {
+  witness(r.eclock, L);
+  if (L < r.emin) return 0;
+  uint64_t B = c.ebuf, cur = r.eclock;
+  if (cur > B && L < cur - B) return 0;
+  uint64_t slot = l * c.ebuf + (L % B);
+  uint64_t* keys = s.eb_keys + slot * c.slot_k;
+  uint32_t cnt = s.eb_cnt[slot];
+  if (cnt) {
+    for (uint32_t i = 0; i < cnt; ++i)
+      if (keys[i] == key) return 0;
+    if (cnt < c.slot_k) {
+      keys[cnt] = key;
+      s.eb_cnt[slot] = cnt + 1;
+    } else {
+      r.err |= kErrEvSlot;
+    }
+  } else {
+    s.eb_ltime[slot] = L;
+    keys[0] = key;
+    s.eb_cnt[slot] = 1;
+  }
+  r.digest = digest_mix(digest_mix(r.digest, kDigUser ^ key), L);
+  return RSF_F_REBROADCAST | RSF_F_DELIVER;
+}
+
+// handle_query (base.rs:981-1119): dedup + rebroadcast decision; filters pass
+__device__ __forceinline__ int h_query(const GCfg& c, const GState& s, uint64_t l, MRegs& r, uint64_t L,
+                                       uint32_t id, bool no_broadcast) {
+  witness(r.qclock, L);
+  if (L < r.qmin) return 0;
+  uint64_t cur = r.qclock, B = c.qbuf;
+  if (cur > B && B < cur - B) return 0;  // reference quirk (base.rs:999)
+  uint64_t slot = l * c.qbuf + (L % B);
+  uint32_t* ids = s.qb_ids + slot * c.slot_k;
+  uint32_t cnt = s.qb_cnt[slot];
+  if (cnt) {
+    if (s.qb_ltime[slot] == L)
+      for (uint32_t i = 0; i < cnt; ++i)
+        if (ids[i] == id) return 0;
+    if (cnt < c.slot_k) {
+      ids[cnt] = id;
+      s.qb_cnt[slot] = cnt + 1;
+    } else {
+      r.err |= kErrQSlot;
+    }
+  } else {
+    s.qb_ltime[slot] = L;
+    ids[0] = id;
+    s.qb_cnt[slot] = 1;
+  }
+  r.digest = digest_mix(digest_mix(r.digest, kDigQuery ^ id), L);
+  return (no_broadcast ? 0 : RSF_F_REBROADCAST) | RSF_F_DELIVER;
+}
+
+__device__ __forceinline__ uint32_t queue_of(uint8_t type) {
+  return type == RSF_MSG_USER_EVENT ? kQEvent : (type == RSF_MSG_QUERY ? kQQuery : kQIntent);
+}
+
+// TransmitLimitedQueue insert, one thread: first empty slot, else replace the
+// last item in send order unless the new item is itself last (prune model).
+__device__ __forceinline__ void queue_insert_serial(const GCfg& c, const GState& s, uint64_t l, uint32_t q,
+                                                    uint32_t rid, uint32_t len) {
+  uint64_t base = (l * 3 + q) * c.qcap;
+  uint32_t seq = s.q_next_seq[l * 3 + q]++;
+  uint32_t slot = kEmpty;
+  for (uint32_t i = 0; i < c.qcap; ++i)
+    if (s.q_rumor[base + i] == kEmpty) {
+      slot = i;
+      break;
+    }
+  if (slot == kEmpty) {
+    uint64_t kmax = 0;
+    for (uint32_t i = 0; i < c.qcap; ++i) {
+      uint32_t tl = s.q_txlen[base + i];
+      uint64_t k = tlq_key(tl & 0xFFFF, tl >> 16, s.q_seq[base + i]);
+      if (slot == kEmpty || k > kmax) {
+        kmax = k;
+        slot = i;
+      }
+    }
+    if (tlq_key(0, len, seq) > kmax) return;
+  }
+  s.q_rumor[base + slot] = rid;
+  s.q_seq[base + slot] = seq;
+  s.q_txlen[base + slot] = (len << 16);
+}
+
+}  // namespace rsf

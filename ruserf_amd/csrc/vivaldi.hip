@@ -1,0 +1,734 @@
+// vivaldi.hip — Vivaldi network coordinates on CDNA4 (gfx950).
+//
+// Restates core/src/coordinate.rs (CoordinateClient::update and helpers,
+// lines 283-499, 557-650, 747-821) as f64 device code.  Compiled with
+// -ffp-contract=off: the reference (Rust) never contracts a*b+c into an FMA,
+// and bit-exact parity with the oracle depends on it.  f64 division and sqrt
+// are IEEE correctly rounded on gfx950 (no -ffast-math).
+//
+// HBM layout (per context):
+//   table[2][n_members][row_stride] f64   ping-pong coordinate tables (AoS rows:
+//                                          portion[dim], error, adjustment, height)
+//   adj  [W][shard_n] f64                  adjustment windows, window-slot-major (coalesced)
+//   adj_idx[shard_n] u32
+//   filt [shard_n][peer_slots][FR] f64     latency filter rings, FR = 4 (F<=3) or 8 (F<=7);
+//                                          the last f64 of a record holds len | head<<32
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/ruserf_amd.h"
+#include "common.h"
+#include "rsf_internal.h"
+
+using namespace rsf;
+
+namespace {
+
+constexpr int kMaxDim = 16;
+constexpr int kMaxFilter = 7;
+constexpr int kMaxWindow = 64;
+
+struct VivParams {
+  uint64_t n;        // members in the table
+  uint64_t lo;       // first member of the shard
+  uint64_t shard_n;  // members in the shard
+  uint32_t peers;    // latency-filter slots per member (= neighbours in round mode)
+  uint32_t dim, W, F, FR, stride;
+  uint32_t k0, k1;   // Philox key (seed)
+  uint32_t round;
+  double error_max, ce, cc, height_min, rho;
+};
+
+// --------------------------------------------------------------------------
+// device restatement of coordinate.rs
+// --------------------------------------------------------------------------
+// rand_f64 (coordinate.rs:812-821); thread_rng -> Philox(seed; draw, call, member, round)
+__device__ __forceinline__ double rand_f64(const VivParams& p, uint32_t call, uint32_t member,
+                                           uint32_t round, uint32_t& draw) {
+  for (;;) {
+    u32x4 o = philox4x32_10(draw++, (kPurposeUnit << 24) | call, member, round, p.k0, p.k1);
+    uint64_t u = (((uint64_t)o.y << 32) | o.x) & 0x7FFFFFFFFFFFFFFFull;
+    double f = (double)u / 9223372036854775808.0;
+    if (f != 1.0) return f;
+  }
+}
+
+// apply_force_in_place (coordinate.rs:614-626) with unit_vector_at inlined (786-810)
+template <int D>
+__device__ __forceinline__ void apply_force(double* me, double& height, const double* other,
+                                            double other_height, double force, uint32_t dim,
+                                            const VivParams& p, uint32_t call, uint32_t member,
+                                            uint32_t round) {
+  double unit[D];
+  double acc = 0.0;
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    if (i < (int)dim) {
+      unit[i] = me[i] - other[i];
+      acc = acc + unit[i] * unit[i];
+    }
+  }
+  double mag = sqrt(acc);
+  if (mag > 1.0e-6) {
+    double rc = 1.0 / mag;
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+      if (i < (int)dim) unit[i] *= rc;
+  } else {
+    uint32_t draw = 0;
+    for (int i = 0; i < D; ++i)  // not unrolled: rare branch, keep code small
+      if (i < (int)dim) unit[i] = rand_f64(p, call, member, round, draw) - 0.5;
+    double a2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+      if (i < (int)dim) a2 = a2 + unit[i] * unit[i];
+    double m2 = sqrt(a2);
+    if (m2 > 1.0e-6) {
+      double rc = 1.0 / m2;
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+        if (i < (int)dim) unit[i] *= rc;
+    } else {
+#pragma unroll
+      for (int i = 0; i < D; ++i) unit[i] = 0.0;
+      unit[0] = 1.0;
+    }
+    mag = 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    if (i < (int)dim) me[i] = me[i] + unit[i] * force;
+  if (mag > 1.0e-6) {
+    height = (height + other_height) * force / mag + height;
+    height = rmax(height, p.height_min);
+  }
+}
+
+// raw_distance_to (coordinate.rs:647-649)
+template <int D>
+__device__ __forceinline__ double raw_distance(const double* a, double ha, const double* b, double hb,
+                                               uint32_t dim) {
+  double acc = 0.0;
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    if (i < (int)dim) {
+      double d = a[i] - b[i];
+      acc = acc + d * d;
+    }
+  return sqrt(acc) + ha + hb;
+}
+
+// distance_to (coordinate.rs:630-644) -> Duration nanoseconds
+template <int D>
+__device__ __forceinline__ uint64_t distance_ns(const double* a, double ha, double adja, const double* b,
+                                                double hb, double adjb, uint32_t dim) {
+  double dist = raw_distance<D>(a, ha, b, hb, dim);
+  double adjusted = dist + adja + adjb;
+  double d = adjusted > 0.0 ? adjusted : dist;
+  return sat_u64(d * 1.0e9);
+}
+
+__device__ __forceinline__ bool finite(double x) { return isfinite(x); }
+
+// Result codes per item: RSF_OK or CoordinateError (check_coordinate order).
+template <int D, int F>
+__device__ __forceinline__ int update_one(double* me, double& err, double& adj, double& h,
+                                          const double* other, double oerr, double oadj, double oh,
+                                          uint32_t odim, uint64_t rtt_ns, double* frec,
+                                          double* adj_col, uint64_t adj_stride, uint32_t* adj_idx_p,
+                                          const VivParams& p, uint32_t member, uint32_t round,
+                                          unsigned long long* resets) {
+  const uint32_t dim = p.dim;
+  // check_coordinate (coordinate.rs:436-446)
+  if (odim != dim) return RSF_ERR_DIM_MISMATCH;
+  bool ok = finite(oerr) && finite(oadj) && finite(oh);
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    if (i < (int)dim) ok = ok && finite(other[i]);
+  if (!ok) return RSF_ERR_INVALID_COORD;
+  if (rtt_ns > 10000000000ull) return RSF_ERR_INVALID_RTT;  // rtt > MAX_RTT (477-481)
+
+  // latency_filter (292-307): ring == Vec push/remove(0) for the median
+  double rtt_seconds;
+  {
+    const int FR = (F <= 3) ? 4 : 8;
+    uint64_t meta = __double_as_longlong(frec[FR - 1]);
+    uint32_t len = (uint32_t)meta, head = (uint32_t)(meta >> 32);
+    double x = as_secs_f64(rtt_ns);
+    double s[F];
+#pragma unroll
+    for (int i = 0; i < F; ++i) s[i] = frec[i];
+    const uint32_t Fr = p.F;
+    if (len < Fr) {
+      uint32_t pos = head + len;
+      if (pos >= Fr) pos -= Fr;
+#pragma unroll
+      for (int i = 0; i < F; ++i)
+        if ((uint32_t)i == pos) s[i] = x;
+      len++;
+    } else {
+#pragma unroll
+      for (int i = 0; i < F; ++i)
+        if ((uint32_t)i == head) s[i] = x;
+      head = (head + 1 == Fr) ? 0 : head + 1;
+    }
+#pragma unroll
+    for (int i = 0; i < F; ++i) frec[i] = s[i];
+    frec[FR - 1] = __longlong_as_double((long long)(((uint64_t)head << 32) | len));
+    // median of the len live samples (sorted copy, index len/2)
+    double t[F];
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < F; ++i) {
+      // live samples are positions head..head+len-1 (mod Fr); their order is irrelevant for a median
+      uint32_t rel = ((uint32_t)i + Fr - head) % Fr;
+      if ((uint32_t)i < Fr && rel < len) t[c++] = s[i];
+    }
+    // insertion sort on c <= F values
+    for (uint32_t i = 1; i < c; ++i) {
+      double v = t[i];
+      uint32_t j = i;
+      while (j > 0 && t[j - 1] > v) {
+        t[j] = t[j - 1];
+        --j;
+      }
+      t[j] = v;
+    }
+    rtt_seconds = t[c / 2];
+  }
+
+  // update_vivaldi (311-330)
+  {
+    double dist = as_secs_f64(distance_ns<D>(me, h, adj, other, oh, oadj, dim));
+    double rtt = rmax(rtt_seconds, 1.0e-6);
+    double wrongness = fabs((dist - rtt) / rtt);
+    double total_error = rmax(err + oerr, 1.0e-6);
+    double weight = err / total_error;
+    err = rmin((p.ce * weight * wrongness) + (err * (1.0 - p.ce * weight)), p.error_max);
+    double force = p.cc * weight * (rtt - dist);
+    apply_force<D>(me, h, other, oh, force, dim, p, 0, member, round);
+  }
+  // update_adjustment (334-346)
+  if (p.W) {
+    double dist = raw_distance<D>(me, h, other, oh, dim);
+    double sample = rtt_seconds - dist;
+    uint32_t idx = *adj_idx_p;
+    double sum = 0.0;
+    for (uint32_t i = 0; i < p.W; ++i) {
+      double v = (i == idx) ? sample : adj_col[(uint64_t)i * adj_stride];
+      sum = sum + v;
+    }
+    adj_col[(uint64_t)idx * adj_stride] = sample;
+    *adj_idx_p = (idx + 1 == p.W) ? 0 : idx + 1;
+    adj = sum / (2.0 * (double)p.W);
+  }
+  // update_gravity (283-289): origin = with_options (portion 0, adj 0, height = height_min)
+  {
+    double zero[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) zero[i] = 0.0;
+    uint64_t secs = distance_ns<D>(zero, p.height_min, 0.0, me, h, adj, dim) / 1000000000ull;
+    double x = (double)secs / p.rho;
+    double force = -1.0 * (x * x);
+    apply_force<D>(me, h, zero, p.height_min, force, dim, p, 1, member, round);
+  }
+  // is_valid / reset (493-496)
+  bool valid = finite(err) && finite(adj) && finite(h);
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    if (i < (int)dim) valid = valid && finite(me[i]);
+  if (!valid) {
+    atomicAdd(resets, 1ull);
+#pragma unroll
+    for (int i = 0; i < D; ++i) me[i] = 0.0;
+    err = p.error_max;
+    adj = 0.0;
+    h = p.height_min;
+  }
+  return RSF_OK;
+}
+
+// synthetic network (BASELINE configs 1/5); the oracle's orc_vivaldi_probe
+__device__ __forceinline__ uint32_t neighbour(const VivParams& p, uint32_t m, uint32_t q) {
+  u32x4 o = philox4x32_10(q, kPurposeNbr << 24, m, 0, p.k0, p.k1);
+  uint32_t x = mulhi32(o.x, (uint32_t)(p.n - 1));
+  return x >= m ? x + 1 : x;
+}
+RSF_HD void true_pos(uint32_t k0, uint32_t k1, uint32_t m, double& x, double& y, double& h) {
+  u32x4 o = philox4x32_10(0, kPurposePos << 24, m, 0, k0, k1);
+  const double s32 = 2.3283064365386963e-10;
+  x = ((double)o.x * s32) * 0.05;
+  y = ((double)o.y * s32) * 0.05;
+  h = ((double)o.z * s32) * 0.002;
+}
+
+template <int D>
+__device__ __forceinline__ void load_row(const double* __restrict__ row, double* v, double& e,
+                                         double& a, double& h, uint32_t dim) {
+  if (D == 8) {
+    const double2* r2 = reinterpret_cast<const double2*>(row);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double2 t = r2[i];
+      v[2 * i] = t.x;
+      v[2 * i + 1] = t.y;
+    }
+    double2 t = r2[4];
+    e = t.x;
+    a = t.y;
+    h = row[10];
+  } else {
+#pragma unroll
+    for (int i = 0; i < D; ++i) v[i] = (i < (int)dim) ? row[i] : 0.0;
+    e = row[dim];
+    a = row[dim + 1];
+    h = row[dim + 2];
+  }
+}
+template <int D>
+__device__ __forceinline__ void store_row(double* __restrict__ row, const double* v, double e, double a,
+                                          double h, uint32_t dim) {
+  if (D == 8) {
+    double2* r2 = reinterpret_cast<double2*>(row);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r2[i] = make_double2(v[2 * i], v[2 * i + 1]);
+    r2[4] = make_double2(e, a);
+    r2[5] = make_double2(h, 0.0);
+  } else {
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+      if (i < (int)dim) row[i] = v[i];
+    row[dim] = e;
+    row[dim + 1] = a;
+    row[dim + 2] = h;
+  }
+}
+
+template <int D, int F>
+__global__ void __launch_bounds__(256) vivaldi_round_kernel(const double* __restrict__ cur,
+                                                            double* __restrict__ nxt,
+                                                            double* __restrict__ adj_win,
+                                                            uint32_t* __restrict__ adj_idx,
+                                                            double* __restrict__ filt,
+                                                            unsigned long long* resets, VivParams p) {
+  uint64_t local = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (local >= p.shard_n) return;
+  const uint32_t m = (uint32_t)(p.lo + local);
+  const int FR = (F <= 3) ? 4 : 8;
+  // synthetic probe (neighbour slot, rtt)
+  u32x4 pr = philox4x32_10(0, kPurposeVProbe << 24, m, p.round, p.k0, p.k1);
+  uint32_t q = mulhi32(pr.x, p.peers);
+  uint32_t peer = neighbour(p, m, q);
+  double xm, ym, hm, xp, yp, hp;
+  true_pos(p.k0, p.k1, m, xm, ym, hm);
+  true_pos(p.k0, p.k1, peer, xp, yp, hp);
+  double dx = xm - xp, dy = ym - yp;
+  double d = sqrt(dx * dx + dy * dy) + hm + hp;
+  double jit = 1.0 + 0.1 * ((double)pr.y * 2.3283064365386963e-10);
+  uint64_t rtt_ns = sat_u64((d * jit) * 1.0e9);
+
+  double me[D], other[D], e, a, h, oe, oa, oh;
+  load_row<D>(cur + (uint64_t)m * p.stride, me, e, a, h, p.dim);
+  load_row<D>(cur + (uint64_t)peer * p.stride, other, oe, oa, oh, p.dim);
+  double* frec = filt + (local * p.peers + q) * FR;
+  double rec[FR];
+  if (FR == 4) {
+    const double2* f2 = reinterpret_cast<const double2*>(frec);
+    double2 t0 = f2[0], t1 = f2[1];
+    rec[0] = t0.x;
+    rec[1] = t0.y;
+    rec[2] = t1.x;
+    rec[3] = t1.y;
+  } else {
+#pragma unroll
+    for (int i = 0; i < FR; ++i) rec[i] = frec[i];
+  }
+  update_one<D, F>(me, e, a, h, other, oe, oa, oh, p.dim, rtt_ns, rec, adj_win + local, p.shard_n,
+                   adj_idx + local, p, m, p.round, resets);
+  if (FR == 4) {
+    double2* f2 = reinterpret_cast<double2*>(frec);
+    f2[0] = make_double2(rec[0], rec[1]);
+    f2[1] = make_double2(rec[2], rec[3]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < FR; ++i) frec[i] = rec[i];
+  }
+  store_row<D>(nxt + (uint64_t)m * p.stride, me, e, a, h, p.dim);
+}
+
+template <int D, int F>
+__global__ void __launch_bounds__(256) vivaldi_batch_kernel(
+    double* __restrict__ table, double* __restrict__ adj_win, uint32_t* __restrict__ adj_idx,
+    double* __restrict__ filt, unsigned long long* resets, const uint32_t* __restrict__ member,
+    const uint32_t* __restrict__ slot, const double* __restrict__ orow,
+    const uint32_t* __restrict__ odim, const uint64_t* __restrict__ rtt, uint64_t n,
+    int32_t* __restrict__ status, double* __restrict__ rows_out, VivParams p) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int FR = (F <= 3) ? 4 : 8;
+  uint32_t m = member[i];
+  uint64_t local = m - p.lo;
+  uint32_t q = slot[i];
+  uint32_t od = odim ? odim[i] : p.dim;
+  double me[D], other[D], e, a, h, oe, oa, oh;
+  load_row<D>(table + (uint64_t)m * p.stride, me, e, a, h, p.dim);
+  const double* o = orow + i * p.stride;
+  // the other's row is laid out with ITS dimensionality; only read it when it matches
+  if (od == p.dim) {
+    load_row<D>(o, other, oe, oa, oh, p.dim);
+  } else {
+    oe = oa = oh = 0.0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) other[k] = 0.0;
+  }
+  double* frec = filt + (local * p.peers + q) * FR;
+  double rec[FR];
+#pragma unroll
+  for (int k = 0; k < FR; ++k) rec[k] = frec[k];
+  int st = update_one<D, F>(me, e, a, h, other, oe, oa, oh, od, rtt[i], rec, adj_win + local,
+                            p.shard_n, adj_idx + local, p, m, p.round, resets);
+  status[i] = st;
+  if (st == RSF_OK) {
+#pragma unroll
+    for (int k = 0; k < FR; ++k) frec[k] = rec[k];
+    store_row<D>(table + (uint64_t)m * p.stride, me, e, a, h, p.dim);
+  }
+  if (rows_out) {
+    double* ro = rows_out + i * p.stride;
+    load_row<D>(table + (uint64_t)m * p.stride, me, e, a, h, p.dim);
+    store_row<D>(ro, me, e, a, h, p.dim);
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256) estimate_rtt_kernel(const double* __restrict__ table,
+                                                           const uint32_t* __restrict__ a,
+                                                           const uint32_t* __restrict__ b, uint64_t n,
+                                                           uint64_t* __restrict__ out, VivParams p) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double va[D], vb[D], ea, aa, ha, eb, ab, hb;
+  load_row<D>(table + (uint64_t)a[i] * p.stride, va, ea, aa, ha, p.dim);
+  load_row<D>(table + (uint64_t)b[i] * p.stride, vb, eb, ab, hb, p.dim);
+  out[i] = distance_ns<D>(va, ha, aa, vb, hb, ab, p.dim);
+}
+
+__global__ void init_rows_kernel(double* table, uint64_t n, uint32_t stride, uint32_t dim, double err,
+                                 double hmin) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double* r = table + i * stride;
+  for (uint32_t k = 0; k < stride; ++k) r[k] = 0.0;
+  r[dim] = err;
+  r[dim + 2] = hmin;
+}
+
+}  // namespace
+
+struct rsf_vivaldi {
+  int device = 0;
+  hipStream_t own = nullptr, stream = nullptr;
+  VivParams p{};
+  double* table[2] = {nullptr, nullptr};
+  int cur = 0;
+  double* adj = nullptr;
+  uint32_t* adj_idx = nullptr;
+  double* filt = nullptr;
+  unsigned long long* resets = nullptr;
+  // batch staging (device)
+  DeviceScratch scratch;
+};
+
+static int set_err_args(const char* m) { return rsf::set_error(RSF_ERR_ARG, m); }
+
+extern "C" {
+
+void rsf_coord_opts_default(rsf_coord_opts* o) {
+  // CoordinateOptions::new (coordinate.rs:200-213)
+  std::memset(o, 0, sizeof(*o));
+  o->dimensionality = 8;
+  o->vivaldi_error_max = 1.5;
+  o->vivaldi_ce = 0.25;
+  o->vivaldi_cc = 0.25;
+  o->adjustment_window_size = 20;
+  o->height_min = 10.0e-6;
+  o->latency_filter_size = 3;
+  o->gravity_rho = 150.0;
+}
+
+uint32_t rsf_coord_row_stride(uint32_t dim) { return ((dim + 3 + 3) / 4) * 4; }
+
+int rsf_vivaldi_create(rsf_vivaldi** out, uint64_t n, uint64_t lo, uint64_t hi, uint32_t peers,
+                       const rsf_coord_opts* o, uint64_t seed, int device) {
+  if (!out || !o) return set_err_args("null argument");
+  *out = nullptr;
+  if (n < 2 || n > 0xFFFFFFFFull || lo >= hi || hi > n || peers == 0)
+    return set_err_args("bad member range / peer slots");
+  if (o->dimensionality == 0 || o->dimensionality > kMaxDim) return set_err_args("dimensionality must be 1..16");
+  if (o->adjustment_window_size > kMaxWindow) return set_err_args("adjustment_window_size must be <= 64");
+  if (o->latency_filter_size == 0 || o->latency_filter_size > kMaxFilter)
+    return set_err_args("latency_filter_size must be 1..7");
+  RSF_HIP(hipSetDevice(device));
+  rsf_vivaldi* v = new (std::nothrow) rsf_vivaldi();
+  if (!v) return rsf::set_error(RSF_ERR_NOMEM, "host allocation failed");
+  v->device = device;
+  VivParams& p = v->p;
+  p.n = n;
+  p.lo = lo;
+  p.shard_n = hi - lo;
+  p.peers = peers;
+  p.dim = o->dimensionality;
+  p.W = o->adjustment_window_size;
+  p.F = o->latency_filter_size;
+  p.FR = p.F <= 3 ? 4 : 8;
+  p.stride = rsf_coord_row_stride(p.dim);
+  p.k0 = (uint32_t)seed;
+  p.k1 = (uint32_t)(seed >> 32);
+  p.error_max = o->vivaldi_error_max;
+  p.ce = o->vivaldi_ce;
+  p.cc = o->vivaldi_cc;
+  p.height_min = o->height_min;
+  p.rho = o->gravity_rho;
+  int rc = RSF_OK;
+  auto fail = [&](int code) {
+    rsf_vivaldi_destroy(v);
+    return code;
+  };
+  if (hipStreamCreateWithFlags(&v->own, hipStreamNonBlocking) != hipSuccess)
+    return fail(rsf::set_error(RSF_ERR_HIP, "hipStreamCreate failed"));
+  v->stream = v->own;
+  size_t tbytes = (size_t)n * p.stride * sizeof(double);
+  if ((rc = rsf::dmalloc((void**)&v->table[0], tbytes)) || (rc = rsf::dmalloc((void**)&v->table[1], tbytes)) ||
+      (rc = rsf::dmalloc((void**)&v->adj, (size_t)(p.W ? p.W : 1) * p.shard_n * sizeof(double))) ||
+      (rc = rsf::dmalloc((void**)&v->adj_idx, (size_t)p.shard_n * sizeof(uint32_t))) ||
+      (rc = rsf::dmalloc((void**)&v->filt, (size_t)p.shard_n * peers * p.FR * sizeof(double))) ||
+      (rc = rsf::dmalloc((void**)&v->resets, sizeof(unsigned long long))))
+    return fail(rc);
+  unsigned blocks = (unsigned)((n + 255) / 256);
+  for (int t = 0; t < 2; ++t)
+    hipLaunchKernelGGL(init_rows_kernel, dim3(blocks), dim3(256), 0, v->stream, v->table[t], n, p.stride,
+                       p.dim, p.error_max, p.height_min);
+  if (hipMemsetAsync(v->adj, 0, (size_t)(p.W ? p.W : 1) * p.shard_n * sizeof(double), v->stream) != hipSuccess ||
+      hipMemsetAsync(v->adj_idx, 0, (size_t)p.shard_n * sizeof(uint32_t), v->stream) != hipSuccess ||
+      hipMemsetAsync(v->filt, 0, (size_t)p.shard_n * peers * p.FR * sizeof(double), v->stream) != hipSuccess ||
+      hipMemsetAsync(v->resets, 0, sizeof(unsigned long long), v->stream) != hipSuccess ||
+      hipStreamSynchronize(v->stream) != hipSuccess)
+    return fail(rsf::set_error(RSF_ERR_HIP, "context initialisation failed"));
+  *out = v;
+  return RSF_OK;
+}
+
+int rsf_vivaldi_destroy(rsf_vivaldi* v) {
+  if (!v) return RSF_OK;
+  hipSetDevice(v->device);
+  if (v->stream) hipStreamSynchronize(v->stream);
+  hipFree(v->table[0]);
+  hipFree(v->table[1]);
+  hipFree(v->adj);
+  hipFree(v->adj_idx);
+  hipFree(v->filt);
+  hipFree(v->resets);
+  v->scratch.release();
+  if (v->own) hipStreamDestroy(v->own);
+  delete v;
+  return RSF_OK;
+}
+
+int rsf_vivaldi_set_stream(rsf_vivaldi* v, void* s) {
+  if (!v) return set_err_args("null context");
+  v->stream = s ? (hipStream_t)s : v->own;
+  return RSF_OK;
+}
+
+int rsf_vivaldi_sync(rsf_vivaldi* v) {
+  if (!v) return set_err_args("null context");
+  RSF_HIP(hipSetDevice(v->device));
+  RSF_HIP(hipStreamSynchronize(v->stream));
+  return RSF_OK;
+}
+
+int rsf_vivaldi_get_coordinates(rsf_vivaldi* v, uint64_t first, uint64_t count, double* rows_out) {
+  if (!v || !rows_out) return set_err_args("null argument");
+  if (first + count > v->p.n || first + count < first) return set_err_args("member range out of bounds");
+  RSF_HIP(hipSetDevice(v->device));
+  RSF_HIP(hipMemcpyAsync(rows_out, v->table[v->cur] + first * v->p.stride, count * v->p.stride * sizeof(double),
+                         hipMemcpyDeviceToHost, v->stream));
+  RSF_HIP(hipStreamSynchronize(v->stream));
+  return RSF_OK;
+}
+
+int rsf_vivaldi_set_coordinate(rsf_vivaldi* v, uint64_t m, const double* portion, uint32_t dim, double error,
+                               double adjustment, double height) {
+  if (!v || (!portion && dim)) return set_err_args("null argument");
+  if (m >= v->p.n) return set_err_args("member out of range");
+  // check_coordinate (coordinate.rs:436-446)
+  if (dim != v->p.dim) return rsf::set_error(RSF_ERR_DIM_MISMATCH, "dimensions aren't compatible");
+  bool ok = std::isfinite(error) && std::isfinite(adjustment) && std::isfinite(height);
+  for (uint32_t i = 0; i < dim; ++i) ok = ok && std::isfinite(portion[i]);
+  if (!ok) return rsf::set_error(RSF_ERR_INVALID_COORD, "invalid coordinate");
+  std::vector<double> row(v->p.stride, 0.0);
+  for (uint32_t i = 0; i < dim; ++i) row[i] = portion[i];
+  row[dim] = error;
+  row[dim + 1] = adjustment;
+  row[dim + 2] = height;
+  RSF_HIP(hipSetDevice(v->device));
+  RSF_HIP(hipMemcpyAsync(v->table[v->cur] + m * v->p.stride, row.data(), v->p.stride * sizeof(double),
+                         hipMemcpyHostToDevice, v->stream));
+  RSF_HIP(hipStreamSynchronize(v->stream));
+  return RSF_OK;
+}
+
+int rsf_vivaldi_forget_node(rsf_vivaldi* v, uint64_t m, uint32_t slot) {
+  if (!v) return set_err_args("null context");
+  if (m < v->p.lo || m >= v->p.lo + v->p.shard_n || slot >= v->p.peers) return set_err_args("member/slot out of range");
+  RSF_HIP(hipSetDevice(v->device));
+  RSF_HIP(hipMemsetAsync(v->filt + ((m - v->p.lo) * v->p.peers + slot) * v->p.FR, 0, v->p.FR * sizeof(double),
+                         v->stream));
+  return RSF_OK;
+}
+
+int rsf_vivaldi_resets(rsf_vivaldi* v, uint64_t* out) {
+  if (!v || !out) return set_err_args("null argument");
+  unsigned long long r = 0;
+  RSF_HIP(hipSetDevice(v->device));
+  RSF_HIP(hipMemcpyAsync(&r, v->resets, sizeof(r), hipMemcpyDeviceToHost, v->stream));
+  RSF_HIP(hipStreamSynchronize(v->stream));
+  *out = r;
+  return RSF_OK;
+}
+
+#define RSF_DISPATCH_DF(D_, F_, ...)                                              \
+  do {                                                                            \
+    if ((D_) == 8 && (F_) <= 3) {                                                 \
+      constexpr int kD = 8, kF = 3;                                               \
+      __VA_ARGS__;                                                                \
+    } else if ((F_) <= 3) {                                                       \
+      constexpr int kD = 16, kF = 3;                                              \
+      __VA_ARGS__;                                                                \
+    } else {                                                                      \
+      constexpr int kD = 16, kF = 7;                                              \
+      __VA_ARGS__;                                                                \
+    }                                                                             \
+  } while (0)
+
+int rsf_vivaldi_update_batch(rsf_vivaldi* v, const uint32_t* member, const uint32_t* slot, const double* orows,
+                             const uint32_t* odim, const uint64_t* rtt, uint64_t n, uint32_t round,
+                             int32_t* status, double* rows_out) {
+  if (!v || (n && (!member || !slot || !orows || !rtt || !status))) return set_err_args("null argument");
+  if (n == 0) return RSF_OK;
+  // host-side precondition checks (the reference would panic / index out of bounds)
+  {
+    std::vector<uint8_t> seen(v->p.shard_n, 0);
+    for (uint64_t i = 0; i < n; ++i) {
+      if (member[i] < v->p.lo || member[i] >= v->p.lo + v->p.shard_n) return set_err_args("member outside shard");
+      if (slot[i] >= v->p.peers) return set_err_args("peer_slot out of range");
+      if (seen[member[i] - v->p.lo]++) return set_err_args("a member appears twice in one batch");
+    }
+  }
+  RSF_HIP(hipSetDevice(v->device));
+  const uint64_t st = v->p.stride;
+  size_t bytes[6] = {n * 4, n * 4, n * st * 8, n * 4, n * 8, n * 4};
+  void* d[6];
+  int rc = v->scratch.take(bytes, 6, d);
+  if (rc) return rc;
+  double* drows_out = nullptr;
+  if (rows_out) {
+    size_t b1[1] = {n * st * 8};
+    if ((rc = v->scratch.take_extra(b1[0], (void**)&drows_out))) return rc;
+  }
+  RSF_HIP(hipMemcpyAsync(d[0], member, n * 4, hipMemcpyHostToDevice, v->stream));
+  RSF_HIP(hipMemcpyAsync(d[1], slot, n * 4, hipMemcpyHostToDevice, v->stream));
+  RSF_HIP(hipMemcpyAsync(d[2], orows, n * st * 8, hipMemcpyHostToDevice, v->stream));
+  if (odim) RSF_HIP(hipMemcpyAsync(d[3], odim, n * 4, hipMemcpyHostToDevice, v->stream));
+  RSF_HIP(hipMemcpyAsync(d[4], rtt, n * 8, hipMemcpyHostToDevice, v->stream));
+  VivParams p = v->p;
+  p.round = round;
+  unsigned blocks = (unsigned)((n + 255) / 256);
+  RSF_DISPATCH_DF(p.dim, p.F,
+                  hipLaunchKernelGGL((vivaldi_batch_kernel<kD, kF>), dim3(blocks), dim3(256), 0, v->stream,
+                                     v->table[v->cur], v->adj, v->adj_idx, v->filt, v->resets,
+                                     (const uint32_t*)d[0], (const uint32_t*)d[1], (const double*)d[2],
+                                     odim ? (const uint32_t*)d[3] : nullptr, (const uint64_t*)d[4], n,
+                                     (int32_t*)d[5], drows_out, p));
+  RSF_HIP(hipGetLastError());
+  RSF_HIP(hipMemcpyAsync(status, d[5], n * 4, hipMemcpyDeviceToHost, v->stream));
+  if (rows_out) RSF_HIP(hipMemcpyAsync(rows_out, drows_out, n * st * 8, hipMemcpyDeviceToHost, v->stream));
+  RSF_HIP(hipStreamSynchronize(v->stream));
+  return RSF_OK;
+}
+
+int rsf_vivaldi_estimate_rtt_device(rsf_vivaldi* v, const uint32_t* a, const uint32_t* b, uint64_t n,
+                                    uint64_t* out) {
+  if (!v || (n && (!a || !b || !out))) return set_err_args("null argument");
+  if (n == 0) return RSF_OK;
+  RSF_HIP(hipSetDevice(v->device));
+  unsigned blocks = (unsigned)((n + 255) / 256);
+  if (v->p.dim == 8)
+    hipLaunchKernelGGL((estimate_rtt_kernel<8>), dim3(blocks), dim3(256), 0, v->stream, v->table[v->cur], a, b,
+                       n, out, v->p);
+  else
+    hipLaunchKernelGGL((estimate_rtt_kernel<16>), dim3(blocks), dim3(256), 0, v->stream, v->table[v->cur], a,
+                       b, n, out, v->p);
+  RSF_HIP(hipGetLastError());
+  return RSF_OK;
+}
+
+int rsf_vivaldi_estimate_rtt_batch(rsf_vivaldi* v, const uint32_t* a, const uint32_t* b, uint64_t n,
+                                   uint64_t* out) {
+  if (!v || (n && (!a || !b || !out))) return set_err_args("null argument");
+  if (n == 0) return RSF_OK;
+  for (uint64_t i = 0; i < n; ++i)
+    if (a[i] >= v->p.n || b[i] >= v->p.n) return set_err_args("member out of range");
+  RSF_HIP(hipSetDevice(v->device));
+  size_t bytes[3] = {n * 4, n * 4, n * 8};
+  void* d[3];
+  int rc = v->scratch.take(bytes, 3, d);
+  if (rc) return rc;
+  RSF_HIP(hipMemcpyAsync(d[0], a, n * 4, hipMemcpyHostToDevice, v->stream));
+  RSF_HIP(hipMemcpyAsync(d[1], b, n * 4, hipMemcpyHostToDevice, v->stream));
+  rc = rsf_vivaldi_estimate_rtt_device(v, (const uint32_t*)d[0], (const uint32_t*)d[1], n, (uint64_t*)d[2]);
+  if (rc) return rc;
+  RSF_HIP(hipMemcpyAsync(out, d[2], n * 8, hipMemcpyDeviceToHost, v->stream));
+  RSF_HIP(hipStreamSynchronize(v->stream));
+  return RSF_OK;
+}
+
+int rsf_vivaldi_round(rsf_vivaldi* v, uint32_t round) {
+  if (!v) return set_err_args("null context");
+  RSF_HIP(hipSetDevice(v->device));
+  VivParams p = v->p;
+  p.round = round;
+  unsigned blocks = (unsigned)((p.shard_n + 255) / 256);
+  const double* cur = v->table[v->cur];
+  double* nxt = v->table[v->cur ^ 1];
+  RSF_DISPATCH_DF(p.dim, p.F,
+                  hipLaunchKernelGGL((vivaldi_round_kernel<kD, kF>), dim3(blocks), dim3(256), 0, v->stream, cur,
+                                     nxt, v->adj, v->adj_idx, v->filt, v->resets, p));
+  RSF_HIP(hipGetLastError());
+  v->cur ^= 1;
+  return RSF_OK;
+}
+
+int rsf_vivaldi_table(rsf_vivaldi* v, double** table_out, uint64_t* stride_out) {
+  if (!v || !table_out) return set_err_args("null argument");
+  *table_out = v->table[v->cur];
+  if (stride_out) *stride_out = v->p.stride;
+  return RSF_OK;
+}
+
+int rsf_vivaldi_true_rtt_ns(rsf_vivaldi* v, uint32_t a, uint32_t b, uint64_t* out) {
+  if (!v || !out) return set_err_args("null argument");
+  double xa, ya, ha, xb, yb, hb;
+  true_pos(v->p.k0, v->p.k1, a, xa, ya, ha);
+  true_pos(v->p.k0, v->p.k1, b, xb, yb, hb);
+  double dx = xa - xb, dy = ya - yb;
+  *out = sat_u64((std::sqrt(dx * dx + dy * dy) + ha + hb) * 1.0e9);
+  return RSF_OK;
+}
+
+}  // extern "C"

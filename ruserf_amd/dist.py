@@ -1,0 +1,94 @@
+"""Multi-GPU gossip rounds: one process per GPU, members sharded by contiguous
+id range, RCCL collectives through torch.distributed.
+
+Per round:
+  1. round_begin   — each shard runs memberlist transitions, refutations and
+                     originations for ITS members; every rumor-table entry of
+                     the round is owned by exactly one shard
+  2. all-reduce    — SUM of the round's rumor block (non-owners hold zeros), so
+                     every shard can resolve every rumor id it will receive
+  3. round_emit    — emission + stable sort by global receiver; the sorted
+                     stream is already grouped by destination shard
+  4. all-to-all    — record counts, then the packed (receiver << 32 | rumor)
+                     records; received chunks are concatenated in source-rank
+                     order = ascending sender id
+  5. round_merge   — stable sort by receiver keeps (sender, position) order, so
+                     the merge is the same canonical order as on one GPU
+
+The driver is generic over the engine object (`GossipEngine` on HIP; the
+gloo tests substitute a CPU stand-in that exercises only the routing).
+"""
+import dataclasses
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .gossip import GossipConfig, GossipEngine
+
+
+class CudaArray:
+    """Zero-copy view of engine-owned HBM for torch (RCCL) collectives."""
+
+    def __init__(self, ptr, n, typestr):
+        self.__cuda_array_interface__ = {"shape": (int(n),), "typestr": typestr, "data": (int(ptr), False),
+                                         "version": 3, "strides": None}
+
+
+def hbm_tensor(ptr, n, typestr="<i8"):
+    if n == 0:
+        return torch.empty(0, dtype=torch.int64, device="cuda")
+    return torch.as_tensor(CudaArray(ptr, n, typestr), device="cuda")
+
+
+class EngineBuffers:
+    """torch views of a GossipEngine's exchange buffers."""
+
+    def __init__(self, eng: GossipEngine):
+        self.eng = eng
+        ptr, cap = eng.send_buffer()
+        self.send = hbm_tensor(ptr, cap)
+        self.recv = torch.empty(cap, dtype=torch.int64, device="cuda")
+
+    def rumor_block(self):
+        ptr, nbytes = self.eng.rumor_block()
+        return hbm_tensor(ptr, nbytes // 8)
+
+    def merge(self, n_recv):
+        self.eng.round_merge(self.recv.data_ptr(), n_recv)
+
+
+class ShardedGossip:
+    def __init__(self, cfg: GossipConfig, rank, world, device=0, engine=None, buffers=None, group=None):
+        if cfg.n_members % world:
+            raise ValueError("n_members must divide evenly over the world")
+        per = cfg.n_members // world
+        self.rank, self.world, self.group = rank, world, group
+        self.shard = (rank * per, (rank + 1) * per)
+        if engine is None:
+            engine = GossipEngine(dataclasses.replace(cfg, shard=self.shard), device)
+            engine.set_stream(torch.cuda.current_stream().cuda_stream)
+        self.eng = engine
+        self.buf = buffers if buffers is not None else EngineBuffers(engine)
+        self.dev = self.buf.recv.device
+        self.last_in = 0
+
+    def round(self, t, ml=None, acts=None):
+        eng, buf = self.eng, self.buf
+        eng.round_begin(t, ml, acts)
+        blk = buf.rumor_block()
+        if blk.numel():
+            dist.all_reduce(blk, group=self.group)
+        counts = eng.round_emit(self.world)
+        send_counts = torch.from_numpy(counts.astype(np.int64)).to(self.dev)
+        recv_counts = torch.empty_like(send_counts)
+        dist.all_to_all_single(recv_counts, send_counts, group=self.group)
+        rc = recv_counts.cpu().tolist()
+        n_in, n_out = int(sum(rc)), int(counts.sum())
+        if n_in > buf.recv.numel():
+            raise RuntimeError(f"shard {self.rank}: {n_in} records exceed the receive capacity {buf.recv.numel()}")
+        dist.all_to_all_single(buf.recv[:n_in], buf.send[:n_out], output_split_sizes=rc,
+                               input_split_sizes=[int(x) for x in counts], group=self.group)
+        buf.merge(n_in)
+        self.last_in = n_in
+        return n_out, n_in

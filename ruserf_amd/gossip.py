@@ -1,0 +1,250 @@
+"""Gossip round engine: host mirror of ruserf's merge/dissemination surface.
+
+The reference's hot path for membership is driven by memberlist through
+`SerfDelegate` (core/src/serf/delegate.rs:111-795): `notify_message`
+dispatches to `handle_node_join_intent` / `handle_node_leave_intent` /
+`handle_user_event` / `handle_query` (core/src/serf/base.rs), re-queueing the
+message when the handler returns true; `broadcast_messages` drains the three
+transmit-limited queues; `notify_join` / `notify_leave` call
+`handle_node_join` / `handle_node_leave`.  `GossipEngine` holds a whole
+cluster (or one shard of it) in HBM and runs those handlers as HIP kernels:
+
+  * `apply_batch(msgs)`   — notify_message over a batch (returns the handler results)
+  * `round(t, ml, acts)`  — one full round: memberlist transitions, originations
+                            (Serf::join/leave/user_event/query/force_leave), emission
+                            (broadcast_messages to k peers), exchange, canonical merge
+  * `round_begin/emit/merge` — the same split for multi-GPU sharding (see dist.py)
+
+There is no CPU execution path: every call goes to libruserf_amd.so.
+"""
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._gossip_sigs import RsfGossipCfg
+from ._lib import check, lib, ptr
+
+# encodings (include/ruserf_amd.h)
+KIND_UNKNOWN, KIND_INTENT_JOIN, KIND_INTENT_LEAVE, KIND_KNOWN = 0, 1, 2, 3
+STATUS_NONE, STATUS_ALIVE, STATUS_LEAVING, STATUS_LEFT, STATUS_FAILED = 0, 1, 2, 3, 4
+MSG_LEAVE, MSG_JOIN, MSG_USER_EVENT, MSG_QUERY = 0, 1, 3, 4
+F_REBROADCAST, F_REFUTE, F_PRUNE, F_DELIVER, F_MEMBER_EVENT = 1, 2, 4, 8, 16
+ACT_JOIN_SELF, ACT_LEAVE_SELF, ACT_FORCE_LEAVE, ACT_USER_EVENT, ACT_QUERY = 1, 2, 3, 4, 5
+ML_JOIN, ML_LEAVE = 1, 2
+
+ACTION_DTYPE = np.dtype([("member", "<u4"), ("act", "<u4"), ("subject", "<u4"), ("name_len", "<u4"),
+                         ("payload_len", "<u4"), ("flags", "<u4"), ("key", "<u8")])
+ML_DTYPE = np.dtype([("subject", "<u4"), ("kind", "<u4"), ("set_alive", "<u4"), ("_r", "<u4")])
+MSG_DTYPE = np.dtype([("receiver", "<u4"), ("subject", "<u4"), ("ltime", "<u8"), ("key", "<u8"), ("type", "u1"),
+                      ("flags", "u1"), ("_r0", "<u2"), ("_r1", "<u4")])
+RUMOR_DTYPE = np.dtype([("ltime", "<u8"), ("key", "<u8"), ("subject", "<u4"), ("type", "u1"), ("flags", "u1"),
+                        ("msg_len", "<u2")])
+assert ACTION_DTYPE.itemsize == 32 and ML_DTYPE.itemsize == 16 and MSG_DTYPE.itemsize == 32
+assert RUMOR_DTYPE.itemsize == 24
+
+
+@dataclass
+class GossipConfig:
+    n_members: int
+    n_subjects: int
+    shard: tuple = None            # (lo, hi); default the whole cluster
+    queue_cap: int = 64            # slots per transmit-limited queue
+    event_buffer_size: int = 512   # Options::event_buffer_size default
+    query_buffer_size: int = 512   # Options::query_buffer_size default
+    slot_k: int = 8
+    fanout: int = 3                # gossip targets per round
+    gossip_limit: int = 8 * 24     # byte budget per gossip message: 8 intents of ~22 B + 2 B overhead
+    gossip_overhead: int = 2
+    retransmit_mult: int = 4       # memberlist LAN default
+    max_refute: int = 4
+    max_rumors: int = 1 << 20
+    seed: int = 0x5EED5EED
+
+    def to_c(self):
+        lo, hi = self.shard if self.shard is not None else (0, self.n_members)
+        return RsfGossipCfg(n_members=self.n_members, shard_lo=lo, shard_hi=hi, n_subjects=self.n_subjects,
+                            queue_cap=self.queue_cap, event_buffer_size=self.event_buffer_size,
+                            query_buffer_size=self.query_buffer_size, slot_k=self.slot_k, fanout=self.fanout,
+                            gossip_limit=self.gossip_limit, gossip_overhead=self.gossip_overhead,
+                            retransmit_mult=self.retransmit_mult, max_refute=self.max_refute,
+                            max_rumors=self.max_rumors, seed=self.seed)
+
+
+def _p(a):
+    return C.c_void_p(a.ctypes.data) if a is not None and len(a) else None
+
+
+class GossipEngine:
+    def __init__(self, cfg: GossipConfig, device=0):
+        self.cfg = cfg
+        self.lo, self.hi = cfg.shard if cfg.shard is not None else (0, cfg.n_members)
+        self.n_loc = self.hi - self.lo
+        h = C.c_void_p()
+        c = cfg.to_c()
+        check(lib().rsf_gossip_create(C.byref(h), C.byref(c), device))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rsf_gossip_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- setup
+    def set_stream(self, s):
+        check(lib().rsf_gossip_set_stream(self._h, C.c_void_p(s)))
+
+    def sync(self):
+        check(lib().rsf_gossip_sync(self._h))
+
+    def set_subjects(self, subject_member):
+        a = np.ascontiguousarray(subject_member, dtype=np.uint32)
+        check(lib().rsf_gossip_set_subjects(self._h, ptr(a, C.c_uint32)))
+
+    def init_views(self, kind, status, ltime):
+        k = np.ascontiguousarray(kind, dtype=np.uint8)
+        s = np.ascontiguousarray(status, dtype=np.uint8)
+        t = np.ascontiguousarray(ltime, dtype=np.uint64)
+        check(lib().rsf_gossip_init_views(self._h, ptr(k, C.c_uint8), ptr(s, C.c_uint8), ptr(t, C.c_uint64)))
+
+    def set_view(self, member, subject, kind, status, ltime):
+        check(lib().rsf_gossip_set_view(self._h, member, subject, kind, status, ltime))
+
+    def set_alive(self, alive):
+        a = np.ascontiguousarray(alive, dtype=np.uint8)
+        check(lib().rsf_gossip_set_alive(self._h, ptr(a, C.c_uint8)))
+
+    def set_clocks(self, member, clock, event_clock, query_clock):
+        check(lib().rsf_gossip_set_clocks(self._h, member, clock, event_clock, query_clock))
+
+    def set_min_times(self, member, event_min, query_min):
+        check(lib().rsf_gossip_set_min_times(self._h, member, event_min, query_min))
+
+    def set_serf_state(self, member, state):
+        check(lib().rsf_gossip_set_serf_state(self._h, member, state))
+
+    # ---- SerfDelegate::notify_message over a batch
+    def apply_batch(self, msgs):
+        msgs = np.ascontiguousarray(msgs, dtype=MSG_DTYPE)
+        n = len(msgs)
+        flags = np.zeros(n, dtype=np.int32)
+        refute = np.zeros(n, dtype=np.uint64)
+        check(lib().rsf_gossip_apply_batch(self._h, _p(msgs), n, ptr(flags, C.c_int32), ptr(refute, C.c_uint64)))
+        return flags, refute
+
+    # ---- rounds
+    def round(self, t, ml=None, acts=None):
+        ml = np.ascontiguousarray(ml if ml is not None else np.zeros(0, ML_DTYPE), dtype=ML_DTYPE)
+        acts = np.ascontiguousarray(acts if acts is not None else np.zeros(0, ACTION_DTYPE), dtype=ACTION_DTYPE)
+        check(lib().rsf_gossip_round(self._h, t, _p(ml), len(ml), _p(acts), len(acts)))
+
+    def round_begin(self, t, ml=None, acts=None):
+        ml = np.ascontiguousarray(ml if ml is not None else np.zeros(0, ML_DTYPE), dtype=ML_DTYPE)
+        acts = np.ascontiguousarray(acts if acts is not None else np.zeros(0, ACTION_DTYPE), dtype=ACTION_DTYPE)
+        check(lib().rsf_gossip_round_begin(self._h, t, _p(ml), len(ml), _p(acts), len(acts)))
+
+    def rumor_block(self):
+        p = C.c_void_p()
+        b = C.c_uint64()
+        check(lib().rsf_gossip_rumor_block(self._h, C.byref(p), C.byref(b)))
+        return p.value, b.value
+
+    def round_emit(self, world):
+        counts = np.zeros(world, dtype=np.uint64)
+        check(lib().rsf_gossip_round_emit(self._h, world, ptr(counts, C.c_uint64)))
+        return counts
+
+    def send_buffer(self):
+        p = C.c_void_p()
+        cap = C.c_uint64()
+        check(lib().rsf_gossip_send_buffer(self._h, C.byref(p), C.byref(cap)))
+        return p.value, cap.value
+
+    def round_merge(self, recv_ptr, n_recv):
+        check(lib().rsf_gossip_round_merge(self._h, C.c_void_p(recv_ptr), n_recv))
+
+    # ---- inspection
+    def members(self):
+        n = self.n_loc
+        out = {k: np.zeros(n, dtype=np.uint64) for k in ["clock", "event_clock", "query_clock", "digest"]}
+        err = np.zeros(n, dtype=np.uint32)
+        ss = np.zeros(n, dtype=np.uint8)
+        check(lib().rsf_gossip_dump_members(self._h, ptr(out["clock"], C.c_uint64), ptr(out["event_clock"], C.c_uint64),
+                                            ptr(out["query_clock"], C.c_uint64), ptr(out["digest"], C.c_uint64),
+                                            ptr(err, C.c_uint32), ptr(ss, C.c_uint8)))
+        out["err"] = err
+        out["serf_state"] = ss
+        return out
+
+    def view(self):
+        n = self.n_loc * self.cfg.n_subjects
+        lt = np.zeros(n, dtype=np.uint64)
+        st = np.zeros(n, dtype=np.uint8)
+        kd = np.zeros(n, dtype=np.uint8)
+        check(lib().rsf_gossip_dump_view(self._h, ptr(lt, C.c_uint64), ptr(st, C.c_uint8), ptr(kd, C.c_uint8)))
+        return lt, st, kd
+
+    def queues(self):
+        n = self.n_loc * 3 * self.cfg.queue_cap
+        r = np.zeros(n, dtype=np.uint32)
+        sq = np.zeros(n, dtype=np.uint32)
+        tx = np.zeros(n, dtype=np.uint16)
+        ln = np.zeros(n, dtype=np.uint16)
+        ns = np.zeros(self.n_loc * 3, dtype=np.uint32)
+        check(lib().rsf_gossip_dump_queues(self._h, ptr(r, C.c_uint32), ptr(sq, C.c_uint32), ptr(tx, C.c_uint16),
+                                           ptr(ln, C.c_uint16), ptr(ns, C.c_uint32)))
+        return r, sq, tx, ln, ns
+
+    def buffers(self):
+        c = self.cfg
+        n = self.n_loc
+        ebl = np.zeros(n * c.event_buffer_size, dtype=np.uint64)
+        ebc = np.zeros(n * c.event_buffer_size, dtype=np.uint32)
+        ebk = np.zeros(n * c.event_buffer_size * c.slot_k, dtype=np.uint64)
+        qbl = np.zeros(n * c.query_buffer_size, dtype=np.uint64)
+        qbc = np.zeros(n * c.query_buffer_size, dtype=np.uint32)
+        qbi = np.zeros(n * c.query_buffer_size * c.slot_k, dtype=np.uint32)
+        check(lib().rsf_gossip_dump_buffers(self._h, ptr(ebl, C.c_uint64), ptr(ebc, C.c_uint32), ptr(ebk, C.c_uint64),
+                                            ptr(qbl, C.c_uint64), ptr(qbc, C.c_uint32), ptr(qbi, C.c_uint32)))
+        return ebl, ebc, ebk, qbl, qbc, qbi
+
+    def rumors(self, first, count):
+        out = np.zeros(count, dtype=RUMOR_DTYPE)
+        check(lib().rsf_gossip_dump_rumors(self._h, first, count, _p(out)))
+        return out
+
+    def refutes(self):
+        c = self.cfg
+        cnt = np.zeros(c.n_subjects, dtype=np.uint32)
+        lt = np.zeros(c.n_subjects * c.max_refute, dtype=np.uint64)
+        check(lib().rsf_gossip_dump_refutes(self._h, ptr(cnt, C.c_uint32), ptr(lt, C.c_uint64)))
+        return cnt, lt
+
+    def last_round_stats(self):
+        s = C.c_uint64()
+        m = C.c_uint64()
+        check(lib().rsf_gossip_last_round_stats(self._h, C.byref(s), C.byref(m)))
+        return s.value, m.value
+
+    # ---- measurement
+    def set_profiling(self, on=True):
+        check(lib().rsf_gossip_set_profiling(self._h, 1 if on else 0))
+
+    def phase_times(self):
+        """Summed device ms of [begin, emit, sort(+exchange), merge] and the rounds covered."""
+        ms = (C.c_double * 4)()
+        r = C.c_uint32()
+        check(lib().rsf_gossip_phase_times(self._h, ms, C.byref(r)))
+        return list(ms), r.value
+
+    def merged_total(self):
+        t = C.c_uint64()
+        check(lib().rsf_gossip_totals(self._h, C.byref(t)))
+        return t.value

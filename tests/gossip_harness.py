@@ -1,0 +1,110 @@
+"""Builds matching (GPU engine, CPU oracle world) pairs and compares their full
+state bit for bit.  Test infrastructure: the oracle is only the checker."""
+import ctypes as C
+
+import numpy as np
+
+import oracle_ffi as O
+
+L = O.lib()
+
+
+def oracle_world(cfg, subj_member, views):
+    wc = O.WorldCfg(n=cfg.n_members, s=cfg.n_subjects, qcap=cfg.queue_cap, ebuf=cfg.event_buffer_size,
+                    qbuf=cfg.query_buffer_size, slot_k=cfg.slot_k, fanout=cfg.fanout, limit=cfg.gossip_limit,
+                    overhead=cfg.gossip_overhead, retransmit_mult=cfg.retransmit_mult, max_refute=cfg.max_refute,
+                    cap_rumors=cfg.max_rumors, seed=cfg.seed)
+    w = O.World()
+    assert L.orc_world_init(C.byref(w), C.byref(wc)) == 0
+    n, s = cfg.n_members, cfg.n_subjects
+    sm = O.arr(w.subj_member, s, np.uint32)
+    sm[:] = subj_member
+    ms = O.arr(w.member_subj, n, np.int32)
+    ms[subj_member] = np.arange(s, dtype=np.int32)
+    kind, status, ltime = views
+    O.arr(w.v_kind, n * s, np.uint8).reshape(n, s)[:] = kind[None, :]
+    O.arr(w.v_status, n * s, np.uint8).reshape(n, s)[:] = status[None, :]
+    O.arr(w.v_ltime, n * s, np.uint64).reshape(n, s)[:] = ltime[None, :]
+    return w
+
+
+def oracle_round(w, t, ml, acts):
+    ml = np.ascontiguousarray(ml, dtype=np.dtype([("subject", "<u4"), ("kind", "<u4"), ("set_alive", "<u4"),
+                                                  ("_r", "<u4")]))
+    acts = np.ascontiguousarray(acts)
+    rc = L.orc_world_round(C.byref(w), t, ml.ctypes.data_as(C.POINTER(O.MlEvent)), len(ml),
+                           acts.ctypes.data_as(C.POINTER(O.Action)), len(acts))
+    assert rc == 0
+
+
+def world_state(w, lo=0, hi=None):
+    n, s, q = w.n, w.s, w.qcap
+    hi = n if hi is None else hi
+    sl = slice(lo, hi)
+    st = {
+        "clock": O.arr(w.clock, n, np.uint64)[sl],
+        "event_clock": O.arr(w.eclock, n, np.uint64)[sl],
+        "query_clock": O.arr(w.qclock, n, np.uint64)[sl],
+        "digest": O.arr(w.digest, n, np.uint64)[sl],
+        "err": O.arr(w.err, n, np.uint32)[sl],
+        "serf_state": O.arr(w.serf_state, n, np.uint8)[sl],
+        "v_ltime": O.arr(w.v_ltime, n * s, np.uint64).reshape(n, s)[sl],
+        "v_status": O.arr(w.v_status, n * s, np.uint8).reshape(n, s)[sl],
+        "v_kind": O.arr(w.v_kind, n * s, np.uint8).reshape(n, s)[sl],
+        "q_rumor": O.arr(w.q_rumor, n * 3 * q, np.uint32).reshape(n, 3 * q)[sl],
+        "q_seq": O.arr(w.q_seq, n * 3 * q, np.uint32).reshape(n, 3 * q)[sl],
+        "q_tx": O.arr(w.q_tx, n * 3 * q, np.uint16).reshape(n, 3 * q)[sl],
+        "q_len": O.arr(w.q_len, n * 3 * q, np.uint16).reshape(n, 3 * q)[sl],
+        "q_next_seq": O.arr(w.q_next_seq, n * 3, np.uint32).reshape(n, 3)[sl],
+        "eb_ltime": O.arr(w.eb_ltime, n * w.ebuf, np.uint64).reshape(n, -1)[sl],
+        "eb_cnt": O.arr(w.eb_cnt, n * w.ebuf, np.uint32).reshape(n, -1)[sl],
+        "eb_keys": O.arr(w.eb_keys, n * w.ebuf * w.slot_k, np.uint64).reshape(n, -1)[sl],
+        "qb_ltime": O.arr(w.qb_ltime, n * w.qbuf, np.uint64).reshape(n, -1)[sl],
+        "qb_cnt": O.arr(w.qb_cnt, n * w.qbuf, np.uint32).reshape(n, -1)[sl],
+        "qb_ids": O.arr(w.qb_ids, n * w.qbuf * w.slot_k, np.uint32).reshape(n, -1)[sl],
+    }
+    return st
+
+
+def engine_state(g):
+    n, s, q = g.n_loc, g.cfg.n_subjects, g.cfg.queue_cap
+    m = g.members()
+    lt, stt, kd = g.view()
+    r, sq, tx, ln, ns = g.queues()
+    ebl, ebc, ebk, qbl, qbc, qbi = g.buffers()
+    return {
+        "clock": m["clock"], "event_clock": m["event_clock"], "query_clock": m["query_clock"],
+        "digest": m["digest"], "err": m["err"], "serf_state": m["serf_state"],
+        "v_ltime": lt.reshape(n, s), "v_status": stt.reshape(n, s), "v_kind": kd.reshape(n, s),
+        "q_rumor": r.reshape(n, -1), "q_seq": sq.reshape(n, -1), "q_tx": tx.reshape(n, -1),
+        "q_len": ln.reshape(n, -1), "q_next_seq": ns.reshape(n, 3),
+        "eb_ltime": ebl.reshape(n, -1), "eb_cnt": ebc.reshape(n, -1), "eb_keys": ebk.reshape(n, -1),
+        "qb_ltime": qbl.reshape(n, -1), "qb_cnt": qbc.reshape(n, -1), "qb_ids": qbi.reshape(n, -1),
+    }
+
+
+def normalize_queues(st):
+    """Queue slots whose rumor is empty carry stale seq/tx/len; zero them for comparison."""
+    st = dict(st)
+    empty = st["q_rumor"] == 0xFFFFFFFF
+    for k in ["q_seq", "q_tx", "q_len"]:
+        a = st[k].copy()
+        a[empty] = 0
+        st[k] = a
+    return st
+
+
+def assert_same(a, b, ctx=""):
+    a = normalize_queues(a)
+    b = normalize_queues(b)
+    for k in a:
+        x, y = np.asarray(a[k]), np.asarray(b[k])
+        if not np.array_equal(x, y):
+            bad = np.argwhere(x != y)
+            raise AssertionError(f"{ctx}: field {k} differs at {len(bad)} places, first {bad[:5].tolist()}: "
+                                 f"got {x[tuple(bad[0])]} expected {y[tuple(bad[0])]}")
+
+
+def oracle_rumors(w):
+    return [(w.rumors[i].type, w.rumors[i].ltime, w.rumors[i].subject, w.rumors[i].key, w.rumors[i].msg_len)
+            for i in range(w.n_rumors)]

@@ -1,0 +1,169 @@
+"""GPU parity of the gossip round (member-state merge + dissemination) against
+the CPU oracle: bit-exact over clocks, views, queues, dedup rings, digests of
+delivered events, refutations and error bits."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import gossip_harness as H
+import oracle_ffi as O
+from ruserf_amd import gossip as G
+from ruserf_amd import workload as W
+
+pytestmark = pytest.mark.gpu
+L = O.lib()
+
+
+def pair(cfg, subj_member, views):
+    g = G.GossipEngine(cfg)
+    g.set_subjects(subj_member)
+    g.init_views(*views)
+    w = H.oracle_world(cfg, subj_member, views)
+    return g, w
+
+
+@pytest.mark.parametrize("n,s,rounds,rate,qcap,limit", [
+    (2000, 64, 12, 0.01, 64, 8 * 24),
+    (1500, 100, 10, 0.03, 16, 8 * 24),
+    (700, 50, 15, 0.02, 8, 1400),
+    (3000, 32, 8, 0.005, 64, 3 * 24),
+])
+def test_intent_rounds_bit_exact(n, s, rounds, rate, qcap, limit):
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=qcap, gossip_limit=limit, max_rumors=1 << 16,
+                         event_buffer_size=64, query_buffer_size=64, slot_k=4)
+    subj, acts, ml = W.intents_workload(n, s, rounds, rate=rate, seed=7 + n)
+    views = W.initial_views(s)
+    g, w = pair(cfg, subj, views)
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t])
+        H.assert_same(H.engine_state(g), H.world_state(w), f"round {t}")
+    assert w.merges > 0
+    assert int(np.sum(H.engine_state(g)["clock"])) > n  # clocks advanced
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
+@pytest.mark.parametrize("n,rounds", [(3000, 14), (1200, 20)])
+def test_churn_and_flood_bit_exact(n, rounds):
+    cfg = G.GossipConfig(n_members=n, n_subjects=max(1, n // 100), queue_cap=32, gossip_limit=400,
+                         max_rumors=1 << 16, event_buffer_size=512, query_buffer_size=512, slot_k=8)
+    subj, acts, ml = W.churn_workload(n, rounds, events_per_round=30, queries_per_round=5, seed=11 + n)
+    views = W.initial_views(len(subj))
+    g, w = pair(cfg, subj, views)
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t])
+        H.assert_same(H.engine_state(g), H.world_state(w), f"round {t}")
+    st = H.engine_state(g)
+    assert np.any(st["eb_cnt"] > 0) and np.any(st["qb_cnt"] > 0)
+    assert np.any(st["v_status"] == G.STATUS_LEFT) or np.any(st["v_status"] == G.STATUS_FAILED)
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
+def test_unknown_subjects_buffer_intents_then_join():
+    """Subjects start unknown: intents go to the recent-intent buffer
+    (upsert_intent), and a memberlist NotifyJoin consumes it (handle_node_join)."""
+    n, s, rounds = 800, 20, 10
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=32, max_rumors=1 << 15,
+                         event_buffer_size=32, query_buffer_size=32, slot_k=2)
+    subj, acts, _ = W.intents_workload(n, s, rounds, rate=0.02, seed=99)
+    views = (np.zeros(s, np.uint8), np.zeros(s, np.uint8), np.zeros(s, np.uint64))
+    g, w = pair(cfg, subj, views)
+    for t in range(rounds):
+        ml = np.zeros(0, G.ML_DTYPE)
+        if t == 6:
+            ml = np.zeros(s, G.ML_DTYPE)
+            ml["subject"] = np.arange(s)
+            ml["kind"] = G.ML_JOIN
+            ml["set_alive"] = 2
+        g.round(t, ml, acts[t])
+        H.oracle_round(w, t, ml, acts[t])
+        H.assert_same(H.engine_state(g), H.world_state(w), f"round {t}")
+    kinds = H.engine_state(g)["v_kind"].copy()
+    # a subject does not receive memberlist's NotifyJoin about itself (m == subject is skipped)
+    kinds[subj, np.arange(s)] = G.KIND_KNOWN
+    assert np.all(kinds == G.KIND_KNOWN)
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
+def test_apply_batch_matches_oracle_handlers():
+    """notify_message over a random batch (join/leave intents, user events,
+    queries), several messages per receiver, in array order per receiver."""
+    n, s = 300, 12
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=8, max_rumors=1024, event_buffer_size=16,
+                         query_buffer_size=16, slot_k=4)
+    subj = W.subjects_for(n, s)
+    rng = np.random.default_rng(5)
+    kinds = rng.integers(0, 4, s).astype(np.uint8)
+    status = rng.integers(0, 5, s).astype(np.uint8)
+    lt = rng.integers(0, 20, s).astype(np.uint64)
+    g, w = pair(cfg, subj, (kinds, status, lt))
+    for rep in range(4):
+        k = 3000
+        msgs = np.zeros(k, G.MSG_DTYPE)
+        msgs["receiver"] = rng.integers(0, n, k)
+        msgs["type"] = rng.choice([G.MSG_JOIN, G.MSG_LEAVE, G.MSG_USER_EVENT, G.MSG_QUERY], k)
+        msgs["subject"] = rng.integers(0, s, k)
+        msgs["ltime"] = rng.integers(0, 60 + 40 * rep, k)
+        msgs["key"] = rng.integers(0, 6, k)
+        msgs["flags"] = rng.integers(0, 2, k)
+        flags, refute = g.apply_batch(msgs)
+        for i in range(k):
+            m, t = int(msgs["receiver"][i]), int(msgs["type"][i])
+            ref = C.c_uint64(0)
+            if t == G.MSG_JOIN:
+                f = L.orc_handle_join_intent(C.byref(w), m, int(msgs["subject"][i]), int(msgs["ltime"][i]))
+            elif t == G.MSG_LEAVE:
+                f = L.orc_handle_leave_intent(C.byref(w), m, int(msgs["subject"][i]), int(msgs["ltime"][i]),
+                                              int(msgs["flags"][i]), C.byref(ref))
+            elif t == G.MSG_USER_EVENT:
+                f = L.orc_handle_user_event(C.byref(w), m, int(msgs["ltime"][i]), int(msgs["key"][i]))
+            else:
+                f = L.orc_handle_query(C.byref(w), m, int(msgs["ltime"][i]), int(msgs["key"][i]), int(msgs["flags"][i]))
+            assert flags[i] == f, (rep, i, t)
+            if f & O.F_REFUTE:
+                assert refute[i] == ref.value
+        H.assert_same(H.engine_state(g), H.world_state(w), f"batch {rep}")
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
+def test_large_round_properties():
+    """1M members (BASELINE configs[1] size), 256 subjects: invariants that hold at
+    any size — Lamport clocks never decrease and exceed every status_time a
+    member has accepted, queue transmit counts stay under the retransmit limit,
+    and two runs with the same seed are identical."""
+    n, s, rounds = 1_000_000, 256, 4
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, max_rumors=1 << 20, event_buffer_size=8, query_buffer_size=8,
+                         slot_k=1)
+    subj, acts, ml = W.intents_workload(n, s, rounds, rate=0.01, seed=1)
+    digests = []
+    for rep in range(2):
+        g = G.GossipEngine(cfg)
+        g.set_subjects(subj)
+        g.init_views(*W.initial_views(s))
+        prev = None
+        for t in range(rounds):
+            g.round(t, ml[t], acts[t])
+            m = g.members()
+            if prev is not None:
+                assert np.all(m["clock"] >= prev)
+            prev = m["clock"]
+        lt, st, kd = g.view()
+        lt = lt.reshape(n, s)
+        known = kd.reshape(n, s) == G.KIND_KNOWN
+        # every status_time accepted from a message was witnessed: clock > ltime (initial views hold ltime 1)
+        accepted = np.where(known & (lt > 1), lt, 0).max(axis=1)
+        assert np.all(accepted < prev)
+        r, sq, tx, ln, ns = g.queues()
+        limit = O.lib().orc_retransmit_limit(4, n)
+        assert np.all(tx[r != 0xFFFFFFFF] < limit)
+        sent, merged = g.last_round_stats()
+        assert sent > 0 and merged == sent
+        digests.append((m["digest"].copy(), lt.sum()))
+        g.close()
+    assert np.array_equal(digests[0][0], digests[1][0]) and digests[0][1] == digests[1][1]

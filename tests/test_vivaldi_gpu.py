@@ -1,0 +1,182 @@
+"""GPU parity: the HIP Vivaldi kernels against the CPU oracle, bit-exact.
+
+North-star tolerance for float64 coordinates is 1e-9 relative; the kernels are
+built with -ffp-contract=off and are expected to be BIT-EXACT, which these
+tests assert (ATOL = RTOL = 0)."""
+import ctypes as C
+import math
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+from ruserf_amd import Coordinate, CoordinateClients, CoordinateError, CoordinateOptions
+
+pytestmark = pytest.mark.gpu
+L = O.lib()
+SEED = 0x5EED5EED
+
+
+def oracle_pop(n, peers, opts, seed=SEED):
+    p = O.VivaldiPop()
+    oo = O.default_opts(dimensionality=opts.dimensionality, height_min=opts.height_min,
+                        latency_filter_size=opts.latency_filter_size,
+                        adjustment_window_size=opts.adjustment_window_size)
+    assert L.orc_vivaldi_pop_init(C.byref(p), n, peers, C.byref(oo), seed) == 0
+    return p
+
+
+def oracle_rows(p):
+    return O.arr(p.rows_cur, p.n * p.row_stride, np.float64).reshape(p.n, p.row_stride).copy()
+
+
+@pytest.mark.parametrize("n,peers,rounds,dim,F", [(1000, 16, 60, 8, 3), (257, 5, 25, 3, 3),
+                                                  (300, 4, 20, 8, 5)])
+def test_population_rounds_bit_exact(n, peers, rounds, dim, F):
+    opts = CoordinateOptions(dimensionality=dim, latency_filter_size=F)
+    g = CoordinateClients(n, peers, opts, seed=SEED)
+    p = oracle_pop(n, peers, opts)
+    for t in range(rounds):
+        g.round(t)
+    L.orc_vivaldi_pop_rounds(C.byref(p), 0, rounds, 8)
+    got, exp = g.get_rows(), oracle_rows(p)
+    assert np.all(np.isfinite(got))
+    np.testing.assert_array_equal(got.view(np.uint64), exp.view(np.uint64))
+    assert g.stats()["resets"] == p.resets
+    L.orc_vivaldi_pop_free(C.byref(p))
+    g.close()
+
+
+def test_population_large_bit_exact():
+    # 200k members x 4 rounds (the oracle needs a few seconds on 8 threads)
+    n, peers, rounds = 200_000, 16, 4
+    opts = CoordinateOptions()
+    g = CoordinateClients(n, peers, opts, seed=SEED ^ 0xABC)
+    p = oracle_pop(n, peers, opts, seed=SEED ^ 0xABC)
+    for t in range(rounds):
+        g.round(t)
+    L.orc_vivaldi_pop_rounds(C.byref(p), 0, rounds, 8)
+    np.testing.assert_array_equal(g.get_rows().view(np.uint64), oracle_rows(p).view(np.uint64))
+    L.orc_vivaldi_pop_free(C.byref(p))
+    g.close()
+
+
+def test_round_is_deterministic_and_converges():
+    n = 1000
+    a = CoordinateClients(n, 16, seed=SEED)
+    b = CoordinateClients(n, 16, seed=SEED)
+    for t in range(200):
+        a.round(t)
+        b.round(t)
+    np.testing.assert_array_equal(a.get_rows(), b.get_rows())
+    # estimate_rtt vs ground truth: median relative error over random pairs
+    rng = np.random.default_rng(1)
+    i = rng.integers(0, n, 4000, dtype=np.uint32)
+    j = rng.integers(0, n, 4000, dtype=np.uint32)
+    keep = i != j
+    est = a.distance_to(i[keep], j[keep]).astype(np.float64)
+    true = np.array([a.true_rtt_ns(int(x), int(y)) for x, y in zip(i[keep], j[keep])], dtype=np.float64)
+    med = np.median(np.abs(est - true) / true)
+    assert med < 0.25, med
+
+
+def test_estimate_rtt_matches_oracle():
+    n = 2000
+    g = CoordinateClients(n, 8, seed=SEED)
+    for t in range(10):
+        g.round(t)
+    rows = g.get_rows()
+    rng = np.random.default_rng(2)
+    a = rng.integers(0, n, 5000, dtype=np.uint32)
+    b = rng.integers(0, n, 5000, dtype=np.uint32)
+    got = g.distance_to(a, b)
+    opts = O.default_opts()
+    for k in range(0, 5000, 7):
+        ca = O.coord(opts, list(rows[a[k], :8]), rows[a[k], 8], rows[a[k], 9], rows[a[k], 10])
+        cb = O.coord(opts, list(rows[b[k], :8]), rows[b[k], 8], rows[b[k], 9], rows[b[k], 10])
+        assert got[k] == L.orc_coord_distance_ns(C.byref(ca), C.byref(cb))
+
+
+def test_update_batch_matches_oracle_clients():
+    """Batched CoordinateClient::update with explicit `other` coordinates, including
+    every error path, against one oracle client per member."""
+    n, slots, dim = 64, 4, 8
+    opts = CoordinateOptions()
+    g = CoordinateClients(n, slots, opts, seed=SEED)
+    oo = O.default_opts()
+    clients = []
+    for m in range(n):
+        c = O.Client()
+        assert L.orc_client_init(C.byref(c), C.byref(oo), slots) == 0
+        clients.append(c)
+    rng = np.random.default_rng(3)
+    for rnd in range(30):
+        members = rng.permutation(n)[:40].astype(np.uint32)
+        slot = rng.integers(0, slots, 40).astype(np.uint32)
+        others, rtts = [], []
+        for i in range(40):
+            o = Coordinate(rng.normal(0, 0.02, dim), float(rng.uniform(0, 1.5)), float(rng.normal(0, 1e-3)),
+                           float(rng.uniform(1e-5, 1e-3)))
+            kind = rng.integers(0, 20)
+            if kind == 0:
+                o.portion[1] = math.nan
+            elif kind == 1:
+                o = Coordinate(np.zeros(3), 1.5, 0.0, 1e-5)
+            rtt = int(rng.integers(0, 200_000_000))
+            if kind == 2:
+                rtt = 10_000_000_001
+            if kind == 3:
+                rtt = 10_000_000_000  # equality is accepted (rtt > MAX_RTT rejects)
+            if kind == 4:
+                rtt = 0
+            others.append(o)
+            rtts.append(rtt)
+        status, rows = g.update_batch(members, slot, others, rtts, round_=rnd)
+        for i in range(40):
+            m = int(members[i])
+            oc = O.coord(oo, list(others[i].portion), others[i].error, others[i].adjustment, others[i].height)
+            r = O.rng(SEED, m, rnd)
+            out = O.Coord()
+            e = L.orc_client_update(C.byref(clients[m]), int(slot[i]), C.byref(oc), rtts[i], C.byref(r), C.byref(out))
+            assert status[i] == e, (rnd, i)
+            c = clients[m].coord
+            exp = np.array(list(c.portion[:8]) + [c.error, c.adjustment, c.height])
+            np.testing.assert_array_equal(rows[i, :11].view(np.uint64), exp.view(np.uint64))
+    for c in clients:
+        L.orc_client_free(C.byref(c))
+    g.close()
+
+
+def test_client_kats_through_engine(kats):
+    k = kats["coordinate"]
+    opts = CoordinateOptions(dimensionality=3)
+    g = CoordinateClients(4, 2, opts)
+    other = Coordinate(np.array(k["client_update"]["other_portion"]), 1.5, 0.0, 10e-6)
+    c = g.update(0, 0, other, k["client_update"]["rtt_ns"])
+    assert c.portion[2] < 0.0  # coordinate.rs:904
+    c.portion[2] = 99.0
+    g.set_coordinate(0, c)
+    assert g.get_coordinate(0).portion[2] == 99.0
+    # invalid pings (coordinate.rs:913-938)
+    g.set_coordinate(1, Coordinate.with_options(opts))
+    g.set_coordinate(2, other)
+    d0 = g.distance_to([1], [2])[0]
+    for ns in k["client_invalid_in_ping_values"]["rtt_ns"]:
+        with pytest.raises(CoordinateError) as ei:
+            g.update(1, 0, other, ns)
+        assert ei.value.code == CoordinateError.INVALID_RTT
+        assert g.distance_to([1], [2])[0] == d0
+    # nan defense (1035-1067)
+    bad = Coordinate(np.array([math.nan, 0.0, 0.0]), 1.5, 0.0, 10e-6)
+    with pytest.raises(CoordinateError) as ei:
+        g.update(3, 0, bad, 250_000_000)
+    assert ei.value.code == CoordinateError.INVALID_COORDINATE
+    with pytest.raises(CoordinateError) as ei:
+        g.set_coordinate(3, Coordinate(np.zeros(6), 1.5, 0.0, 1e-5))
+    assert ei.value.code == CoordinateError.DIMENSIONALITY_MISMATCH
+    # distance_to with height_min 0 (940-954)
+    h0 = CoordinateClients(2, 1, CoordinateOptions(dimensionality=3, height_min=0.0))
+    h0.set_coordinate(1, Coordinate(np.array([0.0, 0.0, 12.345]), 1.5, 0.0, 0.0))
+    assert h0.distance_to([0], [1])[0] == k["client_distance_to"]["expect_ns"]
+    g.close()
+    h0.close()
