@@ -67,6 +67,14 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise EngineError(RSF_ERR_ARG, f"{LIB_PATH} not built: run __graft_entry__.build()")
+    # torch-ROCm ships its own libamdhip64 (same SONAME, loaded by a different
+    # file name): if ours initialised HIP first, torch would load a second
+    # runtime and see no device.  Loading torch first makes libruserf_amd bind
+    # to the runtime already in the process.  (The C ABI itself needs no torch.)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     i = C.c_int
     _sig(L, "rsf_last_error", C.c_char_p, [])

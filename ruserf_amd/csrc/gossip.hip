@@ -35,21 +35,79 @@ constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;
 
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    uint64_t t = __shfl_xor(v, o);
-    v = t < v ? t : v;
+// Wave-wide u64 min/max through DPP (row_ror inside 16-lane rows, then
+// row_bcast15 / row_bcast31 across rows, result in lane 63): VALU-only data
+// movement, no LDS permute round trips.  Every lane of the wave must be active.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  lo = (uint32_t)__builtin_amdgcn_update_dpp((int)lo, (int)lo, CTRL, ROWMASK, 0xF, false);
+  hi = (uint32_t)__builtin_amdgcn_update_dpp((int)hi, (int)hi, CTRL, ROWMASK, 0xF, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t lane63_u64(uint64_t v) {
+  uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+  uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+  return ((uint64_t)hi << 32) | lo;
+}
+#define RSF_DPP_STEP(OP, CTRL, RM)        \
+  {                                       \
+    uint64_t o_ = dpp64<CTRL, RM>(v);     \
+    v = (o_ OP v) ? o_ : v;               \
   }
-  return v;
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+  RSF_DPP_STEP(<, 0xB1, 0xF)   // quad_perm [1,0,3,2]
+  RSF_DPP_STEP(<, 0x4E, 0xF)   // quad_perm [2,3,0,1]
+  RSF_DPP_STEP(<, 0x124, 0xF)  // row_ror:4
+  RSF_DPP_STEP(<, 0x128, 0xF)  // row_ror:8
+  RSF_DPP_STEP(<, 0x142, 0xA)  // row_bcast:15 into rows 1,3
+  RSF_DPP_STEP(<, 0x143, 0xC)  // row_bcast:31 into rows 2,3
+  return lane63_u64(v);
 }
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    uint64_t t = __shfl_xor(v, o);
-    v = t > v ? t : v;
+  RSF_DPP_STEP(>, 0xB1, 0xF)
+  RSF_DPP_STEP(>, 0x4E, 0xF)
+  RSF_DPP_STEP(>, 0x124, 0xF)
+  RSF_DPP_STEP(>, 0x128, 0xF)
+  RSF_DPP_STEP(>, 0x142, 0xA)
+  RSF_DPP_STEP(>, 0x143, 0xC)
+  return lane63_u64(v);
+}
+#undef RSF_DPP_STEP
+
+// inclusive prefix max over the wave (lane 0 first); identity 0
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint64_t dpp64_id0(uint64_t v) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, CTRL, ROWMASK, 0xF, false);
+  hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, CTRL, ROWMASK, 0xF, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+#define RSF_SCAN_STEP(CTRL, RM)            \
+  {                                        \
+    uint64_t o_ = dpp64_id0<CTRL, RM>(v);  \
+    v = o_ > v ? o_ : v;                   \
   }
+__device__ __forceinline__ uint64_t wave_inclusive_max_u64(uint64_t v) {
+  RSF_SCAN_STEP(0x111, 0xF)  // row_shr:1
+  RSF_SCAN_STEP(0x112, 0xF)  // row_shr:2
+  RSF_SCAN_STEP(0x114, 0xF)  // row_shr:4
+  RSF_SCAN_STEP(0x118, 0xF)  // row_shr:8
+  RSF_SCAN_STEP(0x142, 0xA)  // row_bcast:15
+  RSF_SCAN_STEP(0x143, 0xC)  // row_bcast:31
   return v;
+}
+#undef RSF_SCAN_STEP
+// value of the previous lane (lane 0 gets 0): wave_shr:1
+__device__ __forceinline__ uint64_t wave_shr1_u64(uint64_t v) { return dpp64_id0<0x138, 0xF>(v); }
+
+__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int lane) {
+  uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+  uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 // one transmit-limited queue held in registers: lane i owns slot i
@@ -108,6 +166,7 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   bool picked = false;
   int64_t used = 0;
   const bool valid = lane < c.qcap;
+  if (!__ballot(valid && Q.r != kEmpty)) return 0;
   for (;;) {
     int64_t free_b = limit - used - (int64_t)c.overhead;
     if (free_b <= 0) break;
@@ -117,8 +176,8 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
     uint64_t kmin = wave_min_u64(key);
     if (kmin == ~0ull) break;
     int win = __ffsll((long long)__ballot(key == kmin)) - 1;
-    uint32_t rid = __shfl(Q.r, win);
-    uint32_t ln = __shfl(len, win);
+    uint32_t rid = shfl_u32(Q.r, win);
+    uint32_t ln = shfl_u32(len, win);
     if ((int)lane == win) picked = true;
     if (nrec < c.cap_t) {
       if (lane == 0) {
@@ -359,6 +418,17 @@ __global__ void __launch_bounds__(256) first_sentinel_kernel(const uint32_t* __r
   if (keys[i] == kSentinel && (i == 0 || keys[i - 1] != kSentinel)) *n_valid = i;
 }
 
+// One wave per receiver, lane = record.  Records arrive in canonical
+// (sender, position) order in [seg_start, seg_end); a chunk of up to 64 is
+// prefetched lane-parallel (rumor id, rumor body, the receiver's view entry of
+// the subject).  The intent handlers then run IN PARALLEL across lanes:
+//   * LamportClock::witness(t) is c = max(c, t+1), associative, so the clock a
+//     record sees is an exclusive prefix max over earlier intents (DPP scan);
+//   * records about the same subject form a chain (prev/next lane); chains are
+//     walked in depth order, each link taking its predecessor's output entry;
+//   * digest contributions (member events, deliveries), refutations and
+//     re-queues are then applied serially in record order.
+// User events / queries (dedup rings in HBM) run serially in lane 0.
 __global__ void __launch_bounds__(256) merge_kernel(GCfg c, GState s, const uint32_t* __restrict__ vals,
                                                     const uint32_t* __restrict__ seg_start,
                                                     const uint32_t* __restrict__ seg_end) {
@@ -376,28 +446,112 @@ __global__ void __launch_bounds__(256) merge_kernel(GCfg c, GState s, const uint
   MRegs r;
   load_regs(s, l, r);
   ViewE* vrow = s.view + l * c.S;
-  for (uint32_t i = st; i < en; ++i) {
-    const uint32_t rid = vals[i];
-    const rsf_rumor ru = s.rumors[rid];
-    int f = 0;
-    if (lane == 0) {
-      uint64_t ref = 0;
-      switch (ru.type) {
-        case RSF_MSG_JOIN: f = h_join_intent(vrow + ru.subject, r, ru.ltime); break;
-        case RSF_MSG_LEAVE: f = h_leave_intent(vrow + ru.subject, r, ru.subject, ru.ltime, ru.flags & 1, ref); break;
-        case RSF_MSG_USER_EVENT: f = h_user_event(c, s, l, r, ru.ltime, ru.key); break;
-        case RSF_MSG_QUERY: f = h_query(c, s, l, r, ru.ltime, (uint32_t)ru.key, ru.flags & 1); break;
-        default: break;
+  for (uint32_t base = st; base < en; base += kWave) {
+    const uint32_t cnt = min((uint32_t)kWave, en - base);
+    const bool valid = lane < cnt;
+    const uint32_t rid = valid ? vals[base + lane] : 0;
+    rsf_rumor ru{};
+    if (valid) ru = s.rumors[rid];
+    const bool is_view = valid && (ru.type == RSF_MSG_JOIN || ru.type == RSF_MSG_LEAVE);
+    ViewE pre{};
+    if (is_view) pre = vrow[ru.subject];
+    const uint32_t my_subj = is_view ? ru.subject : 0xFFFFFFFFu;
+    // chains: previous / next record of the same subject in this chunk
+    int prev = -1, next = -1;
+    {
+      const uint64_t vmask = __ballot(is_view);
+      uint64_t mm = vmask;
+      while (mm) {
+        const int j = __ffsll((long long)mm) - 1;
+        mm &= mm - 1;
+        const uint32_t sj = shfl_u32(my_subj, j);
+        if (is_view && sj == my_subj) {
+          if (j < (int)lane) prev = j;
+          if (j > (int)lane && next < 0) next = j;
+        }
       }
-      if (f & RSF_F_REFUTE) push_refute(c, s, r, ref);
     }
-    f = __shfl(f, 0);
-    if (f & RSF_F_REBROADCAST) {
-      uint32_t q = queue_of(ru.type);
-      if (q == kQIntent) q_insert_wave(c, Q0, lane, rid, ru.msg_len, nseq0++);
-      else if (q == kQQuery) q_insert_wave(c, Q1, lane, rid, ru.msg_len, nseq1++);
-      else q_insert_wave(c, Q2, lane, rid, ru.msg_len, nseq2++);
+    // Lamport clock each intent record witnesses against: exclusive prefix max
+    const uint64_t wit = is_view ? ru.ltime + 1 : 0;
+    const uint64_t incl = wave_inclusive_max_u64(wit);
+    const uint64_t excl = wave_shr1_u64(incl);
+    const uint64_t clock_before = excl > r.clock ? excl : r.clock;
+    const uint64_t chunk_max = lane63_u64(incl);
+    // walk chains in depth order
+    ViewE v = pre;
+    int f = 0;
+    uint64_t ref = 0, contrib = 0;  // digest word of a MemberEvent (Failed -> Left)
+    bool done = !is_view, dirty = false;
+    // bounded: a chain has at most cnt links, so cnt passes always finish it
+    for (uint32_t pass = 0; pass < cnt; ++pass) {
+      // every lane takes part in each ds_bpermute (an exec-masked source lane reads as 0)
+      const int src = prev < 0 ? (int)lane : prev;
+      const int pdone = __shfl((int)done, src);  // NOT inside `||`: short-circuit would exec-mask it
+      const bool prev_done = prev < 0 || pdone != 0;
+      const uint64_t pl = __shfl(v.ltime, src);
+      const uint32_t pm = (uint32_t)__shfl((int)v.meta, src);
+      const bool pd = __shfl((int)dirty, src) != 0;
+      const bool go = !done && prev_done;
+      if (go) {
+        if (prev >= 0) {
+          v.ltime = pl;
+          v.meta = pm;
+          dirty = pd;
+        }
+        MRegs rr = r;
+        rr.clock = clock_before;
+        rr.digest = 0;
+        const uint64_t lt0 = v.ltime;
+        const uint32_t mt0 = v.meta;
+        if (ru.type == RSF_MSG_JOIN) f = hv_join_intent(v, rr, ru.ltime);
+        else f = hv_leave_intent(v, rr, ru.subject, ru.ltime, ru.flags & 1, ref);
+        if (f & RSF_F_MEMBER_EVENT) contrib = kDigMember | ((uint64_t)kEvLeave << 32) | ru.subject;
+        dirty = dirty || v.ltime != lt0 || v.meta != mt0;
+        done = true;
+      }
+      if (!__ballot(!done)) break;
     }
+    if (next < 0 && is_view && dirty) vrow[my_subj] = v;  // last link writes the subject back
+    if (chunk_max > r.clock) r.clock = chunk_max;
+    // serial part, record order: events/queries (lane 0 handlers), digest, refutes, re-queues
+    const uint64_t serial = __ballot(valid && (!is_view || f != 0));
+    uint64_t mm = serial;
+    while (mm) {
+      const int i = __ffsll((long long)mm) - 1;
+      mm &= mm - 1;
+      const uint32_t tf = shfl_u32((uint32_t)ru.type | ((uint32_t)ru.flags << 8) | ((uint32_t)ru.msg_len << 16), i);
+      const uint8_t type = (uint8_t)(tf & 0xFF);
+      int fi;
+      if (type == RSF_MSG_JOIN || type == RSF_MSG_LEAVE) {
+        fi = (int)shfl_u32((uint32_t)f, i);
+        if (fi & RSF_F_MEMBER_EVENT) r.digest = digest_mix(r.digest, shfl_u64(contrib, i));
+        if (fi & RSF_F_REFUTE) {
+          const uint64_t rf = shfl_u64(ref, i);
+          if (lane == 0) push_refute(c, s, r, rf);
+          r.err = shfl_u32(r.err, 0);
+        }
+      } else {
+        const uint64_t L = shfl_u64(ru.ltime, i);
+        const uint64_t key = shfl_u64(ru.key, i);
+        fi = 0;
+        if (lane == 0) {
+          if (type == RSF_MSG_USER_EVENT) fi = h_user_event(c, s, l, r, L, key);
+          else if (type == RSF_MSG_QUERY) fi = h_query(c, s, l, r, L, (uint32_t)key, (tf >> 8) & 1);
+        }
+        fi = (int)shfl_u32((uint32_t)fi, 0);
+        r.eclock = shfl_u64(r.eclock, 0);
+        r.qclock = shfl_u64(r.qclock, 0);
+        r.digest = shfl_u64(r.digest, 0);
+        r.err = shfl_u32(r.err, 0);
+      }
+      if (fi & RSF_F_REBROADCAST) {
+        const uint32_t q = queue_of(type), rid_i = shfl_u32(rid, i), mlen = tf >> 16;
+        if (q == kQIntent) q_insert_wave(c, Q0, lane, rid_i, mlen, nseq0++);
+        else if (q == kQQuery) q_insert_wave(c, Q1, lane, rid_i, mlen, nseq1++);
+        else q_insert_wave(c, Q2, lane, rid_i, mlen, nseq2++);
+      }
+    }
+    if (base + kWave < en) __threadfence_block();  // next chunk's prefetch must see this chunk's view stores
   }
   q_store(c, s, l, 0, lane, Q0, true);
   q_store(c, s, l, 1, lane, Q1, true);

@@ -135,29 +135,42 @@ __device__ __forceinline__ bool upsert_intent(ViewE* e, uint32_t kind, uint64_t 
   return false;
 }
 
-// handle_node_join_intent (base.rs:1302-1337)
-__device__ __forceinline__ int h_join_intent(ViewE* e, MRegs& r, uint64_t L) {
+// upsert_intent on a register copy
+__device__ __forceinline__ bool upsert_intent_v(ViewE& v, uint32_t kind, uint64_t L) {
+  if (vkind(v.meta) == RSF_KIND_UNKNOWN || L > v.ltime) {
+    v.ltime = L;
+    v.meta = vmeta(vstatus(v.meta), kind);
+    return true;
+  }
+  return false;
+}
+
+// handle_node_join_intent (base.rs:1302-1337) on a register copy of the view entry
+__device__ __forceinline__ int hv_join_intent(ViewE& v, MRegs& r, uint64_t L) {
   witness(r.clock, L);
-  ViewE v = *e;
   if (vkind(v.meta) == RSF_KIND_KNOWN) {
     if (L <= v.ltime) return 0;
     v.ltime = L;
     uint32_t st = vstatus(v.meta);
     if (st == RSF_STATUS_LEAVING) st = RSF_STATUS_ALIVE;
     v.meta = vmeta(st, RSF_KIND_KNOWN);
-    *e = v;
     return RSF_F_REBROADCAST;
   }
-  return upsert_intent(e, RSF_KIND_INTENT_JOIN, L) ? RSF_F_REBROADCAST : 0;
+  return upsert_intent_v(v, RSF_KIND_INTENT_JOIN, L) ? RSF_F_REBROADCAST : 0;
+}
+__device__ __forceinline__ int h_join_intent(ViewE* e, MRegs& r, uint64_t L) {
+  ViewE v = *e;
+  int f = hv_join_intent(v, r, L);
+  *e = v;
+  return f;
 }
 
-// handle_node_leave_intent (base.rs:1409-1528)
-__device__ __forceinline__ int h_leave_intent(ViewE* e, MRegs& r, uint32_t subj, uint64_t L, bool prune,
-                                              uint64_t& refute) {
+// handle_node_leave_intent (base.rs:1409-1528) on a register copy of the view entry
+__device__ __forceinline__ int hv_leave_intent(ViewE& v, MRegs& r, uint32_t subj, uint64_t L, bool prune,
+                                               uint64_t& refute) {
   uint8_t state = r.serf_state;
   witness(r.clock, L);
-  ViewE v = *e;
-  if (vkind(v.meta) != RSF_KIND_KNOWN) return upsert_intent(e, RSF_KIND_INTENT_LEAVE, L) ? RSF_F_REBROADCAST : 0;
+  if (vkind(v.meta) != RSF_KIND_KNOWN) return upsert_intent_v(v, RSF_KIND_INTENT_LEAVE, L) ? RSF_F_REBROADCAST : 0;
   if (L <= v.ltime) return 0;
   if (r.subj == (int32_t)subj && state == kSerfAlive) {
     refute = r.clock;
@@ -180,6 +193,12 @@ __device__ __forceinline__ int h_leave_intent(ViewE* e, MRegs& r, uint32_t subj,
     default: f = 0; break;
   }
   v.meta = vmeta(st, RSF_KIND_KNOWN);
+  return f;
+}
+__device__ __forceinline__ int h_leave_intent(ViewE* e, MRegs& r, uint32_t subj, uint64_t L, bool prune,
+                                              uint64_t& refute) {
+  ViewE v = *e;
+  int f = hv_leave_intent(v, r, subj, L, prune, refute);
   *e = v;
   return f;
 }

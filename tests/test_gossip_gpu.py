@@ -167,3 +167,58 @@ def test_large_round_properties():
         digests.append((m["digest"].copy(), lt.sum()))
         g.close()
     assert np.array_equal(digests[0][0], digests[1][0]) and digests[0][1] == digests[1][1]
+
+
+def test_two_shards_equal_one_context():
+    """The multi-GPU split (round_begin / rumor-block sum / round_emit /
+    all-to-all / round_merge) with two shard contexts on one GPU and the
+    exchange done by hand must reproduce the single-context round exactly."""
+    import torch
+    from ruserf_amd.dist import hbm_tensor
+    n, rounds = 4000, 10
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    subj, acts, ml = W.churn_workload(n, rounds, events_per_round=20, queries_per_round=4, seed=3)
+    s = len(subj)
+    base = dict(n_members=n, n_subjects=s, queue_cap=32, max_rumors=1 << 16, event_buffer_size=128,
+                query_buffer_size=128, slot_k=8)
+    views = W.initial_views(s)
+    one = G.GossipEngine(G.GossipConfig(**base))
+    one.set_stream(stream.cuda_stream)
+    shards = [G.GossipEngine(G.GossipConfig(**base, shard=(0, n // 2))),
+              G.GossipEngine(G.GossipConfig(**base, shard=(n // 2, n)))]
+    for e in [one] + shards:
+        e.set_stream(stream.cuda_stream)
+        e.set_subjects(subj)
+        e.init_views(*views)
+    for t in range(rounds):
+        one.round(t, ml[t], acts[t])
+        for e in shards:
+            e.round_begin(t, ml[t], acts[t])
+        blocks = [hbm_tensor(*e.rumor_block()[:1], e.rumor_block()[1] // 8) for e in shards]
+        total = blocks[0] + blocks[1]
+        for b in blocks:
+            b.copy_(total)
+        counts = [e.round_emit(2) for e in shards]
+        sends = [hbm_tensor(e.send_buffer()[0], int(c.sum())) for e, c in zip(shards, counts)]
+        for dst, e in enumerate(shards):
+            parts = []
+            for src in range(2):
+                off = int(counts[src][:dst].sum())
+                parts.append(sends[src][off: off + int(counts[src][dst])])
+            recv = torch.cat(parts).contiguous()
+            e.round_merge(recv.data_ptr(), recv.numel())
+            stream.synchronize()
+        torch.cuda.synchronize()
+        full = H.engine_state(one)
+        halves = [H.engine_state(e) for e in shards]
+        for k in full:
+            got = np.concatenate([halves[0][k], halves[1][k]])
+            exp = full[k]
+            if k in ("q_seq", "q_tx", "q_len"):
+                empty = np.concatenate([halves[0]["q_rumor"], halves[1]["q_rumor"]]) == 0xFFFFFFFF
+                got = np.where(empty, 0, got)
+                exp = np.where(full["q_rumor"] == 0xFFFFFFFF, 0, exp)
+            assert np.array_equal(got, exp), (t, k)
+    for e in [one] + shards:
+        e.close()
