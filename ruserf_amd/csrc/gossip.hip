@@ -138,46 +138,59 @@ __device__ __forceinline__ void q_store(const GCfg& c, const GState& s, uint64_t
   }
 }
 
-// wave-parallel insert: identical slot choice to queue_insert_serial
+// Queues are kept SORTED in send order: lane i of a queue holds the item with
+// the i-th smallest key (transmits, ~len, ~seq); free slots (kEmpty) follow the
+// live items.  The content is exactly the reference model's (first-free-slot /
+// prune-the-last-item), only the slot order is canonical.
+
+__device__ __forceinline__ uint64_t below_mask(uint32_t lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+
+// insert: position = number of smaller live keys; lanes at/after it shift by
+// one, so on a full queue the last lane (the largest key) falls off = memberlist
+// Prune; a new item that would land past the end is itself the pruned one.
 __device__ __forceinline__ void q_insert_wave(const GCfg& c, QRegs& Q, uint32_t lane, uint32_t rid, uint32_t len,
                                               uint32_t seq) {
   const bool valid = lane < c.qcap;
-  uint64_t empty = __ballot(valid && Q.r == kEmpty);
-  int slot;
-  if (empty) {
-    slot = __ffsll((long long)empty) - 1;
-  } else {
-    uint64_t k = valid ? tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq) : 0;
-    uint64_t kmax = wave_max_u64(k);
-    if (tlq_key(0, len, seq) > kmax) return;
-    slot = __ffsll((long long)__ballot(valid && k == kmax)) - 1;
+  const bool live = valid && Q.r != kEmpty;
+  const uint64_t newkey = tlq_key(0, len, seq);
+  const uint64_t k = live ? tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq) : ~0ull;
+  const uint32_t pos = (uint32_t)__popcll(__ballot(live && k < newkey));
+  if (pos >= c.qcap) return;
+  const int src = lane ? (int)lane - 1 : 0;
+  const uint32_t pr = (uint32_t)__shfl((int)Q.r, src), ps = (uint32_t)__shfl((int)Q.sq, src),
+                 pt = (uint32_t)__shfl((int)Q.tl, src);
+  if (valid && lane > pos) {
+    Q.r = pr;
+    Q.sq = ps;
+    Q.tl = pt;
   }
-  if ((int)lane == slot) {
+  if (lane == pos) {
     Q.r = rid;
     Q.sq = seq;
     Q.tl = len << 16;
   }
 }
 
-// one get_broadcasts call on a register-resident queue; returns bytes used
+// one get_broadcasts call on a sorted register-resident queue; returns bytes used.
+// The lowest unpicked lane that fits IS the reference's pick (lowest transmits, then
+// longest fitting, then newest): every skipped lower lane did not fit and never will.
 __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uint32_t lane, int64_t limit,
                                                     uint32_t recv, uint32_t* stage_key, uint32_t* stage_val,
                                                     uint64_t out_base, uint32_t& nrec, uint32_t& err) {
+  const bool valid = lane < c.qcap;
+  const bool live = valid && Q.r != kEmpty;
+  if (!__ballot(live)) return 0;
+  const uint32_t len = Q.tl >> 16;
   bool picked = false;
   int64_t used = 0;
-  const bool valid = lane < c.qcap;
-  if (!__ballot(valid && Q.r != kEmpty)) return 0;
   for (;;) {
-    int64_t free_b = limit - used - (int64_t)c.overhead;
+    const int64_t free_b = limit - used - (int64_t)c.overhead;
     if (free_b <= 0) break;
-    uint32_t len = Q.tl >> 16;
-    bool elig = valid && Q.r != kEmpty && !picked && (int64_t)len <= free_b;
-    uint64_t key = elig ? tlq_key(Q.tl & 0xFFFF, len, Q.sq) : ~0ull;
-    uint64_t kmin = wave_min_u64(key);
-    if (kmin == ~0ull) break;
-    int win = __ffsll((long long)__ballot(key == kmin)) - 1;
-    uint32_t rid = shfl_u32(Q.r, win);
-    uint32_t ln = shfl_u32(len, win);
+    const uint64_t cand = __ballot(live && !picked && (int64_t)len <= free_b);
+    if (!cand) break;
+    const int win = __ffsll((long long)cand) - 1;
+    const uint32_t rid = shfl_u32(Q.r, win);
+    const uint32_t ln = shfl_u32(len, win);
     if ((int)lane == win) picked = true;
     if (nrec < c.cap_t) {
       if (lane == 0) {
@@ -190,11 +203,40 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
     nrec++;
     used += (int64_t)c.overhead + ln;
   }
+  if (!__ballot(picked)) return used;
+  // transmits+1, or retire at the retransmit limit
+  bool keep = live;
   if (picked) {
-    uint32_t tx = Q.tl & 0xFFFF;
-    if (tx + 1 >= c.tx_limit) Q.r = kEmpty;
-    else Q.tl = Q.tl + 1;
+    if ((Q.tl & 0xFFFF) + 1 >= c.tx_limit) {
+      keep = false;
+      Q.r = kEmpty;
+    } else {
+      Q.tl = Q.tl + 1;
+    }
   }
+  // re-rank: unpicked keepers and bumped keepers are each still sorted; merge them
+  const bool np = keep && !picked, pk = keep && picked;
+  const uint64_t mykey = keep ? tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq) : ~0ull;
+  const uint64_t npmask = __ballot(np), pkmask = __ballot(pk), deadmask = __ballot(valid && !keep);
+  const uint64_t below = below_mask(lane);
+  uint32_t pos;
+  if (np) pos = (uint32_t)__popcll(npmask & below);
+  else if (pk) pos = (uint32_t)__popcll(pkmask & below);
+  else if (valid) pos = (uint32_t)__popcll(npmask | pkmask) + (uint32_t)__popcll(deadmask & below);
+  else pos = lane;
+  uint64_t mm = pkmask;
+  while (mm) {
+    const int p = __ffsll((long long)mm) - 1;
+    mm &= mm - 1;
+    const uint64_t kp = shfl_u64(mykey, p);
+    if (np && kp < mykey) pos++;
+    const uint32_t below_p = (uint32_t)__popcll(__ballot(np && mykey < kp));
+    if ((int)lane == p) pos += below_p;
+  }
+  const int addr = (int)(pos * 4);
+  Q.r = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.r);
+  Q.sq = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.sq);
+  Q.tl = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.tl);
   return used;
 }
 
@@ -394,9 +436,9 @@ __global__ void __launch_bounds__(256) emit_kernel(GCfg c, GState s, uint32_t ro
     used += q_get_broadcasts(c, Q1, lane, (int64_t)c.limit - used, recv, stage_key, stage_val, out_base, nrec, err);
     used += q_get_broadcasts(c, Q2, lane, (int64_t)c.limit - used, recv, stage_key, stage_val, out_base, nrec, err);
   }
-  q_store(c, s, l, 0, lane, Q0, false);
-  q_store(c, s, l, 1, lane, Q1, false);
-  q_store(c, s, l, 2, lane, Q2, false);
+  q_store(c, s, l, 0, lane, Q0, true);
+  q_store(c, s, l, 1, lane, Q1, true);
+  q_store(c, s, l, 2, lane, Q2, true);
   if (err && lane == 0) s.err[l] |= err;
 }
 

@@ -306,33 +306,31 @@ __device__ __forceinline__ uint32_t queue_of(uint8_t type) {
   return type == RSF_MSG_USER_EVENT ? kQEvent : (type == RSF_MSG_QUERY ? kQQuery : kQIntent);
 }
 
-// TransmitLimitedQueue insert, one thread: first empty slot, else replace the
-// last item in send order unless the new item is itself last (prune model).
+// TransmitLimitedQueue insert, one thread, on a key-sorted queue (live items
+// first, ascending (transmits, ~len, ~seq); then free slots): shift the tail by
+// one; on a full queue the largest item falls off (memberlist Prune), and a new
+// item that would land past the end is itself the pruned one.
 __device__ __forceinline__ void queue_insert_serial(const GCfg& c, const GState& s, uint64_t l, uint32_t q,
                                                     uint32_t rid, uint32_t len) {
-  uint64_t base = (l * 3 + q) * c.qcap;
-  uint32_t seq = s.q_next_seq[l * 3 + q]++;
-  uint32_t slot = kEmpty;
-  for (uint32_t i = 0; i < c.qcap; ++i)
-    if (s.q_rumor[base + i] == kEmpty) {
-      slot = i;
-      break;
-    }
-  if (slot == kEmpty) {
-    uint64_t kmax = 0;
-    for (uint32_t i = 0; i < c.qcap; ++i) {
-      uint32_t tl = s.q_txlen[base + i];
-      uint64_t k = tlq_key(tl & 0xFFFF, tl >> 16, s.q_seq[base + i]);
-      if (slot == kEmpty || k > kmax) {
-        kmax = k;
-        slot = i;
-      }
-    }
-    if (tlq_key(0, len, seq) > kmax) return;
+  const uint64_t base = (l * 3 + q) * c.qcap;
+  const uint32_t seq = s.q_next_seq[l * 3 + q]++;
+  const uint64_t newkey = tlq_key(0, len, seq);
+  uint32_t cnt = 0, pos = kEmpty;
+  while (cnt < c.qcap && s.q_rumor[base + cnt] != kEmpty) {
+    const uint32_t tl = s.q_txlen[base + cnt];
+    if (pos == kEmpty && tlq_key(tl & 0xFFFF, tl >> 16, s.q_seq[base + cnt]) > newkey) pos = cnt;
+    cnt++;
   }
-  s.q_rumor[base + slot] = rid;
-  s.q_seq[base + slot] = seq;
-  s.q_txlen[base + slot] = (len << 16);
+  if (pos == kEmpty) pos = cnt;
+  if (pos >= c.qcap) return;
+  for (uint32_t i = (cnt < c.qcap ? cnt : c.qcap - 1); i > pos; --i) {
+    s.q_rumor[base + i] = s.q_rumor[base + i - 1];
+    s.q_seq[base + i] = s.q_seq[base + i - 1];
+    s.q_txlen[base + i] = s.q_txlen[base + i - 1];
+  }
+  s.q_rumor[base + pos] = rid;
+  s.q_seq[base + pos] = seq;
+  s.q_txlen[base + pos] = (len << 16);
 }
 
 }  // namespace rsf

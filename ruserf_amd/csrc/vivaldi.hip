@@ -136,13 +136,17 @@ __device__ __forceinline__ uint64_t distance_ns(const double* a, double ha, doub
 __device__ __forceinline__ bool finite(double x) { return isfinite(x); }
 
 // Result codes per item: RSF_OK or CoordinateError (check_coordinate order).
-template <int D, int F>
+// WW > 0: the window (WW samples, read by the caller into `win` BEFORE any
+// dependent work so all its loads are in flight together) and its index are
+// register-resident; WW == 0: generic runtime window size, read here.
+template <int D, int F, int WW>
 __device__ __forceinline__ int update_one(double* me, double& err, double& adj, double& h,
                                           const double* other, double oerr, double oadj, double oh,
                                           uint32_t odim, uint64_t rtt_ns, double* frec,
                                           double* adj_col, uint64_t adj_stride, uint32_t* adj_idx_p,
                                           const VivParams& p, uint32_t member, uint32_t round,
-                                          unsigned long long* resets) {
+                                          unsigned long long* resets, const double* win = nullptr,
+                                          uint32_t win_idx = 0) {
   const uint32_t dim = p.dim;
   // check_coordinate (coordinate.rs:436-446)
   if (odim != dim) return RSF_ERR_DIM_MISMATCH;
@@ -213,8 +217,19 @@ __device__ __forceinline__ int update_one(double* me, double& err, double& adj, 
     double force = p.cc * weight * (rtt - dist);
     apply_force<D>(me, h, other, oh, force, dim, p, 0, member, round);
   }
-  // update_adjustment (334-346)
-  if (p.W) {
+  // update_adjustment (334-346): samples[idx] = rtt - dist; idx = (idx+1) % W;
+  // adjustment = sequential fold of samples[0..W) / (2W)
+  if (WW > 0) {
+    double dist = raw_distance<D>(me, h, other, oh, dim);
+    double sample = rtt_seconds - dist;
+    const uint32_t idx = win_idx;
+    double sum = 0.0;
+#pragma unroll
+    for (int i = 0; i < WW; ++i) sum = sum + (((uint32_t)i == idx) ? sample : win[i]);
+    adj_col[(uint64_t)idx * adj_stride] = sample;
+    *adj_idx_p = (idx + 1 == (uint32_t)WW) ? 0 : idx + 1;
+    adj = sum / (2.0 * (double)WW);
+  } else if (p.W) {
     double dist = raw_distance<D>(me, h, other, oh, dim);
     double sample = rtt_seconds - dist;
     uint32_t idx = *adj_idx_p;
@@ -309,7 +324,7 @@ __device__ __forceinline__ void store_row(double* __restrict__ row, const double
   }
 }
 
-template <int D, int F>
+template <int D, int F, int WW>
 __global__ void __launch_bounds__(256) vivaldi_round_kernel(const double* __restrict__ cur,
                                                             double* __restrict__ nxt,
                                                             double* __restrict__ adj_win,
@@ -320,20 +335,17 @@ __global__ void __launch_bounds__(256) vivaldi_round_kernel(const double* __rest
   if (local >= p.shard_n) return;
   const uint32_t m = (uint32_t)(p.lo + local);
   const int FR = (F <= 3) ? 4 : 8;
-  // synthetic probe (neighbour slot, rtt)
+  // ---- issue every independent load first: window index, window, own row
+  const uint32_t widx = (WW > 0) ? adj_idx[local] : 0;
+  double win[WW > 0 ? WW : 1];
+#pragma unroll
+  for (int i = 0; i < WW; ++i) win[i] = adj_win[(uint64_t)i * p.shard_n + local];
+  double me[D], other[D], e, a, h, oe, oa, oh;
+  load_row<D>(cur + (uint64_t)m * p.stride, me, e, a, h, p.dim);
+  // ---- synthetic probe (neighbour slot, rtt); then the dependent gathers
   u32x4 pr = philox4x32_10(0, kPurposeVProbe << 24, m, p.round, p.k0, p.k1);
   uint32_t q = mulhi32(pr.x, p.peers);
   uint32_t peer = neighbour(p, m, q);
-  double xm, ym, hm, xp, yp, hp;
-  true_pos(p.k0, p.k1, m, xm, ym, hm);
-  true_pos(p.k0, p.k1, peer, xp, yp, hp);
-  double dx = xm - xp, dy = ym - yp;
-  double d = sqrt(dx * dx + dy * dy) + hm + hp;
-  double jit = 1.0 + 0.1 * ((double)pr.y * 2.3283064365386963e-10);
-  uint64_t rtt_ns = sat_u64((d * jit) * 1.0e9);
-
-  double me[D], other[D], e, a, h, oe, oa, oh;
-  load_row<D>(cur + (uint64_t)m * p.stride, me, e, a, h, p.dim);
   load_row<D>(cur + (uint64_t)peer * p.stride, other, oe, oa, oh, p.dim);
   double* frec = filt + (local * p.peers + q) * FR;
   double rec[FR];
@@ -348,8 +360,16 @@ __global__ void __launch_bounds__(256) vivaldi_round_kernel(const double* __rest
 #pragma unroll
     for (int i = 0; i < FR; ++i) rec[i] = frec[i];
   }
-  update_one<D, F>(me, e, a, h, other, oe, oa, oh, p.dim, rtt_ns, rec, adj_win + local, p.shard_n,
-                   adj_idx + local, p, m, p.round, resets);
+  double xm, ym, hm, xp, yp, hp;
+  true_pos(p.k0, p.k1, m, xm, ym, hm);
+  true_pos(p.k0, p.k1, peer, xp, yp, hp);
+  double dx = xm - xp, dy = ym - yp;
+  double d = sqrt(dx * dx + dy * dy) + hm + hp;
+  double jit = 1.0 + 0.1 * ((double)pr.y * 2.3283064365386963e-10);
+  uint64_t rtt_ns = sat_u64((d * jit) * 1.0e9);
+
+  update_one<D, F, WW>(me, e, a, h, other, oe, oa, oh, p.dim, rtt_ns, rec, adj_win + local, p.shard_n,
+                       adj_idx + local, p, m, p.round, resets, win, widx);
   if (FR == 4) {
     double2* f2 = reinterpret_cast<double2*>(frec);
     f2[0] = make_double2(rec[0], rec[1]);
@@ -390,8 +410,8 @@ __global__ void __launch_bounds__(256) vivaldi_batch_kernel(
   double rec[FR];
 #pragma unroll
   for (int k = 0; k < FR; ++k) rec[k] = frec[k];
-  int st = update_one<D, F>(me, e, a, h, other, oe, oa, oh, od, rtt[i], rec, adj_win + local,
-                            p.shard_n, adj_idx + local, p, m, p.round, resets);
+  int st = update_one<D, F, 0>(me, e, a, h, other, oe, oa, oh, od, rtt[i], rec, adj_win + local,
+                               p.shard_n, adj_idx + local, p, m, p.round, resets);
   status[i] = st;
   if (st == RSF_OK) {
 #pragma unroll
@@ -706,9 +726,13 @@ int rsf_vivaldi_round(rsf_vivaldi* v, uint32_t round) {
   unsigned blocks = (unsigned)((p.shard_n + 255) / 256);
   const double* cur = v->table[v->cur];
   double* nxt = v->table[v->cur ^ 1];
-  RSF_DISPATCH_DF(p.dim, p.F,
-                  hipLaunchKernelGGL((vivaldi_round_kernel<kD, kF>), dim3(blocks), dim3(256), 0, v->stream, cur,
-                                     nxt, v->adj, v->adj_idx, v->filt, v->resets, p));
+  if (p.dim == 8 && p.F <= 3 && p.W == 20)
+    hipLaunchKernelGGL((vivaldi_round_kernel<8, 3, 20>), dim3(blocks), dim3(256), 0, v->stream, cur, nxt, v->adj,
+                       v->adj_idx, v->filt, v->resets, p);
+  else
+    RSF_DISPATCH_DF(p.dim, p.F,
+                    hipLaunchKernelGGL((vivaldi_round_kernel<kD, kF, 0>), dim3(blocks), dim3(256), 0, v->stream,
+                                       cur, nxt, v->adj, v->adj_idx, v->filt, v->resets, p));
   RSF_HIP(hipGetLastError());
   v->cur ^= 1;
   return RSF_OK;

@@ -83,14 +83,29 @@ def engine_state(g):
     }
 
 
-def normalize_queues(st):
-    """Queue slots whose rumor is empty carry stale seq/tx/len; zero them for comparison."""
+def normalize_queues(st, qcap=None):
+    """Queue slot ORDER is an implementation detail (the oracle fills the first free
+    slot, the kernels keep each queue sorted in send order); the queue CONTENT is
+    what the reference defines.  Canonical form: each queue's live items sorted by
+    (transmits, len desc, seq desc), free slots after them and zeroed."""
     st = dict(st)
-    empty = st["q_rumor"] == 0xFFFFFFFF
-    for k in ["q_seq", "q_tx", "q_len"]:
-        a = st[k].copy()
-        a[empty] = 0
-        st[k] = a
+    r = st["q_rumor"]
+    n, w = r.shape
+    q = qcap or (w // 3)
+    rr = r.reshape(n, 3, q)
+    sq = st["q_seq"].reshape(n, 3, q).astype(np.uint64)
+    tx = st["q_tx"].reshape(n, 3, q).astype(np.uint64)
+    ln = st["q_len"].reshape(n, 3, q).astype(np.uint64)
+    empty = rr == 0xFFFFFFFF
+    key = (tx << 48) | ((0xFFFF - ln) << 32) | (0xFFFFFFFF - sq)
+    key = np.where(empty, np.uint64(0xFFFFFFFFFFFFFFFF), key)
+    order = np.argsort(key, axis=2, kind="stable")
+    for k in ["q_rumor", "q_seq", "q_tx", "q_len"]:
+        a = st[k].reshape(n, 3, q)
+        a = np.take_along_axis(a, order, axis=2).copy()
+        if k != "q_rumor":
+            a[np.take_along_axis(empty, order, axis=2)] = 0
+        st[k] = a.reshape(n, w)
     return st
 
 
