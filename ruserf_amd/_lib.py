@@ -9,7 +9,7 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libruserf_amd.so")
+LIB_PATH = os.environ.get("RSF_LIB_PATH") or os.path.join(HERE, "libruserf_amd.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "ruserf_amd.h")
 
 RSF_OK = 0

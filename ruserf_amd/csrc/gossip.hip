@@ -98,6 +98,17 @@ __device__ __forceinline__ uint64_t wave_inclusive_max_u64(uint64_t v) {
   return v;
 }
 #undef RSF_SCAN_STEP
+// inclusive prefix sum over the wave (u32, identity 0)
+__device__ __forceinline__ uint32_t wave_inclusive_sum_u32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return v;
+}
+
 // value of the previous lane (lane 0 gets 0): wave_shr:1
 __device__ __forceinline__ uint64_t wave_shr1_u64(uint64_t v) { return dpp64_id0<0x138, 0xF>(v); }
 
@@ -176,34 +187,43 @@ __device__ __forceinline__ void q_insert_wave(const GCfg& c, QRegs& Q, uint32_t 
 // longest fitting, then newest): every skipped lower lane did not fit and never will.
 __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uint32_t lane, int64_t limit,
                                                     uint32_t recv, uint32_t* stage_key, uint32_t* stage_val,
-                                                    uint64_t out_base, uint32_t& nrec, uint32_t& err) {
+                                                    uint64_t out_base, uint32_t& nrec, uint32_t& err, bool& dirty) {
   const bool valid = lane < c.qcap;
   const bool live = valid && Q.r != kEmpty;
   if (!__ballot(live)) return 0;
   const uint32_t len = Q.tl >> 16;
-  bool picked = false;
-  int64_t used = 0;
+  // Live items are the sorted prefix.  If every earlier item was taken, item i
+  // fits iff the inclusive prefix sum of (overhead + len) is <= limit, so the
+  // leading run of picks comes out of one wave scan; the remaining budget is
+  // then offered to later (shorter) items one by one, as the reference does.
+  const uint32_t cost = live ? c.overhead + len : 0u;
+  const uint32_t incl = wave_inclusive_sum_u32(cost);
+  bool picked = live && limit >= 0 && (int64_t)incl <= limit;
+  const uint64_t run = __ballot(picked);
+  int64_t used = run ? (int64_t)shfl_u32(incl, 63 - __clzll((long long)run)) : 0;
   for (;;) {
     const int64_t free_b = limit - used - (int64_t)c.overhead;
     if (free_b <= 0) break;
     const uint64_t cand = __ballot(live && !picked && (int64_t)len <= free_b);
     if (!cand) break;
     const int win = __ffsll((long long)cand) - 1;
-    const uint32_t rid = shfl_u32(Q.r, win);
-    const uint32_t ln = shfl_u32(len, win);
     if ((int)lane == win) picked = true;
-    if (nrec < c.cap_t) {
-      if (lane == 0) {
-        stage_key[out_base + nrec] = recv;
-        stage_val[out_base + nrec] = rid;
-      }
-    } else {
-      err |= kErrStage;
+    used += (int64_t)c.overhead + shfl_u32(len, win);
+  }
+  // picks are in ascending lane (= send) order: record rank = picked lanes below
+  const uint64_t pmask = __ballot(picked);
+  if (pmask) {
+    const uint32_t npick = (uint32_t)__popcll(pmask);
+    const uint32_t rank = (uint32_t)__popcll(pmask & below_mask(lane));
+    if (picked && nrec + rank < c.cap_t) {
+      stage_key[out_base + nrec + rank] = recv;
+      stage_val[out_base + nrec + rank] = Q.r;
     }
-    nrec++;
-    used += (int64_t)c.overhead + ln;
+    if (nrec + npick > c.cap_t) err |= kErrStage;
+    nrec += npick;
   }
   if (!__ballot(picked)) return used;
+  dirty = true;
   // transmits+1, or retire at the retransmit limit
   bool keep = live;
   if (picked) {
@@ -422,23 +442,29 @@ __global__ void __launch_bounds__(256) emit_kernel(GCfg c, GState s, uint32_t ro
       if (!dup) peers[np++] = cand;
     }
   }
-  QRegs Q0, Q1, Q2;
-  q_load(c, s, l, 0, lane, Q0);
-  q_load(c, s, l, 1, lane, Q1);
-  q_load(c, s, l, 2, lane, Q2);
+  // sorted queues: a queue is empty iff its slot 0 is free -> one 4-byte probe each
+  const uint32_t head = lane < 3 ? s.q_rumor[(l * 3 + lane) * c.qcap] : kEmpty;
+  const bool ne0 = shfl_u32(head, 0) != kEmpty, ne1 = shfl_u32(head, 1) != kEmpty,
+             ne2 = shfl_u32(head, 2) != kEmpty;
+  if (np == 0 || !(ne0 || ne1 || ne2)) return;
+  QRegs Q0{kEmpty, 0, 0}, Q1{kEmpty, 0, 0}, Q2{kEmpty, 0, 0};
+  if (ne0) q_load(c, s, l, 0, lane, Q0);
+  if (ne1) q_load(c, s, l, 1, lane, Q1);
+  if (ne2) q_load(c, s, l, 2, lane, Q2);
   uint32_t err = 0;
+  bool d0 = false, d1 = false, d2 = false;
   for (uint32_t j = 0; j < np; ++j) {
     uint32_t recv = peers[j];
     uint64_t out_base = (l * c.fanout + j) * c.cap_t;
     uint32_t nrec = 0;
     int64_t used = 0;
-    used += q_get_broadcasts(c, Q0, lane, (int64_t)c.limit - used, recv, stage_key, stage_val, out_base, nrec, err);
-    used += q_get_broadcasts(c, Q1, lane, (int64_t)c.limit - used, recv, stage_key, stage_val, out_base, nrec, err);
-    used += q_get_broadcasts(c, Q2, lane, (int64_t)c.limit - used, recv, stage_key, stage_val, out_base, nrec, err);
+    used += q_get_broadcasts(c, Q0, lane, (int64_t)c.limit - used, recv, stage_key, stage_val, out_base, nrec, err, d0);
+    used += q_get_broadcasts(c, Q1, lane, (int64_t)c.limit - used, recv, stage_key, stage_val, out_base, nrec, err, d1);
+    used += q_get_broadcasts(c, Q2, lane, (int64_t)c.limit - used, recv, stage_key, stage_val, out_base, nrec, err, d2);
   }
-  q_store(c, s, l, 0, lane, Q0, true);
-  q_store(c, s, l, 1, lane, Q1, true);
-  q_store(c, s, l, 2, lane, Q2, true);
+  if (d0) q_store(c, s, l, 0, lane, Q0, true);
+  if (d1) q_store(c, s, l, 1, lane, Q1, true);
+  if (d2) q_store(c, s, l, 2, lane, Q2, true);
   if (err && lane == 0) s.err[l] |= err;
 }
 
@@ -471,7 +497,13 @@ __global__ void __launch_bounds__(256) first_sentinel_kernel(const uint32_t* __r
 //   * digest contributions (member events, deliveries), refutations and
 //     re-queues are then applied serially in record order.
 // User events / queries (dedup rings in HBM) run serially in lane 0.
-__global__ void __launch_bounds__(256) merge_kernel(GCfg c, GState s, const uint32_t* __restrict__ vals,
+#ifndef RSF_MERGE_WAVES
+#define RSF_MERGE_WAVES 5  // min waves/SIMD for merge_kernel (register cap)
+#endif
+#ifndef RSF_MERGE_EAGER
+#define RSF_MERGE_EAGER 1  // 0: load the query/event queues only when a chunk needs them
+#endif
+__global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GState s, const uint32_t* __restrict__ vals,
                                                     const uint32_t* __restrict__ seg_start,
                                                     const uint32_t* __restrict__ seg_end) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -480,10 +512,15 @@ __global__ void __launch_bounds__(256) merge_kernel(GCfg c, GState s, const uint
   const uint32_t m = (uint32_t)(c.lo + l);
   const uint32_t st = seg_start[l], en = seg_end[l];
   if (st >= en || !s.alive[m]) return;
-  QRegs Q0, Q1, Q2;
-  q_load(c, s, l, 0, lane, Q0);
-  q_load(c, s, l, 1, lane, Q1);
-  q_load(c, s, l, 2, lane, Q2);
+  // queues are loaded on first need (the record types of a chunk say which) and
+  // written back only if something was inserted
+  QRegs Q0{kEmpty, 0, 0}, Q1{kEmpty, 0, 0}, Q2{kEmpty, 0, 0};
+  bool ld0 = true, ld1 = RSF_MERGE_EAGER, ld2 = RSF_MERGE_EAGER, d0 = false, d1 = false, d2 = false;
+  q_load(c, s, l, 0, lane, Q0);  // intents are the common case: load with the first prefetch
+  if (RSF_MERGE_EAGER) {
+    q_load(c, s, l, 1, lane, Q1);
+    q_load(c, s, l, 2, lane, Q2);
+  }
   uint32_t nseq0 = s.q_next_seq[l * 3 + 0], nseq1 = s.q_next_seq[l * 3 + 1], nseq2 = s.q_next_seq[l * 3 + 2];
   MRegs r;
   load_regs(s, l, r);
@@ -495,6 +532,18 @@ __global__ void __launch_bounds__(256) merge_kernel(GCfg c, GState s, const uint
     rsf_rumor ru{};
     if (valid) ru = s.rumors[rid];
     const bool is_view = valid && (ru.type == RSF_MSG_JOIN || ru.type == RSF_MSG_LEAVE);
+    if (!ld0 && __ballot(is_view)) {
+      q_load(c, s, l, 0, lane, Q0);
+      ld0 = true;
+    }
+    if (!ld1 && __ballot(valid && ru.type == RSF_MSG_QUERY)) {
+      q_load(c, s, l, 1, lane, Q1);
+      ld1 = true;
+    }
+    if (!ld2 && __ballot(valid && ru.type == RSF_MSG_USER_EVENT)) {
+      q_load(c, s, l, 2, lane, Q2);
+      ld2 = true;
+    }
     ViewE pre{};
     if (is_view) pre = vrow[ru.subject];
     const uint32_t my_subj = is_view ? ru.subject : 0xFFFFFFFFu;
@@ -588,21 +637,28 @@ __global__ void __launch_bounds__(256) merge_kernel(GCfg c, GState s, const uint
       }
       if (fi & RSF_F_REBROADCAST) {
         const uint32_t q = queue_of(type), rid_i = shfl_u32(rid, i), mlen = tf >> 16;
-        if (q == kQIntent) q_insert_wave(c, Q0, lane, rid_i, mlen, nseq0++);
-        else if (q == kQQuery) q_insert_wave(c, Q1, lane, rid_i, mlen, nseq1++);
-        else q_insert_wave(c, Q2, lane, rid_i, mlen, nseq2++);
+        if (q == kQIntent) {
+          q_insert_wave(c, Q0, lane, rid_i, mlen, nseq0++);
+          d0 = true;
+        } else if (q == kQQuery) {
+          q_insert_wave(c, Q1, lane, rid_i, mlen, nseq1++);
+          d1 = true;
+        } else {
+          q_insert_wave(c, Q2, lane, rid_i, mlen, nseq2++);
+          d2 = true;
+        }
       }
     }
     if (base + kWave < en) __threadfence_block();  // next chunk's prefetch must see this chunk's view stores
   }
-  q_store(c, s, l, 0, lane, Q0, true);
-  q_store(c, s, l, 1, lane, Q1, true);
-  q_store(c, s, l, 2, lane, Q2, true);
+  if (d0) q_store(c, s, l, 0, lane, Q0, true);
+  if (d1) q_store(c, s, l, 1, lane, Q1, true);
+  if (d2) q_store(c, s, l, 2, lane, Q2, true);
   if (lane == 0) {
     store_regs(s, l, r);
-    s.q_next_seq[l * 3 + 0] = nseq0;
-    s.q_next_seq[l * 3 + 1] = nseq1;
-    s.q_next_seq[l * 3 + 2] = nseq2;
+    if (d0) s.q_next_seq[l * 3 + 0] = nseq0;
+    if (d1) s.q_next_seq[l * 3 + 1] = nseq1;
+    if (d2) s.q_next_seq[l * 3 + 2] = nseq2;
   }
 }
 

@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -139,7 +140,7 @@ __device__ __forceinline__ bool finite(double x) { return isfinite(x); }
 // WW > 0: the window (WW samples, read by the caller into `win` BEFORE any
 // dependent work so all its loads are in flight together) and its index are
 // register-resident; WW == 0: generic runtime window size, read here.
-template <int D, int F, int WW>
+template <int D, int F, int WW, int FRT = (F <= 3 ? 4 : 8)>
 __device__ __forceinline__ int update_one(double* me, double& err, double& adj, double& h,
                                           const double* other, double oerr, double oadj, double oh,
                                           uint32_t odim, uint64_t rtt_ns, double* frec,
@@ -160,7 +161,7 @@ __device__ __forceinline__ int update_one(double* me, double& err, double& adj, 
   // latency_filter (292-307): ring == Vec push/remove(0) for the median
   double rtt_seconds;
   {
-    const int FR = (F <= 3) ? 4 : 8;
+    const int FR = FRT;
     uint64_t meta = __double_as_longlong(frec[FR - 1]);
     uint32_t len = (uint32_t)meta, head = (uint32_t)(meta >> 32);
     double x = as_secs_f64(rtt_ns);
@@ -324,8 +325,11 @@ __device__ __forceinline__ void store_row(double* __restrict__ row, const double
   }
 }
 
-template <int D, int F, int WW>
-__global__ void __launch_bounds__(256) vivaldi_round_kernel(const double* __restrict__ cur,
+template <int D, int F, int WW, int ABL = 0, int FRT = (F <= 3 ? 4 : 8)>
+#ifndef RSF_VIV_WAVES
+#define RSF_VIV_WAVES 1  // min waves/SIMD for the round kernel (a cap of 4 measured slower)
+#endif
+__global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_round_kernel(const double* __restrict__ cur,
                                                             double* __restrict__ nxt,
                                                             double* __restrict__ adj_win,
                                                             uint32_t* __restrict__ adj_idx,
@@ -334,22 +338,37 @@ __global__ void __launch_bounds__(256) vivaldi_round_kernel(const double* __rest
   uint64_t local = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (local >= p.shard_n) return;
   const uint32_t m = (uint32_t)(p.lo + local);
-  const int FR = (F <= 3) ? 4 : 8;
+  const int FR = FRT;
   // ---- issue every independent load first: window index, window, own row
   const uint32_t widx = (WW > 0) ? adj_idx[local] : 0;
   double win[WW > 0 ? WW : 1];
 #pragma unroll
-  for (int i = 0; i < WW; ++i) win[i] = adj_win[(uint64_t)i * p.shard_n + local];
+  for (int i = 0; i < WW; ++i) win[i] = (ABL & 4) ? 0.0 : adj_win[(uint64_t)i * p.shard_n + local];
   double me[D], other[D], e, a, h, oe, oa, oh;
-  load_row<D>(cur + (uint64_t)m * p.stride, me, e, a, h, p.dim);
+  if (ABL & 8) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) me[i] = 0.001 * (double)(m & 7);
+    e = 1.0; a = 0.0; h = 1e-5;
+  } else {
+    load_row<D>(cur + (uint64_t)m * p.stride, me, e, a, h, p.dim);
+  }
   // ---- synthetic probe (neighbour slot, rtt); then the dependent gathers
   u32x4 pr = philox4x32_10(0, kPurposeVProbe << 24, m, p.round, p.k0, p.k1);
   uint32_t q = mulhi32(pr.x, p.peers);
   uint32_t peer = neighbour(p, m, q);
-  load_row<D>(cur + (uint64_t)peer * p.stride, other, oe, oa, oh, p.dim);
+  if (ABL & 1) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) other[i] = me[i] + 0.01;
+    oe = e; oa = a; oh = h;
+  } else {
+    load_row<D>(cur + (uint64_t)peer * p.stride, other, oe, oa, oh, p.dim);
+  }
   double* frec = filt + (local * p.peers + q) * FR;
   double rec[FR];
-  if (FR == 4) {
+  if (ABL & 2) {
+#pragma unroll
+    for (int i = 0; i < FR; ++i) rec[i] = 0.0;
+  } else if (FR == 4) {
     const double2* f2 = reinterpret_cast<const double2*>(frec);
     double2 t0 = f2[0], t1 = f2[1];
     rec[0] = t0.x;
@@ -357,8 +376,13 @@ __global__ void __launch_bounds__(256) vivaldi_round_kernel(const double* __rest
     rec[2] = t1.x;
     rec[3] = t1.y;
   } else {
+    const double2* f2 = reinterpret_cast<const double2*>(frec);
 #pragma unroll
-    for (int i = 0; i < FR; ++i) rec[i] = frec[i];
+    for (int i = 0; i < FR / 2; ++i) {
+      double2 t = f2[i];
+      rec[2 * i] = t.x;
+      rec[2 * i + 1] = t.y;
+    }
   }
   double xm, ym, hm, xp, yp, hp;
   true_pos(p.k0, p.k1, m, xm, ym, hm);
@@ -368,17 +392,19 @@ __global__ void __launch_bounds__(256) vivaldi_round_kernel(const double* __rest
   double jit = 1.0 + 0.1 * ((double)pr.y * 2.3283064365386963e-10);
   uint64_t rtt_ns = sat_u64((d * jit) * 1.0e9);
 
-  update_one<D, F, WW>(me, e, a, h, other, oe, oa, oh, p.dim, rtt_ns, rec, adj_win + local, p.shard_n,
-                       adj_idx + local, p, m, p.round, resets, win, widx);
-  if (FR == 4) {
-    double2* f2 = reinterpret_cast<double2*>(frec);
-    f2[0] = make_double2(rec[0], rec[1]);
-    f2[1] = make_double2(rec[2], rec[3]);
+  update_one<D, F, WW, FRT>(me, e, a, h, other, oe, oa, oh, p.dim, rtt_ns, rec, adj_win + local, p.shard_n,
+                            adj_idx + local, p, m, p.round, resets, win, widx);
+  if (ABL & 2) {
   } else {
+    double2* f2 = reinterpret_cast<double2*>(frec);
 #pragma unroll
-    for (int i = 0; i < FR; ++i) frec[i] = rec[i];
+    for (int i = 0; i < FR / 2; ++i) f2[i] = make_double2(rec[2 * i], rec[2 * i + 1]);
   }
-  store_row<D>(nxt + (uint64_t)m * p.stride, me, e, a, h, p.dim);
+  if (ABL & 16) {
+    if (e == 12345.0) store_row<D>(nxt + (uint64_t)m * p.stride, me, e, a, h, p.dim);
+  } else {
+    store_row<D>(nxt + (uint64_t)m * p.stride, me, e, a, h, p.dim);
+  }
 }
 
 template <int D, int F>
@@ -726,13 +752,36 @@ int rsf_vivaldi_round(rsf_vivaldi* v, uint32_t round) {
   unsigned blocks = (unsigned)((p.shard_n + 255) / 256);
   const double* cur = v->table[v->cur];
   double* nxt = v->table[v->cur ^ 1];
+#ifndef RSF_VIV_ROUND_WW
+#define RSF_VIV_ROUND_WW 20  // 0: runtime-sized window loop for the default config too
+#endif
   if (p.dim == 8 && p.F <= 3 && p.W == 20)
-    hipLaunchKernelGGL((vivaldi_round_kernel<8, 3, 20>), dim3(blocks), dim3(256), 0, v->stream, cur, nxt, v->adj,
-                       v->adj_idx, v->filt, v->resets, p);
+    hipLaunchKernelGGL((vivaldi_round_kernel<8, 3, RSF_VIV_ROUND_WW>), dim3(blocks), dim3(256), 0, v->stream, cur,
+                       nxt, v->adj, v->adj_idx, v->filt, v->resets, p);
   else
     RSF_DISPATCH_DF(p.dim, p.F,
                     hipLaunchKernelGGL((vivaldi_round_kernel<kD, kF, 0>), dim3(blocks), dim3(256), 0, v->stream,
                                        cur, nxt, v->adj, v->adj_idx, v->filt, v->resets, p));
+  RSF_HIP(hipGetLastError());
+  v->cur ^= 1;
+  return RSF_OK;
+}
+
+// diagnostic only (experiments/viv_ablate.py): variants with memory streams removed
+int rsf_vivaldi_round_ablate(rsf_vivaldi* v, uint32_t round, uint32_t mask) {
+  if (!v || v->p.dim != 8 || v->p.F > 3 || v->p.W != 20) return set_err_args("ablation needs D=8 F=3 W=20");
+  VivParams p = v->p;
+  p.round = round;
+  unsigned blocks = (unsigned)((p.shard_n + 255) / 256);
+  const double* cur = v->table[v->cur];
+  double* nxt = v->table[v->cur ^ 1];
+#define ABL_CASE(M) \
+  case M: hipLaunchKernelGGL((vivaldi_round_kernel<8, 3, 20, M>), dim3(blocks), dim3(256), 0, v->stream, cur, nxt, v->adj, v->adj_idx, v->filt, v->resets, p); break;
+  switch (mask) {
+    ABL_CASE(0) ABL_CASE(1) ABL_CASE(2) ABL_CASE(4) ABL_CASE(8) ABL_CASE(16) ABL_CASE(7) ABL_CASE(31)
+    default: return set_err_args("unsupported ablation mask");
+  }
+#undef ABL_CASE
   RSF_HIP(hipGetLastError());
   v->cur ^= 1;
   return RSF_OK;
