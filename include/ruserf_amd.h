@@ -120,8 +120,9 @@ int rsf_vivaldi_estimate_rtt_device(rsf_vivaldi* v, const uint32_t* a, const uin
                                     uint64_t* ns_out);
 
 /* One population round on the synthetic network of BASELINE configs 1/5:
- * every member of the shard probes one Philox-chosen neighbour out of
- * `peer_slots` fixed neighbours, observes rtt = true distance x (1 + U[0,0.1)),
+ * every member of the shard probes neighbour slot (round mod `peer_slots`) of
+ * its fixed, Philox-drawn neighbour list (memberlist's round-robin probe loop),
+ * observes rtt = true distance x (1 + U[0,0.1)),
  * and runs CoordinateClient::update with the neighbour's coordinate as of the
  * END OF THE PREVIOUS ROUND (the ack carries the peer's last coordinate,
  * core/src/serf/delegate.rs:659-779).  Asynchronous; flips the table buffers. */

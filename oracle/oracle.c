@@ -369,7 +369,11 @@ void orc_vivaldi_probe(uint64_t seed, uint32_t n, uint32_t peers, const uint32_t
   seed_key(seed, key);
   uint32_t ctr[4] = {0, PURPOSE_VPROBE << 24, m, round}, o[4];
   orc_philox4x32(ctr, key, o);
-  uint32_t q = mulhi32(o[0], peers);
+  /* memberlist's probe loop walks its member list round-robin (state.go probe():
+     probeIndex advances one node per probe interval; memberlist is a dependency
+     not vendored in /root/reference): slot = round mod peers over the member's
+     fixed, Philox-drawn neighbour list.  o[1] is the RTT jitter. */
+  uint32_t q = round % peers;
   uint32_t p = nbr[(size_t)m * peers + q];
   double xm, ym, hm, xp, yp, hp;
   orc_true_position(seed, m, &xm, &ym, &hm);

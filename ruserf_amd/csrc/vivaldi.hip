@@ -11,8 +11,10 @@
 //                                          portion[dim], error, adjustment, height)
 //   adj  [W][shard_n] f64                  adjustment windows, window-slot-major (coalesced)
 //   adj_idx[shard_n] u32
-//   filt [shard_n][peer_slots][FR] f64     latency filter rings, FR = 4 (F<=3) or 8 (F<=7);
-//                                          the last f64 of a record holds len | head<<32
+//   filt [peer_slots][shard_n][FR] f64     latency filter rings, FR = 4 (F<=3) or 8 (F<=7);
+//                                          the last f64 of a record holds len | head<<32.
+//                                          Slot-major: a round probes one slot for every
+//                                          member, so its filter records stream coalesced.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -353,8 +355,9 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_round_kernel(const
     load_row<D>(cur + (uint64_t)m * p.stride, me, e, a, h, p.dim);
   }
   // ---- synthetic probe (neighbour slot, rtt); then the dependent gathers
+  // probe slot: round-robin over the neighbour list (memberlist's probe loop); uniform per launch
   u32x4 pr = philox4x32_10(0, kPurposeVProbe << 24, m, p.round, p.k0, p.k1);
-  uint32_t q = mulhi32(pr.x, p.peers);
+  const uint32_t q = p.round % p.peers;
   uint32_t peer = neighbour(p, m, q);
   if (ABL & 1) {
 #pragma unroll
@@ -363,7 +366,7 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_round_kernel(const
   } else {
     load_row<D>(cur + (uint64_t)peer * p.stride, other, oe, oa, oh, p.dim);
   }
-  double* frec = filt + (local * p.peers + q) * FR;
+  double* frec = filt + ((uint64_t)q * p.shard_n + local) * FR;
   double rec[FR];
   if (ABL & 2) {
 #pragma unroll
@@ -432,7 +435,7 @@ __global__ void __launch_bounds__(256) vivaldi_batch_kernel(
 #pragma unroll
     for (int k = 0; k < D; ++k) other[k] = 0.0;
   }
-  double* frec = filt + (local * p.peers + q) * FR;
+  double* frec = filt + ((uint64_t)q * p.shard_n + local) * FR;
   double rec[FR];
 #pragma unroll
   for (int k = 0; k < FR; ++k) rec[k] = frec[k];
@@ -633,7 +636,7 @@ int rsf_vivaldi_forget_node(rsf_vivaldi* v, uint64_t m, uint32_t slot) {
   if (!v) return set_err_args("null context");
   if (m < v->p.lo || m >= v->p.lo + v->p.shard_n || slot >= v->p.peers) return set_err_args("member/slot out of range");
   RSF_HIP(hipSetDevice(v->device));
-  RSF_HIP(hipMemsetAsync(v->filt + ((m - v->p.lo) * v->p.peers + slot) * v->p.FR, 0, v->p.FR * sizeof(double),
+  RSF_HIP(hipMemsetAsync(v->filt + ((uint64_t)slot * v->p.shard_n + (m - v->p.lo)) * v->p.FR, 0, v->p.FR * sizeof(double),
                          v->stream));
   return RSF_OK;
 }
