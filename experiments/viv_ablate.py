@@ -20,9 +20,11 @@ torch.cuda.set_stream(torch.cuda.Stream())
 s = torch.cuda.current_stream()
 g = CoordinateClients(n, 16, CoordinateOptions())
 g.set_stream(s.cuda_stream)
+g.round(0)  # fills the context's probe buffers the ablated observe kernels read
 out = {}
 for mask, name in [(0, "full"), (1, "no_peer_gather"), (2, "no_filter"), (4, "no_window"), (8, "no_self_row_read"),
-                   (16, "no_row_write"), (1 | 2 | 4, "self_row_only"), (31, "compute_only"), (0, "full_again")]:
+                   (16, "no_row_write"), (32, "no_probe_inputs"), (1 | 2 | 4, "self_row_only"), (63, "compute_only"),
+                   (0, "full_again")]:
     for r in range(3):
         L.rsf_vivaldi_round_ablate(g._h, r, mask)
     torch.cuda.synchronize()

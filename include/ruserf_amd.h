@@ -128,6 +128,25 @@ int rsf_vivaldi_estimate_rtt_device(rsf_vivaldi* v, const uint32_t* a, const uin
  * core/src/serf/delegate.rs:659-779).  Asynchronous; flips the table buffers. */
 int rsf_vivaldi_round(rsf_vivaldi* v, uint32_t round);
 
+/* The two halves of rsf_vivaldi_round, for callers that bring their own probes.
+ *
+ * rsf_vivaldi_gen_probes: the synthetic network's observations for `round`
+ * (slot round mod peer_slots): peer_out[i] = neighbour of shard member lo+i,
+ * rtt_ns_out[i] its observed RTT.  Device pointers, shard_n entries each.
+ *
+ * rsf_vivaldi_observe: one CoordinateClient::update (coordinate.rs:462-499) per
+ * shard member lo+i with node = the neighbour held in latency-filter slot `slot`,
+ * other = row peer[i] of the table as of the end of the previous round, rtt =
+ * rtt_ns[i] (the batched form of notify_ping_complete, delegate.rs:704-779).
+ * Device pointers, shard_n entries each; status_out (nullable) receives RSF_OK or
+ * RSF_ERR_INVALID_RTT (rtt > 10 s) / RSF_ERR_INVALID_COORD per member, or
+ * RSF_ERR_ARG for peer[i] >= n_members; on an error the member's coordinate and
+ * filter are unchanged.  `round` keys the Philox stream of the degenerate
+ * unit-vector draws (coordinate.rs:812-821).  Asynchronous; flips the tables. */
+int rsf_vivaldi_gen_probes(rsf_vivaldi* v, uint32_t round, uint32_t* peer_out, uint64_t* rtt_ns_out);
+int rsf_vivaldi_observe(rsf_vivaldi* v, uint32_t slot, const uint32_t* peer, const uint64_t* rtt_ns,
+                        int32_t* status_out, uint32_t round);
+
 /* Device pointer of the current full coordinate table (n_members rows) and of
  * this shard's slice, for an all-gather between rounds on multi-GPU runs. */
 int rsf_vivaldi_table(rsf_vivaldi* v, double** table_out, uint64_t* row_stride_out);

@@ -96,6 +96,8 @@ def lib():
     _sig(L, "rsf_vivaldi_estimate_rtt_batch", i, [VP, P32, P32, C.c_uint64, P64])
     _sig(L, "rsf_vivaldi_estimate_rtt_device", i, [VP, VP, VP, C.c_uint64, VP])
     _sig(L, "rsf_vivaldi_round", i, [VP, C.c_uint32])
+    _sig(L, "rsf_vivaldi_gen_probes", i, [VP, C.c_uint32, VP, VP])
+    _sig(L, "rsf_vivaldi_observe", i, [VP, C.c_uint32, VP, VP, VP, C.c_uint32])
     _sig(L, "rsf_vivaldi_table", i, [VP, C.POINTER(VP), P64])
     _sig(L, "rsf_vivaldi_true_rtt_ns", i, [VP, C.c_uint32, C.c_uint32, P64])
     try:

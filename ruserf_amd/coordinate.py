@@ -226,7 +226,17 @@ class CoordinateClients:
 
     # ---- population round (synthetic network)
     def round(self, r):
+        """gen_probes(r) into the context's own buffers, then observe (slot r mod peer_slots)."""
         check(lib().rsf_vivaldi_round(self._h, r))
+
+    def gen_probes(self, r, peer_ptr, rtt_ptr):
+        """Synthetic probes of round r into device buffers (shard_n u32 peers, shard_n u64 rtt ns)."""
+        check(lib().rsf_vivaldi_gen_probes(self._h, r, C.c_void_p(peer_ptr), C.c_void_p(rtt_ptr)))
+
+    def observe(self, slot, peer_ptr, rtt_ptr, status_ptr=None, round_=0):
+        """One update per shard member from device-resident probes (see rsf_vivaldi_observe)."""
+        check(lib().rsf_vivaldi_observe(self._h, slot, C.c_void_p(peer_ptr), C.c_void_p(rtt_ptr),
+                                        C.c_void_p(status_ptr) if status_ptr else None, round_))
 
     def table_ptr(self):
         p = C.c_void_p()

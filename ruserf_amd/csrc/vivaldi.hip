@@ -327,21 +327,58 @@ __device__ __forceinline__ void store_row(double* __restrict__ row, const double
   }
 }
 
-template <int D, int F, int WW, int ABL = 0, int FRT = (F <= 3 ? 4 : 8)>
+// Synthetic network of BASELINE configs 1/5 (the oracle's orc_vivaldi_probe): the
+// harness's INPUT generator, not part of the update path.  Member lo+i probes
+// neighbour slot `slot` (round-robin, memberlist's probe loop); rtt = true distance x
+// (1 + U[0,0.1)) quantised to ns.
+__global__ void __launch_bounds__(256) probe_gen_kernel(VivParams p, uint32_t slot, uint32_t* __restrict__ peer_out,
+                                                        uint64_t* __restrict__ rtt_out) {
+  uint64_t local = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (local >= p.shard_n) return;
+  const uint32_t m = (uint32_t)(p.lo + local);
+  u32x4 pr = philox4x32_10(0, kPurposeVProbe << 24, m, p.round, p.k0, p.k1);
+  uint32_t peer = neighbour(p, m, slot);
+  double xm, ym, hm, xp, yp, hp;
+  true_pos(p.k0, p.k1, m, xm, ym, hm);
+  true_pos(p.k0, p.k1, peer, xp, yp, hp);
+  double dx = xm - xp, dy = ym - yp;
+  double d = sqrt(dx * dx + dy * dy) + hm + hp;
+  double jit = 1.0 + 0.1 * ((double)pr.y * 2.3283064365386963e-10);
+  peer_out[local] = peer;
+  rtt_out[local] = sat_u64((d * jit) * 1.0e9);
+}
+
+// One observation per shard member (the round's hot kernel): member lo+i runs
+// CoordinateClient::update (coordinate.rs:462-499) with node = its neighbour in filter
+// slot `slot`, other = that peer's row of the PREVIOUS table (the ack-carried coordinate,
+// delegate.rs:704-779), rtt = rtt_in[i].  Inputs are read coalesced; the only gather is
+// the peer row.  Writes this member's row to the next table (unchanged on an error).
+// ABL (diagnostic only, rsf_vivaldi_round_ablate) drops memory streams:
+//   1 peer-row gather, 2 filter record, 4 adjustment window, 8 own-row read,
+//   16 own-row write, 32 probe inputs.
 #ifndef RSF_VIV_WAVES
-#define RSF_VIV_WAVES 1  // min waves/SIMD for the round kernel (a cap of 4 measured slower)
+#define RSF_VIV_WAVES 1  // min waves/SIMD for the observe kernel (a cap of 4 measured slower)
 #endif
-__global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_round_kernel(const double* __restrict__ cur,
-                                                            double* __restrict__ nxt,
-                                                            double* __restrict__ adj_win,
-                                                            uint32_t* __restrict__ adj_idx,
-                                                            double* __restrict__ filt,
-                                                            unsigned long long* resets, VivParams p) {
+template <int D, int F, int WW, int ABL = 0, int FRT = (F <= 3 ? 4 : 8)>
+__global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
+    const double* __restrict__ cur, double* __restrict__ nxt, double* __restrict__ adj_win,
+    uint32_t* __restrict__ adj_idx, double* __restrict__ filt, unsigned long long* resets,
+    const uint32_t* __restrict__ peer_in, const uint64_t* __restrict__ rtt_in, int32_t* __restrict__ status,
+    VivParams p, uint32_t slot) {
   uint64_t local = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (local >= p.shard_n) return;
   const uint32_t m = (uint32_t)(p.lo + local);
   const int FR = FRT;
-  // ---- issue every independent load first: window index, window, own row
+  // ---- every independent load first: probe input, window index + window, own row, filter record
+  uint32_t peer;
+  uint64_t rtt_ns;
+  if (ABL & 32) {
+    peer = (uint32_t)((m * 2654435761ull) % p.n);
+    rtt_ns = 20000000ull + (m & 1023);
+  } else {
+    peer = peer_in[local];
+    rtt_ns = rtt_in[local];
+  }
   const uint32_t widx = (WW > 0) ? adj_idx[local] : 0;
   double win[WW > 0 ? WW : 1];
 #pragma unroll
@@ -354,30 +391,11 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_round_kernel(const
   } else {
     load_row<D>(cur + (uint64_t)m * p.stride, me, e, a, h, p.dim);
   }
-  // ---- synthetic probe (neighbour slot, rtt); then the dependent gathers
-  // probe slot: round-robin over the neighbour list (memberlist's probe loop); uniform per launch
-  u32x4 pr = philox4x32_10(0, kPurposeVProbe << 24, m, p.round, p.k0, p.k1);
-  const uint32_t q = p.round % p.peers;
-  uint32_t peer = neighbour(p, m, q);
-  if (ABL & 1) {
-#pragma unroll
-    for (int i = 0; i < D; ++i) other[i] = me[i] + 0.01;
-    oe = e; oa = a; oh = h;
-  } else {
-    load_row<D>(cur + (uint64_t)peer * p.stride, other, oe, oa, oh, p.dim);
-  }
-  double* frec = filt + ((uint64_t)q * p.shard_n + local) * FR;
+  double* frec = filt + ((uint64_t)slot * p.shard_n + local) * FR;
   double rec[FR];
   if (ABL & 2) {
 #pragma unroll
     for (int i = 0; i < FR; ++i) rec[i] = 0.0;
-  } else if (FR == 4) {
-    const double2* f2 = reinterpret_cast<const double2*>(frec);
-    double2 t0 = f2[0], t1 = f2[1];
-    rec[0] = t0.x;
-    rec[1] = t0.y;
-    rec[2] = t1.x;
-    rec[3] = t1.y;
   } else {
     const double2* f2 = reinterpret_cast<const double2*>(frec);
 #pragma unroll
@@ -387,18 +405,23 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_round_kernel(const
       rec[2 * i + 1] = t.y;
     }
   }
-  double xm, ym, hm, xp, yp, hp;
-  true_pos(p.k0, p.k1, m, xm, ym, hm);
-  true_pos(p.k0, p.k1, peer, xp, yp, hp);
-  double dx = xm - xp, dy = ym - yp;
-  double d = sqrt(dx * dx + dy * dy) + hm + hp;
-  double jit = 1.0 + 0.1 * ((double)pr.y * 2.3283064365386963e-10);
-  uint64_t rtt_ns = sat_u64((d * jit) * 1.0e9);
-
-  update_one<D, F, WW, FRT>(me, e, a, h, other, oe, oa, oh, p.dim, rtt_ns, rec, adj_win + local, p.shard_n,
-                            adj_idx + local, p, m, p.round, resets, win, widx);
-  if (ABL & 2) {
+  // ---- the dependent gather: the peer's row of the previous table
+  int st;
+  if (peer >= p.n) {
+    st = RSF_ERR_ARG;
   } else {
+    if (ABL & 1) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) other[i] = me[i] + 0.01;
+      oe = e; oa = a; oh = h;
+    } else {
+      load_row<D>(cur + (uint64_t)peer * p.stride, other, oe, oa, oh, p.dim);
+    }
+    st = update_one<D, F, WW, FRT>(me, e, a, h, other, oe, oa, oh, p.dim, rtt_ns, rec, adj_win + local, p.shard_n,
+                                   adj_idx + local, p, m, p.round, resets, win, widx);
+  }
+  if (status) status[local] = st;
+  if (!(ABL & 2) && st == RSF_OK) {
     double2* f2 = reinterpret_cast<double2*>(frec);
 #pragma unroll
     for (int i = 0; i < FR / 2; ++i) f2[i] = make_double2(rec[2 * i], rec[2 * i + 1]);
@@ -489,6 +512,9 @@ struct rsf_vivaldi {
   uint32_t* adj_idx = nullptr;
   double* filt = nullptr;
   unsigned long long* resets = nullptr;
+  // probe inputs of rsf_vivaldi_round (peer id, rtt ns per shard member)
+  uint32_t* probe_peer = nullptr;
+  uint64_t* probe_rtt = nullptr;
   // batch staging (device)
   DeviceScratch scratch;
 };
@@ -556,7 +582,9 @@ int rsf_vivaldi_create(rsf_vivaldi** out, uint64_t n, uint64_t lo, uint64_t hi, 
       (rc = rsf::dmalloc((void**)&v->adj, (size_t)(p.W ? p.W : 1) * p.shard_n * sizeof(double))) ||
       (rc = rsf::dmalloc((void**)&v->adj_idx, (size_t)p.shard_n * sizeof(uint32_t))) ||
       (rc = rsf::dmalloc((void**)&v->filt, (size_t)p.shard_n * peers * p.FR * sizeof(double))) ||
-      (rc = rsf::dmalloc((void**)&v->resets, sizeof(unsigned long long))))
+      (rc = rsf::dmalloc((void**)&v->resets, sizeof(unsigned long long))) ||
+      (rc = rsf::dmalloc((void**)&v->probe_peer, (size_t)p.shard_n * sizeof(uint32_t))) ||
+      (rc = rsf::dmalloc((void**)&v->probe_rtt, (size_t)p.shard_n * sizeof(uint64_t))))
     return fail(rc);
   unsigned blocks = (unsigned)((n + 255) / 256);
   for (int t = 0; t < 2; ++t)
@@ -582,6 +610,8 @@ int rsf_vivaldi_destroy(rsf_vivaldi* v) {
   hipFree(v->adj_idx);
   hipFree(v->filt);
   hipFree(v->resets);
+  hipFree(v->probe_peer);
+  hipFree(v->probe_rtt);
   v->scratch.release();
   if (v->own) hipStreamDestroy(v->own);
   delete v;
@@ -747,41 +777,76 @@ int rsf_vivaldi_estimate_rtt_batch(rsf_vivaldi* v, const uint32_t* a, const uint
   return RSF_OK;
 }
 
-int rsf_vivaldi_round(rsf_vivaldi* v, uint32_t round) {
-  if (!v) return set_err_args("null context");
+int rsf_vivaldi_gen_probes(rsf_vivaldi* v, uint32_t round, uint32_t* peer_out, uint64_t* rtt_ns_out) {
+  if (!v || !peer_out || !rtt_ns_out) return set_err_args("null argument");
+  RSF_HIP(hipSetDevice(v->device));
+  VivParams p = v->p;
+  p.round = round;
+  unsigned blocks = (unsigned)((p.shard_n + 255) / 256);
+  hipLaunchKernelGGL(probe_gen_kernel, dim3(blocks), dim3(256), 0, v->stream, p, round % p.peers, peer_out,
+                     rtt_ns_out);
+  RSF_HIP(hipGetLastError());
+  return RSF_OK;
+}
+
+#ifndef RSF_VIV_ROUND_WW
+#define RSF_VIV_ROUND_WW 20  // 0: runtime-sized window loop for the default config too
+#endif
+int rsf_vivaldi_observe(rsf_vivaldi* v, uint32_t slot, const uint32_t* peer, const uint64_t* rtt_ns,
+                        int32_t* status_out, uint32_t round) {
+  if (!v || !peer || !rtt_ns) return set_err_args("null argument");
+  if (slot >= v->p.peers) return set_err_args("peer_slot out of range");
   RSF_HIP(hipSetDevice(v->device));
   VivParams p = v->p;
   p.round = round;
   unsigned blocks = (unsigned)((p.shard_n + 255) / 256);
   const double* cur = v->table[v->cur];
   double* nxt = v->table[v->cur ^ 1];
-#ifndef RSF_VIV_ROUND_WW
-#define RSF_VIV_ROUND_WW 20  // 0: runtime-sized window loop for the default config too
-#endif
   if (p.dim == 8 && p.F <= 3 && p.W == 20)
-    hipLaunchKernelGGL((vivaldi_round_kernel<8, 3, RSF_VIV_ROUND_WW>), dim3(blocks), dim3(256), 0, v->stream, cur,
-                       nxt, v->adj, v->adj_idx, v->filt, v->resets, p);
+    hipLaunchKernelGGL((vivaldi_observe_kernel<8, 3, RSF_VIV_ROUND_WW>), dim3(blocks), dim3(256), 0, v->stream,
+                       cur, nxt, v->adj, v->adj_idx, v->filt, v->resets, peer, rtt_ns, status_out, p, slot);
   else
     RSF_DISPATCH_DF(p.dim, p.F,
-                    hipLaunchKernelGGL((vivaldi_round_kernel<kD, kF, 0>), dim3(blocks), dim3(256), 0, v->stream,
-                                       cur, nxt, v->adj, v->adj_idx, v->filt, v->resets, p));
+                    hipLaunchKernelGGL((vivaldi_observe_kernel<kD, kF, 0>), dim3(blocks), dim3(256), 0, v->stream,
+                                       cur, nxt, v->adj, v->adj_idx, v->filt, v->resets, peer, rtt_ns, status_out,
+                                       p, slot));
   RSF_HIP(hipGetLastError());
   v->cur ^= 1;
   return RSF_OK;
 }
 
-// diagnostic only (experiments/viv_ablate.py): variants with memory streams removed
+int rsf_vivaldi_round(rsf_vivaldi* v, uint32_t round) {
+  int rc = rsf_vivaldi_gen_probes(v, round, v ? v->probe_peer : nullptr, v ? v->probe_rtt : nullptr);
+  if (rc) return rc;
+  return rsf_vivaldi_observe(v, round % v->p.peers, v->probe_peer, v->probe_rtt, nullptr, round);
+}
+
+// diagnostic only (experiments/viv_ablate.py): observe-kernel variants with memory
+// streams removed; probes come from the context's own buffers (generate them first
+// with rsf_vivaldi_gen_probes into rsf_vivaldi_probe_buffers)
+int rsf_vivaldi_probe_buffers(rsf_vivaldi* v, uint32_t** peer, uint64_t** rtt) {
+  if (!v || !peer || !rtt) return set_err_args("null argument");
+  *peer = v->probe_peer;
+  *rtt = v->probe_rtt;
+  return RSF_OK;
+}
+
 int rsf_vivaldi_round_ablate(rsf_vivaldi* v, uint32_t round, uint32_t mask) {
   if (!v || v->p.dim != 8 || v->p.F > 3 || v->p.W != 20) return set_err_args("ablation needs D=8 F=3 W=20");
   VivParams p = v->p;
   p.round = round;
+  const uint32_t slot = round % p.peers;
   unsigned blocks = (unsigned)((p.shard_n + 255) / 256);
   const double* cur = v->table[v->cur];
   double* nxt = v->table[v->cur ^ 1];
-#define ABL_CASE(M) \
-  case M: hipLaunchKernelGGL((vivaldi_round_kernel<8, 3, 20, M>), dim3(blocks), dim3(256), 0, v->stream, cur, nxt, v->adj, v->adj_idx, v->filt, v->resets, p); break;
+#define ABL_CASE(M)                                                                                            \
+  case M:                                                                                                      \
+    hipLaunchKernelGGL((vivaldi_observe_kernel<8, 3, 20, M>), dim3(blocks), dim3(256), 0, v->stream, cur, nxt, \
+                       v->adj, v->adj_idx, v->filt, v->resets, v->probe_peer, v->probe_rtt, nullptr, p, slot);  \
+    break;
   switch (mask) {
-    ABL_CASE(0) ABL_CASE(1) ABL_CASE(2) ABL_CASE(4) ABL_CASE(8) ABL_CASE(16) ABL_CASE(7) ABL_CASE(31)
+    ABL_CASE(0) ABL_CASE(1) ABL_CASE(2) ABL_CASE(4) ABL_CASE(8) ABL_CASE(16) ABL_CASE(32) ABL_CASE(7)
+    ABL_CASE(63)
     default: return set_err_args("unsupported ablation mask");
   }
 #undef ABL_CASE

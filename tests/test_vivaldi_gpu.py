@@ -180,3 +180,78 @@ def test_client_kats_through_engine(kats):
     assert h0.distance_to([0], [1])[0] == k["client_distance_to"]["expect_ns"]
     g.close()
     h0.close()
+
+
+def test_gen_probes_match_oracle():
+    """The synthetic network's probes (the bench's resident inputs) equal the oracle's."""
+    import torch
+    n, peers = 5000, 16
+    g = CoordinateClients(n, peers, seed=SEED)
+    nbr = np.empty(n * peers, dtype=np.uint32)
+    L.orc_gen_neighbors(SEED, n, peers, nbr.ctypes.data_as(O.P32))
+    peer = torch.empty(n, dtype=torch.int32, device="cuda")
+    rtt = torch.empty(n, dtype=torch.int64, device="cuda")
+    for r in (0, 1, 17, 1000):
+        g.gen_probes(r, peer.data_ptr(), rtt.data_ptr())
+        torch.cuda.synchronize()
+        gp = peer.cpu().numpy().view(np.uint32)
+        gr = rtt.cpu().numpy().view(np.uint64)
+        for m in range(0, n, 13):
+            slot, ns = C.c_uint32(), C.c_uint64()
+            L.orc_vivaldi_probe(SEED, n, peers, nbr.ctypes.data_as(O.P32), m, r, C.byref(slot), C.byref(ns))
+            assert slot.value == r % peers
+            assert gp[m] == nbr[m * peers + slot.value], (r, m)
+            assert gr[m] == ns.value, (r, m)
+    g.close()
+
+
+def test_observe_explicit_probes_matches_oracle_clients():
+    """rsf_vivaldi_observe with caller-provided, device-resident (peer, rtt) inputs —
+    including invalid RTTs and out-of-range peers — against one oracle client per
+    member fed the same peer coordinates (previous-round snapshot)."""
+    import torch
+    n, slots = 96, 4
+    g = CoordinateClients(n, slots, seed=SEED)
+    oo = O.default_opts()
+    clients = []
+    for m in range(n):
+        c = O.Client()
+        assert L.orc_client_init(C.byref(c), C.byref(oo), slots) == 0
+        clients.append(c)
+    rng = np.random.default_rng(9)
+    stride = g.stride
+    for rnd in range(24):
+        snap = g.get_rows()  # previous-round table (= the oracle clients' coordinates)
+        peer = rng.integers(0, n, n).astype(np.uint32)
+        peer[peer == np.arange(n)] = (peer[peer == np.arange(n)] + 1) % n
+        rtt = rng.integers(1_000_000, 80_000_000, n).astype(np.uint64)
+        kind = rng.integers(0, 16, n)
+        rtt[kind == 0] = 10_000_000_001  # InvalidRTT
+        rtt[kind == 1] = 10_000_000_000  # equality accepted
+        peer[kind == 2] = n + 5          # out of range -> RSF_ERR_ARG
+        dp = torch.from_numpy(peer.view(np.int32)).cuda()
+        dr = torch.from_numpy(rtt.view(np.int64)).cuda()
+        ds = torch.empty(n, dtype=torch.int32, device="cuda")
+        slot = rnd % slots
+        g.observe(slot, dp.data_ptr(), dr.data_ptr(), ds.data_ptr(), round_=rnd)
+        torch.cuda.synchronize()
+        status = ds.cpu().numpy()
+        rows = g.get_rows()
+        for m in range(n):
+            if peer[m] >= n:
+                assert status[m] == -1  # RSF_ERR_ARG
+                np.testing.assert_array_equal(rows[m].view(np.uint64), snap[m].view(np.uint64))
+                continue
+            o = snap[peer[m]]
+            oc = O.coord(oo, list(o[:8]), o[8], o[9], o[10])
+            out = O.Coord()
+            e = L.orc_client_update(C.byref(clients[m]), slot, C.byref(oc), int(rtt[m]), C.byref(O.rng(SEED, m, rnd)),
+                                    C.byref(out))
+            assert status[m] == e, (rnd, m)
+            c = clients[m].coord
+            exp = np.array(list(c.portion[:8]) + [c.error, c.adjustment, c.height])
+            np.testing.assert_array_equal(rows[m, :11].view(np.uint64), exp.view(np.uint64))
+        assert stride == rows.shape[1]
+    for c in clients:
+        L.orc_client_free(C.byref(c))
+    g.close()
