@@ -500,6 +500,21 @@ __global__ void __launch_bounds__(256) first_sentinel_kernel(const uint32_t* __r
 #ifndef RSF_MERGE_WAVES
 #define RSF_MERGE_WAVES 5  // min waves/SIMD for merge_kernel (register cap)
 #endif
+#ifndef RSF_MERGE_PROF
+#define RSF_MERGE_PROF 0  // diagnostic build: per-phase shader-clock totals of merge_kernel
+#endif
+#if RSF_MERGE_PROF
+__device__ unsigned long long g_merge_prof[8];
+#define MPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define MPROF_ADD(i, a, b) \
+  if (lane == 0) atomicAdd(&g_merge_prof[i], (unsigned long long)((b) - (a)))
+#else
+#define MPROF_T(v)
+#define MPROF_ADD(i, a, b)
+#endif
+#ifndef RSF_MERGE_HEADSKIP
+#define RSF_MERGE_HEADSKIP 0  // 1: skip loading a queue whose slot 0 is free (measured slower: spills + a dependent probe)
+#endif
 #ifndef RSF_MERGE_EAGER
 #define RSF_MERGE_EAGER 1  // 0: load the query/event queues only when a chunk needs them
 #endif
@@ -510,6 +525,7 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
   const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x / kWave);
   if (l >= c.n_loc) return;
   const uint32_t m = (uint32_t)(c.lo + l);
+  MPROF_T(t_start);
   const uint32_t st = seg_start[l], en = seg_end[l];
   if (st >= en || !s.alive[m]) return;
   // queues are loaded on first need (the record types of a chunk say which) and
@@ -518,14 +534,18 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
   bool ld0 = true, ld1 = RSF_MERGE_EAGER, ld2 = RSF_MERGE_EAGER, d0 = false, d1 = false, d2 = false;
   q_load(c, s, l, 0, lane, Q0);  // intents are the common case: load with the first prefetch
   if (RSF_MERGE_EAGER) {
-    q_load(c, s, l, 1, lane, Q1);
-    q_load(c, s, l, 2, lane, Q2);
+    // a sorted queue is empty iff its slot 0 is free (wave-uniform probe): skip the load then
+    if (!RSF_MERGE_HEADSKIP || s.q_rumor[(l * 3 + 1) * c.qcap] != kEmpty) q_load(c, s, l, 1, lane, Q1);
+    if (!RSF_MERGE_HEADSKIP || s.q_rumor[(l * 3 + 2) * c.qcap] != kEmpty) q_load(c, s, l, 2, lane, Q2);
   }
   uint32_t nseq0 = s.q_next_seq[l * 3 + 0], nseq1 = s.q_next_seq[l * 3 + 1], nseq2 = s.q_next_seq[l * 3 + 2];
   MRegs r;
   load_regs(s, l, r);
   ViewE* vrow = s.view + l * c.S;
+  MPROF_T(t_setup);
+  MPROF_ADD(0, t_start, t_setup);
   for (uint32_t base = st; base < en; base += kWave) {
+    MPROF_T(t_c0);
     const uint32_t cnt = min((uint32_t)kWave, en - base);
     const bool valid = lane < cnt;
     const uint32_t rid = valid ? vals[base + lane] : 0;
@@ -568,6 +588,8 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
     const uint64_t excl = wave_shr1_u64(incl);
     const uint64_t clock_before = excl > r.clock ? excl : r.clock;
     const uint64_t chunk_max = lane63_u64(incl);
+    MPROF_T(t_c1);
+    MPROF_ADD(1, t_c0, t_c1);
     // walk chains in depth order
     ViewE v = pre;
     int f = 0;
@@ -604,6 +626,8 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
     }
     if (next < 0 && is_view && dirty) vrow[my_subj] = v;  // last link writes the subject back
     if (chunk_max > r.clock) r.clock = chunk_max;
+    MPROF_T(t_c2);
+    MPROF_ADD(2, t_c1, t_c2);
     // serial part, record order: events/queries (lane 0 handlers), digest, refutes, re-queues
     const uint64_t serial = __ballot(valid && (!is_view || f != 0));
     uint64_t mm = serial;
@@ -649,8 +673,11 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
         }
       }
     }
+    MPROF_T(t_c3);
+    MPROF_ADD(3, t_c2, t_c3);
     if (base + kWave < en) __threadfence_block();  // next chunk's prefetch must see this chunk's view stores
   }
+  MPROF_T(t_st0);
   if (d0) q_store(c, s, l, 0, lane, Q0, true);
   if (d1) q_store(c, s, l, 1, lane, Q1, true);
   if (d2) q_store(c, s, l, 2, lane, Q2, true);
@@ -660,6 +687,10 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
     if (d1) s.q_next_seq[l * 3 + 1] = nseq1;
     if (d2) s.q_next_seq[l * 3 + 2] = nseq2;
   }
+  MPROF_T(t_end);
+  MPROF_ADD(4, t_st0, t_end);
+  MPROF_ADD(5, t_start, t_end);
+  if (lane == 0) { MPROF_ADD(6, 0, 1); }
 }
 
 // direct-handler batch: one thread per receiver segment (array order within a receiver)
@@ -1257,6 +1288,21 @@ int rsf_gossip_send_buffer(rsf_gossip* g, void** p, uint64_t* cap) {
   *p = g->send_buf;
   if (cap) *cap = std::max(g->stage_cap, g->recv_cap);
   return RSF_OK;
+}
+
+// diagnostic only (experiments/merge_prof.py, builds with -DRSF_MERGE_PROF=1): reads and
+// clears merge_kernel's per-phase shader-clock totals; returns -1 in normal builds
+int rsf_gossip_merge_prof(uint64_t* out8) {
+#if RSF_MERGE_PROF
+  RSF_HIP(hipDeviceSynchronize());
+  RSF_HIP(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_merge_prof), 8 * sizeof(uint64_t)));
+  unsigned long long z[8] = {};
+  RSF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_merge_prof), z, sizeof(z)));
+  return RSF_OK;
+#else
+  (void)out8;
+  return -1;
+#endif
 }
 
 int rsf_gossip_round_merge(rsf_gossip* g, const uint64_t* recv, uint64_t n_recv) {
