@@ -158,7 +158,10 @@ def run_vivaldi(args, rank, world):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "vivaldi_observe_kernel<8,3,20>", "bytes_per_unit": VIVALDI_BYTES,
-                     "units_per_launch": per, "avg_launch_ms": avg_kernel_s * 1e3},
+                     "units_per_launch": per, "bytes_per_launch": VIVALDI_BYTES * per,
+                     "avg_launch_ms": avg_kernel_s * 1e3},
+        # --members is per GPU unless --members-total; the default keeps 64M members in total
+        "scaling": "strong" if args.members_total else "weak",
     }
 
 
@@ -183,6 +186,25 @@ def cpu_baseline_vivaldi(seconds_target=12.0):
     return {"value": n * rounds / t_total, "unit": "updates/s", "cores": th, "kind": "port",
             "sample": f"oracle Vivaldi rounds, {n} members x {rounds} rounds ({t_total:.1f}s) on {th} threads, "
                       f"{cpu_info()}"}
+
+
+# --------------------------------------------------------------------------- traffic
+def attach_traffic(workload, res):
+    """roofline.traffic = HBM bytes per launch of the dominant kernel from the rocprofv3
+    PMC passes committed under profiles/ (scripts/make_traffic.py; corrections in
+    DESIGN.md §Measurement), when this run's kernel and size match the profiled one."""
+    rl = res["roofline"]
+    try:
+        with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+            ent = json.load(f).get(workload)
+    except (OSError, ValueError):
+        ent = None
+    if not ent or ent["kernel"] != rl["kernel"] or ent["members_per_gpu"] != res["config"]["members_per_gpu"]:
+        return
+    rl["traffic"] = ent["traffic_bytes_per_launch"]
+    rl["traffic_unit"] = "bytes/launch"
+    rl["traffic_vs_algorithmic"] = ent["traffic_bytes_per_launch"] / rl["bytes_per_launch"]
+    rl["traffic_source"] = ent["source"]
 
 
 # --------------------------------------------------------------------------- main
@@ -214,7 +236,8 @@ def main():
         have_gossip = False
     workload = args.workload or ("gossip" if have_gossip else "vivaldi")
     if workload == "vivaldi":
-        args.members = args.members or 64_000_000 // max(1, world) * max(1, world) // world
+        if args.members is None:  # BASELINE configs[4]: 64M members in total, sharded
+            args.members, args.members_total = 64_000_000, True
         res = run_vivaldi(args, rank, world)
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -226,11 +249,12 @@ def main():
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline_gossip(args)
+    attach_traffic(workload, res)
     if rank == 0:
         line = {
             "metric": res["metric"], "value": res["value"], "unit": res["unit"], "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": res["dtype"],
+            "higher_is_better": True, "scaling": res.get("scaling", "weak"), "vs_baseline": None, "dtype": res["dtype"],
             "data": "synthetic", "config": res["config"], "roofline": res["roofline"], "cpu_baseline": cpu,
         }
         for k in res:

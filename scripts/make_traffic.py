@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Writes profiles/traffic.json: corrected HBM bytes per launch of each bench's dominant
+kernel, from the PMC passes under gpurun_out/ (see DESIGN.md §Measurement).
+
+gfx950 corrections (measured by experiments/pmc_calib, profiles/r01/pmc_calibration.txt):
+  * coalesced streaming reads are tallied at 1/2 by FETCH_SIZE (4/8/16 B per lane alike);
+  * random gathers of <= 64 B count one 64-B sector each, i.e. the HBM bytes they move;
+  * WRITE_SIZE is exact for streaming stores.
+Vivaldi: the observe kernel's gather share is isolated by the ablation without the
+peer-row gather (experiments/viv_traffic.sh):  traffic = 2*stream + gather + WRITE.
+Gossip (segment + merge): the streamed bytes are modelled (queue state 3 x qcap x 12 B
+and 8 B of register/segment state per receiver, 4 B per record value) and corrected
+(x2); the rest of FETCH is gather:  traffic = FETCH + stream/2 + WRITE."""
+import csv
+import collections
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+RND = sys.argv[1] if len(sys.argv) > 1 else "r01"
+
+
+def last(path, counter, pat, k=5):
+    v = [float(r["Counter_Value"]) * 1024 for r in csv.DictReader(open(path))
+         if r["Counter_Name"] == counter and pat in r["Kernel_Name"]]
+    return sum(v[-k:]) / len(v[-k:])
+
+
+res = {}
+viv = json.loads(open(os.path.join(ROOT, "profiles", RND, "viv_r01_pmc_ablation.txt")).read().strip().splitlines()[-1])
+res["vivaldi"] = {"kernel": "vivaldi_observe_kernel<8,3,20>", "members_per_gpu": 64_000_000,
+                  "traffic_bytes_per_launch": viv["traffic_bytes"],
+                  "fetch_counter": viv["fetch_counter"], "write_counter": viv["write_counter"],
+                  "gather_counter": viv["gather_counter"],
+                  "source": f"profiles/{RND}/viv_r01_pmc_ablation.txt", "method": "2*stream + gather + WRITE"}
+g = os.path.join(OUT, "prof_gossip_r01")
+f_merge = last(f"{g}_fetch/run_counter_collection.csv", "FETCH_SIZE", "merge_kernel")
+w_merge = last(f"{g}_write/run_counter_collection.csv", "WRITE_SIZE", "merge_kernel")
+f_seg = last(f"{g}_fetch/run_counter_collection.csv", "FETCH_SIZE", "segment_kernel")
+w_seg = last(f"{g}_write/run_counter_collection.csv", "WRITE_SIZE", "segment_kernel")
+line = next(json.loads(x) for x in open(f"{g}_trace.log") if x.startswith("{") and '"metric"' in x)
+n = line["config"]["members_per_gpu"]
+records = line["records_per_round_per_gpu"]
+qcap = line["config"]["queue_cap_per_queue"]
+stream_merge = n * (3 * qcap * 12 + 8) + records * 4
+stream_seg = f_seg * 2
+traffic = (f_merge + stream_merge / 2 + w_merge) + (stream_seg + w_seg)
+res["gossip"] = {"kernel": "segment+merge_kernel", "members_per_gpu": n, "traffic_bytes_per_launch": traffic,
+                 "fetch_counter": f_merge + f_seg, "write_counter": w_merge + w_seg,
+                 "stream_bytes_modelled": stream_merge + stream_seg,
+                 "source": f"profiles/{RND}/gossip_r01_summary.md", "method": "FETCH + stream/2 + WRITE"}
+json.dump(res, open(os.path.join(ROOT, "profiles", "traffic.json"), "w"), indent=1)
+print(json.dumps(res, indent=1))
