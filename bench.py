@@ -73,10 +73,15 @@ def barrier(world):
         torch.distributed.barrier()
 
 
+def coll_device():
+    """Tensors for the bench's own small collectives: HBM under RCCL, host under gloo."""
+    return "cpu" if torch.distributed.get_backend() == "gloo" else "cuda"
+
+
 def max_over_ranks(x, world):
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=coll_device())
     torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     return float(t.item())
 
@@ -84,7 +89,7 @@ def max_over_ranks(x, world):
 def sum_over_ranks(x, world):
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=coll_device())
     torch.distributed.all_reduce(t)
     return float(t.item())
 
@@ -108,7 +113,12 @@ def run_vivaldi(args, rank, world):
         ptr, stride = g.table_ptr()
         full = torch.as_tensor(CudaArray(ptr, (n * stride,), "<f8"), device="cuda")
         mine = full[lo * stride: hi * stride].clone()
-        torch.distributed.all_gather_into_tensor(full, mine)
+        if coll_device() == "cpu":  # gloo rehearsal: host-staged
+            h = torch.empty(full.shape, dtype=full.dtype)
+            torch.distributed.all_gather_into_tensor(h, mine.cpu())
+            full.copy_(h)
+        else:
+            torch.distributed.all_gather_into_tensor(full, mine)
 
     # the probe inputs (peer id, observed rtt) of every round are generated up front by
     # the synthetic network and are resident in HBM when the timed region starts
@@ -222,12 +232,19 @@ def main():
     if world != args.gpus and world == 1 and args.gpus > 1:
         print("run multi-GPU through torch.distributed.run (one process per GPU)", file=sys.stderr)
         sys.exit(2)
-    torch.cuda.set_device(local)
+    # RSF_DIST_BACKEND=gloo rehearses the multi-rank path on fewer GPUs than ranks (ranks
+    # share devices, the exchange is host-staged); the driver's runs use RCCL ("nccl")
+    backend = os.environ.get("RSF_DIST_BACKEND", "nccl")
+    dev = local % torch.cuda.device_count() if backend == "gloo" else local
+    torch.cuda.set_device(dev)
     # every engine launch goes to this stream; torch's default stream handle is NULL,
     # which the C ABI would read as "the context's own stream"
     torch.cuda.set_stream(torch.cuda.Stream())
     if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            torch.distributed.init_process_group("gloo")
+        else:
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", dev))
     import ruserf_amd
     try:
         from ruserf_amd import gossip  # noqa: F401

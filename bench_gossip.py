@@ -89,7 +89,8 @@ def run_gossip(args, rank, world):
     err_members = int(np.count_nonzero(st["err"]))
     eng.set_profiling(False)
     if world > 1:
-        t_ = torch.tensor([wall, float(merged), float(err_members)], dtype=torch.float64, device="cuda")
+        dev = "cpu" if torch.distributed.get_backend() == "gloo" else "cuda"
+        t_ = torch.tensor([wall, float(merged), float(err_members)], dtype=torch.float64, device=dev)
         mx = t_.clone()
         torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX)
         torch.distributed.all_reduce(t_)

@@ -72,23 +72,43 @@ class ShardedGossip:
         self.buf = buffers if buffers is not None else EngineBuffers(engine)
         self.dev = self.buf.recv.device
         self.last_in = 0
+        # RCCL ("nccl") moves HBM directly; gloo (the CPU rehearsal backend: several ranks
+        # sharing one GPU, or CPU stand-ins) needs host tensors, so GPU buffers are staged
+        self.stage = dist.get_backend(group) == "gloo" and self.dev.type == "cuda"
+
+    def _all_reduce(self, t):
+        if self.stage:
+            h = t.cpu()
+            dist.all_reduce(h, group=self.group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, group=self.group)
+
+    def _all_to_all(self, out, inp, out_splits=None, in_splits=None):
+        if self.stage:
+            ho = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_to_all_single(ho, inp.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits,
+                                   group=self.group)
+            out.copy_(ho)
+        else:
+            dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits,
+                                   group=self.group)
 
     def round(self, t, ml=None, acts=None):
         eng, buf = self.eng, self.buf
         eng.round_begin(t, ml, acts)
         blk = buf.rumor_block()
         if blk.numel():
-            dist.all_reduce(blk, group=self.group)
+            self._all_reduce(blk)
         counts = eng.round_emit(self.world)
         send_counts = torch.from_numpy(counts.astype(np.int64)).to(self.dev)
         recv_counts = torch.empty_like(send_counts)
-        dist.all_to_all_single(recv_counts, send_counts, group=self.group)
+        self._all_to_all(recv_counts, send_counts)
         rc = recv_counts.cpu().tolist()
         n_in, n_out = int(sum(rc)), int(counts.sum())
         if n_in > buf.recv.numel():
             raise RuntimeError(f"shard {self.rank}: {n_in} records exceed the receive capacity {buf.recv.numel()}")
-        dist.all_to_all_single(buf.recv[:n_in], buf.send[:n_out], output_split_sizes=rc,
-                               input_split_sizes=[int(x) for x in counts], group=self.group)
+        self._all_to_all(buf.recv[:n_in], buf.send[:n_out], rc, [int(x) for x in counts])
         buf.merge(n_in)
         self.last_in = n_in
         return n_out, n_in
