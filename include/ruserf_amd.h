@@ -301,6 +301,15 @@ int rsf_gossip_rumor_block(rsf_gossip* g, void** dev_ptr, uint64_t* bytes);
 int rsf_gossip_round_emit(rsf_gossip* g, uint32_t world, uint64_t* send_counts);
 int rsf_gossip_send_buffer(rsf_gossip* g, void** dev_ptr, uint64_t* capacity_records);
 int rsf_gossip_round_merge(rsf_gossip* g, const uint64_t* recv_dev, uint64_t n_recv);
+/* Same merge without the receive-side sort: recv_dev holds n_runs runs back to back
+ * (run r = what source shard r sent, run_counts[r] records, runs in source-rank order),
+ * each sorted stably by receiver, as rsf_gossip_round_emit produces them.  The
+ * canonical order (receiver, run, position) is rebuilt by counts + scan + an ordered
+ * scatter.  n_runs <= 32.  A record for a receiver outside this shard, or an unsorted
+ * run, is skipped and reported by rsf_gossip_check_runs (ok = 0). */
+int rsf_gossip_round_merge_runs(rsf_gossip* g, const uint64_t* recv_dev, const uint64_t* run_counts,
+                                uint32_t n_runs);
+int rsf_gossip_check_runs(rsf_gossip* g, int* ok);
 
 /* Inspection (host copies; synchronise).  Arrays are over the shard's members. */
 int rsf_gossip_dump_members(rsf_gossip* g, uint64_t* clock, uint64_t* event_clock, uint64_t* query_clock,

@@ -39,6 +39,8 @@ def declare(L):
     sig("rsf_gossip_round_emit", [VP, C.c_uint32, P64])
     sig("rsf_gossip_send_buffer", [VP, C.POINTER(VP), P64])
     sig("rsf_gossip_round_merge", [VP, VP, C.c_uint64])
+    sig("rsf_gossip_round_merge_runs", [VP, VP, C.POINTER(C.c_uint64), C.c_uint32])
+    sig("rsf_gossip_check_runs", [VP, C.POINTER(C.c_int)])
     sig("rsf_gossip_dump_members", [VP, P64, P64, P64, P64, P32, P8])
     sig("rsf_gossip_dump_view", [VP, P64, P8, P8])
     sig("rsf_gossip_dump_queues", [VP, P32, P32, P16, P16, P32])

@@ -780,6 +780,80 @@ __global__ void unpack_kernel(const uint64_t* __restrict__ in, uint64_t n, uint3
   vals[i] = (uint32_t)x;
 }
 
+// ---- multi-GPU receive side without a second sort.  The received buffer is n_runs
+// runs (one per source shard, concatenated in source-rank = ascending-sender order),
+// each already sorted (stably) by receiver.  The canonical merge order is (receiver,
+// run, position in run); it is built from run boundaries, per-(run, receiver) counts,
+// one scan over receivers and an ordered scatter.
+__device__ __forceinline__ uint32_t run_of(const uint64_t* __restrict__ off, uint32_t n_runs, uint64_t i) {
+  uint32_t lo = 0, hi = n_runs;  // largest r with off[r] <= i (an empty run is never chosen)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (off[mid] <= i) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(256) runs_bounds_kernel(const uint64_t* __restrict__ rec, uint64_t n,
+                                                          const uint64_t* __restrict__ off, uint32_t n_runs,
+                                                          uint64_t lo, uint64_t n_loc, uint32_t* __restrict__ rstart,
+                                                          uint32_t* __restrict__ rend,
+                                                          unsigned long long* __restrict__ bad) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = run_of(off, n_runs, i);
+  const uint32_t k = (uint32_t)(rec[i] >> 32);
+  const uint64_t l = (uint64_t)k - lo;
+  const bool first = i == off[r] || (uint32_t)(rec[i - 1] >> 32) != k;
+  const bool last = i + 1 == off[r + 1] || (uint32_t)(rec[i + 1] >> 32) != k;
+  if (l >= n_loc || (i > off[r] && (uint32_t)(rec[i - 1] >> 32) > k)) {  // not ours / run not sorted
+    atomicOr(bad, 1ull);
+    return;
+  }
+  if (first) rstart[r * n_loc + l] = (uint32_t)i;
+  if (last) rend[r * n_loc + l] = (uint32_t)(i + 1);
+}
+
+__global__ void __launch_bounds__(256) runs_base_kernel(uint32_t n_runs, uint64_t n_loc,
+                                                        const uint32_t* __restrict__ rstart,
+                                                        const uint32_t* __restrict__ rend, uint32_t* __restrict__ rbase,
+                                                        uint32_t* __restrict__ total) {
+  const uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= n_loc) return;
+  uint32_t acc = 0;
+  for (uint32_t r = 0; r < n_runs; ++r) {
+    const uint64_t idx = r * n_loc + l;
+    rbase[idx] = acc;
+    acc += rend[idx] - rstart[idx];
+  }
+  total[l] = acc;
+}
+
+__global__ void __launch_bounds__(256) runs_scatter_kernel(const uint64_t* __restrict__ rec, uint64_t n,
+                                                           const uint64_t* __restrict__ off, uint32_t n_runs,
+                                                           uint64_t lo, uint64_t n_loc,
+                                                           const uint32_t* __restrict__ rstart,
+                                                           const uint32_t* __restrict__ rbase,
+                                                           const uint32_t* __restrict__ seg_start,
+                                                           uint32_t* __restrict__ vals) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = run_of(off, n_runs, i);
+  const uint64_t x = rec[i];
+  const uint64_t l = (uint64_t)(uint32_t)(x >> 32) - lo;
+  if (l >= n_loc) return;
+  const uint64_t idx = r * n_loc + l;
+  vals[seg_start[l] + rbase[idx] + (uint32_t)(i - rstart[idx])] = (uint32_t)x;
+}
+
+__global__ void __launch_bounds__(256) seg_end_kernel(uint64_t n_loc, const uint32_t* __restrict__ seg_start,
+                                                      const uint32_t* __restrict__ total,
+                                                      uint32_t* __restrict__ seg_end) {
+  const uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l < n_loc) seg_end[l] = seg_start[l] + total[l];
+}
+
 __global__ void accumulate_kernel(unsigned long long* counters) {
   if (threadIdx.x == 0 && blockIdx.x == 0) counters[60] += counters[0];
 }
@@ -817,6 +891,12 @@ struct rsf_gossip {
   uint32_t cur_round = 0;
   bool merged_from_stage = true;
   uint64_t total_merged_host = 0;  // multi-GPU merges (n_recv known on host)
+  // run-merge tables of rsf_gossip_round_merge_runs: [run_cap][n_loc] u32 x3, [n_loc] u32
+  uint32_t *run_start = nullptr, *run_end = nullptr, *run_base = nullptr, *run_total = nullptr;
+  uint64_t* d_run_off = nullptr;
+  uint32_t run_cap = 0;
+  void* scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
   // phase profiling: marks per round [begin, after begin, after emit, after sort, after merge]
   bool profiling = false;
   static constexpr int kMarks = 5, kMaxProfRounds = 256;
@@ -990,7 +1070,8 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   s.q_rumor, s.q_seq,      s.q_txlen,      s.q_next_seq,  s.eb_ltime, s.eb_cnt,     s.eb_keys,
                   s.qb_ltime, s.qb_cnt,    s.qb_ids,       s.rumors,      g->d_ml,    g->d_acts,    g->stage_key,
                   g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters,
-                  g->sort_tmp};
+                  g->sort_tmp, g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
+                  g->scan_tmp};
   for (void* p : ptrs)
     if (p) hipFree(p);
   g->scratch.release();
@@ -1232,6 +1313,15 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round) {
   return RSF_OK;
 }
 
+static int launch_merge(rsf_gossip* g, const uint32_t* vals) {
+  const GCfg& c = g->c;
+  hipLaunchKernelGGL(merge_kernel, dim3(grid1(c.n_loc, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0, g->stream,
+                     c, g->s, vals, g->seg_start, g->seg_end);
+  RSF_HIP(hipGetLastError());
+  mark(g, 4);
+  return RSF_OK;
+}
+
 static int segment_and_merge(rsf_gossip* g, const uint32_t* keys, const uint32_t* vals, uint64_t n) {
   const GCfg& c = g->c;
   hipStream_t st = g->stream;
@@ -1241,11 +1331,7 @@ static int segment_and_merge(rsf_gossip* g, const uint32_t* keys, const uint32_t
     hipLaunchKernelGGL(segment_kernel, dim3(grid1(n)), dim3(256), 0, st, keys, n, c.lo, g->seg_start, g->seg_end,
                        g->d_counters + 63);
   }
-  hipLaunchKernelGGL(merge_kernel, dim3(grid1(c.n_loc, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0, st, c,
-                     g->s, vals, g->seg_start, g->seg_end);
-  RSF_HIP(hipGetLastError());
-  mark(g, 4);
-  return RSF_OK;
+  return launch_merge(g, vals);
 }
 
 extern "C" {
@@ -1263,7 +1349,7 @@ int rsf_gossip_round(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml, uint
 }
 
 int rsf_gossip_round_emit(rsf_gossip* g, uint32_t world, uint64_t* send_counts) {
-  if (!g || !send_counts || world == 0 || world > 62) return gerr("bad argument");
+  if (!g || !send_counts || world == 0 || world > 32) return gerr("bad argument");  // d_counters[1..world+1]
   const GCfg& c = g->c;
   if (c.N % world || c.n_loc != c.N / world) return gerr("shards must be equal contiguous ranges of n_members");
   RSF_HIP(hipSetDevice(g->device));
@@ -1322,6 +1408,73 @@ int rsf_gossip_round_merge(rsf_gossip* g, const uint64_t* recv, uint64_t n_recv)
     hipEventRecord(g->ev[g->prof_rounds][3], g->stream);  // exchange time lands in the sort slot
   }
   return segment_and_merge(g, g->sort_key, g->sort_val, n_recv);
+}
+
+int rsf_gossip_round_merge_runs(rsf_gossip* g, const uint64_t* recv, const uint64_t* run_counts, uint32_t n_runs) {
+  if (!g || (n_runs && !run_counts) || n_runs > 32) return gerr("bad argument");
+  const GCfg& c = g->c;
+  uint64_t off[63];
+  off[0] = 0;
+  for (uint32_t r = 0; r < n_runs; ++r) off[r + 1] = off[r] + run_counts[r];
+  const uint64_t n = n_runs ? off[n_runs] : 0;
+  if (n && !recv) return gerr("null argument");
+  if (n > g->recv_cap) return rsf::set_error(RSF_ERR_OVERFLOW, "receive buffer capacity exceeded");
+  RSF_HIP(hipSetDevice(g->device));
+  hipStream_t st = g->stream;
+  if (n_runs > g->run_cap) {
+    for (void* p : {(void*)g->run_start, (void*)g->run_end, (void*)g->run_base})
+      if (p) hipFree(p);
+    g->run_start = g->run_end = g->run_base = nullptr;
+    g->run_cap = 0;
+    const size_t tab = (size_t)n_runs * c.n_loc * 4;
+    int rc;
+    if ((rc = rsf::dmalloc((void**)&g->run_start, tab)) || (rc = rsf::dmalloc((void**)&g->run_end, tab)) ||
+        (rc = rsf::dmalloc((void**)&g->run_base, tab)))
+      return rc;
+    g->run_cap = n_runs;
+  }
+  if (!g->run_total) {
+    int rc;
+    if ((rc = rsf::dmalloc((void**)&g->run_total, c.n_loc * 4)) || (rc = rsf::dmalloc((void**)&g->d_run_off, 63 * 8)))
+      return rc;
+    size_t tb = 0;
+    RSF_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, g->run_total, g->seg_start, (int)c.n_loc, st));
+    if ((rc = rsf::dmalloc(&g->scan_tmp, tb))) return rc;
+    g->scan_tmp_bytes = tb;
+  }
+  RSF_HIP(hipMemcpyAsync(g->d_run_off, off, (n_runs + 1) * 8, hipMemcpyHostToDevice, st));
+  const size_t tab = (size_t)n_runs * c.n_loc * 4;
+  RSF_HIP(hipMemsetAsync(g->run_start, 0, tab, st));
+  RSF_HIP(hipMemsetAsync(g->run_end, 0, tab, st));
+  RSF_HIP(hipMemsetAsync(g->d_counters + 62, 0, 8, st));
+  if (n)
+    hipLaunchKernelGGL(runs_bounds_kernel, dim3(grid1(n)), dim3(256), 0, st, recv, n, g->d_run_off, n_runs, c.lo,
+                       c.n_loc, g->run_start, g->run_end, g->d_counters + 62);
+  hipLaunchKernelGGL(runs_base_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, n_runs, c.n_loc, g->run_start,
+                     g->run_end, g->run_base, g->run_total);
+  size_t tb = g->scan_tmp_bytes;
+  RSF_HIP(hipcub::DeviceScan::ExclusiveSum(g->scan_tmp, tb, g->run_total, g->seg_start, (int)c.n_loc, st));
+  if (n)
+    hipLaunchKernelGGL(runs_scatter_kernel, dim3(grid1(n)), dim3(256), 0, st, recv, n, g->d_run_off, n_runs, c.lo,
+                       c.n_loc, g->run_start, g->run_base, g->seg_start, g->sort_val);
+  hipLaunchKernelGGL(seg_end_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, c.n_loc, g->seg_start, g->run_total,
+                     g->seg_end);
+  RSF_HIP(hipGetLastError());
+  g->last_merged = n;
+  g->total_merged_host += n;
+  if (g->profiling && g->prof_rounds < rsf_gossip::kMaxProfRounds)
+    hipEventRecord(g->ev[g->prof_rounds][3], g->stream);  // exchange time lands in the sort slot
+  return launch_merge(g, g->sort_val);
+}
+
+int rsf_gossip_check_runs(rsf_gossip* g, int* ok) {
+  if (!g || !ok) return gerr("null argument");
+  unsigned long long bad = 0;
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemcpyAsync(&bad, g->d_counters + 62, 8, hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  *ok = bad == 0;
+  return RSF_OK;
 }
 
 int rsf_gossip_dump_members(rsf_gossip* g, uint64_t* clock, uint64_t* ec, uint64_t* qc, uint64_t* digest, uint32_t* err,

@@ -12,8 +12,10 @@ Per round:
   4. all-to-all    — record counts, then the packed (receiver << 32 | rumor)
                      records; received chunks are concatenated in source-rank
                      order = ascending sender id
-  5. round_merge   — stable sort by receiver keeps (sender, position) order, so
-                     the merge is the same canonical order as on one GPU
+  5. round_merge_runs — the received runs (one per source, each receiver-sorted)
+                     are interleaved into (receiver, source rank, position) order by
+                     counts + scan + an ordered scatter — no second sort — which is
+                     the same canonical order as on one GPU
 
 The driver is generic over the engine object (`GossipEngine` on HIP; the
 gloo tests substitute a CPU stand-in that exercises only the routing).
@@ -54,8 +56,8 @@ class EngineBuffers:
         ptr, nbytes = self.eng.rumor_block()
         return hbm_tensor(ptr, nbytes // 8)
 
-    def merge(self, n_recv):
-        self.eng.round_merge(self.recv.data_ptr(), n_recv)
+    def merge(self, n_recv, run_counts):
+        self.eng.round_merge_runs(self.recv.data_ptr(), run_counts)
 
 
 class ShardedGossip:
@@ -109,6 +111,6 @@ class ShardedGossip:
         if n_in > buf.recv.numel():
             raise RuntimeError(f"shard {self.rank}: {n_in} records exceed the receive capacity {buf.recv.numel()}")
         self._all_to_all(buf.recv[:n_in], buf.send[:n_out], rc, [int(x) for x in counts])
-        buf.merge(n_in)
+        buf.merge(n_in, rc)
         self.last_in = n_in
         return n_out, n_in

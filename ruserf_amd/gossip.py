@@ -170,6 +170,16 @@ class GossipEngine:
     def round_merge(self, recv_ptr, n_recv):
         check(lib().rsf_gossip_round_merge(self._h, C.c_void_p(recv_ptr), n_recv))
 
+    def round_merge_runs(self, recv_ptr, run_counts):
+        """Merge the received runs (one per source shard, each receiver-sorted) without a sort."""
+        rc = np.ascontiguousarray(run_counts, dtype=np.uint64)
+        check(lib().rsf_gossip_round_merge_runs(self._h, C.c_void_p(recv_ptr), ptr(rc, C.c_uint64), len(rc)))
+
+    def runs_ok(self):
+        ok = C.c_int()
+        check(lib().rsf_gossip_check_runs(self._h, C.byref(ok)))
+        return bool(ok.value)
+
     # ---- inspection
     def members(self):
         n = self.n_loc

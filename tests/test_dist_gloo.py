@@ -56,7 +56,7 @@ class FakeBuffers:
     def rumor_block(self):
         return self.eng.block
 
-    def merge(self, n):
+    def merge(self, n, run_counts=None):
         self.eng.received.append(self.recv[:n].clone().numpy())
 
 

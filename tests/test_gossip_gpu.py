@@ -169,10 +169,12 @@ def test_large_round_properties():
     assert np.array_equal(digests[0][0], digests[1][0]) and digests[0][1] == digests[1][1]
 
 
-def test_two_shards_equal_one_context():
+@pytest.mark.parametrize("runs", [False, True, "with_empty_runs"])
+def test_two_shards_equal_one_context(runs):
     """The multi-GPU split (round_begin / rumor-block sum / round_emit /
-    all-to-all / round_merge) with two shard contexts on one GPU and the
-    exchange done by hand must reproduce the single-context round exactly."""
+    all-to-all / round_merge or round_merge_runs) with two shard contexts on one
+    GPU and the exchange done by hand must reproduce the single-context round
+    exactly."""
     import torch
     from ruserf_amd.dist import hbm_tensor
     n, rounds = 4000, 10
@@ -207,7 +209,14 @@ def test_two_shards_equal_one_context():
                 off = int(counts[src][:dst].sum())
                 parts.append(sends[src][off: off + int(counts[src][dst])])
             recv = torch.cat(parts).contiguous()
-            e.round_merge(recv.data_ptr(), recv.numel())
+            if runs:
+                counts_r = [p.numel() for p in parts]
+                if runs == "with_empty_runs":  # sources that sent nothing change nothing
+                    counts_r = [0] + counts_r[:1] + [0, 0] + counts_r[1:] + [0]
+                e.round_merge_runs(recv.data_ptr(), counts_r)
+                assert e.runs_ok()
+            else:
+                e.round_merge(recv.data_ptr(), recv.numel())
             stream.synchronize()
         torch.cuda.synchronize()
         full = H.normalize_queues(H.engine_state(one))
