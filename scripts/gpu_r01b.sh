@@ -1,0 +1,6 @@
+set -o pipefail
+S=scripts/gpu_step.sh
+bash $S pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread && \
+bash $S smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" && \
+bash $S bench_gossip 400 python -u bench.py && \
+bash $S bench_vivaldi 400 python -u bench.py --workload vivaldi
