@@ -182,6 +182,64 @@ __device__ __forceinline__ void q_insert_wave(const GCfg& c, QRegs& Q, uint32_t 
   }
 }
 
+// Batched insert of new items (transmits 0) into a sorted queue, equivalent to
+// q_insert_wave on each of them in lane order (seq = seq0, seq0+1, ...):
+// inserting into a bounded sorted queue and pruning the largest key keeps the
+// qcap smallest keys of everything inserted so far, so the result is the qcap
+// smallest of (queue items U new items).  Keys are distinct (seqs are unique).
+//   existing item i (sorted lane i) lands at i + #(new keys below it);
+//   new item j lands at #(existing keys below it) + #(new keys below it).
+// One pass over the new items counts both, then every slot PULLS its item
+// (ds_bpermute): slots taken by new items are marked in a 64-bit mask, the
+// others take the existing items in order.
+__device__ __forceinline__ void q_insert_batch(const GCfg& c, QRegs& Q, uint32_t lane, bool ins, uint32_t rid,
+                                               uint32_t len, uint32_t seq0, uint64_t newmask) {
+  const bool valid = lane < c.qcap;
+  const bool live = valid && Q.r != kEmpty;
+  const uint32_t n_live = (uint32_t)__popcll(__ballot(live));
+  const uint32_t myseq = seq0 + (uint32_t)__popcll(newmask & below_mask(lane));
+  const uint64_t nkey = ins ? tlq_key(0, len, myseq) : ~0ull;
+  const uint64_t ekey = live ? tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq) : ~0ull;
+  uint32_t n_rank = 0, e_less = 0;
+  uint64_t mm = newmask;
+  while (mm) {
+    const int k = __ffsll((long long)mm) - 1;
+    mm &= mm - 1;
+    const uint64_t bk = shfl_u64(nkey, k);
+    const bool eb = live && bk < ekey;
+    n_rank += (ins && bk < nkey) ? 1u : 0u;
+    const uint32_t el = n_live - (uint32_t)__popcll(__ballot(eb));
+    e_less = (int)lane == k ? el : e_less;
+  }
+  const uint32_t pos_n = e_less + n_rank;
+  // destinations of the surviving new items and, per destination, its source lane
+  uint64_t dm = 0;
+  uint32_t srcn = 0;
+  mm = __ballot(ins && pos_n < c.qcap);
+  while (mm) {
+    const int k = __ffsll((long long)mm) - 1;
+    mm &= mm - 1;
+    const uint32_t d = shfl_u32(pos_n, k);
+    dm |= 1ull << d;
+    srcn = lane == d ? (uint32_t)k : srcn;
+  }
+  const bool is_new = (dm >> lane) & 1;
+  const uint32_t ei = lane - (uint32_t)__popcll(dm & below_mask(lane));
+  const bool is_old = !is_new && valid && ei < n_live;
+  const int a_new = (int)(srcn * 4), a_old = (int)((is_old ? ei : lane) * 4);
+  const uint32_t nr = (uint32_t)__builtin_amdgcn_ds_bpermute(a_new, (int)rid);
+  const uint32_t ns = (uint32_t)__builtin_amdgcn_ds_bpermute(a_new, (int)myseq);
+  const uint32_t nl = (uint32_t)__builtin_amdgcn_ds_bpermute(a_new, (int)len);
+  const uint32_t orr = (uint32_t)__builtin_amdgcn_ds_bpermute(a_old, (int)Q.r);
+  const uint32_t os = (uint32_t)__builtin_amdgcn_ds_bpermute(a_old, (int)Q.sq);
+  const uint32_t ot = (uint32_t)__builtin_amdgcn_ds_bpermute(a_old, (int)Q.tl);
+  if (valid) {
+    Q.r = is_new ? nr : (is_old ? orr : kEmpty);
+    Q.sq = is_new ? ns : (is_old ? os : 0u);
+    Q.tl = is_new ? (nl << 16) : (is_old ? ot : 0u);
+  }
+}
+
 // one get_broadcasts call on a sorted register-resident queue; returns bytes used.
 // The lowest unpicked lane that fits IS the reference's pick (lowest transmits, then
 // longest fitting, then newest): every skipped lower lane did not fit and never will.
@@ -414,24 +472,34 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
 __global__ void __launch_bounds__(256) emit_kernel(GCfg c, GState s, uint32_t round, uint32_t* __restrict__ stage_key,
                                                    uint32_t* __restrict__ stage_val) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x / kWave);
+  const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   if (l >= c.n_loc) return;
   const uint32_t m = (uint32_t)(c.lo + l);
-  if (!s.alive[m]) return;
+  // Independent loads first, in one round trip: own liveness, the three queue
+  // heads (sorted queues: a queue is empty iff its slot 0 is free) and the
+  // liveness of the first 64 Philox peer candidates.
+  const bool alive_m = s.alive[m] != 0;
+  const uint32_t head = lane < 3 ? s.q_rumor[(l * 3 + lane) * c.qcap] : kEmpty;
+  const uint32_t attempts = 64 * c.fanout;
+  auto candidate = [&](uint32_t a, uint32_t& p) -> bool {
+    p = 0;
+    if (a >= attempts) return false;
+    u32x4 o = philox4x32_10(a, kPurposePeer << 24, m, round, c.k0, c.k1);
+    p = mulhi32(o.x, (uint32_t)(c.N - 1));
+    if (p >= m) p++;
+    return s.alive[p] != 0;
+  };
+  uint32_t p_first;
+  const bool ok_first = candidate(lane, p_first);
+  asm volatile("" ::: "memory");  // keep the loads above the exit (compiler barrier only)
+  if (!alive_m) return;
   // kRandomNodes model: attempts a = 0,1,2,... in order, live, distinct, != m
   uint32_t peers[8];
   uint32_t np = 0;
-  const uint32_t attempts = 64 * c.fanout;
   for (uint32_t b0 = 0; b0 < attempts && np < c.fanout; b0 += kWave) {
-    uint32_t a = b0 + lane;
-    uint32_t p = 0;
-    bool ok = false;
-    if (a < attempts) {
-      u32x4 o = philox4x32_10(a, kPurposePeer << 24, m, round, c.k0, c.k1);
-      p = mulhi32(o.x, (uint32_t)(c.N - 1));
-      if (p >= m) p++;
-      ok = s.alive[p] != 0;
-    }
+    uint32_t p = p_first;
+    bool ok = ok_first;
+    if (b0) ok = candidate(b0 + lane, p);
     uint64_t mask = __ballot(ok);
     while (mask && np < c.fanout) {
       int li = __ffsll((long long)mask) - 1;
@@ -442,8 +510,6 @@ __global__ void __launch_bounds__(256) emit_kernel(GCfg c, GState s, uint32_t ro
       if (!dup) peers[np++] = cand;
     }
   }
-  // sorted queues: a queue is empty iff its slot 0 is free -> one 4-byte probe each
-  const uint32_t head = lane < 3 ? s.q_rumor[(l * 3 + lane) * c.qcap] : kEmpty;
   const bool ne0 = shfl_u32(head, 0) != kEmpty, ne1 = shfl_u32(head, 1) != kEmpty,
              ne2 = shfl_u32(head, 2) != kEmpty;
   if (np == 0 || !(ne0 || ne1 || ne2)) return;
@@ -468,15 +534,32 @@ __global__ void __launch_bounds__(256) emit_kernel(GCfg c, GState s, uint32_t ro
   if (err && lane == 0) s.err[l] |= err;
 }
 
+// Record decoration: what merge_kernel needs to address the view entry (the
+// subject) and to pick the queue, written beside the sorted rumor ids so the
+// merge issues its view-entry load in the same round trip as the rumor-body
+// load instead of after it.
+constexpr uint32_t kDecQuery = 0xFFFFFFFEu, kDecEvent = 0xFFFFFFFDu, kDecViewMax = 0xFFFFFFF0u;
+__device__ __forceinline__ uint32_t decorate(const rsf_rumor* __restrict__ rumors, uint32_t rid) {
+  const rsf_rumor* p = rumors + rid;
+  const uint8_t t = p->type;
+  if (t == RSF_MSG_QUERY) return kDecQuery;
+  if (t == RSF_MSG_USER_EVENT) return kDecEvent;
+  return p->subject;
+}
+
+// segment bounds per receiver + record decoration (keys == nullptr: decoration only)
 __global__ void __launch_bounds__(256) segment_kernel(const uint32_t* __restrict__ keys, uint64_t n, uint64_t lo,
                                                       uint32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_end,
-                                                      unsigned long long* /*unused*/) {
+                                                      const uint32_t* __restrict__ vals,
+                                                      const rsf_rumor* __restrict__ rumors,
+                                                      uint32_t* __restrict__ dec) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t k = keys[i];
   if (k == kSentinel) return;
   if (i == 0 || keys[i - 1] != k) seg_start[k - lo] = (uint32_t)i;
   if (i + 1 == n || keys[i + 1] != k) seg_end[k - lo] = (uint32_t)(i + 1);
+  if (dec) dec[i] = decorate(rumors, vals[i]);
 }
 
 __global__ void __launch_bounds__(256) first_sentinel_kernel(const uint32_t* __restrict__ keys, uint64_t n,
@@ -498,7 +581,7 @@ __global__ void __launch_bounds__(256) first_sentinel_kernel(const uint32_t* __r
 //     re-queues are then applied serially in record order.
 // User events / queries (dedup rings in HBM) run serially in lane 0.
 #ifndef RSF_MERGE_WAVES
-#define RSF_MERGE_WAVES 5  // min waves/SIMD for merge_kernel (register cap)
+#define RSF_MERGE_WAVES 8  // min waves/SIMD for merge_kernel (register cap; 8 measured fastest)
 #endif
 #ifndef RSF_MERGE_PROF
 #define RSF_MERGE_PROF 0  // diagnostic build: per-phase shader-clock totals of merge_kernel
@@ -515,23 +598,45 @@ __device__ unsigned long long g_merge_prof[8];
 #ifndef RSF_MERGE_HEADSKIP
 #define RSF_MERGE_HEADSKIP 0  // 1: skip loading a queue whose slot 0 is free (measured slower: spills + a dependent probe)
 #endif
+#ifndef RSF_MERGE_DEC
+#define RSF_MERGE_DEC 1  // 1: view-entry loads addressed from the record decoration (one round trip less)
+#endif
 #ifndef RSF_MERGE_EAGER
-#define RSF_MERGE_EAGER 1  // 0: load the query/event queues only when a chunk needs them
+#define RSF_MERGE_EAGER (!RSF_MERGE_DEC)  // 0: load the query/event queues only when a chunk needs them
+#endif
+#ifndef RSF_MERGE_BATCH
+#define RSF_MERGE_BATCH 1  // 1: a chunk's intent re-queues go in with one q_insert_batch
+#endif
+#ifndef RSF_MERGE_HOIST
+#define RSF_MERGE_HOIST 1  // 1: queue/register loads issued before the segment-bounds check
+#endif
+#ifndef RSF_MERGE_UNIFORM
+#define RSF_MERGE_UNIFORM 1  // 1: the wave's member index is made scalar (readfirstlane)
 #endif
 __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GState s, const uint32_t* __restrict__ vals,
+                                                    const uint32_t* __restrict__ dec,
                                                     const uint32_t* __restrict__ seg_start,
                                                     const uint32_t* __restrict__ seg_end) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
+#if RSF_MERGE_UNIFORM
+  const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+#else
   const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x / kWave);
+#endif
   if (l >= c.n_loc) return;
   const uint32_t m = (uint32_t)(c.lo + l);
   MPROF_T(t_start);
   const uint32_t st = seg_start[l], en = seg_end[l];
-  if (st >= en || !s.alive[m]) return;
-  // queues are loaded on first need (the record types of a chunk say which) and
-  // written back only if something was inserted
+  const bool skip = st >= en || !s.alive[m];
+  if (!RSF_MERGE_HOIST && skip) return;
+  // The intent queue and the member's registers do not depend on the segment
+  // bounds: with RSF_MERGE_HOIST they are issued in the same round trip (the
+  // 5% of receivers without records pay one wasted queue read for it).
+  // Query/event queues are loaded on first need and every queue is written
+  // back only if something was inserted.
   QRegs Q0{kEmpty, 0, 0}, Q1{kEmpty, 0, 0}, Q2{kEmpty, 0, 0};
   bool ld0 = true, ld1 = RSF_MERGE_EAGER, ld2 = RSF_MERGE_EAGER, d0 = false, d1 = false, d2 = false;
+  (void)ld0;
   q_load(c, s, l, 0, lane, Q0);  // intents are the common case: load with the first prefetch
   if (RSF_MERGE_EAGER) {
     // a sorted queue is empty iff its slot 0 is free (wave-uniform probe): skip the load then
@@ -541,6 +646,10 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
   uint32_t nseq0 = s.q_next_seq[l * 3 + 0], nseq1 = s.q_next_seq[l * 3 + 1], nseq2 = s.q_next_seq[l * 3 + 2];
   MRegs r;
   load_regs(s, l, r);
+  if (RSF_MERGE_HOIST) {
+    asm volatile("" ::: "memory");  // keep the loads above the exit (compiler barrier only)
+    if (skip) return;
+  }
   ViewE* vrow = s.view + l * c.S;
   MPROF_T(t_setup);
   MPROF_ADD(0, t_start, t_setup);
@@ -549,6 +658,25 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
     const uint32_t cnt = min((uint32_t)kWave, en - base);
     const bool valid = lane < cnt;
     const uint32_t rid = valid ? vals[base + lane] : 0;
+#if RSF_MERGE_DEC
+    // decoration (same round trip as the rumor ids): subject of an intent, or the
+    // queue of an event / query; invalid lanes read as neither
+    const uint32_t dsub = valid ? dec[base + lane] : kEmpty;
+    const bool is_view = dsub < kDecViewMax;
+    if (!ld1 && __ballot(dsub == kDecQuery)) {
+      q_load(c, s, l, 1, lane, Q1);
+      ld1 = true;
+    }
+    if (!ld2 && __ballot(dsub == kDecEvent)) {
+      q_load(c, s, l, 2, lane, Q2);
+      ld2 = true;
+    }
+    rsf_rumor ru{};
+    if (valid) ru = s.rumors[rid];
+    ViewE pre{};
+    if (is_view) pre = vrow[dsub];  // issued beside the rumor-body load
+    const uint32_t my_subj = is_view ? dsub : 0xFFFFFFFFu;
+#else
     rsf_rumor ru{};
     if (valid) ru = s.rumors[rid];
     const bool is_view = valid && (ru.type == RSF_MSG_JOIN || ru.type == RSF_MSG_LEAVE);
@@ -567,6 +695,7 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
     ViewE pre{};
     if (is_view) pre = vrow[ru.subject];
     const uint32_t my_subj = is_view ? ru.subject : 0xFFFFFFFFu;
+#endif
     // chains: previous / next record of the same subject in this chunk
     int prev = -1, next = -1;
     {
@@ -628,8 +757,21 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
     if (chunk_max > r.clock) r.clock = chunk_max;
     MPROF_T(t_c2);
     MPROF_ADD(2, t_c1, t_c2);
+#if RSF_MERGE_BATCH
+    // intent re-queues of the chunk in one batch (the intent queue takes nothing else)
+    const bool ins = is_view && (f & RSF_F_REBROADCAST);
+    const uint64_t newmask = __ballot(ins);
+    if (newmask) {
+      q_insert_batch(c, Q0, lane, ins, rid, ru.msg_len, nseq0, newmask);
+      nseq0 += (uint32_t)__popcll(newmask);
+      d0 = true;
+    }
+    // serial part, record order: events/queries (lane 0 handlers), digest, refutes
+    const uint64_t serial = __ballot(valid && (!is_view || (f & (RSF_F_MEMBER_EVENT | RSF_F_REFUTE))));
+#else
     // serial part, record order: events/queries (lane 0 handlers), digest, refutes, re-queues
     const uint64_t serial = __ballot(valid && (!is_view || f != 0));
+#endif
     uint64_t mm = serial;
     while (mm) {
       const int i = __ffsll((long long)mm) - 1;
@@ -662,8 +804,10 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
       if (fi & RSF_F_REBROADCAST) {
         const uint32_t q = queue_of(type), rid_i = shfl_u32(rid, i), mlen = tf >> 16;
         if (q == kQIntent) {
-          q_insert_wave(c, Q0, lane, rid_i, mlen, nseq0++);
-          d0 = true;
+          if (!RSF_MERGE_BATCH) {
+            q_insert_wave(c, Q0, lane, rid_i, mlen, nseq0++);
+            d0 = true;
+          }
         } else if (q == kQQuery) {
           q_insert_wave(c, Q1, lane, rid_i, mlen, nseq1++);
           d1 = true;
@@ -836,7 +980,9 @@ __global__ void __launch_bounds__(256) runs_scatter_kernel(const uint64_t* __res
                                                            const uint32_t* __restrict__ rstart,
                                                            const uint32_t* __restrict__ rbase,
                                                            const uint32_t* __restrict__ seg_start,
-                                                           uint32_t* __restrict__ vals) {
+                                                           uint32_t* __restrict__ vals,
+                                                           const rsf_rumor* __restrict__ rumors,
+                                                           uint32_t* __restrict__ dec) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t r = run_of(off, n_runs, i);
@@ -844,7 +990,9 @@ __global__ void __launch_bounds__(256) runs_scatter_kernel(const uint64_t* __res
   const uint64_t l = (uint64_t)(uint32_t)(x >> 32) - lo;
   if (l >= n_loc) return;
   const uint64_t idx = r * n_loc + l;
-  vals[seg_start[l] + rbase[idx] + (uint32_t)(i - rstart[idx])] = (uint32_t)x;
+  const uint32_t pos = seg_start[l] + rbase[idx] + (uint32_t)(i - rstart[idx]);
+  vals[pos] = (uint32_t)x;
+  dec[pos] = decorate(rumors, (uint32_t)x);
 }
 
 __global__ void __launch_bounds__(256) seg_end_kernel(uint64_t n_loc, const uint32_t* __restrict__ seg_start,
@@ -882,6 +1030,7 @@ struct rsf_gossip {
   uint64_t stage_cap = 0, recv_cap = 0;
   uint32_t *stage_key = nullptr, *stage_val = nullptr, *sort_key = nullptr, *sort_val = nullptr;
   uint32_t *seg_start = nullptr, *seg_end = nullptr;
+  uint32_t* rec_dec = nullptr;  // record decoration beside sort_val (segment_kernel / runs_scatter_kernel)
   uint64_t* send_buf = nullptr;
   unsigned long long* d_counters = nullptr;  // [0] n_valid, [1..] shard bounds
   void* sort_tmp = nullptr;
@@ -1015,7 +1164,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   g->recv_cap = g->stage_cap + g->stage_cap / 2 + 4096;
   const uint64_t pipe = std::max(g->stage_cap, g->recv_cap);
   if (GA(g->stage_key, pipe * 4) || GA(g->stage_val, pipe * 4) || GA(g->sort_key, pipe * 4) ||
-      GA(g->sort_val, pipe * 4) || GA(g->seg_start, n * 4) || GA(g->seg_end, n * 4) || GA(g->send_buf, pipe * 8) ||
+      GA(g->sort_val, pipe * 4) || GA(g->seg_start, n * 4) || GA(g->seg_end, n * 4) || GA(g->send_buf, pipe * 8) || GA(g->rec_dec, pipe * 4) ||
       GA(g->d_counters, 64 * 8))
     return fail(rc);
 #undef GA
@@ -1069,7 +1218,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   s.alive,  s.serf_state,  s.member_subj,  s.subj_member, s.refute_cnt, s.refute_ltime, s.view,
                   s.q_rumor, s.q_seq,      s.q_txlen,      s.q_next_seq,  s.eb_ltime, s.eb_cnt,     s.eb_keys,
                   s.qb_ltime, s.qb_cnt,    s.qb_ids,       s.rumors,      g->d_ml,    g->d_acts,    g->stage_key,
-                  g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters,
+                  g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters, g->rec_dec,
                   g->sort_tmp, g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
                   g->scan_tmp};
   for (void* p : ptrs)
@@ -1224,7 +1373,7 @@ int rsf_gossip_apply_batch(rsf_gossip* g, const rsf_msg* msgs, uint64_t n, int32
   RSF_HIP(hipMemsetAsync(g->seg_start, 0, c.n_loc * 4, g->stream));
   RSF_HIP(hipMemsetAsync(g->seg_end, 0, c.n_loc * 4, g->stream));
   hipLaunchKernelGGL(segment_kernel, dim3(grid1(n)), dim3(256), 0, g->stream, (const uint32_t*)d[2], n, 0ull,
-                     g->seg_start, g->seg_end, g->d_counters);
+                     g->seg_start, g->seg_end, (const uint32_t*)nullptr, (const rsf_rumor*)nullptr, (uint32_t*)nullptr);
   hipLaunchKernelGGL(apply_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, g->stream, c, g->s, (const rsf_msg*)d[0],
                      (const uint32_t*)d[4], g->seg_start, g->seg_end, (int32_t*)d[5], (uint64_t*)d[6]);
   RSF_HIP(hipGetLastError());
@@ -1316,7 +1465,7 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round) {
 static int launch_merge(rsf_gossip* g, const uint32_t* vals) {
   const GCfg& c = g->c;
   hipLaunchKernelGGL(merge_kernel, dim3(grid1(c.n_loc, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0, g->stream,
-                     c, g->s, vals, g->seg_start, g->seg_end);
+                     c, g->s, vals, (const uint32_t*)g->rec_dec, g->seg_start, g->seg_end);
   RSF_HIP(hipGetLastError());
   mark(g, 4);
   return RSF_OK;
@@ -1329,7 +1478,7 @@ static int segment_and_merge(rsf_gossip* g, const uint32_t* keys, const uint32_t
   RSF_HIP(hipMemsetAsync(g->seg_end, 0, c.n_loc * 4, st));
   if (n) {
     hipLaunchKernelGGL(segment_kernel, dim3(grid1(n)), dim3(256), 0, st, keys, n, c.lo, g->seg_start, g->seg_end,
-                       g->d_counters + 63);
+                       vals, (const rsf_rumor*)g->s.rumors, g->rec_dec);
   }
   return launch_merge(g, vals);
 }
@@ -1456,7 +1605,8 @@ int rsf_gossip_round_merge_runs(rsf_gossip* g, const uint64_t* recv, const uint6
   RSF_HIP(hipcub::DeviceScan::ExclusiveSum(g->scan_tmp, tb, g->run_total, g->seg_start, (int)c.n_loc, st));
   if (n)
     hipLaunchKernelGGL(runs_scatter_kernel, dim3(grid1(n)), dim3(256), 0, st, recv, n, g->d_run_off, n_runs, c.lo,
-                       c.n_loc, g->run_start, g->run_base, g->seg_start, g->sort_val);
+                       c.n_loc, g->run_start, g->run_base, g->seg_start, g->sort_val, (const rsf_rumor*)g->s.rumors,
+                       g->rec_dec);
   hipLaunchKernelGGL(seg_end_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, c.n_loc, g->seg_start, g->run_total,
                      g->seg_end);
   RSF_HIP(hipGetLastError());
