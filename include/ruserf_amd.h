@@ -311,6 +311,29 @@ int rsf_gossip_round_merge_runs(rsf_gossip* g, const uint64_t* recv_dev, const u
                                 uint32_t n_runs);
 int rsf_gossip_check_runs(rsf_gossip* g, int* ok);
 
+/* ---- push/pull anti-entropy (SerfDelegate::local_state / merge_remote_state,
+ * core/src/serf/delegate.rs:376-554) ---------------------------------------
+ * Receiver `receiver` merges the local_state of `sender`: the three Lamport
+ * clocks (witnessed minus one), status_ltimes (its KNOWN view entries, as
+ * artificial join intents), left_members (KNOWN entries with status Left, as
+ * leave intents one past their status time) and its user-event buffer (as
+ * handle_user_event with cc = false).  Every sender's state is snapshotted
+ * before any merge of the batch (memberlist sends its local state before it
+ * merges the remote one), so a symmetric exchange is the pair (a<-b, b<-a) in
+ * one batch.  Canonical order inside one merge: left members in subject-slot
+ * order, then the other entries in slot order, then the buffer in index order
+ * (the reference iterates an IndexSet and a HashMap).  Both members must be in
+ * the shard; receivers of one batch must be distinct; dead receivers skip. */
+typedef struct rsf_pp_pair {
+  uint32_t receiver, sender;
+} rsf_pp_pair;
+#define RSF_PP_JOIN 1               /* merge_remote_state(is_join = true) */
+#define RSF_PP_EVENT_JOIN_IGNORE 2  /* Options::event_join_ignore (min_time = event_ltime on a join) */
+/* host pairs; validated; synchronises */
+int rsf_gossip_push_pull(rsf_gossip* g, const rsf_pp_pair* pairs, uint64_t n, uint32_t flags);
+/* device pairs, asynchronous, not validated (the throughput path) */
+int rsf_gossip_push_pull_device(rsf_gossip* g, const rsf_pp_pair* pairs_dev, uint64_t n, uint32_t flags);
+
 /* Inspection (host copies; synchronise).  Arrays are over the shard's members. */
 int rsf_gossip_dump_members(rsf_gossip* g, uint64_t* clock, uint64_t* event_clock, uint64_t* query_clock,
                             uint64_t* digest, uint32_t* err, uint8_t* serf_state);

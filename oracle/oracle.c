@@ -1036,6 +1036,69 @@ int orc_world_round(orc_world* w, uint32_t round, const orc_ml_event* ml, uint32
 }
 
 /* ------------------------------------------------------------------------ */
+/* push/pull anti-entropy  core/src/serf/delegate.rs:422-554                */
+int orc_merge_remote_state(orc_world* w, uint32_t r, const orc_pp_state* pp, int is_join, int event_join_ignore) {
+  if (!w->alive[r]) return 0;
+  /* witness the Lamport clocks first, minus one (delegate.rs:459-475) */
+  if (pp->clock > 0) orc_clock_witness(&w->clock[r], pp->clock - 1);
+  if (pp->eclock > 0) orc_clock_witness(&w->eclock[r], pp->eclock - 1);
+  if (pp->qclock > 0) orc_clock_witness(&w->qclock[r], pp->qclock - 1);
+  /* left members first, one past their status time (delegate.rs:477-499) */
+  for (uint32_t subj = 0; subj < w->s; ++subj) {
+    if (pp->v_kind[subj] != ORC_K_KNOWN || pp->v_status[subj] != ORC_ST_LEFT) continue;
+    uint64_t ref = 0;
+    int f = orc_handle_leave_intent(w, r, subj, pp->v_ltime[subj] + 1, 0, &ref);
+    if (f & ORC_F_REFUTE) push_refute(w, r, ref);
+  }
+  /* artificial join intents for the other status_ltimes (delegate.rs:501-511) */
+  for (uint32_t subj = 0; subj < w->s; ++subj) {
+    if (pp->v_kind[subj] != ORC_K_KNOWN || pp->v_status[subj] == ORC_ST_LEFT) continue;
+    orc_handle_join_intent(w, r, subj, pp->v_ltime[subj]);
+  }
+  /* eventJoinIgnore (delegate.rs:513-521) */
+  if (is_join && event_join_ignore && pp->eclock > w->emin[r]) w->emin[r] = pp->eclock;
+  /* every buffered user event, cc = false (delegate.rs:523-541) */
+  for (uint32_t i = 0; i < w->ebuf; ++i)
+    for (uint32_t k = 0; k < pp->eb_cnt[i]; ++k)
+      orc_handle_user_event(w, r, pp->eb_ltime[i], pp->eb_keys[(size_t)i * w->slot_k + k]);
+  return 0;
+}
+
+int orc_push_pull(orc_world* w, const uint32_t* recv, const uint32_t* send, uint32_t n, int is_join,
+                  int event_join_ignore) {
+  const size_t s = w->s, eb = w->ebuf, ek = (size_t)w->ebuf * w->slot_k;
+  const size_t per = s * 8 + s + s + eb * 8 + eb * 4 + ek * 8 + 24;
+  uint8_t* slab = (uint8_t*)malloc(per * (n ? n : 1));
+  orc_pp_state* st = (orc_pp_state*)malloc(sizeof(orc_pp_state) * (n ? n : 1));
+  if (!slab || !st) {
+    free(slab);
+    free(st);
+    return -1;
+  }
+  for (uint32_t i = 0; i < n; ++i) { /* local_state snapshots (delegate.rs:376-420) */
+    uint32_t m = send[i];
+    uint8_t* p = slab + per * i;
+    uint64_t* lt = (uint64_t*)p;
+    uint64_t* ebl = lt + s;
+    uint64_t* ebk = ebl + eb;
+    uint32_t* ebc = (uint32_t*)(ebk + ek);
+    uint8_t* stt = (uint8_t*)(ebc + eb);
+    uint8_t* kd = stt + s;
+    memcpy(lt, w->v_ltime + (size_t)m * s, s * 8);
+    memcpy(stt, w->v_status + (size_t)m * s, s);
+    memcpy(kd, w->v_kind + (size_t)m * s, s);
+    memcpy(ebl, w->eb_ltime + (size_t)m * eb, eb * 8);
+    memcpy(ebc, w->eb_cnt + (size_t)m * eb, eb * 4);
+    memcpy(ebk, w->eb_keys + (size_t)m * ek, ek * 8);
+    st[i] = (orc_pp_state){w->clock[m], w->eclock[m], w->qclock[m], lt, stt, kd, ebl, ebc, ebk};
+  }
+  for (uint32_t i = 0; i < n; ++i) orc_merge_remote_state(w, recv[i], &st[i], is_join, event_join_ignore);
+  free(slab);
+  free(st);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------ */
 /* UserEventCoalescer  core/src/coalesce/user.rs:52-97                      */
 /* ------------------------------------------------------------------------ */
 uint32_t orc_coalesce_user_events(const orc_uevent* in, uint32_t n, orc_uevent* out) {

@@ -290,6 +290,31 @@ int orc_world_round(orc_world* w, uint32_t round, const orc_ml_event* ml, uint32
 uint32_t orc_pick_peers(uint64_t seed, uint32_t n, const uint8_t* alive, uint32_t m, uint32_t round,
                         uint32_t k, uint32_t* out);
 
+/* ---- push/pull anti-entropy (M7; core/src/serf/delegate.rs:376-554) ----- */
+/* A member's local_state (delegate.rs:376-420) as the merge reads it: clocks,
+ * status_ltimes (the KNOWN view entries), left_members (KNOWN entries with
+ * status Left) and the user-event buffer.  Untracked members are implicitly
+ * Alive with status_time 0: their artificial join intents are no-ops. */
+typedef struct {
+  uint64_t clock, eclock, qclock;
+  const uint64_t* v_ltime; /* [s] */
+  const uint8_t* v_status; /* [s] */
+  const uint8_t* v_kind;   /* [s] */
+  const uint64_t* eb_ltime;/* [ebuf] */
+  const uint32_t* eb_cnt;  /* [ebuf] */
+  const uint64_t* eb_keys; /* [ebuf * slot_k] */
+} orc_pp_state;
+/* merge_remote_state (delegate.rs:422-554) of `pp` at receiver r.  Canonical
+ * order: left members in subject-slot order, then the other status_ltimes in
+ * slot order (the reference iterates an IndexSet and a HashMap), then the event
+ * buffer in index order.  A dead receiver ignores the message.  Returns 0. */
+int orc_merge_remote_state(orc_world* w, uint32_t r, const orc_pp_state* pp, int is_join, int event_join_ignore);
+/* A batch of push/pull merges: every sender's local_state is taken at batch
+ * start (memberlist sends its local state before merging the remote one),
+ * then receiver recv[i] merges sender send[i]'s state, in batch order. */
+int orc_push_pull(orc_world* w, const uint32_t* recv, const uint32_t* send, uint32_t n, int is_join,
+                  int event_join_ignore);
+
 /* ---- user-event coalescer (core/src/coalesce/user.rs:52-97) ------------- */
 typedef struct {
   uint32_t name;

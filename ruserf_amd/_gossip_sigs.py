@@ -51,3 +51,5 @@ def declare(L):
     sig("rsf_gossip_set_profiling", [VP, i])
     sig("rsf_gossip_phase_times", [VP, C.POINTER(C.c_double), P32])
     sig("rsf_gossip_totals", [VP, P64])
+    sig("rsf_gossip_push_pull", [VP, VP, C.c_uint64, C.c_uint32])
+    sig("rsf_gossip_push_pull_device", [VP, VP, C.c_uint64, C.c_uint32])

@@ -837,6 +837,176 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
   if (lane == 0) { MPROF_ADD(6, 0, 1); }
 }
 
+// ---- push/pull anti-entropy (M7): merge_remote_state of a sender's local_state
+// (core/src/serf/delegate.rs:376-554).  Snapshot semantics: memberlist sends its
+// local state before it merges the remote one, so every sender's state is copied
+// to a slab first (streaming, one block per pair), then merged.
+struct PPSlab {
+  ViewE* view;        // [pair][S]
+  uint64_t* eb_ltime; // [pair][ebuf]
+  uint32_t* eb_cnt;   // [pair][ebuf]
+  uint64_t* eb_keys;  // [pair][ebuf * slot_k]
+  uint64_t* clocks;   // [pair][4]: clock, event clock, query clock, -
+};
+
+__global__ void __launch_bounds__(256) pp_snapshot_kernel(GCfg c, GState s, const rsf_pp_pair* __restrict__ pairs,
+                                                          PPSlab sl) {
+  const uint64_t p = blockIdx.x;
+  const uint64_t l = pairs[p].sender - c.lo;
+  const uint4* vsrc = reinterpret_cast<const uint4*>(s.view + l * c.S);
+  uint4* vdst = reinterpret_cast<uint4*>(sl.view + p * c.S);
+  for (uint32_t i = threadIdx.x; i < c.S; i += blockDim.x) vdst[i] = vsrc[i];
+  for (uint32_t i = threadIdx.x; i < c.ebuf; i += blockDim.x) {
+    sl.eb_ltime[p * c.ebuf + i] = s.eb_ltime[l * c.ebuf + i];
+    sl.eb_cnt[p * c.ebuf + i] = s.eb_cnt[l * c.ebuf + i];
+  }
+  const uint64_t nk = (uint64_t)c.ebuf * c.slot_k;
+  for (uint64_t i = threadIdx.x; i < nk; i += blockDim.x) sl.eb_keys[p * nk + i] = s.eb_keys[l * nk + i];
+  if (threadIdx.x == 0) {
+    sl.clocks[p * 4 + 0] = s.clock[l];
+    sl.clocks[p * 4 + 1] = s.eclock[l];
+    sl.clocks[p * 4 + 2] = s.qclock[l];
+  }
+}
+
+// One wave per pair (receiver).  Lanes walk the subject slots 64 at a time:
+// left members run handle_node_leave_intent(status_time + 1), the other known
+// entries handle_node_join_intent(status_time); subjects are distinct, so lanes
+// are independent except for the Lamport clock, whose value at each leave is an
+// inclusive prefix max over the left members before it (all leaves precede all
+// joins, delegate.rs:477-511).  The event buffer is walked the same way: sender
+// slot i holds events of ltime = i (mod B), so it lands in receiver slot i and
+// lanes touch distinct slots; the event clock is again a prefix max.  Member
+// events, refutations and deliveries are digested serially in order.
+__global__ void __launch_bounds__(256) pp_merge_kernel(GCfg c, GState s, const rsf_pp_pair* __restrict__ pairs,
+                                                       uint64_t n_pairs, PPSlab sl, uint32_t flags) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint64_t p = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  if (p >= n_pairs) return;
+  const uint32_t m = pairs[p].receiver;
+  const uint64_t l = m - c.lo;
+  if (!s.alive[m]) return;
+  MRegs r;
+  load_regs(s, l, r);
+  const uint64_t pl = sl.clocks[p * 4 + 0], pel = sl.clocks[p * 4 + 1], pql = sl.clocks[p * 4 + 2];
+  if (pl > 0) witness(r.clock, pl - 1);
+  if (pel > 0) witness(r.eclock, pel - 1);
+  if (pql > 0) witness(r.qclock, pql - 1);
+  // ---- status_ltimes / left_members
+  const ViewE* sv = sl.view + p * c.S;
+  ViewE* vrow = s.view + l * c.S;
+  uint64_t c_leave = r.clock, c_join = r.clock;
+  for (uint32_t base = 0; base < c.S; base += kWave) {
+    const uint32_t subj = base + lane;
+    const bool valid = subj < c.S;
+    ViewE se{};
+    if (valid) se = sv[subj];
+    const bool known = valid && vkind(se.meta) == RSF_KIND_KNOWN;
+    const bool left = known && vstatus(se.meta) == RSF_STATUS_LEFT;
+    const bool join = known && !left;
+    ViewE v{};
+    if (known) v = vrow[subj];
+    const uint64_t L = left ? se.ltime + 1 : se.ltime;
+    const uint64_t incl = wave_inclusive_max_u64(left ? L + 1 : 0);
+    const uint64_t excl = wave_shr1_u64(incl);
+    int f = 0;
+    uint64_t ref = 0;
+    if (known) {
+      MRegs rr = r;
+      rr.clock = excl > c_leave ? excl : c_leave;
+      rr.digest = 0;
+      const uint64_t lt0 = v.ltime;
+      const uint32_t mt0 = v.meta;
+      if (left) f = hv_leave_intent(v, rr, subj, L, false, ref);
+      else f = hv_join_intent(v, rr, L);
+      if (v.ltime != lt0 || v.meta != mt0) vrow[subj] = v;
+    }
+    const uint64_t lmax = lane63_u64(incl);
+    if (lmax > c_leave) c_leave = lmax;
+    const uint64_t jmax = wave_max_u64(join ? L + 1 : 0);
+    if (jmax > c_join) c_join = jmax;
+    uint64_t mm = __ballot(f & (RSF_F_MEMBER_EVENT | RSF_F_REFUTE));
+    while (mm) {
+      const int i = __ffsll((long long)mm) - 1;
+      mm &= mm - 1;
+      const uint32_t fi = shfl_u32((uint32_t)f, i);
+      if (fi & RSF_F_MEMBER_EVENT)
+        r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)kEvLeave << 32) | (base + (uint32_t)i));
+      if (fi & RSF_F_REFUTE) {
+        const uint64_t rf = shfl_u64(ref, i);
+        if (lane == 0) push_refute(c, s, r, rf);
+        r.err = shfl_u32(r.err, 0);
+      }
+    }
+  }
+  r.clock = c_leave > c_join ? c_leave : c_join;
+  // ---- eventJoinIgnore (delegate.rs:513-521)
+  if ((flags & 3) == 3 && pel > r.emin) r.emin = pel;
+  // ---- the sender's event buffer, index order (delegate.rs:523-541)
+  const uint64_t B = c.ebuf;
+  uint64_t ec = r.eclock;
+  for (uint32_t base = 0; base < c.ebuf; base += kWave) {
+    const uint32_t i = base + lane;
+    const bool valid = i < c.ebuf;
+    const uint32_t cnt = valid ? sl.eb_cnt[p * c.ebuf + i] : 0u;
+    const uint64_t L = cnt ? sl.eb_ltime[p * c.ebuf + i] : 0ull;
+    const uint64_t incl = wave_inclusive_max_u64(cnt ? L + 1 : 0);
+    const uint64_t excl = wave_shr1_u64(incl);
+    uint64_t cur = excl > ec ? excl : ec;
+    if (cnt && L + 1 > cur) cur = L + 1;  // witness(L) of this slot's events
+    uint32_t dmask = 0, e_err = 0;
+    if (cnt && !(L < r.emin) && !(cur > B && L < cur - B)) {
+      const uint64_t rs = l * c.ebuf + (L % B);
+      if ((L % B) != i) {
+        e_err = kErrEvSlot;  // a ring slot not at ltime mod B: never produced by handle_user_event
+      } else {
+        uint64_t* rk = s.eb_keys + rs * c.slot_k;
+        const uint64_t* sk = sl.eb_keys + (p * c.ebuf + i) * c.slot_k;
+        uint32_t rc = s.eb_cnt[rs];
+        const uint32_t rc0 = rc;
+        for (uint32_t k = 0; k < cnt; ++k) {
+          const uint64_t key = sk[k];
+          bool dup = false;
+          for (uint32_t j = 0; j < rc; ++j) dup |= rk[j] == key;
+          if (dup) continue;
+          if (rc == 0) {
+            s.eb_ltime[rs] = L;
+            rk[0] = key;
+            rc = 1;
+          } else if (rc < c.slot_k) {
+            rk[rc++] = key;
+          } else {
+            e_err |= kErrEvSlot;
+          }
+          dmask |= 1u << k;
+        }
+        if (rc != rc0) s.eb_cnt[rs] = rc;
+      }
+    }
+    const uint64_t emax = lane63_u64(incl);
+    if (emax > ec) ec = emax;
+    uint64_t mm = __ballot(dmask != 0 || e_err != 0);
+    while (mm) {
+      const int j = __ffsll((long long)mm) - 1;
+      mm &= mm - 1;
+      r.err |= shfl_u32(e_err, j);
+      uint32_t dm = shfl_u32(dmask, j);
+      const uint64_t Lj = shfl_u64(L, j);
+      const uint64_t* skj = sl.eb_keys + (p * c.ebuf + base + (uint32_t)j) * c.slot_k;
+      while (dm) {
+        const int k = __ffs(dm) - 1;
+        dm &= dm - 1;
+        r.digest = digest_mix(digest_mix(r.digest, kDigUser ^ skj[k]), Lj);
+      }
+    }
+  }
+  r.eclock = ec;
+  if (lane == 0) {
+    store_regs(s, l, r);
+    s.emin[l] = r.emin;
+  }
+}
+
 // direct-handler batch: one thread per receiver segment (array order within a receiver)
 __global__ void __launch_bounds__(256) apply_kernel(GCfg c, GState s, const rsf_msg* __restrict__ msgs,
                                                     const uint32_t* __restrict__ order,
@@ -1030,6 +1200,8 @@ struct rsf_gossip {
   uint64_t stage_cap = 0, recv_cap = 0;
   uint32_t *stage_key = nullptr, *stage_val = nullptr, *sort_key = nullptr, *sort_val = nullptr;
   uint32_t *seg_start = nullptr, *seg_end = nullptr;
+  void* pp_buf = nullptr;  // push/pull snapshot slab (grow-only)
+  uint64_t pp_cap = 0;
   uint32_t* rec_dec = nullptr;  // record decoration beside sort_val (segment_kernel / runs_scatter_kernel)
   uint64_t* send_buf = nullptr;
   unsigned long long* d_counters = nullptr;  // [0] n_valid, [1..] shard bounds
@@ -1218,7 +1390,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   s.alive,  s.serf_state,  s.member_subj,  s.subj_member, s.refute_cnt, s.refute_ltime, s.view,
                   s.q_rumor, s.q_seq,      s.q_txlen,      s.q_next_seq,  s.eb_ltime, s.eb_cnt,     s.eb_keys,
                   s.qb_ltime, s.qb_cnt,    s.qb_ids,       s.rumors,      g->d_ml,    g->d_acts,    g->stage_key,
-                  g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters, g->rec_dec,
+                  g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters, g->rec_dec, g->pp_buf,
                   g->sort_tmp, g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
                   g->scan_tmp};
   for (void* p : ptrs)
@@ -1615,6 +1787,70 @@ int rsf_gossip_round_merge_runs(rsf_gossip* g, const uint64_t* recv, const uint6
   if (g->profiling && g->prof_rounds < rsf_gossip::kMaxProfRounds)
     hipEventRecord(g->ev[g->prof_rounds][3], g->stream);  // exchange time lands in the sort slot
   return launch_merge(g, g->sort_val);
+}
+
+static size_t pp_bytes_per_pair(const GCfg& c) {
+  return (size_t)c.S * sizeof(ViewE) + (size_t)c.ebuf * 12 + (size_t)c.ebuf * c.slot_k * 8 + 32;
+}
+
+int rsf_gossip_push_pull_device(rsf_gossip* g, const rsf_pp_pair* pairs, uint64_t n, uint32_t flags) {
+  if (!g || (n && !pairs)) return gerr("null argument");
+  if (n == 0) return RSF_OK;
+  const GCfg& c = g->c;
+  RSF_HIP(hipSetDevice(g->device));
+  if (n > g->pp_cap) {
+    if (g->pp_buf) {
+      RSF_HIP(hipStreamSynchronize(g->stream));
+      hipFree(g->pp_buf);
+    }
+    g->pp_buf = nullptr;
+    g->pp_cap = 0;
+    int rc = rsf::dmalloc(&g->pp_buf, pp_bytes_per_pair(c) * n);
+    if (rc) return rc;
+    g->pp_cap = n;
+  }
+  // slab regions, each 16-byte aligned
+  char* b = (char*)g->pp_buf;
+  PPSlab sl;
+  sl.view = (ViewE*)b;
+  b += (size_t)c.S * sizeof(ViewE) * n;
+  sl.eb_keys = (uint64_t*)b;
+  b += (size_t)c.ebuf * c.slot_k * 8 * n;
+  sl.eb_ltime = (uint64_t*)b;
+  b += (size_t)c.ebuf * 8 * n;
+  sl.clocks = (uint64_t*)b;
+  b += (size_t)32 * n;
+  sl.eb_cnt = (uint32_t*)b;
+  hipLaunchKernelGGL(pp_snapshot_kernel, dim3((unsigned)n), dim3(256), 0, g->stream, c, g->s, pairs, sl);
+  hipLaunchKernelGGL(pp_merge_kernel, dim3(grid1(n, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0, g->stream, c,
+                     g->s, pairs, n, sl, flags);
+  RSF_HIP(hipGetLastError());
+  return RSF_OK;
+}
+
+int rsf_gossip_push_pull(rsf_gossip* g, const rsf_pp_pair* pairs, uint64_t n, uint32_t flags) {
+  if (!g || (n && !pairs)) return gerr("null argument");
+  if (n == 0) return RSF_OK;
+  if (n > 0x7FFFFFFFull) return gerr("batch too large");
+  const GCfg& c = g->c;
+  std::vector<uint32_t> rs(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    const rsf_pp_pair& x = pairs[i];
+    if (x.receiver < c.lo || x.receiver >= c.lo + c.n_loc || x.sender < c.lo || x.sender >= c.lo + c.n_loc)
+      return gerr("push/pull members must be in the shard");
+    rs[i] = x.receiver;
+  }
+  std::sort(rs.begin(), rs.end());
+  if (std::adjacent_find(rs.begin(), rs.end()) != rs.end()) return gerr("receivers of one push/pull batch must be distinct");
+  RSF_HIP(hipSetDevice(g->device));
+  size_t bytes[1] = {n * sizeof(rsf_pp_pair)};
+  void* d[1];
+  int rc = g->scratch.take(bytes, 1, d);
+  if (rc) return rc;
+  RSF_HIP(hipMemcpyAsync(d[0], pairs, bytes[0], hipMemcpyHostToDevice, g->stream));
+  if ((rc = rsf_gossip_push_pull_device(g, (const rsf_pp_pair*)d[0], n, flags))) return rc;
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  return RSF_OK;
 }
 
 int rsf_gossip_check_runs(rsf_gossip* g, int* ok) {

@@ -14,6 +14,8 @@ cluster (or one shard of it) in HBM and runs those handlers as HIP kernels:
                             (Serf::join/leave/user_event/query/force_leave), emission
                             (broadcast_messages to k peers), exchange, canonical merge
   * `round_begin/emit/merge` — the same split for multi-GPU sharding (see dist.py)
+  * `push_pull(pairs)`    — local_state / merge_remote_state (delegate.rs:376-554) for a
+                            batch of (receiver, sender) pairs: push/pull anti-entropy
 
 There is no CPU execution path: every call goes to libruserf_amd.so.
 """
@@ -33,6 +35,7 @@ MSG_LEAVE, MSG_JOIN, MSG_USER_EVENT, MSG_QUERY = 0, 1, 3, 4
 F_REBROADCAST, F_REFUTE, F_PRUNE, F_DELIVER, F_MEMBER_EVENT = 1, 2, 4, 8, 16
 ACT_JOIN_SELF, ACT_LEAVE_SELF, ACT_FORCE_LEAVE, ACT_USER_EVENT, ACT_QUERY = 1, 2, 3, 4, 5
 ML_JOIN, ML_LEAVE = 1, 2
+PP_JOIN, PP_EVENT_JOIN_IGNORE = 1, 2
 
 ACTION_DTYPE = np.dtype([("member", "<u4"), ("act", "<u4"), ("subject", "<u4"), ("name_len", "<u4"),
                          ("payload_len", "<u4"), ("flags", "<u4"), ("key", "<u8")])
@@ -41,6 +44,7 @@ MSG_DTYPE = np.dtype([("receiver", "<u4"), ("subject", "<u4"), ("ltime", "<u8"),
                       ("flags", "u1"), ("_r0", "<u2"), ("_r1", "<u4")])
 RUMOR_DTYPE = np.dtype([("ltime", "<u8"), ("key", "<u8"), ("subject", "<u4"), ("type", "u1"), ("flags", "u1"),
                         ("msg_len", "<u2")])
+PP_PAIR_DTYPE = np.dtype([("receiver", "<u4"), ("sender", "<u4")])
 assert ACTION_DTYPE.itemsize == 32 and ML_DTYPE.itemsize == 16 and MSG_DTYPE.itemsize == 32
 assert RUMOR_DTYPE.itemsize == 24
 
@@ -138,6 +142,19 @@ class GossipEngine:
         refute = np.zeros(n, dtype=np.uint64)
         check(lib().rsf_gossip_apply_batch(self._h, _p(msgs), n, ptr(flags, C.c_int32), ptr(refute, C.c_uint64)))
         return flags, refute
+
+    # ---- push/pull anti-entropy: merge_remote_state(local_state(sender)) at receiver
+    def push_pull(self, pairs, is_join=False, event_join_ignore=False):
+        """pairs: (receiver, sender) rows; senders are snapshotted before any merge,
+        receivers must be distinct (a symmetric exchange is both directions)."""
+        pairs = np.ascontiguousarray(pairs, dtype=PP_PAIR_DTYPE)
+        flags = (PP_JOIN if is_join else 0) | (PP_EVENT_JOIN_IGNORE if event_join_ignore else 0)
+        check(lib().rsf_gossip_push_pull(self._h, _p(pairs), len(pairs), flags))
+
+    def push_pull_device(self, pairs_ptr, n, is_join=False, event_join_ignore=False):
+        """device-pointer variant (asynchronous, unvalidated): the throughput path"""
+        flags = (PP_JOIN if is_join else 0) | (PP_EVENT_JOIN_IGNORE if event_join_ignore else 0)
+        check(lib().rsf_gossip_push_pull_device(self._h, C.c_void_p(pairs_ptr), n, flags))
 
     # ---- rounds
     def round(self, t, ml=None, acts=None):

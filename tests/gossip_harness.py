@@ -123,3 +123,25 @@ def assert_same(a, b, ctx=""):
 def oracle_rumors(w):
     return [(w.rumors[i].type, w.rumors[i].ltime, w.rumors[i].subject, w.rumors[i].key, w.rumors[i].msg_len)
             for i in range(w.n_rumors)]
+
+
+def oracle_push_pull(w, pairs, is_join=False, event_join_ignore=False):
+    pairs = np.ascontiguousarray(pairs)
+    recv = np.ascontiguousarray(pairs["receiver"], dtype=np.uint32)
+    send = np.ascontiguousarray(pairs["sender"], dtype=np.uint32)
+    assert L.orc_push_pull(C.byref(w), O.ptr(recv, C.c_uint32), O.ptr(send, C.c_uint32), len(pairs),
+                           int(is_join), int(event_join_ignore)) == 0
+
+
+def matching_pairs(rng, members, both=True):
+    """A random perfect matching over `members` as push/pull (receiver, sender) rows:
+    each exchange a<->b contributes (a<-b) and (b<-a)."""
+    from ruserf_amd.gossip import PP_PAIR_DTYPE
+    m = rng.permutation(np.asarray(members, dtype=np.uint32))
+    m = m[: len(m) // 2 * 2].reshape(-1, 2)
+    rows = [(a, b) for a, b in m] + ([(b, a) for a, b in m] if both else [])
+    out = np.zeros(len(rows), PP_PAIR_DTYPE)
+    if rows:
+        out["receiver"] = [r[0] for r in rows]
+        out["sender"] = [r[1] for r in rows]
+    return out

@@ -194,10 +194,20 @@ def lib():
                                   C.POINTER(Action), C.c_uint32]
     L.orc_pick_peers.argtypes = [C.c_uint64, C.c_uint32, P8, C.c_uint32, C.c_uint32, C.c_uint32, P32]
     L.orc_pick_peers.restype = C.c_uint32
+    L.orc_merge_remote_state.argtypes = [C.POINTER(World), C.c_uint32, C.POINTER(PPState), C.c_int, C.c_int]
+    L.orc_push_pull.argtypes = [C.POINTER(World), P32, P32, C.c_uint32, C.c_int, C.c_int]
     L.orc_coalesce_user_events.argtypes = [C.POINTER(UEvent), C.c_uint32, C.POINTER(UEvent)]
     L.orc_coalesce_user_events.restype = C.c_uint32
     _lib = L
     return L
+
+
+class PPState(C.Structure):
+    """orc_pp_state: a member's local_state as merge_remote_state reads it"""
+    _fields_ = [("clock", C.c_uint64), ("eclock", C.c_uint64), ("qclock", C.c_uint64),
+                ("v_ltime", C.POINTER(C.c_uint64)), ("v_status", C.POINTER(C.c_uint8)),
+                ("v_kind", C.POINTER(C.c_uint8)), ("eb_ltime", C.POINTER(C.c_uint64)),
+                ("eb_cnt", C.POINTER(C.c_uint32)), ("eb_keys", C.POINTER(C.c_uint64))]
 
 
 def default_opts(**kw):

@@ -307,32 +307,35 @@ def test_leave_transitions_and_refute():
 
 
 def test_delegate_merge_remote_state(kats):
-    """merge_remote_state (delegate.rs:422-554) driven through the oracle's handlers."""
+    """merge_remote_state (delegate.rs:422-554) through orc_merge_remote_state: the
+    reference test's PushPullMessage becomes a sender local_state (status_ltimes ->
+    KNOWN entries, left_members -> status Left, the event buffer slot 45)."""
     k = kats["merge"]["delegate_merge_remote_state"]
     pp = k["pp"]
     # subjects: test=0, foo=1; receiver = member 0
     w = make_world(n=3, s=2)
-    def witness(arr_, v):
-        if not v < arr_[0]:
-            arr_[0] = v + 1
-    if pp["ltime"] > 0:
-        witness(w.clock, pp["ltime"] - 1)
-    if pp["event_ltime"] > 0:
-        witness(w.eclock, pp["event_ltime"] - 1)
-    if pp["query_ltime"] > 0:
-        witness(w.qclock, pp["query_ltime"] - 1)
     subj = {"test": 0, "foo": 1}
-    st = dict(pp["status_ltimes"])
-    for node in pp["left_members"]:
-        L.orc_handle_leave_intent(C.byref(w), 0, subj[node], st[node] + 1, 0, None)
-    for node, lt in pp["status_ltimes"]:
-        if node in pp["left_members"]:
-            continue
-        L.orc_handle_join_intent(C.byref(w), 0, subj[node], lt)
     names = {"test": 1}
+    v_lt = np.zeros(2, np.uint64)
+    v_st = np.zeros(2, np.uint8)
+    v_kd = np.zeros(2, np.uint8)
+    for node, lt in pp["status_ltimes"]:
+        v_lt[subj[node]] = lt
+        v_kd[subj[node]] = O.K_KNOWN
+        v_st[subj[node]] = O.ST_LEFT if node in pp["left_members"] else O.ST_ALIVE
+    eb_lt = np.zeros(w.ebuf, np.uint64)
+    eb_cnt = np.zeros(w.ebuf, np.uint32)
+    eb_keys = np.zeros(w.ebuf * w.slot_k, np.uint64)
     for ltime, evs in pp["events"]:
-        for name, payload in evs:
-            L.orc_handle_user_event(C.byref(w), 0, ltime, names[name] << 32)
+        slot = ltime % w.ebuf
+        eb_lt[slot] = ltime
+        for name, _payload in evs:
+            eb_keys[slot * w.slot_k + eb_cnt[slot]] = names[name] << 32
+            eb_cnt[slot] += 1
+    st = O.PPState(pp["ltime"], pp["event_ltime"], pp["query_ltime"], O.ptr(v_lt, C.c_uint64),
+                   O.ptr(v_st, C.c_uint8), O.ptr(v_kd, C.c_uint8), O.ptr(eb_lt, C.c_uint64),
+                   O.ptr(eb_cnt, C.c_uint32), O.ptr(eb_keys, C.c_uint64))
+    assert L.orc_merge_remote_state(C.byref(w), 0, C.byref(st), 0, 0) == 0
     e = k["expect"]
     assert w.clock[0] == e["clock"]
     assert list(intent(w, 0, 0)) == e["intent_test"]
