@@ -33,6 +33,12 @@ extern "C" {
 #define RSF_ERR_HIP (-2)         /* HIP runtime error; see rsf_last_error() */
 #define RSF_ERR_NOMEM (-3)       /* device allocation failed */
 #define RSF_ERR_OVERFLOW (-4)    /* a fixed-capacity device structure overflowed */
+/* wire codecs (per item) */
+#define RSF_SKIPPED 4              /* empty message / ping payload: the reference returns early */
+#define RSF_ERR_CODEC_SHORT (-10)  /* NotEnoughBytes / varint buffer underflow */
+#define RSF_ERR_CODEC_TYPE (-11)   /* unknown MessageType tag, a kind this codec does not carry, or a bad PING_VERSION */
+#define RSF_ERR_CODEC_VARINT (-12) /* varint longer than 10 bytes / overflowing u64 */
+#define RSF_ERR_CODEC_LEN (-13)    /* length field the reference would panic on (< header) or dim > max */
 
 /* Last error message of the calling thread (static storage, never NULL). */
 const char* rsf_last_error(void);
@@ -146,6 +152,20 @@ int rsf_vivaldi_round(rsf_vivaldi* v, uint32_t round);
 int rsf_vivaldi_gen_probes(rsf_vivaldi* v, uint32_t round, uint32_t* peer_out, uint64_t* rtt_ns_out);
 int rsf_vivaldi_observe(rsf_vivaldi* v, uint32_t slot, const uint32_t* peer, const uint64_t* rtt_ns,
                         int32_t* status_out, uint32_t round);
+
+/* = SerfDelegate::ack_payload (core/src/serf/delegate.rs:659-701) for n members:
+ * out + i*out_stride receives [PING_VERSION=1][Coordinate encoding] of member[i]'s
+ * current coordinate (29 + 8*dim bytes).  Device pointers, asynchronous. */
+int rsf_vivaldi_ack_payloads(rsf_vivaldi* v, const uint32_t* member, uint64_t n, uint8_t* out, uint64_t out_stride);
+/* = SerfDelegate::notify_ping_complete (delegate.rs:704-779) over n acks: member[i]
+ * (in the shard; distinct in a batch) received payload bytes [off[i], off[i+1]) of
+ * `payload` with round-trip rtt_ns[i] from the node in latency-filter slot slot[i].
+ * status[i]: RSF_SKIPPED (empty payload), RSF_ERR_CODEC_TYPE (version byte),
+ * RSF_ERR_CODEC_* (Coordinate::decode), else CoordinateClient::update's result.
+ * Device pointers, asynchronous; updates the current table in place. */
+int rsf_vivaldi_observe_acks(rsf_vivaldi* v, const uint32_t* member, const uint32_t* slot, const uint8_t* payload,
+                             const uint64_t* off, const uint64_t* rtt_ns, uint64_t n, uint32_t round,
+                             int32_t* status);
 
 /* Device pointer of the current full coordinate table (n_members rows) and of
  * this shard's slice, for an all-gather between rounds on multi-GPU runs. */
@@ -354,6 +374,51 @@ int rsf_gossip_phase_times(rsf_gossip* g, double* ms_out, uint32_t* rounds_out);
 int rsf_gossip_totals(rsf_gossip* g, uint64_t* merged_total);
 /* records emitted / merged by the last round (this shard) */
 int rsf_gossip_last_round_stats(rsf_gossip* g, uint64_t* records_sent, uint64_t* records_merged);
+
+/* ======================================================================== */
+/* Wire codecs                                              */
+/* ======================================================================== */
+/* All pointers are device memory; calls are asynchronous on `stream`
+ * (hipStream_t, NULL = default stream).  Formats (ruserf_amd/csrc/codec.h):
+ *   Coordinate  u32 BE total length | error | adjustment | height | portion[], f64 BE
+ *               (core/src/coordinate.rs:663-745)
+ *   frame       [MessageType tag][message]; Join = u32 BE len | varint ltime | id,
+ *               Leave = u32 BE len | prune | varint ltime | id, UserEvent = u32 BE len |
+ *               cc | varint ltime | name | payload (types/src/{join,leave,user_event}.rs)
+ *   id / name / payload: u32 BE byte length | bytes; varint: LEB128 (transformable 0.1,
+ *               un-vendored: restated, parity unpinned) */
+
+/* one Join / Leave / UserEvent message; strings are (offset, length) into a byte
+ * buffer: the caller's blob on encode, the decoded frame buffer on decode */
+typedef struct rsf_wire_msg {
+  uint8_t type;       /* RSF_MSG_LEAVE / RSF_MSG_JOIN / RSF_MSG_USER_EVENT (tag byte) */
+  uint8_t flag;       /* leave: prune; user event: cc */
+  uint16_t _r0;
+  int32_t status;     /* decode: RSF_OK / RSF_SKIPPED / RSF_ERR_CODEC_* */
+  uint64_t ltime;
+  uint64_t a_off;     /* join/leave: node id; user event: name */
+  uint64_t b_off;     /* user event: payload */
+  uint32_t a_len, b_len;
+  uint32_t frame_len; /* decode: 1 + the length the reference's decode returns */
+  uint32_t _r1;
+} rsf_wire_msg;
+
+/* off[0] = 0, off[i+1] = off[i] + encoded frame length of msgs[i] (n+1 entries) */
+int rsf_wire_encoded_lengths(const rsf_wire_msg* msgs, uint64_t n, uint64_t* off, void* stream);
+/* frames of msgs[i] at out + off[i] (off from rsf_wire_encoded_lengths); status optional */
+int rsf_wire_encode(const rsf_wire_msg* msgs, uint64_t n, const uint8_t* blob, const uint64_t* off, uint8_t* out,
+                    int32_t* status, void* stream);
+/* notify_message's frame dispatch + decode_message (delegate.rs:157-305,
+ * transform.rs:266-300) for frames [off[i], off[i+1]) of buf */
+int rsf_wire_decode(const uint8_t* buf, const uint64_t* off, uint64_t n, rsf_wire_msg* out, void* stream);
+/* Coordinate::encode of n rows (portion[dim], error, adjustment, height; row_stride
+ * doubles apart) to out + i*out_stride, optionally behind the PING_VERSION byte */
+int rsf_coord_encode(const double* rows, uint32_t dim, uint32_t row_stride, uint64_t n, uint8_t* out,
+                     uint64_t out_stride, int ping_version_prefix, void* stream);
+/* Coordinate::decode of [off[i], off[i+1]) into rows (row_stride >= max_dim + 3);
+ * dim_out optional; status RSF_OK / RSF_SKIPPED (empty ping payload) / RSF_ERR_CODEC_* */
+int rsf_coord_decode(const uint8_t* in, const uint64_t* off, uint64_t n, int ping_version_prefix, double* rows,
+                     uint32_t row_stride, uint32_t max_dim, uint32_t* dim_out, int32_t* status, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1099,6 +1099,210 @@ int orc_push_pull(orc_world* w, const uint32_t* recv, const uint32_t* send, uint
 }
 
 /* ------------------------------------------------------------------------ */
+/* Wire codecs                                                              */
+/* byteorder::NetworkEndian */
+static void w_u32(uint8_t* d, uint32_t v) {
+  for (int i = 3; i >= 0; --i, v >>= 8) d[i] = (uint8_t)v;
+}
+static uint32_t r_u32(const uint8_t* s) {
+  uint32_t v = 0;
+  for (int i = 0; i < 4; ++i) v = (v << 8) | s[i];
+  return v;
+}
+static void w_f64(uint8_t* d, double x) {
+  uint64_t u;
+  memcpy(&u, &x, 8);
+  for (int i = 7; i >= 0; --i, u >>= 8) d[i] = (uint8_t)u;
+}
+static double r_f64(const uint8_t* s) {
+  uint64_t u = 0;
+  for (int i = 0; i < 8; ++i) u = (u << 8) | s[i];
+  double x;
+  memcpy(&x, &u, 8);
+  return x;
+}
+
+/* transformable::utils::encode_varint / decode_varint (LEB128, at most 10 bytes) */
+uint32_t orc_varint_len(uint64_t v) {
+  uint32_t n = 1;
+  for (; v >= 0x80; v >>= 7) n++;
+  return n;
+}
+uint32_t orc_varint_encode(uint64_t v, uint8_t* dst) {
+  uint32_t n = 0;
+  for (; v >= 0x80; v >>= 7) dst[n++] = (uint8_t)((v & 0x7F) | 0x80);
+  dst[n++] = (uint8_t)v;
+  return n;
+}
+uint32_t orc_varint_decode(const uint8_t* src, uint64_t n, uint64_t* v, int* err) {
+  uint64_t x = 0;
+  for (uint32_t i = 0; i < 10; ++i) {
+    if (i >= n) {
+      *err = ORC_E_SHORT;
+      return 0;
+    }
+    if (i == 9 && src[i] > 1) break; /* would overflow u64 */
+    x |= (uint64_t)(src[i] & 0x7F) << (7 * i);
+    if (!(src[i] & 0x80)) {
+      *v = x;
+      return i + 1;
+    }
+  }
+  *err = ORC_E_VARINT;
+  return 0;
+}
+
+/* Coordinate::encode  coordinate.rs:666-692 */
+uint32_t orc_coord_encode(const double* row, uint32_t dim, uint8_t* dst) {
+  uint32_t encoded_len = 4 + 8 * dim + 8 * 3, off = 0;
+  w_u32(dst + off, encoded_len);
+  off += 4;
+  w_f64(dst + off, row[dim]); /* error */
+  off += 8;
+  w_f64(dst + off, row[dim + 1]); /* adjustment */
+  off += 8;
+  w_f64(dst + off, row[dim + 2]); /* height */
+  off += 8;
+  for (uint32_t i = 0; i < dim; ++i, off += 8) w_f64(dst + off, row[i]);
+  return off;
+}
+
+/* Coordinate::decode  coordinate.rs:698-745 (release semantics: floor of the portion
+ * count; a length below the header would underflow `len - 4 - 3 * 8` and panic) */
+int orc_coord_decode(const uint8_t* src, uint64_t src_len, uint32_t max_dim, double* row, uint32_t* dim) {
+  if (src_len < 4 + 3 * 8) return ORC_E_SHORT;
+  uint64_t len = r_u32(src);
+  if (src_len < len) return ORC_E_SHORT;
+  if (len < 4 + 3 * 8) return ORC_E_LEN;
+  uint64_t num_portion = (len - 4 - 3 * 8) / 8;
+  if (num_portion > max_dim) return ORC_E_LEN;
+  uint64_t off = 4;
+  double error = r_f64(src + off);
+  off += 8;
+  double adjustment = r_f64(src + off);
+  off += 8;
+  double height = r_f64(src + off);
+  off += 8;
+  for (uint64_t i = 0; i < num_portion; ++i, off += 8) row[i] = r_f64(src + off);
+  row[num_portion] = error;
+  row[num_portion + 1] = adjustment;
+  row[num_portion + 2] = height;
+  *dim = (uint32_t)num_portion;
+  return 0;
+}
+
+/* SmolStr / Bytes (transformable 0.1): u32 BE byte length | bytes */
+static uint32_t put_bytes(uint8_t* d, const uint8_t* blob, uint64_t off, uint32_t n) {
+  w_u32(d, n);
+  memcpy(d + 4, blob + off, n);
+  return 4 + n;
+}
+static int get_bytes(const uint8_t* src, uint64_t src_len, uint64_t* o, uint32_t* n) {
+  if (src_len < 4) return ORC_E_SHORT;
+  uint32_t len = r_u32(src);
+  if (src_len - 4 < len) return ORC_E_SHORT;
+  *o = 4;
+  *n = len;
+  return 0;
+}
+
+uint32_t orc_wire_frame_len(const orc_wire_msg* m) {
+  switch (m->type) {
+    case ORC_MSG_JOIN: return 1 + 4 + orc_varint_len(m->ltime) + 4 + m->a_len;        /* join.rs:132-134 */
+    case ORC_MSG_LEAVE: return 1 + 4 + 1 + 4 + m->a_len + orc_varint_len(m->ltime);   /* leave.rs:88-90 */
+    case ORC_MSG_USER_EVENT:                                                        /* user_event.rs:330-332 */
+      return 1 + 4 + orc_varint_len(m->ltime) + 4 + m->a_len + 4 + m->b_len + 1;
+    default: return 0;
+  }
+}
+
+/* raw[0] = tag; encode_message(&msg, &mut raw[1..])  (base.rs:373, api.rs:293) */
+uint32_t orc_wire_encode(const orc_wire_msg* m, const uint8_t* blob, uint8_t* dst) {
+  uint32_t total = orc_wire_frame_len(m);
+  if (!total) return 0;
+  dst[0] = m->type;
+  uint8_t* b = dst + 1;
+  uint32_t off = 0;
+  w_u32(b, total - 1); /* encoded_len of the message */
+  off += 4;
+  if (m->type == ORC_MSG_JOIN) { /* join.rs:82-104 */
+    off += orc_varint_encode(m->ltime, b + off);
+    off += put_bytes(b + off, blob, m->a_off, m->a_len);
+  } else if (m->type == ORC_MSG_LEAVE) { /* leave.rs:62-86 */
+    b[off++] = m->flag ? 1 : 0;
+    off += orc_varint_encode(m->ltime, b + off);
+    off += put_bytes(b + off, blob, m->a_off, m->a_len);
+  } else { /* user_event.rs:306-328 */
+    b[off++] = m->flag ? 1 : 0;
+    off += orc_varint_encode(m->ltime, b + off);
+    off += put_bytes(b + off, blob, m->a_off, m->a_len);
+    off += put_bytes(b + off, blob, m->b_off, m->b_len);
+  }
+  return 1 + off;
+}
+
+void orc_wire_decode(const uint8_t* buf, uint64_t fo, uint64_t flen, orc_wire_msg* m) {
+  memset(m, 0, sizeof(*m));
+  if (flen == 0) { /* notify_message: an empty message is ignored (delegate.rs:158-161) */
+    m->status = ORC_SKIPPED;
+    return;
+  }
+  const uint8_t* src = buf + fo + 1; /* decode_message(ty, &msg[1..]) */
+  uint64_t n = flen - 1, base = fo + 1, o, sl;
+  uint32_t len, rd, slen;
+  int err = 0;
+  m->type = buf[fo];
+  switch (m->type) {
+    case ORC_MSG_JOIN: /* JoinMessage::decode  join.rs:106-130 */
+      if (n < 4) { m->status = ORC_E_SHORT; return; }
+      len = r_u32(src);
+      if (n < len) { m->status = ORC_E_SHORT; return; }
+      o = 4;
+      if (!(rd = orc_varint_decode(src + o, n - o, &m->ltime, &err))) { m->status = err; return; }
+      o += rd;
+      if ((err = get_bytes(src + o, n - o, &sl, &slen))) { m->status = err; return; }
+      m->a_off = base + o + sl;
+      m->a_len = slen;
+      m->frame_len = 1 + len;
+      return;
+    case ORC_MSG_LEAVE: /* LeaveMessage::decode  leave.rs:92-120 */
+      if (n < 5) { m->status = ORC_E_SHORT; return; }
+      len = r_u32(src);
+      if (n + 5 < len) { m->status = ORC_E_SHORT; return; }
+      m->flag = src[4] != 0;
+      o = 5;
+      if (!(rd = orc_varint_decode(src + o, n - o, &m->ltime, &err))) { m->status = err; return; }
+      o += rd;
+      if ((err = get_bytes(src + o, n - o, &sl, &slen))) { m->status = err; return; }
+      m->a_off = base + o + sl;
+      m->a_len = slen;
+      m->frame_len = (uint32_t)(1 + o + 4 + slen); /* Ok((offset, ..)) */
+      return;
+    case ORC_MSG_USER_EVENT: /* UserEventMessage::decode  user_event.rs:334-370 */
+      if (n < 4) { m->status = ORC_E_SHORT; return; }
+      len = r_u32(src);
+      if (n < len) { m->status = ORC_E_SHORT; return; }
+      if (n < 5) { m->status = ORC_E_SHORT; return; } /* src[4] would be out of bounds */
+      m->flag = src[4] != 0;
+      o = 5;
+      if (!(rd = orc_varint_decode(src + o, n - o, &m->ltime, &err))) { m->status = err; return; }
+      o += rd;
+      if ((err = get_bytes(src + o, n - o, &sl, &slen))) { m->status = err; return; }
+      m->a_off = base + o + sl;
+      m->a_len = slen;
+      o += sl + slen;
+      if ((err = get_bytes(src + o, n - o, &sl, &slen))) { m->status = err; return; }
+      m->b_off = base + o + sl;
+      m->b_len = slen;
+      m->frame_len = 1 + len;
+      return;
+    default:
+      m->status = ORC_E_TYPE;
+      return;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
 /* UserEventCoalescer  core/src/coalesce/user.rs:52-97                      */
 /* ------------------------------------------------------------------------ */
 uint32_t orc_coalesce_user_events(const orc_uevent* in, uint32_t n, orc_uevent* out) {

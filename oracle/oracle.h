@@ -315,6 +315,29 @@ int orc_merge_remote_state(orc_world* w, uint32_t r, const orc_pp_state* pp, int
 int orc_push_pull(orc_world* w, const uint32_t* recv, const uint32_t* send, uint32_t n, int is_join,
                   int event_join_ignore);
 
+/* ---- wire codecs ----------------------------------------- */
+/* status codes as include/ruserf_amd.h: 0 ok, 4 skipped, -10 short, -11 type, -12 varint, -13 len */
+enum { ORC_SKIPPED = 4, ORC_E_SHORT = -10, ORC_E_TYPE = -11, ORC_E_VARINT = -12, ORC_E_LEN = -13 };
+/* same layout as rsf_wire_msg */
+typedef struct {
+  uint8_t type, flag;
+  uint16_t _r0;
+  int32_t status;
+  uint64_t ltime, a_off, b_off;
+  uint32_t a_len, b_len, frame_len, _r1;
+} orc_wire_msg;
+uint32_t orc_varint_len(uint64_t v);
+uint32_t orc_varint_encode(uint64_t v, uint8_t* dst);
+/* returns bytes read (0 on error, *err set) */
+uint32_t orc_varint_decode(const uint8_t* src, uint64_t n, uint64_t* v, int* err);
+/* Coordinate codec (core/src/coordinate.rs:663-745); row = portion[dim], error, adjustment, height */
+uint32_t orc_coord_encode(const double* row, uint32_t dim, uint8_t* dst);
+int orc_coord_decode(const uint8_t* src, uint64_t n, uint32_t max_dim, double* row, uint32_t* dim);
+/* serf frames [tag][Join | Leave | UserEvent] */
+uint32_t orc_wire_frame_len(const orc_wire_msg* m);
+uint32_t orc_wire_encode(const orc_wire_msg* m, const uint8_t* blob, uint8_t* dst);
+void orc_wire_decode(const uint8_t* buf, uint64_t frame_off, uint64_t frame_len, orc_wire_msg* m);
+
 /* ---- user-event coalescer (core/src/coalesce/user.rs:52-97) ------------- */
 typedef struct {
   uint32_t name;

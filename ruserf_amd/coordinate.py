@@ -238,6 +238,20 @@ class CoordinateClients:
         check(lib().rsf_vivaldi_observe(self._h, slot, C.c_void_p(peer_ptr), C.c_void_p(rtt_ptr),
                                         C.c_void_p(status_ptr) if status_ptr else None, round_))
 
+    # ---- the ping seam from wire bytes (SerfDelegate::ack_payload / notify_ping_complete)
+    def ack_payloads_device(self, members_ptr, n, out_ptr, out_stride):
+        """[PING_VERSION][Coordinate] of members[i] at out + i*out_stride (device pointers)."""
+        from . import codec
+        check(codec._L().rsf_vivaldi_ack_payloads(self._h, C.c_void_p(members_ptr), n, C.c_void_p(out_ptr),
+                                                   out_stride))
+
+    def observe_acks_device(self, members_ptr, slots_ptr, payload_ptr, off_ptr, rtt_ptr, n, status_ptr, round_=0):
+        """notify_ping_complete over n acks (device pointers, asynchronous)."""
+        from . import codec
+        check(codec._L().rsf_vivaldi_observe_acks(self._h, C.c_void_p(members_ptr), C.c_void_p(slots_ptr),
+                                                   C.c_void_p(payload_ptr), C.c_void_p(off_ptr),
+                                                   C.c_void_p(rtt_ptr), n, round_, C.c_void_p(status_ptr)))
+
     def table_ptr(self):
         p = C.c_void_p()
         s = C.c_uint64()

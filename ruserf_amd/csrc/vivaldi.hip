@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../include/ruserf_amd.h"
+#include "codec.h"
 #include "common.h"
 #include "rsf_internal.h"
 
@@ -477,6 +478,68 @@ __global__ void __launch_bounds__(256) vivaldi_batch_kernel(
   }
 }
 
+// notify_ping_complete (core/src/serf/delegate.rs:704-779) from wire bytes: the
+// ack payload is [PING_VERSION][Coordinate BE encoding]; an empty payload is
+// ignored, another version byte or a decode error drops the ack, then
+// CoordinateClient::update runs with the decoded coordinate (its dimension
+// check reports a mismatch).  One lane per ack, members distinct in a batch.
+template <int D, int F>
+__global__ void __launch_bounds__(256) vivaldi_ack_kernel(
+    double* __restrict__ table, double* __restrict__ adj_win, uint32_t* __restrict__ adj_idx,
+    double* __restrict__ filt, unsigned long long* resets, const uint32_t* __restrict__ member,
+    const uint32_t* __restrict__ slot, const uint8_t* __restrict__ payload, const uint64_t* __restrict__ off,
+    const uint64_t* __restrict__ rtt, uint64_t n, int32_t* __restrict__ status, VivParams p) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int FR = (F <= 3) ? 4 : 8;
+  const uint32_t m = member[i];
+  const uint64_t local = m - p.lo;
+  const uint64_t a = off[i], b = off[i + 1];
+  int st;
+  if (b < a || local >= p.shard_n || slot[i] >= p.peers) {
+    st = RSF_ERR_ARG;
+  } else if (b == a) {
+    st = RSF_SKIPPED;
+  } else if (payload[a] != rsf::kPingVersion) {
+    st = RSF_ERR_CODEC_TYPE;
+  } else {
+    double orow[kMaxDim + 3];
+    uint32_t od = 0;
+    st = rsf::coord_decode(payload + a + 1, b - a - 1, kMaxDim, orow, &od);
+    if (st == RSF_OK) {
+      double me[D], other[D], e, ad, h;
+#pragma unroll
+      for (int k = 0; k < D; ++k) other[k] = (k < (int)od) ? orow[k] : 0.0;
+      const double oe = orow[od], oa = orow[od + 1], oh = orow[od + 2];
+      load_row<D>(table + (uint64_t)m * p.stride, me, e, ad, h, p.dim);
+      double* frec = filt + ((uint64_t)slot[i] * p.shard_n + local) * FR;
+      double rec[FR];
+#pragma unroll
+      for (int k = 0; k < FR; ++k) rec[k] = frec[k];
+      st = update_one<D, F, 0>(me, e, ad, h, other, oe, oa, oh, od, rtt[i], rec, adj_win + local, p.shard_n,
+                               adj_idx + local, p, m, p.round, resets);
+      if (st == RSF_OK) {
+#pragma unroll
+        for (int k = 0; k < FR; ++k) frec[k] = rec[k];
+        store_row<D>(table + (uint64_t)m * p.stride, me, e, ad, h, p.dim);
+      }
+    }
+  }
+  status[i] = st;
+}
+
+// ack_payload (delegate.rs:659-701): [PING_VERSION][get_coordinate() encoded]
+__global__ void __launch_bounds__(256) ack_payload_kernel(const double* __restrict__ table,
+                                                          const uint32_t* __restrict__ member, uint64_t n,
+                                                          uint8_t* __restrict__ out, uint64_t out_stride,
+                                                          VivParams p) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t* d = out + i * out_stride;
+  d[0] = rsf::kPingVersion;
+  rsf::coord_encode(d + 1, table + (uint64_t)member[i] * p.stride, p.dim);
+}
+
 template <int D>
 __global__ void __launch_bounds__(256) estimate_rtt_kernel(const double* __restrict__ table,
                                                            const uint32_t* __restrict__ a,
@@ -738,6 +801,35 @@ int rsf_vivaldi_update_batch(rsf_vivaldi* v, const uint32_t* member, const uint3
   RSF_HIP(hipMemcpyAsync(status, d[5], n * 4, hipMemcpyDeviceToHost, v->stream));
   if (rows_out) RSF_HIP(hipMemcpyAsync(rows_out, drows_out, n * st * 8, hipMemcpyDeviceToHost, v->stream));
   RSF_HIP(hipStreamSynchronize(v->stream));
+  return RSF_OK;
+}
+
+int rsf_vivaldi_ack_payloads(rsf_vivaldi* v, const uint32_t* member, uint64_t n, uint8_t* out,
+                             uint64_t out_stride) {
+  if (!v || (n && (!member || !out))) return set_err_args("null argument");
+  if (out_stride < 1ull + rsf::kCoordHdr + 8ull * v->p.dim) return set_err_args("output stride too small");
+  if (n == 0) return RSF_OK;
+  RSF_HIP(hipSetDevice(v->device));
+  hipLaunchKernelGGL(ack_payload_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, v->stream,
+                     v->table[v->cur], member, n, out, out_stride, v->p);
+  RSF_HIP(hipGetLastError());
+  return RSF_OK;
+}
+
+int rsf_vivaldi_observe_acks(rsf_vivaldi* v, const uint32_t* member, const uint32_t* slot, const uint8_t* payload,
+                             const uint64_t* off, const uint64_t* rtt_ns, uint64_t n, uint32_t round,
+                             int32_t* status) {
+  if (!v || (n && (!member || !slot || !payload || !off || !rtt_ns || !status))) return set_err_args("null argument");
+  if (n == 0) return RSF_OK;
+  RSF_HIP(hipSetDevice(v->device));
+  VivParams p = v->p;
+  p.round = round;
+  unsigned blocks = (unsigned)((n + 255) / 256);
+  RSF_DISPATCH_DF(p.dim, p.F,
+                  hipLaunchKernelGGL((vivaldi_ack_kernel<kD, kF>), dim3(blocks), dim3(256), 0, v->stream,
+                                     v->table[v->cur], v->adj, v->adj_idx, v->filt, v->resets, member, slot, payload,
+                                     off, rtt_ns, n, status, p));
+  RSF_HIP(hipGetLastError());
   return RSF_OK;
 }
 

@@ -196,6 +196,21 @@ def lib():
     L.orc_pick_peers.restype = C.c_uint32
     L.orc_merge_remote_state.argtypes = [C.POINTER(World), C.c_uint32, C.POINTER(PPState), C.c_int, C.c_int]
     L.orc_push_pull.argtypes = [C.POINTER(World), P32, P32, C.c_uint32, C.c_int, C.c_int]
+    L.orc_varint_len.argtypes = [C.c_uint64]
+    L.orc_varint_len.restype = C.c_uint32
+    L.orc_varint_encode.argtypes = [C.c_uint64, P8]
+    L.orc_varint_encode.restype = C.c_uint32
+    L.orc_varint_decode.argtypes = [P8, C.c_uint64, P64, C.POINTER(C.c_int)]
+    L.orc_varint_decode.restype = C.c_uint32
+    L.orc_coord_encode.argtypes = [C.POINTER(C.c_double), C.c_uint32, P8]
+    L.orc_coord_encode.restype = C.c_uint32
+    L.orc_coord_decode.argtypes = [P8, C.c_uint64, C.c_uint32, C.POINTER(C.c_double), P32]
+    L.orc_coord_decode.restype = C.c_int
+    L.orc_wire_frame_len.argtypes = [C.c_void_p]
+    L.orc_wire_frame_len.restype = C.c_uint32
+    L.orc_wire_encode.argtypes = [C.c_void_p, P8, P8]
+    L.orc_wire_encode.restype = C.c_uint32
+    L.orc_wire_decode.argtypes = [P8, C.c_uint64, C.c_uint64, C.c_void_p]
     L.orc_coalesce_user_events.argtypes = [C.POINTER(UEvent), C.c_uint32, C.POINTER(UEvent)]
     L.orc_coalesce_user_events.restype = C.c_uint32
     _lib = L
