@@ -354,10 +354,27 @@ int rsf_gossip_push_pull(rsf_gossip* g, const rsf_pp_pair* pairs, uint64_t n, ui
 /* device pairs, asynchronous, not validated (the throughput path) */
 int rsf_gossip_push_pull_device(rsf_gossip* g, const rsf_pp_pair* pairs_dev, uint64_t n, uint32_t flags);
 
+/* ---- Reaper (Serf's reaper tick, core/src/serf/base.rs:519-601, 1782-1784) ----
+ * Times are in the engine's clock, which rsf_gossip_round / _round_begin set to
+ * the round number (rsf_gossip_set_now sets it for rsf_gossip_apply_batch).
+ * Handlers stamp it as a member's leave_time (Alive -> Failed, Leaving -> Left,
+ * base.rs:1355, 1364; kept when Failed -> Left by a leave intent) and as a
+ * buffered intent's wall time (upsert_intent, base.rs:1813, 1822).  At every
+ * live member: failed members with now - leave_time > reconnect_timeout, then
+ * left members past tombstone_timeout, are erased (the view entry returns to
+ * unknown) with a Reap MemberEvent each (subject-slot order; the reference walks
+ * its failed/left lists); intents past recent_intent_timeout are dropped.
+ * Asynchronous.  (erase_node's CoordinateClient::forget_node is the caller's:
+ * rsf_vivaldi_forget_node.) */
+int rsf_gossip_reap(rsf_gossip* g, uint32_t now, uint32_t reconnect_timeout, uint32_t tombstone_timeout,
+                    uint32_t recent_intent_timeout);
+int rsf_gossip_set_now(rsf_gossip* g, uint32_t now);
+
 /* Inspection (host copies; synchronise).  Arrays are over the shard's members. */
 int rsf_gossip_dump_members(rsf_gossip* g, uint64_t* clock, uint64_t* event_clock, uint64_t* query_clock,
                             uint64_t* digest, uint32_t* err, uint8_t* serf_state);
-int rsf_gossip_dump_view(rsf_gossip* g, uint64_t* ltime, uint8_t* status, uint8_t* kind);
+/* time (optional): the leave time of a Failed/Left entry or the wall time of a buffered intent */
+int rsf_gossip_dump_view(rsf_gossip* g, uint64_t* ltime, uint8_t* status, uint8_t* kind, uint32_t* time);
 int rsf_gossip_dump_queues(rsf_gossip* g, uint32_t* rumor, uint32_t* seq, uint16_t* transmits, uint16_t* len,
                            uint32_t* next_seq);
 int rsf_gossip_dump_buffers(rsf_gossip* g, uint64_t* eb_ltime, uint32_t* eb_cnt, uint64_t* eb_keys,

@@ -551,7 +551,7 @@ uint64_t orc_digest_mix(uint64_t d, uint64_t x) {
 #define DIG_USER 0x1000000000000000ull
 #define DIG_QUERY 0x2000000000000000ull
 #define DIG_MEMBER 0x3000000000000000ull
-enum { EV_JOIN = 0, EV_LEAVE = 1, EV_FAILED = 2 };
+enum { EV_JOIN = 0, EV_LEAVE = 1, EV_FAILED = 2, EV_REAP = 3 };
 
 static inline void digest_member_event(orc_world* w, uint32_t m, uint32_t ev, uint32_t subj) {
   w->digest[m] = orc_digest_mix(w->digest[m], DIG_MEMBER | ((uint64_t)ev << 32) | subj);
@@ -583,7 +583,7 @@ int orc_world_init(orc_world* w, const orc_world_cfg* c) {
       A(q_seq, n * 3 * c->qcap) || A(q_tx, n * 3 * c->qcap) || A(q_len, n * 3 * c->qcap) ||
       A(q_next_seq, n * 3) || A(eb_ltime, n * c->ebuf) || A(eb_cnt, n * c->ebuf) ||
       A(eb_keys, n * c->ebuf * c->slot_k) || A(qb_ltime, n * c->qbuf) || A(qb_cnt, n * c->qbuf) ||
-      A(qb_ids, n * c->qbuf * c->slot_k) || A(rumors, c->cap_rumors ? c->cap_rumors : 1)) {
+      A(qb_ids, n * c->qbuf * c->slot_k) || A(rumors, c->cap_rumors ? c->cap_rumors : 1) || A(v_time, n * s)) {
     orc_world_free(w);
     return -1;
   }
@@ -607,7 +607,7 @@ void orc_world_free(orc_world* w) {
                   w->serf_state, w->err, w->subj_member, w->member_subj, w->refute_cnt,
                   w->refute_ltime, w->v_ltime, w->v_status, w->v_kind, w->q_rumor, w->q_seq,
                   w->q_tx, w->q_len, w->q_next_seq, w->eb_ltime, w->eb_cnt, w->eb_keys,
-                  w->qb_ltime, w->qb_cnt, w->qb_ids, w->rumors};
+                  w->qb_ltime, w->qb_cnt, w->qb_ids, w->rumors, w->v_time};
   for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) free(ptrs[i]);
   memset(w, 0, sizeof(*w));
 }
@@ -618,11 +618,13 @@ int orc_upsert_intent(orc_world* w, uint32_t m, uint32_t subj, uint8_t kind, uin
   if (w->v_kind[e] == ORC_K_UNKNOWN) {
     w->v_kind[e] = kind;
     w->v_ltime[e] = ltime;
+    w->v_time[e] = w->now; /* wall_time: stamper() */
     return 1;
   }
   if (ltime > w->v_ltime[e]) {
     w->v_kind[e] = kind;
     w->v_ltime[e] = ltime;
+    w->v_time[e] = w->now;
     return 1;
   }
   return 0;
@@ -672,6 +674,7 @@ int orc_handle_leave_intent(orc_world* w, uint32_t m, uint32_t subj, uint64_t lt
 /* handle_node_join (memberlist NotifyJoin)  base.rs:1167-1298 */
 int orc_handle_node_join(orc_world* w, uint32_t m, uint32_t subj) {
   size_t e = (size_t)m * w->s + subj;
+  w->v_time[e] = 0; /* leave_time: None (1226, 1265) */
   if (w->v_kind[e] == ORC_K_KNOWN) {
     w->v_status[e] = ORC_ST_ALIVE; /* status_time kept (1225) */
   } else {
@@ -696,9 +699,11 @@ int orc_handle_node_leave(orc_world* w, uint32_t m, uint32_t subj) {
   if (w->v_kind[e] != ORC_K_KNOWN) return 0;
   if (w->v_status[e] == ORC_ST_LEAVING) {
     w->v_status[e] = ORC_ST_LEFT;
+    w->v_time[e] = w->now; /* leave_time = now (1355) */
     digest_member_event(w, m, EV_LEAVE, subj);
   } else if (w->v_status[e] == ORC_ST_ALIVE) {
     w->v_status[e] = ORC_ST_FAILED;
+    w->v_time[e] = w->now; /* (1364) */
     digest_member_event(w, m, EV_FAILED, subj);
   } else {
     return 0;
@@ -895,6 +900,7 @@ static void broadcast_join(orc_world* w, uint32_t m, uint64_t ltime, uint32_t ri
 int orc_world_round(orc_world* w, uint32_t round, const orc_ml_event* ml, uint32_t n_ml,
                     const orc_action* acts, uint32_t n_acts) {
   const uint32_t n = w->n, k = w->fanout;
+  w->now = round;
   /* rumor ids of this round: [refutes: s*max_refute][actions: n_acts] */
   uint32_t base = w->n_rumors;
   uint32_t need = w->s * w->max_refute + n_acts;
@@ -1095,6 +1101,42 @@ int orc_push_pull(orc_world* w, const uint32_t* recv, const uint32_t* send, uint
   for (uint32_t i = 0; i < n; ++i) orc_merge_remote_state(w, recv[i], &st[i], is_join, event_join_ignore);
   free(slab);
   free(st);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Reaper  base.rs:519-601 (reap!, erase_node!), 1782-1784 (reap_intents)   */
+static void erase_entry(orc_world* w, size_t e) {
+  w->v_kind[e] = ORC_K_UNKNOWN;
+  w->v_status[e] = ORC_ST_NONE;
+  w->v_ltime[e] = 0;
+  w->v_time[e] = 0;
+}
+
+int orc_reap(orc_world* w, uint32_t now, uint32_t reconnect_timeout, uint32_t tombstone_timeout,
+             uint32_t recent_intent_timeout) {
+  for (uint32_t m = 0; m < w->n; ++m) {
+    if (!w->alive[m]) continue;
+    const size_t row = (size_t)m * w->s;
+    /* reap_failed, then reap_left (run(), 588-589) */
+    for (int pass = 0; pass < 2; ++pass) {
+      const uint8_t st = pass == 0 ? ORC_ST_FAILED : ORC_ST_LEFT;
+      const uint32_t timeout = pass == 0 ? reconnect_timeout : tombstone_timeout;
+      for (uint32_t subj = 0; subj < w->s; ++subj) {
+        size_t e = row + subj;
+        if (w->v_kind[e] != ORC_K_KNOWN || w->v_status[e] != st) continue;
+        if ((uint32_t)(now - w->v_time[e]) <= timeout) continue; /* leave_time.elapsed() <= timeout */
+        erase_entry(w, e);                                        /* members.states.remove */
+        digest_member_event(w, m, EV_REAP, subj);                 /* MemberEventType::Reap */
+      }
+    }
+    /* reap_intents: retain (now - wall_time) <= timeout */
+    for (uint32_t subj = 0; subj < w->s; ++subj) {
+      size_t e = row + subj;
+      if (w->v_kind[e] != ORC_K_INTENT_JOIN && w->v_kind[e] != ORC_K_INTENT_LEAVE) continue;
+      if ((uint32_t)(now - w->v_time[e]) > recent_intent_timeout) erase_entry(w, e);
+    }
+  }
   return 0;
 }
 

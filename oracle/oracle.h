@@ -224,6 +224,10 @@ typedef struct {
   uint32_t n_rumors, cap_rumors;
   /* stats */
   uint64_t merges, sends, deliveries;
+  /* [n][s] leave_time of a Failed/Left member or wall time of a buffered intent
+   * (base.rs:1355, 1364, 1813, 1822), in the caller's time unit (rounds) */
+  uint32_t* v_time;
+  uint32_t now; /* the current time stamped by the handlers (orc_world_round sets it to the round) */
 } orc_world;
 
 typedef struct {
@@ -314,6 +318,16 @@ int orc_merge_remote_state(orc_world* w, uint32_t r, const orc_pp_state* pp, int
  * then receiver recv[i] merges sender send[i]'s state, in batch order. */
 int orc_push_pull(orc_world* w, const uint32_t* recv, const uint32_t* send, uint32_t n, int is_join,
                   int event_join_ignore);
+
+/* ---- Reaper (M8; core/src/serf/base.rs:519-601, 1782-1784) -------------- */
+/* One reaper tick at every live member: failed members whose leave time is
+ * more than reconnect_timeout old, then left members older than
+ * tombstone_timeout, are erased (erase_node: the state is removed and a Reap
+ * MemberEvent emitted, in subject-slot order; the reference walks its
+ * failed/left lists), then intents older than recent_intent_timeout are
+ * dropped (reap_intents).  `elapsed <= timeout` keeps an entry, as reap! does. */
+int orc_reap(orc_world* w, uint32_t now, uint32_t reconnect_timeout, uint32_t tombstone_timeout,
+             uint32_t recent_intent_timeout);
 
 /* ---- wire codecs ----------------------------------------- */
 /* status codes as include/ruserf_amd.h: 0 ok, 4 skipped, -10 short, -11 type, -12 varint, -13 len */

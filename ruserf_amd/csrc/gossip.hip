@@ -338,7 +338,7 @@ __global__ void __launch_bounds__(256) ml_kernel(GCfg c, GState s, const rsf_ml_
     if (al && m != sm) {
       ViewE* v = s.view + l * c.S + subj;
       if (ml[e].kind == RSF_ML_JOIN) h_node_join(v, r, subj);
-      else h_node_leave(v, r, subj);
+      else h_node_leave(v, r, subj, c.now);
       touched = true;
     }
     if (sm == m && ml[e].set_alive == 0) al = false;
@@ -385,7 +385,7 @@ __device__ __forceinline__ void broadcast_join(const GCfg& c, const GState& s, u
                                                uint32_t rid) {
   uint32_t subj = (uint32_t)r.subj;
   witness(r.clock, L);
-  h_join_intent(s.view + l * c.S + subj, r, L);
+  h_join_intent(s.view + l * c.S + subj, r, L, c.now);
   uint32_t len = msg_len(RSF_MSG_JOIN, L, 0, 0);
   put_rumor(s, rid, RSF_MSG_JOIN, 0, subj, L, 0, len);
   queue_insert_serial(c, s, l, kQIntent, rid, len);
@@ -430,7 +430,7 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
       uint64_t lt = r.clock;
       r.clock++;
       uint32_t subj = (uint32_t)r.subj;
-      h_leave_intent(s.view + l * c.S + subj, r, subj, lt, false, ref);
+      h_leave_intent(s.view + l * c.S + subj, r, subj, lt, false, ref, c.now);
       uint32_t len = msg_len(RSF_MSG_LEAVE, lt, 0, 0);
       put_rumor(s, rid, RSF_MSG_LEAVE, 0, subj, lt, 0, len);
       queue_insert_serial(c, s, l, kQIntent, rid, len);
@@ -439,7 +439,7 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
     case RSF_ACT_FORCE_LEAVE: {
       uint64_t lt = r.clock;
       bool prune = x.flags & 1;
-      int f = h_leave_intent(s.view + l * c.S + x.subject, r, x.subject, lt, prune, ref);
+      int f = h_leave_intent(s.view + l * c.S + x.subject, r, x.subject, lt, prune, ref, c.now);
       if (f & RSF_F_REFUTE) push_refute(c, s, r, ref);
       uint32_t len = msg_len(RSF_MSG_LEAVE, lt, 0, 0);
       put_rumor(s, rid, RSF_MSG_LEAVE, prune ? 1 : 0, x.subject, lt, 0, len);
@@ -731,24 +731,26 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
       const int pdone = __shfl((int)done, src);  // NOT inside `||`: short-circuit would exec-mask it
       const bool prev_done = prev < 0 || pdone != 0;
       const uint64_t pl = __shfl(v.ltime, src);
-      const uint32_t pm = (uint32_t)__shfl((int)v.meta, src);
-      const bool pd = __shfl((int)dirty, src) != 0;
+      // meta uses 16 bits: the predecessor's dirty flag rides in bit 31
+      const uint32_t pmd = (uint32_t)__shfl((int)(v.meta | (dirty ? 0x80000000u : 0u)), src);
+      const uint32_t pt = (uint32_t)__shfl((int)v.t, src);
       const bool go = !done && prev_done;
       if (go) {
         if (prev >= 0) {
           v.ltime = pl;
-          v.meta = pm;
-          dirty = pd;
+          v.meta = pmd & 0x7FFFFFFFu;
+          v.t = pt;
+          dirty = (pmd >> 31) != 0;
         }
         MRegs rr = r;
         rr.clock = clock_before;
         rr.digest = 0;
         const uint64_t lt0 = v.ltime;
-        const uint32_t mt0 = v.meta;
-        if (ru.type == RSF_MSG_JOIN) f = hv_join_intent(v, rr, ru.ltime);
-        else f = hv_leave_intent(v, rr, ru.subject, ru.ltime, ru.flags & 1, ref);
+        const uint32_t mt0 = v.meta, t0 = v.t;
+        if (ru.type == RSF_MSG_JOIN) f = hv_join_intent(v, rr, ru.ltime, c.now);
+        else f = hv_leave_intent(v, rr, ru.subject, ru.ltime, ru.flags & 1, ref, c.now);
         if (f & RSF_F_MEMBER_EVENT) contrib = kDigMember | ((uint64_t)kEvLeave << 32) | ru.subject;
-        dirty = dirty || v.ltime != lt0 || v.meta != mt0;
+        dirty = dirty || v.ltime != lt0 || v.meta != mt0 || v.t != t0;
         done = true;
       }
       if (!__ballot(!done)) break;
@@ -917,9 +919,10 @@ __global__ void __launch_bounds__(256) pp_merge_kernel(GCfg c, GState s, const r
       rr.digest = 0;
       const uint64_t lt0 = v.ltime;
       const uint32_t mt0 = v.meta;
-      if (left) f = hv_leave_intent(v, rr, subj, L, false, ref);
-      else f = hv_join_intent(v, rr, L);
-      if (v.ltime != lt0 || v.meta != mt0) vrow[subj] = v;
+      const uint32_t t0 = v.t;
+      if (left) f = hv_leave_intent(v, rr, subj, L, false, ref, c.now);
+      else f = hv_join_intent(v, rr, L, c.now);
+      if (v.ltime != lt0 || v.meta != mt0 || v.t != t0) vrow[subj] = v;
     }
     const uint64_t lmax = lane63_u64(incl);
     if (lmax > c_leave) c_leave = lmax;
@@ -1007,6 +1010,48 @@ __global__ void __launch_bounds__(256) pp_merge_kernel(GCfg c, GState s, const r
   }
 }
 
+// ---- Reaper (M8; core/src/serf/base.rs:519-601, 1782-1784).  One wave per live
+// member, lanes over subject slots (16-B coalesced view reads).  Pass 1 erases
+// failed members past reconnect_timeout and intents past recent_intent_timeout
+// and digests the failed reaps in slot order; pass 2 (only where a left member
+// is due) erases left members past tombstone_timeout and digests them, so every
+// failed Reap event precedes every left one, as reap_failed precedes reap_left.
+constexpr uint32_t kEvReap = 3;
+__global__ void __launch_bounds__(256) reap_kernel(GCfg c, GState s, uint32_t now, uint32_t rc_to, uint32_t ts_to,
+                                                   uint32_t in_to) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  if (l >= c.n_loc) return;
+  if (!s.alive[c.lo + l]) return;
+  ViewE* vrow = s.view + l * c.S;
+  uint64_t dig = s.digest[l];
+  const uint64_t d0 = dig;
+  bool any_left = false;
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1 && !any_left) break;
+    for (uint32_t base = 0; base < c.S; base += kWave) {
+      const uint32_t subj = base + lane;
+      ViewE v{};
+      if (subj < c.S) v = vrow[subj];
+      const uint32_t kind = vkind(v.meta), st = vstatus(v.meta), age = now - v.t;
+      const bool known = subj < c.S && kind == RSF_KIND_KNOWN;
+      const bool failed = known && st == RSF_STATUS_FAILED && age > rc_to;   // leave_time.elapsed() > timeout
+      const bool left = known && st == RSF_STATUS_LEFT && age > ts_to;
+      const bool intent = subj < c.S && (kind == RSF_KIND_INTENT_JOIN || kind == RSF_KIND_INTENT_LEAVE) && age > in_to;
+      const bool reap = pass == 0 ? failed : left;
+      if (reap || (pass == 0 && intent)) vrow[subj] = ViewE{0ull, 0u, 0u};  // erase_node / reap_intents
+      if (pass == 0) any_left = any_left || __ballot(left) != 0;
+      uint64_t mm = __ballot(reap);
+      while (mm) {  // Reap member events, slot order
+        const int i = __ffsll((long long)mm) - 1;
+        mm &= mm - 1;
+        dig = digest_mix(dig, kDigMember | ((uint64_t)kEvReap << 32) | (base + (uint32_t)i));
+      }
+    }
+  }
+  if (lane == 0 && dig != d0) s.digest[l] = dig;
+}
+
 // direct-handler batch: one thread per receiver segment (array order within a receiver)
 __global__ void __launch_bounds__(256) apply_kernel(GCfg c, GState s, const rsf_msg* __restrict__ msgs,
                                                     const uint32_t* __restrict__ order,
@@ -1026,8 +1071,8 @@ __global__ void __launch_bounds__(256) apply_kernel(GCfg c, GState s, const rsf_
     uint64_t ref = 0;
     int f = 0;
     switch (x.type) {
-      case RSF_MSG_JOIN: f = h_join_intent(vrow + x.subject, r, x.ltime); break;
-      case RSF_MSG_LEAVE: f = h_leave_intent(vrow + x.subject, r, x.subject, x.ltime, x.flags & 1, ref); break;
+      case RSF_MSG_JOIN: f = h_join_intent(vrow + x.subject, r, x.ltime, c.now); break;
+      case RSF_MSG_LEAVE: f = h_leave_intent(vrow + x.subject, r, x.subject, x.ltime, x.flags & 1, ref, c.now); break;
       case RSF_MSG_USER_EVENT: f = h_user_event(c, s, l, r, x.ltime, x.key); break;
       case RSF_MSG_QUERY: f = h_query(c, s, l, r, x.ltime, (uint32_t)x.key, x.flags & 1); break;
       default: f = 0; break;
@@ -1054,7 +1099,7 @@ __global__ void init_views_kernel(ViewE* view, uint64_t n_loc, uint32_t S, const
   ViewE v;
   v.ltime = ltime[subj];
   v.meta = vmeta(status[subj], kind[subj]);
-  v._pad = 0;
+  v.t = 0;
   view[i] = v;
 }
 
@@ -1463,7 +1508,7 @@ int rsf_gossip_set_view(rsf_gossip* g, uint64_t m, uint32_t subj, uint8_t kind, 
   ViewE v;
   v.ltime = ltime;
   v.meta = status | ((uint32_t)kind << 8);
-  v._pad = 0;
+  v.t = 0;
   RSF_HIP(hipSetDevice(g->device));
   RSF_HIP(hipMemcpyAsync(g->s.view + (m - c.lo) * c.S + subj, &v, sizeof(v), hipMemcpyHostToDevice, g->stream));
   RSF_HIP(hipStreamSynchronize(g->stream));
@@ -1584,6 +1629,7 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
   hipStream_t st = g->stream;
   mark(g, 0);
   g->cur_round = round;
+  g->c.now = round;  // handlers stamp leave / intent times with the round
   g->round_base = g->n_rumors;
   g->round_abase = g->round_base + c.S * c.max_refute;
   g->round_need = (uint32_t)need;
@@ -1853,6 +1899,23 @@ int rsf_gossip_push_pull(rsf_gossip* g, const rsf_pp_pair* pairs, uint64_t n, ui
   return RSF_OK;
 }
 
+int rsf_gossip_reap(rsf_gossip* g, uint32_t now, uint32_t reconnect_timeout, uint32_t tombstone_timeout,
+                    uint32_t recent_intent_timeout) {
+  if (!g) return gerr("null context");
+  const GCfg& c = g->c;
+  RSF_HIP(hipSetDevice(g->device));
+  hipLaunchKernelGGL(reap_kernel, dim3(grid1(c.n_loc, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0, g->stream, c,
+                     g->s, now, reconnect_timeout, tombstone_timeout, recent_intent_timeout);
+  RSF_HIP(hipGetLastError());
+  return RSF_OK;
+}
+
+int rsf_gossip_set_now(rsf_gossip* g, uint32_t now) {
+  if (!g) return gerr("null context");
+  g->c.now = now;
+  return RSF_OK;
+}
+
 int rsf_gossip_check_runs(rsf_gossip* g, int* ok) {
   if (!g || !ok) return gerr("null argument");
   unsigned long long bad = 0;
@@ -1879,7 +1942,7 @@ int rsf_gossip_dump_members(rsf_gossip* g, uint64_t* clock, uint64_t* ec, uint64
   return RSF_OK;
 }
 
-int rsf_gossip_dump_view(rsf_gossip* g, uint64_t* ltime, uint8_t* status, uint8_t* kind) {
+int rsf_gossip_dump_view(rsf_gossip* g, uint64_t* ltime, uint8_t* status, uint8_t* kind, uint32_t* time) {
   if (!g || !ltime || !status || !kind) return gerr("null argument");
   const uint64_t cnt = g->c.n_loc * g->c.S;
   std::vector<ViewE> v(cnt);
@@ -1890,6 +1953,7 @@ int rsf_gossip_dump_view(rsf_gossip* g, uint64_t* ltime, uint8_t* status, uint8_
     ltime[i] = v[i].ltime;
     status[i] = (uint8_t)(v[i].meta & 0xFF);
     kind[i] = (uint8_t)((v[i].meta >> 8) & 0xFF);
+    if (time) time[i] = v[i].t;
   }
   return RSF_OK;
 }

@@ -24,13 +24,14 @@ struct GCfg {
   uint64_t N, lo, n_loc;
   uint32_t S, qcap, ebuf, qbuf, slot_k, fanout, limit, overhead, tx_limit, max_refute, cap_t;
   uint32_t k0, k1;
+  uint32_t now;  // time stamped into view entries (leave_time / intent wall time); = the round
 };
 
 // view entry: members.states[subject] (status, status_time) or recent_intents[subject]
 struct __align__(16) ViewE {
   uint64_t ltime;
   uint32_t meta;  // status | kind << 8
-  uint32_t _pad;
+  uint32_t t;     // leave_time of a Failed/Left member, wall time of a buffered intent (base.rs:1355, 1364, 1813)
 };
 
 struct GState {
@@ -124,11 +125,12 @@ __device__ __forceinline__ uint32_t vkind(uint32_t meta) { return (meta >> 8) & 
 __device__ __forceinline__ uint32_t vmeta(uint32_t status, uint32_t kind) { return status | (kind << 8); }
 
 // upsert_intent (base.rs:1797-1828)
-__device__ __forceinline__ bool upsert_intent(ViewE* e, uint32_t kind, uint64_t L) {
+__device__ __forceinline__ bool upsert_intent(ViewE* e, uint32_t kind, uint64_t L, uint32_t now) {
   ViewE v = *e;
   if (vkind(v.meta) == RSF_KIND_UNKNOWN || L > v.ltime) {
     v.ltime = L;
     v.meta = vmeta(vstatus(v.meta), kind);
+    v.t = now;
     *e = v;
     return true;
   }
@@ -136,17 +138,18 @@ __device__ __forceinline__ bool upsert_intent(ViewE* e, uint32_t kind, uint64_t 
 }
 
 // upsert_intent on a register copy
-__device__ __forceinline__ bool upsert_intent_v(ViewE& v, uint32_t kind, uint64_t L) {
+__device__ __forceinline__ bool upsert_intent_v(ViewE& v, uint32_t kind, uint64_t L, uint32_t now) {
   if (vkind(v.meta) == RSF_KIND_UNKNOWN || L > v.ltime) {
     v.ltime = L;
     v.meta = vmeta(vstatus(v.meta), kind);
+    v.t = now;  // wall_time = stamper() (base.rs:1813, 1822)
     return true;
   }
   return false;
 }
 
 // handle_node_join_intent (base.rs:1302-1337) on a register copy of the view entry
-__device__ __forceinline__ int hv_join_intent(ViewE& v, MRegs& r, uint64_t L) {
+__device__ __forceinline__ int hv_join_intent(ViewE& v, MRegs& r, uint64_t L, uint32_t now) {
   witness(r.clock, L);
   if (vkind(v.meta) == RSF_KIND_KNOWN) {
     if (L <= v.ltime) return 0;
@@ -156,21 +159,21 @@ __device__ __forceinline__ int hv_join_intent(ViewE& v, MRegs& r, uint64_t L) {
     v.meta = vmeta(st, RSF_KIND_KNOWN);
     return RSF_F_REBROADCAST;
   }
-  return upsert_intent_v(v, RSF_KIND_INTENT_JOIN, L) ? RSF_F_REBROADCAST : 0;
+  return upsert_intent_v(v, RSF_KIND_INTENT_JOIN, L, now) ? RSF_F_REBROADCAST : 0;
 }
-__device__ __forceinline__ int h_join_intent(ViewE* e, MRegs& r, uint64_t L) {
+__device__ __forceinline__ int h_join_intent(ViewE* e, MRegs& r, uint64_t L, uint32_t now) {
   ViewE v = *e;
-  int f = hv_join_intent(v, r, L);
+  int f = hv_join_intent(v, r, L, now);
   *e = v;
   return f;
 }
 
 // handle_node_leave_intent (base.rs:1409-1528) on a register copy of the view entry
 __device__ __forceinline__ int hv_leave_intent(ViewE& v, MRegs& r, uint32_t subj, uint64_t L, bool prune,
-                                               uint64_t& refute) {
+                                               uint64_t& refute, uint32_t now) {
   uint8_t state = r.serf_state;
   witness(r.clock, L);
-  if (vkind(v.meta) != RSF_KIND_KNOWN) return upsert_intent_v(v, RSF_KIND_INTENT_LEAVE, L) ? RSF_F_REBROADCAST : 0;
+  if (vkind(v.meta) != RSF_KIND_KNOWN) return upsert_intent_v(v, RSF_KIND_INTENT_LEAVE, L, now) ? RSF_F_REBROADCAST : 0;
   if (L <= v.ltime) return 0;
   if (r.subj == (int32_t)subj && state == kSerfAlive) {
     refute = r.clock;
@@ -196,9 +199,9 @@ __device__ __forceinline__ int hv_leave_intent(ViewE& v, MRegs& r, uint32_t subj
   return f;
 }
 __device__ __forceinline__ int h_leave_intent(ViewE* e, MRegs& r, uint32_t subj, uint64_t L, bool prune,
-                                              uint64_t& refute) {
+                                              uint64_t& refute, uint32_t now) {
   ViewE v = *e;
-  int f = hv_leave_intent(v, r, subj, L, prune, refute);
+  int f = hv_leave_intent(v, r, subj, L, prune, refute, now);
   *e = v;
   return f;
 }
@@ -207,6 +210,7 @@ __device__ __forceinline__ int h_leave_intent(ViewE* e, MRegs& r, uint32_t subj,
 __device__ __forceinline__ int h_node_join(ViewE* e, MRegs& r, uint32_t subj) {
   ViewE v = *e;
   uint32_t kind = vkind(v.meta);
+  v.t = 0;  // leave_time: None (base.rs:1226, 1265)
   if (kind == RSF_KIND_KNOWN) {
     v.meta = vmeta(RSF_STATUS_ALIVE, RSF_KIND_KNOWN);
   } else {
@@ -226,7 +230,7 @@ __device__ __forceinline__ int h_node_join(ViewE* e, MRegs& r, uint32_t subj) {
 }
 
 // handle_node_leave (base.rs:1339-1407)
-__device__ __forceinline__ int h_node_leave(ViewE* e, MRegs& r, uint32_t subj) {
+__device__ __forceinline__ int h_node_leave(ViewE* e, MRegs& r, uint32_t subj, uint32_t now) {
   ViewE v = *e;
   if (vkind(v.meta) != RSF_KIND_KNOWN) return 0;
   uint32_t st = vstatus(v.meta), ev;
@@ -240,6 +244,7 @@ __device__ __forceinline__ int h_node_leave(ViewE* e, MRegs& r, uint32_t subj) {
     return 0;
   }
   v.meta = vmeta(st, RSF_KIND_KNOWN);
+  v.t = now;  // leave_time = now (base.rs:1355, 1364)
   *e = v;
   r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)ev << 32) | subj);
   return RSF_F_MEMBER_EVENT;

@@ -210,13 +210,22 @@ class GossipEngine:
         out["serf_state"] = ss
         return out
 
-    def view(self):
+    def view(self, with_time=False):
         n = self.n_loc * self.cfg.n_subjects
         lt = np.zeros(n, dtype=np.uint64)
         st = np.zeros(n, dtype=np.uint8)
         kd = np.zeros(n, dtype=np.uint8)
-        check(lib().rsf_gossip_dump_view(self._h, ptr(lt, C.c_uint64), ptr(st, C.c_uint8), ptr(kd, C.c_uint8)))
-        return lt, st, kd
+        tm = np.zeros(n, dtype=np.uint32)
+        check(lib().rsf_gossip_dump_view(self._h, ptr(lt, C.c_uint64), ptr(st, C.c_uint8), ptr(kd, C.c_uint8),
+                                          ptr(tm, C.c_uint32)))
+        return (lt, st, kd, tm) if with_time else (lt, st, kd)
+
+    # ---- Reaper tick (base.rs:519-601): times in rounds
+    def reap(self, now, reconnect_timeout, tombstone_timeout, recent_intent_timeout):
+        check(lib().rsf_gossip_reap(self._h, now, reconnect_timeout, tombstone_timeout, recent_intent_timeout))
+
+    def set_now(self, now):
+        check(lib().rsf_gossip_set_now(self._h, now))
 
     def queues(self):
         n = self.n_loc * 3 * self.cfg.queue_cap

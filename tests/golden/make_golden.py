@@ -119,6 +119,15 @@ def main():
                     ["witness", 41, 42], ["witness", 30, 42]],
         },
         "merge": {
+            "serf_reap_handler": {
+                "ref": "core/src/serf/base/tests/serf/reap.rs:41-131 (Reaper::run, base.rs:580-601)",
+                "tombstone_timeout_s": 6, "recent_intent_timeout_s": 7,
+                # left_members entries with leave_time = now - age
+                "left_ages_s": [0, 5, 10], "expect_left_remaining": 2,
+                # recent_intents: (node, type, ltime, age)
+                "intents": [["alice", "join", 1, 0], ["bob", "join", 2, 10], ["carol", "leave", 1, 0],
+                            ["doug", "leave", 2, 10]],
+                "expect_intents_kept": ["alice", "carol"]},
             "join_intent_buffer_early": {
                 "ref": "core/src/serf/base/tests/serf/join.rs:8-35",
                 "subject_known": False, "ltime": 10,

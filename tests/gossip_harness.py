@@ -51,6 +51,7 @@ def world_state(w, lo=0, hi=None):
         "v_ltime": O.arr(w.v_ltime, n * s, np.uint64).reshape(n, s)[sl],
         "v_status": O.arr(w.v_status, n * s, np.uint8).reshape(n, s)[sl],
         "v_kind": O.arr(w.v_kind, n * s, np.uint8).reshape(n, s)[sl],
+        "v_time": O.arr(w.v_time, n * s, np.uint32).reshape(n, s)[sl],
         "q_rumor": O.arr(w.q_rumor, n * 3 * q, np.uint32).reshape(n, 3 * q)[sl],
         "q_seq": O.arr(w.q_seq, n * 3 * q, np.uint32).reshape(n, 3 * q)[sl],
         "q_tx": O.arr(w.q_tx, n * 3 * q, np.uint16).reshape(n, 3 * q)[sl],
@@ -69,13 +70,14 @@ def world_state(w, lo=0, hi=None):
 def engine_state(g):
     n, s, q = g.n_loc, g.cfg.n_subjects, g.cfg.queue_cap
     m = g.members()
-    lt, stt, kd = g.view()
+    lt, stt, kd, vt = g.view(with_time=True)
     r, sq, tx, ln, ns = g.queues()
     ebl, ebc, ebk, qbl, qbc, qbi = g.buffers()
     return {
         "clock": m["clock"], "event_clock": m["event_clock"], "query_clock": m["query_clock"],
         "digest": m["digest"], "err": m["err"], "serf_state": m["serf_state"],
         "v_ltime": lt.reshape(n, s), "v_status": stt.reshape(n, s), "v_kind": kd.reshape(n, s),
+        "v_time": vt.reshape(n, s),
         "q_rumor": r.reshape(n, -1), "q_seq": sq.reshape(n, -1), "q_tx": tx.reshape(n, -1),
         "q_len": ln.reshape(n, -1), "q_next_seq": ns.reshape(n, 3),
         "eb_ltime": ebl.reshape(n, -1), "eb_cnt": ebc.reshape(n, -1), "eb_keys": ebk.reshape(n, -1),

@@ -82,7 +82,8 @@ class World(C.Structure):
                 ("q_next_seq", P32), ("eb_ltime", P64), ("eb_cnt", P32), ("eb_keys", P64),
                 ("qb_ltime", P64), ("qb_cnt", P32), ("qb_ids", P32),
                 ("rumors", C.POINTER(Rumor)), ("n_rumors", C.c_uint32), ("cap_rumors", C.c_uint32),
-                ("merges", C.c_uint64), ("sends", C.c_uint64), ("deliveries", C.c_uint64)]
+                ("merges", C.c_uint64), ("sends", C.c_uint64), ("deliveries", C.c_uint64),
+                ("v_time", P32), ("now", C.c_uint32)]
 
 
 class WorldCfg(C.Structure):
@@ -196,6 +197,7 @@ def lib():
     L.orc_pick_peers.restype = C.c_uint32
     L.orc_merge_remote_state.argtypes = [C.POINTER(World), C.c_uint32, C.POINTER(PPState), C.c_int, C.c_int]
     L.orc_push_pull.argtypes = [C.POINTER(World), P32, P32, C.c_uint32, C.c_int, C.c_int]
+    L.orc_reap.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
     L.orc_varint_len.argtypes = [C.c_uint64]
     L.orc_varint_len.restype = C.c_uint32
     L.orc_varint_encode.argtypes = [C.c_uint64, P8]

@@ -416,3 +416,28 @@ def test_retransmit_limit():
     # memberlist retransmitLimit = mult * ceil(log10(n+1)) (parity unpinned)
     for n, exp in [(1, 4), (9, 4), (10, 8), (99, 8), (100, 12), (1_000_000, 28), (999_999, 24)]:
         assert L.orc_retransmit_limit(4, n) == exp
+
+
+def test_serf_reap_handler(kats):
+    """Reaper tick (reap.rs:41-131): left members older than tombstone_timeout and
+    intents older than recent_intent_timeout go, the rest stay.  Each reference
+    left_members entry is its own subject here; time unit = seconds, now = 100."""
+    k = kats["merge"]["serf_reap_handler"]
+    ages, intents = k["left_ages_s"], k["intents"]
+    s = len(ages) + len(intents)
+    w = make_world(n=s + 2, s=s)
+    now = 100
+    for i, age in enumerate(ages):
+        set_known(w, 0, i, O.ST_LEFT, 0)
+        w.v_time[i] = now - age
+    for j, (_node, ty, lt, age) in enumerate(intents):
+        w.now = now - age
+        assert L.orc_upsert_intent(C.byref(w), 0, len(ages) + j, O.K_JOIN if ty == "join" else O.K_LEAVE, lt) == 1
+    d0 = w.digest[0]
+    L.orc_reap(C.byref(w), now, 1 << 30, k["tombstone_timeout_s"], k["recent_intent_timeout_s"])
+    left = [w.v_kind[i] == O.K_KNOWN and w.v_status[i] == O.ST_LEFT for i in range(len(ages))]
+    assert sum(left) == k["expect_left_remaining"]
+    kept = [node for j, (node, *_r) in enumerate(intents) if w.v_kind[len(ages) + j] != O.K_UNKNOWN]
+    assert kept == k["expect_intents_kept"]
+    assert w.digest[0] != d0  # one Reap member event was emitted
+    L.orc_world_free(C.byref(w))
