@@ -4,9 +4,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload gossip|vivaldi]
 
 One step = one pass of the hot path over one batch of synthetic input:
-  gossip  : one gossip round over the shard's members (BASELINE configs[1]:
-            1M members per GPU, fanout k=3, member-state merge + Lamport
-            clocks) -> metric "node-rounds/s"
+  gossip  : one gossip round over the shard's members -> metric "node-rounds/s".
+            Default 2M members per GPU: BASELINE's metric is quoted at 16M members
+            (configs[2], 16M over 8 GPUs); SURVEY §8(d) C3 weak-scales it at 2M/GPU
+            over 1/2/4/8 GPUs, so N=1 runs one 2M shard.  configs[1] (1M on one GPU)
+            is `--members 1000000`.
   vivaldi : one Vivaldi round (every member probes one neighbour and runs
             CoordinateClient::update) (configs[4]) -> "Vivaldi updates/s"
 Multi-GPU: one process per GPU (torch.distributed over RCCL), members sharded
@@ -268,7 +270,7 @@ def main():
             cpu = cpu_baseline_pushpull(args)
     else:
         from bench_gossip import run_gossip, cpu_baseline_gossip
-        args.members = args.members or 1_000_000
+        args.members = args.members or 2_000_000
         res = run_gossip(args, rank, world)
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:

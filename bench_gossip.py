@@ -112,7 +112,9 @@ def run_gossip(args, rank, world):
         "ms_per_step": wall / args.steps * 1e3, "dtype": "u64",
         "config": {"workload": f"gossip rounds, {n} members ({per}/GPU), fanout k=3, {SUBJECTS} tracked subjects, "
                                f"1% of members originate a join/leave intent per round, member-state merge + "
-                               f"Lamport clocks (BASELINE configs[1]{'/[2]' if world > 1 else ''})",
+                               f"Lamport clocks ("
+                               + ("BASELINE configs[2] shard: 2M members/GPU, 16M at 8 GPUs)" if per == 2_000_000
+                                  else "BASELINE configs[1])" if per == 1_000_000 and world == 1 else "custom size)"),
                    "members": n, "members_per_gpu": per, "fanout": 3, "items_per_target": 8,
                    "queue_cap_per_queue": cfg.queue_cap, "subjects": SUBJECTS,
                    "settle_rounds": SETTLE_ROUNDS, "parallelism": f"members sharded x{world}"},

@@ -393,6 +393,26 @@ int rsf_gossip_totals(rsf_gossip* g, uint64_t* merged_total);
 int rsf_gossip_last_round_stats(rsf_gossip* g, uint64_t* records_sent, uint64_t* records_merged);
 
 /* ======================================================================== */
+/* User-event coalescer (UserEventCoalescer, core/src/coalesce/user.rs:52-97) */
+/* ======================================================================== */
+/* One event handed to a coalescer (handle() == true: cc events only); 24 bytes.
+ * `group` names the coalescer (e.g. the member whose event stream it is), `name`
+ * the event name (interned), `payload` an opaque key carried through. */
+typedef struct rsf_user_event {
+  uint32_t group, name;
+  uint64_t ltime;
+  uint64_t payload;
+} rsf_user_event;
+/* coalesce() of every event in array order, then flush(), for all groups at once:
+ * out receives, group by ascending group, the flushed events — names in first-
+ * insertion (IndexMap) order, each name's events with its final maximum ltime in
+ * arrival order (a larger ltime clears the name's list, an equal one appends, an
+ * older one is dropped).  Device pointers; *n_out (host) = events written;
+ * synchronises the stream. */
+int rsf_coalesce_user_events(const rsf_user_event* in, uint64_t n, rsf_user_event* out, uint64_t* n_out,
+                             void* stream);
+
+/* ======================================================================== */
 /* Wire codecs                                              */
 /* ======================================================================== */
 /* All pointers are device memory; calls are asynchronous on `stream`

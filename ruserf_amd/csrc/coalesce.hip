@@ -1,0 +1,156 @@
+// coalesce.hip — UserEventCoalescer (core/src/coalesce/user.rs:52-97) for many
+// coalescers at once (one per member's event stream), as sorts and scans.
+//
+// Per coalescer the reference keeps an IndexMap name -> (latest ltime, events):
+// an event with a larger ltime clears the name's list, an equal ltime appends,
+// an older one is dropped; flush drains names in first-insertion order.  So an
+// event survives iff its ltime equals its name's final maximum, and the flush
+// order is (name's first arrival, arrival).  On the GPU:
+//   1. stable radix sort of (group, name) keys, arrival index as value
+//   2. segment heads -> segment ids (scan), segmented max of ltime, first arrival
+//   3. survivors keyed (group, first arrival of their name), stable sort, gather.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "../../include/ruserf_amd.h"
+#include "rsf_internal.h"
+
+namespace {
+
+inline unsigned grid1(uint64_t n, unsigned b = 256) { return (unsigned)((n + b - 1) / b); }
+
+__global__ void ce_keys_kernel(const rsf_user_event* __restrict__ in, uint64_t n, uint64_t* __restrict__ key,
+                               uint32_t* __restrict__ idx) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  key[i] = ((uint64_t)in[i].group << 32) | in[i].name;
+  idx[i] = (uint32_t)i;
+}
+
+// head flags (as u32 for the scan) and the ltimes in sorted order
+__global__ void ce_heads_kernel(const rsf_user_event* __restrict__ in, const uint64_t* __restrict__ key,
+                                const uint32_t* __restrict__ idx, uint64_t n, uint32_t* __restrict__ head,
+                                uint64_t* __restrict__ lt) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  head[i] = (i == 0 || key[i] != key[i - 1]) ? 1u : 0u;
+  lt[i] = in[idx[i]].ltime;
+}
+
+// seg[i] = inclusive scan of heads (1-based segment id); per segment: start index
+__global__ void ce_starts_kernel(const uint32_t* __restrict__ head, const uint32_t* __restrict__ seg, uint64_t n,
+                                 uint32_t* __restrict__ start) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (head[i]) start[seg[i] - 1] = (uint32_t)i;
+}
+
+// per segment: max ltime (a serial walk per segment would be unbounded; this is
+// an atomic max over the segment's elements instead)
+__global__ void ce_segmax_kernel(const uint32_t* __restrict__ seg, const uint64_t* __restrict__ lt, uint64_t n,
+                                 unsigned long long* __restrict__ segmax) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = seg[i] - 1;
+  // most segments are runs of one: skip the atomic unless a neighbour shares the segment
+  const bool alone = (i == 0 || seg[i - 1] != seg[i]) && (i + 1 == n || seg[i + 1] != seg[i]);
+  if (alone) segmax[s] = lt[i];
+  else atomicMax(&segmax[s], (unsigned long long)lt[i]);
+}
+
+// survivors: key2 = (group, first arrival of the name), value = arrival index
+__global__ void ce_survivors_kernel(const uint64_t* __restrict__ key, const uint32_t* __restrict__ idx,
+                                    const uint32_t* __restrict__ seg, const uint32_t* __restrict__ start,
+                                    const uint64_t* __restrict__ lt, const unsigned long long* __restrict__ segmax,
+                                    uint64_t n, uint64_t* __restrict__ key2, uint32_t* __restrict__ flag) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = seg[i] - 1;
+  flag[i] = lt[i] == (uint64_t)segmax[s] ? 1u : 0u;
+  key2[i] = (key[i] & 0xFFFFFFFF00000000ull) | idx[start[s]];  // stable sort: the segment's first = first arrival
+}
+
+__global__ void ce_gather_kernel(const rsf_user_event* __restrict__ in, const uint32_t* __restrict__ order,
+                                 uint64_t n, rsf_user_event* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = in[order[i]];
+}
+
+struct Scratch {
+  hipStream_t st;
+  void* p = nullptr;
+  explicit Scratch(hipStream_t s) : st(s) {}
+  ~Scratch() {
+    if (p) hipFreeAsync(p, st);
+  }
+};
+
+}  // namespace
+
+extern "C" int rsf_coalesce_user_events(const rsf_user_event* in, uint64_t n, rsf_user_event* out, uint64_t* n_out,
+                                        void* stream) {
+  if (!n_out || (n && (!in || !out))) return rsf::set_error(RSF_ERR_ARG, "null argument");
+  *n_out = 0;
+  if (n == 0) return RSF_OK;
+  if (n >= 0x7FFFFFFFull) return rsf::set_error(RSF_ERR_ARG, "batch too large");
+  hipStream_t st = (hipStream_t)stream;
+  const int ni = (int)n;
+  // buffers: key/key_s/key2/key2_s u64 x4, idx/idx_s/head/seg/start/flag/sel_v/ord u32 x8, lt u64, segmax u64
+  size_t tmp_sort = 0, tmp_scan = 0, tmp_sel = 0, tmp_sort2 = 0;
+  uint64_t *key = nullptr, *key_s = nullptr, *key2 = nullptr, *key2_s = nullptr, *lt = nullptr;
+  uint32_t *idx = nullptr, *idx_s = nullptr, *head = nullptr, *seg = nullptr, *start = nullptr, *flag = nullptr,
+           *sel_k_unused = nullptr, *sel_v = nullptr, *ord = nullptr;
+  (void)sel_k_unused;
+  unsigned long long* segmax = nullptr;
+  uint64_t* sel_k = nullptr;
+  int* d_nsel = nullptr;
+  RSF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_sort, key, key_s, idx, idx_s, ni, 0, 64, st));
+  RSF_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tmp_scan, head, seg, ni, st));
+  RSF_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp_sel, key2, flag, sel_k, d_nsel, ni, st));
+  size_t tmp_sel2 = 0;
+  RSF_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp_sel2, idx_s, flag, sel_v, d_nsel, ni, st));
+  RSF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_sort2, key2, key2_s, sel_v, ord, ni, 0, 64, st));
+  size_t tmp = std::max(std::max(tmp_sort, tmp_scan), std::max(std::max(tmp_sel, tmp_sel2), tmp_sort2));
+  const size_t n8 = ((size_t)n * 8 + 255) & ~(size_t)255, n4 = ((size_t)n * 4 + 255) & ~(size_t)255;
+  const size_t total = 6 * n8 + 8 * n4 + 256 + ((tmp + 255) & ~(size_t)255);
+  Scratch sc(st);
+  RSF_HIP(hipMallocAsync(&sc.p, total, st));
+  char* b = (char*)sc.p;
+  auto take8 = [&](void* pp) { *(char**)pp = b; b += n8; };
+  auto take4 = [&](void* pp) { *(char**)pp = b; b += n4; };
+  take8(&key); take8(&key_s); take8(&key2); take8(&key2_s); take8(&lt); take8(&segmax);
+  take4(&idx); take4(&idx_s); take4(&head); take4(&seg); take4(&start); take4(&flag); take4(&sel_v); take4(&ord);
+  d_nsel = (int*)b;
+  b += 256;
+  void* t = b;
+  sel_k = key2_s;  // the selected survivor keys land here, then sort back into key2
+  const unsigned g = grid1(n);
+  hipLaunchKernelGGL(ce_keys_kernel, dim3(g), dim3(256), 0, st, in, n, key, idx);
+  size_t tb = tmp;
+  RSF_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, key, key_s, idx, idx_s, ni, 0, 64, st));
+  hipLaunchKernelGGL(ce_heads_kernel, dim3(g), dim3(256), 0, st, in, key_s, idx_s, n, head, lt);
+  tb = tmp;
+  RSF_HIP(hipcub::DeviceScan::InclusiveSum(t, tb, head, seg, ni, st));
+  RSF_HIP(hipMemsetAsync(segmax, 0, (size_t)n * 8, st));
+  hipLaunchKernelGGL(ce_starts_kernel, dim3(g), dim3(256), 0, st, head, seg, n, start);
+  hipLaunchKernelGGL(ce_segmax_kernel, dim3(g), dim3(256), 0, st, seg, lt, n, segmax);
+  hipLaunchKernelGGL(ce_survivors_kernel, dim3(g), dim3(256), 0, st, key_s, idx_s, seg, start, lt, segmax, n, key2,
+                     flag);
+  RSF_HIP(hipGetLastError());
+  tb = tmp;
+  RSF_HIP(hipcub::DeviceSelect::Flagged(t, tb, key2, flag, sel_k, d_nsel, ni, st));
+  tb = tmp;
+  RSF_HIP(hipcub::DeviceSelect::Flagged(t, tb, idx_s, flag, sel_v, d_nsel, ni, st));
+  int nsel = 0;
+  RSF_HIP(hipMemcpyAsync(&nsel, d_nsel, sizeof(int), hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipStreamSynchronize(st));
+  if (nsel > 0) {
+    tb = tmp;
+    RSF_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, sel_k, key2, sel_v, ord, nsel, 0, 64, st));
+    hipLaunchKernelGGL(ce_gather_kernel, dim3(grid1((uint64_t)nsel)), dim3(256), 0, st, in, ord, (uint64_t)nsel, out);
+    RSF_HIP(hipGetLastError());
+  }
+  *n_out = (uint64_t)nsel;
+  return RSF_OK;
+}
