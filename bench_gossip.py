@@ -99,13 +99,13 @@ def run_gossip(args, rank, world):
         merged_all, err_all = float(merged), float(err_members)
     node_rounds = n * args.steps
     avg = [x / max(1, nr) for x in phase_ms]  # ms per round per phase
-    names = ["begin (memberlist+refute+originate)", "emit_kernel", "sort" + ("+exchange" if world > 1 else ""),
-             "segment+merge_kernel"]
+    names = ["begin (memberlist+refute+originate)", "peers+group sort", "emit_kernel" + ("+exchange" if world > 1 else ""),
+             "merge_kernel"]
     senders = per
     records = merged / max(1, args.steps)  # records per round on this shard
     emit_b, merge_b = kernel_bytes(cfg.queue_cap, senders, records)
-    dom = 1 if avg[1] >= avg[3] else 3
-    dom_bytes = emit_b if dom == 1 else merge_b
+    dom = 2 if avg[2] >= avg[3] else 3
+    dom_bytes = emit_b if dom == 2 else merge_b
     achieved = dom_bytes / (avg[dom] / 1e3) / 1e9
     return {
         "metric": "gossip node-rounds/s", "value": node_rounds / wall, "unit": "node-rounds/s",

@@ -34,6 +34,9 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;
+// record decoration (what merge_kernel needs to address the view entry before the rumor
+// body arrives): the subject slot of an intent, or the queue of a query / user event
+constexpr uint32_t kDecQuery = 0xFFFFFFFEu, kDecEvent = 0xFFFFFFFDu, kDecViewMax = 0xFFFFFFF0u;
 
 // Wave-wide u64 min/max through DPP (row_ror inside 16-lane rows, then
 // row_bcast15 / row_bcast31 across rows, result in lane 63): VALU-only data
@@ -124,6 +127,7 @@ __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int lane) {
 // one transmit-limited queue held in registers: lane i owns slot i
 struct QRegs {
   uint32_t r, sq, tl;  // rumor id (kEmpty = free), insertion seq, transmits | len << 16
+  uint32_t dec = 0;    // emit only: the item's record decoration (subject / kDecQuery / kDecEvent)
 };
 
 __device__ __forceinline__ void q_load(const GCfg& c, const GState& s, uint64_t l, uint32_t q, uint32_t lane,
@@ -243,8 +247,9 @@ __device__ __forceinline__ void q_insert_batch(const GCfg& c, QRegs& Q, uint32_t
 // one get_broadcasts call on a sorted register-resident queue; returns bytes used.
 // The lowest unpicked lane that fits IS the reference's pick (lowest transmits, then
 // longest fitting, then newest): every skipped lower lane did not fit and never will.
+template <bool PERMUTE_DEC>
 __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uint32_t lane, int64_t limit,
-                                                    uint32_t recv, uint32_t* stage_key, uint32_t* stage_val,
+                                                    uint32_t* stage_val, uint32_t* stage_dec,
                                                     uint64_t out_base, uint32_t& nrec, uint32_t& err, bool& dirty) {
   const bool valid = lane < c.qcap;
   const bool live = valid && Q.r != kEmpty;
@@ -274,8 +279,8 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
     const uint32_t npick = (uint32_t)__popcll(pmask);
     const uint32_t rank = (uint32_t)__popcll(pmask & below_mask(lane));
     if (picked && nrec + rank < c.cap_t) {
-      stage_key[out_base + nrec + rank] = recv;
       stage_val[out_base + nrec + rank] = Q.r;
+      stage_dec[out_base + nrec + rank] = Q.dec;
     }
     if (nrec + npick > c.cap_t) err |= kErrStage;
     nrec += npick;
@@ -315,6 +320,7 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   Q.r = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.r);
   Q.sq = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.sq);
   Q.tl = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.tl);
+  if (PERMUTE_DEC) Q.dec = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.dec);
   return used;
 }
 
@@ -469,64 +475,98 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
   store_regs(s, l, r);
 }
 
-__global__ void __launch_bounds__(256) emit_kernel(GCfg c, GState s, uint32_t round, uint32_t* __restrict__ stage_key,
-                                                   uint32_t* __restrict__ stage_val) {
+// Peer selection (memberlist kRandomNodes model): attempts a = 0,1,2,... in order, each a
+// Philox draw over the other N-1 members, kept if live and not yet chosen, until `fanout`
+// peers.  One thread per member; grp_key[l*fanout + j] = j-th peer (kSentinel: none, or a
+// dead sender).  Sender l's records to its j-th peer form GROUP l*fanout + j.
+constexpr uint32_t kPeerBatch = 4;
+__global__ void __launch_bounds__(256) peers_kernel(GCfg c, GState s, uint32_t round, uint32_t* __restrict__ grp_key) {
+  const uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= c.n_loc) return;
+  const uint32_t m = (uint32_t)(c.lo + l);
+  uint32_t peers[8];
+  uint32_t np = 0;
+  if (s.alive[m]) {
+    const uint32_t attempts = 64 * c.fanout;
+    for (uint32_t a0 = 0; a0 < attempts && np < c.fanout; a0 += kPeerBatch) {
+      uint32_t p[kPeerBatch];
+      bool ok[kPeerBatch];
+#pragma unroll
+      for (uint32_t b = 0; b < kPeerBatch; ++b) {  // the batch's liveness loads go out together
+        u32x4 o = philox4x32_10(a0 + b, kPurposePeer << 24, m, round, c.k0, c.k1);
+        p[b] = mulhi32(o.x, (uint32_t)(c.N - 1));
+        if (p[b] >= m) p[b]++;
+        ok[b] = a0 + b < attempts && s.alive[p[b]] != 0;
+      }
+#pragma unroll
+      for (uint32_t b = 0; b < kPeerBatch; ++b) {
+        if (!ok[b] || np >= c.fanout) continue;
+        bool dup = false;
+        for (uint32_t j = 0; j < np; ++j) dup |= peers[j] == p[b];
+        if (!dup) peers[np++] = p[b];
+      }
+    }
+  }
+  for (uint32_t j = 0; j < c.fanout; ++j) grp_key[l * c.fanout + j] = j < np ? peers[j] : kSentinel;
+}
+
+// After the stable sort of the groups by receiver: slot[gid] = the group's position in
+// receiver order (where emit_kernel writes its records: cap_t slots per group), and, for
+// a context that merges its own records, each receiver's range of groups.
+__global__ void __launch_bounds__(256) grp_index_kernel(const uint32_t* __restrict__ key_s,
+                                                        const uint32_t* __restrict__ id_s, uint64_t n, uint64_t lo,
+                                                        uint32_t* __restrict__ slot, uint32_t* __restrict__ seg_start,
+                                                        uint32_t* __restrict__ seg_end) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t key = key_s[i];
+  if (key == kSentinel) return;
+  slot[id_s[i]] = (uint32_t)i;
+  if (seg_start) {
+    if (i == 0 || key_s[i - 1] != key) seg_start[key - lo] = (uint32_t)i;
+    if (i + 1 == n || key_s[i + 1] != key) seg_end[key - lo] = (uint32_t)(i + 1);
+  }
+}
+
+// ONE WAVE PER SENDER: lane i owns slot i of each of its three queues.  For each peer
+// (grp_key, from peers_kernel) broadcast_messages drains intent -> query -> event under
+// one byte budget; the group's records (rumor id + decoration) go to cap_t slots at the
+// group's sorted position, its record count to cnt_s.
+__global__ void __launch_bounds__(256) emit_kernel(GCfg c, GState s, const uint32_t* __restrict__ grp_key,
+                                                   const uint32_t* __restrict__ slot, uint32_t* __restrict__ cnt_s,
+                                                   uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   if (l >= c.n_loc) return;
-  const uint32_t m = (uint32_t)(c.lo + l);
-  // Independent loads first, in one round trip: own liveness, the three queue
-  // heads (sorted queues: a queue is empty iff its slot 0 is free) and the
-  // liveness of the first 64 Philox peer candidates.
-  const bool alive_m = s.alive[m] != 0;
+  // Independent loads first, in one round trip: the three queue heads (sorted queues: a
+  // queue is empty iff its slot 0 is free), the peers and their group slots.
   const uint32_t head = lane < 3 ? s.q_rumor[(l * 3 + lane) * c.qcap] : kEmpty;
-  const uint32_t attempts = 64 * c.fanout;
-  auto candidate = [&](uint32_t a, uint32_t& p) -> bool {
-    p = 0;
-    if (a >= attempts) return false;
-    u32x4 o = philox4x32_10(a, kPurposePeer << 24, m, round, c.k0, c.k1);
-    p = mulhi32(o.x, (uint32_t)(c.N - 1));
-    if (p >= m) p++;
-    return s.alive[p] != 0;
-  };
-  uint32_t p_first;
-  const bool ok_first = candidate(lane, p_first);
-  asm volatile("" ::: "memory");  // keep the loads above the exit (compiler barrier only)
-  if (!alive_m) return;
-  // kRandomNodes model: attempts a = 0,1,2,... in order, live, distinct, != m
-  uint32_t peers[8];
-  uint32_t np = 0;
-  for (uint32_t b0 = 0; b0 < attempts && np < c.fanout; b0 += kWave) {
-    uint32_t p = p_first;
-    bool ok = ok_first;
-    if (b0) ok = candidate(b0 + lane, p);
-    uint64_t mask = __ballot(ok);
-    while (mask && np < c.fanout) {
-      int li = __ffsll((long long)mask) - 1;
-      mask &= mask - 1;
-      uint32_t cand = __shfl(p, li);
-      bool dup = false;
-      for (uint32_t j = 0; j < np; ++j) dup |= (peers[j] == cand);
-      if (!dup) peers[np++] = cand;
-    }
-  }
+  const uint32_t gk = lane < c.fanout ? grp_key[l * c.fanout + lane] : kSentinel;
+  const uint32_t gs = lane < c.fanout ? slot[l * c.fanout + lane] : 0u;
+  const uint64_t pm = __ballot(gk != kSentinel);  // peers are a prefix of the fanout slots
+  const uint32_t np = (uint32_t)__popcll(pm);
   const bool ne0 = shfl_u32(head, 0) != kEmpty, ne1 = shfl_u32(head, 1) != kEmpty,
              ne2 = shfl_u32(head, 2) != kEmpty;
   if (np == 0 || !(ne0 || ne1 || ne2)) return;
-  QRegs Q0{kEmpty, 0, 0}, Q1{kEmpty, 0, 0}, Q2{kEmpty, 0, 0};
-  if (ne0) q_load(c, s, l, 0, lane, Q0);
+  QRegs Q0{kEmpty, 0, 0}, Q1{kEmpty, 0, 0, kDecQuery}, Q2{kEmpty, 0, 0, kDecEvent};
+  if (ne0) {
+    q_load(c, s, l, 0, lane, Q0);
+    // decoration of the intents: their subject slots (subject and type share one 8-B word)
+    if (Q0.r != kEmpty) Q0.dec = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(s.rumors + Q0.r) + 16);
+  }
   if (ne1) q_load(c, s, l, 1, lane, Q1);
   if (ne2) q_load(c, s, l, 2, lane, Q2);
   uint32_t err = 0;
   bool d0 = false, d1 = false, d2 = false;
   for (uint32_t j = 0; j < np; ++j) {
-    uint32_t recv = peers[j];
-    uint64_t out_base = (l * c.fanout + j) * c.cap_t;
+    const uint32_t gslot = shfl_u32(gs, j);
+    const uint64_t out_base = (uint64_t)gslot * c.cap_t;
     uint32_t nrec = 0;
     int64_t used = 0;
-    used += q_get_broadcasts(c, Q0, lane, (int64_t)c.limit - used, recv, stage_key, stage_val, out_base, nrec, err, d0);
-    used += q_get_broadcasts(c, Q1, lane, (int64_t)c.limit - used, recv, stage_key, stage_val, out_base, nrec, err, d1);
-    used += q_get_broadcasts(c, Q2, lane, (int64_t)c.limit - used, recv, stage_key, stage_val, out_base, nrec, err, d2);
+    used += q_get_broadcasts<true>(c, Q0, lane, (int64_t)c.limit - used, out_val, out_dec, out_base, nrec, err, d0);
+    used += q_get_broadcasts<false>(c, Q1, lane, (int64_t)c.limit - used, out_val, out_dec, out_base, nrec, err, d1);
+    used += q_get_broadcasts<false>(c, Q2, lane, (int64_t)c.limit - used, out_val, out_dec, out_base, nrec, err, d2);
+    if (lane == 0 && nrec) cnt_s[gslot] = min(nrec, c.cap_t);
   }
   if (d0) q_store(c, s, l, 0, lane, Q0, true);
   if (d1) q_store(c, s, l, 1, lane, Q1, true);
@@ -538,13 +578,14 @@ __global__ void __launch_bounds__(256) emit_kernel(GCfg c, GState s, uint32_t ro
 // subject) and to pick the queue, written beside the sorted rumor ids so the
 // merge issues its view-entry load in the same round trip as the rumor-body
 // load instead of after it.
-constexpr uint32_t kDecQuery = 0xFFFFFFFEu, kDecEvent = 0xFFFFFFFDu, kDecViewMax = 0xFFFFFFF0u;
 __device__ __forceinline__ uint32_t decorate(const rsf_rumor* __restrict__ rumors, uint32_t rid) {
-  const rsf_rumor* p = rumors + rid;
-  const uint8_t t = p->type;
+  // subject and type share one aligned 8-B word (offset 16): one load, no dependent second one
+  static_assert(offsetof(rsf_rumor, subject) == 16 && offsetof(rsf_rumor, type) == 20, "rumor layout");
+  const uint2 w = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(rumors + rid) + 16);
+  const uint8_t t = (uint8_t)w.y;
   if (t == RSF_MSG_QUERY) return kDecQuery;
   if (t == RSF_MSG_USER_EVENT) return kDecEvent;
-  return p->subject;
+  return w.x;
 }
 
 // segment bounds per receiver + record decoration (keys == nullptr: decoration only)
@@ -562,11 +603,29 @@ __global__ void __launch_bounds__(256) segment_kernel(const uint32_t* __restrict
   if (dec) dec[i] = decorate(rumors, vals[i]);
 }
 
-__global__ void __launch_bounds__(256) first_sentinel_kernel(const uint32_t* __restrict__ keys, uint64_t n,
-                                                             unsigned long long* n_valid) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// ---- multi-GPU send side: the records of the receiver-sorted groups (cap_t slots each,
+// cnt[i] used) compacted into one receiver-ordered record stream [end[i-1], end[i])
+// (end = inclusive scan of cnt); the last valid group publishes the record count.
+// kLanesPerGroup lanes per group, one record per lane.
+constexpr uint32_t kLanesPerGroup = 16;
+__global__ void __launch_bounds__(256) grp_expand_kernel(const uint32_t* __restrict__ key_s,
+                                                         const uint32_t* __restrict__ end, uint64_t n,
+                                                         uint32_t cap_t, const uint32_t* __restrict__ slots,
+                                                         uint32_t* __restrict__ out_key, uint32_t* __restrict__ out_val,
+                                                         unsigned long long* n_valid) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i = t / kLanesPerGroup;
+  const uint32_t sub = (uint32_t)t % kLanesPerGroup;
   if (i >= n) return;
-  if (keys[i] == kSentinel && (i == 0 || keys[i - 1] != kSentinel)) *n_valid = i;
+  const uint32_t key = key_s[i];
+  if (key == kSentinel) return;
+  const uint32_t o = i ? end[i - 1] : 0u, e = end[i];
+  const uint32_t* src = slots + i * cap_t;
+  for (uint32_t k = sub; o + k < e; k += kLanesPerGroup) {
+    out_val[o + k] = src[k];
+    out_key[o + k] = key;
+  }
+  if (sub == 0 && (i + 1 == n || key_s[i + 1] == kSentinel)) *n_valid = e;
 }
 
 // One wave per receiver, lane = record.  Records arrive in canonical
@@ -613,10 +672,15 @@ __device__ unsigned long long g_merge_prof[8];
 #ifndef RSF_MERGE_UNIFORM
 #define RSF_MERGE_UNIFORM 1  // 1: the wave's member index is made scalar (readfirstlane)
 #endif
+// Input layouts: flat (gcnt == nullptr, stride 1): records [seg_start, seg_end) in
+// canonical order; grouped (emit_kernel's): groups [seg_start, seg_end) of `stride`
+// slots each, group g holding gcnt[g] records, so lane = slot and the empty slots of a
+// group are holes (invalid lanes) in an otherwise canonical lane order.
 __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GState s, const uint32_t* __restrict__ vals,
                                                     const uint32_t* __restrict__ dec,
                                                     const uint32_t* __restrict__ seg_start,
-                                                    const uint32_t* __restrict__ seg_end) {
+                                                    const uint32_t* __restrict__ seg_end,
+                                                    const uint32_t* __restrict__ gcnt, uint32_t stride) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
 #if RSF_MERGE_UNIFORM
   const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -653,15 +717,27 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
   ViewE* vrow = s.view + l * c.S;
   MPROF_T(t_setup);
   MPROF_ADD(0, t_start, t_setup);
-  for (uint32_t base = st; base < en; base += kWave) {
+  const uint64_t vs = (uint64_t)st * stride, ve = (uint64_t)en * stride;
+  for (uint64_t base = vs; base < ve; base += kWave) {
     MPROF_T(t_c0);
-    const uint32_t cnt = min((uint32_t)kWave, en - base);
-    const bool valid = lane < cnt;
-    const uint32_t rid = valid ? vals[base + lane] : 0;
+    const uint32_t cnt = (uint32_t)min((uint64_t)kWave, ve - base);  // lanes in this chunk
+    const uint64_t slot = base + lane;
+    const bool in = lane < cnt;
+    // slot contents and the group's record count in one round trip (holes read stale ids)
+    const uint32_t rid0 = in ? vals[slot] : 0;
+    uint32_t gk = 1, gc = 1;
+    if (gcnt && in) {
+      const uint64_t g = slot / stride;
+      gk = (uint32_t)(slot - g * stride);
+      gc = gcnt[g];
+    }
 #if RSF_MERGE_DEC
     // decoration (same round trip as the rumor ids): subject of an intent, or the
     // queue of an event / query; invalid lanes read as neither
-    const uint32_t dsub = valid ? dec[base + lane] : kEmpty;
+    const uint32_t dsub0 = in ? dec[slot] : kEmpty;
+    const bool valid = in && (!gcnt || gk < gc);
+    const uint32_t rid = valid ? rid0 : 0;
+    const uint32_t dsub = valid ? dsub0 : kEmpty;
     const bool is_view = dsub < kDecViewMax;
     if (!ld1 && __ballot(dsub == kDecQuery)) {
       q_load(c, s, l, 1, lane, Q1);
@@ -677,6 +753,8 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
     if (is_view) pre = vrow[dsub];  // issued beside the rumor-body load
     const uint32_t my_subj = is_view ? dsub : 0xFFFFFFFFu;
 #else
+    const bool valid = in && (!gcnt || gk < gc);
+    const uint32_t rid = valid ? rid0 : 0;
     rsf_rumor ru{};
     if (valid) ru = s.rumors[rid];
     const bool is_view = valid && (ru.type == RSF_MSG_JOIN || ru.type == RSF_MSG_LEAVE);
@@ -821,7 +899,7 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
     }
     MPROF_T(t_c3);
     MPROF_ADD(3, t_c2, t_c3);
-    if (base + kWave < en) __threadfence_block();  // next chunk's prefetch must see this chunk's view stores
+    if (base + kWave < ve) __threadfence_block();  // next chunk's prefetch must see this chunk's view stores
   }
   MPROF_T(t_st0);
   if (d0) q_store(c, s, l, 0, lane, Q0, true);
@@ -1103,6 +1181,11 @@ __global__ void init_views_kernel(ViewE* view, uint64_t n_loc, uint32_t S, const
   view[i] = v;
 }
 
+__global__ void iota_u32_kernel(uint32_t* p, uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = (uint32_t)i;
+}
+
 __global__ void fill_u64_kernel(uint64_t* p, uint64_t n, uint64_t v) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
@@ -1248,6 +1331,14 @@ struct rsf_gossip {
   void* pp_buf = nullptr;  // push/pull snapshot slab (grow-only)
   uint64_t pp_cap = 0;
   uint32_t* rec_dec = nullptr;  // record decoration beside sort_val (segment_kernel / runs_scatter_kernel)
+  // record groups (emit_kernel): [n_loc * fanout] receiver / count, sorted copies, ids, offsets
+  uint64_t n_groups = 0;
+  // record groups: [n_loc * fanout] peers (emit order) -> sorted by receiver (key_s, id_s);
+  // slot[gid] = sorted position; cnt[sorted] = records; off = inclusive scan of cnt (multi-GPU)
+  uint32_t *grp_key = nullptr, *grp_cnt = nullptr, *grp_key_s = nullptr, *grp_id = nullptr, *grp_id_s = nullptr,
+           *grp_slot = nullptr, *grp_off = nullptr, *stage_dec = nullptr;
+  void* grp_scan_tmp = nullptr;
+  size_t grp_scan_bytes = 0;
   uint64_t* send_buf = nullptr;
   unsigned long long* d_counters = nullptr;  // [0] n_valid, [1..] shard bounds
   void* sort_tmp = nullptr;
@@ -1378,13 +1469,29 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
       GA(s.rumors, (size_t)cfg->max_rumors * sizeof(rsf_rumor)))
     return fail(rc);
   g->stage_cap = n * c.fanout * c.cap_t;
+  if (g->stage_cap >= 0xFFFFFFFFull) return fail(gerr("n_members x fanout x per-target records must fit 32 bits"));
   g->recv_cap = g->stage_cap + g->stage_cap / 2 + 4096;
   const uint64_t pipe = std::max(g->stage_cap, g->recv_cap);
   if (GA(g->stage_key, pipe * 4) || GA(g->stage_val, pipe * 4) || GA(g->sort_key, pipe * 4) ||
       GA(g->sort_val, pipe * 4) || GA(g->seg_start, n * 4) || GA(g->seg_end, n * 4) || GA(g->send_buf, pipe * 8) || GA(g->rec_dec, pipe * 4) ||
       GA(g->d_counters, 64 * 8))
     return fail(rc);
+  g->n_groups = n * c.fanout;
+  if (GA(g->grp_key, g->n_groups * 4) || GA(g->grp_cnt, g->n_groups * 4) || GA(g->grp_key_s, g->n_groups * 4) ||
+      GA(g->grp_id, g->n_groups * 4) || GA(g->grp_id_s, g->n_groups * 4) || GA(g->grp_slot, g->n_groups * 4) ||
+      GA(g->grp_off, g->n_groups * 4) || GA(g->stage_dec, g->stage_cap * 4))
+    return fail(rc);
 #undef GA
+  {
+    size_t tb = 0, tr = 0;
+    if (hipcub::DeviceScan::InclusiveSum(nullptr, tb, g->grp_cnt, g->grp_off, (int)g->n_groups, g->stream) !=
+            hipSuccess ||
+        hipcub::DeviceReduce::Sum(nullptr, tr, g->grp_cnt, (unsigned long long*)g->d_counters, (int)g->n_groups,
+                                  g->stream) != hipSuccess)
+      return fail(rsf::set_error(RSF_ERR_HIP, "hipcub scan sizing failed"));
+    g->grp_scan_bytes = std::max(tb, tr);
+    if ((rc = dmalloc(&g->grp_scan_tmp, tb))) return fail(rc);
+  }
   size_t tmp = 0;
   if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, g->stage_key, g->sort_key, g->stage_val, g->sort_val,
                                          (int)pipe, 0, g->end_bit, g->stream) != hipSuccess)
@@ -1421,6 +1528,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   hipLaunchKernelGGL(fill_u64_kernel, dim3(grid1(n)), dim3(256), 0, st, s.clock, n, 1ull);
   hipLaunchKernelGGL(fill_u64_kernel, dim3(grid1(n)), dim3(256), 0, st, s.eclock, n, 1ull);
   hipLaunchKernelGGL(fill_u64_kernel, dim3(grid1(n)), dim3(256), 0, st, s.qclock, n, 1ull);
+  hipLaunchKernelGGL(iota_u32_kernel, dim3(grid1(g->n_groups)), dim3(256), 0, st, g->grp_id, g->n_groups);
   if (hipStreamSynchronize(st) != hipSuccess) return fail(rsf::set_error(RSF_ERR_HIP, "context init sync failed"));
   *out = g;
   return RSF_OK;
@@ -1437,7 +1545,8 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   s.qb_ltime, s.qb_cnt,    s.qb_ids,       s.rumors,      g->d_ml,    g->d_acts,    g->stage_key,
                   g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters, g->rec_dec, g->pp_buf,
                   g->sort_tmp, g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
-                  g->scan_tmp};
+                  g->scan_tmp, g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
+                  g->grp_slot, g->grp_off, g->stage_dec, g->grp_scan_tmp};
   for (void* p : ptrs)
     if (p) hipFree(p);
   g->scratch.release();
@@ -1660,30 +1769,55 @@ int rsf_gossip_rumor_block(rsf_gossip* g, void** p, uint64_t* bytes) {
 
 }  // extern "C"
 
-static int emit_and_sort(rsf_gossip* g, uint32_t round) {
+// Emission in canonical order.  peers_kernel draws every sender's peers; a stable radix
+// sort of the GROUPS (sender, peer) by receiver (n_loc * fanout keys, not records) fixes
+// where each group's records go, so emit_kernel writes them in merge order directly:
+// cap_t slots per group, in (receiver; sender, position) order, with the group's count.
+// local: this context merges its own records (single context): also each receiver's
+// range of groups for merge_kernel.  Otherwise the groups are compacted into one
+// receiver-ordered record stream (sort_key / sort_val, n_valid) for the exchange.
+static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local) {
   const GCfg& c = g->c;
   hipStream_t st = g->stream;
-  RSF_HIP(hipMemsetAsync(g->stage_key, 0xFF, g->stage_cap * 4, st));
-  hipLaunchKernelGGL(emit_kernel, dim3(grid1(c.n_loc, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0, st, c, g->s,
-                     round, g->stage_key, g->stage_val);
+  const uint64_t ng = g->n_groups;
+  hipLaunchKernelGGL(peers_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, c, g->s, round, g->grp_key);
+  RSF_HIP(hipGetLastError());
+  int rc = sort_pairs(g, g->grp_key, g->grp_key_s, g->grp_id, g->grp_id_s, ng);
+  if (rc) return rc;
+  RSF_HIP(hipMemsetAsync(g->grp_cnt, 0, ng * 4, st));
+  if (local) {
+    RSF_HIP(hipMemsetAsync(g->seg_start, 0, c.n_loc * 4, st));
+    RSF_HIP(hipMemsetAsync(g->seg_end, 0, c.n_loc * 4, st));
+  }
+  hipLaunchKernelGGL(grp_index_kernel, dim3(grid1(ng)), dim3(256), 0, st, g->grp_key_s, g->grp_id_s, ng, c.lo,
+                     g->grp_slot, local ? g->seg_start : nullptr, local ? g->seg_end : nullptr);
   RSF_HIP(hipGetLastError());
   mark(g, 2);
-  int rc = sort_pairs(g, g->stage_key, g->sort_key, g->stage_val, g->sort_val, g->stage_cap);
-  if (rc) return rc;
-  // n_valid = index of the first sentinel (records of dead/absent slots sort last)
-  hipLaunchKernelGGL(fill_u64_kernel, dim3(1), dim3(64), 0, st, (uint64_t*)g->d_counters, 1ull,
-                     (uint64_t)g->stage_cap);
-  hipLaunchKernelGGL(first_sentinel_kernel, dim3(grid1(g->stage_cap)), dim3(256), 0, st, g->sort_key, g->stage_cap,
-                     g->d_counters);
+  hipLaunchKernelGGL(emit_kernel, dim3(grid1(c.n_loc, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0, st, c, g->s,
+                     g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec);
   RSF_HIP(hipGetLastError());
+  size_t tb = g->grp_scan_bytes;
+  if (local) {
+    RSF_HIP(hipcub::DeviceReduce::Sum(g->grp_scan_tmp, tb, g->grp_cnt, (unsigned long long*)g->d_counters, (int)ng,
+                                      st));
+  } else {
+    RSF_HIP(hipcub::DeviceScan::InclusiveSum(g->grp_scan_tmp, tb, g->grp_cnt, g->grp_off, (int)ng, st));
+    RSF_HIP(hipMemsetAsync(g->d_counters, 0, 8, st));
+    hipLaunchKernelGGL(grp_expand_kernel, dim3(grid1(ng * kLanesPerGroup)), dim3(256), 0, st, g->grp_key_s,
+                       g->grp_off, ng, c.cap_t, g->stage_val, g->sort_key, g->sort_val, g->d_counters);
+    RSF_HIP(hipGetLastError());
+  }
   mark(g, 3);
   return RSF_OK;
 }
 
-static int launch_merge(rsf_gossip* g, const uint32_t* vals) {
+// grouped: the records are emit_kernel's groups (stage_val / stage_dec, cap_t slots, grp_cnt);
+// otherwise a flat record stream (vals, rec_dec)
+static int launch_merge(rsf_gossip* g, const uint32_t* vals, bool grouped = false) {
   const GCfg& c = g->c;
   hipLaunchKernelGGL(merge_kernel, dim3(grid1(c.n_loc, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0, g->stream,
-                     c, g->s, vals, (const uint32_t*)g->rec_dec, g->seg_start, g->seg_end);
+                     c, g->s, grouped ? g->stage_val : vals, grouped ? g->stage_dec : (const uint32_t*)g->rec_dec,
+                     g->seg_start, g->seg_end, grouped ? g->grp_cnt : nullptr, grouped ? c.cap_t : 1u);
   RSF_HIP(hipGetLastError());
   mark(g, 4);
   return RSF_OK;
@@ -1709,10 +1843,10 @@ int rsf_gossip_round(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml, uint
   if (g->c.n_loc != g->c.N) return gerr("sharded context: use round_begin / round_emit / round_merge");
   int rc = rsf_gossip_round_begin(g, round, ml, n_ml, acts, n_acts);
   if (rc) return rc;
-  if ((rc = emit_and_sort(g, round))) return rc;
+  if ((rc = emit_and_sort(g, round, true))) return rc;
   g->merged_from_stage = true;
   hipLaunchKernelGGL(accumulate_kernel, dim3(1), dim3(64), 0, g->stream, g->d_counters);
-  return segment_and_merge(g, g->sort_key, g->sort_val, g->stage_cap);
+  return launch_merge(g, nullptr, true);
 }
 
 int rsf_gossip_round_emit(rsf_gossip* g, uint32_t world, uint64_t* send_counts) {
@@ -1720,7 +1854,7 @@ int rsf_gossip_round_emit(rsf_gossip* g, uint32_t world, uint64_t* send_counts) 
   const GCfg& c = g->c;
   if (c.N % world || c.n_loc != c.N / world) return gerr("shards must be equal contiguous ranges of n_members");
   RSF_HIP(hipSetDevice(g->device));
-  int rc = emit_and_sort(g, g->cur_round);
+  int rc = emit_and_sort(g, g->cur_round, false);
   if (rc) return rc;
   hipStream_t st = g->stream;
   hipLaunchKernelGGL(shard_bounds_kernel, dim3(1), dim3(64), 0, st, g->sort_key, g->d_counters, c.N / world, world,

@@ -7,7 +7,8 @@ Per round:
                      the round is owned by exactly one shard
   2. all-reduce    — SUM of the round's rumor block (non-owners hold zeros), so
                      every shard can resolve every rumor id it will receive
-  3. round_emit    — emission + stable sort by global receiver; the sorted
+  3. round_emit    — peer draw + stable sort of the record groups by global receiver,
+                     emission in that order, compaction into one stream; the sorted
                      stream is already grouped by destination shard
   4. all-to-all    — record counts, then the packed (receiver << 32 | rumor)
                      records; received chunks are concatenated in source-rank

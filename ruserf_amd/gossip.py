@@ -274,7 +274,7 @@ class GossipEngine:
         check(lib().rsf_gossip_set_profiling(self._h, 1 if on else 0))
 
     def phase_times(self):
-        """Summed device ms of [begin, emit, sort(+exchange), merge] and the rounds covered."""
+        """Summed device ms of [begin, peers + group sort, emit(+exchange), merge] and the rounds covered."""
         ms = (C.c_double * 4)()
         r = C.c_uint32()
         check(lib().rsf_gossip_phase_times(self._h, ms, C.byref(r)))
