@@ -654,66 +654,87 @@ __device__ unsigned long long g_merge_prof[8];
 #define MPROF_T(v)
 #define MPROF_ADD(i, a, b)
 #endif
-#ifndef RSF_MERGE_HEADSKIP
-#define RSF_MERGE_HEADSKIP 0  // 1: skip loading a queue whose slot 0 is free (measured slower: spills + a dependent probe)
-#endif
 #ifndef RSF_MERGE_DEC
 #define RSF_MERGE_DEC 1  // 1: view-entry loads addressed from the record decoration (one round trip less)
-#endif
-#ifndef RSF_MERGE_EAGER
-#define RSF_MERGE_EAGER (!RSF_MERGE_DEC)  // 0: load the query/event queues only when a chunk needs them
 #endif
 #ifndef RSF_MERGE_BATCH
 #define RSF_MERGE_BATCH 1  // 1: a chunk's intent re-queues go in with one q_insert_batch
 #endif
-#ifndef RSF_MERGE_HOIST
-#define RSF_MERGE_HOIST 1  // 1: queue/register loads issued before the segment-bounds check
-#endif
-#ifndef RSF_MERGE_UNIFORM
-#define RSF_MERGE_UNIFORM 1  // 1: the wave's member index is made scalar (readfirstlane)
-#endif
-// Input layouts: flat (gcnt == nullptr, stride 1): records [seg_start, seg_end) in
-// canonical order; grouped (emit_kernel's): groups [seg_start, seg_end) of `stride`
-// slots each, group g holding gcnt[g] records, so lane = slot and the empty slots of a
-// group are holes (invalid lanes) in an otherwise canonical lane order.
-__global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GState s, const uint32_t* __restrict__ vals,
-                                                    const uint32_t* __restrict__ dec,
-                                                    const uint32_t* __restrict__ seg_start,
-                                                    const uint32_t* __restrict__ seg_end,
-                                                    const uint32_t* __restrict__ gcnt, uint32_t stride) {
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-#if RSF_MERGE_UNIFORM
-  const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-#else
-  const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x / kWave);
-#endif
-  if (l >= c.n_loc) return;
-  const uint32_t m = (uint32_t)(c.lo + l);
+// What a receiver's merge needs before its records: segment bounds, liveness, the queues'
+// next insertion seqs and the member's registers, issued a receiver AHEAD (merge_kernel)
+// as ONE lane-distributed load: lane j fetches dword j of the setup (kSu* below) from its
+// own array, so the prefetch holds one vector register until merge_one reads the fields
+// out with readlane.  The intent queue is loaded by merge_one beside the first records.
+enum : uint32_t {
+  kSuStart, kSuEnd, kSuAlive, kSuSeq0, kSuSeq1, kSuSeq2, kSuClock, kSuEClock = kSuClock + 2,
+  kSuQClock = kSuEClock + 2, kSuEMin = kSuQClock + 2, kSuQMin = kSuEMin + 2, kSuDigest = kSuQMin + 2,
+  kSuErr = kSuDigest + 2, kSuSerf, kSuSubj, kSuLanes
+};
+// per-lane source: byte address = base + l * mult + off (alive / serf_state: the aligned
+// dword holding the byte)
+struct MSetupLane {
+  const char* base;
+  uint32_t mult, off;
+};
+__device__ __forceinline__ MSetupLane merge_setup_lane(const GCfg& c, const GState& s,
+                                                       const uint32_t* __restrict__ seg_start,
+                                                       const uint32_t* __restrict__ seg_end, uint32_t lane) {
+  const char* b = (const char*)seg_start;
+  uint32_t mult = 4, off = 0;
+  if (lane == kSuEnd) b = (const char*)seg_end;
+  if (lane == kSuAlive) b = (const char*)s.alive + c.lo, mult = 1;
+  if (lane >= kSuSeq0 && lane <= kSuSeq2) b = (const char*)s.q_next_seq, mult = 12, off = 4 * (lane - kSuSeq0);
+  const uint64_t* u64s[6] = {s.clock, s.eclock, s.qclock, s.emin, s.qmin, s.digest};
+#pragma unroll
+  for (uint32_t k = 0; k < 6; ++k)
+    if (lane == kSuClock + 2 * k || lane == kSuClock + 2 * k + 1)
+      b = (const char*)u64s[k], mult = 8, off = 4 * (lane - kSuClock - 2 * k);
+  if (lane == kSuErr) b = (const char*)s.err;
+  if (lane == kSuSerf) b = (const char*)s.serf_state, mult = 1;
+  if (lane == kSuSubj) b = (const char*)s.member_subj;
+  return MSetupLane{b, mult, off};
+}
+__device__ __forceinline__ uint32_t merge_setup(const MSetupLane& sl, uint64_t l, uint32_t lane) {
+  uint32_t v = 0;
+  if (lane < kSuLanes) {
+    const uintptr_t a = (uintptr_t)(sl.base + l * sl.mult + sl.off);
+    // a global (not flat) load: flat loads also count on lgkmcnt, which every ds_bpermute
+    // wait of the current receiver would then drain
+    v = *(const __attribute__((address_space(1))) uint32_t*)(a & ~(uintptr_t)3);
+    v >>= 8 * (uint32_t)(a & 3);  // byte fields: shift the byte down
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t su64(uint32_t v, uint32_t k) {
+  return ((uint64_t)shfl_u32(v, k + 1) << 32) | shfl_u32(v, k);
+}
+
+// One receiver (one wave).  Input layouts: flat (gcnt == nullptr, stride 1): records
+// [seg_start, seg_end) in canonical order; grouped (emit_kernel's): groups [seg_start,
+// seg_end) of `stride` slots each, group g holding gcnt[g] records, so lane = slot and the
+// empty slots of a group are holes (invalid lanes) in an otherwise canonical lane order.
+// Query/event queues are loaded on first need; a queue is written back only if something
+// was inserted.
+__device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const uint32_t* __restrict__ vals,
+                                          const uint32_t* __restrict__ dec, const uint32_t* __restrict__ gcnt,
+                                          uint32_t stride, uint64_t l, uint32_t lane, uint32_t su) {
   MPROF_T(t_start);
-  const uint32_t st = seg_start[l], en = seg_end[l];
-  const bool skip = st >= en || !s.alive[m];
-  if (!RSF_MERGE_HOIST && skip) return;
-  // The intent queue and the member's registers do not depend on the segment
-  // bounds: with RSF_MERGE_HOIST they are issued in the same round trip (the
-  // 5% of receivers without records pay one wasted queue read for it).
-  // Query/event queues are loaded on first need and every queue is written
-  // back only if something was inserted.
+  const uint32_t st = shfl_u32(su, kSuStart), en = shfl_u32(su, kSuEnd);
+  if (st >= en || (shfl_u32(su, kSuAlive) & 0xFF) == 0) return;
   QRegs Q0{kEmpty, 0, 0}, Q1{kEmpty, 0, 0}, Q2{kEmpty, 0, 0};
-  bool ld0 = true, ld1 = RSF_MERGE_EAGER, ld2 = RSF_MERGE_EAGER, d0 = false, d1 = false, d2 = false;
-  (void)ld0;
-  q_load(c, s, l, 0, lane, Q0);  // intents are the common case: load with the first prefetch
-  if (RSF_MERGE_EAGER) {
-    // a sorted queue is empty iff its slot 0 is free (wave-uniform probe): skip the load then
-    if (!RSF_MERGE_HEADSKIP || s.q_rumor[(l * 3 + 1) * c.qcap] != kEmpty) q_load(c, s, l, 1, lane, Q1);
-    if (!RSF_MERGE_HEADSKIP || s.q_rumor[(l * 3 + 2) * c.qcap] != kEmpty) q_load(c, s, l, 2, lane, Q2);
-  }
-  uint32_t nseq0 = s.q_next_seq[l * 3 + 0], nseq1 = s.q_next_seq[l * 3 + 1], nseq2 = s.q_next_seq[l * 3 + 2];
+  q_load(c, s, l, 0, lane, Q0);  // intents are the common case
+  bool ld1 = false, ld2 = false, d0 = false, d1 = false, d2 = false;
+  uint32_t nseq0 = shfl_u32(su, kSuSeq0), nseq1 = shfl_u32(su, kSuSeq1), nseq2 = shfl_u32(su, kSuSeq2);
   MRegs r;
-  load_regs(s, l, r);
-  if (RSF_MERGE_HOIST) {
-    asm volatile("" ::: "memory");  // keep the loads above the exit (compiler barrier only)
-    if (skip) return;
-  }
+  r.clock = su64(su, kSuClock);
+  r.eclock = su64(su, kSuEClock);
+  r.qclock = su64(su, kSuQClock);
+  r.emin = su64(su, kSuEMin);
+  r.qmin = su64(su, kSuQMin);
+  r.digest = su64(su, kSuDigest);
+  r.err = shfl_u32(su, kSuErr);
+  r.serf_state = (uint8_t)shfl_u32(su, kSuSerf);
+  r.subj = (int32_t)shfl_u32(su, kSuSubj);
   ViewE* vrow = s.view + l * c.S;
   MPROF_T(t_setup);
   MPROF_ADD(0, t_start, t_setup);
@@ -915,6 +936,36 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
   MPROF_ADD(4, t_st0, t_end);
   MPROF_ADD(5, t_start, t_end);
   if (lane == 0) { MPROF_ADD(6, 0, 1); }
+}
+
+// Persistent waves (grid = what fits on the chip at once): wave w merges receivers
+// w, w + nw, w + 2nw, ... and issues the NEXT receiver's setup loads before merging the
+// current one, so that round trip overlaps this receiver's work instead of starting it.
+// Receivers are independent (each touches only its own view row, queues and registers).
+#ifndef RSF_MERGE_PERSIST
+#define RSF_MERGE_PERSIST 0  // 1: persistent waves (measured 14% slower than hardware wave dispatch)
+#endif
+__global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GState s, const uint32_t* __restrict__ vals,
+                                                    const uint32_t* __restrict__ dec,
+                                                    const uint32_t* __restrict__ seg_start,
+                                                    const uint32_t* __restrict__ seg_end,
+                                                    const uint32_t* __restrict__ gcnt, uint32_t stride) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  if (l >= c.n_loc) return;
+  const MSetupLane sl = merge_setup_lane(c, s, seg_start, seg_end, lane);
+  uint32_t cur = merge_setup(sl, l, lane);
+  for (;;) {
+    const uint64_t ln = l + nw;
+    const bool more = RSF_MERGE_PERSIST && ln < c.n_loc;
+    uint32_t nxt = 0;
+    if (more) nxt = merge_setup(sl, ln, lane);
+    merge_one(c, s, vals, dec, gcnt, stride, l, lane, cur);
+    if (!more) break;
+    cur = nxt;
+    l = ln;
+  }
 }
 
 // ---- push/pull anti-entropy (M7): merge_remote_state of a sender's local_state
@@ -1339,6 +1390,7 @@ struct rsf_gossip {
            *grp_slot = nullptr, *grp_off = nullptr, *stage_dec = nullptr;
   void* grp_scan_tmp = nullptr;
   size_t grp_scan_bytes = 0;
+  unsigned merge_blocks = 1;  // merge_kernel's persistent grid: resident blocks per CU x CUs
   uint64_t* send_buf = nullptr;
   unsigned long long* d_counters = nullptr;  // [0] n_valid, [1..] shard bounds
   void* sort_tmp = nullptr;
@@ -1490,6 +1542,11 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
                                   g->stream) != hipSuccess)
       return fail(rsf::set_error(RSF_ERR_HIP, "hipcub scan sizing failed"));
     g->grp_scan_bytes = std::max(tb, tr);
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, merge_kernel, kWave * kWavesPerBlock, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+      return fail(rsf::set_error(RSF_ERR_HIP, "occupancy query failed"));
+    g->merge_blocks = (unsigned)std::max(1, per_cu * cus);
     if ((rc = dmalloc(&g->grp_scan_tmp, tb))) return fail(rc);
   }
   size_t tmp = 0;
@@ -1815,7 +1872,9 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local) {
 // otherwise a flat record stream (vals, rec_dec)
 static int launch_merge(rsf_gossip* g, const uint32_t* vals, bool grouped = false) {
   const GCfg& c = g->c;
-  hipLaunchKernelGGL(merge_kernel, dim3(grid1(c.n_loc, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0, g->stream,
+  const unsigned blocks = RSF_MERGE_PERSIST ? std::min<unsigned>(grid1(c.n_loc, kWavesPerBlock), g->merge_blocks)
+                                            : grid1(c.n_loc, kWavesPerBlock);
+  hipLaunchKernelGGL(merge_kernel, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, g->stream,
                      c, g->s, grouped ? g->stage_val : vals, grouped ? g->stage_dec : (const uint32_t*)g->rec_dec,
                      g->seg_start, g->seg_end, grouped ? g->grp_cnt : nullptr, grouped ? c.cap_t : 1u);
   RSF_HIP(hipGetLastError());
