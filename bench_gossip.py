@@ -29,16 +29,19 @@ def gossip_cfg(n_total, rounds_total, world, shard=None):
                         retransmit_mult=4, max_refute=4, max_rumors=per_round * rounds_total + 1024, seed=SEED)
 
 
-def kernel_bytes(qcap, senders, records):
-    """Algorithmic HBM bytes (roofline):
-    emit  : per live sender the three queues are scanned (rumor id, insertion seq,
-            transmits|len = 12 B per slot), picked slots' transmit words written
-            back (4 B) and records emitted (receiver + rumor id = 8 B)
-    merge : per received record B_merge = 64 B (record 16, view slot read 16 +
-            write 16, clock r/w 16) plus each receiver's queue
-            state read (12 B per slot)."""
-    emit = senders * 3 * qcap * 12 + records * (4 + 8)
-    merge = records * 64 + senders * 3 * qcap * 12
+def kernel_bytes(qcap, senders, records, fanout=3):
+    """Algorithmic HBM bytes per launch, what each kernel must move in
+    this workload (intents only: the query/event queues stay empty and are never
+    loaded; the intent queue is 12 B per slot: rumor id, insertion seq, transmits|len):
+    emit  : per live sender its peers + group slots (8 B per peer), the intent queue
+            read and written back (it is re-ranked after every pick), and per record
+            the rumor id + decoration written (8 B), per group its count (4 B)
+    merge : per received record SURVEY's B_merge = 64 B (record 16, view entry read 16
+            + write 16, clock r/w 16) plus each receiver's intent queue read and
+            written back (re-queues)."""
+    queue_rw = 2 * qcap * 12
+    emit = senders * (fanout * 8 + queue_rw + fanout * 4) + records * 8
+    merge = records * 64 + senders * queue_rw
     return emit, merge
 
 
@@ -117,6 +120,7 @@ def run_gossip(args, rank, world):
                                   else "BASELINE configs[1])" if per == 1_000_000 and world == 1 else "custom size)"),
                    "members": n, "members_per_gpu": per, "fanout": 3, "items_per_target": 8,
                    "queue_cap_per_queue": cfg.queue_cap, "subjects": SUBJECTS,
+                   "record_slots_per_group": min(3 * cfg.queue_cap, cfg.gossip_limit // (cfg.gossip_overhead + 18)),
                    "settle_rounds": SETTLE_ROUNDS, "parallelism": f"members sharded x{world}"},
         "merges_per_s": merged_all / wall,
         "records_per_round_per_gpu": records,

@@ -654,9 +654,6 @@ __device__ unsigned long long g_merge_prof[8];
 #define MPROF_T(v)
 #define MPROF_ADD(i, a, b)
 #endif
-#ifndef RSF_MERGE_DEC
-#define RSF_MERGE_DEC 1  // 1: view-entry loads addressed from the record decoration (one round trip less)
-#endif
 #ifndef RSF_MERGE_BATCH
 #define RSF_MERGE_BATCH 1  // 1: a chunk's intent re-queues go in with one q_insert_batch
 #endif
@@ -709,6 +706,19 @@ __device__ __forceinline__ uint64_t su64(uint32_t v, uint32_t k) {
   return ((uint64_t)shfl_u32(v, k + 1) << 32) | shfl_u32(v, k);
 }
 
+// The query and event queues of a wave's receiver, parked in LDS between uses: only
+// query / event records touch them, and holding them in registers beside the intent
+// path spilled it at the 8-wave register cap.
+struct QLds {
+  uint32_t r[kWave], sq[kWave], tl[kWave];
+};
+__device__ __forceinline__ void qlds_put(QLds& q, uint32_t lane, const QRegs& Q) {
+  q.r[lane] = Q.r;
+  q.sq[lane] = Q.sq;
+  q.tl[lane] = Q.tl;
+}
+__device__ __forceinline__ QRegs qlds_get(const QLds& q, uint32_t lane) { return QRegs{q.r[lane], q.sq[lane], q.tl[lane]}; }
+
 // One receiver (one wave).  Input layouts: flat (gcnt == nullptr, stride 1): records
 // [seg_start, seg_end) in canonical order; grouped (emit_kernel's): groups [seg_start,
 // seg_end) of `stride` slots each, group g holding gcnt[g] records, so lane = slot and the
@@ -717,11 +727,11 @@ __device__ __forceinline__ uint64_t su64(uint32_t v, uint32_t k) {
 // was inserted.
 __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const uint32_t* __restrict__ vals,
                                           const uint32_t* __restrict__ dec, const uint32_t* __restrict__ gcnt,
-                                          uint32_t stride, uint64_t l, uint32_t lane, uint32_t su) {
+                                          uint32_t stride, uint64_t l, uint32_t lane, uint32_t su, QLds* ql) {
   MPROF_T(t_start);
   const uint32_t st = shfl_u32(su, kSuStart), en = shfl_u32(su, kSuEnd);
   if (st >= en || (shfl_u32(su, kSuAlive) & 0xFF) == 0) return;
-  QRegs Q0{kEmpty, 0, 0}, Q1{kEmpty, 0, 0}, Q2{kEmpty, 0, 0};
+  QRegs Q0{kEmpty, 0, 0};
   q_load(c, s, l, 0, lane, Q0);  // intents are the common case
   bool ld1 = false, ld2 = false, d0 = false, d1 = false, d2 = false;
   uint32_t nseq0 = shfl_u32(su, kSuSeq0), nseq1 = shfl_u32(su, kSuSeq1), nseq2 = shfl_u32(su, kSuSeq2);
@@ -752,7 +762,6 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
       gk = (uint32_t)(slot - g * stride);
       gc = gcnt[g];
     }
-#if RSF_MERGE_DEC
     // decoration (same round trip as the rumor ids): subject of an intent, or the
     // queue of an event / query; invalid lanes read as neither
     const uint32_t dsub0 = in ? dec[slot] : kEmpty;
@@ -761,11 +770,15 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     const uint32_t dsub = valid ? dsub0 : kEmpty;
     const bool is_view = dsub < kDecViewMax;
     if (!ld1 && __ballot(dsub == kDecQuery)) {
-      q_load(c, s, l, 1, lane, Q1);
+      QRegs t{kEmpty, 0, 0};
+      q_load(c, s, l, 1, lane, t);
+      qlds_put(ql[0], lane, t);
       ld1 = true;
     }
     if (!ld2 && __ballot(dsub == kDecEvent)) {
-      q_load(c, s, l, 2, lane, Q2);
+      QRegs t{kEmpty, 0, 0};
+      q_load(c, s, l, 2, lane, t);
+      qlds_put(ql[1], lane, t);
       ld2 = true;
     }
     rsf_rumor ru{};
@@ -773,28 +786,6 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     ViewE pre{};
     if (is_view) pre = vrow[dsub];  // issued beside the rumor-body load
     const uint32_t my_subj = is_view ? dsub : 0xFFFFFFFFu;
-#else
-    const bool valid = in && (!gcnt || gk < gc);
-    const uint32_t rid = valid ? rid0 : 0;
-    rsf_rumor ru{};
-    if (valid) ru = s.rumors[rid];
-    const bool is_view = valid && (ru.type == RSF_MSG_JOIN || ru.type == RSF_MSG_LEAVE);
-    if (!ld0 && __ballot(is_view)) {
-      q_load(c, s, l, 0, lane, Q0);
-      ld0 = true;
-    }
-    if (!ld1 && __ballot(valid && ru.type == RSF_MSG_QUERY)) {
-      q_load(c, s, l, 1, lane, Q1);
-      ld1 = true;
-    }
-    if (!ld2 && __ballot(valid && ru.type == RSF_MSG_USER_EVENT)) {
-      q_load(c, s, l, 2, lane, Q2);
-      ld2 = true;
-    }
-    ViewE pre{};
-    if (is_view) pre = vrow[ru.subject];
-    const uint32_t my_subj = is_view ? ru.subject : 0xFFFFFFFFu;
-#endif
     // chains: previous / next record of the same subject in this chunk
     int prev = -1, next = -1;
     {
@@ -910,10 +901,14 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
             d0 = true;
           }
         } else if (q == kQQuery) {
-          q_insert_wave(c, Q1, lane, rid_i, mlen, nseq1++);
+          QRegs t = qlds_get(ql[0], lane);
+          q_insert_wave(c, t, lane, rid_i, mlen, nseq1++);
+          qlds_put(ql[0], lane, t);
           d1 = true;
         } else {
-          q_insert_wave(c, Q2, lane, rid_i, mlen, nseq2++);
+          QRegs t = qlds_get(ql[1], lane);
+          q_insert_wave(c, t, lane, rid_i, mlen, nseq2++);
+          qlds_put(ql[1], lane, t);
           d2 = true;
         }
       }
@@ -924,8 +919,8 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
   }
   MPROF_T(t_st0);
   if (d0) q_store(c, s, l, 0, lane, Q0, true);
-  if (d1) q_store(c, s, l, 1, lane, Q1, true);
-  if (d2) q_store(c, s, l, 2, lane, Q2, true);
+  if (d1) q_store(c, s, l, 1, lane, qlds_get(ql[0], lane), true);
+  if (d2) q_store(c, s, l, 2, lane, qlds_get(ql[1], lane), true);
   if (lane == 0) {
     store_regs(s, l, r);
     if (d0) s.q_next_seq[l * 3 + 0] = nseq0;
@@ -951,6 +946,8 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
                                                     const uint32_t* __restrict__ seg_end,
                                                     const uint32_t* __restrict__ gcnt, uint32_t stride) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
+  __shared__ QLds qlds[kWavesPerBlock][2];
+  QLds* ql = qlds[threadIdx.x / kWave];
   const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
   uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   if (l >= c.n_loc) return;
@@ -961,7 +958,7 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
     const bool more = RSF_MERGE_PERSIST && ln < c.n_loc;
     uint32_t nxt = 0;
     if (more) nxt = merge_setup(sl, ln, lane);
-    merge_one(c, s, vals, dec, gcnt, stride, l, lane, cur);
+    merge_one(c, s, vals, dec, gcnt, stride, l, lane, cur, ql);
     if (!more) break;
     cur = nxt;
     l = ln;

@@ -8,9 +8,9 @@ gfx950 corrections (measured by experiments/pmc_calib, profiles/r01/pmc_calibrat
   * WRITE_SIZE is exact for streaming stores.
 Vivaldi: the observe kernel's gather share is isolated by the ablation without the
 peer-row gather (experiments/viv_traffic.sh):  traffic = 2*stream + gather + WRITE.
-Gossip (segment + merge): the streamed bytes are modelled (queue state 3 x qcap x 12 B
-and 8 B of register/segment state per receiver, 4 B per record value) and corrected
-(x2); the rest of FETCH is gather:  traffic = FETCH + stream/2 + WRITE."""
+Gossip (merge_kernel): the streamed bytes are modelled (the intent queue, qcap x 12 B per
+receiver, and the (sender, peer) groups' record slots, cap_t x 8 B + a 4-B count each) and
+corrected (x2); the rest of FETCH is gather:  traffic = FETCH + stream/2 + WRITE."""
 import csv
 import collections
 import json
@@ -38,18 +38,18 @@ res["vivaldi"] = {"kernel": "vivaldi_observe_kernel<8,3,20>", "members_per_gpu":
 g = os.path.join(OUT, "prof_gossip_r01")
 f_merge = last(f"{g}_fetch/run_counter_collection.csv", "FETCH_SIZE", "merge_kernel")
 w_merge = last(f"{g}_write/run_counter_collection.csv", "WRITE_SIZE", "merge_kernel")
-f_seg = last(f"{g}_fetch/run_counter_collection.csv", "FETCH_SIZE", "segment_kernel")
-w_seg = last(f"{g}_write/run_counter_collection.csv", "WRITE_SIZE", "segment_kernel")
 line = next(json.loads(x) for x in open(f"{g}_trace.log") if x.startswith("{") and '"metric"' in x)
 n = line["config"]["members_per_gpu"]
-records = line["records_per_round_per_gpu"]
 qcap = line["config"]["queue_cap_per_queue"]
-stream_merge = n * (3 * qcap * 12 + 8) + records * 4
-stream_seg = f_seg * 2
-traffic = (f_merge + stream_merge / 2 + w_merge) + (stream_seg + w_seg)
-res["gossip"] = {"kernel": "segment+merge_kernel", "members_per_gpu": n, "traffic_bytes_per_launch": traffic,
-                 "fetch_counter": f_merge + f_seg, "write_counter": w_merge + w_seg,
-                 "stream_bytes_modelled": stream_merge + stream_seg,
+fanout = line["config"]["fanout"]
+cap_t = line["config"]["record_slots_per_group"]
+# coalesced streams of merge_kernel (tallied at 1/2 by FETCH_SIZE): the intent queue
+# (12 B per slot) and the group slots it reads (rumor id + decoration, 8 B per slot; one
+# group per (sender, peer), n * fanout in all) with their counts (4 B per group)
+stream_merge = n * qcap * 12 + n * fanout * (cap_t * 8 + 4)
+traffic = f_merge + stream_merge / 2 + w_merge
+res["gossip"] = {"kernel": "merge_kernel", "members_per_gpu": n, "traffic_bytes_per_launch": traffic,
+                 "fetch_counter": f_merge, "write_counter": w_merge, "stream_bytes_modelled": stream_merge,
                  "source": f"profiles/{RND}/gossip_r01_summary.md", "method": "FETCH + stream/2 + WRITE"}
 json.dump(res, open(os.path.join(ROOT, "profiles", "traffic.json"), "w"), indent=1)
 print(json.dumps(res, indent=1))

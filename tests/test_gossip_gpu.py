@@ -28,6 +28,7 @@ def pair(cfg, subj_member, views):
     (1500, 100, 10, 0.03, 16, 8 * 24),
     (700, 50, 15, 0.02, 8, 1400),
     (3000, 32, 8, 0.005, 64, 3 * 24),
+    (1000, 40, 8, 0.05, 64, 4000),  # 192 record slots per (sender, peer) group: groups span several chunks
 ])
 def test_intent_rounds_bit_exact(n, s, rounds, rate, qcap, limit):
     cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=qcap, gossip_limit=limit, max_rumors=1 << 16,
