@@ -538,22 +538,21 @@ __global__ void __launch_bounds__(256) emit_kernel(GCfg c, GState s, const uint3
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   if (l >= c.n_loc) return;
-  // Independent loads first, in one round trip: the three queue heads (sorted queues: a
-  // queue is empty iff its slot 0 is free), the peers and their group slots.
-  const uint32_t head = lane < 3 ? s.q_rumor[(l * 3 + lane) * c.qcap] : kEmpty;
+  // Independent loads first, in one round trip: the intent queue (the common case; a
+  // sorted queue is empty iff its slot 0 is free), the query/event queue heads, the peers
+  // and their group slots.
+  QRegs Q0{kEmpty, 0, 0}, Q1{kEmpty, 0, 0, kDecQuery}, Q2{kEmpty, 0, 0, kDecEvent};
+  q_load(c, s, l, 0, lane, Q0);
+  const uint32_t head = lane >= 1 && lane < 3 ? s.q_rumor[(l * 3 + lane) * c.qcap] : kEmpty;
   const uint32_t gk = lane < c.fanout ? grp_key[l * c.fanout + lane] : kSentinel;
   const uint32_t gs = lane < c.fanout ? slot[l * c.fanout + lane] : 0u;
   const uint64_t pm = __ballot(gk != kSentinel);  // peers are a prefix of the fanout slots
   const uint32_t np = (uint32_t)__popcll(pm);
-  const bool ne0 = shfl_u32(head, 0) != kEmpty, ne1 = shfl_u32(head, 1) != kEmpty,
+  const bool ne0 = shfl_u32(Q0.r, 0) != kEmpty, ne1 = shfl_u32(head, 1) != kEmpty,
              ne2 = shfl_u32(head, 2) != kEmpty;
   if (np == 0 || !(ne0 || ne1 || ne2)) return;
-  QRegs Q0{kEmpty, 0, 0}, Q1{kEmpty, 0, 0, kDecQuery}, Q2{kEmpty, 0, 0, kDecEvent};
-  if (ne0) {
-    q_load(c, s, l, 0, lane, Q0);
-    // decoration of the intents: their subject slots (subject and type share one 8-B word)
-    if (Q0.r != kEmpty) Q0.dec = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(s.rumors + Q0.r) + 16);
-  }
+  // decoration of the intents: their subject slots (subject and type share one 8-B word)
+  if (Q0.r != kEmpty) Q0.dec = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(s.rumors + Q0.r) + 16);
   if (ne1) q_load(c, s, l, 1, lane, Q1);
   if (ne2) q_load(c, s, l, 2, lane, Q2);
   uint32_t err = 0;
