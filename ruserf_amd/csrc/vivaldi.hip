@@ -360,14 +360,22 @@ __global__ void __launch_bounds__(256) probe_gen_kernel(VivParams p, uint32_t sl
 #ifndef RSF_VIV_WAVES
 #define RSF_VIV_WAVES 1  // min waves/SIMD for the observe kernel (a cap of 4 measured slower)
 #endif
+#ifndef RSF_VIV_COOP
+#define RSF_VIV_COOP 1  // 1: peer rows gathered two lanes per row through LDS (D == 8)
+#endif
 template <int D, int F, int WW, int ABL = 0, int FRT = (F <= 3 ? 4 : 8)>
 __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
     const double* __restrict__ cur, double* __restrict__ nxt, double* __restrict__ adj_win,
     uint32_t* __restrict__ adj_idx, double* __restrict__ filt, unsigned long long* resets,
     const uint32_t* __restrict__ peer_in, const uint64_t* __restrict__ rtt_in, int32_t* __restrict__ status,
     VivParams p, uint32_t slot) {
-  uint64_t local = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (local >= p.shard_n) return;
+  // D == 8: the peer rows are gathered two lanes per row (below), so every lane of the
+  // wave stays to take part; a lane past the shard end only helps with the gather.
+  constexpr bool kCoop = RSF_VIV_COOP && (D == 8) && !(ABL & 1);
+  const uint64_t local0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = local0 < p.shard_n;
+  if (!kCoop && !active) return;
+  const uint64_t local = active ? local0 : p.shard_n - 1;  // inactive lanes read a valid member, store nothing
   const uint32_t m = (uint32_t)(p.lo + local);
   const int FR = FRT;
   // ---- every independent load first: probe input, window index + window, own row, filter record
@@ -407,6 +415,41 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
     }
   }
   // ---- the dependent gather: the peer's row of the previous table
+  if constexpr (kCoop) {
+    // Two lanes per row, 48 B each, staged through LDS: one wave-instruction then touches
+    // 32 rows' pages instead of 64.  Uniformly random rows over a table of several GB are
+    // bound by address-translation reach, and halving the distinct pages per instruction
+    // took a 96-B row gather over 6.4 GB from 1.46 to 3.22 TB/s (experiments/gather_coop.hip,
+    // profiles/r01/gather_coop.txt).
+    __shared__ double2 prow[256 / 64][64][6];
+    double2(*pw)[6] = prow[threadIdx.x / 64];
+    const uint32_t lane = threadIdx.x & 63, half = lane & 1;
+    const uint32_t want = (active && peer < p.n) ? peer : 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t ps = 0; ps < 2; ++ps) {
+      const uint32_t who = 32 * ps + (lane >> 1);
+      const uint32_t pp = (uint32_t)__shfl((int)want, (int)who);
+      if (pp != 0xFFFFFFFFu) {
+        const double2* r2 = reinterpret_cast<const double2*>(cur + (uint64_t)pp * 12) + half * 3;
+        const double2 x0 = r2[0], x1 = r2[1], x2 = r2[2];
+        pw[who][half * 3 + 0] = x0;
+        pw[who][half * 3 + 1] = x1;
+        pw[who][half * 3 + 2] = x2;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const double2 t = pw[lane][i];
+      other[2 * i] = t.x;
+      other[2 * i + 1] = t.y;
+    }
+    oe = pw[lane][4].x;
+    oa = pw[lane][4].y;
+    oh = pw[lane][5].x;
+    if (!active) return;
+  }
   int st;
   if (peer >= p.n) {
     st = RSF_ERR_ARG;
@@ -415,7 +458,7 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
 #pragma unroll
       for (int i = 0; i < D; ++i) other[i] = me[i] + 0.01;
       oe = e; oa = a; oh = h;
-    } else {
+    } else if (!kCoop) {
       load_row<D>(cur + (uint64_t)peer * p.stride, other, oe, oa, oh, p.dim);
     }
     st = update_one<D, F, WW, FRT>(me, e, a, h, other, oe, oa, oh, p.dim, rtt_ns, rec, adj_win + local, p.shard_n,
