@@ -363,6 +363,9 @@ __global__ void __launch_bounds__(256) probe_gen_kernel(VivParams p, uint32_t sl
 #ifndef RSF_VIV_COOP
 #define RSF_VIV_COOP 1  // 1: peer rows gathered two lanes per row through LDS (D == 8)
 #endif
+#ifndef RSF_VIV_ROWT
+#define RSF_VIV_ROWT 1  // 1: own rows read / written as coalesced 1 KB pieces through LDS (D == 8)
+#endif
 template <int D, int F, int WW, int ABL = 0, int FRT = (F <= 3 ? 4 : 8)>
 __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
     const double* __restrict__ cur, double* __restrict__ nxt, double* __restrict__ adj_win,
@@ -393,10 +396,39 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
 #pragma unroll
   for (int i = 0; i < WW; ++i) win[i] = (ABL & 4) ? 0.0 : adj_win[(uint64_t)i * p.shard_n + local];
   double me[D], other[D], e, a, h, oe, oa, oh;
+  // D == 8: one 6 KB LDS block per wave, used in turn for the wave's own rows (read and
+  // written as 1 KB coalesced pieces, 16 B per lane, instead of six 16-B loads per lane at
+  // a 96-B stride) and for the peer rows.
+  constexpr bool kRowT = RSF_VIV_ROWT && kCoop && !(ABL & 8) && !(ABL & 16);
+  __shared__ double2 stage[kCoop ? 256 / 64 : 1][64 * 6];
+  double2* sw = stage[kCoop ? threadIdx.x / 64 : 0];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wbase = local0 - lane;  // the wave's first (shard-local) member
+  const uint32_t wrows = wbase >= p.shard_n ? 0u : (uint32_t)min((uint64_t)64, p.shard_n - wbase);
   if (ABL & 8) {
 #pragma unroll
     for (int i = 0; i < D; ++i) me[i] = 0.001 * (double)(m & 7);
     e = 1.0; a = 0.0; h = 1e-5;
+  } else if constexpr (kRowT) {
+    const double2* src = reinterpret_cast<const double2*>(cur + (p.lo + wbase) * 12);
+#pragma unroll
+    for (uint32_t k = 0; k < 6; ++k) {
+      const uint32_t i = lane + 64 * k;
+      if (i < wrows * 6) sw[i] = src[i];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const double2 t = sw[lane * 6 + i];
+      me[2 * i] = t.x;
+      me[2 * i + 1] = t.y;
+    }
+    e = sw[lane * 6 + 4].x;
+    a = sw[lane * 6 + 4].y;
+    h = sw[lane * 6 + 5].x;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   } else {
     load_row<D>(cur + (uint64_t)m * p.stride, me, e, a, h, p.dim);
   }
@@ -421,9 +453,7 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
     // bound by address-translation reach, and halving the distinct pages per instruction
     // took a 96-B row gather over 6.4 GB from 1.46 to 3.22 TB/s (experiments/gather_coop.hip,
     // profiles/r01/gather_coop.txt).
-    __shared__ double2 prow[256 / 64][64][6];
-    double2(*pw)[6] = prow[threadIdx.x / 64];
-    const uint32_t lane = threadIdx.x & 63, half = lane & 1;
+    const uint32_t half = lane & 1;
     const uint32_t want = (active && peer < p.n) ? peer : 0xFFFFFFFFu;
 #pragma unroll
     for (uint32_t ps = 0; ps < 2; ++ps) {
@@ -432,26 +462,27 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
       if (pp != 0xFFFFFFFFu) {
         const double2* r2 = reinterpret_cast<const double2*>(cur + (uint64_t)pp * 12) + half * 3;
         const double2 x0 = r2[0], x1 = r2[1], x2 = r2[2];
-        pw[who][half * 3 + 0] = x0;
-        pw[who][half * 3 + 1] = x1;
-        pw[who][half * 3 + 2] = x2;
+        sw[who * 6 + half * 3 + 0] = x0;
+        sw[who * 6 + half * 3 + 1] = x1;
+        sw[who * 6 + half * 3 + 2] = x2;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const double2 t = pw[lane][i];
+      const double2 t = sw[lane * 6 + i];
       other[2 * i] = t.x;
       other[2 * i + 1] = t.y;
     }
-    oe = pw[lane][4].x;
-    oa = pw[lane][4].y;
-    oh = pw[lane][5].x;
-    if (!active) return;
+    oe = sw[lane * 6 + 4].x;
+    oa = sw[lane * 6 + 4].y;
+    oh = sw[lane * 6 + 5].x;
+    if (!kRowT && !active) return;
   }
-  int st;
-  if (peer >= p.n) {
+  int st = RSF_OK;
+  if (!active) {
+  } else if (peer >= p.n) {
     st = RSF_ERR_ARG;
   } else {
     if (ABL & 1) {
@@ -464,13 +495,28 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
     st = update_one<D, F, WW, FRT>(me, e, a, h, other, oe, oa, oh, p.dim, rtt_ns, rec, adj_win + local, p.shard_n,
                                    adj_idx + local, p, m, p.round, resets, win, widx);
   }
-  if (status) status[local] = st;
-  if (!(ABL & 2) && st == RSF_OK) {
+  if (active && status) status[local] = st;
+  if (active && !(ABL & 2) && st == RSF_OK) {
     double2* f2 = reinterpret_cast<double2*>(frec);
 #pragma unroll
     for (int i = 0; i < FR / 2; ++i) f2[i] = make_double2(rec[2 * i], rec[2 * i + 1]);
   }
-  if (ABL & 16) {
+  if constexpr (kRowT) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sw[lane * 6 + i] = make_double2(me[2 * i], me[2 * i + 1]);
+    sw[lane * 6 + 4] = make_double2(e, a);
+    sw[lane * 6 + 5] = make_double2(h, 0.0);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    double2* dst = reinterpret_cast<double2*>(nxt + (p.lo + wbase) * 12);
+#pragma unroll
+    for (uint32_t k = 0; k < 6; ++k) {
+      const uint32_t i = lane + 64 * k;
+      if (i < wrows * 6) dst[i] = sw[i];
+    }
+  } else if (ABL & 16) {
     if (e == 12345.0) store_row<D>(nxt + (uint64_t)m * p.stride, me, e, a, h, p.dim);
   } else {
     store_row<D>(nxt + (uint64_t)m * p.stride, me, e, a, h, p.dim);
