@@ -11,8 +11,13 @@
 //                                          portion[dim], error, adjustment, height)
 //   adj  [W][shard_n] f64                  adjustment windows, window-slot-major (coalesced)
 //   adj_idx[shard_n] u32
-//   filt [peer_slots][shard_n][FR] f64     latency filter rings, FR = 4 (F<=3) or 8 (F<=7);
-//                                          the last f64 of a record holds len | head<<32.
+//   filt [peer_slots][shard_n][FR] f64     latency filter rings.  F <= 3: FR = 2, one 16-B
+//                                          record of the samples' u64 nanoseconds packed as
+//                                          34-bit fields (filter samples are as_secs_f64 of
+//                                          an rtt <= 10 s < 2^34 ns, so the f64 sample is
+//                                          rebuilt exactly) + len, head (2 bits each).
+//                                          F <= 7: FR = 8 f64 samples, the last word holds
+//                                          len | head<<32.
 //                                          Slot-major: a round probes one slot for every
 //                                          member, so its filter records stream coalesced.
 #include <hip/hip_runtime.h>
@@ -143,7 +148,11 @@ __device__ __forceinline__ bool finite(double x) { return isfinite(x); }
 // WW > 0: the window (WW samples, read by the caller into `win` BEFORE any
 // dependent work so all its loads are in flight together) and its index are
 // register-resident; WW == 0: generic runtime window size, read here.
-template <int D, int F, int WW, int FRT = (F <= 3 ? 4 : 8)>
+// f64 words per latency-filter record (see the layout note at the top)
+constexpr RSF_HD int filt_words(uint32_t F) { return F <= 3 ? 2 : 8; }
+constexpr uint64_t kNs34 = (1ull << 34) - 1;
+
+template <int D, int F, int WW, int FRT = filt_words(F)>
 __device__ __forceinline__ int update_one(double* me, double& err, double& adj, double& h,
                                           const double* other, double oerr, double oadj, double oh,
                                           uint32_t odim, uint64_t rtt_ns, double* frec,
@@ -163,7 +172,47 @@ __device__ __forceinline__ int update_one(double* me, double& err, double& adj, 
 
   // latency_filter (292-307): ring == Vec push/remove(0) for the median
   double rtt_seconds;
-  {
+  if constexpr (FRT == 2) {
+    // packed record: lo = ns0 | ns1<<34 (low 30 bits); hi = ns1>>30 | ns2<<4 | len<<38 | head<<40
+    const uint64_t lo = (uint64_t)__double_as_longlong(frec[0]), hi = (uint64_t)__double_as_longlong(frec[1]);
+    uint64_t ns[3] = {lo & kNs34, (lo >> 34) | ((hi & 0xFull) << 30), (hi >> 4) & kNs34};
+    uint32_t len = (uint32_t)(hi >> 38) & 3u, head = (uint32_t)(hi >> 40) & 3u;
+    const uint32_t Fr = p.F;
+    if (len < Fr) {
+      uint32_t pos = head + len;
+      if (pos >= Fr) pos -= Fr;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if ((uint32_t)i == pos) ns[i] = rtt_ns;
+      len++;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if ((uint32_t)i == head) ns[i] = rtt_ns;
+      head = (head + 1 == Fr) ? 0 : head + 1;
+    }
+    frec[0] = __longlong_as_double((long long)(ns[0] | (ns[1] << 34)));
+    frec[1] = __longlong_as_double(
+        (long long)((ns[1] >> 30) | (ns[2] << 4) | ((uint64_t)len << 38) | ((uint64_t)head << 40)));
+    // median of the len live samples (as_secs_f64 of each, sorted, index len/2)
+    double t[3];
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      uint32_t rel = ((uint32_t)i + Fr - head) % Fr;
+      if ((uint32_t)i < Fr && rel < len) t[c++] = as_secs_f64(ns[i]);
+    }
+    for (uint32_t i = 1; i < c; ++i) {
+      double v = t[i];
+      uint32_t j = i;
+      while (j > 0 && t[j - 1] > v) {
+        t[j] = t[j - 1];
+        --j;
+      }
+      t[j] = v;
+    }
+    rtt_seconds = t[c / 2];
+  } else {
     const int FR = FRT;
     uint64_t meta = __double_as_longlong(frec[FR - 1]);
     uint32_t len = (uint32_t)meta, head = (uint32_t)(meta >> 32);
@@ -366,7 +415,7 @@ __global__ void __launch_bounds__(256) probe_gen_kernel(VivParams p, uint32_t sl
 #ifndef RSF_VIV_ROWT
 #define RSF_VIV_ROWT 1  // 1: own rows read / written as coalesced 1 KB pieces through LDS (D == 8)
 #endif
-template <int D, int F, int WW, int ABL = 0, int FRT = (F <= 3 ? 4 : 8)>
+template <int D, int F, int WW, int ABL = 0, int FRT = filt_words(F)>
 __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
     const double* __restrict__ cur, double* __restrict__ nxt, double* __restrict__ adj_win,
     uint32_t* __restrict__ adj_idx, double* __restrict__ filt, unsigned long long* resets,
@@ -523,6 +572,127 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
   }
 }
 
+// The D == 8, W == 20 round kernel with its loads ordered for two overlapping round trips:
+// (1) the probe input, then the member-side streams (window, own rows, filter) issued
+// unconditionally (clamped addresses instead of per-load branches, which made every load
+// wait for all earlier ones); (2) the peer gather, issued as soon as the peer id returns,
+// so it travels while the member-side streams are still arriving instead of after them.
+// Own rows and peer rows go through two 6 KB LDS blocks per wave: own rows as coalesced
+// 1 KB pieces, peer rows two lanes per row (half the pages per wave-instruction).
+// Same arithmetic as vivaldi_observe_kernel<8, F, 20> (update_one).
+#ifndef RSF_VIV_PIPE
+#define RSF_VIV_PIPE 1
+#endif
+template <int F, int FRT = filt_words(F)>
+__global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_pipe_kernel(
+    const double* __restrict__ cur, double* __restrict__ nxt, double* __restrict__ adj_win,
+    uint32_t* __restrict__ adj_idx, double* __restrict__ filt, unsigned long long* resets,
+    const uint32_t* __restrict__ peer_in, const uint64_t* __restrict__ rtt_in, int32_t* __restrict__ status,
+    VivParams p, uint32_t slot) {
+  constexpr int D = 8, WW = 20, FR = FRT;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t local0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t wbase = local0 - lane;  // the wave's first shard-local member
+  if (wbase >= p.shard_n) return;        // wave-uniform: no lane of this wave has a member
+  const uint32_t wrows = (uint32_t)min((uint64_t)64, p.shard_n - wbase);
+  const bool active = lane < wrows;
+  const uint64_t local = active ? local0 : p.shard_n - 1;  // inactive lanes read a valid member, store nothing
+  const uint32_t m = (uint32_t)(p.lo + local);
+  // ---- round trip 1: probe input first, then every member-side stream
+  const uint32_t peer = peer_in[local];
+  const uint64_t rtt_ns = rtt_in[local];
+  const uint32_t widx = adj_idx[local];
+  double win[WW];
+#pragma unroll
+  for (int i = 0; i < WW; ++i) win[i] = adj_win[(uint64_t)i * p.shard_n + local];
+  const double2* src = reinterpret_cast<const double2*>(cur + (p.lo + wbase) * 12);
+  const uint32_t last = wrows * 6 - 1;
+  double2 own[6];
+#pragma unroll
+  for (uint32_t k = 0; k < 6; ++k) own[k] = src[min(lane + 64 * k, last)];
+  double* frec = filt + ((uint64_t)slot * p.shard_n + local) * FR;
+  double rec[FR];
+  {
+    const double2* f2 = reinterpret_cast<const double2*>(frec);
+#pragma unroll
+    for (int i = 0; i < FR / 2; ++i) {
+      const double2 t = f2[i];
+      rec[2 * i] = t.x;
+      rec[2 * i + 1] = t.y;
+    }
+  }
+  // ---- round trip 2: the peer rows of the previous table, two lanes per row
+  const uint32_t half = lane & 1;
+  const uint32_t want = (active && peer < p.n) ? peer : 0u;  // row 0 stands in for an error lane
+  // the rtt load would otherwise be sunk into update_one's branch as a third round trip;
+  // it was issued right after the peer id, so waiting for it here costs nothing
+  asm volatile("" ::"v"(rtt_ns));
+  double2 g[6];
+#pragma unroll
+  for (uint32_t ps = 0; ps < 2; ++ps) {
+    const uint32_t pp = (uint32_t)__shfl((int)want, (int)(32 * ps + (lane >> 1)));
+    const double2* r2 = reinterpret_cast<const double2*>(cur + (uint64_t)pp * 12) + half * 3;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) g[ps * 3 + j] = r2[j];
+  }
+  __shared__ double2 stage[256 / 64][2][64 * 6];
+  double2* so = stage[threadIdx.x / 64][0];
+  double2* sp = stage[threadIdx.x / 64][1];
+#pragma unroll
+  for (uint32_t k = 0; k < 6; ++k) so[lane + 64 * k] = own[k];
+#pragma unroll
+  for (uint32_t ps = 0; ps < 2; ++ps)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) sp[(32 * ps + (lane >> 1)) * 6 + half * 3 + j] = g[ps * 3 + j];
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  double me[D], other[D], e, a, h, oe, oa, oh;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const double2 t = so[lane * 6 + i];
+    me[2 * i] = t.x;
+    me[2 * i + 1] = t.y;
+    const double2 u = sp[lane * 6 + i];
+    other[2 * i] = u.x;
+    other[2 * i + 1] = u.y;
+  }
+  e = so[lane * 6 + 4].x;
+  a = so[lane * 6 + 4].y;
+  h = so[lane * 6 + 5].x;
+  oe = sp[lane * 6 + 4].x;
+  oa = sp[lane * 6 + 4].y;
+  oh = sp[lane * 6 + 5].x;
+  int st = RSF_OK;
+  if (!active) {
+  } else if (peer >= p.n) {
+    st = RSF_ERR_ARG;
+  } else {
+    st = update_one<D, F, WW, FRT>(me, e, a, h, other, oe, oa, oh, p.dim, rtt_ns, rec, adj_win + local, p.shard_n,
+                                   adj_idx + local, p, m, p.round, resets, win, widx);
+  }
+  if (active && status) status[local] = st;
+  if (active && st == RSF_OK) {
+    double2* f2 = reinterpret_cast<double2*>(frec);
+#pragma unroll
+    for (int i = 0; i < FR / 2; ++i) f2[i] = make_double2(rec[2 * i], rec[2 * i + 1]);
+  }
+  // ---- own rows back out through LDS as coalesced 1 KB pieces
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) so[lane * 6 + i] = make_double2(me[2 * i], me[2 * i + 1]);
+  so[lane * 6 + 4] = make_double2(e, a);
+  so[lane * 6 + 5] = make_double2(h, 0.0);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  double2* dst = reinterpret_cast<double2*>(nxt + (p.lo + wbase) * 12);
+#pragma unroll
+  for (uint32_t k = 0; k < 6; ++k) {
+    const uint32_t i = lane + 64 * k;
+    if (i <= last) dst[i] = so[i];
+  }
+}
+
 template <int D, int F>
 __global__ void __launch_bounds__(256) vivaldi_batch_kernel(
     double* __restrict__ table, double* __restrict__ adj_win, uint32_t* __restrict__ adj_idx,
@@ -532,7 +702,7 @@ __global__ void __launch_bounds__(256) vivaldi_batch_kernel(
     int32_t* __restrict__ status, double* __restrict__ rows_out, VivParams p) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int FR = (F <= 3) ? 4 : 8;
+  const int FR = filt_words(F);
   uint32_t m = member[i];
   uint64_t local = m - p.lo;
   uint32_t q = slot[i];
@@ -580,7 +750,7 @@ __global__ void __launch_bounds__(256) vivaldi_ack_kernel(
     const uint64_t* __restrict__ rtt, uint64_t n, int32_t* __restrict__ status, VivParams p) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int FR = (F <= 3) ? 4 : 8;
+  const int FR = filt_words(F);
   const uint32_t m = member[i];
   const uint64_t local = m - p.lo;
   const uint64_t a = off[i], b = off[i + 1];
@@ -712,7 +882,7 @@ int rsf_vivaldi_create(rsf_vivaldi** out, uint64_t n, uint64_t lo, uint64_t hi, 
   p.dim = o->dimensionality;
   p.W = o->adjustment_window_size;
   p.F = o->latency_filter_size;
-  p.FR = p.F <= 3 ? 4 : 8;
+  p.FR = filt_words(p.F);
   p.stride = rsf_coord_row_stride(p.dim);
   p.k0 = (uint32_t)seed;
   p.k1 = (uint32_t)(seed >> 32);
@@ -983,7 +1153,10 @@ int rsf_vivaldi_observe(rsf_vivaldi* v, uint32_t slot, const uint32_t* peer, con
   unsigned blocks = (unsigned)((p.shard_n + 255) / 256);
   const double* cur = v->table[v->cur];
   double* nxt = v->table[v->cur ^ 1];
-  if (p.dim == 8 && p.F <= 3 && p.W == 20)
+  if (RSF_VIV_PIPE && p.dim == 8 && p.F <= 3 && p.W == 20 && p.stride == 12 && RSF_VIV_ROUND_WW == 20)
+    hipLaunchKernelGGL((vivaldi_observe_pipe_kernel<3>), dim3(blocks), dim3(256), 0, v->stream, cur, nxt, v->adj,
+                       v->adj_idx, v->filt, v->resets, peer, rtt_ns, status_out, p, slot);
+  else if (p.dim == 8 && p.F <= 3 && p.W == 20)
     hipLaunchKernelGGL((vivaldi_observe_kernel<8, 3, RSF_VIV_ROUND_WW>), dim3(blocks), dim3(256), 0, v->stream,
                        cur, nxt, v->adj, v->adj_idx, v->filt, v->resets, peer, rtt_ns, status_out, p, slot);
   else
