@@ -10,7 +10,7 @@
 //   table[2][n_members][row_stride] f64   ping-pong coordinate tables (AoS rows:
 //                                          portion[dim], error, adjustment, height)
 //   adj  [W][shard_n] f64                  adjustment windows, window-slot-major (coalesced)
-//   adj_idx[shard_n] u32
+//   adj_idx[shard_n] u8 (W <= 64)
 //   filt [peer_slots][shard_n][FR] f64     latency filter rings.  F <= 3: FR = 2, one 16-B
 //                                          record of the samples' u64 nanoseconds packed as
 //                                          34-bit fields (filter samples are as_secs_f64 of
@@ -156,7 +156,7 @@ template <int D, int F, int WW, int FRT = filt_words(F), bool NTS = false>
 __device__ __forceinline__ int update_one(double* me, double& err, double& adj, double& h,
                                           const double* other, double oerr, double oadj, double oh,
                                           uint32_t odim, uint64_t rtt_ns, double* frec,
-                                          double* adj_col, uint64_t adj_stride, uint32_t* adj_idx_p,
+                                          double* adj_col, uint64_t adj_stride, uint8_t* adj_idx_p,
                                           const VivParams& p, uint32_t member, uint32_t round,
                                           unsigned long long* resets, const double* win = nullptr,
                                           uint32_t win_idx = 0) {
@@ -282,10 +282,10 @@ __device__ __forceinline__ int update_one(double* me, double& err, double& adj, 
     const uint32_t nidx = (idx + 1 == (uint32_t)WW) ? 0 : idx + 1;
     if constexpr (NTS) {
       __builtin_nontemporal_store(sample, adj_col + (uint64_t)idx * adj_stride);
-      __builtin_nontemporal_store(nidx, adj_idx_p);
+      __builtin_nontemporal_store((uint8_t)nidx, adj_idx_p);
     } else {
       adj_col[(uint64_t)idx * adj_stride] = sample;
-      *adj_idx_p = nidx;
+      *adj_idx_p = (uint8_t)nidx;
     }
     adj = sum / (2.0 * (double)WW);
   } else if (p.W) {
@@ -298,7 +298,7 @@ __device__ __forceinline__ int update_one(double* me, double& err, double& adj, 
       sum = sum + v;
     }
     adj_col[(uint64_t)idx * adj_stride] = sample;
-    *adj_idx_p = (idx + 1 == p.W) ? 0 : idx + 1;
+    *adj_idx_p = (uint8_t)((idx + 1 == p.W) ? 0 : idx + 1);
     adj = sum / (2.0 * (double)p.W);
   }
   // update_gravity (283-289): origin = with_options (portion 0, adj 0, height = height_min)
@@ -424,7 +424,7 @@ __global__ void __launch_bounds__(256) probe_gen_kernel(VivParams p, uint32_t sl
 template <int D, int F, int WW, int ABL = 0, int FRT = filt_words(F)>
 __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
     const double* __restrict__ cur, double* __restrict__ nxt, double* __restrict__ adj_win,
-    uint32_t* __restrict__ adj_idx, double* __restrict__ filt, unsigned long long* resets,
+    uint8_t* __restrict__ adj_idx, double* __restrict__ filt, unsigned long long* resets,
     const uint32_t* __restrict__ peer_in, const uint64_t* __restrict__ rtt_in, int32_t* __restrict__ status,
     VivParams p, uint32_t slot) {
   // D == 8: the peer rows are gathered two lanes per row (below), so every lane of the
@@ -619,7 +619,7 @@ __device__ __forceinline__ void st_s(double2* p, double2 x) {
 template <int F, int FRT = filt_words(F)>
 __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_pipe_kernel(
     const double* __restrict__ cur, double* __restrict__ nxt, double* __restrict__ adj_win,
-    uint32_t* __restrict__ adj_idx, double* __restrict__ filt, unsigned long long* resets,
+    uint8_t* __restrict__ adj_idx, double* __restrict__ filt, unsigned long long* resets,
     const uint32_t* __restrict__ peer_in, const uint64_t* __restrict__ rtt_in, int32_t* __restrict__ status,
     VivParams p, uint32_t slot) {
   constexpr int D = 8, WW = 20, FR = FRT;
@@ -736,7 +736,7 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_pipe_kerne
 
 template <int D, int F>
 __global__ void __launch_bounds__(256) vivaldi_batch_kernel(
-    double* __restrict__ table, double* __restrict__ adj_win, uint32_t* __restrict__ adj_idx,
+    double* __restrict__ table, double* __restrict__ adj_win, uint8_t* __restrict__ adj_idx,
     double* __restrict__ filt, unsigned long long* resets, const uint32_t* __restrict__ member,
     const uint32_t* __restrict__ slot, const double* __restrict__ orow,
     const uint32_t* __restrict__ odim, const uint64_t* __restrict__ rtt, uint64_t n,
@@ -785,7 +785,7 @@ __global__ void __launch_bounds__(256) vivaldi_batch_kernel(
 // check reports a mismatch).  One lane per ack, members distinct in a batch.
 template <int D, int F>
 __global__ void __launch_bounds__(256) vivaldi_ack_kernel(
-    double* __restrict__ table, double* __restrict__ adj_win, uint32_t* __restrict__ adj_idx,
+    double* __restrict__ table, double* __restrict__ adj_win, uint8_t* __restrict__ adj_idx,
     double* __restrict__ filt, unsigned long long* resets, const uint32_t* __restrict__ member,
     const uint32_t* __restrict__ slot, const uint8_t* __restrict__ payload, const uint64_t* __restrict__ off,
     const uint64_t* __restrict__ rtt, uint64_t n, int32_t* __restrict__ status, VivParams p) {
@@ -872,7 +872,7 @@ struct rsf_vivaldi {
   double* table[2] = {nullptr, nullptr};
   int cur = 0;
   double* adj = nullptr;
-  uint32_t* adj_idx = nullptr;
+  uint8_t* adj_idx = nullptr;
   double* filt = nullptr;
   unsigned long long* resets = nullptr;
   // probe inputs of rsf_vivaldi_round (peer id, rtt ns per shard member)
@@ -943,7 +943,7 @@ int rsf_vivaldi_create(rsf_vivaldi** out, uint64_t n, uint64_t lo, uint64_t hi, 
   size_t tbytes = (size_t)n * p.stride * sizeof(double);
   if ((rc = rsf::dmalloc((void**)&v->table[0], tbytes)) || (rc = rsf::dmalloc((void**)&v->table[1], tbytes)) ||
       (rc = rsf::dmalloc((void**)&v->adj, (size_t)(p.W ? p.W : 1) * p.shard_n * sizeof(double))) ||
-      (rc = rsf::dmalloc((void**)&v->adj_idx, (size_t)p.shard_n * sizeof(uint32_t))) ||
+      (rc = rsf::dmalloc((void**)&v->adj_idx, (size_t)p.shard_n * sizeof(uint8_t))) ||
       (rc = rsf::dmalloc((void**)&v->filt, (size_t)p.shard_n * peers * p.FR * sizeof(double))) ||
       (rc = rsf::dmalloc((void**)&v->resets, sizeof(unsigned long long))) ||
       (rc = rsf::dmalloc((void**)&v->probe_peer, (size_t)p.shard_n * sizeof(uint32_t))) ||
@@ -954,7 +954,7 @@ int rsf_vivaldi_create(rsf_vivaldi** out, uint64_t n, uint64_t lo, uint64_t hi, 
     hipLaunchKernelGGL(init_rows_kernel, dim3(blocks), dim3(256), 0, v->stream, v->table[t], n, p.stride,
                        p.dim, p.error_max, p.height_min);
   if (hipMemsetAsync(v->adj, 0, (size_t)(p.W ? p.W : 1) * p.shard_n * sizeof(double), v->stream) != hipSuccess ||
-      hipMemsetAsync(v->adj_idx, 0, (size_t)p.shard_n * sizeof(uint32_t), v->stream) != hipSuccess ||
+      hipMemsetAsync(v->adj_idx, 0, (size_t)p.shard_n * sizeof(uint8_t), v->stream) != hipSuccess ||
       hipMemsetAsync(v->filt, 0, (size_t)p.shard_n * peers * p.FR * sizeof(double), v->stream) != hipSuccess ||
       hipMemsetAsync(v->resets, 0, sizeof(unsigned long long), v->stream) != hipSuccess ||
       hipStreamSynchronize(v->stream) != hipSuccess)
