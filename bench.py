@@ -169,7 +169,7 @@ def run_vivaldi(args, rank, world):
                    "members": n, "members_per_gpu": per, "parallelism": f"members sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "vivaldi_observe_kernel<8,3,20>", "bytes_per_unit": VIVALDI_BYTES,
+                     "kernel": "vivaldi_observe_pipe_kernel<3>", "bytes_per_unit": VIVALDI_BYTES,
                      "units_per_launch": per, "bytes_per_launch": VIVALDI_BYTES * per,
                      "avg_launch_ms": avg_kernel_s * 1e3},
         # --members is per GPU unless --members-total; the default keeps 64M members in total

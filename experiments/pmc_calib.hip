@@ -16,26 +16,38 @@ __device__ inline uint32_t mix(uint64_t i) {
   return (uint32_t)z;
 }
 
-template <typename T>
+// NT: non-temporal loads / stores (the Vivaldi round kernel's member-side streams)
+template <typename T, bool NT = false>
 __global__ void stream_read(const T* __restrict__ a, uint64_t n, uint64_t* sink) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  T v = a[i];
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
-  uint32_t x = 0;
-  for (unsigned k = 0; k < sizeof(T) / 4; ++k) x ^= w[k];
+  T v;
+  if constexpr (NT) v = __builtin_nontemporal_load(a + i); else v = a[i];
+  uint64_t x = 0;
+  if constexpr (sizeof(T) < 4) {
+    x = (uint64_t)v;
+  } else {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
+    for (unsigned k = 0; k < sizeof(T) / 4; ++k) x ^= w[k];
+  }
   if (x == 0x12345679u) sink[0] = x;
 }
 
-template <typename T>
+template <typename T, bool NT = false>
 __global__ void stream_write(T* __restrict__ a, uint64_t n) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   T v;
-  uint32_t* w = reinterpret_cast<uint32_t*>(&v);
-  for (unsigned k = 0; k < sizeof(T) / 4; ++k) w[k] = (uint32_t)i + k;
-  a[i] = v;
+  if constexpr (sizeof(T) < 4) {
+    v = (T)i;
+  } else {
+    uint32_t* w = reinterpret_cast<uint32_t*>(&v);
+    for (unsigned k = 0; k < sizeof(T) / 4; ++k) w[k] = (uint32_t)i + k;
+  }
+  if constexpr (NT) __builtin_nontemporal_store(v, a + i); else a[i] = v;
 }
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
 
 // random record gather: REC bytes per lane from a random REC-aligned slot (16-B loads)
 template <int REC>
@@ -99,6 +111,25 @@ int main() {
   hipLaunchKernelGGL(scatter<32>, grid(lanes), dim3(256), 0, 0, (uint4*)buf, bytes / 32, lanes);
   printf("calib scatter64 %llu\n", (unsigned long long)(lanes * 64));
   hipLaunchKernelGGL(scatter<64>, grid(lanes), dim3(256), 0, 0, (uint4*)buf, bytes / 64, lanes);
+  // appended shapes (keep the order above stable for older summaries)
+  printf("calib stream_read1 %llu\n", (unsigned long long)bytes);
+  hipLaunchKernelGGL((stream_read<uint8_t>), grid(bytes), dim3(256), 0, 0, (const uint8_t*)buf, bytes, sink);
+  printf("calib stream_read1_nt %llu\n", (unsigned long long)bytes);
+  hipLaunchKernelGGL((stream_read<uint8_t, true>), grid(bytes), dim3(256), 0, 0, (const uint8_t*)buf, bytes, sink);
+  printf("calib stream_read4_nt %llu\n", (unsigned long long)bytes);
+  hipLaunchKernelGGL((stream_read<uint32_t, true>), grid(bytes / 4), dim3(256), 0, 0, (const uint32_t*)buf, bytes / 4, sink);
+  printf("calib stream_read8_nt %llu\n", (unsigned long long)bytes);
+  hipLaunchKernelGGL((stream_read<u32x2v, true>), grid(bytes / 8), dim3(256), 0, 0, (const u32x2v*)buf, bytes / 8, sink);
+  printf("calib stream_read16_nt %llu\n", (unsigned long long)bytes);
+  hipLaunchKernelGGL((stream_read<u32x4v, true>), grid(bytes / 16), dim3(256), 0, 0, (const u32x4v*)buf, bytes / 16, sink);
+  printf("calib stream_write1 %llu\n", (unsigned long long)bytes);
+  hipLaunchKernelGGL((stream_write<uint8_t>), grid(bytes), dim3(256), 0, 0, (uint8_t*)buf, bytes);
+  printf("calib stream_write1_nt %llu\n", (unsigned long long)bytes);
+  hipLaunchKernelGGL((stream_write<uint8_t, true>), grid(bytes), dim3(256), 0, 0, (uint8_t*)buf, bytes);
+  printf("calib stream_write8_nt %llu\n", (unsigned long long)bytes);
+  hipLaunchKernelGGL((stream_write<u32x2v, true>), grid(bytes / 8), dim3(256), 0, 0, (u32x2v*)buf, bytes / 8);
+  printf("calib stream_write16_nt %llu\n", (unsigned long long)bytes);
+  hipLaunchKernelGGL((stream_write<u32x4v, true>), grid(bytes / 16), dim3(256), 0, 0, (u32x4v*)buf, bytes / 16);
   CK(hipDeviceSynchronize());
   CK(hipFree(buf));
   CK(hipFree(sink));

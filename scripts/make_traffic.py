@@ -6,8 +6,12 @@ gfx950 corrections (measured by experiments/pmc_calib, profiles/r01/pmc_calibrat
   * coalesced streaming reads are tallied at 1/2 by FETCH_SIZE (4/8/16 B per lane alike);
   * random gathers of <= 64 B count one 64-B sector each, i.e. the HBM bytes they move;
   * WRITE_SIZE is exact for streaming stores.
-Vivaldi: the observe kernel's gather share is isolated by the ablation without the
-peer-row gather (experiments/viv_traffic.sh):  traffic = 2*stream + gather + WRITE.
+Vivaldi (vivaldi_observe_pipe_kernel): the peer-row gather (96 B per member, tallied at
+0.998, gather96) is modelled and the rest of FETCH is the coalesced streams (tallied at 1/2,
+non-temporal loads alike: stream_read*_nt); byte-wide loads (the u8 window index) are not
+tallied at all (stream_read1), so they are added from the model:
+    traffic = 2*(FETCH - 0.998*gather) + gather + idx + WRITE   (idx = 1 B per member).
+The modelled FETCH (streams/2 + 0.998*gather) is printed beside the measured one.
 Gossip (merge_kernel): the streamed bytes are modelled (the intent queue, qcap x 12 B per
 receiver, and the (sender, peer) groups' record slots, cap_t x 8 B + a 4-B count each) and
 corrected (x2); the rest of FETCH is gather:  traffic = FETCH + stream/2 + WRITE."""
@@ -29,13 +33,22 @@ def last(path, counter, pat, k=5):
 
 
 res = {}
-viv = json.loads(open(os.path.join(ROOT, "profiles", RND, "viv_r01_pmc_ablation.txt")).read().strip().splitlines()[-1])
-res["vivaldi"] = {"kernel": "vivaldi_observe_kernel<8,3,20>", "members_per_gpu": 64_000_000,
-                  "traffic_bytes_per_launch": viv["traffic_bytes"],
-                  "fetch_counter": viv["fetch_counter"], "write_counter": viv["write_counter"],
-                  "gather_counter": viv["gather_counter"],
-                  "source": f"profiles/{RND}/viv_r01_pmc_ablation.txt", "method": "2*stream + gather + WRITE"}
-g = os.path.join(OUT, "prof_gossip_r01")
+VTAG = os.environ.get("VIV_TAG", "viv_r01c")
+v = os.path.join(OUT, f"prof_{VTAG}")
+f_viv = last(f"{v}_fetch/run_counter_collection.csv", "FETCH_SIZE", "vivaldi_observe_pipe_kernel")
+w_viv = last(f"{v}_write/run_counter_collection.csv", "WRITE_SIZE", "vivaldi_observe_pipe_kernel")
+vline = next(json.loads(x) for x in open(f"{v}_trace.log") if x.startswith("{") and '"metric"' in x)
+nv = vline["config"]["members_per_gpu"]
+gather = 96 * nv
+streams = nv * (96 + 16 + 160 + 4 + 8)  # own row, filter record, window, peer id, rtt (all coalesced)
+traffic_v = 2 * (f_viv - 0.998 * gather) + gather + nv + w_viv
+res["vivaldi"] = {"kernel": "vivaldi_observe_pipe_kernel<3>", "members_per_gpu": nv,
+                  "traffic_bytes_per_launch": traffic_v, "fetch_counter": f_viv, "write_counter": w_viv,
+                  "gather_bytes_modelled": gather, "fetch_modelled": streams / 2 + 0.998 * gather,
+                  "source": f"profiles/{RND}/{VTAG}_summary.md",
+                  "method": "2*(FETCH - 0.998*gather) + gather + u8 index read + WRITE"}
+GTAG = os.environ.get("GOSSIP_TAG", "gossip_r01c")
+g = os.path.join(OUT, f"prof_{GTAG}")
 f_merge = last(f"{g}_fetch/run_counter_collection.csv", "FETCH_SIZE", "merge_kernel")
 w_merge = last(f"{g}_write/run_counter_collection.csv", "WRITE_SIZE", "merge_kernel")
 line = next(json.loads(x) for x in open(f"{g}_trace.log") if x.startswith("{") and '"metric"' in x)
@@ -50,6 +63,6 @@ stream_merge = n * qcap * 12 + n * fanout * (cap_t * 8 + 4)
 traffic = f_merge + stream_merge / 2 + w_merge
 res["gossip"] = {"kernel": "merge_kernel", "members_per_gpu": n, "traffic_bytes_per_launch": traffic,
                  "fetch_counter": f_merge, "write_counter": w_merge, "stream_bytes_modelled": stream_merge,
-                 "source": f"profiles/{RND}/gossip_r01_summary.md", "method": "FETCH + stream/2 + WRITE"}
+                 "source": f"profiles/{RND}/{GTAG}_summary.md", "method": "FETCH + stream/2 + WRITE"}
 json.dump(res, open(os.path.join(ROOT, "profiles", "traffic.json"), "w"), indent=1)
 print(json.dumps(res, indent=1))
