@@ -108,9 +108,14 @@ def run_vivaldi(args, rank, world):
     g.set_stream(stream.cuda_stream)
     table = None
 
-    def refresh():
-        # all-gather of the coordinate table (peers read last round's rows)
-        if world == 1:
+    R = max(1, args.refresh_every)
+
+    def refresh(r):
+        # all-gather of the coordinate table (peers read last round's rows).  With R > 1
+        # (R = 8) the table is refreshed after every R-th round only, so
+        # rows of other shards are up to R rounds old -- the reference reads a peer's
+        # coordinate from its last ack, which is as stale as the probe schedule makes it.
+        if world == 1 or (r + 1) % R:
             return
         ptr, stride = g.table_ptr()
         full = torch.as_tensor(CudaArray(ptr, (n * stride,), "<f8"), device="cuda")
@@ -121,6 +126,12 @@ def run_vivaldi(args, rank, world):
             full.copy_(h)
         else:
             torch.distributed.all_gather_into_tensor(full, mine)
+        if R > 1:
+            # the tables ping-pong every round and an even R would always refresh the same
+            # one: the other table's rows of remote shards are brought up to date on-device
+            other = torch.as_tensor(CudaArray(read_ptr[0], (n * stride,), "<f8"), device="cuda")
+            other[: lo * stride].copy_(full[: lo * stride])
+            other[hi * stride:].copy_(full[hi * stride:])
 
     # the probe inputs (peer id, observed rtt) of every round are generated up front by
     # the synthetic network and are resident in HBM when the timed region starts
@@ -131,12 +142,15 @@ def run_vivaldi(args, rank, world):
         g.gen_probes(r, peer[r].data_ptr(), rtt[r].data_ptr())
     step = [0]
 
+    read_ptr = [None]  # the table a round reads (the other one after it)
+
     def observe(r):
+        read_ptr[0] = g.table_ptr()[0]
         g.observe(r % 16, peer[r].data_ptr(), rtt[r].data_ptr(), None, r)
 
     for _ in range(args.warmup):
         observe(step[0])
-        refresh()
+        refresh(step[0])
         step[0] += 1
     torch.cuda.synchronize()
     barrier(world)
@@ -148,7 +162,7 @@ def run_vivaldi(args, rank, world):
         evs[i][0].record(stream)
         observe(step[0])
         evs[i][1].record(stream)
-        refresh()
+        refresh(step[0])
         step[0] += 1
     torch.cuda.synchronize()
     barrier(world)
@@ -166,7 +180,8 @@ def run_vivaldi(args, rank, world):
         "config": {"workload": f"Vivaldi rounds (BASELINE configs[4] shape), {n} members, D=8 f64, height + "
                                f"latency filter F=3, adjustment window W=20, 16 neighbours/member probed round-robin, "
                                f"probe inputs (peer, rtt) pre-generated in HBM",
-                   "members": n, "members_per_gpu": per, "parallelism": f"members sharded x{world}"},
+                   "members": n, "members_per_gpu": per, "parallelism": f"members sharded x{world}",
+                   "table_refresh_every_rounds": R},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "vivaldi_observe_pipe_kernel<3>", "bytes_per_unit": VIVALDI_BYTES,
@@ -229,6 +244,8 @@ def main():
     ap.add_argument("--members", type=int, default=None, help="members per GPU")
     ap.add_argument("--members-total", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--refresh-every", type=int, default=1,
+                    help="vivaldi, N>1: all-gather the coordinate table after every R-th round (C5: 1 and 8)")
     args = ap.parse_args()
     rank, world, local = env_rank()
     if world != args.gpus and world == 1 and args.gpus > 1:

@@ -66,4 +66,23 @@ RSF_HD double as_secs_f64(uint64_t ns) {
 RSF_HD double rmax(double a, double b) { return fmax(a, b); }
 RSF_HD double rmin(double a, double b) { return fmin(a, b); }
 
+// XCD-aware block order.  The dispatcher hands block b to XCD b % 8 (each XCD has its
+// own L2 and translation caches); remapping gives every XCD one contiguous range of
+// the logical blocks, so neighbouring members (adjacent records, segment bounds, rows
+// in the same 2 MB page) are served by one L2 instead of eight.  A bijection on
+// [0, nb) for any nb.
+#ifndef RSF_XCD_REMAP
+#define RSF_XCD_REMAP 0  // measured ~1% slower for merge/emit and Vivaldi
+#endif
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
+#if RSF_XCD_REMAP
+  constexpr uint32_t kXcd = 8;
+  const uint32_t x = b % kXcd, i = b / kXcd, q = nb / kXcd, r = nb % kXcd;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+#else
+  (void)nb;
+  return b;
+#endif
+}
+
 }  // namespace rsf

@@ -532,24 +532,45 @@ __global__ void __launch_bounds__(256) grp_index_kernel(const uint32_t* __restri
 // (grp_key, from peers_kernel) broadcast_messages drains intent -> query -> event under
 // one byte budget; the group's records (rumor id + decoration) go to cap_t slots at the
 // group's sorted position, its record count to cnt_s.
-__global__ void __launch_bounds__(256) emit_kernel(GCfg c, GState s, const uint32_t* __restrict__ grp_key,
-                                                   const uint32_t* __restrict__ slot, uint32_t* __restrict__ cnt_s,
-                                                   uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec) {
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  if (l >= c.n_loc) return;
-  // Independent loads first, in one round trip: the intent queue (the common case; a
-  // sorted queue is empty iff its slot 0 is free), the query/event queue heads, the peers
-  // and their group slots.
-  QRegs Q0{kEmpty, 0, 0}, Q1{kEmpty, 0, 0, kDecQuery}, Q2{kEmpty, 0, 0, kDecEvent};
-  q_load(c, s, l, 0, lane, Q0);
-  const uint32_t head = lane >= 1 && lane < 3 ? s.q_rumor[(l * 3 + lane) * c.qcap] : kEmpty;
-  const uint32_t gk = lane < c.fanout ? grp_key[l * c.fanout + lane] : kSentinel;
-  const uint32_t gs = lane < c.fanout ? slot[l * c.fanout + lane] : 0u;
-  const uint64_t pm = __ballot(gk != kSentinel);  // peers are a prefix of the fanout slots
+// Members per wave in emit_kernel / merge_kernel: with more than one, a wave issues the
+// first round trip of every member it owns before working through them, so the loads
+// of the next member are in flight while the current one runs (the kernels run at the
+// 8-waves/SIMD hardware cap and wait on memory half the time).
+#ifndef RSF_EMIT_PER_WAVE
+#define RSF_EMIT_PER_WAVE 1  // emit: 2, 8 and 16 per wave measured slower
+#endif
+#ifndef RSF_MERGE_PER_WAVE
+#define RSF_MERGE_PER_WAVE 8  // merge: 8 receivers per wave measured fastest (4.30 -> 4.06 ms at 2M; 2, 4, 16, 32 between)
+#endif
+
+// a sender's first round trip: the intent queue (the common case; a sorted queue is
+// empty iff its slot 0 is free), the query/event queue heads, the peers and their
+// group slots
+struct EmitIn {
+  QRegs Q0;
+  uint32_t head, gk, gs;
+};
+__device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const uint32_t* __restrict__ grp_key,
+                                          const uint32_t* __restrict__ slot, uint64_t l, uint32_t lane, EmitIn& e) {
+  e.Q0 = QRegs{kEmpty, 0, 0};
+  e.head = kEmpty;
+  e.gk = kSentinel;
+  e.gs = 0;
+  if (l >= c.n_loc) return;  // wave-uniform: a wave's last member may lie past the shard
+  q_load(c, s, l, 0, lane, e.Q0);
+  e.head = lane >= 1 && lane < 3 ? s.q_rumor[(l * 3 + lane) * c.qcap] : kEmpty;
+  e.gk = lane < c.fanout ? grp_key[l * c.fanout + lane] : kSentinel;
+  e.gs = lane < c.fanout ? slot[l * c.fanout + lane] : 0u;
+}
+__device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_t l, uint32_t lane, EmitIn& e,
+                                         uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val,
+                                         uint32_t* __restrict__ out_dec) {
+  QRegs& Q0 = e.Q0;
+  QRegs Q1{kEmpty, 0, 0, kDecQuery}, Q2{kEmpty, 0, 0, kDecEvent};
+  const uint64_t pm = __ballot(e.gk != kSentinel);  // peers are a prefix of the fanout slots
   const uint32_t np = (uint32_t)__popcll(pm);
-  const bool ne0 = shfl_u32(Q0.r, 0) != kEmpty, ne1 = shfl_u32(head, 1) != kEmpty,
-             ne2 = shfl_u32(head, 2) != kEmpty;
+  const bool ne0 = shfl_u32(Q0.r, 0) != kEmpty, ne1 = shfl_u32(e.head, 1) != kEmpty,
+             ne2 = shfl_u32(e.head, 2) != kEmpty;
   if (np == 0 || !(ne0 || ne1 || ne2)) return;
   // decoration of the intents: their subject slots (subject and type share one 8-B word)
   if (Q0.r != kEmpty) Q0.dec = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(s.rumors + Q0.r) + 16);
@@ -558,7 +579,7 @@ __global__ void __launch_bounds__(256) emit_kernel(GCfg c, GState s, const uint3
   uint32_t err = 0;
   bool d0 = false, d1 = false, d2 = false;
   for (uint32_t j = 0; j < np; ++j) {
-    const uint32_t gslot = shfl_u32(gs, j);
+    const uint32_t gslot = shfl_u32(e.gs, j);
     const uint64_t out_base = (uint64_t)gslot * c.cap_t;
     uint32_t nrec = 0;
     int64_t used = 0;
@@ -571,6 +592,26 @@ __global__ void __launch_bounds__(256) emit_kernel(GCfg c, GState s, const uint3
   if (d1) q_store(c, s, l, 1, lane, Q1, true);
   if (d2) q_store(c, s, l, 2, lane, Q2, true);
   if (err && lane == 0) s.err[l] |= err;
+}
+
+__global__ void __launch_bounds__(256) emit_kernel(GCfg c, GState s, const uint32_t* __restrict__ grp_key,
+                                                   const uint32_t* __restrict__ slot, uint32_t* __restrict__ cnt_s,
+                                                   uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint64_t l = ((uint64_t)xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock +
+                      (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)) * RSF_EMIT_PER_WAVE;
+  if (l >= c.n_loc) return;
+  EmitIn cur, nxt;
+  emit_load(c, s, grp_key, slot, l, lane, cur);
+  if (RSF_EMIT_PER_WAVE == 1) {
+    emit_run(c, s, l, lane, cur, cnt_s, out_val, out_dec);
+    return;
+  }
+  for (uint32_t k = 0; k < RSF_EMIT_PER_WAVE; ++k) {
+    if (k + 1 < RSF_EMIT_PER_WAVE) emit_load(c, s, grp_key, slot, l + k + 1, lane, nxt);
+    if (l + k < c.n_loc) emit_run(c, s, l + k, lane, cur, cnt_s, out_val, out_dec);
+    cur = nxt;
+  }
 }
 
 // Record decoration: what merge_kernel needs to address the view entry (the
@@ -948,10 +989,21 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
   __shared__ QLds qlds[kWavesPerBlock][2];
   QLds* ql = qlds[threadIdx.x / kWave];
   const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
-  uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  uint64_t l = (uint64_t)(RSF_MERGE_PERSIST ? blockIdx.x : xcd_block(blockIdx.x, gridDim.x)) * kWavesPerBlock +
+               (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  if (!RSF_MERGE_PERSIST) l *= RSF_MERGE_PER_WAVE;
   if (l >= c.n_loc) return;
   const MSetupLane sl = merge_setup_lane(c, s, seg_start, seg_end, lane);
   uint32_t cur = merge_setup(sl, l, lane);
+  if (!RSF_MERGE_PERSIST && RSF_MERGE_PER_WAVE > 1) {
+    // every owned receiver's setup is in flight before the first merge starts
+    for (uint32_t k = 0; k < RSF_MERGE_PER_WAVE && l + k < c.n_loc; ++k) {
+      const uint32_t nxt = k + 1 < RSF_MERGE_PER_WAVE && l + k + 1 < c.n_loc ? merge_setup(sl, l + k + 1, lane) : 0u;
+      merge_one(c, s, vals, dec, gcnt, stride, l + k, lane, cur, ql);
+      cur = nxt;
+    }
+    return;
+  }
   for (;;) {
     const uint64_t ln = l + nw;
     const bool more = RSF_MERGE_PERSIST && ln < c.n_loc;
@@ -1846,7 +1898,7 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local) {
                      g->grp_slot, local ? g->seg_start : nullptr, local ? g->seg_end : nullptr);
   RSF_HIP(hipGetLastError());
   mark(g, 2);
-  hipLaunchKernelGGL(emit_kernel, dim3(grid1(c.n_loc, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0, st, c, g->s,
+  hipLaunchKernelGGL(emit_kernel, dim3(grid1((c.n_loc + RSF_EMIT_PER_WAVE - 1) / RSF_EMIT_PER_WAVE, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0, st, c, g->s,
                      g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec);
   RSF_HIP(hipGetLastError());
   size_t tb = g->grp_scan_bytes;
@@ -1869,7 +1921,8 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local) {
 static int launch_merge(rsf_gossip* g, const uint32_t* vals, bool grouped = false) {
   const GCfg& c = g->c;
   const unsigned blocks = RSF_MERGE_PERSIST ? std::min<unsigned>(grid1(c.n_loc, kWavesPerBlock), g->merge_blocks)
-                                            : grid1(c.n_loc, kWavesPerBlock);
+                                            : grid1((c.n_loc + RSF_MERGE_PER_WAVE - 1) / RSF_MERGE_PER_WAVE,
+                                                    kWavesPerBlock);
   hipLaunchKernelGGL(merge_kernel, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, g->stream,
                      c, g->s, grouped ? g->stage_val : vals, grouped ? g->stage_dec : (const uint32_t*)g->rec_dec,
                      g->seg_start, g->seg_end, grouped ? g->grp_cnt : nullptr, grouped ? c.cap_t : 1u);

@@ -589,6 +589,9 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
 #ifndef RSF_VIV_PIPE
 #define RSF_VIV_PIPE 1
 #endif
+#ifndef RSF_VIV_XCD
+#define RSF_VIV_XCD 0  // 1: XCD-contiguous block order (common.h xcd_block)
+#endif
 #ifndef RSF_VIV_NT
 // non-temporal hints (bit 1: member-side loads/stores in the round kernel, 2: its window-slot
 // and window-index stores, 4: the peer gather).  The member-side streams are touched once
@@ -624,7 +627,8 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_pipe_kerne
     VivParams p, uint32_t slot) {
   constexpr int D = 8, WW = 20, FR = FRT;
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t local0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t bid = RSF_VIV_XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint64_t local0 = (uint64_t)bid * blockDim.x + threadIdx.x;
   const uint64_t wbase = local0 - lane;  // the wave's first shard-local member
   if (wbase >= p.shard_n) return;        // wave-uniform: no lane of this wave has a member
   const uint32_t wrows = (uint32_t)min((uint64_t)64, p.shard_n - wbase);
