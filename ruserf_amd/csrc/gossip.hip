@@ -680,7 +680,7 @@ __global__ void __launch_bounds__(256) grp_expand_kernel(const uint32_t* __restr
 //     re-queues are then applied serially in record order.
 // User events / queries (dedup rings in HBM) run serially in lane 0.
 #ifndef RSF_MERGE_WAVES
-#define RSF_MERGE_WAVES 8  // min waves/SIMD for merge_kernel (register cap; 8 measured fastest)
+#define RSF_MERGE_WAVES 7  // min waves/SIMD for merge_kernel (register cap; 7 measured fastest with 8 receivers per wave, 8 before)
 #endif
 #ifndef RSF_MERGE_PROF
 #define RSF_MERGE_PROF 0  // diagnostic build: per-phase shader-clock totals of merge_kernel
@@ -693,6 +693,9 @@ __device__ unsigned long long g_merge_prof[8];
 #else
 #define MPROF_T(v)
 #define MPROF_ADD(i, a, b)
+#endif
+#ifndef RSF_MERGE_CHAIN_BY_SUBJECT
+#define RSF_MERGE_CHAIN_BY_SUBJECT 1  // 1: chain detection loops over distinct subjects, not records
 #endif
 #ifndef RSF_MERGE_BATCH
 #define RSF_MERGE_BATCH 1  // 1: a chunk's intent re-queues go in with one q_insert_batch
@@ -798,9 +801,11 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     const uint32_t rid0 = in ? vals[slot] : 0;
     uint32_t gk = 1, gc = 1;
     if (gcnt && in) {
-      const uint64_t g = slot / stride;
-      gk = (uint32_t)(slot - g * stride);
-      gc = gcnt[g];
+      // group of the slot relative to the receiver's first group: a 32-bit division
+      // (a receiver's slot range is small) instead of a 64-bit one
+      const uint32_t rel = (uint32_t)(base - vs) + lane, gr = rel / stride;
+      gk = rel - gr * stride;
+      gc = gcnt[st + gr];
     }
     // decoration (same round trip as the rumor ids): subject of an intent, or the
     // queue of an event / query; invalid lanes read as neither
@@ -828,6 +833,23 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     const uint32_t my_subj = is_view ? dsub : 0xFFFFFFFFu;
     // chains: previous / next record of the same subject in this chunk
     int prev = -1, next = -1;
+#if RSF_MERGE_CHAIN_BY_SUBJECT
+    {
+      // one pass per DISTINCT subject: the ballot of the lanes holding it is the chain,
+      // each lane's neighbours are the nearest set bits below and above it
+      uint64_t mm = __ballot(is_view), same = 0;
+      while (mm) {
+        const uint32_t sj = shfl_u32(my_subj, __ffsll((long long)mm) - 1);
+        const bool hit = my_subj == sj;  // non-view lanes hold 0xFFFFFFFF, never a subject
+        const uint64_t grp = __ballot(hit);
+        if (hit) same = grp;
+        mm &= ~grp;
+      }
+      const uint64_t below = same & ((1ull << lane) - 1), above = same & ~((2ull << lane) - 1);
+      prev = below ? 63 - __clzll((long long)below) : -1;
+      next = above ? __ffsll((long long)above) - 1 : -1;
+    }
+#else
     {
       const uint64_t vmask = __ballot(is_view);
       uint64_t mm = vmask;
@@ -841,6 +863,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
         }
       }
     }
+#endif
     // Lamport clock each intent record witnesses against: exclusive prefix max
     const uint64_t wit = is_view ? ru.ltime + 1 : 0;
     const uint64_t incl = wave_inclusive_max_u64(wit);
