@@ -457,6 +457,78 @@ int rsf_coord_encode(const double* rows, uint32_t dim, uint32_t row_stride, uint
 int rsf_coord_decode(const uint8_t* in, const uint64_t* off, uint64_t n, int ping_version_prefix, double* rows,
                      uint32_t row_stride, uint32_t max_dim, uint32_t* dim_out, int32_t* status, void* stream);
 
+/* ======================================================================== */
+/* memberlist SWIM layer model                        */
+/* ======================================================================== */
+/* memberlist's failure detector state per (member, subject): the incarnation merge of
+ * alive / suspect / dead messages and the suspicion timers.  The reference does not
+ * vendor memberlist (memberlist-core 0.2, a semver range with no lockfile; called from
+ * core/src/serf/base.rs:208-225 and delegate.rs notify_join/leave): PARITY UNPINNED.
+ * Restated from memberlist's published state machine (state aliveNode / suspectNode /
+ * deadNode / refute and the suspicion timer), identically in oracle/oracle.c.
+ * Time is an integer tick (the caller's clock, e.g. ms). */
+#define RSF_SWIM_ALIVE 0
+#define RSF_SWIM_SUSPECT 1
+#define RSF_SWIM_DEAD 2
+#define RSF_SWIM_LEFT 3
+#define RSF_SWIM_UNKNOWN 255      /* not in nodeMap */
+#define RSF_SWIM_MSG_ALIVE 0      /* alive{incarnation, node} */
+#define RSF_SWIM_MSG_SUSPECT 1    /* suspect{incarnation, node, from} */
+#define RSF_SWIM_MSG_DEAD 2       /* dead{incarnation, node, from}; from == node: the node left */
+#define RSF_SWIM_MAX_CONFIRM 4    /* suspicion confirmations tracked per entry (k <= 4) */
+/* result flags per message */
+#define RSF_SWIM_F_REBROADCAST 1  /* encodeAndBroadcast of the message */
+#define RSF_SWIM_F_REFUTE 2       /* about the receiver itself: refute() broadcast alive{new incarnation} */
+#define RSF_SWIM_F_NOTIFY_JOIN 4  /* Events.NotifyJoin (unknown/dead/left -> alive) */
+#define RSF_SWIM_F_NOTIFY_LEAVE 8 /* Events.NotifyLeave (-> dead / left) */
+#define RSF_SWIM_F_SUSPECT 16     /* alive -> suspect: a suspicion timer started */
+#define RSF_SWIM_F_CONFIRM 32     /* a new independent confirmation of a running suspicion */
+
+typedef struct rsf_swim_cfg {
+  uint64_t n_members;              /* N (member ids are global) */
+  uint64_t shard_lo, shard_hi;     /* receivers owned by this context */
+  uint32_t n_subjects;             /* S: the members whose entries are tracked */
+  uint32_t suspicion_k;            /* SuspicionMult - 2 confirmations (0 .. RSF_SWIM_MAX_CONFIRM) */
+  /* suspicion timeout after c confirmations, c = 0..k, in ticks: memberlist's
+   * max - log(c+1)/log(k+1) * (max - min), floored, at least min (host-computed) */
+  uint32_t timeout[RSF_SWIM_MAX_CONFIRM + 1];
+  uint32_t _reserved;
+} rsf_swim_cfg;
+
+/* one received message for rsf_swim_apply_batch; 24 bytes */
+typedef struct rsf_swim_msg {
+  uint32_t receiver;    /* member id (in the shard) */
+  uint32_t subject;     /* subject slot the message is about */
+  uint32_t incarnation;
+  uint32_t from;        /* member id of the accuser (suspect / dead) */
+  uint32_t type;        /* RSF_SWIM_MSG_* */
+  uint32_t _reserved;
+} rsf_swim_msg;
+
+typedef struct rsf_swim rsf_swim;
+int rsf_swim_create(rsf_swim** out, const rsf_swim_cfg* cfg, int device);
+int rsf_swim_destroy(rsf_swim* w);
+int rsf_swim_set_stream(rsf_swim* w, void* hip_stream);
+/* subject slot -> member id (S entries, host) */
+int rsf_swim_set_subjects(rsf_swim* w, const uint32_t* subject_member);
+/* initial entry of every subject replicated into every receiver's row (S each, host);
+ * and every receiver's own incarnation (m.incarnation) = self_incarnation */
+int rsf_swim_init(rsf_swim* w, const uint8_t* state, const uint32_t* incarnation, uint32_t self_incarnation);
+/* per-receiver "left" flag (m.hasLeft(): a dead message about self is not refuted) */
+int rsf_swim_set_left(rsf_swim* w, uint64_t member, uint8_t left);
+/* aliveNode / suspectNode / deadNode for n messages (host).  A receiver's messages are
+ * applied in array order at tick `now`; receivers run in parallel.  flags_out[i] =
+ * RSF_SWIM_F_*; refute_inc_out[i] (optional) = the incarnation a refutation broadcast. */
+int rsf_swim_apply_batch(rsf_swim* w, const rsf_swim_msg* msgs, uint64_t n, uint32_t now, int32_t* flags_out,
+                         uint32_t* refute_inc_out);
+/* suspicion timers due at `now` (now - state_change >= timeout[confirmations]) fire:
+ * deadNode{entry incarnation, from = the receiver}.  *n_fired (host) = timers fired. */
+int rsf_swim_tick(rsf_swim* w, uint32_t now, uint64_t* n_fired);
+/* rows of receivers [first, first + count): per entry state, incarnation, state-change
+ * tick, confirmations; and those receivers' own incarnations (host buffers) */
+int rsf_swim_dump(rsf_swim* w, uint64_t first, uint64_t count, uint8_t* state, uint32_t* incarnation,
+                  uint32_t* change, uint8_t* n_confirm, uint32_t* self_incarnation);
+
 #ifdef __cplusplus
 }
 #endif

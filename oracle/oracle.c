@@ -1375,3 +1375,192 @@ uint32_t orc_coalesce_user_events(const orc_uevent* in, uint32_t n, orc_uevent* 
   free(grp);
   return o;
 }
+
+/* ======================================================================
+ * memberlist SWIM model.  PARITY UNPINNED: memberlist-core 0.2
+ * is not vendored (reference Cargo.toml:27-29; call sites core/src/serf/base.rs:208-225).
+ * States: 0 alive, 1 suspect, 2 dead, 3 left, 255 unknown.  Flags: 1 rebroadcast,
+ * 2 refute, 4 notify join, 8 notify leave, 16 suspicion started, 32 confirmation.
+ * ====================================================================== */
+enum { SW_ALIVE = 0, SW_SUSPECT = 1, SW_DEAD = 2, SW_LEFT = 3, SW_UNKNOWN = 255 };
+
+int orc_swim_init(orc_swim* w, uint64_t lo, uint64_t n_loc, uint32_t S, uint32_t k, const uint32_t* timeout,
+                  const uint32_t* subject_member, const uint8_t* state0, const uint32_t* inc0, uint32_t self_inc0) {
+  memset(w, 0, sizeof(*w));
+  w->lo = lo;
+  w->n_loc = n_loc;
+  w->S = S;
+  w->k = k;
+  for (int i = 0; i < 5; ++i) w->timeout[i] = timeout[i];
+  uint64_t ne = n_loc * S;
+  w->state = malloc(ne);
+  w->inc = malloc(ne * 4);
+  w->change = calloc(ne, 4);
+  w->nconf = calloc(ne, 1);
+  w->accuser = calloc(ne * 5, 4);
+  w->self_inc = malloc(n_loc * 4);
+  w->left = calloc(n_loc, 1);
+  w->subject_member = malloc((size_t)S * 4);
+  if (!w->state || !w->inc || !w->change || !w->nconf || !w->accuser || !w->self_inc || !w->left ||
+      !w->subject_member)
+    return -1;
+  memcpy(w->subject_member, subject_member, (size_t)S * 4);
+  for (uint64_t r = 0; r < n_loc; ++r) {
+    w->self_inc[r] = self_inc0;
+    for (uint32_t s = 0; s < S; ++s) {
+      w->state[r * S + s] = state0[s];
+      w->inc[r * S + s] = inc0[s];
+    }
+  }
+  return 0;
+}
+
+void orc_swim_free(orc_swim* w) {
+  free(w->state);
+  free(w->inc);
+  free(w->change);
+  free(w->nconf);
+  free(w->accuser);
+  free(w->self_inc);
+  free(w->left);
+  free(w->subject_member);
+  memset(w, 0, sizeof(*w));
+}
+
+void orc_swim_set_left(orc_swim* w, uint64_t member, uint8_t left) { w->left[member - w->lo] = left; }
+
+/* refute(me, accusedInc): inc = nextIncarnation(); if accusedInc >= inc,
+ * inc = skipIncarnation(accusedInc - inc + 1); me.Incarnation = inc */
+static uint32_t sw_refute_o(orc_swim* w, uint64_t r, uint64_t e, uint32_t accused) {
+  uint32_t inc = ++w->self_inc[r];
+  if (accused >= inc) {
+    w->self_inc[r] += accused - inc + 1;
+    inc = w->self_inc[r];
+  }
+  w->inc[e] = inc;
+  return inc;
+}
+
+/* aliveNode(a, notify, bootstrap=false).  A node never heard of is first added to
+ * nodeMap as StateDead with incarnation 0, then the incarnation checks run. */
+static int sw_alive_node(orc_swim* w, uint64_t r, uint64_t e, int is_local, uint32_t a_inc, uint32_t now,
+                         uint32_t* ref) {
+  if (w->state[e] == SW_UNKNOWN) {
+    w->state[e] = SW_DEAD;
+    w->inc[e] = 0;
+    w->change[e] = 0;
+    w->nconf[e] = 0;
+  }
+  if (a_inc <= w->inc[e] && !is_local) return 0;  /* old incarnation, not about us */
+  if (a_inc < w->inc[e] && is_local) return 0;    /* strictly older, about us */
+  w->nconf[e] = 0;                                /* delete(m.nodeTimers, a.Node) */
+  uint8_t old_state = w->state[e];
+  int flags = 0;
+  if (is_local) {
+    if (a_inc == w->inc[e]) return 0; /* same incarnation and (model) same meta: nothing to refute */
+    *ref = sw_refute_o(w, r, e, a_inc);
+    flags |= 2;
+  } else {
+    flags |= 1;
+    w->inc[e] = a_inc;
+    if (w->state[e] != SW_ALIVE) {
+      w->state[e] = SW_ALIVE;
+      w->change[e] = now;
+    }
+  }
+  if (old_state == SW_DEAD || old_state == SW_LEFT) flags |= 4; /* NotifyJoin */
+  return flags;
+}
+
+/* suspectNode(s) */
+static int sw_suspect_node(orc_swim* w, uint64_t r, uint64_t e, int is_local, uint32_t s_inc, uint32_t from,
+                           uint32_t now, uint32_t* ref) {
+  if (w->state[e] == SW_UNKNOWN) return 0;
+  if (s_inc < w->inc[e]) return 0;
+  if (w->state[e] == SW_SUSPECT) { /* timer exists: timer.Confirm(s.From) */
+    uint32_t n = w->nconf[e];
+    if (n >= w->k) return 0;
+    uint32_t* acc = w->accuser + e * 5;
+    for (uint32_t i = 0; i <= n; ++i)
+      if (acc[i] == from) return 0;
+    acc[n + 1] = from;
+    w->nconf[e] = (uint8_t)(n + 1);
+    return 1 | 32;
+  }
+  if (w->state[e] != SW_ALIVE) return 0;
+  if (is_local) {
+    *ref = sw_refute_o(w, r, e, s_inc);
+    return 2;
+  }
+  w->inc[e] = s_inc;
+  w->state[e] = SW_SUSPECT;
+  w->change[e] = now;
+  w->accuser[e * 5] = from;
+  w->nconf[e] = 0;
+  return 1 | 16;
+}
+
+/* deadNode(d) */
+static int sw_dead_node(orc_swim* w, uint64_t r, uint64_t e, int is_local, uint32_t d_inc, int node_is_from,
+                        uint32_t now, uint32_t* ref) {
+  if (w->state[e] == SW_UNKNOWN) return 0;
+  if (d_inc < w->inc[e]) return 0;
+  w->nconf[e] = 0; /* delete(m.nodeTimers, d.Node) */
+  if (w->state[e] == SW_DEAD || w->state[e] == SW_LEFT) return 0;
+  if (is_local && !w->left[r]) {
+    *ref = sw_refute_o(w, r, e, d_inc);
+    return 2;
+  }
+  w->inc[e] = d_inc;
+  w->state[e] = node_is_from ? SW_LEFT : SW_DEAD;
+  w->change[e] = now;
+  return 1 | 8;
+}
+
+void orc_swim_apply(orc_swim* w, const orc_swim_msg* m, uint64_t n, uint32_t now, int32_t* flags, uint32_t* refute_inc) {
+  for (uint64_t i = 0; i < n; ++i) {
+    uint64_t r = m[i].receiver - w->lo, e = r * w->S + m[i].subject;
+    uint32_t node = w->subject_member[m[i].subject];
+    int is_local = node == m[i].receiver;
+    uint32_t ref = 0;
+    int f = 0;
+    switch (m[i].type) {
+      case 0: f = sw_alive_node(w, r, e, is_local, m[i].incarnation, now, &ref); break;
+      case 1: f = sw_suspect_node(w, r, e, is_local, m[i].incarnation, m[i].from, now, &ref); break;
+      case 2: f = sw_dead_node(w, r, e, is_local, m[i].incarnation, node == m[i].from, now, &ref); break;
+      default: break;
+    }
+    flags[i] = f;
+    if (refute_inc) refute_inc[i] = ref;
+  }
+}
+
+/* suspicion timeout: the timer fires once now - start >= timeout(confirmations) and runs
+ * deadNode{Incarnation: state.Incarnation, Node, From: m.config.Name} */
+uint64_t orc_swim_tick(orc_swim* w, uint32_t now) {
+  uint64_t fired = 0;
+  for (uint64_t r = 0; r < w->n_loc; ++r)
+    for (uint32_t s = 0; s < w->S; ++s) {
+      uint64_t e = r * w->S + s;
+      if (w->state[e] != SW_SUSPECT) continue;
+      uint32_t c = w->nconf[e] <= w->k ? w->nconf[e] : w->k;
+      if (now - w->change[e] < w->timeout[c]) continue;
+      uint32_t me = (uint32_t)(w->lo + r), node = w->subject_member[s], ref = 0;
+      sw_dead_node(w, r, e, node == me, w->inc[e], node == me, now, &ref);
+      fired++;
+    }
+  return fired;
+}
+
+void orc_swim_dump(const orc_swim* w, uint64_t first, uint64_t count, uint8_t* state, uint32_t* inc, uint32_t* change,
+                   uint8_t* nconf, uint32_t* self_inc) {
+  for (uint64_t i = 0; i < count * w->S; ++i) {
+    uint64_t e = first * w->S + i;
+    int known = w->state[e] != SW_UNKNOWN;
+    state[i] = w->state[e];
+    inc[i] = known ? w->inc[e] : 0;
+    change[i] = known ? w->change[e] : 0;
+    nconf[i] = w->state[e] == SW_SUSPECT ? w->nconf[e] : 0;
+  }
+  for (uint64_t r = 0; r < count; ++r) self_inc[r] = w->self_inc[first + r];
+}

@@ -362,6 +362,39 @@ typedef struct {
  * IndexMap insertion order.  Returns number written. */
 uint32_t orc_coalesce_user_events(const orc_uevent* in, uint32_t n, orc_uevent* out);
 
+/* ---- memberlist SWIM layer model -------------------- */
+/* memberlist-core 0.2 is not vendored in the reference: PARITY UNPINNED.  A restatement
+ * of memberlist's published state machine -- aliveNode, suspectNode, deadNode, refute,
+ * suspicion.Confirm and the suspicion timeout -- for the entries (receiver, subject) of
+ * a shard.  Message layout = rsf_swim_msg; states / flags as include/ruserf_amd.h. */
+typedef struct orc_swim_msg {
+  uint32_t receiver, subject, incarnation, from, type, reserved;
+} orc_swim_msg;
+typedef struct orc_swim {
+  uint64_t lo, n_loc;
+  uint32_t S, k;
+  uint32_t timeout[5];
+  uint8_t* state;    /* [n_loc * S], 255 = not in nodeMap */
+  uint32_t* inc;     /* [n_loc * S] */
+  uint32_t* change;  /* [n_loc * S] state-change tick */
+  uint8_t* nconf;    /* [n_loc * S] confirmations of the running suspicion */
+  uint32_t* accuser; /* [n_loc * S * 5] first accuser, then the confirmers */
+  uint32_t* self_inc;/* [n_loc] m.incarnation */
+  uint8_t* left;     /* [n_loc] m.hasLeft() */
+  uint32_t* subject_member; /* [S] */
+} orc_swim;
+int orc_swim_init(orc_swim* w, uint64_t lo, uint64_t n_loc, uint32_t S, uint32_t k, const uint32_t* timeout,
+                  const uint32_t* subject_member, const uint8_t* state0, const uint32_t* inc0, uint32_t self_inc0);
+void orc_swim_free(orc_swim* w);
+void orc_swim_set_left(orc_swim* w, uint64_t member, uint8_t left);
+/* messages applied one by one in array order at tick now */
+void orc_swim_apply(orc_swim* w, const orc_swim_msg* m, uint64_t n, uint32_t now, int32_t* flags, uint32_t* refute_inc);
+/* suspicion timers due at now fire deadNode{inc, from = receiver}; returns how many */
+uint64_t orc_swim_tick(orc_swim* w, uint32_t now);
+/* as rsf_swim_dump: unknown entries read as (255, 0, 0, 0); confirmations only while suspect */
+void orc_swim_dump(const orc_swim* w, uint64_t first, uint64_t count, uint8_t* state, uint32_t* inc, uint32_t* change,
+                   uint8_t* nconf, uint32_t* self_inc);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,5 +10,5 @@ from .coordinate import (Coordinate, CoordinateClients, CoordinateError,  # noqa
                          CoordinateOptions)
 
 __version__ = "0.1.0"
-from . import gossip, workload  # noqa: F401,E402
+from . import gossip, swim, workload  # noqa: F401,E402
 from .gossip import GossipConfig, GossipEngine  # noqa: F401,E402

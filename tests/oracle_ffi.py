@@ -215,8 +215,70 @@ def lib():
     L.orc_wire_decode.argtypes = [P8, C.c_uint64, C.c_uint64, C.c_void_p]
     L.orc_coalesce_user_events.argtypes = [C.POINTER(UEvent), C.c_uint32, C.POINTER(UEvent)]
     L.orc_coalesce_user_events.restype = C.c_uint32
+    L.orc_swim_init.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, P32, P32, P8, P32,
+                                C.c_uint32]
+    L.orc_swim_free.argtypes = [C.c_void_p]
+    L.orc_swim_free.restype = None
+    L.orc_swim_set_left.argtypes = [C.c_void_p, C.c_uint64, C.c_uint8]
+    L.orc_swim_set_left.restype = None
+    L.orc_swim_apply.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.POINTER(C.c_int32), P32]
+    L.orc_swim_apply.restype = None
+    L.orc_swim_tick.argtypes = [C.c_void_p, C.c_uint32]
+    L.orc_swim_tick.restype = C.c_uint64
+    L.orc_swim_dump.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, P8, P32, P32, P8, P32]
+    L.orc_swim_dump.restype = None
     _lib = L
     return L
+
+
+class OrcSwim(C.Structure):
+    _fields_ = [("lo", C.c_uint64), ("n_loc", C.c_uint64), ("S", C.c_uint32), ("k", C.c_uint32),
+                ("timeout", C.c_uint32 * 5), ("_pad", C.c_uint32)] + \
+               [(f, C.c_void_p) for f in ("state", "inc", "change", "nconf", "accuser", "self_inc", "left",
+                                          "subject_member")]
+
+
+class OracleSwim:
+    """The oracle's memberlist SWIM model (orc_swim_*), same surface as ruserf_amd.swim.SwimState."""
+
+    def __init__(self, lo, n_loc, S, k, timeouts, subject_member, state0, inc0, self_inc0=1):
+        self.L, self.S, self.lo, self.n_loc = lib(), S, lo, n_loc
+        self.w = OrcSwim()
+        t = np.ascontiguousarray(timeouts, np.uint32)
+        sm = np.ascontiguousarray(subject_member, np.uint32)
+        st = np.ascontiguousarray(state0, np.uint8)
+        ic = np.ascontiguousarray(inc0, np.uint32)
+        rc = self.L.orc_swim_init(C.byref(self.w), lo, n_loc, S, k, t.ctypes.data_as(P32), sm.ctypes.data_as(P32),
+                                  st.ctypes.data_as(P8), ic.ctypes.data_as(P32), self_inc0)
+        assert rc == 0
+
+    def close(self):
+        self.L.orc_swim_free(C.byref(self.w))
+
+    def set_left(self, member, left=True):
+        self.L.orc_swim_set_left(C.byref(self.w), member, 1 if left else 0)
+
+    def apply(self, msgs, now):
+        n = len(msgs)
+        f = np.zeros(n, np.int32)
+        r = np.zeros(n, np.uint32)
+        m = np.ascontiguousarray(msgs)
+        self.L.orc_swim_apply(C.byref(self.w), m.ctypes.data, n, now, f.ctypes.data_as(C.POINTER(C.c_int32)),
+                              r.ctypes.data_as(P32))
+        return f, r
+
+    def tick(self, now):
+        return int(self.L.orc_swim_tick(C.byref(self.w), now))
+
+    def dump(self, first=0, count=None):
+        count = self.n_loc - first if count is None else count
+        S = self.S
+        st, inc, ch = np.zeros(count * S, np.uint8), np.zeros(count * S, np.uint32), np.zeros(count * S, np.uint32)
+        nc, si = np.zeros(count * S, np.uint8), np.zeros(count, np.uint32)
+        self.L.orc_swim_dump(C.byref(self.w), first, count, st.ctypes.data_as(P8), inc.ctypes.data_as(P32),
+                             ch.ctypes.data_as(P32), nc.ctypes.data_as(P8), si.ctypes.data_as(P32))
+        return {"state": st.reshape(count, S), "incarnation": inc.reshape(count, S),
+                "change": ch.reshape(count, S), "n_confirm": nc.reshape(count, S), "self_incarnation": si}
 
 
 class PPState(C.Structure):
