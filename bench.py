@@ -259,7 +259,10 @@ def main():
     # every engine launch goes to this stream; torch's default stream handle is NULL,
     # which the C ABI would read as "the context's own stream"
     torch.cuda.set_stream(torch.cuda.Stream())
-    if world > 1:
+    # RSF_FORCE_SHARDED=1 (under torch.distributed.run, one rank): the gossip bench runs the
+    # multi-GPU code path (ShardedGossip, RCCL collectives) on one GPU, to price its overhead
+    forced = os.environ.get("RSF_FORCE_SHARDED") == "1"
+    if world > 1 or forced:
         if backend == "gloo":
             torch.distributed.init_process_group("gloo")
         else:
@@ -304,7 +307,7 @@ def main():
             if k not in line and k not in ("metric",):
                 line[k] = res[k]
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if world > 1 or forced:
         torch.distributed.destroy_process_group()
 
 

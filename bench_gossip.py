@@ -56,7 +56,7 @@ def run_gossip(args, rank, world):
     subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED)
     views = W.initial_views(SUBJECTS)
     stream = torch.cuda.current_stream()
-    if world == 1:
+    if world == 1 and os.environ.get("RSF_FORCE_SHARDED") != "1":
         eng = GossipEngine(cfg, device=torch.cuda.current_device())
         eng.set_stream(stream.cuda_stream)
         step_fn = lambda t: eng.round(t, ml[t], acts[t])  # noqa: E731
@@ -121,7 +121,9 @@ def run_gossip(args, rank, world):
                    "members": n, "members_per_gpu": per, "fanout": 3, "items_per_target": 8,
                    "queue_cap_per_queue": cfg.queue_cap, "subjects": SUBJECTS,
                    "record_slots_per_group": min(3 * cfg.queue_cap, cfg.gossip_limit // (cfg.gossip_overhead + 18)),
-                   "settle_rounds": SETTLE_ROUNDS, "parallelism": f"members sharded x{world}"},
+                   "settle_rounds": SETTLE_ROUNDS, "parallelism": f"members sharded x{world}"
+                   + (" (multi-GPU code path forced)" if world == 1 and os.environ.get("RSF_FORCE_SHARDED") == "1"
+                      else "")},
         "merges_per_s": merged_all / wall,
         "records_per_round_per_gpu": records,
         "error_members": err_all,

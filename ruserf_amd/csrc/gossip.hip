@@ -648,11 +648,11 @@ __global__ void __launch_bounds__(256) segment_kernel(const uint32_t* __restrict
 // (end = inclusive scan of cnt); the last valid group publishes the record count.
 // kLanesPerGroup lanes per group, one record per lane.
 constexpr uint32_t kLanesPerGroup = 16;
+// The records go out packed as (receiver << 32 | rumor id): the exchange's send format.
 __global__ void __launch_bounds__(256) grp_expand_kernel(const uint32_t* __restrict__ key_s,
                                                          const uint32_t* __restrict__ end, uint64_t n,
                                                          uint32_t cap_t, const uint32_t* __restrict__ slots,
-                                                         uint32_t* __restrict__ out_key, uint32_t* __restrict__ out_val,
-                                                         unsigned long long* n_valid) {
+                                                         uint64_t* __restrict__ out, unsigned long long* n_valid) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t i = t / kLanesPerGroup;
   const uint32_t sub = (uint32_t)t % kLanesPerGroup;
@@ -661,10 +661,7 @@ __global__ void __launch_bounds__(256) grp_expand_kernel(const uint32_t* __restr
   if (key == kSentinel) return;
   const uint32_t o = i ? end[i - 1] : 0u, e = end[i];
   const uint32_t* src = slots + i * cap_t;
-  for (uint32_t k = sub; o + k < e; k += kLanesPerGroup) {
-    out_val[o + k] = src[k];
-    out_key[o + k] = key;
-  }
+  for (uint32_t k = sub; o + k < e; k += kLanesPerGroup) out[o + k] = ((uint64_t)key << 32) | src[k];
   if (sub == 0 && (i + 1 == n || key_s[i + 1] == kSentinel)) *n_valid = e;
 }
 
@@ -1313,7 +1310,7 @@ __global__ void fill_u64_kernel(uint64_t* p, uint64_t n, uint64_t v) {
   if (i < n) p[i] = v;
 }
 
-__global__ void shard_bounds_kernel(const uint32_t* __restrict__ keys, const unsigned long long* n_valid,
+__global__ void shard_bounds_kernel(const uint64_t* __restrict__ rec, const unsigned long long* n_valid,
                                     uint64_t per, uint32_t world, unsigned long long* __restrict__ bounds) {
   uint32_t w = threadIdx.x;
   if (w > world) return;
@@ -1322,17 +1319,10 @@ __global__ void shard_bounds_kernel(const uint32_t* __restrict__ keys, const uns
   uint64_t lo = 0, hi = nv;
   while (lo < hi) {
     uint64_t mid = (lo + hi) / 2;
-    if (keys[mid] < target) lo = mid + 1;
+    if ((rec[mid] >> 32) < target) lo = mid + 1;
     else hi = mid;
   }
   bounds[w] = (w == world) ? nv : lo;
-}
-
-__global__ void pack_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
-                            const unsigned long long* n_valid, uint64_t* __restrict__ out) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= *n_valid) return;
-  out[i] = ((uint64_t)keys[i] << 32) | vals[i];
 }
 
 __global__ void unpack_kernel(const uint64_t* __restrict__ in, uint64_t n, uint32_t* __restrict__ keys,
@@ -1903,7 +1893,7 @@ int rsf_gossip_rumor_block(rsf_gossip* g, void** p, uint64_t* bytes) {
 // cap_t slots per group, in (receiver; sender, position) order, with the group's count.
 // local: this context merges its own records (single context): also each receiver's
 // range of groups for merge_kernel.  Otherwise the groups are compacted into one
-// receiver-ordered record stream (sort_key / sort_val, n_valid) for the exchange.
+// receiver-ordered record stream (packed into send_buf, n_valid) for the exchange.
 static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local) {
   const GCfg& c = g->c;
   hipStream_t st = g->stream;
@@ -1932,7 +1922,7 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local) {
     RSF_HIP(hipcub::DeviceScan::InclusiveSum(g->grp_scan_tmp, tb, g->grp_cnt, g->grp_off, (int)ng, st));
     RSF_HIP(hipMemsetAsync(g->d_counters, 0, 8, st));
     hipLaunchKernelGGL(grp_expand_kernel, dim3(grid1(ng * kLanesPerGroup)), dim3(256), 0, st, g->grp_key_s,
-                       g->grp_off, ng, c.cap_t, g->stage_val, g->sort_key, g->sort_val, g->d_counters);
+                       g->grp_off, ng, c.cap_t, g->stage_val, g->send_buf, g->d_counters);
     RSF_HIP(hipGetLastError());
   }
   mark(g, 3);
@@ -1988,10 +1978,9 @@ int rsf_gossip_round_emit(rsf_gossip* g, uint32_t world, uint64_t* send_counts) 
   int rc = emit_and_sort(g, g->cur_round, false);
   if (rc) return rc;
   hipStream_t st = g->stream;
-  hipLaunchKernelGGL(shard_bounds_kernel, dim3(1), dim3(64), 0, st, g->sort_key, g->d_counters, c.N / world, world,
+  // emit_and_sort left the stream packed in send_buf (grp_expand_kernel)
+  hipLaunchKernelGGL(shard_bounds_kernel, dim3(1), dim3(64), 0, st, g->send_buf, g->d_counters, c.N / world, world,
                      g->d_counters + 1);
-  hipLaunchKernelGGL(pack_kernel, dim3(grid1(g->stage_cap)), dim3(256), 0, st, g->sort_key, g->sort_val,
-                     g->d_counters, g->send_buf);
   RSF_HIP(hipGetLastError());
   unsigned long long b[64];
   RSF_HIP(hipMemcpyAsync(b, g->d_counters, (world + 2) * 8, hipMemcpyDeviceToHost, st));

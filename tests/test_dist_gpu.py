@@ -69,3 +69,50 @@ def test_two_ranks_gloo_equal_one_context():
     for k in full:
         assert np.array_equal(np.concatenate([got[0][k], got[1][k]]), full[k]), k
     one.close()
+
+
+def _worker_rccl(port, q):
+    """ShardedGossip over RCCL ("nccl") with one rank: the exact collectives, stream
+    ordering and zero-copy engine buffers of the driver's multi-GPU bench."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    torch.cuda.set_stream(torch.cuda.Stream())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    from ruserf_amd import workload as W
+    from ruserf_amd.dist import ShardedGossip
+    cfg, subj, acts, ml = _cfg()
+    sg = ShardedGossip(cfg, 0, 1, device=0)
+    assert not sg.stage  # RCCL moves HBM directly
+    sg.eng.set_subjects(subj)
+    sg.eng.init_views(*W.initial_views(len(subj)))
+    for t in range(ROUNDS):
+        sg.round(t, ml[t], acts[t])
+    torch.cuda.synchronize()
+    st = H.normalize_queues(H.engine_state(sg.eng))
+    q.put({k: np.asarray(v) for k, v in st.items()})
+    sg.eng.close()
+    dist.destroy_process_group()
+
+
+def test_one_rank_rccl_equal_one_context():
+    from ruserf_amd import gossip as G
+    from ruserf_amd import workload as W
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29400 + os.getpid() % 1000
+    p = ctx.Process(target=_worker_rccl, args=(port, q))
+    p.start()
+    got = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    cfg, subj, acts, ml = _cfg()
+    one = G.GossipEngine(cfg)
+    one.set_subjects(subj)
+    one.init_views(*W.initial_views(len(subj)))
+    for t in range(ROUNDS):
+        one.round(t, ml[t], acts[t])
+    full = H.normalize_queues(H.engine_state(one))
+    for k in full:
+        assert np.array_equal(got[k], full[k]), k
+    one.close()
