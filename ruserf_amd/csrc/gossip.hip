@@ -536,6 +536,9 @@ __global__ void __launch_bounds__(256) grp_index_kernel(const uint32_t* __restri
 // first round trip of every member it owns before working through them, so the loads
 // of the next member are in flight while the current one runs (the kernels run at the
 // 8-waves/SIMD hardware cap and wait on memory half the time).
+#ifndef RSF_EMIT_WPB
+#define RSF_EMIT_WPB 1  // waves per emit_kernel block (1 measured ~1% faster than 2 or 4; 16: +8%)
+#endif
 #ifndef RSF_EMIT_PER_WAVE
 #define RSF_EMIT_PER_WAVE 1  // emit: 2, 8 and 16 per wave measured slower
 #endif
@@ -594,11 +597,11 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   if (err && lane == 0) s.err[l] |= err;
 }
 
-__global__ void __launch_bounds__(256) emit_kernel(GCfg c, GState s, const uint32_t* __restrict__ grp_key,
+__global__ void __launch_bounds__(64 * RSF_EMIT_WPB) emit_kernel(GCfg c, GState s, const uint32_t* __restrict__ grp_key,
                                                    const uint32_t* __restrict__ slot, uint32_t* __restrict__ cnt_s,
                                                    uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint64_t l = ((uint64_t)xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock +
+  const uint64_t l = ((uint64_t)xcd_block(blockIdx.x, gridDim.x) * RSF_EMIT_WPB +
                       (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)) * RSF_EMIT_PER_WAVE;
   if (l >= c.n_loc) return;
   EmitIn cur, nxt;
@@ -1911,7 +1914,8 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local) {
                      g->grp_slot, local ? g->seg_start : nullptr, local ? g->seg_end : nullptr);
   RSF_HIP(hipGetLastError());
   mark(g, 2);
-  hipLaunchKernelGGL(emit_kernel, dim3(grid1((c.n_loc + RSF_EMIT_PER_WAVE - 1) / RSF_EMIT_PER_WAVE, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0, st, c, g->s,
+  hipLaunchKernelGGL(emit_kernel, dim3(grid1((c.n_loc + RSF_EMIT_PER_WAVE - 1) / RSF_EMIT_PER_WAVE, RSF_EMIT_WPB)),
+                     dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s,
                      g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec);
   RSF_HIP(hipGetLastError());
   size_t tb = g->grp_scan_bytes;
