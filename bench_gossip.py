@@ -107,7 +107,10 @@ def run_gossip(args, rank, world):
     senders = per
     records = merged / max(1, args.steps)  # records per round on this shard
     emit_b, merge_b = kernel_bytes(cfg.queue_cap, senders, records)
-    dom = 2 if avg[2] >= avg[3] else 3
+    # with the exchange (N > 1, or the multi-GPU path forced) phase 2 also holds the
+    # collectives and the receive-side reordering, so the roofline is the merge kernel's
+    sharded = world > 1 or os.environ.get("RSF_FORCE_SHARDED") == "1"
+    dom = 3 if sharded or avg[3] >= avg[2] else 2
     dom_bytes = emit_b if dom == 2 else merge_b
     achieved = dom_bytes / (avg[dom] / 1e3) / 1e9
     return {
