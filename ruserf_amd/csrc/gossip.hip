@@ -576,7 +576,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
              ne2 = shfl_u32(e.head, 2) != kEmpty;
   if (np == 0 || !(ne0 || ne1 || ne2)) return;
   // decoration of the intents: their subject slots (subject and type share one 8-B word)
-  if (Q0.r != kEmpty) Q0.dec = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(s.rumors + Q0.r) + 16);
+  if (Q0.r != kEmpty) Q0.dec = s.rdec[Q0.r];
   if (ne1) q_load(c, s, l, 1, lane, Q1);
   if (ne2) q_load(c, s, l, 2, lane, Q2);
   uint32_t err = 0;
@@ -631,11 +631,21 @@ __device__ __forceinline__ uint32_t decorate(const rsf_rumor* __restrict__ rumor
   return w.x;
 }
 
+// The round's rumor block decorated once into a dense 4-B table (rdec): emission and the
+// receive side look a record's decoration up there instead of in the 24-B rumor bodies,
+// a table 6x denser in L2 / Infinity Cache.  Run after the block is complete (after the
+// all-reduce on the multi-GPU path).
+__global__ void __launch_bounds__(256) dec_fill_kernel(const rsf_rumor* __restrict__ rumors, uint32_t* __restrict__ rdec,
+                                                       uint64_t base, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) rdec[base + i] = decorate(rumors, (uint32_t)(base + i));
+}
+
 // segment bounds per receiver + record decoration (keys == nullptr: decoration only)
 __global__ void __launch_bounds__(256) segment_kernel(const uint32_t* __restrict__ keys, uint64_t n, uint64_t lo,
                                                       uint32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_end,
                                                       const uint32_t* __restrict__ vals,
-                                                      const rsf_rumor* __restrict__ rumors,
+                                                      const uint32_t* __restrict__ rdec,
                                                       uint32_t* __restrict__ dec) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -643,7 +653,7 @@ __global__ void __launch_bounds__(256) segment_kernel(const uint32_t* __restrict
   if (k == kSentinel) return;
   if (i == 0 || keys[i - 1] != k) seg_start[k - lo] = (uint32_t)i;
   if (i + 1 == n || keys[i + 1] != k) seg_end[k - lo] = (uint32_t)(i + 1);
-  if (dec) dec[i] = decorate(rumors, vals[i]);
+  if (dec) dec[i] = rdec[vals[i]];
 }
 
 // ---- multi-GPU send side: the records of the receiver-sorted groups (cap_t slots each,
@@ -1394,7 +1404,7 @@ __global__ void __launch_bounds__(256) runs_scatter_kernel(const uint64_t* __res
                                                            const uint32_t* __restrict__ rbase,
                                                            const uint32_t* __restrict__ seg_start,
                                                            uint32_t* __restrict__ vals,
-                                                           const rsf_rumor* __restrict__ rumors,
+                                                           const uint32_t* __restrict__ rdec,
                                                            uint32_t* __restrict__ dec) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -1405,7 +1415,7 @@ __global__ void __launch_bounds__(256) runs_scatter_kernel(const uint64_t* __res
   const uint64_t idx = r * n_loc + l;
   const uint32_t pos = seg_start[l] + rbase[idx] + (uint32_t)(i - rstart[idx]);
   vals[pos] = (uint32_t)x;
-  dec[pos] = decorate(rumors, (uint32_t)x);
+  dec[pos] = rdec[(uint32_t)x];
 }
 
 __global__ void __launch_bounds__(256) seg_end_kernel(uint64_t n_loc, const uint32_t* __restrict__ seg_start,
@@ -1582,7 +1592,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
       GA(s.q_txlen, n * 3 * c.qcap * 4) || GA(s.q_next_seq, n * 3 * 4) || GA(s.eb_ltime, n * c.ebuf * 8) ||
       GA(s.eb_cnt, n * c.ebuf * 4) || GA(s.eb_keys, n * c.ebuf * c.slot_k * 8) || GA(s.qb_ltime, n * c.qbuf * 8) ||
       GA(s.qb_cnt, n * c.qbuf * 4) || GA(s.qb_ids, n * c.qbuf * c.slot_k * 4) ||
-      GA(s.rumors, (size_t)cfg->max_rumors * sizeof(rsf_rumor)))
+      GA(s.rumors, (size_t)cfg->max_rumors * sizeof(rsf_rumor)) || GA(s.rdec, (size_t)cfg->max_rumors * 4))
     return fail(rc);
   g->stage_cap = n * c.fanout * c.cap_t;
   if (g->stage_cap >= 0xFFFFFFFFull) return fail(gerr("n_members x fanout x per-target records must fit 32 bits"));
@@ -1644,6 +1654,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   ms(s.qb_cnt, 0, n * c.qbuf * 4);
   ms(s.qb_ids, 0, n * c.qbuf * c.slot_k * 4);
   ms(s.rumors, 0, (size_t)cfg->max_rumors * sizeof(rsf_rumor));
+  ms(s.rdec, 0, (size_t)cfg->max_rumors * 4);
   if (!ok) return fail(rsf::set_error(RSF_ERR_HIP, "context initialisation failed"));
   // Serf::new increments every clock once (base.rs:195-199)
   hipLaunchKernelGGL(fill_u64_kernel, dim3(grid1(n)), dim3(256), 0, st, s.clock, n, 1ull);
@@ -1663,7 +1674,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
   void* ptrs[] = {s.clock,  s.eclock,      s.qclock,       s.emin,        s.qmin,     s.digest,     s.err,
                   s.alive,  s.serf_state,  s.member_subj,  s.subj_member, s.refute_cnt, s.refute_ltime, s.view,
                   s.q_rumor, s.q_seq,      s.q_txlen,      s.q_next_seq,  s.eb_ltime, s.eb_cnt,     s.eb_keys,
-                  s.qb_ltime, s.qb_cnt,    s.qb_ids,       s.rumors,      g->d_ml,    g->d_acts,    g->stage_key,
+                  s.qb_ltime, s.qb_cnt,    s.qb_ids,       s.rumors,      s.rdec,       g->d_ml,    g->d_acts,    g->stage_key,
                   g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters, g->rec_dec, g->pp_buf,
                   g->sort_tmp, g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
                   g->scan_tmp, g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
@@ -1820,7 +1831,7 @@ int rsf_gossip_apply_batch(rsf_gossip* g, const rsf_msg* msgs, uint64_t n, int32
   RSF_HIP(hipMemsetAsync(g->seg_start, 0, c.n_loc * 4, g->stream));
   RSF_HIP(hipMemsetAsync(g->seg_end, 0, c.n_loc * 4, g->stream));
   hipLaunchKernelGGL(segment_kernel, dim3(grid1(n)), dim3(256), 0, g->stream, (const uint32_t*)d[2], n, 0ull,
-                     g->seg_start, g->seg_end, (const uint32_t*)nullptr, (const rsf_rumor*)nullptr, (uint32_t*)nullptr);
+                     g->seg_start, g->seg_end, (const uint32_t*)nullptr, (const uint32_t*)nullptr, (uint32_t*)nullptr);
   hipLaunchKernelGGL(apply_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, g->stream, c, g->s, (const rsf_msg*)d[0],
                      (const uint32_t*)d[4], g->seg_start, g->seg_end, (int32_t*)d[5], (uint64_t*)d[6]);
   RSF_HIP(hipGetLastError());
@@ -1901,6 +1912,9 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local) {
   const GCfg& c = g->c;
   hipStream_t st = g->stream;
   const uint64_t ng = g->n_groups;
+  if (g->round_need)
+    hipLaunchKernelGGL(dec_fill_kernel, dim3(grid1(g->round_need)), dim3(256), 0, st, (const rsf_rumor*)g->s.rumors,
+                       g->s.rdec, (uint64_t)g->round_base, (uint64_t)g->round_need);
   hipLaunchKernelGGL(peers_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, c, g->s, round, g->grp_key);
   RSF_HIP(hipGetLastError());
   int rc = sort_pairs(g, g->grp_key, g->grp_key_s, g->grp_id, g->grp_id_s, ng);
@@ -1955,7 +1969,7 @@ static int segment_and_merge(rsf_gossip* g, const uint32_t* keys, const uint32_t
   RSF_HIP(hipMemsetAsync(g->seg_end, 0, c.n_loc * 4, st));
   if (n) {
     hipLaunchKernelGGL(segment_kernel, dim3(grid1(n)), dim3(256), 0, st, keys, n, c.lo, g->seg_start, g->seg_end,
-                       vals, (const rsf_rumor*)g->s.rumors, g->rec_dec);
+                       vals, (const uint32_t*)g->s.rdec, g->rec_dec);
   }
   return launch_merge(g, vals);
 }
@@ -2081,7 +2095,7 @@ int rsf_gossip_round_merge_runs(rsf_gossip* g, const uint64_t* recv, const uint6
   RSF_HIP(hipcub::DeviceScan::ExclusiveSum(g->scan_tmp, tb, g->run_total, g->seg_start, (int)c.n_loc, st));
   if (n)
     hipLaunchKernelGGL(runs_scatter_kernel, dim3(grid1(n)), dim3(256), 0, st, recv, n, g->d_run_off, n_runs, c.lo,
-                       c.n_loc, g->run_start, g->run_base, g->seg_start, g->sort_val, (const rsf_rumor*)g->s.rumors,
+                       c.n_loc, g->run_start, g->run_base, g->seg_start, g->sort_val, (const uint32_t*)g->s.rdec,
                        g->rec_dec);
   hipLaunchKernelGGL(seg_end_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, c.n_loc, g->seg_start, g->run_total,
                      g->seg_end);

@@ -52,6 +52,7 @@ struct GState {
   uint32_t* qb_cnt;
   uint32_t* qb_ids;
   rsf_rumor* rumors;
+  uint32_t* rdec;  // per rumor id: its record decoration (subject / kDecQuery / kDecEvent), 4 B
 };
 
 // per-member scalar state held in registers while a kernel works on it
