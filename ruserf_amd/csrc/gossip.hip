@@ -635,10 +635,27 @@ __device__ __forceinline__ uint32_t decorate(const rsf_rumor* __restrict__ rumor
 // receive side look a record's decoration up there instead of in the 24-B rumor bodies,
 // a table 6x denser in L2 / Infinity Cache.  Run after the block is complete (after the
 // all-reduce on the multi-GPU path).
+// The same pass keeps the rumor bodies without their 8-B key (only user events and
+// queries need it) as aligned 16-B records for the merge kernel's gather.
 __global__ void __launch_bounds__(256) dec_fill_kernel(const rsf_rumor* __restrict__ rumors, uint32_t* __restrict__ rdec,
-                                                       uint64_t base, uint64_t n) {
+                                                       uint4* __restrict__ rbody, uint64_t base, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) rdec[base + i] = decorate(rumors, (uint32_t)(base + i));
+  if (i >= n) return;
+  rdec[base + i] = decorate(rumors, (uint32_t)(base + i));
+  const uint2* w = reinterpret_cast<const uint2*>(rumors + base + i);  // ltime | key | subject..msg_len
+  const uint2 lt = w[0], tail = w[2];
+  rbody[base + i] = make_uint4(lt.x, lt.y, tail.x, tail.y);
+}
+// a rumor rebuilt from its 16-B body (+ the key when the record needs it)
+__device__ __forceinline__ rsf_rumor rumor_from_body(uint4 b, uint64_t key) {
+  rsf_rumor ru;
+  ru.ltime = ((uint64_t)b.y << 32) | b.x;
+  ru.key = key;
+  ru.subject = b.z;
+  ru.type = (uint8_t)(b.w & 0xFF);
+  ru.flags = (uint8_t)((b.w >> 8) & 0xFF);
+  ru.msg_len = (uint16_t)(b.w >> 16);
+  return ru;
 }
 
 // segment bounds per receiver + record decoration (keys == nullptr: decoration only)
@@ -837,7 +854,11 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
       ld2 = true;
     }
     rsf_rumor ru{};
-    if (valid) ru = s.rumors[rid];
+    if (valid) {  // the key only for user events / queries (the decoration says which)
+      const uint4 b = s.rbody[rid];
+      const uint64_t key = (dsub == kDecQuery || dsub == kDecEvent) ? s.rumors[rid].key : 0ull;
+      ru = rumor_from_body(b, key);
+    }
     ViewE pre{};
     if (is_view) pre = vrow[dsub];  // issued beside the rumor-body load
     const uint32_t my_subj = is_view ? dsub : 0xFFFFFFFFu;
@@ -1592,7 +1613,8 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
       GA(s.q_txlen, n * 3 * c.qcap * 4) || GA(s.q_next_seq, n * 3 * 4) || GA(s.eb_ltime, n * c.ebuf * 8) ||
       GA(s.eb_cnt, n * c.ebuf * 4) || GA(s.eb_keys, n * c.ebuf * c.slot_k * 8) || GA(s.qb_ltime, n * c.qbuf * 8) ||
       GA(s.qb_cnt, n * c.qbuf * 4) || GA(s.qb_ids, n * c.qbuf * c.slot_k * 4) ||
-      GA(s.rumors, (size_t)cfg->max_rumors * sizeof(rsf_rumor)) || GA(s.rdec, (size_t)cfg->max_rumors * 4))
+      GA(s.rumors, (size_t)cfg->max_rumors * sizeof(rsf_rumor)) || GA(s.rdec, (size_t)cfg->max_rumors * 4) ||
+      GA(s.rbody, (size_t)cfg->max_rumors * 16))
     return fail(rc);
   g->stage_cap = n * c.fanout * c.cap_t;
   if (g->stage_cap >= 0xFFFFFFFFull) return fail(gerr("n_members x fanout x per-target records must fit 32 bits"));
@@ -1655,6 +1677,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   ms(s.qb_ids, 0, n * c.qbuf * c.slot_k * 4);
   ms(s.rumors, 0, (size_t)cfg->max_rumors * sizeof(rsf_rumor));
   ms(s.rdec, 0, (size_t)cfg->max_rumors * 4);
+  ms(s.rbody, 0, (size_t)cfg->max_rumors * 16);
   if (!ok) return fail(rsf::set_error(RSF_ERR_HIP, "context initialisation failed"));
   // Serf::new increments every clock once (base.rs:195-199)
   hipLaunchKernelGGL(fill_u64_kernel, dim3(grid1(n)), dim3(256), 0, st, s.clock, n, 1ull);
@@ -1674,7 +1697,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
   void* ptrs[] = {s.clock,  s.eclock,      s.qclock,       s.emin,        s.qmin,     s.digest,     s.err,
                   s.alive,  s.serf_state,  s.member_subj,  s.subj_member, s.refute_cnt, s.refute_ltime, s.view,
                   s.q_rumor, s.q_seq,      s.q_txlen,      s.q_next_seq,  s.eb_ltime, s.eb_cnt,     s.eb_keys,
-                  s.qb_ltime, s.qb_cnt,    s.qb_ids,       s.rumors,      s.rdec,       g->d_ml,    g->d_acts,    g->stage_key,
+                  s.qb_ltime, s.qb_cnt,    s.qb_ids,       s.rumors,      s.rdec,       s.rbody,      g->d_ml,    g->d_acts,    g->stage_key,
                   g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters, g->rec_dec, g->pp_buf,
                   g->sort_tmp, g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
                   g->scan_tmp, g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
@@ -1914,7 +1937,7 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local) {
   const uint64_t ng = g->n_groups;
   if (g->round_need)
     hipLaunchKernelGGL(dec_fill_kernel, dim3(grid1(g->round_need)), dim3(256), 0, st, (const rsf_rumor*)g->s.rumors,
-                       g->s.rdec, (uint64_t)g->round_base, (uint64_t)g->round_need);
+                       g->s.rdec, g->s.rbody, (uint64_t)g->round_base, (uint64_t)g->round_need);
   hipLaunchKernelGGL(peers_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, c, g->s, round, g->grp_key);
   RSF_HIP(hipGetLastError());
   int rc = sort_pairs(g, g->grp_key, g->grp_key_s, g->grp_id, g->grp_id_s, ng);

@@ -53,6 +53,7 @@ struct GState {
   uint32_t* qb_ids;
   rsf_rumor* rumors;
   uint32_t* rdec;  // per rumor id: its record decoration (subject / kDecQuery / kDecEvent), 4 B
+  uint4* rbody;    // per rumor id: the rumor without its key (ltime, subject, type, flags, msg_len), 16 B
 };
 
 // per-member scalar state held in registers while a kernel works on it
