@@ -248,6 +248,9 @@ __device__ __forceinline__ void q_insert_batch(const GCfg& c, QRegs& Q, uint32_t
 // The lowest unpicked lane that fits IS the reference's pick (lowest transmits, then
 // longest fitting, then newest): every skipped lower lane did not fit and never will.
 template <bool PERMUTE_DEC>
+#ifndef RSF_EMIT_NT
+#define RSF_EMIT_NT 0  // emit: records written non-temporally
+#endif
 __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uint32_t lane, int64_t limit,
                                                     uint32_t* stage_val, uint32_t* stage_dec,
                                                     uint64_t out_base, uint32_t& nrec, uint32_t& err, bool& dirty) {
@@ -279,8 +282,13 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
     const uint32_t npick = (uint32_t)__popcll(pmask);
     const uint32_t rank = (uint32_t)__popcll(pmask & below_mask(lane));
     if (picked && nrec + rank < c.cap_t) {
+#if RSF_EMIT_NT
+      __builtin_nontemporal_store(Q.r, stage_val + out_base + nrec + rank);
+      __builtin_nontemporal_store(Q.dec, stage_dec + out_base + nrec + rank);
+#else
       stage_val[out_base + nrec + rank] = Q.r;
       stage_dec[out_base + nrec + rank] = Q.dec;
+#endif
     }
     if (nrec + npick > c.cap_t) err |= kErrStage;
     nrec += npick;
@@ -706,6 +714,17 @@ __global__ void __launch_bounds__(256) grp_expand_kernel(const uint32_t* __restr
 //   * digest contributions (member events, deliveries), refutations and
 //     re-queues are then applied serially in record order.
 // User events / queries (dedup rings in HBM) run serially in lane 0.
+#ifndef RSF_MERGE_NT
+#define RSF_MERGE_NT 0  // merge: records (ids, decorations, group counts) read non-temporally
+#endif
+// the merge's record streams are read once per round
+__device__ __forceinline__ uint32_t rec_ld(const uint32_t* p) {
+#if RSF_MERGE_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
 #ifndef RSF_MERGE_WAVES
 #define RSF_MERGE_WAVES 7  // min waves/SIMD for merge_kernel (register cap; 7 measured fastest with 8 receivers per wave, 8 before)
 #endif
@@ -825,18 +844,18 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     const uint64_t slot = base + lane;
     const bool in = lane < cnt;
     // slot contents and the group's record count in one round trip (holes read stale ids)
-    const uint32_t rid0 = in ? vals[slot] : 0;
+    const uint32_t rid0 = in ? rec_ld(vals + slot) : 0;
     uint32_t gk = 1, gc = 1;
     if (gcnt && in) {
       // group of the slot relative to the receiver's first group: a 32-bit division
       // (a receiver's slot range is small) instead of a 64-bit one
       const uint32_t rel = (uint32_t)(base - vs) + lane, gr = rel / stride;
       gk = rel - gr * stride;
-      gc = gcnt[st + gr];
+      gc = rec_ld(gcnt + st + gr);
     }
     // decoration (same round trip as the rumor ids): subject of an intent, or the
     // queue of an event / query; invalid lanes read as neither
-    const uint32_t dsub0 = in ? dec[slot] : kEmpty;
+    const uint32_t dsub0 = in ? rec_ld(dec + slot) : kEmpty;
     const bool valid = in && (!gcnt || gk < gc);
     const uint32_t rid = valid ? rid0 : 0;
     const uint32_t dsub = valid ? dsub0 : kEmpty;
