@@ -130,13 +130,22 @@ struct QRegs {
   uint32_t dec = 0;    // emit only: the item's record decoration (subject / kDecQuery / kDecEvent)
 };
 
+#ifndef RSF_Q_NT
+#define RSF_Q_NT 0  // broadcast queues (touched once by emit, once by merge per round) read / written non-temporally
+#endif
 __device__ __forceinline__ void q_load(const GCfg& c, const GState& s, uint64_t l, uint32_t q, uint32_t lane,
                                        QRegs& Q) {
   if (lane < c.qcap) {
     uint64_t i = (l * 3 + q) * c.qcap + lane;
+#if RSF_Q_NT
+    Q.r = __builtin_nontemporal_load(s.q_rumor + i);
+    Q.sq = __builtin_nontemporal_load(s.q_seq + i);
+    Q.tl = __builtin_nontemporal_load(s.q_txlen + i);
+#else
     Q.r = s.q_rumor[i];
     Q.sq = s.q_seq[i];
     Q.tl = s.q_txlen[i];
+#endif
   } else {
     Q.r = kEmpty;
     Q.sq = 0;
@@ -147,9 +156,15 @@ __device__ __forceinline__ void q_store(const GCfg& c, const GState& s, uint64_t
                                         const QRegs& Q, bool with_seq) {
   if (lane < c.qcap) {
     uint64_t i = (l * 3 + q) * c.qcap + lane;
+#if RSF_Q_NT
+    __builtin_nontemporal_store(Q.r, s.q_rumor + i);
+    __builtin_nontemporal_store(Q.tl, s.q_txlen + i);
+    if (with_seq) __builtin_nontemporal_store(Q.sq, s.q_seq + i);
+#else
     s.q_rumor[i] = Q.r;
     s.q_txlen[i] = Q.tl;
     if (with_seq) s.q_seq[i] = Q.sq;
+#endif
   }
 }
 
