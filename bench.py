@@ -1,7 +1,12 @@
 #!/usr/bin/env python3
 """bench.py — the driver's benchmark contract for ruserf_amd.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload gossip|vivaldi]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload gossip|vivaldi|pushpull|churn]
+
+BASELINE.json's metric has two halves, "gossip node-rounds/sec (whole node) at 16M
+members; Vivaldi updates/sec".  The default run measures both in one invocation: the
+gossip leg is the line's `value`, the Vivaldi leg (configs[4], 64M members) is the
+line's `vivaldi` object with its own ms_per_step, roofline and cpu_baseline.
 
 One step = one pass of the hot path over one batch of synthetic input:
   gossip  : one gossip round over the shard's members -> metric "node-rounds/s".
@@ -192,7 +197,7 @@ def run_vivaldi(args, rank, world):
     }
 
 
-def cpu_baseline_vivaldi(seconds_target=12.0):
+def cpu_baseline_vivaldi(seconds_target=8.0):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as O  # test infrastructure: the checker / CPU baseline only
     L = O.lib()
@@ -244,6 +249,7 @@ def main():
     ap.add_argument("--members", type=int, default=None, help="members per GPU")
     ap.add_argument("--members-total", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-vivaldi", action="store_true", help="gossip: skip the Vivaldi leg of the line")
     ap.add_argument("--refresh-every", type=int, default=1,
                     help="vivaldi, N>1: all-gather the coordinate table after every R-th round (C5: 1 and 8)")
     args = ap.parse_args()
@@ -295,7 +301,23 @@ def main():
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline_gossip(args)
-    attach_traffic(workload, res)
+        attach_traffic(workload, res)
+        if not args.no_vivaldi:
+            # the metric's second half, timed in the same invocation (configs[4]: 64M members)
+            vargs = argparse.Namespace(**vars(args))
+            vargs.members, vargs.members_total = 64_000_000, True
+            torch.cuda.empty_cache()
+            vres = run_vivaldi(vargs, rank, world)
+            attach_traffic("vivaldi", vres)
+            vcpu = None
+            if rank == 0 and world == 1 and not args.no_cpu_baseline:
+                vcpu = cpu_baseline_vivaldi()
+            res["vivaldi"] = {"metric": vres["metric"], "value": vres["value"], "unit": vres["unit"],
+                              "steps": args.steps, "warmup": args.warmup, "ms_per_step": vres["ms_per_step"],
+                              "scaling": vres["scaling"], "dtype": vres["dtype"], "config": vres["config"],
+                              "roofline": vres["roofline"], "cpu_baseline": vcpu}
+    if workload != "gossip":
+        attach_traffic(workload, res)
     if rank == 0:
         line = {
             "metric": res["metric"], "value": res["value"], "unit": res["unit"], "n_gpus": world,

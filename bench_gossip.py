@@ -23,26 +23,36 @@ HBM_PEAK_GBS = 8000.0
 
 def gossip_cfg(n_total, rounds_total, world, shard=None):
     from ruserf_amd.gossip import GossipConfig
+    # rumor ring: a power of two holding >= 64 rounds of rumor blocks (ids recycle after that)
     per_round = SUBJECTS * 4 + int(round(n_total * 0.01))
+    ring = 1 << max(10, (per_round * 64 - 1).bit_length())
     return GossipConfig(n_members=n_total, n_subjects=SUBJECTS, shard=shard, queue_cap=64, event_buffer_size=512,
                         query_buffer_size=512, slot_k=1, fanout=3, gossip_limit=8 * 24, gossip_overhead=2,
-                        retransmit_mult=4, max_refute=4, max_rumors=per_round * rounds_total + 1024, seed=SEED)
+                        retransmit_mult=4, max_refute=4, max_rumors=ring, seed=SEED)
+
+
+# B_merge = 16 (record read) + 16 (view entry read) + 16 (view entry write)
+# + 16 (clock r/w, counted once per record as an upper bound) = 64 B per merged record
+B_MERGE = 64
 
 
 def kernel_bytes(qcap, senders, records, fanout=3):
-    """Algorithmic HBM bytes per launch, what each kernel must move in
-    this workload (intents only: the query/event queues stay empty and are never
-    loaded; the intent queue is 12 B per slot: rumor id, insertion seq, transmits|len):
+    """Algorithmic HBM bytes per launch.
+
+    `roofline` (the driver line) prices the merge kernel with SURVEY §8(d)'s model
+    only: B_MERGE = 64 B per merged record.  The extended model (reported beside it)
+    adds what this engine's queue model must also move (intents
+    only: the query/event queues stay empty; the intent queue is 12 B per slot):
     emit  : per live sender its peers + group slots (8 B per peer), the intent queue
             read and written back (it is re-ranked after every pick), and per record
             the rumor id + decoration written (8 B), per group its count (4 B)
-    merge : per received record SURVEY's B_merge = 64 B (record 16, view entry read 16
-            + write 16, clock r/w 16) plus each receiver's intent queue read and
-            written back (re-queues)."""
+    merge : B_MERGE per record plus each receiver's intent queue read and written
+            back (re-queues)."""
     queue_rw = 2 * qcap * 12
     emit = senders * (fanout * 8 + queue_rw + fanout * 4) + records * 8
-    merge = records * 64 + senders * queue_rw
-    return emit, merge
+    merge_s8d = records * B_MERGE
+    merge_ext = merge_s8d + senders * queue_rw
+    return emit, merge_s8d, merge_ext
 
 
 def run_gossip(args, rank, world):
@@ -74,6 +84,7 @@ def run_gossip(args, rank, world):
     if world > 1:
         torch.distributed.barrier()
     merged0 = eng.merged_total()
+    pruned0 = int(eng.pruned().astype(np.uint64).sum())
     eng.set_profiling(True)
     torch.cuda.synchronize()
     if world > 1:
@@ -88,31 +99,37 @@ def run_gossip(args, rank, world):
     wall = time.perf_counter() - t0
     phase_ms, nr = eng.phase_times()
     merged = eng.merged_total() - merged0
+    pruned = int(eng.pruned().astype(np.uint64).sum()) - pruned0
     st = eng.members()
-    err_members = int(np.count_nonzero(st["err"]))
+    from ruserf_amd.gossip import E_QUEUE_PRUNE
+    # capacity errors other than the bounded queue's counted prunes (reported separately)
+    err_members = int(np.count_nonzero(st["err"] & ~np.uint32(E_QUEUE_PRUNE)))
+    qprune_members = int(np.count_nonzero(st["err"] & np.uint32(E_QUEUE_PRUNE)))
     eng.set_profiling(False)
     if world > 1:
         dev = "cpu" if torch.distributed.get_backend() == "gloo" else "cuda"
-        t_ = torch.tensor([wall, float(merged), float(err_members)], dtype=torch.float64, device=dev)
+        t_ = torch.tensor([wall, float(merged), float(err_members), float(pruned), float(qprune_members)],
+                          dtype=torch.float64, device=dev)
         mx = t_.clone()
         torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX)
         torch.distributed.all_reduce(t_)
-        wall, merged_all, err_all = float(mx[0]), float(t_[1]), float(t_[2])
+        wall, merged_all, err_all, pruned_all, qpm_all = float(mx[0]), float(t_[1]), float(t_[2]), float(t_[3]), \
+            float(t_[4])
     else:
-        merged_all, err_all = float(merged), float(err_members)
+        merged_all, err_all, pruned_all, qpm_all = float(merged), float(err_members), float(pruned), \
+            float(qprune_members)
+    eng.close()  # free the shard's HBM before bench.py's next leg
     node_rounds = n * args.steps
     avg = [x / max(1, nr) for x in phase_ms]  # ms per round per phase
     names = ["begin (memberlist+refute+originate)", "peers+group sort", "emit_kernel" + ("+exchange" if world > 1 else ""),
              "merge_kernel"]
     senders = per
     records = merged / max(1, args.steps)  # records per round on this shard
-    emit_b, merge_b = kernel_bytes(cfg.queue_cap, senders, records)
-    # with the exchange (N > 1, or the multi-GPU path forced) phase 2 also holds the
-    # collectives and the receive-side reordering, so the roofline is the merge kernel's
-    sharded = world > 1 or os.environ.get("RSF_FORCE_SHARDED") == "1"
-    dom = 3 if sharded or avg[3] >= avg[2] else 2
-    dom_bytes = emit_b if dom == 2 else merge_b
-    achieved = dom_bytes / (avg[dom] / 1e3) / 1e9
+    emit_b, merge_b, merge_ext = kernel_bytes(cfg.queue_cap, senders, records)
+    # the dominant kernel is the merge (phase 3); the roofline prices it with §8(d)'s bytes
+    dom = 3
+    achieved = merge_b / (avg[dom] / 1e3) / 1e9
+    achieved_ext = merge_ext / (avg[dom] / 1e3) / 1e9
     return {
         "metric": "gossip node-rounds/s", "value": node_rounds / wall, "unit": "node-rounds/s",
         "ms_per_step": wall / args.steps * 1e3, "dtype": "u64",
@@ -130,36 +147,60 @@ def run_gossip(args, rank, world):
         "merges_per_s": merged_all / wall,
         "records_per_round_per_gpu": records,
         "error_members": err_all,
+        # the bounded queue model (queue_cap slots) drops live items when full; counted, not silent
+        "queue_pruned_per_round": pruned_all / args.steps,
+        "queue_pruned_per_merged_record": pruned_all / max(1.0, merged_all),
+        "queue_prune_members": qpm_all,
         "phases_ms_per_round": dict(zip(names, avg)),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": names[dom],
-                     "bytes_per_launch": dom_bytes, "avg_launch_ms": avg[dom]},
+                     "bytes_model": "SURVEY 8(d): B_merge = 64 B per merged record",
+                     "bytes_per_unit": B_MERGE, "units_per_launch": records,
+                     "bytes_per_launch": merge_b, "avg_launch_ms": avg[dom],
+                     "extended": {"bytes_per_launch": merge_ext, "achieved": achieved_ext,
+                                  "frac": achieved_ext / HBM_PEAK_GBS,
+                                  "model": "B_merge per record + each receiver's intent queue read + "
+                                           "written back (2 x queue_cap x 12 B)"},
+                     "emit_kernel": {"avg_launch_ms": avg[2], "bytes_per_launch": emit_b,
+                                     "achieved": emit_b / (avg[2] / 1e3) / 1e9 if avg[2] else None}},
     }
 
 
-def cpu_baseline_gossip(args, seconds_target=12.0):
-    """The oracle's round (a single-threaded restatement of the same path) on a
-    bounded sample: N members, same subject count, settled, then timed."""
+def cpu_baseline_gossip(args, seconds_target=10.0, n=200_000):
+    """The oracle's round (the C restatement of the same path) on a bounded sample:
+    n members, the same subject count and workload, settled, then timed with all the
+    box's threads (orc_world_round_mt: member loops partitioned over pthreads, results
+    identical to one thread) and with one thread (both rates + the CPU)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import gossip_harness as H  # test infrastructure: checker / CPU baseline only
+    from bench import cpu_info, cpu_threads
     from ruserf_amd import workload as W
-    n = 100_000
-    rounds_total = 40
+    th = cpu_threads()
+    rounds_total = SETTLE_ROUNDS + 40
     cfg = gossip_cfg(n, rounds_total, 1)
     subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED)
     w = H.oracle_world(cfg, subj, W.initial_views(SUBJECTS))
     t = 0
     for _ in range(SETTLE_ROUNDS):
-        H.oracle_round(w, t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t], threads=th)
         t += 1
-    done, spent = 0, 0.0
-    while spent < seconds_target and t < rounds_total:
-        t0 = time.perf_counter()
-        H.oracle_round(w, t, ml[t], acts[t])
-        spent += time.perf_counter() - t0
-        done += 1
-        t += 1
+
+    def timed(threads, budget, max_rounds):
+        nonlocal t
+        done, spent = 0, 0.0
+        while spent < budget and done < max_rounds and t < rounds_total:
+            t0 = time.perf_counter()
+            H.oracle_round(w, t, ml[t], acts[t], threads=threads)
+            spent += time.perf_counter() - t0
+            done += 1
+            t += 1
+        return done, spent
+    done_mt, spent_mt = timed(th, seconds_target, 30)
+    done_1, spent_1 = timed(1, seconds_target / 2, 4)
     H.L.orc_world_free(C.byref(w))
-    return {"value": n * done / spent, "unit": "node-rounds/s", "cores": 1, "kind": "port",
-            "sample": f"oracle gossip rounds, {n} members, {SUBJECTS} subjects, {done} settled rounds "
-                      f"({spent:.1f}s), single thread"}
+    return {"value": n * done_mt / spent_mt, "unit": "node-rounds/s", "cores": th, "kind": "port",
+            "value_1thread": n * done_1 / spent_1,
+            "cpu_model": cpu_info(),
+            "sample": f"oracle gossip rounds (orc_world_round_mt), {n} members, {SUBJECTS} subjects, same workload "
+                      f"settled {SETTLE_ROUNDS} rounds; {done_mt} rounds on {th} threads ({spent_mt:.1f}s), "
+                      f"{done_1} rounds on 1 thread ({spent_1:.1f}s); {cpu_info()}"}

@@ -25,7 +25,7 @@ def pp_cfg(n, rounds):
     per_round = SUBJECTS * 4 + int(round(n * 0.01)) + 256
     return GossipConfig(n_members=n, n_subjects=SUBJECTS, queue_cap=64, event_buffer_size=512,
                         query_buffer_size=512, slot_k=1, fanout=3, gossip_limit=8 * 24, gossip_overhead=2,
-                        retransmit_mult=4, max_refute=4, max_rumors=per_round * rounds + 1024, seed=SEED)
+                        retransmit_mult=4, max_refute=4, max_rumors=1 << max(10, (per_round * rounds - 1).bit_length()), seed=SEED)
 
 
 def state_bytes(cfg):

@@ -204,6 +204,15 @@ int rsf_vivaldi_true_rtt_ns(rsf_vivaldi* v, uint32_t a, uint32_t b, uint64_t* ns
 #define RSF_F_PRUNE 4           /* prune requested (base.rs:1472-1523) */
 #define RSF_F_DELIVER 8         /* event/query delivered to the application (event_tx) */
 #define RSF_F_MEMBER_EVENT 16   /* a MemberEvent was emitted */
+/* per-member error bits (rsf_gossip_dump_members err[]): a fixed capacity of the
+ * round model was exceeded.  RSF_E_QUEUE_PRUNE is the model's bounded queue dropping
+ * a live item (the largest in send order, as memberlist's Prune would); the count of
+ * such drops is rsf_gossip_dump_pruned's. */
+#define RSF_E_EVSLOT 1          /* a user-event dedup slot held slot_k keys already */
+#define RSF_E_QSLOT 2           /* a query dedup slot held slot_k ids already */
+#define RSF_E_REFUTE 4          /* more than max_refute refutations of a subject in one round */
+#define RSF_E_STAGE 8           /* a (sender, peer) message held more than cap_t records */
+#define RSF_E_QUEUE_PRUNE 16    /* a transmit-limited queue was full: a live item was dropped */
 
 typedef struct rsf_gossip_cfg {
   uint64_t n_members;          /* N (global) */
@@ -218,7 +227,9 @@ typedef struct rsf_gossip_cfg {
   uint32_t gossip_overhead;    /* per-message compound overhead */
   uint32_t retransmit_mult;    /* memberlist retransmit_mult (LAN: 4) */
   uint32_t max_refute;         /* refutations buffered per subject per round, 1..4 */
-  uint32_t max_rumors;         /* rumor table capacity */
+  uint32_t max_rumors;         /* rumor ring capacity, a power of two: every round takes a block of
+                                  n_subjects * max_refute + n_acts ids; a queue item whose slot has
+                                  been recycled since expires at its member's next emission */
   uint32_t _reserved;
   uint64_t seed;               /* Philox key of peer selection */
 } rsf_gossip_cfg;
@@ -369,6 +380,21 @@ int rsf_gossip_push_pull_device(rsf_gossip* g, const rsf_pp_pair* pairs_dev, uin
 int rsf_gossip_reap(rsf_gossip* g, uint32_t now, uint32_t reconnect_timeout, uint32_t tombstone_timeout,
                     uint32_t recent_intent_timeout);
 int rsf_gossip_set_now(rsf_gossip* g, uint32_t now);
+
+/* ---- QueueChecker (core/src/serf/base.rs:703-760) ---------------------------
+ * One checker tick over the three queues of every shard member: max =
+ * max_queue_depth, or, when min_queue_depth > 0, max(2 * n_members, min_queue_depth)
+ * (get_queue_max); a queue holding >= max items is pruned to max (memberlist
+ * TransmitLimitedQueue::prune drops the last items in send order).  depth_warning
+ * is the log threshold.  Host outputs (optional, 3 entries each, per queue
+ * intent / query / event): items queued over the shard, members at or above the
+ * warning depth, items pruned.  Synchronises. */
+int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_queue_depth,
+                            uint32_t depth_warning, uint64_t* num_queued, uint64_t* n_warn, uint64_t* n_pruned);
+/* Per shard member (host, n_loc each, cumulative; either may be NULL): pruned = live
+ * items its bounded queues dropped when full; expired = queue items dropped at
+ * emission because their rumor slot was recycled (see max_rumors). */
+int rsf_gossip_dump_pruned(rsf_gossip* g, uint32_t* pruned, uint32_t* expired);
 
 /* Inspection (host copies; synchronise).  Arrays are over the shard's members. */
 int rsf_gossip_dump_members(rsf_gossip* g, uint64_t* clock, uint64_t* event_clock, uint64_t* query_clock,

@@ -560,7 +560,8 @@ static inline void digest_member_event(orc_world* w, uint32_t m, uint32_t ev, ui
 int orc_world_init(orc_world* w, const orc_world_cfg* c) {
   memset(w, 0, sizeof(*w));
   if (c->n < 2 || c->s == 0 || c->s > c->n || c->qcap == 0 || c->qcap > 64 || c->ebuf == 0 ||
-      c->qbuf == 0 || c->slot_k == 0 || c->fanout == 0 || c->fanout >= c->n || c->max_refute == 0)
+      c->qbuf == 0 || c->slot_k == 0 || c->fanout == 0 || c->fanout >= c->n || c->max_refute == 0 ||
+      c->cap_rumors == 0 || (c->cap_rumors & (c->cap_rumors - 1)) || c->cap_rumors > (1u << 31))
     return -1;
   w->n = c->n;
   w->s = c->s;
@@ -583,12 +584,15 @@ int orc_world_init(orc_world* w, const orc_world_cfg* c) {
       A(q_seq, n * 3 * c->qcap) || A(q_tx, n * 3 * c->qcap) || A(q_len, n * 3 * c->qcap) ||
       A(q_next_seq, n * 3) || A(eb_ltime, n * c->ebuf) || A(eb_cnt, n * c->ebuf) ||
       A(eb_keys, n * c->ebuf * c->slot_k) || A(qb_ltime, n * c->qbuf) || A(qb_cnt, n * c->qbuf) ||
-      A(qb_ids, n * c->qbuf * c->slot_k) || A(rumors, c->cap_rumors ? c->cap_rumors : 1) || A(v_time, n * s)) {
+      A(qb_ids, n * c->qbuf * c->slot_k) || A(rumors, c->cap_rumors ? c->cap_rumors : 1) || A(v_time, n * s) ||
+      A(q_pruned, n) || A(q_expired, n) || A(rgen, c->cap_rumors ? c->cap_rumors : 1)) {
     orc_world_free(w);
     return -1;
   }
 #undef A
   w->cap_rumors = c->cap_rumors;
+  w->rbits = 0;
+  while ((1u << w->rbits) < c->cap_rumors && w->rbits < 31) w->rbits++;
   for (size_t m = 0; m < n; ++m) {
     /* Serf::new: every clock incremented once (base.rs:195-199) */
     w->clock[m] = 1;
@@ -607,7 +611,7 @@ void orc_world_free(orc_world* w) {
                   w->serf_state, w->err, w->subj_member, w->member_subj, w->refute_cnt,
                   w->refute_ltime, w->v_ltime, w->v_status, w->v_kind, w->q_rumor, w->q_seq,
                   w->q_tx, w->q_len, w->q_next_seq, w->eb_ltime, w->eb_cnt, w->eb_keys,
-                  w->qb_ltime, w->qb_cnt, w->qb_ids, w->rumors, w->v_time};
+                  w->qb_ltime, w->qb_cnt, w->qb_ids, w->rumors, w->v_time, w->q_pruned, w->q_expired, w->rgen};
   for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) free(ptrs[i]);
   memset(w, 0, sizeof(*w));
 }
@@ -643,6 +647,18 @@ int orc_handle_join_intent(orc_world* w, uint32_t m, uint32_t subj, uint64_t lti
   return orc_upsert_intent(w, m, subj, ORC_K_INTENT_JOIN, ltime) ? ORC_F_REBROADCAST : 0;
 }
 
+static void erase_entry(orc_world* w, size_t e);
+
+/* handle_prune  base.rs:1587-1612: erase_node! (members.states.remove; the member also
+ * leaves left_members) and a Reap MemberEvent.  The reference first sleeps
+ * broadcast_timeout + leave_propagate_delay when the member is Leaving; the round
+ * model erases at once. */
+static int handle_prune(orc_world* w, uint32_t m, uint32_t subj, size_t e) {
+  erase_entry(w, e);
+  digest_member_event(w, m, EV_REAP, subj);
+  return ORC_F_PRUNE;
+}
+
 /* handle_node_leave_intent  base.rs:1409-1528 */
 int orc_handle_leave_intent(orc_world* w, uint32_t m, uint32_t subj, uint64_t ltime, int prune,
                             uint64_t* refute_ltime) {
@@ -657,16 +673,18 @@ int orc_handle_leave_intent(orc_world* w, uint32_t m, uint32_t subj, uint64_t lt
     return ORC_F_REFUTE;
   }
   w->v_ltime[e] = ltime; /* 1464 */
-  int pf = prune ? ORC_F_PRUNE : 0;
   switch (w->v_status[e]) {
     case ORC_ST_NONE: return 0;
-    case ORC_ST_ALIVE: w->v_status[e] = ORC_ST_LEAVING; return ORC_F_REBROADCAST | pf;
+    case ORC_ST_ALIVE: /* 1469-1478 */
+      w->v_status[e] = ORC_ST_LEAVING;
+      return ORC_F_REBROADCAST | (prune ? handle_prune(w, m, subj, e) : 0);
     case ORC_ST_LEAVING:
-    case ORC_ST_LEFT: return ORC_F_REBROADCAST | pf;
-    case ORC_ST_FAILED:
+    case ORC_ST_LEFT: /* 1479-1486 */
+      return ORC_F_REBROADCAST | (prune ? handle_prune(w, m, subj, e) : 0);
+    case ORC_ST_FAILED: /* 1487-1526: Failed -> Left, Leave event, then the prune */
       w->v_status[e] = ORC_ST_LEFT;
       digest_member_event(w, m, EV_LEAVE, subj);
-      return ORC_F_REBROADCAST | ORC_F_MEMBER_EVENT | pf;
+      return ORC_F_REBROADCAST | ORC_F_MEMBER_EVENT | (prune ? handle_prune(w, m, subj, e) : 0);
     default: return 0;
   }
 }
@@ -764,7 +782,7 @@ static inline uint64_t tlq_key(uint16_t tx, uint16_t len, uint32_t seq) {
 void orc_queue_insert(orc_world* w, uint32_t m, uint32_t q, uint32_t rumor) {
   size_t base = ((size_t)m * 3 + q) * w->qcap;
   uint32_t seq = w->q_next_seq[(size_t)m * 3 + q]++;
-  uint16_t len = w->rumors[rumor].msg_len;
+  uint16_t len = w->rumors[rumor & (w->cap_rumors - 1)].msg_len;
   uint32_t slot = EMPTY_RUMOR;
   for (uint32_t i = 0; i < w->qcap; ++i)
     if (w->q_rumor[base + i] == EMPTY_RUMOR) {
@@ -772,6 +790,8 @@ void orc_queue_insert(orc_world* w, uint32_t m, uint32_t q, uint32_t rumor) {
       break;
     }
   if (slot == EMPTY_RUMOR) { /* full: prune the last item in send order */
+    w->q_pruned[m]++;
+    w->err[m] |= ORC_E_QUEUE_PRUNE;
     uint64_t kmax = 0;
     for (uint32_t i = 0; i < w->qcap; ++i) {
       uint64_t k = tlq_key(w->q_tx[base + i], w->q_len[base + i], w->q_seq[base + i]);
@@ -786,6 +806,29 @@ void orc_queue_insert(orc_world* w, uint32_t m, uint32_t q, uint32_t rumor) {
   w->q_seq[base + slot] = seq;
   w->q_tx[base + slot] = 0;
   w->q_len[base + slot] = len;
+}
+
+uint32_t orc_rumor_generations(const orc_world* w) {
+  /* ids gen << rbits | slot never reach 0xFFFFFFFF (the empty-queue-slot marker) */
+  return w->rbits >= 32 ? 1u : (uint32_t)((1ull << (32 - w->rbits)) - 1);
+}
+
+int orc_rumor_live(const orc_world* w, uint32_t rid) {
+  return w->rgen[rid & (w->cap_rumors - 1)] == (rid >> w->rbits);
+}
+
+uint32_t orc_queue_expire(orc_world* w, uint32_t m, uint32_t q) {
+  size_t base = ((size_t)m * 3 + q) * w->qcap;
+  uint32_t cnt = 0;
+  for (uint32_t i = 0; i < w->qcap; ++i) {
+    if (w->q_rumor[base + i] == EMPTY_RUMOR || orc_rumor_live(w, w->q_rumor[base + i])) continue;
+    w->q_rumor[base + i] = EMPTY_RUMOR;
+    w->q_seq[base + i] = 0;
+    w->q_tx[base + i] = 0;
+    w->q_len[base + i] = 0;
+    cnt++;
+  }
+  return cnt;
 }
 
 /* get_broadcasts: lowest transmits first, then the largest message that fits,
@@ -826,6 +869,40 @@ uint32_t orc_queue_get_broadcasts(orc_world* w, uint32_t m, uint32_t q, uint32_t
   return cnt;
 }
 
+void orc_check_queues(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
+                      uint64_t* stats) {
+  uint64_t st[9] = {0};
+  uint64_t mx = max_queue_depth; /* get_queue_max  base.rs:748-759 */
+  if (min_queue_depth > 0) mx = 2ull * w->n > min_queue_depth ? 2ull * w->n : min_queue_depth;
+  for (uint32_t m = 0; m < w->n; ++m)
+    for (uint32_t q = 0; q < 3; ++q) {
+      size_t base = ((size_t)m * 3 + q) * w->qcap;
+      uint32_t numq = 0;
+      for (uint32_t i = 0; i < w->qcap; ++i) numq += w->q_rumor[base + i] != EMPTY_RUMOR;
+      st[q] += numq;
+      if (numq >= depth_warning) st[3 + q]++;
+      while (numq > mx) { /* numq >= max -> prune(max): drop the max item until max remain */
+        uint32_t worst = EMPTY_RUMOR;
+        uint64_t kmax = 0;
+        for (uint32_t i = 0; i < w->qcap; ++i) {
+          if (w->q_rumor[base + i] == EMPTY_RUMOR) continue;
+          uint64_t k = tlq_key(w->q_tx[base + i], w->q_len[base + i], w->q_seq[base + i]);
+          if (worst == EMPTY_RUMOR || k > kmax) {
+            kmax = k;
+            worst = i;
+          }
+        }
+        w->q_rumor[base + worst] = EMPTY_RUMOR;
+        w->q_seq[base + worst] = 0;
+        w->q_tx[base + worst] = 0;
+        w->q_len[base + worst] = 0;
+        numq--;
+        st[6 + q]++;
+      }
+    }
+  if (stats) memcpy(stats, st, sizeof(st));
+}
+
 /* kRandomNodes model: k distinct live peers != m, Philox-drawn (memberlist util.go; unpinned) */
 uint32_t orc_pick_peers(uint64_t seed, uint32_t n, const uint8_t* alive, uint32_t m, uint32_t round,
                         uint32_t k, uint32_t* out) {
@@ -852,7 +929,7 @@ static uint32_t queue_of(uint8_t type) {
 
 static uint32_t new_rumor(orc_world* w, uint32_t id, uint8_t type, uint8_t flags, uint32_t subject,
                           uint64_t ltime, uint64_t key, uint32_t name_len, uint32_t payload_len) {
-  orc_rumor* r = &w->rumors[id];
+  orc_rumor* r = &w->rumors[id & (w->cap_rumors - 1)];
   r->type = type;
   r->flags = flags;
   r->subject = subject;
@@ -871,7 +948,7 @@ static void push_refute(orc_world* w, uint32_t m, uint64_t ltime) {
 
 /* apply one received rumor at receiver r  (notify_message, delegate.rs:157-305) */
 static void merge_one(orc_world* w, uint32_t r, uint32_t rid) {
-  const orc_rumor* ru = &w->rumors[rid];
+  const orc_rumor* ru = &w->rumors[rid & (w->cap_rumors - 1)];
   int f = 0;
   uint64_t refute = 0;
   switch (ru->type) {
@@ -883,7 +960,6 @@ static void merge_one(orc_world* w, uint32_t r, uint32_t rid) {
     case ORC_MSG_QUERY: f = orc_handle_query(w, r, ru->ltime, (uint32_t)ru->key, ru->flags & 1); break;
     default: return;
   }
-  w->merges++;
   if (f & ORC_F_REFUTE) push_refute(w, r, refute);
   if (f & ORC_F_REBROADCAST) orc_queue_insert(w, r, queue_of(ru->type), rid);
 }
@@ -897,30 +973,148 @@ static void broadcast_join(orc_world* w, uint32_t m, uint64_t ltime, uint32_t ri
   orc_queue_insert(w, m, ORC_Q_INTENT, rid);
 }
 
-int orc_world_round(orc_world* w, uint32_t round, const orc_ml_event* ml, uint32_t n_ml,
-                    const orc_action* acts, uint32_t n_acts) {
-  const uint32_t n = w->n, k = w->fanout;
+/* ---- the round's member-parallel phases.  Members are independent inside each
+ * phase (a handler touches only its receiver's state; the rumor table and the
+ * liveness array are read-only there), so the threaded round is identical to
+ * the sequential one: it only partitions the member loops over threads. */
+typedef struct {
+  orc_world* w;
+  uint32_t lo, hi, round;
+  const orc_ml_event* ml;
+  uint32_t n_ml;
+  /* emission output (sender range [lo, hi) in sender order) */
+  uint32_t *rec_recv, *rec_rumor;
+  size_t nrec, cap;
+  /* merge input */
+  const uint32_t *off, *order;
+  uint64_t merges, sends;
+  int phase, fail;
+} world_job;
+
+/* 1. memberlist-detected transitions (M6) at every live member but the subject.
+ *    Per member: events in order; its liveness changes only by events about itself. */
+static void phase_ml(world_job* j) {
+  orc_world* w = j->w;
+  for (uint32_t m = j->lo; m < j->hi; ++m) {
+    uint8_t al = w->alive[m];
+    for (uint32_t e = 0; e < j->n_ml; ++e) {
+      uint32_t subj = j->ml[e].subject, sm = w->subj_member[subj];
+      if (sm == m && j->ml[e].set_alive == 1) {
+        al = 1;
+        w->serf_state[m] = ORC_SERF_ALIVE;
+      }
+      if (al && m != sm) {
+        if (j->ml[e].kind == ORC_ML_JOIN) orc_handle_node_join(w, m, subj);
+        else orc_handle_node_leave(w, m, subj);
+      }
+      if (sm == m && j->ml[e].set_alive == 0) al = 0;
+    }
+    w->alive[m] = al;
+  }
+}
+
+/* 4. emission: each live sender, k peers, broadcast_messages (delegate.rs:307-374) */
+static void phase_emit(world_job* j) {
+  orc_world* w = j->w;
+  const uint32_t n = w->n, k = w->fanout, cap_t = 3 * w->qcap;
+  uint32_t peers[64], buf[3 * 64];
+  j->cap = (size_t)(j->hi - j->lo) * k * cap_t;
+  j->rec_recv = (uint32_t*)malloc((j->cap ? j->cap : 1) * sizeof(uint32_t));
+  j->rec_rumor = (uint32_t*)malloc((j->cap ? j->cap : 1) * sizeof(uint32_t));
+  if (!j->rec_recv || !j->rec_rumor) {
+    j->fail = 1;
+    return;
+  }
+  for (uint32_t m = j->lo; m < j->hi; ++m) {
+    if (!w->alive[m]) continue;
+    uint32_t np = orc_pick_peers(w->seed, n, w->alive, m, j->round, k, peers);
+    if (np) /* items whose rumor slot was recycled have expired */
+      for (uint32_t q = 0; q < 3; ++q) w->q_expired[m] += orc_queue_expire(w, m, q);
+    for (uint32_t p = 0; p < np; ++p) {
+      uint32_t used = 0, got = 0, b;
+      for (uint32_t q = 0; q < 3; ++q) {
+        got += orc_queue_get_broadcasts(w, m, q, w->limit - used, buf + got, cap_t - got, &b);
+        used += b;
+      }
+      for (uint32_t i = 0; i < got; ++i) {
+        j->rec_recv[j->nrec] = peers[p];
+        j->rec_rumor[j->nrec] = buf[i];
+        j->nrec++;
+      }
+      j->sends += got;
+    }
+  }
+}
+
+/* 5. merge at every live receiver, its records in canonical (sender, position) order */
+static void phase_merge(world_job* j) {
+  orc_world* w = j->w;
+  for (uint32_t r = j->lo; r < j->hi; ++r) {
+    if (!w->alive[r]) continue;
+    for (uint32_t i = j->off[r]; i < j->off[r + 1]; ++i) {
+      merge_one(w, r, j->order[i]);
+      j->merges++;
+    }
+  }
+}
+
+static void* world_worker(void* arg) {
+  world_job* j = (world_job*)arg;
+  if (j->phase == 1) phase_ml(j);
+  else if (j->phase == 4) phase_emit(j);
+  else phase_merge(j);
+  return NULL;
+}
+
+static void run_phase(world_job* jobs, int nt) {
+  if (nt == 1) {
+    world_worker(&jobs[0]);
+    return;
+  }
+  pthread_t th[256];
+  for (int i = 0; i < nt; ++i) pthread_create(&th[i], NULL, world_worker, &jobs[i]);
+  for (int i = 0; i < nt; ++i) pthread_join(th[i], NULL);
+}
+
+int orc_world_round_mt(orc_world* w, uint32_t round, const orc_ml_event* ml, uint32_t n_ml,
+                       const orc_action* acts, uint32_t n_acts, int nthreads) {
+  const uint32_t n = w->n;
+  int nt = nthreads < 1 ? 1 : (nthreads > 256 ? 256 : nthreads);
+  if ((uint32_t)nt > n) nt = (int)n;
+  world_job jobs[256];
+  memset(jobs, 0, sizeof(world_job) * (size_t)nt);
+  const uint32_t per = (n + (uint32_t)nt - 1) / (uint32_t)nt;
+  for (int i = 0; i < nt; ++i) {
+    uint32_t lo = (uint32_t)i * per, hi = lo + per;
+    jobs[i].w = w;
+    jobs[i].lo = lo < n ? lo : n;
+    jobs[i].hi = hi < n ? hi : n;
+    jobs[i].round = round;
+    jobs[i].ml = ml;
+    jobs[i].n_ml = n_ml;
+  }
   w->now = round;
-  /* rumor ids of this round: [refutes: s*max_refute][actions: n_acts] */
-  uint32_t base = w->n_rumors;
+  /* rumor ids of this round: [refutes: s*max_refute][actions: n_acts], a contiguous
+   * block of the ring (restarting at slot 0 with the next generation when it would
+   * cross the end); id = generation << rbits | slot */
   uint32_t need = w->s * w->max_refute + n_acts;
-  if (base + need > w->cap_rumors) return -1;
-  for (uint32_t i = 0; i < need; ++i) w->rumors[base + i].type = 0xFF;
+  if (need > w->cap_rumors) return -1;
+  if (w->n_rumors + need > w->cap_rumors) {
+    w->n_rumors = 0;
+    w->gen = (w->gen + 1) % orc_rumor_generations(w);
+  }
+  const uint32_t slot0 = w->n_rumors;
+  uint32_t base = (uint32_t)(((uint64_t)w->gen << w->rbits) | slot0);
+  for (uint32_t i = 0; i < need; ++i) {
+    w->rumors[slot0 + i].type = 0xFF;
+    w->rgen[slot0 + i] = w->gen;
+  }
   w->n_rumors += need;
 
-  /* 1. memberlist-detected transitions (M6) at every live member but the subject */
-  for (uint32_t e = 0; e < n_ml; ++e) {
-    uint32_t subj = ml[e].subject, sm = w->subj_member[subj];
-    if (ml[e].set_alive == 1) {
-      w->alive[sm] = 1;
-      w->serf_state[sm] = ORC_SERF_ALIVE;
-    }
-    for (uint32_t m = 0; m < n; ++m) {
-      if (!w->alive[m] || m == sm) continue;
-      if (ml[e].kind == ORC_ML_JOIN) orc_handle_node_join(w, m, subj);
-      else orc_handle_node_leave(w, m, subj);
-    }
-    if (ml[e].set_alive == 0) w->alive[sm] = 0;
+  /* 1. memberlist transitions */
+  if (n_ml) {
+    for (int i = 0; i < nt; ++i) jobs[i].phase = 1;
+    run_phase(jobs, nt);
   }
 
   /* 2. refutations scheduled by the previous round's merges (spawn_detach) */
@@ -981,64 +1175,52 @@ int orc_world_round(orc_world* w, uint32_t round, const orc_ml_event* ml, uint32
     }
   }
 
-  /* 4. emission: each live sender, k peers, broadcast_messages (delegate.rs:307-374) */
-  uint32_t cap_t = 3 * w->qcap;
-  size_t cap = (size_t)n * k * cap_t;
-  uint32_t* rec_recv = (uint32_t*)malloc(cap * sizeof(uint32_t));
-  uint32_t* rec_rumor = (uint32_t*)malloc(cap * sizeof(uint32_t));
-  if (!rec_recv || !rec_rumor) {
-    free(rec_recv);
-    free(rec_rumor);
-    return -1;
-  }
+  /* 4. emission, sender ranges in parallel; the records stay in sender order */
+  for (int i = 0; i < nt; ++i) jobs[i].phase = 4;
+  run_phase(jobs, nt);
+  int fail = 0;
   size_t nrec = 0;
-  uint32_t peers[64], buf[3 * 64];
-  for (uint32_t m = 0; m < n; ++m) {
-    if (!w->alive[m]) continue;
-    uint32_t np = orc_pick_peers(w->seed, n, w->alive, m, round, k, peers);
-    for (uint32_t j = 0; j < np; ++j) {
-      uint32_t used = 0, got = 0, b;
-      for (uint32_t q = 0; q < 3; ++q) {
-        got += orc_queue_get_broadcasts(w, m, q, w->limit - used, buf + got, cap_t - got, &b);
-        used += b;
-      }
-      for (uint32_t i = 0; i < got; ++i) {
-        rec_recv[nrec] = peers[j];
-        rec_rumor[nrec] = buf[i];
-        nrec++;
-      }
-      w->sends += got;
-    }
+  for (int i = 0; i < nt; ++i) {
+    fail |= jobs[i].fail;
+    nrec += jobs[i].nrec;
+    w->sends += jobs[i].sends;
   }
 
   /* 5. merge in canonical (sender, position) order per receiver: stable
    *    counting sort by receiver keeps the sender-major emission order. */
   uint32_t* off = (uint32_t*)calloc((size_t)n + 1, sizeof(uint32_t));
   uint32_t* order = (uint32_t*)malloc((nrec ? nrec : 1) * sizeof(uint32_t));
-  if (!off || !order) {
-    free(rec_recv);
-    free(rec_rumor);
-    free(off);
-    free(order);
-    return -1;
-  }
-  for (size_t i = 0; i < nrec; ++i) off[rec_recv[i] + 1]++;
-  for (uint32_t r = 0; r < n; ++r) off[r + 1] += off[r];
-  {
-    uint32_t* cur = (uint32_t*)malloc(((size_t)n + 1) * sizeof(uint32_t));
+  uint32_t* cur = (uint32_t*)malloc(((size_t)n + 1) * sizeof(uint32_t));
+  if (!fail && off && order && cur) {
+    for (int t = 0; t < nt; ++t)
+      for (size_t i = 0; i < jobs[t].nrec; ++i) off[jobs[t].rec_recv[i] + 1]++;
+    for (uint32_t r = 0; r < n; ++r) off[r + 1] += off[r];
     memcpy(cur, off, ((size_t)n + 1) * sizeof(uint32_t));
-    for (size_t i = 0; i < nrec; ++i) order[cur[rec_recv[i]]++] = rec_rumor[i];
-    free(cur);
+    for (int t = 0; t < nt; ++t)
+      for (size_t i = 0; i < jobs[t].nrec; ++i) order[cur[jobs[t].rec_recv[i]]++] = jobs[t].rec_rumor[i];
+    for (int i = 0; i < nt; ++i) {
+      jobs[i].phase = 5;
+      jobs[i].off = off;
+      jobs[i].order = order;
+    }
+    run_phase(jobs, nt);
+    for (int i = 0; i < nt; ++i) w->merges += jobs[i].merges;
+  } else {
+    fail = 1;
   }
-  for (uint32_t r = 0; r < n; ++r) {
-    if (!w->alive[r]) continue;
-    for (uint32_t i = off[r]; i < off[r + 1]; ++i) merge_one(w, r, order[i]);
+  for (int i = 0; i < nt; ++i) {
+    free(jobs[i].rec_recv);
+    free(jobs[i].rec_rumor);
   }
   free(off);
   free(order);
-  free(rec_recv);
-  free(rec_rumor);
-  return 0;
+  free(cur);
+  return fail ? -1 : 0;
+}
+
+int orc_world_round(orc_world* w, uint32_t round, const orc_ml_event* ml, uint32_t n_ml,
+                    const orc_action* acts, uint32_t n_acts) {
+  return orc_world_round_mt(w, round, ml, n_ml, acts, n_acts, 1);
 }
 
 /* ------------------------------------------------------------------------ */

@@ -177,7 +177,7 @@ enum {
   ORC_F_MEMBER_EVENT = 16 /* a MemberEvent was emitted */
 };
 /* world error bits */
-enum { ORC_E_EVSLOT_FULL = 1, ORC_E_QSLOT_FULL = 2, ORC_E_REFUTE_FULL = 4 };
+enum { ORC_E_EVSLOT_FULL = 1, ORC_E_QSLOT_FULL = 2, ORC_E_REFUTE_FULL = 4, ORC_E_QUEUE_PRUNE = 16 };
 
 typedef struct {
   uint8_t type;     /* ORC_MSG_* */
@@ -228,6 +228,12 @@ typedef struct {
    * (base.rs:1355, 1364, 1813, 1822), in the caller's time unit (rounds) */
   uint32_t* v_time;
   uint32_t now; /* the current time stamped by the handlers (orc_world_round sets it to the round) */
+  uint32_t* q_pruned; /* [n] live items dropped by a full queue (cumulative) */
+  /* rumor table = a ring of cap_rumors (a power of two) slots; a rumor id is
+   * generation << rbits | slot.  n_rumors is the ring cursor (next free slot). */
+  uint32_t* q_expired; /* [n] queue items dropped at emission because their rumor slot was recycled */
+  uint32_t* rgen;      /* [cap_rumors] generation of the rumor held in each slot */
+  uint32_t gen, rbits;
 } orc_world;
 
 typedef struct {
@@ -250,10 +256,21 @@ int orc_handle_user_event(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key
 int orc_handle_query(orc_world* w, uint32_t m, uint64_t ltime, uint32_t id, int no_broadcast);
 int orc_upsert_intent(orc_world* w, uint32_t m, uint32_t subj, uint8_t kind, uint64_t ltime);
 
+/* rumor ring: generations per cycle, liveness of an id, expiry of a member's queue */
+uint32_t orc_rumor_generations(const orc_world* w);
+int orc_rumor_live(const orc_world* w, uint32_t rid);
+uint32_t orc_queue_expire(orc_world* w, uint32_t m, uint32_t q);
+
 /* transmit-limited queue model */
 void orc_queue_insert(orc_world* w, uint32_t m, uint32_t q, uint32_t rumor);
 uint32_t orc_queue_get_broadcasts(orc_world* w, uint32_t m, uint32_t q, uint32_t limit,
                                   uint32_t* out, uint32_t max_out, uint32_t* bytes_used);
+/* QueueChecker tick (core/src/serf/base.rs:703-760) over every member's queues: max =
+ * max_queue_depth, or max(2n, min_queue_depth) when min_queue_depth > 0; a queue with
+ * >= max items is pruned to max (the last items in send order).  stats[9] (optional):
+ * per queue queued items, members at/above depth_warning, items pruned. */
+void orc_check_queues(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
+                      uint64_t* stats);
 
 uint32_t orc_msg_len(uint8_t type, uint64_t ltime, uint32_t name_len, uint32_t payload_len);
 uint64_t orc_digest_mix(uint64_t d, uint64_t x);
@@ -291,6 +308,10 @@ typedef struct {
  *   receivers in canonical (sender, position) order. */
 int orc_world_round(orc_world* w, uint32_t round, const orc_ml_event* ml, uint32_t n_ml,
                     const orc_action* acts, uint32_t n_acts);
+/* the same round with its member loops (memberlist transitions, emission, merge)
+ * partitioned over nthreads pthreads: identical results (the CPU baseline's all-core rate) */
+int orc_world_round_mt(orc_world* w, uint32_t round, const orc_ml_event* ml, uint32_t n_ml,
+                       const orc_action* acts, uint32_t n_acts, int nthreads);
 uint32_t orc_pick_peers(uint64_t seed, uint32_t n, const uint8_t* alive, uint32_t m, uint32_t round,
                         uint32_t k, uint32_t* out);
 

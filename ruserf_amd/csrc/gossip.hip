@@ -178,14 +178,16 @@ __device__ __forceinline__ uint64_t below_mask(uint32_t lane) { return lane ? (~
 // insert: position = number of smaller live keys; lanes at/after it shift by
 // one, so on a full queue the last lane (the largest key) falls off = memberlist
 // Prune; a new item that would land past the end is itself the pruned one.
-__device__ __forceinline__ void q_insert_wave(const GCfg& c, QRegs& Q, uint32_t lane, uint32_t rid, uint32_t len,
-                                              uint32_t seq) {
+// Returns 1 when the queue was full (a live item, possibly the new one, was dropped).
+__device__ __forceinline__ uint32_t q_insert_wave(const GCfg& c, QRegs& Q, uint32_t lane, uint32_t rid, uint32_t len,
+                                                  uint32_t seq) {
   const bool valid = lane < c.qcap;
   const bool live = valid && Q.r != kEmpty;
   const uint64_t newkey = tlq_key(0, len, seq);
   const uint64_t k = live ? tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq) : ~0ull;
+  const uint32_t full = (uint32_t)__popcll(__ballot(live)) == c.qcap ? 1u : 0u;
   const uint32_t pos = (uint32_t)__popcll(__ballot(live && k < newkey));
-  if (pos >= c.qcap) return;
+  if (pos >= c.qcap) return full;
   const int src = lane ? (int)lane - 1 : 0;
   const uint32_t pr = (uint32_t)__shfl((int)Q.r, src), ps = (uint32_t)__shfl((int)Q.sq, src),
                  pt = (uint32_t)__shfl((int)Q.tl, src);
@@ -199,6 +201,7 @@ __device__ __forceinline__ void q_insert_wave(const GCfg& c, QRegs& Q, uint32_t 
     Q.sq = seq;
     Q.tl = len << 16;
   }
+  return full;
 }
 
 // Batched insert of new items (transmits 0) into a sorted queue, equivalent to
@@ -210,8 +213,9 @@ __device__ __forceinline__ void q_insert_wave(const GCfg& c, QRegs& Q, uint32_t 
 //   new item j lands at #(existing keys below it) + #(new keys below it).
 // One pass over the new items counts both, then every slot PULLS its item
 // (ds_bpermute): slots taken by new items are marked in a 64-bit mask, the
-// others take the existing items in order.
-__device__ __forceinline__ void q_insert_batch(const GCfg& c, QRegs& Q, uint32_t lane, bool ins, uint32_t rid,
+// others take the existing items in order.  Returns the number of live items
+// that did not fit (memberlist Prune of the queue's tail).
+__device__ __forceinline__ uint32_t q_insert_batch(const GCfg& c, QRegs& Q, uint32_t lane, bool ins, uint32_t rid,
                                                uint32_t len, uint32_t seq0, uint64_t newmask) {
   const bool valid = lane < c.qcap;
   const bool live = valid && Q.r != kEmpty;
@@ -257,6 +261,34 @@ __device__ __forceinline__ void q_insert_batch(const GCfg& c, QRegs& Q, uint32_t
     Q.sq = is_new ? ns : (is_old ? os : 0u);
     Q.tl = is_new ? (nl << 16) : (is_old ? ot : 0u);
   }
+  const uint32_t total = n_live + (uint32_t)__popcll(newmask);
+  return total > c.qcap ? total - c.qcap : 0u;
+}
+
+// Items whose rumor slot was recycled (the slot's generation is no longer the id's)
+// expire: they are dropped and the survivors keep their sorted order at the front.
+// Returns the number dropped (wave-uniform).
+__device__ __forceinline__ uint32_t q_expire(const GCfg& c, QRegs& Q, uint32_t lane, bool stale, bool permute_dec) {
+  const bool valid = lane < c.qcap;
+  const bool live = valid && Q.r != kEmpty;
+  const uint64_t sm = __ballot(live && stale);
+  if (!sm) return 0;
+  const bool keep = live && !stale;
+  const uint64_t km = __ballot(keep), vm = __ballot(valid);
+  const uint64_t below = below_mask(lane);
+  const uint32_t pos = keep ? (uint32_t)__popcll(km & below)
+                            : (valid ? (uint32_t)__popcll(km) + (uint32_t)__popcll(vm & ~km & below) : lane);
+  if (valid && !keep) {
+    Q.r = kEmpty;
+    Q.sq = 0;
+    Q.tl = 0;
+  }
+  const int addr = (int)(pos * 4);
+  Q.r = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.r);
+  Q.sq = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.sq);
+  Q.tl = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.tl);
+  if (permute_dec) Q.dec = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.dec);
+  return (uint32_t)__popcll(sm);
 }
 
 // one get_broadcasts call on a sorted register-resident queue; returns bytes used.
@@ -386,7 +418,7 @@ __global__ void ml_alive_kernel(GState s, const rsf_ml_event* __restrict__ ml, u
   }
 }
 
-__device__ __forceinline__ void put_rumor(const GState& s, uint32_t rid, uint8_t type, uint8_t flags, uint32_t subj,
+__device__ __forceinline__ void put_rumor(const GCfg& c, const GState& s, uint32_t rid, uint8_t type, uint8_t flags, uint32_t subj,
                                           uint64_t L, uint64_t key, uint32_t len) {
   rsf_rumor ru;
   ru.ltime = L;
@@ -395,7 +427,7 @@ __device__ __forceinline__ void put_rumor(const GState& s, uint32_t rid, uint8_t
   ru.type = type;
   ru.flags = flags;
   ru.msg_len = (uint16_t)len;
-  s.rumors[rid] = ru;
+  s.rumors[rid & c.rmask] = ru;
 }
 
 __device__ __forceinline__ void push_refute(const GCfg& c, const GState& s, MRegs& r, uint64_t ltime) {
@@ -416,8 +448,8 @@ __device__ __forceinline__ void broadcast_join(const GCfg& c, const GState& s, u
   witness(r.clock, L);
   h_join_intent(s.view + l * c.S + subj, r, L, c.now);
   uint32_t len = msg_len(RSF_MSG_JOIN, L, 0, 0);
-  put_rumor(s, rid, RSF_MSG_JOIN, 0, subj, L, 0, len);
-  queue_insert_serial(c, s, l, kQIntent, rid, len);
+  put_rumor(c, s, rid, RSF_MSG_JOIN, 0, subj, L, 0, len);
+  queue_insert_serial(c, s, l, kQIntent, rid, len, r);
 }
 
 __global__ void __launch_bounds__(256) refute_kernel(GCfg c, GState s, uint32_t base) {
@@ -461,8 +493,8 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
       uint32_t subj = (uint32_t)r.subj;
       h_leave_intent(s.view + l * c.S + subj, r, subj, lt, false, ref, c.now);
       uint32_t len = msg_len(RSF_MSG_LEAVE, lt, 0, 0);
-      put_rumor(s, rid, RSF_MSG_LEAVE, 0, subj, lt, 0, len);
-      queue_insert_serial(c, s, l, kQIntent, rid, len);
+      put_rumor(c, s, rid, RSF_MSG_LEAVE, 0, subj, lt, 0, len);
+      queue_insert_serial(c, s, l, kQIntent, rid, len, r);
       break;
     }
     case RSF_ACT_FORCE_LEAVE: {
@@ -471,8 +503,8 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
       int f = h_leave_intent(s.view + l * c.S + x.subject, r, x.subject, lt, prune, ref, c.now);
       if (f & RSF_F_REFUTE) push_refute(c, s, r, ref);
       uint32_t len = msg_len(RSF_MSG_LEAVE, lt, 0, 0);
-      put_rumor(s, rid, RSF_MSG_LEAVE, prune ? 1 : 0, x.subject, lt, 0, len);
-      queue_insert_serial(c, s, l, kQIntent, rid, len);
+      put_rumor(c, s, rid, RSF_MSG_LEAVE, prune ? 1 : 0, x.subject, lt, 0, len);
+      queue_insert_serial(c, s, l, kQIntent, rid, len, r);
       break;
     }
     case RSF_ACT_USER_EVENT: {
@@ -480,8 +512,8 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
       r.eclock++;
       h_user_event(c, s, l, r, lt, x.key);
       uint32_t len = msg_len(RSF_MSG_USER_EVENT, lt, x.name_len, x.payload_len);
-      put_rumor(s, rid, RSF_MSG_USER_EVENT, 0, 0, lt, x.key, len);
-      queue_insert_serial(c, s, l, kQEvent, rid, len);
+      put_rumor(c, s, rid, RSF_MSG_USER_EVENT, 0, 0, lt, x.key, len);
+      queue_insert_serial(c, s, l, kQEvent, rid, len, r);
       break;
     }
     case RSF_ACT_QUERY: {
@@ -489,8 +521,8 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
       bool nb = x.flags & 1;
       h_query(c, s, l, r, lt, (uint32_t)x.key, nb);
       uint32_t len = msg_len(RSF_MSG_QUERY, lt, x.name_len, x.payload_len);
-      put_rumor(s, rid, RSF_MSG_QUERY, nb ? 1 : 0, 0, lt, (uint32_t)x.key, len);
-      queue_insert_serial(c, s, l, kQQuery, rid, len);
+      put_rumor(c, s, rid, RSF_MSG_QUERY, nb ? 1 : 0, 0, lt, (uint32_t)x.key, len);
+      queue_insert_serial(c, s, l, kQQuery, rid, len, r);
       break;
     }
     default: break;
@@ -598,12 +630,23 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   const bool ne0 = shfl_u32(Q0.r, 0) != kEmpty, ne1 = shfl_u32(e.head, 1) != kEmpty,
              ne2 = shfl_u32(e.head, 2) != kEmpty;
   if (np == 0 || !(ne0 || ne1 || ne2)) return;
-  // decoration of the intents: their subject slots (subject and type share one 8-B word)
-  if (Q0.r != kEmpty) Q0.dec = s.rdec[Q0.r];
+  // decoration of the intents (their subject slots) and each item's rumor generation
+  uint32_t g0 = 0, g1 = 0, g2 = 0;
+  if (Q0.r != kEmpty) {
+    Q0.dec = s.rdec[Q0.r & c.rmask];
+    g0 = s.rgen[Q0.r & c.rmask];
+  }
   if (ne1) q_load(c, s, l, 1, lane, Q1);
   if (ne2) q_load(c, s, l, 2, lane, Q2);
+  if (Q1.r != kEmpty) g1 = s.rgen[Q1.r & c.rmask];
+  if (Q2.r != kEmpty) g2 = s.rgen[Q2.r & c.rmask];
   uint32_t err = 0;
-  bool d0 = false, d1 = false, d2 = false;
+  // items of recycled rumor slots expire before the first get_broadcasts
+  const uint32_t x0 = q_expire(c, Q0, lane, g0 != (Q0.r >> c.rbits), true);
+  const uint32_t x1 = q_expire(c, Q1, lane, g1 != (Q1.r >> c.rbits), false);
+  const uint32_t x2 = q_expire(c, Q2, lane, g2 != (Q2.r >> c.rbits), false);
+  bool d0 = x0 != 0, d1 = x1 != 0, d2 = x2 != 0;
+  if ((x0 | x1 | x2) && lane == 0) s.q_expired[l] += x0 + x1 + x2;
   for (uint32_t j = 0; j < np; ++j) {
     const uint32_t gslot = shfl_u32(e.gs, j);
     const uint64_t out_base = (uint64_t)gslot * c.cap_t;
@@ -661,10 +704,12 @@ __device__ __forceinline__ uint32_t decorate(const rsf_rumor* __restrict__ rumor
 // The same pass keeps the rumor bodies without their 8-B key (only user events and
 // queries need it) as aligned 16-B records for the merge kernel's gather.
 __global__ void __launch_bounds__(256) dec_fill_kernel(const rsf_rumor* __restrict__ rumors, uint32_t* __restrict__ rdec,
-                                                       uint4* __restrict__ rbody, uint64_t base, uint64_t n) {
+                                                       uint4* __restrict__ rbody, uint32_t* __restrict__ rgen,
+                                                       uint32_t gen, uint64_t base, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   rdec[base + i] = decorate(rumors, (uint32_t)(base + i));
+  rgen[base + i] = gen;  // ids of the slot's previous generation expire
   const uint2* w = reinterpret_cast<const uint2*>(rumors + base + i);  // ltime | key | subject..msg_len
   const uint2 lt = w[0], tail = w[2];
   rbody[base + i] = make_uint4(lt.x, lt.y, tail.x, tail.y);
@@ -686,14 +731,14 @@ __global__ void __launch_bounds__(256) segment_kernel(const uint32_t* __restrict
                                                       uint32_t* __restrict__ seg_start, uint32_t* __restrict__ seg_end,
                                                       const uint32_t* __restrict__ vals,
                                                       const uint32_t* __restrict__ rdec,
-                                                      uint32_t* __restrict__ dec) {
+                                                      uint32_t* __restrict__ dec, uint32_t rmask) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t k = keys[i];
   if (k == kSentinel) return;
   if (i == 0 || keys[i - 1] != k) seg_start[k - lo] = (uint32_t)i;
   if (i + 1 == n || keys[i + 1] != k) seg_end[k - lo] = (uint32_t)(i + 1);
-  if (dec) dec[i] = rdec[vals[i]];
+  if (dec) dec[i] = rdec[vals[i] & rmask];
 }
 
 // ---- multi-GPU send side: the records of the receiver-sorted groups (cap_t slots each,
@@ -838,6 +883,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
   QRegs Q0{kEmpty, 0, 0};
   q_load(c, s, l, 0, lane, Q0);  // intents are the common case
   bool ld1 = false, ld2 = false, d0 = false, d1 = false, d2 = false;
+  uint32_t qdrop = 0;  // live queue items dropped by full queues (wave-uniform)
   uint32_t nseq0 = shfl_u32(su, kSuSeq0), nseq1 = shfl_u32(su, kSuSeq1), nseq2 = shfl_u32(su, kSuSeq2);
   MRegs r;
   r.clock = su64(su, kSuClock);
@@ -889,8 +935,8 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     }
     rsf_rumor ru{};
     if (valid) {  // the key only for user events / queries (the decoration says which)
-      const uint4 b = s.rbody[rid];
-      const uint64_t key = (dsub == kDecQuery || dsub == kDecEvent) ? s.rumors[rid].key : 0ull;
+      const uint4 b = s.rbody[rid & c.rmask];
+      const uint64_t key = (dsub == kDecQuery || dsub == kDecEvent) ? s.rumors[rid & c.rmask].key : 0ull;
       ru = rumor_from_body(b, key);
     }
     ViewE pre{};
@@ -982,12 +1028,13 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     const bool ins = is_view && (f & RSF_F_REBROADCAST);
     const uint64_t newmask = __ballot(ins);
     if (newmask) {
-      q_insert_batch(c, Q0, lane, ins, rid, ru.msg_len, nseq0, newmask);
+      qdrop += q_insert_batch(c, Q0, lane, ins, rid, ru.msg_len, nseq0, newmask);
       nseq0 += (uint32_t)__popcll(newmask);
       d0 = true;
     }
     // serial part, record order: events/queries (lane 0 handlers), digest, refutes
-    const uint64_t serial = __ballot(valid && (!is_view || (f & (RSF_F_MEMBER_EVENT | RSF_F_REFUTE))));
+    const uint64_t serial =
+        __ballot(valid && (!is_view || (f & (RSF_F_MEMBER_EVENT | RSF_F_REFUTE | RSF_F_PRUNE))));
 #else
     // serial part, record order: events/queries (lane 0 handlers), digest, refutes, re-queues
     const uint64_t serial = __ballot(valid && (!is_view || f != 0));
@@ -1002,6 +1049,8 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
       if (type == RSF_MSG_JOIN || type == RSF_MSG_LEAVE) {
         fi = (int)shfl_u32((uint32_t)f, i);
         if (fi & RSF_F_MEMBER_EVENT) r.digest = digest_mix(r.digest, shfl_u64(contrib, i));
+        if (fi & RSF_F_PRUNE)  // handle_prune's Reap event, after the Leave event of a Failed member
+          r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)kEvReap << 32) | shfl_u32(ru.subject, i));
         if (fi & RSF_F_REFUTE) {
           const uint64_t rf = shfl_u64(ref, i);
           if (lane == 0) push_refute(c, s, r, rf);
@@ -1025,17 +1074,17 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
         const uint32_t q = queue_of(type), rid_i = shfl_u32(rid, i), mlen = tf >> 16;
         if (q == kQIntent) {
           if (!RSF_MERGE_BATCH) {
-            q_insert_wave(c, Q0, lane, rid_i, mlen, nseq0++);
+            qdrop += q_insert_wave(c, Q0, lane, rid_i, mlen, nseq0++);
             d0 = true;
           }
         } else if (q == kQQuery) {
           QRegs t = qlds_get(ql[0], lane);
-          q_insert_wave(c, t, lane, rid_i, mlen, nseq1++);
+          qdrop += q_insert_wave(c, t, lane, rid_i, mlen, nseq1++);
           qlds_put(ql[0], lane, t);
           d1 = true;
         } else {
           QRegs t = qlds_get(ql[1], lane);
-          q_insert_wave(c, t, lane, rid_i, mlen, nseq2++);
+          qdrop += q_insert_wave(c, t, lane, rid_i, mlen, nseq2++);
           qlds_put(ql[1], lane, t);
           d2 = true;
         }
@@ -1049,8 +1098,10 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
   if (d0) q_store(c, s, l, 0, lane, Q0, true);
   if (d1) q_store(c, s, l, 1, lane, qlds_get(ql[0], lane), true);
   if (d2) q_store(c, s, l, 2, lane, qlds_get(ql[1], lane), true);
+  if (qdrop) r.err |= kErrQueue;
   if (lane == 0) {
     store_regs(s, l, r);
+    if (qdrop) s.q_pruned[l] += qdrop;
     if (d0) s.q_next_seq[l * 3 + 0] = nseq0;
     if (d1) s.q_next_seq[l * 3 + 1] = nseq1;
     if (d2) s.q_next_seq[l * 3 + 2] = nseq2;
@@ -1281,7 +1332,6 @@ __global__ void __launch_bounds__(256) pp_merge_kernel(GCfg c, GState s, const r
 // and digests the failed reaps in slot order; pass 2 (only where a left member
 // is due) erases left members past tombstone_timeout and digests them, so every
 // failed Reap event precedes every left one, as reap_failed precedes reap_left.
-constexpr uint32_t kEvReap = 3;
 __global__ void __launch_bounds__(256) reap_kernel(GCfg c, GState s, uint32_t now, uint32_t rc_to, uint32_t ts_to,
                                                    uint32_t in_to) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -1460,7 +1510,7 @@ __global__ void __launch_bounds__(256) runs_scatter_kernel(const uint64_t* __res
                                                            const uint32_t* __restrict__ seg_start,
                                                            uint32_t* __restrict__ vals,
                                                            const uint32_t* __restrict__ rdec,
-                                                           uint32_t* __restrict__ dec) {
+                                                           uint32_t* __restrict__ dec, uint32_t rmask) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t r = run_of(off, n_runs, i);
@@ -1470,7 +1520,7 @@ __global__ void __launch_bounds__(256) runs_scatter_kernel(const uint64_t* __res
   const uint64_t idx = r * n_loc + l;
   const uint32_t pos = seg_start[l] + rbase[idx] + (uint32_t)(i - rstart[idx]);
   vals[pos] = (uint32_t)x;
-  dec[pos] = rdec[(uint32_t)x];
+  dec[pos] = rdec[(uint32_t)x & rmask];
 }
 
 __global__ void __launch_bounds__(256) seg_end_kernel(uint64_t n_loc, const uint32_t* __restrict__ seg_start,
@@ -1478,6 +1528,31 @@ __global__ void __launch_bounds__(256) seg_end_kernel(uint64_t n_loc, const uint
                                                       uint32_t* __restrict__ seg_end) {
   const uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (l < n_loc) seg_end[l] = seg_start[l] + total[l];
+}
+
+// QueueChecker tick (base.rs:703-760): one thread per (member, queue).  A sorted queue's
+// live items are its leading slots, so num_queued is the first free slot; prune(max)
+// drops the items past `max`, the last ones in send order (memberlist
+// TransmitLimitedQueue::prune).  stats[q] = queued, stats[3 + q] = members at or above
+// the warning depth, stats[6 + q] = pruned.
+__global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uint32_t max_depth, uint32_t warn,
+                                                           unsigned long long* __restrict__ stats) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= c.n_loc * 3) return;
+  const uint32_t q = (uint32_t)(t % 3);
+  const uint64_t base = t * c.qcap;
+  uint32_t n = 0;
+  while (n < c.qcap && s.q_rumor[base + n] != kEmpty) n++;
+  if (n) atomicAdd(stats + q, (unsigned long long)n);
+  if (n >= warn) atomicAdd(stats + 3 + q, 1ull);
+  if (n > max_depth) {  // numq >= max -> prune(max): retain max
+    for (uint32_t i = max_depth; i < n; ++i) {
+      s.q_rumor[base + i] = kEmpty;
+      s.q_seq[base + i] = 0;
+      s.q_txlen[base + i] = 0;
+    }
+    atomicAdd(stats + 6 + q, (unsigned long long)(n - max_depth));
+  }
 }
 
 __global__ void accumulate_kernel(unsigned long long* counters) {
@@ -1498,8 +1573,10 @@ struct rsf_gossip {
   hipStream_t own = nullptr, stream = nullptr;
   GCfg c{};
   GState s{};
-  uint32_t n_rumors = 0, max_rumors = 0;
-  uint32_t round_base = 0, round_abase = 0, round_need = 0;
+  // rumor ring: cursor (next free slot) and generation; the round's block is slots
+  // [round_slot, round_slot + round_need), its ids round_base + i (gen << rbits | slot)
+  uint32_t n_rumors = 0, max_rumors = 0, gen = 0;
+  uint32_t round_slot = 0, round_base = 0, round_abase = 0, round_need = 0;
   // per-round device lists
   rsf_ml_event* d_ml = nullptr;
   rsf_action* d_acts = nullptr;
@@ -1594,7 +1671,8 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   if (cfg->fanout == 0 || cfg->fanout > 8 || cfg->fanout >= N) return gerr("fanout must be 1..8 and < n_members");
   if (cfg->gossip_limit > 0xFFFFFF || cfg->gossip_overhead > 0xFFFF) return gerr("gossip budget too large");
   if (cfg->max_refute == 0 || cfg->max_refute > 4) return gerr("max_refute must be 1..4");
-  if (cfg->max_rumors == 0) return gerr("max_rumors must be > 0");
+  if (cfg->max_rumors == 0 || (cfg->max_rumors & (cfg->max_rumors - 1)) || cfg->max_rumors > (1u << 31))
+    return gerr("max_rumors must be a power of two <= 2^31 (the rumor ring)");
   RSF_HIP(hipSetDevice(device));
   rsf_gossip* g = new (std::nothrow) rsf_gossip();
   if (!g) return rsf::set_error(RSF_ERR_NOMEM, "host allocation failed");
@@ -1628,6 +1706,9 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   c.k0 = (uint32_t)cfg->seed;
   c.k1 = (uint32_t)(cfg->seed >> 32);
   g->max_rumors = cfg->max_rumors;
+  c.rbits = 0;
+  while ((1u << c.rbits) < cfg->max_rumors) c.rbits++;
+  c.rmask = cfg->max_rumors - 1;
   g->end_bit = bits_for(N);
   auto fail = [&](int code) {
     rsf_gossip_destroy(g);
@@ -1644,11 +1725,11 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
       GA(s.digest, n * 8) || GA(s.err, n * 4) || GA(s.alive, N) || GA(s.serf_state, n) || GA(s.member_subj, n * 4) ||
       GA(s.subj_member, S * 4) || GA(s.refute_cnt, S * 4) || GA(s.refute_ltime, S * c.max_refute * 8) ||
       GA(s.view, n * S * sizeof(ViewE)) || GA(s.q_rumor, n * 3 * c.qcap * 4) || GA(s.q_seq, n * 3 * c.qcap * 4) ||
-      GA(s.q_txlen, n * 3 * c.qcap * 4) || GA(s.q_next_seq, n * 3 * 4) || GA(s.eb_ltime, n * c.ebuf * 8) ||
+      GA(s.q_txlen, n * 3 * c.qcap * 4) || GA(s.q_next_seq, n * 3 * 4) || GA(s.q_pruned, n * 4) || GA(s.q_expired, n * 4) || GA(s.eb_ltime, n * c.ebuf * 8) ||
       GA(s.eb_cnt, n * c.ebuf * 4) || GA(s.eb_keys, n * c.ebuf * c.slot_k * 8) || GA(s.qb_ltime, n * c.qbuf * 8) ||
       GA(s.qb_cnt, n * c.qbuf * 4) || GA(s.qb_ids, n * c.qbuf * c.slot_k * 4) ||
       GA(s.rumors, (size_t)cfg->max_rumors * sizeof(rsf_rumor)) || GA(s.rdec, (size_t)cfg->max_rumors * 4) ||
-      GA(s.rbody, (size_t)cfg->max_rumors * 16))
+      GA(s.rbody, (size_t)cfg->max_rumors * 16) || GA(s.rgen, (size_t)cfg->max_rumors * 4))
     return fail(rc);
   g->stage_cap = n * c.fanout * c.cap_t;
   if (g->stage_cap >= 0xFFFFFFFFull) return fail(gerr("n_members x fanout x per-target records must fit 32 bits"));
@@ -1703,6 +1784,9 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   ms(s.q_seq, 0, n * 3 * c.qcap * 4);
   ms(s.q_txlen, 0, n * 3 * c.qcap * 4);
   ms(s.q_next_seq, 0, n * 3 * 4);
+  ms(s.q_pruned, 0, n * 4);
+  ms(s.q_expired, 0, n * 4);
+  ms(s.rgen, 0, (size_t)cfg->max_rumors * 4);
   ms(s.eb_ltime, 0, n * c.ebuf * 8);
   ms(s.eb_cnt, 0, n * c.ebuf * 4);
   ms(s.eb_keys, 0, n * c.ebuf * c.slot_k * 8);
@@ -1730,7 +1814,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
   GState& s = g->s;
   void* ptrs[] = {s.clock,  s.eclock,      s.qclock,       s.emin,        s.qmin,     s.digest,     s.err,
                   s.alive,  s.serf_state,  s.member_subj,  s.subj_member, s.refute_cnt, s.refute_ltime, s.view,
-                  s.q_rumor, s.q_seq,      s.q_txlen,      s.q_next_seq,  s.eb_ltime, s.eb_cnt,     s.eb_keys,
+                  s.q_rumor, s.q_seq,      s.q_txlen,      s.q_next_seq,  s.q_pruned, s.q_expired, s.rgen,  s.eb_ltime, s.eb_cnt,     s.eb_keys,
                   s.qb_ltime, s.qb_cnt,    s.qb_ids,       s.rumors,      s.rdec,       s.rbody,      g->d_ml,    g->d_acts,    g->stage_key,
                   g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters, g->rec_dec, g->pp_buf,
                   g->sort_tmp, g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
@@ -1888,7 +1972,8 @@ int rsf_gossip_apply_batch(rsf_gossip* g, const rsf_msg* msgs, uint64_t n, int32
   RSF_HIP(hipMemsetAsync(g->seg_start, 0, c.n_loc * 4, g->stream));
   RSF_HIP(hipMemsetAsync(g->seg_end, 0, c.n_loc * 4, g->stream));
   hipLaunchKernelGGL(segment_kernel, dim3(grid1(n)), dim3(256), 0, g->stream, (const uint32_t*)d[2], n, 0ull,
-                     g->seg_start, g->seg_end, (const uint32_t*)nullptr, (const uint32_t*)nullptr, (uint32_t*)nullptr);
+                     g->seg_start, g->seg_end, (const uint32_t*)nullptr, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                     0u);
   hipLaunchKernelGGL(apply_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, g->stream, c, g->s, (const rsf_msg*)d[0],
                      (const uint32_t*)d[4], g->seg_start, g->seg_end, (int32_t*)d[5], (uint64_t*)d[6]);
   RSF_HIP(hipGetLastError());
@@ -1920,7 +2005,7 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
     if (std::adjacent_find(ms.begin(), ms.end()) != ms.end()) return gerr("actions of one round must name distinct members");
   }
   uint64_t need = (uint64_t)c.S * c.max_refute + n_acts;
-  if ((uint64_t)g->n_rumors + need > g->max_rumors) return rsf::set_error(RSF_ERR_OVERFLOW, "rumor table full");
+  if (need > g->max_rumors) return rsf::set_error(RSF_ERR_OVERFLOW, "one round's rumors exceed the rumor ring");
   RSF_HIP(hipSetDevice(g->device));
   int rc = ensure_lists(g, n_ml, n_acts);
   if (rc) return rc;
@@ -1928,11 +2013,17 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
   mark(g, 0);
   g->cur_round = round;
   g->c.now = round;  // handlers stamp leave / intent times with the round
-  g->round_base = g->n_rumors;
+  if ((uint64_t)g->n_rumors + need > g->max_rumors) {  // the block restarts the ring, next generation
+    g->n_rumors = 0;
+    const uint32_t gens = c.rbits >= 32 ? 1u : (uint32_t)((1ull << (32 - c.rbits)) - 1);
+    g->gen = (g->gen + 1) % gens;
+  }
+  g->round_slot = g->n_rumors;
+  g->round_base = (uint32_t)(((uint64_t)g->gen << c.rbits) | g->round_slot);
   g->round_abase = g->round_base + c.S * c.max_refute;
   g->round_need = (uint32_t)need;
   g->n_rumors += (uint32_t)need;
-  RSF_HIP(hipMemsetAsync(g->s.rumors + g->round_base, 0, need * sizeof(rsf_rumor), st));
+  RSF_HIP(hipMemsetAsync(g->s.rumors + g->round_slot, 0, need * sizeof(rsf_rumor), st));
   if (n_ml) {
     RSF_HIP(hipMemcpyAsync(g->d_ml, ml, n_ml * sizeof(rsf_ml_event), hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(ml_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, c, g->s, g->d_ml, n_ml);
@@ -1951,7 +2042,7 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
 
 int rsf_gossip_rumor_block(rsf_gossip* g, void** p, uint64_t* bytes) {
   if (!g || !p || !bytes) return gerr("null argument");
-  *p = g->s.rumors + g->round_base;
+  *p = g->s.rumors + g->round_slot;
   *bytes = (uint64_t)g->round_need * sizeof(rsf_rumor);
   return RSF_OK;
 }
@@ -1971,7 +2062,7 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local) {
   const uint64_t ng = g->n_groups;
   if (g->round_need)
     hipLaunchKernelGGL(dec_fill_kernel, dim3(grid1(g->round_need)), dim3(256), 0, st, (const rsf_rumor*)g->s.rumors,
-                       g->s.rdec, g->s.rbody, (uint64_t)g->round_base, (uint64_t)g->round_need);
+                       g->s.rdec, g->s.rbody, g->s.rgen, g->gen, (uint64_t)g->round_slot, (uint64_t)g->round_need);
   hipLaunchKernelGGL(peers_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, c, g->s, round, g->grp_key);
   RSF_HIP(hipGetLastError());
   int rc = sort_pairs(g, g->grp_key, g->grp_key_s, g->grp_id, g->grp_id_s, ng);
@@ -2026,7 +2117,7 @@ static int segment_and_merge(rsf_gossip* g, const uint32_t* keys, const uint32_t
   RSF_HIP(hipMemsetAsync(g->seg_end, 0, c.n_loc * 4, st));
   if (n) {
     hipLaunchKernelGGL(segment_kernel, dim3(grid1(n)), dim3(256), 0, st, keys, n, c.lo, g->seg_start, g->seg_end,
-                       vals, (const uint32_t*)g->s.rdec, g->rec_dec);
+                       vals, (const uint32_t*)g->s.rdec, g->rec_dec, c.rmask);
   }
   return launch_merge(g, vals);
 }
@@ -2153,7 +2244,7 @@ int rsf_gossip_round_merge_runs(rsf_gossip* g, const uint64_t* recv, const uint6
   if (n)
     hipLaunchKernelGGL(runs_scatter_kernel, dim3(grid1(n)), dim3(256), 0, st, recv, n, g->d_run_off, n_runs, c.lo,
                        c.n_loc, g->run_start, g->run_base, g->seg_start, g->sort_val, (const uint32_t*)g->s.rdec,
-                       g->rec_dec);
+                       g->rec_dec, c.rmask);
   hipLaunchKernelGGL(seg_end_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, c.n_loc, g->seg_start, g->run_total,
                      g->seg_end);
   RSF_HIP(hipGetLastError());
@@ -2242,6 +2333,39 @@ int rsf_gossip_reap(rsf_gossip* g, uint32_t now, uint32_t reconnect_timeout, uin
 int rsf_gossip_set_now(rsf_gossip* g, uint32_t now) {
   if (!g) return gerr("null context");
   g->c.now = now;
+  return RSF_OK;
+}
+
+int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
+                            uint64_t* num_queued, uint64_t* n_warn, uint64_t* n_pruned) {
+  if (!g) return gerr("null context");
+  const GCfg& c = g->c;
+  // get_queue_max (base.rs:748-759): members.states.len() is every member the node knows
+  uint64_t mx = max_queue_depth;
+  if (min_queue_depth > 0) mx = std::max<uint64_t>(2 * c.N, min_queue_depth);
+  const uint32_t max_depth = (uint32_t)std::min<uint64_t>(mx, 0xFFFFFFFFull);
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, g->stream));
+  hipLaunchKernelGGL(check_queues_kernel, dim3(grid1(c.n_loc * 3)), dim3(256), 0, g->stream, c, g->s, max_depth,
+                     depth_warning, g->d_counters + 40);
+  RSF_HIP(hipGetLastError());
+  unsigned long long st[9];
+  RSF_HIP(hipMemcpyAsync(st, g->d_counters + 40, sizeof(st), hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  for (int q = 0; q < 3; ++q) {
+    if (num_queued) num_queued[q] = st[q];
+    if (n_warn) n_warn[q] = st[3 + q];
+    if (n_pruned) n_pruned[q] = st[6 + q];
+  }
+  return RSF_OK;
+}
+
+int rsf_gossip_dump_pruned(rsf_gossip* g, uint32_t* pruned, uint32_t* expired) {
+  if (!g) return gerr("null context");
+  RSF_HIP(hipSetDevice(g->device));
+  if (pruned) RSF_HIP(hipMemcpyAsync(pruned, g->s.q_pruned, g->c.n_loc * 4, hipMemcpyDeviceToHost, g->stream));
+  if (expired) RSF_HIP(hipMemcpyAsync(expired, g->s.q_expired, g->c.n_loc * 4, hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
   return RSF_OK;
 }
 

@@ -15,9 +15,15 @@ constexpr uint32_t kMinMsgLen = 18;  // smallest encoded message of the length m
 constexpr uint64_t kDigUser = 0x1000000000000000ull;
 constexpr uint64_t kDigQuery = 0x2000000000000000ull;
 constexpr uint64_t kDigMember = 0x3000000000000000ull;
-enum : uint32_t { kEvJoin = 0, kEvLeave = 1, kEvFailed = 2 };
+enum : uint32_t { kEvJoin = 0, kEvLeave = 1, kEvFailed = 2, kEvReap = 3 };
 enum : uint32_t { kQIntent = 0, kQQuery = 1, kQEvent = 2 };
-enum : uint32_t { kErrEvSlot = 1, kErrQSlot = 2, kErrRefute = 4, kErrStage = 8 };
+enum : uint32_t {
+  kErrEvSlot = RSF_E_EVSLOT,
+  kErrQSlot = RSF_E_QSLOT,
+  kErrRefute = RSF_E_REFUTE,
+  kErrStage = RSF_E_STAGE,
+  kErrQueue = RSF_E_QUEUE_PRUNE
+};
 enum : uint8_t { kSerfAlive = 0, kSerfLeaving = 1, kSerfLeft = 2, kSerfShutdown = 3 };
 
 struct GCfg {
@@ -25,6 +31,8 @@ struct GCfg {
   uint32_t S, qcap, ebuf, qbuf, slot_k, fanout, limit, overhead, tx_limit, max_refute, cap_t;
   uint32_t k0, k1;
   uint32_t now;  // time stamped into view entries (leave_time / intent wall time); = the round
+  // rumor ring: max_rumors = 2^rbits slots; a rumor id is generation << rbits | slot
+  uint32_t rbits, rmask;
 };
 
 // view entry: members.states[subject] (status, status_time) or recent_intents[subject]
@@ -45,6 +53,8 @@ struct GState {
   uint64_t* refute_ltime; // [S][max_refute]
   ViewE* view;            // [n_loc][S]
   uint32_t *q_rumor, *q_seq, *q_txlen, *q_next_seq;  // [n_loc][3][qcap], next_seq [n_loc][3]
+  uint32_t* q_pruned;     // [n_loc] live queue items dropped by a full queue (memberlist Prune), cumulative
+  uint32_t* q_expired;    // [n_loc] queue items dropped at emission: their rumor slot was recycled
   uint64_t* eb_ltime;
   uint32_t* eb_cnt;
   uint64_t* eb_keys;
@@ -54,6 +64,7 @@ struct GState {
   rsf_rumor* rumors;
   uint32_t* rdec;  // per rumor id: its record decoration (subject / kDecQuery / kDecEvent), 4 B
   uint4* rbody;    // per rumor id: the rumor without its key (ltime, subject, type, flags, msg_len), 16 B
+  uint32_t* rgen;  // per rumor slot: the generation of the rumor it holds (ids of older generations expired)
 };
 
 // per-member scalar state held in registers while a kernel works on it
@@ -198,6 +209,14 @@ __device__ __forceinline__ int hv_leave_intent(ViewE& v, MRegs& r, uint32_t subj
     default: f = 0; break;
   }
   v.meta = vmeta(st, RSF_KIND_KNOWN);
+  if (f & RSF_F_PRUNE) {
+    // handle_prune (base.rs:1587-1612): erase_node! removes the member's state (and it
+    // leaves the left list), then a Reap MemberEvent.  The reference sleeps
+    // broadcast_timeout + leave_propagate_delay first when the member is Leaving; the
+    // round model erases at once.
+    v = ViewE{0ull, vmeta(RSF_STATUS_NONE, RSF_KIND_UNKNOWN), 0u};
+    r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)kEvReap << 32) | subj);
+  }
   return f;
 }
 __device__ __forceinline__ int h_leave_intent(ViewE* e, MRegs& r, uint32_t subj, uint64_t L, bool prune,
@@ -317,8 +336,9 @@ __device__ __forceinline__ uint32_t queue_of(uint8_t type) {
 // first, ascending (transmits, ~len, ~seq); then free slots): shift the tail by
 // one; on a full queue the largest item falls off (memberlist Prune), and a new
 // item that would land past the end is itself the pruned one.
+// A full queue loses one live item: counted in q_pruned[l] and flagged (kErrQueue).
 __device__ __forceinline__ void queue_insert_serial(const GCfg& c, const GState& s, uint64_t l, uint32_t q,
-                                                    uint32_t rid, uint32_t len) {
+                                                    uint32_t rid, uint32_t len, MRegs& r) {
   const uint64_t base = (l * 3 + q) * c.qcap;
   const uint32_t seq = s.q_next_seq[l * 3 + q]++;
   const uint64_t newkey = tlq_key(0, len, seq);
@@ -327,6 +347,10 @@ __device__ __forceinline__ void queue_insert_serial(const GCfg& c, const GState&
     const uint32_t tl = s.q_txlen[base + cnt];
     if (pos == kEmpty && tlq_key(tl & 0xFFFF, tl >> 16, s.q_seq[base + cnt]) > newkey) pos = cnt;
     cnt++;
+  }
+  if (cnt == c.qcap) {
+    s.q_pruned[l] += 1;
+    r.err |= kErrQueue;
   }
   if (pos == kEmpty) pos = cnt;
   if (pos >= c.qcap) return;

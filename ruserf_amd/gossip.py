@@ -33,6 +33,10 @@ KIND_UNKNOWN, KIND_INTENT_JOIN, KIND_INTENT_LEAVE, KIND_KNOWN = 0, 1, 2, 3
 STATUS_NONE, STATUS_ALIVE, STATUS_LEAVING, STATUS_LEFT, STATUS_FAILED = 0, 1, 2, 3, 4
 MSG_LEAVE, MSG_JOIN, MSG_USER_EVENT, MSG_QUERY = 0, 1, 3, 4
 F_REBROADCAST, F_REFUTE, F_PRUNE, F_DELIVER, F_MEMBER_EVENT = 1, 2, 4, 8, 16
+# per-member error bits (members()["err"])
+E_EVSLOT, E_QSLOT, E_REFUTE, E_STAGE, E_QUEUE_PRUNE = 1, 2, 4, 8, 16
+# QueueOptions defaults (core/src/options.rs:494-530)
+MAX_QUEUE_DEPTH, MIN_QUEUE_DEPTH, QUEUE_DEPTH_WARNING = 4096, 0, 128
 ACT_JOIN_SELF, ACT_LEAVE_SELF, ACT_FORCE_LEAVE, ACT_USER_EVENT, ACT_QUERY = 1, 2, 3, 4, 5
 ML_JOIN, ML_LEAVE = 1, 2
 PP_JOIN, PP_EVENT_JOIN_IGNORE = 1, 2
@@ -63,7 +67,7 @@ class GossipConfig:
     gossip_overhead: int = 2
     retransmit_mult: int = 4       # memberlist LAN default
     max_refute: int = 4
-    max_rumors: int = 1 << 20
+    max_rumors: int = 1 << 20      # rumor ring (a power of two); ids recycle after a full cycle
     seed: int = 0x5EED5EED
 
     def to_c(self):
@@ -226,6 +230,27 @@ class GossipEngine:
 
     def set_now(self, now):
         check(lib().rsf_gossip_set_now(self._h, now))
+
+    def pruned(self):
+        """Per member: live queue items its bounded queues dropped when full (cumulative)."""
+        out = np.zeros(self.n_loc, dtype=np.uint32)
+        check(lib().rsf_gossip_dump_pruned(self._h, ptr(out, C.c_uint32), None))
+        return out
+
+    def expired(self):
+        """Per member: queue items dropped at emission because their rumor slot was recycled."""
+        out = np.zeros(self.n_loc, dtype=np.uint32)
+        check(lib().rsf_gossip_dump_pruned(self._h, None, ptr(out, C.c_uint32)))
+        return out
+
+    def check_queues(self, max_queue_depth=MAX_QUEUE_DEPTH, min_queue_depth=MIN_QUEUE_DEPTH,
+                     depth_warning=QUEUE_DEPTH_WARNING):
+        """One QueueChecker tick (base.rs:703-760) over the intent / query / event queues:
+        returns {queued, warn, pruned}, 3 counts each."""
+        q, w, p = (np.zeros(3, dtype=np.uint64) for _ in range(3))
+        check(lib().rsf_gossip_check_queues(self._h, max_queue_depth, min_queue_depth, depth_warning,
+                                            ptr(q, C.c_uint64), ptr(w, C.c_uint64), ptr(p, C.c_uint64)))
+        return {"queued": q, "warn": w, "pruned": p}
 
     def queues(self):
         n = self.n_loc * 3 * self.cfg.queue_cap

@@ -34,12 +34,13 @@ def _sample(rng, pool, k):
     return pool[np.sort(idx)]
 
 
-def intents_workload(n, s, rounds, rate=0.01, seed=0x5EED5EED):
+def intents_workload(n, s, rounds, rate=0.01, seed=0x5EED5EED, prune_frac=0.1):
     """Per round: round(rate*n) distinct members originate one intent.  A
     subject member broadcasts its own join (Serf::join -> broadcast_join) or
     leave (Serf::leave); any other member issues force_leave (remove_failed_node,
-    base.rs:474-500) about a random subject.  Returns (subj_member, [acts per round],
-    [ml per round])."""
+    base.rs:474-500) about a random subject, a fraction `prune_frac` of them with
+    prune (remove_failed_node_prune, api.rs:565 -> handle_prune).  Returns
+    (subj_member, [acts per round], [ml per round])."""
     rng = np.random.Generator(np.random.Philox(seed))
     subj_member = subjects_for(n, s)
     member_subj = np.full(n, -1, dtype=np.int64)
@@ -54,22 +55,25 @@ def intents_workload(n, s, rounds, rate=0.01, seed=0x5EED5EED):
         coin = rng.integers(0, 2, size=k)
         a["act"] = np.where(is_subj, np.where(coin == 0, ACT_JOIN_SELF, ACT_LEAVE_SELF), ACT_FORCE_LEAVE)
         a["subject"] = np.where(is_subj, 0, rng.integers(0, s, size=k))
+        a["flags"] = np.where(is_subj, 0, (rng.random(size=k) < prune_frac).astype(np.uint32))
         acts_all.append(a)
         ml_all.append(np.zeros(0, dtype=ML_DTYPE))
     return subj_member, acts_all, ml_all
 
 
 def churn_workload(n, rounds, churn=0.01, events_per_round=100, queries_per_round=10, names=16,
-                   seed=0x5EED5EED):
+                   seed=0x5EED5EED, prune_frac=0.25):
     """configs[3]: S = churn*n subjects; each fails (memberlist NotifyLeave ->
-    Failed, then a force_leave two rounds later) or leaves gracefully (Serf::leave,
-    then NotifyLeave three rounds later) at a random round; plus per round a
-    user-event flood (16 names, 32-byte payloads, cc 50%) and queries."""
+    Failed, then a force_leave two rounds later, a fraction `prune_frac` of them
+    with prune) or leaves gracefully (Serf::leave, then NotifyLeave three rounds
+    later) at a random round; plus per round a user-event flood (16 names, 32-byte
+    payloads, cc 50%) and queries."""
     rng = np.random.Generator(np.random.Philox(seed))
     s = max(1, int(round(n * churn)))
     subj_member = subjects_for(n, s)
     when = rng.integers(1, max(2, rounds - 4), size=s)
     graceful = rng.integers(0, 2, size=s).astype(bool)
+    pruned = rng.random(size=s) < prune_frac
     dead = np.zeros(n, dtype=bool)
     payload_id = 1
     acts_all, ml_all = [], []
@@ -96,7 +100,7 @@ def churn_workload(n, rounds, churn=0.01, events_per_round=100, queries_per_roun
         for m, act, subj in fixed:
             rows.append((m, act, subj, 0, 0, 0, 0))
         for m, subj in zip(fl, forced):
-            rows.append((m, ACT_FORCE_LEAVE, subj, 0, 0, 0, 0))
+            rows.append((m, ACT_FORCE_LEAVE, subj, 0, 0, int(pruned[subj]), 0))
         for m in ev:
             name = int(rng.integers(0, names))
             rows.append((m, ACT_USER_EVENT, 0, 8, 32, int(rng.integers(0, 2)), (name << 32) | payload_id))

@@ -1,5 +1,5 @@
 #!/bin/bash
-# full GPU test suite + smoke, one process each, fault-aware
+# GPU test suite only (optionally a subset: scripts/gpu_tests.sh tests/test_x.py ...)
 S=scripts/gpu_step.sh
-bash $S pytest_gpu 700 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread && \
-bash $S smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+T=${@:-tests}
+bash $S pytest_gpu 900 python -u -m pytest $T -m gpu -v --timeout 300 --timeout-method thread

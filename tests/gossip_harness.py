@@ -28,12 +28,12 @@ def oracle_world(cfg, subj_member, views):
     return w
 
 
-def oracle_round(w, t, ml, acts):
+def oracle_round(w, t, ml, acts, threads=1):
     ml = np.ascontiguousarray(ml, dtype=np.dtype([("subject", "<u4"), ("kind", "<u4"), ("set_alive", "<u4"),
                                                   ("_r", "<u4")]))
     acts = np.ascontiguousarray(acts)
-    rc = L.orc_world_round(C.byref(w), t, ml.ctypes.data_as(C.POINTER(O.MlEvent)), len(ml),
-                           acts.ctypes.data_as(C.POINTER(O.Action)), len(acts))
+    rc = L.orc_world_round_mt(C.byref(w), t, ml.ctypes.data_as(C.POINTER(O.MlEvent)), len(ml),
+                              acts.ctypes.data_as(C.POINTER(O.Action)), len(acts), threads)
     assert rc == 0
 
 
@@ -63,6 +63,8 @@ def world_state(w, lo=0, hi=None):
         "qb_ltime": O.arr(w.qb_ltime, n * w.qbuf, np.uint64).reshape(n, -1)[sl],
         "qb_cnt": O.arr(w.qb_cnt, n * w.qbuf, np.uint32).reshape(n, -1)[sl],
         "qb_ids": O.arr(w.qb_ids, n * w.qbuf * w.slot_k, np.uint32).reshape(n, -1)[sl],
+        "q_pruned": O.arr(w.q_pruned, n, np.uint32)[sl],
+        "q_expired": O.arr(w.q_expired, n, np.uint32)[sl],
     }
     return st
 
@@ -82,6 +84,8 @@ def engine_state(g):
         "q_len": ln.reshape(n, -1), "q_next_seq": ns.reshape(n, 3),
         "eb_ltime": ebl.reshape(n, -1), "eb_cnt": ebc.reshape(n, -1), "eb_keys": ebk.reshape(n, -1),
         "qb_ltime": qbl.reshape(n, -1), "qb_cnt": qbc.reshape(n, -1), "qb_ids": qbi.reshape(n, -1),
+        "q_pruned": g.pruned(),
+        "q_expired": g.expired(),
     }
 
 
@@ -123,6 +127,7 @@ def assert_same(a, b, ctx=""):
 
 
 def oracle_rumors(w):
+    """the rumor ring's slots up to the cursor"""
     return [(w.rumors[i].type, w.rumors[i].ltime, w.rumors[i].subject, w.rumors[i].key, w.rumors[i].msg_len)
             for i in range(w.n_rumors)]
 

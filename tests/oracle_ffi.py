@@ -83,7 +83,8 @@ class World(C.Structure):
                 ("qb_ltime", P64), ("qb_cnt", P32), ("qb_ids", P32),
                 ("rumors", C.POINTER(Rumor)), ("n_rumors", C.c_uint32), ("cap_rumors", C.c_uint32),
                 ("merges", C.c_uint64), ("sends", C.c_uint64), ("deliveries", C.c_uint64),
-                ("v_time", P32), ("now", C.c_uint32)]
+                ("v_time", P32), ("now", C.c_uint32), ("q_pruned", P32), ("q_expired", P32), ("rgen", P32),
+                ("gen", C.c_uint32), ("rbits", C.c_uint32)]
 
 
 class WorldCfg(C.Structure):
@@ -193,10 +194,16 @@ def lib():
     L.orc_digest_mix.restype = C.c_uint64
     L.orc_world_round.argtypes = [C.POINTER(World), C.c_uint32, C.POINTER(MlEvent), C.c_uint32,
                                   C.POINTER(Action), C.c_uint32]
+    L.orc_world_round_mt.argtypes = [C.POINTER(World), C.c_uint32, C.POINTER(MlEvent), C.c_uint32,
+                                     C.POINTER(Action), C.c_uint32, C.c_int]
+    L.orc_rumor_live.argtypes = [C.POINTER(World), C.c_uint32]
+    L.orc_rumor_live.restype = C.c_int
     L.orc_pick_peers.argtypes = [C.c_uint64, C.c_uint32, P8, C.c_uint32, C.c_uint32, C.c_uint32, P32]
     L.orc_pick_peers.restype = C.c_uint32
     L.orc_merge_remote_state.argtypes = [C.POINTER(World), C.c_uint32, C.POINTER(PPState), C.c_int, C.c_int]
     L.orc_push_pull.argtypes = [C.POINTER(World), P32, P32, C.c_uint32, C.c_int, C.c_int]
+    L.orc_check_queues.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint32, C.c_uint32, P64]
+    L.orc_check_queues.restype = None
     L.orc_reap.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
     L.orc_varint_len.argtypes = [C.c_uint64]
     L.orc_varint_len.restype = C.c_uint32

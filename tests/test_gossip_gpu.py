@@ -41,7 +41,81 @@ def test_intent_rounds_bit_exact(n, s, rounds, rate, qcap, limit):
         H.oracle_round(w, t, ml[t], acts[t])
         H.assert_same(H.engine_state(g), H.world_state(w), f"round {t}")
     assert w.merges > 0
-    assert int(np.sum(H.engine_state(g)["clock"])) > n  # clocks advanced
+    st = H.engine_state(g)
+    assert int(np.sum(st["clock"])) > n  # clocks advanced
+    # views start KNOWN: entries that are not were erased by a pruned force_leave
+    assert np.any(st["v_kind"] != G.KIND_KNOWN)
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
+def test_rumor_ring_recycles_bit_exact():
+    """A rumor ring far smaller than the run: blocks restart the ring with the next
+    generation, and queue items whose slot was recycled expire at their member's next
+    emission, identically to the oracle (churn + flood: intents, events, queries)."""
+    n, rounds = 1200, 40
+    subj, acts, ml = W.churn_workload(n, rounds, events_per_round=25, queries_per_round=4, seed=77)
+    s = len(subj)
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=24, gossip_limit=300, max_rumors=256,
+                         event_buffer_size=128, query_buffer_size=128, slot_k=8, max_refute=2)
+    g, w = pair(cfg, subj, W.initial_views(s))
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t])
+        H.assert_same(H.engine_state(g), H.world_state(w), f"round {t}")
+    st = H.engine_state(g)
+    assert w.gen >= 3 and st["q_expired"].sum() > 0
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
+def test_long_run_ring_1m():
+    """2,000 rounds at 1M members (configs[1] size) with the default-size ring: no
+    RSF_ERR_OVERFLOW however long the engine runs; clocks keep advancing."""
+    n, s, rounds = 1_000_000, 64, 2000
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=16, max_rumors=1 << 16, event_buffer_size=8,
+                         query_buffer_size=8, slot_k=1, max_refute=1)
+    subj, acts, ml = W.intents_workload(n, s, 50, rate=0.001, seed=3)
+    g = G.GossipEngine(cfg)
+    g.set_subjects(subj)
+    g.init_views(*W.initial_views(s))
+    c0 = None
+    for t in range(rounds):
+        g.round(t, ml[t % 50], acts[t % 50])
+        if t == 10:
+            c0 = g.members()["clock"].copy()
+    m = g.members()
+    assert np.all(m["clock"] >= c0) and m["clock"].max() > c0.max()
+    assert int(g.expired().astype(np.uint64).sum()) >= 0
+    g.close()
+
+
+@pytest.mark.parametrize("prune_frac", [0.0, 0.5, 1.0])
+def test_prune_and_queue_overflow_bit_exact(prune_frac):
+    """force_leave(prune) -> handle_prune (base.rs:1587-1612) erases the member at every
+    receiver that accepts the leave (Reap event), the next intent is buffered; small
+    queues overflow, and every dropped live item is counted (q_pruned) and flagged
+    (RSF_E_QUEUE_PRUNE) identically to the oracle.  Ends with a QueueChecker tick."""
+    n, s, rounds = 1500, 24, 14
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=6, gossip_limit=4 * 24, max_rumors=1 << 16,
+                         event_buffer_size=64, query_buffer_size=64, slot_k=4)
+    subj, acts, ml = W.intents_workload(n, s, rounds, rate=0.03, seed=21, prune_frac=prune_frac)
+    views = W.initial_views(s)
+    g, w = pair(cfg, subj, views)
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t])
+        H.assert_same(H.engine_state(g), H.world_state(w), f"round {t}")
+    st = H.engine_state(g)
+    assert st["q_pruned"].sum() > 0 and np.all((st["err"] & G.E_QUEUE_PRUNE != 0) == (st["q_pruned"] > 0))
+    erased = np.count_nonzero(st["v_kind"] != G.KIND_KNOWN)
+    assert (erased > 0) == (prune_frac > 0)
+    for mx, mn, warn in [(4096, 0, 128), (3, 0, 2), (0, 2, 1)]:
+        got = g.check_queues(mx, mn, warn)
+        exp = (C.c_uint64 * 9)()
+        L.orc_check_queues(C.byref(w), mx, mn, warn, exp)
+        assert list(got["queued"]) + list(got["warn"]) + list(got["pruned"]) == list(exp), (mx, mn, warn)
+        H.assert_same(H.engine_state(g), H.world_state(w), f"checker {mx}")
     g.close()
     L.orc_world_free(C.byref(w))
 
@@ -70,7 +144,8 @@ def test_unknown_subjects_buffer_intents_then_join():
     n, s, rounds = 800, 20, 10
     cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=32, max_rumors=1 << 15,
                          event_buffer_size=32, query_buffer_size=32, slot_k=2)
-    subj, acts, _ = W.intents_workload(n, s, rounds, rate=0.02, seed=99)
+    # no pruned force_leaves here: a prune after the NotifyJoin would erase the member again
+    subj, acts, _ = W.intents_workload(n, s, rounds, rate=0.02, seed=99, prune_frac=0.0)
     views = (np.zeros(s, np.uint8), np.zeros(s, np.uint8), np.zeros(s, np.uint64))
     g, w = pair(cfg, subj, views)
     for t in range(rounds):

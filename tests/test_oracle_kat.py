@@ -306,6 +306,66 @@ def test_leave_transitions_and_refute():
     L.orc_world_free(C.byref(w))
 
 
+def test_leave_intent_prune():
+    """force_leave(prune=true) (api.rs:565 remove_failed_node_prune -> base.rs:474-500)
+    -> handle_node_leave_intent -> handle_prune (base.rs:1472-1526, 1587-1612): the
+    member is erased from members.states (the reference test serf_remove_failed_node_prune,
+    tests/serf/remove.rs:96-164, waits for the survivors to count 2 nodes, i.e. the
+    failed member gone), a Reap MemberEvent follows (after the Leave event of a Failed
+    member), the message is still rebroadcast; the next intent about the member is
+    buffered by upsert_intent as for any unknown member."""
+    reap = lambda d, subj: L.orc_digest_mix(d, 0x3000000000000000 | (3 << 32) | subj)  # noqa: E731
+    leave = lambda d, subj: L.orc_digest_mix(d, 0x3000000000000000 | (1 << 32) | subj)  # noqa: E731
+    for st, flags, events in [
+        (O.ST_FAILED, O.F_REBROADCAST | O.F_MEMBER_EVENT | O.F_PRUNE, [leave, reap]),
+        (O.ST_ALIVE, O.F_REBROADCAST | O.F_PRUNE, [reap]),
+        (O.ST_LEAVING, O.F_REBROADCAST | O.F_PRUNE, [reap]),
+        (O.ST_LEFT, O.F_REBROADCAST | O.F_PRUNE, [reap]),
+        (O.ST_NONE, 0, []),
+    ]:
+        w = make_world(n=3, s=1)
+        set_known(w, 0, 0, st, 5)
+        f = L.orc_handle_leave_intent(C.byref(w), 0, 0, 9, 1, None)
+        assert f == flags
+        d = 0
+        for ev in events:
+            d = ev(d, 0)
+        assert w.digest[0] == d
+        if flags & O.F_PRUNE:
+            assert (w.v_kind[0], w.v_status[0], w.v_ltime[0]) == (O.K_UNKNOWN, O.ST_NONE, 0)
+            # erased: an older leave intent is now buffered, as for a member never seen
+            f2 = L.orc_handle_leave_intent(C.byref(w), 0, 0, 7, 0, None)
+            assert f2 == O.F_REBROADCAST and intent(w, 0, 0) == ("leave", 7)
+        else:
+            assert w.v_kind[0] == O.K_KNOWN and w.v_ltime[0] == 9
+        # a stale prune (ltime <= status_time) changes nothing
+        w2 = make_world(n=3, s=1)
+        set_known(w2, 0, 0, st, 5)
+        assert L.orc_handle_leave_intent(C.byref(w2), 0, 0, 5, 1, None) == 0
+        assert w2.v_kind[0] == O.K_KNOWN and w2.digest[0] == 0
+        L.orc_world_free(C.byref(w))
+        L.orc_world_free(C.byref(w2))
+
+
+def test_queue_prune_counted_and_checker():
+    """The bounded queue model drops the last item in send order when full, and
+    counts it (RSF_E_QUEUE_PRUNE); QueueChecker (base.rs:703-760) prunes to max."""
+    w = make_world(n=2, s=1, qcap=4)
+    for i in range(6):
+        w.rumors[i].type = 1
+        w.rumors[i].msg_len = 20
+        L.orc_queue_insert(C.byref(w), 0, 0, i)
+    assert w.q_pruned[0] == 2 and w.err[0] & 16
+    live = sorted(w.q_rumor[i] for i in range(4))
+    assert live == [2, 3, 4, 5]  # same transmits and length: the oldest (smallest seq) go first
+    st = (C.c_uint64 * 9)()
+    L.orc_check_queues(C.byref(w), 4096, 0, 3, st)
+    assert list(st) == [4, 0, 0, 1, 0, 0, 0, 0, 0]
+    L.orc_check_queues(C.byref(w), 1, 0, 128, st)  # max 1 -> three dropped, the newest kept
+    assert list(st)[6] == 3 and [w.q_rumor[i] for i in range(4) if w.q_rumor[i] != 0xFFFFFFFF] == [5]
+    L.orc_world_free(C.byref(w))
+
+
 def test_delegate_merge_remote_state(kats):
     """merge_remote_state (delegate.rs:422-554) through orc_merge_remote_state: the
     reference test's PushPullMessage becomes a sender local_state (status_ltimes ->
