@@ -245,7 +245,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["gossip", "vivaldi", "pushpull"], default=None)
+    ap.add_argument("--workload", choices=["gossip", "vivaldi", "pushpull", "churn"], default=None)
     ap.add_argument("--members", type=int, default=None, help="members per GPU")
     ap.add_argument("--members-total", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -287,6 +287,12 @@ def main():
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline_vivaldi()
+    elif workload == "churn":
+        from bench_churn import cpu_baseline_churn, run_churn
+        res = run_churn(args, rank, world)
+        cpu = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline_churn(args)
     elif workload == "pushpull":
         from bench_pushpull import cpu_baseline_pushpull, run_pushpull
         args.members = args.members or 1_000_000

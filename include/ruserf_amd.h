@@ -213,6 +213,7 @@ int rsf_vivaldi_true_rtt_ns(rsf_vivaldi* v, uint32_t a, uint32_t b, uint64_t* ns
 #define RSF_E_REFUTE 4          /* more than max_refute refutations of a subject in one round */
 #define RSF_E_STAGE 8           /* a (sender, peer) message held more than cap_t records */
 #define RSF_E_QUEUE_PRUNE 16    /* a transmit-limited queue was full: a live item was dropped */
+#define RSF_E_DELIVERY_LOG 32   /* the delivery log of a member was full (deliveries happened, unlogged) */
 
 typedef struct rsf_gossip_cfg {
   uint64_t n_members;          /* N (global) */
@@ -221,7 +222,8 @@ typedef struct rsf_gossip_cfg {
   uint32_t queue_cap;          /* slots per transmit-limited queue, 1..64 */
   uint32_t event_buffer_size;  /* Options::event_buffer_size (default 512) */
   uint32_t query_buffer_size;  /* Options::query_buffer_size (default 512) */
-  uint32_t slot_k;             /* events / query ids kept per dedup slot, 1..16 */
+  uint32_t slot_k;             /* events / query ids kept per dedup slot, 1..64 (the reference's
+                                  slot list is unbounded; overflow sets RSF_E_EVSLOT / RSF_E_QSLOT) */
   uint32_t fanout;             /* gossip targets per round (memberlist gossip_nodes), 1..8 */
   uint32_t gossip_limit;       /* byte budget per gossip message (memberlist UDP budget) */
   uint32_t gossip_overhead;    /* per-message compound overhead */
@@ -272,7 +274,7 @@ typedef struct rsf_msg {
   uint64_t ltime;
   uint64_t key;
   uint8_t type;      /* RSF_MSG_* */
-  uint8_t flags;     /* leave: prune; query: no_broadcast */
+  uint8_t flags;     /* leave: prune; query: no_broadcast; user event: cc (coalesce) */
   uint16_t _r0;
   uint32_t _r1;
 } rsf_msg;
@@ -380,6 +382,25 @@ int rsf_gossip_push_pull_device(rsf_gossip* g, const rsf_pp_pair* pairs_dev, uin
 int rsf_gossip_reap(rsf_gossip* g, uint32_t now, uint32_t reconnect_timeout, uint32_t tombstone_timeout,
                     uint32_t recent_intent_timeout);
 int rsf_gossip_set_now(rsf_gossip* g, uint32_t now);
+
+/* ---- delivery log: the UserEvents handle_user_event sends to the application
+ * (event_tx, core/src/serf/base.rs:831-835) -- what a consumer, e.g. the
+ * coalesce_loop (core/src/coalesce.rs:66-155), reads.  Each member logs up to
+ * per_member deliveries (in delivery order) since the last round_begin: its own
+ * originations (Serf::user_event handles the event locally first), then the
+ * round's merges; rsf_gossip_apply_batch and push/pull replays append to the
+ * current log.  Overflow sets RSF_E_DELIVERY_LOG.  per_member = 0 turns it off. */
+typedef struct rsf_delivery {
+  uint64_t ltime;
+  uint64_t key;      /* (name_id << 32) | payload_id, as rsf_action.key */
+  uint32_t member;
+  uint8_t cc;        /* UserEventMessage::cc: the coalescer's handle() (coalesce/user.rs:30-34) */
+  uint8_t _r[3];
+} rsf_delivery;
+int rsf_gossip_set_delivery_log(rsf_gossip* g, uint32_t per_member);
+/* The log, member by member (ascending id), each member's deliveries in order, into
+ * out (host, capacity `cap` entries); *n_out = entries written.  Synchronises. */
+int rsf_gossip_dump_deliveries(rsf_gossip* g, rsf_delivery* out, uint64_t cap, uint64_t* n_out);
 
 /* ---- QueueChecker (core/src/serf/base.rs:703-760) ---------------------------
  * One checker tick over the three queues of every shard member: max =

@@ -611,7 +611,8 @@ void orc_world_free(orc_world* w) {
                   w->serf_state, w->err, w->subj_member, w->member_subj, w->refute_cnt,
                   w->refute_ltime, w->v_ltime, w->v_status, w->v_kind, w->q_rumor, w->q_seq,
                   w->q_tx, w->q_len, w->q_next_seq, w->eb_ltime, w->eb_cnt, w->eb_keys,
-                  w->qb_ltime, w->qb_cnt, w->qb_ids, w->rumors, w->v_time, w->q_pruned, w->q_expired, w->rgen};
+                  w->qb_ltime, w->qb_cnt, w->qb_ids, w->rumors, w->v_time, w->q_pruned, w->q_expired, w->rgen,
+                  w->dlog, w->dcnt};
   for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) free(ptrs[i]);
   memset(w, 0, sizeof(*w));
 }
@@ -729,8 +730,41 @@ int orc_handle_node_leave(orc_world* w, uint32_t m, uint32_t subj) {
   return ORC_F_MEMBER_EVENT;
 }
 
-/* handle_user_event  base.rs:770-837 */
+int orc_world_set_delivery_log(orc_world* w, uint32_t per_member) {
+  free(w->dlog);
+  free(w->dcnt);
+  w->dlog = NULL;
+  w->dcnt = NULL;
+  w->dcap = 0;
+  if (!per_member) return 0;
+  w->dlog = (uint64_t*)calloc((size_t)w->n * per_member * 3, sizeof(uint64_t));
+  w->dcnt = (uint32_t*)calloc(w->n, sizeof(uint32_t));
+  if (!w->dlog || !w->dcnt) return -1;
+  w->dcap = per_member;
+  return 0;
+}
+
+/* event_tx.send(UserEvent) (base.rs:831-835) into the member's delivery log */
+static void dlog_put(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key, int cc) {
+  if (!w->dcap) return;
+  uint32_t k = w->dcnt[m];
+  if (k < w->dcap) {
+    uint64_t* e = w->dlog + ((size_t)m * w->dcap + k) * 3;
+    e[0] = ltime;
+    e[1] = key;
+    e[2] = cc ? 1 : 0;
+  } else {
+    w->err[m] |= ORC_E_DLOG;
+  }
+  w->dcnt[m] = k + 1;
+}
+
 int orc_handle_user_event(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key) {
+  return orc_handle_user_event_cc(w, m, ltime, key, 0);
+}
+
+/* handle_user_event  base.rs:770-837 */
+int orc_handle_user_event_cc(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key, int cc) {
   orc_clock_witness(&w->eclock[m], ltime);
   if (ltime < w->emin[m]) return 0;
   uint64_t B = w->ebuf, cur = w->eclock[m];
@@ -748,6 +782,7 @@ int orc_handle_user_event(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key
     w->eb_cnt[slot] = 1;
   }
   w->digest[m] = orc_digest_mix(orc_digest_mix(w->digest[m], DIG_USER ^ key), ltime);
+  dlog_put(w, m, ltime, key, cc);
   return ORC_F_REBROADCAST | ORC_F_DELIVER;
 }
 
@@ -956,7 +991,7 @@ static void merge_one(orc_world* w, uint32_t r, uint32_t rid) {
     case ORC_MSG_LEAVE:
       f = orc_handle_leave_intent(w, r, ru->subject, ru->ltime, ru->flags & 1, &refute);
       break;
-    case ORC_MSG_USER_EVENT: f = orc_handle_user_event(w, r, ru->ltime, ru->key); break;
+    case ORC_MSG_USER_EVENT: f = orc_handle_user_event_cc(w, r, ru->ltime, ru->key, ru->flags & 1); break;
     case ORC_MSG_QUERY: f = orc_handle_query(w, r, ru->ltime, (uint32_t)ru->key, ru->flags & 1); break;
     default: return;
   }
@@ -1110,6 +1145,7 @@ int orc_world_round_mt(orc_world* w, uint32_t round, const orc_ml_event* ml, uin
     w->rgen[slot0 + i] = w->gen;
   }
   w->n_rumors += need;
+  if (w->dcap) memset(w->dcnt, 0, (size_t)n * sizeof(uint32_t)); /* the round's delivery log */
 
   /* 1. memberlist transitions */
   if (n_ml) {
@@ -1158,8 +1194,8 @@ int orc_world_round_mt(orc_world* w, uint32_t round, const orc_ml_event* ml, uin
       case ORC_ACT_USER_EVENT: { /* Serf::user_event  api.rs:247-315 */
         uint64_t lt = w->eclock[m];
         orc_clock_increment(&w->eclock[m]);
-        orc_handle_user_event(w, m, lt, x->key);
-        new_rumor(w, rid, ORC_MSG_USER_EVENT, 0, 0, lt, x->key, x->name_len, x->payload_len);
+        orc_handle_user_event_cc(w, m, lt, x->key, x->flags & 1);
+        new_rumor(w, rid, ORC_MSG_USER_EVENT, (uint8_t)(x->flags & 1), 0, lt, x->key, x->name_len, x->payload_len);
         orc_queue_insert(w, m, ORC_Q_EVENT, rid);
         break;
       }

@@ -177,7 +177,7 @@ enum {
   ORC_F_MEMBER_EVENT = 16 /* a MemberEvent was emitted */
 };
 /* world error bits */
-enum { ORC_E_EVSLOT_FULL = 1, ORC_E_QSLOT_FULL = 2, ORC_E_REFUTE_FULL = 4, ORC_E_QUEUE_PRUNE = 16 };
+enum { ORC_E_EVSLOT_FULL = 1, ORC_E_QSLOT_FULL = 2, ORC_E_REFUTE_FULL = 4, ORC_E_QUEUE_PRUNE = 16, ORC_E_DLOG = 32 };
 
 typedef struct {
   uint8_t type;     /* ORC_MSG_* */
@@ -234,6 +234,11 @@ typedef struct {
   uint32_t* q_expired; /* [n] queue items dropped at emission because their rumor slot was recycled */
   uint32_t* rgen;      /* [cap_rumors] generation of the rumor held in each slot */
   uint32_t gen, rbits;
+  /* delivery log (rsf_gossip_set_delivery_log): per member up to dcap UserEvents sent to
+   * the application since the round began, {ltime, key, cc} */
+  uint64_t* dlog;  /* [n][dcap][3] */
+  uint32_t* dcnt;  /* [n] */
+  uint32_t dcap;
 } orc_world;
 
 typedef struct {
@@ -253,6 +258,9 @@ int orc_handle_leave_intent(orc_world* w, uint32_t m, uint32_t subj, uint64_t lt
 int orc_handle_node_join(orc_world* w, uint32_t m, uint32_t subj);
 int orc_handle_node_leave(orc_world* w, uint32_t m, uint32_t subj);
 int orc_handle_user_event(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key);
+/* the same with the message's cc flag, which only the delivery log records */
+int orc_handle_user_event_cc(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key, int cc);
+int orc_world_set_delivery_log(orc_world* w, uint32_t per_member);
 int orc_handle_query(orc_world* w, uint32_t m, uint64_t ltime, uint32_t id, int no_broadcast);
 int orc_upsert_intent(orc_world* w, uint32_t m, uint32_t subj, uint8_t kind, uint64_t ltime);
 

@@ -57,3 +57,5 @@ def declare(L):
     sig("rsf_gossip_push_pull_device", [VP, VP, C.c_uint64, C.c_uint32])
     sig("rsf_gossip_check_queues", [VP, C.c_uint32, C.c_uint32, C.c_uint32, P64, P64, P64])
     sig("rsf_gossip_dump_pruned", [VP, P32, P32])
+    sig("rsf_gossip_set_delivery_log", [VP, C.c_uint32])
+    sig("rsf_gossip_dump_deliveries", [VP, VP, C.c_uint64, P64])

@@ -510,9 +510,10 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
     case RSF_ACT_USER_EVENT: {
       uint64_t lt = r.eclock;
       r.eclock++;
-      h_user_event(c, s, l, r, lt, x.key);
+      const bool cc = x.flags & 1;
+      h_user_event(c, s, l, r, lt, x.key, cc);
       uint32_t len = msg_len(RSF_MSG_USER_EVENT, lt, x.name_len, x.payload_len);
-      put_rumor(c, s, rid, RSF_MSG_USER_EVENT, 0, 0, lt, x.key, len);
+      put_rumor(c, s, rid, RSF_MSG_USER_EVENT, cc ? 1 : 0, 0, lt, x.key, len);
       queue_insert_serial(c, s, l, kQEvent, rid, len, r);
       break;
     }
@@ -1061,7 +1062,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
         const uint64_t key = shfl_u64(ru.key, i);
         fi = 0;
         if (lane == 0) {
-          if (type == RSF_MSG_USER_EVENT) fi = h_user_event(c, s, l, r, L, key);
+          if (type == RSF_MSG_USER_EVENT) fi = h_user_event(c, s, l, r, L, key, (tf >> 8) & 1);
           else if (type == RSF_MSG_QUERY) fi = h_query(c, s, l, r, L, (uint32_t)key, (tf >> 8) & 1);
         }
         fi = (int)shfl_u32((uint32_t)fi, 0);
@@ -1273,7 +1274,8 @@ __global__ void __launch_bounds__(256) pp_merge_kernel(GCfg c, GState s, const r
     const uint64_t excl = wave_shr1_u64(incl);
     uint64_t cur = excl > ec ? excl : ec;
     if (cnt && L + 1 > cur) cur = L + 1;  // witness(L) of this slot's events
-    uint32_t dmask = 0, e_err = 0;
+    uint64_t dmask = 0;  // delivered keys of this slot (slot_k <= 64)
+    uint32_t e_err = 0;
     if (cnt && !(L < r.emin) && !(cur > B && L < cur - B)) {
       const uint64_t rs = l * c.ebuf + (L % B);
       if ((L % B) != i) {
@@ -1297,7 +1299,7 @@ __global__ void __launch_bounds__(256) pp_merge_kernel(GCfg c, GState s, const r
           } else {
             e_err |= kErrEvSlot;
           }
-          dmask |= 1u << k;
+          dmask |= 1ull << k;
         }
         if (rc != rc0) s.eb_cnt[rs] = rc;
       }
@@ -1309,13 +1311,15 @@ __global__ void __launch_bounds__(256) pp_merge_kernel(GCfg c, GState s, const r
       const int j = __ffsll((long long)mm) - 1;
       mm &= mm - 1;
       r.err |= shfl_u32(e_err, j);
-      uint32_t dm = shfl_u32(dmask, j);
+      uint64_t dm = shfl_u64(dmask, j);
       const uint64_t Lj = shfl_u64(L, j);
       const uint64_t* skj = sl.eb_keys + (p * c.ebuf + base + (uint32_t)j) * c.slot_k;
       while (dm) {
-        const int k = __ffs(dm) - 1;
+        const int k = __ffsll((long long)dm) - 1;
         dm &= dm - 1;
         r.digest = digest_mix(digest_mix(r.digest, kDigUser ^ skj[k]), Lj);
+        if (lane == 0) dlog_put(c, s, l, r, Lj, skj[k], false);
+        r.err = shfl_u32(r.err, 0);
       }
     }
   }
@@ -1388,7 +1392,7 @@ __global__ void __launch_bounds__(256) apply_kernel(GCfg c, GState s, const rsf_
     switch (x.type) {
       case RSF_MSG_JOIN: f = h_join_intent(vrow + x.subject, r, x.ltime, c.now); break;
       case RSF_MSG_LEAVE: f = h_leave_intent(vrow + x.subject, r, x.subject, x.ltime, x.flags & 1, ref, c.now); break;
-      case RSF_MSG_USER_EVENT: f = h_user_event(c, s, l, r, x.ltime, x.key); break;
+      case RSF_MSG_USER_EVENT: f = h_user_event(c, s, l, r, x.ltime, x.key, x.flags & 1); break;
       case RSF_MSG_QUERY: f = h_query(c, s, l, r, x.ltime, (uint32_t)x.key, x.flags & 1); break;
       default: f = 0; break;
     }
@@ -1667,7 +1671,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   if (cfg->n_subjects == 0 || cfg->n_subjects > N) return gerr("n_subjects must be in [1, n_members]");
   if (cfg->queue_cap == 0 || cfg->queue_cap > 64) return gerr("queue_cap must be 1..64");
   if (cfg->event_buffer_size == 0 || cfg->query_buffer_size == 0) return gerr("dedup buffers must be non-empty");
-  if (cfg->slot_k == 0 || cfg->slot_k > 16) return gerr("slot_k must be 1..16");
+  if (cfg->slot_k == 0 || cfg->slot_k > 64) return gerr("slot_k must be 1..64");
   if (cfg->fanout == 0 || cfg->fanout > 8 || cfg->fanout >= N) return gerr("fanout must be 1..8 and < n_members");
   if (cfg->gossip_limit > 0xFFFFFF || cfg->gossip_overhead > 0xFFFF) return gerr("gossip budget too large");
   if (cfg->max_refute == 0 || cfg->max_refute > 4) return gerr("max_refute must be 1..4");
@@ -1819,7 +1823,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters, g->rec_dec, g->pp_buf,
                   g->sort_tmp, g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
                   g->scan_tmp, g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
-                  g->grp_slot, g->grp_off, g->stage_dec, g->grp_scan_tmp};
+                  g->grp_slot, g->grp_off, g->stage_dec, g->grp_scan_tmp, s.dlog, s.dcnt};
   for (void* p : ptrs)
     if (p) hipFree(p);
   g->scratch.release();
@@ -2024,6 +2028,7 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
   g->round_need = (uint32_t)need;
   g->n_rumors += (uint32_t)need;
   RSF_HIP(hipMemsetAsync(g->s.rumors + g->round_slot, 0, need * sizeof(rsf_rumor), st));
+  if (g->c.dcap) RSF_HIP(hipMemsetAsync(g->s.dcnt, 0, c.n_loc * 4, st));  // the round's delivery log
   if (n_ml) {
     RSF_HIP(hipMemcpyAsync(g->d_ml, ml, n_ml * sizeof(rsf_ml_event), hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(ml_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, c, g->s, g->d_ml, n_ml);
@@ -2366,6 +2371,53 @@ int rsf_gossip_dump_pruned(rsf_gossip* g, uint32_t* pruned, uint32_t* expired) {
   if (pruned) RSF_HIP(hipMemcpyAsync(pruned, g->s.q_pruned, g->c.n_loc * 4, hipMemcpyDeviceToHost, g->stream));
   if (expired) RSF_HIP(hipMemcpyAsync(expired, g->s.q_expired, g->c.n_loc * 4, hipMemcpyDeviceToHost, g->stream));
   RSF_HIP(hipStreamSynchronize(g->stream));
+  return RSF_OK;
+}
+
+int rsf_gossip_set_delivery_log(rsf_gossip* g, uint32_t per_member) {
+  if (!g) return gerr("null context");
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  if (g->s.dlog) hipFree(g->s.dlog);
+  if (g->s.dcnt) hipFree(g->s.dcnt);
+  g->s.dlog = nullptr;
+  g->s.dcnt = nullptr;
+  g->c.dcap = 0;
+  if (!per_member) return RSF_OK;
+  int rc;
+  if ((rc = rsf::dmalloc((void**)&g->s.dlog, (size_t)g->c.n_loc * per_member * 16)) ||
+      (rc = rsf::dmalloc((void**)&g->s.dcnt, g->c.n_loc * 4)))
+    return rc;
+  RSF_HIP(hipMemsetAsync(g->s.dcnt, 0, g->c.n_loc * 4, g->stream));
+  g->c.dcap = per_member;
+  return RSF_OK;
+}
+
+int rsf_gossip_dump_deliveries(rsf_gossip* g, rsf_delivery* out, uint64_t cap, uint64_t* n_out) {
+  if (!g || !n_out || (cap && !out)) return gerr("null argument");
+  *n_out = 0;
+  const GCfg& c = g->c;
+  if (!c.dcap) return RSF_OK;
+  std::vector<uint32_t> cnt(c.n_loc);
+  std::vector<uint4> log((size_t)c.n_loc * c.dcap);
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemcpyAsync(cnt.data(), g->s.dcnt, c.n_loc * 4, hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipMemcpyAsync(log.data(), g->s.dlog, log.size() * 16, hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  uint64_t o = 0;
+  for (uint64_t l = 0; l < c.n_loc; ++l)
+    for (uint32_t k = 0; k < std::min(cnt[l], c.dcap); ++k) {
+      if (o >= cap) return rsf::set_error(RSF_ERR_OVERFLOW, "delivery dump capacity exceeded");
+      const uint4 e = log[l * c.dcap + k];
+      const uint64_t lt = ((uint64_t)e.y << 32) | e.x;
+      rsf_delivery& d = out[o++];
+      d.ltime = lt & ~(1ull << 63);
+      d.key = ((uint64_t)e.w << 32) | e.z;
+      d.member = (uint32_t)(c.lo + l);
+      d.cc = (uint8_t)(lt >> 63);
+      d._r[0] = d._r[1] = d._r[2] = 0;
+    }
+  *n_out = o;
   return RSF_OK;
 }
 

@@ -22,7 +22,8 @@ enum : uint32_t {
   kErrQSlot = RSF_E_QSLOT,
   kErrRefute = RSF_E_REFUTE,
   kErrStage = RSF_E_STAGE,
-  kErrQueue = RSF_E_QUEUE_PRUNE
+  kErrQueue = RSF_E_QUEUE_PRUNE,
+  kErrDlog = RSF_E_DELIVERY_LOG
 };
 enum : uint8_t { kSerfAlive = 0, kSerfLeaving = 1, kSerfLeft = 2, kSerfShutdown = 3 };
 
@@ -33,6 +34,7 @@ struct GCfg {
   uint32_t now;  // time stamped into view entries (leave_time / intent wall time); = the round
   // rumor ring: max_rumors = 2^rbits slots; a rumor id is generation << rbits | slot
   uint32_t rbits, rmask;
+  uint32_t dcap;  // delivery log entries per member (0: log off)
 };
 
 // view entry: members.states[subject] (status, status_time) or recent_intents[subject]
@@ -65,6 +67,8 @@ struct GState {
   uint32_t* rdec;  // per rumor id: its record decoration (subject / kDecQuery / kDecEvent), 4 B
   uint4* rbody;    // per rumor id: the rumor without its key (ltime, subject, type, flags, msg_len), 16 B
   uint32_t* rgen;  // per rumor slot: the generation of the rumor it holds (ids of older generations expired)
+  uint4* dlog;     // [n_loc][dcap] user events delivered to the application: ltime | cc << 63, key
+  uint32_t* dcnt;  // [n_loc] deliveries since the log was cleared
 };
 
 // per-member scalar state held in registers while a kernel works on it
@@ -271,9 +275,23 @@ __device__ __forceinline__ int h_node_leave(ViewE* e, MRegs& r, uint32_t subj, u
   return RSF_F_MEMBER_EVENT;
 }
 
-// handle_user_event (base.rs:770-837)
+// one delivery (event_tx.send of a UserEvent, base.rs:831-835) into the member's log slot
+__device__ __forceinline__ void dlog_put(const GCfg& c, const GState& s, uint64_t l, MRegs& r, uint64_t L,
+                                         uint64_t key, bool cc) {
+  if (!c.dcap) return;
+  const uint32_t k = s.dcnt[l];
+  if (k < c.dcap) {
+    const uint64_t lt = L | (cc ? (1ull << 63) : 0ull);
+    s.dlog[l * c.dcap + k] = make_uint4((uint32_t)lt, (uint32_t)(lt >> 32), (uint32_t)key, (uint32_t)(key >> 32));
+  } else {
+    r.err |= kErrDlog;
+  }
+  s.dcnt[l] = k + 1;
+}
+
+// handle_user_event (base.rs:770-837); cc = the message's coalesce flag (delivery log only)
 __device__ __forceinline__ int h_user_event(const GCfg& c, const GState& s, uint64_t l, MRegs& r, uint64_t L,
-                                            uint64_t key) {
+                                            uint64_t key, bool cc) {
   witness(r.eclock, L);
   if (L < r.emin) return 0;
   uint64_t B = c.ebuf, cur = r.eclock;
@@ -296,6 +314,7 @@ __device__ __forceinline__ int h_user_event(const GCfg& c, const GState& s, uint
     s.eb_cnt[slot] = 1;
   }
   r.digest = digest_mix(digest_mix(r.digest, kDigUser ^ key), L);
+  dlog_put(c, s, l, r, L, key, cc);
   return RSF_F_REBROADCAST | RSF_F_DELIVER;
 }
 

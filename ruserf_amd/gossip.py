@@ -49,8 +49,9 @@ MSG_DTYPE = np.dtype([("receiver", "<u4"), ("subject", "<u4"), ("ltime", "<u8"),
 RUMOR_DTYPE = np.dtype([("ltime", "<u8"), ("key", "<u8"), ("subject", "<u4"), ("type", "u1"), ("flags", "u1"),
                         ("msg_len", "<u2")])
 PP_PAIR_DTYPE = np.dtype([("receiver", "<u4"), ("sender", "<u4")])
+DELIVERY_DTYPE = np.dtype([("ltime", "<u8"), ("key", "<u8"), ("member", "<u4"), ("cc", "u1"), ("_r", "u1", 3)])
 assert ACTION_DTYPE.itemsize == 32 and ML_DTYPE.itemsize == 16 and MSG_DTYPE.itemsize == 32
-assert RUMOR_DTYPE.itemsize == 24
+assert RUMOR_DTYPE.itemsize == 24 and DELIVERY_DTYPE.itemsize == 24
 
 
 @dataclass
@@ -230,6 +231,20 @@ class GossipEngine:
 
     def set_now(self, now):
         check(lib().rsf_gossip_set_now(self._h, now))
+
+    # ---- delivery log: UserEvents sent to the application (event_tx, base.rs:831-835)
+    def set_delivery_log(self, per_member):
+        """Log up to per_member deliveries per member per round (0 turns the log off)."""
+        self._dcap = int(per_member)
+        check(lib().rsf_gossip_set_delivery_log(self._h, self._dcap))
+
+    def deliveries(self):
+        """This round's deliveries (DELIVERY_DTYPE), member by member, each in delivery order."""
+        cap = self.n_loc * max(1, getattr(self, "_dcap", 0))
+        out = np.zeros(cap, dtype=DELIVERY_DTYPE)
+        n = C.c_uint64()
+        check(lib().rsf_gossip_dump_deliveries(self._h, _p(out), cap, C.byref(n)))
+        return out[: n.value]
 
     def pruned(self):
         """Per member: live queue items its bounded queues dropped when full (cumulative)."""

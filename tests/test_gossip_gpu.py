@@ -302,3 +302,91 @@ def test_two_shards_equal_one_context(runs):
             assert np.array_equal(got, full[k]), (t, k)
     for e in [one] + shards:
         e.close()
+
+
+def _threads():
+    import os
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", n)), 16))
+
+
+def _oracle_deliveries(w):
+    """the oracle's delivery log as (member, ltime, key, cc) rows, member-major"""
+    n, cap = w.n, w.dcap
+    cnt = np.minimum(O.arr(w.dcnt, n, np.uint32), cap)
+    log = O.arr(w.dlog, n * cap * 3, np.uint64).reshape(n, cap, 3)
+    mask = np.arange(cap)[None, :] < cnt[:, None]
+    mem = np.broadcast_to(np.arange(n, dtype=np.uint32)[:, None], (n, cap))[mask]
+    e = log[mask]
+    return mem, e[:, 0], e[:, 1], e[:, 2].astype(np.uint8)
+
+
+def test_configs3_100k_churn_flood_coalesce():
+    """BASELINE configs[3] at full size: 100k members, 1% churn (1000 subjects fail or
+    leave, a quarter of the failures force-left with prune), a flood of 100 user events
+    (16 names, 32-B payloads, cc 50%) + 10 queries per round, event/query buffers 512,
+    retransmit mult 4.  Bit-exact against the oracle every round (clocks, digests of
+    every delivery, error bits, queue drops, the delivery log); the full state at the
+    end.  Each member's cc deliveries then go through the GPU UserEventCoalescer
+    (coalesce/user.rs:52-97) with one coalescer per member, checked against the
+    oracle's coalescer on a sample of members."""
+    from ruserf_amd.coalesce import USER_EVENT_DTYPE, coalesce_user_events
+    n, rounds = 100_000, 9
+    subj, acts, ml = W.churn_workload(n, rounds, events_per_round=100, queries_per_round=10, seed=2024)
+    s = len(subj)
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=64, gossip_limit=1400, max_rumors=1 << 16,
+                         event_buffer_size=512, query_buffer_size=512, slot_k=16)
+    g, w = pair(cfg, subj, W.initial_views(s))
+    dcap = 256
+    g.set_delivery_log(dcap)
+    assert L.orc_world_set_delivery_log(C.byref(w), dcap) == 0
+    th = _threads()
+    logs = []
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t], threads=th)
+        m = g.members()
+        for k, ok in [("clock", w.clock), ("event_clock", w.eclock), ("query_clock", w.qclock),
+                      ("digest", w.digest), ("err", w.err)]:
+            exp = O.arr(ok, n, np.uint32 if k == "err" else np.uint64)
+            assert np.array_equal(m[k], exp), (t, k)
+        assert np.array_equal(g.pruned(), O.arr(w.q_pruned, n, np.uint32)), t
+        d = g.deliveries()
+        om, ol, ok_, oc = _oracle_deliveries(w)
+        assert np.array_equal(d["member"], om) and np.array_equal(d["ltime"], ol), t
+        assert np.array_equal(d["key"], ok_) and np.array_equal(d["cc"], oc), t
+        logs.append(d)
+    H.assert_same(H.engine_state(g), H.world_state(w), "final")
+    st = H.engine_state(g)
+    assert np.any(st["v_status"] == G.STATUS_LEFT) and np.any(st["v_kind"] == G.KIND_UNKNOWN)
+    # coalescing of the cc deliveries, one coalescer per member (stable by member: arrival order kept)
+    d = np.concatenate(logs)
+    d = d[d["cc"] == 1]
+    order = np.argsort(d["member"], kind="stable")
+    d = d[order]
+    ev = np.zeros(len(d), USER_EVENT_DTYPE)
+    ev["group"] = d["member"]
+    ev["name"] = (d["key"] >> np.uint64(32)).astype(np.uint32)
+    ev["ltime"] = d["ltime"]
+    ev["payload"] = d["key"] & np.uint64(0xFFFFFFFF)
+    got = coalesce_user_events(ev)
+    assert 0 < len(got) < len(ev)
+    sample = np.random.default_rng(1).choice(np.unique(ev["group"]), 2000, replace=False)
+    bounds = np.searchsorted(ev["group"], np.stack([sample, sample + 1]))
+    gb = np.searchsorted(got["group"], np.stack([sample, sample + 1]))
+    for i in range(len(sample)):
+        sel = ev[bounds[0, i]:bounds[1, i]]
+        arr = (O.UEvent * len(sel))()
+        for j, e in enumerate(sel):
+            arr[j].name, arr[j].ltime, arr[j].payload = int(e["name"]), int(e["ltime"]), int(e["payload"])
+        res = (O.UEvent * len(sel))()
+        k = L.orc_coalesce_user_events(arr, len(sel), res)
+        mine = got[gb[0, i]:gb[1, i]]
+        assert k == len(mine)
+        assert [(r.name, r.ltime, r.payload) for r in res[:k]] == \
+            [(int(x["name"]), int(x["ltime"]), int(x["payload"])) for x in mine]
+    g.close()
+    L.orc_world_free(C.byref(w))

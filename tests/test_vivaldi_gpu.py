@@ -255,3 +255,140 @@ def test_observe_explicit_probes_matches_oracle_clients():
     for c in clients:
         L.orc_client_free(C.byref(c))
     g.close()
+
+
+class _DevArray:
+    """zero-copy torch view of engine-owned HBM (test hook)"""
+
+    def __init__(self, ptr, n, typestr="<f8"):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (int(ptr), False),
+                                         "version": 3, "strides": None}
+
+
+def _table(g):
+    import torch
+    ptr, stride = g.table_ptr()
+    return torch.as_tensor(_DevArray(ptr, g.n * stride), device="cuda").view(g.n, stride)
+
+
+def test_forget_node_matches_oracle_clients():
+    """CoordinateClient::forget_node (coordinate.rs:455-457) drops a peer's latency-filter
+    samples: updates before and after a forget, against oracle clients that forget the
+    same (member, slot) at the same point (the reference's test_client_latency_filter,
+    coordinate.rs:1024-1032, through the whole update)."""
+    n, slots = 48, 3
+    g = CoordinateClients(n, slots, CoordinateOptions(), seed=SEED)
+    oo = O.default_opts()
+    clients = []
+    for m in range(n):
+        c = O.Client()
+        assert L.orc_client_init(C.byref(c), C.byref(oo), slots) == 0
+        clients.append(c)
+    rng = np.random.default_rng(13)
+    for rnd in range(24):
+        if rnd % 4 == 3:  # forget a few (member, slot) pairs
+            for m, s in zip(rng.integers(0, n, 10), rng.integers(0, slots, 10)):
+                g.forget_node(int(m), int(s))
+                L.orc_client_forget_node(C.byref(clients[int(m)]), int(s))
+        members = rng.permutation(n)[:32].astype(np.uint32)
+        slot = rng.integers(0, slots, 32).astype(np.uint32)
+        others = [Coordinate(rng.normal(0, 0.02, 8), float(rng.uniform(0.1, 1.5)), float(rng.normal(0, 1e-3)),
+                             float(rng.uniform(1e-5, 1e-3))) for _ in range(32)]
+        rtts = [int(x) for x in rng.integers(1_000_000, 300_000_000, 32)]
+        status, rows = g.update_batch(members, slot, others, rtts, round_=rnd)
+        for i in range(32):
+            m = int(members[i])
+            o = others[i]
+            oc = O.coord(oo, list(o.portion), o.error, o.adjustment, o.height)
+            out = O.Coord()
+            e = L.orc_client_update(C.byref(clients[m]), int(slot[i]), C.byref(oc), rtts[i],
+                                    C.byref(O.rng(SEED, m, rnd)), C.byref(out))
+            assert status[i] == e == 0
+            c = clients[m].coord
+            exp = np.array(list(c.portion[:8]) + [c.error, c.adjustment, c.height])
+            np.testing.assert_array_equal(rows[i, :11].view(np.uint64), exp.view(np.uint64))
+    for c in clients:
+        L.orc_client_free(C.byref(c))
+    g.close()
+
+
+def test_nan_defense_reset_through_engine():
+    """test_client_nan_defense (coordinate.rs:1061-1066): a poisoned internal coordinate
+    is reset by the next update (stats().resets == 1) -- the engine's table poisoned in
+    HBM, the oracle client's in memory, same update, same bits."""
+    import torch
+    opts = CoordinateOptions(dimensionality=3)
+    g = CoordinateClients(2, 1, opts, seed=SEED)
+    t = _table(g)
+    t[0, 0] = float("nan")
+    torch.cuda.synchronize()
+    other = Coordinate.with_options(opts)
+    c = g.update(0, 0, other, 250_000_000)
+    assert c.is_valid() and g.stats()["resets"] == 1
+    oo = O.default_opts(dimensionality=3)
+    cl = O.Client()
+    assert L.orc_client_init(C.byref(cl), C.byref(oo), 1) == 0
+    cl.coord.portion[0] = float("nan")
+    out = O.Coord()
+    assert L.orc_client_update(C.byref(cl), 0, C.byref(O.coord(oo, [0.0, 0.0, 0.0])), 250_000_000,
+                               C.byref(O.rng(SEED, 0, 0)), C.byref(out)) == 0
+    assert cl.resets == 1
+    exp = np.array(list(cl.coord.portion[:3]) + [cl.coord.error, cl.coord.adjustment, cl.coord.height])
+    np.testing.assert_array_equal(g.get_rows(0, 1)[0, :6].view(np.uint64), exp.view(np.uint64))
+    L.orc_client_free(C.byref(cl))
+    g.close()
+
+
+def test_64m_population_properties_and_sampled_parity():
+    """BASELINE configs[4] at full size: 64M members, D=8, F=3, W=20, 16 neighbours.
+    Four rounds from device-resident probes; a 10k-member sample is checked BIT-EXACT
+    every round against oracle clients fed the same probe and the peer's row of the
+    previous-round table; the whole table stays finite with no resets; a second
+    context with the same seed produces the same table."""
+    import torch
+    n, peers, rounds, ns = 64_000_000, 16, 4, 10_000
+    rng = np.random.default_rng(64)
+    sample = np.sort(rng.choice(n, ns, replace=False)).astype(np.int64)
+    sidx = torch.from_numpy(sample).cuda()
+    oo = O.default_opts()
+    clients = []
+    for _ in range(ns):
+        c = O.Client()
+        assert L.orc_client_init(C.byref(c), C.byref(oo), peers) == 0
+        clients.append(c)
+    g = CoordinateClients(n, peers, CoordinateOptions(), seed=SEED)
+    peer = torch.empty(n, dtype=torch.int32, device="cuda")
+    rtt = torch.empty(n, dtype=torch.int64, device="cuda")
+    for r in range(rounds):
+        g.gen_probes(r, peer.data_ptr(), rtt.data_ptr())
+        g.sync()  # the engine runs on its own stream; torch reads the probes next
+        prev = _table(g)
+        sp = peer[sidx].long()
+        prow = prev[sp].cpu().numpy()
+        srtt = rtt[sidx].cpu().numpy().view(np.uint64)
+        g.observe(r % peers, peer.data_ptr(), rtt.data_ptr(), None, r)
+        torch.cuda.synchronize()
+        got = _table(g)[sidx].cpu().numpy()
+        for i in range(ns):
+            m = int(sample[i])
+            o = prow[i]
+            oc = O.coord(oo, list(o[:8]), o[8], o[9], o[10])
+            out = O.Coord()
+            assert L.orc_client_update(C.byref(clients[i]), r % peers, C.byref(oc), int(srtt[i]),
+                                       C.byref(O.rng(SEED, m, r)), C.byref(out)) == 0
+            c = clients[i].coord
+            exp = np.array(list(c.portion[:8]) + [c.error, c.adjustment, c.height])
+            np.testing.assert_array_equal(got[i, :11].view(np.uint64), exp.view(np.uint64), err_msg=f"r{r} m{m}")
+    full = _table(g)[:, :11]
+    assert bool(torch.isfinite(full).all())
+    assert g.stats()["resets"] == 0
+    h = CoordinateClients(n, peers, CoordinateOptions(), seed=SEED)
+    for r in range(rounds):
+        h.gen_probes(r, peer.data_ptr(), rtt.data_ptr())
+        h.observe(r % peers, peer.data_ptr(), rtt.data_ptr(), None, r)
+    torch.cuda.synchronize()
+    assert torch.equal(_table(h)[:, :11].view(torch.int64), full.view(torch.int64))
+    for c in clients:
+        L.orc_client_free(C.byref(c))
+    g.close()
+    h.close()
