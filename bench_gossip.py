@@ -18,6 +18,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 SEED = 0x5EED5EED
 SUBJECTS = 4096
 SETTLE_ROUNDS = 12   # setup: bring the cluster to gossip steady state (queues saturated) before timing
+# fraction of force_leaves issued with prune (remove_failed_node_prune); RSF_PRUNE_FRAC overrides
+PRUNE_FRAC = float(os.environ.get("RSF_PRUNE_FRAC", 0.1))
 HBM_PEAK_GBS = 8000.0
 
 
@@ -63,7 +65,7 @@ def run_gossip(args, rank, world):
     n = per * world
     rounds_total = SETTLE_ROUNDS + args.warmup + args.steps
     cfg = gossip_cfg(n, rounds_total, world)
-    subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED)
+    subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED, prune_frac=PRUNE_FRAC)
     views = W.initial_views(SUBJECTS)
     stream = torch.cuda.current_stream()
     if world == 1 and os.environ.get("RSF_FORCE_SHARDED") != "1":
@@ -178,7 +180,7 @@ def cpu_baseline_gossip(args, seconds_target=10.0, n=200_000):
     th = cpu_threads()
     rounds_total = SETTLE_ROUNDS + 40
     cfg = gossip_cfg(n, rounds_total, 1)
-    subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED)
+    subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED, prune_frac=PRUNE_FRAC)
     w = H.oracle_world(cfg, subj, W.initial_views(SUBJECTS))
     t = 0
     for _ in range(SETTLE_ROUNDS):

@@ -561,7 +561,7 @@ int orc_world_init(orc_world* w, const orc_world_cfg* c) {
   memset(w, 0, sizeof(*w));
   if (c->n < 2 || c->s == 0 || c->s > c->n || c->qcap == 0 || c->qcap > 64 || c->ebuf == 0 ||
       c->qbuf == 0 || c->slot_k == 0 || c->fanout == 0 || c->fanout >= c->n || c->max_refute == 0 ||
-      c->cap_rumors == 0 || (c->cap_rumors & (c->cap_rumors - 1)) || c->cap_rumors > (1u << 31))
+      c->cap_rumors == 0 || (c->cap_rumors & (c->cap_rumors - 1)) || c->cap_rumors > (1u << 30))
     return -1;
   w->n = c->n;
   w->s = c->s;
@@ -584,15 +584,15 @@ int orc_world_init(orc_world* w, const orc_world_cfg* c) {
       A(q_seq, n * 3 * c->qcap) || A(q_tx, n * 3 * c->qcap) || A(q_len, n * 3 * c->qcap) ||
       A(q_next_seq, n * 3) || A(eb_ltime, n * c->ebuf) || A(eb_cnt, n * c->ebuf) ||
       A(eb_keys, n * c->ebuf * c->slot_k) || A(qb_ltime, n * c->qbuf) || A(qb_cnt, n * c->qbuf) ||
-      A(qb_ids, n * c->qbuf * c->slot_k) || A(rumors, c->cap_rumors ? c->cap_rumors : 1) || A(v_time, n * s) ||
-      A(q_pruned, n) || A(q_expired, n) || A(rgen, c->cap_rumors ? c->cap_rumors : 1)) {
+      A(qb_ids, n * c->qbuf * c->slot_k) || A(rumors, 2 * (size_t)c->cap_rumors) || A(v_time, n * s) ||
+      A(q_pruned, n) || A(q_expired, n)) {
     orc_world_free(w);
     return -1;
   }
 #undef A
   w->cap_rumors = c->cap_rumors;
   w->rbits = 0;
-  while ((1u << w->rbits) < c->cap_rumors && w->rbits < 31) w->rbits++;
+  while ((1u << w->rbits) < c->cap_rumors) w->rbits++;
   for (size_t m = 0; m < n; ++m) {
     /* Serf::new: every clock incremented once (base.rs:195-199) */
     w->clock[m] = 1;
@@ -611,7 +611,7 @@ void orc_world_free(orc_world* w) {
                   w->serf_state, w->err, w->subj_member, w->member_subj, w->refute_cnt,
                   w->refute_ltime, w->v_ltime, w->v_status, w->v_kind, w->q_rumor, w->q_seq,
                   w->q_tx, w->q_len, w->q_next_seq, w->eb_ltime, w->eb_cnt, w->eb_keys,
-                  w->qb_ltime, w->qb_cnt, w->qb_ids, w->rumors, w->v_time, w->q_pruned, w->q_expired, w->rgen,
+                  w->qb_ltime, w->qb_cnt, w->qb_ids, w->rumors, w->v_time, w->q_pruned, w->q_expired,
                   w->dlog, w->dcnt};
   for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) free(ptrs[i]);
   memset(w, 0, sizeof(*w));
@@ -817,7 +817,7 @@ static inline uint64_t tlq_key(uint16_t tx, uint16_t len, uint32_t seq) {
 void orc_queue_insert(orc_world* w, uint32_t m, uint32_t q, uint32_t rumor) {
   size_t base = ((size_t)m * 3 + q) * w->qcap;
   uint32_t seq = w->q_next_seq[(size_t)m * 3 + q]++;
-  uint16_t len = w->rumors[rumor & (w->cap_rumors - 1)].msg_len;
+  uint16_t len = w->rumors[orc_rumor_index(w, rumor)].msg_len;
   uint32_t slot = EMPTY_RUMOR;
   for (uint32_t i = 0; i < w->qcap; ++i)
     if (w->q_rumor[base + i] == EMPTY_RUMOR) {
@@ -844,12 +844,19 @@ void orc_queue_insert(orc_world* w, uint32_t m, uint32_t q, uint32_t rumor) {
 }
 
 uint32_t orc_rumor_generations(const orc_world* w) {
-  /* ids gen << rbits | slot never reach 0xFFFFFFFF (the empty-queue-slot marker) */
-  return w->rbits >= 32 ? 1u : (uint32_t)((1ull << (32 - w->rbits)) - 1);
+  /* even, so the parity alternates across the wrap; ids gen << rbits | slot never reach
+   * 0xFFFFFFFF (the empty-queue-slot marker) */
+  return (uint32_t)((1ull << (32 - w->rbits)) - 2);
+}
+
+uint32_t orc_rumor_index(const orc_world* w, uint32_t rid) {
+  /* two generations resident: the id's generation parity selects the table half */
+  return rid & ((w->cap_rumors << 1) - 1);
 }
 
 int orc_rumor_live(const orc_world* w, uint32_t rid) {
-  return w->rgen[rid & (w->cap_rumors - 1)] == (rid >> w->rbits);
+  const uint32_t G = orc_rumor_generations(w);
+  return (w->gen + G - (rid >> w->rbits) % G) % G < 2;
 }
 
 uint32_t orc_queue_expire(orc_world* w, uint32_t m, uint32_t q) {
@@ -964,7 +971,7 @@ static uint32_t queue_of(uint8_t type) {
 
 static uint32_t new_rumor(orc_world* w, uint32_t id, uint8_t type, uint8_t flags, uint32_t subject,
                           uint64_t ltime, uint64_t key, uint32_t name_len, uint32_t payload_len) {
-  orc_rumor* r = &w->rumors[id & (w->cap_rumors - 1)];
+  orc_rumor* r = &w->rumors[orc_rumor_index(w, id)];
   r->type = type;
   r->flags = flags;
   r->subject = subject;
@@ -983,7 +990,7 @@ static void push_refute(orc_world* w, uint32_t m, uint64_t ltime) {
 
 /* apply one received rumor at receiver r  (notify_message, delegate.rs:157-305) */
 static void merge_one(orc_world* w, uint32_t r, uint32_t rid) {
-  const orc_rumor* ru = &w->rumors[rid & (w->cap_rumors - 1)];
+  const orc_rumor* ru = &w->rumors[orc_rumor_index(w, rid)];
   int f = 0;
   uint64_t refute = 0;
   switch (ru->type) {
@@ -1063,8 +1070,6 @@ static void phase_emit(world_job* j) {
   for (uint32_t m = j->lo; m < j->hi; ++m) {
     if (!w->alive[m]) continue;
     uint32_t np = orc_pick_peers(w->seed, n, w->alive, m, j->round, k, peers);
-    if (np) /* items whose rumor slot was recycled have expired */
-      for (uint32_t q = 0; q < 3; ++q) w->q_expired[m] += orc_queue_expire(w, m, q);
     for (uint32_t p = 0; p < np; ++p) {
       uint32_t used = 0, got = 0, b;
       for (uint32_t q = 0; q < 3; ++q) {
@@ -1137,13 +1142,13 @@ int orc_world_round_mt(orc_world* w, uint32_t round, const orc_ml_event* ml, uin
   if (w->n_rumors + need > w->cap_rumors) {
     w->n_rumors = 0;
     w->gen = (w->gen + 1) % orc_rumor_generations(w);
+    /* this generation reuses the table half of generation gen - 2: its queued ids expire */
+    for (uint32_t m = 0; m < n; ++m)
+      for (uint32_t q = 0; q < 3; ++q) w->q_expired[m] += orc_queue_expire(w, m, q);
   }
   const uint32_t slot0 = w->n_rumors;
   uint32_t base = (uint32_t)(((uint64_t)w->gen << w->rbits) | slot0);
-  for (uint32_t i = 0; i < need; ++i) {
-    w->rumors[slot0 + i].type = 0xFF;
-    w->rgen[slot0 + i] = w->gen;
-  }
+  for (uint32_t i = 0; i < need; ++i) w->rumors[orc_rumor_index(w, base + i)].type = 0xFF;
   w->n_rumors += need;
   if (w->dcap) memset(w->dcnt, 0, (size_t)n * sizeof(uint32_t)); /* the round's delivery log */
 

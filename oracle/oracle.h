@@ -229,10 +229,10 @@ typedef struct {
   uint32_t* v_time;
   uint32_t now; /* the current time stamped by the handlers (orc_world_round sets it to the round) */
   uint32_t* q_pruned; /* [n] live items dropped by a full queue (cumulative) */
-  /* rumor table = a ring of cap_rumors (a power of two) slots; a rumor id is
-   * generation << rbits | slot.  n_rumors is the ring cursor (next free slot). */
-  uint32_t* q_expired; /* [n] queue items dropped at emission because their rumor slot was recycled */
-  uint32_t* rgen;      /* [cap_rumors] generation of the rumor held in each slot */
+  /* rumor ring: cap_rumors (a power of two) slots per generation; a rumor id is
+   * generation << rbits | slot, stored at index id & (2 cap - 1) (two generations
+   * resident, by parity).  n_rumors is the ring cursor (next free slot). */
+  uint32_t* q_expired; /* [n] queue items dropped when the ring wrapped onto their generation's half */
   uint32_t gen, rbits;
   /* delivery log (rsf_gossip_set_delivery_log): per member up to dcap UserEvents sent to
    * the application since the round began, {ltime, key, cc} */
@@ -264,8 +264,9 @@ int orc_world_set_delivery_log(orc_world* w, uint32_t per_member);
 int orc_handle_query(orc_world* w, uint32_t m, uint64_t ltime, uint32_t id, int no_broadcast);
 int orc_upsert_intent(orc_world* w, uint32_t m, uint32_t subj, uint8_t kind, uint64_t ltime);
 
-/* rumor ring: generations per cycle, liveness of an id, expiry of a member's queue */
+/* rumor ring: generations per cycle, table index and liveness of an id, expiry of a member's queue */
 uint32_t orc_rumor_generations(const orc_world* w);
+uint32_t orc_rumor_index(const orc_world* w, uint32_t rid);
 int orc_rumor_live(const orc_world* w, uint32_t rid);
 uint32_t orc_queue_expire(orc_world* w, uint32_t m, uint32_t q);
 

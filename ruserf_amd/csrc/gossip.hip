@@ -216,7 +216,7 @@ __device__ __forceinline__ uint32_t q_insert_wave(const GCfg& c, QRegs& Q, uint3
 // others take the existing items in order.  Returns the number of live items
 // that did not fit (memberlist Prune of the queue's tail).
 __device__ __forceinline__ uint32_t q_insert_batch(const GCfg& c, QRegs& Q, uint32_t lane, bool ins, uint32_t rid,
-                                               uint32_t len, uint32_t seq0, uint64_t newmask) {
+                                                   uint32_t len, uint32_t seq0, uint64_t newmask) {
   const bool valid = lane < c.qcap;
   const bool live = valid && Q.r != kEmpty;
   const uint32_t n_live = (uint32_t)__popcll(__ballot(live));
@@ -631,23 +631,12 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   const bool ne0 = shfl_u32(Q0.r, 0) != kEmpty, ne1 = shfl_u32(e.head, 1) != kEmpty,
              ne2 = shfl_u32(e.head, 2) != kEmpty;
   if (np == 0 || !(ne0 || ne1 || ne2)) return;
-  // decoration of the intents (their subject slots) and each item's rumor generation
-  uint32_t g0 = 0, g1 = 0, g2 = 0;
-  if (Q0.r != kEmpty) {
-    Q0.dec = s.rdec[Q0.r & c.rmask];
-    g0 = s.rgen[Q0.r & c.rmask];
-  }
+  bool d0 = false, d1 = false, d2 = false;
+  uint32_t err = 0;
+  // decoration of the intents: their subject slots (subject and type share one 8-B word)
+  if (Q0.r != kEmpty) Q0.dec = s.rdec[Q0.r & c.rmask];
   if (ne1) q_load(c, s, l, 1, lane, Q1);
   if (ne2) q_load(c, s, l, 2, lane, Q2);
-  if (Q1.r != kEmpty) g1 = s.rgen[Q1.r & c.rmask];
-  if (Q2.r != kEmpty) g2 = s.rgen[Q2.r & c.rmask];
-  uint32_t err = 0;
-  // items of recycled rumor slots expire before the first get_broadcasts
-  const uint32_t x0 = q_expire(c, Q0, lane, g0 != (Q0.r >> c.rbits), true);
-  const uint32_t x1 = q_expire(c, Q1, lane, g1 != (Q1.r >> c.rbits), false);
-  const uint32_t x2 = q_expire(c, Q2, lane, g2 != (Q2.r >> c.rbits), false);
-  bool d0 = x0 != 0, d1 = x1 != 0, d2 = x2 != 0;
-  if ((x0 | x1 | x2) && lane == 0) s.q_expired[l] += x0 + x1 + x2;
   for (uint32_t j = 0; j < np; ++j) {
     const uint32_t gslot = shfl_u32(e.gs, j);
     const uint64_t out_base = (uint64_t)gslot * c.cap_t;
@@ -661,7 +650,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   if (d0) q_store(c, s, l, 0, lane, Q0, true);
   if (d1) q_store(c, s, l, 1, lane, Q1, true);
   if (d2) q_store(c, s, l, 2, lane, Q2, true);
-  if (err && lane == 0) s.err[l] |= err;
+  if (err && lane == 0) s.err[l] |= err;  // rare: a stage overflow
 }
 
 __global__ void __launch_bounds__(64 * RSF_EMIT_WPB) emit_kernel(GCfg c, GState s, const uint32_t* __restrict__ grp_key,
@@ -705,12 +694,10 @@ __device__ __forceinline__ uint32_t decorate(const rsf_rumor* __restrict__ rumor
 // The same pass keeps the rumor bodies without their 8-B key (only user events and
 // queries need it) as aligned 16-B records for the merge kernel's gather.
 __global__ void __launch_bounds__(256) dec_fill_kernel(const rsf_rumor* __restrict__ rumors, uint32_t* __restrict__ rdec,
-                                                       uint4* __restrict__ rbody, uint32_t* __restrict__ rgen,
-                                                       uint32_t gen, uint64_t base, uint64_t n) {
+                                                       uint4* __restrict__ rbody, uint64_t base, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   rdec[base + i] = decorate(rumors, (uint32_t)(base + i));
-  rgen[base + i] = gen;  // ids of the slot's previous generation expire
   const uint2* w = reinterpret_cast<const uint2*>(rumors + base + i);  // ltime | key | subject..msg_len
   const uint2 lt = w[0], tail = w[2];
   rbody[base + i] = make_uint4(lt.x, lt.y, tail.x, tail.y);
@@ -804,9 +791,6 @@ __device__ unsigned long long g_merge_prof[8];
 #ifndef RSF_MERGE_CHAIN_BY_SUBJECT
 #define RSF_MERGE_CHAIN_BY_SUBJECT 1  // 1: chain detection loops over distinct subjects, not records
 #endif
-#ifndef RSF_MERGE_BATCH
-#define RSF_MERGE_BATCH 1  // 1: a chunk's intent re-queues go in with one q_insert_batch
-#endif
 // What a receiver's merge needs before its records: segment bounds, liveness, the queues'
 // next insertion seqs and the member's registers, issued a receiver AHEAD (merge_kernel)
 // as ONE lane-distributed load: lane j fetches dword j of the setup (kSu* below) from its
@@ -815,7 +799,7 @@ __device__ unsigned long long g_merge_prof[8];
 enum : uint32_t {
   kSuStart, kSuEnd, kSuAlive, kSuSeq0, kSuSeq1, kSuSeq2, kSuClock, kSuEClock = kSuClock + 2,
   kSuQClock = kSuEClock + 2, kSuEMin = kSuQClock + 2, kSuQMin = kSuEMin + 2, kSuDigest = kSuQMin + 2,
-  kSuErr = kSuDigest + 2, kSuSerf, kSuSubj, kSuLanes
+  kSuErr = kSuDigest + 2, kSuSerf, kSuSubj, kSuPruned, kSuLanes
 };
 // per-lane source: byte address = base + l * mult + off (alive / serf_state: the aligned
 // dword holding the byte)
@@ -839,6 +823,7 @@ __device__ __forceinline__ MSetupLane merge_setup_lane(const GCfg& c, const GSta
   if (lane == kSuErr) b = (const char*)s.err;
   if (lane == kSuSerf) b = (const char*)s.serf_state, mult = 1;
   if (lane == kSuSubj) b = (const char*)s.member_subj;
+  if (lane == kSuPruned) b = (const char*)s.q_pruned;
   return MSetupLane{b, mult, off};
 }
 __device__ __forceinline__ uint32_t merge_setup(const MSetupLane& sl, uint64_t l, uint32_t lane) {
@@ -869,6 +854,63 @@ __device__ __forceinline__ void qlds_put(QLds& q, uint32_t lane, const QRegs& Q)
 }
 __device__ __forceinline__ QRegs qlds_get(const QLds& q, uint32_t lane) { return QRegs{q.r[lane], q.sq[lane], q.tl[lane]}; }
 
+// q_insert_batch over the DISTINCT LENGTHS of the new items instead of the items.  New
+// items all have transmits 0 and newer seqs than anything queued, so:
+//   new j lands at  #{queued: tx 0, len > len_j} + #{new: len > len_j} + #{new: len == len_j, later lane}
+//   queued i (lane i) lands at  i + (tx_i > 0 ? n_new : #{new: len >= len_i})
+// -- one pass per distinct new length (the message-length model has a handful), then
+// every item is written to its place in the wave's LDS row and read back in order.
+// Same result and drop count as q_insert_batch.
+__device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, uint32_t lane, bool ins, uint32_t rid,
+                                                       uint32_t len, uint32_t seq0, uint64_t newmask, QLds& row) {
+  const bool valid = lane < c.qcap;
+  const bool live = valid && Q.r != kEmpty;
+  const uint32_t n_live = (uint32_t)__popcll(__ballot(live));
+  const uint32_t n_new = (uint32_t)__popcll(newmask);
+  const uint64_t below = below_mask(lane), above = ~below & ~(1ull << lane);
+  const uint32_t myseq = seq0 + (uint32_t)__popcll(newmask & below);
+  const bool etx0 = live && (Q.tl & 0xFFFF) == 0;
+  const uint32_t elen = Q.tl >> 16;
+  uint32_t pos_n = 0, pos_e = lane + ((live && !etx0) ? n_new : 0u);
+  uint64_t rem = newmask;
+  while (rem) {
+    const uint32_t L = shfl_u32(len, __ffsll((long long)rem) - 1);
+    const uint64_t same = __ballot(ins && len == L);
+    rem &= ~same;
+    const uint32_t gt_new = (uint32_t)__popcll(__ballot(ins && len > L));
+    const uint32_t gt_old = (uint32_t)__popcll(__ballot(etx0 && elen > L));
+    if (ins && len == L) pos_n = gt_old + gt_new + (uint32_t)__popcll(same & above);
+    if (etx0 && elen <= L) pos_e += (uint32_t)__popcll(same);
+  }
+  if (ins && pos_n < c.qcap) {
+    row.r[pos_n] = rid;
+    row.sq[pos_n] = myseq;
+    row.tl[pos_n] = len << 16;
+  }
+  if (live && pos_e < c.qcap) {
+    row.r[pos_e] = Q.r;
+    row.sq[pos_e] = Q.sq;
+    row.tl[pos_e] = Q.tl;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint32_t total = n_live + n_new;
+  if (valid) {
+    if (lane < total) {
+      Q.r = row.r[lane];
+      Q.sq = row.sq[lane];
+      Q.tl = row.tl[lane];
+    } else {
+      Q.r = kEmpty;
+      Q.sq = 0;
+      Q.tl = 0;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();  // the row is free once every lane has read it
+  return total > c.qcap ? total - c.qcap : 0u;
+}
+
 // One receiver (one wave).  Input layouts: flat (gcnt == nullptr, stride 1): records
 // [seg_start, seg_end) in canonical order; grouped (emit_kernel's): groups [seg_start,
 // seg_end) of `stride` slots each, group g holding gcnt[g] records, so lane = slot and the
@@ -877,7 +919,8 @@ __device__ __forceinline__ QRegs qlds_get(const QLds& q, uint32_t lane) { return
 // was inserted.
 __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const uint32_t* __restrict__ vals,
                                           const uint32_t* __restrict__ dec, const uint32_t* __restrict__ gcnt,
-                                          uint32_t stride, uint64_t l, uint32_t lane, uint32_t su, QLds* ql) {
+                                          uint32_t stride, uint64_t l, uint32_t lane, uint32_t su, QLds* ql,
+                                          uint32_t* __restrict__ sbits) {
   MPROF_T(t_start);
   const uint32_t st = shfl_u32(su, kSuStart), en = shfl_u32(su, kSuEnd);
   if (st >= en || (shfl_u32(su, kSuAlive) & 0xFF) == 0) return;
@@ -946,7 +989,16 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     // chains: previous / next record of the same subject in this chunk
     int prev = -1, next = -1;
 #if RSF_MERGE_CHAIN_BY_SUBJECT
-    {
+    // fast path: chunk subjects hashed into the wave's 4096-bit LDS map; no clash means
+    // every subject is distinct in the chunk, so there are no chains to link
+    bool clash = false;
+    if (is_view) {
+      const uint32_t h = my_subj & 4095u;
+      const uint32_t old = atomicOr(sbits + (h >> 5), 1u << (h & 31));
+      clash = (old >> (h & 31)) & 1u;
+      sbits[h >> 5] = 0u;  // LDS ops of a wave run in order: every lane's OR has returned
+    }
+    if (__ballot(clash)) {
       // one pass per DISTINCT subject: the ballot of the lanes holding it is the chain,
       // each lane's neighbours are the nearest set bits below and above it
       uint64_t mm = __ballot(is_view), same = 0;
@@ -1013,7 +1065,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
         const uint64_t lt0 = v.ltime;
         const uint32_t mt0 = v.meta, t0 = v.t;
         if (ru.type == RSF_MSG_JOIN) f = hv_join_intent(v, rr, ru.ltime, c.now);
-        else f = hv_leave_intent(v, rr, ru.subject, ru.ltime, ru.flags & 1, ref, c.now);
+        else f = hv_leave_intent<false>(v, rr, ru.subject, ru.ltime, ru.flags & 1, ref, c.now);
         if (f & RSF_F_MEMBER_EVENT) contrib = kDigMember | ((uint64_t)kEvLeave << 32) | ru.subject;
         dirty = dirty || v.ltime != lt0 || v.meta != mt0 || v.t != t0;
         done = true;
@@ -1024,22 +1076,17 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     if (chunk_max > r.clock) r.clock = chunk_max;
     MPROF_T(t_c2);
     MPROF_ADD(2, t_c1, t_c2);
-#if RSF_MERGE_BATCH
     // intent re-queues of the chunk in one batch (the intent queue takes nothing else)
     const bool ins = is_view && (f & RSF_F_REBROADCAST);
     const uint64_t newmask = __ballot(ins);
     if (newmask) {
-      qdrop += q_insert_batch(c, Q0, lane, ins, rid, ru.msg_len, nseq0, newmask);
+      qdrop += q_insert_batch_lds(c, Q0, lane, ins, rid, ru.msg_len, nseq0, newmask, ql[2]);
       nseq0 += (uint32_t)__popcll(newmask);
       d0 = true;
     }
     // serial part, record order: events/queries (lane 0 handlers), digest, refutes
     const uint64_t serial =
         __ballot(valid && (!is_view || (f & (RSF_F_MEMBER_EVENT | RSF_F_REFUTE | RSF_F_PRUNE))));
-#else
-    // serial part, record order: events/queries (lane 0 handlers), digest, refutes, re-queues
-    const uint64_t serial = __ballot(valid && (!is_view || f != 0));
-#endif
     uint64_t mm = serial;
     while (mm) {
       const int i = __ffsll((long long)mm) - 1;
@@ -1074,10 +1121,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
       if (fi & RSF_F_REBROADCAST) {
         const uint32_t q = queue_of(type), rid_i = shfl_u32(rid, i), mlen = tf >> 16;
         if (q == kQIntent) {
-          if (!RSF_MERGE_BATCH) {
-            qdrop += q_insert_wave(c, Q0, lane, rid_i, mlen, nseq0++);
-            d0 = true;
-          }
+          // intents went in above, batched per chunk
         } else if (q == kQQuery) {
           QRegs t = qlds_get(ql[0], lane);
           qdrop += q_insert_wave(c, t, lane, rid_i, mlen, nseq1++);
@@ -1100,9 +1144,18 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
   if (d1) q_store(c, s, l, 1, lane, qlds_get(ql[0], lane), true);
   if (d2) q_store(c, s, l, 2, lane, qlds_get(ql[1], lane), true);
   if (qdrop) r.err |= kErrQueue;
+  const uint32_t pruned0 = shfl_u32(su, kSuPruned);
+  // registers go back only where they changed (the setup lanes hold the old values)
+  const bool w_clock = r.clock != su64(su, kSuClock), w_eclock = r.eclock != su64(su, kSuEClock),
+             w_qclock = r.qclock != su64(su, kSuQClock), w_digest = r.digest != su64(su, kSuDigest),
+             w_err = r.err != shfl_u32(su, kSuErr);
   if (lane == 0) {
-    store_regs(s, l, r);
-    if (qdrop) s.q_pruned[l] += qdrop;
+    if (w_clock) s.clock[l] = r.clock;
+    if (w_eclock) s.eclock[l] = r.eclock;
+    if (w_qclock) s.qclock[l] = r.qclock;
+    if (w_digest) s.digest[l] = r.digest;
+    if (w_err) s.err[l] = r.err;
+    if (qdrop) s.q_pruned[l] = pruned0 + qdrop;
     if (d0) s.q_next_seq[l * 3 + 0] = nseq0;
     if (d1) s.q_next_seq[l * 3 + 1] = nseq1;
     if (d2) s.q_next_seq[l * 3 + 2] = nseq2;
@@ -1126,8 +1179,11 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
                                                     const uint32_t* __restrict__ seg_end,
                                                     const uint32_t* __restrict__ gcnt, uint32_t stride) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
-  __shared__ QLds qlds[kWavesPerBlock][2];
+  __shared__ QLds qlds[kWavesPerBlock][3];  // query queue, event queue, insert scratch
+  __shared__ uint32_t subj_bits[kWavesPerBlock][128];  // chain detection (zero between chunks)
   QLds* ql = qlds[threadIdx.x / kWave];
+  uint32_t* sbits = subj_bits[threadIdx.x / kWave];
+  for (uint32_t i = threadIdx.x & (kWave - 1); i < 128; i += kWave) sbits[i] = 0u;
   const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
   uint64_t l = (uint64_t)(RSF_MERGE_PERSIST ? blockIdx.x : xcd_block(blockIdx.x, gridDim.x)) * kWavesPerBlock +
                (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -1139,7 +1195,7 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
     // every owned receiver's setup is in flight before the first merge starts
     for (uint32_t k = 0; k < RSF_MERGE_PER_WAVE && l + k < c.n_loc; ++k) {
       const uint32_t nxt = k + 1 < RSF_MERGE_PER_WAVE && l + k + 1 < c.n_loc ? merge_setup(sl, l + k + 1, lane) : 0u;
-      merge_one(c, s, vals, dec, gcnt, stride, l + k, lane, cur, ql);
+      merge_one(c, s, vals, dec, gcnt, stride, l + k, lane, cur, ql, sbits);
       cur = nxt;
     }
     return;
@@ -1149,7 +1205,7 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
     const bool more = RSF_MERGE_PERSIST && ln < c.n_loc;
     uint32_t nxt = 0;
     if (more) nxt = merge_setup(sl, ln, lane);
-    merge_one(c, s, vals, dec, gcnt, stride, l, lane, cur, ql);
+    merge_one(c, s, vals, dec, gcnt, stride, l, lane, cur, ql, sbits);
     if (!more) break;
     cur = nxt;
     l = ln;
@@ -1559,6 +1615,29 @@ __global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uin
   }
 }
 
+// Generations alive: gen and gen - 1 (modulo the generation count, even so that the
+// parity alternates across the wrap).
+__host__ __device__ inline uint32_t rumor_generations(const GCfg& c) { return (uint32_t)((1ull << (32 - c.rbits)) - 2); }
+
+// At the start of generation `gen` (the ring wrapped): every queue drops its items of
+// generation gen - 2, whose table half this generation overwrites.  One wave per
+// (member, queue), lane = queue slot; the survivors keep their sorted order.
+__global__ void __launch_bounds__(256) expire_kernel(GCfg c, GState s, uint32_t gen) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  if (t >= c.n_loc * 3) return;
+  const uint64_t l = t / 3;
+  const uint32_t q = (uint32_t)(t % 3);
+  QRegs Q{kEmpty, 0, 0};
+  q_load(c, s, l, q, lane, Q);
+  const uint32_t G = rumor_generations(c);
+  const uint32_t age = (gen + G - (Q.r >> c.rbits) % G) % G;
+  const uint32_t x = q_expire(c, Q, lane, age >= 2, false);
+  if (!x) return;
+  q_store(c, s, l, q, lane, Q, true);
+  if (x && lane == 0) atomicAdd(s.q_expired + l, x);
+}
+
 __global__ void accumulate_kernel(unsigned long long* counters) {
   if (threadIdx.x == 0 && blockIdx.x == 0) counters[60] += counters[0];
 }
@@ -1675,8 +1754,8 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   if (cfg->fanout == 0 || cfg->fanout > 8 || cfg->fanout >= N) return gerr("fanout must be 1..8 and < n_members");
   if (cfg->gossip_limit > 0xFFFFFF || cfg->gossip_overhead > 0xFFFF) return gerr("gossip budget too large");
   if (cfg->max_refute == 0 || cfg->max_refute > 4) return gerr("max_refute must be 1..4");
-  if (cfg->max_rumors == 0 || (cfg->max_rumors & (cfg->max_rumors - 1)) || cfg->max_rumors > (1u << 31))
-    return gerr("max_rumors must be a power of two <= 2^31 (the rumor ring)");
+  if (cfg->max_rumors == 0 || (cfg->max_rumors & (cfg->max_rumors - 1)) || cfg->max_rumors > (1u << 30))
+    return gerr("max_rumors must be a power of two <= 2^30 (the rumor ring)");
   RSF_HIP(hipSetDevice(device));
   rsf_gossip* g = new (std::nothrow) rsf_gossip();
   if (!g) return rsf::set_error(RSF_ERR_NOMEM, "host allocation failed");
@@ -1712,7 +1791,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   g->max_rumors = cfg->max_rumors;
   c.rbits = 0;
   while ((1u << c.rbits) < cfg->max_rumors) c.rbits++;
-  c.rmask = cfg->max_rumors - 1;
+  c.rmask = (cfg->max_rumors << 1) - 1;
   g->end_bit = bits_for(N);
   auto fail = [&](int code) {
     rsf_gossip_destroy(g);
@@ -1732,8 +1811,8 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
       GA(s.q_txlen, n * 3 * c.qcap * 4) || GA(s.q_next_seq, n * 3 * 4) || GA(s.q_pruned, n * 4) || GA(s.q_expired, n * 4) || GA(s.eb_ltime, n * c.ebuf * 8) ||
       GA(s.eb_cnt, n * c.ebuf * 4) || GA(s.eb_keys, n * c.ebuf * c.slot_k * 8) || GA(s.qb_ltime, n * c.qbuf * 8) ||
       GA(s.qb_cnt, n * c.qbuf * 4) || GA(s.qb_ids, n * c.qbuf * c.slot_k * 4) ||
-      GA(s.rumors, (size_t)cfg->max_rumors * sizeof(rsf_rumor)) || GA(s.rdec, (size_t)cfg->max_rumors * 4) ||
-      GA(s.rbody, (size_t)cfg->max_rumors * 16) || GA(s.rgen, (size_t)cfg->max_rumors * 4))
+      GA(s.rumors, (size_t)cfg->max_rumors * 2 * sizeof(rsf_rumor)) ||
+      GA(s.rdec, (size_t)cfg->max_rumors * 2 * 4) || GA(s.rbody, (size_t)cfg->max_rumors * 2 * 16))
     return fail(rc);
   g->stage_cap = n * c.fanout * c.cap_t;
   if (g->stage_cap >= 0xFFFFFFFFull) return fail(gerr("n_members x fanout x per-target records must fit 32 bits"));
@@ -1790,16 +1869,15 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   ms(s.q_next_seq, 0, n * 3 * 4);
   ms(s.q_pruned, 0, n * 4);
   ms(s.q_expired, 0, n * 4);
-  ms(s.rgen, 0, (size_t)cfg->max_rumors * 4);
   ms(s.eb_ltime, 0, n * c.ebuf * 8);
   ms(s.eb_cnt, 0, n * c.ebuf * 4);
   ms(s.eb_keys, 0, n * c.ebuf * c.slot_k * 8);
   ms(s.qb_ltime, 0, n * c.qbuf * 8);
   ms(s.qb_cnt, 0, n * c.qbuf * 4);
   ms(s.qb_ids, 0, n * c.qbuf * c.slot_k * 4);
-  ms(s.rumors, 0, (size_t)cfg->max_rumors * sizeof(rsf_rumor));
-  ms(s.rdec, 0, (size_t)cfg->max_rumors * 4);
-  ms(s.rbody, 0, (size_t)cfg->max_rumors * 16);
+  ms(s.rumors, 0, (size_t)cfg->max_rumors * 2 * sizeof(rsf_rumor));
+  ms(s.rdec, 0, (size_t)cfg->max_rumors * 2 * 4);
+  ms(s.rbody, 0, (size_t)cfg->max_rumors * 2 * 16);
   if (!ok) return fail(rsf::set_error(RSF_ERR_HIP, "context initialisation failed"));
   // Serf::new increments every clock once (base.rs:195-199)
   hipLaunchKernelGGL(fill_u64_kernel, dim3(grid1(n)), dim3(256), 0, st, s.clock, n, 1ull);
@@ -1818,7 +1896,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
   GState& s = g->s;
   void* ptrs[] = {s.clock,  s.eclock,      s.qclock,       s.emin,        s.qmin,     s.digest,     s.err,
                   s.alive,  s.serf_state,  s.member_subj,  s.subj_member, s.refute_cnt, s.refute_ltime, s.view,
-                  s.q_rumor, s.q_seq,      s.q_txlen,      s.q_next_seq,  s.q_pruned, s.q_expired, s.rgen,  s.eb_ltime, s.eb_cnt,     s.eb_keys,
+                  s.q_rumor, s.q_seq,      s.q_txlen,      s.q_next_seq,  s.q_pruned, s.q_expired,  s.eb_ltime, s.eb_cnt,     s.eb_keys,
                   s.qb_ltime, s.qb_cnt,    s.qb_ids,       s.rumors,      s.rdec,       s.rbody,      g->d_ml,    g->d_acts,    g->stage_key,
                   g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters, g->rec_dec, g->pp_buf,
                   g->sort_tmp, g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
@@ -2019,15 +2097,19 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
   g->c.now = round;  // handlers stamp leave / intent times with the round
   if ((uint64_t)g->n_rumors + need > g->max_rumors) {  // the block restarts the ring, next generation
     g->n_rumors = 0;
-    const uint32_t gens = c.rbits >= 32 ? 1u : (uint32_t)((1ull << (32 - c.rbits)) - 1);
-    g->gen = (g->gen + 1) % gens;
+    g->gen = (g->gen + 1) % rumor_generations(c);
+    // this generation reuses the half of the table of generation gen - 2: queued ids of
+    // that generation expire now, before anything reads or re-queues them
+    hipLaunchKernelGGL(expire_kernel, dim3(grid1(c.n_loc * 3, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0,
+                       g->stream, c, g->s, g->gen);
   }
   g->round_slot = g->n_rumors;
   g->round_base = (uint32_t)(((uint64_t)g->gen << c.rbits) | g->round_slot);
   g->round_abase = g->round_base + c.S * c.max_refute;
   g->round_need = (uint32_t)need;
   g->n_rumors += (uint32_t)need;
-  RSF_HIP(hipMemsetAsync(g->s.rumors + g->round_slot, 0, need * sizeof(rsf_rumor), st));
+  const uint32_t round_pidx = g->round_base & c.rmask;  // physical index: generation parity | slot
+  RSF_HIP(hipMemsetAsync(g->s.rumors + round_pidx, 0, need * sizeof(rsf_rumor), st));
   if (g->c.dcap) RSF_HIP(hipMemsetAsync(g->s.dcnt, 0, c.n_loc * 4, st));  // the round's delivery log
   if (n_ml) {
     RSF_HIP(hipMemcpyAsync(g->d_ml, ml, n_ml * sizeof(rsf_ml_event), hipMemcpyHostToDevice, st));
@@ -2047,7 +2129,7 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
 
 int rsf_gossip_rumor_block(rsf_gossip* g, void** p, uint64_t* bytes) {
   if (!g || !p || !bytes) return gerr("null argument");
-  *p = g->s.rumors + g->round_slot;
+  *p = g->s.rumors + (g->round_base & g->c.rmask);
   *bytes = (uint64_t)g->round_need * sizeof(rsf_rumor);
   return RSF_OK;
 }
@@ -2067,7 +2149,7 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local) {
   const uint64_t ng = g->n_groups;
   if (g->round_need)
     hipLaunchKernelGGL(dec_fill_kernel, dim3(grid1(g->round_need)), dim3(256), 0, st, (const rsf_rumor*)g->s.rumors,
-                       g->s.rdec, g->s.rbody, g->s.rgen, g->gen, (uint64_t)g->round_slot, (uint64_t)g->round_need);
+                       g->s.rdec, g->s.rbody, (uint64_t)(g->round_base & c.rmask), (uint64_t)g->round_need);
   hipLaunchKernelGGL(peers_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, c, g->s, round, g->grp_key);
   RSF_HIP(hipGetLastError());
   int rc = sort_pairs(g, g->grp_key, g->grp_key_s, g->grp_id, g->grp_id_s, ng);
@@ -2502,7 +2584,7 @@ int rsf_gossip_dump_buffers(rsf_gossip* g, uint64_t* eb_ltime, uint32_t* eb_cnt,
 
 int rsf_gossip_dump_rumors(rsf_gossip* g, uint32_t first, uint32_t count, rsf_rumor* out) {
   if (!g || (count && !out)) return gerr("null argument");
-  if ((uint64_t)first + count > g->max_rumors) return gerr("rumor range out of bounds");
+  if ((uint64_t)first + count > 2ull * g->max_rumors) return gerr("rumor range out of bounds");
   RSF_HIP(hipSetDevice(g->device));
   RSF_HIP(hipMemcpyAsync(out, g->s.rumors + first, (size_t)count * sizeof(rsf_rumor), hipMemcpyDeviceToHost, g->stream));
   RSF_HIP(hipStreamSynchronize(g->stream));

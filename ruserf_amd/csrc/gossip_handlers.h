@@ -32,7 +32,8 @@ struct GCfg {
   uint32_t S, qcap, ebuf, qbuf, slot_k, fanout, limit, overhead, tx_limit, max_refute, cap_t;
   uint32_t k0, k1;
   uint32_t now;  // time stamped into view entries (leave_time / intent wall time); = the round
-  // rumor ring: max_rumors = 2^rbits slots; a rumor id is generation << rbits | slot
+  // rumor ring: max_rumors = 2^rbits slots per generation; a rumor id is generation << rbits | slot,
+  // stored at id & rmask (rmask = 2^(rbits+1) - 1: two generations resident, by parity)
   uint32_t rbits, rmask;
   uint32_t dcap;  // delivery log entries per member (0: log off)
 };
@@ -56,7 +57,7 @@ struct GState {
   ViewE* view;            // [n_loc][S]
   uint32_t *q_rumor, *q_seq, *q_txlen, *q_next_seq;  // [n_loc][3][qcap], next_seq [n_loc][3]
   uint32_t* q_pruned;     // [n_loc] live queue items dropped by a full queue (memberlist Prune), cumulative
-  uint32_t* q_expired;    // [n_loc] queue items dropped at emission: their rumor slot was recycled
+  uint32_t* q_expired;    // [n_loc] queue items dropped when the rumor ring wrapped onto their generation
   uint64_t* eb_ltime;
   uint32_t* eb_cnt;
   uint64_t* eb_keys;
@@ -64,9 +65,8 @@ struct GState {
   uint32_t* qb_cnt;
   uint32_t* qb_ids;
   rsf_rumor* rumors;
-  uint32_t* rdec;  // per rumor id: its record decoration (subject / kDecQuery / kDecEvent), 4 B
+  uint32_t* rdec;  // per rumor: its record decoration (subject / kDecQuery / kDecEvent), 4 B
   uint4* rbody;    // per rumor id: the rumor without its key (ltime, subject, type, flags, msg_len), 16 B
-  uint32_t* rgen;  // per rumor slot: the generation of the rumor it holds (ids of older generations expired)
   uint4* dlog;     // [n_loc][dcap] user events delivered to the application: ltime | cc << 63, key
   uint32_t* dcnt;  // [n_loc] deliveries since the log was cleared
 };
@@ -185,7 +185,10 @@ __device__ __forceinline__ int h_join_intent(ViewE* e, MRegs& r, uint64_t L, uin
   return f;
 }
 
-// handle_node_leave_intent (base.rs:1409-1528) on a register copy of the view entry
+// handle_node_leave_intent (base.rs:1409-1528) on a register copy of the view entry.
+// DIGEST = false: the caller digests the member events itself from the returned flags
+// (merge_kernel's chain walk, which runs the handlers lane-parallel).
+template <bool DIGEST = true>
 __device__ __forceinline__ int hv_leave_intent(ViewE& v, MRegs& r, uint32_t subj, uint64_t L, bool prune,
                                                uint64_t& refute, uint32_t now) {
   uint8_t state = r.serf_state;
@@ -207,7 +210,7 @@ __device__ __forceinline__ int hv_leave_intent(ViewE& v, MRegs& r, uint32_t subj
     case RSF_STATUS_LEFT: f = RSF_F_REBROADCAST | pf; break;
     case RSF_STATUS_FAILED:
       st = RSF_STATUS_LEFT;
-      r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)kEvLeave << 32) | subj);
+      if (DIGEST) r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)kEvLeave << 32) | subj);
       f = RSF_F_REBROADCAST | RSF_F_MEMBER_EVENT | pf;
       break;
     default: f = 0; break;
@@ -219,7 +222,7 @@ __device__ __forceinline__ int hv_leave_intent(ViewE& v, MRegs& r, uint32_t subj
     // broadcast_timeout + leave_propagate_delay first when the member is Leaving; the
     // round model erases at once.
     v = ViewE{0ull, vmeta(RSF_STATUS_NONE, RSF_KIND_UNKNOWN), 0u};
-    r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)kEvReap << 32) | subj);
+    if (DIGEST) r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)kEvReap << 32) | subj);
   }
   return f;
 }
@@ -356,10 +359,16 @@ __device__ __forceinline__ uint32_t queue_of(uint8_t type) {
 // one; on a full queue the largest item falls off (memberlist Prune), and a new
 // item that would land past the end is itself the pruned one.
 // A full queue loses one live item: counted in q_pruned[l] and flagged (kErrQueue).
+__device__ __forceinline__ void queue_insert_item(const GCfg& c, const GState& s, uint64_t l, uint32_t q,
+                                                  uint32_t rid, uint32_t len, uint32_t seq, MRegs& r);
 __device__ __forceinline__ void queue_insert_serial(const GCfg& c, const GState& s, uint64_t l, uint32_t q,
                                                     uint32_t rid, uint32_t len, MRegs& r) {
-  const uint64_t base = (l * 3 + q) * c.qcap;
   const uint32_t seq = s.q_next_seq[l * 3 + q]++;
+  queue_insert_item(c, s, l, q, rid, len, seq, r);
+}
+__device__ __forceinline__ void queue_insert_item(const GCfg& c, const GState& s, uint64_t l, uint32_t q,
+                                                  uint32_t rid, uint32_t len, uint32_t seq, MRegs& r) {
+  const uint64_t base = (l * 3 + q) * c.qcap;
   const uint64_t newkey = tlq_key(0, len, seq);
   uint32_t cnt = 0, pos = kEmpty;
   while (cnt < c.qcap && s.q_rumor[base + cnt] != kEmpty) {

@@ -83,7 +83,7 @@ class World(C.Structure):
                 ("qb_ltime", P64), ("qb_cnt", P32), ("qb_ids", P32),
                 ("rumors", C.POINTER(Rumor)), ("n_rumors", C.c_uint32), ("cap_rumors", C.c_uint32),
                 ("merges", C.c_uint64), ("sends", C.c_uint64), ("deliveries", C.c_uint64),
-                ("v_time", P32), ("now", C.c_uint32), ("q_pruned", P32), ("q_expired", P32), ("rgen", P32),
+                ("v_time", P32), ("now", C.c_uint32), ("q_pruned", P32), ("q_expired", P32),
                 ("gen", C.c_uint32), ("rbits", C.c_uint32), ("dlog", P64), ("dcnt", P32), ("dcap", C.c_uint32)]
 
 
@@ -198,6 +198,8 @@ def lib():
                                      C.POINTER(Action), C.c_uint32, C.c_int]
     L.orc_world_set_delivery_log.argtypes = [C.POINTER(World), C.c_uint32]
     L.orc_handle_user_event_cc.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint64, C.c_uint64, C.c_int]
+    L.orc_rumor_index.argtypes = [C.POINTER(World), C.c_uint32]
+    L.orc_rumor_index.restype = C.c_uint32
     L.orc_rumor_live.argtypes = [C.POINTER(World), C.c_uint32]
     L.orc_rumor_live.restype = C.c_int
     L.orc_pick_peers.argtypes = [C.c_uint64, C.c_uint32, P8, C.c_uint32, C.c_uint32, C.c_uint32, P32]

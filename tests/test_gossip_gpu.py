@@ -51,8 +51,8 @@ def test_intent_rounds_bit_exact(n, s, rounds, rate, qcap, limit):
 
 def test_rumor_ring_recycles_bit_exact():
     """A rumor ring far smaller than the run: blocks restart the ring with the next
-    generation, and queue items whose slot was recycled expire at their member's next
-    emission, identically to the oracle (churn + flood: intents, events, queries)."""
+    generation, two generations resident; at each wrap the queued ids of generation
+    gen - 2 expire, identically to the oracle (churn + flood: intents, events, queries)."""
     n, rounds = 1200, 40
     subj, acts, ml = W.churn_workload(n, rounds, events_per_round=25, queries_per_round=4, seed=77)
     s = len(subj)

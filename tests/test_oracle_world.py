@@ -38,8 +38,8 @@ def test_threaded_round_identical(kind):
 
 def test_rumor_ring_wraps_and_expires():
     """A ring of 128 slots over 30 rounds: blocks restart at slot 0 with the next
-    generation; ids of an older generation are no longer live and expire from the
-    queues at emission; threaded and sequential rounds agree."""
+    generation; two generations stay resident (by parity), so when the ring wraps the
+    queued ids of generation gen - 2 expire; threaded and sequential rounds agree."""
     n, rounds = 800, 30
     subj, acts, ml = W.churn_workload(n, rounds, events_per_round=20, queries_per_round=3, seed=8)
     s = len(subj)
@@ -53,12 +53,15 @@ def test_rumor_ring_wraps_and_expires():
         H.oracle_round(w4, t, ml[t], acts[t], threads=4)
     H.assert_same(H.world_state(w4), H.world_state(w1), "ring")
     assert w1.rbits == 7 and w1.gen >= 3
-    live_id = (w1.gen << 7) | 0
-    stale_id = ((w1.gen - 1) << 7) | 0
-    assert L.orc_rumor_live(C.byref(w1), live_id) == 1 and L.orc_rumor_live(C.byref(w1), stale_id) == 0
+    live = [((w1.gen - k) << 7) | 5 for k in (0, 1)]
+    stale_id = ((w1.gen - 2) << 7) | 5
+    assert all(L.orc_rumor_live(C.byref(w1), i) == 1 for i in live)
+    assert L.orc_rumor_live(C.byref(w1), stale_id) == 0
+    # generation parity picks the table half
+    assert L.orc_rumor_index(C.byref(w1), live[0]) != L.orc_rumor_index(C.byref(w1), live[1])
     assert O.arr(w1.q_expired, n, np.uint32).sum() > 0
-    # every queued id is of a live generation or will expire at its member's next emission
+    # every queued id is of a live generation
     q = O.arr(w1.q_rumor, n * 3 * cfg.queue_cap, np.uint32)
-    assert np.all(q[q != 0xFFFFFFFF] >> 7 <= w1.gen)
+    assert all(L.orc_rumor_live(C.byref(w1), int(i)) for i in np.unique(q[q != 0xFFFFFFFF]))
     L.orc_world_free(C.byref(w1))
     L.orc_world_free(C.byref(w4))
