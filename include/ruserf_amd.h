@@ -343,6 +343,22 @@ int rsf_gossip_round_merge(rsf_gossip* g, const uint64_t* recv_dev, uint64_t n_r
 int rsf_gossip_round_merge_runs(rsf_gossip* g, const uint64_t* recv_dev, const uint64_t* run_counts,
                                 uint32_t n_runs);
 int rsf_gossip_check_runs(rsf_gossip* g, int* ok);
+/* The exchange without host synchronisation (the multi-GPU bench path): fixed-capacity
+ * buckets, one per destination shard.  rsf_gossip_bucket_buffers allocates (once per
+ * world size) and returns the send and receive buffers, `world` buckets of bucket_bytes
+ * each, device memory.  round_emit_buckets emits straight into the send buckets (each
+ * holds its shard's (sender, peer) groups sorted by receiver: a header with the group
+ * count, the receivers, record counts, rumor ids and record decorations).  The caller
+ * moves bucket w of every rank to rank w (one all-to-all of equal splits, e.g.
+ * ncclAllToAll), concatenated in source-rank order, then round_merge_buckets merges
+ * straight from the received buckets: per receiver its groups of every source in
+ * source-rank order = the canonical (receiver; sender, position) order.  A bucket over
+ * its capacity, or a receiver outside the shard, is recorded and reported by
+ * rsf_gossip_bucket_status (ok = 0 from then on: the rounds since are not valid). */
+int rsf_gossip_bucket_buffers(rsf_gossip* g, uint32_t world, void** send, void** recv, uint64_t* bucket_bytes);
+int rsf_gossip_round_emit_buckets(rsf_gossip* g, uint32_t world);
+int rsf_gossip_round_merge_buckets(rsf_gossip* g, uint32_t world);
+int rsf_gossip_bucket_status(rsf_gossip* g, int* ok);
 
 /* ---- push/pull anti-entropy (SerfDelegate::local_state / merge_remote_state,
  * core/src/serf/delegate.rs:376-554) ---------------------------------------

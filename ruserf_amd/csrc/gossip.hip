@@ -328,7 +328,7 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   if (pmask) {
     const uint32_t npick = (uint32_t)__popcll(pmask);
     const uint32_t rank = (uint32_t)__popcll(pmask & below_mask(lane));
-    if (picked && nrec + rank < c.cap_t) {
+    if (picked && nrec + rank < c.cap_t && stage_val) {
 #if RSF_EMIT_NT
       __builtin_nontemporal_store(Q.r, stage_val + out_base + nrec + rank);
       __builtin_nontemporal_store(Q.dec, stage_dec + out_base + nrec + rank);
@@ -602,6 +602,20 @@ __global__ void __launch_bounds__(256) grp_index_kernel(const uint32_t* __restri
 #define RSF_MERGE_PER_WAVE 8  // merge: 8 receivers per wave measured fastest (4.30 -> 4.06 ms at 2M; 2, 4, 16, 32 between)
 #endif
 
+// Multi-GPU exchange buckets (rsf_gossip_round_emit_buckets): one bucket per destination
+// shard, u32 layout [n_groups, 3 x pad | keys[gcap] | cnt[gcap] | vals[gcap * cap_t] |
+// decs[gcap * cap_t]]; the groups of a bucket are sorted by receiver.  On the receive side
+// the world's buckets arrive back to back in source-rank order = runs.
+constexpr uint32_t kMaxRuns = 8;
+struct Buckets {
+  const uint32_t* base;  // receive buffer (RUNS merge); emission writes through `send`
+  uint32_t* send;        // send buffer (emission into buckets)
+  const uint32_t* wstart;  // emission: per destination shard, its first group in sorted order
+  uint64_t per;            // members per shard
+  uint64_t stride_u32;   // one bucket
+  uint32_t keys_off, cnt_off, vals_off, decs_off, gcap, n_runs;
+};
+
 // a sender's first round trip: the intent queue (the common case; a sorted queue is
 // empty iff its slot 0 is free), the query/event queue heads, the peers and their
 // group slots
@@ -621,9 +635,10 @@ __device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const 
   e.gk = lane < c.fanout ? grp_key[l * c.fanout + lane] : kSentinel;
   e.gs = lane < c.fanout ? slot[l * c.fanout + lane] : 0u;
 }
+template <bool BKT>
 __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_t l, uint32_t lane, EmitIn& e,
                                          uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val,
-                                         uint32_t* __restrict__ out_dec) {
+                                         uint32_t* __restrict__ out_dec, const Buckets& bk) {
   QRegs& Q0 = e.Q0;
   QRegs Q1{kEmpty, 0, 0, kDecQuery}, Q2{kEmpty, 0, 0, kDecEvent};
   const uint64_t pm = __ballot(e.gk != kSentinel);  // peers are a prefix of the fanout slots
@@ -635,17 +650,38 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   uint32_t err = 0;
   // decoration of the intents: their subject slots (subject and type share one 8-B word)
   if (Q0.r != kEmpty) Q0.dec = s.rdec[Q0.r & c.rmask];
+  // buckets: each peer's destination shard and that bucket's first group (same round trip)
+  uint32_t wdst = 0, wfirst = 0;
+  if (BKT && lane < np) {
+    wdst = (uint32_t)(e.gk / bk.per);
+    wfirst = bk.wstart[wdst];
+  }
   if (ne1) q_load(c, s, l, 1, lane, Q1);
   if (ne2) q_load(c, s, l, 2, lane, Q2);
   for (uint32_t j = 0; j < np; ++j) {
     const uint32_t gslot = shfl_u32(e.gs, j);
-    const uint64_t out_base = (uint64_t)gslot * c.cap_t;
+    uint64_t out_base = (uint64_t)gslot * c.cap_t;
+    uint32_t* ov = out_val;
+    uint32_t* od = out_dec;
+    uint32_t* oc = cnt_s + gslot;
+    if (BKT) {  // the group's place in its destination's bucket
+      const uint32_t w = shfl_u32(wdst, j), idx = gslot - shfl_u32(wfirst, j);
+      uint32_t* b = bk.send + (uint64_t)w * bk.stride_u32;
+      if (idx < bk.gcap) {
+        ov = b + bk.vals_off;
+        od = b + bk.decs_off;
+        oc = b + bk.cnt_off + idx;
+        out_base = (uint64_t)idx * c.cap_t;
+      } else {
+        ov = od = oc = nullptr;  // over the bucket capacity: flagged by the bounds kernel
+      }
+    }
     uint32_t nrec = 0;
     int64_t used = 0;
-    used += q_get_broadcasts<true>(c, Q0, lane, (int64_t)c.limit - used, out_val, out_dec, out_base, nrec, err, d0);
-    used += q_get_broadcasts<false>(c, Q1, lane, (int64_t)c.limit - used, out_val, out_dec, out_base, nrec, err, d1);
-    used += q_get_broadcasts<false>(c, Q2, lane, (int64_t)c.limit - used, out_val, out_dec, out_base, nrec, err, d2);
-    if (lane == 0 && nrec) cnt_s[gslot] = min(nrec, c.cap_t);
+    used += q_get_broadcasts<true>(c, Q0, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d0);
+    used += q_get_broadcasts<false>(c, Q1, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d1);
+    used += q_get_broadcasts<false>(c, Q2, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d2);
+    if (lane == 0 && oc && nrec) *oc = min(nrec, c.cap_t);
   }
   if (d0) q_store(c, s, l, 0, lane, Q0, true);
   if (d1) q_store(c, s, l, 1, lane, Q1, true);
@@ -653,9 +689,11 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   if (err && lane == 0) s.err[l] |= err;  // rare: a stage overflow
 }
 
+template <bool BKT>
 __global__ void __launch_bounds__(64 * RSF_EMIT_WPB) emit_kernel(GCfg c, GState s, const uint32_t* __restrict__ grp_key,
                                                    const uint32_t* __restrict__ slot, uint32_t* __restrict__ cnt_s,
-                                                   uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec) {
+                                                   uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec,
+                                                   Buckets bk) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint64_t l = ((uint64_t)xcd_block(blockIdx.x, gridDim.x) * RSF_EMIT_WPB +
                       (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)) * RSF_EMIT_PER_WAVE;
@@ -663,12 +701,12 @@ __global__ void __launch_bounds__(64 * RSF_EMIT_WPB) emit_kernel(GCfg c, GState 
   EmitIn cur, nxt;
   emit_load(c, s, grp_key, slot, l, lane, cur);
   if (RSF_EMIT_PER_WAVE == 1) {
-    emit_run(c, s, l, lane, cur, cnt_s, out_val, out_dec);
+    emit_run<BKT>(c, s, l, lane, cur, cnt_s, out_val, out_dec, bk);
     return;
   }
   for (uint32_t k = 0; k < RSF_EMIT_PER_WAVE; ++k) {
     if (k + 1 < RSF_EMIT_PER_WAVE) emit_load(c, s, grp_key, slot, l + k + 1, lane, nxt);
-    if (l + k < c.n_loc) emit_run(c, s, l + k, lane, cur, cnt_s, out_val, out_dec);
+    if (l + k < c.n_loc) emit_run<BKT>(c, s, l + k, lane, cur, cnt_s, out_val, out_dec, bk);
     cur = nxt;
   }
 }
@@ -799,7 +837,8 @@ __device__ unsigned long long g_merge_prof[8];
 enum : uint32_t {
   kSuStart, kSuEnd, kSuAlive, kSuSeq0, kSuSeq1, kSuSeq2, kSuClock, kSuEClock = kSuClock + 2,
   kSuQClock = kSuEClock + 2, kSuEMin = kSuQClock + 2, kSuQMin = kSuEMin + 2, kSuDigest = kSuQMin + 2,
-  kSuErr = kSuDigest + 2, kSuSerf, kSuSubj, kSuPruned, kSuLanes
+  kSuErr = kSuDigest + 2, kSuSerf, kSuSubj, kSuPruned, kSuRun,  // kSuRun + 2r, + 2r + 1: run r's groups
+  kSuLanes = kSuRun + 2 * kMaxRuns
 };
 // per-lane source: byte address = base + l * mult + off (alive / serf_state: the aligned
 // dword holding the byte)
@@ -809,10 +848,17 @@ struct MSetupLane {
 };
 __device__ __forceinline__ MSetupLane merge_setup_lane(const GCfg& c, const GState& s,
                                                        const uint32_t* __restrict__ seg_start,
-                                                       const uint32_t* __restrict__ seg_end, uint32_t lane) {
+                                                       const uint32_t* __restrict__ seg_end, uint32_t lane,
+                                                       uint32_t n_runs) {
   const char* b = (const char*)seg_start;
   uint32_t mult = 4, off = 0;
   if (lane == kSuEnd) b = (const char*)seg_end;
+  // bucket input: seg_start / seg_end are [run][n_loc] group ranges
+  if (lane >= kSuRun && lane < kSuRun + 2 * n_runs) {
+    const uint32_t r = (lane - kSuRun) >> 1;
+    b = (const char*)((lane - kSuRun) & 1 ? seg_end : seg_start);
+    off = (uint32_t)(r * c.n_loc * 4);
+  }
   if (lane == kSuAlive) b = (const char*)s.alive + c.lo, mult = 1;
   if (lane >= kSuSeq0 && lane <= kSuSeq2) b = (const char*)s.q_next_seq, mult = 12, off = 4 * (lane - kSuSeq0);
   const uint64_t* u64s[6] = {s.clock, s.eclock, s.qclock, s.emin, s.qmin, s.digest};
@@ -828,7 +874,7 @@ __device__ __forceinline__ MSetupLane merge_setup_lane(const GCfg& c, const GSta
 }
 __device__ __forceinline__ uint32_t merge_setup(const MSetupLane& sl, uint64_t l, uint32_t lane) {
   uint32_t v = 0;
-  if (lane < kSuLanes) {
+  if (lane < kSuLanes && sl.base) {
     const uintptr_t a = (uintptr_t)(sl.base + l * sl.mult + sl.off);
     // a global (not flat) load: flat loads also count on lgkmcnt, which every ds_bpermute
     // wait of the current receiver would then drain
@@ -917,13 +963,30 @@ __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, 
 // empty slots of a group are holes (invalid lanes) in an otherwise canonical lane order.
 // Query/event queues are loaded on first need; a queue is written back only if something
 // was inserted.
+template <bool RUNS>
 __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const uint32_t* __restrict__ vals,
                                           const uint32_t* __restrict__ dec, const uint32_t* __restrict__ gcnt,
                                           uint32_t stride, uint64_t l, uint32_t lane, uint32_t su, QLds* ql,
-                                          uint32_t* __restrict__ sbits) {
+                                          uint32_t* __restrict__ sbits, const Buckets& bk) {
   MPROF_T(t_start);
-  const uint32_t st = shfl_u32(su, kSuStart), en = shfl_u32(su, kSuEnd);
-  if (st >= en || (shfl_u32(su, kSuAlive) & 0xFF) == 0) return;
+  uint32_t st = 0, en = 0, total;
+  uint32_t rcum[kMaxRuns + 1], rst[kMaxRuns];  // runs: cumulative slots, first group per run
+  if (RUNS) {
+    rcum[0] = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < kMaxRuns; ++r) {
+      const uint32_t a = r < bk.n_runs ? shfl_u32(su, kSuRun + 2 * r) : 0u;
+      const uint32_t b = r < bk.n_runs ? shfl_u32(su, kSuRun + 2 * r + 1) : 0u;
+      rst[r] = a;
+      rcum[r + 1] = rcum[r] + (b - a) * stride;
+    }
+    total = rcum[kMaxRuns];
+  } else {
+    st = shfl_u32(su, kSuStart);
+    en = shfl_u32(su, kSuEnd);
+    total = st < en ? (en - st) * stride : 0u;
+  }
+  if (total == 0 || (shfl_u32(su, kSuAlive) & 0xFF) == 0) return;
   QRegs Q0{kEmpty, 0, 0};
   q_load(c, s, l, 0, lane, Q0);  // intents are the common case
   bool ld1 = false, ld2 = false, d0 = false, d1 = false, d2 = false;
@@ -942,26 +1005,49 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
   ViewE* vrow = s.view + l * c.S;
   MPROF_T(t_setup);
   MPROF_ADD(0, t_start, t_setup);
-  const uint64_t vs = (uint64_t)st * stride, ve = (uint64_t)en * stride;
-  for (uint64_t base = vs; base < ve; base += kWave) {
+  const uint64_t vs = (uint64_t)st * stride;
+  for (uint32_t vb = 0; vb < total; vb += kWave) {
     MPROF_T(t_c0);
-    const uint32_t cnt = (uint32_t)min((uint64_t)kWave, ve - base);  // lanes in this chunk
-    const uint64_t slot = base + lane;
+    const uint32_t cnt = min((uint32_t)kWave, total - vb);  // lanes in this chunk
     const bool in = lane < cnt;
-    // slot contents and the group's record count in one round trip (holes read stale ids)
-    const uint32_t rid0 = in ? rec_ld(vals + slot) : 0;
-    uint32_t gk = 1, gc = 1;
-    if (gcnt && in) {
-      // group of the slot relative to the receiver's first group: a 32-bit division
-      // (a receiver's slot range is small) instead of a 64-bit one
-      const uint32_t rel = (uint32_t)(base - vs) + lane, gr = rel / stride;
+    const uint32_t vi = vb + lane;  // this lane's slot in the receiver's slot list
+    uint32_t rid0 = 0, dsub0 = kEmpty, gk = 1, gc = 1;
+    if (RUNS) {
+      // the run holding slot v, then its group and place in the group
+      uint32_t r = 0;
+#pragma unroll
+      for (uint32_t q = 1; q < kMaxRuns; ++q) r = vi >= rcum[q] ? q : r;
+      uint32_t cr = 0, sr = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < kMaxRuns; ++q) {
+        cr = q == r ? rcum[q] : cr;
+        sr = q == r ? rst[q] : sr;
+      }
+      const uint32_t rel = vi - cr, gr = rel / stride;
       gk = rel - gr * stride;
-      gc = rec_ld(gcnt + st + gr);
+      const uint64_t g = (uint64_t)sr + gr;
+      const uint32_t* b = bk.base + (uint64_t)r * bk.stride_u32;
+      if (in) {
+        rid0 = rec_ld(b + bk.vals_off + g * stride + gk);
+        dsub0 = rec_ld(b + bk.decs_off + g * stride + gk);
+        gc = rec_ld(b + bk.cnt_off + g);
+      }
+    } else {
+      // slot contents and the group's record count in one round trip (holes read stale ids)
+      const uint64_t slot = vs + vi;
+      rid0 = in ? rec_ld(vals + slot) : 0;
+      if (gcnt && in) {
+        // group of the slot relative to the receiver's first group: a 32-bit division
+        // (a receiver's slot range is small) instead of a 64-bit one
+        const uint32_t gr = vi / stride;
+        gk = vi - gr * stride;
+        gc = rec_ld(gcnt + st + gr);
+      }
+      // decoration (same round trip as the rumor ids): subject of an intent, or the
+      // queue of an event / query; invalid lanes read as neither
+      dsub0 = in ? rec_ld(dec + slot) : kEmpty;
     }
-    // decoration (same round trip as the rumor ids): subject of an intent, or the
-    // queue of an event / query; invalid lanes read as neither
-    const uint32_t dsub0 = in ? rec_ld(dec + slot) : kEmpty;
-    const bool valid = in && (!gcnt || gk < gc);
+    const bool valid = in && (!(RUNS || gcnt) || gk < gc);
     const uint32_t rid = valid ? rid0 : 0;
     const uint32_t dsub = valid ? dsub0 : kEmpty;
     const bool is_view = dsub < kDecViewMax;
@@ -1137,7 +1223,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     }
     MPROF_T(t_c3);
     MPROF_ADD(3, t_c2, t_c3);
-    if (base + kWave < ve) __threadfence_block();  // next chunk's prefetch must see this chunk's view stores
+    if (vb + kWave < total) __threadfence_block();  // next chunk's prefetch must see this chunk's view stores
   }
   MPROF_T(t_st0);
   if (d0) q_store(c, s, l, 0, lane, Q0, true);
@@ -1173,11 +1259,12 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
 #ifndef RSF_MERGE_PERSIST
 #define RSF_MERGE_PERSIST 0  // 1: persistent waves (measured 14% slower than hardware wave dispatch)
 #endif
+template <bool RUNS>
 __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GState s, const uint32_t* __restrict__ vals,
                                                     const uint32_t* __restrict__ dec,
                                                     const uint32_t* __restrict__ seg_start,
                                                     const uint32_t* __restrict__ seg_end,
-                                                    const uint32_t* __restrict__ gcnt, uint32_t stride) {
+                                                    const uint32_t* __restrict__ gcnt, uint32_t stride, Buckets bk) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
   __shared__ QLds qlds[kWavesPerBlock][3];  // query queue, event queue, insert scratch
   __shared__ uint32_t subj_bits[kWavesPerBlock][128];  // chain detection (zero between chunks)
@@ -1189,13 +1276,13 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
                (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   if (!RSF_MERGE_PERSIST) l *= RSF_MERGE_PER_WAVE;
   if (l >= c.n_loc) return;
-  const MSetupLane sl = merge_setup_lane(c, s, seg_start, seg_end, lane);
+  const MSetupLane sl = merge_setup_lane(c, s, seg_start, seg_end, lane, RUNS ? bk.n_runs : 0u);
   uint32_t cur = merge_setup(sl, l, lane);
   if (!RSF_MERGE_PERSIST && RSF_MERGE_PER_WAVE > 1) {
     // every owned receiver's setup is in flight before the first merge starts
     for (uint32_t k = 0; k < RSF_MERGE_PER_WAVE && l + k < c.n_loc; ++k) {
       const uint32_t nxt = k + 1 < RSF_MERGE_PER_WAVE && l + k + 1 < c.n_loc ? merge_setup(sl, l + k + 1, lane) : 0u;
-      merge_one(c, s, vals, dec, gcnt, stride, l + k, lane, cur, ql, sbits);
+      merge_one<RUNS>(c, s, vals, dec, gcnt, stride, l + k, lane, cur, ql, sbits, bk);
       cur = nxt;
     }
     return;
@@ -1205,7 +1292,7 @@ __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GSt
     const bool more = RSF_MERGE_PERSIST && ln < c.n_loc;
     uint32_t nxt = 0;
     if (more) nxt = merge_setup(sl, ln, lane);
-    merge_one(c, s, vals, dec, gcnt, stride, l, lane, cur, ql, sbits);
+    merge_one<RUNS>(c, s, vals, dec, gcnt, stride, l, lane, cur, ql, sbits, bk);
     if (!more) break;
     cur = nxt;
     l = ln;
@@ -1638,8 +1725,84 @@ __global__ void __launch_bounds__(256) expire_kernel(GCfg c, GState s, uint32_t 
   if (x && lane == 0) atomicAdd(s.q_expired + l, x);
 }
 
-__global__ void accumulate_kernel(unsigned long long* counters) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) counters[60] += counters[0];
+// ---- multi-GPU exchange buckets: the sorted groups split by destination shard.
+// bounds: wstart[w] = first sorted group whose receiver is in shard w (sentinel groups,
+// dead senders, sort last); each bucket's header = its group count (overflow flagged).
+__global__ void bucket_bounds_kernel(const uint32_t* __restrict__ key_s, uint64_t n, uint64_t per, uint32_t world,
+                                     uint32_t* __restrict__ wstart, uint32_t* __restrict__ send, uint64_t stride_u32,
+                                     uint32_t gcap, unsigned long long* __restrict__ flags) {
+  const uint32_t w = threadIdx.x;
+  if (w > world) return;
+  auto first_ge = [&](uint64_t target) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) / 2;
+      if ((uint64_t)key_s[mid] < target) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo;
+  };
+  const uint64_t a = first_ge((uint64_t)w * per);
+  wstart[w] = (uint32_t)a;
+  if (w == world) return;
+  const uint64_t b = first_ge((uint64_t)(w + 1) * per), ng = b - a;
+  send[(uint64_t)w * stride_u32] = (uint32_t)(ng < gcap ? ng : gcap);
+  if (ng > gcap) atomicOr(flags, 1ull);
+}
+// every group's key in its bucket and a zero count (emission writes the non-empty ones)
+__global__ void __launch_bounds__(256) bucket_fill_kernel(const uint32_t* __restrict__ key_s, uint64_t n, uint64_t per,
+                                                          const uint32_t* __restrict__ wstart, Buckets bk) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t key = key_s[i];
+  if (key == kSentinel) return;
+  const uint32_t w = (uint32_t)(key / per), idx = (uint32_t)(i - wstart[w]);
+  if (idx >= bk.gcap) return;
+  uint32_t* b = bk.send + (uint64_t)w * bk.stride_u32;
+  b[bk.keys_off + idx] = key;
+  b[bk.cnt_off + idx] = 0u;
+}
+// receive side: per (run r, receiver) the range of its groups in bucket r; the records
+// merged (group counts) summed for the statistics; a receiver outside the shard or an
+// unsorted bucket is flagged
+__global__ void __launch_bounds__(256) bucket_index_kernel(Buckets bk, uint64_t lo, uint64_t n_loc,
+                                                           uint32_t* __restrict__ rstart, uint32_t* __restrict__ rend,
+                                                           unsigned long long* __restrict__ merged,
+                                                           unsigned long long* __restrict__ flags) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t r = (uint32_t)(t / bk.gcap), i = (uint32_t)(t % bk.gcap);
+  uint32_t cnt = 0;
+  if (r < bk.n_runs) {
+    const uint32_t* b = bk.base + (uint64_t)r * bk.stride_u32;
+    const uint32_t ng = b[0];
+    if (i < ng) {
+      const uint32_t key = b[bk.keys_off + i];
+      const uint64_t l = (uint64_t)key - lo;
+      cnt = b[bk.cnt_off + i];
+      if (l >= n_loc || (i > 0 && b[bk.keys_off + i - 1] > key)) {
+        atomicOr(flags, 2ull);
+        cnt = 0;
+      } else {
+        if (i == 0 || b[bk.keys_off + i - 1] != key) rstart[(uint64_t)r * n_loc + l] = i;
+        if (i + 1 == ng || b[bk.keys_off + i + 1] != key) rend[(uint64_t)r * n_loc + l] = i + 1;
+      }
+    }
+  }
+  // block sum of the records, one atomic per block
+  __shared__ uint32_t part[4];
+  uint32_t v = cnt;
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long sum = (unsigned long long)part[0] + part[1] + part[2] + part[3];
+    if (sum) atomicAdd(merged, sum);
+  }
+}
+
+// counters[60] (records merged since creation) += counters[from] (this round's)
+__global__ void accumulate_kernel(unsigned long long* counters, uint32_t from) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) counters[60] += counters[from];
 }
 
 inline unsigned grid1(uint64_t n, unsigned b = 256) { return (unsigned)((n + b - 1) / b); }
@@ -1687,7 +1850,10 @@ struct rsf_gossip {
   int end_bit = 32;
   uint64_t last_sent = 0, last_merged = 0;
   uint32_t cur_round = 0;
-  bool merged_from_stage = true;
+  bool merged_from_stage = true, merged_from_buckets = false;
+  // bucket exchange: send / receive buffers (world buckets each), group ranges per run
+  uint32_t *bkt_send = nullptr, *bkt_recv = nullptr, *d_rstart = nullptr, *d_rend = nullptr, *d_wstart = nullptr;
+  uint32_t bkt_world = 0, bkt_gcap = 0;
   uint64_t total_merged_host = 0;  // multi-GPU merges (n_recv known on host)
   // run-merge tables of rsf_gossip_round_merge_runs: [run_cap][n_loc] u32 x3, [n_loc] u32
   uint32_t *run_start = nullptr, *run_end = nullptr, *run_base = nullptr, *run_total = nullptr;
@@ -1837,7 +2003,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
       return fail(rsf::set_error(RSF_ERR_HIP, "hipcub scan sizing failed"));
     g->grp_scan_bytes = std::max(tb, tr);
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, merge_kernel, kWave * kWavesPerBlock, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, merge_kernel<false>, kWave * kWavesPerBlock, 0) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
       return fail(rsf::set_error(RSF_ERR_HIP, "occupancy query failed"));
     g->merge_blocks = (unsigned)std::max(1, per_cu * cus);
@@ -1901,7 +2067,8 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters, g->rec_dec, g->pp_buf,
                   g->sort_tmp, g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
                   g->scan_tmp, g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
-                  g->grp_slot, g->grp_off, g->stage_dec, g->grp_scan_tmp, s.dlog, s.dcnt};
+                  g->grp_slot, g->grp_off, g->stage_dec, g->grp_scan_tmp, s.dlog, s.dcnt,
+                  g->bkt_send, g->bkt_recv, g->d_rstart, g->d_rend, g->d_wstart};
   for (void* p : ptrs)
     if (p) hipFree(p);
   g->scratch.release();
@@ -2143,7 +2310,9 @@ int rsf_gossip_rumor_block(rsf_gossip* g, void** p, uint64_t* bytes) {
 // local: this context merges its own records (single context): also each receiver's
 // range of groups for merge_kernel.  Otherwise the groups are compacted into one
 // receiver-ordered record stream (packed into send_buf, n_valid) for the exchange.
-static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local) {
+// bucket mode (world > 0): emission straight into the destination shards' buckets
+static Buckets send_buckets(rsf_gossip* g);
+static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t world = 0) {
   const GCfg& c = g->c;
   hipStream_t st = g->stream;
   const uint64_t ng = g->n_groups;
@@ -2162,10 +2331,23 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local) {
   hipLaunchKernelGGL(grp_index_kernel, dim3(grid1(ng)), dim3(256), 0, st, g->grp_key_s, g->grp_id_s, ng, c.lo,
                      g->grp_slot, local ? g->seg_start : nullptr, local ? g->seg_end : nullptr);
   RSF_HIP(hipGetLastError());
+  const dim3 egrid(grid1((c.n_loc + RSF_EMIT_PER_WAVE - 1) / RSF_EMIT_PER_WAVE, RSF_EMIT_WPB));
+  if (world) {
+    const Buckets bk = send_buckets(g);
+    hipLaunchKernelGGL(bucket_bounds_kernel, dim3(1), dim3(64), 0, st, (const uint32_t*)g->grp_key_s, ng, bk.per, world,
+                       g->d_wstart, g->bkt_send, bk.stride_u32, bk.gcap, g->d_counters + 58);
+    hipLaunchKernelGGL(bucket_fill_kernel, dim3(grid1(ng)), dim3(256), 0, st, (const uint32_t*)g->grp_key_s, ng, bk.per,
+                       (const uint32_t*)g->d_wstart, bk);
+    mark(g, 2);
+    hipLaunchKernelGGL(emit_kernel<true>, egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key, g->grp_slot,
+                       g->grp_cnt, g->stage_val, g->stage_dec, bk);
+    RSF_HIP(hipGetLastError());
+    mark(g, 3);
+    return RSF_OK;
+  }
   mark(g, 2);
-  hipLaunchKernelGGL(emit_kernel, dim3(grid1((c.n_loc + RSF_EMIT_PER_WAVE - 1) / RSF_EMIT_PER_WAVE, RSF_EMIT_WPB)),
-                     dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s,
-                     g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec);
+  hipLaunchKernelGGL(emit_kernel<false>, egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key, g->grp_slot,
+                     g->grp_cnt, g->stage_val, g->stage_dec, Buckets{});
   RSF_HIP(hipGetLastError());
   size_t tb = g->grp_scan_bytes;
   if (local) {
@@ -2189,12 +2371,34 @@ static int launch_merge(rsf_gossip* g, const uint32_t* vals, bool grouped = fals
   const unsigned blocks = RSF_MERGE_PERSIST ? std::min<unsigned>(grid1(c.n_loc, kWavesPerBlock), g->merge_blocks)
                                             : grid1((c.n_loc + RSF_MERGE_PER_WAVE - 1) / RSF_MERGE_PER_WAVE,
                                                     kWavesPerBlock);
-  hipLaunchKernelGGL(merge_kernel, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, g->stream,
+  hipLaunchKernelGGL(merge_kernel<false>, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, g->stream,
                      c, g->s, grouped ? g->stage_val : vals, grouped ? g->stage_dec : (const uint32_t*)g->rec_dec,
-                     g->seg_start, g->seg_end, grouped ? g->grp_cnt : nullptr, grouped ? c.cap_t : 1u);
+                     g->seg_start, g->seg_end, grouped ? g->grp_cnt : nullptr, grouped ? c.cap_t : 1u, Buckets{});
   RSF_HIP(hipGetLastError());
   mark(g, 4);
   return RSF_OK;
+}
+
+// ---- bucket exchange (multi-GPU without host synchronisation) -------------------------
+static Buckets bucket_layout(const rsf_gossip* g, uint32_t world) {
+  const GCfg& c = g->c;
+  Buckets b{};
+  b.gcap = g->bkt_gcap;
+  b.keys_off = 4;
+  b.cnt_off = b.keys_off + b.gcap;
+  b.vals_off = b.cnt_off + b.gcap;
+  b.decs_off = b.vals_off + b.gcap * c.cap_t;
+  b.stride_u32 = ((uint64_t)b.decs_off + (uint64_t)b.gcap * c.cap_t + 63) & ~63ull;  // 256-B aligned buckets
+  b.per = world ? c.N / world : c.N;
+  b.n_runs = world;
+  return b;
+}
+static Buckets send_buckets(rsf_gossip* g) {
+  Buckets b = bucket_layout(g, g->bkt_world);
+  b.send = g->bkt_send;
+  b.wstart = g->d_wstart;
+  b.base = g->bkt_recv;
+  return b;
 }
 
 static int segment_and_merge(rsf_gossip* g, const uint32_t* keys, const uint32_t* vals, uint64_t n) {
@@ -2219,8 +2423,86 @@ int rsf_gossip_round(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml, uint
   if (rc) return rc;
   if ((rc = emit_and_sort(g, round, true))) return rc;
   g->merged_from_stage = true;
-  hipLaunchKernelGGL(accumulate_kernel, dim3(1), dim3(64), 0, g->stream, g->d_counters);
+  g->merged_from_buckets = false;
+  hipLaunchKernelGGL(accumulate_kernel, dim3(1), dim3(64), 0, g->stream, g->d_counters, 0u);
   return launch_merge(g, nullptr, true);
+}
+
+int rsf_gossip_bucket_buffers(rsf_gossip* g, uint32_t world, void** send, void** recv, uint64_t* bucket_bytes) {
+  if (!g || !send || !recv || !bucket_bytes || world == 0 || world > kMaxRuns) return gerr("bad argument");
+  const GCfg& c = g->c;
+  if (c.N % world || c.n_loc != c.N / world) return gerr("shards must be equal contiguous ranges of n_members");
+  if (world != g->bkt_world) {
+    RSF_HIP(hipSetDevice(g->device));
+    RSF_HIP(hipStreamSynchronize(g->stream));
+    for (void* p : {(void*)g->bkt_send, (void*)g->bkt_recv, (void*)g->d_rstart, (void*)g->d_rend})
+      if (p) hipFree(p);
+    g->bkt_send = g->bkt_recv = g->d_rstart = g->d_rend = nullptr;
+    g->bkt_world = 0;
+    // groups per destination: n_loc * fanout / world for uniform peers; the capacity holds
+    // 1/8 more plus 4096 (overflow is flagged, rsf_gossip_bucket_status)
+    const uint64_t expect = (c.n_loc * c.fanout + world - 1) / world;
+    const uint64_t gcap = std::min<uint64_t>(expect + expect / 8 + 4096, c.n_loc * c.fanout);
+    g->bkt_gcap = (uint32_t)gcap;
+    const Buckets b = bucket_layout(g, world);
+    const size_t bytes = (size_t)b.stride_u32 * 4 * world;
+    int rc;
+    if ((rc = rsf::dmalloc((void**)&g->bkt_send, bytes)) || (rc = rsf::dmalloc((void**)&g->bkt_recv, bytes)) ||
+        (rc = rsf::dmalloc((void**)&g->d_rstart, (size_t)world * c.n_loc * 4)) ||
+        (rc = rsf::dmalloc((void**)&g->d_rend, (size_t)world * c.n_loc * 4)))
+      return rc;
+    if (!g->d_wstart && (rc = rsf::dmalloc((void**)&g->d_wstart, (kMaxRuns + 1) * 4))) return rc;
+    RSF_HIP(hipMemset(g->bkt_send, 0, bytes));
+    RSF_HIP(hipMemset(g->bkt_recv, 0, bytes));
+    g->bkt_world = world;
+  }
+  *send = g->bkt_send;
+  *recv = g->bkt_recv;
+  *bucket_bytes = bucket_layout(g, world).stride_u32 * 4;
+  return RSF_OK;
+}
+
+int rsf_gossip_round_emit_buckets(rsf_gossip* g, uint32_t world) {
+  if (!g || world == 0 || world != g->bkt_world) return gerr("call rsf_gossip_bucket_buffers(world) first");
+  RSF_HIP(hipSetDevice(g->device));
+  int rc = emit_and_sort(g, g->cur_round, false, world);
+  if (rc) return rc;
+  g->merged_from_stage = false;
+  g->merged_from_buckets = true;
+  return RSF_OK;
+}
+
+int rsf_gossip_round_merge_buckets(rsf_gossip* g, uint32_t world) {
+  if (!g || world == 0 || world != g->bkt_world) return gerr("call rsf_gossip_bucket_buffers(world) first");
+  const GCfg& c = g->c;
+  RSF_HIP(hipSetDevice(g->device));
+  hipStream_t st = g->stream;
+  const Buckets bk = send_buckets(g);
+  RSF_HIP(hipMemsetAsync(g->d_rstart, 0, (size_t)world * c.n_loc * 4, st));
+  RSF_HIP(hipMemsetAsync(g->d_rend, 0, (size_t)world * c.n_loc * 4, st));
+  RSF_HIP(hipMemsetAsync(g->d_counters + 57, 0, 8, st));
+  hipLaunchKernelGGL(bucket_index_kernel, dim3(grid1((uint64_t)world * bk.gcap)), dim3(256), 0, st, bk, c.lo, c.n_loc,
+                     g->d_rstart, g->d_rend, g->d_counters + 57, g->d_counters + 58);
+  hipLaunchKernelGGL(accumulate_kernel, dim3(1), dim3(64), 0, st, g->d_counters, 57u);
+  if (g->profiling && g->prof_rounds < rsf_gossip::kMaxProfRounds)
+    hipEventRecord(g->ev[g->prof_rounds][3], g->stream);  // exchange time lands in the sort slot
+  const unsigned blocks = grid1((c.n_loc + RSF_MERGE_PER_WAVE - 1) / RSF_MERGE_PER_WAVE, kWavesPerBlock);
+  hipLaunchKernelGGL(merge_kernel<true>, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, st, c, g->s,
+                     (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)g->d_rstart,
+                     (const uint32_t*)g->d_rend, (const uint32_t*)nullptr, c.cap_t, bk);
+  RSF_HIP(hipGetLastError());
+  mark(g, 4);
+  return RSF_OK;
+}
+
+int rsf_gossip_bucket_status(rsf_gossip* g, int* ok) {
+  if (!g || !ok) return gerr("null argument");
+  unsigned long long f = 0;
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemcpyAsync(&f, g->d_counters + 58, 8, hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  *ok = f == 0;
+  return RSF_OK;
 }
 
 int rsf_gossip_round_emit(rsf_gossip* g, uint32_t world, uint64_t* send_counts) {
@@ -2240,6 +2522,7 @@ int rsf_gossip_round_emit(rsf_gossip* g, uint32_t world, uint64_t* send_counts) 
   RSF_HIP(hipStreamSynchronize(st));
   for (uint32_t w = 0; w < world; ++w) send_counts[w] = b[1 + w + 1] - b[1 + w];
   g->merged_from_stage = false;
+  g->merged_from_buckets = false;
   return RSF_OK;
 }
 
@@ -2647,6 +2930,13 @@ int rsf_gossip_last_round_stats(rsf_gossip* g, uint64_t* sent, uint64_t* merged)
   RSF_HIP(hipSetDevice(g->device));
   RSF_HIP(hipMemcpyAsync(&nv, g->d_counters, 8, hipMemcpyDeviceToHost, g->stream));
   RSF_HIP(hipStreamSynchronize(g->stream));
+  if (g->merged_from_buckets) {  // bucket exchange: this shard's merged records; emission is not summed
+    RSF_HIP(hipMemcpyAsync(&nv, g->d_counters + 57, 8, hipMemcpyDeviceToHost, g->stream));
+    RSF_HIP(hipStreamSynchronize(g->stream));
+    if (sent) *sent = 0;
+    if (merged) *merged = nv;
+    return RSF_OK;
+  }
   if (sent) *sent = nv;
   if (merged) *merged = g->merged_from_stage ? nv : g->last_merged;
   return RSF_OK;

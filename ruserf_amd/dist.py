@@ -7,19 +7,23 @@ Per round:
                      the round is owned by exactly one shard
   2. all-reduce    — SUM of the round's rumor block (non-owners hold zeros), so
                      every shard can resolve every rumor id it will receive
-  3. round_emit    — peer draw + stable sort of the record groups by global receiver,
-                     emission in that order, compaction into one stream; the sorted
-                     stream is already grouped by destination shard
-  4. all-to-all    — record counts, then the packed (receiver << 32 | rumor)
-                     records; received chunks are concatenated in source-rank
-                     order = ascending sender id
-  5. round_merge_runs — the received runs (one per source, each receiver-sorted)
-                     are interleaved into (receiver, source rank, position) order by
-                     counts + scan + an ordered scatter — no second sort — which is
-                     the same canonical order as on one GPU
+  3. exchange, by default through fixed-capacity BUCKETS (no host synchronisation):
+       round_emit_buckets  — peer draw, stable sort of the (sender, peer) groups by
+                             global receiver, emission straight into one bucket per
+                             destination shard
+       all-to-all          — equal splits: bucket w of every rank goes to rank w,
+                             concatenated in source-rank order
+       round_merge_buckets — per receiver, its groups of every source in source-rank
+                             order = the canonical (receiver; sender, position) order,
+                             merged straight from the received buckets
+     Bucket overflow (a destination receiving far more groups than the uniform share)
+     is recorded on the device and checked by `check()`.
+     The counts exchange (world > 8, or exchange="counts"): round_emit compacts the
+     records into one receiver-sorted stream, the counts go through an all-to-all and
+     the host, then the records, and round_merge_runs rebuilds the canonical order.
 
-The driver is generic over the engine object (`GossipEngine` on HIP; the
-gloo tests substitute a CPU stand-in that exercises only the routing).
+The driver is generic over the engine object (`GossipEngine` on HIP; the gloo
+tests substitute a CPU stand-in that exercises only the routing).
 """
 import dataclasses
 
@@ -28,6 +32,8 @@ import torch
 import torch.distributed as dist
 
 from .gossip import GossipConfig, GossipEngine
+
+MAX_BUCKET_WORLD = 8  # kMaxRuns in csrc/gossip.hip
 
 
 class CudaArray:
@@ -47,22 +53,40 @@ def hbm_tensor(ptr, n, typestr="<i8"):
 class EngineBuffers:
     """torch views of a GossipEngine's exchange buffers."""
 
-    def __init__(self, eng: GossipEngine):
+    def __init__(self, eng: GossipEngine, world=1, buckets=True):
         self.eng = eng
-        ptr, cap = eng.send_buffer()
-        self.send = hbm_tensor(ptr, cap)
-        self.recv = torch.empty(cap, dtype=torch.int64, device="cuda")
+        self.world = world
+        self.buckets = buckets
+        if buckets:
+            sp, rp, bb = eng.bucket_buffers(world)
+            self.bucket_words = bb // 4
+            self.send = hbm_tensor(sp, world * self.bucket_words, "<i4")
+            self.recv = hbm_tensor(rp, world * self.bucket_words, "<i4")
+        else:
+            ptr, cap = eng.send_buffer()
+            self.send = hbm_tensor(ptr, cap)
+            self.recv = torch.empty(cap, dtype=torch.int64, device="cuda")
 
     def rumor_block(self):
         ptr, nbytes = self.eng.rumor_block()
         return hbm_tensor(ptr, nbytes // 8)
 
-    def merge(self, n_recv, run_counts):
-        self.eng.round_merge_runs(self.recv.data_ptr(), run_counts)
+    def emit(self):
+        self.eng.round_emit_buckets(self.world)
+
+    def merge(self, n_recv=None, run_counts=None):
+        if self.buckets:
+            self.eng.round_merge_buckets(self.world)
+        else:
+            self.eng.round_merge_runs(self.recv.data_ptr(), run_counts)
+
+    def ok(self):
+        return self.eng.bucket_ok() if self.buckets else self.eng.runs_ok()
 
 
 class ShardedGossip:
-    def __init__(self, cfg: GossipConfig, rank, world, device=0, engine=None, buffers=None, group=None):
+    def __init__(self, cfg: GossipConfig, rank, world, device=0, engine=None, buffers=None, group=None,
+                 exchange="buckets"):
         if cfg.n_members % world:
             raise ValueError("n_members must divide evenly over the world")
         per = cfg.n_members // world
@@ -72,7 +96,9 @@ class ShardedGossip:
             engine = GossipEngine(dataclasses.replace(cfg, shard=self.shard), device)
             engine.set_stream(torch.cuda.current_stream().cuda_stream)
         self.eng = engine
-        self.buf = buffers if buffers is not None else EngineBuffers(engine)
+        want = exchange == "buckets" and world <= MAX_BUCKET_WORLD
+        self.buf = buffers if buffers is not None else EngineBuffers(engine, world, want)
+        self.buckets = getattr(self.buf, "buckets", False)
         self.dev = self.buf.recv.device
         self.last_in = 0
         # RCCL ("nccl") moves HBM directly; gloo (the CPU rehearsal backend: several ranks
@@ -103,6 +129,11 @@ class ShardedGossip:
         blk = buf.rumor_block()
         if blk.numel():
             self._all_reduce(blk)
+        if self.buckets:
+            buf.emit()
+            self._all_to_all(buf.recv, buf.send)  # equal splits: one bucket per rank
+            buf.merge()
+            return None
         counts = eng.round_emit(self.world)
         send_counts = torch.from_numpy(counts.astype(np.int64)).to(self.dev)
         recv_counts = torch.empty_like(send_counts)
@@ -115,3 +146,8 @@ class ShardedGossip:
         buf.merge(n_in, rc)
         self.last_in = n_in
         return n_out, n_in
+
+    def check(self):
+        """True if no exchange capacity was exceeded and every record reached its shard
+        (synchronises; call between rounds when validating, and after a timed run)."""
+        return self.buf.ok()

@@ -197,6 +197,24 @@ class GossipEngine:
         rc = np.ascontiguousarray(run_counts, dtype=np.uint64)
         check(lib().rsf_gossip_round_merge_runs(self._h, C.c_void_p(recv_ptr), ptr(rc, C.c_uint64), len(rc)))
 
+    # ---- the exchange without host synchronisation: fixed-capacity buckets per destination
+    def bucket_buffers(self, world):
+        """(send ptr, recv ptr, bucket bytes): `world` buckets each, device memory"""
+        s, r, b = C.c_void_p(), C.c_void_p(), C.c_uint64()
+        check(lib().rsf_gossip_bucket_buffers(self._h, world, C.byref(s), C.byref(r), C.byref(b)))
+        return s.value, r.value, b.value
+
+    def round_emit_buckets(self, world):
+        check(lib().rsf_gossip_round_emit_buckets(self._h, world))
+
+    def round_merge_buckets(self, world):
+        check(lib().rsf_gossip_round_merge_buckets(self._h, world))
+
+    def bucket_ok(self):
+        ok = C.c_int()
+        check(lib().rsf_gossip_bucket_status(self._h, C.byref(ok)))
+        return bool(ok.value)
+
     def runs_ok(self):
         ok = C.c_int()
         check(lib().rsf_gossip_check_runs(self._h, C.byref(ok)))

@@ -123,3 +123,68 @@ def test_sharded_round_routing_gloo():
             for rcv in np.unique(keys):
                 sel = senders[keys[order] == rcv]
                 assert np.all(np.diff(sel) >= 0)
+
+
+class FakeBucketBuffers:
+    """Bucket exchange stand-in: every rank fills bucket w with (src, w, i) words; the
+    merge records what arrived (must be each source's bucket for this rank, in
+    source-rank order)."""
+
+    def __init__(self, rank, words=16):
+        self.rank, self.words, self.buckets = rank, words, True
+        self.block = torch.zeros(12, dtype=torch.int64)
+        self.send = torch.zeros(WORLD * words, dtype=torch.int32)
+        self.recv = torch.zeros(WORLD * words, dtype=torch.int32)
+        self.received = []
+
+    def rumor_block(self):
+        return self.block
+
+    def emit(self):
+        for w in range(WORLD):
+            self.send[w * self.words:(w + 1) * self.words] = torch.tensor(
+                [1000 * self.rank + 100 * w + i for i in range(self.words)], dtype=torch.int32)
+
+    def merge(self, n_recv=None, run_counts=None):
+        self.received.append(self.recv.clone().numpy())
+
+    def ok(self):
+        return True
+
+
+class FakeBeginEngine:
+    def round_begin(self, t, ml, acts):
+        pass
+
+
+def _worker_buckets(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    from ruserf_amd.dist import ShardedGossip
+    from ruserf_amd.gossip import GossipConfig
+    buf = FakeBucketBuffers(rank)
+    sg = ShardedGossip(GossipConfig(n_members=N, n_subjects=4), rank, WORLD, engine=FakeBeginEngine(), buffers=buf)
+    assert sg.buckets
+    sg.round(0)
+    assert sg.check()
+    q.put((rank, buf.received[-1]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_round_buckets_gloo():
+    """The bucket exchange: one all-to-all of equal splits, no host-side counts; rank r
+    receives bucket r of every source, in source-rank order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + (os.getpid() % 2000)
+    procs = [ctx.Process(target=_worker_buckets, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(WORLD))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank in range(WORLD):
+        want = np.concatenate([[1000 * src + 100 * rank + i for i in range(16)] for src in range(WORLD)])
+        assert np.array_equal(res[rank], want.astype(np.int32))

@@ -39,6 +39,7 @@ def _worker(rank, port, q):
     for t in range(ROUNDS):
         sg.round(t, ml[t], acts[t])
     torch.cuda.synchronize()
+    assert sg.buckets and sg.check()
     st = H.normalize_queues(H.engine_state(sg.eng))
     q.put((rank, {k: np.asarray(v) for k, v in st.items()}))
     dist.barrier()
@@ -71,7 +72,7 @@ def test_two_ranks_gloo_equal_one_context():
     one.close()
 
 
-def _worker_rccl(port, q):
+def _worker_rccl(port, q, exchange="buckets"):
     """ShardedGossip over RCCL ("nccl") with one rank: the exact collectives, stream
     ordering and zero-copy engine buffers of the driver's multi-GPU bench."""
     import torch.distributed as dist
@@ -82,26 +83,28 @@ def _worker_rccl(port, q):
     from ruserf_amd import workload as W
     from ruserf_amd.dist import ShardedGossip
     cfg, subj, acts, ml = _cfg()
-    sg = ShardedGossip(cfg, 0, 1, device=0)
+    sg = ShardedGossip(cfg, 0, 1, device=0, exchange=exchange)
     assert not sg.stage  # RCCL moves HBM directly
     sg.eng.set_subjects(subj)
     sg.eng.init_views(*W.initial_views(len(subj)))
     for t in range(ROUNDS):
         sg.round(t, ml[t], acts[t])
     torch.cuda.synchronize()
+    assert sg.buckets == (exchange == "buckets") and sg.check()
     st = H.normalize_queues(H.engine_state(sg.eng))
     q.put({k: np.asarray(v) for k, v in st.items()})
     sg.eng.close()
     dist.destroy_process_group()
 
 
-def test_one_rank_rccl_equal_one_context():
+@pytest.mark.parametrize("exchange", ["buckets", "counts"])
+def test_one_rank_rccl_equal_one_context(exchange):
     from ruserf_amd import gossip as G
     from ruserf_amd import workload as W
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29400 + os.getpid() % 1000
-    p = ctx.Process(target=_worker_rccl, args=(port, q))
+    p = ctx.Process(target=_worker_rccl, args=(port, q, exchange))
     p.start()
     got = q.get(timeout=300)
     p.join(timeout=60)

@@ -245,7 +245,7 @@ def test_large_round_properties():
     assert np.array_equal(digests[0][0], digests[1][0]) and digests[0][1] == digests[1][1]
 
 
-@pytest.mark.parametrize("runs", [False, True, "with_empty_runs"])
+@pytest.mark.parametrize("runs", [False, True, "with_empty_runs", "buckets"])
 def test_two_shards_equal_one_context(runs):
     """The multi-GPU split (round_begin / rumor-block sum / round_emit /
     all-to-all / round_merge or round_merge_runs) with two shard contexts on one
@@ -277,6 +277,27 @@ def test_two_shards_equal_one_context(runs):
         total = blocks[0] + blocks[1]
         for b in blocks:
             b.copy_(total)
+        if runs == "buckets":  # fixed-capacity buckets, the all-to-all done by hand
+            bufs = [e.bucket_buffers(2) for e in shards]
+            words = bufs[0][2] // 4
+            for e in shards:
+                e.round_emit_buckets(2)
+            stream.synchronize()
+            for dst, e in enumerate(shards):
+                recv = hbm_tensor(bufs[dst][1], 2 * words, "<i4")
+                for src in range(2):
+                    send = hbm_tensor(bufs[src][0], 2 * words, "<i4")
+                    recv[src * words:(src + 1) * words].copy_(send[dst * words:(dst + 1) * words])
+            stream.synchronize()
+            for e in shards:
+                e.round_merge_buckets(2)
+            stream.synchronize()
+            assert all(e.bucket_ok() for e in shards)
+            full = H.normalize_queues(H.engine_state(one))
+            halves = [H.normalize_queues(H.engine_state(e)) for e in shards]
+            for k in full:
+                assert np.array_equal(np.concatenate([halves[0][k], halves[1][k]]), full[k]), (t, k)
+            continue
         counts = [e.round_emit(2) for e in shards]
         sends = [hbm_tensor(e.send_buffer()[0], int(c.sum())) for e, c in zip(shards, counts)]
         for dst, e in enumerate(shards):
