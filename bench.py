@@ -114,13 +114,21 @@ def run_vivaldi(args, rank, world):
     table = None
 
     R = max(1, args.refresh_every)
+    # N > 1, R = 1: the targeted exchange (only the rows of this round's remote peers,
+    # fetched from their owners before the round); R > 1 or --vivaldi-exchange allgather:
+    # an all-gather of the table after every R-th round
+    targeted = world > 1 and R == 1 and args.vivaldi_exchange == "targeted"
+    sv = None
+    if targeted:
+        from ruserf_amd.dist import ShardedVivaldi
+        sv = ShardedVivaldi(g, rank, world)
 
     def refresh(r):
         # all-gather of the coordinate table (peers read last round's rows).  With R > 1
         # (R = 8) the table is refreshed after every R-th round only, so
         # rows of other shards are up to R rounds old -- the reference reads a peer's
         # coordinate from its last ack, which is as stale as the probe schedule makes it.
-        if world == 1 or (r + 1) % R:
+        if world == 1 or targeted or (r + 1) % R:
             return
         ptr, stride = g.table_ptr()
         full = torch.as_tensor(CudaArray(ptr, (n * stride,), "<f8"), device="cuda")
@@ -153,7 +161,12 @@ def run_vivaldi(args, rank, world):
         read_ptr[0] = g.table_ptr()[0]
         g.observe(r % 16, peer[r].data_ptr(), rtt[r].data_ptr(), None, r)
 
+    def fetch(r):
+        if targeted:
+            sv.fetch(peer[r].data_ptr())
+
     for _ in range(args.warmup):
+        fetch(step[0])
         observe(step[0])
         refresh(step[0])
         step[0] += 1
@@ -164,6 +177,7 @@ def run_vivaldi(args, rank, world):
     t0 = time.perf_counter()
     kernel_ms = []
     for i in range(args.steps):
+        fetch(step[0])
         evs[i][0].record(stream)
         observe(step[0])
         evs[i][1].record(stream)
@@ -174,6 +188,8 @@ def run_vivaldi(args, rank, world):
     wall = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in evs]
     wall = max_over_ranks(wall, world)
+    if targeted and not sv.check():
+        raise RuntimeError("vivaldi exchange: a request bucket overflowed")
     avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
     updates = per * world * args.steps
     value = updates / wall
@@ -186,7 +202,9 @@ def run_vivaldi(args, rank, world):
                                f"latency filter F=3, adjustment window W=20, 16 neighbours/member probed round-robin, "
                                f"probe inputs (peer, rtt) pre-generated in HBM",
                    "members": n, "members_per_gpu": per, "parallelism": f"members sharded x{world}",
-                   "table_refresh_every_rounds": R},
+                   "table_refresh_every_rounds": R,
+                   "exchange": ("targeted peer rows" if targeted else f"table all-gather every {R} rounds")
+                   if world > 1 else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "vivaldi_observe_pipe_kernel<3>", "bytes_per_unit": VIVALDI_BYTES,
@@ -252,6 +270,8 @@ def main():
     ap.add_argument("--no-vivaldi", action="store_true", help="gossip: skip the Vivaldi leg of the line")
     ap.add_argument("--refresh-every", type=int, default=1,
                     help="vivaldi, N>1: all-gather the coordinate table after every R-th round (C5: 1 and 8)")
+    ap.add_argument("--vivaldi-exchange", choices=["targeted", "allgather"], default="targeted",
+                    help="vivaldi, N>1, R=1: fetch only the round's remote peer rows, or all-gather the table")
     args = ap.parse_args()
     rank, world, local = env_rank()
     if world != args.gpus and world == 1 and args.gpus > 1:

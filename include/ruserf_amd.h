@@ -171,6 +171,27 @@ int rsf_vivaldi_observe_acks(rsf_vivaldi* v, const uint32_t* member, const uint3
  * this shard's slice, for an all-gather between rounds on multi-GPU runs. */
 int rsf_vivaldi_table(rsf_vivaldi* v, double** table_out, uint64_t* row_stride_out);
 
+/* Targeted peer-row exchange (multi-GPU): per round each shard fetches
+ * only the rows of its members' remote peers from their owners, in place of a full-table
+ * all-gather.  Shards are equal contiguous ranges.  Buffers are fixed-capacity buckets,
+ * one per shard (device memory, allocated once per world size):
+ *   req_send / req_recv : world buckets of req_bucket_bytes (u32 count + peer ids)
+ *   rep_send / rep_recv : world buckets of rep_bucket_bytes (rows, row_stride doubles)
+ * A round: exchange_requests(peer) -> all-to-all req_send -> req_recv (equal splits) ->
+ * exchange_serve (copies the requested rows of this shard's current table) ->
+ * all-to-all rep_send -> rep_recv -> exchange_apply (writes each row into this shard's
+ * current table at its peer's place) -> rsf_vivaldi_observe.  Capacity overflow or a
+ * request for a row the shard does not own is reported by exchange_status (ok = 0). */
+typedef struct rsf_vivaldi_xbufs {
+  void *req_send, *req_recv, *rep_send, *rep_recv;
+  uint64_t req_bucket_bytes, rep_bucket_bytes;
+} rsf_vivaldi_xbufs;
+int rsf_vivaldi_exchange_buffers(rsf_vivaldi* v, uint32_t world, rsf_vivaldi_xbufs* out);
+int rsf_vivaldi_exchange_requests(rsf_vivaldi* v, uint32_t world, const uint32_t* peer);
+int rsf_vivaldi_exchange_serve(rsf_vivaldi* v, uint32_t world);
+int rsf_vivaldi_exchange_apply(rsf_vivaldi* v, uint32_t world);
+int rsf_vivaldi_exchange_status(rsf_vivaldi* v, int* ok);
+
 /* Ground truth of the synthetic network (for convergence reporting). */
 int rsf_vivaldi_true_rtt_ns(rsf_vivaldi* v, uint32_t a, uint32_t b, uint64_t* ns_out);
 

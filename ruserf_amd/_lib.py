@@ -28,6 +28,11 @@ class EngineError(RuntimeError):
         self.code = code
 
 
+class RsfVivaldiXbufs(C.Structure):
+    _fields_ = [("req_send", C.c_void_p), ("req_recv", C.c_void_p), ("rep_send", C.c_void_p),
+                ("rep_recv", C.c_void_p), ("req_bucket_bytes", C.c_uint64), ("rep_bucket_bytes", C.c_uint64)]
+
+
 class RsfCoordOpts(C.Structure):
     _fields_ = [("dimensionality", C.c_uint32), ("adjustment_window_size", C.c_uint32),
                 ("latency_filter_size", C.c_uint32), ("_reserved", C.c_uint32),
@@ -100,6 +105,11 @@ def lib():
     _sig(L, "rsf_vivaldi_observe", i, [VP, C.c_uint32, VP, VP, VP, C.c_uint32])
     _sig(L, "rsf_vivaldi_table", i, [VP, C.POINTER(VP), P64])
     _sig(L, "rsf_vivaldi_true_rtt_ns", i, [VP, C.c_uint32, C.c_uint32, P64])
+    _sig(L, "rsf_vivaldi_exchange_buffers", i, [VP, C.c_uint32, C.POINTER(RsfVivaldiXbufs)])
+    _sig(L, "rsf_vivaldi_exchange_requests", i, [VP, C.c_uint32, VP])
+    _sig(L, "rsf_vivaldi_exchange_serve", i, [VP, C.c_uint32])
+    _sig(L, "rsf_vivaldi_exchange_apply", i, [VP, C.c_uint32])
+    _sig(L, "rsf_vivaldi_exchange_status", i, [VP, C.POINTER(C.c_int)])
     try:
         from . import _gossip_sigs
         _gossip_sigs.declare(L)

@@ -258,6 +258,28 @@ class CoordinateClients:
         check(lib().rsf_vivaldi_table(self._h, C.byref(p), C.byref(s)))
         return p.value, s.value
 
+    # ---- targeted peer-row exchange (multi-GPU; see dist.ShardedVivaldi)
+    def exchange_buffers(self, world):
+        """Device pointers + bucket sizes of the request / reply buckets for `world` shards."""
+        from ._lib import RsfVivaldiXbufs
+        x = RsfVivaldiXbufs()
+        check(lib().rsf_vivaldi_exchange_buffers(self._h, world, C.byref(x)))
+        return {k: getattr(x, k) for k, _ in RsfVivaldiXbufs._fields_}
+
+    def exchange_requests(self, world, peer_ptr):
+        check(lib().rsf_vivaldi_exchange_requests(self._h, world, C.c_void_p(peer_ptr)))
+
+    def exchange_serve(self, world):
+        check(lib().rsf_vivaldi_exchange_serve(self._h, world))
+
+    def exchange_apply(self, world):
+        check(lib().rsf_vivaldi_exchange_apply(self._h, world))
+
+    def exchange_ok(self):
+        ok = C.c_int()
+        check(lib().rsf_vivaldi_exchange_status(self._h, C.byref(ok)))
+        return bool(ok.value)
+
     def true_rtt_ns(self, a, b):
         o = C.c_uint64()
         check(lib().rsf_vivaldi_true_rtt_ns(self._h, a, b, C.byref(o)))

@@ -884,9 +884,72 @@ struct rsf_vivaldi {
   uint64_t* probe_rtt = nullptr;
   // batch staging (device)
   DeviceScratch scratch;
+  // targeted peer-row exchange (multi-GPU): request buckets (u32: [count, 3 x pad, ids[cap]])
+  // and reply buckets (cap rows of `stride` doubles), world of each, send and receive
+  uint32_t xw = 0, xcap = 0;
+  uint64_t req_words = 0, rep_doubles = 0;
+  uint32_t *req_send = nullptr, *req_recv = nullptr, *xcnt = nullptr;
+  double *rep_send = nullptr, *rep_recv = nullptr;
+  unsigned long long* xflags = nullptr;
 };
 
 static int set_err_args(const char* m) { return rsf::set_error(RSF_ERR_ARG, m); }
+
+// ---- targeted peer-row exchange: each shard asks the owners for the rows
+// of this round's remote peers only, instead of all-gathering the whole table.
+// requests: one thread per shard member whose peer lives on another shard
+__global__ void __launch_bounds__(256) xreq_pack_kernel(const uint32_t* __restrict__ peer, uint64_t lo, uint64_t shard_n,
+                                                        uint64_t per, uint32_t* __restrict__ req, uint64_t req_words,
+                                                        uint32_t cap, uint32_t* __restrict__ cnt,
+                                                        unsigned long long* __restrict__ flags) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= shard_n) return;
+  const uint32_t p = peer[i];
+  if ((uint64_t)p - lo < shard_n) return;  // own shard: the row is local
+  const uint32_t w = (uint32_t)(p / per);
+  const uint32_t k = atomicAdd(cnt + w, 1u);
+  if (k < cap) req[(uint64_t)w * req_words + 4 + k] = p;
+  else atomicOr(flags, 1ull);
+}
+__global__ void xreq_header_kernel(uint32_t* __restrict__ req, uint64_t req_words, const uint32_t* __restrict__ cnt,
+                                   uint32_t world, uint32_t cap) {
+  const uint32_t w = threadIdx.x;
+  if (w < world) req[(uint64_t)w * req_words] = cnt[w] < cap ? cnt[w] : cap;
+}
+// owner side: the requested rows of this shard, copied in request order into the reply bucket
+__global__ void __launch_bounds__(256) xserve_kernel(const uint32_t* __restrict__ req, uint64_t req_words,
+                                                     const double* __restrict__ table, uint64_t lo, uint64_t shard_n,
+                                                     uint32_t stride, double* __restrict__ rep, uint64_t rep_doubles,
+                                                     uint32_t world, uint32_t cap, unsigned long long* __restrict__ flags) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t w = (uint32_t)(t / cap), i = (uint32_t)(t % cap);
+  if (w >= world) return;
+  const uint32_t* b = req + (uint64_t)w * req_words;
+  if (i >= b[0]) return;
+  const uint32_t id = b[4 + i];
+  if ((uint64_t)id - lo >= shard_n) {
+    atomicOr(flags, 2ull);
+    return;
+  }
+  const double2* src = reinterpret_cast<const double2*>(table + (uint64_t)id * stride);
+  double2* dst = reinterpret_cast<double2*>(rep + (uint64_t)w * rep_doubles + (uint64_t)i * stride);
+  for (uint32_t k = 0; k < stride / 2; ++k) dst[k] = src[k];
+}
+// requester side: each reply row lands at its peer's place in this shard's table copy
+__global__ void __launch_bounds__(256) xapply_kernel(const uint32_t* __restrict__ req, uint64_t req_words,
+                                                     const double* __restrict__ rep, uint64_t rep_doubles,
+                                                     double* __restrict__ table, uint32_t stride, uint32_t world,
+                                                     uint32_t cap) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t w = (uint32_t)(t / cap), i = (uint32_t)(t % cap);
+  if (w >= world) return;
+  const uint32_t* b = req + (uint64_t)w * req_words;
+  if (i >= b[0]) return;
+  const uint32_t id = b[4 + i];
+  const double2* src = reinterpret_cast<const double2*>(rep + (uint64_t)w * rep_doubles + (uint64_t)i * stride);
+  double2* dst = reinterpret_cast<double2*>(table + (uint64_t)id * stride);
+  for (uint32_t k = 0; k < stride / 2; ++k) dst[k] = src[k];
+}
 
 extern "C" {
 
@@ -979,6 +1042,9 @@ int rsf_vivaldi_destroy(rsf_vivaldi* v) {
   hipFree(v->resets);
   hipFree(v->probe_peer);
   hipFree(v->probe_rtt);
+  for (void* q : {(void*)v->req_send, (void*)v->req_recv, (void*)v->xcnt, (void*)v->rep_send, (void*)v->rep_recv,
+                  (void*)v->xflags})
+    if (q) hipFree(q);
   v->scratch.release();
   if (v->own) hipStreamDestroy(v->own);
   delete v;
@@ -1251,6 +1317,96 @@ int rsf_vivaldi_round_ablate(rsf_vivaldi* v, uint32_t round, uint32_t mask) {
 #undef ABL_CASE
   RSF_HIP(hipGetLastError());
   v->cur ^= 1;
+  return RSF_OK;
+}
+
+int rsf_vivaldi_exchange_buffers(rsf_vivaldi* v, uint32_t world, rsf_vivaldi_xbufs* out) {
+  if (!v || !out || world == 0) return set_err_args("bad argument");
+  const VivParams& p = v->p;
+  if (p.n % world || p.shard_n != p.n / world || p.lo % p.shard_n) return set_err_args("shards must be equal ranges");
+  if (world != v->xw) {
+    RSF_HIP(hipSetDevice(v->device));
+    RSF_HIP(hipStreamSynchronize(v->stream));
+    for (void* q : {(void*)v->req_send, (void*)v->req_recv, (void*)v->xcnt, (void*)v->rep_send, (void*)v->rep_recv,
+                    (void*)v->xflags})
+      if (q) hipFree(q);
+    v->req_send = v->req_recv = v->xcnt = nullptr;
+    v->rep_send = v->rep_recv = nullptr;
+    v->xflags = nullptr;
+    v->xw = 0;
+    // one probe per member and round: about shard_n / world requests per owner for
+    // uniformly drawn peers; the buckets hold 1/8 more plus 4096 (overflow flagged)
+    const uint64_t expect = (p.shard_n + world - 1) / world;
+    v->xcap = (uint32_t)std::min<uint64_t>(expect + expect / 8 + 4096, p.shard_n);
+    v->req_words = ((4 + (uint64_t)v->xcap) + 63) & ~63ull;
+    v->rep_doubles = (uint64_t)v->xcap * p.stride;
+    int rc;
+    if ((rc = rsf::dmalloc((void**)&v->req_send, v->req_words * 4 * world)) ||
+        (rc = rsf::dmalloc((void**)&v->req_recv, v->req_words * 4 * world)) ||
+        (rc = rsf::dmalloc((void**)&v->rep_send, v->rep_doubles * 8 * world)) ||
+        (rc = rsf::dmalloc((void**)&v->rep_recv, v->rep_doubles * 8 * world)) ||
+        (rc = rsf::dmalloc((void**)&v->xcnt, 4 * world)) || (rc = rsf::dmalloc((void**)&v->xflags, 8)))
+      return rc;
+    RSF_HIP(hipMemset(v->req_send, 0, v->req_words * 4 * world));
+    RSF_HIP(hipMemset(v->req_recv, 0, v->req_words * 4 * world));
+    RSF_HIP(hipMemset(v->xflags, 0, 8));
+    v->xw = world;
+  }
+  out->req_send = v->req_send;
+  out->req_recv = v->req_recv;
+  out->rep_send = v->rep_send;
+  out->rep_recv = v->rep_recv;
+  out->req_bucket_bytes = v->req_words * 4;
+  out->rep_bucket_bytes = v->rep_doubles * 8;
+  return RSF_OK;
+}
+
+int rsf_vivaldi_exchange_requests(rsf_vivaldi* v, uint32_t world, const uint32_t* peer) {
+  if (!v || !peer || world != v->xw) return set_err_args("call rsf_vivaldi_exchange_buffers(world) first");
+  const VivParams& p = v->p;
+  RSF_HIP(hipSetDevice(v->device));
+  RSF_HIP(hipMemsetAsync(v->xcnt, 0, 4 * world, v->stream));
+  hipLaunchKernelGGL(xreq_pack_kernel, dim3((unsigned)((p.shard_n + 255) / 256)), dim3(256), 0, v->stream, peer, p.lo,
+                     p.shard_n, p.shard_n, v->req_send, v->req_words, v->xcap, v->xcnt, v->xflags);
+  hipLaunchKernelGGL(xreq_header_kernel, dim3(1), dim3(64), 0, v->stream, v->req_send, v->req_words,
+                     (const uint32_t*)v->xcnt, world, v->xcap);
+  RSF_HIP(hipGetLastError());
+  return RSF_OK;
+}
+
+int rsf_vivaldi_exchange_serve(rsf_vivaldi* v, uint32_t world) {
+  if (!v || world != v->xw) return set_err_args("call rsf_vivaldi_exchange_buffers(world) first");
+  const VivParams& p = v->p;
+  RSF_HIP(hipSetDevice(v->device));
+  const uint64_t n = (uint64_t)world * v->xcap;
+  hipLaunchKernelGGL(xserve_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, v->stream,
+                     (const uint32_t*)v->req_recv, v->req_words, (const double*)v->table[v->cur], p.lo, p.shard_n,
+                     p.stride, v->rep_send, v->rep_doubles, world, v->xcap, v->xflags);
+  RSF_HIP(hipGetLastError());
+  return RSF_OK;
+}
+
+int rsf_vivaldi_exchange_apply(rsf_vivaldi* v, uint32_t world) {
+  if (!v || world != v->xw) return set_err_args("call rsf_vivaldi_exchange_buffers(world) first");
+  const VivParams& p = v->p;
+  RSF_HIP(hipSetDevice(v->device));
+  const uint64_t n = (uint64_t)world * v->xcap;
+  hipLaunchKernelGGL(xapply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, v->stream,
+                     (const uint32_t*)v->req_send, v->req_words, (const double*)v->rep_recv, v->rep_doubles,
+                     v->table[v->cur], p.stride, world, v->xcap);
+  RSF_HIP(hipGetLastError());
+  return RSF_OK;
+}
+
+int rsf_vivaldi_exchange_status(rsf_vivaldi* v, int* ok) {
+  if (!v || !ok) return set_err_args("null argument");
+  unsigned long long f = 0;
+  if (v->xflags) {
+    RSF_HIP(hipSetDevice(v->device));
+    RSF_HIP(hipMemcpyAsync(&f, v->xflags, 8, hipMemcpyDeviceToHost, v->stream));
+    RSF_HIP(hipStreamSynchronize(v->stream));
+  }
+  *ok = f == 0;
   return RSF_OK;
 }
 

@@ -24,6 +24,12 @@ Per round:
 
 The driver is generic over the engine object (`GossipEngine` on HIP; the gloo
 tests substitute a CPU stand-in that exercises only the routing).
+
+Vivaldi rounds (ShardedVivaldi): each shard holds the whole coordinate table but
+updates only its own rows; a round fetches just the rows of its members' remote
+peers from their owners (request all-to-all, owners copy the rows, reply all-to-all,
+rows written in place), then observes -- the targeted exchange of SURVEY §8(e) in
+place of an all-gather of the table.
 """
 import dataclasses
 
@@ -84,6 +90,56 @@ class EngineBuffers:
         return self.eng.bucket_ok() if self.buckets else self.eng.runs_ok()
 
 
+def _staged(group, dev):
+    # RCCL ("nccl") moves HBM directly; gloo (the CPU rehearsal backend: several ranks
+    # sharing one GPU, or CPU stand-ins) needs host tensors, so GPU buffers are staged
+    return dist.get_backend(group) == "gloo" and dev.type == "cuda"
+
+
+def all_to_all(out, inp, stage, group=None, out_splits=None, in_splits=None):
+    if stage:
+        ho = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(ho, inp.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits,
+                               group=group)
+        out.copy_(ho)
+    else:
+        dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
+
+
+class ShardedVivaldi:
+    """Vivaldi rounds over members sharded by equal contiguous ranges (one
+    CoordinateClients context per rank, created with shard=(lo, hi))."""
+
+    def __init__(self, clients, rank, world, group=None):
+        if clients.n % world or clients.hi - clients.lo != clients.n // world:
+            raise ValueError("members must be sharded in equal contiguous ranges")
+        self.g, self.rank, self.world, self.group = clients, rank, world, group
+        b = clients.exchange_buffers(world)
+        self.req_send = hbm_tensor(b["req_send"], world * b["req_bucket_bytes"] // 4, "<i4")
+        self.req_recv = hbm_tensor(b["req_recv"], world * b["req_bucket_bytes"] // 4, "<i4")
+        self.rep_send = hbm_tensor(b["rep_send"], world * b["rep_bucket_bytes"] // 8, "<f8")
+        self.rep_recv = hbm_tensor(b["rep_recv"], world * b["rep_bucket_bytes"] // 8, "<f8")
+        self.stage = _staged(group, self.req_send.device)
+
+    def fetch(self, peer_ptr):
+        """Bring the rows of this round's remote peers into the current table."""
+        g, w = self.g, self.world
+        g.exchange_requests(w, peer_ptr)
+        all_to_all(self.req_recv, self.req_send, self.stage, self.group)
+        g.exchange_serve(w)
+        all_to_all(self.rep_recv, self.rep_send, self.stage, self.group)
+        g.exchange_apply(w)
+
+    def round(self, r, peer_ptr, rtt_ptr, status_ptr=None, slots=16):
+        if self.world > 1:
+            self.fetch(peer_ptr)
+        self.g.observe(r % slots, peer_ptr, rtt_ptr, status_ptr, r)
+
+    def check(self):
+        """True if no request bucket overflowed and every request reached its owner."""
+        return self.g.exchange_ok()
+
+
 class ShardedGossip:
     def __init__(self, cfg: GossipConfig, rank, world, device=0, engine=None, buffers=None, group=None,
                  exchange="buckets"):
@@ -101,9 +157,7 @@ class ShardedGossip:
         self.buckets = getattr(self.buf, "buckets", False)
         self.dev = self.buf.recv.device
         self.last_in = 0
-        # RCCL ("nccl") moves HBM directly; gloo (the CPU rehearsal backend: several ranks
-        # sharing one GPU, or CPU stand-ins) needs host tensors, so GPU buffers are staged
-        self.stage = dist.get_backend(group) == "gloo" and self.dev.type == "cuda"
+        self.stage = _staged(group, self.dev)
 
     def _all_reduce(self, t):
         if self.stage:
@@ -114,14 +168,7 @@ class ShardedGossip:
             dist.all_reduce(t, group=self.group)
 
     def _all_to_all(self, out, inp, out_splits=None, in_splits=None):
-        if self.stage:
-            ho = torch.empty(out.shape, dtype=out.dtype)
-            dist.all_to_all_single(ho, inp.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits,
-                                   group=self.group)
-            out.copy_(ho)
-        else:
-            dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits,
-                                   group=self.group)
+        all_to_all(out, inp, self.stage, self.group, out_splits, in_splits)
 
     def round(self, t, ml=None, acts=None):
         eng, buf = self.eng, self.buf
