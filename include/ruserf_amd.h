@@ -439,6 +439,42 @@ int rsf_gossip_set_delivery_log(rsf_gossip* g, uint32_t per_member);
  * out (host, capacity `cap` entries); *n_out = entries written.  Synchronises. */
 int rsf_gossip_dump_deliveries(rsf_gossip* g, rsf_delivery* out, uint64_t cap, uint64_t* n_out);
 
+/* ---- Snapshot log (core/src/snapshot.rs) and restart (core/src/serf/base.rs:122-204)
+ * Replaces Options::snapshot_path + Snapshot::from_replay_result / open_and_replay_snapshot
+ * (snapshot.rs:233-530) and Serf::new's clock replay (base.rs:128-204).  Every member gets a
+ * snapshotter: its alive set follows the Join / Leave / Failed member events (process_member_event,
+ * snapshot.rs:686-711), its event / query clocks the largest delivered ltimes (663-684), and a
+ * member's Serf::leave stops it (handle_leave, 568-586).  Node records carry the subject index
+ * as the node bytes: [tag][u32 LE 4][u32 LE subject]; clock records [tag][u64 LE].
+ *   enable_snapshot : allocate and start (alive set = each member's known Alive / Leaving members)
+ *   snapshot_encode : members [first, first+count) as compacted snapshot files (compact(),
+ *                     786-880; after a leave also the Leave record and the shutdown clock):
+ *                     offsets (device, count+1 u64) = each file's start, *total = bytes; with
+ *                     out = NULL only the sizes; out (device) needs out_cap >= *total
+ *   restart         : members (host, distinct, this shard) restart from their files (host bytes,
+ *                     offsets[n+1]): replay, clocks 1 then witness(old), event/query min time =
+ *                     old + 1, fresh member state, then handle_rejoin (1741-1770).  result[i] =
+ *                     1 rejoined, 0 alone, RSF_SNAP_ERR_* (the member is left unchanged).
+ *   dump_snapshot   : the snapshotters' state (bits [n_loc][ceil(S/32)], state [n_loc][4] =
+ *                     {event clock, query clock, clock at leave, flags bit0 leaving}) */
+#define RSF_SNAP_ERR_RECORD (-1)    /* SnapshotError::UnknownRecordType */
+#define RSF_SNAP_ERR_TRUNCATED (-2) /* SnapshotError::Replay (unexpected end of a record) */
+#define RSF_SNAP_ERR_NODE (-3)      /* a node record that does not decode */
+int rsf_gossip_enable_snapshot(rsf_gossip* g, int rejoin_after_leave);
+int rsf_gossip_snapshot_encode(rsf_gossip* g, uint64_t first, uint64_t count, uint64_t* offsets, uint8_t* out,
+                               uint64_t out_cap, uint64_t* total);
+int rsf_gossip_restart(rsf_gossip* g, const uint32_t* members, uint32_t n, const uint8_t* files,
+                       const uint64_t* offsets, int32_t* result);
+int rsf_gossip_dump_snapshot(rsf_gossip* g, uint32_t* bits, uint64_t* state);
+
+/* Reconnector tick (core/src/serf/base.rs:632-701; replaces Reconnector::spawn's loop body).
+ * At every live member: num_failed / num_alive over its view (num_alive = states - failed - left,
+ * at least 1); with that probability (rng.gen::<f32>(), a Philox draw of (seed, member, tick))
+ * it tries one failed member (gen_range(0..num_failed), ascending subject order).  The try
+ * succeeds when that member is up, and memberlist's join then notifies handle_node_join.
+ * target (device, n_loc u32, may be NULL) = the tried subject, 0xFFFFFFFF none. */
+int rsf_gossip_reconnect(rsf_gossip* g, uint32_t tick, uint32_t* target);
+
 /* ---- QueueChecker (core/src/serf/base.rs:703-760) ---------------------------
  * One checker tick over the three queues of every shard member: max =
  * max_queue_depth, or, when min_queue_depth > 0, max(2 * n_members, min_queue_depth)

@@ -553,8 +553,26 @@ uint64_t orc_digest_mix(uint64_t d, uint64_t x) {
 #define DIG_MEMBER 0x3000000000000000ull
 enum { EV_JOIN = 0, EV_LEAVE = 1, EV_FAILED = 2, EV_REAP = 3 };
 
+/* the snapshotter's process_member_event (snapshot.rs:686-711): Join adds the node to
+ * the alive set, Leave / Failed remove it; nothing is recorded after a leave */
+static inline void snap_member_event(orc_world* w, uint32_t m, uint32_t ev, uint32_t subj) {
+  if (!w->snap_bits || (w->snap_sn[(size_t)m * 4 + 3] & 1)) return;
+  uint32_t* word = w->snap_bits + (size_t)m * w->snap_w + (subj >> 5);
+  if (ev == EV_JOIN) *word |= 1u << (subj & 31);
+  else if (ev == EV_LEAVE || ev == EV_FAILED) *word &= ~(1u << (subj & 31));
+}
+
 static inline void digest_member_event(orc_world* w, uint32_t m, uint32_t ev, uint32_t subj) {
   w->digest[m] = orc_digest_mix(w->digest[m], DIG_MEMBER | ((uint64_t)ev << 32) | subj);
+  snap_member_event(w, m, ev, subj);
+}
+
+/* process_user_event / process_query_event (snapshot.rs:663-684): the largest ltime
+ * handed to the application */
+static inline void snap_clock(orc_world* w, uint32_t m, int which, uint64_t ltime) {
+  if (!w->snap_sn) return;
+  uint64_t* sn = w->snap_sn + (size_t)m * 4;
+  if (!(sn[3] & 1) && ltime > sn[which]) sn[which] = ltime;
 }
 
 int orc_world_init(orc_world* w, const orc_world_cfg* c) {
@@ -612,7 +630,7 @@ void orc_world_free(orc_world* w) {
                   w->refute_ltime, w->v_ltime, w->v_status, w->v_kind, w->q_rumor, w->q_seq,
                   w->q_tx, w->q_len, w->q_next_seq, w->eb_ltime, w->eb_cnt, w->eb_keys,
                   w->qb_ltime, w->qb_cnt, w->qb_ids, w->rumors, w->v_time, w->q_pruned, w->q_expired,
-                  w->dlog, w->dcnt};
+                  w->dlog, w->dcnt, w->snap_bits, w->snap_sn};
   for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) free(ptrs[i]);
   memset(w, 0, sizeof(*w));
 }
@@ -649,6 +667,7 @@ int orc_handle_join_intent(orc_world* w, uint32_t m, uint32_t subj, uint64_t lti
 }
 
 static void erase_entry(orc_world* w, size_t e);
+static void snap_leave(orc_world* w, uint32_t m);
 
 /* handle_prune  base.rs:1587-1612: erase_node! (members.states.remove; the member also
  * leaves left_members) and a Reap MemberEvent.  The reference first sleeps
@@ -783,6 +802,7 @@ int orc_handle_user_event_cc(orc_world* w, uint32_t m, uint64_t ltime, uint64_t 
   }
   w->digest[m] = orc_digest_mix(orc_digest_mix(w->digest[m], DIG_USER ^ key), ltime);
   dlog_put(w, m, ltime, key, cc);
+  snap_clock(w, m, 0, ltime);
   return ORC_F_REBROADCAST | ORC_F_DELIVER;
 }
 
@@ -806,6 +826,7 @@ int orc_handle_query(orc_world* w, uint32_t m, uint64_t ltime, uint32_t id, int 
     w->qb_cnt[slot] = 1;
   }
   w->digest[m] = orc_digest_mix(orc_digest_mix(w->digest[m], DIG_QUERY ^ id), ltime);
+  snap_clock(w, m, 1, ltime);
   return (no_broadcast ? 0 : ORC_F_REBROADCAST) | ORC_F_DELIVER;
 }
 
@@ -1181,6 +1202,7 @@ int orc_world_round_mt(orc_world* w, uint32_t round, const orc_ml_event* ml, uin
       case ORC_ACT_LEAVE_SELF: { /* Serf::leave  api.rs:473-503 */
         w->serf_state[m] = ORC_SERF_LEAVING;
         uint64_t lt = w->clock[m];
+        if (w->snap_sn) snap_leave(w, m);
         orc_clock_increment(&w->clock[m]);
         uint32_t subj = (uint32_t)w->member_subj[m];
         orc_handle_leave_intent(w, m, subj, lt, 0, NULL);
@@ -1786,4 +1808,343 @@ void orc_swim_dump(const orc_swim* w, uint64_t first, uint64_t count, uint8_t* s
     nconf[i] = w->state[e] == SW_SUSPECT ? w->nconf[e] : 0;
   }
   for (uint64_t r = 0; r < count; ++r) self_inc[r] = w->self_inc[first + r];
+}
+
+/* ------------------------------------------------------------------------ */
+/* Snapshot log (core/src/snapshot.rs) and Reconnector (base.rs:632-701)    */
+/* ------------------------------------------------------------------------ */
+#define PURPOSE_RECONNECT 7u
+#define SNAP_BYTES_PER_NODE 128u   /* snapshot.rs:56 */
+#define SNAP_COMPACTION_THRESHOLD 2u /* snapshot.rs:60 */
+
+static void le64(uint8_t* d, uint64_t v) {
+  for (int i = 0; i < 8; ++i, v >>= 8) d[i] = (uint8_t)v;
+}
+static uint64_t rd_le64(const uint8_t* s) {
+  uint64_t v = 0;
+  for (int i = 7; i >= 0; --i) v = (v << 8) | s[i];
+  return v;
+}
+static uint32_t rd_le32(const uint8_t* s) { return (uint32_t)s[0] | (uint32_t)s[1] << 8 | (uint32_t)s[2] << 16 | (uint32_t)s[3] << 24; }
+
+/* SnapshotRecord::encode (snapshot.rs:159-218): node records [tag][u32 LE len][node],
+ * clock records [tag][u64 LE], others [tag].  Returns the bytes written (out may be NULL). */
+static uint32_t snap_rec_node(uint8_t* out, uint8_t tag, uint32_t subj) {
+  if (out) {
+    out[0] = tag;
+    out[1] = 4;
+    out[2] = out[3] = out[4] = 0;
+    out[5] = (uint8_t)subj;
+    out[6] = (uint8_t)(subj >> 8);
+    out[7] = (uint8_t)(subj >> 16);
+    out[8] = (uint8_t)(subj >> 24);
+  }
+  return 9;
+}
+static uint32_t snap_rec_clock(uint8_t* out, uint8_t tag, uint64_t t) {
+  if (out) {
+    out[0] = tag;
+    le64(out + 1, t);
+  }
+  return 9;
+}
+
+int orc_snapshot_replay(const uint8_t* f, uint64_t len, int rejoin, uint32_t s, uint32_t* alive, uint64_t clocks[3]) {
+  const uint32_t words = (s + 31) / 32;
+  memset(alive, 0, (size_t)words * 4);
+  clocks[0] = clocks[1] = clocks[2] = 0;
+  uint64_t p = 0;
+  while (p < len) {
+    const uint8_t tag = f[p++];
+    switch (tag) {
+      case ORC_SNAP_ALIVE:
+      case ORC_SNAP_NOT_ALIVE: {
+        if (len - p < 4) return ORC_SNAP_ERR_TRUNCATED;
+        uint32_t n = rd_le32(f + p);
+        p += 4;
+        if (len - p < n) return ORC_SNAP_ERR_TRUNCATED;
+        if (n != 4) return ORC_SNAP_ERR_NODE; /* TransformDelegate::decode_node fails */
+        uint32_t subj = rd_le32(f + p);
+        p += 4;
+        if (subj >= s) return ORC_SNAP_ERR_NODE;
+        if (tag == ORC_SNAP_ALIVE) alive[subj >> 5] |= 1u << (subj & 31);
+        else alive[subj >> 5] &= ~(1u << (subj & 31));
+        break;
+      }
+      case ORC_SNAP_CLOCK:
+      case ORC_SNAP_EVENT_CLOCK:
+      case ORC_SNAP_QUERY_CLOCK:
+        if (len - p < 8) return ORC_SNAP_ERR_TRUNCATED;
+        clocks[tag - ORC_SNAP_CLOCK] = rd_le64(f + p);
+        p += 8;
+        break;
+      case ORC_SNAP_COORDINATE:
+      case ORC_SNAP_COMMENT: break;
+      case ORC_SNAP_LEAVE: /* ignored when re-joining after a leave (snapshot.rs:324-334) */
+        if (rejoin) break;
+        memset(alive, 0, (size_t)words * 4);
+        clocks[0] = clocks[1] = clocks[2] = 0;
+        break;
+      default: return ORC_SNAP_ERR_RECORD; /* UnknownRecordType */
+    }
+  }
+  return 0;
+}
+
+/* ---- the in-memory Snapshotter */
+static int snap_put(orc_snapshotter* sp, const uint8_t* rec, uint32_t n) {
+  if (sp->len + n > sp->cap) {
+    uint64_t c = sp->cap ? sp->cap * 2 : 256;
+    while (c < sp->len + n) c *= 2;
+    uint8_t* b = (uint8_t*)realloc(sp->buf, c);
+    if (!b) return -1;
+    sp->buf = b;
+    sp->cap = c;
+  }
+  memcpy(sp->buf + sp->len, rec, n);
+  sp->len += n;
+  return 0;
+}
+
+static uint64_t snap_popcount(const orc_snapshotter* sp) {
+  uint64_t c = 0;
+  for (uint32_t i = 0; i < (sp->s + 31) / 32; ++i) c += (uint64_t)__builtin_popcount(sp->alive[i]);
+  return c;
+}
+
+/* compact (snapshot.rs:786-880): the alive nodes, then the three clocks */
+static void snap_compact(orc_snapshotter* sp) {
+  uint8_t rec[9];
+  sp->len = 0;
+  for (uint32_t subj = 0; subj < sp->s; ++subj)
+    if (sp->alive[subj >> 5] >> (subj & 31) & 1) snap_put(sp, rec, snap_rec_node(rec, ORC_SNAP_ALIVE, subj));
+  snap_put(sp, rec, snap_rec_clock(rec, ORC_SNAP_CLOCK, sp->last_clock));
+  snap_put(sp, rec, snap_rec_clock(rec, ORC_SNAP_EVENT_CLOCK, sp->last_event_clock));
+  snap_put(sp, rec, snap_rec_clock(rec, ORC_SNAP_QUERY_CLOCK, sp->last_query_clock));
+  sp->offset = sp->len;
+  sp->compactions++;
+}
+
+/* try_append / append_line (snapshot.rs:722-776): write, then compact past
+ * max(alive * 128 * 2, min_compact_size) (snapshot_max_size, 778-784) */
+static void snap_append(orc_snapshotter* sp, const uint8_t* rec, uint32_t n) {
+  if (snap_put(sp, rec, n)) return;
+  sp->offset += n;
+  uint64_t th = snap_popcount(sp) * SNAP_BYTES_PER_NODE * SNAP_COMPACTION_THRESHOLD;
+  if (th < sp->min_compact) th = sp->min_compact;
+  if (sp->offset > th) snap_compact(sp);
+}
+
+int orc_snapshotter_open(orc_snapshotter* sp, uint32_t s, const uint8_t* file, uint64_t len, uint64_t min_compact,
+                         int rejoin) {
+  memset(sp, 0, sizeof(*sp));
+  sp->s = s;
+  sp->alive = (uint32_t*)calloc((s + 31) / 32 + 1, 4);
+  if (!sp->alive) return -1;
+  uint64_t clocks[3] = {0, 0, 0};
+  if (len) {
+    int rc = orc_snapshot_replay(file, len, rejoin, s, sp->alive, clocks);
+    if (rc) return rc;
+    if (snap_put(sp, file, (uint32_t)len)) return -1;
+  }
+  sp->offset = len;
+  sp->last_clock = clocks[0];
+  sp->last_event_clock = clocks[1];
+  sp->last_query_clock = clocks[2];
+  sp->min_compact = min_compact;
+  sp->rejoin = rejoin;
+  return 0;
+}
+
+void orc_snapshotter_free(orc_snapshotter* sp) {
+  free(sp->buf);
+  free(sp->alive);
+  memset(sp, 0, sizeof(*sp));
+}
+
+void orc_snapshotter_user_event(orc_snapshotter* sp, uint64_t ltime) {
+  if (sp->leaving || ltime <= sp->last_event_clock) return; /* stream_flush_event!: stop after a leave */
+  sp->last_event_clock = ltime;
+  uint8_t rec[9];
+  snap_append(sp, rec, snap_rec_clock(rec, ORC_SNAP_EVENT_CLOCK, ltime));
+}
+
+void orc_snapshotter_query(orc_snapshotter* sp, uint64_t ltime) {
+  if (sp->leaving || ltime <= sp->last_query_clock) return;
+  sp->last_query_clock = ltime;
+  uint8_t rec[9];
+  snap_append(sp, rec, snap_rec_clock(rec, ORC_SNAP_QUERY_CLOCK, ltime));
+}
+
+/* update_clock (snapshot.rs:713-720): last_seen = clock.time() - 1 (saturating) */
+void orc_snapshotter_update_clock(orc_snapshotter* sp, uint64_t clock_time) {
+  uint64_t last_seen = clock_time ? clock_time - 1 : 0;
+  if (last_seen > sp->last_clock) {
+    sp->last_clock = last_seen;
+    uint8_t rec[9];
+    snap_append(sp, rec, snap_rec_clock(rec, ORC_SNAP_CLOCK, last_seen));
+  }
+}
+
+void orc_snapshotter_member_event(orc_snapshotter* sp, uint32_t ev, uint32_t subj, uint64_t clock_time) {
+  if (sp->leaving || subj >= sp->s) return;
+  uint8_t rec[9];
+  if (ev == EV_JOIN) {
+    sp->alive[subj >> 5] |= 1u << (subj & 31);
+    snap_append(sp, rec, snap_rec_node(rec, ORC_SNAP_ALIVE, subj));
+  } else if (ev == EV_LEAVE || ev == EV_FAILED) {
+    sp->alive[subj >> 5] &= ~(1u << (subj & 31));
+    snap_append(sp, rec, snap_rec_node(rec, ORC_SNAP_NOT_ALIVE, subj));
+  }
+  orc_snapshotter_update_clock(sp, clock_time);
+}
+
+/* handle_leave (snapshot.rs:568-586) */
+void orc_snapshotter_leave(orc_snapshotter* sp) {
+  sp->leaving = 1;
+  if (!sp->rejoin) memset(sp->alive, 0, (size_t)((sp->s + 31) / 32) * 4);
+  uint8_t rec = ORC_SNAP_LEAVE;
+  snap_append(sp, &rec, 1);
+}
+
+/* ---- the world's snapshotters */
+int orc_world_enable_snapshot(orc_world* w, int rejoin_after_leave) {
+  free(w->snap_bits);
+  free(w->snap_sn);
+  w->snap_w = (w->s + 31) / 32;
+  w->snap_bits = (uint32_t*)calloc((size_t)w->n * w->snap_w, 4);
+  w->snap_sn = (uint64_t*)calloc((size_t)w->n * 4, 8);
+  if (!w->snap_bits || !w->snap_sn) return -1;
+  w->snap_rejoin = rejoin_after_leave;
+  for (uint32_t m = 0; m < w->n; ++m)
+    for (uint32_t subj = 0; subj < w->s; ++subj) {
+      size_t e = (size_t)m * w->s + subj;
+      if (w->v_kind[e] == ORC_K_KNOWN && (w->v_status[e] == ORC_ST_ALIVE || w->v_status[e] == ORC_ST_LEAVING))
+        w->snap_bits[(size_t)m * w->snap_w + (subj >> 5)] |= 1u << (subj & 31);
+    }
+  return 0;
+}
+
+/* Snapshot::leave at Serf::leave: the clock ticker's last value, then recording stops */
+static void snap_leave(orc_world* w, uint32_t m) {
+  uint64_t* sn = w->snap_sn + (size_t)m * 4;
+  if (sn[3] & 1) return;
+  sn[2] = w->clock[m] ? w->clock[m] - 1 : 0;
+  sn[3] |= 1;
+  if (!w->snap_rejoin) memset(w->snap_bits + (size_t)m * w->snap_w, 0, (size_t)w->snap_w * 4);
+}
+
+uint64_t orc_world_snapshot_encode(const orc_world* w, uint32_t m, uint8_t* out) {
+  if (!w->snap_bits) return 0;
+  const uint32_t* bits = w->snap_bits + (size_t)m * w->snap_w;
+  const uint64_t* sn = w->snap_sn + (size_t)m * 4;
+  const uint64_t now_clock = w->clock[m] ? w->clock[m] - 1 : 0;
+  const int leaving = (int)(sn[3] & 1);
+  uint64_t p = 0;
+  for (uint32_t subj = 0; subj < w->s; ++subj)
+    if (bits[subj >> 5] >> (subj & 31) & 1) p += snap_rec_node(out ? out + p : NULL, ORC_SNAP_ALIVE, subj);
+  p += snap_rec_clock(out ? out + p : NULL, ORC_SNAP_CLOCK, leaving ? sn[2] : now_clock);
+  p += snap_rec_clock(out ? out + p : NULL, ORC_SNAP_EVENT_CLOCK, sn[0]);
+  p += snap_rec_clock(out ? out + p : NULL, ORC_SNAP_QUERY_CLOCK, sn[1]);
+  if (leaving) {
+    if (out) out[p] = ORC_SNAP_LEAVE;
+    p += 1;
+    /* the shutdown's update_clock (snapshot.rs:622-623) */
+    if (now_clock > sn[2]) p += snap_rec_clock(out ? out + p : NULL, ORC_SNAP_CLOCK, now_clock);
+  }
+  return p;
+}
+
+int orc_world_restart(orc_world* w, uint32_t m, const uint8_t* file, uint64_t len) {
+  if (!w->snap_bits || m >= w->n) return -1;
+  uint32_t* bits = w->snap_bits + (size_t)m * w->snap_w;
+  uint64_t old[3];
+  uint32_t* tmp = (uint32_t*)calloc(w->snap_w + 1, 4);
+  if (!tmp) return -1;
+  int rc = orc_snapshot_replay(file, len, w->snap_rejoin, w->s, tmp, old);
+  if (!rc) memcpy(bits, tmp, (size_t)w->snap_w * 4); /* a file that does not replay changes nothing */
+  free(tmp);
+  if (rc) return rc;
+  /* Serf::new (base.rs:122-204): clocks start at 1, then witness the replayed ones;
+   * events / queries older than the snapshot are ignored from now on */
+  w->clock[m] = w->eclock[m] = w->qclock[m] = 1;
+  orc_clock_witness(&w->clock[m], old[0]);
+  orc_clock_witness(&w->eclock[m], old[1]);
+  orc_clock_witness(&w->qclock[m], old[2]);
+  w->emin[m] = old[1] + 1;
+  w->qmin[m] = old[2] + 1;
+  w->serf_state[m] = ORC_SERF_ALIVE;
+  /* a fresh process: no member states, intents, queued broadcasts, event / query buffers */
+  for (uint32_t subj = 0; subj < w->s; ++subj) erase_entry(w, (size_t)m * w->s + subj);
+  for (uint32_t i = 0; i < 3 * w->qcap; ++i) {
+    size_t q = (size_t)m * 3 * w->qcap + i;
+    w->q_rumor[q] = EMPTY_RUMOR;
+    w->q_seq[q] = 0;
+    w->q_tx[q] = 0;
+    w->q_len[q] = 0;
+  }
+  for (uint32_t q = 0; q < 3; ++q) w->q_next_seq[(size_t)m * 3 + q] = 0;
+  memset(w->eb_ltime + (size_t)m * w->ebuf, 0, (size_t)w->ebuf * 8);
+  memset(w->eb_cnt + (size_t)m * w->ebuf, 0, (size_t)w->ebuf * 4);
+  memset(w->eb_keys + (size_t)m * w->ebuf * w->slot_k, 0, (size_t)w->ebuf * w->slot_k * 8);
+  memset(w->qb_ltime + (size_t)m * w->qbuf, 0, (size_t)w->qbuf * 8);
+  memset(w->qb_cnt + (size_t)m * w->qbuf, 0, (size_t)w->qbuf * 4);
+  memset(w->qb_ids + (size_t)m * w->qbuf * w->slot_k, 0, (size_t)w->qbuf * w->slot_k * 4);
+  if (w->member_subj[m] >= 0) w->refute_cnt[w->member_subj[m]] = 0;
+  uint64_t* sn = w->snap_sn + (size_t)m * 4;
+  sn[0] = old[1];
+  sn[1] = old[2];
+  sn[2] = 0;
+  sn[3] = 0;
+  /* handle_rejoin (base.rs:1741-1770): memberlist.join to the replayed nodes until one
+   * answers; memberlist's state exchange then notifies a join of every live member */
+  int joined = 0;
+  for (uint32_t subj = 0; subj < w->s && !joined; ++subj)
+    if ((bits[subj >> 5] >> (subj & 31) & 1) && (int32_t)subj != w->member_subj[m] && w->alive[w->subj_member[subj]])
+      joined = 1;
+  if (joined)
+    for (uint32_t subj = 0; subj < w->s; ++subj)
+      if ((int32_t)subj != w->member_subj[m] && w->alive[w->subj_member[subj]]) orc_handle_node_join(w, m, subj);
+  return joined;
+}
+
+uint32_t orc_world_reconnect(orc_world* w, uint32_t tick, uint32_t* target) {
+  uint32_t key[2];
+  seed_key(w->seed, key);
+  uint32_t joins = 0;
+  for (uint32_t m = 0; m < w->n; ++m) {
+    target[m] = EMPTY_RUMOR;
+    if (!w->alive[m]) continue;
+    const size_t row = (size_t)m * w->s;
+    uint32_t failed = 0, left = 0, known = 1; /* members.states holds the local node too */
+    for (uint32_t subj = 0; subj < w->s; ++subj) {
+      if ((int32_t)subj == w->member_subj[m] || w->v_kind[row + subj] != ORC_K_KNOWN) continue;
+      known++;
+      failed += w->v_status[row + subj] == ORC_ST_FAILED;
+      left += w->v_status[row + subj] == ORC_ST_LEFT;
+    }
+    if (!failed) continue;
+    uint32_t alive_n = known - failed - left;
+    if (alive_n < 1) alive_n = 1;
+    const float prob = (float)failed / (float)alive_n;
+    uint32_t ctr[4] = {0, PURPOSE_RECONNECT << 24, m, tick}, o[4];
+    orc_philox4x32(ctr, key, o);
+    const float r = (float)(o[0] >> 8) * (1.0f / 16777216.0f); /* rng.gen::<f32>() */
+    if (r > prob) continue;
+    uint32_t idx = (uint32_t)(((uint64_t)o[1] * failed) >> 32); /* gen_range(0..num_failed) */
+    for (uint32_t subj = 0; subj < w->s; ++subj) {
+      if ((int32_t)subj == w->member_subj[m] || w->v_kind[row + subj] != ORC_K_KNOWN ||
+          w->v_status[row + subj] != ORC_ST_FAILED)
+        continue;
+      if (idx-- == 0) {
+        target[m] = subj;
+        break;
+      }
+    }
+    if (w->alive[w->subj_member[target[m]]]) {
+      orc_handle_node_join(w, m, target[m]);
+      joins++;
+    }
+  }
+  return joins;
 }

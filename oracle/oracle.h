@@ -239,6 +239,13 @@ typedef struct {
   uint64_t* dlog;  /* [n][dcap][3] */
   uint32_t* dcnt;  /* [n] */
   uint32_t dcap;
+  /* snapshotter per member (orc_world_enable_snapshot; snapshot.rs): the alive set as a
+   * bitset over subjects, and {last event clock, last query clock, last clock at leave,
+   * flags (bit 0: leaving -- recording stopped)} */
+  uint32_t* snap_bits; /* [n][snap_w] */
+  uint32_t snap_w;
+  int32_t snap_rejoin; /* Options::rejoin_after_leave */
+  uint64_t* snap_sn;   /* [n][4] */
 } orc_world;
 
 typedef struct {
@@ -424,6 +431,51 @@ uint64_t orc_swim_tick(orc_swim* w, uint32_t now);
 /* as rsf_swim_dump: unknown entries read as (255, 0, 0, 0); confirmations only while suspect */
 void orc_swim_dump(const orc_swim* w, uint64_t first, uint64_t count, uint8_t* state, uint32_t* inc, uint32_t* change,
                    uint8_t* nconf, uint32_t* self_inc);
+
+/* ---- Snapshot log (core/src/snapshot.rs) --------------------------------- */
+/* record tags (snapshot.rs:196-203); a node is [u32 LE len][node bytes], here the node
+ * bytes are the subject index as u32 LE (the model's node identity) */
+enum { ORC_SNAP_ALIVE = 0, ORC_SNAP_NOT_ALIVE = 1, ORC_SNAP_CLOCK = 2, ORC_SNAP_EVENT_CLOCK = 3,
+       ORC_SNAP_QUERY_CLOCK = 4, ORC_SNAP_COORDINATE = 5, ORC_SNAP_LEAVE = 6, ORC_SNAP_COMMENT = 7 };
+enum { ORC_SNAP_ERR_RECORD = -1, ORC_SNAP_ERR_TRUNCATED = -2, ORC_SNAP_ERR_NODE = -3 };
+/* open_and_replay_snapshot (snapshot.rs:233-345): alive bitset over s subjects and the
+ * last clock / event clock / query clock; 0 or ORC_SNAP_ERR_* */
+int orc_snapshot_replay(const uint8_t* file, uint64_t len, int rejoin_after_leave, uint32_t s, uint32_t* alive_bits,
+                        uint64_t clocks[3]);
+/* one Snapshotter writing an append-only log in memory (Snapshot::stream and the
+ * process_* handlers, snapshot.rs:588-800, compaction included) */
+typedef struct {
+  uint8_t* buf;
+  uint64_t len, cap, offset, min_compact, compactions;
+  uint32_t* alive;
+  uint32_t s;
+  uint64_t last_clock, last_event_clock, last_query_clock;
+  int leaving, rejoin;
+} orc_snapshotter;
+/* replays `file` (may be empty) and continues its log: open_and_replay_snapshot + from_replay_result */
+int orc_snapshotter_open(orc_snapshotter* sp, uint32_t s, const uint8_t* file, uint64_t len, uint64_t min_compact,
+                         int rejoin_after_leave);
+void orc_snapshotter_free(orc_snapshotter* sp);
+void orc_snapshotter_user_event(orc_snapshotter* sp, uint64_t ltime);
+void orc_snapshotter_query(orc_snapshotter* sp, uint64_t ltime);
+/* MemberEvent (ev: 0 join, 1 leave, 2 failed, others ignored) with the clock's current time */
+void orc_snapshotter_member_event(orc_snapshotter* sp, uint32_t ev, uint32_t subj, uint64_t clock_time);
+void orc_snapshotter_update_clock(orc_snapshotter* sp, uint64_t clock_time);
+void orc_snapshotter_leave(orc_snapshotter* sp);
+
+/* the world's snapshotters: enable (alive set = each member's known Alive/Leaving
+ * subjects), the member's snapshot file as it would be at shutdown (a compacted
+ * prefix; after a leave the Leave record and the shutdown clock), and a restart of a
+ * member from a file (Serf::new with snapshot_path, base.rs:122-204: replay, clocks
+ * witnessed, event/query min times, fresh state, rejoin of the replayed nodes) */
+int orc_world_enable_snapshot(orc_world* w, int rejoin_after_leave);
+uint64_t orc_world_snapshot_encode(const orc_world* w, uint32_t m, uint8_t* out);
+int orc_world_restart(orc_world* w, uint32_t m, const uint8_t* file, uint64_t len);
+
+/* Reconnector tick (base.rs:632-701) at every live member; target[m] = the failed subject
+ * it tried (0xFFFFFFFF: none).  A try succeeds when the target member is up, and then
+ * memberlist's join notifies handle_node_join.  Returns the successful joins. */
+uint32_t orc_world_reconnect(orc_world* w, uint32_t tick, uint32_t* target);
 
 #ifdef __cplusplus
 }

@@ -63,3 +63,8 @@ def declare(L):
     sig("rsf_gossip_round_merge_buckets", [VP, C.c_uint32])
     sig("rsf_gossip_bucket_status", [VP, C.POINTER(C.c_int)])
     sig("rsf_gossip_dump_deliveries", [VP, VP, C.c_uint64, P64])
+    sig("rsf_gossip_enable_snapshot", [VP, i])
+    sig("rsf_gossip_snapshot_encode", [VP, C.c_uint64, C.c_uint64, VP, VP, C.c_uint64, P64])
+    sig("rsf_gossip_restart", [VP, P32, C.c_uint32, P8, P64, C.POINTER(C.c_int32)])
+    sig("rsf_gossip_dump_snapshot", [VP, P32, P64])
+    sig("rsf_gossip_reconnect", [VP, C.c_uint32, VP])

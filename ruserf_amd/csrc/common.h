@@ -18,6 +18,7 @@ enum : uint32_t {
   kPurposeVProbe = 3,  // Vivaldi synthetic probe: neighbour slot + jitter
   kPurposeNbr = 5,     // Vivaldi fixed neighbour set
   kPurposePos = 6,     // Vivaldi ground-truth positions
+  kPurposeReconnect = 7,  // Reconnector: throttle draw + failed-member pick
 };
 
 struct u32x4 {

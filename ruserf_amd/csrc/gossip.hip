@@ -398,8 +398,12 @@ __global__ void __launch_bounds__(256) ml_kernel(GCfg c, GState s, const rsf_ml_
     }
     if (al && m != sm) {
       ViewE* v = s.view + l * c.S + subj;
-      if (ml[e].kind == RSF_ML_JOIN) h_node_join(v, r, subj);
-      else h_node_leave(v, r, subj, c.now);
+      if (ml[e].kind == RSF_ML_JOIN) {
+        h_node_join(v, r, subj);
+        snap_member(c, s, l, subj, true);
+      } else if (h_node_leave(v, r, subj, c.now) & RSF_F_MEMBER_EVENT) {
+        snap_member(c, s, l, subj, false);
+      }
       touched = true;
     }
     if (sm == m && ml[e].set_alive == 0) al = false;
@@ -489,6 +493,14 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
     case RSF_ACT_LEAVE_SELF: {
       r.serf_state = kSerfLeaving;
       uint64_t lt = r.clock;
+      if (s.snap_sn && !(s.snap_sn[l * 4 + 3] & 1)) {
+        // Snapshot::leave (snapshot.rs:568-586): the clock ticker's last value, then the
+        // alive set is dropped (unless rejoin_after_leave) and recording stops
+        s.snap_sn[l * 4 + 2] = lt ? lt - 1 : 0;
+        s.snap_sn[l * 4 + 3] |= 1;
+        if (!c.snap_rejoin)
+          for (uint32_t k = 0; k < c.snap_w; ++k) s.snap_bits[l * c.snap_w + k] = 0;
+      }
       r.clock++;
       uint32_t subj = (uint32_t)r.subj;
       h_leave_intent(s.view + l * c.S + subj, r, subj, lt, false, ref, c.now);
@@ -2068,7 +2080,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   g->sort_tmp, g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
                   g->scan_tmp, g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
                   g->grp_slot, g->grp_off, g->stage_dec, g->grp_scan_tmp, s.dlog, s.dcnt,
-                  g->bkt_send, g->bkt_recv, g->d_rstart, g->d_rend, g->d_wstart};
+                  g->bkt_send, g->bkt_recv, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn};
   for (void* p : ptrs)
     if (p) hipFree(p);
   g->scratch.release();
@@ -2939,6 +2951,410 @@ int rsf_gossip_last_round_stats(rsf_gossip* g, uint64_t* sent, uint64_t* merged)
   }
   if (sent) *sent = nv;
   if (merged) *merged = g->merged_from_stage ? nv : g->last_merged;
+  return RSF_OK;
+}
+
+}  // extern "C"
+
+// ======================================================================================
+// Snapshot log (core/src/snapshot.rs) and Reconnector (core/src/serf/base.rs:632-701)
+// ======================================================================================
+// Per member, the snapshotter's state lives beside the member state: the alive set as a
+// bitset over subjects (updated by ml_kernel's Join / Leave / Failed member events), the
+// largest delivered event / query ltime (h_user_event / h_query), the clock at a leave.
+// The snapshot file is produced on demand in its compacted form (snapshot.rs:786-880):
+// [Alive node]* Clock EventClock QueryClock, then after a leave: Leave and the shutdown
+// clock.  Records: node [tag][u32 LE 4][u32 LE subject], clocks [tag][u64 LE].
+namespace {
+
+constexpr uint8_t kSnapAlive = 0, kSnapClock = 2, kSnapEventClock = 3, kSnapQueryClock = 4, kSnapLeave = 6;
+
+__global__ void __launch_bounds__(256) snap_init_kernel(GCfg c, GState s) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= c.n_loc * c.snap_w) return;
+  const uint64_t l = t / c.snap_w;
+  const uint32_t k = (uint32_t)(t % c.snap_w);
+  uint32_t bits = 0;
+  for (uint32_t b = 0; b < 32; ++b) {
+    const uint32_t j = k * 32 + b;
+    if (j >= c.S) break;
+    const uint32_t meta = s.view[l * c.S + j].meta;
+    const uint32_t st = vstatus(meta);
+    if (vkind(meta) == RSF_KIND_KNOWN && (st == RSF_STATUS_ALIVE || st == RSF_STATUS_LEAVING)) bits |= 1u << b;
+  }
+  s.snap_bits[t] = bits;
+  if (k == 0) {
+    for (int i = 0; i < 4; ++i) s.snap_sn[l * 4 + i] = 0;
+  }
+}
+
+__device__ __forceinline__ uint64_t snap_now_clock(const GState& s, uint64_t l) {
+  const uint64_t ck = s.clock[l];
+  return ck ? ck - 1 : 0;  // update_clock: clock.time() - 1, saturating (snapshot.rs:713-720)
+}
+
+__global__ void __launch_bounds__(256) snap_size_kernel(GCfg c, GState s, uint64_t l0, uint64_t count,
+                                                        uint64_t* __restrict__ sizes) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > count) return;
+  if (i == count) {
+    sizes[i] = 0;
+    return;
+  }
+  const uint64_t l = l0 + i;
+  uint64_t alive = 0;
+  for (uint32_t k = 0; k < c.snap_w; ++k) alive += __popc(s.snap_bits[l * c.snap_w + k]);
+  uint64_t b = alive * 9 + 27;
+  const uint64_t* sn = s.snap_sn + l * 4;
+  if (sn[3] & 1) b += 1 + (snap_now_clock(s, l) > sn[2] ? 9 : 0);
+  sizes[i] = b;
+}
+
+__device__ __forceinline__ uint8_t* snap_put_clock(uint8_t* p, uint8_t tag, uint64_t t) {
+  p[0] = tag;
+  for (int i = 0; i < 8; ++i) p[1 + i] = (uint8_t)(t >> (8 * i));
+  return p + 9;
+}
+
+__global__ void __launch_bounds__(256) snap_encode_kernel(GCfg c, GState s, uint64_t l0, uint64_t count,
+                                                          const uint64_t* __restrict__ offs, uint8_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const uint64_t l = l0 + i;
+  uint8_t* p = out + offs[i];
+  for (uint32_t k = 0; k < c.snap_w; ++k) {
+    uint32_t w = s.snap_bits[l * c.snap_w + k];
+    while (w) {
+      const uint32_t j = k * 32 + (uint32_t)__builtin_ctz(w);
+      w &= w - 1;
+      p[0] = kSnapAlive;
+      p[1] = 4;
+      p[2] = p[3] = p[4] = 0;
+      p[5] = (uint8_t)j;
+      p[6] = (uint8_t)(j >> 8);
+      p[7] = (uint8_t)(j >> 16);
+      p[8] = (uint8_t)(j >> 24);
+      p += 9;
+    }
+  }
+  const uint64_t* sn = s.snap_sn + l * 4;
+  const bool leaving = sn[3] & 1;
+  const uint64_t now = snap_now_clock(s, l);
+  p = snap_put_clock(p, kSnapClock, leaving ? sn[2] : now);
+  p = snap_put_clock(p, kSnapEventClock, sn[0]);
+  p = snap_put_clock(p, kSnapQueryClock, sn[1]);
+  if (leaving) {
+    *p++ = kSnapLeave;
+    if (now > sn[2]) p = snap_put_clock(p, kSnapClock, now);  // the shutdown's update_clock
+  }
+}
+
+// open_and_replay_snapshot (snapshot.rs:233-345) of one restarted member's file into
+// scratch (bits, clocks); res = 0 or RSF_SNAP_ERR_*
+__global__ void __launch_bounds__(256) snap_replay_kernel(GCfg c, const uint8_t* __restrict__ files,
+                                                          const uint64_t* __restrict__ offs, uint32_t n,
+                                                          uint32_t* __restrict__ bits, uint64_t* __restrict__ clk,
+                                                          int32_t* __restrict__ res) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t* b = bits + (uint64_t)i * c.snap_w;
+  uint64_t* ck = clk + (uint64_t)i * 3;
+  for (uint32_t k = 0; k < c.snap_w; ++k) b[k] = 0;
+  ck[0] = ck[1] = ck[2] = 0;
+  const uint8_t* f = files + offs[i];
+  const uint64_t len = offs[i + 1] - offs[i];
+  uint64_t p = 0;
+  int32_t rc = 0;
+  while (p < len && !rc) {
+    const uint8_t tag = f[p++];
+    if (tag == 0 || tag == 1) {
+      if (len - p < 4) { rc = RSF_SNAP_ERR_TRUNCATED; break; }
+      const uint32_t nl = f[p] | f[p + 1] << 8 | f[p + 2] << 16 | (uint32_t)f[p + 3] << 24;
+      p += 4;
+      if (len - p < nl) { rc = RSF_SNAP_ERR_TRUNCATED; break; }
+      if (nl != 4) { rc = RSF_SNAP_ERR_NODE; break; }
+      const uint32_t j = f[p] | f[p + 1] << 8 | f[p + 2] << 16 | (uint32_t)f[p + 3] << 24;
+      p += 4;
+      if (j >= c.S) { rc = RSF_SNAP_ERR_NODE; break; }
+      if (tag == 0) b[j >> 5] |= 1u << (j & 31);
+      else b[j >> 5] &= ~(1u << (j & 31));
+    } else if (tag >= 2 && tag <= 4) {
+      if (len - p < 8) { rc = RSF_SNAP_ERR_TRUNCATED; break; }
+      uint64_t t = 0;
+      for (int k = 7; k >= 0; --k) t = (t << 8) | f[p + k];
+      ck[tag - 2] = t;
+      p += 8;
+    } else if (tag == 5 || tag == 7) {
+      // Coordinate / Comment: nothing to replay
+    } else if (tag == 6) {
+      if (c.snap_rejoin) continue;  // a previous leave is ignored when re-joining
+      for (uint32_t k = 0; k < c.snap_w; ++k) b[k] = 0;
+      ck[0] = ck[1] = ck[2] = 0;
+    } else {
+      rc = RSF_SNAP_ERR_RECORD;
+    }
+  }
+  res[i] = rc;
+}
+
+// a fresh process for every restarted member whose file replayed: no member states or
+// intents, no queued broadcasts, empty event / query buffers (one block per member)
+__global__ void __launch_bounds__(256) snap_reset_kernel(GCfg c, GState s, const uint32_t* __restrict__ members,
+                                                         const int32_t* __restrict__ res) {
+  const uint32_t i = blockIdx.x;
+  if (res[i] < 0) return;
+  const uint64_t l = members[i] - c.lo;
+  for (uint32_t j = threadIdx.x; j < c.S; j += blockDim.x) s.view[l * c.S + j] = ViewE{0ull, 0u, 0u};
+  for (uint32_t j = threadIdx.x; j < 3 * c.qcap; j += blockDim.x) {
+    s.q_rumor[l * 3 * c.qcap + j] = kEmpty;
+    s.q_seq[l * 3 * c.qcap + j] = 0;
+    s.q_txlen[l * 3 * c.qcap + j] = 0;
+  }
+  if (threadIdx.x < 3) s.q_next_seq[l * 3 + threadIdx.x] = 0;
+  for (uint32_t j = threadIdx.x; j < c.ebuf; j += blockDim.x) {
+    s.eb_ltime[l * c.ebuf + j] = 0;
+    s.eb_cnt[l * c.ebuf + j] = 0;
+  }
+  for (uint32_t j = threadIdx.x; j < c.ebuf * c.slot_k; j += blockDim.x) s.eb_keys[l * c.ebuf * c.slot_k + j] = 0;
+  for (uint32_t j = threadIdx.x; j < c.qbuf; j += blockDim.x) {
+    s.qb_ltime[l * c.qbuf + j] = 0;
+    s.qb_cnt[l * c.qbuf + j] = 0;
+  }
+  for (uint32_t j = threadIdx.x; j < c.qbuf * c.slot_k; j += blockDim.x) s.qb_ids[l * c.qbuf * c.slot_k + j] = 0;
+}
+
+// Serf::new with a snapshot (base.rs:122-204): clocks start at 1 and witness the replayed
+// ones, events / queries up to the replayed clocks are not delivered again, the
+// snapshotter continues from the replay; then handle_rejoin (base.rs:1741-1770):
+// memberlist.join to the replayed nodes until one is up, after which memberlist's state
+// exchange notifies a join of every live member (res = 1 rejoined, 0 alone)
+__global__ void __launch_bounds__(256) snap_restart_kernel(GCfg c, GState s, const uint32_t* __restrict__ members,
+                                                           uint32_t n, const uint32_t* __restrict__ bits,
+                                                           const uint64_t* __restrict__ clk,
+                                                           int32_t* __restrict__ res) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || res[i] < 0) return;
+  const uint64_t l = members[i] - c.lo;
+  const uint64_t* ck = clk + (uint64_t)i * 3;
+  MRegs r;
+  load_regs(s, l, r);
+  r.clock = r.eclock = r.qclock = 1;
+  witness(r.clock, ck[0]);
+  witness(r.eclock, ck[1]);
+  witness(r.qclock, ck[2]);
+  r.serf_state = kSerfAlive;
+  s.emin[l] = ck[1] + 1;
+  s.qmin[l] = ck[2] + 1;
+  if (r.subj >= 0) s.refute_cnt[r.subj] = 0;
+  uint32_t* row = s.snap_bits + l * c.snap_w;
+  for (uint32_t k = 0; k < c.snap_w; ++k) row[k] = bits[(uint64_t)i * c.snap_w + k];
+  uint64_t* sn = s.snap_sn + l * 4;
+  sn[0] = ck[1];
+  sn[1] = ck[2];
+  sn[2] = 0;
+  sn[3] = 0;
+  bool joined = false;
+  for (uint32_t j = 0; j < c.S && !joined; ++j)
+    if ((row[j >> 5] >> (j & 31) & 1) && (int32_t)j != r.subj && s.alive[s.subj_member[j]]) joined = true;
+  if (joined)
+    for (uint32_t j = 0; j < c.S; ++j)
+      if ((int32_t)j != r.subj && s.alive[s.subj_member[j]]) {
+        h_node_join(s.view + l * c.S + j, r, j);
+        snap_member(c, s, l, j, true);
+      }
+  store_regs(s, l, r);
+  res[i] = joined ? 1 : 0;
+}
+
+// Reconnector tick (base.rs:647-690), one wave per member: count the failed / left /
+// known members of the view; with probability failed / (known - failed - left) try a
+// uniformly drawn failed member; the try succeeds when that member is up, and memberlist's
+// join then notifies handle_node_join
+__global__ void __launch_bounds__(256) reconnect_kernel(GCfg c, GState s, uint32_t tick, uint32_t* __restrict__ target) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint64_t l = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  if (l >= c.n_loc) return;
+  const uint32_t m = (uint32_t)(c.lo + l);
+  if (target && lane == 0) target[l] = kEmpty;
+  if (!s.alive[m]) return;
+  const int32_t own = s.member_subj[l];
+  const ViewE* row = s.view + l * c.S;
+  uint32_t failed = 0, left = 0, known = 1;  // members.states holds the local node too
+  for (uint32_t j0 = 0; j0 < c.S; j0 += kWave) {
+    const uint32_t j = j0 + lane;
+    uint32_t meta = 0;
+    if (j < c.S && (int32_t)j != own) meta = row[j].meta;
+    const bool kn = vkind(meta) == RSF_KIND_KNOWN;
+    known += (uint32_t)__popcll(__ballot(kn));
+    failed += (uint32_t)__popcll(__ballot(kn && vstatus(meta) == RSF_STATUS_FAILED));
+    left += (uint32_t)__popcll(__ballot(kn && vstatus(meta) == RSF_STATUS_LEFT));
+  }
+  if (!failed) return;
+  uint32_t alive_n = known - failed - left;
+  if (alive_n < 1) alive_n = 1;
+  const float prob = __fdiv_rn((float)failed, (float)alive_n);
+  const u32x4 o = philox4x32_10(0, kPurposeReconnect << 24, m, tick, c.k0, c.k1);
+  const float rr = (float)(o.x >> 8) * (1.0f / 16777216.0f);  // rng.gen::<f32>()
+  if (rr > prob) return;
+  uint32_t idx = mulhi32(o.y, failed);  // gen_range(0..num_failed)
+  uint32_t tj = kEmpty;
+  for (uint32_t j0 = 0; j0 < c.S && tj == kEmpty; j0 += kWave) {
+    const uint32_t j = j0 + lane;
+    uint32_t meta = 0;
+    if (j < c.S && (int32_t)j != own) meta = row[j].meta;
+    const bool fa = vkind(meta) == RSF_KIND_KNOWN && vstatus(meta) == RSF_STATUS_FAILED;
+    const unsigned long long mask = __ballot(fa);
+    const uint32_t cnt = (uint32_t)__popcll(mask);
+    if (idx < cnt) {
+      const bool hit = fa && (uint32_t)__popcll(mask & ((1ull << lane) - 1)) == idx;
+      const unsigned long long hm = __ballot(hit);
+      tj = j0 + (uint32_t)__builtin_ctzll(hm);
+    } else {
+      idx -= cnt;
+    }
+  }
+  if (lane != 0) return;
+  if (target) target[l] = tj;
+  if (!s.alive[s.subj_member[tj]]) return;
+  MRegs r;
+  load_regs(s, l, r);
+  h_node_join(s.view + l * c.S + tj, r, tj);
+  snap_member(c, s, l, tj, true);
+  store_regs(s, l, r);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rsf_gossip_enable_snapshot(rsf_gossip* g, int rejoin_after_leave) {
+  if (!g) return gerr("null context");
+  GCfg& c = g->c;
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  if (g->s.snap_bits) hipFree(g->s.snap_bits);
+  if (g->s.snap_sn) hipFree(g->s.snap_sn);
+  g->s.snap_bits = nullptr;
+  g->s.snap_sn = nullptr;
+  c.snap_w = (c.S + 31) / 32;
+  c.snap_rejoin = rejoin_after_leave ? 1 : 0;
+  int rc;
+  if ((rc = rsf::dmalloc((void**)&g->s.snap_bits, c.n_loc * c.snap_w * 4)) ||
+      (rc = rsf::dmalloc((void**)&g->s.snap_sn, c.n_loc * 32)))
+    return rc;
+  const uint64_t nt = c.n_loc * c.snap_w;
+  hipLaunchKernelGGL(snap_init_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, g->stream, c, g->s);
+  RSF_HIP(hipGetLastError());
+  return RSF_OK;
+}
+
+int rsf_gossip_snapshot_encode(rsf_gossip* g, uint64_t first, uint64_t count, uint64_t* offsets, uint8_t* out,
+                               uint64_t out_cap, uint64_t* total) {
+  if (!g || !offsets || !total) return gerr("null argument");
+  const GCfg& c = g->c;
+  if (!g->s.snap_bits) return gerr("snapshot not enabled (rsf_gossip_enable_snapshot)");
+  if (first < c.lo || first + count > c.lo + c.n_loc || count == 0 || count > 0x7FFFFFFFull)
+    return gerr("member range outside this context's shard");
+  RSF_HIP(hipSetDevice(g->device));
+  hipStream_t st = g->stream;
+  const uint64_t l0 = first - c.lo;
+  uint64_t* sizes = nullptr;
+  void* tmp = nullptr;
+  size_t tb = 0;
+  int rc;
+  if ((rc = rsf::dmalloc((void**)&sizes, (count + 1) * 8))) return rc;
+  hipLaunchKernelGGL(snap_size_kernel, dim3((unsigned)((count + 256) / 256)), dim3(256), 0, st, c, g->s, l0, count,
+                     sizes);
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, tb, sizes, offsets, (int)(count + 1), st) != hipSuccess ||
+      (rc = rsf::dmalloc(&tmp, tb)) ||
+      hipcub::DeviceScan::ExclusiveSum(tmp, tb, sizes, offsets, (int)(count + 1), st) != hipSuccess) {
+    hipFree(sizes);
+    if (tmp) hipFree(tmp);
+    return rc ? rc : rsf::set_error(RSF_ERR_HIP, "snapshot offset scan failed");
+  }
+  RSF_HIP(hipMemcpyAsync(total, offsets + count, 8, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipStreamSynchronize(st));
+  hipFree(sizes);
+  hipFree(tmp);
+  if (!out) return RSF_OK;
+  if (*total > out_cap) return rsf::set_error(RSF_ERR_OVERFLOW, "snapshot output capacity exceeded");
+  hipLaunchKernelGGL(snap_encode_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, c, g->s, l0, count,
+                     (const uint64_t*)offsets, out);
+  RSF_HIP(hipGetLastError());
+  return RSF_OK;
+}
+
+int rsf_gossip_restart(rsf_gossip* g, const uint32_t* members, uint32_t n, const uint8_t* files,
+                       const uint64_t* offsets, int32_t* result) {
+  if (!g || (n && (!members || !offsets || !result))) return gerr("null argument");
+  const GCfg& c = g->c;
+  if (!g->s.snap_bits) return gerr("snapshot not enabled (rsf_gossip_enable_snapshot)");
+  if (!n) return RSF_OK;
+  std::vector<uint32_t> sorted(members, members + n);
+  std::sort(sorted.begin(), sorted.end());
+  for (uint32_t i = 0; i < n; ++i) {
+    if (sorted[i] < c.lo || sorted[i] >= c.lo + c.n_loc) return gerr("restarted member outside this shard");
+    if (i && sorted[i] == sorted[i - 1]) return gerr("a member is restarted twice in one call");
+    if (offsets[i + 1] < offsets[i]) return gerr("snapshot offsets must not decrease");
+  }
+  const uint64_t bytes = offsets[n] - offsets[0];
+  if (bytes && !files) return gerr("null snapshot files");
+  std::vector<uint64_t> offs(n + 1);
+  for (uint32_t i = 0; i <= n; ++i) offs[i] = offsets[i] - offsets[0];
+  RSF_HIP(hipSetDevice(g->device));
+  hipStream_t st = g->stream;
+  uint32_t *d_mem = nullptr, *d_bits = nullptr;
+  uint64_t *d_offs = nullptr, *d_clk = nullptr;
+  uint8_t* d_files = nullptr;
+  int32_t* d_res = nullptr;
+  int rc;
+  auto release = [&]() {
+    for (void* p : {(void*)d_mem, (void*)d_bits, (void*)d_offs, (void*)d_clk, (void*)d_files, (void*)d_res})
+      if (p) hipFree(p);
+  };
+  if ((rc = rsf::dmalloc((void**)&d_mem, (size_t)n * 4)) || (rc = rsf::dmalloc((void**)&d_bits, (size_t)n * c.snap_w * 4)) ||
+      (rc = rsf::dmalloc((void**)&d_offs, (size_t)(n + 1) * 8)) || (rc = rsf::dmalloc((void**)&d_clk, (size_t)n * 24)) ||
+      (rc = rsf::dmalloc((void**)&d_files, std::max<uint64_t>(bytes, 1))) || (rc = rsf::dmalloc((void**)&d_res, (size_t)n * 4))) {
+    release();
+    return rc;
+  }
+  bool ok = hipMemcpyAsync(d_mem, members, (size_t)n * 4, hipMemcpyHostToDevice, st) == hipSuccess &&
+            hipMemcpyAsync(d_offs, offs.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, st) == hipSuccess &&
+            (!bytes || hipMemcpyAsync(d_files, files + offsets[0], bytes, hipMemcpyHostToDevice, st) == hipSuccess);
+  if (ok) {
+    hipLaunchKernelGGL(snap_replay_kernel, dim3((n + 255) / 256), dim3(256), 0, st, c, (const uint8_t*)d_files,
+                       (const uint64_t*)d_offs, n, d_bits, d_clk, d_res);
+    hipLaunchKernelGGL(snap_reset_kernel, dim3(n), dim3(256), 0, st, c, g->s, (const uint32_t*)d_mem,
+                       (const int32_t*)d_res);
+    hipLaunchKernelGGL(snap_restart_kernel, dim3((n + 255) / 256), dim3(256), 0, st, c, g->s, (const uint32_t*)d_mem,
+                       n, (const uint32_t*)d_bits, (const uint64_t*)d_clk, d_res);
+    ok = hipGetLastError() == hipSuccess &&
+         hipMemcpyAsync(result, d_res, (size_t)n * 4, hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipStreamSynchronize(st) == hipSuccess;
+  }
+  release();
+  return ok ? RSF_OK : rsf::set_error(RSF_ERR_HIP, "snapshot restart failed");
+}
+
+int rsf_gossip_reconnect(rsf_gossip* g, uint32_t tick, uint32_t* target) {
+  if (!g) return gerr("null context");
+  const GCfg& c = g->c;
+  RSF_HIP(hipSetDevice(g->device));
+  const uint64_t threads = c.n_loc * kWave;
+  hipLaunchKernelGGL(reconnect_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, g->stream, c, g->s, tick,
+                     target);
+  RSF_HIP(hipGetLastError());
+  return RSF_OK;
+}
+
+int rsf_gossip_dump_snapshot(rsf_gossip* g, uint32_t* bits, uint64_t* state) {
+  if (!g || !bits || !state) return gerr("null argument");
+  const GCfg& c = g->c;
+  if (!g->s.snap_bits) return gerr("snapshot not enabled (rsf_gossip_enable_snapshot)");
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemcpyAsync(bits, g->s.snap_bits, c.n_loc * c.snap_w * 4, hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipMemcpyAsync(state, g->s.snap_sn, c.n_loc * 32, hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
   return RSF_OK;
 }
 

@@ -36,6 +36,7 @@ struct GCfg {
   // stored at id & rmask (rmask = 2^(rbits+1) - 1: two generations resident, by parity)
   uint32_t rbits, rmask;
   uint32_t dcap;  // delivery log entries per member (0: log off)
+  uint32_t snap_w, snap_rejoin;  // snapshotter: bitset words per member, rejoin_after_leave
 };
 
 // view entry: members.states[subject] (status, status_time) or recent_intents[subject]
@@ -69,6 +70,10 @@ struct GState {
   uint4* rbody;    // per rumor id: the rumor without its key (ltime, subject, type, flags, msg_len), 16 B
   uint4* dlog;     // [n_loc][dcap] user events delivered to the application: ltime | cc << 63, key
   uint32_t* dcnt;  // [n_loc] deliveries since the log was cleared
+  // snapshotter per member (rsf_gossip_enable_snapshot; null: off): the alive set as a bitset
+  // over subjects, and {last event clock, last query clock, last clock at leave, flags}
+  uint32_t* snap_bits;  // [n_loc][snap_w]
+  uint64_t* snap_sn;    // [n_loc][4]; flags bit 0: leaving (recording stopped)
 };
 
 // per-member scalar state held in registers while a kernel works on it
@@ -278,6 +283,21 @@ __device__ __forceinline__ int h_node_leave(ViewE* e, MRegs& r, uint32_t subj, u
   return RSF_F_MEMBER_EVENT;
 }
 
+// the snapshotter's process_user_event / process_query_event (snapshot.rs:663-684): the
+// largest ltime handed to the application (which = 0: events, 1: queries)
+__device__ __forceinline__ void snap_clock(const GState& s, uint64_t l, int which, uint64_t L) {
+  if (!s.snap_sn) return;
+  uint64_t* sn = s.snap_sn + l * 4;
+  if (!(sn[3] & 1) && L > sn[which]) sn[which] = L;
+}
+// process_member_event (snapshot.rs:686-711): Join adds the node, Leave / Failed remove it
+__device__ __forceinline__ void snap_member(const GCfg& c, const GState& s, uint64_t l, uint32_t subj, bool join) {
+  if (!s.snap_bits || (s.snap_sn[l * 4 + 3] & 1)) return;
+  uint32_t* w = s.snap_bits + l * c.snap_w + (subj >> 5);
+  const uint32_t b = 1u << (subj & 31);
+  *w = join ? (*w | b) : (*w & ~b);
+}
+
 // one delivery (event_tx.send of a UserEvent, base.rs:831-835) into the member's log slot
 __device__ __forceinline__ void dlog_put(const GCfg& c, const GState& s, uint64_t l, MRegs& r, uint64_t L,
                                          uint64_t key, bool cc) {
@@ -318,6 +338,7 @@ __device__ __forceinline__ int h_user_event(const GCfg& c, const GState& s, uint
   }
   r.digest = digest_mix(digest_mix(r.digest, kDigUser ^ key), L);
   dlog_put(c, s, l, r, L, key, cc);
+  snap_clock(s, l, 0, L);
   return RSF_F_REBROADCAST | RSF_F_DELIVER;
 }
 
@@ -347,6 +368,7 @@ __device__ __forceinline__ int h_query(const GCfg& c, const GState& s, uint64_t 
     s.qb_cnt[slot] = 1;
   }
   r.digest = digest_mix(digest_mix(r.digest, kDigQuery ^ id), L);
+  snap_clock(s, l, 1, L);
   return (no_broadcast ? 0 : RSF_F_REBROADCAST) | RSF_F_DELIVER;
 }
 

@@ -88,6 +88,7 @@ def _p(a):
 class GossipEngine:
     def __init__(self, cfg: GossipConfig, device=0):
         self.cfg = cfg
+        self.device = int(device)
         self.lo, self.hi = cfg.shard if cfg.shard is not None else (0, cfg.n_members)
         self.n_loc = self.hi - self.lo
         h = C.c_void_p()
@@ -263,6 +264,62 @@ class GossipEngine:
         n = C.c_uint64()
         check(lib().rsf_gossip_dump_deliveries(self._h, _p(out), cap, C.byref(n)))
         return out[: n.value]
+
+    # ---- snapshot log + restart (snapshot.rs; base.rs:122-204) and the Reconnector
+    def enable_snapshot(self, rejoin_after_leave=False):
+        """Start every member's snapshotter (Options::snapshot_path set)."""
+        self._snap_w = (self.cfg.n_subjects + 31) // 32
+        check(lib().rsf_gossip_enable_snapshot(self._h, int(bool(rejoin_after_leave))))
+
+    def snapshot_files(self, first=None, count=None):
+        """The snapshot files of members [first, first+count) (global ids), compacted:
+        (offsets u64[count+1], bytes u8) on the host, built on the device."""
+        import torch
+        first = self.lo if first is None else int(first)
+        count = self.n_loc - (first - self.lo) if count is None else int(count)
+        dev = torch.device("cuda", self.device)
+        offs = torch.empty(count + 1, dtype=torch.int64, device=dev)
+        total = C.c_uint64()
+        check(lib().rsf_gossip_snapshot_encode(self._h, first, count, C.c_void_p(offs.data_ptr()), None, 0,
+                                               C.byref(total)))
+        out = torch.empty(max(1, total.value), dtype=torch.uint8, device=dev)
+        check(lib().rsf_gossip_snapshot_encode(self._h, first, count, C.c_void_p(offs.data_ptr()),
+                                               C.c_void_p(out.data_ptr()), out.numel(), C.byref(total)))
+        self.sync()
+        return offs.cpu().numpy().view(np.uint64), out[: total.value].cpu().numpy()
+
+    def restart(self, members, files):
+        """Restart members (global ids) from snapshot files (bytes each); per member 1 =
+        rejoined, 0 = alone, <0 = the file did not replay (member unchanged)."""
+        m = np.ascontiguousarray(members, dtype=np.uint32)
+        offs = np.zeros(len(m) + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum([len(f) for f in files])
+        blob = np.frombuffer(b"".join(bytes(f) for f in files) or b"\0", dtype=np.uint8).copy()
+        res = np.zeros(len(m), dtype=np.int32)
+        check(lib().rsf_gossip_restart(self._h, ptr(m, C.c_uint32), len(m), ptr(blob, C.c_uint8),
+                                       ptr(offs, C.c_uint64), res.ctypes.data_as(C.POINTER(C.c_int32))))
+        return res
+
+    def snapshot_state(self):
+        """(alive bits [n_loc][ceil(S/32)] u32, [n_loc][4] u64 {event clock, query clock,
+        clock at leave, flags})"""
+        bits = np.zeros((self.n_loc, self._snap_w), dtype=np.uint32)
+        st = np.zeros((self.n_loc, 4), dtype=np.uint64)
+        check(lib().rsf_gossip_dump_snapshot(self._h, ptr(bits, C.c_uint32), ptr(st, C.c_uint64)))
+        return bits, st
+
+    def reconnect(self, tick, target_ptr=None):
+        """One Reconnector tick at every member (asynchronous); with target_ptr (device,
+        n_loc u32) the tried subject per member (0xFFFFFFFF: none)."""
+        check(lib().rsf_gossip_reconnect(self._h, tick, C.c_void_p(target_ptr) if target_ptr else None))
+
+    def reconnect_targets(self, tick):
+        """reconnect(tick), returning the targets on the host (synchronises)."""
+        import torch
+        t = torch.empty(self.n_loc, dtype=torch.int32, device=torch.device("cuda", self.device))
+        self.reconnect(tick, t.data_ptr())
+        self.sync()
+        return t.cpu().numpy().view(np.uint32)
 
     def pruned(self):
         """Per member: live queue items its bounded queues dropped when full (cumulative)."""

@@ -84,7 +84,8 @@ class World(C.Structure):
                 ("rumors", C.POINTER(Rumor)), ("n_rumors", C.c_uint32), ("cap_rumors", C.c_uint32),
                 ("merges", C.c_uint64), ("sends", C.c_uint64), ("deliveries", C.c_uint64),
                 ("v_time", P32), ("now", C.c_uint32), ("q_pruned", P32), ("q_expired", P32),
-                ("gen", C.c_uint32), ("rbits", C.c_uint32), ("dlog", P64), ("dcnt", P32), ("dcap", C.c_uint32)]
+                ("gen", C.c_uint32), ("rbits", C.c_uint32), ("dlog", P64), ("dcnt", P32), ("dcap", C.c_uint32),
+                ("snap_bits", P32), ("snap_w", C.c_uint32), ("snap_rejoin", C.c_int32), ("snap_sn", P64)]
 
 
 class WorldCfg(C.Structure):
@@ -238,8 +239,32 @@ def lib():
     L.orc_swim_tick.restype = C.c_uint64
     L.orc_swim_dump.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, P8, P32, P32, P8, P32]
     L.orc_swim_dump.restype = None
+    L.orc_snapshot_replay.argtypes = [P8, C.c_uint64, C.c_int, C.c_uint32, P32, P64]
+    L.orc_snapshotter_open.argtypes = [C.POINTER(Snapshotter), C.c_uint32, P8, C.c_uint64, C.c_uint64, C.c_int]
+    L.orc_snapshotter_free.argtypes = [C.POINTER(Snapshotter)]
+    L.orc_snapshotter_free.restype = None
+    for f in ("orc_snapshotter_user_event", "orc_snapshotter_query", "orc_snapshotter_update_clock"):
+        getattr(L, f).argtypes = [C.POINTER(Snapshotter), C.c_uint64]
+        getattr(L, f).restype = None
+    L.orc_snapshotter_member_event.argtypes = [C.POINTER(Snapshotter), C.c_uint32, C.c_uint32, C.c_uint64]
+    L.orc_snapshotter_member_event.restype = None
+    L.orc_snapshotter_leave.argtypes = [C.POINTER(Snapshotter)]
+    L.orc_snapshotter_leave.restype = None
+    L.orc_world_enable_snapshot.argtypes = [C.POINTER(World), C.c_int]
+    L.orc_world_snapshot_encode.argtypes = [C.POINTER(World), C.c_uint32, P8]
+    L.orc_world_snapshot_encode.restype = C.c_uint64
+    L.orc_world_restart.argtypes = [C.POINTER(World), C.c_uint32, P8, C.c_uint64]
+    L.orc_world_reconnect.argtypes = [C.POINTER(World), C.c_uint32, P32]
+    L.orc_world_reconnect.restype = C.c_uint32
     _lib = L
     return L
+
+
+class Snapshotter(C.Structure):
+    _fields_ = [("buf", P8), ("len", C.c_uint64), ("cap", C.c_uint64), ("offset", C.c_uint64),
+                ("min_compact", C.c_uint64), ("compactions", C.c_uint64), ("alive", P32), ("s", C.c_uint32),
+                ("last_clock", C.c_uint64), ("last_event_clock", C.c_uint64), ("last_query_clock", C.c_uint64),
+                ("leaving", C.c_int), ("rejoin", C.c_int)]
 
 
 class OrcSwim(C.Structure):
