@@ -153,6 +153,22 @@ int rsf_vivaldi_gen_probes(rsf_vivaldi* v, uint32_t round, uint32_t* peer_out, u
 int rsf_vivaldi_observe(rsf_vivaldi* v, uint32_t slot, const uint32_t* peer, const uint64_t* rtt_ns,
                         int32_t* status_out, uint32_t round);
 
+/* memberlist's probe loop feeding the coordinates (memberlist is not
+ * vendored: parity unpinned).  rsf_vivaldi_probe: member lo+i probes neighbour slot
+ * (round mod peer_slots) on the synthetic network; the probe is acked when both processes
+ * are up (up: device, N bytes of global liveness), with rtt as rsf_vivaldi_gen_probes;
+ * a timed-out probe gets rtt UINT64_MAX (rsf_vivaldi_observe then leaves the member
+ * unchanged, as no notify_ping_complete happens) and acked 0.  Device pointers, shard_n
+ * each.  rsf_vivaldi_probe_acks: the acks on the wire -- for each acked probe the
+ * target's ack_payload ([PING_VERSION][Coordinate] of its current row) at off_out[i]
+ * (off_out: shard_n+1, an empty range for a timeout) in payload_out (>= shard_n x
+ * (29 + 8 dim) bytes), ready for rsf_vivaldi_observe_acks over members lo..lo+shard_n.
+ * Timed-out probes feed rsf_swim_probe_failures.  Asynchronous. */
+int rsf_vivaldi_probe(rsf_vivaldi* v, uint32_t round, const uint8_t* up, uint32_t* peer_out, uint64_t* rtt_ns_out,
+                      uint8_t* acked_out);
+int rsf_vivaldi_probe_acks(rsf_vivaldi* v, const uint32_t* peer, const uint8_t* acked, uint64_t* off_out,
+                           uint8_t* payload_out, uint64_t payload_cap);
+
 /* = SerfDelegate::ack_payload (core/src/serf/delegate.rs:659-701) for n members:
  * out + i*out_stride receives [PING_VERSION=1][Coordinate encoding] of member[i]'s
  * current coordinate (29 + 8*dim bytes).  Device pointers, asynchronous. */
@@ -279,9 +295,12 @@ typedef struct rsf_action {
 } rsf_action;
 
 /* memberlist-detected transitions applied at every live member (NotifyJoin /
- * NotifyLeave -> handle_node_join / handle_node_leave, base.rs:1167-1407) */
+ * NotifyLeave / NotifyUpdate -> handle_node_join / handle_node_leave / handle_node_update,
+ * base.rs:1167-1407, 1532-1583; an update emits the Update member event for a known member,
+ * tags are the host's) */
 #define RSF_ML_JOIN 1
 #define RSF_ML_LEAVE 2
+#define RSF_ML_UPDATE 3
 typedef struct rsf_ml_event {
   uint32_t subject, kind;
   uint32_t set_alive; /* 1: the subject's process becomes live first; 0: dead afterwards; 2: unchanged */
@@ -648,6 +667,13 @@ int rsf_swim_tick(rsf_swim* w, uint32_t now, uint64_t* n_fired);
  * tick, confirmations; and those receivers' own incarnations (host buffers) */
 int rsf_swim_dump(rsf_swim* w, uint64_t first, uint64_t count, uint8_t* state, uint32_t* incarnation,
                   uint32_t* change, uint8_t* n_confirm, uint32_t* self_incarnation);
+/* memberlist probeNode's failure path: receiver lo+i probed member target[i]
+ * and got no ack (acked[i] == 0): suspectNode{its entry's incarnation, target, from =
+ * receiver} when target is a tracked subject; a receiver whose process is down (up[] of
+ * N bytes, nullable) does not probe.  Device pointers (n_loc entries; flags_out nullable:
+ * RSF_SWIM_F_* per receiver), asynchronous.  Feed it rsf_vivaldi_probe's peer / acked. */
+int rsf_swim_probe_failures(rsf_swim* w, const uint32_t* target, const uint8_t* acked, const uint8_t* up,
+                            uint32_t now, int32_t* flags_out);
 
 #ifdef __cplusplus
 }

@@ -551,7 +551,7 @@ uint64_t orc_digest_mix(uint64_t d, uint64_t x) {
 #define DIG_USER 0x1000000000000000ull
 #define DIG_QUERY 0x2000000000000000ull
 #define DIG_MEMBER 0x3000000000000000ull
-enum { EV_JOIN = 0, EV_LEAVE = 1, EV_FAILED = 2, EV_REAP = 3 };
+enum { EV_JOIN = 0, EV_LEAVE = 1, EV_FAILED = 2, EV_REAP = 3, EV_UPDATE = 4 };
 
 /* the snapshotter's process_member_event (snapshot.rs:686-711): Join adds the node to
  * the alive set, Leave / Failed remove it; nothing is recorded after a leave */
@@ -728,6 +728,14 @@ int orc_handle_node_join(orc_world* w, uint32_t m, uint32_t subj) {
     w->v_ltime[e] = st;
   }
   digest_member_event(w, m, EV_JOIN, subj);
+  return ORC_F_MEMBER_EVENT;
+}
+
+/* handle_node_update (memberlist NotifyUpdate)  base.rs:1532-1583: a member with state
+ * gets its attributes (tags: host-side) and the Update MemberEvent */
+int orc_handle_node_update(orc_world* w, uint32_t m, uint32_t subj) {
+  if (w->v_kind[(size_t)m * w->s + subj] != ORC_K_KNOWN) return 0;
+  digest_member_event(w, m, EV_UPDATE, subj);
   return ORC_F_MEMBER_EVENT;
 }
 
@@ -1068,6 +1076,7 @@ static void phase_ml(world_job* j) {
       }
       if (al && m != sm) {
         if (j->ml[e].kind == ORC_ML_JOIN) orc_handle_node_join(w, m, subj);
+        else if (j->ml[e].kind == ORC_ML_UPDATE) orc_handle_node_update(w, m, subj);
         else orc_handle_node_leave(w, m, subj);
       }
       if (sm == m && j->ml[e].set_alive == 0) al = 0;

@@ -264,6 +264,7 @@ int orc_handle_leave_intent(orc_world* w, uint32_t m, uint32_t subj, uint64_t lt
                             uint64_t* refute_ltime);
 int orc_handle_node_join(orc_world* w, uint32_t m, uint32_t subj);
 int orc_handle_node_leave(orc_world* w, uint32_t m, uint32_t subj);
+int orc_handle_node_update(orc_world* w, uint32_t m, uint32_t subj);
 int orc_handle_user_event(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key);
 /* the same with the message's cc flag, which only the delivery log records */
 int orc_handle_user_event_cc(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key, int cc);
@@ -310,7 +311,7 @@ typedef struct {
 } orc_action;
 
 /* memberlist-detected transitions (M6) applied at every live member */
-enum { ORC_ML_JOIN = 1, ORC_ML_LEAVE = 2 };
+enum { ORC_ML_JOIN = 1, ORC_ML_LEAVE = 2, ORC_ML_UPDATE = 3 };
 typedef struct {
   uint32_t subject;
   uint32_t kind;     /* ORC_ML_* */

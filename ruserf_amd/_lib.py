@@ -105,6 +105,8 @@ def lib():
     _sig(L, "rsf_vivaldi_observe", i, [VP, C.c_uint32, VP, VP, VP, C.c_uint32])
     _sig(L, "rsf_vivaldi_table", i, [VP, C.POINTER(VP), P64])
     _sig(L, "rsf_vivaldi_true_rtt_ns", i, [VP, C.c_uint32, C.c_uint32, P64])
+    _sig(L, "rsf_vivaldi_probe", i, [VP, C.c_uint32, VP, VP, VP, VP])
+    _sig(L, "rsf_vivaldi_probe_acks", i, [VP, VP, VP, VP, VP, C.c_uint64])
     _sig(L, "rsf_vivaldi_exchange_buffers", i, [VP, C.c_uint32, C.POINTER(RsfVivaldiXbufs)])
     _sig(L, "rsf_vivaldi_exchange_requests", i, [VP, C.c_uint32, VP])
     _sig(L, "rsf_vivaldi_exchange_serve", i, [VP, C.c_uint32])

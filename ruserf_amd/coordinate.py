@@ -238,6 +238,17 @@ class CoordinateClients:
         check(lib().rsf_vivaldi_observe(self._h, slot, C.c_void_p(peer_ptr), C.c_void_p(rtt_ptr),
                                         C.c_void_p(status_ptr) if status_ptr else None, round_))
 
+    # ---- memberlist's probe loop (see ruserf_amd.probe.ProbeLoop)
+    def probe(self, r, up_ptr, peer_ptr, rtt_ptr, acked_ptr):
+        """Probes of round r with process liveness up[N] (device pointers, asynchronous)."""
+        check(lib().rsf_vivaldi_probe(self._h, r, C.c_void_p(up_ptr), C.c_void_p(peer_ptr), C.c_void_p(rtt_ptr),
+                                      C.c_void_p(acked_ptr)))
+
+    def probe_acks(self, peer_ptr, acked_ptr, off_ptr, payload_ptr, payload_cap):
+        """The acked probes' ack payloads on the wire (device pointers, asynchronous)."""
+        check(lib().rsf_vivaldi_probe_acks(self._h, C.c_void_p(peer_ptr), C.c_void_p(acked_ptr),
+                                           C.c_void_p(off_ptr), C.c_void_p(payload_ptr), payload_cap))
+
     # ---- the ping seam from wire bytes (SerfDelegate::ack_payload / notify_ping_complete)
     def ack_payloads_device(self, members_ptr, n, out_ptr, out_stride):
         """[PING_VERSION][Coordinate] of members[i] at out + i*out_stride (device pointers)."""

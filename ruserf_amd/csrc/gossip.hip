@@ -401,6 +401,8 @@ __global__ void __launch_bounds__(256) ml_kernel(GCfg c, GState s, const rsf_ml_
       if (ml[e].kind == RSF_ML_JOIN) {
         h_node_join(v, r, subj);
         snap_member(c, s, l, subj, true);
+      } else if (ml[e].kind == RSF_ML_UPDATE) {
+        h_node_update(v, r, subj);
       } else if (h_node_leave(v, r, subj, c.now) & RSF_F_MEMBER_EVENT) {
         snap_member(c, s, l, subj, false);
       }

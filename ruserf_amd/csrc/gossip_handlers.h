@@ -15,7 +15,7 @@ constexpr uint32_t kMinMsgLen = 18;  // smallest encoded message of the length m
 constexpr uint64_t kDigUser = 0x1000000000000000ull;
 constexpr uint64_t kDigQuery = 0x2000000000000000ull;
 constexpr uint64_t kDigMember = 0x3000000000000000ull;
-enum : uint32_t { kEvJoin = 0, kEvLeave = 1, kEvFailed = 2, kEvReap = 3 };
+enum : uint32_t { kEvJoin = 0, kEvLeave = 1, kEvFailed = 2, kEvReap = 3, kEvUpdate = 4 };
 enum : uint32_t { kQIntent = 0, kQQuery = 1, kQEvent = 2 };
 enum : uint32_t {
   kErrEvSlot = RSF_E_EVSLOT,
@@ -259,6 +259,13 @@ __device__ __forceinline__ int h_node_join(ViewE* e, MRegs& r, uint32_t subj) {
   }
   *e = v;
   r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)kEvJoin << 32) | subj);
+  return RSF_F_MEMBER_EVENT;
+}
+
+// handle_node_update (base.rs:1532-1583): a member with state gets the Update event
+__device__ __forceinline__ int h_node_update(const ViewE* e, MRegs& r, uint32_t subj) {
+  if (vkind(e->meta) != RSF_KIND_KNOWN) return 0;
+  r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)kEvUpdate << 32) | subj);
   return RSF_F_MEMBER_EVENT;
 }
 

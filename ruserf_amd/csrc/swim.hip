@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <vector>
+
 #include "../../include/ruserf_amd.h"
 #include "rsf_internal.h"
 
@@ -199,6 +201,28 @@ __global__ void __launch_bounds__(256) sw_tick_kernel(SwimCfg c, SwimDev d, uint
   atomicAdd(fired, 1ull);
 }
 
+// memberlist probeNode's failure path: a receiver whose probe of `target` got no ack runs
+// suspectNode{incarnation = its entry's, node = target, from = itself} (a tracked subject
+// only; a dead prober process does not probe).  flags[l] = RSF_SWIM_F_* (0: no suspicion)
+__global__ void __launch_bounds__(256) sw_probe_fail_kernel(SwimCfg c, SwimDev d, const int32_t* __restrict__ msubj,
+                                                            const uint32_t* __restrict__ target,
+                                                            const uint8_t* __restrict__ acked,
+                                                            const uint8_t* __restrict__ up, uint32_t now,
+                                                            int32_t* __restrict__ flags) {
+  const uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= c.n_loc) return;
+  const uint32_t me = (uint32_t)(c.lo + l), t = target[l];
+  int f = 0;
+  const int32_t j = msubj[t];
+  if (!acked[l] && (!up || up[me]) && t != me && j >= 0) {
+    SwimE e = d.view[l * c.S + (uint32_t)j];
+    uint32_t self_inc = d.self_inc[l], ref = 0;
+    f = sw_suspect(e, false, self_inc, e.inc, me, c.k, now, ref);
+    d.view[l * c.S + (uint32_t)j] = e;
+  }
+  if (flags) flags[l] = f;
+}
+
 __global__ void sw_init_kernel(SwimE* __restrict__ view, uint64_t n_loc, uint32_t S, const uint8_t* __restrict__ st,
                                const uint32_t* __restrict__ inc, uint32_t* __restrict__ self_inc, uint32_t self0) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -220,6 +244,8 @@ struct rsf_swim {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   unsigned long long* d_fired = nullptr;
+  int32_t* d_msubj = nullptr;  // [N] member id -> subject slot (-1: untracked)
+  uint64_t N = 0;
   rsf::DeviceScratch scratch;
 };
 
@@ -235,6 +261,7 @@ int rsf_swim_create(rsf_swim** out, const rsf_swim_cfg* cfg, int device) {
   RSF_HIP(hipSetDevice(device));
   rsf_swim* w = new rsf_swim();
   w->device = device;
+  w->N = cfg->n_members;
   w->c.lo = cfg->shard_lo;
   w->c.n_loc = cfg->shard_hi - cfg->shard_lo;
   w->c.S = cfg->n_subjects;
@@ -271,6 +298,7 @@ int rsf_swim_destroy(rsf_swim* w) {
   hipFree(w->d.left);
   hipFree(w->d.subj_member);
   hipFree(w->d_fired);
+  if (w->d_msubj) hipFree(w->d_msubj);
   w->scratch.release();
   if (w->own_stream && w->stream) hipStreamDestroy(w->stream);
   delete w;
@@ -292,8 +320,29 @@ int rsf_swim_set_stream(rsf_swim* w, void* s) {
 int rsf_swim_set_subjects(rsf_swim* w, const uint32_t* subject_member) {
   if (!w || !subject_member) return rsf::set_error(RSF_ERR_ARG, "null argument");
   RSF_HIP(hipSetDevice(w->device));
+  std::vector<int32_t> msubj(w->N, -1);
+  for (uint32_t s = 0; s < w->c.S; ++s) {
+    if (subject_member[s] >= w->N) return rsf::set_error(RSF_ERR_ARG, "subject member out of range");
+    msubj[subject_member[s]] = (int32_t)s;
+  }
+  if (!w->d_msubj) {
+    int rc = rsf::dmalloc((void**)&w->d_msubj, w->N * 4);
+    if (rc) return rc;
+  }
   RSF_HIP(hipMemcpyAsync(w->d.subj_member, subject_member, (uint64_t)w->c.S * 4, hipMemcpyHostToDevice, w->stream));
+  RSF_HIP(hipMemcpyAsync(w->d_msubj, msubj.data(), w->N * 4, hipMemcpyHostToDevice, w->stream));
   RSF_HIP(hipStreamSynchronize(w->stream));
+  return RSF_OK;
+}
+
+int rsf_swim_probe_failures(rsf_swim* w, const uint32_t* target, const uint8_t* acked, const uint8_t* up,
+                            uint32_t now, int32_t* flags_out) {
+  if (!w || !target || !acked) return rsf::set_error(RSF_ERR_ARG, "null argument");
+  if (!w->d_msubj) return rsf::set_error(RSF_ERR_ARG, "call rsf_swim_set_subjects first");
+  RSF_HIP(hipSetDevice(w->device));
+  hipLaunchKernelGGL(sw_probe_fail_kernel, dim3(grid1(w->c.n_loc)), dim3(256), 0, w->stream, w->c, w->d,
+                     (const int32_t*)w->d_msubj, target, acked, up, now, flags_out);
+  RSF_HIP(hipGetLastError());
   return RSF_OK;
 }
 

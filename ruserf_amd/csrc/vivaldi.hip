@@ -21,6 +21,7 @@
 //                                          Slot-major: a round probes one slot for every
 //                                          member, so its filter records stream coalesced.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -402,6 +403,52 @@ __global__ void __launch_bounds__(256) probe_gen_kernel(VivParams p, uint32_t sl
   double jit = 1.0 + 0.1 * ((double)pr.y * 2.3283064365386963e-10);
   peer_out[local] = peer;
   rtt_out[local] = sat_u64((d * jit) * 1.0e9);
+}
+
+// memberlist's probe loop on the same synthetic network (memberlist is not
+// vendored: parity unpinned): member lo+i probes neighbour slot `slot`; the probe is acked
+// when both processes are up (up[], global liveness), else it times out.  Acked: rtt as
+// probe_gen_kernel.  Timed out: rtt = UINT64_MAX, which CoordinateClient::update rejects
+// (rtt > 10 s) so the member is unchanged, as no notify_ping_complete happens.
+// len_out (optional): the ack payload's length (0: no ack) for the offsets scan.
+__global__ void __launch_bounds__(256) probe_live_kernel(VivParams p, uint32_t slot, const uint8_t* __restrict__ up,
+                                                         uint32_t* __restrict__ peer_out, uint64_t* __restrict__ rtt_out,
+                                                         uint8_t* __restrict__ acked_out) {
+  uint64_t local = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (local >= p.shard_n) return;
+  const uint32_t m = (uint32_t)(p.lo + local);
+  u32x4 pr = philox4x32_10(0, kPurposeVProbe << 24, m, p.round, p.k0, p.k1);
+  uint32_t peer = neighbour(p, m, slot);
+  const bool acked = up[m] && up[peer] && peer != m;
+  double xm, ym, hm, xp, yp, hp;
+  true_pos(p.k0, p.k1, m, xm, ym, hm);
+  true_pos(p.k0, p.k1, peer, xp, yp, hp);
+  double dx = xm - xp, dy = ym - yp;
+  double d = sqrt(dx * dx + dy * dy) + hm + hp;
+  double jit = 1.0 + 0.1 * ((double)pr.y * 2.3283064365386963e-10);
+  peer_out[local] = peer;
+  rtt_out[local] = acked ? sat_u64((d * jit) * 1.0e9) : UINT64_MAX;
+  acked_out[local] = acked ? 1 : 0;
+}
+
+// SerfDelegate::ack_payload at the probed node (delegate.rs:659-701): for every acked
+// probe, [PING_VERSION][Coordinate] of the target's current row at off[i]; sizes first
+__global__ void __launch_bounds__(256) probe_len_kernel(const uint8_t* __restrict__ acked, uint64_t n, uint64_t plen,
+                                                        uint64_t* __restrict__ len) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) len[i] = acked[i] ? plen : 0;
+  if (i == n) len[i] = 0;
+}
+__global__ void __launch_bounds__(256) probe_payload_kernel(const double* __restrict__ table,
+                                                            const uint32_t* __restrict__ peer,
+                                                            const uint8_t* __restrict__ acked,
+                                                            const uint64_t* __restrict__ off, uint64_t n,
+                                                            uint8_t* __restrict__ out, VivParams p) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !acked[i]) return;
+  uint8_t* d = out + off[i];
+  d[0] = rsf::kPingVersion;
+  rsf::coord_encode(d + 1, table + (uint64_t)peer[i] * p.stride, p.dim);
 }
 
 // One observation per shard member (the round's hot kernel): member lo+i runs
@@ -891,6 +938,10 @@ struct rsf_vivaldi {
   uint32_t *req_send = nullptr, *req_recv = nullptr, *xcnt = nullptr;
   double *rep_send = nullptr, *rep_recv = nullptr;
   unsigned long long* xflags = nullptr;
+  // probe loop: ack payload sizes -> offsets (scan scratch)
+  uint64_t* plen = nullptr;
+  void* ptmp = nullptr;
+  size_t ptmp_bytes = 0;
 };
 
 static int set_err_args(const char* m) { return rsf::set_error(RSF_ERR_ARG, m); }
@@ -1043,7 +1094,7 @@ int rsf_vivaldi_destroy(rsf_vivaldi* v) {
   hipFree(v->probe_peer);
   hipFree(v->probe_rtt);
   for (void* q : {(void*)v->req_send, (void*)v->req_recv, (void*)v->xcnt, (void*)v->rep_send, (void*)v->rep_recv,
-                  (void*)v->xflags})
+                  (void*)v->xflags, (void*)v->plen, v->ptmp})
     if (q) hipFree(q);
   v->scratch.release();
   if (v->own) hipStreamDestroy(v->own);
@@ -1247,6 +1298,46 @@ int rsf_vivaldi_gen_probes(rsf_vivaldi* v, uint32_t round, uint32_t* peer_out, u
   unsigned blocks = (unsigned)((p.shard_n + 255) / 256);
   hipLaunchKernelGGL(probe_gen_kernel, dim3(blocks), dim3(256), 0, v->stream, p, round % p.peers, peer_out,
                      rtt_ns_out);
+  RSF_HIP(hipGetLastError());
+  return RSF_OK;
+}
+
+int rsf_vivaldi_probe(rsf_vivaldi* v, uint32_t round, const uint8_t* up, uint32_t* peer_out, uint64_t* rtt_ns_out,
+                      uint8_t* acked_out) {
+  if (!v || !up || !peer_out || !rtt_ns_out || !acked_out) return set_err_args("null argument");
+  RSF_HIP(hipSetDevice(v->device));
+  VivParams p = v->p;
+  p.round = round;
+  unsigned blocks = (unsigned)((p.shard_n + 255) / 256);
+  hipLaunchKernelGGL(probe_live_kernel, dim3(blocks), dim3(256), 0, v->stream, p, round % p.peers, up, peer_out,
+                     rtt_ns_out, acked_out);
+  RSF_HIP(hipGetLastError());
+  return RSF_OK;
+}
+
+int rsf_vivaldi_probe_acks(rsf_vivaldi* v, const uint32_t* peer, const uint8_t* acked, uint64_t* off_out,
+                           uint8_t* payload_out, uint64_t payload_cap) {
+  if (!v || !peer || !acked || !off_out || !payload_out) return set_err_args("null argument");
+  const VivParams& p = v->p;
+  const uint64_t plen = 1ull + rsf::kCoordHdr + 8ull * p.dim, n = p.shard_n;
+  if (payload_cap < n * plen) return set_err_args("payload buffer smaller than shard_n x ack payload");
+  RSF_HIP(hipSetDevice(v->device));
+  int rc;
+  if (!v->plen && (rc = rsf::dmalloc((void**)&v->plen, (n + 1) * 8))) return rc;
+  size_t tb = 0;
+  RSF_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, v->plen, off_out, (int)(n + 1), v->stream));
+  if (tb > v->ptmp_bytes) {
+    if (v->ptmp) hipFree(v->ptmp);
+    v->ptmp = nullptr;
+    v->ptmp_bytes = 0;
+    if ((rc = rsf::dmalloc(&v->ptmp, tb))) return rc;
+    v->ptmp_bytes = tb;
+  }
+  const unsigned blocks = (unsigned)((n + 256) / 256);
+  hipLaunchKernelGGL(probe_len_kernel, dim3(blocks), dim3(256), 0, v->stream, acked, n, plen, v->plen);
+  RSF_HIP(hipcub::DeviceScan::ExclusiveSum(v->ptmp, tb, v->plen, off_out, (int)(n + 1), v->stream));
+  hipLaunchKernelGGL(probe_payload_kernel, dim3(blocks), dim3(256), 0, v->stream, (const double*)v->table[v->cur],
+                     peer, acked, (const uint64_t*)off_out, n, payload_out, p);
   RSF_HIP(hipGetLastError());
   return RSF_OK;
 }

@@ -38,7 +38,7 @@ E_EVSLOT, E_QSLOT, E_REFUTE, E_STAGE, E_QUEUE_PRUNE = 1, 2, 4, 8, 16
 # QueueOptions defaults (core/src/options.rs:494-530)
 MAX_QUEUE_DEPTH, MIN_QUEUE_DEPTH, QUEUE_DEPTH_WARNING = 4096, 0, 128
 ACT_JOIN_SELF, ACT_LEAVE_SELF, ACT_FORCE_LEAVE, ACT_USER_EVENT, ACT_QUERY = 1, 2, 3, 4, 5
-ML_JOIN, ML_LEAVE = 1, 2
+ML_JOIN, ML_LEAVE, ML_UPDATE = 1, 2, 3
 PP_JOIN, PP_EVENT_JOIN_IGNORE = 1, 2
 
 ACTION_DTYPE = np.dtype([("member", "<u4"), ("act", "<u4"), ("subject", "<u4"), ("name_len", "<u4"),

@@ -69,6 +69,7 @@ def _declare(L):
     sig("rsf_swim_apply_batch", [VP, VP, C.c_uint64, C.c_uint32, PI32, P32])
     sig("rsf_swim_tick", [VP, C.c_uint32, C.POINTER(C.c_uint64)])
     sig("rsf_swim_dump", [VP, C.c_uint64, C.c_uint64, P8, P32, P32, P8, P32])
+    sig("rsf_swim_probe_failures", [VP, VP, VP, VP, C.c_uint32, VP])
     L._swim_declared = True
 
 
@@ -115,6 +116,16 @@ class SwimState:
         s = np.ascontiguousarray(state, dtype=np.uint8)
         i = np.ascontiguousarray(incarnation, dtype=np.uint32)
         check(lib().rsf_swim_init(self._h, ptr(s, C.c_uint8), ptr(i, C.c_uint32), self_incarnation))
+
+    def set_stream(self, hip_stream_ptr):
+        check(lib().rsf_swim_set_stream(self._h, C.c_void_p(hip_stream_ptr)))
+
+    def probe_failures(self, target_ptr, acked_ptr, up_ptr, now, flags_ptr=None):
+        """probeNode's failure path at every receiver of the shard (device pointers, see
+        rsf_swim_probe_failures): a probe without ack suspects its (tracked) target."""
+        check(lib().rsf_swim_probe_failures(self._h, C.c_void_p(target_ptr), C.c_void_p(acked_ptr),
+                                            C.c_void_p(up_ptr) if up_ptr else None, now,
+                                            C.c_void_p(flags_ptr) if flags_ptr else None))
 
     def set_left(self, member, left=True):
         check(lib().rsf_swim_set_left(self._h, member, 1 if left else 0))

@@ -121,7 +121,7 @@ ST_NONE, ST_ALIVE, ST_LEAVING, ST_LEFT, ST_FAILED = 0, 1, 2, 3, 4
 K_UNKNOWN, K_JOIN, K_LEAVE, K_KNOWN = 0, 1, 2, 3
 F_REBROADCAST, F_REFUTE, F_PRUNE, F_DELIVER, F_MEMBER_EVENT = 1, 2, 4, 8, 16
 ACT_JOIN_SELF, ACT_LEAVE_SELF, ACT_FORCE_LEAVE, ACT_USER_EVENT, ACT_QUERY = 1, 2, 3, 4, 5
-ML_JOIN, ML_LEAVE = 1, 2
+ML_JOIN, ML_LEAVE, ML_UPDATE = 1, 2, 3
 
 _lib = None
 
@@ -182,6 +182,7 @@ def lib():
                                           C.c_int, P64]
     L.orc_handle_node_join.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint32]
     L.orc_handle_node_leave.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint32]
+    L.orc_handle_node_update.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint32]
     L.orc_handle_user_event.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint64, C.c_uint64]
     L.orc_handle_query.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint64, C.c_uint32, C.c_int]
     L.orc_upsert_intent.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint32, C.c_uint8, C.c_uint64]

@@ -220,6 +220,22 @@ def test_world_restart_from_snapshot():
     L.orc_world_free(C.byref(w))
 
 
+def test_node_update_emits_update_event_for_known_members():
+    """handle_node_update (base.rs:1532-1583): only a member with state gets the Update
+    event; the view is unchanged."""
+    w, cfg, subj, acts, ml = _world(rounds=1)
+    n, s = w.n, w.s
+    dig = O.arr(w.digest, n, np.uint64)
+    kind = O.arr(w.v_kind, n * s, np.uint8).reshape(n, s)
+    kind[3, 1] = O.K_UNKNOWN
+    d0 = int(dig[3])
+    assert L.orc_handle_node_update(C.byref(w), 3, 1) == 0 and int(dig[3]) == d0
+    view0 = kind.copy()
+    assert L.orc_handle_node_update(C.byref(w), 3, 2) == O.F_MEMBER_EVENT and int(dig[3]) != d0
+    assert np.array_equal(kind, view0)
+    L.orc_world_free(C.byref(w))
+
+
 def test_reconnect_targets_failed_members_only():
     w, cfg, subj, acts, ml = _world(n=800, rounds=10, seed=6)
     n, s = w.n, w.s

@@ -20,6 +20,13 @@ L = O.lib()
 def _setup(n, rounds, seed, false_failures=0):
     subj, acts, ml = W.churn_workload(n, rounds, events_per_round=20, queries_per_round=4, seed=seed)
     s = len(subj)
+    rng_u = np.random.default_rng(seed + 1)
+    for t in range(rounds):  # NotifyUpdate -> handle_node_update (Update member events)
+        extra = np.zeros(3, dtype=ml[t].dtype)
+        extra["subject"] = rng_u.choice(s, 3, replace=False)
+        extra["kind"] = G.ML_UPDATE
+        extra["set_alive"] = 2
+        ml[t] = np.concatenate([ml[t], extra])
     if false_failures:
         # memberlist marks some up members failed (set_alive 2: liveness unchanged), so a
         # Reconnector try can succeed
