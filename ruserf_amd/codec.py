@@ -52,7 +52,7 @@ def _L():
 
 def _dev(a):
     import torch
-    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    return torch.from_numpy(np.require(a, requirements=["C", "W"])).cuda()
 
 
 def _empty(n, dtype):

@@ -2032,6 +2032,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   hipStream_t st = g->stream;
   bool ok = true;
   auto ms = [&](void* p, int v, size_t b) { ok = ok && hipMemsetAsync(p, v, b, st) == hipSuccess; };
+  ms(g->d_counters, 0, 64 * 8);  // status flags and running totals start at zero
   ms(s.emin, 0, n * 8);
   ms(s.qmin, 0, n * 8);
   ms(s.digest, 0, n * 8);
@@ -2252,7 +2253,7 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
   if (!g || (n_ml && !ml) || (n_acts && !acts)) return gerr("null argument");
   const GCfg& c = g->c;
   for (uint32_t e = 0; e < n_ml; ++e)
-    if (ml[e].subject >= c.S || (ml[e].kind != RSF_ML_JOIN && ml[e].kind != RSF_ML_LEAVE) || ml[e].set_alive > 2)
+    if (ml[e].subject >= c.S || (ml[e].kind != RSF_ML_JOIN && ml[e].kind != RSF_ML_LEAVE && ml[e].kind != RSF_ML_UPDATE) || ml[e].set_alive > 2)
       return gerr("bad memberlist event");
   // actions: known kinds, members in range, distinct members
   {

@@ -23,7 +23,10 @@ class ProbeLoop:
     def __init__(self, clients: CoordinateClients, swim: SwimState = None, wire=True, stream=None):
         self.v, self.swim, self.wire = clients, swim, wire
         self.dev = torch.device("cuda", torch.cuda.current_device())
-        self.stream = stream or torch.cuda.current_stream()
+        # a stream of its own: torch's default stream has the NULL handle, which the C ABI
+        # reads as "each context's own stream", and then the probe (coordinate context) and
+        # the suspicion (SWIM context) would not be ordered
+        self.stream = stream if stream is not None and stream.cuda_stream else torch.cuda.Stream()
         clients.set_stream(self.stream.cuda_stream)
         if swim is not None:
             swim.set_stream(self.stream.cuda_stream)
@@ -44,6 +47,7 @@ class ProbeLoop:
     def round(self, r, up, now=None):
         """One probe round; `up` = uint8 CUDA tensor of every member's process liveness."""
         v = self.v
+        self.stream.wait_stream(torch.cuda.current_stream())  # `up` and the caller's prior work
         with torch.cuda.stream(self.stream):
             v.probe(r, up.data_ptr(), self.peer.data_ptr(), self.rtt.data_ptr(), self.acked.data_ptr())
             slot = r % v.peer_slots

@@ -51,7 +51,7 @@ def test_wire_path_equals_table_path():
         assert np.array_equal(acked, pb.acked.cpu().numpy().astype(bool))
         sa, sb = pa.status.cpu().numpy(), pb.status.cpu().numpy()
         assert np.all(sa[acked] == sb[acked])
-        assert np.all(sa[~acked] == 1)  # RSF_SKIPPED: no ack, no update
+        assert np.all(sa[~acked] == 4)  # RSF_SKIPPED: no ack, no update
         assert np.all(sb[~acked] != 0)  # rtt > 10 s: rejected, member unchanged
         assert torch.equal(_table(a)[:, :11].view(torch.int64), _table(b)[:, :11].view(torch.int64)), r
     a.close()
