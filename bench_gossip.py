@@ -86,7 +86,9 @@ def run_gossip(args, rank, world):
     if world > 1:
         torch.distributed.barrier()
     merged0 = eng.merged_total()
-    pruned0 = int(eng.pruned().astype(np.uint64).sum())
+    # as of each member's last emission (no flush): the timed rounds' emissions apply
+    # exactly the timed rounds' worth of pending re-queues
+    pruned0 = eng.pruned_total(flush=False)
     eng.set_profiling(True)
     torch.cuda.synchronize()
     if world > 1:
@@ -101,7 +103,7 @@ def run_gossip(args, rank, world):
     wall = time.perf_counter() - t0
     phase_ms, nr = eng.phase_times()
     merged = eng.merged_total() - merged0
-    pruned = int(eng.pruned().astype(np.uint64).sum()) - pruned0
+    pruned = eng.pruned_total(flush=False) - pruned0
     st = eng.members()
     from ruserf_amd.gossip import E_QUEUE_PRUNE
     # capacity errors other than the bounded queue's counted prunes (reported separately)

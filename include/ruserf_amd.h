@@ -508,6 +508,17 @@ int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t mi
  * items its bounded queues dropped when full; expired = queue items dropped at
  * emission because their rumor slot was recycled (see max_rumors). */
 int rsf_gossip_dump_pruned(rsf_gossip* g, uint32_t* pruned, uint32_t* expired);
+/* Re-queues are deferred: a handler's rebroadcast (and an origination's enqueue) is
+ * appended to the member's pending list and applied to its queues as one batch at the
+ * member's next emission -- exactly the reference's one-by-one inserts, since inserting
+ * into a bounded sorted queue without picks in between keeps the qcap smallest keys of
+ * everything inserted.  rsf_gossip_flush applies every pending list now; the inspection
+ * calls (dump_queues / dump_members / dump_pruned) and check_queues flush first, so they
+ * always show the reference's state.  Asynchronous. */
+int rsf_gossip_flush(rsf_gossip* g);
+/* Sum of dump_pruned's counts over the shard (flush = 0: without applying the pending
+ * lists first, i.e. as of every member's last emission).  Synchronises. */
+int rsf_gossip_pruned_total(rsf_gossip* g, int flush, uint64_t* total);
 
 /* Inspection (host copies; synchronise).  Arrays are over the shard's members. */
 int rsf_gossip_dump_members(rsf_gossip* g, uint64_t* clock, uint64_t* event_clock, uint64_t* query_clock,

@@ -57,6 +57,8 @@ def declare(L):
     sig("rsf_gossip_push_pull_device", [VP, VP, C.c_uint64, C.c_uint32])
     sig("rsf_gossip_check_queues", [VP, C.c_uint32, C.c_uint32, C.c_uint32, P64, P64, P64])
     sig("rsf_gossip_dump_pruned", [VP, P32, P32])
+    sig("rsf_gossip_flush", [VP])
+    sig("rsf_gossip_pruned_total", [VP, C.c_int, C.POINTER(C.c_uint64)])
     sig("rsf_gossip_set_delivery_log", [VP, C.c_uint32])
     sig("rsf_gossip_bucket_buffers", [VP, C.c_uint32, C.POINTER(VP), C.POINTER(VP), P64])
     sig("rsf_gossip_round_emit_buckets", [VP, C.c_uint32])

@@ -133,8 +133,11 @@ struct QRegs {
 #ifndef RSF_Q_NT
 #define RSF_Q_NT 0  // broadcast queues (touched once by emit, once by merge per round) read / written non-temporally
 #endif
+// The intent queue also keeps each item's record decoration (its subject slot, q_dec);
+// the query / event queues' decoration is the queue itself.
 __device__ __forceinline__ void q_load(const GCfg& c, const GState& s, uint64_t l, uint32_t q, uint32_t lane,
                                        QRegs& Q) {
+  Q.dec = q == 1 ? kDecQuery : kDecEvent;
   if (lane < c.qcap) {
     uint64_t i = (l * 3 + q) * c.qcap + lane;
 #if RSF_Q_NT
@@ -146,6 +149,7 @@ __device__ __forceinline__ void q_load(const GCfg& c, const GState& s, uint64_t 
     Q.sq = s.q_seq[i];
     Q.tl = s.q_txlen[i];
 #endif
+    if (q == 0) Q.dec = s.q_dec[l * c.qcap + lane];
   } else {
     Q.r = kEmpty;
     Q.sq = 0;
@@ -165,6 +169,7 @@ __device__ __forceinline__ void q_store(const GCfg& c, const GState& s, uint64_t
     s.q_txlen[i] = Q.tl;
     if (with_seq) s.q_seq[i] = Q.sq;
 #endif
+    if (q == 0) s.q_dec[l * c.qcap + lane] = Q.dec;
   }
 }
 
@@ -379,6 +384,122 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   return used;
 }
 
+// One LDS row per wave: scratch of the batched insert (q_insert_batch_lds).
+struct QLds {
+  uint32_t r[kWave], sq[kWave], tl[kWave], dec[kWave];
+};
+
+// Batched insert of new items (transmits 0, seqs seq0, seq0 + 1, ... in lane order over
+// `newmask`) into a sorted register-resident queue: the result is the qcap smallest keys of
+// (queue items U new items), exactly memberlist's insert-then-prune one at a time.  Done
+// over the DISTINCT LENGTHS of the new items instead of the items.  New items all have
+// transmits 0 and newer seqs than anything queued, so:
+//   new j lands at  #{queued: tx 0, len > len_j} + #{new: len > len_j} + #{new: len == len_j, later lane}
+//   queued i (lane i) lands at  i + (tx_i > 0 ? n_new : #{new: len >= len_i})
+// -- one pass per distinct new length (the message-length model has a handful), then
+// every item is written to its place in the wave's LDS row and read back in order.
+// DEC: the items' record decorations (Q.dec / dec) move with them.
+// Returns the number of live items that did not fit (memberlist Prune of the tail).
+template <bool DEC>
+__device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, uint32_t lane, bool ins, uint32_t rid,
+                                                       uint32_t dec, uint32_t len, uint32_t seq0, uint64_t newmask,
+                                                       QLds& row) {
+  const bool valid = lane < c.qcap;
+  const bool live = valid && Q.r != kEmpty;
+  const uint32_t n_live = (uint32_t)__popcll(__ballot(live));
+  const uint32_t n_new = (uint32_t)__popcll(newmask);
+  const uint64_t below = below_mask(lane), above = ~below & ~(1ull << lane);
+  const uint32_t myseq = seq0 + (uint32_t)__popcll(newmask & below);
+  const bool etx0 = live && (Q.tl & 0xFFFF) == 0;
+  const uint32_t elen = Q.tl >> 16;
+  uint32_t pos_n = 0, pos_e = lane + ((live && !etx0) ? n_new : 0u);
+  uint64_t rem = newmask;
+  while (rem) {
+    const uint32_t L = shfl_u32(len, __ffsll((long long)rem) - 1);
+    const uint64_t same = __ballot(ins && len == L);
+    rem &= ~same;
+    const uint32_t gt_new = (uint32_t)__popcll(__ballot(ins && len > L));
+    const uint32_t gt_old = (uint32_t)__popcll(__ballot(etx0 && elen > L));
+    if (ins && len == L) pos_n = gt_old + gt_new + (uint32_t)__popcll(same & above);
+    if (etx0 && elen <= L) pos_e += (uint32_t)__popcll(same);
+  }
+  if (ins && pos_n < c.qcap) {
+    row.r[pos_n] = rid;
+    row.sq[pos_n] = myseq;
+    row.tl[pos_n] = len << 16;
+    if (DEC) row.dec[pos_n] = dec;
+  }
+  if (live && pos_e < c.qcap) {
+    row.r[pos_e] = Q.r;
+    row.sq[pos_e] = Q.sq;
+    row.tl[pos_e] = Q.tl;
+    if (DEC) row.dec[pos_e] = Q.dec;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint32_t total = n_live + n_new;
+  if (valid) {
+    if (lane < total) {
+      Q.r = row.r[lane];
+      Q.sq = row.sq[lane];
+      Q.tl = row.tl[lane];
+      if (DEC) Q.dec = row.dec[lane];
+    } else {
+      Q.r = kEmpty;
+      Q.sq = 0;
+      Q.tl = 0;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();  // the row is free once every lane has read it
+  return total > c.qcap ? total - c.qcap : 0u;
+}
+
+// A member's pending re-queues (pc: their packed counts, which the caller may hold in
+// registers) applied to its queues by one wave (lane = slot / entry):
+// per queue, its entries in insertion order take the next seqs and go in as one batch.
+// Adds the live items dropped to q_pruned and returns their number (the caller flags
+// kErrQueue).  merge_kernel calls it only when a list would overflow.
+__device__ __forceinline__ uint32_t pend_flush_wave(const GCfg& c, const GState& s, uint64_t l, uint32_t lane,
+                                                 uint32_t pc, QLds& row) {
+  const uint32_t n = pend_total(pc);
+  if (n == 0) return 0;
+  uint32_t prid = 0, pdec = 0, plq = 0;
+  if (lane < n) {
+    prid = s.p_rid[l * kPend + lane];
+    pdec = s.p_dec[l * kPend + lane];
+    plq = s.p_lq[l * kPend + lane];
+  }
+  uint32_t drops = 0;
+  for (uint32_t q = 0; q < 3; ++q) {
+    const uint32_t nq = (pc >> (8 * q)) & 0xFF;
+    if (!nq) continue;
+    QRegs Q{kEmpty, 0, 0};
+    q_load(c, s, l, q, lane, Q);
+    const uint32_t seq0 = s.q_next_seq[l * 3 + q];
+    const bool ins = lane < n && (plq >> 16) == q;
+    drops += q_insert_batch_lds<true>(c, Q, lane, ins, prid, pdec, plq & 0xFFFF, seq0, __ballot(ins), row);
+    q_store(c, s, l, q, lane, Q, true);
+    if (lane == 0) s.q_next_seq[l * 3 + q] = seq0 + nq;
+  }
+  if (lane == 0) {
+    s.p_cnt[l] = 0;
+    if (drops) s.q_pruned[l] += drops;
+  }
+  return drops;
+}
+
+// every member's pending re-queues applied (before anything but emission reads the queues)
+__global__ void __launch_bounds__(256) pend_flush_kernel(GCfg c, GState s) {
+  __shared__ QLds rows[kWavesPerBlock];
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  if (l >= c.n_loc) return;
+  const uint32_t pc = s.p_cnt[l];
+  if (!pc) return;
+  if (pend_flush_wave(c, s, l, lane, pc, rows[threadIdx.x / kWave]) && lane == 0) s.err[l] |= kErrQueue;
+}
+
 // ---------------------------------------------------------------- kernels
 __global__ void __launch_bounds__(256) ml_kernel(GCfg c, GState s, const rsf_ml_event* __restrict__ ml,
                                                  uint32_t n_ml) {
@@ -455,7 +576,7 @@ __device__ __forceinline__ void broadcast_join(const GCfg& c, const GState& s, u
   h_join_intent(s.view + l * c.S + subj, r, L, c.now);
   uint32_t len = msg_len(RSF_MSG_JOIN, L, 0, 0);
   put_rumor(c, s, rid, RSF_MSG_JOIN, 0, subj, L, 0, len);
-  queue_insert_serial(c, s, l, kQIntent, rid, len, r);
+  pend_push_serial(c, s, l, kQIntent, rid, subj, len, r);
 }
 
 __global__ void __launch_bounds__(256) refute_kernel(GCfg c, GState s, uint32_t base) {
@@ -508,7 +629,7 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
       h_leave_intent(s.view + l * c.S + subj, r, subj, lt, false, ref, c.now);
       uint32_t len = msg_len(RSF_MSG_LEAVE, lt, 0, 0);
       put_rumor(c, s, rid, RSF_MSG_LEAVE, 0, subj, lt, 0, len);
-      queue_insert_serial(c, s, l, kQIntent, rid, len, r);
+      pend_push_serial(c, s, l, kQIntent, rid, subj, len, r);
       break;
     }
     case RSF_ACT_FORCE_LEAVE: {
@@ -518,7 +639,7 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
       if (f & RSF_F_REFUTE) push_refute(c, s, r, ref);
       uint32_t len = msg_len(RSF_MSG_LEAVE, lt, 0, 0);
       put_rumor(c, s, rid, RSF_MSG_LEAVE, prune ? 1 : 0, x.subject, lt, 0, len);
-      queue_insert_serial(c, s, l, kQIntent, rid, len, r);
+      pend_push_serial(c, s, l, kQIntent, rid, x.subject, len, r);
       break;
     }
     case RSF_ACT_USER_EVENT: {
@@ -528,7 +649,7 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
       h_user_event(c, s, l, r, lt, x.key, cc);
       uint32_t len = msg_len(RSF_MSG_USER_EVENT, lt, x.name_len, x.payload_len);
       put_rumor(c, s, rid, RSF_MSG_USER_EVENT, cc ? 1 : 0, 0, lt, x.key, len);
-      queue_insert_serial(c, s, l, kQEvent, rid, len, r);
+      pend_push_serial(c, s, l, kQEvent, rid, kDecEvent, len, r);
       break;
     }
     case RSF_ACT_QUERY: {
@@ -537,7 +658,7 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
       h_query(c, s, l, r, lt, (uint32_t)x.key, nb);
       uint32_t len = msg_len(RSF_MSG_QUERY, lt, x.name_len, x.payload_len);
       put_rumor(c, s, rid, RSF_MSG_QUERY, nb ? 1 : 0, 0, lt, (uint32_t)x.key, len);
-      queue_insert_serial(c, s, l, kQQuery, rid, len, r);
+      pend_push_serial(c, s, l, kQQuery, rid, kDecQuery, len, r);
       break;
     }
     default: break;
@@ -631,11 +752,17 @@ struct Buckets {
 };
 
 // a sender's first round trip: the intent queue (the common case; a sorted queue is
-// empty iff its slot 0 is free), the query/event queue heads, the peers and their
-// group slots
+// empty iff its slot 0 is free), the peers and their group slots, and one lane-distributed
+// word per lane (`head`): lanes 1, 2 the query / event queue heads, kEhPend the pending
+// re-queue counts, kEhSeq + q the queues' next insertion seqs, kEhPruned, kEhErr
+enum : uint32_t { kEhPend = 3, kEhSeq = 4, kEhPruned = 7, kEhErr = 8 };
+#ifndef RSF_EMIT_PEND_RT1
+#define RSF_EMIT_PEND_RT1 0  // 1: the pending entries are loaded in the first round trip, every lane
+#endif
 struct EmitIn {
   QRegs Q0;
   uint32_t head, gk, gs;
+  uint32_t prid = 0, pdec = 0, plq = 0;  // RSF_EMIT_PEND_RT1
 };
 __device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const uint32_t* __restrict__ grp_key,
                                           const uint32_t* __restrict__ slot, uint64_t l, uint32_t lane, EmitIn& e) {
@@ -645,25 +772,43 @@ __device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const 
   e.gs = 0;
   if (l >= c.n_loc) return;  // wave-uniform: a wave's last member may lie past the shard
   q_load(c, s, l, 0, lane, e.Q0);
-  e.head = lane >= 1 && lane < 3 ? s.q_rumor[(l * 3 + lane) * c.qcap] : kEmpty;
+  const uint32_t* hp = nullptr;
+  if (lane == 1 || lane == 2) hp = s.q_rumor + (l * 3 + lane) * c.qcap;
+  else if (lane == kEhPend) hp = s.p_cnt + l;
+  else if (lane >= kEhSeq && lane < kEhSeq + 3) hp = s.q_next_seq + l * 3 + (lane - kEhSeq);
+  else if (lane == kEhPruned) hp = s.q_pruned + l;
+  else if (lane == kEhErr) hp = s.err + l;
+  if (hp) e.head = *hp;
   e.gk = lane < c.fanout ? grp_key[l * c.fanout + lane] : kSentinel;
   e.gs = lane < c.fanout ? slot[l * c.fanout + lane] : 0u;
+  if (RSF_EMIT_PEND_RT1) {
+    e.prid = s.p_rid[l * kPend + lane];
+    e.pdec = s.p_dec[l * kPend + lane];
+    e.plq = s.p_lq[l * kPend + lane];
+  }
 }
 template <bool BKT>
 __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_t l, uint32_t lane, EmitIn& e,
                                          uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val,
-                                         uint32_t* __restrict__ out_dec, const Buckets& bk) {
+                                         uint32_t* __restrict__ out_dec, const Buckets& bk, QLds& row) {
   QRegs& Q0 = e.Q0;
   QRegs Q1{kEmpty, 0, 0, kDecQuery}, Q2{kEmpty, 0, 0, kDecEvent};
   const uint64_t pm = __ballot(e.gk != kSentinel);  // peers are a prefix of the fanout slots
   const uint32_t np = (uint32_t)__popcll(pm);
-  const bool ne0 = shfl_u32(Q0.r, 0) != kEmpty, ne1 = shfl_u32(e.head, 1) != kEmpty,
-             ne2 = shfl_u32(e.head, 2) != kEmpty;
+  const uint32_t pc = shfl_u32(e.head, kEhPend), npend = pend_total(pc);
+  const bool ne0 = shfl_u32(Q0.r, 0) != kEmpty || (pc & 0xFF), ne1 = shfl_u32(e.head, 1) != kEmpty || ((pc >> 8) & 0xFF),
+             ne2 = shfl_u32(e.head, 2) != kEmpty || ((pc >> 16) & 0xFF);
+  // no peers: nothing is sent, and the pending re-queues wait for the next emission
   if (np == 0 || !(ne0 || ne1 || ne2)) return;
   bool d0 = false, d1 = false, d2 = false;
   uint32_t err = 0;
-  // decoration of the intents: their subject slots (subject and type share one 8-B word)
-  if (Q0.r != kEmpty) Q0.dec = s.rdec[Q0.r & c.rmask];
+  // the pending re-queues (merge_kernel's and the originations' since the last emission)
+  uint32_t prid = e.prid, pdec = e.pdec, plq = e.plq;
+  if (!RSF_EMIT_PEND_RT1 && lane < npend) {
+    prid = s.p_rid[l * kPend + lane];
+    pdec = s.p_dec[l * kPend + lane];
+    plq = s.p_lq[l * kPend + lane];
+  }
   // buckets: each peer's destination shard and that bucket's first group (same round trip)
   uint32_t wdst = 0, wfirst = 0;
   if (BKT && lane < np) {
@@ -672,6 +817,36 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   }
   if (ne1) q_load(c, s, l, 1, lane, Q1);
   if (ne2) q_load(c, s, l, 2, lane, Q2);
+  if (npend) {
+    // applied first: in the reference they were queued when the messages arrived
+    uint32_t drops = 0;
+    const uint32_t pq = plq >> 16, plen = plq & 0xFFFF;
+    const bool in = lane < npend;
+    if (pc & 0xFF) {
+      const bool ins = in && pq == 0;
+      drops += q_insert_batch_lds<true>(c, Q0, lane, ins, prid, pdec, plen, shfl_u32(e.head, kEhSeq), __ballot(ins), row);
+      d0 = true;
+    }
+    if ((pc >> 8) & 0xFF) {
+      const bool ins = in && pq == 1;
+      drops += q_insert_batch_lds<false>(c, Q1, lane, ins, prid, 0u, plen, shfl_u32(e.head, kEhSeq + 1), __ballot(ins), row);
+      d1 = true;
+    }
+    if ((pc >> 16) & 0xFF) {
+      const bool ins = in && pq == 2;
+      drops += q_insert_batch_lds<false>(c, Q2, lane, ins, prid, 0u, plen, shfl_u32(e.head, kEhSeq + 2), __ballot(ins), row);
+      d2 = true;
+    }
+    if (lane == kEhPend) s.p_cnt[l] = 0;
+    if (lane >= kEhSeq && lane < kEhSeq + 3) {
+      const uint32_t nq = (pc >> (8 * (lane - kEhSeq))) & 0xFF;
+      if (nq) s.q_next_seq[l * 3 + (lane - kEhSeq)] = e.head + nq;
+    }
+    if (drops) {
+      if (lane == kEhPruned) s.q_pruned[l] = e.head + drops;
+      err |= kErrQueue;
+    }
+  }
   for (uint32_t j = 0; j < np; ++j) {
     const uint32_t gslot = shfl_u32(e.gs, j);
     uint64_t out_base = (uint64_t)gslot * c.cap_t;
@@ -700,7 +875,8 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   if (d0) q_store(c, s, l, 0, lane, Q0, true);
   if (d1) q_store(c, s, l, 1, lane, Q1, true);
   if (d2) q_store(c, s, l, 2, lane, Q2, true);
-  if (err && lane == 0) s.err[l] |= err;  // rare: a stage overflow
+  // flags: a queue prune (counted), a stage overflow (rare); written only when new
+  if (lane == kEhErr && (err & ~e.head)) s.err[l] = e.head | err;
 }
 
 template <bool BKT>
@@ -708,19 +884,21 @@ __global__ void __launch_bounds__(64 * RSF_EMIT_WPB) emit_kernel(GCfg c, GState 
                                                    const uint32_t* __restrict__ slot, uint32_t* __restrict__ cnt_s,
                                                    uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec,
                                                    Buckets bk) {
+  __shared__ QLds rows[RSF_EMIT_WPB];
   const uint32_t lane = threadIdx.x & (kWave - 1);
+  QLds& row = rows[threadIdx.x / kWave];
   const uint64_t l = ((uint64_t)xcd_block(blockIdx.x, gridDim.x) * RSF_EMIT_WPB +
                       (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)) * RSF_EMIT_PER_WAVE;
   if (l >= c.n_loc) return;
   EmitIn cur, nxt;
   emit_load(c, s, grp_key, slot, l, lane, cur);
   if (RSF_EMIT_PER_WAVE == 1) {
-    emit_run<BKT>(c, s, l, lane, cur, cnt_s, out_val, out_dec, bk);
+    emit_run<BKT>(c, s, l, lane, cur, cnt_s, out_val, out_dec, bk, row);
     return;
   }
   for (uint32_t k = 0; k < RSF_EMIT_PER_WAVE; ++k) {
     if (k + 1 < RSF_EMIT_PER_WAVE) emit_load(c, s, grp_key, slot, l + k + 1, lane, nxt);
-    if (l + k < c.n_loc) emit_run<BKT>(c, s, l + k, lane, cur, cnt_s, out_val, out_dec, bk);
+    if (l + k < c.n_loc) emit_run<BKT>(c, s, l + k, lane, cur, cnt_s, out_val, out_dec, bk, row);
     cur = nxt;
   }
 }
@@ -843,15 +1021,15 @@ __device__ unsigned long long g_merge_prof[8];
 #ifndef RSF_MERGE_CHAIN_BY_SUBJECT
 #define RSF_MERGE_CHAIN_BY_SUBJECT 1  // 1: chain detection loops over distinct subjects, not records
 #endif
-// What a receiver's merge needs before its records: segment bounds, liveness, the queues'
-// next insertion seqs and the member's registers, issued a receiver AHEAD (merge_kernel)
+// What a receiver's merge needs before its records: segment bounds, liveness, the pending
+// re-queue counts and the member's registers, issued a receiver AHEAD (merge_kernel)
 // as ONE lane-distributed load: lane j fetches dword j of the setup (kSu* below) from its
 // own array, so the prefetch holds one vector register until merge_one reads the fields
-// out with readlane.  The intent queue is loaded by merge_one beside the first records.
+// out with readlane.
 enum : uint32_t {
-  kSuStart, kSuEnd, kSuAlive, kSuSeq0, kSuSeq1, kSuSeq2, kSuClock, kSuEClock = kSuClock + 2,
+  kSuStart, kSuEnd, kSuAlive, kSuPend, kSuClock, kSuEClock = kSuClock + 2,
   kSuQClock = kSuEClock + 2, kSuEMin = kSuQClock + 2, kSuQMin = kSuEMin + 2, kSuDigest = kSuQMin + 2,
-  kSuErr = kSuDigest + 2, kSuSerf, kSuSubj, kSuPruned, kSuRun,  // kSuRun + 2r, + 2r + 1: run r's groups
+  kSuErr = kSuDigest + 2, kSuSerf, kSuSubj, kSuRun,  // kSuRun + 2r, + 2r + 1: run r's groups
   kSuLanes = kSuRun + 2 * kMaxRuns
 };
 // per-lane source: byte address = base + l * mult + off (alive / serf_state: the aligned
@@ -874,7 +1052,7 @@ __device__ __forceinline__ MSetupLane merge_setup_lane(const GCfg& c, const GSta
     off = (uint32_t)(r * c.n_loc * 4);
   }
   if (lane == kSuAlive) b = (const char*)s.alive + c.lo, mult = 1;
-  if (lane >= kSuSeq0 && lane <= kSuSeq2) b = (const char*)s.q_next_seq, mult = 12, off = 4 * (lane - kSuSeq0);
+  if (lane == kSuPend) b = (const char*)s.p_cnt;
   const uint64_t* u64s[6] = {s.clock, s.eclock, s.qclock, s.emin, s.qmin, s.digest};
 #pragma unroll
   for (uint32_t k = 0; k < 6; ++k)
@@ -883,7 +1061,6 @@ __device__ __forceinline__ MSetupLane merge_setup_lane(const GCfg& c, const GSta
   if (lane == kSuErr) b = (const char*)s.err;
   if (lane == kSuSerf) b = (const char*)s.serf_state, mult = 1;
   if (lane == kSuSubj) b = (const char*)s.member_subj;
-  if (lane == kSuPruned) b = (const char*)s.q_pruned;
   return MSetupLane{b, mult, off};
 }
 __device__ __forceinline__ uint32_t merge_setup(const MSetupLane& sl, uint64_t l, uint32_t lane) {
@@ -901,87 +1078,25 @@ __device__ __forceinline__ uint64_t su64(uint32_t v, uint32_t k) {
   return ((uint64_t)shfl_u32(v, k + 1) << 32) | shfl_u32(v, k);
 }
 
-// The query and event queues of a wave's receiver, parked in LDS between uses: only
-// query / event records touch them, and holding them in registers beside the intent
-// path spilled it at the 8-wave register cap.
-struct QLds {
-  uint32_t r[kWave], sq[kWave], tl[kWave];
-};
-__device__ __forceinline__ void qlds_put(QLds& q, uint32_t lane, const QRegs& Q) {
-  q.r[lane] = Q.r;
-  q.sq[lane] = Q.sq;
-  q.tl[lane] = Q.tl;
-}
-__device__ __forceinline__ QRegs qlds_get(const QLds& q, uint32_t lane) { return QRegs{q.r[lane], q.sq[lane], q.tl[lane]}; }
-
-// q_insert_batch over the DISTINCT LENGTHS of the new items instead of the items.  New
-// items all have transmits 0 and newer seqs than anything queued, so:
-//   new j lands at  #{queued: tx 0, len > len_j} + #{new: len > len_j} + #{new: len == len_j, later lane}
-//   queued i (lane i) lands at  i + (tx_i > 0 ? n_new : #{new: len >= len_i})
-// -- one pass per distinct new length (the message-length model has a handful), then
-// every item is written to its place in the wave's LDS row and read back in order.
-// Same result and drop count as q_insert_batch.
-__device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, uint32_t lane, bool ins, uint32_t rid,
-                                                       uint32_t len, uint32_t seq0, uint64_t newmask, QLds& row) {
-  const bool valid = lane < c.qcap;
-  const bool live = valid && Q.r != kEmpty;
-  const uint32_t n_live = (uint32_t)__popcll(__ballot(live));
-  const uint32_t n_new = (uint32_t)__popcll(newmask);
-  const uint64_t below = below_mask(lane), above = ~below & ~(1ull << lane);
-  const uint32_t myseq = seq0 + (uint32_t)__popcll(newmask & below);
-  const bool etx0 = live && (Q.tl & 0xFFFF) == 0;
-  const uint32_t elen = Q.tl >> 16;
-  uint32_t pos_n = 0, pos_e = lane + ((live && !etx0) ? n_new : 0u);
-  uint64_t rem = newmask;
-  while (rem) {
-    const uint32_t L = shfl_u32(len, __ffsll((long long)rem) - 1);
-    const uint64_t same = __ballot(ins && len == L);
-    rem &= ~same;
-    const uint32_t gt_new = (uint32_t)__popcll(__ballot(ins && len > L));
-    const uint32_t gt_old = (uint32_t)__popcll(__ballot(etx0 && elen > L));
-    if (ins && len == L) pos_n = gt_old + gt_new + (uint32_t)__popcll(same & above);
-    if (etx0 && elen <= L) pos_e += (uint32_t)__popcll(same);
-  }
-  if (ins && pos_n < c.qcap) {
-    row.r[pos_n] = rid;
-    row.sq[pos_n] = myseq;
-    row.tl[pos_n] = len << 16;
-  }
-  if (live && pos_e < c.qcap) {
-    row.r[pos_e] = Q.r;
-    row.sq[pos_e] = Q.sq;
-    row.tl[pos_e] = Q.tl;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const uint32_t total = n_live + n_new;
-  if (valid) {
-    if (lane < total) {
-      Q.r = row.r[lane];
-      Q.sq = row.sq[lane];
-      Q.tl = row.tl[lane];
-    } else {
-      Q.r = kEmpty;
-      Q.sq = 0;
-      Q.tl = 0;
-    }
-  }
-  __builtin_amdgcn_wave_barrier();  // the row is free once every lane has read it
-  return total > c.qcap ? total - c.qcap : 0u;
-}
-
 // One receiver (one wave).  Input layouts: flat (gcnt == nullptr, stride 1): records
 // [seg_start, seg_end) in canonical order; grouped (emit_kernel's): groups [seg_start,
 // seg_end) of `stride` slots each, group g holding gcnt[g] records, so lane = slot and the
 // empty slots of a group are holes (invalid lanes) in an otherwise canonical lane order.
-// Query/event queues are loaded on first need; a queue is written back only if something
-// was inserted.
-template <bool RUNS>
+// Re-queues go to the member's pending list (applied at its next emission); the merge
+// never reads or writes the queues themselves, except to apply a list that would overflow.
+// Receivers whose pending list might overflow during the merge (pending + slots > kPend)
+// are not merged by merge_kernel: they go to a list that merge_big_kernel works through
+// afterwards with the in-merge list application compiled in (BIG), which the common path
+// then need not carry (its registers).  Receivers are independent, so the order is free.
+struct BigList {
+  uint32_t* ids;            // [n_loc]
+  unsigned long long* n;    // count (reset before each merge)
+};
+template <bool RUNS, bool BIG>
 __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const uint32_t* __restrict__ vals,
                                           const uint32_t* __restrict__ dec, const uint32_t* __restrict__ gcnt,
-                                          uint32_t stride, uint64_t l, uint32_t lane, uint32_t su, QLds* ql,
-                                          uint32_t* __restrict__ sbits, const Buckets& bk) {
+                                          uint32_t stride, uint64_t l, uint32_t lane, uint32_t su, QLds* row,
+                                          uint32_t* __restrict__ sbits, const Buckets& bk, const BigList& big) {
   MPROF_T(t_start);
   uint32_t st = 0, en = 0, total;
   uint32_t rcum[kMaxRuns + 1], rst[kMaxRuns];  // runs: cumulative slots, first group per run
@@ -1001,11 +1116,17 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     total = st < en ? (en - st) * stride : 0u;
   }
   if (total == 0 || (shfl_u32(su, kSuAlive) & 0xFF) == 0) return;
-  QRegs Q0{kEmpty, 0, 0};
-  q_load(c, s, l, 0, lane, Q0);  // intents are the common case
-  bool ld1 = false, ld2 = false, d0 = false, d1 = false, d2 = false;
-  uint32_t qdrop = 0;  // live queue items dropped by full queues (wave-uniform)
-  uint32_t nseq0 = shfl_u32(su, kSuSeq0), nseq1 = shfl_u32(su, kSuSeq1), nseq2 = shfl_u32(su, kSuSeq2);
+  // pending re-queues: packed per-queue counts and their total (wave-uniform)
+  const uint32_t pc0 = shfl_u32(su, kSuPend);
+  uint32_t pc = pc0, pn = pend_total(pc0);
+  if (!BIG && pn + total > kPendMerge) {  // at most one re-queue per record slot: might not fit
+    if (lane == 0) big.ids[atomicAdd(big.n, 1ull)] = (uint32_t)l;
+    return;
+  }
+  uint32_t qdrop = 0;  // live queue items dropped by full queues (a list applied here)
+  uint32_t* const p_rid = s.p_rid + l * kPend;
+  uint32_t* const p_dec = s.p_dec + l * kPend;
+  uint32_t* const p_lq = s.p_lq + l * kPend;
   MRegs r;
   r.clock = su64(su, kSuClock);
   r.eclock = su64(su, kSuEClock);
@@ -1023,6 +1144,13 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
   for (uint32_t vb = 0; vb < total; vb += kWave) {
     MPROF_T(t_c0);
     const uint32_t cnt = min((uint32_t)kWave, total - vb);  // lanes in this chunk
+    if (BIG && pn + cnt > kPendMerge) {
+      // the chunk's re-queues (at most one per record) might not fit the pending list:
+      // apply the list to the queues first (rare: a receiver of many records)
+      __threadfence_block();
+      qdrop += pend_flush_wave(c, s, l, lane, pc, *row);
+      pc = pn = 0;
+    }
     const bool in = lane < cnt;
     const uint32_t vi = vb + lane;  // this lane's slot in the receiver's slot list
     uint32_t rid0 = 0, dsub0 = kEmpty, gk = 1, gc = 1;
@@ -1065,18 +1193,6 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     const uint32_t rid = valid ? rid0 : 0;
     const uint32_t dsub = valid ? dsub0 : kEmpty;
     const bool is_view = dsub < kDecViewMax;
-    if (!ld1 && __ballot(dsub == kDecQuery)) {
-      QRegs t{kEmpty, 0, 0};
-      q_load(c, s, l, 1, lane, t);
-      qlds_put(ql[0], lane, t);
-      ld1 = true;
-    }
-    if (!ld2 && __ballot(dsub == kDecEvent)) {
-      QRegs t{kEmpty, 0, 0};
-      q_load(c, s, l, 2, lane, t);
-      qlds_put(ql[1], lane, t);
-      ld2 = true;
-    }
     rsf_rumor ru{};
     if (valid) {  // the key only for user events / queries (the decoration says which)
       const uint4 b = s.rbody[rid & c.rmask];
@@ -1176,13 +1292,19 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     if (chunk_max > r.clock) r.clock = chunk_max;
     MPROF_T(t_c2);
     MPROF_ADD(2, t_c1, t_c2);
-    // intent re-queues of the chunk in one batch (the intent queue takes nothing else)
+    // intent re-queues of the chunk appended to the pending list in one batch (record order)
     const bool ins = is_view && (f & RSF_F_REBROADCAST);
     const uint64_t newmask = __ballot(ins);
     if (newmask) {
-      qdrop += q_insert_batch_lds(c, Q0, lane, ins, rid, ru.msg_len, nseq0, newmask, ql[2]);
-      nseq0 += (uint32_t)__popcll(newmask);
-      d0 = true;
+      const uint32_t k = (uint32_t)__popcll(newmask);
+      if (ins) {
+        const uint32_t i = pn + (uint32_t)__popcll(newmask & below_mask(lane));
+        p_rid[i] = rid;
+        p_dec[i] = dsub;
+        p_lq[i] = ru.msg_len;  // queue 0
+      }
+      pn += k;
+      pc += k;
     }
     // serial part, record order: events/queries (lane 0 handlers), digest, refutes
     const uint64_t serial =
@@ -1218,21 +1340,15 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
         r.digest = shfl_u64(r.digest, 0);
         r.err = shfl_u32(r.err, 0);
       }
-      if (fi & RSF_F_REBROADCAST) {
-        const uint32_t q = queue_of(type), rid_i = shfl_u32(rid, i), mlen = tf >> 16;
-        if (q == kQIntent) {
-          // intents went in above, batched per chunk
-        } else if (q == kQQuery) {
-          QRegs t = qlds_get(ql[0], lane);
-          qdrop += q_insert_wave(c, t, lane, rid_i, mlen, nseq1++);
-          qlds_put(ql[0], lane, t);
-          d1 = true;
-        } else {
-          QRegs t = qlds_get(ql[1], lane);
-          qdrop += q_insert_wave(c, t, lane, rid_i, mlen, nseq2++);
-          qlds_put(ql[1], lane, t);
-          d2 = true;
+      const uint32_t q = queue_of(type);
+      if ((fi & RSF_F_REBROADCAST) && q != kQIntent) {  // intents went in above, batched per chunk
+        if (lane == 0) {
+          p_rid[pn] = shfl_u32(rid, i);
+          p_dec[pn] = q == kQQuery ? kDecQuery : kDecEvent;
+          p_lq[pn] = (tf >> 16) | (q << 16);
         }
+        pn++;
+        pc += 1u << (8 * q);
       }
     }
     MPROF_T(t_c3);
@@ -1240,11 +1356,12 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     if (vb + kWave < total) __threadfence_block();  // next chunk's prefetch must see this chunk's view stores
   }
   MPROF_T(t_st0);
-  if (d0) q_store(c, s, l, 0, lane, Q0, true);
-  if (d1) q_store(c, s, l, 1, lane, qlds_get(ql[0], lane), true);
-  if (d2) q_store(c, s, l, 2, lane, qlds_get(ql[1], lane), true);
+  if (BIG && pn > kPendMerge) {  // leave the originations' headroom (kPendMerge)
+    __threadfence_block();
+    qdrop += pend_flush_wave(c, s, l, lane, pc, *row);
+    pc = pn = 0;
+  }
   if (qdrop) r.err |= kErrQueue;
-  const uint32_t pruned0 = shfl_u32(su, kSuPruned);
   // registers go back only where they changed (the setup lanes hold the old values)
   const bool w_clock = r.clock != su64(su, kSuClock), w_eclock = r.eclock != su64(su, kSuEClock),
              w_qclock = r.qclock != su64(su, kSuQClock), w_digest = r.digest != su64(su, kSuDigest),
@@ -1255,10 +1372,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     if (w_qclock) s.qclock[l] = r.qclock;
     if (w_digest) s.digest[l] = r.digest;
     if (w_err) s.err[l] = r.err;
-    if (qdrop) s.q_pruned[l] = pruned0 + qdrop;
-    if (d0) s.q_next_seq[l * 3 + 0] = nseq0;
-    if (d1) s.q_next_seq[l * 3 + 1] = nseq1;
-    if (d2) s.q_next_seq[l * 3 + 2] = nseq2;
+    if (pc != pc0 || qdrop) s.p_cnt[l] = pc;
   }
   MPROF_T(t_end);
   MPROF_ADD(4, t_st0, t_end);
@@ -1266,50 +1380,51 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
   if (lane == 0) { MPROF_ADD(6, 0, 1); }
 }
 
-// Persistent waves (grid = what fits on the chip at once): wave w merges receivers
-// w, w + nw, w + 2nw, ... and issues the NEXT receiver's setup loads before merging the
-// current one, so that round trip overlaps this receiver's work instead of starting it.
-// Receivers are independent (each touches only its own view row, queues and registers).
-#ifndef RSF_MERGE_PERSIST
-#define RSF_MERGE_PERSIST 0  // 1: persistent waves (measured 14% slower than hardware wave dispatch)
-#endif
 template <bool RUNS>
 __global__ void __launch_bounds__(256, RSF_MERGE_WAVES) merge_kernel(GCfg c, GState s, const uint32_t* __restrict__ vals,
                                                     const uint32_t* __restrict__ dec,
                                                     const uint32_t* __restrict__ seg_start,
                                                     const uint32_t* __restrict__ seg_end,
-                                                    const uint32_t* __restrict__ gcnt, uint32_t stride, Buckets bk) {
+                                                    const uint32_t* __restrict__ gcnt, uint32_t stride, Buckets bk,
+                                                    BigList big) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
-  __shared__ QLds qlds[kWavesPerBlock][3];  // query queue, event queue, insert scratch
   __shared__ uint32_t subj_bits[kWavesPerBlock][128];  // chain detection (zero between chunks)
-  QLds* ql = qlds[threadIdx.x / kWave];
   uint32_t* sbits = subj_bits[threadIdx.x / kWave];
   for (uint32_t i = threadIdx.x & (kWave - 1); i < 128; i += kWave) sbits[i] = 0u;
-  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
-  uint64_t l = (uint64_t)(RSF_MERGE_PERSIST ? blockIdx.x : xcd_block(blockIdx.x, gridDim.x)) * kWavesPerBlock +
-               (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  if (!RSF_MERGE_PERSIST) l *= RSF_MERGE_PER_WAVE;
+  const uint64_t l = ((uint64_t)xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock +
+                      (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)) * RSF_MERGE_PER_WAVE;
   if (l >= c.n_loc) return;
   const MSetupLane sl = merge_setup_lane(c, s, seg_start, seg_end, lane, RUNS ? bk.n_runs : 0u);
   uint32_t cur = merge_setup(sl, l, lane);
-  if (!RSF_MERGE_PERSIST && RSF_MERGE_PER_WAVE > 1) {
-    // every owned receiver's setup is in flight before the first merge starts
-    for (uint32_t k = 0; k < RSF_MERGE_PER_WAVE && l + k < c.n_loc; ++k) {
-      const uint32_t nxt = k + 1 < RSF_MERGE_PER_WAVE && l + k + 1 < c.n_loc ? merge_setup(sl, l + k + 1, lane) : 0u;
-      merge_one<RUNS>(c, s, vals, dec, gcnt, stride, l + k, lane, cur, ql, sbits, bk);
-      cur = nxt;
-    }
-    return;
-  }
-  for (;;) {
-    const uint64_t ln = l + nw;
-    const bool more = RSF_MERGE_PERSIST && ln < c.n_loc;
-    uint32_t nxt = 0;
-    if (more) nxt = merge_setup(sl, ln, lane);
-    merge_one<RUNS>(c, s, vals, dec, gcnt, stride, l, lane, cur, ql, sbits, bk);
-    if (!more) break;
+  // every owned receiver's setup is in flight one receiver ahead of its merge
+  for (uint32_t k = 0; k < RSF_MERGE_PER_WAVE && l + k < c.n_loc; ++k) {
+    const uint32_t nxt = k + 1 < RSF_MERGE_PER_WAVE && l + k + 1 < c.n_loc ? merge_setup(sl, l + k + 1, lane) : 0u;
+    merge_one<RUNS, false>(c, s, vals, dec, gcnt, stride, l + k, lane, cur, nullptr, sbits, bk, big);
     cur = nxt;
-    l = ln;
+  }
+}
+
+// the receivers merge_kernel deferred (BigList), grid-stride over the list
+template <bool RUNS>
+__global__ void __launch_bounds__(256) merge_big_kernel(GCfg c, GState s, const uint32_t* __restrict__ vals,
+                                                        const uint32_t* __restrict__ dec,
+                                                        const uint32_t* __restrict__ seg_start,
+                                                        const uint32_t* __restrict__ seg_end,
+                                                        const uint32_t* __restrict__ gcnt, uint32_t stride, Buckets bk,
+                                                        BigList big) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  __shared__ QLds qlds[kWavesPerBlock];  // scratch of a pending list applied here
+  __shared__ uint32_t subj_bits[kWavesPerBlock][128];
+  QLds& ql = qlds[threadIdx.x / kWave];
+  uint32_t* sbits = subj_bits[threadIdx.x / kWave];
+  for (uint32_t i = lane; i < 128; i += kWave) sbits[i] = 0u;
+  const uint64_t n = *big.n;
+  const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+  const MSetupLane sl = merge_setup_lane(c, s, seg_start, seg_end, lane, RUNS ? bk.n_runs : 0u);
+  for (uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+       i < n; i += nw) {
+    const uint64_t l = big.ids[i];
+    merge_one<RUNS, true>(c, s, vals, dec, gcnt, stride, l, lane, merge_setup(sl, l, lane), &ql, sbits, bk, big);
   }
 }
 
@@ -1733,7 +1848,7 @@ __global__ void __launch_bounds__(256) expire_kernel(GCfg c, GState s, uint32_t 
   q_load(c, s, l, q, lane, Q);
   const uint32_t G = rumor_generations(c);
   const uint32_t age = (gen + G - (Q.r >> c.rbits) % G) % G;
-  const uint32_t x = q_expire(c, Q, lane, age >= 2, false);
+  const uint32_t x = q_expire(c, Q, lane, age >= 2, q == 0);
   if (!x) return;
   q_store(c, s, l, q, lane, Q, true);
   if (x && lane == 0) atomicAdd(s.q_expired + l, x);
@@ -1856,7 +1971,8 @@ struct rsf_gossip {
            *grp_slot = nullptr, *grp_off = nullptr, *stage_dec = nullptr;
   void* grp_scan_tmp = nullptr;
   size_t grp_scan_bytes = 0;
-  unsigned merge_blocks = 1;  // merge_kernel's persistent grid: resident blocks per CU x CUs
+  unsigned merge_blocks = 1;  // merge_big_kernel's grid: merge_kernel's resident blocks per CU x CUs
+  uint32_t* big_ids = nullptr;  // receivers deferred to merge_big_kernel (count: d_counters[52])
   uint64_t* send_buf = nullptr;
   unsigned long long* d_counters = nullptr;  // [0] n_valid, [1..] shard bounds
   void* sort_tmp = nullptr;
@@ -1890,6 +2006,15 @@ static void mark(rsf_gossip* g, int k) {
   if (!g->profiling || g->prof_rounds >= rsf_gossip::kMaxProfRounds) return;
   hipEventRecord(g->ev[g->prof_rounds][k], g->stream);
   if (k == rsf_gossip::kMarks - 1) g->prof_rounds++;
+}
+
+// Every member's pending re-queues applied to its queues: before anything other than
+// emission reads the queues, the queue-prune counters or the error flags.
+static int flush_pending(rsf_gossip* g) {
+  hipLaunchKernelGGL(pend_flush_kernel, dim3(grid1(g->c.n_loc, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0,
+                     g->stream, g->c, g->s);
+  RSF_HIP(hipGetLastError());
+  return RSF_OK;
 }
 
 static int ensure_lists(rsf_gossip* g, uint32_t n_ml, uint32_t n_acts) {
@@ -1988,11 +2113,12 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
       GA(s.digest, n * 8) || GA(s.err, n * 4) || GA(s.alive, N) || GA(s.serf_state, n) || GA(s.member_subj, n * 4) ||
       GA(s.subj_member, S * 4) || GA(s.refute_cnt, S * 4) || GA(s.refute_ltime, S * c.max_refute * 8) ||
       GA(s.view, n * S * sizeof(ViewE)) || GA(s.q_rumor, n * 3 * c.qcap * 4) || GA(s.q_seq, n * 3 * c.qcap * 4) ||
-      GA(s.q_txlen, n * 3 * c.qcap * 4) || GA(s.q_next_seq, n * 3 * 4) || GA(s.q_pruned, n * 4) || GA(s.q_expired, n * 4) || GA(s.eb_ltime, n * c.ebuf * 8) ||
+      GA(s.q_txlen, n * 3 * c.qcap * 4) || GA(s.q_dec, n * c.qcap * 4) || GA(s.q_next_seq, n * 3 * 4) || GA(s.q_pruned, n * 4) || GA(s.q_expired, n * 4) || GA(s.eb_ltime, n * c.ebuf * 8) ||
       GA(s.eb_cnt, n * c.ebuf * 4) || GA(s.eb_keys, n * c.ebuf * c.slot_k * 8) || GA(s.qb_ltime, n * c.qbuf * 8) ||
       GA(s.qb_cnt, n * c.qbuf * 4) || GA(s.qb_ids, n * c.qbuf * c.slot_k * 4) ||
       GA(s.rumors, (size_t)cfg->max_rumors * 2 * sizeof(rsf_rumor)) ||
-      GA(s.rdec, (size_t)cfg->max_rumors * 2 * 4) || GA(s.rbody, (size_t)cfg->max_rumors * 2 * 16))
+      GA(s.rdec, (size_t)cfg->max_rumors * 2 * 4) || GA(s.rbody, (size_t)cfg->max_rumors * 2 * 16) ||
+      GA(s.p_rid, n * kPend * 4) || GA(s.p_dec, n * kPend * 4) || GA(s.p_lq, n * kPend * 4) || GA(s.p_cnt, n * 4))
     return fail(rc);
   g->stage_cap = n * c.fanout * c.cap_t;
   if (g->stage_cap >= 0xFFFFFFFFull) return fail(gerr("n_members x fanout x per-target records must fit 32 bits"));
@@ -2005,7 +2131,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   g->n_groups = n * c.fanout;
   if (GA(g->grp_key, g->n_groups * 4) || GA(g->grp_cnt, g->n_groups * 4) || GA(g->grp_key_s, g->n_groups * 4) ||
       GA(g->grp_id, g->n_groups * 4) || GA(g->grp_id_s, g->n_groups * 4) || GA(g->grp_slot, g->n_groups * 4) ||
-      GA(g->grp_off, g->n_groups * 4) || GA(g->stage_dec, g->stage_cap * 4))
+      GA(g->grp_off, g->n_groups * 4) || GA(g->stage_dec, g->stage_cap * 4) || GA(g->big_ids, n * 4))
     return fail(rc);
 #undef GA
   {
@@ -2047,9 +2173,11 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   ms(s.q_rumor, 0xFF, n * 3 * c.qcap * 4);
   ms(s.q_seq, 0, n * 3 * c.qcap * 4);
   ms(s.q_txlen, 0, n * 3 * c.qcap * 4);
+  ms(s.q_dec, 0, n * c.qcap * 4);
   ms(s.q_next_seq, 0, n * 3 * 4);
   ms(s.q_pruned, 0, n * 4);
   ms(s.q_expired, 0, n * 4);
+  ms(s.p_cnt, 0, n * 4);
   ms(s.eb_ltime, 0, n * c.ebuf * 8);
   ms(s.eb_cnt, 0, n * c.ebuf * 4);
   ms(s.eb_keys, 0, n * c.ebuf * c.slot_k * 8);
@@ -2077,13 +2205,14 @@ int rsf_gossip_destroy(rsf_gossip* g) {
   GState& s = g->s;
   void* ptrs[] = {s.clock,  s.eclock,      s.qclock,       s.emin,        s.qmin,     s.digest,     s.err,
                   s.alive,  s.serf_state,  s.member_subj,  s.subj_member, s.refute_cnt, s.refute_ltime, s.view,
-                  s.q_rumor, s.q_seq,      s.q_txlen,      s.q_next_seq,  s.q_pruned, s.q_expired,  s.eb_ltime, s.eb_cnt,     s.eb_keys,
+                  s.q_rumor, s.q_seq,      s.q_txlen,      s.q_dec,      s.q_next_seq,  s.q_pruned, s.q_expired,  s.eb_ltime, s.eb_cnt,     s.eb_keys,
                   s.qb_ltime, s.qb_cnt,    s.qb_ids,       s.rumors,      s.rdec,       s.rbody,      g->d_ml,    g->d_acts,    g->stage_key,
                   g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters, g->rec_dec, g->pp_buf,
                   g->sort_tmp, g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
                   g->scan_tmp, g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
                   g->grp_slot, g->grp_off, g->stage_dec, g->grp_scan_tmp, s.dlog, s.dcnt,
-                  g->bkt_send, g->bkt_recv, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn};
+                  g->bkt_send, g->bkt_recv, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn,
+                  s.p_rid, s.p_dec, s.p_lq, s.p_cnt, g->big_ids};
   for (void* p : ptrs)
     if (p) hipFree(p);
   g->scratch.release();
@@ -2282,6 +2411,7 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
     g->gen = (g->gen + 1) % rumor_generations(c);
     // this generation reuses the half of the table of generation gen - 2: queued ids of
     // that generation expire now, before anything reads or re-queues them
+    if ((rc = flush_pending(g))) return rc;
     hipLaunchKernelGGL(expire_kernel, dim3(grid1(c.n_loc * 3, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0,
                        g->stream, c, g->s, g->gen);
   }
@@ -2381,15 +2511,31 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
 
 // grouped: the records are emit_kernel's groups (stage_val / stage_dec, cap_t slots, grp_cnt);
 // otherwise a flat record stream (vals, rec_dec)
+static BigList big_list(rsf_gossip* g) { return BigList{g->big_ids, g->d_counters + 52}; }
+// merge_kernel over every receiver, then merge_big_kernel over the ones it deferred
+template <bool RUNS>
+static int merge_launch(rsf_gossip* g, const uint32_t* vals, const uint32_t* dec, const uint32_t* start,
+                        const uint32_t* end, const uint32_t* gcnt, uint32_t stride, const Buckets& bk) {
+  const GCfg& c = g->c;
+  const BigList big = big_list(g);
+  RSF_HIP(hipMemsetAsync(big.n, 0, 8, g->stream));
+  const unsigned blocks = grid1((c.n_loc + RSF_MERGE_PER_WAVE - 1) / RSF_MERGE_PER_WAVE, kWavesPerBlock);
+  hipLaunchKernelGGL(merge_kernel<RUNS>, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, g->stream, c, g->s, vals, dec,
+                     start, end, gcnt, stride, bk, big);
+  hipLaunchKernelGGL(merge_big_kernel<RUNS>, dim3(std::min(g->merge_blocks, blocks)), dim3(kWave * kWavesPerBlock), 0,
+                     g->stream, c, g->s, vals, dec, start, end, gcnt, stride, bk, big);
+  RSF_HIP(hipGetLastError());
+  return RSF_OK;
+}
+
+// grouped: the records are emit_kernel's groups (stage_val / stage_dec, cap_t slots, grp_cnt);
+// otherwise a flat record stream (vals, rec_dec)
 static int launch_merge(rsf_gossip* g, const uint32_t* vals, bool grouped = false) {
   const GCfg& c = g->c;
-  const unsigned blocks = RSF_MERGE_PERSIST ? std::min<unsigned>(grid1(c.n_loc, kWavesPerBlock), g->merge_blocks)
-                                            : grid1((c.n_loc + RSF_MERGE_PER_WAVE - 1) / RSF_MERGE_PER_WAVE,
-                                                    kWavesPerBlock);
-  hipLaunchKernelGGL(merge_kernel<false>, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, g->stream,
-                     c, g->s, grouped ? g->stage_val : vals, grouped ? g->stage_dec : (const uint32_t*)g->rec_dec,
-                     g->seg_start, g->seg_end, grouped ? g->grp_cnt : nullptr, grouped ? c.cap_t : 1u, Buckets{});
-  RSF_HIP(hipGetLastError());
+  int rc = merge_launch<false>(g, grouped ? g->stage_val : vals, grouped ? g->stage_dec : (const uint32_t*)g->rec_dec,
+                               g->seg_start, g->seg_end, grouped ? g->grp_cnt : nullptr, grouped ? c.cap_t : 1u,
+                               Buckets{});
+  if (rc) return rc;
   mark(g, 4);
   return RSF_OK;
 }
@@ -2501,11 +2647,8 @@ int rsf_gossip_round_merge_buckets(rsf_gossip* g, uint32_t world) {
   hipLaunchKernelGGL(accumulate_kernel, dim3(1), dim3(64), 0, st, g->d_counters, 57u);
   if (g->profiling && g->prof_rounds < rsf_gossip::kMaxProfRounds)
     hipEventRecord(g->ev[g->prof_rounds][3], g->stream);  // exchange time lands in the sort slot
-  const unsigned blocks = grid1((c.n_loc + RSF_MERGE_PER_WAVE - 1) / RSF_MERGE_PER_WAVE, kWavesPerBlock);
-  hipLaunchKernelGGL(merge_kernel<true>, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, st, c, g->s,
-                     (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)g->d_rstart,
-                     (const uint32_t*)g->d_rend, (const uint32_t*)nullptr, c.cap_t, bk);
-  RSF_HIP(hipGetLastError());
+  int rc = merge_launch<true>(g, nullptr, nullptr, g->d_rstart, g->d_rend, nullptr, c.cap_t, bk);
+  if (rc) return rc;
   mark(g, 4);
   return RSF_OK;
 }
@@ -2730,6 +2873,8 @@ int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t mi
   if (min_queue_depth > 0) mx = std::max<uint64_t>(2 * c.N, min_queue_depth);
   const uint32_t max_depth = (uint32_t)std::min<uint64_t>(mx, 0xFFFFFFFFull);
   RSF_HIP(hipSetDevice(g->device));
+  int rc = flush_pending(g);
+  if (rc) return rc;
   RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, g->stream));
   hipLaunchKernelGGL(check_queues_kernel, dim3(grid1(c.n_loc * 3)), dim3(256), 0, g->stream, c, g->s, max_depth,
                      depth_warning, g->d_counters + 40);
@@ -2745,9 +2890,31 @@ int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t mi
   return RSF_OK;
 }
 
+int rsf_gossip_flush(rsf_gossip* g) {
+  if (!g) return gerr("null context");
+  RSF_HIP(hipSetDevice(g->device));
+  return flush_pending(g);
+}
+
+int rsf_gossip_pruned_total(rsf_gossip* g, int flush, uint64_t* total) {
+  if (!g || !total) return gerr("null argument");
+  RSF_HIP(hipSetDevice(g->device));
+  int rc;
+  if (flush && (rc = flush_pending(g))) return rc;
+  std::vector<uint32_t> v(g->c.n_loc);
+  RSF_HIP(hipMemcpyAsync(v.data(), g->s.q_pruned, g->c.n_loc * 4, hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  uint64_t t = 0;
+  for (uint32_t x : v) t += x;
+  *total = t;
+  return RSF_OK;
+}
+
 int rsf_gossip_dump_pruned(rsf_gossip* g, uint32_t* pruned, uint32_t* expired) {
   if (!g) return gerr("null context");
   RSF_HIP(hipSetDevice(g->device));
+  int rc = flush_pending(g);
+  if (rc) return rc;
   if (pruned) RSF_HIP(hipMemcpyAsync(pruned, g->s.q_pruned, g->c.n_loc * 4, hipMemcpyDeviceToHost, g->stream));
   if (expired) RSF_HIP(hipMemcpyAsync(expired, g->s.q_expired, g->c.n_loc * 4, hipMemcpyDeviceToHost, g->stream));
   RSF_HIP(hipStreamSynchronize(g->stream));
@@ -2817,6 +2984,8 @@ int rsf_gossip_dump_members(rsf_gossip* g, uint64_t* clock, uint64_t* ec, uint64
   const uint64_t n = g->c.n_loc;
   hipStream_t st = g->stream;
   RSF_HIP(hipSetDevice(g->device));
+  int rc = flush_pending(g);  // queue-prune flags
+  if (rc) return rc;
   if (clock) RSF_HIP(hipMemcpyAsync(clock, g->s.clock, n * 8, hipMemcpyDeviceToHost, st));
   if (ec) RSF_HIP(hipMemcpyAsync(ec, g->s.eclock, n * 8, hipMemcpyDeviceToHost, st));
   if (qc) RSF_HIP(hipMemcpyAsync(qc, g->s.qclock, n * 8, hipMemcpyDeviceToHost, st));
@@ -2850,6 +3019,8 @@ int rsf_gossip_dump_queues(rsf_gossip* g, uint32_t* rumor, uint32_t* seq, uint16
   std::vector<uint32_t> tl(cnt);
   hipStream_t st = g->stream;
   RSF_HIP(hipSetDevice(g->device));
+  int rc = flush_pending(g);
+  if (rc) return rc;
   RSF_HIP(hipMemcpyAsync(rumor, g->s.q_rumor, cnt * 4, hipMemcpyDeviceToHost, st));
   RSF_HIP(hipMemcpyAsync(seq, g->s.q_seq, cnt * 4, hipMemcpyDeviceToHost, st));
   RSF_HIP(hipMemcpyAsync(tl.data(), g->s.q_txlen, cnt * 4, hipMemcpyDeviceToHost, st));
@@ -3114,6 +3285,7 @@ __global__ void __launch_bounds__(256) snap_reset_kernel(GCfg c, GState s, const
     s.q_txlen[l * 3 * c.qcap + j] = 0;
   }
   if (threadIdx.x < 3) s.q_next_seq[l * 3 + threadIdx.x] = 0;
+  if (threadIdx.x == 0) s.p_cnt[l] = 0;  // nothing pending either
   for (uint32_t j = threadIdx.x; j < c.ebuf; j += blockDim.x) {
     s.eb_ltime[l * c.ebuf + j] = 0;
     s.eb_cnt[l * c.ebuf + j] = 0;
@@ -3305,6 +3477,10 @@ int rsf_gossip_restart(rsf_gossip* g, const uint32_t* members, uint32_t n, const
   std::vector<uint64_t> offs(n + 1);
   for (uint32_t i = 0; i <= n; ++i) offs[i] = offsets[i] - offsets[0];
   RSF_HIP(hipSetDevice(g->device));
+  // the restarted processes' queues are dropped: what was pending reaches them first, as
+  // the reference queued it when the messages arrived (its prunes are counted)
+  int frc = flush_pending(g);
+  if (frc) return frc;
   hipStream_t st = g->stream;
   uint32_t *d_mem = nullptr, *d_bits = nullptr;
   uint64_t *d_offs = nullptr, *d_clk = nullptr;

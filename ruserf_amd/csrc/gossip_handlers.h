@@ -57,6 +57,7 @@ struct GState {
   uint64_t* refute_ltime; // [S][max_refute]
   ViewE* view;            // [n_loc][S]
   uint32_t *q_rumor, *q_seq, *q_txlen, *q_next_seq;  // [n_loc][3][qcap], next_seq [n_loc][3]
+  uint32_t* q_dec;        // [n_loc][qcap] intent queue: each item's record decoration (subject slot)
   uint32_t* q_pruned;     // [n_loc] live queue items dropped by a full queue (memberlist Prune), cumulative
   uint32_t* q_expired;    // [n_loc] queue items dropped when the rumor ring wrapped onto their generation
   uint64_t* eb_ltime;
@@ -74,7 +75,24 @@ struct GState {
   // over subjects, and {last event clock, last query clock, last clock at leave, flags}
   uint32_t* snap_bits;  // [n_loc][snap_w]
   uint64_t* snap_sn;    // [n_loc][4]; flags bit 0: leaving (recording stopped)
+  // Pending re-queues (deferred TransmitLimitedQueue inserts).  A handler's "rebroadcast"
+  // appends (rumor id, record decoration, msg_len | queue << 16) to the member's list in
+  // insertion order; the list is applied to the queues as one batch per queue at the
+  // member's next emission (emit_kernel, which holds the queues in registers anyway), or by
+  // pend_flush_* before anything else reads the queues.  Inserting new items and pruning
+  // the largest key is order-free between picks (the queue keeps the qcap smallest keys of
+  // everything inserted), so the deferred batch is exactly the reference's one-by-one
+  // insert.  p_cnt[l] packs the entries per queue: n0 | n1 << 8 | n2 << 16 (sum <= kPend).
+  uint32_t *p_rid, *p_dec, *p_lq;  // [n_loc][kPend]
+  uint32_t* p_cnt;                 // [n_loc]
 };
+constexpr uint32_t kPend = 64;  // pending entries per member (one wave's lanes)
+// The merge leaves a member at most kPendMerge entries, so the round's originations and
+// refutations (at most 1 + max_refute <= 5 per member) append without applying the list
+// serially; a member that emits nothing for many rounds can still fill it (then the
+// serial application runs, slow but exact).
+constexpr uint32_t kPendMerge = kPend - 8;
+RSF_HD uint32_t pend_total(uint32_t pc) { return (pc & 0xFF) + ((pc >> 8) & 0xFF) + ((pc >> 16) & 0xFF); }
 
 // per-member scalar state held in registers while a kernel works on it
 struct MRegs {
@@ -389,14 +407,7 @@ __device__ __forceinline__ uint32_t queue_of(uint8_t type) {
 // item that would land past the end is itself the pruned one.
 // A full queue loses one live item: counted in q_pruned[l] and flagged (kErrQueue).
 __device__ __forceinline__ void queue_insert_item(const GCfg& c, const GState& s, uint64_t l, uint32_t q,
-                                                  uint32_t rid, uint32_t len, uint32_t seq, MRegs& r);
-__device__ __forceinline__ void queue_insert_serial(const GCfg& c, const GState& s, uint64_t l, uint32_t q,
-                                                    uint32_t rid, uint32_t len, MRegs& r) {
-  const uint32_t seq = s.q_next_seq[l * 3 + q]++;
-  queue_insert_item(c, s, l, q, rid, len, seq, r);
-}
-__device__ __forceinline__ void queue_insert_item(const GCfg& c, const GState& s, uint64_t l, uint32_t q,
-                                                  uint32_t rid, uint32_t len, uint32_t seq, MRegs& r) {
+                                                  uint32_t rid, uint32_t dec, uint32_t len, uint32_t seq, MRegs& r) {
   const uint64_t base = (l * 3 + q) * c.qcap;
   const uint64_t newkey = tlq_key(0, len, seq);
   uint32_t cnt = 0, pos = kEmpty;
@@ -415,10 +426,38 @@ __device__ __forceinline__ void queue_insert_item(const GCfg& c, const GState& s
     s.q_rumor[base + i] = s.q_rumor[base + i - 1];
     s.q_seq[base + i] = s.q_seq[base + i - 1];
     s.q_txlen[base + i] = s.q_txlen[base + i - 1];
+    if (q == 0) s.q_dec[l * c.qcap + i] = s.q_dec[l * c.qcap + i - 1];
   }
+  if (q == 0) s.q_dec[l * c.qcap + pos] = dec;
   s.q_rumor[base + pos] = rid;
   s.q_seq[base + pos] = seq;
   s.q_txlen[base + pos] = (len << 16);
+}
+
+// the member's pending re-queues applied one by one, in insertion order (one thread)
+__device__ __forceinline__ void pend_flush_serial(const GCfg& c, const GState& s, uint64_t l, MRegs& r) {
+  const uint32_t n = pend_total(s.p_cnt[l]);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t lq = s.p_lq[l * kPend + i], q = lq >> 16;
+    queue_insert_item(c, s, l, q, s.p_rid[l * kPend + i], s.p_dec[l * kPend + i], lq & 0xFFFF,
+                      s.q_next_seq[l * 3 + q]++, r);
+  }
+  s.p_cnt[l] = 0;
+}
+
+// re-queue on queue q (one thread): appended to the pending list (a full list is applied first)
+__device__ __forceinline__ void pend_push_serial(const GCfg& c, const GState& s, uint64_t l, uint32_t q,
+                                                 uint32_t rid, uint32_t dec, uint32_t len, MRegs& r) {
+  uint32_t pc = s.p_cnt[l];
+  if (pend_total(pc) >= kPend) {
+    pend_flush_serial(c, s, l, r);
+    pc = 0;
+  }
+  const uint32_t i = pend_total(pc);
+  s.p_rid[l * kPend + i] = rid;
+  s.p_dec[l * kPend + i] = dec;
+  s.p_lq[l * kPend + i] = len | (q << 16);
+  s.p_cnt[l] = pc + (1u << (8 * q));
 }
 
 }  // namespace rsf

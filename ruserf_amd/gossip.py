@@ -327,6 +327,17 @@ class GossipEngine:
         check(lib().rsf_gossip_dump_pruned(self._h, ptr(out, C.c_uint32), None))
         return out
 
+    def flush(self):
+        """Apply every member's pending re-queues to its queues (asynchronous; the
+        inspection calls do it themselves)."""
+        check(lib().rsf_gossip_flush(self._h))
+
+    def pruned_total(self, flush=True):
+        """Sum of pruned() over the shard; flush=False: as of each member's last emission."""
+        out = C.c_uint64(0)
+        check(lib().rsf_gossip_pruned_total(self._h, 1 if flush else 0, C.byref(out)))
+        return int(out.value)
+
     def expired(self):
         """Per member: queue items dropped at emission because their rumor slot was recycled."""
         out = np.zeros(self.n_loc, dtype=np.uint32)
