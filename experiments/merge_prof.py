@@ -1,4 +1,5 @@
-"""Diagnostic only: per-phase shader-clock totals of merge_kernel at the bench's
+"""Diagnostic only: per-phase shader-clock totals of merge_kernel (or, with argv[2] ==
+"emit" and a -DRSF_EMIT_PROF=1 library, of emit_kernel) at the bench's
 1M-member gossip workload (needs a library built with -DRSF_MERGE_PROF=1, loaded
 via RSF_LIB_PATH).  Phases: 0 setup (segment bounds, queue + register loads),
 1 chunk loads (records, rumors, view entries, chains, clock scan), 2 chain walk,
@@ -36,6 +37,8 @@ torch.cuda.synchronize()
 L.rsf_gossip_merge_prof(buf)
 v = list(buf)
 names = ["setup", "chunk_loads", "chain_walk", "serial", "stores", "total", "waves"]
+if len(sys.argv) > 2 and sys.argv[2] == "emit":  # a library built with -DRSF_EMIT_PROF=1
+    names = ["rt1_wait", "rt2_pending_apply", "picks", "stores", "-", "total", "waves"]
 out = {k: v[i] for i, k in enumerate(names)}
 out["share"] = {k: round(v[i] / max(1, v[5]), 3) for i, k in enumerate(names[:5])}
 out["cycles_per_wave"] = v[5] / max(1, v[6])

@@ -460,16 +460,45 @@ __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, 
 // per queue, its entries in insertion order take the next seqs and go in as one batch.
 // Adds the live items dropped to q_pruned and returns their number (the caller flags
 // kErrQueue).  merge_kernel calls it only when a list would overflow.
+// The entries of one queue from the wave's two batches of the list (lanes 0..63 hold
+// entries lane and 64 + lane) go in as one batch after the other, seqs continuing.
+struct PendRegs {
+  uint32_t rid[2], dec[2], lq[2];
+};
+__device__ __forceinline__ void pend_load(const GState& s, uint64_t l, uint32_t lane, uint32_t n, PendRegs& p) {
+#pragma unroll
+  for (uint32_t b = 0; b < 2; ++b) {
+    p.rid[b] = p.dec[b] = p.lq[b] = 0;
+    if (b * kWave + lane < n) {
+      const uint64_t i = l * kPend + b * kWave + lane;
+      p.rid[b] = s.p_rid[i];
+      p.dec[b] = s.p_dec[i];
+      p.lq[b] = s.p_lq[i];
+    }
+  }
+}
+template <bool DEC>
+__device__ __forceinline__ uint32_t pend_apply(const GCfg& c, QRegs& Q, uint32_t lane, uint32_t q, uint32_t n,
+                                               const PendRegs& p, uint32_t seq0, QLds& row) {
+  uint32_t drops = 0, seq = seq0;
+#pragma unroll
+  for (uint32_t b = 0; b < 2; ++b) {
+    if (b * kWave >= n) break;
+    const bool ins = b * kWave + lane < n && (p.lq[b] >> 16) == q;
+    const uint64_t m = __ballot(ins);
+    if (!m) continue;
+    drops += q_insert_batch_lds<DEC>(c, Q, lane, ins, p.rid[b], p.dec[b], p.lq[b] & 0xFFFF, seq, m, row);
+    seq += (uint32_t)__popcll(m);
+  }
+  return drops;
+}
+
 __device__ __forceinline__ uint32_t pend_flush_wave(const GCfg& c, const GState& s, uint64_t l, uint32_t lane,
-                                                 uint32_t pc, QLds& row) {
+                                                    uint32_t pc, QLds& row) {
   const uint32_t n = pend_total(pc);
   if (n == 0) return 0;
-  uint32_t prid = 0, pdec = 0, plq = 0;
-  if (lane < n) {
-    prid = s.p_rid[l * kPend + lane];
-    pdec = s.p_dec[l * kPend + lane];
-    plq = s.p_lq[l * kPend + lane];
-  }
+  PendRegs p;
+  pend_load(s, l, lane, n, p);
   uint32_t drops = 0;
   for (uint32_t q = 0; q < 3; ++q) {
     const uint32_t nq = (pc >> (8 * q)) & 0xFF;
@@ -477,8 +506,7 @@ __device__ __forceinline__ uint32_t pend_flush_wave(const GCfg& c, const GState&
     QRegs Q{kEmpty, 0, 0};
     q_load(c, s, l, q, lane, Q);
     const uint32_t seq0 = s.q_next_seq[l * 3 + q];
-    const bool ins = lane < n && (plq >> 16) == q;
-    drops += q_insert_batch_lds<true>(c, Q, lane, ins, prid, pdec, plq & 0xFFFF, seq0, __ballot(ins), row);
+    drops += pend_apply<true>(c, Q, lane, q, n, p, seq0, row);
     q_store(c, s, l, q, lane, Q, true);
     if (lane == 0) s.q_next_seq[l * 3 + q] = seq0 + nq;
   }
@@ -751,18 +779,40 @@ struct Buckets {
   uint32_t keys_off, cnt_off, vals_off, decs_off, gcap, n_runs;
 };
 
+#ifndef RSF_MERGE_PROF
+#define RSF_MERGE_PROF 0  // diagnostic build: per-phase shader-clock totals of merge_kernel
+#endif
+#ifndef RSF_EMIT_PROF
+#define RSF_EMIT_PROF 0  // diagnostic build: per-phase shader-clock totals of emit_kernel (same counters)
+#endif
+#if RSF_MERGE_PROF || RSF_EMIT_PROF
+__device__ unsigned long long g_merge_prof[8];
+#endif
+#if RSF_MERGE_PROF
+#define MPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define MPROF_ADD(i, a, b) \
+  if (lane == 0) atomicAdd(&g_merge_prof[i], (unsigned long long)((b) - (a)))
+#else
+#define MPROF_T(v)
+#define MPROF_ADD(i, a, b)
+#endif
+#if RSF_EMIT_PROF
+#define EPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define EPROF_ADD(i, a, b) \
+  if (lane == 0) atomicAdd(&g_merge_prof[i], (unsigned long long)((b) - (a)))
+#else
+#define EPROF_T(v)
+#define EPROF_ADD(i, a, b)
+#endif
+
 // a sender's first round trip: the intent queue (the common case; a sorted queue is
 // empty iff its slot 0 is free), the peers and their group slots, and one lane-distributed
 // word per lane (`head`): lanes 1, 2 the query / event queue heads, kEhPend the pending
 // re-queue counts, kEhSeq + q the queues' next insertion seqs, kEhPruned, kEhErr
 enum : uint32_t { kEhPend = 3, kEhSeq = 4, kEhPruned = 7, kEhErr = 8 };
-#ifndef RSF_EMIT_PEND_RT1
-#define RSF_EMIT_PEND_RT1 0  // 1: the pending entries are loaded in the first round trip, every lane
-#endif
 struct EmitIn {
   QRegs Q0;
   uint32_t head, gk, gs;
-  uint32_t prid = 0, pdec = 0, plq = 0;  // RSF_EMIT_PEND_RT1
 };
 __device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const uint32_t* __restrict__ grp_key,
                                           const uint32_t* __restrict__ slot, uint64_t l, uint32_t lane, EmitIn& e) {
@@ -781,16 +831,12 @@ __device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const 
   if (hp) e.head = *hp;
   e.gk = lane < c.fanout ? grp_key[l * c.fanout + lane] : kSentinel;
   e.gs = lane < c.fanout ? slot[l * c.fanout + lane] : 0u;
-  if (RSF_EMIT_PEND_RT1) {
-    e.prid = s.p_rid[l * kPend + lane];
-    e.pdec = s.p_dec[l * kPend + lane];
-    e.plq = s.p_lq[l * kPend + lane];
-  }
 }
 template <bool BKT>
 __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_t l, uint32_t lane, EmitIn& e,
                                          uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val,
                                          uint32_t* __restrict__ out_dec, const Buckets& bk, QLds& row) {
+  EPROF_T(t0);
   QRegs& Q0 = e.Q0;
   QRegs Q1{kEmpty, 0, 0, kDecQuery}, Q2{kEmpty, 0, 0, kDecEvent};
   const uint64_t pm = __ballot(e.gk != kSentinel);  // peers are a prefix of the fanout slots
@@ -800,15 +846,13 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
              ne2 = shfl_u32(e.head, 2) != kEmpty || ((pc >> 16) & 0xFF);
   // no peers: nothing is sent, and the pending re-queues wait for the next emission
   if (np == 0 || !(ne0 || ne1 || ne2)) return;
+  EPROF_T(t1);
+  EPROF_ADD(0, t0, t1);
   bool d0 = false, d1 = false, d2 = false;
   uint32_t err = 0;
   // the pending re-queues (merge_kernel's and the originations' since the last emission)
-  uint32_t prid = e.prid, pdec = e.pdec, plq = e.plq;
-  if (!RSF_EMIT_PEND_RT1 && lane < npend) {
-    prid = s.p_rid[l * kPend + lane];
-    pdec = s.p_dec[l * kPend + lane];
-    plq = s.p_lq[l * kPend + lane];
-  }
+  PendRegs pr;
+  pend_load(s, l, lane, npend, pr);
   // buckets: each peer's destination shard and that bucket's first group (same round trip)
   uint32_t wdst = 0, wfirst = 0;
   if (BKT && lane < np) {
@@ -820,21 +864,16 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   if (npend) {
     // applied first: in the reference they were queued when the messages arrived
     uint32_t drops = 0;
-    const uint32_t pq = plq >> 16, plen = plq & 0xFFFF;
-    const bool in = lane < npend;
     if (pc & 0xFF) {
-      const bool ins = in && pq == 0;
-      drops += q_insert_batch_lds<true>(c, Q0, lane, ins, prid, pdec, plen, shfl_u32(e.head, kEhSeq), __ballot(ins), row);
+      drops += pend_apply<true>(c, Q0, lane, 0, npend, pr, shfl_u32(e.head, kEhSeq), row);
       d0 = true;
     }
     if ((pc >> 8) & 0xFF) {
-      const bool ins = in && pq == 1;
-      drops += q_insert_batch_lds<false>(c, Q1, lane, ins, prid, 0u, plen, shfl_u32(e.head, kEhSeq + 1), __ballot(ins), row);
+      drops += pend_apply<false>(c, Q1, lane, 1, npend, pr, shfl_u32(e.head, kEhSeq + 1), row);
       d1 = true;
     }
     if ((pc >> 16) & 0xFF) {
-      const bool ins = in && pq == 2;
-      drops += q_insert_batch_lds<false>(c, Q2, lane, ins, prid, 0u, plen, shfl_u32(e.head, kEhSeq + 2), __ballot(ins), row);
+      drops += pend_apply<false>(c, Q2, lane, 2, npend, pr, shfl_u32(e.head, kEhSeq + 2), row);
       d2 = true;
     }
     if (lane == kEhPend) s.p_cnt[l] = 0;
@@ -847,6 +886,8 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
       err |= kErrQueue;
     }
   }
+  EPROF_T(t2);
+  EPROF_ADD(1, t1, t2);
   for (uint32_t j = 0; j < np; ++j) {
     const uint32_t gslot = shfl_u32(e.gs, j);
     uint64_t out_base = (uint64_t)gslot * c.cap_t;
@@ -872,11 +913,17 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
     used += q_get_broadcasts<false>(c, Q2, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d2);
     if (lane == 0 && oc && nrec) *oc = min(nrec, c.cap_t);
   }
+  EPROF_T(t3);
+  EPROF_ADD(2, t2, t3);
   if (d0) q_store(c, s, l, 0, lane, Q0, true);
   if (d1) q_store(c, s, l, 1, lane, Q1, true);
   if (d2) q_store(c, s, l, 2, lane, Q2, true);
   // flags: a queue prune (counted), a stage overflow (rare); written only when new
   if (lane == kEhErr && (err & ~e.head)) s.err[l] = e.head | err;
+  EPROF_T(t4);
+  EPROF_ADD(3, t3, t4);
+  EPROF_ADD(5, t0, t4);
+  if (lane == 0) { EPROF_ADD(6, 0, 1); }
 }
 
 template <bool BKT>
@@ -1005,18 +1052,6 @@ __device__ __forceinline__ uint32_t rec_ld(const uint32_t* p) {
 }
 #ifndef RSF_MERGE_WAVES
 #define RSF_MERGE_WAVES 7  // min waves/SIMD for merge_kernel (register cap; 7 measured fastest with 8 receivers per wave, 8 before)
-#endif
-#ifndef RSF_MERGE_PROF
-#define RSF_MERGE_PROF 0  // diagnostic build: per-phase shader-clock totals of merge_kernel
-#endif
-#if RSF_MERGE_PROF
-__device__ unsigned long long g_merge_prof[8];
-#define MPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#define MPROF_ADD(i, a, b) \
-  if (lane == 0) atomicAdd(&g_merge_prof[i], (unsigned long long)((b) - (a)))
-#else
-#define MPROF_T(v)
-#define MPROF_ADD(i, a, b)
 #endif
 #ifndef RSF_MERGE_CHAIN_BY_SUBJECT
 #define RSF_MERGE_CHAIN_BY_SUBJECT 1  // 1: chain detection loops over distinct subjects, not records
@@ -1200,7 +1235,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
       ru = rumor_from_body(b, key);
     }
     ViewE pre{};
-    if (is_view) pre = vrow[dsub];  // issued beside the rumor-body load
+    if (is_view) pre = vrow[dsub];  // issued beside the rumor-body load (a non-temporal load measured far slower)
     const uint32_t my_subj = is_view ? dsub : 0xFFFFFFFFu;
     // chains: previous / next record of the same subject in this chunk
     int prev = -1, next = -1;
@@ -2694,7 +2729,7 @@ int rsf_gossip_send_buffer(rsf_gossip* g, void** p, uint64_t* cap) {
 // diagnostic only (experiments/merge_prof.py, builds with -DRSF_MERGE_PROF=1): reads and
 // clears merge_kernel's per-phase shader-clock totals; returns -1 in normal builds
 int rsf_gossip_merge_prof(uint64_t* out8) {
-#if RSF_MERGE_PROF
+#if RSF_MERGE_PROF || RSF_EMIT_PROF
   RSF_HIP(hipDeviceSynchronize());
   RSF_HIP(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_merge_prof), 8 * sizeof(uint64_t)));
   unsigned long long z[8] = {};

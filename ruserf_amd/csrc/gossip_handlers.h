@@ -86,7 +86,7 @@ struct GState {
   uint32_t *p_rid, *p_dec, *p_lq;  // [n_loc][kPend]
   uint32_t* p_cnt;                 // [n_loc]
 };
-constexpr uint32_t kPend = 64;  // pending entries per member (one wave's lanes)
+constexpr uint32_t kPend = 128;  // pending entries per member (two per lane of a wave)
 // The merge leaves a member at most kPendMerge entries, so the round's originations and
 // refutations (at most 1 + max_refute <= 5 per member) append without applying the list
 // serially; a member that emits nothing for many rounds can still fill it (then the
