@@ -299,83 +299,81 @@ __device__ __forceinline__ uint32_t q_expire(const GCfg& c, QRegs& Q, uint32_t l
 // one get_broadcasts call on a sorted register-resident queue; returns bytes used.
 // The lowest unpicked lane that fits IS the reference's pick (lowest transmits, then
 // longest fitting, then newest): every skipped lower lane did not fit and never will.
-template <bool PERMUTE_DEC>
+// Written over wave-uniform lane masks (live, picked, kept): the selection loops are
+// scalar work on one 64-bit mask instead of per-lane flags under exec masking.
 #ifndef RSF_EMIT_NT
 #define RSF_EMIT_NT 0  // emit: records written non-temporally
 #endif
+template <bool PERMUTE_DEC>
 __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uint32_t lane, int64_t limit,
                                                     uint32_t* stage_val, uint32_t* stage_dec,
                                                     uint64_t out_base, uint32_t& nrec, uint32_t& err, bool& dirty) {
   const bool valid = lane < c.qcap;
-  const bool live = valid && Q.r != kEmpty;
-  if (!__ballot(live)) return 0;
+  const uint64_t live_m = __ballot(valid && Q.r != kEmpty);  // a sorted queue: a prefix
+  if (!live_m) return 0;
+  const bool live = (live_m >> lane) & 1;
   const uint32_t len = Q.tl >> 16;
-  // Live items are the sorted prefix.  If every earlier item was taken, item i
-  // fits iff the inclusive prefix sum of (overhead + len) is <= limit, so the
-  // leading run of picks comes out of one wave scan; the remaining budget is
-  // then offered to later (shorter) items one by one, as the reference does.
-  const uint32_t cost = live ? c.overhead + len : 0u;
-  const uint32_t incl = wave_inclusive_sum_u32(cost);
-  bool picked = live && limit >= 0 && (int64_t)incl <= limit;
-  const uint64_t run = __ballot(picked);
-  int64_t used = run ? (int64_t)shfl_u32(incl, 63 - __clzll((long long)run)) : 0;
+  // Live items are the sorted prefix.  If every earlier item was taken, item i fits iff
+  // the inclusive prefix sum of (overhead + len) is <= limit, so the leading run of picks
+  // comes out of one wave scan; the remaining budget is then offered to later (shorter)
+  // items one by one, as the reference does.
+  const uint32_t incl = wave_inclusive_sum_u32(live ? c.overhead + len : 0u);
+  uint64_t pick_m = limit >= 0 ? (__ballot((int64_t)incl <= limit) & live_m) : 0ull;
+  int64_t used = pick_m ? (int64_t)shfl_u32(incl, 63 - __clzll((long long)pick_m)) : 0;
   for (;;) {
     const int64_t free_b = limit - used - (int64_t)c.overhead;
     if (free_b <= 0) break;
-    const uint64_t cand = __ballot(live && !picked && (int64_t)len <= free_b);
+    const uint64_t cand = __ballot((int64_t)len <= free_b) & live_m & ~pick_m;
     if (!cand) break;
     const int win = __ffsll((long long)cand) - 1;
-    if ((int)lane == win) picked = true;
+    pick_m |= 1ull << win;
     used += (int64_t)c.overhead + shfl_u32(len, win);
   }
+  if (!pick_m) return used;
   // picks are in ascending lane (= send) order: record rank = picked lanes below
-  const uint64_t pmask = __ballot(picked);
-  if (pmask) {
-    const uint32_t npick = (uint32_t)__popcll(pmask);
-    const uint32_t rank = (uint32_t)__popcll(pmask & below_mask(lane));
-    if (picked && nrec + rank < c.cap_t && stage_val) {
+  const uint64_t below = below_mask(lane);
+  const bool picked = (pick_m >> lane) & 1;
+  const uint32_t npick = (uint32_t)__popcll(pick_m);
+  const uint32_t rank = (uint32_t)__popcll(pick_m & below);
+  if (picked && nrec + rank < c.cap_t && stage_val) {
 #if RSF_EMIT_NT
-      __builtin_nontemporal_store(Q.r, stage_val + out_base + nrec + rank);
-      __builtin_nontemporal_store(Q.dec, stage_dec + out_base + nrec + rank);
+    __builtin_nontemporal_store(Q.r, stage_val + out_base + nrec + rank);
+    __builtin_nontemporal_store(Q.dec, stage_dec + out_base + nrec + rank);
 #else
-      stage_val[out_base + nrec + rank] = Q.r;
-      stage_dec[out_base + nrec + rank] = Q.dec;
+    stage_val[out_base + nrec + rank] = Q.r;
+    stage_dec[out_base + nrec + rank] = Q.dec;
 #endif
-    }
-    if (nrec + npick > c.cap_t) err |= kErrStage;
-    nrec += npick;
   }
-  if (!__ballot(picked)) return used;
+  if (nrec + npick > c.cap_t) err |= kErrStage;
+  nrec += npick;
   dirty = true;
   // transmits+1, or retire at the retransmit limit
-  bool keep = live;
-  if (picked) {
-    if ((Q.tl & 0xFFFF) + 1 >= c.tx_limit) {
-      keep = false;
-      Q.r = kEmpty;
-    } else {
-      Q.tl = Q.tl + 1;
-    }
-  }
-  // re-rank: unpicked keepers and bumped keepers are each still sorted; merge them
-  const bool np = keep && !picked, pk = keep && picked;
-  const uint64_t mykey = keep ? tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq) : ~0ull;
-  const uint64_t npmask = __ballot(np), pkmask = __ballot(pk), deadmask = __ballot(valid && !keep);
-  const uint64_t below = below_mask(lane);
+  const bool retire = picked && (Q.tl & 0xFFFF) + 1 >= c.tx_limit;
+  if (retire) Q.r = kEmpty;
+  else if (picked) Q.tl = Q.tl + 1;
+  // re-rank: the unpicked keepers (np) and the bumped keepers (pk) are each still sorted;
+  // merge them.  Keys are distinct, so for an unpicked lane "bumped key kp < mine" is the
+  // negation of "mine < kp": one compare per bumped item serves both directions.
+  const uint64_t pk_m = pick_m & ~__ballot(retire), np_m = live_m & ~pick_m;
+  const uint64_t kept_m = pk_m | np_m;
+  const bool np = (np_m >> lane) & 1, pk = (pk_m >> lane) & 1;
+  const uint64_t mykey = tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq);
   uint32_t pos;
-  if (np) pos = (uint32_t)__popcll(npmask & below);
-  else if (pk) pos = (uint32_t)__popcll(pkmask & below);
-  else if (valid) pos = (uint32_t)__popcll(npmask | pkmask) + (uint32_t)__popcll(deadmask & below);
+  if (np) pos = (uint32_t)__popcll(np_m & below);
+  else if (pk) pos = (uint32_t)__popcll(pk_m & below);
+  else if (valid) pos = (uint32_t)__popcll(kept_m) + (uint32_t)__popcll(~kept_m & below);
   else pos = lane;
-  uint64_t mm = pkmask;
+  uint64_t mm = pk_m;
+  uint32_t extra = 0;  // bumped lanes: unpicked keepers below them
   while (mm) {
     const int p = __ffsll((long long)mm) - 1;
     mm &= mm - 1;
     const uint64_t kp = shfl_u64(mykey, p);
-    if (np && kp < mykey) pos++;
-    const uint32_t below_p = (uint32_t)__popcll(__ballot(np && mykey < kp));
-    if ((int)lane == p) pos += below_p;
+    const uint64_t gt = __ballot(kp < mykey) & np_m;  // unpicked lanes above bumped p
+    if ((gt >> lane) & 1) pos++;
+    if ((int)lane == p) extra = (uint32_t)__popcll(np_m & ~gt);
   }
+  if (pk) pos += extra;
   const int addr = (int)(pos * 4);
   Q.r = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.r);
   Q.sq = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.sq);
