@@ -43,17 +43,19 @@ def kernel_bytes(qcap, senders, records, fanout=3):
 
     `roofline` (the driver line) prices the merge kernel with SURVEY §8(d)'s model
     only: B_MERGE = 64 B per merged record.  The extended model (reported beside it)
-    adds what this engine's queue model must also move (intents
-    only: the query/event queues stay empty; the intent queue is 12 B per slot):
-    emit  : per live sender its peers + group slots (8 B per peer), the intent queue
-            read and written back (it is re-ranked after every pick), and per record
-            the rumor id + decoration written (8 B), per group its count (4 B)
-    merge : B_MERGE per record plus each receiver's intent queue read and written
-            back (re-queues)."""
-    queue_rw = 2 * qcap * 12
-    emit = senders * (fanout * 8 + queue_rw + fanout * 4) + records * 8
+    adds what this engine's queue model must also move (intents only:
+    the query/event queues stay empty):
+    emit  : per live sender its peers + group slots (8 B per peer), the intent queue read
+            and written back (16 B per slot: rumor id, seq, transmits|len, decoration; it
+            is re-ranked after every pick), its pending re-queues read (12 B each, about
+            one per record merged), and per record the rumor id + decoration written
+            (8 B), per group its count (4 B)
+    merge : B_MERGE per record plus the re-queue appended to the receiver's pending list
+            (12 B; the merge no longer reads or writes the queues)."""
+    queue_rw = 2 * qcap * 16
+    emit = senders * (fanout * 8 + queue_rw + fanout * 4) + records * (8 + 12)
     merge_s8d = records * B_MERGE
-    merge_ext = merge_s8d + senders * queue_rw
+    merge_ext = merge_s8d + records * 12
     return emit, merge_s8d, merge_ext
 
 
@@ -163,8 +165,8 @@ def run_gossip(args, rank, world):
                      "bytes_per_launch": merge_b, "avg_launch_ms": avg[dom],
                      "extended": {"bytes_per_launch": merge_ext, "achieved": achieved_ext,
                                   "frac": achieved_ext / HBM_PEAK_GBS,
-                                  "model": "B_merge per record + each receiver's intent queue read + "
-                                           "written back (2 x queue_cap x 12 B)"},
+                                  "model": "B_merge per record + its re-queue appended to the "
+                                           "receiver's pending list (12 B)"},
                      "emit_kernel": {"avg_launch_ms": avg[2], "bytes_per_launch": emit_b,
                                      "achieved": emit_b / (avg[2] / 1e3) / 1e9 if avg[2] else None}},
     }

@@ -1,0 +1,8 @@
+#!/bin/bash
+# current tree: default bench line, rocprofv3 of the gossip round, forced multi-GPU path on one GPU
+S=scripts/gpu_step.sh
+bash $S bench_default 500 python -u bench.py && \
+bash scripts/profile.sh r02x_gossip gossip --no-vivaldi && \
+bash $S bench_single 300 python -u bench.py --workload gossip --steps 20 --warmup 3 --no-cpu-baseline --no-vivaldi && \
+RSF_FORCE_SHARDED=1 bash $S bench_sharded1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+  --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 1 --workload gossip --steps 20 --warmup 3 --no-cpu-baseline --no-vivaldi

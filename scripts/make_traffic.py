@@ -12,9 +12,9 @@ non-temporal loads alike: stream_read*_nt); byte-wide loads (the u8 window index
 tallied at all (stream_read1), so they are added from the model:
     traffic = 2*(FETCH - 0.998*gather) + gather + idx + WRITE   (idx = 1 B per member).
 The modelled FETCH (streams/2 + 0.998*gather) is printed beside the measured one.
-Gossip (merge_kernel): the streamed bytes are modelled (the intent queue, qcap x 12 B per
-receiver, and the (sender, peer) groups' record slots, cap_t x 8 B + a 4-B count each) and
-corrected (x2); the rest of FETCH is gather:  traffic = FETCH + stream/2 + WRITE."""
+Gossip (merge_kernel): the streamed bytes are modelled (the (sender, peer) groups' record
+slots, cap_t x 8 B + a 4-B count each) and corrected (x2); the rest of FETCH is gather:
+traffic = FETCH + stream/2 + WRITE."""
 import csv
 import collections
 import json
@@ -61,10 +61,11 @@ n = line["config"]["members_per_gpu"]
 qcap = line["config"]["queue_cap_per_queue"]
 fanout = line["config"]["fanout"]
 cap_t = line["config"]["record_slots_per_group"]
-# coalesced streams of merge_kernel (tallied at 1/2 by FETCH_SIZE): the intent queue
-# (12 B per slot) and the group slots it reads (rumor id + decoration, 8 B per slot; one
-# group per (sender, peer), n * fanout in all) with their counts (4 B per group)
-stream_merge = n * qcap * 12 + n * fanout * (cap_t * 8 + 4)
+# coalesced streams of merge_kernel (tallied at 1/2 by FETCH_SIZE): the (sender, peer) groups'
+# record slots (rumor id + decoration, 8 B per slot; one group per (sender, peer), n * fanout
+# in all) with their counts (4 B per group).  The merge no longer reads the broadcast queues
+# (re-queues go to the pending lists, written, not read).
+stream_merge = n * fanout * (cap_t * 8 + 4)
 traffic = f_merge + stream_merge / 2 + w_merge
 res["gossip"] = {"kernel": "merge_kernel", "members_per_gpu": n, "traffic_bytes_per_launch": traffic,
                  "fetch_counter": f_merge, "write_counter": w_merge, "stream_bytes_modelled": stream_merge,
