@@ -296,6 +296,12 @@ __device__ __forceinline__ uint32_t q_expire(const GCfg& c, QRegs& Q, uint32_t l
   return (uint32_t)__popcll(sm);
 }
 
+// One LDS row per wave: scratch of the batched insert (q_insert_batch_lds) and of the
+// re-rank after a pick (q_get_broadcasts).
+struct alignas(16) QLds {
+  uint32_t r[kWave], sq[kWave], tl[kWave], dec[kWave];
+};
+
 // one get_broadcasts call on a sorted register-resident queue; returns bytes used.
 // The lowest unpicked lane that fits IS the reference's pick (lowest transmits, then
 // longest fitting, then newest): every skipped lower lane did not fit and never will.
@@ -307,7 +313,8 @@ __device__ __forceinline__ uint32_t q_expire(const GCfg& c, QRegs& Q, uint32_t l
 template <bool PERMUTE_DEC>
 __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uint32_t lane, int64_t limit,
                                                     uint32_t* stage_val, uint32_t* stage_dec,
-                                                    uint64_t out_base, uint32_t& nrec, uint32_t& err, bool& dirty) {
+                                                    uint64_t out_base, uint32_t& nrec, uint32_t& err, bool& dirty,
+                                                    QLds& row) {
   const bool valid = lane < c.qcap;
   const uint64_t live_m = __ballot(valid && Q.r != kEmpty);  // a sorted queue: a prefix
   if (!live_m) return 0;
@@ -352,28 +359,40 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   if (retire) Q.r = kEmpty;
   else if (picked) Q.tl = Q.tl + 1;
   // re-rank: the unpicked keepers (np) and the bumped keepers (pk) are each still sorted;
-  // merge them.  Keys are distinct, so for an unpicked lane "bumped key kp < mine" is the
-  // negation of "mine < kp": one compare per bumped item serves both directions.
+  // merge them.  Each list's keys go to the wave's LDS row in order, and every keeper
+  // counts the other list's keys below its own by a binary search there (keys are
+  // distinct), all lanes at once: a handful of LDS reads instead of a wave-wide pass per
+  // bumped item.
   const uint64_t pk_m = pick_m & ~__ballot(retire), np_m = live_m & ~pick_m;
   const uint64_t kept_m = pk_m | np_m;
   const bool np = (np_m >> lane) & 1, pk = (pk_m >> lane) & 1;
   const uint64_t mykey = tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq);
+  uint64_t* const keys_np = reinterpret_cast<uint64_t*>(row.r);  // r + sq: 64 keys
+  uint64_t* const keys_pk = reinterpret_cast<uint64_t*>(row.tl);  // tl + dec: 64 keys
+  const uint32_t r_np = (uint32_t)__popcll(np_m & below), r_pk = (uint32_t)__popcll(pk_m & below);
+  if (np) keys_np[r_np] = mykey;
+  if (pk) keys_pk[r_pk] = mykey;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   uint32_t pos;
-  if (np) pos = (uint32_t)__popcll(np_m & below);
-  else if (pk) pos = (uint32_t)__popcll(pk_m & below);
-  else if (valid) pos = (uint32_t)__popcll(kept_m) + (uint32_t)__popcll(~kept_m & below);
-  else pos = lane;
-  uint64_t mm = pk_m;
-  uint32_t extra = 0;  // bumped lanes: unpicked keepers below them
-  while (mm) {
-    const int p = __ffsll((long long)mm) - 1;
-    mm &= mm - 1;
-    const uint64_t kp = shfl_u64(mykey, p);
-    const uint64_t gt = __ballot(kp < mykey) & np_m;  // unpicked lanes above bumped p
-    if ((gt >> lane) & 1) pos++;
-    if ((int)lane == p) extra = (uint32_t)__popcll(np_m & ~gt);
+  if (np || pk) {
+    const uint64_t* other = np ? keys_pk : keys_np;
+    uint32_t lo = 0, len = (uint32_t)__popcll(np ? pk_m : np_m);
+    while (len) {  // lower_bound of mykey in the other list
+      const uint32_t half = len >> 1;
+      if (other[lo + half] < mykey) {
+        lo += half + 1;
+        len -= half + 1;
+      } else {
+        len = half;
+      }
+    }
+    pos = (np ? r_np : r_pk) + lo;
+  } else {
+    pos = valid ? (uint32_t)__popcll(kept_m) + (uint32_t)__popcll(~kept_m & below) : lane;
   }
-  if (pk) pos += extra;
+  __builtin_amdgcn_wave_barrier();  // the row is free once every lane has searched it
   const int addr = (int)(pos * 4);
   Q.r = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.r);
   Q.sq = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.sq);
@@ -381,11 +400,6 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   if (PERMUTE_DEC) Q.dec = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.dec);
   return used;
 }
-
-// One LDS row per wave: scratch of the batched insert (q_insert_batch_lds).
-struct QLds {
-  uint32_t r[kWave], sq[kWave], tl[kWave], dec[kWave];
-};
 
 // Batched insert of new items (transmits 0, seqs seq0, seq0 + 1, ... in lane order over
 // `newmask`) into a sorted register-resident queue: the result is the qcap smallest keys of
@@ -906,9 +920,9 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
     }
     uint32_t nrec = 0;
     int64_t used = 0;
-    used += q_get_broadcasts<true>(c, Q0, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d0);
-    used += q_get_broadcasts<false>(c, Q1, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d1);
-    used += q_get_broadcasts<false>(c, Q2, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d2);
+    used += q_get_broadcasts<true>(c, Q0, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d0, row);
+    used += q_get_broadcasts<false>(c, Q1, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d1, row);
+    used += q_get_broadcasts<false>(c, Q2, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d2, row);
     if (lane == 0 && oc && nrec) *oc = min(nrec, c.cap_t);
   }
   EPROF_T(t3);
