@@ -70,7 +70,8 @@ def run_gossip(args, rank, world):
     subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED, prune_frac=PRUNE_FRAC)
     views = W.initial_views(SUBJECTS)
     stream = torch.cuda.current_stream()
-    if world == 1 and os.environ.get("RSF_FORCE_SHARDED") != "1":
+    sharded = not (world == 1 and os.environ.get("RSF_FORCE_SHARDED") != "1")
+    if not sharded:
         eng = GossipEngine(cfg, device=torch.cuda.current_device())
         eng.set_stream(stream.cuda_stream)
         step_fn = lambda t: eng.round(t, ml[t], acts[t])  # noqa: E731
@@ -103,6 +104,8 @@ def run_gossip(args, rank, world):
     if world > 1:
         torch.distributed.barrier()
     wall = time.perf_counter() - t0
+    # multi-GPU path: no bucket overflowed and every record reached its shard (read after timing)
+    exchange_ok = sg.check() if sharded else None
     phase_ms, nr = eng.phase_times()
     merged = eng.merged_total() - merged0
     pruned = eng.pruned_total(flush=False) - pruned0
@@ -114,13 +117,14 @@ def run_gossip(args, rank, world):
     eng.set_profiling(False)
     if world > 1:
         dev = "cpu" if torch.distributed.get_backend() == "gloo" else "cuda"
-        t_ = torch.tensor([wall, float(merged), float(err_members), float(pruned), float(qprune_members)],
-                          dtype=torch.float64, device=dev)
+        t_ = torch.tensor([wall, float(merged), float(err_members), float(pruned), float(qprune_members),
+                           float(bool(exchange_ok))], dtype=torch.float64, device=dev)
         mx = t_.clone()
         torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX)
         torch.distributed.all_reduce(t_)
         wall, merged_all, err_all, pruned_all, qpm_all = float(mx[0]), float(t_[1]), float(t_[2]), float(t_[3]), \
             float(t_[4])
+        exchange_ok = int(t_[5]) == world  # every rank's buckets held
     else:
         merged_all, err_all, pruned_all, qpm_all = float(merged), float(err_members), float(pruned), \
             float(qprune_members)
@@ -153,6 +157,7 @@ def run_gossip(args, rank, world):
         "merges_per_s": merged_all / wall,
         "records_per_round_per_gpu": records,
         "error_members": err_all,
+        "exchange_ok": exchange_ok,
         # the bounded queue model (queue_cap slots) drops live items when full; counted, not silent
         "queue_pruned_per_round": pruned_all / args.steps,
         "queue_pruned_per_merged_record": pruned_all / max(1.0, merged_all),

@@ -345,10 +345,10 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   if (picked && nrec + rank < c.cap_t && stage_val) {
 #if RSF_EMIT_NT
     __builtin_nontemporal_store(Q.r, stage_val + out_base + nrec + rank);
-    __builtin_nontemporal_store(Q.dec, stage_dec + out_base + nrec + rank);
+    if (stage_dec) __builtin_nontemporal_store(Q.dec, stage_dec + out_base + nrec + rank);
 #else
     stage_val[out_base + nrec + rank] = Q.r;
-    stage_dec[out_base + nrec + rank] = Q.dec;
+    if (stage_dec) stage_dec[out_base + nrec + rank] = Q.dec;
 #endif
   }
   if (nrec + npick > c.cap_t) err |= kErrStage;
@@ -778,9 +778,11 @@ __global__ void __launch_bounds__(256) grp_index_kernel(const uint32_t* __restri
 #endif
 
 // Multi-GPU exchange buckets (rsf_gossip_round_emit_buckets): one bucket per destination
-// shard, u32 layout [n_groups, 3 x pad | keys[gcap] | cnt[gcap] | vals[gcap * cap_t] |
-// decs[gcap * cap_t]]; the groups of a bucket are sorted by receiver.  On the receive side
-// the world's buckets arrive back to back in source-rank order = runs.
+// shard, u32 layout [n_groups, 3 x pad | keys[gcap] | cnt[gcap] | vals[gcap * cap_t]]; the
+// groups of a bucket are sorted by receiver.  On the receive side the world's buckets arrive
+// back to back in source-rank order = runs.  Record decorations do not travel: every shard
+// holds the whole rumor table, so the receive side rebuilds them from the rumor ids into a
+// local array (`decs`, [run][gcap * cap_t]) -- 44 B per group on the wire instead of 80.
 constexpr uint32_t kMaxRuns = 8;
 struct Buckets {
   const uint32_t* base;  // receive buffer (RUNS merge); emission writes through `send`
@@ -788,7 +790,8 @@ struct Buckets {
   const uint32_t* wstart;  // emission: per destination shard, its first group in sorted order
   uint64_t per;            // members per shard
   uint64_t stride_u32;   // one bucket
-  uint32_t keys_off, cnt_off, vals_off, decs_off, gcap, n_runs;
+  const uint32_t* decs;  // receive side: the records' decorations, [run][gcap * cap_t]
+  uint32_t keys_off, cnt_off, vals_off, gcap, n_runs;
 };
 
 #ifndef RSF_MERGE_PROF
@@ -911,7 +914,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
       uint32_t* b = bk.send + (uint64_t)w * bk.stride_u32;
       if (idx < bk.gcap) {
         ov = b + bk.vals_off;
-        od = b + bk.decs_off;
+        od = nullptr;  // decorations are rebuilt on the receive side
         oc = b + bk.cnt_off + idx;
         out_base = (uint64_t)idx * c.cap_t;
       } else {
@@ -1218,7 +1221,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
       const uint32_t* b = bk.base + (uint64_t)r * bk.stride_u32;
       if (in) {
         rid0 = rec_ld(b + bk.vals_off + g * stride + gk);
-        dsub0 = rec_ld(b + bk.decs_off + g * stride + gk);
+        dsub0 = rec_ld(bk.decs + (uint64_t)r * bk.gcap * stride + g * stride + gk);
         gc = rec_ld(b + bk.cnt_off + g);
       }
     } else {
@@ -1940,40 +1943,51 @@ __global__ void __launch_bounds__(256) bucket_fill_kernel(const uint32_t* __rest
 }
 // receive side: per (run r, receiver) the range of its groups in bucket r; the records
 // merged (group counts) summed for the statistics; a receiver outside the shard or an
-// unsorted bucket is flagged
+// unsorted bucket is flagged.  Grid-stride over a bounded grid: one atomic per block (an
+// atomic per 256 groups on one address serialised into ~0.25 ms at 6M groups).
+constexpr unsigned kBucketIndexBlocks = 1024;
 __global__ void __launch_bounds__(256) bucket_index_kernel(Buckets bk, uint64_t lo, uint64_t n_loc,
                                                            uint32_t* __restrict__ rstart, uint32_t* __restrict__ rend,
                                                            unsigned long long* __restrict__ merged,
                                                            unsigned long long* __restrict__ flags) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t r = (uint32_t)(t / bk.gcap), i = (uint32_t)(t % bk.gcap);
-  uint32_t cnt = 0;
-  if (r < bk.n_runs) {
+  const uint64_t n = (uint64_t)bk.n_runs * bk.gcap;
+  uint64_t sum = 0;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = (uint32_t)(t / bk.gcap), i = (uint32_t)(t % bk.gcap);
     const uint32_t* b = bk.base + (uint64_t)r * bk.stride_u32;
     const uint32_t ng = b[0];
-    if (i < ng) {
-      const uint32_t key = b[bk.keys_off + i];
-      const uint64_t l = (uint64_t)key - lo;
-      cnt = b[bk.cnt_off + i];
-      if (l >= n_loc || (i > 0 && b[bk.keys_off + i - 1] > key)) {
-        atomicOr(flags, 2ull);
-        cnt = 0;
-      } else {
-        if (i == 0 || b[bk.keys_off + i - 1] != key) rstart[(uint64_t)r * n_loc + l] = i;
-        if (i + 1 == ng || b[bk.keys_off + i + 1] != key) rend[(uint64_t)r * n_loc + l] = i + 1;
-      }
+    if (i >= ng) continue;
+    const uint32_t key = b[bk.keys_off + i];
+    const uint64_t l = (uint64_t)key - lo;
+    if (l >= n_loc || (i > 0 && b[bk.keys_off + i - 1] > key)) {
+      atomicOr(flags, 2ull);
+      continue;
     }
+    sum += b[bk.cnt_off + i];
+    if (i == 0 || b[bk.keys_off + i - 1] != key) rstart[(uint64_t)r * n_loc + l] = i;
+    if (i + 1 == ng || b[bk.keys_off + i + 1] != key) rend[(uint64_t)r * n_loc + l] = i + 1;
   }
-  // block sum of the records, one atomic per block
-  __shared__ uint32_t part[4];
-  uint32_t v = cnt;
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+  __shared__ uint64_t part[4];
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = sum;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned long long sum = (unsigned long long)part[0] + part[1] + part[2] + part[3];
-    if (sum) atomicAdd(merged, sum);
+    const unsigned long long tot = part[0] + part[1] + part[2] + part[3];
+    if (tot) atomicAdd(merged, tot);
   }
+}
+// receive side: every record slot of a received group gets its decoration from the
+// replicated rumor table (slots past the group's count are never read by the merge)
+__global__ void __launch_bounds__(256) bucket_dec_kernel(Buckets bk, uint32_t cap_t, const uint32_t* __restrict__ rdec,
+                                                         uint32_t rmask, uint32_t* __restrict__ decs) {
+  const uint64_t per = (uint64_t)bk.gcap * cap_t;
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t r = (uint32_t)(t / per);
+  if (r >= bk.n_runs) return;
+  const uint64_t i = t - (uint64_t)r * per, grp = i / cap_t;
+  const uint32_t* b = bk.base + (uint64_t)r * bk.stride_u32;
+  if (grp >= b[0] || (uint32_t)(i - grp * cap_t) >= b[bk.cnt_off + grp]) return;
+  decs[t] = rdec[b[bk.vals_off + i] & rmask];
 }
 
 // counters[60] (records merged since creation) += counters[from] (this round's)
@@ -2029,7 +2043,7 @@ struct rsf_gossip {
   uint32_t cur_round = 0;
   bool merged_from_stage = true, merged_from_buckets = false;
   // bucket exchange: send / receive buffers (world buckets each), group ranges per run
-  uint32_t *bkt_send = nullptr, *bkt_recv = nullptr, *d_rstart = nullptr, *d_rend = nullptr, *d_wstart = nullptr;
+  uint32_t *bkt_send = nullptr, *bkt_recv = nullptr, *bkt_dec = nullptr, *d_rstart = nullptr, *d_rend = nullptr, *d_wstart = nullptr;
   uint32_t bkt_world = 0, bkt_gcap = 0;
   uint64_t total_merged_host = 0;  // multi-GPU merges (n_recv known on host)
   // run-merge tables of rsf_gossip_round_merge_runs: [run_cap][n_loc] u32 x3, [n_loc] u32
@@ -2258,7 +2272,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   g->sort_tmp, g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
                   g->scan_tmp, g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
                   g->grp_slot, g->grp_off, g->stage_dec, g->grp_scan_tmp, s.dlog, s.dcnt,
-                  g->bkt_send, g->bkt_recv, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn,
+                  g->bkt_send, g->bkt_recv, g->bkt_dec, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn,
                   s.p_rid, s.p_dec, s.p_lq, s.p_cnt, g->big_ids};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -2595,8 +2609,7 @@ static Buckets bucket_layout(const rsf_gossip* g, uint32_t world) {
   b.keys_off = 4;
   b.cnt_off = b.keys_off + b.gcap;
   b.vals_off = b.cnt_off + b.gcap;
-  b.decs_off = b.vals_off + b.gcap * c.cap_t;
-  b.stride_u32 = ((uint64_t)b.decs_off + (uint64_t)b.gcap * c.cap_t + 63) & ~63ull;  // 256-B aligned buckets
+  b.stride_u32 = ((uint64_t)b.vals_off + (uint64_t)b.gcap * c.cap_t + 63) & ~63ull;  // 256-B aligned buckets
   b.per = world ? c.N / world : c.N;
   b.n_runs = world;
   return b;
@@ -2606,6 +2619,7 @@ static Buckets send_buckets(rsf_gossip* g) {
   b.send = g->bkt_send;
   b.wstart = g->d_wstart;
   b.base = g->bkt_recv;
+  b.decs = g->bkt_dec;
   return b;
 }
 
@@ -2643,9 +2657,9 @@ int rsf_gossip_bucket_buffers(rsf_gossip* g, uint32_t world, void** send, void**
   if (world != g->bkt_world) {
     RSF_HIP(hipSetDevice(g->device));
     RSF_HIP(hipStreamSynchronize(g->stream));
-    for (void* p : {(void*)g->bkt_send, (void*)g->bkt_recv, (void*)g->d_rstart, (void*)g->d_rend})
+    for (void* p : {(void*)g->bkt_send, (void*)g->bkt_recv, (void*)g->bkt_dec, (void*)g->d_rstart, (void*)g->d_rend})
       if (p) hipFree(p);
-    g->bkt_send = g->bkt_recv = g->d_rstart = g->d_rend = nullptr;
+    g->bkt_send = g->bkt_recv = g->bkt_dec = g->d_rstart = g->d_rend = nullptr;
     g->bkt_world = 0;
     // groups per destination: n_loc * fanout / world for uniform peers; the capacity holds
     // 1/8 more plus 4096 (overflow is flagged, rsf_gossip_bucket_status)
@@ -2656,6 +2670,7 @@ int rsf_gossip_bucket_buffers(rsf_gossip* g, uint32_t world, void** send, void**
     const size_t bytes = (size_t)b.stride_u32 * 4 * world;
     int rc;
     if ((rc = rsf::dmalloc((void**)&g->bkt_send, bytes)) || (rc = rsf::dmalloc((void**)&g->bkt_recv, bytes)) ||
+        (rc = rsf::dmalloc((void**)&g->bkt_dec, (size_t)world * gcap * c.cap_t * 4)) ||
         (rc = rsf::dmalloc((void**)&g->d_rstart, (size_t)world * c.n_loc * 4)) ||
         (rc = rsf::dmalloc((void**)&g->d_rend, (size_t)world * c.n_loc * 4)))
       return rc;
@@ -2689,8 +2704,11 @@ int rsf_gossip_round_merge_buckets(rsf_gossip* g, uint32_t world) {
   RSF_HIP(hipMemsetAsync(g->d_rstart, 0, (size_t)world * c.n_loc * 4, st));
   RSF_HIP(hipMemsetAsync(g->d_rend, 0, (size_t)world * c.n_loc * 4, st));
   RSF_HIP(hipMemsetAsync(g->d_counters + 57, 0, 8, st));
-  hipLaunchKernelGGL(bucket_index_kernel, dim3(grid1((uint64_t)world * bk.gcap)), dim3(256), 0, st, bk, c.lo, c.n_loc,
-                     g->d_rstart, g->d_rend, g->d_counters + 57, g->d_counters + 58);
+  hipLaunchKernelGGL(bucket_index_kernel, dim3(std::min<uint64_t>(grid1((uint64_t)world * bk.gcap), kBucketIndexBlocks)),
+                     dim3(256), 0, st, bk, c.lo, c.n_loc, g->d_rstart, g->d_rend, g->d_counters + 57,
+                     g->d_counters + 58);
+  hipLaunchKernelGGL(bucket_dec_kernel, dim3(grid1((uint64_t)world * bk.gcap * c.cap_t)), dim3(256), 0, st, bk, c.cap_t,
+                     (const uint32_t*)g->s.rdec, c.rmask, g->bkt_dec);
   hipLaunchKernelGGL(accumulate_kernel, dim3(1), dim3(64), 0, st, g->d_counters, 57u);
   if (g->profiling && g->prof_rounds < rsf_gossip::kMaxProfRounds)
     hipEventRecord(g->ev[g->prof_rounds][3], g->stream);  // exchange time lands in the sort slot
