@@ -482,10 +482,10 @@ __device__ __forceinline__ void pend_load(const GState& s, uint64_t l, uint32_t 
   for (uint32_t b = 0; b < 2; ++b) {
     p.rid[b] = p.dec[b] = p.lq[b] = 0;
     if (b * kWave + lane < n) {
-      const uint64_t i = l * kPend + b * kWave + lane;
-      p.rid[b] = s.p_rid[i];
-      p.dec[b] = s.p_dec[i];
-      p.lq[b] = s.p_lq[i];
+      const GState::PendE e = s.p_ent[l * kPend + b * kWave + lane];
+      p.rid[b] = e.rid;
+      p.dec[b] = e.dec;
+      p.lq[b] = e.lq;
     }
   }
 }
@@ -1174,9 +1174,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     return;
   }
   uint32_t qdrop = 0;  // live queue items dropped by full queues (a list applied here)
-  uint32_t* const p_rid = s.p_rid + l * kPend;
-  uint32_t* const p_dec = s.p_dec + l * kPend;
-  uint32_t* const p_lq = s.p_lq + l * kPend;
+  GState::PendE* const p_ent = s.p_ent + l * kPend;
   MRegs r;
   r.clock = su64(su, kSuClock);
   r.eclock = su64(su, kSuEClock);
@@ -1349,9 +1347,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
       const uint32_t k = (uint32_t)__popcll(newmask);
       if (ins) {
         const uint32_t i = pn + (uint32_t)__popcll(newmask & below_mask(lane));
-        p_rid[i] = rid;
-        p_dec[i] = dsub;
-        p_lq[i] = ru.msg_len;  // queue 0
+        p_ent[i] = GState::PendE{rid, dsub, ru.msg_len};  // queue 0
       }
       pn += k;
       pc += k;
@@ -1393,9 +1389,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
       const uint32_t q = queue_of(type);
       if ((fi & RSF_F_REBROADCAST) && q != kQIntent) {  // intents went in above, batched per chunk
         if (lane == 0) {
-          p_rid[pn] = shfl_u32(rid, i);
-          p_dec[pn] = q == kQQuery ? kDecQuery : kDecEvent;
-          p_lq[pn] = (tf >> 16) | (q << 16);
+          p_ent[pn] = GState::PendE{shfl_u32(rid, i), q == kQQuery ? kDecQuery : kDecEvent, (tf >> 16) | (q << 16)};
         }
         pn++;
         pc += 1u << (8 * q);
@@ -2179,7 +2173,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
       GA(s.qb_cnt, n * c.qbuf * 4) || GA(s.qb_ids, n * c.qbuf * c.slot_k * 4) ||
       GA(s.rumors, (size_t)cfg->max_rumors * 2 * sizeof(rsf_rumor)) ||
       GA(s.rdec, (size_t)cfg->max_rumors * 2 * 4) || GA(s.rbody, (size_t)cfg->max_rumors * 2 * 16) ||
-      GA(s.p_rid, n * kPend * 4) || GA(s.p_dec, n * kPend * 4) || GA(s.p_lq, n * kPend * 4) || GA(s.p_cnt, n * 4))
+      GA(s.p_ent, n * kPend * sizeof(GState::PendE)) || GA(s.p_cnt, n * 4))
     return fail(rc);
   g->stage_cap = n * c.fanout * c.cap_t;
   if (g->stage_cap >= 0xFFFFFFFFull) return fail(gerr("n_members x fanout x per-target records must fit 32 bits"));
@@ -2273,7 +2267,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   g->scan_tmp, g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
                   g->grp_slot, g->grp_off, g->stage_dec, g->grp_scan_tmp, s.dlog, s.dcnt,
                   g->bkt_send, g->bkt_recv, g->bkt_dec, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn,
-                  s.p_rid, s.p_dec, s.p_lq, s.p_cnt, g->big_ids};
+                  s.p_ent, s.p_cnt, g->big_ids};
   for (void* p : ptrs)
     if (p) hipFree(p);
   g->scratch.release();

@@ -83,7 +83,7 @@ struct GState {
   // the largest key is order-free between picks (the queue keeps the qcap smallest keys of
   // everything inserted), so the deferred batch is exactly the reference's one-by-one
   // insert.  p_cnt[l] packs the entries per queue: n0 | n1 << 8 | n2 << 16 (sum <= kPend).
-  uint32_t *p_rid, *p_dec, *p_lq;  // [n_loc][kPend]
+  struct PendE { uint32_t rid, dec, lq; } * p_ent;  // [n_loc][kPend], 12-B entries: one contiguous append
   uint32_t* p_cnt;                 // [n_loc]
 };
 constexpr uint32_t kPend = 128;  // pending entries per member (two per lane of a wave)
@@ -438,8 +438,9 @@ __device__ __forceinline__ void queue_insert_item(const GCfg& c, const GState& s
 __device__ __forceinline__ void pend_flush_serial(const GCfg& c, const GState& s, uint64_t l, MRegs& r) {
   const uint32_t n = pend_total(s.p_cnt[l]);
   for (uint32_t i = 0; i < n; ++i) {
-    const uint32_t lq = s.p_lq[l * kPend + i], q = lq >> 16;
-    queue_insert_item(c, s, l, q, s.p_rid[l * kPend + i], s.p_dec[l * kPend + i], lq & 0xFFFF,
+    const GState::PendE e = s.p_ent[l * kPend + i];
+    const uint32_t q = e.lq >> 16;
+    queue_insert_item(c, s, l, q, e.rid, e.dec, e.lq & 0xFFFF,
                       s.q_next_seq[l * 3 + q]++, r);
   }
   s.p_cnt[l] = 0;
@@ -454,9 +455,7 @@ __device__ __forceinline__ void pend_push_serial(const GCfg& c, const GState& s,
     pc = 0;
   }
   const uint32_t i = pend_total(pc);
-  s.p_rid[l * kPend + i] = rid;
-  s.p_dec[l * kPend + i] = dec;
-  s.p_lq[l * kPend + i] = len | (q << 16);
+  s.p_ent[l * kPend + i] = GState::PendE{rid, dec, len | (q << 16)};
   s.p_cnt[l] = pc + (1u << (8 * q));
 }
 
