@@ -255,6 +255,17 @@ def attach_traffic(workload, res):
     rl["traffic_unit"] = "bytes/launch"
     rl["traffic_vs_algorithmic"] = ent["traffic_bytes_per_launch"] / rl["bytes_per_launch"]
     rl["traffic_source"] = ent["source"]
+    # the dominant kernel against the floor of its access pattern (random 64-B sectors read
+    # and written), measured by a microbenchmark with no protocol logic
+    try:
+        with open(os.path.join(ROOT, "profiles", "pattern_floor.json")) as f:
+            fl = json.load(f).get(workload)
+    except (OSError, ValueError):
+        fl = None
+    if fl and fl["kernel"] == rl["kernel"] and fl["members_per_gpu"] == res["config"]["members_per_gpu"]:
+        rl["pattern_floor"] = {"ms": fl["floor_ms"], "kernel_ms": rl["avg_launch_ms"],
+                               "floor_over_kernel": fl["floor_ms"] / rl["avg_launch_ms"], "what": fl["what"],
+                               "source": fl["source"]}
 
 
 # --------------------------------------------------------------------------- main

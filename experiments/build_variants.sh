@@ -9,7 +9,7 @@ mkdir -p experiments/libs
 while [ $# -gt 1 ]; do
   name=$1; defs=$2; shift 2
   d=experiments/libs/build_$name; mkdir -p $d
-  for s in capi vivaldi gossip codec coalesce swim; do /opt/rocm/bin/hipcc $F $defs -c $CS/$s.hip -o $d/$s.o & done; wait
+  for s in capi vivaldi gossip codec coalesce swim intern; do /opt/rocm/bin/hipcc $F $defs -c $CS/$s.hip -o $d/$s.o & done; wait
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o experiments/libs/lib_$name.so $d/*.o
   echo built $name
 done

@@ -607,6 +607,29 @@ int rsf_coord_encode(const double* rows, uint32_t dim, uint32_t row_stride, uint
 int rsf_coord_decode(const uint8_t* in, const uint64_t* off, uint64_t n, int ping_version_prefix, double* rows,
                      uint32_t row_stride, uint32_t max_dim, uint32_t* dim_out, int32_t* status, void* stream);
 
+/* Device-side interning of user-event names and payloads: a user event's identity
+ * `(name, payload)`, compared by value in handle_user_event (core/src/serf/base.rs:801-806)
+ * and by name in the coalescer (coalesce/user.rs:60-75), becomes the exact key
+ * (name_id << 32) | payload_id of rsf_action.key / rsf_msg.key without a host table.
+ * Equal bytes <-> equal id (bytes are compared; FNV-1a only picks the probe start);
+ * new strings take ids in order of first occurrence in the batch, so ids equal those
+ * of a host interner walking the strings in order. */
+typedef struct rsf_interner rsf_interner;
+int rsf_interner_create(rsf_interner** out, uint32_t max_ids, uint64_t arena_bytes, int device);
+int rsf_interner_destroy(rsf_interner* t);
+/* ids committed so far and arena bytes used (host values; no synchronisation) */
+int rsf_interner_count(const rsf_interner* t, uint32_t* n_ids, uint64_t* arena_used);
+/* ids[i] = id of bytes [buf + off[i], + len[i]); len[i] == 0xFFFFFFFF: nothing to intern,
+ * ids[i] = 0xFFFFFFFF.  Device pointers; synchronises `stream` once (to size the new
+ * strings); RSF_ERR_OVERFLOW (nothing committed) when max_ids or the arena would overflow */
+int rsf_intern(rsf_interner* t, const uint8_t* buf, const uint64_t* off, const uint32_t* len, uint64_t n,
+               uint32_t* ids, void* stream);
+/* decoded frames (rsf_wire_decode over buf) -> keys[i] = (name_id << 32) | payload_id for a
+ * decoded user event, 0 otherwise: the wire-bytes -> identity step of notify_message
+ * (delegate.rs:157-305) on the device */
+int rsf_wire_event_keys(rsf_interner* names, rsf_interner* payloads, const uint8_t* buf, const rsf_wire_msg* msgs,
+                        uint64_t n, uint64_t* keys, void* stream);
+
 /* ======================================================================== */
 /* memberlist SWIM layer model                        */
 /* ======================================================================== */

@@ -1,0 +1,125 @@
+"""Device interning (csrc/intern.hip): ids equal a host interner walking the strings in
+order (first occurrence -> next id), across batches; overflow commits nothing; and the
+wire path end to end on the device: frames -> rsf_wire_decode -> rsf_wire_event_keys ->
+notify_message (rsf_gossip_apply_batch) with the dedup of handle_user_event
+(base.rs:770-837) against the oracle fed host-interned keys."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import codec_oracle as CO
+import gossip_harness as H
+import oracle_ffi as O
+from ruserf_amd import codec as K
+from ruserf_amd import gossip as G
+from ruserf_amd import workload as W
+from ruserf_amd._lib import EngineError
+from ruserf_amd.intern import NO_STRING, Interner, wire_event_keys
+
+pytestmark = pytest.mark.gpu
+
+
+class HostInterner:
+    def __init__(self):
+        self.ids = {}
+
+    def __call__(self, s):
+        if s is None:
+            return NO_STRING
+        return self.ids.setdefault(bytes(s), len(self.ids))
+
+
+def vocabulary(rng, k):
+    words = {b"", b"a", b"aa", b"a\0", b"\0a", bytes(300)}  # empty, prefixes, zero bytes, a long one
+    while len(words) < k:
+        words.add(rng.integers(0, 256, rng.integers(1, 40), dtype=np.uint8).tobytes())
+    return sorted(words)
+
+
+def test_intern_matches_host_first_occurrence():
+    rng = np.random.default_rng(21)
+    vocab = vocabulary(rng, 600)
+    t, host = Interner(max_ids=4096, arena_bytes=1 << 20), HostInterner()
+    for batch in range(4):
+        k = 20000
+        pick = rng.integers(0, len(vocab) if batch else 200, k)  # later batches: old and new strings mixed
+        strings = [None if rng.random() < 0.02 else vocab[i] for i in pick]
+        got = t.intern(strings)
+        exp = np.array([host(s) for s in strings], np.uint32)
+        np.testing.assert_array_equal(got, exp, err_msg=f"batch {batch}")
+        assert t.count()[0] == len(host.ids)
+    assert t.count()[1] == sum(len(s) for s in host.ids)
+    t.close()
+
+
+def test_intern_overflow_commits_nothing():
+    t = Interner(max_ids=10, arena_bytes=1 << 12)
+    assert list(t.intern([b"x", b"y", b"x"])) == [0, 1, 0]
+    with pytest.raises(EngineError):
+        t.intern([bytes([i]) * 3 for i in range(20)])
+    assert t.count() == (2, 2)
+    assert list(t.intern([b"y", b"z", None])) == [1, 2, NO_STRING]
+    t.close()
+
+
+def test_wire_frames_to_apply_batch_end_to_end():
+    rng = np.random.default_rng(22)
+    n_members, s = 200, 8
+    names = [b"deploy", b"restart", b"", b"cfg-reload", b"x" * 70]
+    payloads = [b"", b"v1", b"v2", bytes(range(40)), b"\xff\x00\xff"]
+    blob = b"".join(names + payloads)
+    noff = np.cumsum([0] + [len(x) for x in names])
+    poff = len(b"".join(names)) + np.cumsum([0] + [len(x) for x in payloads])
+    k = 6000
+    m = np.zeros(k, K.WIRE_MSG_DTYPE)
+    m["type"] = rng.choice([G.MSG_USER_EVENT] * 4 + [G.MSG_JOIN], k)
+    m["flag"] = rng.integers(0, 2, k)
+    m["ltime"] = rng.integers(0, 40, k)
+    ni, pi = rng.integers(0, len(names), k), rng.integers(0, len(payloads), k)
+    m["a_off"], m["a_len"] = noff[ni], [len(names[i]) for i in ni]
+    m["b_off"] = np.where(m["type"] == G.MSG_USER_EVENT, poff[pi], 0)
+    m["b_len"] = np.where(m["type"] == G.MSG_USER_EVENT, [len(payloads[i]) for i in pi], 0)
+    buf, off = CO.wire_encode(m, np.frombuffer(blob, np.uint8))
+    dec = K.decode_messages(buf, off)
+    assert np.all(dec["status"] == 0)
+    tn, tp = Interner(max_ids=64, arena_bytes=1 << 12), Interner(max_ids=64, arena_bytes=1 << 12)
+    keys = wire_event_keys(tn, tp, buf, dec)
+    hn, hp = HostInterner(), HostInterner()
+    ev = dec["type"] == G.MSG_USER_EVENT
+    exp = np.zeros(k, np.uint64)
+    for i in np.flatnonzero(ev):
+        a, b = int(dec["a_off"][i]), int(dec["b_off"][i])
+        nm = buf[a:a + int(dec["a_len"][i])].tobytes()
+        pl = buf[b:b + int(dec["b_len"][i])].tobytes()
+        exp[i] = (hn(nm) << 32) | hp(pl)
+    np.testing.assert_array_equal(keys, exp)
+    # notify_message of the decoded user events, keyed on the device, against the oracle
+    cfg = G.GossipConfig(n_members=n_members, n_subjects=s, queue_cap=8, max_rumors=1024, event_buffer_size=16,
+                         query_buffer_size=16, slot_k=4)
+    subj = W.subjects_for(n_members, s)
+    views = (np.zeros(s, np.uint8), np.zeros(s, np.uint8), np.zeros(s, np.uint64))
+    g = G.GossipEngine(cfg)
+    g.set_subjects(subj)
+    g.init_views(*views)
+    w = H.oracle_world(cfg, subj, views)
+    L = O.lib()
+    idx = np.flatnonzero(ev)
+    msgs = np.zeros(len(idx), G.MSG_DTYPE)
+    msgs["receiver"] = rng.integers(0, n_members // 10, len(idx))  # many events per receiver: dedup hits
+    msgs["type"] = G.MSG_USER_EVENT
+    msgs["ltime"] = dec["ltime"][idx]
+    msgs["key"] = keys[idx]
+    msgs["flags"] = dec["flag"][idx]
+    flags, _ = g.apply_batch(msgs)
+    dups = 0
+    for j, i in enumerate(idx):
+        f = L.orc_handle_user_event(C.byref(w), int(msgs["receiver"][j]), int(msgs["ltime"][j]), int(exp[i]))
+        assert flags[j] == f, j
+        dups += not (f & O.F_REBROADCAST)
+    assert dups > len(idx) // 4  # the identity comparison was exercised
+    H.assert_same(H.engine_state(g), H.world_state(w), "wire user events")
+    g.close()
+    L.orc_world_free(C.byref(w))
+    tn.close()
+    tp.close()
