@@ -525,6 +525,9 @@ int rsf_gossip_dump_members(rsf_gossip* g, uint64_t* clock, uint64_t* event_cloc
                             uint64_t* digest, uint32_t* err, uint8_t* serf_state);
 /* time (optional): the leave time of a Failed/Left entry or the wall time of a buffered intent */
 int rsf_gossip_dump_view(rsf_gossip* g, uint64_t* ltime, uint8_t* status, uint8_t* kind, uint32_t* time);
+/* the same for local rows [row0, row0 + rows) only (rows x n_subjects entries) */
+int rsf_gossip_dump_view_rows(rsf_gossip* g, uint64_t row0, uint64_t rows, uint64_t* ltime, uint8_t* status,
+                              uint8_t* kind, uint32_t* time);
 int rsf_gossip_dump_queues(rsf_gossip* g, uint32_t* rumor, uint32_t* seq, uint16_t* transmits, uint16_t* len,
                            uint32_t* next_seq);
 int rsf_gossip_dump_buffers(rsf_gossip* g, uint64_t* eb_ltime, uint32_t* eb_cnt, uint64_t* eb_keys,

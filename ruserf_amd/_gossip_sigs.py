@@ -43,6 +43,7 @@ def declare(L):
     sig("rsf_gossip_check_runs", [VP, C.POINTER(C.c_int)])
     sig("rsf_gossip_dump_members", [VP, P64, P64, P64, P64, P32, P8])
     sig("rsf_gossip_dump_view", [VP, P64, P8, P8, P32])
+    sig("rsf_gossip_dump_view_rows", [VP, C.c_uint64, C.c_uint64, P64, P8, P8, P32])
     sig("rsf_gossip_reap", [VP, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32])
     sig("rsf_gossip_set_now", [VP, C.c_uint32])
     sig("rsf_gossip_dump_queues", [VP, P32, P32, P16, P16, P32])

@@ -37,6 +37,25 @@ constexpr uint32_t kSentinel = 0xFFFFFFFFu;
 // record decoration (what merge_kernel needs to address the view entry before the rumor
 // body arrives): the subject slot of an intent, or the queue of a query / user event
 constexpr uint32_t kDecQuery = 0xFFFFFFFEu, kDecEvent = 0xFFFFFFFDu, kDecViewMax = 0xFFFFFFF0u;
+// Range guards on the round kernels' data-dependent indices (group slot, record slot,
+// subject, pending-list index): a violation is recorded (g_merge_prof[0] bit k, the value in
+// [1 + k % 7], readable through rsf_gossip_merge_prof) and the access skipped.  They never
+// fire on valid input.  They stay on: at 1M members x 4096 subjects the build without them
+// faulted inside merge_kernel in the first round while every guarded index was in range
+// (experiments/cfg1_checks.py), i.e. the fault followed the code generated
+// without them, not the data.
+#ifndef RSF_CHECKS
+#define RSF_CHECKS 1
+#endif
+#if RSF_MERGE_PROF || RSF_EMIT_PROF || RSF_CHECKS
+__device__ unsigned long long g_merge_prof[8];
+#endif
+#if RSF_CHECKS
+#define RSF_BAD(k, cond, val) \
+  ((cond) ? (atomicOr(&g_merge_prof[0], 1ull << (k)), g_merge_prof[1 + ((k) % 7)] = (unsigned long long)(val), true) : false)
+#else
+#define RSF_BAD(k, cond, val) false
+#endif
 
 // Wave-wide u64 min/max through DPP (row_ror inside 16-lane rows, then
 // row_bcast15 / row_bcast31 across rows, result in lane 63): VALU-only data
@@ -752,6 +771,7 @@ __global__ void __launch_bounds__(256) grp_index_kernel(const uint32_t* __restri
   if (i >= n) return;
   const uint32_t key = key_s[i];
   if (key == kSentinel) return;
+  if (RSF_BAD(2, id_s[i] >= n, id_s[i]) || RSF_BAD(3, seg_start && key - lo >= n, key)) return;
   slot[id_s[i]] = (uint32_t)i;
   if (seg_start) {
     if (i == 0 || key_s[i - 1] != key) seg_start[key - lo] = (uint32_t)i;
@@ -799,9 +819,6 @@ struct Buckets {
 #endif
 #ifndef RSF_EMIT_PROF
 #define RSF_EMIT_PROF 0  // diagnostic build: per-phase shader-clock totals of emit_kernel (same counters)
-#endif
-#if RSF_MERGE_PROF || RSF_EMIT_PROF
-__device__ unsigned long long g_merge_prof[8];
 #endif
 #if RSF_MERGE_PROF
 #define MPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
@@ -1225,6 +1242,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     } else {
       // slot contents and the group's record count in one round trip (holes read stale ids)
       const uint64_t slot = vs + vi;
+      if (RSF_BAD(6, in && slot >= (uint64_t)c.n_loc * c.fanout * c.cap_t, slot)) return;
       rid0 = in ? rec_ld(vals + slot) : 0;
       if (gcnt && in) {
         // group of the slot relative to the receiver's first group: a 32-bit division
@@ -1240,7 +1258,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     const bool valid = in && (!(RUNS || gcnt) || gk < gc);
     const uint32_t rid = valid ? rid0 : 0;
     const uint32_t dsub = valid ? dsub0 : kEmpty;
-    const bool is_view = dsub < kDecViewMax;
+    const bool is_view = dsub < kDecViewMax && !RSF_BAD(4, dsub < kDecViewMax && dsub >= c.S, dsub);
     rsf_rumor ru{};
     if (valid) {  // the key only for user events / queries (the decoration says which)
       const uint4 b = s.rbody[rid & c.rmask];
@@ -1347,6 +1365,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
       const uint32_t k = (uint32_t)__popcll(newmask);
       if (ins) {
         const uint32_t i = pn + (uint32_t)__popcll(newmask & below_mask(lane));
+        if (RSF_BAD(5, i >= kPend, i)) return;
         p_ent[i] = GState::PendE{rid, dsub, ru.msg_len};  // queue 0
       }
       pn += k;
@@ -1990,6 +2009,19 @@ __global__ void accumulate_kernel(unsigned long long* counters, uint32_t from) {
 }
 
 inline unsigned grid1(uint64_t n, unsigned b = 256) { return (unsigned)((n + b - 1) / b); }
+#ifndef RSF_SYNC_DEBUG
+#define RSF_SYNC_DEBUG 0  // diagnostic build: synchronise after every launch of the round and name a failing one
+#endif
+#define RSF_DBG_SYNC(st, name)                                                                 \
+  do {                                                                                         \
+    if (RSF_SYNC_DEBUG) {                                                                      \
+      const hipError_t e_ = hipStreamSynchronize(st);                                          \
+      if (e_ != hipSuccess) {                                                                  \
+        fprintf(stderr, "RSF_SYNC_DEBUG: after %s: %s\n", name, hipGetErrorString(e_));        \
+        return rsf::set_hip_error(e_, name, __FILE__, __LINE__);                              \
+      }                                                                                        \
+    }                                                                                          \
+  } while (0)
 inline int bits_for(uint64_t n) {
   int b = 1;
   while (b < 32 && ((1ull << b) <= n)) ++b;
@@ -2484,10 +2516,12 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
     hipLaunchKernelGGL(ml_alive_kernel, dim3(1), dim3(64), 0, st, g->s, g->d_ml, n_ml);
   }
   hipLaunchKernelGGL(refute_kernel, dim3(grid1(c.S)), dim3(256), 0, st, c, g->s, g->round_base);
+  RSF_DBG_SYNC(st, "refute_kernel");
   if (n_acts) {
     RSF_HIP(hipMemcpyAsync(g->d_acts, acts, n_acts * sizeof(rsf_action), hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(originate_kernel, dim3(grid1(n_acts)), dim3(256), 0, st, c, g->s, g->d_acts, n_acts,
                        g->round_abase);
+    RSF_DBG_SYNC(st, "originate_kernel");
   }
   RSF_HIP(hipGetLastError());
   mark(g, 1);
@@ -2519,10 +2553,13 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
   if (g->round_need)
     hipLaunchKernelGGL(dec_fill_kernel, dim3(grid1(g->round_need)), dim3(256), 0, st, (const rsf_rumor*)g->s.rumors,
                        g->s.rdec, g->s.rbody, (uint64_t)(g->round_base & c.rmask), (uint64_t)g->round_need);
+  RSF_DBG_SYNC(st, "dec_fill_kernel");
   hipLaunchKernelGGL(peers_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, c, g->s, round, g->grp_key);
   RSF_HIP(hipGetLastError());
+  RSF_DBG_SYNC(st, "peers_kernel");
   int rc = sort_pairs(g, g->grp_key, g->grp_key_s, g->grp_id, g->grp_id_s, ng);
   if (rc) return rc;
+  RSF_DBG_SYNC(st, "group sort");
   RSF_HIP(hipMemsetAsync(g->grp_cnt, 0, ng * 4, st));
   if (local) {
     RSF_HIP(hipMemsetAsync(g->seg_start, 0, c.n_loc * 4, st));
@@ -2531,6 +2568,7 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
   hipLaunchKernelGGL(grp_index_kernel, dim3(grid1(ng)), dim3(256), 0, st, g->grp_key_s, g->grp_id_s, ng, c.lo,
                      g->grp_slot, local ? g->seg_start : nullptr, local ? g->seg_end : nullptr);
   RSF_HIP(hipGetLastError());
+  RSF_DBG_SYNC(st, "grp_index_kernel");
   const dim3 egrid(grid1((c.n_loc + RSF_EMIT_PER_WAVE - 1) / RSF_EMIT_PER_WAVE, RSF_EMIT_WPB));
   if (world) {
     const Buckets bk = send_buckets(g);
@@ -2549,6 +2587,7 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
   hipLaunchKernelGGL(emit_kernel<false>, egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key, g->grp_slot,
                      g->grp_cnt, g->stage_val, g->stage_dec, Buckets{});
   RSF_HIP(hipGetLastError());
+  RSF_DBG_SYNC(st, "emit_kernel");
   size_t tb = g->grp_scan_bytes;
   if (local) {
     RSF_HIP(hipcub::DeviceReduce::Sum(g->grp_scan_tmp, tb, g->grp_cnt, (unsigned long long*)g->d_counters, (int)ng,
@@ -2577,9 +2616,11 @@ static int merge_launch(rsf_gossip* g, const uint32_t* vals, const uint32_t* dec
   const unsigned blocks = grid1((c.n_loc + RSF_MERGE_PER_WAVE - 1) / RSF_MERGE_PER_WAVE, kWavesPerBlock);
   hipLaunchKernelGGL(merge_kernel<RUNS>, dim3(blocks), dim3(kWave * kWavesPerBlock), 0, g->stream, c, g->s, vals, dec,
                      start, end, gcnt, stride, bk, big);
+  RSF_DBG_SYNC(g->stream, "merge_kernel");
   hipLaunchKernelGGL(merge_big_kernel<RUNS>, dim3(std::min(g->merge_blocks, blocks)), dim3(kWave * kWavesPerBlock), 0,
                      g->stream, c, g->s, vals, dec, start, end, gcnt, stride, bk, big);
   RSF_HIP(hipGetLastError());
+  RSF_DBG_SYNC(g->stream, "merge_big_kernel");
   return RSF_OK;
 }
 
@@ -2753,7 +2794,7 @@ int rsf_gossip_send_buffer(rsf_gossip* g, void** p, uint64_t* cap) {
 // diagnostic only (experiments/merge_prof.py, builds with -DRSF_MERGE_PROF=1): reads and
 // clears merge_kernel's per-phase shader-clock totals; returns -1 in normal builds
 int rsf_gossip_merge_prof(uint64_t* out8) {
-#if RSF_MERGE_PROF || RSF_EMIT_PROF
+#if RSF_MERGE_PROF || RSF_EMIT_PROF || RSF_CHECKS
   RSF_HIP(hipDeviceSynchronize());
   RSF_HIP(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_merge_prof), 8 * sizeof(uint64_t)));
   unsigned long long z[8] = {};
@@ -3055,12 +3096,14 @@ int rsf_gossip_dump_members(rsf_gossip* g, uint64_t* clock, uint64_t* ec, uint64
   return RSF_OK;
 }
 
-int rsf_gossip_dump_view(rsf_gossip* g, uint64_t* ltime, uint8_t* status, uint8_t* kind, uint32_t* time) {
+int rsf_gossip_dump_view_rows(rsf_gossip* g, uint64_t row0, uint64_t rows, uint64_t* ltime, uint8_t* status,
+                              uint8_t* kind, uint32_t* time) {
   if (!g || !ltime || !status || !kind) return gerr("null argument");
-  const uint64_t cnt = g->c.n_loc * g->c.S;
+  if (row0 > g->c.n_loc || rows > g->c.n_loc - row0) return gerr("rows outside the shard");
+  const uint64_t cnt = rows * g->c.S;
   std::vector<ViewE> v(cnt);
   RSF_HIP(hipSetDevice(g->device));
-  RSF_HIP(hipMemcpyAsync(v.data(), g->s.view, cnt * sizeof(ViewE), hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipMemcpyAsync(v.data(), g->s.view + row0 * g->c.S, cnt * sizeof(ViewE), hipMemcpyDeviceToHost, g->stream));
   RSF_HIP(hipStreamSynchronize(g->stream));
   for (uint64_t i = 0; i < cnt; ++i) {
     ltime[i] = v[i].ltime;
@@ -3069,6 +3112,11 @@ int rsf_gossip_dump_view(rsf_gossip* g, uint64_t* ltime, uint8_t* status, uint8_
     if (time) time[i] = v[i].t;
   }
   return RSF_OK;
+}
+
+int rsf_gossip_dump_view(rsf_gossip* g, uint64_t* ltime, uint8_t* status, uint8_t* kind, uint32_t* time) {
+  if (!g) return gerr("null argument");
+  return rsf_gossip_dump_view_rows(g, 0, g->c.n_loc, ltime, status, kind, time);
 }
 
 int rsf_gossip_dump_queues(rsf_gossip* g, uint32_t* rumor, uint32_t* seq, uint16_t* tx, uint16_t* len,

@@ -234,14 +234,16 @@ class GossipEngine:
         out["serf_state"] = ss
         return out
 
-    def view(self, with_time=False):
-        n = self.n_loc * self.cfg.n_subjects
+    def view(self, with_time=False, rows=None):
+        """the view (local rows x subjects, flattened); rows=(row0, count) for a slice"""
+        row0, cnt = rows if rows is not None else (0, self.n_loc)
+        n = cnt * self.cfg.n_subjects
         lt = np.zeros(n, dtype=np.uint64)
         st = np.zeros(n, dtype=np.uint8)
         kd = np.zeros(n, dtype=np.uint8)
         tm = np.zeros(n, dtype=np.uint32)
-        check(lib().rsf_gossip_dump_view(self._h, ptr(lt, C.c_uint64), ptr(st, C.c_uint8), ptr(kd, C.c_uint8),
-                                          ptr(tm, C.c_uint32)))
+        check(lib().rsf_gossip_dump_view_rows(self._h, row0, cnt, ptr(lt, C.c_uint64), ptr(st, C.c_uint8),
+                                               ptr(kd, C.c_uint8), ptr(tm, C.c_uint32)))
         return (lt, st, kd, tm) if with_time else (lt, st, kd)
 
     # ---- Reaper tick (base.rs:519-601): times in rounds

@@ -245,6 +245,52 @@ def test_large_round_properties():
     assert np.array_equal(digests[0][0], digests[1][0]) and digests[0][1] == digests[1][1]
 
 
+def test_configs1_full_shape_properties():
+    """BASELINE configs[1] as specified: 1M members, 4096 tracked subjects, 32 rounds of
+    the 1% intent workload (prune mix included).  The view (64 GB) is too large for the
+    oracle, so size-independent properties: clocks never decrease; on sampled rows every
+    accepted status_time was witnessed (clock > ltime); transmits stay under the limit;
+    no capacity error but the counted queue prunes; the same seed gives the same
+    digests and sampled views."""
+    n, s, rounds = 1_000_000, 4096, 32
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, max_rumors=1 << 20, event_buffer_size=8, query_buffer_size=8,
+                         slot_k=1)
+    subj, acts, ml = W.intents_workload(n, s, rounds, rate=0.01, seed=3, prune_frac=0.1)
+    sample = [(0, 64), (n // 2 - 32, 64), (n - 64, 64)]
+    runs = []
+    for rep in range(2):
+        g = G.GossipEngine(cfg)
+        g.set_subjects(subj)
+        g.init_views(*W.initial_views(s))
+        prev = None
+        for t in range(rounds):
+            g.round(t, ml[t], acts[t])
+            if t % 8 == 7 or t == rounds - 1:
+                m = g.members()
+                if prev is not None:
+                    assert np.all(m["clock"] >= prev), t
+                prev = m["clock"]
+        assert np.all((m["err"] & ~np.uint32(G.E_QUEUE_PRUNE)) == 0)
+        views = []
+        for r0, cnt in sample:
+            lt, st, kd = g.view(rows=(r0, cnt))
+            lt, known = lt.reshape(cnt, s), kd.reshape(cnt, s) == G.KIND_KNOWN
+            accepted = np.where(known & (lt > 1), lt, 0).max(axis=1)
+            assert np.all(accepted < m["clock"][r0:r0 + cnt])
+            views.append((lt.copy(), st.copy(), kd.copy()))
+        r, sq, tx, ln, ns = g.queues()
+        limit = O.lib().orc_retransmit_limit(4, n)
+        assert np.all(tx[r != 0xFFFFFFFF] < limit)
+        sent, merged = g.last_round_stats()
+        assert sent > 0 and merged == sent
+        runs.append((m["digest"].copy(), m["clock"].copy(), views))
+        g.close()
+    assert np.array_equal(runs[0][0], runs[1][0]) and np.array_equal(runs[0][1], runs[1][1])
+    for a, b in zip(runs[0][2], runs[1][2]):
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+
+
 @pytest.mark.parametrize("runs", [False, True, "with_empty_runs", "buckets"])
 def test_two_shards_equal_one_context(runs):
     """The multi-GPU split (round_begin / rumor-block sum / round_emit /
