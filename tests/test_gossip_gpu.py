@@ -49,6 +49,28 @@ def test_intent_rounds_bit_exact(n, s, rounds, rate, qcap, limit):
     L.orc_world_free(C.byref(w))
 
 
+def test_bench_shape_bit_exact():
+    """The bench's configuration (4096 subjects, queue_cap 64, 8 intents of budget per
+    target, slot_k 1, 512-slot dedup rings) at 20k members with 5% originating per round:
+    the queues saturate as in the bench (every member receives far more new intents than
+    it can send), so bounded-queue prunes, full pending lists and merge_big_kernel are all
+    on the path; bit-exact against the oracle after every round."""
+    n, s, rounds = 20000, 4096, 12
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=64, gossip_limit=8 * 24, gossip_overhead=2,
+                         max_rumors=1 << 18, event_buffer_size=512, query_buffer_size=512, slot_k=1)
+    subj, acts, ml = W.intents_workload(n, s, rounds, rate=0.05, seed=2024)
+    views = W.initial_views(s)
+    g, w = pair(cfg, subj, views)
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t])
+        H.assert_same(H.engine_state(g), H.world_state(w), f"round {t}")
+    st = H.engine_state(g)
+    assert int(st["q_pruned"].sum()) > 0  # saturated: the bounded queues dropped items
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
 def test_rumor_ring_recycles_bit_exact():
     """A rumor ring far smaller than the run: blocks restart the ring with the next
     generation, two generations resident; at each wrap the queued ids of generation
