@@ -388,7 +388,8 @@ int rsf_gossip_check_runs(rsf_gossip* g, int* ok);
  * world size) and returns the send and receive buffers, `world` buckets of bucket_bytes
  * each, device memory.  round_emit_buckets emits straight into the send buckets (each
  * holds its shard's (sender, peer) groups sorted by receiver: a header with the group
- * count, the receivers, record counts, rumor ids and record decorations).  The caller
+ * count, the receivers, record counts and rumor ids; the record decorations are rebuilt
+ * on the receive side from the replicated rumor table).  The caller
  * moves bucket w of every rank to rank w (one all-to-all of equal splits, e.g.
  * ncclAllToAll), concatenated in source-rank order, then round_merge_buckets merges
  * straight from the received buckets: per receiver its groups of every source in
