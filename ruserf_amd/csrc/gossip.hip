@@ -37,13 +37,11 @@ constexpr uint32_t kSentinel = 0xFFFFFFFFu;
 // record decoration (what merge_kernel needs to address the view entry before the rumor
 // body arrives): the subject slot of an intent, or the queue of a query / user event
 constexpr uint32_t kDecQuery = 0xFFFFFFFEu, kDecEvent = 0xFFFFFFFDu, kDecViewMax = 0xFFFFFFF0u;
-// Range guards on the round kernels' data-dependent indices (group slot, record slot,
-// subject, pending-list index): a violation is recorded (g_merge_prof[0] bit k, the value in
-// [1 + k % 7], readable through rsf_gossip_merge_prof) and the access skipped.  They never
-// fire on valid input.  They stay on: at 1M members x 4096 subjects the build without them
-// faulted inside merge_kernel in the first round while every guarded index was in range
-// (experiments/cfg1_checks.py), i.e. the fault followed the code generated
-// without them, not the data.
+// Range guards on the round kernels' data-dependent indices (record slot, subject and
+// pending-list index in the merge, sorted group ids): a violation is recorded
+// (g_merge_prof[0] bit k, the value in [1 + k % 7], readable through rsf_gossip_merge_prof)
+// and the access skipped.  They never fire on valid input; RSF_CHECKS=2 adds guards on every
+// other data-dependent index (diagnostic builds; DESIGN.md §5, open issue at 1M x 4096).
 #ifndef RSF_CHECKS
 #define RSF_CHECKS 1
 #endif
@@ -55,6 +53,12 @@ __device__ unsigned long long g_merge_prof[8];
   ((cond) ? (atomicOr(&g_merge_prof[0], 1ull << (k)), g_merge_prof[1 + ((k) % 7)] = (unsigned long long)(val), true) : false)
 #else
 #define RSF_BAD(k, cond, val) false
+#endif
+// RSF_CHECKS >= 2 (diagnostic builds): further guards on every data-dependent index
+#if RSF_CHECKS >= 2
+#define RSF_BAD2(k, cond, val) RSF_BAD(k, cond, val)
+#else
+#define RSF_BAD2(k, cond, val) false
 #endif
 
 // Wave-wide u64 min/max through DPP (row_ror inside 16-lane rows, then
@@ -618,6 +622,7 @@ __device__ __forceinline__ void put_rumor(const GCfg& c, const GState& s, uint32
 
 __device__ __forceinline__ void push_refute(const GCfg& c, const GState& s, MRegs& r, uint64_t ltime) {
   if (r.subj < 0) return;
+  if (RSF_BAD2(11, (uint32_t)r.subj >= c.S, r.subj)) return;
   uint32_t cnt = s.refute_cnt[r.subj];
   if (cnt < c.max_refute) {
     s.refute_ltime[(uint64_t)r.subj * c.max_refute + cnt] = ltime;
@@ -666,6 +671,7 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
   uint32_t rid = abase + a;
   MRegs r;
   load_regs(s, l, r);
+  if (RSF_BAD2(13, (x.act == RSF_ACT_JOIN_SELF || x.act == RSF_ACT_LEAVE_SELF) && (uint32_t)r.subj >= c.S, r.subj)) return;
   uint64_t ref = 0;
   switch (x.act) {
     case RSF_ACT_JOIN_SELF:
@@ -874,6 +880,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   const uint64_t pm = __ballot(e.gk != kSentinel);  // peers are a prefix of the fanout slots
   const uint32_t np = (uint32_t)__popcll(pm);
   const uint32_t pc = shfl_u32(e.head, kEhPend), npend = pend_total(pc);
+  if (RSF_BAD2(8, npend > kPend || ((pc >> 24) != 0), pc)) return;
   const bool ne0 = shfl_u32(Q0.r, 0) != kEmpty || (pc & 0xFF), ne1 = shfl_u32(e.head, 1) != kEmpty || ((pc >> 8) & 0xFF),
              ne2 = shfl_u32(e.head, 2) != kEmpty || ((pc >> 16) & 0xFF);
   // no peers: nothing is sent, and the pending re-queues wait for the next emission
@@ -922,6 +929,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   EPROF_ADD(1, t1, t2);
   for (uint32_t j = 0; j < np; ++j) {
     const uint32_t gslot = shfl_u32(e.gs, j);
+    if (RSF_BAD2(7, !BKT && gslot >= c.n_loc * c.fanout, gslot)) return;
     uint64_t out_base = (uint64_t)gslot * c.cap_t;
     uint32_t* ov = out_val;
     uint32_t* od = out_dec;
@@ -1180,12 +1188,14 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
   } else {
     st = shfl_u32(su, kSuStart);
     en = shfl_u32(su, kSuEnd);
+    if (RSF_BAD2(10, st > en || en > c.n_loc * c.fanout, ((uint64_t)st << 32) | en)) return;
     total = st < en ? (en - st) * stride : 0u;
   }
   if (total == 0 || (shfl_u32(su, kSuAlive) & 0xFF) == 0) return;
   // pending re-queues: packed per-queue counts and their total (wave-uniform)
   const uint32_t pc0 = shfl_u32(su, kSuPend);
   uint32_t pc = pc0, pn = pend_total(pc0);
+  if (RSF_BAD2(12, pn > kPend || (pc0 >> 24) != 0, pc0)) return;
   if (!BIG && pn + total > kPendMerge) {  // at most one re-queue per record slot: might not fit
     if (lane == 0) big.ids[atomicAdd(big.n, 1ull)] = (uint32_t)l;
     return;
@@ -1249,6 +1259,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
         // (a receiver's slot range is small) instead of a 64-bit one
         const uint32_t gr = vi / stride;
         gk = vi - gr * stride;
+        if (RSF_BAD2(9, (uint64_t)st + gr >= c.n_loc * c.fanout, st + gr)) return;
         gc = rec_ld(gcnt + st + gr);
       }
       // decoration (same round trip as the rumor ids): subject of an intent, or the
@@ -2274,6 +2285,11 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   ms(s.rumors, 0, (size_t)cfg->max_rumors * 2 * sizeof(rsf_rumor));
   ms(s.rdec, 0, (size_t)cfg->max_rumors * 2 * 4);
   ms(s.rbody, 0, (size_t)cfg->max_rumors * 2 * 16);
+  // emission's group slots and the record stage start defined (grp_index_kernel writes the
+  // slot of every group with a receiver each round; a slot it did not write stays in range)
+  ms(g->grp_slot, 0, g->n_groups * 4);
+  ms(g->stage_val, 0, g->stage_cap * 4);
+  ms(g->stage_dec, 0xFF, g->stage_cap * 4);
   if (!ok) return fail(rsf::set_error(RSF_ERR_HIP, "context initialisation failed"));
   // Serf::new increments every clock once (base.rs:195-199)
   hipLaunchKernelGGL(fill_u64_kernel, dim3(grid1(n)), dim3(256), 0, st, s.clock, n, 1ull);

@@ -1,5 +1,8 @@
 #!/bin/bash
+# final tree: GPU suite, smoke, default bench line; then the 1M-member bench line (configs[1])
 S=scripts/gpu_step.sh
-bash $S pytest_viv 600 python -u -m pytest tests/test_dist_vivaldi_gpu.py tests/test_vivaldi_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread && \
-RSF_DIST_BACKEND=gloo bash $S viv_gloo2 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 --workload vivaldi --members 4000000 --members-total --steps 3 --warmup 1 --no-cpu-baseline && \
-bash $S viv1 300 python3 bench.py --workload vivaldi --steps 10 --warmup 2 --no-cpu-baseline
+bash $S pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread && \
+bash $S smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" && \
+bash $S bench_default 500 python -u bench.py && \
+bash $S bench_1m 300 python -u bench.py --workload gossip --members 1000000 --steps 32 --warmup 3 --no-cpu-baseline --no-vivaldi
+grep -h '^{' gpurun_out/bench_default.log gpurun_out/bench_1m.log | cut -c1-250; tail -2 gpurun_out/pytest_gpu.log; tail -2 gpurun_out/bench_1m.log | cut -c1-300
