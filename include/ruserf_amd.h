@@ -400,6 +400,9 @@ int rsf_gossip_bucket_buffers(rsf_gossip* g, uint32_t world, void** send, void**
 int rsf_gossip_round_emit_buckets(rsf_gossip* g, uint32_t world);
 int rsf_gossip_round_merge_buckets(rsf_gossip* g, uint32_t world);
 int rsf_gossip_bucket_status(rsf_gossip* g, int* ok);
+/* diagnostic: device addresses of the context's main buffers (order in gossip.hip); returns
+ * the count written */
+int rsf_gossip_debug_ptrs(rsf_gossip* g, uint64_t* out, uint32_t n);
 
 /* ---- push/pull anti-entropy (SerfDelegate::local_state / merge_remote_state,
  * core/src/serf/delegate.rs:376-554) ---------------------------------------

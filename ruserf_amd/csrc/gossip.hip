@@ -2807,6 +2807,23 @@ int rsf_gossip_send_buffer(rsf_gossip* g, void** p, uint64_t* cap) {
   return RSF_OK;
 }
 
+// diagnostic only: device addresses of the context's main buffers and of a global in the
+// library's code object (open issue: an address-dependent fault).  Order:
+// view, p_ent, q_rumor, stage_val, stage_dec, grp_slot, grp_cnt, seg_start, rbody, rumors,
+// rdec, clock, code-object global (0 without one).  Returns the count written.
+int rsf_gossip_debug_ptrs(rsf_gossip* g, uint64_t* out, uint32_t n) {
+  if (!g || !out) return gerr("null argument");
+  const void* p[13] = {g->s.view, g->s.p_ent, g->s.q_rumor, g->stage_val, g->stage_dec, g->grp_slot, g->grp_cnt,
+                       g->seg_start, g->s.rbody, g->s.rumors, g->s.rdec, g->s.clock, nullptr};
+#if RSF_MERGE_PROF || RSF_EMIT_PROF || RSF_CHECKS
+  void* sym = nullptr;
+  if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_merge_prof)) == hipSuccess) p[12] = sym;
+#endif
+  const uint32_t k = n < 13 ? n : 13;
+  for (uint32_t i = 0; i < k; ++i) out[i] = (uint64_t)(uintptr_t)p[i];
+  return (int)k;
+}
+
 // diagnostic only (experiments/merge_prof.py, builds with -DRSF_MERGE_PROF=1): reads and
 // clears merge_kernel's per-phase shader-clock totals; returns -1 in normal builds
 int rsf_gossip_merge_prof(uint64_t* out8) {
