@@ -2134,8 +2134,22 @@ static int ensure_lists(rsf_gossip* g, uint32_t n_ml, uint32_t n_acts) {
   return RSF_OK;
 }
 
+// hipcub does not check the temporary-storage size it is given, and the requirement need not
+// grow monotonically with the item count (the algorithm depends on the size): every sort
+// queries its own requirement and the buffer grows to it.
 static int sort_pairs(rsf_gossip* g, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout,
                       uint64_t n) {
+  size_t need = 0;
+  RSF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, need, kin, kout, vin, vout, (int)n, 0, g->end_bit, g->stream));
+  if (need > g->sort_tmp_bytes) {
+    RSF_HIP(hipStreamSynchronize(g->stream));  // the old buffer may be in use by earlier work
+    hipFree(g->sort_tmp);
+    g->sort_tmp = nullptr;
+    g->sort_tmp_bytes = 0;
+    int rc = rsf::dmalloc(&g->sort_tmp, need);
+    if (rc) return rc;
+    g->sort_tmp_bytes = need;
+  }
   size_t tmp = g->sort_tmp_bytes;
   RSF_HIP(hipcub::DeviceRadixSort::SortPairs(g->sort_tmp, tmp, kin, kout, vin, vout, (int)n, 0, g->end_bit,
                                              g->stream));
@@ -2247,10 +2261,14 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
     g->merge_blocks = (unsigned)std::max(1, per_cu * cus);
     if ((rc = dmalloc(&g->grp_scan_tmp, tb))) return fail(rc);
   }
-  size_t tmp = 0;
+  // sized for both sorts a round runs (the groups; the record stream of the counts path)
+  size_t tmp = 0, tmp_g = 0;
   if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, g->stage_key, g->sort_key, g->stage_val, g->sort_val,
-                                         (int)pipe, 0, g->end_bit, g->stream) != hipSuccess)
+                                         (int)pipe, 0, g->end_bit, g->stream) != hipSuccess ||
+      hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_g, g->grp_key, g->grp_key_s, g->grp_id, g->grp_id_s,
+                                         (int)g->n_groups, 0, g->end_bit, g->stream) != hipSuccess)
     return fail(rsf::set_error(RSF_ERR_HIP, "hipcub sort sizing failed"));
+  tmp = std::max(tmp, tmp_g);
   g->sort_tmp_bytes = tmp;
   if ((rc = dmalloc(&g->sort_tmp, tmp))) return fail(rc);
   hipStream_t st = g->stream;
@@ -2810,16 +2828,21 @@ int rsf_gossip_send_buffer(rsf_gossip* g, void** p, uint64_t* cap) {
 // diagnostic only: device addresses of the context's main buffers and of a global in the
 // library's code object (open issue: an address-dependent fault).  Order:
 // view, p_ent, q_rumor, stage_val, stage_dec, grp_slot, grp_cnt, seg_start, rbody, rumors,
-// rdec, clock, code-object global (0 without one).  Returns the count written.
+// rdec, clock, code-object global (0 without one), big_ids, sort_tmp, grp_scan_tmp, d_counters,
+// d_acts, grp_key, grp_key_s, grp_id, grp_id_s, grp_off, stage_key, sort_key, sort_val,
+// send_buf, rec_dec, seg_end, p_cnt, err, member_subj.  Returns the count written.
 int rsf_gossip_debug_ptrs(rsf_gossip* g, uint64_t* out, uint32_t n) {
   if (!g || !out) return gerr("null argument");
-  const void* p[13] = {g->s.view, g->s.p_ent, g->s.q_rumor, g->stage_val, g->stage_dec, g->grp_slot, g->grp_cnt,
-                       g->seg_start, g->s.rbody, g->s.rumors, g->s.rdec, g->s.clock, nullptr};
+  const void* p[32] = {g->s.view, g->s.p_ent, g->s.q_rumor, g->stage_val, g->stage_dec, g->grp_slot, g->grp_cnt,
+                       g->seg_start, g->s.rbody, g->s.rumors, g->s.rdec, g->s.clock, nullptr,
+                       g->big_ids, g->sort_tmp, g->grp_scan_tmp, g->d_counters, g->d_acts, g->grp_key, g->grp_key_s,
+                       g->grp_id, g->grp_id_s, g->grp_off, g->stage_key, g->sort_key, g->sort_val, g->send_buf,
+                       g->rec_dec, g->seg_end, g->s.p_cnt, g->s.err, g->s.member_subj};
 #if RSF_MERGE_PROF || RSF_EMIT_PROF || RSF_CHECKS
   void* sym = nullptr;
   if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_merge_prof)) == hipSuccess) p[12] = sym;
 #endif
-  const uint32_t k = n < 13 ? n : 13;
+  const uint32_t k = n < 32 ? n : 32;
   for (uint32_t i = 0; i < k; ++i) out[i] = (uint64_t)(uintptr_t)p[i];
   return (int)k;
 }
