@@ -403,6 +403,9 @@ int rsf_gossip_bucket_status(rsf_gossip* g, int* ok);
 /* diagnostic: device addresses of the context's main buffers (order in gossip.hip); returns
  * the count written */
 int rsf_gossip_debug_ptrs(rsf_gossip* g, uint64_t* out, uint32_t n);
+/* diagnostic (builds with RSF_GUARD_ZONES): bytes changed in the guard zones before / after
+ * stage_dec, before / after big_ids and after the sort's storage; -1 without zones */
+int rsf_gossip_debug_zones(rsf_gossip* g, uint64_t* out5);
 
 /* ---- push/pull anti-entropy (SerfDelegate::local_state / merge_remote_state,
  * core/src/serf/delegate.rs:376-554) ---------------------------------------

@@ -2071,6 +2071,9 @@ struct rsf_gossip {
   size_t grp_scan_bytes = 0;
   unsigned merge_blocks = 1;  // merge_big_kernel's grid: merge_kernel's resident blocks per CU x CUs
   uint32_t* big_ids = nullptr;  // receivers deferred to merge_big_kernel (count: d_counters[52])
+  // RSF_GUARD_ZONES (diagnostic builds): 0xA5-filled zones before and after big_ids and
+  // stage_dec and after the sort's storage; rsf_gossip_debug_zones counts changed bytes
+  char *big_base = nullptr, *dec_base = nullptr;
   uint64_t* send_buf = nullptr;
   unsigned long long* d_counters = nullptr;  // [0] n_valid, [1..] shard bounds
   void* sort_tmp = nullptr;
@@ -2137,6 +2140,10 @@ static int ensure_lists(rsf_gossip* g, uint32_t n_ml, uint32_t n_acts) {
 // hipcub does not check the temporary-storage size it is given, and the requirement need not
 // grow monotonically with the item count (the algorithm depends on the size): every sort
 // queries its own requirement and the buffer grows to it.
+#ifndef RSF_GUARD_ZONES
+#define RSF_GUARD_ZONES 0
+#endif
+constexpr size_t kZone = RSF_GUARD_ZONES ? (2u << 20) : 0;
 static int sort_pairs(rsf_gossip* g, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout,
                       uint64_t n) {
   size_t need = 0;
@@ -2146,9 +2153,10 @@ static int sort_pairs(rsf_gossip* g, const uint32_t* kin, uint32_t* kout, const 
     hipFree(g->sort_tmp);
     g->sort_tmp = nullptr;
     g->sort_tmp_bytes = 0;
-    int rc = rsf::dmalloc(&g->sort_tmp, need);
+    int rc = rsf::dmalloc(&g->sort_tmp, need + kZone);
     if (rc) return rc;
     g->sort_tmp_bytes = need;
+    if (kZone) RSF_HIP(hipMemset((char*)g->sort_tmp + need, 0xA5, kZone));
   }
   size_t tmp = g->sort_tmp_bytes;
   RSF_HIP(hipcub::DeviceRadixSort::SortPairs(g->sort_tmp, tmp, kin, kout, vin, vout, (int)n, 0, g->end_bit,
@@ -2243,8 +2251,17 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   g->n_groups = n * c.fanout;
   if (GA(g->grp_key, g->n_groups * 4) || GA(g->grp_cnt, g->n_groups * 4) || GA(g->grp_key_s, g->n_groups * 4) ||
       GA(g->grp_id, g->n_groups * 4) || GA(g->grp_id_s, g->n_groups * 4) || GA(g->grp_slot, g->n_groups * 4) ||
-      GA(g->grp_off, g->n_groups * 4) || GA(g->stage_dec, g->stage_cap * 4) || GA(g->big_ids, n * 4))
+      GA(g->grp_off, g->n_groups * 4) || GA(g->dec_base, g->stage_cap * 4 + 2 * kZone) ||
+      GA(g->big_base, n * 4 + 2 * kZone))
     return fail(rc);
+  g->stage_dec = (uint32_t*)(g->dec_base + kZone);
+  g->big_ids = (uint32_t*)(g->big_base + kZone);
+  if (kZone) {
+    bool zok = true;
+    for (char* z : {g->dec_base, g->dec_base + kZone + g->stage_cap * 4, g->big_base, g->big_base + kZone + n * 4})
+      zok = zok && hipMemset(z, 0xA5, kZone) == hipSuccess;
+    if (!zok) return fail(rsf::set_error(RSF_ERR_HIP, "guard zone init failed"));
+  }
 #undef GA
   {
     size_t tb = 0, tr = 0;
@@ -2270,7 +2287,9 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
     return fail(rsf::set_error(RSF_ERR_HIP, "hipcub sort sizing failed"));
   tmp = std::max(tmp, tmp_g);
   g->sort_tmp_bytes = tmp;
-  if ((rc = dmalloc(&g->sort_tmp, tmp))) return fail(rc);
+  if ((rc = dmalloc(&g->sort_tmp, tmp + kZone))) return fail(rc);
+  if (kZone && hipMemset((char*)g->sort_tmp + tmp, 0xA5, kZone) != hipSuccess)
+    return fail(rsf::set_error(RSF_ERR_HIP, "guard zone init failed"));
   hipStream_t st = g->stream;
   bool ok = true;
   auto ms = [&](void* p, int v, size_t b) { ok = ok && hipMemsetAsync(p, v, b, st) == hipSuccess; };
@@ -2331,9 +2350,9 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters, g->rec_dec, g->pp_buf,
                   g->sort_tmp, g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
                   g->scan_tmp, g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
-                  g->grp_slot, g->grp_off, g->stage_dec, g->grp_scan_tmp, s.dlog, s.dcnt,
+                  g->grp_slot, g->grp_off, g->dec_base, g->grp_scan_tmp, s.dlog, s.dcnt,
                   g->bkt_send, g->bkt_recv, g->bkt_dec, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn,
-                  s.p_ent, s.p_cnt, g->big_ids};
+                  s.p_ent, s.p_cnt, g->big_base};
   for (void* p : ptrs)
     if (p) hipFree(p);
   g->scratch.release();
@@ -2822,6 +2841,25 @@ int rsf_gossip_send_buffer(rsf_gossip* g, void** p, uint64_t* cap) {
   if (!g || !p) return gerr("null argument");
   *p = g->send_buf;
   if (cap) *cap = std::max(g->stage_cap, g->recv_cap);
+  return RSF_OK;
+}
+
+// diagnostic (RSF_GUARD_ZONES builds): changed bytes in the guard zones, in the order before
+// stage_dec, after stage_dec, before big_ids, after big_ids, after the sort's storage
+// (synchronises); -1 without zones
+int rsf_gossip_debug_zones(rsf_gossip* g, uint64_t* out5) {
+  if (!g || !out5) return gerr("null argument");
+  if (!kZone) return -1;
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  const char* z[5] = {g->dec_base, g->dec_base + kZone + g->stage_cap * 4, g->big_base,
+                      g->big_base + kZone + g->c.n_loc * 4, (const char*)g->sort_tmp + g->sort_tmp_bytes};
+  std::vector<uint8_t> v(kZone);
+  for (int k = 0; k < 5; ++k) {
+    RSF_HIP(hipMemcpy(v.data(), z[k], kZone, hipMemcpyDeviceToHost));
+    uint64_t c = 0;
+    for (uint8_t b : v) c += b != 0xA5;
+    out5[k] = c;
+  }
   return RSF_OK;
 }
 
