@@ -2182,13 +2182,6 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   if (cfg->max_rumors == 0 || (cfg->max_rumors & (cfg->max_rumors - 1)) || cfg->max_rumors > (1u << 30))
     return gerr("max_rumors must be a power of two <= 2^30 (the rumor ring)");
   RSF_HIP(hipSetDevice(device));
-  {
-    // load the library's code object before the context's allocations (a kernel attribute
-    // query does): with it loaded after ~70 GB of allocations, the 1M x 4096 shape has
-    // raised an illegal access (open issue); loaded first, it never has
-    hipFuncAttributes fa;
-    RSF_HIP(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&merge_kernel<false>)));
-  }
   rsf_gossip* g = new (std::nothrow) rsf_gossip();
   if (!g) return rsf::set_error(RSF_ERR_NOMEM, "host allocation failed");
   g->device = device;
