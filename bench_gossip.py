@@ -115,6 +115,7 @@ def run_gossip(args, rank, world):
     err_members = int(np.count_nonzero(st["err"] & ~np.uint32(E_QUEUE_PRUNE)))
     qprune_members = int(np.count_nonzero(st["err"] & np.uint32(E_QUEUE_PRUNE)))
     eng.set_profiling(False)
+    canaries_ok = all(eng.cub_canaries())  # no hipCUB call wrote past its temporary storage
     if world > 1:
         dev = "cpu" if torch.distributed.get_backend() == "gloo" else "cuda"
         t_ = torch.tensor([wall, float(merged), float(err_members), float(pruned), float(qprune_members),
@@ -158,6 +159,7 @@ def run_gossip(args, rank, world):
         "records_per_round_per_gpu": records,
         "error_members": err_all,
         "exchange_ok": exchange_ok,
+        "cub_canaries_intact": canaries_ok,
         # the bounded queue model (queue_cap slots) drops live items when full; counted, not silent
         "queue_pruned_per_round": pruned_all / args.steps,
         "queue_pruned_per_merged_record": pruned_all / max(1.0, merged_all),

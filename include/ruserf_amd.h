@@ -404,8 +404,13 @@ int rsf_gossip_bucket_status(rsf_gossip* g, int* ok);
  * the count written */
 int rsf_gossip_debug_ptrs(rsf_gossip* g, uint64_t* out, uint32_t n);
 /* diagnostic (builds with RSF_GUARD_ZONES): bytes changed in the guard zones before / after
- * stage_dec, before / after big_ids and after the sort's storage; -1 without zones */
-int rsf_gossip_debug_zones(rsf_gossip* g, uint64_t* out5);
+ * stage_dec and before / after big_ids; -1 without zones */
+int rsf_gossip_debug_zones(rsf_gossip* g, uint64_t* out4);
+/* diagnostic: every hipCUB temporary is sized per call and followed by a 256-B canary;
+ * out3[k] = 1 if the canary after the radix-sort, group reduce/scan and run-merge scan
+ * storage is intact (or the buffer was never used), 0 if something wrote past the end.
+ * Synchronises the context's stream. */
+int rsf_gossip_debug_canaries(rsf_gossip* g, int* out3);
 
 /* ---- push/pull anti-entropy (SerfDelegate::local_state / merge_remote_state,
  * core/src/serf/delegate.rs:376-554) ---------------------------------------

@@ -2117,6 +2117,15 @@ int orc_world_restart(orc_world* w, uint32_t m, const uint8_t* file, uint64_t le
   return joined;
 }
 
+/* Reconnector throttle (base.rs:670-671):
+ * num_alive = (states.len() - num_failed - left_members.len()).max(1);
+ * prob = num_failed as f32 / num_alive as f32 (usize -> f32 rounds to nearest) */
+float orc_reconnect_prob(uint64_t states, uint64_t failed, uint64_t left) {
+  uint64_t alive = states - failed - left;
+  if (alive < 1) alive = 1;
+  return (float)failed / (float)alive;
+}
+
 uint32_t orc_world_reconnect(orc_world* w, uint32_t tick, uint32_t* target) {
   uint32_t key[2];
   seed_key(w->seed, key);
@@ -2125,7 +2134,11 @@ uint32_t orc_world_reconnect(orc_world* w, uint32_t tick, uint32_t* target) {
     target[m] = EMPTY_RUMOR;
     if (!w->alive[m]) continue;
     const size_t row = (size_t)m * w->s;
-    uint32_t failed = 0, left = 0, known = 1; /* members.states holds the local node too */
+    /* members.states.len(): the n - s untracked members (implicitly Alive; the local node
+     * is one of them unless it is a subject), the local node if it is a subject, and the
+     * tracked subjects it knows */
+    uint64_t known = (uint64_t)(w->n - w->s) + (w->member_subj[m] >= 0 ? 1u : 0u);
+    uint32_t failed = 0, left = 0;
     for (uint32_t subj = 0; subj < w->s; ++subj) {
       if ((int32_t)subj == w->member_subj[m] || w->v_kind[row + subj] != ORC_K_KNOWN) continue;
       known++;
@@ -2133,9 +2146,7 @@ uint32_t orc_world_reconnect(orc_world* w, uint32_t tick, uint32_t* target) {
       left += w->v_status[row + subj] == ORC_ST_LEFT;
     }
     if (!failed) continue;
-    uint32_t alive_n = known - failed - left;
-    if (alive_n < 1) alive_n = 1;
-    const float prob = (float)failed / (float)alive_n;
+    const float prob = orc_reconnect_prob(known, failed, left);
     uint32_t ctr[4] = {0, PURPOSE_RECONNECT << 24, m, tick}, o[4];
     orc_philox4x32(ctr, key, o);
     const float r = (float)(o[0] >> 8) * (1.0f / 16777216.0f); /* rng.gen::<f32>() */

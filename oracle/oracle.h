@@ -477,6 +477,9 @@ int orc_world_restart(orc_world* w, uint32_t m, const uint8_t* file, uint64_t le
  * it tried (0xFFFFFFFF: none).  A try succeeds when the target member is up, and then
  * memberlist's join notifies handle_node_join.  Returns the successful joins. */
 uint32_t orc_world_reconnect(orc_world* w, uint32_t tick, uint32_t* target);
+/* the Reconnector's throttle probability given members.states.len(), the failed and left
+ * counts (base.rs:670-671) */
+float orc_reconnect_prob(uint64_t states, uint64_t failed, uint64_t left);
 
 #ifdef __cplusplus
 }

@@ -71,3 +71,4 @@ def declare(L):
     sig("rsf_gossip_restart", [VP, P32, C.c_uint32, P8, P64, C.POINTER(C.c_int32)])
     sig("rsf_gossip_dump_snapshot", [VP, P32, P64])
     sig("rsf_gossip_reconnect", [VP, C.c_uint32, VP])
+    sig("rsf_gossip_debug_canaries", [VP, C.POINTER(C.c_int)])

@@ -60,6 +60,19 @@ __device__ unsigned long long g_merge_prof[8];
 #else
 #define RSF_BAD2(k, cond, val) false
 #endif
+// wave-uniform forms for per-lane conditions: the whole wave records and skips together, so
+// no lane leaves while the others go on through wave-wide ballots and shuffles.  Only in
+// converged code (every lane of the wave active).
+#if RSF_CHECKS
+#define RSF_BAD_W(k, cond, val) (__ballot(RSF_BAD(k, cond, val)) != 0)
+#else
+#define RSF_BAD_W(k, cond, val) false
+#endif
+#if RSF_CHECKS >= 2
+#define RSF_BAD2_W(k, cond, val) RSF_BAD_W(k, cond, val)
+#else
+#define RSF_BAD2_W(k, cond, val) false
+#endif
 
 // Wave-wide u64 min/max through DPP (row_ror inside 16-lane rows, then
 // row_bcast15 / row_bcast31 across rows, result in lane 63): VALU-only data
@@ -1252,15 +1265,17 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     } else {
       // slot contents and the group's record count in one round trip (holes read stale ids)
       const uint64_t slot = vs + vi;
-      if (RSF_BAD(6, in && slot >= (uint64_t)c.n_loc * c.fanout * c.cap_t, slot)) return;
+      if (RSF_BAD_W(6, in && slot >= (uint64_t)c.n_loc * c.fanout * c.cap_t, slot)) return;
       rid0 = in ? rec_ld(vals + slot) : 0;
-      if (gcnt && in) {
+      if (gcnt) {
         // group of the slot relative to the receiver's first group: a 32-bit division
         // (a receiver's slot range is small) instead of a 64-bit one
         const uint32_t gr = vi / stride;
-        gk = vi - gr * stride;
-        if (RSF_BAD2(9, (uint64_t)st + gr >= c.n_loc * c.fanout, st + gr)) return;
-        gc = rec_ld(gcnt + st + gr);
+        if (RSF_BAD2_W(9, in && (uint64_t)st + gr >= c.n_loc * c.fanout, st + gr)) return;
+        if (in) {
+          gk = vi - gr * stride;
+          gc = rec_ld(gcnt + st + gr);
+        }
       }
       // decoration (same round trip as the rumor ids): subject of an intent, or the
       // queue of an event / query; invalid lanes read as neither
@@ -1374,11 +1389,9 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     const uint64_t newmask = __ballot(ins);
     if (newmask) {
       const uint32_t k = (uint32_t)__popcll(newmask);
-      if (ins) {
-        const uint32_t i = pn + (uint32_t)__popcll(newmask & below_mask(lane));
-        if (RSF_BAD(5, i >= kPend, i)) return;
-        p_ent[i] = GState::PendE{rid, dsub, ru.msg_len};  // queue 0
-      }
+      const uint32_t i = pn + (uint32_t)__popcll(newmask & below_mask(lane));
+      if (RSF_BAD_W(5, ins && i >= kPend, i)) return;
+      if (ins) p_ent[i] = GState::PendE{rid, dsub, ru.msg_len};  // queue 0
       pn += k;
       pc += k;
     }
@@ -2067,8 +2080,7 @@ struct rsf_gossip {
   // slot[gid] = sorted position; cnt[sorted] = records; off = inclusive scan of cnt (multi-GPU)
   uint32_t *grp_key = nullptr, *grp_cnt = nullptr, *grp_key_s = nullptr, *grp_id = nullptr, *grp_id_s = nullptr,
            *grp_slot = nullptr, *grp_off = nullptr, *stage_dec = nullptr;
-  void* grp_scan_tmp = nullptr;
-  size_t grp_scan_bytes = 0;
+  rsf::CubTemp grp_tmp;  // the group count reduce / scan (each call sized by cub_run)
   unsigned merge_blocks = 1;  // merge_big_kernel's grid: merge_kernel's resident blocks per CU x CUs
   uint32_t* big_ids = nullptr;  // receivers deferred to merge_big_kernel (count: d_counters[52])
   // RSF_GUARD_ZONES (diagnostic builds): 0xA5-filled zones before and after big_ids and
@@ -2076,8 +2088,7 @@ struct rsf_gossip {
   char *big_base = nullptr, *dec_base = nullptr;
   uint64_t* send_buf = nullptr;
   unsigned long long* d_counters = nullptr;  // [0] n_valid, [1..] shard bounds
-  void* sort_tmp = nullptr;
-  size_t sort_tmp_bytes = 0;
+  rsf::CubTemp sort_tmp;  // every radix sort of the round (sort_pairs)
   int end_bit = 32;
   uint64_t last_sent = 0, last_merged = 0;
   uint32_t cur_round = 0;
@@ -2090,8 +2101,7 @@ struct rsf_gossip {
   uint32_t *run_start = nullptr, *run_end = nullptr, *run_base = nullptr, *run_total = nullptr;
   uint64_t* d_run_off = nullptr;
   uint32_t run_cap = 0;
-  void* scan_tmp = nullptr;
-  size_t scan_tmp_bytes = 0;
+  rsf::CubTemp scan_tmp;  // rsf_gossip_round_merge_runs' segment scan
   // phase profiling: marks per round [begin, after begin, after emit, after sort, after merge]
   bool profiling = false;
   static constexpr int kMarks = 5, kMaxProfRounds = 256;
@@ -2137,31 +2147,21 @@ static int ensure_lists(rsf_gossip* g, uint32_t n_ml, uint32_t n_acts) {
   return RSF_OK;
 }
 
-// hipcub does not check the temporary-storage size it is given, and the requirement need not
-// grow monotonically with the item count (the algorithm depends on the size): every sort
-// queries its own requirement and the buffer grows to it.
 #ifndef RSF_GUARD_ZONES
-#define RSF_GUARD_ZONES 0
+#define RSF_GUARD_ZONES 0  // diagnostic builds: 0xA5 zones around stage_dec and big_ids
 #endif
 constexpr size_t kZone = RSF_GUARD_ZONES ? (2u << 20) : 0;
+// every radix sort sizes its own temporary storage (rsf::cub_run)
 static int sort_pairs(rsf_gossip* g, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout,
                       uint64_t n) {
-  size_t need = 0;
-  RSF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, need, kin, kout, vin, vout, (int)n, 0, g->end_bit, g->stream));
-  if (need > g->sort_tmp_bytes) {
-    RSF_HIP(hipStreamSynchronize(g->stream));  // the old buffer may be in use by earlier work
-    hipFree(g->sort_tmp);
-    g->sort_tmp = nullptr;
-    g->sort_tmp_bytes = 0;
-    int rc = rsf::dmalloc(&g->sort_tmp, need + kZone);
-    if (rc) return rc;
-    g->sort_tmp_bytes = need;
-    if (kZone) RSF_HIP(hipMemset((char*)g->sort_tmp + need, 0xA5, kZone));
-  }
-  size_t tmp = g->sort_tmp_bytes;
-  RSF_HIP(hipcub::DeviceRadixSort::SortPairs(g->sort_tmp, tmp, kin, kout, vin, vout, (int)n, 0, g->end_bit,
-                                             g->stream));
-  return RSF_OK;
+  const int end_bit = g->end_bit;
+  hipStream_t st = g->stream;
+  return rsf::cub_run(
+      g->sort_tmp, st,
+      [&](void* t, size_t& b) {
+        return hipcub::DeviceRadixSort::SortPairs(t, b, kin, kout, vin, vout, (int)n, 0, end_bit, st);
+      },
+      "group/record radix sort");
 }
 
 extern "C" {
@@ -2264,32 +2264,13 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   }
 #undef GA
   {
-    size_t tb = 0, tr = 0;
-    if (hipcub::DeviceScan::InclusiveSum(nullptr, tb, g->grp_cnt, g->grp_off, (int)g->n_groups, g->stream) !=
-            hipSuccess ||
-        hipcub::DeviceReduce::Sum(nullptr, tr, g->grp_cnt, (unsigned long long*)g->d_counters, (int)g->n_groups,
-                                  g->stream) != hipSuccess)
-      return fail(rsf::set_error(RSF_ERR_HIP, "hipcub scan sizing failed"));
-    g->grp_scan_bytes = std::max(tb, tr);
     int per_cu = 0, cus = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, merge_kernel<false>, kWave * kWavesPerBlock, 0) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
       return fail(rsf::set_error(RSF_ERR_HIP, "occupancy query failed"));
     g->merge_blocks = (unsigned)std::max(1, per_cu * cus);
-    if ((rc = dmalloc(&g->grp_scan_tmp, tb))) return fail(rc);
   }
-  // sized for both sorts a round runs (the groups; the record stream of the counts path)
-  size_t tmp = 0, tmp_g = 0;
-  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, g->stage_key, g->sort_key, g->stage_val, g->sort_val,
-                                         (int)pipe, 0, g->end_bit, g->stream) != hipSuccess ||
-      hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_g, g->grp_key, g->grp_key_s, g->grp_id, g->grp_id_s,
-                                         (int)g->n_groups, 0, g->end_bit, g->stream) != hipSuccess)
-    return fail(rsf::set_error(RSF_ERR_HIP, "hipcub sort sizing failed"));
-  tmp = std::max(tmp, tmp_g);
-  g->sort_tmp_bytes = tmp;
-  if ((rc = dmalloc(&g->sort_tmp, tmp + kZone))) return fail(rc);
-  if (kZone && hipMemset((char*)g->sort_tmp + tmp, 0xA5, kZone) != hipSuccess)
-    return fail(rsf::set_error(RSF_ERR_HIP, "guard zone init failed"));
+  // the hipCUB temporaries are sized per call at their first use (rsf::cub_run)
   hipStream_t st = g->stream;
   bool ok = true;
   auto ms = [&](void* p, int v, size_t b) { ok = ok && hipMemsetAsync(p, v, b, st) == hipSuccess; };
@@ -2348,14 +2329,17 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   s.q_rumor, s.q_seq,      s.q_txlen,      s.q_dec,      s.q_next_seq,  s.q_pruned, s.q_expired,  s.eb_ltime, s.eb_cnt,     s.eb_keys,
                   s.qb_ltime, s.qb_cnt,    s.qb_ids,       s.rumors,      s.rdec,       s.rbody,      g->d_ml,    g->d_acts,    g->stage_key,
                   g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters, g->rec_dec, g->pp_buf,
-                  g->sort_tmp, g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
-                  g->scan_tmp, g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
-                  g->grp_slot, g->grp_off, g->dec_base, g->grp_scan_tmp, s.dlog, s.dcnt,
+                  g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
+                  g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
+                  g->grp_slot, g->grp_off, g->dec_base, s.dlog, s.dcnt,
                   g->bkt_send, g->bkt_recv, g->bkt_dec, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn,
                   s.p_ent, s.p_cnt, g->big_base};
   for (void* p : ptrs)
     if (p) hipFree(p);
   g->scratch.release();
+  g->sort_tmp.release();
+  g->grp_tmp.release();
+  g->scan_tmp.release();
   if (g->events_made)
     for (auto& row : g->ev)
       for (auto& e : row) hipEventDestroy(e);
@@ -2641,12 +2625,23 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
                      g->grp_cnt, g->stage_val, g->stage_dec, Buckets{});
   RSF_HIP(hipGetLastError());
   RSF_DBG_SYNC(st, "emit_kernel");
-  size_t tb = g->grp_scan_bytes;
   if (local) {
-    RSF_HIP(hipcub::DeviceReduce::Sum(g->grp_scan_tmp, tb, g->grp_cnt, (unsigned long long*)g->d_counters, (int)ng,
-                                      st));
+    unsigned long long* sum = (unsigned long long*)g->d_counters;
+    const uint32_t* cnt = g->grp_cnt;
+    int rc2 = rsf::cub_run(
+        g->grp_tmp, st,
+        [&](void* t, size_t& b) { return hipcub::DeviceReduce::Sum(t, b, cnt, sum, (int)ng, st); },
+        "group count reduce");
+    if (rc2) return rc2;
+    RSF_DBG_SYNC(st, "group count reduce");
   } else {
-    RSF_HIP(hipcub::DeviceScan::InclusiveSum(g->grp_scan_tmp, tb, g->grp_cnt, g->grp_off, (int)ng, st));
+    const uint32_t* cnt = g->grp_cnt;
+    uint32_t* off = g->grp_off;
+    int rc2 = rsf::cub_run(
+        g->grp_tmp, st, [&](void* t, size_t& b) { return hipcub::DeviceScan::InclusiveSum(t, b, cnt, off, (int)ng, st); },
+        "group count scan");
+    if (rc2) return rc2;
+    RSF_DBG_SYNC(st, "group count scan");
     RSF_HIP(hipMemsetAsync(g->d_counters, 0, 8, st));
     hipLaunchKernelGGL(grp_expand_kernel, dim3(grid1(ng * kLanesPerGroup)), dim3(256), 0, st, g->grp_key_s,
                        g->grp_off, ng, c.cap_t, g->stage_val, g->send_buf, g->d_counters);
@@ -2845,20 +2840,33 @@ int rsf_gossip_send_buffer(rsf_gossip* g, void** p, uint64_t* cap) {
 }
 
 // diagnostic (RSF_GUARD_ZONES builds): changed bytes in the guard zones, in the order before
-// stage_dec, after stage_dec, before big_ids, after big_ids, after the sort's storage
-// (synchronises); -1 without zones
-int rsf_gossip_debug_zones(rsf_gossip* g, uint64_t* out5) {
-  if (!g || !out5) return gerr("null argument");
+// stage_dec, after stage_dec, before big_ids, after big_ids (synchronises); -1 without zones
+int rsf_gossip_debug_zones(rsf_gossip* g, uint64_t* out4) {
+  if (!g || !out4) return gerr("null argument");
   if (!kZone) return -1;
   RSF_HIP(hipStreamSynchronize(g->stream));
-  const char* z[5] = {g->dec_base, g->dec_base + kZone + g->stage_cap * 4, g->big_base,
-                      g->big_base + kZone + g->c.n_loc * 4, (const char*)g->sort_tmp + g->sort_tmp_bytes};
+  const char* z[4] = {g->dec_base, g->dec_base + kZone + g->stage_cap * 4, g->big_base,
+                      g->big_base + kZone + g->c.n_loc * 4};
   std::vector<uint8_t> v(kZone);
-  for (int k = 0; k < 5; ++k) {
+  for (int k = 0; k < 4; ++k) {
     RSF_HIP(hipMemcpy(v.data(), z[k], kZone, hipMemcpyDeviceToHost));
     uint64_t c = 0;
     for (uint8_t b : v) c += b != 0xA5;
-    out5[k] = c;
+    out4[k] = c;
+  }
+  return RSF_OK;
+}
+
+// the canaries past the hipCUB temporaries (rsf::CubTemp): radix sorts, group count
+// reduce/scan, run-merge scan; 1 = intact (or never allocated), 0 = overrun (synchronises)
+int rsf_gossip_debug_canaries(rsf_gossip* g, int* out3) {
+  if (!g || !out3) return gerr("null argument");
+  RSF_HIP(hipSetDevice(g->device));
+  const rsf::CubTemp* t[3] = {&g->sort_tmp, &g->grp_tmp, &g->scan_tmp};
+  for (int k = 0; k < 3; ++k) {
+    const int r = t[k]->canary_intact(g->stream);
+    if (r < 0) return r;
+    out3[k] = r;
   }
   return RSF_OK;
 }
@@ -2866,14 +2874,14 @@ int rsf_gossip_debug_zones(rsf_gossip* g, uint64_t* out5) {
 // diagnostic only: device addresses of the context's main buffers and of a global in the
 // library's code object (open issue: an address-dependent fault).  Order:
 // view, p_ent, q_rumor, stage_val, stage_dec, grp_slot, grp_cnt, seg_start, rbody, rumors,
-// rdec, clock, code-object global (0 without one), big_ids, sort_tmp, grp_scan_tmp, d_counters,
+// rdec, clock, code-object global (0 without one), big_ids, sort_tmp, grp_tmp, d_counters,
 // d_acts, grp_key, grp_key_s, grp_id, grp_id_s, grp_off, stage_key, sort_key, sort_val,
 // send_buf, rec_dec, seg_end, p_cnt, err, member_subj.  Returns the count written.
 int rsf_gossip_debug_ptrs(rsf_gossip* g, uint64_t* out, uint32_t n) {
   if (!g || !out) return gerr("null argument");
   const void* p[32] = {g->s.view, g->s.p_ent, g->s.q_rumor, g->stage_val, g->stage_dec, g->grp_slot, g->grp_cnt,
                        g->seg_start, g->s.rbody, g->s.rumors, g->s.rdec, g->s.clock, nullptr,
-                       g->big_ids, g->sort_tmp, g->grp_scan_tmp, g->d_counters, g->d_acts, g->grp_key, g->grp_key_s,
+                       g->big_ids, g->sort_tmp.p, g->grp_tmp.p, g->d_counters, g->d_acts, g->grp_key, g->grp_key_s,
                        g->grp_id, g->grp_id_s, g->grp_off, g->stage_key, g->sort_key, g->sort_val, g->send_buf,
                        g->rec_dec, g->seg_end, g->s.p_cnt, g->s.err, g->s.member_subj};
 #if RSF_MERGE_PROF || RSF_EMIT_PROF || RSF_CHECKS
@@ -2946,10 +2954,6 @@ int rsf_gossip_round_merge_runs(rsf_gossip* g, const uint64_t* recv, const uint6
     int rc;
     if ((rc = rsf::dmalloc((void**)&g->run_total, c.n_loc * 4)) || (rc = rsf::dmalloc((void**)&g->d_run_off, 63 * 8)))
       return rc;
-    size_t tb = 0;
-    RSF_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, g->run_total, g->seg_start, (int)c.n_loc, st));
-    if ((rc = rsf::dmalloc(&g->scan_tmp, tb))) return rc;
-    g->scan_tmp_bytes = tb;
   }
   RSF_HIP(hipMemcpyAsync(g->d_run_off, off, (n_runs + 1) * 8, hipMemcpyHostToDevice, st));
   const size_t tab = (size_t)n_runs * c.n_loc * 4;
@@ -2961,8 +2965,15 @@ int rsf_gossip_round_merge_runs(rsf_gossip* g, const uint64_t* recv, const uint6
                        c.n_loc, g->run_start, g->run_end, g->d_counters + 62);
   hipLaunchKernelGGL(runs_base_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, n_runs, c.n_loc, g->run_start,
                      g->run_end, g->run_base, g->run_total);
-  size_t tb = g->scan_tmp_bytes;
-  RSF_HIP(hipcub::DeviceScan::ExclusiveSum(g->scan_tmp, tb, g->run_total, g->seg_start, (int)c.n_loc, st));
+  {
+    const uint32_t* tot = g->run_total;
+    uint32_t* seg = g->seg_start;
+    const int nl = (int)c.n_loc;
+    int rc = rsf::cub_run(
+        g->scan_tmp, st, [&](void* t, size_t& b) { return hipcub::DeviceScan::ExclusiveSum(t, b, tot, seg, nl, st); },
+        "run-merge segment scan");
+    if (rc) return rc;
+  }
   if (n)
     hipLaunchKernelGGL(runs_scatter_kernel, dim3(grid1(n)), dim3(256), 0, st, recv, n, g->d_run_off, n_runs, c.lo,
                        c.n_loc, g->run_start, g->run_base, g->seg_start, g->sort_val, (const uint32_t*)g->s.rdec,
@@ -3542,10 +3553,13 @@ __global__ void __launch_bounds__(256) snap_restart_kernel(GCfg c, GState s, con
   res[i] = joined ? 1 : 0;
 }
 
-// Reconnector tick (base.rs:647-690), one wave per member: count the failed / left /
-// known members of the view; with probability failed / (known - failed - left) try a
-// uniformly drawn failed member; the try succeeds when that member is up, and memberlist's
-// join then notifies handle_node_join
+// Reconnector tick (base.rs:647-690), one wave per member: count the failed / left
+// members of the view; with probability num_failed / max(states.len() - failed - left, 1)
+// (base.rs:670-671) try a uniformly drawn failed member; the try succeeds when that member
+// is up, and memberlist's join then notifies handle_node_join.  states.len() is every
+// member the node knows: the N - S untracked members (implicitly Alive, the local node
+// among them when it is not a subject), the local node when it is a subject, and the
+// tracked subjects whose entry is KNOWN.
 __global__ void __launch_bounds__(256) reconnect_kernel(GCfg c, GState s, uint32_t tick, uint32_t* __restrict__ target) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint64_t l = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
@@ -3555,7 +3569,8 @@ __global__ void __launch_bounds__(256) reconnect_kernel(GCfg c, GState s, uint32
   if (!s.alive[m]) return;
   const int32_t own = s.member_subj[l];
   const ViewE* row = s.view + l * c.S;
-  uint32_t failed = 0, left = 0, known = 1;  // members.states holds the local node too
+  uint32_t failed = 0, left = 0;
+  uint64_t known = (c.N - c.S) + (own >= 0 ? 1u : 0u);  // members.states: see above
   for (uint32_t j0 = 0; j0 < c.S; j0 += kWave) {
     const uint32_t j = j0 + lane;
     uint32_t meta = 0;
@@ -3566,9 +3581,9 @@ __global__ void __launch_bounds__(256) reconnect_kernel(GCfg c, GState s, uint32
     left += (uint32_t)__popcll(__ballot(kn && vstatus(meta) == RSF_STATUS_LEFT));
   }
   if (!failed) return;
-  uint32_t alive_n = known - failed - left;
+  uint64_t alive_n = known - failed - left;
   if (alive_n < 1) alive_n = 1;
-  const float prob = __fdiv_rn((float)failed, (float)alive_n);
+  const float prob = __fdiv_rn((float)failed, (float)alive_n);  // usize as f32: round to nearest
   const u32x4 o = philox4x32_10(0, kPurposeReconnect << 24, m, tick, c.k0, c.k1);
   const float rr = (float)(o.x >> 8) * (1.0f / 16777216.0f);  // rng.gen::<f32>()
   if (rr > prob) return;

@@ -68,9 +68,68 @@ struct DeviceScratch {
   }
 };
 
+// hipCUB temporary storage.  hipcub does not check the size it is handed, and a call's
+// requirement depends on the algorithm, the item count and the types, so no size queried
+// for one call may be used for another: every call goes through cub_run, which queries
+// that call's own requirement and grows the buffer to it.  A kCanary-byte 0xA5 canary is
+// written past the requested bytes at every allocation; canary_intact() reads it back
+// (diagnostics and tests: an overrun of the temporary storage changes it).
+struct CubTemp {
+  static constexpr size_t kCanary = 256;
+  void* p = nullptr;
+  size_t bytes = 0;  // usable bytes; the canary follows them
+  int ensure(size_t need, hipStream_t st) {
+    if (p && need <= bytes) return RSF_OK;
+    if (p) {
+      (void)hipStreamSynchronize(st);  // the old buffer may be in use by queued work
+      (void)hipFree(p);
+    }
+    p = nullptr;
+    bytes = 0;
+    int rc = dmalloc(&p, need + kCanary);
+    if (rc) return rc;
+    if (hipMemsetAsync((char*)p + need, 0xA5, kCanary, st) != hipSuccess)
+      return set_error(RSF_ERR_HIP, "canary initialisation failed");
+    bytes = need;
+    return RSF_OK;
+  }
+  // 1 if the canary is untouched (or nothing was allocated), 0 if not, <0 on a HIP error;
+  // synchronises the stream
+  int canary_intact(hipStream_t st) const {
+    if (!p) return 1;
+    unsigned char h[kCanary];
+    if (hipMemcpyAsync(h, (const char*)p + bytes, kCanary, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return set_error(RSF_ERR_HIP, "canary read failed");
+    for (size_t i = 0; i < kCanary; ++i)
+      if (h[i] != 0xA5) return 0;
+    return 1;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+// One hipCUB device-wide call: f(void* tmp, size_t& bytes) -> hipError_t is invoked once
+// with tmp == nullptr to size the call, then with storage of at least that size.
+template <class F>
+inline int cub_run(CubTemp& t, hipStream_t st, F&& f, const char* what) {
+  size_t need = 0;
+  hipError_t e = f(nullptr, need);
+  if (e != hipSuccess) return set_hip_error(e, what, __FILE__, __LINE__);
+  int rc = t.ensure(need, st);
+  if (rc) return rc;
+  size_t b = t.bytes;
+  e = f(t.p, b);
+  if (e != hipSuccess) return set_hip_error(e, what, __FILE__, __LINE__);
+  return RSF_OK;
+}
+
 }  // namespace rsf
 
-#define RSF_HIP(call)                                                         \
+#define RSF_HIP(call)                                                       \
   do {                                                                        \
     hipError_t rsf_e_ = (call);                                               \
     if (rsf_e_ != hipSuccess) return rsf::set_hip_error(rsf_e_, #call, __FILE__, __LINE__); \

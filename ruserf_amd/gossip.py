@@ -408,6 +408,13 @@ class GossipEngine:
         check(lib().rsf_gossip_phase_times(self._h, ms, C.byref(r)))
         return list(ms), r.value
 
+    def cub_canaries(self):
+        """[sort, group reduce/scan, run-merge scan]: True if the canary after that hipCUB
+        temporary is intact (nothing wrote past the storage the call asked for); synchronises."""
+        out = (C.c_int * 3)()
+        check(lib().rsf_gossip_debug_canaries(self._h, out))
+        return [bool(x) for x in out]
+
     def merged_total(self):
         t = C.c_uint64()
         check(lib().rsf_gossip_totals(self._h, C.byref(t)))

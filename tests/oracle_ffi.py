@@ -257,6 +257,8 @@ def lib():
     L.orc_world_restart.argtypes = [C.POINTER(World), C.c_uint32, P8, C.c_uint64]
     L.orc_world_reconnect.argtypes = [C.POINTER(World), C.c_uint32, P32]
     L.orc_world_reconnect.restype = C.c_uint32
+    L.orc_reconnect_prob.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
+    L.orc_reconnect_prob.restype = C.c_float
     _lib = L
     return L
 

@@ -261,3 +261,63 @@ def test_reconnect_targets_failed_members_only():
     nf = ((kind == O.K_KNOWN) & (status == O.ST_FAILED)).sum(1)
     assert np.all(tgt[nf == 0] == 0xFFFFFFFF)
     L.orc_world_free(C.byref(w))
+
+
+def test_reconnect_probability_formula_hand_worked():
+    """base.rs:670-671: num_alive = (members.states.len() - num_failed - left_members.len()).max(1),
+    prob = num_failed as f32 / num_alive as f32.  At configs[1]'s shape (N = 1M members, S = 4096
+    tracked subjects) a member that is not a subject knows the N - S untracked members
+    (implicitly Alive, itself among them) plus the tracked subjects it knows: with all 4096
+    known, 10 failed and 5 left, states.len() = 1_000_000 and prob = 10 / 999_985."""
+    n, s = 1_000_000, 4096
+    states = (n - s) + s
+    got = L.orc_reconnect_prob(states, 10, 5)
+    assert np.float32(got) == np.float32(10) / np.float32(999_985)
+    assert abs(got - 1.0000150e-5) < 1e-11
+    # the subject itself is not one of the N - S: it adds itself (known = N - S + 1 + tracked others)
+    assert np.float32(L.orc_reconnect_prob((n - s) + 1 + 4095, 3, 0)) == np.float32(3) / np.float32(n - 3)
+    # .max(1): every known member failed or left
+    assert L.orc_reconnect_prob(7, 4, 3) == 4.0
+    # the tracked-only count (round-2 model) would be ~244x larger at this shape
+    assert L.orc_reconnect_prob(s + 1, 10, 5) / got > 240
+
+
+def test_reconnect_throttle_uses_states_len():
+    """The world's Reconnector draws each member's throttle exactly as the formula above with
+    states.len() = (n - s) + [member is a subject] + its KNOWN tracked subjects, and the same
+    Philox draw (purpose 7, counter (0, 7 << 24, member, tick))."""
+    w, cfg, subj, acts, ml = _world(n=800, rounds=10, seed=6)
+    n, s = w.n, w.s
+    for t in range(len(ml)):
+        H.oracle_round(w, t, ml[t], acts[t])
+    kind = O.arr(w.v_kind, n * s, np.uint8).reshape(n, s).copy()
+    status = O.arr(w.v_status, n * s, np.uint8).reshape(n, s).copy()
+    msubj = O.arr(w.member_subj, n, np.int32).copy()
+    alive = O.arr(w.alive, n, np.uint8).copy()
+    seed = cfg.seed
+    key = np.array([seed & 0xFFFFFFFF, seed >> 32], np.uint32)
+    tick = 5
+    expect_try = np.zeros(n, bool)
+    for m in range(n):
+        if not alive[m]:
+            continue
+        own = int(msubj[m])
+        mask = np.ones(s, bool)
+        if own >= 0:
+            mask[own] = False
+        kn = mask & (kind[m] == O.K_KNOWN)
+        failed = int((kn & (status[m] == O.ST_FAILED)).sum())
+        left = int((kn & (status[m] == O.ST_LEFT)).sum())
+        if failed == 0:
+            continue
+        states = (n - s) + (1 if own >= 0 else 0) + int(kn.sum())
+        prob = np.float32(failed) / np.float32(max(states - failed - left, 1))
+        ctr = np.array([0, 7 << 24, m, tick], np.uint32)
+        out = np.zeros(4, np.uint32)
+        L.orc_philox4x32(O.ptr(ctr, C.c_uint32), O.ptr(key, C.c_uint32), O.ptr(out, C.c_uint32))
+        r = np.float32(int(out[0]) >> 8) * np.float32(1.0 / 16777216.0)
+        expect_try[m] = not (r > prob)
+    tgt = np.zeros(n, np.uint32)
+    L.orc_world_reconnect(C.byref(w), tick, O.ptr(tgt, C.c_uint32))
+    assert np.array_equal(tgt != 0xFFFFFFFF, expect_try)
+    L.orc_world_free(C.byref(w))
