@@ -338,6 +338,52 @@ struct alignas(16) QLds {
   uint32_t r[kWave], sq[kWave], tl[kWave], dec[kWave];
 };
 
+// Re-rank after picks: the unpicked keepers (np_m) and the bumped keepers (pk_m) are each
+// still sorted in lane order; merge them, free lanes after.  Each list's keys go to the
+// wave's LDS row in order, and every keeper counts the other list's keys below its own by a
+// binary search there (keys are distinct), all lanes at once: a handful of LDS reads
+// instead of a wave-wide pass per bumped item.
+template <bool PERMUTE_DEC>
+__device__ __forceinline__ void q_rerank(const GCfg& c, QRegs& Q, uint32_t lane, uint64_t pk_m, uint64_t np_m,
+                                         QLds& row) {
+  const bool valid = lane < c.qcap;
+  const uint64_t below = below_mask(lane);
+  const uint64_t kept_m = pk_m | np_m;
+  const bool np = (np_m >> lane) & 1, pk = (pk_m >> lane) & 1;
+  const uint64_t mykey = tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq);
+  uint64_t* const keys_np = reinterpret_cast<uint64_t*>(row.r);  // r + sq: 64 keys
+  uint64_t* const keys_pk = reinterpret_cast<uint64_t*>(row.tl);  // tl + dec: 64 keys
+  const uint32_t r_np = (uint32_t)__popcll(np_m & below), r_pk = (uint32_t)__popcll(pk_m & below);
+  if (np) keys_np[r_np] = mykey;
+  if (pk) keys_pk[r_pk] = mykey;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  uint32_t pos;
+  if (np || pk) {
+    const uint64_t* other = np ? keys_pk : keys_np;
+    uint32_t lo = 0, len = (uint32_t)__popcll(np ? pk_m : np_m);
+    while (len) {  // lower_bound of mykey in the other list
+      const uint32_t half = len >> 1;
+      if (other[lo + half] < mykey) {
+        lo += half + 1;
+        len -= half + 1;
+      } else {
+        len = half;
+      }
+    }
+    pos = (np ? r_np : r_pk) + lo;
+  } else {
+    pos = valid ? (uint32_t)__popcll(kept_m) + (uint32_t)__popcll(~kept_m & below) : lane;
+  }
+  __builtin_amdgcn_wave_barrier();  // the row is free once every lane has searched it
+  const int addr = (int)(pos * 4);
+  Q.r = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.r);
+  Q.sq = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.sq);
+  Q.tl = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.tl);
+  if (PERMUTE_DEC) Q.dec = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.dec);
+}
+
 // one get_broadcasts call on a sorted register-resident queue; returns bytes used.
 // The lowest unpicked lane that fits IS the reference's pick (lowest transmits, then
 // longest fitting, then newest): every skipped lower lane did not fit and never will.
@@ -345,6 +391,9 @@ struct alignas(16) QLds {
 // scalar work on one 64-bit mask instead of per-lane flags under exec masking.
 #ifndef RSF_EMIT_NT
 #define RSF_EMIT_NT 0  // emit: records written non-temporally
+#endif
+#ifndef RSF_EMIT_LAZY
+#define RSF_EMIT_LAZY 1  // emit: one deferred re-rank per queue per emission (q_get_broadcasts_lazy)
 #endif
 template <bool PERMUTE_DEC>
 __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uint32_t lane, int64_t limit,
@@ -394,46 +443,82 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   const bool retire = picked && (Q.tl & 0xFFFF) + 1 >= c.tx_limit;
   if (retire) Q.r = kEmpty;
   else if (picked) Q.tl = Q.tl + 1;
-  // re-rank: the unpicked keepers (np) and the bumped keepers (pk) are each still sorted;
-  // merge them.  Each list's keys go to the wave's LDS row in order, and every keeper
-  // counts the other list's keys below its own by a binary search there (keys are
-  // distinct), all lanes at once: a handful of LDS reads instead of a wave-wide pass per
-  // bumped item.
-  const uint64_t pk_m = pick_m & ~__ballot(retire), np_m = live_m & ~pick_m;
-  const uint64_t kept_m = pk_m | np_m;
-  const bool np = (np_m >> lane) & 1, pk = (pk_m >> lane) & 1;
-  const uint64_t mykey = tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq);
-  uint64_t* const keys_np = reinterpret_cast<uint64_t*>(row.r);  // r + sq: 64 keys
-  uint64_t* const keys_pk = reinterpret_cast<uint64_t*>(row.tl);  // tl + dec: 64 keys
-  const uint32_t r_np = (uint32_t)__popcll(np_m & below), r_pk = (uint32_t)__popcll(pk_m & below);
-  if (np) keys_np[r_np] = mykey;
-  if (pk) keys_pk[r_pk] = mykey;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  uint32_t pos;
-  if (np || pk) {
-    const uint64_t* other = np ? keys_pk : keys_np;
-    uint32_t lo = 0, len = (uint32_t)__popcll(np ? pk_m : np_m);
-    while (len) {  // lower_bound of mykey in the other list
-      const uint32_t half = len >> 1;
-      if (other[lo + half] < mykey) {
-        lo += half + 1;
-        len -= half + 1;
-      } else {
-        len = half;
-      }
+  q_rerank<PERMUTE_DEC>(c, Q, lane, pick_m & ~__ballot(retire), live_m & ~pick_m, row);
+  return used;
+}
+
+// get_broadcasts with the re-rank deferred.  Between the fanout peers' calls of one
+// emission a queue is left in VIRTUAL order: the items picked so far (`cons`, all from the
+// queue's lowest transmit class t0) are bumped or retired in place but not moved.  The
+// actual send order is then [unpicked items of class t0, in lane order] followed by the
+// merge of everything else, so a call whose picks all come from that leading run -- the
+// prefix that fits, then later shorter items, as long as the next candidate is still of
+// class t0 -- picks exactly what the reference would.  When the next candidate could lie
+// past the run (its order there is not known without the merge), the deferred re-rank is
+// done and the exact q_get_broadcasts runs.  The caller materialises (q_materialize) after
+// the last peer.  Three re-ranks per emission become one in the common case.
+template <bool PERMUTE_DEC>
+__device__ __forceinline__ void q_materialize(const GCfg& c, QRegs& Q, uint32_t lane, uint64_t& cons, QLds& row) {
+  if (!cons) return;
+  const uint64_t live_m = __ballot(lane < c.qcap && Q.r != kEmpty);
+  q_rerank<PERMUTE_DEC>(c, Q, lane, cons & live_m, live_m & ~cons, row);
+  cons = 0;
+}
+template <bool PERMUTE_DEC>
+__device__ __forceinline__ int64_t q_get_broadcasts_lazy(const GCfg& c, QRegs& Q, uint32_t lane, int64_t limit,
+                                                         uint32_t* stage_val, uint32_t* stage_dec, uint64_t out_base,
+                                                         uint32_t& nrec, uint32_t& err, bool& dirty, QLds& row,
+                                                         uint64_t& cons, uint32_t& t0) {
+  const bool valid = lane < c.qcap;
+  const uint64_t live_m = __ballot(valid && Q.r != kEmpty);
+  if (!live_m) return 0;
+  if (!cons) t0 = shfl_u32(Q.tl, 0) & 0xFFFF;  // materialised: lane 0 holds the smallest key
+  const uint32_t len = Q.tl >> 16;
+  const uint64_t a_m = __ballot(valid && Q.r != kEmpty && (Q.tl & 0xFFFF) == t0) & ~cons;
+  const bool in_a = (a_m >> lane) & 1;
+  const uint32_t incl = wave_inclusive_sum_u32(in_a ? c.overhead + len : 0u);
+  uint64_t pick_m = limit >= 0 ? (__ballot((int64_t)incl <= limit) & a_m) : 0ull;
+  int64_t used = pick_m ? (int64_t)shfl_u32(incl, 63 - __clzll((long long)pick_m)) : 0;
+  bool exact = false;
+  for (;;) {
+    const int64_t free_b = limit - used - (int64_t)c.overhead;
+    if (free_b <= 0) break;
+    const uint64_t fit = __ballot((int64_t)len <= free_b) & live_m & ~pick_m;
+    if (!fit) break;
+    const uint64_t cand = fit & a_m;
+    if (!cand) {  // the next candidate lies past the class-t0 run
+      exact = true;
+      break;
     }
-    pos = (np ? r_np : r_pk) + lo;
-  } else {
-    pos = valid ? (uint32_t)__popcll(kept_m) + (uint32_t)__popcll(~kept_m & below) : lane;
+    const int win = __ffsll((long long)cand) - 1;
+    pick_m |= 1ull << win;
+    used += (int64_t)c.overhead + shfl_u32(len, win);
   }
-  __builtin_amdgcn_wave_barrier();  // the row is free once every lane has searched it
-  const int addr = (int)(pos * 4);
-  Q.r = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.r);
-  Q.sq = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.sq);
-  Q.tl = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.tl);
-  if (PERMUTE_DEC) Q.dec = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.dec);
+  if (exact) {
+    q_materialize<PERMUTE_DEC>(c, Q, lane, cons, row);
+    return q_get_broadcasts<PERMUTE_DEC>(c, Q, lane, limit, stage_val, stage_dec, out_base, nrec, err, dirty, row);
+  }
+  if (!pick_m) return used;
+  const uint64_t below = below_mask(lane);
+  const bool picked = (pick_m >> lane) & 1;
+  const uint32_t npick = (uint32_t)__popcll(pick_m);
+  const uint32_t rank = (uint32_t)__popcll(pick_m & below);
+  if (picked && nrec + rank < c.cap_t && stage_val) {
+#if RSF_EMIT_NT
+    __builtin_nontemporal_store(Q.r, stage_val + out_base + nrec + rank);
+    if (stage_dec) __builtin_nontemporal_store(Q.dec, stage_dec + out_base + nrec + rank);
+#else
+    stage_val[out_base + nrec + rank] = Q.r;
+    if (stage_dec) stage_dec[out_base + nrec + rank] = Q.dec;
+#endif
+  }
+  if (nrec + npick > c.cap_t) err |= kErrStage;
+  nrec += npick;
+  dirty = true;
+  const bool retire = picked && (Q.tl & 0xFFFF) + 1 >= c.tx_limit;
+  if (retire) Q.r = kEmpty;
+  else if (picked) Q.tl = Q.tl + 1;
+  cons |= pick_m;
   return used;
 }
 
@@ -940,6 +1025,10 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   }
   EPROF_T(t2);
   EPROF_ADD(1, t1, t2);
+#if RSF_EMIT_LAZY
+  uint64_t cons0 = 0, cons1 = 0, cons2 = 0;  // picks whose re-rank is deferred (q_get_broadcasts_lazy)
+  uint32_t t00 = 0, t01 = 0, t02 = 0;
+#endif
   for (uint32_t j = 0; j < np; ++j) {
     const uint32_t gslot = shfl_u32(e.gs, j);
     if (RSF_BAD2(7, !BKT && gslot >= c.n_loc * c.fanout, gslot)) return;
@@ -961,11 +1050,25 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
     }
     uint32_t nrec = 0;
     int64_t used = 0;
+#if RSF_EMIT_LAZY
+    used += q_get_broadcasts_lazy<true>(c, Q0, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d0, row,
+                                        cons0, t00);
+    used += q_get_broadcasts_lazy<false>(c, Q1, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d1, row,
+                                         cons1, t01);
+    used += q_get_broadcasts_lazy<false>(c, Q2, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d2, row,
+                                         cons2, t02);
+#else
     used += q_get_broadcasts<true>(c, Q0, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d0, row);
     used += q_get_broadcasts<false>(c, Q1, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d1, row);
     used += q_get_broadcasts<false>(c, Q2, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d2, row);
+#endif
     if (lane == 0 && oc && nrec) *oc = min(nrec, c.cap_t);
   }
+#if RSF_EMIT_LAZY
+  q_materialize<true>(c, Q0, lane, cons0, row);
+  q_materialize<false>(c, Q1, lane, cons1, row);
+  q_materialize<false>(c, Q2, lane, cons2, row);
+#endif
   EPROF_T(t3);
   EPROF_ADD(2, t2, t3);
   if (d0) q_store(c, s, l, 0, lane, Q0, true);

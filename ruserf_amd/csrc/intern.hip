@@ -224,73 +224,121 @@ int rsf_interner_count(const rsf_interner* t, uint32_t* n_ids, uint64_t* arena_u
   return RSF_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// One batch through an interner in two steps, so that a caller interning into several
+// tables can check every capacity before committing any (rsf_wire_event_keys).
+// plan: hashes, sort, equal-bytes runs, lookups of the existing table, the new ids' ranks
+// and arena offsets -> n_new, bytes_new.  commit: insert and write the ids.
+struct InternPlan {
+  rsf_interner* t = nullptr;
+  const uint8_t* buf = nullptr;
+  const uint64_t* off = nullptr;
+  const uint32_t* len = nullptr;
+  uint64_t n = 0;
+  hipStream_t st = nullptr;
+  void* mem = nullptr;  // scratch (hipMallocAsync on st), freed by ~InternPlan
+  uint64_t *h = nullptr, *h_s = nullptr, *new_len = nullptr, *aoff = nullptr;
+  uint32_t *idx = nullptr, *idx_s = nullptr, *rep = nullptr, *found = nullptr, *is_new = nullptr, *rank = nullptr,
+           *head = nullptr, *run_start = nullptr;
+  uint64_t n_new = 0, bytes_new = 0;
+  ~InternPlan() {
+    if (mem) hipFreeAsync(mem, st);
+  }
+};
+
+int intern_plan(InternPlan& P) {
+  const uint64_t n = P.n;
+  hipStream_t st = P.st;
+  rsf_interner* t = P.t;
+  const int ni = (int)n;
+  size_t t_sort = 0, t_scan4 = 0, t_scan8 = 0, t_max = 0;
+  // every hipCUB call below is sized here for its own types and count; the temporary
+  // storage is the largest of them
+  RSF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t_sort, P.h, P.h_s, P.idx, P.idx_s, ni, 0, 64, st));
+  RSF_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan4, P.is_new, P.rank, ni, st));
+  RSF_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan8, P.new_len, P.aoff, ni, st));
+  RSF_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, t_max, P.head, P.run_start, hipcub::Max(), ni, st));
+  const size_t tmp = std::max(std::max(t_sort, t_max), std::max(t_scan4, t_scan8));
+  const size_t n8 = ((size_t)n * 8 + 255) & ~(size_t)255, n4 = ((size_t)n * 4 + 255) & ~(size_t)255;
+  RSF_HIP(hipMallocAsync(&P.mem, 4 * n8 + 8 * n4 + ((tmp + 255) & ~(size_t)255), st));
+  char* b = (char*)P.mem;
+  auto take8 = [&](uint64_t** pp) { *pp = (uint64_t*)b; b += n8; };
+  auto take4 = [&](uint32_t** pp) { *pp = (uint32_t*)b; b += n4; };
+  take8(&P.h); take8(&P.h_s); take8(&P.new_len); take8(&P.aoff);
+  take4(&P.idx); take4(&P.idx_s); take4(&P.rep); take4(&P.found); take4(&P.is_new); take4(&P.rank); take4(&P.head);
+  take4(&P.run_start);
+  void* tp = b;
+  const unsigned g = grid1(n);
+  hipLaunchKernelGGL(in_hash_kernel, dim3(g), dim3(256), 0, st, P.buf, P.off, P.len, n, P.h, P.idx);
+  size_t tb = tmp;
+  RSF_HIP(hipcub::DeviceRadixSort::SortPairs(tp, tb, P.h, P.h_s, P.idx, P.idx_s, ni, 0, 64, st));
+  hipLaunchKernelGGL(in_heads_kernel, dim3(g), dim3(256), 0, st, P.h_s, n, P.head);
+  tb = tmp;
+  RSF_HIP(hipcub::DeviceScan::InclusiveScan(tp, tb, P.head, P.run_start, hipcub::Max(), ni, st));
+  RSF_HIP(hipMemsetAsync(P.is_new, 0, (size_t)n * 4, st));
+  RSF_HIP(hipMemsetAsync(P.new_len, 0, (size_t)n * 8, st));
+  hipLaunchKernelGGL(in_group_kernel, dim3(g), dim3(256), 0, st, P.buf, P.off, P.len, P.h_s, P.idx_s, P.run_start, n,
+                     *t, P.rep, P.found, P.is_new, P.new_len);
+  tb = tmp;
+  RSF_HIP(hipcub::DeviceScan::ExclusiveSum(tp, tb, P.is_new, P.rank, ni, st));
+  tb = tmp;
+  RSF_HIP(hipcub::DeviceScan::ExclusiveSum(tp, tb, P.new_len, P.aoff, ni, st));
+  // totals: last rank + last flag, last offset + last length
+  uint32_t last[2];
+  uint64_t lastb[2];
+  RSF_HIP(hipMemcpyAsync(&last[0], P.rank + n - 1, 4, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipMemcpyAsync(&last[1], P.is_new + n - 1, 4, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipMemcpyAsync(&lastb[0], P.aoff + n - 1, 8, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipMemcpyAsync(&lastb[1], P.new_len + n - 1, 8, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipStreamSynchronize(st));
+  P.n_new = (uint64_t)last[0] + last[1];
+  P.bytes_new = lastb[0] + lastb[1];
+  return RSF_OK;
+}
+
+bool intern_fits(const InternPlan& P) {
+  return P.t->n_ids + P.n_new <= P.t->max_ids && P.t->arena_used + P.bytes_new <= P.t->arena_cap;
+}
+
+int intern_commit(InternPlan& P, uint32_t* ids) {
+  rsf_interner* t = P.t;
+  const unsigned g = grid1(P.n);
+  hipLaunchKernelGGL(in_insert_kernel, dim3(g), dim3(256), 0, P.st, P.buf, P.off, P.len, P.h_s, P.idx_s, P.rep, P.n,
+                     *t, P.rank, P.aoff, P.found);
+  hipLaunchKernelGGL(in_ids_kernel, dim3(g), dim3(256), 0, P.st, P.idx_s, P.rep, P.found, P.n, ids);
+  RSF_HIP(hipGetLastError());
+  t->n_ids += (uint32_t)P.n_new;
+  t->arena_used += P.bytes_new;
+  return RSF_OK;
+}
+}  // namespace
+
+extern "C" {
+
 int rsf_intern(rsf_interner* t, const uint8_t* buf, const uint64_t* off, const uint32_t* len, uint64_t n,
                uint32_t* ids, void* stream) {
   if (!t || (n && (!buf || !off || !len || !ids))) return rsf::set_error(RSF_ERR_ARG, "null argument");
   if (n == 0) return RSF_OK;
   if (n >= 0x7FFFFFFFull) return rsf::set_error(RSF_ERR_ARG, "batch too large");
   RSF_HIP(hipSetDevice(t->device));
-  hipStream_t st = (hipStream_t)stream;
-  const int ni = (int)n;
-  uint64_t *h = nullptr, *h_s = nullptr, *new_len = nullptr, *aoff = nullptr;
-  uint32_t *idx = nullptr, *idx_s = nullptr, *rep = nullptr, *found = nullptr, *is_new = nullptr, *rank = nullptr,
-           *head = nullptr, *run_start = nullptr;
-  size_t t_sort = 0, t_scan4 = 0, t_scan8 = 0, t_max = 0;
-  RSF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t_sort, h, h_s, idx, idx_s, ni, 0, 64, st));
-  RSF_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan4, is_new, rank, ni, st));
-  RSF_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan8, new_len, aoff, ni, st));
-  RSF_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, t_max, head, run_start, hipcub::Max(), ni, st));
-  const size_t tmp = std::max(std::max(t_sort, t_max), std::max(t_scan4, t_scan8));
-  const size_t n8 = ((size_t)n * 8 + 255) & ~(size_t)255, n4 = ((size_t)n * 4 + 255) & ~(size_t)255;
-  Scratch sc(st);
-  RSF_HIP(hipMallocAsync(&sc.p, 4 * n8 + 8 * n4 + ((tmp + 255) & ~(size_t)255), st));
-  char* b = (char*)sc.p;
-  auto take8 = [&](uint64_t** pp) { *pp = (uint64_t*)b; b += n8; };
-  auto take4 = [&](uint32_t** pp) { *pp = (uint32_t*)b; b += n4; };
-  take8(&h); take8(&h_s); take8(&new_len); take8(&aoff);
-  take4(&idx); take4(&idx_s); take4(&rep); take4(&found); take4(&is_new); take4(&rank); take4(&head);
-  take4(&run_start);
-  void* tp = b;
-  const unsigned g = grid1(n);
-  hipLaunchKernelGGL(in_hash_kernel, dim3(g), dim3(256), 0, st, buf, off, len, n, h, idx);
-  size_t tb = tmp;
-  RSF_HIP(hipcub::DeviceRadixSort::SortPairs(tp, tb, h, h_s, idx, idx_s, ni, 0, 64, st));
-  hipLaunchKernelGGL(in_heads_kernel, dim3(g), dim3(256), 0, st, h_s, n, head);
-  tb = tmp;
-  RSF_HIP(hipcub::DeviceScan::InclusiveScan(tp, tb, head, run_start, hipcub::Max(), ni, st));
-  RSF_HIP(hipMemsetAsync(is_new, 0, (size_t)n * 4, st));
-  RSF_HIP(hipMemsetAsync(new_len, 0, (size_t)n * 8, st));
-  hipLaunchKernelGGL(in_group_kernel, dim3(g), dim3(256), 0, st, buf, off, len, h_s, idx_s, run_start, n, *t, rep,
-                     found, is_new, new_len);
-  tb = tmp;
-  RSF_HIP(hipcub::DeviceScan::ExclusiveSum(tp, tb, is_new, rank, ni, st));
-  tb = tmp;
-  RSF_HIP(hipcub::DeviceScan::ExclusiveSum(tp, tb, new_len, aoff, ni, st));
-  // totals: last rank + last flag, last offset + last length
-  uint32_t last[2];
-  uint64_t lastb[2];
-  RSF_HIP(hipMemcpyAsync(&last[0], rank + n - 1, 4, hipMemcpyDeviceToHost, st));
-  RSF_HIP(hipMemcpyAsync(&last[1], is_new + n - 1, 4, hipMemcpyDeviceToHost, st));
-  RSF_HIP(hipMemcpyAsync(&lastb[0], aoff + n - 1, 8, hipMemcpyDeviceToHost, st));
-  RSF_HIP(hipMemcpyAsync(&lastb[1], new_len + n - 1, 8, hipMemcpyDeviceToHost, st));
-  RSF_HIP(hipStreamSynchronize(st));
-  const uint64_t n_new = (uint64_t)last[0] + last[1], bytes_new = lastb[0] + lastb[1];
-  if (t->n_ids + n_new > t->max_ids || t->arena_used + bytes_new > t->arena_cap)
-    return rsf::set_error(RSF_ERR_OVERFLOW, "interner full (max_ids or arena bytes)");
-  hipLaunchKernelGGL(in_insert_kernel, dim3(g), dim3(256), 0, st, buf, off, len, h_s, idx_s, rep, n, *t, rank, aoff,
-                     found);
-  hipLaunchKernelGGL(in_ids_kernel, dim3(g), dim3(256), 0, st, idx_s, rep, found, n, ids);
-  RSF_HIP(hipGetLastError());
-  t->n_ids += (uint32_t)n_new;
-  t->arena_used += bytes_new;
-  return RSF_OK;
+  InternPlan P;
+  P.t = t, P.buf = buf, P.off = off, P.len = len, P.n = n, P.st = (hipStream_t)stream;
+  int rc = intern_plan(P);
+  if (rc) return rc;
+  if (!intern_fits(P)) return rsf::set_error(RSF_ERR_OVERFLOW, "interner full (max_ids or arena bytes)");
+  return intern_commit(P, ids);
 }
 
+// Both interners are planned before either is committed: a batch that would overflow
+// either one fails with neither table changed.
 int rsf_wire_event_keys(rsf_interner* names, rsf_interner* payloads, const uint8_t* buf, const rsf_wire_msg* msgs,
                         uint64_t n, uint64_t* keys, void* stream) {
   if (!names || !payloads || (n && (!buf || !msgs || !keys))) return rsf::set_error(RSF_ERR_ARG, "null argument");
   if (n == 0) return RSF_OK;
   if (n >= 0x7FFFFFFFull) return rsf::set_error(RSF_ERR_ARG, "batch too large");
+  if (names == payloads) return rsf::set_error(RSF_ERR_ARG, "names and payloads need separate interners");
   hipStream_t st = (hipStream_t)stream;
   const size_t n8 = ((size_t)n * 8 + 255) & ~(size_t)255, n4 = ((size_t)n * 4 + 255) & ~(size_t)255;
   Scratch sc(st);
@@ -304,9 +352,14 @@ int rsf_wire_event_keys(rsf_interner* names, rsf_interner* payloads, const uint8
   uint32_t* pid = (uint32_t*)(b + 2 * n8 + 3 * n4);
   hipLaunchKernelGGL(in_wire_kernel, dim3(grid1(n)), dim3(256), 0, st, msgs, n, noff, nlen, poff, plen);
   RSF_HIP(hipGetLastError());
-  int rc = rsf_intern(names, buf, noff, nlen, n, nid, stream);
-  if (rc) return rc;
-  if ((rc = rsf_intern(payloads, buf, poff, plen, n, pid, stream))) return rc;
+  InternPlan pn, pp;
+  pn.t = names, pn.buf = buf, pn.off = noff, pn.len = nlen, pn.n = n, pn.st = st;
+  pp.t = payloads, pp.buf = buf, pp.off = poff, pp.len = plen, pp.n = n, pp.st = st;
+  int rc;
+  if ((rc = intern_plan(pn)) || (rc = intern_plan(pp))) return rc;
+  if (!intern_fits(pn) || !intern_fits(pp))
+    return rsf::set_error(RSF_ERR_OVERFLOW, "interner full (max_ids or arena bytes); neither table changed");
+  if ((rc = intern_commit(pn, nid)) || (rc = intern_commit(pp, pid))) return rc;
   hipLaunchKernelGGL(in_keys_kernel, dim3(grid1(n)), dim3(256), 0, st, msgs, nid, pid, n, keys);
   RSF_HIP(hipGetLastError());
   return RSF_OK;

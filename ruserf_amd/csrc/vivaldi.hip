@@ -964,7 +964,7 @@ __global__ void __launch_bounds__(256) xreq_pack_kernel(const uint32_t* __restri
 }
 __global__ void xreq_header_kernel(uint32_t* __restrict__ req, uint64_t req_words, const uint32_t* __restrict__ cnt,
                                    uint32_t world, uint32_t cap) {
-  const uint32_t w = threadIdx.x;
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w < world) req[(uint64_t)w * req_words] = cnt[w] < cap ? cnt[w] : cap;
 }
 // owner side: the requested rows of this shard, copied in request order into the reply bucket
@@ -1459,7 +1459,7 @@ int rsf_vivaldi_exchange_requests(rsf_vivaldi* v, uint32_t world, const uint32_t
   RSF_HIP(hipMemsetAsync(v->xcnt, 0, 4 * world, v->stream));
   hipLaunchKernelGGL(xreq_pack_kernel, dim3((unsigned)((p.shard_n + 255) / 256)), dim3(256), 0, v->stream, peer, p.lo,
                      p.shard_n, p.shard_n, v->req_send, v->req_words, v->xcap, v->xcnt, v->xflags);
-  hipLaunchKernelGGL(xreq_header_kernel, dim3(1), dim3(64), 0, v->stream, v->req_send, v->req_words,
+  hipLaunchKernelGGL(xreq_header_kernel, dim3((world + 63) / 64), dim3(64), 0, v->stream, v->req_send, v->req_words,
                      (const uint32_t*)v->xcnt, world, v->xcap);
   RSF_HIP(hipGetLastError());
   return RSF_OK;

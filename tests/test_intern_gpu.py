@@ -123,3 +123,28 @@ def test_wire_frames_to_apply_batch_end_to_end():
     L.orc_world_free(C.byref(w))
     tn.close()
     tp.close()
+
+
+def test_wire_event_keys_overflow_changes_neither_table():
+    """rsf_wire_event_keys plans both interners before committing either: when the payloads
+    would overflow, the call fails and the names table is unchanged too."""
+    names = [b"n%d" % i for i in range(4)]
+    payloads = [b"p%03d" % i for i in range(40)]
+    k = 40
+    m = np.zeros(k, K.WIRE_MSG_DTYPE)
+    m["type"] = G.MSG_USER_EVENT
+    blob = b"".join(names + payloads)
+    noff = np.cumsum([0] + [len(x) for x in names])
+    poff = len(b"".join(names)) + np.cumsum([0] + [len(x) for x in payloads])
+    m["a_off"], m["a_len"] = noff[np.arange(k) % 4], 2
+    m["b_off"], m["b_len"] = poff[np.arange(k)], 4
+    buf, off = CO.wire_encode(m, np.frombuffer(blob, np.uint8))
+    dec = K.decode_messages(buf, off)
+    tn, tp = Interner(max_ids=64, arena_bytes=1 << 12), Interner(max_ids=16, arena_bytes=1 << 12)
+    with pytest.raises(EngineError):
+        wire_event_keys(tn, tp, buf, dec)
+    assert tn.count() == (0, 0) and tp.count() == (0, 0)
+    keys = wire_event_keys(tn, Interner(max_ids=64, arena_bytes=1 << 12), buf, dec)
+    assert tn.count() == (4, 8) and len(np.unique(keys)) == k
+    tn.close()
+    tp.close()
