@@ -48,8 +48,8 @@ def _engine(n, rounds_total):
 
 
 def run_churn(args, rank, world):
-    from ruserf_amd.coalesce import USER_EVENT_DTYPE, coalesce_user_events
-    from ruserf_amd.gossip import ACT_USER_EVENT, E_QUEUE_PRUNE
+    from ruserf_amd.coalesce import MEMBER_EVENT_DTYPE, USER_EVENT_DTYPE, MemberEventCoalescer, coalesce_user_events
+    from ruserf_amd.gossip import ACT_USER_EVENT, DELIVERY_MEMBER_EVENT, DELIVERY_USER_EVENT, E_QUEUE_PRUNE
     n = args.members or N_DEFAULT
     timed_rounds = args.warmup + args.steps
     rounds_total = timed_rounds + TAIL
@@ -79,7 +79,10 @@ def run_churn(args, rank, world):
         wall = float(t_[0])
     # ---- delivery pass (untimed), the same rounds with the delivery log
     eng, subj, acts, ml = _engine(n, rounds_total)
-    eng.set_delivery_log(512)
+    eng.set_delivery_log(768)
+    # member events: one MemberEventCoalescer per member over its stream, a quantum per round
+    mcoal = MemberEventCoalescer(n, len(subj))
+    mev_in = mev_out = 0
     dead = np.zeros(n, dtype=bool)
     per_round = []
     for t in range(rounds_total):
@@ -89,7 +92,15 @@ def run_churn(args, rank, world):
                 dead[subj[e["subject"]]] = True
             elif e["set_alive"] == 1:
                 dead[subj[e["subject"]]] = False
-        per_round.append(eng.deliveries())
+        d = eng.deliveries()
+        me = d[d["kind"] == DELIVERY_MEMBER_EVENT]
+        if len(me):
+            mev = np.zeros(len(me), MEMBER_EVENT_DTYPE)
+            mev["group"], mev["node"], mev["type"] = me["member"], me["key"], me["ltime"]
+            mev_in += len(me)
+            mev_out += len(mcoal.flush(mev))
+        per_round.append(d[d["kind"] == DELIVERY_USER_EVENT])
+    mcoal.close()
     st = eng.members()
     pruned = int(eng.pruned().astype(np.uint64).sum())
     err_other = int(np.count_nonzero(st["err"] & ~np.uint32(E_QUEUE_PRUNE)))
@@ -161,6 +172,7 @@ def run_churn(args, rank, world):
                                         "p90": float(np.percentile(lat, 90)) if len(lat) else None,
                                         "max": int(lat.max()) if len(lat) else None},
             "cc_deliveries": int(len(ev)), "after_coalescing": int(coalesced),
+            "member_events": int(mev_in), "member_events_after_coalescing": int(mev_out),
             "queue_pruned_total": pruned, "error_members_other": err_other, "members_by_error_bit": err_bits,
         },
     }

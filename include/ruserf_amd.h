@@ -451,19 +451,36 @@ int rsf_gossip_reap(rsf_gossip* g, uint32_t now, uint32_t reconnect_timeout, uin
                     uint32_t recent_intent_timeout);
 int rsf_gossip_set_now(rsf_gossip* g, uint32_t now);
 
-/* ---- delivery log: the UserEvents handle_user_event sends to the application
- * (event_tx, core/src/serf/base.rs:831-835) -- what a consumer, e.g. the
- * coalesce_loop (core/src/coalesce.rs:66-155), reads.  Each member logs up to
- * per_member deliveries (in delivery order) since the last round_begin: its own
- * originations (Serf::user_event handles the event locally first), then the
- * round's merges; rsf_gossip_apply_batch and push/pull replays append to the
- * current log.  Overflow sets RSF_E_DELIVERY_LOG.  per_member = 0 turns it off. */
+/* ---- delivery log: the events a member's Serf sends to the application on its
+ * event channel (event_tx) -- what a consumer, e.g. the coalesce_loop
+ * (core/src/coalesce.rs:66-155), reads: the UserEvents handle_user_event delivers
+ * (core/src/serf/base.rs:831-835) and the MemberEvents of handle_node_join /
+ * handle_node_leave / handle_node_update, of a leave intent that moves a Failed
+ * member to Left, of handle_prune and of the Reaper (base.rs:1167-1612, 519-601), in
+ * the order the member produced them.  Each member logs up to per_member entries
+ * since the last round_begin: its own memberlist transitions and originations, then
+ * the round's merges; rsf_gossip_apply_batch, push/pull, the Reaper, the Reconnector
+ * and restarts append to the current log.  Overflow sets RSF_E_DELIVERY_LOG.
+ * per_member = 0 turns it off. */
+enum {
+  RSF_DELIVERY_USER_EVENT = 0,
+  RSF_DELIVERY_MEMBER_EVENT = 1
+};
+/* MemberEventType (core/src/event.rs) of a RSF_DELIVERY_MEMBER_EVENT entry */
+enum {
+  RSF_MEMBER_EVENT_JOIN = 0,
+  RSF_MEMBER_EVENT_LEAVE = 1,
+  RSF_MEMBER_EVENT_FAILED = 2,
+  RSF_MEMBER_EVENT_REAP = 3,
+  RSF_MEMBER_EVENT_UPDATE = 4
+};
 typedef struct rsf_delivery {
-  uint64_t ltime;
-  uint64_t key;      /* (name_id << 32) | payload_id, as rsf_action.key */
+  uint64_t ltime;    /* user event: its Lamport time; member event: the RSF_MEMBER_EVENT_* type */
+  uint64_t key;      /* user event: (name_id << 32) | payload_id, as rsf_action.key; member event: the subject slot */
   uint32_t member;
   uint8_t cc;        /* UserEventMessage::cc: the coalescer's handle() (coalesce/user.rs:30-34) */
-  uint8_t _r[3];
+  uint8_t kind;      /* RSF_DELIVERY_USER_EVENT / RSF_DELIVERY_MEMBER_EVENT */
+  uint8_t _r[2];
 } rsf_delivery;
 int rsf_gossip_set_delivery_log(rsf_gossip* g, uint32_t per_member);
 /* The log, member by member (ascending id), each member's deliveries in order, into
@@ -576,6 +593,34 @@ typedef struct rsf_user_event {
  * synchronises the stream. */
 int rsf_coalesce_user_events(const rsf_user_event* in, uint64_t n, rsf_user_event* out, uint64_t* n_out,
                              void* stream);
+
+/* ---- MemberEventCoalescer (core/src/coalesce/member.rs:60-118) for many coalescers at
+ * once.  A coalescer (`group`, e.g. the member whose event stream it reads) keeps
+ * last_events[node] = the type it last flushed for that node (none at first); one
+ * quantum's events are coalesced (latest_events: per node the LAST event in arrival
+ * order wins) and flushed: a node's event is dropped when its type equals the node's
+ * last flushed type, unless the type is Update (a tag update always passes); otherwise
+ * it is sent (with the latest event's member) and becomes the node's last type.  The
+ * reference groups the flushed
+ * members by type in HashMap order (unspecified); here the flushed events come out
+ * sorted by (group, type, node).  Types are RSF_MEMBER_EVENT_*; nodes < n_nodes,
+ * groups < n_groups.  The coalesce_loop's quantum / quiescent timers are the caller's:
+ * a call is one flush over the events of one quantum. */
+typedef struct rsf_member_event {
+  uint32_t group, node, type;
+  uint32_t member;  /* opaque, carried through: the Member the event holds (e.g. an id of its
+                     * tags); the flushed event carries the latest arrival's */
+} rsf_member_event;
+typedef struct rsf_member_coalescer rsf_member_coalescer;
+int rsf_member_coalescer_create(rsf_member_coalescer** out, uint32_t n_groups, uint32_t n_nodes, int device);
+int rsf_member_coalescer_destroy(rsf_member_coalescer* mc);
+/* in / out: device pointers (out holds up to n events); *n_out (host) = events flushed.
+ * An event outside the group / node / type ranges is an RSF_ERR_ARG (nothing is
+ * flushed).  Synchronises the stream. */
+int rsf_member_coalescer_flush(rsf_member_coalescer* mc, const rsf_member_event* in, uint64_t n,
+                               rsf_member_event* out, uint64_t* n_out, void* stream);
+/* the coalescers' last_events table, [n_groups][n_nodes] bytes (0xFF = none), to host */
+int rsf_member_coalescer_dump(rsf_member_coalescer* mc, uint8_t* last_out);
 
 /* ======================================================================== */
 /* Wire codecs                                              */

@@ -562,9 +562,14 @@ static inline void snap_member_event(orc_world* w, uint32_t m, uint32_t ev, uint
   else if (ev == EV_LEAVE || ev == EV_FAILED) *word &= ~(1u << (subj & 31));
 }
 
+static void dlog_put(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key, int cc);
+/* a MemberEvent sent to the application (event_tx): the order-sensitive digest, the
+ * snapshotter, and the delivery log (tagged: ltime word = ORC_LOG_MEMBER | type, key =
+ * subject), so the log is the member's whole event stream in production order */
 static inline void digest_member_event(orc_world* w, uint32_t m, uint32_t ev, uint32_t subj) {
   w->digest[m] = orc_digest_mix(w->digest[m], DIG_MEMBER | ((uint64_t)ev << 32) | subj);
   snap_member_event(w, m, ev, subj);
+  dlog_put(w, m, ORC_LOG_MEMBER | ev, subj, 0);
 }
 
 /* process_user_event / process_query_event (snapshot.rs:663-684): the largest ltime
@@ -2167,4 +2172,44 @@ uint32_t orc_world_reconnect(orc_world* w, uint32_t tick, uint32_t* target) {
     }
   }
   return joins;
+}
+
+/* ---- MemberEventCoalescer  coalesce/member.rs:60-118 -------------------------------- */
+typedef struct {
+  uint64_t key; /* group << 32 | node */
+  uint64_t arrival;
+} mc_item;
+static int mc_cmp(const void* a, const void* b) {
+  const mc_item *x = (const mc_item*)a, *y = (const mc_item*)b;
+  if (x->key != y->key) return x->key < y->key ? -1 : 1;
+  return x->arrival < y->arrival ? -1 : (x->arrival > y->arrival);
+}
+static int mc_out_cmp(const void* a, const void* b) {
+  const orc_mevent *x = (const orc_mevent*)a, *y = (const orc_mevent*)b;
+  if (x->group != y->group) return x->group < y->group ? -1 : 1;
+  if (x->type != y->type) return x->type < y->type ? -1 : 1;
+  return x->node < y->node ? -1 : (x->node > y->node);
+}
+uint64_t orc_member_coalesce(uint8_t* last, uint32_t n_nodes, const orc_mevent* in, uint64_t n, orc_mevent* out) {
+  if (!n) return 0;
+  mc_item* it = (mc_item*)malloc(n * sizeof(mc_item));
+  if (!it) return 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    it[i].key = ((uint64_t)in[i].group << 32) | in[i].node;
+    it[i].arrival = i;
+  }
+  qsort(it, n, sizeof(mc_item), mc_cmp);
+  uint64_t k = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (i + 1 < n && it[i + 1].key == it[i].key) continue; /* latest_events.insert: the last one stays */
+    const orc_mevent* e = &in[it[i].arrival];
+    uint8_t* lp = last + (size_t)e->group * n_nodes + e->node;
+    /* Some(&previous) if previous == cev.ty && cev.ty != Update => continue */
+    if (*lp == e->type && e->type != 4u) continue;
+    *lp = (uint8_t)e->type; /* self.last_events.insert(id, cev.ty) */
+    out[k++] = *e; /* the latest CoalesceEvent's member */
+  }
+  free(it);
+  qsort(out, k, sizeof(orc_mevent), mc_out_cmp);
+  return k;
 }

@@ -268,6 +268,10 @@ int orc_handle_node_update(orc_world* w, uint32_t m, uint32_t subj);
 int orc_handle_user_event(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key);
 /* the same with the message's cc flag, which only the delivery log records */
 int orc_handle_user_event_cc(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key, int cc);
+/* Delivery log: per member up to per_member entries per round of its event stream in
+ * production order, 3 u64 each: user events (ltime, key, cc); member events
+ * (ORC_LOG_MEMBER | MemberEventType, subject, 0) */
+#define ORC_LOG_MEMBER (1ull << 62)
 int orc_world_set_delivery_log(orc_world* w, uint32_t per_member);
 int orc_handle_query(orc_world* w, uint32_t m, uint64_t ltime, uint32_t id, int no_broadcast);
 int orc_upsert_intent(orc_world* w, uint32_t m, uint32_t subj, uint8_t kind, uint64_t ltime);
@@ -480,6 +484,17 @@ uint32_t orc_world_reconnect(orc_world* w, uint32_t tick, uint32_t* target);
 /* the Reconnector's throttle probability given members.states.len(), the failed and left
  * counts (base.rs:670-671) */
 float orc_reconnect_prob(uint64_t states, uint64_t failed, uint64_t left);
+
+/* MemberEventCoalescer (coalesce/member.rs:60-118), one per group.  last: the groups'
+ * last_events tables [n_groups][n_nodes] (0xFF = none), updated.  coalesce() of the n events
+ * in arrival order (latest_events.insert: the last event per (group, node) wins), then
+ * flush(): skip a node whose type equals its last flushed type unless it is Update (4),
+ * else record the type and send the member.  The flushed events go to out sorted by
+ * (group, type, node) (the reference's HashMap order is unspecified); returns their count. */
+typedef struct orc_mevent {
+  uint32_t group, node, type, member; /* member: opaque, carried through (the Member clone) */
+} orc_mevent;
+uint64_t orc_member_coalesce(uint8_t* last, uint32_t n_nodes, const orc_mevent* in, uint64_t n, orc_mevent* out);
 
 #ifdef __cplusplus
 }

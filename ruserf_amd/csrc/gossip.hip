@@ -683,10 +683,15 @@ __global__ void __launch_bounds__(256) ml_kernel(GCfg c, GState s, const rsf_ml_
       if (ml[e].kind == RSF_ML_JOIN) {
         h_node_join(v, r, subj);
         snap_member(c, s, l, subj, true);
+        mlog_put(c, s, l, r.err, kEvJoin, subj);
       } else if (ml[e].kind == RSF_ML_UPDATE) {
-        h_node_update(v, r, subj);
-      } else if (h_node_leave(v, r, subj, c.now) & RSF_F_MEMBER_EVENT) {
-        snap_member(c, s, l, subj, false);
+        if (h_node_update(v, r, subj)) mlog_put(c, s, l, r.err, kEvUpdate, subj);
+      } else {
+        const int f = h_node_leave(v, r, subj, c.now);
+        if (f & RSF_F_MEMBER_EVENT) {
+          snap_member(c, s, l, subj, false);
+          mlog_put(c, s, l, r.err, (uint32_t)f >> kFEvShift, subj);
+        }
       }
       touched = true;
     }
@@ -789,7 +794,7 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
       }
       r.clock++;
       uint32_t subj = (uint32_t)r.subj;
-      h_leave_intent(s.view + l * c.S + subj, r, subj, lt, false, ref, c.now);
+      mlog_intent(c, s, l, r.err, h_leave_intent(s.view + l * c.S + subj, r, subj, lt, false, ref, c.now), subj);
       uint32_t len = msg_len(RSF_MSG_LEAVE, lt, 0, 0);
       put_rumor(c, s, rid, RSF_MSG_LEAVE, 0, subj, lt, 0, len);
       pend_push_serial(c, s, l, kQIntent, rid, subj, len, r);
@@ -799,6 +804,7 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
       uint64_t lt = r.clock;
       bool prune = x.flags & 1;
       int f = h_leave_intent(s.view + l * c.S + x.subject, r, x.subject, lt, prune, ref, c.now);
+      mlog_intent(c, s, l, r.err, f, x.subject);
       if (f & RSF_F_REFUTE) push_refute(c, s, r, ref);
       uint32_t len = msg_len(RSF_MSG_LEAVE, lt, 0, 0);
       put_rumor(c, s, rid, RSF_MSG_LEAVE, prune ? 1 : 0, x.subject, lt, 0, len);
@@ -1513,6 +1519,11 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
         if (fi & RSF_F_MEMBER_EVENT) r.digest = digest_mix(r.digest, shfl_u64(contrib, i));
         if (fi & RSF_F_PRUNE)  // handle_prune's Reap event, after the Leave event of a Failed member
           r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)kEvReap << 32) | shfl_u32(ru.subject, i));
+        if (c.dcap && (fi & (RSF_F_MEMBER_EVENT | RSF_F_PRUNE))) {
+          const uint32_t sj = shfl_u32(ru.subject, i);
+          if (lane == 0) mlog_intent(c, s, l, r.err, fi, sj);
+          r.err = shfl_u32(r.err, 0);
+        }
         if (fi & RSF_F_REFUTE) {
           const uint64_t rf = shfl_u64(ref, i);
           if (lane == 0) push_refute(c, s, r, rf);
@@ -1712,8 +1723,11 @@ __global__ void __launch_bounds__(256) pp_merge_kernel(GCfg c, GState s, const r
       const int i = __ffsll((long long)mm) - 1;
       mm &= mm - 1;
       const uint32_t fi = shfl_u32((uint32_t)f, i);
-      if (fi & RSF_F_MEMBER_EVENT)
+      if (fi & RSF_F_MEMBER_EVENT) {
         r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)kEvLeave << 32) | (base + (uint32_t)i));
+        if (lane == 0) mlog_put(c, s, l, r.err, kEvLeave, base + (uint32_t)i);
+        r.err = shfl_u32(r.err, 0);
+      }
       if (fi & RSF_F_REFUTE) {
         const uint64_t rf = shfl_u64(ref, i);
         if (lane == 0) push_refute(c, s, r, rf);
@@ -1807,6 +1821,7 @@ __global__ void __launch_bounds__(256) reap_kernel(GCfg c, GState s, uint32_t no
   ViewE* vrow = s.view + l * c.S;
   uint64_t dig = s.digest[l];
   const uint64_t d0 = dig;
+  uint32_t lerr = 0;  // delivery-log overflow
   bool any_left = false;
   for (int pass = 0; pass < 2; ++pass) {
     if (pass == 1 && !any_left) break;
@@ -1827,10 +1842,12 @@ __global__ void __launch_bounds__(256) reap_kernel(GCfg c, GState s, uint32_t no
         const int i = __ffsll((long long)mm) - 1;
         mm &= mm - 1;
         dig = digest_mix(dig, kDigMember | ((uint64_t)kEvReap << 32) | (base + (uint32_t)i));
+        if (lane == 0) mlog_put(c, s, l, lerr, kEvReap, base + (uint32_t)i);
       }
     }
   }
   if (lane == 0 && dig != d0) s.digest[l] = dig;
+  if (lane == 0 && lerr) s.err[l] |= lerr;
 }
 
 // direct-handler batch: one thread per receiver segment (array order within a receiver)
@@ -1853,7 +1870,10 @@ __global__ void __launch_bounds__(256) apply_kernel(GCfg c, GState s, const rsf_
     int f = 0;
     switch (x.type) {
       case RSF_MSG_JOIN: f = h_join_intent(vrow + x.subject, r, x.ltime, c.now); break;
-      case RSF_MSG_LEAVE: f = h_leave_intent(vrow + x.subject, r, x.subject, x.ltime, x.flags & 1, ref, c.now); break;
+      case RSF_MSG_LEAVE:
+        f = h_leave_intent(vrow + x.subject, r, x.subject, x.ltime, x.flags & 1, ref, c.now);
+        mlog_intent(c, s, l, r.err, f, x.subject);
+        break;
       case RSF_MSG_USER_EVENT: f = h_user_event(c, s, l, r, x.ltime, x.key, x.flags & 1); break;
       case RSF_MSG_QUERY: f = h_query(c, s, l, r, x.ltime, (uint32_t)x.key, x.flags & 1); break;
       default: f = 0; break;
@@ -3266,11 +3286,13 @@ int rsf_gossip_dump_deliveries(rsf_gossip* g, rsf_delivery* out, uint64_t cap, u
       const uint4 e = log[l * c.dcap + k];
       const uint64_t lt = ((uint64_t)e.y << 32) | e.x;
       rsf_delivery& d = out[o++];
-      d.ltime = lt & ~(1ull << 63);
+      const bool mev = (lt & kLogMemberTag) != 0;
+      d.ltime = lt & ~((1ull << 63) | kLogMemberTag);
       d.key = ((uint64_t)e.w << 32) | e.z;
       d.member = (uint32_t)(c.lo + l);
       d.cc = (uint8_t)(lt >> 63);
-      d._r[0] = d._r[1] = d._r[2] = 0;
+      d.kind = mev ? RSF_DELIVERY_MEMBER_EVENT : RSF_DELIVERY_USER_EVENT;
+      d._r[0] = d._r[1] = 0;
     }
   *n_out = o;
   return RSF_OK;
@@ -3651,6 +3673,7 @@ __global__ void __launch_bounds__(256) snap_restart_kernel(GCfg c, GState s, con
       if ((int32_t)j != r.subj && s.alive[s.subj_member[j]]) {
         h_node_join(s.view + l * c.S + j, r, j);
         snap_member(c, s, l, j, true);
+        mlog_put(c, s, l, r.err, kEvJoin, j);
       }
   store_regs(s, l, r);
   res[i] = joined ? 1 : 0;
@@ -3714,6 +3737,7 @@ __global__ void __launch_bounds__(256) reconnect_kernel(GCfg c, GState s, uint32
   load_regs(s, l, r);
   h_node_join(s.view + l * c.S + tj, r, tj);
   snap_member(c, s, l, tj, true);
+  mlog_put(c, s, l, r.err, kEvJoin, tj);
   store_regs(s, l, r);
 }
 

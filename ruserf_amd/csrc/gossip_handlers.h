@@ -16,6 +16,7 @@ constexpr uint64_t kDigUser = 0x1000000000000000ull;
 constexpr uint64_t kDigQuery = 0x2000000000000000ull;
 constexpr uint64_t kDigMember = 0x3000000000000000ull;
 enum : uint32_t { kEvJoin = 0, kEvLeave = 1, kEvFailed = 2, kEvReap = 3, kEvUpdate = 4 };
+constexpr uint32_t kFEvShift = 8;  // h_node_leave: its MemberEventType in bits 8..10 of the result
 enum : uint32_t { kQIntent = 0, kQQuery = 1, kQEvent = 2 };
 enum : uint32_t {
   kErrEvSlot = RSF_E_EVSLOT,
@@ -305,7 +306,7 @@ __device__ __forceinline__ int h_node_leave(ViewE* e, MRegs& r, uint32_t subj, u
   v.t = now;  // leave_time = now (base.rs:1355, 1364)
   *e = v;
   r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)ev << 32) | subj);
-  return RSF_F_MEMBER_EVENT;
+  return RSF_F_MEMBER_EVENT | (int)(ev << kFEvShift);  // the event type rides above the flags (internal)
 }
 
 // the snapshotter's process_user_event / process_query_event (snapshot.rs:663-684): the
@@ -324,17 +325,37 @@ __device__ __forceinline__ void snap_member(const GCfg& c, const GState& s, uint
 }
 
 // one delivery (event_tx.send of a UserEvent, base.rs:831-835) into the member's log slot
+__device__ __forceinline__ void dlog_put_raw(const GCfg& c, const GState& s, uint64_t l, uint32_t& err, uint64_t lt,
+                                             uint64_t key) {
+  const uint32_t k = s.dcnt[l];
+  if (k < c.dcap) {
+    s.dlog[l * c.dcap + k] = make_uint4((uint32_t)lt, (uint32_t)(lt >> 32), (uint32_t)key, (uint32_t)(key >> 32));
+  } else {
+    err |= kErrDlog;
+  }
+  s.dcnt[l] = k + 1;
+}
 __device__ __forceinline__ void dlog_put(const GCfg& c, const GState& s, uint64_t l, MRegs& r, uint64_t L,
                                          uint64_t key, bool cc) {
   if (!c.dcap) return;
-  const uint32_t k = s.dcnt[l];
-  if (k < c.dcap) {
-    const uint64_t lt = L | (cc ? (1ull << 63) : 0ull);
-    s.dlog[l * c.dcap + k] = make_uint4((uint32_t)lt, (uint32_t)(lt >> 32), (uint32_t)key, (uint32_t)(key >> 32));
-  } else {
-    r.err |= kErrDlog;
-  }
-  s.dcnt[l] = k + 1;
+  dlog_put_raw(c, s, l, r.err, L | (cc ? (1ull << 63) : 0ull), key);
+}
+// a MemberEvent (event_tx.send of a MemberEvent: handle_node_join / leave / update, the
+// Failed -> Left leave intent, handle_prune, the Reaper) into the same log, so the
+// application's stream keeps member and user events in the order they were produced;
+// bit 62 of the time word tags it (a Lamport time never reaches 2^62), the key is the subject
+constexpr uint64_t kLogMemberTag = 1ull << 62;
+__device__ __forceinline__ void mlog_put(const GCfg& c, const GState& s, uint64_t l, uint32_t& err, uint32_t ev,
+                                         uint32_t subj) {
+  if (!c.dcap) return;
+  dlog_put_raw(c, s, l, err, kLogMemberTag | ev, subj);
+}
+// the member events of an intent handler's result: Failed -> Left (Leave), then handle_prune (Reap)
+__device__ __forceinline__ void mlog_intent(const GCfg& c, const GState& s, uint64_t l, uint32_t& err, int f,
+                                            uint32_t subj) {
+  if (!c.dcap) return;
+  if (f & RSF_F_MEMBER_EVENT) mlog_put(c, s, l, err, kEvLeave, subj);
+  if (f & RSF_F_PRUNE) mlog_put(c, s, l, err, kEvReap, subj);
 }
 
 // handle_user_event (base.rs:770-837); cc = the message's coalesce flag (delivery log only)

@@ -49,7 +49,10 @@ MSG_DTYPE = np.dtype([("receiver", "<u4"), ("subject", "<u4"), ("ltime", "<u8"),
 RUMOR_DTYPE = np.dtype([("ltime", "<u8"), ("key", "<u8"), ("subject", "<u4"), ("type", "u1"), ("flags", "u1"),
                         ("msg_len", "<u2")])
 PP_PAIR_DTYPE = np.dtype([("receiver", "<u4"), ("sender", "<u4")])
-DELIVERY_DTYPE = np.dtype([("ltime", "<u8"), ("key", "<u8"), ("member", "<u4"), ("cc", "u1"), ("_r", "u1", 3)])
+# kind: DELIVERY_USER_EVENT (ltime, key) or DELIVERY_MEMBER_EVENT (ltime = MemberEventType, key = subject)
+DELIVERY_DTYPE = np.dtype([("ltime", "<u8"), ("key", "<u8"), ("member", "<u4"), ("cc", "u1"), ("kind", "u1"),
+                           ("_r", "u1", 2)])
+DELIVERY_USER_EVENT, DELIVERY_MEMBER_EVENT = 0, 1
 assert ACTION_DTYPE.itemsize == 32 and ML_DTYPE.itemsize == 16 and MSG_DTYPE.itemsize == 32
 assert RUMOR_DTYPE.itemsize == 24 and DELIVERY_DTYPE.itemsize == 24
 

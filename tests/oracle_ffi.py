@@ -115,6 +115,13 @@ class _UEvent(C.Structure):
 
 UEvent = _UEvent
 
+
+class MEvent(C.Structure):
+    _fields_ = [("group", C.c_uint32), ("node", C.c_uint32), ("type", C.c_uint32), ("member", C.c_uint32)]
+
+
+LOG_MEMBER = 1 << 62  # delivery-log tag of a member event (oracle.h ORC_LOG_MEMBER)
+
 # enums (oracle.h)
 OK, ERR_DIM, ERR_COORD, ERR_RTT = 0, 1, 2, 3
 ST_NONE, ST_ALIVE, ST_LEAVING, ST_LEFT, ST_FAILED = 0, 1, 2, 3, 4
@@ -228,6 +235,9 @@ def lib():
     L.orc_wire_decode.argtypes = [P8, C.c_uint64, C.c_uint64, C.c_void_p]
     L.orc_coalesce_user_events.argtypes = [C.POINTER(UEvent), C.c_uint32, C.POINTER(UEvent)]
     L.orc_coalesce_user_events.restype = C.c_uint32
+    L.orc_member_coalesce.argtypes = [C.POINTER(C.c_uint8), C.c_uint32, C.POINTER(MEvent), C.c_uint64,
+                                      C.POINTER(MEvent)]
+    L.orc_member_coalesce.restype = C.c_uint64
     L.orc_swim_init.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, P32, P32, P8, P32,
                                 C.c_uint32]
     L.orc_swim_free.argtypes = [C.c_void_p]
@@ -370,3 +380,16 @@ def arr(ptr, n, dtype):
 
 def ptr(a, ctype):
     return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def member_coalesce(last, events):
+    """oracle MemberEventCoalescer flush over (group, node, type, member) rows; last: the
+    [n_groups][n_nodes] u8 table, updated in place -> flushed rows (numpy structured)"""
+    from ruserf_amd.coalesce import MEMBER_EVENT_DTYPE
+    ev = np.ascontiguousarray(events, dtype=MEMBER_EVENT_DTYPE)
+    n = len(ev)
+    out = np.zeros(max(1, n), MEMBER_EVENT_DTYPE)
+    assert last.flags.c_contiguous and last.dtype == np.uint8
+    k = lib().orc_member_coalesce(last.ctypes.data_as(C.POINTER(C.c_uint8)), last.shape[1],
+                                  ev.ctypes.data_as(C.POINTER(MEvent)), n, out.ctypes.data_as(C.POINTER(MEvent)))
+    return out[:k].copy()

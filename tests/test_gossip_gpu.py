@@ -405,14 +405,17 @@ def _threads():
 
 
 def _oracle_deliveries(w):
-    """the oracle's delivery log as (member, ltime, key, cc) rows, member-major"""
+    """the oracle's delivery log as (member, ltime, key, cc, kind) rows, member-major (a member
+    event's ltime word is LOG_MEMBER | type: kind 1, ltime = the type)"""
     n, cap = w.n, w.dcap
     cnt = np.minimum(O.arr(w.dcnt, n, np.uint32), cap)
     log = O.arr(w.dlog, n * cap * 3, np.uint64).reshape(n, cap, 3)
     mask = np.arange(cap)[None, :] < cnt[:, None]
     mem = np.broadcast_to(np.arange(n, dtype=np.uint32)[:, None], (n, cap))[mask]
     e = log[mask]
-    return mem, e[:, 0], e[:, 1], e[:, 2].astype(np.uint8)
+    kind = ((e[:, 0] & np.uint64(O.LOG_MEMBER)) != 0).astype(np.uint8)
+    lt = e[:, 0] & ~np.uint64(O.LOG_MEMBER)
+    return mem, lt, e[:, 1], e[:, 2].astype(np.uint8), kind
 
 
 def test_configs3_100k_churn_flood_coalesce():
@@ -420,22 +423,28 @@ def test_configs3_100k_churn_flood_coalesce():
     leave, a quarter of the failures force-left with prune), a flood of 100 user events
     (16 names, 32-B payloads, cc 50%) + 10 queries per round, event/query buffers 512,
     retransmit mult 4.  Bit-exact against the oracle every round (clocks, digests of
-    every delivery, error bits, queue drops, the delivery log); the full state at the
-    end.  Each member's cc deliveries then go through the GPU UserEventCoalescer
-    (coalesce/user.rs:52-97) with one coalescer per member, checked against the
-    oracle's coalescer on a sample of members."""
-    from ruserf_amd.coalesce import USER_EVENT_DTYPE, coalesce_user_events
+    every delivery, error bits, queue drops, the delivery log of user and member events);
+    the full state at the end.  Each member's member events go through the GPU
+    MemberEventCoalescer (coalesce/member.rs:60-118), one per member, a quantum per round,
+    bit-exact against the oracle's; each member's cc deliveries then go through the GPU
+    UserEventCoalescer (coalesce/user.rs:52-97), checked against the oracle's coalescer on
+    a sample of members."""
+    from ruserf_amd.coalesce import MEMBER_EVENT_DTYPE, NO_EVENT, USER_EVENT_DTYPE, MemberEventCoalescer, \
+        coalesce_user_events
     n, rounds = 100_000, 9
     subj, acts, ml = W.churn_workload(n, rounds, events_per_round=100, queries_per_round=10, seed=2024)
     s = len(subj)
     cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=64, gossip_limit=1400, max_rumors=1 << 16,
                          event_buffer_size=512, query_buffer_size=512, slot_k=16)
     g, w = pair(cfg, subj, W.initial_views(s))
-    dcap = 256
+    dcap = 512
     g.set_delivery_log(dcap)
     assert L.orc_world_set_delivery_log(C.byref(w), dcap) == 0
     th = _threads()
     logs = []
+    mcoal = MemberEventCoalescer(n, s)
+    mlast = np.full((n, s), NO_EVENT, np.uint8)
+    n_mev = n_mflushed = 0
     for t in range(rounds):
         g.round(t, ml[t], acts[t])
         H.oracle_round(w, t, ml[t], acts[t], threads=th)
@@ -446,13 +455,24 @@ def test_configs3_100k_churn_flood_coalesce():
             assert np.array_equal(m[k], exp), (t, k)
         assert np.array_equal(g.pruned(), O.arr(w.q_pruned, n, np.uint32)), t
         d = g.deliveries()
-        om, ol, ok_, oc = _oracle_deliveries(w)
+        om, ol, ok_, oc, okind = _oracle_deliveries(w)
         assert np.array_equal(d["member"], om) and np.array_equal(d["ltime"], ol), t
         assert np.array_equal(d["key"], ok_) and np.array_equal(d["cc"], oc), t
-        logs.append(d)
+        assert np.array_equal(d["kind"], okind), t
+        me = d[d["kind"] == G.DELIVERY_MEMBER_EVENT]
+        mev = np.zeros(len(me), MEMBER_EVENT_DTYPE)
+        mev["group"], mev["node"], mev["type"] = me["member"], me["key"], me["ltime"]
+        got_m = mcoal.flush(mev)
+        assert np.array_equal(got_m, O.member_coalesce(mlast, mev)), t
+        n_mev += len(mev)
+        n_mflushed += len(got_m)
+        logs.append(d[d["kind"] == G.DELIVERY_USER_EVENT])
     H.assert_same(H.engine_state(g), H.world_state(w), "final")
     st = H.engine_state(g)
     assert np.any(st["v_status"] == G.STATUS_LEFT) and np.any(st["v_kind"] == G.KIND_UNKNOWN)
+    assert 0 < n_mflushed < n_mev  # member events were produced and some coalesced away
+    assert np.array_equal(mcoal.last_events(), mlast)
+    mcoal.close()
     # coalescing of the cc deliveries, one coalescer per member (stable by member: arrival order kept)
     d = np.concatenate(logs)
     d = d[d["cc"] == 1]
