@@ -238,6 +238,41 @@ def cpu_baseline_vivaldi(seconds_target=8.0):
                       f"{cpu_info()}"}
 
 
+def c1_leg(rounds=1000, n=1000, with_gpu=True):
+    """BASELINE configs[0] / SURVEY §8(d) C1: Vivaldi over a 1k-node synthetic RTT matrix on
+    the CPU path -- the oracle (the C restatement of CoordinateClient::update; the Rust
+    reference cannot be built here) on one thread: n clients, each probing one of its 16
+    fixed neighbours per round (peer coordinates from the previous round), `rounds` rounds
+    = n x rounds updates.  Reports updates/s and the final median |est - true| / true over
+    all pairs.  with_gpu: the same rounds on the HIP engine, bit-exact against it."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O  # test infrastructure: the C1 CPU path and its checker
+    L = O.lib()
+    p = O.VivaldiPop()
+    oo = O.default_opts()
+    L.orc_vivaldi_pop_init(C.byref(p), n, 16, C.byref(oo), SEED)
+    t = time.perf_counter()
+    L.orc_vivaldi_pop_rounds(C.byref(p), 0, rounds, 1)
+    spent = time.perf_counter() - t
+    med = L.orc_vivaldi_pop_median_rel_error(C.byref(p))
+    out = {"config": f"BASELINE configs[0]: {n} Vivaldi clients, D=8, default CoordinateOptions, 16 neighbours "
+                     f"each probed one per round with x(1+U[0,0.1)) jitter, {rounds} rounds = {n * rounds} updates",
+           "cpu_updates_per_s": n * rounds / spent, "cpu_seconds": spent, "cores": 1, "kind": "port",
+           "cpu_model": cpu_info(), "median_rel_rtt_error_all_pairs": med, "resets": int(p.resets)}
+    if with_gpu:
+        from ruserf_amd import CoordinateClients, CoordinateOptions
+        g = CoordinateClients(n, 16, CoordinateOptions(), seed=SEED, device=torch.cuda.current_device())
+        g.set_stream(torch.cuda.current_stream().cuda_stream)
+        for r in range(rounds):
+            g.round(r)
+        torch.cuda.synchronize()
+        exp = O.arr(p.rows_cur, n * p.row_stride, np.float64).reshape(n, p.row_stride)
+        out["gpu_bit_exact"] = bool(np.array_equal(g.get_rows().view(np.uint64), exp.view(np.uint64)))
+        g.close()
+    L.orc_vivaldi_pop_free(C.byref(p))
+    return out
+
+
 # --------------------------------------------------------------------------- traffic
 def attach_traffic(workload, res):
     """roofline.traffic = HBM bytes per launch of the dominant kernel from the rocprofv3
@@ -318,6 +353,7 @@ def main():
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline_vivaldi()
+            res["configs0_c1"] = c1_leg()
     elif workload == "churn":
         from bench_churn import cpu_baseline_churn, run_churn
         res = run_churn(args, rank, world)
@@ -353,6 +389,8 @@ def main():
                               "steps": args.steps, "warmup": args.warmup, "ms_per_step": vres["ms_per_step"],
                               "scaling": vres["scaling"], "dtype": vres["dtype"], "config": vres["config"],
                               "roofline": vres["roofline"], "cpu_baseline": vcpu}
+            if rank == 0 and world == 1 and not args.no_cpu_baseline:
+                res["vivaldi"]["configs0_c1"] = c1_leg()
     if workload != "gossip":
         attach_traffic(workload, res)
     if rank == 0:

@@ -2213,3 +2213,39 @@ uint64_t orc_member_coalesce(uint8_t* last, uint32_t n_nodes, const orc_mevent* 
   qsort(out, k, sizeof(orc_mevent), mc_out_cmp);
   return k;
 }
+
+/* ---- C1 accuracy: median relative error of estimate_rtt over all pairs ------------ */
+static int dbl_cmp(const void* a, const void* b) {
+  const double x = *(const double*)a, y = *(const double*)b;
+  return x < y ? -1 : (x > y);
+}
+double orc_vivaldi_pop_median_rel_error(const orc_vivaldi_pop* p) {
+  const uint32_t n = p->n, dim = p->opts.dimensionality, st = p->row_stride;
+  if (n < 2) return 0.0;
+  double *x = (double*)malloc(n * sizeof(double)), *y = (double*)malloc(n * sizeof(double)),
+         *h = (double*)malloc(n * sizeof(double));
+  const uint64_t pairs = (uint64_t)n * (n - 1) / 2;
+  double* rel = (double*)malloc(pairs * sizeof(double));
+  if (!x || !y || !h || !rel) {
+    free(x), free(y), free(h), free(rel);
+    return -1.0;
+  }
+  for (uint32_t i = 0; i < n; ++i) orc_true_position(p->seed, i, &x[i], &y[i], &h[i]);
+  uint64_t k = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    orc_coord a;
+    row_to_coord(p->rows_cur + (size_t)i * st, dim, &a);
+    for (uint32_t j = i + 1; j < n; ++j) {
+      orc_coord b;
+      row_to_coord(p->rows_cur + (size_t)j * st, dim, &b);
+      const double dx = x[i] - x[j], dy = y[i] - y[j];
+      const double tr = (double)sat_u64((sqrt(dx * dx + dy * dy) + h[i] + h[j]) * 1.0e9);
+      const double est = (double)orc_coord_distance_ns(&a, &b);
+      rel[k++] = fabs(est - tr) / tr;
+    }
+  }
+  qsort(rel, k, sizeof(double), dbl_cmp);
+  const double med = (k & 1) ? rel[k / 2] : 0.5 * (rel[k / 2 - 1] + rel[k / 2]);
+  free(x), free(y), free(h), free(rel);
+  return med;
+}

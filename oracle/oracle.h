@@ -150,6 +150,10 @@ void orc_true_position(uint64_t seed, uint32_t m, double* x, double* y, double* 
  * Every member probes once per round; peers are read from the previous-round table. */
 int orc_vivaldi_pop_rounds(orc_vivaldi_pop* p, uint32_t round0, uint32_t rounds, int nthreads);
 void orc_gen_neighbors(uint64_t seed, uint32_t n, uint32_t peers, uint32_t* nbr);
+/* SURVEY §8(d) C1's accuracy figure over the population's current coordinates: the median
+ * over all pairs i < j of |est - true| / true, est = distance_to (ns, coordinate.rs:630-644),
+ * true = the synthetic network's noiseless rtt |x_i - x_j| + h_i + h_j in ns */
+double orc_vivaldi_pop_median_rel_error(const orc_vivaldi_pop* p);
 
 /* ---- Lamport clock (types/src/clock.rs:142-182) ------------------------- */
 static inline void orc_clock_witness(uint64_t* clock, uint64_t t) {

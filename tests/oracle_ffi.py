@@ -175,6 +175,8 @@ def lib():
                                        C.POINTER(CoordOpts), C.c_uint64]
     L.orc_vivaldi_pop_free.argtypes = [C.POINTER(VivaldiPop)]
     L.orc_vivaldi_pop_rounds.argtypes = [C.POINTER(VivaldiPop), C.c_uint32, C.c_uint32, C.c_int]
+    L.orc_vivaldi_pop_median_rel_error.argtypes = [C.POINTER(VivaldiPop)]
+    L.orc_vivaldi_pop_median_rel_error.restype = C.c_double
     L.orc_vivaldi_probe.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, P32, C.c_uint32, C.c_uint32,
                                     P32, P64]
     L.orc_true_position.argtypes = [C.c_uint64, C.c_uint32, C.POINTER(C.c_double),

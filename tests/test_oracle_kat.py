@@ -501,3 +501,13 @@ def test_serf_reap_handler(kats):
     assert kept == k["expect_intents_kept"]
     assert w.digest[0] != d0  # one Reap member event was emitted
     L.orc_world_free(C.byref(w))
+
+
+def test_configs0_c1_converges_on_cpu():
+    """BASELINE configs[0] on the CPU path: 1000 clients x 1000 rounds of the
+    oracle's CoordinateClient::update over the synthetic 1k-node RTT matrix; the final median
+    |estimate_rtt - true| / true over all pairs is small (~5%), and no coordinate reset."""
+    import bench
+    r = bench.c1_leg(with_gpu=False)
+    assert r["median_rel_rtt_error_all_pairs"] < 0.1
+    assert r["resets"] == 0 and r["cpu_updates_per_s"] > 0

@@ -392,3 +392,11 @@ def test_64m_population_properties_and_sampled_parity():
         L.orc_client_free(C.byref(c))
     g.close()
     h.close()
+
+
+def test_configs0_c1_gpu_matches_cpu_path():
+    """configs[0]'s 1k-node run (bench.c1_leg, 300 rounds): the HIP engine's coordinates are
+    bit-identical to the CPU path's after every update."""
+    import bench
+    r = bench.c1_leg(rounds=300)
+    assert r["gpu_bit_exact"] and r["median_rel_rtt_error_all_pairs"] < 0.2
