@@ -256,7 +256,7 @@ typedef struct rsf_gossip_cfg {
   uint64_t n_members;          /* N (global) */
   uint64_t shard_lo, shard_hi; /* members owned by this context */
   uint32_t n_subjects;         /* S */
-  uint32_t queue_cap;          /* slots per transmit-limited queue, 1..64 */
+  uint32_t queue_cap;          /* slots per transmit-limited queue, 1..256 (65..256: four slots per lane) */
   uint32_t event_buffer_size;  /* Options::event_buffer_size (default 512) */
   uint32_t query_buffer_size;  /* Options::query_buffer_size (default 512) */
   uint32_t slot_k;             /* events / query ids kept per dedup slot, 1..64 (the reference's

@@ -582,7 +582,7 @@ static inline void snap_clock(orc_world* w, uint32_t m, int which, uint64_t ltim
 
 int orc_world_init(orc_world* w, const orc_world_cfg* c) {
   memset(w, 0, sizeof(*w));
-  if (c->n < 2 || c->s == 0 || c->s > c->n || c->qcap == 0 || c->qcap > 64 || c->ebuf == 0 ||
+  if (c->n < 2 || c->s == 0 || c->s > c->n || c->qcap == 0 || c->qcap > 256 || c->ebuf == 0 ||
       c->qbuf == 0 || c->slot_k == 0 || c->fanout == 0 || c->fanout >= c->n || c->max_refute == 0 ||
       c->cap_rumors == 0 || (c->cap_rumors & (c->cap_rumors - 1)) || c->cap_rumors > (1u << 30))
     return -1;

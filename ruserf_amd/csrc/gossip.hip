@@ -650,15 +650,26 @@ __device__ __forceinline__ uint32_t pend_flush_wave(const GCfg& c, const GState&
   return drops;
 }
 
+#include "gossip_queue4.h"
+
+// a member's pending list applied to queues of either layout (qcap <= 64: one slot per
+// lane; up to 256: four, gossip_queue4.h); `row` is a QLds4 (which holds a QLds)
+__device__ __forceinline__ uint32_t pend_flush_any(const GCfg& c, const GState& s, uint64_t l, uint32_t lane,
+                                                   uint32_t pc, QLds4& row) {
+  if (c.qcap > kWave) return q4_pend_flush_wave(c, s, l, lane, pc, row);
+  return pend_flush_wave(c, s, l, lane, pc, *reinterpret_cast<QLds*>(&row));
+}
+static_assert(sizeof(QLds4) >= sizeof(QLds), "a QLds4 row holds a QLds");
+
 // every member's pending re-queues applied (before anything but emission reads the queues)
 __global__ void __launch_bounds__(256) pend_flush_kernel(GCfg c, GState s) {
-  __shared__ QLds rows[kWavesPerBlock];
+  __shared__ QLds4 rows[kWavesPerBlock];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   if (l >= c.n_loc) return;
   const uint32_t pc = s.p_cnt[l];
   if (!pc) return;
-  if (pend_flush_wave(c, s, l, lane, pc, rows[threadIdx.x / kWave]) && lane == 0) s.err[l] |= kErrQueue;
+  if (pend_flush_any(c, s, l, lane, pc, rows[threadIdx.x / kWave]) && lane == 0) s.err[l] |= kErrQueue;
 }
 
 // ---------------------------------------------------------------- kernels
@@ -1088,6 +1099,116 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   if (lane == 0) { EPROF_ADD(6, 0, 1); }
 }
 
+// emission for queues of 65..256 slots (gossip_queue4.h): emit_run's steps with four slots
+// per lane; no prefetch of the next sender and no deferred re-rank
+template <bool BKT>
+__device__ __forceinline__ void emit_run4(const GCfg& c, const GState& s, const uint32_t* __restrict__ grp_key,
+                                          const uint32_t* __restrict__ slot, uint64_t l, uint32_t lane,
+                                          uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val,
+                                          uint32_t* __restrict__ out_dec, const Buckets& bk, QLds4& row) {
+  // one lane-distributed word (emit_load's `head`, lane 0 = the intent queue's slot 0)
+  const uint32_t* hp = nullptr;
+  if (lane < 3) hp = s.q_rumor + (l * 3 + lane) * c.qcap;
+  else if (lane == kEhPend) hp = s.p_cnt + l;
+  else if (lane >= kEhSeq && lane < kEhSeq + 3) hp = s.q_next_seq + l * 3 + (lane - kEhSeq);
+  else if (lane == kEhPruned) hp = s.q_pruned + l;
+  else if (lane == kEhErr) hp = s.err + l;
+  const uint32_t head = hp ? *hp : kEmpty;
+  const uint32_t gk = lane < c.fanout ? grp_key[l * c.fanout + lane] : kSentinel;
+  const uint32_t gs = lane < c.fanout ? slot[l * c.fanout + lane] : 0u;
+  const uint32_t np = (uint32_t)__popcll(__ballot(gk != kSentinel));
+  const uint32_t pc = shfl_u32(head, kEhPend), npend = pend_total(pc);
+  const bool ne0 = shfl_u32(head, 0) != kEmpty || (pc & 0xFF), ne1 = shfl_u32(head, 1) != kEmpty || ((pc >> 8) & 0xFF),
+             ne2 = shfl_u32(head, 2) != kEmpty || ((pc >> 16) & 0xFF);
+  if (np == 0 || !(ne0 || ne1 || ne2)) return;
+  bool d0 = false, d1 = false, d2 = false;
+  uint32_t err = 0;
+  PendRegs pr;
+  pend_load(s, l, lane, npend, pr);
+  uint32_t wdst = 0, wfirst = 0;
+  if (BKT && lane < np) {
+    wdst = (uint32_t)(gk / bk.per);
+    wfirst = bk.wstart[wdst];
+  }
+  Q4 Q0, Q1, Q2;
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) {
+    Q0.r[k] = Q1.r[k] = Q2.r[k] = kEmpty;
+    Q0.sq[k] = Q1.sq[k] = Q2.sq[k] = Q0.tl[k] = Q1.tl[k] = Q2.tl[k] = 0;
+    Q0.dec[k] = 0;
+    Q1.dec[k] = kDecQuery;
+    Q2.dec[k] = kDecEvent;
+  }
+  if (ne0) q4_load(c, s, l, 0, lane, Q0);
+  if (ne1) q4_load(c, s, l, 1, lane, Q1);
+  if (ne2) q4_load(c, s, l, 2, lane, Q2);
+  if (npend) {
+    uint32_t drops = 0;
+    if (pc & 0xFF) {
+      drops += q4_pend_apply<true>(c, Q0, lane, 0, npend, pr, shfl_u32(head, kEhSeq), row);
+      d0 = true;
+    }
+    if ((pc >> 8) & 0xFF) {
+      drops += q4_pend_apply<false>(c, Q1, lane, 1, npend, pr, shfl_u32(head, kEhSeq + 1), row);
+      d1 = true;
+    }
+    if ((pc >> 16) & 0xFF) {
+      drops += q4_pend_apply<false>(c, Q2, lane, 2, npend, pr, shfl_u32(head, kEhSeq + 2), row);
+      d2 = true;
+    }
+    if (lane == kEhPend) s.p_cnt[l] = 0;
+    if (lane >= kEhSeq && lane < kEhSeq + 3) {
+      const uint32_t nq = (pc >> (8 * (lane - kEhSeq))) & 0xFF;
+      if (nq) s.q_next_seq[l * 3 + (lane - kEhSeq)] = head + nq;
+    }
+    if (drops) {
+      if (lane == kEhPruned) s.q_pruned[l] = head + drops;
+      err |= kErrQueue;
+    }
+  }
+  for (uint32_t j = 0; j < np; ++j) {
+    const uint32_t gslot = shfl_u32(gs, j);
+    uint64_t out_base = (uint64_t)gslot * c.cap_t;
+    uint32_t* ov = out_val;
+    uint32_t* od = out_dec;
+    uint32_t* oc = cnt_s + gslot;
+    if (BKT) {
+      const uint32_t w = shfl_u32(wdst, j), idx = gslot - shfl_u32(wfirst, j);
+      uint32_t* b = bk.send + (uint64_t)w * bk.stride_u32;
+      if (idx < bk.gcap) {
+        ov = b + bk.vals_off;
+        od = nullptr;
+        oc = b + bk.cnt_off + idx;
+        out_base = (uint64_t)idx * c.cap_t;
+      } else {
+        ov = od = oc = nullptr;
+      }
+    }
+    uint32_t nrec = 0;
+    int64_t used = 0;
+    used += q4_get_broadcasts<true>(c, Q0, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d0, row);
+    used += q4_get_broadcasts<false>(c, Q1, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d1, row);
+    used += q4_get_broadcasts<false>(c, Q2, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d2, row);
+    if (lane == 0 && oc && nrec) *oc = min(nrec, c.cap_t);
+  }
+  if (d0) q4_store(c, s, l, 0, lane, Q0);
+  if (d1) q4_store(c, s, l, 1, lane, Q1);
+  if (d2) q4_store(c, s, l, 2, lane, Q2);
+  if (lane == kEhErr && (err & ~head)) s.err[l] = head | err;
+}
+
+template <bool BKT>
+__global__ void __launch_bounds__(64) emit4_kernel(GCfg c, GState s, const uint32_t* __restrict__ grp_key,
+                                                   const uint32_t* __restrict__ slot, uint32_t* __restrict__ cnt_s,
+                                                   uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec,
+                                                   Buckets bk) {
+  __shared__ QLds4 row;
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint64_t l = blockIdx.x;
+  if (l >= c.n_loc) return;
+  emit_run4<BKT>(c, s, grp_key, slot, l, lane, cnt_s, out_val, out_dec, bk, row);
+}
+
 template <bool BKT>
 __global__ void __launch_bounds__(64 * RSF_EMIT_WPB) emit_kernel(GCfg c, GState s, const uint32_t* __restrict__ grp_key,
                                                    const uint32_t* __restrict__ slot, uint32_t* __restrict__ cnt_s,
@@ -1292,7 +1413,7 @@ struct BigList {
 template <bool RUNS, bool BIG>
 __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const uint32_t* __restrict__ vals,
                                           const uint32_t* __restrict__ dec, const uint32_t* __restrict__ gcnt,
-                                          uint32_t stride, uint64_t l, uint32_t lane, uint32_t su, QLds* row,
+                                          uint32_t stride, uint64_t l, uint32_t lane, uint32_t su, QLds4* row,
                                           uint32_t* __restrict__ sbits, const Buckets& bk, const BigList& big) {
   MPROF_T(t_start);
   uint32_t st = 0, en = 0, total;
@@ -1345,7 +1466,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
       // the chunk's re-queues (at most one per record) might not fit the pending list:
       // apply the list to the queues first (rare: a receiver of many records)
       __threadfence_block();
-      qdrop += pend_flush_wave(c, s, l, lane, pc, *row);
+      qdrop += pend_flush_any(c, s, l, lane, pc, *row);
       pc = pn = 0;
     }
     const bool in = lane < cnt;
@@ -1559,7 +1680,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
   MPROF_T(t_st0);
   if (BIG && pn > kPendMerge) {  // leave the originations' headroom (kPendMerge)
     __threadfence_block();
-    qdrop += pend_flush_wave(c, s, l, lane, pc, *row);
+    qdrop += pend_flush_any(c, s, l, lane, pc, *row);
     pc = pn = 0;
   }
   if (qdrop) r.err |= kErrQueue;
@@ -1614,9 +1735,9 @@ __global__ void __launch_bounds__(256) merge_big_kernel(GCfg c, GState s, const 
                                                         const uint32_t* __restrict__ gcnt, uint32_t stride, Buckets bk,
                                                         BigList big) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
-  __shared__ QLds qlds[kWavesPerBlock];  // scratch of a pending list applied here
+  __shared__ QLds4 qlds[kWavesPerBlock];  // scratch of a pending list applied here
   __shared__ uint32_t subj_bits[kWavesPerBlock][128];
-  QLds& ql = qlds[threadIdx.x / kWave];
+  QLds4& ql = qlds[threadIdx.x / kWave];
   uint32_t* sbits = subj_bits[threadIdx.x / kWave];
   for (uint32_t i = lane; i < 128; i += kWave) sbits[i] = 0u;
   const uint64_t n = *big.n;
@@ -2054,9 +2175,22 @@ __global__ void __launch_bounds__(256) expire_kernel(GCfg c, GState s, uint32_t 
   if (t >= c.n_loc * 3) return;
   const uint64_t l = t / 3;
   const uint32_t q = (uint32_t)(t % 3);
+  const uint32_t G = rumor_generations(c);
+  if (c.qcap > kWave) {
+    __shared__ QLds4 rows[kWavesPerBlock];
+    Q4 Q;
+    q4_load(c, s, l, q, lane, Q);
+    bool stale[kQK];
+#pragma unroll
+    for (uint32_t k = 0; k < kQK; ++k) stale[k] = (gen + G - (Q.r[k] >> c.rbits) % G) % G >= 2;
+    const uint32_t x = q4_expire(c, Q, lane, stale, q == 0, rows[threadIdx.x / kWave]);
+    if (!x) return;
+    q4_store(c, s, l, q, lane, Q);
+    if (lane == 0) atomicAdd(s.q_expired + l, x);
+    return;
+  }
   QRegs Q{kEmpty, 0, 0};
   q_load(c, s, l, q, lane, Q);
-  const uint32_t G = rumor_generations(c);
   const uint32_t age = (gen + G - (Q.r >> c.rbits) % G) % G;
   const uint32_t x = q_expire(c, Q, lane, age >= 2, q == 0);
   if (!x) return;
@@ -2296,7 +2430,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   if (N < 2 || N >= 0xFFFFFFFFull) return gerr("n_members must be in [2, 2^32-1)");
   if (cfg->shard_lo >= cfg->shard_hi || cfg->shard_hi > N) return gerr("bad shard range");
   if (cfg->n_subjects == 0 || cfg->n_subjects > N) return gerr("n_subjects must be in [1, n_members]");
-  if (cfg->queue_cap == 0 || cfg->queue_cap > 64) return gerr("queue_cap must be 1..64");
+  if (cfg->queue_cap == 0 || cfg->queue_cap > 256) return gerr("queue_cap must be 1..256");
   if (cfg->event_buffer_size == 0 || cfg->query_buffer_size == 0) return gerr("dedup buffers must be non-empty");
   if (cfg->slot_k == 0 || cfg->slot_k > 64) return gerr("slot_k must be 1..64");
   if (cfg->fanout == 0 || cfg->fanout > 8 || cfg->fanout >= N) return gerr("fanout must be 1..8 and < n_members");
@@ -2737,15 +2871,23 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
     hipLaunchKernelGGL(bucket_fill_kernel, dim3(grid1(ng)), dim3(256), 0, st, (const uint32_t*)g->grp_key_s, ng, bk.per,
                        (const uint32_t*)g->d_wstart, bk);
     mark(g, 2);
-    hipLaunchKernelGGL(emit_kernel<true>, egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key, g->grp_slot,
-                       g->grp_cnt, g->stage_val, g->stage_dec, bk);
+    if (c.qcap > kWave)
+      hipLaunchKernelGGL(emit4_kernel<true>, dim3((unsigned)c.n_loc), dim3(kWave), 0, st, c, g->s, g->grp_key,
+                         g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk);
+    else
+      hipLaunchKernelGGL(emit_kernel<true>, egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key, g->grp_slot,
+                         g->grp_cnt, g->stage_val, g->stage_dec, bk);
     RSF_HIP(hipGetLastError());
     mark(g, 3);
     return RSF_OK;
   }
   mark(g, 2);
-  hipLaunchKernelGGL(emit_kernel<false>, egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key, g->grp_slot,
-                     g->grp_cnt, g->stage_val, g->stage_dec, Buckets{});
+  if (c.qcap > kWave)
+    hipLaunchKernelGGL(emit4_kernel<false>, dim3((unsigned)c.n_loc), dim3(kWave), 0, st, c, g->s, g->grp_key,
+                       g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, Buckets{});
+  else
+    hipLaunchKernelGGL(emit_kernel<false>, egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key, g->grp_slot,
+                       g->grp_cnt, g->stage_val, g->stage_dec, Buckets{});
   RSF_HIP(hipGetLastError());
   RSF_DBG_SYNC(st, "emit_kernel");
   if (local) {

@@ -1,0 +1,355 @@
+// gossip_queue4.h — transmit-limited queues of 65..256 slots (queue_cap up to 256; the
+// reference's max_queue_depth is 4096, core/src/options.rs:249).  Included by gossip.hip
+// after the one-slot-per-lane queue functions, whose invariants these keep exactly:
+//   * a queue is SORTED in send order by the key (transmits, ~len, ~seq), live items first;
+//   * get_broadcasts picks the leading run that fits the byte budget, then offers what is
+//     left to later (shorter) items one by one, bumps the picks (or retires them at the
+//     retransmit limit) and re-ranks;
+//   * a batch of new items (transmits 0, increasing seqs) keeps the qcap smallest keys of
+//     (queue U batch), the rest are counted as pruned (memberlist Prune of the tail).
+// Layout in registers: lane i holds the four sorted slots 4i .. 4i + 3 (slot order is lane
+// major, so prefix operations are a four-step local prefix plus one wave scan of the lanes'
+// totals).  Re-orderings go through the wave's 256-entry LDS row (QLds4): every item is
+// written to its new slot and read back in blocked order.
+#pragma once
+
+constexpr uint32_t kQK = 4;              // slots per lane
+constexpr uint32_t kQ4Cap = kWave * kQK;  // 256
+
+struct Q4 {
+  uint32_t r[kQK], sq[kQK], tl[kQK], dec[kQK];
+};
+struct alignas(16) QLds4 {
+  uint32_t r[kQ4Cap], sq[kQ4Cap], tl[kQ4Cap], dec[kQ4Cap];
+};
+
+__device__ __forceinline__ void lds_fence_wave() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// exclusive prefix over the lanes of a per-lane count (lane 0 first); `total` = the sum
+__device__ __forceinline__ uint32_t lanes_excl(uint32_t v, uint32_t& total) {
+  const uint32_t inc = wave_inclusive_sum_u32(v);
+  total = shfl_u32(inc, kWave - 1);
+  return inc - v;
+}
+// register k of a uniform slot index's lane (k wave-uniform): select, then readlane
+__device__ __forceinline__ uint32_t q4_pick(const uint32_t (&a)[kQK], uint32_t k) {
+  return k == 0 ? a[0] : k == 1 ? a[1] : k == 2 ? a[2] : a[3];
+}
+
+__device__ __forceinline__ void q4_load(const GCfg& c, const GState& s, uint64_t l, uint32_t q, uint32_t lane, Q4& Q) {
+  const uint64_t base = (l * 3 + q) * c.qcap;
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) {
+    const uint32_t slot = lane * kQK + k;
+    Q.dec[k] = q == 1 ? kDecQuery : kDecEvent;
+    if (slot < c.qcap) {
+      Q.r[k] = s.q_rumor[base + slot];
+      Q.sq[k] = s.q_seq[base + slot];
+      Q.tl[k] = s.q_txlen[base + slot];
+      if (q == 0) Q.dec[k] = s.q_dec[l * c.qcap + slot];
+    } else {
+      Q.r[k] = kEmpty;
+      Q.sq[k] = 0;
+      Q.tl[k] = 0;
+    }
+  }
+}
+__device__ __forceinline__ void q4_store(const GCfg& c, const GState& s, uint64_t l, uint32_t q, uint32_t lane,
+                                         const Q4& Q) {
+  const uint64_t base = (l * 3 + q) * c.qcap;
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) {
+    const uint32_t slot = lane * kQK + k;
+    if (slot < c.qcap) {
+      s.q_rumor[base + slot] = Q.r[k];
+      s.q_seq[base + slot] = Q.sq[k];
+      s.q_txlen[base + slot] = Q.tl[k];
+      if (q == 0) s.q_dec[l * c.qcap + slot] = Q.dec[k];
+    }
+  }
+}
+__device__ __forceinline__ bool q4_live(const GCfg& c, const Q4& Q, uint32_t lane, uint32_t k) {
+  return lane * kQK + k < c.qcap && Q.r[k] != kEmpty;
+}
+
+// every item with dst[k] < qcap written to slot dst[k] of the row, then read back in
+// blocked order; slots >= n_fill become free
+template <bool DEC>
+__device__ __forceinline__ void q4_scatter(const GCfg& c, Q4& Q, uint32_t lane, const uint32_t (&dst)[kQK],
+                                           uint32_t n_fill, QLds4& row) {
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) {
+    if (dst[k] < c.qcap) {
+      row.r[dst[k]] = Q.r[k];
+      row.sq[dst[k]] = Q.sq[k];
+      row.tl[dst[k]] = Q.tl[k];
+      if (DEC) row.dec[dst[k]] = Q.dec[k];
+    }
+  }
+  lds_fence_wave();
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) {
+    const uint32_t slot = lane * kQK + k;
+    if (slot < n_fill && slot < c.qcap) {
+      Q.r[k] = row.r[slot];
+      Q.sq[k] = row.sq[slot];
+      Q.tl[k] = row.tl[slot];
+      if (DEC) Q.dec[k] = row.dec[slot];
+    } else if (slot < c.qcap) {
+      Q.r[k] = kEmpty;
+      Q.sq[k] = 0;
+      Q.tl[k] = 0;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();  // the row is free once every lane has read it
+}
+
+// Re-rank after picks (q_rerank): the unpicked keepers np and the bumped keepers pk are
+// each sorted in slot order; each keeper's new slot = its rank in its list + the number of
+// the other list's keys below its own (binary search over the other list's keys in LDS).
+template <bool DEC>
+__device__ __forceinline__ void q4_rerank(const GCfg& c, Q4& Q, uint32_t lane, const bool (&np)[kQK],
+                                          const bool (&pk)[kQK], QLds4& row) {
+  uint32_t c_np = 0, c_pk = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) {
+    c_np += np[k];
+    c_pk += pk[k];
+  }
+  uint32_t n_np, n_pk;
+  uint32_t r_np = lanes_excl(c_np, n_np), r_pk = lanes_excl(c_pk, n_pk);
+  uint64_t* const keys_np = reinterpret_cast<uint64_t*>(row.r);   // r + sq: 256 keys
+  uint64_t* const keys_pk = reinterpret_cast<uint64_t*>(row.tl);  // tl + dec: 256 keys
+  uint64_t key[kQK];
+  uint32_t rk[kQK];
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) {
+    key[k] = tlq_key(Q.tl[k] & 0xFFFF, Q.tl[k] >> 16, Q.sq[k]);
+    rk[k] = np[k] ? r_np : r_pk;
+    if (np[k]) keys_np[r_np++] = key[k];
+    if (pk[k]) keys_pk[r_pk++] = key[k];
+  }
+  lds_fence_wave();
+  uint32_t dst[kQK];
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) {
+    dst[k] = kEmpty;
+    if (np[k] || pk[k]) {
+      const uint64_t* other = np[k] ? keys_pk : keys_np;
+      uint32_t lo = 0, len = np[k] ? n_pk : n_np;
+      while (len) {  // lower_bound of key in the other list
+        const uint32_t half = len >> 1;
+        if (other[lo + half] < key[k]) {
+          lo += half + 1;
+          len -= half + 1;
+        } else {
+          len = half;
+        }
+      }
+      dst[k] = rk[k] + lo;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();  // the keys are dead once every lane has searched them
+  q4_scatter<DEC>(c, Q, lane, dst, n_np + n_pk, row);
+}
+
+// one get_broadcasts call (q_get_broadcasts) on a sorted four-slot-per-lane queue
+template <bool DEC>
+__device__ __forceinline__ int64_t q4_get_broadcasts(const GCfg& c, Q4& Q, uint32_t lane, int64_t limit,
+                                                     uint32_t* stage_val, uint32_t* stage_dec, uint64_t out_base,
+                                                     uint32_t& nrec, uint32_t& err, bool& dirty, QLds4& row) {
+  bool live[kQK];
+  uint32_t len[kQK], incl[kQK], a = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) {
+    live[k] = q4_live(c, Q, lane, k);
+    len[k] = Q.tl[k] >> 16;
+    a += live[k] ? c.overhead + len[k] : 0u;
+    incl[k] = a;
+  }
+  uint32_t tot;
+  const uint32_t base = lanes_excl(a, tot);
+  if (!__ballot(live[0])) return 0;  // a sorted queue: empty iff slot 0 is free
+  bool pick[kQK];
+  uint32_t lead = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) {
+    incl[k] += base;
+    pick[k] = limit >= 0 && live[k] && (int64_t)incl[k] <= limit;
+    lead += pick[k];
+  }
+  uint32_t n_lead;
+  (void)lanes_excl(lead, n_lead);
+  // the leading run is the first n_lead slots: used = the prefix sum at its last slot
+  int64_t used = 0;
+  if (n_lead) {
+    const uint32_t s = n_lead - 1;
+    used = (int64_t)shfl_u32(q4_pick(incl, s % kQK), (int)(s / kQK));
+  }
+  for (;;) {
+    const int64_t free_b = limit - used - (int64_t)c.overhead;
+    if (free_b <= 0) break;
+    uint32_t first = kQK;  // this lane's first candidate slot
+#pragma unroll
+    for (int k = kQK - 1; k >= 0; --k)
+      if (live[k] && !pick[k] && (int64_t)len[k] <= free_b) first = (uint32_t)k;
+    const uint64_t cm = __ballot(first < kQK);
+    if (!cm) break;
+    const int wl = __ffsll((long long)cm) - 1;
+    const uint32_t wk = shfl_u32(first, wl);
+#pragma unroll
+    for (uint32_t k = 0; k < kQK; ++k)
+      if ((int)lane == wl && k == wk) pick[k] = true;
+    used += (int64_t)c.overhead + shfl_u32(q4_pick(len, wk), wl);
+  }
+  uint32_t pl = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) pl += pick[k];
+  uint32_t npick;
+  uint32_t rank = lanes_excl(pl, npick);
+  if (!npick) return used;
+  bool np[kQK], pk[kQK];
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) {
+    if (pick[k]) {
+      if (nrec + rank < c.cap_t && stage_val) {
+        stage_val[out_base + nrec + rank] = Q.r[k];
+        if (stage_dec) stage_dec[out_base + nrec + rank] = Q.dec[k];
+      }
+      rank++;
+    }
+    const bool retire = pick[k] && (Q.tl[k] & 0xFFFF) + 1 >= c.tx_limit;
+    if (retire) Q.r[k] = kEmpty;
+    else if (pick[k]) Q.tl[k] = Q.tl[k] + 1;
+    np[k] = live[k] && !pick[k];
+    pk[k] = pick[k] && !retire;
+  }
+  if (nrec + npick > c.cap_t) err |= kErrStage;
+  nrec += npick;
+  dirty = true;
+  q4_rerank<DEC>(c, Q, lane, np, pk, row);
+  return used;
+}
+
+// Batched insert of new items (q_insert_batch_lds): lane i offers at most one new item
+// (ins, rid, dec, len; seqs seq0, seq0 + 1, ... in lane order over `newmask`).  Returns the
+// live items that did not fit.
+template <bool DEC>
+__device__ __forceinline__ uint32_t q4_insert_batch(const GCfg& c, Q4& Q, uint32_t lane, bool ins, uint32_t rid,
+                                                    uint32_t dec, uint32_t len, uint32_t seq0, uint64_t newmask,
+                                                    QLds4& row) {
+  bool live[kQK], etx0[kQK];
+  uint32_t elen[kQK], pos_e[kQK], cl = 0;
+  const uint32_t n_new = (uint32_t)__popcll(newmask);
+  const uint64_t below = below_mask(lane), above = ~below & ~(1ull << lane);
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) {
+    live[k] = q4_live(c, Q, lane, k);
+    cl += live[k];
+    etx0[k] = live[k] && (Q.tl[k] & 0xFFFF) == 0;
+    elen[k] = Q.tl[k] >> 16;
+    pos_e[k] = lane * kQK + k + ((live[k] && !etx0[k]) ? n_new : 0u);
+  }
+  uint32_t n_live;
+  (void)lanes_excl(cl, n_live);
+  const uint32_t myseq = seq0 + (uint32_t)__popcll(newmask & below);
+  uint32_t pos_n = 0;
+  uint64_t rem = newmask;
+  while (rem) {
+    const uint32_t L = shfl_u32(len, __ffsll((long long)rem) - 1);
+    const uint64_t same = __ballot(ins && len == L);
+    rem &= ~same;
+    const uint32_t gt_new = (uint32_t)__popcll(__ballot(ins && len > L));
+    uint32_t go = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kQK; ++k) go += (etx0[k] && elen[k] > L) ? 1u : 0u;
+    uint32_t gt_old;
+    (void)lanes_excl(go, gt_old);
+    if (ins && len == L) pos_n = gt_old + gt_new + (uint32_t)__popcll(same & above);
+#pragma unroll
+    for (uint32_t k = 0; k < kQK; ++k)
+      if (etx0[k] && elen[k] <= L) pos_e[k] += (uint32_t)__popcll(same);
+  }
+  if (ins && pos_n < c.qcap) {
+    row.r[pos_n] = rid;
+    row.sq[pos_n] = myseq;
+    row.tl[pos_n] = len << 16;
+    if (DEC) row.dec[pos_n] = dec;
+  }
+  uint32_t dst[kQK];
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) dst[k] = live[k] ? pos_e[k] : kEmpty;
+  const uint32_t total = n_live + n_new;
+  q4_scatter<DEC>(c, Q, lane, dst, total, row);
+  return total > c.qcap ? total - c.qcap : 0u;
+}
+
+template <bool DEC>
+__device__ __forceinline__ uint32_t q4_pend_apply(const GCfg& c, Q4& Q, uint32_t lane, uint32_t q, uint32_t n,
+                                                  const PendRegs& p, uint32_t seq0, QLds4& row) {
+  uint32_t drops = 0, seq = seq0;
+#pragma unroll
+  for (uint32_t b = 0; b < 2; ++b) {
+    if (b * kWave >= n) break;
+    const bool ins = b * kWave + lane < n && (p.lq[b] >> 16) == q;
+    const uint64_t m = __ballot(ins);
+    if (!m) continue;
+    drops += q4_insert_batch<DEC>(c, Q, lane, ins, p.rid[b], p.dec[b], p.lq[b] & 0xFFFF, seq, m, row);
+    seq += (uint32_t)__popcll(m);
+  }
+  return drops;
+}
+
+// pend_flush_wave for queues of more than 64 slots
+__device__ __forceinline__ uint32_t q4_pend_flush_wave(const GCfg& c, const GState& s, uint64_t l, uint32_t lane,
+                                                       uint32_t pc, QLds4& row) {
+  const uint32_t n = pend_total(pc);
+  if (n == 0) return 0;
+  PendRegs p;
+  pend_load(s, l, lane, n, p);
+  uint32_t drops = 0;
+  for (uint32_t q = 0; q < 3; ++q) {
+    const uint32_t nq = (pc >> (8 * q)) & 0xFF;
+    if (!nq) continue;
+    Q4 Q;
+    q4_load(c, s, l, q, lane, Q);
+    const uint32_t seq0 = s.q_next_seq[l * 3 + q];
+    drops += q4_pend_apply<true>(c, Q, lane, q, n, p, seq0, row);
+    q4_store(c, s, l, q, lane, Q);
+    if (lane == 0) s.q_next_seq[l * 3 + q] = seq0 + nq;
+  }
+  if (lane == 0) {
+    s.p_cnt[l] = 0;
+    if (drops) s.q_pruned[l] += drops;
+  }
+  return drops;
+}
+
+// q_expire: stale items dropped, the survivors keep their order at the front
+__device__ __forceinline__ uint32_t q4_expire(const GCfg& c, Q4& Q, uint32_t lane, const bool (&stale)[kQK], bool dec,
+                                              QLds4& row) {
+  bool keep[kQK];
+  uint32_t ck = 0, cs = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) {
+    const bool live = q4_live(c, Q, lane, k);
+    keep[k] = live && !stale[k];
+    ck += keep[k];
+    cs += live && stale[k];
+  }
+  uint32_t n_stale;
+  (void)lanes_excl(cs, n_stale);
+  if (!n_stale) return 0;
+  uint32_t n_keep;
+  uint32_t r = lanes_excl(ck, n_keep);
+  uint32_t dst[kQK];
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) dst[k] = keep[k] ? r++ : kEmpty;
+  if (dec) q4_scatter<true>(c, Q, lane, dst, n_keep, row);
+  else q4_scatter<false>(c, Q, lane, dst, n_keep, row);
+  return n_stale;
+}

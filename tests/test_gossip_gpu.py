@@ -72,6 +72,54 @@ def test_bench_shape_bit_exact():
     L.orc_world_free(C.byref(w))
 
 
+@pytest.mark.parametrize("qcap,limit,rate,n", [(256, 8 * 24, 0.05, 6000), (128, 4000, 0.05, 2000),
+                                               (65, 1400, 0.03, 1500), (200, 6 * 24, 0.3, 800)])
+def test_queue_cap_over_64_bit_exact(qcap, limit, rate, n):
+    """Queues of 65..256 slots (four slots per lane of the emitting wave, gossip_queue4.h):
+    queues filling past 64 items under the bench's 8-intent budget (qcap 256, 200), wide
+    budgets that overflow a 128-slot queue (groups of up to 200 records), an odd capacity
+    (65, overflowing); bit-exact against the oracle after every round, then two
+    QueueChecker ticks."""
+    s, rounds = 64, 12
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=qcap, gossip_limit=limit, gossip_overhead=2,
+                         max_rumors=1 << 17, event_buffer_size=64, query_buffer_size=64, slot_k=4)
+    subj, acts, ml = W.intents_workload(n, s, rounds, rate=rate, seed=qcap + n)
+    g, w = pair(cfg, subj, W.initial_views(s))
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t])
+        H.assert_same(H.engine_state(g), H.world_state(w), f"round {t}")
+    r = g.queues()[0].reshape(n, 3, qcap)
+    assert np.count_nonzero(r[:, 0, :] != 0xFFFFFFFF, axis=1).max() > 64  # more than one slot per lane in use
+    for mx, mn, warn in [(4096, 0, 128), (100, 0, 64)]:
+        got = g.check_queues(mx, mn, warn)
+        exp = (C.c_uint64 * 9)()
+        L.orc_check_queues(C.byref(w), mx, mn, warn, exp)
+        assert list(got["queued"]) + list(got["warn"]) + list(got["pruned"]) == list(exp), (mx, mn, warn)
+        H.assert_same(H.engine_state(g), H.world_state(w), f"checker {mx}")
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
+def test_queue_cap_256_churn_flood_ring_bit_exact():
+    """qcap 256 with user events, queries and churn, and a rumor ring small enough to wrap:
+    the four-slot-per-lane expiry, the query / event queues and their pending lists."""
+    n, rounds = 1200, 40
+    subj, acts, ml = W.churn_workload(n, rounds, events_per_round=25, queries_per_round=4, seed=78)
+    s = len(subj)
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=256, gossip_limit=600, max_rumors=256,
+                         event_buffer_size=128, query_buffer_size=128, slot_k=8, max_refute=2)
+    g, w = pair(cfg, subj, W.initial_views(s))
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t])
+        H.assert_same(H.engine_state(g), H.world_state(w), f"round {t}")
+    st = H.engine_state(g)
+    assert w.gen >= 3 and st["q_expired"].sum() > 0
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
 def test_rumor_ring_recycles_bit_exact():
     """A rumor ring far smaller than the run: blocks restart the ring with the next
     generation, two generations resident; at each wrap the queued ids of generation
