@@ -313,6 +313,10 @@ def main():
     ap.add_argument("--members", type=int, default=None, help="members per GPU")
     ap.add_argument("--members-total", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--queue-cap", type=int, default=64,
+                    help="gossip: slots per transmit-limited queue (1..256; the reference's max_queue_depth is 4096)")
+    ap.add_argument("--settle", type=int, default=None,
+                    help="gossip: untimed rounds before warmup (default 12: queues saturated)")
     ap.add_argument("--no-vivaldi", action="store_true", help="gossip: skip the Vivaldi leg of the line")
     ap.add_argument("--refresh-every", type=int, default=1,
                     help="vivaldi, N>1: all-gather the coordinate table after every R-th round (C5: 1 and 8)")

@@ -23,12 +23,12 @@ PRUNE_FRAC = float(os.environ.get("RSF_PRUNE_FRAC", 0.1))
 HBM_PEAK_GBS = 8000.0
 
 
-def gossip_cfg(n_total, rounds_total, world, shard=None):
+def gossip_cfg(n_total, rounds_total, world, shard=None, queue_cap=64):
     from ruserf_amd.gossip import GossipConfig
     # rumor ring: a power of two holding >= 64 rounds of rumor blocks (ids recycle after that)
     per_round = SUBJECTS * 4 + int(round(n_total * 0.01))
     ring = 1 << max(10, (per_round * 64 - 1).bit_length())
-    return GossipConfig(n_members=n_total, n_subjects=SUBJECTS, shard=shard, queue_cap=64, event_buffer_size=512,
+    return GossipConfig(n_members=n_total, n_subjects=SUBJECTS, shard=shard, queue_cap=queue_cap, event_buffer_size=512,
                         query_buffer_size=512, slot_k=1, fanout=3, gossip_limit=8 * 24, gossip_overhead=2,
                         retransmit_mult=4, max_refute=4, max_rumors=ring, seed=SEED)
 
@@ -65,8 +65,9 @@ def run_gossip(args, rank, world):
     from ruserf_amd.gossip import GossipEngine
     per = args.members
     n = per * world
-    rounds_total = SETTLE_ROUNDS + args.warmup + args.steps
-    cfg = gossip_cfg(n, rounds_total, world)
+    settle = SETTLE_ROUNDS if args.settle is None else args.settle
+    rounds_total = settle + args.warmup + args.steps
+    cfg = gossip_cfg(n, rounds_total, world, queue_cap=args.queue_cap)
     subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED, prune_frac=PRUNE_FRAC)
     views = W.initial_views(SUBJECTS)
     stream = torch.cuda.current_stream()
@@ -82,7 +83,7 @@ def run_gossip(args, rank, world):
     eng.set_subjects(subj)
     eng.init_views(*views)
     t = 0
-    for _ in range(SETTLE_ROUNDS + args.warmup):
+    for _ in range(settle + args.warmup):
         step_fn(t)
         t += 1
     torch.cuda.synchronize()
@@ -152,7 +153,7 @@ def run_gossip(args, rank, world):
                    "members": n, "members_per_gpu": per, "fanout": 3, "items_per_target": 8,
                    "queue_cap_per_queue": cfg.queue_cap, "subjects": SUBJECTS,
                    "record_slots_per_group": min(3 * cfg.queue_cap, cfg.gossip_limit // (cfg.gossip_overhead + 18)),
-                   "settle_rounds": SETTLE_ROUNDS, "parallelism": f"members sharded x{world}"
+                   "settle_rounds": settle, "parallelism": f"members sharded x{world}"
                    + (" (multi-GPU code path forced)" if world == 1 and os.environ.get("RSF_FORCE_SHARDED") == "1"
                       else "")},
         "merges_per_s": merged_all / wall,
@@ -190,7 +191,7 @@ def cpu_baseline_gossip(args, seconds_target=10.0, n=200_000):
     from ruserf_amd import workload as W
     th = cpu_threads()
     rounds_total = SETTLE_ROUNDS + 40
-    cfg = gossip_cfg(n, rounds_total, 1)
+    cfg = gossip_cfg(n, rounds_total, 1, queue_cap=getattr(args, "queue_cap", 64))
     subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED, prune_frac=PRUNE_FRAC)
     w = H.oracle_world(cfg, subj, W.initial_views(SUBJECTS))
     t = 0
