@@ -123,28 +123,14 @@ def run_vivaldi(args, rank, world):
         from ruserf_amd.dist import ShardedVivaldi
         sv = ShardedVivaldi(g, rank, world)
 
+    refresher = None
+    if world > 1 and not targeted:
+        from ruserf_amd.dist import VivaldiTableRefresh
+        refresher = VivaldiTableRefresh(g, rank, world, R)
+
     def refresh(r):
-        # all-gather of the coordinate table (peers read last round's rows).  With R > 1
-        # (R = 8) the table is refreshed after every R-th round only, so
-        # rows of other shards are up to R rounds old -- the reference reads a peer's
-        # coordinate from its last ack, which is as stale as the probe schedule makes it.
-        if world == 1 or targeted or (r + 1) % R:
-            return
-        ptr, stride = g.table_ptr()
-        full = torch.as_tensor(CudaArray(ptr, (n * stride,), "<f8"), device="cuda")
-        mine = full[lo * stride: hi * stride].clone()
-        if coll_device() == "cpu":  # gloo rehearsal: host-staged
-            h = torch.empty(full.shape, dtype=full.dtype)
-            torch.distributed.all_gather_into_tensor(h, mine.cpu())
-            full.copy_(h)
-        else:
-            torch.distributed.all_gather_into_tensor(full, mine)
-        if R > 1:
-            # the tables ping-pong every round and an even R would always refresh the same
-            # one: the other table's rows of remote shards are brought up to date on-device
-            other = torch.as_tensor(CudaArray(read_ptr[0], (n * stride,), "<f8"), device="cuda")
-            other[: lo * stride].copy_(full[: lo * stride])
-            other[hi * stride:].copy_(full[hi * stride:])
+        if refresher is not None:
+            refresher.after_round(r, read_ptr[0])
 
     # the probe inputs (peer id, observed rtt) of every round are generated up front by
     # the synthetic network and are resident in HBM when the timed region starts

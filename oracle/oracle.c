@@ -430,9 +430,20 @@ typedef struct {
   orc_vivaldi_pop* p;
   uint32_t round, lo, hi;
   uint64_t resets;
+  const double* stale;   /* NULL, or the rows of the last table refresh (members outside shard_n) */
+  uint32_t shard_n;
 } viv_job;
 
-static void viv_member(orc_vivaldi_pop* p, uint32_t m, uint32_t round, uint64_t* resets) {
+/* the row member m reads for peer `peer`: the previous round's, or (stale != NULL, peer in
+ * another shard of shard_n members) the row as of the last refresh of the table */
+static inline const double* viv_peer_row(const orc_vivaldi_pop* p, const double* stale, uint32_t shard_n, uint32_t m,
+                                         uint32_t peer) {
+  if (stale && peer / shard_n != m / shard_n) return stale + (size_t)peer * p->row_stride;
+  return p->rows_cur + (size_t)peer * p->row_stride;
+}
+
+static void viv_member(orc_vivaldi_pop* p, uint32_t m, uint32_t round, uint64_t* resets, const double* stale,
+                       uint32_t shard_n) {
   const uint32_t dim = p->opts.dimensionality, F = p->opts.latency_filter_size;
   const uint32_t W = p->opts.adjustment_window_size;
   uint32_t slot;
@@ -441,7 +452,7 @@ static void viv_member(orc_vivaldi_pop* p, uint32_t m, uint32_t round, uint64_t*
   uint32_t peer = p->nbr[(size_t)m * p->peers + slot];
   orc_coord me, other, origin;
   row_to_coord(p->rows_cur + (size_t)m * p->row_stride, dim, &me);
-  row_to_coord(p->rows_cur + (size_t)peer * p->row_stride, dim, &other);
+  row_to_coord(viv_peer_row(p, stale, shard_n, m, peer), dim, &other);
   orc_coord_with_options(&p->opts, &origin);
   /* filter (Vec semantics) over the flat [n][peers][F] store */
   orc_filter f;
@@ -466,11 +477,22 @@ static void viv_member(orc_vivaldi_pop* p, uint32_t m, uint32_t round, uint64_t*
 
 static void* viv_worker(void* arg) {
   viv_job* j = (viv_job*)arg;
-  for (uint32_t m = j->lo; m < j->hi; ++m) viv_member(j->p, m, j->round, &j->resets);
+  for (uint32_t m = j->lo; m < j->hi; ++m) viv_member(j->p, m, j->round, &j->resets, j->stale, j->shard_n);
   return NULL;
 }
 
+static int viv_rounds(orc_vivaldi_pop* p, uint32_t round0, uint32_t rounds, int nthreads, double* stale,
+                      uint32_t shard_n, uint32_t refresh_every);
 int orc_vivaldi_pop_rounds(orc_vivaldi_pop* p, uint32_t round0, uint32_t rounds, int nthreads) {
+  return viv_rounds(p, round0, rounds, nthreads, NULL, p->n, 1);
+}
+int orc_vivaldi_pop_rounds_stale(orc_vivaldi_pop* p, uint32_t round0, uint32_t rounds, int nthreads, double* stale,
+                                 uint32_t shard_n, uint32_t refresh_every) {
+  if (!stale || shard_n == 0 || refresh_every == 0) return -1;
+  return viv_rounds(p, round0, rounds, nthreads, stale, shard_n, refresh_every);
+}
+static int viv_rounds(orc_vivaldi_pop* p, uint32_t round0, uint32_t rounds, int nthreads, double* stale,
+                      uint32_t shard_n, uint32_t refresh_every) {
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 256) nthreads = 256;
   pthread_t th[256];
@@ -486,6 +508,8 @@ int orc_vivaldi_pop_rounds(orc_vivaldi_pop* p, uint32_t round0, uint32_t rounds,
       jobs[i].lo = lo < p->n ? lo : p->n;
       jobs[i].hi = hi;
       jobs[i].resets = 0;
+      jobs[i].stale = stale;
+      jobs[i].shard_n = shard_n;
       if (nthreads == 1) {
         viv_worker(&jobs[i]);
       } else {
@@ -498,6 +522,8 @@ int orc_vivaldi_pop_rounds(orc_vivaldi_pop* p, uint32_t round0, uint32_t rounds,
     double* tmp = p->rows_cur;
     p->rows_cur = p->rows_nxt;
     p->rows_nxt = tmp;
+    /* the table refresh (an all-gather of every shard's rows) after every refresh_every-th round */
+    if (stale && (t + 1) % refresh_every == 0) memcpy(stale, p->rows_cur, sizeof(double) * (size_t)p->n * p->row_stride);
   }
   return 0;
 }

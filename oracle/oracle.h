@@ -150,6 +150,13 @@ void orc_true_position(uint64_t seed, uint32_t m, double* x, double* y, double* 
  * Every member probes once per round; peers are read from the previous-round table. */
 int orc_vivaldi_pop_rounds(orc_vivaldi_pop* p, uint32_t round0, uint32_t rounds, int nthreads);
 void orc_gen_neighbors(uint64_t seed, uint32_t n, uint32_t peers, uint32_t* nbr);
+/* The rounds of members sharded into ranges of shard_n whose coordinate table is refreshed
+ * by an all-gather after every refresh_every-th round (SURVEY §8(d) C5, R = 8): a member reads
+ * a peer of its own shard from the previous round's table and a peer of another shard from
+ * `stale`, the [n][row_stride] rows as of the last refresh (the caller initialises it to the
+ * population's rows; it is updated at every refresh). */
+int orc_vivaldi_pop_rounds_stale(orc_vivaldi_pop* p, uint32_t round0, uint32_t rounds, int nthreads, double* stale,
+                                 uint32_t shard_n, uint32_t refresh_every);
 /* SURVEY §8(d) C1's accuracy figure over the population's current coordinates: the median
  * over all pairs i < j of |est - true| / true, est = distance_to (ns, coordinate.rs:630-644),
  * true = the synthetic network's noiseless rtt |x_i - x_j| + h_i + h_j in ns */

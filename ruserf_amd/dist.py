@@ -140,6 +140,50 @@ class ShardedVivaldi:
         return self.g.exchange_ok()
 
 
+class VivaldiTableRefresh:
+    """The all-gather variant of the Vivaldi exchange (R = 1 and R = 8):
+    after every R-th round each rank's own rows of the table the next round reads are
+    all-gathered into every rank's copy, so rows of other shards are up to R rounds old
+    (the reference reads a peer's coordinate from its last ack, as stale as the probe
+    schedule makes it).  The context's two tables ping-pong every round; with R > 1 an even
+    R would always refresh the same one, so the other table's remote rows are brought up to
+    date on the device as well."""
+
+    def __init__(self, clients, rank, world, refresh_every=1, group=None):
+        if clients.n % world or clients.hi - clients.lo != clients.n // world:
+            raise ValueError("members must be sharded in equal contiguous ranges")
+        self.g, self.rank, self.world, self.R, self.group = clients, rank, world, int(refresh_every), group
+        self.lo, self.hi = clients.lo, clients.hi
+        self.stride = clients.table_ptr()[1]
+        self.stage = None
+
+    def _table(self, ptr):
+        t = hbm_tensor(ptr, self.g.n * self.stride, "<f8")
+        if self.stage is None:
+            self.stage = _staged(self.group, t.device)
+        return t
+
+    def after_round(self, r, read_ptr):
+        """Call after round r's observe; read_ptr = the table that round read (the
+        other one of the pair after the swap)."""
+        if self.world == 1 or (r + 1) % self.R:
+            return
+        ptr, _ = self.g.table_ptr()
+        full = self._table(ptr)
+        lo, hi = self.lo * self.stride, self.hi * self.stride
+        mine = full[lo:hi].clone()
+        if self.stage:  # gloo rehearsal: host-staged
+            h = torch.empty(full.shape, dtype=full.dtype)
+            dist.all_gather_into_tensor(h, mine.cpu(), group=self.group)
+            full.copy_(h)
+        else:
+            dist.all_gather_into_tensor(full, mine, group=self.group)
+        if self.R > 1:
+            other = self._table(read_ptr)
+            other[:lo].copy_(full[:lo])
+            other[hi:].copy_(full[hi:])
+
+
 class ShardedGossip:
     def __init__(self, cfg: GossipConfig, rank, world, device=0, engine=None, buffers=None, group=None,
                  exchange="buckets"):

@@ -176,6 +176,8 @@ def lib():
     L.orc_vivaldi_pop_free.argtypes = [C.POINTER(VivaldiPop)]
     L.orc_vivaldi_pop_rounds.argtypes = [C.POINTER(VivaldiPop), C.c_uint32, C.c_uint32, C.c_int]
     L.orc_vivaldi_pop_median_rel_error.argtypes = [C.POINTER(VivaldiPop)]
+    L.orc_vivaldi_pop_rounds_stale.argtypes = [C.POINTER(VivaldiPop), C.c_uint32, C.c_uint32, C.c_int,
+                                               C.POINTER(C.c_double), C.c_uint32, C.c_uint32]
     L.orc_vivaldi_pop_median_rel_error.restype = C.c_double
     L.orc_vivaldi_probe.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, P32, C.c_uint32, C.c_uint32,
                                     P32, P64]
