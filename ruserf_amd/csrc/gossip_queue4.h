@@ -23,6 +23,11 @@ struct alignas(16) QLds4 {
   uint32_t r[kQ4Cap], sq[kQ4Cap], tl[kQ4Cap], dec[kQ4Cap];
 };
 
+// Orders the wave's LDS accesses before it against those after it.  The fences are what
+// the compiler honours: wave_barrier alone does not order memory operations, and the row is
+// accessed through different types (u32 fields, u64 keys), so type-based alias analysis
+// would otherwise let it move a store of one kind across a load of the other.  Every
+// operation below starts and ends its use of the row with one.
 __device__ __forceinline__ void lds_fence_wave() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -81,6 +86,7 @@ __device__ __forceinline__ bool q4_live(const GCfg& c, const Q4& Q, uint32_t lan
 template <bool DEC>
 __device__ __forceinline__ void q4_scatter(const GCfg& c, Q4& Q, uint32_t lane, const uint32_t (&dst)[kQK],
                                            uint32_t n_fill, QLds4& row) {
+  lds_fence_wave();  // earlier reads of the row (keys, a previous read-back) come first
 #pragma unroll
   for (uint32_t k = 0; k < kQK; ++k) {
     if (dst[k] < c.qcap) {
@@ -105,7 +111,7 @@ __device__ __forceinline__ void q4_scatter(const GCfg& c, Q4& Q, uint32_t lane, 
       Q.tl[k] = 0;
     }
   }
-  __builtin_amdgcn_wave_barrier();  // the row is free once every lane has read it
+  lds_fence_wave();  // the row is free once every lane has read it
 }
 
 // Re-rank after picks (q_rerank): the unpicked keepers np and the bumped keepers pk are
@@ -124,6 +130,7 @@ __device__ __forceinline__ void q4_rerank(const GCfg& c, Q4& Q, uint32_t lane, c
   uint32_t r_np = lanes_excl(c_np, n_np), r_pk = lanes_excl(c_pk, n_pk);
   uint64_t* const keys_np = reinterpret_cast<uint64_t*>(row.r);   // r + sq: 256 keys
   uint64_t* const keys_pk = reinterpret_cast<uint64_t*>(row.tl);  // tl + dec: 256 keys
+  lds_fence_wave();
   uint64_t key[kQK];
   uint32_t rk[kQK];
 #pragma unroll
@@ -153,8 +160,7 @@ __device__ __forceinline__ void q4_rerank(const GCfg& c, Q4& Q, uint32_t lane, c
       dst[k] = rk[k] + lo;
     }
   }
-  __builtin_amdgcn_wave_barrier();  // the keys are dead once every lane has searched them
-  q4_scatter<DEC>(c, Q, lane, dst, n_np + n_pk, row);
+  q4_scatter<DEC>(c, Q, lane, dst, n_np + n_pk, row);  // (it fences the searches first)
 }
 
 // one get_broadcasts call (q_get_broadcasts) on a sorted four-slot-per-lane queue
@@ -274,6 +280,7 @@ __device__ __forceinline__ uint32_t q4_insert_batch(const GCfg& c, Q4& Q, uint32
     for (uint32_t k = 0; k < kQK; ++k)
       if (etx0[k] && elen[k] <= L) pos_e[k] += (uint32_t)__popcll(same);
   }
+  lds_fence_wave();
   if (ins && pos_n < c.qcap) {
     row.r[pos_n] = rid;
     row.sq[pos_n] = myseq;
