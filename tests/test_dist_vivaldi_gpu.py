@@ -135,7 +135,7 @@ def test_allgather_refresh_matches_stale_oracle(R):
     stale = O.arr(pop.rows_cur, N * pop.row_stride, np.float64).copy()
     assert L.orc_vivaldi_pop_rounds_stale(C.byref(pop), 0, ROUNDS, 8, stale.ctypes.data_as(C.POINTER(C.c_double)),
                                           N // world, R) == 0
-    exp = O.arr(pop.rows_cur, N * pop.row_stride, np.float64).reshape(N, pop.row_stride)
+    exp = O.arr(pop.rows_cur, N * pop.row_stride, np.float64).reshape(N, pop.row_stride).copy()
     sharded = np.concatenate([got[r] for r in range(world)])
     assert np.array_equal(sharded.view(np.uint64), exp.view(np.uint64))
     if R > 1:  # the staleness matters: the fresh-table rounds differ
