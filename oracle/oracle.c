@@ -608,7 +608,7 @@ static inline void snap_clock(orc_world* w, uint32_t m, int which, uint64_t ltim
 
 int orc_world_init(orc_world* w, const orc_world_cfg* c) {
   memset(w, 0, sizeof(*w));
-  if (c->n < 2 || c->s == 0 || c->s > c->n || c->qcap == 0 || c->qcap > 256 || c->ebuf == 0 ||
+  if (c->n < 2 || c->s == 0 || c->s > c->n || c->qcap == 0 || c->qcap > ORC_MAX_QCAP || c->ebuf == 0 ||
       c->qbuf == 0 || c->slot_k == 0 || c->fanout == 0 || c->fanout >= c->n || c->max_refute == 0 ||
       c->cap_rumors == 0 || (c->cap_rumors & (c->cap_rumors - 1)) || c->cap_rumors > (1u << 30))
     return -1;
@@ -939,7 +939,7 @@ uint32_t orc_queue_expire(orc_world* w, uint32_t m, uint32_t q) {
 uint32_t orc_queue_get_broadcasts(orc_world* w, uint32_t m, uint32_t q, uint32_t limit,
                                   uint32_t* out, uint32_t max_out, uint32_t* bytes_used) {
   size_t base = ((size_t)m * 3 + q) * w->qcap;
-  uint64_t picked = 0;
+  uint8_t picked[ORC_MAX_QCAP] = {0}; /* per slot: taken by this call */
   int64_t used = 0;
   uint32_t cnt = 0;
   for (;;) {
@@ -948,7 +948,7 @@ uint32_t orc_queue_get_broadcasts(orc_world* w, uint32_t m, uint32_t q, uint32_t
     uint32_t best = EMPTY_RUMOR;
     uint64_t kbest = UINT64_MAX;
     for (uint32_t i = 0; i < w->qcap; ++i) {
-      if (w->q_rumor[base + i] == EMPTY_RUMOR || (picked >> i & 1)) continue;
+      if (w->q_rumor[base + i] == EMPTY_RUMOR || picked[i]) continue;
       if ((int64_t)w->q_len[base + i] > free_b) continue;
       uint64_t k = tlq_key(w->q_tx[base + i], w->q_len[base + i], w->q_seq[base + i]);
       if (k < kbest) {
@@ -960,10 +960,10 @@ uint32_t orc_queue_get_broadcasts(orc_world* w, uint32_t m, uint32_t q, uint32_t
     if (cnt < max_out) out[cnt] = w->q_rumor[base + best];
     cnt++;
     used += (int64_t)w->overhead + w->q_len[base + best];
-    picked |= 1ull << best;
+    picked[best] = 1;
   }
   for (uint32_t i = 0; i < w->qcap; ++i) {
-    if (!(picked >> i & 1)) continue;
+    if (!picked[i]) continue;
     if ((uint32_t)w->q_tx[base + i] + 1 >= w->tx_limit) w->q_rumor[base + i] = EMPTY_RUMOR;
     else w->q_tx[base + i]++;
   }
@@ -1120,7 +1120,7 @@ static void phase_ml(world_job* j) {
 static void phase_emit(world_job* j) {
   orc_world* w = j->w;
   const uint32_t n = w->n, k = w->fanout, cap_t = 3 * w->qcap;
-  uint32_t peers[64], buf[3 * 64];
+  uint32_t peers[64], buf[3 * ORC_MAX_QCAP];
   j->cap = (size_t)(j->hi - j->lo) * k * cap_t;
   j->rec_recv = (uint32_t*)malloc((j->cap ? j->cap : 1) * sizeof(uint32_t));
   j->rec_rumor = (uint32_t*)malloc((j->cap ? j->cap : 1) * sizeof(uint32_t));

@@ -283,6 +283,7 @@ int orc_handle_user_event_cc(orc_world* w, uint32_t m, uint64_t ltime, uint64_t 
  * production order, 3 u64 each: user events (ltime, key, cc); member events
  * (ORC_LOG_MEMBER | MemberEventType, subject, 0) */
 #define ORC_LOG_MEMBER (1ull << 62)
+#define ORC_MAX_QCAP 256 /* slots per transmit-limited queue (the engine's queue_cap range) */
 int orc_world_set_delivery_log(orc_world* w, uint32_t per_member);
 int orc_handle_query(orc_world* w, uint32_t m, uint64_t ltime, uint32_t id, int no_broadcast);
 int orc_upsert_intent(orc_world* w, uint32_t m, uint32_t subj, uint8_t kind, uint64_t ltime);
