@@ -224,6 +224,21 @@ def cpu_baseline_vivaldi(seconds_target=8.0):
                       f"{cpu_info()}"}
 
 
+def configs1_point(args, rank, world, queue_cap, settle, warmup, steps):
+    """One more gossip measurement at configs[1]'s 1M members (see main)."""
+    from bench_gossip import run_gossip
+    a = argparse.Namespace(**vars(args))
+    a.members, a.queue_cap, a.settle, a.warmup, a.steps = 1_000_000, queue_cap, settle, warmup, steps
+    torch.cuda.empty_cache()
+    r = run_gossip(a, rank, world)
+    keep = ["value", "unit", "ms_per_step", "merges_per_s", "records_per_round_per_gpu", "queue_pruned_per_round",
+            "queue_pruned_per_merged_record", "error_members", "cub_canaries_intact", "phases_ms_per_round"]
+    out = {"metric": r["metric"], "steps": steps, "warmup": warmup, **{k: r[k] for k in keep}, "config": r["config"]}
+    out["roofline"] = {k: r["roofline"][k] for k in ["bound", "achieved", "peak", "unit", "frac", "kernel",
+                                                      "bytes_per_launch", "avg_launch_ms"]}
+    return out
+
+
 def c1_leg(rounds=1000, n=1000, with_gpu=True):
     """BASELINE configs[0] / SURVEY §8(d) C1: Vivaldi over a 1k-node synthetic RTT matrix on
     the CPU path -- the oracle (the C restatement of CoordinateClient::update; the Rust
@@ -301,6 +316,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--queue-cap", type=int, default=64,
                     help="gossip: slots per transmit-limited queue (1..256; the reference's max_queue_depth is 4096)")
+    ap.add_argument("--no-extra-points", action="store_true",
+                    help="gossip: skip the configs[1] points (1M members, 64- and 256-slot queues)")
     ap.add_argument("--settle", type=int, default=None,
                     help="gossip: untimed rounds before warmup (default 12: queues saturated)")
     ap.add_argument("--no-vivaldi", action="store_true", help="gossip: skip the Vivaldi leg of the line")
@@ -365,6 +382,13 @@ def main():
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline_gossip(args)
         attach_traffic(workload, res)
+        if world == 1 and not args.no_extra_points and args.members != 1_000_000:
+            # BASELINE configs[1] on one GPU (1M members, the same workload), at the default
+            # 64-slot queues (saturated: the flood fills every queue each round) and at 256
+            # slots over the first rounds, where no queue overflows -- the rounds of the
+            # reference's queue, unbounded between QueueChecker ticks
+            res["configs1_points"] = [configs1_point(args, rank, world, 64, None, args.warmup, args.steps),
+                                      configs1_point(args, rank, world, 256, 3, 1, 6)]
         if not args.no_vivaldi:
             # the metric's second half, timed in the same invocation (configs[4]: 64M members)
             vargs = argparse.Namespace(**vars(args))

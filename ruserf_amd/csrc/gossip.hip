@@ -64,7 +64,7 @@ __device__ unsigned long long g_merge_prof[8];
 // no lane leaves while the others go on through wave-wide ballots and shuffles.  Only in
 // converged code (every lane of the wave active).
 #if RSF_CHECKS
-#define RSF_BAD_W(k, cond, val) (__ballot(RSF_BAD(k, cond, val)) != 0)
+#define RSF_BAD_W(k, cond, val) (ballot(RSF_BAD(k, cond, val)) != 0)
 #else
 #define RSF_BAD_W(k, cond, val) false
 #endif
@@ -73,6 +73,11 @@ __device__ unsigned long long g_merge_prof[8];
 #else
 #define RSF_BAD2_W(k, cond, val) false
 #endif
+
+// Ballot of a per-lane condition straight from its compare.  HIP's __ballot takes an int, so
+// the condition is first materialised as 0/1 in a VGPR and compared again (two extra vector
+// instructions per ballot, and the emission and merge kernels take dozens per member).
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
 // Wave-wide u64 min/max through DPP (row_ror inside 16-lane rows, then
 // row_bcast15 / row_bcast31 across rows, result in lane 63): VALU-only data
@@ -226,8 +231,8 @@ __device__ __forceinline__ uint32_t q_insert_wave(const GCfg& c, QRegs& Q, uint3
   const bool live = valid && Q.r != kEmpty;
   const uint64_t newkey = tlq_key(0, len, seq);
   const uint64_t k = live ? tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq) : ~0ull;
-  const uint32_t full = (uint32_t)__popcll(__ballot(live)) == c.qcap ? 1u : 0u;
-  const uint32_t pos = (uint32_t)__popcll(__ballot(live && k < newkey));
+  const uint32_t full = (uint32_t)__popcll(ballot(live)) == c.qcap ? 1u : 0u;
+  const uint32_t pos = (uint32_t)__popcll(ballot(live && k < newkey));
   if (pos >= c.qcap) return full;
   const int src = lane ? (int)lane - 1 : 0;
   const uint32_t pr = (uint32_t)__shfl((int)Q.r, src), ps = (uint32_t)__shfl((int)Q.sq, src),
@@ -260,7 +265,7 @@ __device__ __forceinline__ uint32_t q_insert_batch(const GCfg& c, QRegs& Q, uint
                                                    uint32_t len, uint32_t seq0, uint64_t newmask) {
   const bool valid = lane < c.qcap;
   const bool live = valid && Q.r != kEmpty;
-  const uint32_t n_live = (uint32_t)__popcll(__ballot(live));
+  const uint32_t n_live = (uint32_t)__popcll(ballot(live));
   const uint32_t myseq = seq0 + (uint32_t)__popcll(newmask & below_mask(lane));
   const uint64_t nkey = ins ? tlq_key(0, len, myseq) : ~0ull;
   const uint64_t ekey = live ? tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq) : ~0ull;
@@ -272,14 +277,14 @@ __device__ __forceinline__ uint32_t q_insert_batch(const GCfg& c, QRegs& Q, uint
     const uint64_t bk = shfl_u64(nkey, k);
     const bool eb = live && bk < ekey;
     n_rank += (ins && bk < nkey) ? 1u : 0u;
-    const uint32_t el = n_live - (uint32_t)__popcll(__ballot(eb));
+    const uint32_t el = n_live - (uint32_t)__popcll(ballot(eb));
     e_less = (int)lane == k ? el : e_less;
   }
   const uint32_t pos_n = e_less + n_rank;
   // destinations of the surviving new items and, per destination, its source lane
   uint64_t dm = 0;
   uint32_t srcn = 0;
-  mm = __ballot(ins && pos_n < c.qcap);
+  mm = ballot(ins && pos_n < c.qcap);
   while (mm) {
     const int k = __ffsll((long long)mm) - 1;
     mm &= mm - 1;
@@ -312,10 +317,10 @@ __device__ __forceinline__ uint32_t q_insert_batch(const GCfg& c, QRegs& Q, uint
 __device__ __forceinline__ uint32_t q_expire(const GCfg& c, QRegs& Q, uint32_t lane, bool stale, bool permute_dec) {
   const bool valid = lane < c.qcap;
   const bool live = valid && Q.r != kEmpty;
-  const uint64_t sm = __ballot(live && stale);
+  const uint64_t sm = ballot(live && stale);
   if (!sm) return 0;
   const bool keep = live && !stale;
-  const uint64_t km = __ballot(keep), vm = __ballot(valid);
+  const uint64_t km = ballot(keep), vm = ballot(valid);
   const uint64_t below = below_mask(lane);
   const uint32_t pos = keep ? (uint32_t)__popcll(km & below)
                             : (valid ? (uint32_t)__popcll(km) + (uint32_t)__popcll(vm & ~km & below) : lane);
@@ -401,7 +406,7 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
                                                     uint64_t out_base, uint32_t& nrec, uint32_t& err, bool& dirty,
                                                     QLds& row) {
   const bool valid = lane < c.qcap;
-  const uint64_t live_m = __ballot(valid && Q.r != kEmpty);  // a sorted queue: a prefix
+  const uint64_t live_m = ballot(valid && Q.r != kEmpty);  // a sorted queue: a prefix
   if (!live_m) return 0;
   const bool live = (live_m >> lane) & 1;
   const uint32_t len = Q.tl >> 16;
@@ -410,12 +415,12 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   // comes out of one wave scan; the remaining budget is then offered to later (shorter)
   // items one by one, as the reference does.
   const uint32_t incl = wave_inclusive_sum_u32(live ? c.overhead + len : 0u);
-  uint64_t pick_m = limit >= 0 ? (__ballot((int64_t)incl <= limit) & live_m) : 0ull;
+  uint64_t pick_m = limit >= 0 ? (ballot((int64_t)incl <= limit) & live_m) : 0ull;
   int64_t used = pick_m ? (int64_t)shfl_u32(incl, 63 - __clzll((long long)pick_m)) : 0;
   for (;;) {
     const int64_t free_b = limit - used - (int64_t)c.overhead;
     if (free_b <= 0) break;
-    const uint64_t cand = __ballot((int64_t)len <= free_b) & live_m & ~pick_m;
+    const uint64_t cand = ballot((int64_t)len <= free_b) & live_m & ~pick_m;
     if (!cand) break;
     const int win = __ffsll((long long)cand) - 1;
     pick_m |= 1ull << win;
@@ -443,7 +448,7 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   const bool retire = picked && (Q.tl & 0xFFFF) + 1 >= c.tx_limit;
   if (retire) Q.r = kEmpty;
   else if (picked) Q.tl = Q.tl + 1;
-  q_rerank<PERMUTE_DEC>(c, Q, lane, pick_m & ~__ballot(retire), live_m & ~pick_m, row);
+  q_rerank<PERMUTE_DEC>(c, Q, lane, pick_m & ~ballot(retire), live_m & ~pick_m, row);
   return used;
 }
 
@@ -460,7 +465,7 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
 template <bool PERMUTE_DEC>
 __device__ __forceinline__ void q_materialize(const GCfg& c, QRegs& Q, uint32_t lane, uint64_t& cons, QLds& row) {
   if (!cons) return;
-  const uint64_t live_m = __ballot(lane < c.qcap && Q.r != kEmpty);
+  const uint64_t live_m = ballot(lane < c.qcap && Q.r != kEmpty);
   q_rerank<PERMUTE_DEC>(c, Q, lane, cons & live_m, live_m & ~cons, row);
   cons = 0;
 }
@@ -470,20 +475,20 @@ __device__ __forceinline__ int64_t q_get_broadcasts_lazy(const GCfg& c, QRegs& Q
                                                          uint32_t& nrec, uint32_t& err, bool& dirty, QLds& row,
                                                          uint64_t& cons, uint32_t& t0) {
   const bool valid = lane < c.qcap;
-  const uint64_t live_m = __ballot(valid && Q.r != kEmpty);
+  const uint64_t live_m = ballot(valid && Q.r != kEmpty);
   if (!live_m) return 0;
   if (!cons) t0 = shfl_u32(Q.tl, 0) & 0xFFFF;  // materialised: lane 0 holds the smallest key
   const uint32_t len = Q.tl >> 16;
-  const uint64_t a_m = __ballot(valid && Q.r != kEmpty && (Q.tl & 0xFFFF) == t0) & ~cons;
+  const uint64_t a_m = ballot(valid && Q.r != kEmpty && (Q.tl & 0xFFFF) == t0) & ~cons;
   const bool in_a = (a_m >> lane) & 1;
   const uint32_t incl = wave_inclusive_sum_u32(in_a ? c.overhead + len : 0u);
-  uint64_t pick_m = limit >= 0 ? (__ballot((int64_t)incl <= limit) & a_m) : 0ull;
+  uint64_t pick_m = limit >= 0 ? (ballot((int64_t)incl <= limit) & a_m) : 0ull;
   int64_t used = pick_m ? (int64_t)shfl_u32(incl, 63 - __clzll((long long)pick_m)) : 0;
   bool exact = false;
   for (;;) {
     const int64_t free_b = limit - used - (int64_t)c.overhead;
     if (free_b <= 0) break;
-    const uint64_t fit = __ballot((int64_t)len <= free_b) & live_m & ~pick_m;
+    const uint64_t fit = ballot((int64_t)len <= free_b) & live_m & ~pick_m;
     if (!fit) break;
     const uint64_t cand = fit & a_m;
     if (!cand) {  // the next candidate lies past the class-t0 run
@@ -539,7 +544,7 @@ __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, 
                                                        QLds& row) {
   const bool valid = lane < c.qcap;
   const bool live = valid && Q.r != kEmpty;
-  const uint32_t n_live = (uint32_t)__popcll(__ballot(live));
+  const uint32_t n_live = (uint32_t)__popcll(ballot(live));
   const uint32_t n_new = (uint32_t)__popcll(newmask);
   const uint64_t below = below_mask(lane), above = ~below & ~(1ull << lane);
   const uint32_t myseq = seq0 + (uint32_t)__popcll(newmask & below);
@@ -549,10 +554,10 @@ __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, 
   uint64_t rem = newmask;
   while (rem) {
     const uint32_t L = shfl_u32(len, __ffsll((long long)rem) - 1);
-    const uint64_t same = __ballot(ins && len == L);
+    const uint64_t same = ballot(ins && len == L);
     rem &= ~same;
-    const uint32_t gt_new = (uint32_t)__popcll(__ballot(ins && len > L));
-    const uint32_t gt_old = (uint32_t)__popcll(__ballot(etx0 && elen > L));
+    const uint32_t gt_new = (uint32_t)__popcll(ballot(ins && len > L));
+    const uint32_t gt_old = (uint32_t)__popcll(ballot(etx0 && elen > L));
     if (ins && len == L) pos_n = gt_old + gt_new + (uint32_t)__popcll(same & above);
     if (etx0 && elen <= L) pos_e += (uint32_t)__popcll(same);
   }
@@ -618,7 +623,7 @@ __device__ __forceinline__ uint32_t pend_apply(const GCfg& c, QRegs& Q, uint32_t
   for (uint32_t b = 0; b < 2; ++b) {
     if (b * kWave >= n) break;
     const bool ins = b * kWave + lane < n && (p.lq[b] >> 16) == q;
-    const uint64_t m = __ballot(ins);
+    const uint64_t m = ballot(ins);
     if (!m) continue;
     drops += q_insert_batch_lds<DEC>(c, Q, lane, ins, p.rid[b], p.dec[b], p.lq[b] & 0xFFFF, seq, m, row);
     seq += (uint32_t)__popcll(m);
@@ -963,9 +968,15 @@ struct Buckets {
 // word per lane (`head`): lanes 1, 2 the query / event queue heads, kEhPend the pending
 // re-queue counts, kEhSeq + q the queues' next insertion seqs, kEhPruned, kEhErr
 enum : uint32_t { kEhPend = 3, kEhSeq = 4, kEhPruned = 7, kEhErr = 8 };
+#ifndef RSF_EMIT_SPEC_PEND
+#define RSF_EMIT_SPEC_PEND 0  // 1: the first 64 pending entries loaded in the first round trip, unconditionally (measured +0.15 ms at 2M: the extra bytes cost more than the round trip)
+#endif
 struct EmitIn {
   QRegs Q0;
   uint32_t head, gk, gs;
+#if RSF_EMIT_SPEC_PEND
+  GState::PendE p0;  // pending entry `lane` (valid when lane < the member's count)
+#endif
 };
 __device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const uint32_t* __restrict__ grp_key,
                                           const uint32_t* __restrict__ slot, uint64_t l, uint32_t lane, EmitIn& e) {
@@ -984,6 +995,11 @@ __device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const 
   if (hp) e.head = *hp;
   e.gk = lane < c.fanout ? grp_key[l * c.fanout + lane] : kSentinel;
   e.gs = lane < c.fanout ? slot[l * c.fanout + lane] : 0u;
+#if RSF_EMIT_SPEC_PEND
+  // the pending list's first half does not depend on the count: issued with the first round
+  // trip instead of a second one after it (entries past the count are ignored)
+  e.p0 = s.p_ent[l * kPend + lane];
+#endif
 }
 template <bool BKT>
 __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_t l, uint32_t lane, EmitIn& e,
@@ -992,7 +1008,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   EPROF_T(t0);
   QRegs& Q0 = e.Q0;
   QRegs Q1{kEmpty, 0, 0, kDecQuery}, Q2{kEmpty, 0, 0, kDecEvent};
-  const uint64_t pm = __ballot(e.gk != kSentinel);  // peers are a prefix of the fanout slots
+  const uint64_t pm = ballot(e.gk != kSentinel);  // peers are a prefix of the fanout slots
   const uint32_t np = (uint32_t)__popcll(pm);
   const uint32_t pc = shfl_u32(e.head, kEhPend), npend = pend_total(pc);
   if (RSF_BAD2(8, npend > kPend || ((pc >> 24) != 0), pc)) return;
@@ -1006,7 +1022,20 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   uint32_t err = 0;
   // the pending re-queues (merge_kernel's and the originations' since the last emission)
   PendRegs pr;
+#if RSF_EMIT_SPEC_PEND
+  pr.rid[0] = lane < npend ? e.p0.rid : 0u;
+  pr.dec[0] = lane < npend ? e.p0.dec : 0u;
+  pr.lq[0] = lane < npend ? e.p0.lq : 0u;
+  pr.rid[1] = pr.dec[1] = pr.lq[1] = 0;
+  if (npend > kWave && kWave + lane < npend) {
+    const GState::PendE x = s.p_ent[l * kPend + kWave + lane];
+    pr.rid[1] = x.rid;
+    pr.dec[1] = x.dec;
+    pr.lq[1] = x.lq;
+  }
+#else
   pend_load(s, l, lane, npend, pr);
+#endif
   // buckets: each peer's destination shard and that bucket's first group (same round trip)
   uint32_t wdst = 0, wfirst = 0;
   if (BKT && lane < np) {
@@ -1068,12 +1097,16 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
     uint32_t nrec = 0;
     int64_t used = 0;
 #if RSF_EMIT_LAZY
-    used += q_get_broadcasts_lazy<true>(c, Q0, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d0, row,
-                                        cons0, t00);
-    used += q_get_broadcasts_lazy<false>(c, Q1, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d1, row,
-                                         cons1, t01);
-    used += q_get_broadcasts_lazy<false>(c, Q2, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d2, row,
-                                         cons2, t02);
+    // (a queue that was empty before the pending list and got nothing from it stays empty)
+    if (ne0)
+      used += q_get_broadcasts_lazy<true>(c, Q0, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d0, row,
+                                          cons0, t00);
+    if (ne1)
+      used += q_get_broadcasts_lazy<false>(c, Q1, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d1, row,
+                                           cons1, t01);
+    if (ne2)
+      used += q_get_broadcasts_lazy<false>(c, Q2, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d2, row,
+                                           cons2, t02);
 #else
     used += q_get_broadcasts<true>(c, Q0, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d0, row);
     used += q_get_broadcasts<false>(c, Q1, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d1, row);
@@ -1116,7 +1149,7 @@ __device__ __forceinline__ void emit_run4(const GCfg& c, const GState& s, const 
   const uint32_t head = hp ? *hp : kEmpty;
   const uint32_t gk = lane < c.fanout ? grp_key[l * c.fanout + lane] : kSentinel;
   const uint32_t gs = lane < c.fanout ? slot[l * c.fanout + lane] : 0u;
-  const uint32_t np = (uint32_t)__popcll(__ballot(gk != kSentinel));
+  const uint32_t np = (uint32_t)__popcll(ballot(gk != kSentinel));
   const uint32_t pc = shfl_u32(head, kEhPend), npend = pend_total(pc);
   const bool ne0 = shfl_u32(head, 0) != kEmpty || (pc & 0xFF), ne1 = shfl_u32(head, 1) != kEmpty || ((pc >> 8) & 0xFF),
              ne2 = shfl_u32(head, 2) != kEmpty || ((pc >> 16) & 0xFF);
@@ -1536,14 +1569,14 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
       clash = (old >> (h & 31)) & 1u;
       sbits[h >> 5] = 0u;  // LDS ops of a wave run in order: every lane's OR has returned
     }
-    if (__ballot(clash)) {
+    if (ballot(clash)) {
       // one pass per DISTINCT subject: the ballot of the lanes holding it is the chain,
       // each lane's neighbours are the nearest set bits below and above it
-      uint64_t mm = __ballot(is_view), same = 0;
+      uint64_t mm = ballot(is_view), same = 0;
       while (mm) {
         const uint32_t sj = shfl_u32(my_subj, __ffsll((long long)mm) - 1);
         const bool hit = my_subj == sj;  // non-view lanes hold 0xFFFFFFFF, never a subject
-        const uint64_t grp = __ballot(hit);
+        const uint64_t grp = ballot(hit);
         if (hit) same = grp;
         mm &= ~grp;
       }
@@ -1553,7 +1586,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     }
 #else
     {
-      const uint64_t vmask = __ballot(is_view);
+      const uint64_t vmask = ballot(is_view);
       uint64_t mm = vmask;
       while (mm) {
         const int j = __ffsll((long long)mm) - 1;
@@ -1608,7 +1641,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
         dirty = dirty || v.ltime != lt0 || v.meta != mt0 || v.t != t0;
         done = true;
       }
-      if (!__ballot(!done)) break;
+      if (!ballot(!done)) break;
     }
     if (next < 0 && is_view && dirty) vrow[my_subj] = v;  // last link writes the subject back
     if (chunk_max > r.clock) r.clock = chunk_max;
@@ -1616,7 +1649,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     MPROF_ADD(2, t_c1, t_c2);
     // intent re-queues of the chunk appended to the pending list in one batch (record order)
     const bool ins = is_view && (f & RSF_F_REBROADCAST);
-    const uint64_t newmask = __ballot(ins);
+    const uint64_t newmask = ballot(ins);
     if (newmask) {
       const uint32_t k = (uint32_t)__popcll(newmask);
       const uint32_t i = pn + (uint32_t)__popcll(newmask & below_mask(lane));
@@ -1627,7 +1660,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     }
     // serial part, record order: events/queries (lane 0 handlers), digest, refutes
     const uint64_t serial =
-        __ballot(valid && (!is_view || (f & (RSF_F_MEMBER_EVENT | RSF_F_REFUTE | RSF_F_PRUNE))));
+        ballot(valid && (!is_view || (f & (RSF_F_MEMBER_EVENT | RSF_F_REFUTE | RSF_F_PRUNE))));
     uint64_t mm = serial;
     while (mm) {
       const int i = __ffsll((long long)mm) - 1;
@@ -1839,7 +1872,7 @@ __global__ void __launch_bounds__(256) pp_merge_kernel(GCfg c, GState s, const r
     if (lmax > c_leave) c_leave = lmax;
     const uint64_t jmax = wave_max_u64(join ? L + 1 : 0);
     if (jmax > c_join) c_join = jmax;
-    uint64_t mm = __ballot(f & (RSF_F_MEMBER_EVENT | RSF_F_REFUTE));
+    uint64_t mm = ballot(f & (RSF_F_MEMBER_EVENT | RSF_F_REFUTE));
     while (mm) {
       const int i = __ffsll((long long)mm) - 1;
       mm &= mm - 1;
@@ -1903,7 +1936,7 @@ __global__ void __launch_bounds__(256) pp_merge_kernel(GCfg c, GState s, const r
     }
     const uint64_t emax = lane63_u64(incl);
     if (emax > ec) ec = emax;
-    uint64_t mm = __ballot(dmask != 0 || e_err != 0);
+    uint64_t mm = ballot(dmask != 0 || e_err != 0);
     while (mm) {
       const int j = __ffsll((long long)mm) - 1;
       mm &= mm - 1;
@@ -1957,8 +1990,8 @@ __global__ void __launch_bounds__(256) reap_kernel(GCfg c, GState s, uint32_t no
       const bool intent = subj < c.S && (kind == RSF_KIND_INTENT_JOIN || kind == RSF_KIND_INTENT_LEAVE) && age > in_to;
       const bool reap = pass == 0 ? failed : left;
       if (reap || (pass == 0 && intent)) vrow[subj] = ViewE{0ull, 0u, 0u};  // erase_node / reap_intents
-      if (pass == 0) any_left = any_left || __ballot(left) != 0;
-      uint64_t mm = __ballot(reap);
+      if (pass == 0) any_left = any_left || ballot(left) != 0;
+      uint64_t mm = ballot(reap);
       while (mm) {  // Reap member events, slot order
         const int i = __ffsll((long long)mm) - 1;
         mm &= mm - 1;
@@ -2239,11 +2272,20 @@ __global__ void __launch_bounds__(256) bucket_fill_kernel(const uint32_t* __rest
 // merged (group counts) summed for the statistics; a receiver outside the shard or an
 // unsorted bucket is flagged.  Grid-stride over a bounded grid: one atomic per block (an
 // atomic per 256 groups on one address serialised into ~0.25 ms at 6M groups).
-constexpr unsigned kBucketIndexBlocks = 1024;
+// With RSF_BUCKET_DEC_FUSED the same pass also rebuilds the decorations of each group's
+// records from the replicated rumor table (bucket_dec_kernel's work, one thread per group
+// instead of one per record slot: measured 0.32 ms per round at 2M members as a kernel of
+// its own, most of it launching and indexing 61M mostly idle threads).
+#ifndef RSF_BUCKET_DEC_FUSED
+#define RSF_BUCKET_DEC_FUSED 1
+#endif
+constexpr unsigned kBucketIndexBlocks = RSF_BUCKET_DEC_FUSED ? 4096 : 1024;
 __global__ void __launch_bounds__(256) bucket_index_kernel(Buckets bk, uint64_t lo, uint64_t n_loc,
                                                            uint32_t* __restrict__ rstart, uint32_t* __restrict__ rend,
                                                            unsigned long long* __restrict__ merged,
-                                                           unsigned long long* __restrict__ flags) {
+                                                           unsigned long long* __restrict__ flags, uint32_t cap_t,
+                                                           const uint32_t* __restrict__ rdec, uint32_t rmask,
+                                                           uint32_t* __restrict__ decs) {
   const uint64_t n = (uint64_t)bk.n_runs * bk.gcap;
   uint64_t sum = 0;
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
@@ -2257,9 +2299,16 @@ __global__ void __launch_bounds__(256) bucket_index_kernel(Buckets bk, uint64_t 
       atomicOr(flags, 2ull);
       continue;
     }
-    sum += b[bk.cnt_off + i];
+    const uint32_t cnt = b[bk.cnt_off + i];
+    sum += cnt;
     if (i == 0 || b[bk.keys_off + i - 1] != key) rstart[(uint64_t)r * n_loc + l] = i;
     if (i + 1 == ng || b[bk.keys_off + i + 1] != key) rend[(uint64_t)r * n_loc + l] = i + 1;
+    if (decs) {
+      const uint32_t* v = b + bk.vals_off + (uint64_t)i * cap_t;
+      uint32_t* d = decs + ((uint64_t)r * bk.gcap + i) * cap_t;
+      const uint32_t k_end = cnt < cap_t ? cnt : cap_t;
+      for (uint32_t k = 0; k < k_end; ++k) d[k] = rdec[v[k] & rmask];
+    }
   }
   __shared__ uint64_t part[4];
   for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
@@ -3054,9 +3103,11 @@ int rsf_gossip_round_merge_buckets(rsf_gossip* g, uint32_t world) {
   RSF_HIP(hipMemsetAsync(g->d_counters + 57, 0, 8, st));
   hipLaunchKernelGGL(bucket_index_kernel, dim3(std::min<uint64_t>(grid1((uint64_t)world * bk.gcap), kBucketIndexBlocks)),
                      dim3(256), 0, st, bk, c.lo, c.n_loc, g->d_rstart, g->d_rend, g->d_counters + 57,
-                     g->d_counters + 58);
-  hipLaunchKernelGGL(bucket_dec_kernel, dim3(grid1((uint64_t)world * bk.gcap * c.cap_t)), dim3(256), 0, st, bk, c.cap_t,
-                     (const uint32_t*)g->s.rdec, c.rmask, g->bkt_dec);
+                     g->d_counters + 58, c.cap_t, (const uint32_t*)g->s.rdec, c.rmask,
+                     RSF_BUCKET_DEC_FUSED ? g->bkt_dec : nullptr);
+  if (!RSF_BUCKET_DEC_FUSED)
+    hipLaunchKernelGGL(bucket_dec_kernel, dim3(grid1((uint64_t)world * bk.gcap * c.cap_t)), dim3(256), 0, st, bk,
+                       c.cap_t, (const uint32_t*)g->s.rdec, c.rmask, g->bkt_dec);
   hipLaunchKernelGGL(accumulate_kernel, dim3(1), dim3(64), 0, st, g->d_counters, 57u);
   if (g->profiling && g->prof_rounds < rsf_gossip::kMaxProfRounds)
     hipEventRecord(g->ev[g->prof_rounds][3], g->stream);  // exchange time lands in the sort slot
@@ -3844,9 +3895,9 @@ __global__ void __launch_bounds__(256) reconnect_kernel(GCfg c, GState s, uint32
     uint32_t meta = 0;
     if (j < c.S && (int32_t)j != own) meta = row[j].meta;
     const bool kn = vkind(meta) == RSF_KIND_KNOWN;
-    known += (uint32_t)__popcll(__ballot(kn));
-    failed += (uint32_t)__popcll(__ballot(kn && vstatus(meta) == RSF_STATUS_FAILED));
-    left += (uint32_t)__popcll(__ballot(kn && vstatus(meta) == RSF_STATUS_LEFT));
+    known += (uint32_t)__popcll(ballot(kn));
+    failed += (uint32_t)__popcll(ballot(kn && vstatus(meta) == RSF_STATUS_FAILED));
+    left += (uint32_t)__popcll(ballot(kn && vstatus(meta) == RSF_STATUS_LEFT));
   }
   if (!failed) return;
   uint64_t alive_n = known - failed - left;
@@ -3862,11 +3913,11 @@ __global__ void __launch_bounds__(256) reconnect_kernel(GCfg c, GState s, uint32
     uint32_t meta = 0;
     if (j < c.S && (int32_t)j != own) meta = row[j].meta;
     const bool fa = vkind(meta) == RSF_KIND_KNOWN && vstatus(meta) == RSF_STATUS_FAILED;
-    const unsigned long long mask = __ballot(fa);
+    const unsigned long long mask = ballot(fa);
     const uint32_t cnt = (uint32_t)__popcll(mask);
     if (idx < cnt) {
       const bool hit = fa && (uint32_t)__popcll(mask & ((1ull << lane) - 1)) == idx;
-      const unsigned long long hm = __ballot(hit);
+      const unsigned long long hm = ballot(hit);
       tj = j0 + (uint32_t)__builtin_ctzll(hm);
     } else {
       idx -= cnt;

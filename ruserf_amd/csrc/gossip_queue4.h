@@ -179,7 +179,7 @@ __device__ __forceinline__ int64_t q4_get_broadcasts(const GCfg& c, Q4& Q, uint3
   }
   uint32_t tot;
   const uint32_t base = lanes_excl(a, tot);
-  if (!__ballot(live[0])) return 0;  // a sorted queue: empty iff slot 0 is free
+  if (!ballot(live[0])) return 0;  // a sorted queue: empty iff slot 0 is free
   bool pick[kQK];
   uint32_t lead = 0;
 #pragma unroll
@@ -203,7 +203,7 @@ __device__ __forceinline__ int64_t q4_get_broadcasts(const GCfg& c, Q4& Q, uint3
 #pragma unroll
     for (int k = kQK - 1; k >= 0; --k)
       if (live[k] && !pick[k] && (int64_t)len[k] <= free_b) first = (uint32_t)k;
-    const uint64_t cm = __ballot(first < kQK);
+    const uint64_t cm = ballot(first < kQK);
     if (!cm) break;
     const int wl = __ffsll((long long)cm) - 1;
     const uint32_t wk = shfl_u32(first, wl);
@@ -267,9 +267,9 @@ __device__ __forceinline__ uint32_t q4_insert_batch(const GCfg& c, Q4& Q, uint32
   uint64_t rem = newmask;
   while (rem) {
     const uint32_t L = shfl_u32(len, __ffsll((long long)rem) - 1);
-    const uint64_t same = __ballot(ins && len == L);
+    const uint64_t same = ballot(ins && len == L);
     rem &= ~same;
-    const uint32_t gt_new = (uint32_t)__popcll(__ballot(ins && len > L));
+    const uint32_t gt_new = (uint32_t)__popcll(ballot(ins && len > L));
     uint32_t go = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kQK; ++k) go += (etx0[k] && elen[k] > L) ? 1u : 0u;
@@ -303,7 +303,7 @@ __device__ __forceinline__ uint32_t q4_pend_apply(const GCfg& c, Q4& Q, uint32_t
   for (uint32_t b = 0; b < 2; ++b) {
     if (b * kWave >= n) break;
     const bool ins = b * kWave + lane < n && (p.lq[b] >> 16) == q;
-    const uint64_t m = __ballot(ins);
+    const uint64_t m = ballot(ins);
     if (!m) continue;
     drops += q4_insert_batch<DEC>(c, Q, lane, ins, p.rid[b], p.dec[b], p.lq[b] & 0xFFFF, seq, m, row);
     seq += (uint32_t)__popcll(m);
