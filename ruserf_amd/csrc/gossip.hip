@@ -2373,6 +2373,18 @@ struct rsf_gossip {
   rsf_ml_event* d_ml = nullptr;
   rsf_action* d_acts = nullptr;
   uint32_t cap_ml = 0, cap_acts = 0;
+  // the round's host lists go to the device from pinned staging (two slots, each reused
+  // once the copy issued from it two rounds earlier has completed): a copy from pageable
+  // memory would block the host until the stream drained, leaving the GPU idle while the
+  // next round is prepared and launched
+#ifndef RSF_PIN_STAGING
+#define RSF_PIN_STAGING 1
+#endif
+  void* pin[2] = {nullptr, nullptr};
+  size_t pin_cap[2] = {0, 0};
+  hipEvent_t pin_ev[2] = {nullptr, nullptr};
+  bool pin_used[2] = {false, false};
+  int pin_next = 0;
   // record pipeline
   uint64_t stage_cap = 0, recv_cap = 0;
   uint32_t *stage_key = nullptr, *stage_val = nullptr, *sort_key = nullptr, *sort_val = nullptr;
@@ -2643,6 +2655,10 @@ int rsf_gossip_destroy(rsf_gossip* g) {
   for (void* p : ptrs)
     if (p) hipFree(p);
   g->scratch.release();
+  for (int k = 0; k < 2; ++k) {
+    if (g->pin[k]) hipHostFree(g->pin[k]);
+    if (g->pin_ev[k]) hipEventDestroy(g->pin_ev[k]);
+  }
   g->sort_tmp.release();
   g->grp_tmp.release();
   g->scan_tmp.release();
@@ -2853,18 +2869,48 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
   const uint32_t round_pidx = g->round_base & c.rmask;  // physical index: generation parity | slot
   RSF_HIP(hipMemsetAsync(g->s.rumors + round_pidx, 0, need * sizeof(rsf_rumor), st));
   if (g->c.dcap) RSF_HIP(hipMemsetAsync(g->s.dcnt, 0, c.n_loc * 4, st));  // the round's delivery log
+  const size_t b_ml = (size_t)n_ml * sizeof(rsf_ml_event), b_acts = (size_t)n_acts * sizeof(rsf_action);
+  const char* pin_ml = nullptr;
+  const char* pin_acts = nullptr;
+  int pin_k = -1;
+  if (!RSF_PIN_STAGING) {
+    pin_ml = (const char*)ml;
+    pin_acts = (const char*)acts;
+  } else if (b_ml + b_acts) {
+    const int k = pin_k = g->pin_next;
+    g->pin_next ^= 1;
+    if (g->pin_used[k]) RSF_HIP(hipEventSynchronize(g->pin_ev[k]));  // its previous copy has landed
+    if (!g->pin_ev[k]) RSF_HIP(hipEventCreateWithFlags(&g->pin_ev[k], hipEventDisableTiming));
+    if (b_ml + b_acts > g->pin_cap[k]) {
+      if (g->pin[k]) RSF_HIP(hipHostFree(g->pin[k]));
+      g->pin[k] = nullptr;
+      g->pin_cap[k] = 0;
+      const size_t cap = std::max<size_t>(b_ml + b_acts, 1 << 20);
+      RSF_HIP(hipHostMalloc(&g->pin[k], cap, hipHostMallocDefault));
+      g->pin_cap[k] = cap;
+    }
+    char* p = (char*)g->pin[k];
+    if (b_ml) memcpy(p, ml, b_ml);
+    if (b_acts) memcpy(p + b_ml, acts, b_acts);
+    pin_ml = p;
+    pin_acts = p + b_ml;
+  }
   if (n_ml) {
-    RSF_HIP(hipMemcpyAsync(g->d_ml, ml, n_ml * sizeof(rsf_ml_event), hipMemcpyHostToDevice, st));
+    RSF_HIP(hipMemcpyAsync(g->d_ml, pin_ml, b_ml, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(ml_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, c, g->s, g->d_ml, n_ml);
     hipLaunchKernelGGL(ml_alive_kernel, dim3(1), dim3(64), 0, st, g->s, g->d_ml, n_ml);
   }
   hipLaunchKernelGGL(refute_kernel, dim3(grid1(c.S)), dim3(256), 0, st, c, g->s, g->round_base);
   RSF_DBG_SYNC(st, "refute_kernel");
   if (n_acts) {
-    RSF_HIP(hipMemcpyAsync(g->d_acts, acts, n_acts * sizeof(rsf_action), hipMemcpyHostToDevice, st));
+    RSF_HIP(hipMemcpyAsync(g->d_acts, pin_acts, b_acts, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(originate_kernel, dim3(grid1(n_acts)), dim3(256), 0, st, c, g->s, g->d_acts, n_acts,
                        g->round_abase);
     RSF_DBG_SYNC(st, "originate_kernel");
+  }
+  if (pin_k >= 0) {  // the slot is free again once the stream has passed this point
+    RSF_HIP(hipEventRecord(g->pin_ev[pin_k], st));
+    g->pin_used[pin_k] = true;
   }
   RSF_HIP(hipGetLastError());
   mark(g, 1);
