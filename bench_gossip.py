@@ -94,6 +94,8 @@ def run_gossip(args, rank, world):
     # exactly the timed rounds' worth of pending re-queues
     pruned0 = eng.pruned_total(flush=False)
     eng.set_profiling(True)
+    if sharded:
+        sg.set_timing(True)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -107,6 +109,7 @@ def run_gossip(args, rank, world):
     wall = time.perf_counter() - t0
     # multi-GPU path: no bucket overflowed and every record reached its shard (read after timing)
     exchange_ok = sg.check() if sharded else None
+    exchange_ms = sg.exchange_times() if sharded else None
     phase_ms, nr = eng.phase_times()
     merged = eng.merged_total() - merged0
     pruned = eng.pruned_total(flush=False) - pruned0
@@ -166,6 +169,8 @@ def run_gossip(args, rank, world):
         "queue_pruned_per_merged_record": pruned_all / max(1.0, merged_all),
         "queue_prune_members": qpm_all,
         "phases_ms_per_round": dict(zip(names, avg)),
+        # multi-GPU path: device time of the round's collectives (inside the phases above)
+        "collectives_ms_per_round": exchange_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": names[dom],
                      "bytes_model": "SURVEY 8(d): B_merge = 64 B per merged record",

@@ -388,12 +388,14 @@ int rsf_gossip_check_runs(rsf_gossip* g, int* ok);
  * world size) and returns the send and receive buffers, `world` buckets of bucket_bytes
  * each, device memory.  round_emit_buckets emits straight into the send buckets (each
  * holds its shard's (sender, peer) groups sorted by receiver: a header with the group
- * count, the receivers, record counts and rumor ids; the record decorations are rebuilt
- * on the receive side from the replicated rumor table).  The caller
- * moves bucket w of every rank to rank w (one all-to-all of equal splits, e.g.
- * ncclAllToAll), concatenated in source-rank order, then round_merge_buckets merges
- * straight from the received buckets: per receiver its groups of every source in
- * source-rank order = the canonical (receiver; sender, position) order.  A bucket over
+ * count, the receivers, record counts and rumor ids; the record decorations are looked
+ * up on the receive side from the replicated rumor table).  The caller moves bucket w of
+ * every rank r to slot r of rank w's receive buffer (source-rank order), for every w other
+ * than r itself -- a shard's own bucket is read from its send buffer, so its receive slot is
+ * never read and need not be filled (grouped point-to-point sends/receives, or an
+ * all-to-all of equal splits, which also copies the unused self slot); then
+ * round_merge_buckets merges straight from the buckets: per receiver its groups of every
+ * source in source-rank order = the canonical (receiver; sender, position) order.  A bucket over
  * its capacity, or a receiver outside the shard, is recorded and reported by
  * rsf_gossip_bucket_status (ok = 0 from then on: the rounds since are not valid). */
 int rsf_gossip_bucket_buffers(rsf_gossip* g, uint32_t world, void** send, void** recv, uint64_t* bucket_bytes);

@@ -926,18 +926,28 @@ __global__ void __launch_bounds__(256) grp_index_kernel(const uint32_t* __restri
 // Multi-GPU exchange buckets (rsf_gossip_round_emit_buckets): one bucket per destination
 // shard, u32 layout [n_groups, 3 x pad | keys[gcap] | cnt[gcap] | vals[gcap * cap_t]]; the
 // groups of a bucket are sorted by receiver.  On the receive side the world's buckets arrive
-// back to back in source-rank order = runs.  Record decorations do not travel: every shard
-// holds the whole rumor table, so the receive side rebuilds them from the rumor ids into a
-// local array (`decs`, [run][gcap * cap_t]) -- 44 B per group on the wire instead of 80.
+// back to back in source-rank order = runs.  The bucket a shard addresses to itself never
+// travels: the receive side reads run `self_run` from the send buffer (the receive buffer's
+// slot for it is left as it is), so the exchange moves (world - 1) buckets per rank.
+// Record decorations do not travel either: every shard holds the whole rumor table, so the
+// receive side looks them up from the rumor ids (rdec, L2-resident) -- 44 B per group on
+// the wire instead of 80.
 constexpr uint32_t kMaxRuns = 8;
+#ifndef RSF_BUCKET_DEC_MODE
+#define RSF_BUCKET_DEC_MODE 2  // receive-side decorations: see bucket_index_kernel
+#endif
 struct Buckets {
   const uint32_t* base;  // receive buffer (RUNS merge); emission writes through `send`
   uint32_t* send;        // send buffer (emission into buckets)
   const uint32_t* wstart;  // emission: per destination shard, its first group in sorted order
   uint64_t per;            // members per shard
   uint64_t stride_u32;   // one bucket
-  const uint32_t* decs;  // receive side: the records' decorations, [run][gcap * cap_t]
-  uint32_t keys_off, cnt_off, vals_off, gcap, n_runs;
+  const uint32_t* decs;  // RSF_BUCKET_DEC_MODE < 2: the records' decorations, [run][gcap * cap_t]
+  uint32_t keys_off, cnt_off, vals_off, gcap, n_runs, self_run;
+  // run r's bucket on the receive side
+  __device__ __forceinline__ const uint32_t* run(uint32_t r) const {
+    return (r == self_run ? (const uint32_t*)send : base) + (uint64_t)r * stride_u32;
+  }
 };
 
 #ifndef RSF_MERGE_PROF
@@ -1001,6 +1011,18 @@ __device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const 
   e.p0 = s.p_ent[l * kPend + lane];
 #endif
 }
+// buckets: lanes < np write their group's receiver key (and, when nothing will be emitted,
+// its zero count) into the destination bucket -- the bucket headers come from emission
+// itself, no separate pass over the sorted groups
+__device__ __forceinline__ void bkt_group_keys(const Buckets& bk, uint32_t lane, uint32_t np, uint32_t gk, uint32_t gs,
+                                               bool zero_count) {
+  if (lane >= np) return;
+  const uint32_t w = (uint32_t)(gk / bk.per), idx = gs - bk.wstart[w];
+  if (idx >= bk.gcap) return;  // over the bucket capacity: flagged by the bounds kernel
+  uint32_t* b = bk.send + (uint64_t)w * bk.stride_u32;
+  b[bk.keys_off + idx] = gk;
+  if (zero_count) b[bk.cnt_off + idx] = 0u;
+}
 template <bool BKT>
 __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_t l, uint32_t lane, EmitIn& e,
                                          uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val,
@@ -1015,7 +1037,10 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   const bool ne0 = shfl_u32(Q0.r, 0) != kEmpty || (pc & 0xFF), ne1 = shfl_u32(e.head, 1) != kEmpty || ((pc >> 8) & 0xFF),
              ne2 = shfl_u32(e.head, 2) != kEmpty || ((pc >> 16) & 0xFF);
   // no peers: nothing is sent, and the pending re-queues wait for the next emission
-  if (np == 0 || !(ne0 || ne1 || ne2)) return;
+  if (np == 0 || !(ne0 || ne1 || ne2)) {
+    if (BKT) bkt_group_keys(bk, lane, np, e.gk, e.gs, true);
+    return;
+  }
   EPROF_T(t1);
   EPROF_ADD(0, t0, t1);
   bool d0 = false, d1 = false, d2 = false;
@@ -1041,6 +1066,8 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   if (BKT && lane < np) {
     wdst = (uint32_t)(e.gk / bk.per);
     wfirst = bk.wstart[wdst];
+    const uint32_t idx = e.gs - wfirst;
+    if (idx < bk.gcap) bk.send[(uint64_t)wdst * bk.stride_u32 + bk.keys_off + idx] = e.gk;
   }
   if (ne1) q_load(c, s, l, 1, lane, Q1);
   if (ne2) q_load(c, s, l, 2, lane, Q2);
@@ -1112,7 +1139,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
     used += q_get_broadcasts<false>(c, Q1, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d1, row);
     used += q_get_broadcasts<false>(c, Q2, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d2, row);
 #endif
-    if (lane == 0 && oc && nrec) *oc = min(nrec, c.cap_t);
+    if (lane == 0 && oc && (BKT || nrec)) *oc = min(nrec, c.cap_t);  // buckets: every group's count
   }
 #if RSF_EMIT_LAZY
   q_materialize<true>(c, Q0, lane, cons0, row);
@@ -1153,7 +1180,10 @@ __device__ __forceinline__ void emit_run4(const GCfg& c, const GState& s, const 
   const uint32_t pc = shfl_u32(head, kEhPend), npend = pend_total(pc);
   const bool ne0 = shfl_u32(head, 0) != kEmpty || (pc & 0xFF), ne1 = shfl_u32(head, 1) != kEmpty || ((pc >> 8) & 0xFF),
              ne2 = shfl_u32(head, 2) != kEmpty || ((pc >> 16) & 0xFF);
-  if (np == 0 || !(ne0 || ne1 || ne2)) return;
+  if (np == 0 || !(ne0 || ne1 || ne2)) {
+    if (BKT) bkt_group_keys(bk, lane, np, gk, gs, true);
+    return;
+  }
   bool d0 = false, d1 = false, d2 = false;
   uint32_t err = 0;
   PendRegs pr;
@@ -1162,6 +1192,8 @@ __device__ __forceinline__ void emit_run4(const GCfg& c, const GState& s, const 
   if (BKT && lane < np) {
     wdst = (uint32_t)(gk / bk.per);
     wfirst = bk.wstart[wdst];
+    const uint32_t idx = gs - wfirst;
+    if (idx < bk.gcap) bk.send[(uint64_t)wdst * bk.stride_u32 + bk.keys_off + idx] = gk;
   }
   Q4 Q0, Q1, Q2;
 #pragma unroll
@@ -1222,7 +1254,7 @@ __device__ __forceinline__ void emit_run4(const GCfg& c, const GState& s, const 
     used += q4_get_broadcasts<true>(c, Q0, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d0, row);
     used += q4_get_broadcasts<false>(c, Q1, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d1, row);
     used += q4_get_broadcasts<false>(c, Q2, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d2, row);
-    if (lane == 0 && oc && nrec) *oc = min(nrec, c.cap_t);
+    if (lane == 0 && oc && (BKT || nrec)) *oc = min(nrec, c.cap_t);
   }
   if (d0) q4_store(c, s, l, 0, lane, Q0);
   if (d1) q4_store(c, s, l, 1, lane, Q1);
@@ -1519,10 +1551,14 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
       const uint32_t rel = vi - cr, gr = rel / stride;
       gk = rel - gr * stride;
       const uint64_t g = (uint64_t)sr + gr;
-      const uint32_t* b = bk.base + (uint64_t)r * bk.stride_u32;
+      const uint32_t* b = bk.run(r);
       if (in) {
         rid0 = rec_ld(b + bk.vals_off + g * stride + gk);
+#if RSF_BUCKET_DEC_MODE < 2
         dsub0 = rec_ld(bk.decs + (uint64_t)r * bk.gcap * stride + g * stride + gk);
+#else
+        dsub0 = s.rdec[rid0 & c.rmask];  // decorations do not travel (see Buckets)
+#endif
         gc = rec_ld(b + bk.cnt_off + g);
       }
     } else {
@@ -2255,31 +2291,17 @@ __global__ void bucket_bounds_kernel(const uint32_t* __restrict__ key_s, uint64_
   send[(uint64_t)w * stride_u32] = (uint32_t)(ng < gcap ? ng : gcap);
   if (ng > gcap) atomicOr(flags, 1ull);
 }
-// every group's key in its bucket and a zero count (emission writes the non-empty ones)
-__global__ void __launch_bounds__(256) bucket_fill_kernel(const uint32_t* __restrict__ key_s, uint64_t n, uint64_t per,
-                                                          const uint32_t* __restrict__ wstart, Buckets bk) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t key = key_s[i];
-  if (key == kSentinel) return;
-  const uint32_t w = (uint32_t)(key / per), idx = (uint32_t)(i - wstart[w]);
-  if (idx >= bk.gcap) return;
-  uint32_t* b = bk.send + (uint64_t)w * bk.stride_u32;
-  b[bk.keys_off + idx] = key;
-  b[bk.cnt_off + idx] = 0u;
-}
 // receive side: per (run r, receiver) the range of its groups in bucket r; the records
 // merged (group counts) summed for the statistics; a receiver outside the shard or an
 // unsorted bucket is flagged.  Grid-stride over a bounded grid: one atomic per block (an
 // atomic per 256 groups on one address serialised into ~0.25 ms at 6M groups).
-// With RSF_BUCKET_DEC_FUSED the same pass also rebuilds the decorations of each group's
-// records from the replicated rumor table (bucket_dec_kernel's work, one thread per group
-// instead of one per record slot: measured 0.32 ms per round at 2M members as a kernel of
-// its own, most of it launching and indexing 61M mostly idle threads).
-#ifndef RSF_BUCKET_DEC_FUSED
-#define RSF_BUCKET_DEC_FUSED 1
-#endif
-constexpr unsigned kBucketIndexBlocks = RSF_BUCKET_DEC_FUSED ? 4096 : 1024;
+// RSF_BUCKET_DEC_MODE: where the receive side gets its records' decorations --
+//   0  bucket_dec_kernel rebuilds them into `decs` (one thread per record slot: 0.32 ms per
+//      round at 2M members, most of it launching and indexing 61M mostly idle threads)
+//   1  this pass rebuilds them (one thread per group: measured slower still, 6.24 vs 6.11
+//      ms per round, the per-group loops diverge)
+//   2  the merge looks each one up from the rumor id it has just read (no pass, no array)
+constexpr unsigned kBucketIndexBlocks = RSF_BUCKET_DEC_MODE == 1 ? 4096 : 1024;
 __global__ void __launch_bounds__(256) bucket_index_kernel(Buckets bk, uint64_t lo, uint64_t n_loc,
                                                            uint32_t* __restrict__ rstart, uint32_t* __restrict__ rend,
                                                            unsigned long long* __restrict__ merged,
@@ -2290,7 +2312,7 @@ __global__ void __launch_bounds__(256) bucket_index_kernel(Buckets bk, uint64_t 
   uint64_t sum = 0;
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t r = (uint32_t)(t / bk.gcap), i = (uint32_t)(t % bk.gcap);
-    const uint32_t* b = bk.base + (uint64_t)r * bk.stride_u32;
+    const uint32_t* b = bk.run(r);
     const uint32_t ng = b[0];
     if (i >= ng) continue;
     const uint32_t key = b[bk.keys_off + i];
@@ -2328,7 +2350,7 @@ __global__ void __launch_bounds__(256) bucket_dec_kernel(Buckets bk, uint32_t ca
   const uint32_t r = (uint32_t)(t / per);
   if (r >= bk.n_runs) return;
   const uint64_t i = t - (uint64_t)r * per, grp = i / cap_t;
-  const uint32_t* b = bk.base + (uint64_t)r * bk.stride_u32;
+  const uint32_t* b = bk.run(r);
   if (grp >= b[0] || (uint32_t)(i - grp * cap_t) >= b[bk.cnt_off + grp]) return;
   decs[t] = rdec[b[bk.vals_off + i] & rmask];
 }
@@ -2963,8 +2985,6 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
     const Buckets bk = send_buckets(g);
     hipLaunchKernelGGL(bucket_bounds_kernel, dim3(1), dim3(64), 0, st, (const uint32_t*)g->grp_key_s, ng, bk.per, world,
                        g->d_wstart, g->bkt_send, bk.stride_u32, bk.gcap, g->d_counters + 58);
-    hipLaunchKernelGGL(bucket_fill_kernel, dim3(grid1(ng)), dim3(256), 0, st, (const uint32_t*)g->grp_key_s, ng, bk.per,
-                       (const uint32_t*)g->d_wstart, bk);
     mark(g, 2);
     if (c.qcap > kWave)
       hipLaunchKernelGGL(emit4_kernel<true>, dim3((unsigned)c.n_loc), dim3(kWave), 0, st, c, g->s, g->grp_key,
@@ -3055,6 +3075,7 @@ static Buckets bucket_layout(const rsf_gossip* g, uint32_t world) {
   b.stride_u32 = ((uint64_t)b.vals_off + (uint64_t)b.gcap * c.cap_t + 63) & ~63ull;  // 256-B aligned buckets
   b.per = world ? c.N / world : c.N;
   b.n_runs = world;
+  b.self_run = (uint32_t)(c.lo / b.per);
   return b;
 }
 static Buckets send_buckets(rsf_gossip* g) {
@@ -3113,7 +3134,7 @@ int rsf_gossip_bucket_buffers(rsf_gossip* g, uint32_t world, void** send, void**
     const size_t bytes = (size_t)b.stride_u32 * 4 * world;
     int rc;
     if ((rc = rsf::dmalloc((void**)&g->bkt_send, bytes)) || (rc = rsf::dmalloc((void**)&g->bkt_recv, bytes)) ||
-        (rc = rsf::dmalloc((void**)&g->bkt_dec, (size_t)world * gcap * c.cap_t * 4)) ||
+        (RSF_BUCKET_DEC_MODE < 2 && (rc = rsf::dmalloc((void**)&g->bkt_dec, (size_t)world * gcap * c.cap_t * 4))) ||
         (rc = rsf::dmalloc((void**)&g->d_rstart, (size_t)world * c.n_loc * 4)) ||
         (rc = rsf::dmalloc((void**)&g->d_rend, (size_t)world * c.n_loc * 4)))
       return rc;
@@ -3150,8 +3171,8 @@ int rsf_gossip_round_merge_buckets(rsf_gossip* g, uint32_t world) {
   hipLaunchKernelGGL(bucket_index_kernel, dim3(std::min<uint64_t>(grid1((uint64_t)world * bk.gcap), kBucketIndexBlocks)),
                      dim3(256), 0, st, bk, c.lo, c.n_loc, g->d_rstart, g->d_rend, g->d_counters + 57,
                      g->d_counters + 58, c.cap_t, (const uint32_t*)g->s.rdec, c.rmask,
-                     RSF_BUCKET_DEC_FUSED ? g->bkt_dec : nullptr);
-  if (!RSF_BUCKET_DEC_FUSED)
+                     RSF_BUCKET_DEC_MODE == 1 ? g->bkt_dec : nullptr);
+  if (RSF_BUCKET_DEC_MODE == 0)
     hipLaunchKernelGGL(bucket_dec_kernel, dim3(grid1((uint64_t)world * bk.gcap * c.cap_t)), dim3(256), 0, st, bk,
                        c.cap_t, (const uint32_t*)g->s.rdec, c.rmask, g->bkt_dec);
   hipLaunchKernelGGL(accumulate_kernel, dim3(1), dim3(64), 0, st, g->d_counters, 57u);

@@ -11,8 +11,10 @@ Per round:
        round_emit_buckets  — peer draw, stable sort of the (sender, peer) groups by
                              global receiver, emission straight into one bucket per
                              destination shard
-       all-to-all          — equal splits: bucket w of every rank goes to rank w,
-                             concatenated in source-rank order
+       exchange            — bucket w of every rank goes to slot (source rank) of rank
+                             w's receive buffer: grouped point-to-point sends/receives
+                             (one RCCL group), every pair except the rank's own bucket,
+                             which the merge reads from the send buffer in place
        round_merge_buckets — per receiver, its groups of every source in source-rank
                              order = the canonical (receiver; sender, position) order,
                              merged straight from the received buckets
@@ -94,6 +96,30 @@ def _staged(group, dev):
     # RCCL ("nccl") moves HBM directly; gloo (the CPU rehearsal backend: several ranks
     # sharing one GPU, or CPU stand-ins) needs host tensors, so GPU buffers are staged
     return dist.get_backend(group) == "gloo" and dev.type == "cuda"
+
+
+def exchange_buckets(recv, send, words, rank, world, stage, group=None):
+    """Bucket w of `send` to rank w's slot `rank` of `recv` for every w != rank, one
+    grouped batch of sends/receives (the self bucket is read in place by the merge)."""
+    if world == 1:
+        return
+    if stage:
+        hs, hr = send.cpu(), torch.empty(recv.shape, dtype=recv.dtype)
+    else:
+        hs, hr = send, recv
+    ops = []
+    for w in range(world):
+        if w == rank:
+            continue
+        peer = w if group is None else dist.get_global_rank(group, w)
+        ops.append(dist.P2POp(dist.isend, hs[w * words:(w + 1) * words], peer, group))
+        ops.append(dist.P2POp(dist.irecv, hr[w * words:(w + 1) * words], peer, group))
+    for req in dist.batch_isend_irecv(ops):
+        req.wait()
+    if stage:
+        for w in range(world):
+            if w != rank:
+                recv[w * words:(w + 1) * words].copy_(hr[w * words:(w + 1) * words])
 
 
 def all_to_all(out, inp, stage, group=None, out_splits=None, in_splits=None):
@@ -202,6 +228,26 @@ class ShardedGossip:
         self.dev = self.buf.recv.device
         self.last_in = 0
         self.stage = _staged(group, self.dev)
+        self._timing, self._ev = False, []
+
+    def set_timing(self, on):
+        """Record stream events around the round's collectives (the rumor-block all-reduce
+        and the bucket exchange) for exchange_times(); off by default."""
+        self._timing, self._ev = bool(on) and self.dev.type == "cuda", []
+
+    def _mark(self, events, i):
+        if self._timing:
+            events[i].record()
+
+    def exchange_times(self):
+        """Mean ms per timed round of the rumor-block all-reduce and the bucket exchange
+        (device time between stream events; synchronises)."""
+        if not self._ev:
+            return {}
+        torch.cuda.synchronize()
+        ar = sum(e[0].elapsed_time(e[1]) for e in self._ev) / len(self._ev)
+        ex = sum(e[2].elapsed_time(e[3]) for e in self._ev) / len(self._ev)
+        return {"rumor_block_all_reduce": ar, "bucket_exchange": ex, "rounds": len(self._ev)}
 
     def _all_reduce(self, t):
         if self.stage:
@@ -216,14 +262,21 @@ class ShardedGossip:
 
     def round(self, t, ml=None, acts=None):
         eng, buf = self.eng, self.buf
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if self._timing else None
         eng.round_begin(t, ml, acts)
         blk = buf.rumor_block()
+        self._mark(ev, 0)
         if blk.numel():
             self._all_reduce(blk)
+        self._mark(ev, 1)
         if self.buckets:
             buf.emit()
-            self._all_to_all(buf.recv, buf.send)  # equal splits: one bucket per rank
+            self._mark(ev, 2)
+            exchange_buckets(buf.recv, buf.send, buf.bucket_words, self.rank, self.world, self.stage, self.group)
+            self._mark(ev, 3)
             buf.merge()
+            if ev:
+                self._ev.append(ev)
             return None
         counts = eng.round_emit(self.world)
         send_counts = torch.from_numpy(counts.astype(np.int64)).to(self.dev)

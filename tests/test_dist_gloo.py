@@ -130,18 +130,18 @@ class FakeBucketBuffers:
     merge records what arrived (must be each source's bucket for this rank, in
     source-rank order)."""
 
-    def __init__(self, rank, words=16):
-        self.rank, self.words, self.buckets = rank, words, True
+    def __init__(self, rank, world, words=16):
+        self.rank, self.world, self.words, self.bucket_words, self.buckets = rank, world, words, words, True
         self.block = torch.zeros(12, dtype=torch.int64)
-        self.send = torch.zeros(WORLD * words, dtype=torch.int32)
-        self.recv = torch.zeros(WORLD * words, dtype=torch.int32)
+        self.send = torch.zeros(world * words, dtype=torch.int32)
+        self.recv = torch.zeros(world * words, dtype=torch.int32)
         self.received = []
 
     def rumor_block(self):
         return self.block
 
     def emit(self):
-        for w in range(WORLD):
+        for w in range(self.world):
             self.send[w * self.words:(w + 1) * self.words] = torch.tensor(
                 [1000 * self.rank + 100 * w + i for i in range(self.words)], dtype=torch.int32)
 
@@ -157,13 +157,13 @@ class FakeBeginEngine:
         pass
 
 
-def _worker_buckets(rank, port, q):
+def _worker_buckets(rank, port, q, world):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     from ruserf_amd.dist import ShardedGossip
     from ruserf_amd.gossip import GossipConfig
-    buf = FakeBucketBuffers(rank)
-    sg = ShardedGossip(GossipConfig(n_members=N, n_subjects=4), rank, WORLD, engine=FakeBeginEngine(), buffers=buf)
+    buf = FakeBucketBuffers(rank, world)
+    sg = ShardedGossip(GossipConfig(n_members=N * 3, n_subjects=4), rank, world, engine=FakeBeginEngine(), buffers=buf)
     assert sg.buckets
     sg.round(0)
     assert sg.check()
@@ -172,19 +172,22 @@ def _worker_buckets(rank, port, q):
     dist.destroy_process_group()
 
 
-def test_sharded_round_buckets_gloo():
-    """The bucket exchange: one all-to-all of equal splits, no host-side counts; rank r
-    receives bucket r of every source, in source-rank order."""
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_round_buckets_gloo(world):
+    """The bucket exchange: grouped point-to-point sends/receives, no host-side counts; rank r
+    receives bucket r of every other source, in source-rank order."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 31500 + (os.getpid() % 2000)
-    procs = [ctx.Process(target=_worker_buckets, args=(r, port, q)) for r in range(WORLD)]
+    port = 31500 + world * 2000 + (os.getpid() % 2000)
+    procs = [ctx.Process(target=_worker_buckets, args=(r, port, q, world)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(WORLD))
+    res = dict(q.get(timeout=120) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank in range(WORLD):
-        want = np.concatenate([[1000 * src + 100 * rank + i for i in range(16)] for src in range(WORLD)])
+    for rank in range(world):
+        # the self slot is never filled: the merge reads the rank's own bucket from its send buffer
+        want = np.concatenate([[1000 * src + 100 * rank + i if src != rank else 0 for i in range(16)]
+                               for src in range(world)])
         assert np.array_equal(res[rank], want.astype(np.int32))
