@@ -1,6 +1,7 @@
 #!/bin/bash
 # Builds libruserf_amd variants into ab/ (git-ignored, travels to the GPU box) for A/B
 # timing within one gpurun call (load one with RSF_LIB_PATH=$PWD/ab/lib_NAME.so).
+# REV=<rev> builds gossip.hip as of that git revision instead of the working tree.
 # Only gossip.hip is rebuilt with the extra defines; the other objects come from the main
 # build (make -C ruserf_amd/csrc first).  Usage: build_variants.sh name "-DFLAG=.. ..." ...
 set -e
@@ -11,7 +12,12 @@ mkdir -p ab
 while [ $# -gt 1 ]; do
   name=$1; defs=$2; shift 2
   d=ab/build_$name; mkdir -p $d
-  /opt/rocm/bin/hipcc $F $defs -c $CS/gossip.hip -o $d/gossip.o
+  src=$CS/gossip.hip
+  if [ -n "$REV" ]; then  # REV=<git rev>: gossip.hip (and its headers) as of that revision
+    rm -rf $d/src && mkdir -p $d/src && git archive "$REV" ruserf_amd/csrc include | tar -x -C $d/src
+    src=$d/src/ruserf_amd/csrc/gossip.hip
+  fi
+  /opt/rocm/bin/hipcc $F $defs -c $src -o $d/gossip.o
   objs=""
   for s in capi vivaldi codec coalesce swim intern; do objs="$objs $CS/build/$s.o"; done
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ab/lib_$name.so $d/gossip.o $objs

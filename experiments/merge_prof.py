@@ -38,8 +38,8 @@ L.rsf_gossip_merge_prof(buf)
 v = list(buf)
 names = ["setup", "chunk_loads", "chain_walk", "serial", "stores", "total", "waves"]
 if len(sys.argv) > 2 and sys.argv[2] == "emit":  # a library built with -DRSF_EMIT_PROF=1
-    names = ["rt1_wait", "rt2_pending_apply", "picks", "stores", "-", "total", "waves"]
+    names = ["rt1_wait", "rt2_wait", "pending_apply", "pick_loop", "materialize", "total", "waves", "stores"]
 out = {k: v[i] for i, k in enumerate(names)}
-out["share"] = {k: round(v[i] / max(1, v[5]), 3) for i, k in enumerate(names[:5])}
+out["share"] = {k: round(v[i] / max(1, v[5]), 3) for i, k in enumerate(names) if k not in ("total", "waves")}
 out["cycles_per_wave"] = v[5] / max(1, v[6])
 print(json.dumps(out))

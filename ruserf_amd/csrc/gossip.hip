@@ -220,6 +220,16 @@ __device__ __forceinline__ void q_store(const GCfg& c, const GState& s, uint64_t
 // prune-the-last-item), only the slot order is canonical.
 
 __device__ __forceinline__ uint64_t below_mask(uint32_t lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+// popcount of m over the lanes below this one (v_mbcnt: two vector instructions, no mask build)
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// this lane's bit of a wave-uniform mask (the mask is used as the lane condition directly)
+__device__ __forceinline__ bool lane_bit(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+// popcount of m over the lanes above this one
+__device__ __forceinline__ uint32_t mbcnt_above(uint64_t m) {
+  return (uint32_t)__popcll(m) - mbcnt(m) - (lane_bit(m) ? 1u : 0u);
+}
 
 // insert: position = number of smaller live keys; lanes at/after it shift by
 // one, so on a full queue the last lane (the largest key) falls off = memberlist
@@ -266,7 +276,7 @@ __device__ __forceinline__ uint32_t q_insert_batch(const GCfg& c, QRegs& Q, uint
   const bool valid = lane < c.qcap;
   const bool live = valid && Q.r != kEmpty;
   const uint32_t n_live = (uint32_t)__popcll(ballot(live));
-  const uint32_t myseq = seq0 + (uint32_t)__popcll(newmask & below_mask(lane));
+  const uint32_t myseq = seq0 + mbcnt(newmask);
   const uint64_t nkey = ins ? tlq_key(0, len, myseq) : ~0ull;
   const uint64_t ekey = live ? tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq) : ~0ull;
   uint32_t n_rank = 0, e_less = 0;
@@ -292,8 +302,8 @@ __device__ __forceinline__ uint32_t q_insert_batch(const GCfg& c, QRegs& Q, uint
     dm |= 1ull << d;
     srcn = lane == d ? (uint32_t)k : srcn;
   }
-  const bool is_new = (dm >> lane) & 1;
-  const uint32_t ei = lane - (uint32_t)__popcll(dm & below_mask(lane));
+  const bool is_new = lane_bit(dm);
+  const uint32_t ei = lane - mbcnt(dm);
   const bool is_old = !is_new && valid && ei < n_live;
   const int a_new = (int)(srcn * 4), a_old = (int)((is_old ? ei : lane) * 4);
   const uint32_t nr = (uint32_t)__builtin_amdgcn_ds_bpermute(a_new, (int)rid);
@@ -321,9 +331,7 @@ __device__ __forceinline__ uint32_t q_expire(const GCfg& c, QRegs& Q, uint32_t l
   if (!sm) return 0;
   const bool keep = live && !stale;
   const uint64_t km = ballot(keep), vm = ballot(valid);
-  const uint64_t below = below_mask(lane);
-  const uint32_t pos = keep ? (uint32_t)__popcll(km & below)
-                            : (valid ? (uint32_t)__popcll(km) + (uint32_t)__popcll(vm & ~km & below) : lane);
+  const uint32_t pos = keep ? mbcnt(km) : (valid ? (uint32_t)__popcll(km) + mbcnt(vm & ~km) : lane);
   if (valid && !keep) {
     Q.r = kEmpty;
     Q.sq = 0;
@@ -352,13 +360,12 @@ template <bool PERMUTE_DEC>
 __device__ __forceinline__ void q_rerank(const GCfg& c, QRegs& Q, uint32_t lane, uint64_t pk_m, uint64_t np_m,
                                          QLds& row) {
   const bool valid = lane < c.qcap;
-  const uint64_t below = below_mask(lane);
   const uint64_t kept_m = pk_m | np_m;
-  const bool np = (np_m >> lane) & 1, pk = (pk_m >> lane) & 1;
+  const bool np = lane_bit(np_m), pk = lane_bit(pk_m);
   const uint64_t mykey = tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq);
   uint64_t* const keys_np = reinterpret_cast<uint64_t*>(row.r);  // r + sq: 64 keys
   uint64_t* const keys_pk = reinterpret_cast<uint64_t*>(row.tl);  // tl + dec: 64 keys
-  const uint32_t r_np = (uint32_t)__popcll(np_m & below), r_pk = (uint32_t)__popcll(pk_m & below);
+  const uint32_t r_np = mbcnt(np_m), r_pk = mbcnt(pk_m);
   if (np) keys_np[r_np] = mykey;
   if (pk) keys_pk[r_pk] = mykey;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -379,7 +386,7 @@ __device__ __forceinline__ void q_rerank(const GCfg& c, QRegs& Q, uint32_t lane,
     }
     pos = (np ? r_np : r_pk) + lo;
   } else {
-    pos = valid ? (uint32_t)__popcll(kept_m) + (uint32_t)__popcll(~kept_m & below) : lane;
+    pos = valid ? (uint32_t)__popcll(kept_m) + mbcnt(~kept_m) : lane;
   }
   __builtin_amdgcn_wave_barrier();  // the row is free once every lane has searched it
   const int addr = (int)(pos * 4);
@@ -397,6 +404,9 @@ __device__ __forceinline__ void q_rerank(const GCfg& c, QRegs& Q, uint32_t lane,
 #ifndef RSF_EMIT_NT
 #define RSF_EMIT_NT 0  // emit: records written non-temporally
 #endif
+#ifndef RSF_EMIT_MULTI
+#define RSF_EMIT_MULTI 1  // emit: all peers' picks per queue in one pass (q_pick_peers); 0: per peer (q_get_broadcasts_lazy)
+#endif
 #ifndef RSF_EMIT_LAZY
 #define RSF_EMIT_LAZY 1  // emit: one deferred re-rank per queue per emission (q_get_broadcasts_lazy)
 #endif
@@ -408,7 +418,7 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   const bool valid = lane < c.qcap;
   const uint64_t live_m = ballot(valid && Q.r != kEmpty);  // a sorted queue: a prefix
   if (!live_m) return 0;
-  const bool live = (live_m >> lane) & 1;
+  const bool live = lane_bit(live_m);
   const uint32_t len = Q.tl >> 16;
   // Live items are the sorted prefix.  If every earlier item was taken, item i fits iff
   // the inclusive prefix sum of (overhead + len) is <= limit, so the leading run of picks
@@ -428,10 +438,9 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   }
   if (!pick_m) return used;
   // picks are in ascending lane (= send) order: record rank = picked lanes below
-  const uint64_t below = below_mask(lane);
-  const bool picked = (pick_m >> lane) & 1;
+  const bool picked = lane_bit(pick_m);
   const uint32_t npick = (uint32_t)__popcll(pick_m);
-  const uint32_t rank = (uint32_t)__popcll(pick_m & below);
+  const uint32_t rank = mbcnt(pick_m);
   if (picked && nrec + rank < c.cap_t && stage_val) {
 #if RSF_EMIT_NT
     __builtin_nontemporal_store(Q.r, stage_val + out_base + nrec + rank);
@@ -480,7 +489,7 @@ __device__ __forceinline__ int64_t q_get_broadcasts_lazy(const GCfg& c, QRegs& Q
   if (!cons) t0 = shfl_u32(Q.tl, 0) & 0xFFFF;  // materialised: lane 0 holds the smallest key
   const uint32_t len = Q.tl >> 16;
   const uint64_t a_m = ballot(valid && Q.r != kEmpty && (Q.tl & 0xFFFF) == t0) & ~cons;
-  const bool in_a = (a_m >> lane) & 1;
+  const bool in_a = lane_bit(a_m);
   const uint32_t incl = wave_inclusive_sum_u32(in_a ? c.overhead + len : 0u);
   uint64_t pick_m = limit >= 0 ? (ballot((int64_t)incl <= limit) & a_m) : 0ull;
   int64_t used = pick_m ? (int64_t)shfl_u32(incl, 63 - __clzll((long long)pick_m)) : 0;
@@ -504,10 +513,9 @@ __device__ __forceinline__ int64_t q_get_broadcasts_lazy(const GCfg& c, QRegs& Q
     return q_get_broadcasts<PERMUTE_DEC>(c, Q, lane, limit, stage_val, stage_dec, out_base, nrec, err, dirty, row);
   }
   if (!pick_m) return used;
-  const uint64_t below = below_mask(lane);
-  const bool picked = (pick_m >> lane) & 1;
+  const bool picked = lane_bit(pick_m);
   const uint32_t npick = (uint32_t)__popcll(pick_m);
-  const uint32_t rank = (uint32_t)__popcll(pick_m & below);
+  const uint32_t rank = mbcnt(pick_m);
   if (picked && nrec + rank < c.cap_t && stage_val) {
 #if RSF_EMIT_NT
     __builtin_nontemporal_store(Q.r, stage_val + out_base + nrec + rank);
@@ -525,6 +533,143 @@ __device__ __forceinline__ int64_t q_get_broadcasts_lazy(const GCfg& c, QRegs& Q
   else if (picked) Q.tl = Q.tl + 1;
   cons |= pick_m;
   return used;
+}
+
+// All the fanout peers' get_broadcasts calls on ONE queue in one pass (queue-major emission).
+// A peer's picks from queue q depend only on q's state after the earlier peers' picks from q
+// and on what the peer's earlier queues left of its byte budget, so running queue 0 for every
+// peer, then queue 1, then queue 2 picks exactly what the reference's peer-major
+// broadcast_messages loop picks.  Within a queue this is q_get_broadcasts_lazy's rule for
+// every peer: while all picks come from the queue's lowest transmit class t0 (the leading run
+// of the sorted queue), the send order is [unpicked class-t0 items in lane order] followed by
+// everything else, so ONE prefix sum of the run's costs serves every peer (each peer's prefix
+// is a further stretch of the same sums), the picked items are bumped in place and the re-rank
+// runs once at the end.  Picks are recorded per lane (peer, slot in the peer's group) and
+// written together after the last peer.  When a peer's next candidate could lie past the run,
+// the deferred picks are written and re-ranked into place and the remaining peers run the
+// exact q_get_broadcasts one by one.
+// Per-peer state is lane-distributed: lane j (< np) holds peer j's bytes used so far (used_v),
+// records written so far (nrec_v) and the element offset of its group's record slots from
+// ov / od (off_v; ~0 = no output: a bucket over capacity).
+template <bool PERMUTE_DEC>
+__device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t lane, uint32_t np, uint32_t& used_v,
+                                             uint32_t& nrec_v, uint64_t off_v, uint32_t* ov, uint32_t* od,
+                                             uint32_t& err, bool& dirty, QLds& row, uint64_t* ep = nullptr) {
+  const bool valid = lane < c.qcap;
+  const uint64_t live_m = ballot(valid && Q.r != kEmpty);  // a sorted queue: a prefix
+  if (!live_m) return;
+#if RSF_EMIT_PROF
+  const uint64_t pp0 = __builtin_amdgcn_s_memtime();
+#endif
+  const uint32_t t0 = shfl_u32(Q.tl, 0) & 0xFFFF;  // lane 0 holds the smallest key
+  const uint32_t len = Q.tl >> 16;
+  const uint64_t a_m = ballot(valid && Q.r != kEmpty && (Q.tl & 0xFFFF) == t0);
+  const bool retire_all = t0 + 1 >= c.tx_limit;  // every pick of class t0 retires (or none does)
+  uint32_t incl = wave_inclusive_sum_u32(lane_bit(a_m) ? c.overhead + len : 0u);
+  uint32_t base = 0;      // the sums consumed by the picks so far (while they are a prefix of the run)
+  bool prefix = true;     // the picks so far are a prefix of the class-t0 run
+  uint64_t cons = 0;      // picked so far (all of class t0), bumped in place, not yet written
+  uint64_t gone = 0;      // picked and retiring: no longer candidates
+  uint32_t pk_peer = 0, pk_pos = 0;  // a picked lane: its peer and its slot in the peer's group
+  uint32_t j = 0;
+  bool exact = false;
+  for (; j < np; ++j) {
+    const int64_t limit = (int64_t)c.limit - (int64_t)shfl_u32(used_v, j);
+    const uint64_t rem = a_m & ~cons;
+    if (!prefix) {  // a skip broke the run's prefix: sums of what is left of it
+      incl = wave_inclusive_sum_u32(lane_bit(rem) ? c.overhead + len : 0u);
+      base = 0;
+      prefix = true;
+    }
+    uint64_t pick = limit >= 0 ? (ballot((int64_t)(incl - base) <= limit && incl >= base) & rem) : 0ull;
+    const uint32_t top = pick ? shfl_u32(incl, 63 - __clzll((long long)pick)) : base;
+    int64_t used = (int64_t)(top - base);
+    bool skipped = false;
+    for (;;) {
+      const int64_t free_b = limit - used - (int64_t)c.overhead;
+      if (free_b <= 0) break;
+      const uint64_t fit = ballot((int64_t)len <= free_b) & live_m & ~gone & ~pick;
+      if (!fit) break;
+      const uint64_t cand = fit & rem;
+      if (!cand) {  // the next candidate lies past the class-t0 run (or is a bumped pick)
+        exact = true;
+        break;
+      }
+      const int win = __ffsll((long long)cand) - 1;
+      pick |= 1ull << win;
+      used += (int64_t)c.overhead + shfl_u32(len, win);
+      skipped = true;
+    }
+    if (exact) break;
+    if (pick) {
+      const uint32_t npick = (uint32_t)__popcll(pick);
+      const uint32_t nrec = shfl_u32(nrec_v, j);
+      if (lane_bit(pick)) {
+        pk_peer = j;
+        pk_pos = nrec + mbcnt(pick);  // picks in ascending lane (= send) order
+      }
+      if (nrec + npick > c.cap_t) err |= kErrStage;
+      if (lane == j) nrec_v = nrec + npick;
+      cons |= pick;
+      if (retire_all) gone |= pick;
+      dirty = true;
+      if (skipped) prefix = false;
+      else base = top;
+    }
+    if (lane == j) used_v += (uint32_t)used;
+  }
+#if RSF_EMIT_PROF
+  const uint64_t pp1 = __builtin_amdgcn_s_memtime();
+  ep[0] += pp1 - pp0;  // picks (prefix sums, fit loops)
+  if (exact) ep[4] += 1;  // emissions that needed the exact path
+#endif
+  if (cons) {
+    // the deferred picks: records to their groups, then transmits + 1 or retired
+    const bool picked = lane_bit(cons);
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)off_v, (int)pk_peer);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(off_v >> 32), (int)pk_peer);
+    const uint64_t off = ((uint64_t)hi << 32) | lo;
+    if (picked && pk_pos < c.cap_t && off != ~0ull) {
+#if RSF_EMIT_NT
+      __builtin_nontemporal_store(Q.r, ov + off + pk_pos);
+      if (od) __builtin_nontemporal_store(Q.dec, od + off + pk_pos);
+#else
+      ov[off + pk_pos] = Q.r;
+      if (od) od[off + pk_pos] = Q.dec;
+#endif
+    }
+    if (picked) {
+      if (retire_all) Q.r = kEmpty;
+      else Q.tl = Q.tl + 1;
+    }
+#if RSF_EMIT_PROF
+    const uint64_t pp2 = __builtin_amdgcn_s_memtime();
+    ep[1] += pp2 - pp1;  // deferred stores + bumps
+#endif
+    q_rerank<PERMUTE_DEC>(c, Q, lane, cons & ~gone, live_m & ~cons, row);
+#if RSF_EMIT_PROF
+    ep[2] += __builtin_amdgcn_s_memtime() - pp2;  // re-rank
+#endif
+  }
+#if RSF_EMIT_PROF
+  const uint64_t pp3 = __builtin_amdgcn_s_memtime();
+#endif
+  // the remaining peers exactly, one re-rank after each
+  for (; j < np; ++j) {
+    const int64_t limit = (int64_t)c.limit - (int64_t)shfl_u32(used_v, j);
+    uint32_t nrec = shfl_u32(nrec_v, j);
+    const uint64_t off = shfl_u64(off_v, j);
+    const bool out = off != ~0ull;
+    const int64_t used = q_get_broadcasts<PERMUTE_DEC>(c, Q, lane, limit, out ? ov : nullptr, out ? od : nullptr,
+                                                       out ? off : 0ull, nrec, err, dirty, row);
+    if (lane == j) {
+      used_v += (uint32_t)used;
+      nrec_v = nrec;
+    }
+  }
+#if RSF_EMIT_PROF
+  ep[3] += __builtin_amdgcn_s_memtime() - pp3;  // exact tail
+#endif
 }
 
 // Batched insert of new items (transmits 0, seqs seq0, seq0 + 1, ... in lane order over
@@ -546,8 +691,7 @@ __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, 
   const bool live = valid && Q.r != kEmpty;
   const uint32_t n_live = (uint32_t)__popcll(ballot(live));
   const uint32_t n_new = (uint32_t)__popcll(newmask);
-  const uint64_t below = below_mask(lane), above = ~below & ~(1ull << lane);
-  const uint32_t myseq = seq0 + (uint32_t)__popcll(newmask & below);
+  const uint32_t myseq = seq0 + mbcnt(newmask);
   const bool etx0 = live && (Q.tl & 0xFFFF) == 0;
   const uint32_t elen = Q.tl >> 16;
   uint32_t pos_n = 0, pos_e = lane + ((live && !etx0) ? n_new : 0u);
@@ -558,7 +702,7 @@ __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, 
     rem &= ~same;
     const uint32_t gt_new = (uint32_t)__popcll(ballot(ins && len > L));
     const uint32_t gt_old = (uint32_t)__popcll(ballot(etx0 && elen > L));
-    if (ins && len == L) pos_n = gt_old + gt_new + (uint32_t)__popcll(same & above);
+    if (ins && len == L) pos_n = gt_old + gt_new + mbcnt_above(same);
     if (etx0 && elen <= L) pos_e += (uint32_t)__popcll(same);
   }
   if (ins && pos_n < c.qcap) {
@@ -965,9 +1109,13 @@ struct Buckets {
 #define MPROF_ADD(i, a, b)
 #endif
 #if RSF_EMIT_PROF
+// phase times accumulate in the wave's own (scalar) registers and go out once at the end,
+// spread over 512 counter rows: an atomic on one shared address per phase would make every
+// following phase wait for that contended atomic (vmcnt also counts it)
+__device__ unsigned long long g_eprof[512 * 8];
+__device__ unsigned long long g_eprof2[512 * 8];  // q_pick_peers' own split
 #define EPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#define EPROF_ADD(i, a, b) \
-  if (lane == 0) atomicAdd(&g_merge_prof[i], (unsigned long long)((b) - (a)))
+#define EPROF_ADD(i, a, b) ep_acc[i] += (uint64_t)((b) - (a))
 #else
 #define EPROF_T(v)
 #define EPROF_ADD(i, a, b)
@@ -979,7 +1127,7 @@ struct Buckets {
 // re-queue counts, kEhSeq + q the queues' next insertion seqs, kEhPruned, kEhErr
 enum : uint32_t { kEhPend = 3, kEhSeq = 4, kEhPruned = 7, kEhErr = 8 };
 #ifndef RSF_EMIT_SPEC_PEND
-#define RSF_EMIT_SPEC_PEND 0  // 1: the first 64 pending entries loaded in the first round trip, unconditionally (measured +0.15 ms at 2M: the extra bytes cost more than the round trip)
+#define RSF_EMIT_SPEC_PEND 0  // K > 0: the first K pending entries loaded in the first round trip, unconditionally (K = 64 measured +0.15 ms at 2M: the extra bytes cost more than the round trip)
 #endif
 struct EmitIn {
   QRegs Q0;
@@ -1008,7 +1156,8 @@ __device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const 
 #if RSF_EMIT_SPEC_PEND
   // the pending list's first half does not depend on the count: issued with the first round
   // trip instead of a second one after it (entries past the count are ignored)
-  e.p0 = s.p_ent[l * kPend + lane];
+  e.p0 = GState::PendE{0u, 0u, 0u};
+  if (lane < RSF_EMIT_SPEC_PEND) e.p0 = s.p_ent[l * kPend + lane];
 #endif
 }
 // buckets: lanes < np write their group's receiver key (and, when nothing will be emitted,
@@ -1027,6 +1176,10 @@ template <bool BKT>
 __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_t l, uint32_t lane, EmitIn& e,
                                          uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val,
                                          uint32_t* __restrict__ out_dec, const Buckets& bk, QLds& row) {
+#if RSF_EMIT_PROF
+  uint64_t ep_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t g_eprof_sub[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // inside q_pick_peers (intent queue)
+#endif
   EPROF_T(t0);
   QRegs& Q0 = e.Q0;
   QRegs Q1{kEmpty, 0, 0, kDecQuery}, Q2{kEmpty, 0, 0, kDecEvent};
@@ -1048,15 +1201,13 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   // the pending re-queues (merge_kernel's and the originations' since the last emission)
   PendRegs pr;
 #if RSF_EMIT_SPEC_PEND
-  pr.rid[0] = lane < npend ? e.p0.rid : 0u;
-  pr.dec[0] = lane < npend ? e.p0.dec : 0u;
-  pr.lq[0] = lane < npend ? e.p0.lq : 0u;
-  pr.rid[1] = pr.dec[1] = pr.lq[1] = 0;
-  if (npend > kWave && kWave + lane < npend) {
-    const GState::PendE x = s.p_ent[l * kPend + kWave + lane];
-    pr.rid[1] = x.rid;
-    pr.dec[1] = x.dec;
-    pr.lq[1] = x.lq;
+  if (npend <= RSF_EMIT_SPEC_PEND) {
+    pr.rid[0] = lane < npend ? e.p0.rid : 0u;
+    pr.dec[0] = lane < npend ? e.p0.dec : 0u;
+    pr.lq[0] = lane < npend ? e.p0.lq : 0u;
+    pr.rid[1] = pr.dec[1] = pr.lq[1] = 0;
+  } else {
+    pend_load(s, l, lane, npend, pr);
   }
 #else
   pend_load(s, l, lane, npend, pr);
@@ -1071,6 +1222,11 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   }
   if (ne1) q_load(c, s, l, 1, lane, Q1);
   if (ne2) q_load(c, s, l, 2, lane, Q2);
+#if RSF_EMIT_PROF
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic split: round trip 2 vs the apply
+  EPROF_T(t1b);
+  EPROF_ADD(1, t1, t1b);
+#endif
   if (npend) {
     // applied first: in the reference they were queued when the messages arrived
     uint32_t drops = 0;
@@ -1097,7 +1253,49 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
     }
   }
   EPROF_T(t2);
-  EPROF_ADD(1, t1, t2);
+#if RSF_EMIT_PROF
+  EPROF_ADD(2, t1b, t2);
+#endif
+#if RSF_EMIT_MULTI
+  {
+    // queue-major: every peer's picks from the intent queue, then the query queue, then the
+    // event queue (q_pick_peers).  Lane j < np holds peer j's group: where its records go
+    // (off: element offset from the output base) and where its count goes (oc).
+    if (RSF_BAD2_W(7, !BKT && lane < np && e.gs >= c.n_loc * c.fanout, e.gs)) return;
+    uint64_t off = ~0ull;
+    uint32_t* ov = out_val;
+    uint32_t* od = out_dec;
+    uint32_t* oc = nullptr;
+    if (lane < np) {
+      if (BKT) {
+        const uint32_t idx = e.gs - wfirst;
+        if (idx < bk.gcap) {
+          off = (uint64_t)wdst * bk.stride_u32 + bk.vals_off + (uint64_t)idx * c.cap_t;
+          oc = bk.send + (uint64_t)wdst * bk.stride_u32 + bk.cnt_off + idx;
+        }
+      } else {
+        off = (uint64_t)e.gs * c.cap_t;
+        oc = cnt_s + e.gs;
+      }
+    }
+    if (BKT) {
+      ov = bk.send;
+      od = nullptr;  // decorations are rebuilt on the receive side
+    }
+    uint32_t used_v = 0, nrec_v = 0;
+#if RSF_EMIT_PROF
+    uint64_t* const ep = g_eprof_sub;
+#else
+    uint64_t* const ep = nullptr;
+#endif
+    if (ne0) q_pick_peers<true>(c, Q0, lane, np, used_v, nrec_v, off, ov, od, err, d0, row, ep);
+    if (ne1) q_pick_peers<false>(c, Q1, lane, np, used_v, nrec_v, off, ov, od, err, d1, row);
+    if (ne2) q_pick_peers<false>(c, Q2, lane, np, used_v, nrec_v, off, ov, od, err, d2, row);
+    if (oc && (BKT || nrec_v)) *oc = min(nrec_v, c.cap_t);  // buckets: every group's count
+  }
+  EPROF_T(t2b);
+  EPROF_ADD(3, t2, t2b);
+#else
 #if RSF_EMIT_LAZY
   uint64_t cons0 = 0, cons1 = 0, cons2 = 0;  // picks whose re-rank is deferred (q_get_broadcasts_lazy)
   uint32_t t00 = 0, t01 = 0, t02 = 0;
@@ -1141,22 +1339,33 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
 #endif
     if (lane == 0 && oc && (BKT || nrec)) *oc = min(nrec, c.cap_t);  // buckets: every group's count
   }
+  EPROF_T(t2b);
+  EPROF_ADD(3, t2, t2b);
 #if RSF_EMIT_LAZY
   q_materialize<true>(c, Q0, lane, cons0, row);
   q_materialize<false>(c, Q1, lane, cons1, row);
   q_materialize<false>(c, Q2, lane, cons2, row);
 #endif
+#endif  // RSF_EMIT_MULTI
   EPROF_T(t3);
-  EPROF_ADD(2, t2, t3);
+  EPROF_ADD(4, t2b, t3);
   if (d0) q_store(c, s, l, 0, lane, Q0, true);
   if (d1) q_store(c, s, l, 1, lane, Q1, true);
   if (d2) q_store(c, s, l, 2, lane, Q2, true);
   // flags: a queue prune (counted), a stage overflow (rare); written only when new
   if (lane == kEhErr && (err & ~e.head)) s.err[l] = e.head | err;
   EPROF_T(t4);
-  EPROF_ADD(3, t3, t4);
+  EPROF_ADD(7, t3, t4);
   EPROF_ADD(5, t0, t4);
-  if (lane == 0) { EPROF_ADD(6, 0, 1); }
+#if RSF_EMIT_PROF
+  ep_acc[6] = 1;
+  if (lane == 0)
+    for (int i = 0; i < 8; ++i)
+      if (ep_acc[i]) atomicAdd(&g_eprof[(blockIdx.x & 511) * 8 + i], (unsigned long long)ep_acc[i]);
+  if (lane == 0)
+    for (int i = 0; i < 5; ++i)
+      if (g_eprof_sub[i]) atomicAdd(&g_eprof2[(blockIdx.x & 511) * 8 + i], (unsigned long long)g_eprof_sub[i]);
+#endif
 }
 
 // emission for queues of 65..256 slots (gossip_queue4.h): emit_run's steps with four slots
@@ -1688,7 +1897,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
     const uint64_t newmask = ballot(ins);
     if (newmask) {
       const uint32_t k = (uint32_t)__popcll(newmask);
-      const uint32_t i = pn + (uint32_t)__popcll(newmask & below_mask(lane));
+      const uint32_t i = pn + mbcnt(newmask);
       if (RSF_BAD_W(5, ins && i >= kPend, i)) return;
       if (ins) p_ent[i] = GState::PendE{rid, dsub, ru.msg_len};  // queue 0
       pn += k;
@@ -3284,6 +3493,24 @@ int rsf_gossip_merge_prof(uint64_t* out8) {
   RSF_HIP(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_merge_prof), 8 * sizeof(uint64_t)));
   unsigned long long z[8] = {};
   RSF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_merge_prof), z, sizeof(z)));
+#if RSF_EMIT_PROF
+  {
+    std::vector<unsigned long long> w(512 * 8), zw(512 * 8, 0ull);
+    RSF_HIP(hipMemcpyFromSymbol(w.data(), HIP_SYMBOL(g_eprof), w.size() * sizeof(unsigned long long)));
+    RSF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_eprof), zw.data(), zw.size() * sizeof(unsigned long long)));
+    for (int i = 0; i < 8; ++i) {
+      out8[i] = 0;
+      for (int r = 0; r < 512; ++r) out8[i] += w[r * 8 + i];
+    }
+    RSF_HIP(hipMemcpyFromSymbol(w.data(), HIP_SYMBOL(g_eprof2), w.size() * sizeof(unsigned long long)));
+    RSF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_eprof2), zw.data(), zw.size() * sizeof(unsigned long long)));
+    for (int i = 0; i < 5; ++i) {
+      unsigned long long t = 0;
+      for (int r = 0; r < 512; ++r) t += w[r * 8 + i];
+      fprintf(stderr, "eprof2[%d] %llu\n", i, t);
+    }
+  }
+#endif
   return RSF_OK;
 #else
   (void)out8;

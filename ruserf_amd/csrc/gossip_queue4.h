@@ -251,7 +251,6 @@ __device__ __forceinline__ uint32_t q4_insert_batch(const GCfg& c, Q4& Q, uint32
   bool live[kQK], etx0[kQK];
   uint32_t elen[kQK], pos_e[kQK], cl = 0;
   const uint32_t n_new = (uint32_t)__popcll(newmask);
-  const uint64_t below = below_mask(lane), above = ~below & ~(1ull << lane);
 #pragma unroll
   for (uint32_t k = 0; k < kQK; ++k) {
     live[k] = q4_live(c, Q, lane, k);
@@ -262,7 +261,7 @@ __device__ __forceinline__ uint32_t q4_insert_batch(const GCfg& c, Q4& Q, uint32
   }
   uint32_t n_live;
   (void)lanes_excl(cl, n_live);
-  const uint32_t myseq = seq0 + (uint32_t)__popcll(newmask & below);
+  const uint32_t myseq = seq0 + mbcnt(newmask);
   uint32_t pos_n = 0;
   uint64_t rem = newmask;
   while (rem) {
@@ -275,7 +274,7 @@ __device__ __forceinline__ uint32_t q4_insert_batch(const GCfg& c, Q4& Q, uint32
     for (uint32_t k = 0; k < kQK; ++k) go += (etx0[k] && elen[k] > L) ? 1u : 0u;
     uint32_t gt_old;
     (void)lanes_excl(go, gt_old);
-    if (ins && len == L) pos_n = gt_old + gt_new + (uint32_t)__popcll(same & above);
+    if (ins && len == L) pos_n = gt_old + gt_new + mbcnt_above(same);
 #pragma unroll
     for (uint32_t k = 0; k < kQK; ++k)
       if (etx0[k] && elen[k] <= L) pos_e[k] += (uint32_t)__popcll(same);

@@ -639,6 +639,11 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
 #ifndef RSF_VIV_XCD
 #define RSF_VIV_XCD 0  // 1: XCD-contiguous block order (common.h xcd_block)
 #endif
+#ifndef RSF_VIV_LDS1
+// 1: own rows and peer rows pass through ONE 6 KB LDS block per wave, one after the other
+// (24 KB per block instead of 48), so LDS no longer caps the kernel at 3 waves/SIMD
+#define RSF_VIV_LDS1 0
+#endif
 #ifndef RSF_VIV_NT
 // non-temporal hints (bit 1: member-side loads/stores in the round kernel, 2: its window-slot
 // and window-index stores, 4: the peer gather).  The member-side streams are touched once
@@ -726,15 +731,23 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_pipe_kerne
       }
     }
   }
+#if RSF_VIV_LDS1
+  __shared__ double2 stage[256 / 64][1][64 * 6];
+  double2* so = stage[threadIdx.x / 64][0];
+  double2* sp = so;
+#else
   __shared__ double2 stage[256 / 64][2][64 * 6];
   double2* so = stage[threadIdx.x / 64][0];
   double2* sp = stage[threadIdx.x / 64][1];
+#endif
 #pragma unroll
   for (uint32_t k = 0; k < 6; ++k) so[lane + 64 * k] = own[k];
+#if !RSF_VIV_LDS1
 #pragma unroll
   for (uint32_t ps = 0; ps < 2; ++ps)
 #pragma unroll
     for (int j = 0; j < 3; ++j) sp[(32 * ps + (lane >> 1)) * 6 + half * 3 + j] = g[ps * 3 + j];
+#endif
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   double me[D], other[D], e, a, h, oe, oa, oh;
@@ -743,13 +756,27 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_pipe_kerne
     const double2 t = so[lane * 6 + i];
     me[2 * i] = t.x;
     me[2 * i + 1] = t.y;
-    const double2 u = sp[lane * 6 + i];
-    other[2 * i] = u.x;
-    other[2 * i + 1] = u.y;
   }
   e = so[lane * 6 + 4].x;
   a = so[lane * 6 + 4].y;
   h = so[lane * 6 + 5].x;
+#if RSF_VIV_LDS1
+  // the block is free once every lane has read its own row; the peer rows follow
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (uint32_t ps = 0; ps < 2; ++ps)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) sp[(32 * ps + (lane >> 1)) * 6 + half * 3 + j] = g[ps * 3 + j];
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#endif
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const double2 u = sp[lane * 6 + i];
+    other[2 * i] = u.x;
+    other[2 * i + 1] = u.y;
+  }
   oe = sp[lane * 6 + 4].x;
   oa = sp[lane * 6 + 4].y;
   oh = sp[lane * 6 + 5].x;
