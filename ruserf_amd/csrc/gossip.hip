@@ -361,33 +361,29 @@ __device__ __forceinline__ void q_rerank(const GCfg& c, QRegs& Q, uint32_t lane,
                                          QLds& row) {
   const bool valid = lane < c.qcap;
   const uint64_t kept_m = pk_m | np_m;
-  const bool np = lane_bit(np_m), pk = lane_bit(pk_m);
+  const bool np = lane_bit(np_m), kept = lane_bit(kept_m);
   const uint64_t mykey = tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq);
   uint64_t* const keys_np = reinterpret_cast<uint64_t*>(row.r);  // r + sq: 64 keys
   uint64_t* const keys_pk = reinterpret_cast<uint64_t*>(row.tl);  // tl + dec: 64 keys
-  const uint32_t r_np = mbcnt(np_m), r_pk = mbcnt(pk_m);
-  if (np) keys_np[r_np] = mykey;
-  if (pk) keys_pk[r_pk] = mykey;
+  const uint32_t r_own = np ? mbcnt(np_m) : mbcnt(pk_m);
+  if (kept) (np ? keys_np : keys_pk)[r_own] = mykey;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  uint32_t pos;
-  if (np || pk) {
-    const uint64_t* other = np ? keys_pk : keys_np;
-    uint32_t lo = 0, len = (uint32_t)__popcll(np ? pk_m : np_m);
-    while (len) {  // lower_bound of mykey in the other list
-      const uint32_t half = len >> 1;
-      if (other[lo + half] < mykey) {
-        lo += half + 1;
-        len -= half + 1;
-      } else {
-        len = half;
-      }
-    }
-    pos = (np ? r_np : r_pk) + lo;
-  } else {
-    pos = valid ? (uint32_t)__popcll(kept_m) + mbcnt(~kept_m) : lane;
+  // lower_bound of mykey in the other list, branchless: a keeper's other list holds at most 63
+  // keys (both lists share the wave's 64 lanes), so steps 32 .. 1 reach every count
+  const uint64_t* const other = np ? keys_pk : keys_np;
+  const uint32_t n_pk = (uint32_t)__popcll(pk_m), n_np = (uint32_t)__popcll(np_m);
+  const uint32_t n_other = np ? n_pk : n_np;
+  const uint32_t last = n_other ? n_other - 1 : 0u;
+  uint32_t lo = 0;
+#pragma unroll
+  for (uint32_t step = 32; step; step >>= 1) {
+    const uint32_t probe = lo + step;
+    const uint64_t v = other[min(probe - 1, last)];
+    lo = ((probe <= n_other) & (v < mykey)) ? probe : lo;  // `&`: no short-circuit branch around the read
   }
+  const uint32_t pos = kept ? r_own + lo : (valid ? n_pk + n_np + mbcnt(~kept_m) : lane);
   __builtin_amdgcn_wave_barrier();  // the row is free once every lane has searched it
   const int addr = (int)(pos * 4);
   Q.r = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.r);
@@ -425,12 +421,12 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   // comes out of one wave scan; the remaining budget is then offered to later (shorter)
   // items one by one, as the reference does.
   const uint32_t incl = wave_inclusive_sum_u32(live ? c.overhead + len : 0u);
-  uint64_t pick_m = limit >= 0 ? (ballot((int64_t)incl <= limit) & live_m) : 0ull;
+  uint64_t pick_m = limit >= 0 ? (ballot(incl <= (uint32_t)limit) & live_m) : 0ull;
   int64_t used = pick_m ? (int64_t)shfl_u32(incl, 63 - __clzll((long long)pick_m)) : 0;
   for (;;) {
     const int64_t free_b = limit - used - (int64_t)c.overhead;
     if (free_b <= 0) break;
-    const uint64_t cand = ballot((int64_t)len <= free_b) & live_m & ~pick_m;
+    const uint64_t cand = ballot(len <= (uint32_t)free_b) & live_m & ~pick_m;
     if (!cand) break;
     const int win = __ffsll((long long)cand) - 1;
     pick_m |= 1ull << win;
@@ -455,9 +451,10 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   dirty = true;
   // transmits+1, or retire at the retransmit limit
   const bool retire = picked && (Q.tl & 0xFFFF) + 1 >= c.tx_limit;
-  if (retire) Q.r = kEmpty;
-  else if (picked) Q.tl = Q.tl + 1;
-  q_rerank<PERMUTE_DEC>(c, Q, lane, pick_m & ~ballot(retire), live_m & ~pick_m, row);
+  const uint64_t ret_m = ballot(retire);
+  Q.r = retire ? kEmpty : Q.r;
+  Q.tl = (picked && !retire) ? Q.tl + 1 : Q.tl;
+  q_rerank<PERMUTE_DEC>(c, Q, lane, pick_m & ~ret_m, live_m & ~pick_m, row);
   return used;
 }
 
@@ -563,7 +560,7 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
 #endif
   const uint32_t t0 = shfl_u32(Q.tl, 0) & 0xFFFF;  // lane 0 holds the smallest key
   const uint32_t len = Q.tl >> 16;
-  const uint64_t a_m = ballot(valid && Q.r != kEmpty && (Q.tl & 0xFFFF) == t0);
+  const uint64_t a_m = ballot((Q.tl & 0xFFFF) == t0) & live_m;
   const bool retire_all = t0 + 1 >= c.tx_limit;  // every pick of class t0 retires (or none does)
   uint32_t incl = wave_inclusive_sum_u32(lane_bit(a_m) ? c.overhead + len : 0u);
   uint32_t base = 0;      // the sums consumed by the picks so far (while they are a prefix of the run)
@@ -581,14 +578,15 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
       base = 0;
       prefix = true;
     }
-    uint64_t pick = limit >= 0 ? (ballot((int64_t)(incl - base) <= limit && incl >= base) & rem) : 0ull;
+    // (lanes before the consumed prefix wrap to huge sums and fail the compare; masked anyway)
+    uint64_t pick = limit >= 0 ? (ballot(incl - base <= (uint32_t)limit) & rem) : 0ull;
     const uint32_t top = pick ? shfl_u32(incl, 63 - __clzll((long long)pick)) : base;
     int64_t used = (int64_t)(top - base);
     bool skipped = false;
     for (;;) {
       const int64_t free_b = limit - used - (int64_t)c.overhead;
       if (free_b <= 0) break;
-      const uint64_t fit = ballot((int64_t)len <= free_b) & live_m & ~gone & ~pick;
+      const uint64_t fit = ballot(len <= (uint32_t)free_b) & live_m & ~gone & ~pick;
       if (!fit) break;
       const uint64_t cand = fit & rem;
       if (!cand) {  // the next candidate lies past the class-t0 run (or is a bumped pick)
@@ -604,19 +602,18 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
     if (pick) {
       const uint32_t npick = (uint32_t)__popcll(pick);
       const uint32_t nrec = shfl_u32(nrec_v, j);
-      if (lane_bit(pick)) {
-        pk_peer = j;
-        pk_pos = nrec + mbcnt(pick);  // picks in ascending lane (= send) order
-      }
+      const bool pb = lane_bit(pick);
+      pk_peer = pb ? j : pk_peer;
+      pk_pos = pb ? nrec + mbcnt(pick) : pk_pos;  // picks in ascending lane (= send) order
       if (nrec + npick > c.cap_t) err |= kErrStage;
-      if (lane == j) nrec_v = nrec + npick;
+      nrec_v = lane == j ? nrec + npick : nrec_v;
       cons |= pick;
       if (retire_all) gone |= pick;
       dirty = true;
       if (skipped) prefix = false;
       else base = top;
     }
-    if (lane == j) used_v += (uint32_t)used;
+    used_v += lane == j ? (uint32_t)used : 0u;
   }
 #if RSF_EMIT_PROF
   const uint64_t pp1 = __builtin_amdgcn_s_memtime();
@@ -638,10 +635,8 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
       if (od) od[off + pk_pos] = Q.dec;
 #endif
     }
-    if (picked) {
-      if (retire_all) Q.r = kEmpty;
-      else Q.tl = Q.tl + 1;
-    }
+    Q.r = (picked && retire_all) ? kEmpty : Q.r;
+    Q.tl = (picked && !retire_all) ? Q.tl + 1 : Q.tl;
 #if RSF_EMIT_PROF
     const uint64_t pp2 = __builtin_amdgcn_s_memtime();
     ep[1] += pp2 - pp1;  // deferred stores + bumps
@@ -662,10 +657,8 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
     const bool out = off != ~0ull;
     const int64_t used = q_get_broadcasts<PERMUTE_DEC>(c, Q, lane, limit, out ? ov : nullptr, out ? od : nullptr,
                                                        out ? off : 0ull, nrec, err, dirty, row);
-    if (lane == j) {
-      used_v += (uint32_t)used;
-      nrec_v = nrec;
-    }
+    used_v += lane == j ? (uint32_t)used : 0u;
+    nrec_v = lane == j ? nrec : nrec_v;
   }
 #if RSF_EMIT_PROF
   ep[3] += __builtin_amdgcn_s_memtime() - pp3;  // exact tail
@@ -688,22 +681,24 @@ __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, 
                                                        uint32_t dec, uint32_t len, uint32_t seq0, uint64_t newmask,
                                                        QLds& row) {
   const bool valid = lane < c.qcap;
-  const bool live = valid && Q.r != kEmpty;
-  const uint32_t n_live = (uint32_t)__popcll(ballot(live));
+  const uint64_t live_m = ballot(valid && Q.r != kEmpty);
+  const bool live = lane_bit(live_m);
+  const uint32_t n_live = (uint32_t)__popcll(live_m);
   const uint32_t n_new = (uint32_t)__popcll(newmask);
   const uint32_t myseq = seq0 + mbcnt(newmask);
-  const bool etx0 = live && (Q.tl & 0xFFFF) == 0;
+  const uint64_t etx0_m = ballot((Q.tl & 0xFFFF) == 0) & live_m;  // queued items of transmits 0
   const uint32_t elen = Q.tl >> 16;
-  uint32_t pos_n = 0, pos_e = lane + ((live && !etx0) ? n_new : 0u);
+  uint32_t pos_n = 0, pos_e = lane + (lane_bit(live_m & ~etx0_m) ? n_new : 0u);
+  // one pass per distinct new length, over wave-uniform masks (ins == this lane's bit of newmask)
   uint64_t rem = newmask;
   while (rem) {
     const uint32_t L = shfl_u32(len, __ffsll((long long)rem) - 1);
-    const uint64_t same = ballot(ins && len == L);
+    const uint64_t same = ballot(len == L) & newmask;
     rem &= ~same;
-    const uint32_t gt_new = (uint32_t)__popcll(ballot(ins && len > L));
-    const uint32_t gt_old = (uint32_t)__popcll(ballot(etx0 && elen > L));
-    if (ins && len == L) pos_n = gt_old + gt_new + mbcnt_above(same);
-    if (etx0 && elen <= L) pos_e += (uint32_t)__popcll(same);
+    const uint64_t gt_old_m = ballot(elen > L) & etx0_m;
+    const uint32_t base = (uint32_t)__popcll(ballot(len > L) & newmask) + (uint32_t)__popcll(gt_old_m);
+    pos_n = lane_bit(same) ? base + mbcnt_above(same) : pos_n;
+    pos_e += lane_bit(etx0_m & ~gt_old_m) ? (uint32_t)__popcll(same) : 0u;
   }
   if (ins && pos_n < c.qcap) {
     row.r[pos_n] = rid;
@@ -721,16 +716,16 @@ __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, 
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const uint32_t total = n_live + n_new;
-  if (valid) {
-    if (lane < total) {
-      Q.r = row.r[lane];
-      Q.sq = row.sq[lane];
-      Q.tl = row.tl[lane];
-      if (DEC) Q.dec = row.dec[lane];
-    } else {
-      Q.r = kEmpty;
-      Q.sq = 0;
-      Q.tl = 0;
+  {
+    // every lane reads its slot; lanes past the items (or the queue) select the free value
+    const bool take = valid && lane < total;
+    const uint32_t r = row.r[lane], sq = row.sq[lane], tl = row.tl[lane];
+    Q.r = take ? r : (valid ? kEmpty : Q.r);
+    Q.sq = take ? sq : (valid ? 0u : Q.sq);
+    Q.tl = take ? tl : (valid ? 0u : Q.tl);
+    if (DEC) {
+      const uint32_t d = row.dec[lane];
+      Q.dec = take ? d : Q.dec;
     }
   }
   __builtin_amdgcn_wave_barrier();  // the row is free once every lane has read it
