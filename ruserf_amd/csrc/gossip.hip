@@ -331,7 +331,8 @@ __device__ __forceinline__ uint32_t q_expire(const GCfg& c, QRegs& Q, uint32_t l
   if (!sm) return 0;
   const bool keep = live && !stale;
   const uint64_t km = ballot(keep), vm = ballot(valid);
-  const uint32_t pos = keep ? mbcnt(km) : (valid ? (uint32_t)__popcll(km) + mbcnt(vm & ~km) : lane);
+  const uint32_t mb_k = mbcnt(km), mb_f = mbcnt(vm & ~km);
+  const uint32_t pos = keep ? mb_k : (valid ? (uint32_t)__popcll(km) + mb_f : lane);
   if (valid && !keep) {
     Q.r = kEmpty;
     Q.sq = 0;
@@ -365,7 +366,9 @@ __device__ __forceinline__ void q_rerank(const GCfg& c, QRegs& Q, uint32_t lane,
   const uint64_t mykey = tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq);
   uint64_t* const keys_np = reinterpret_cast<uint64_t*>(row.r);  // r + sq: 64 keys
   uint64_t* const keys_pk = reinterpret_cast<uint64_t*>(row.tl);  // tl + dec: 64 keys
-  const uint32_t r_own = np ? mbcnt(np_m) : mbcnt(pk_m);
+  // (mbcnt is convergent: computed outside any select arm, or the select becomes a branch)
+  const uint32_t mb_np = mbcnt(np_m), mb_pk = mbcnt(pk_m), mb_free = mbcnt(~kept_m);
+  const uint32_t r_own = np ? mb_np : mb_pk;
   if (kept) (np ? keys_np : keys_pk)[r_own] = mykey;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -383,7 +386,8 @@ __device__ __forceinline__ void q_rerank(const GCfg& c, QRegs& Q, uint32_t lane,
     const uint64_t v = other[min(probe - 1, last)];
     lo = ((probe <= n_other) & (v < mykey)) ? probe : lo;  // `&`: no short-circuit branch around the read
   }
-  const uint32_t pos = kept ? r_own + lo : (valid ? n_pk + n_np + mbcnt(~kept_m) : lane);
+  const uint32_t pos_free = valid ? n_pk + n_np + mb_free : lane;
+  const uint32_t pos = kept ? r_own + lo : pos_free;
   __builtin_amdgcn_wave_barrier();  // the row is free once every lane has searched it
   const int addr = (int)(pos * 4);
   Q.r = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)Q.r);
@@ -603,8 +607,9 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
       const uint32_t npick = (uint32_t)__popcll(pick);
       const uint32_t nrec = shfl_u32(nrec_v, j);
       const bool pb = lane_bit(pick);
+      const uint32_t mb = mbcnt(pick);
       pk_peer = pb ? j : pk_peer;
-      pk_pos = pb ? nrec + mbcnt(pick) : pk_pos;  // picks in ascending lane (= send) order
+      pk_pos = pb ? nrec + mb : pk_pos;  // picks in ascending lane (= send) order
       if (nrec + npick > c.cap_t) err |= kErrStage;
       nrec_v = lane == j ? nrec + npick : nrec_v;
       cons |= pick;
@@ -697,7 +702,8 @@ __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, 
     rem &= ~same;
     const uint64_t gt_old_m = ballot(elen > L) & etx0_m;
     const uint32_t base = (uint32_t)__popcll(ballot(len > L) & newmask) + (uint32_t)__popcll(gt_old_m);
-    pos_n = lane_bit(same) ? base + mbcnt_above(same) : pos_n;
+    const uint32_t ab = mbcnt_above(same);
+    pos_n = lane_bit(same) ? base + ab : pos_n;
     pos_e += lane_bit(etx0_m & ~gt_old_m) ? (uint32_t)__popcll(same) : 0u;
   }
   if (ins && pos_n < c.qcap) {
@@ -720,9 +726,10 @@ __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, 
     // every lane reads its slot; lanes past the items (or the queue) select the free value
     const bool take = valid && lane < total;
     const uint32_t r = row.r[lane], sq = row.sq[lane], tl = row.tl[lane];
-    Q.r = take ? r : (valid ? kEmpty : Q.r);
-    Q.sq = take ? sq : (valid ? 0u : Q.sq);
-    Q.tl = take ? tl : (valid ? 0u : Q.tl);
+    const uint32_t fr = valid ? kEmpty : Q.r, fs = valid ? 0u : Q.sq, ft = valid ? 0u : Q.tl;
+    Q.r = take ? r : fr;
+    Q.sq = take ? sq : fs;
+    Q.tl = take ? tl : ft;
     if (DEC) {
       const uint32_t d = row.dec[lane];
       Q.dec = take ? d : Q.dec;
