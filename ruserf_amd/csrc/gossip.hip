@@ -1229,9 +1229,10 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   EPROF_T(t1b);
   EPROF_ADD(1, t1, t1b);
 #endif
+  uint32_t drops_all = 0;
   if (npend) {
     // applied first: in the reference they were queued when the messages arrived
-    uint32_t drops = 0;
+    uint32_t& drops = drops_all;
     if (pc & 0xFF) {
       drops += pend_apply<true>(c, Q0, lane, 0, npend, pr, shfl_u32(e.head, kEhSeq), row);
       d0 = true;
@@ -1244,15 +1245,9 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
       drops += pend_apply<false>(c, Q2, lane, 2, npend, pr, shfl_u32(e.head, kEhSeq + 2), row);
       d2 = true;
     }
-    if (lane == kEhPend) s.p_cnt[l] = 0;
-    if (lane >= kEhSeq && lane < kEhSeq + 3) {
-      const uint32_t nq = (pc >> (8 * (lane - kEhSeq))) & 0xFF;
-      if (nq) s.q_next_seq[l * 3 + (lane - kEhSeq)] = e.head + nq;
-    }
-    if (drops) {
-      if (lane == kEhPruned) s.q_pruned[l] = e.head + drops;
-      err |= kErrQueue;
-    }
+    if (drops) err |= kErrQueue;
+    // (the list's bookkeeping -- count, next seqs, prune count -- is written at the end: a store
+    // here would make the compiler wait for it before reusing its registers)
   }
   EPROF_T(t2);
 #if RSF_EMIT_PROF
@@ -1354,8 +1349,20 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   if (d0) q_store(c, s, l, 0, lane, Q0, true);
   if (d1) q_store(c, s, l, 1, lane, Q1, true);
   if (d2) q_store(c, s, l, 2, lane, Q2, true);
-  // flags: a queue prune (counted), a stage overflow (rare); written only when new
-  if (lane == kEhErr && (err & ~e.head)) s.err[l] = e.head | err;
+  // the member's bookkeeping as ONE lane-distributed store (each lane of `head` writes its own
+  // word back where it changed): the applied pending list's count (0) and the queues' next
+  // seqs, the prune count, the error flags (a queue prune, a stage overflow; only when new)
+  {
+    const uint32_t qi = lane - kEhSeq;
+    const uint32_t nq = qi < 3 ? (pc >> (8 * qi)) & 0xFF : 0u;
+    const bool w_pend = npend && lane == kEhPend, w_seq = npend && nq != 0;
+    const bool w_pr = drops_all && lane == kEhPruned, w_err = lane == kEhErr && (err & ~e.head);
+    uint32_t* const base = w_pend ? s.p_cnt : w_seq ? s.q_next_seq : w_pr ? s.q_pruned : s.err;
+    const uint64_t idx = w_seq ? l * 3 + qi : l;
+    const uint32_t v = w_pend ? 0u : w_seq ? e.head + nq : w_pr ? e.head + drops_all : (e.head | err);
+    if (w_pend || w_seq || w_pr || w_err) base[idx] = v;
+  }
+
   EPROF_T(t4);
   EPROF_ADD(7, t3, t4);
   EPROF_ADD(5, t0, t4);
@@ -1485,11 +1492,15 @@ __global__ void __launch_bounds__(64) emit4_kernel(GCfg c, GState s, const uint3
   emit_run4<BKT>(c, s, grp_key, slot, l, lane, cnt_s, out_val, out_dec, bk, row);
 }
 
-template <bool BKT>
-__global__ void __launch_bounds__(64 * RSF_EMIT_WPB) emit_kernel(GCfg c, GState s, const uint32_t* __restrict__ grp_key,
+// FULL: queue_cap == 64 (one slot per lane of the wave), known at compile time -- every
+// `lane < qcap` test and its branch fold away (the bench configuration)
+template <bool BKT, bool FULL>
+__global__ void __launch_bounds__(64 * RSF_EMIT_WPB) emit_kernel(GCfg c_in, GState s, const uint32_t* __restrict__ grp_key,
                                                    const uint32_t* __restrict__ slot, uint32_t* __restrict__ cnt_s,
                                                    uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec,
                                                    Buckets bk) {
+  GCfg c = c_in;
+  if (FULL) c.qcap = kWave;
   __shared__ QLds rows[RSF_EMIT_WPB];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   QLds& row = rows[threadIdx.x / kWave];
@@ -3200,9 +3211,12 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
     if (c.qcap > kWave)
       hipLaunchKernelGGL(emit4_kernel<true>, dim3((unsigned)c.n_loc), dim3(kWave), 0, st, c, g->s, g->grp_key,
                          g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk);
+    else if (c.qcap == kWave)
+      hipLaunchKernelGGL((emit_kernel<true, true>), egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key,
+                         g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk);
     else
-      hipLaunchKernelGGL(emit_kernel<true>, egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key, g->grp_slot,
-                         g->grp_cnt, g->stage_val, g->stage_dec, bk);
+      hipLaunchKernelGGL((emit_kernel<true, false>), egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key,
+                         g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk);
     RSF_HIP(hipGetLastError());
     mark(g, 3);
     return RSF_OK;
@@ -3211,9 +3225,12 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
   if (c.qcap > kWave)
     hipLaunchKernelGGL(emit4_kernel<false>, dim3((unsigned)c.n_loc), dim3(kWave), 0, st, c, g->s, g->grp_key,
                        g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, Buckets{});
+  else if (c.qcap == kWave)
+    hipLaunchKernelGGL((emit_kernel<false, true>), egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key,
+                       g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, Buckets{});
   else
-    hipLaunchKernelGGL(emit_kernel<false>, egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key, g->grp_slot,
-                       g->grp_cnt, g->stage_val, g->stage_dec, Buckets{});
+    hipLaunchKernelGGL((emit_kernel<false, false>), egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key,
+                       g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, Buckets{});
   RSF_HIP(hipGetLastError());
   RSF_DBG_SYNC(st, "emit_kernel");
   if (local) {
