@@ -1449,6 +1449,36 @@ __device__ __forceinline__ void emit_run4(const GCfg& c, const GState& s, const 
       err |= kErrQueue;
     }
   }
+#if RSF_EMIT_MULTI
+  {
+    // queue-major, as emit_run: every peer's picks from each queue in one pass (q4_pick_peers)
+    uint64_t off = ~0ull;
+    uint32_t* ov = out_val;
+    uint32_t* od = out_dec;
+    uint32_t* oc = nullptr;
+    if (lane < np) {
+      if (BKT) {
+        const uint32_t idx = gs - wfirst;
+        if (idx < bk.gcap) {
+          off = (uint64_t)wdst * bk.stride_u32 + bk.vals_off + (uint64_t)idx * c.cap_t;
+          oc = bk.send + (uint64_t)wdst * bk.stride_u32 + bk.cnt_off + idx;
+        }
+      } else {
+        off = (uint64_t)gs * c.cap_t;
+        oc = cnt_s + gs;
+      }
+    }
+    if (BKT) {
+      ov = bk.send;
+      od = nullptr;
+    }
+    uint32_t used_v = 0, nrec_v = 0;
+    if (ne0) q4_pick_peers<true>(c, Q0, lane, np, used_v, nrec_v, off, ov, od, err, d0, row);
+    if (ne1) q4_pick_peers<false>(c, Q1, lane, np, used_v, nrec_v, off, ov, od, err, d1, row);
+    if (ne2) q4_pick_peers<false>(c, Q2, lane, np, used_v, nrec_v, off, ov, od, err, d2, row);
+    if (oc && (BKT || nrec_v)) *oc = min(nrec_v, c.cap_t);
+  }
+#else
   for (uint32_t j = 0; j < np; ++j) {
     const uint32_t gslot = shfl_u32(gs, j);
     uint64_t out_base = (uint64_t)gslot * c.cap_t;
@@ -1474,6 +1504,7 @@ __device__ __forceinline__ void emit_run4(const GCfg& c, const GState& s, const 
     used += q4_get_broadcasts<false>(c, Q2, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d2, row);
     if (lane == 0 && oc && (BKT || nrec)) *oc = min(nrec, c.cap_t);
   }
+#endif
   if (d0) q4_store(c, s, l, 0, lane, Q0);
   if (d1) q4_store(c, s, l, 1, lane, Q1);
   if (d2) q4_store(c, s, l, 2, lane, Q2);

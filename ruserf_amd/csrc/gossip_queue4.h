@@ -144,21 +144,19 @@ __device__ __forceinline__ void q4_rerank(const GCfg& c, Q4& Q, uint32_t lane, c
   uint32_t dst[kQK];
 #pragma unroll
   for (uint32_t k = 0; k < kQK; ++k) {
-    dst[k] = kEmpty;
-    if (np[k] || pk[k]) {
-      const uint64_t* other = np[k] ? keys_pk : keys_np;
-      uint32_t lo = 0, len = np[k] ? n_pk : n_np;
-      while (len) {  // lower_bound of key in the other list
-        const uint32_t half = len >> 1;
-        if (other[lo + half] < key[k]) {
-          lo += half + 1;
-          len -= half + 1;
-        } else {
-          len = half;
-        }
-      }
-      dst[k] = rk[k] + lo;
+    // lower_bound of the key in the other list, branchless (a keeper's other list holds at
+    // most 255 keys: steps 128 .. 1 reach every count); non-keepers search harmlessly
+    const uint64_t* other = np[k] ? keys_pk : keys_np;
+    const uint32_t n_other = np[k] ? n_pk : n_np;
+    const uint32_t last = n_other ? n_other - 1 : 0u;
+    uint32_t lo = 0;
+#pragma unroll
+    for (uint32_t step = 128; step; step >>= 1) {
+      const uint32_t probe = lo + step;
+      const uint64_t v = other[min(probe - 1, last)];
+      lo = ((probe <= n_other) & (v < key[k])) ? probe : lo;  // `&`: no branch around the read
     }
+    dst[k] = (np[k] || pk[k]) ? rk[k] + lo : kEmpty;
   }
   q4_scatter<DEC>(c, Q, lane, dst, n_np + n_pk, row);  // (it fences the searches first)
 }
@@ -239,6 +237,147 @@ __device__ __forceinline__ int64_t q4_get_broadcasts(const GCfg& c, Q4& Q, uint3
   dirty = true;
   q4_rerank<DEC>(c, Q, lane, np, pk, row);
   return used;
+}
+
+// All the fanout peers' picks from one four-slot-per-lane queue in one pass (q_pick_peers):
+// while every pick comes from the lowest transmit class t0 (the leading run of the sorted
+// queue) one prefix sum serves every peer, picks are bumped in place and written together,
+// and the re-rank runs once; a peer whose next candidate could lie past the run sends the
+// rest through the exact q4_get_broadcasts.  Lane-distributed per-peer state as in
+// q_pick_peers (used_v, nrec_v, off_v).
+template <bool DEC>
+__device__ __forceinline__ void q4_pick_peers(const GCfg& c, Q4& Q, uint32_t lane, uint32_t np, uint32_t& used_v,
+                                              uint32_t& nrec_v, uint64_t off_v, uint32_t* ov, uint32_t* od,
+                                              uint32_t& err, bool& dirty, QLds4& row) {
+  bool live[kQK], a[kQK], cons[kQK], gone[kQK];
+  uint32_t len[kQK], incl[kQK], pk_peer[kQK], pk_pos[kQK];
+  if (!ballot(q4_live(c, Q, lane, 0))) return;  // a sorted queue: empty iff slot 0 is free
+  const uint32_t t0 = shfl_u32(Q.tl[0], 0) & 0xFFFF;  // slot 0 holds the smallest key
+  const bool retire_all = t0 + 1 >= c.tx_limit;
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) {
+    live[k] = q4_live(c, Q, lane, k);
+    len[k] = Q.tl[k] >> 16;
+    a[k] = live[k] && (Q.tl[k] & 0xFFFF) == t0;
+    cons[k] = gone[k] = false;
+    pk_peer[k] = pk_pos[k] = 0;
+  }
+  // inclusive prefix sums of the costs over the slots of `m` (slot order = lane major)
+  auto scan = [&](const bool (&m)[kQK]) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kQK; ++k) {
+      acc += m[k] ? c.overhead + len[k] : 0u;
+      incl[k] = acc;
+    }
+    uint32_t tot;
+    const uint32_t b = lanes_excl(acc, tot);
+#pragma unroll
+    for (uint32_t k = 0; k < kQK; ++k) incl[k] += b;
+  };
+  scan(a);
+  uint32_t base = 0;
+  bool prefix = true;
+  uint32_t j = 0;
+  bool exact = false;
+  for (; j < np; ++j) {
+    const int64_t limit = (int64_t)c.limit - (int64_t)shfl_u32(used_v, j);
+    bool rem[kQK], pick[kQK];
+#pragma unroll
+    for (uint32_t k = 0; k < kQK; ++k) rem[k] = a[k] && !cons[k];
+    if (!prefix) {
+      scan(rem);
+      base = 0;
+      prefix = true;
+    }
+    uint32_t mx = 0;  // the prefix sum at the last slot of the leading run that fits
+#pragma unroll
+    for (uint32_t k = 0; k < kQK; ++k) {
+      pick[k] = limit >= 0 && rem[k] && incl[k] - base <= (uint32_t)limit;
+      mx = pick[k] ? incl[k] : mx;
+    }
+    const uint32_t top = ballot(mx != 0) ? (uint32_t)wave_max_u64(mx) : base;
+    int64_t used = (int64_t)(top - base);
+    bool skipped = false;
+    for (;;) {
+      const int64_t free_b = limit - used - (int64_t)c.overhead;
+      if (free_b <= 0) break;
+      uint32_t first_fit = kQK, first_cand = kQK;  // this lane's first fitting / candidate slot
+#pragma unroll
+      for (int k = kQK - 1; k >= 0; --k) {
+        const bool f = live[k] && !gone[k] && !pick[k] && len[k] <= (uint32_t)free_b;
+        first_fit = f ? (uint32_t)k : first_fit;
+        first_cand = (f && rem[k]) ? (uint32_t)k : first_cand;
+      }
+      if (!ballot(first_fit < kQK)) break;
+      const uint64_t cm = ballot(first_cand < kQK);
+      if (!cm) {  // the next candidate lies past the class-t0 run (or is a bumped pick)
+        exact = true;
+        break;
+      }
+      const int wl = __ffsll((long long)cm) - 1;
+      const uint32_t wk = shfl_u32(first_cand, wl);
+#pragma unroll
+      for (uint32_t k = 0; k < kQK; ++k) pick[k] = pick[k] || ((int)lane == wl && k == wk);
+      used += (int64_t)c.overhead + shfl_u32(q4_pick(len, wk), wl);
+      skipped = true;
+    }
+    if (exact) break;
+    uint32_t pl = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kQK; ++k) pl += pick[k];
+    uint32_t npick;
+    uint32_t rank = lanes_excl(pl, npick);
+    if (npick) {
+      const uint32_t nrec = shfl_u32(nrec_v, j);
+#pragma unroll
+      for (uint32_t k = 0; k < kQK; ++k) {
+        pk_peer[k] = pick[k] ? j : pk_peer[k];
+        pk_pos[k] = pick[k] ? nrec + rank : pk_pos[k];  // picks in slot (= send) order
+        rank += pick[k] ? 1u : 0u;
+        cons[k] = cons[k] || pick[k];
+        gone[k] = gone[k] || (pick[k] && retire_all);
+      }
+      if (nrec + npick > c.cap_t) err |= kErrStage;
+      nrec_v = lane == j ? nrec + npick : nrec_v;
+      dirty = true;
+      if (skipped) prefix = false;
+      else base = top;
+    }
+    used_v += lane == j ? (uint32_t)used : 0u;
+  }
+  bool any = false;
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) any = any || cons[k];
+  if (ballot(any)) {
+    // the deferred picks: records to their groups, then transmits + 1 or retired, one re-rank
+    bool npk[kQK], pkk[kQK];
+#pragma unroll
+    for (uint32_t k = 0; k < kQK; ++k) {
+      const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)off_v, (int)pk_peer[k]);
+      const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(off_v >> 32), (int)pk_peer[k]);
+      const uint64_t off = ((uint64_t)hi << 32) | lo;
+      if (cons[k] && pk_pos[k] < c.cap_t && off != ~0ull) {
+        ov[off + pk_pos[k]] = Q.r[k];
+        if (od) od[off + pk_pos[k]] = Q.dec[k];
+      }
+      npk[k] = live[k] && !cons[k];
+      pkk[k] = cons[k] && !gone[k];
+      Q.r[k] = (cons[k] && retire_all) ? kEmpty : Q.r[k];
+      Q.tl[k] = (cons[k] && !retire_all) ? Q.tl[k] + 1 : Q.tl[k];
+    }
+    q4_rerank<DEC>(c, Q, lane, npk, pkk, row);
+  }
+  for (; j < np; ++j) {  // the remaining peers exactly, one re-rank after each
+    const int64_t limit = (int64_t)c.limit - (int64_t)shfl_u32(used_v, j);
+    uint32_t nrec = shfl_u32(nrec_v, j);
+    const uint64_t off = shfl_u64(off_v, j);
+    const bool out = off != ~0ull;
+    const int64_t used = q4_get_broadcasts<DEC>(c, Q, lane, limit, out ? ov : nullptr, out ? od : nullptr,
+                                                out ? off : 0ull, nrec, err, dirty, row);
+    used_v += lane == j ? (uint32_t)used : 0u;
+    nrec_v = lane == j ? nrec : nrec_v;
+  }
 }
 
 // Batched insert of new items (q_insert_batch_lds): lane i offers at most one new item
