@@ -1168,7 +1168,7 @@ __device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const 
 __device__ __forceinline__ void bkt_group_keys(const Buckets& bk, uint32_t lane, uint32_t np, uint32_t gk, uint32_t gs,
                                                bool zero_count) {
   if (lane >= np) return;
-  const uint32_t w = (uint32_t)(gk / bk.per), idx = gs - bk.wstart[w];
+  const uint32_t w = gk / (uint32_t)bk.per, idx = gs - bk.wstart[w];  // members per shard < 2^32: a 32-bit division
   if (idx >= bk.gcap) return;  // over the bucket capacity: flagged by the bounds kernel
   uint32_t* b = bk.send + (uint64_t)w * bk.stride_u32;
   b[bk.keys_off + idx] = gk;
@@ -1217,7 +1217,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   // buckets: each peer's destination shard and that bucket's first group (same round trip)
   uint32_t wdst = 0, wfirst = 0;
   if (BKT && lane < np) {
-    wdst = (uint32_t)(e.gk / bk.per);
+    wdst = e.gk / (uint32_t)bk.per;  // 32-bit division (members per shard < 2^32)
     wfirst = bk.wstart[wdst];
     const uint32_t idx = e.gs - wfirst;
     if (idx < bk.gcap) bk.send[(uint64_t)wdst * bk.stride_u32 + bk.keys_off + idx] = e.gk;
@@ -1408,7 +1408,7 @@ __device__ __forceinline__ void emit_run4(const GCfg& c, const GState& s, const 
   pend_load(s, l, lane, npend, pr);
   uint32_t wdst = 0, wfirst = 0;
   if (BKT && lane < np) {
-    wdst = (uint32_t)(gk / bk.per);
+    wdst = gk / (uint32_t)bk.per;
     wfirst = bk.wstart[wdst];
     const uint32_t idx = gs - wfirst;
     if (idx < bk.gcap) bk.send[(uint64_t)wdst * bk.stride_u32 + bk.keys_off + idx] = gk;
