@@ -369,23 +369,22 @@ __device__ __forceinline__ void q_rerank(const GCfg& c, QRegs& Q, uint32_t lane,
   // (mbcnt is convergent: computed outside any select arm, or the select becomes a branch)
   const uint32_t mb_np = mbcnt(np_m), mb_pk = mbcnt(pk_m), mb_free = mbcnt(~kept_m);
   const uint32_t r_own = np ? mb_np : mb_pk;
+  // both lists padded with keys above every real one (LDS writes of a wave land in order, so
+  // the real keys overwrite the padding): the search needs no bounds test
+  keys_np[lane] = ~0ull;
+  keys_pk[lane] = ~0ull;
   if (kept) (np ? keys_np : keys_pk)[r_own] = mykey;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // lower_bound of mykey in the other list, branchless: a keeper's other list holds at most 63
-  // keys (both lists share the wave's 64 lanes), so steps 32 .. 1 reach every count
+  // keys (both lists share the wave's 64 lanes), so steps 32 .. 1 reach every count, and the
+  // probes stay inside the 64-key row
   const uint64_t* const other = np ? keys_pk : keys_np;
   const uint32_t n_pk = (uint32_t)__popcll(pk_m), n_np = (uint32_t)__popcll(np_m);
-  const uint32_t n_other = np ? n_pk : n_np;
-  const uint32_t last = n_other ? n_other - 1 : 0u;
   uint32_t lo = 0;
 #pragma unroll
-  for (uint32_t step = 32; step; step >>= 1) {
-    const uint32_t probe = lo + step;
-    const uint64_t v = other[min(probe - 1, last)];
-    lo = ((probe <= n_other) & (v < mykey)) ? probe : lo;  // `&`: no short-circuit branch around the read
-  }
+  for (uint32_t step = 32; step; step >>= 1) lo = other[lo + step - 1] < mykey ? lo + step : lo;
   const uint32_t pos_free = valid ? n_pk + n_np + mb_free : lane;
   const uint32_t pos = kept ? r_own + lo : pos_free;
   __builtin_amdgcn_wave_barrier();  // the row is free once every lane has searched it

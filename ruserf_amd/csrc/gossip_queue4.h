@@ -131,6 +131,13 @@ __device__ __forceinline__ void q4_rerank(const GCfg& c, Q4& Q, uint32_t lane, c
   uint64_t* const keys_np = reinterpret_cast<uint64_t*>(row.r);   // r + sq: 256 keys
   uint64_t* const keys_pk = reinterpret_cast<uint64_t*>(row.tl);  // tl + dec: 256 keys
   lds_fence_wave();
+  // both lists padded with keys above every real one (the real keys overwrite the padding:
+  // LDS writes of a wave land in order), so the search needs no bounds test
+#pragma unroll
+  for (uint32_t k = 0; k < kQK; ++k) {
+    keys_np[lane * kQK + k] = ~0ull;
+    keys_pk[lane * kQK + k] = ~0ull;
+  }
   uint64_t key[kQK];
   uint32_t rk[kQK];
 #pragma unroll
@@ -147,15 +154,9 @@ __device__ __forceinline__ void q4_rerank(const GCfg& c, Q4& Q, uint32_t lane, c
     // lower_bound of the key in the other list, branchless (a keeper's other list holds at
     // most 255 keys: steps 128 .. 1 reach every count); non-keepers search harmlessly
     const uint64_t* other = np[k] ? keys_pk : keys_np;
-    const uint32_t n_other = np[k] ? n_pk : n_np;
-    const uint32_t last = n_other ? n_other - 1 : 0u;
     uint32_t lo = 0;
 #pragma unroll
-    for (uint32_t step = 128; step; step >>= 1) {
-      const uint32_t probe = lo + step;
-      const uint64_t v = other[min(probe - 1, last)];
-      lo = ((probe <= n_other) & (v < key[k])) ? probe : lo;  // `&`: no branch around the read
-    }
+    for (uint32_t step = 128; step; step >>= 1) lo = other[lo + step - 1] < key[k] ? lo + step : lo;
     dst[k] = (np[k] || pk[k]) ? rk[k] + lo : kEmpty;
   }
   q4_scatter<DEC>(c, Q, lane, dst, n_np + n_pk, row);  // (it fences the searches first)
