@@ -549,3 +549,28 @@ def test_configs3_100k_churn_flood_coalesce():
             [(int(x["name"]), int(x["ltime"]), int(x["payload"])) for x in mine]
     g.close()
     L.orc_world_free(C.byref(w))
+
+
+@pytest.mark.parametrize("qcap,fanout,mult,limit", [(64, 1, 1, 300), (64, 5, 2, 240), (64, 3, 1, 90),
+                                                    (256, 4, 1, 260), (100, 2, 3, 500)])
+def test_emission_pick_paths_bit_exact(qcap, fanout, mult, limit):
+    """The queue-major emission (every peer's picks from one queue in a pass, q_pick_peers /
+    q4_pick_peers) on the paths the bench shape rarely takes: one and five peers; a
+    retransmit limit of 1-3 (every pick of a class retires, or classes run out within one
+    emission and the exact per-peer fallback takes over); budgets that leave room for later
+    shorter items (user events and queries of many lengths: skips break the prefix run);
+    bit-exact against the oracle's per-peer broadcast_messages after every round."""
+    n, rounds = 1500, 14
+    subj, acts, ml = W.churn_workload(n, rounds, events_per_round=40, queries_per_round=6, seed=qcap * 7 + fanout)
+    s = len(subj)
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=qcap, gossip_limit=limit, gossip_overhead=3,
+                         fanout=fanout, retransmit_mult=mult, max_rumors=1 << 14, event_buffer_size=128,
+                         query_buffer_size=128, slot_k=8)
+    g, w = pair(cfg, subj, W.initial_views(s))
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t])
+        H.assert_same(H.engine_state(g), H.world_state(w), f"round {t}")
+    assert w.merges > 0
+    g.close()
+    L.orc_world_free(C.byref(w))
