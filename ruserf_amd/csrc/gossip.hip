@@ -1034,15 +1034,25 @@ __global__ void __launch_bounds__(256) peers_kernel(GCfg c, GState s, uint32_t r
 // After the stable sort of the groups by receiver: slot[gid] = the group's position in
 // receiver order (where emit_kernel writes its records: cap_t slots per group), and, for
 // a context that merges its own records, each receiver's range of groups.
+// Bucket emission (wstart non-null): a group's slot word is its destination shard w (top
+// kBktWBits bits) and its place in that shard's bucket (i - wstart[w]), so emission needs
+// neither a division nor a dependent load of wstart.
+constexpr uint32_t kBktWShift = 26, kBktIdxMask = (1u << kBktWShift) - 1;
 __global__ void __launch_bounds__(256) grp_index_kernel(const uint32_t* __restrict__ key_s,
                                                         const uint32_t* __restrict__ id_s, uint64_t n, uint64_t lo,
                                                         uint32_t* __restrict__ slot, uint32_t* __restrict__ seg_start,
-                                                        uint32_t* __restrict__ seg_end) {
+                                                        uint32_t* __restrict__ seg_end,
+                                                        const uint32_t* __restrict__ wstart = nullptr, uint32_t per = 0) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t key = key_s[i];
   if (key == kSentinel) return;
   if (RSF_BAD(2, id_s[i] >= n, id_s[i]) || RSF_BAD(3, seg_start && key - lo >= n, key)) return;
+  if (wstart) {
+    const uint32_t w = key / per;
+    slot[id_s[i]] = (w << kBktWShift) | (((uint32_t)i - wstart[w]) & kBktIdxMask);
+    return;
+  }
   slot[id_s[i]] = (uint32_t)i;
   if (seg_start) {
     if (i == 0 || key_s[i - 1] != key) seg_start[key - lo] = (uint32_t)i;
@@ -1167,7 +1177,7 @@ __device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const 
 __device__ __forceinline__ void bkt_group_keys(const Buckets& bk, uint32_t lane, uint32_t np, uint32_t gk, uint32_t gs,
                                                bool zero_count) {
   if (lane >= np) return;
-  const uint32_t w = gk / (uint32_t)bk.per, idx = gs - bk.wstart[w];  // members per shard < 2^32: a 32-bit division
+  const uint32_t w = gs >> kBktWShift, idx = gs & kBktIdxMask;  // pre-encoded by grp_index_kernel
   if (idx >= bk.gcap) return;  // over the bucket capacity: flagged by the bounds kernel
   uint32_t* b = bk.send + (uint64_t)w * bk.stride_u32;
   b[bk.keys_off + idx] = gk;
@@ -1214,11 +1224,10 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   pend_load(s, l, lane, npend, pr);
 #endif
   // buckets: each peer's destination shard and that bucket's first group (same round trip)
-  uint32_t wdst = 0, wfirst = 0;
+  uint32_t wdst = 0;  // (bucket mode: the slot word holds the shard and the bucket place)
   if (BKT && lane < np) {
-    wdst = e.gk / (uint32_t)bk.per;  // 32-bit division (members per shard < 2^32)
-    wfirst = bk.wstart[wdst];
-    const uint32_t idx = e.gs - wfirst;
+    wdst = e.gs >> kBktWShift;
+    const uint32_t idx = e.gs & kBktIdxMask;
     if (idx < bk.gcap) bk.send[(uint64_t)wdst * bk.stride_u32 + bk.keys_off + idx] = e.gk;
   }
   if (ne1) q_load(c, s, l, 1, lane, Q1);
@@ -1264,7 +1273,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
     uint32_t* oc = nullptr;
     if (lane < np) {
       if (BKT) {
-        const uint32_t idx = e.gs - wfirst;
+        const uint32_t idx = e.gs & kBktIdxMask;
         if (idx < bk.gcap) {
           off = (uint64_t)wdst * bk.stride_u32 + bk.vals_off + (uint64_t)idx * c.cap_t;
           oc = bk.send + (uint64_t)wdst * bk.stride_u32 + bk.cnt_off + idx;
@@ -1304,7 +1313,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
     uint32_t* od = out_dec;
     uint32_t* oc = cnt_s + gslot;
     if (BKT) {  // the group's place in its destination's bucket
-      const uint32_t w = shfl_u32(wdst, j), idx = gslot - shfl_u32(wfirst, j);
+      const uint32_t w = gslot >> kBktWShift, idx = gslot & kBktIdxMask;
       uint32_t* b = bk.send + (uint64_t)w * bk.stride_u32;
       if (idx < bk.gcap) {
         ov = b + bk.vals_off;
@@ -1405,11 +1414,10 @@ __device__ __forceinline__ void emit_run4(const GCfg& c, const GState& s, const 
   uint32_t err = 0;
   PendRegs pr;
   pend_load(s, l, lane, npend, pr);
-  uint32_t wdst = 0, wfirst = 0;
+  uint32_t wdst = 0;
   if (BKT && lane < np) {
-    wdst = gk / (uint32_t)bk.per;
-    wfirst = bk.wstart[wdst];
-    const uint32_t idx = gs - wfirst;
+    wdst = gs >> kBktWShift;
+    const uint32_t idx = gs & kBktIdxMask;
     if (idx < bk.gcap) bk.send[(uint64_t)wdst * bk.stride_u32 + bk.keys_off + idx] = gk;
   }
   Q4 Q0, Q1, Q2;
@@ -1457,7 +1465,7 @@ __device__ __forceinline__ void emit_run4(const GCfg& c, const GState& s, const 
     uint32_t* oc = nullptr;
     if (lane < np) {
       if (BKT) {
-        const uint32_t idx = gs - wfirst;
+        const uint32_t idx = gs & kBktIdxMask;
         if (idx < bk.gcap) {
           off = (uint64_t)wdst * bk.stride_u32 + bk.vals_off + (uint64_t)idx * c.cap_t;
           oc = bk.send + (uint64_t)wdst * bk.stride_u32 + bk.cnt_off + idx;
@@ -1485,7 +1493,7 @@ __device__ __forceinline__ void emit_run4(const GCfg& c, const GState& s, const 
     uint32_t* od = out_dec;
     uint32_t* oc = cnt_s + gslot;
     if (BKT) {
-      const uint32_t w = shfl_u32(wdst, j), idx = gslot - shfl_u32(wfirst, j);
+      const uint32_t w = gslot >> kBktWShift, idx = gslot & kBktIdxMask;
       uint32_t* b = bk.send + (uint64_t)w * bk.stride_u32;
       if (idx < bk.gcap) {
         ov = b + bk.vals_off;
@@ -3228,15 +3236,17 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
     RSF_HIP(hipMemsetAsync(g->seg_start, 0, c.n_loc * 4, st));
     RSF_HIP(hipMemsetAsync(g->seg_end, 0, c.n_loc * 4, st));
   }
-  hipLaunchKernelGGL(grp_index_kernel, dim3(grid1(ng)), dim3(256), 0, st, g->grp_key_s, g->grp_id_s, ng, c.lo,
-                     g->grp_slot, local ? g->seg_start : nullptr, local ? g->seg_end : nullptr);
-  RSF_HIP(hipGetLastError());
-  RSF_DBG_SYNC(st, "grp_index_kernel");
   const dim3 egrid(grid1((c.n_loc + RSF_EMIT_PER_WAVE - 1) / RSF_EMIT_PER_WAVE, RSF_EMIT_WPB));
   if (world) {
+    // buckets: the shard bounds first, then every group's slot word = (shard, place in bucket)
+    if (ng > kBktIdxMask || world >= (1u << (32 - kBktWShift))) return gerr("too many groups for bucket emission");
     const Buckets bk = send_buckets(g);
     hipLaunchKernelGGL(bucket_bounds_kernel, dim3(1), dim3(64), 0, st, (const uint32_t*)g->grp_key_s, ng, bk.per, world,
                        g->d_wstart, g->bkt_send, bk.stride_u32, bk.gcap, g->d_counters + 58);
+    hipLaunchKernelGGL(grp_index_kernel, dim3(grid1(ng)), dim3(256), 0, st, g->grp_key_s, g->grp_id_s, ng, c.lo,
+                       g->grp_slot, nullptr, nullptr, (const uint32_t*)g->d_wstart, (uint32_t)bk.per);
+    RSF_HIP(hipGetLastError());
+    RSF_DBG_SYNC(st, "grp_index_kernel");
     mark(g, 2);
     if (c.qcap > kWave)
       hipLaunchKernelGGL(emit4_kernel<true>, dim3((unsigned)c.n_loc), dim3(kWave), 0, st, c, g->s, g->grp_key,
@@ -3251,6 +3261,10 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
     mark(g, 3);
     return RSF_OK;
   }
+  hipLaunchKernelGGL(grp_index_kernel, dim3(grid1(ng)), dim3(256), 0, st, g->grp_key_s, g->grp_id_s, ng, c.lo,
+                     g->grp_slot, local ? g->seg_start : nullptr, local ? g->seg_end : nullptr);
+  RSF_HIP(hipGetLastError());
+  RSF_DBG_SYNC(st, "grp_index_kernel");
   mark(g, 2);
   if (c.qcap > kWave)
     hipLaunchKernelGGL(emit4_kernel<false>, dim3((unsigned)c.n_loc), dim3(kWave), 0, st, c, g->s, g->grp_key,
