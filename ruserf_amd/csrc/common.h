@@ -56,11 +56,17 @@ RSF_HD uint64_t sat_u64(double x) {
   return (uint64_t)x;
 }
 
-// Duration::as_secs_f64 = secs as f64 + nanos as f64 / 1e9
+// Duration::as_secs_f64 = secs as f64 + nanos as f64 / 1e9.  The division is done as
+// q0 = x * RN(1e-9), then one FMA correction: for every integer x in [0, 1e9) -- the whole
+// domain of nanos -- this equals the correctly rounded x / 1e9 (checked exhaustively,
+// tests/test_div1e9.py), in 3 f64 operations instead of the ~10 of a general division.
 RSF_HD double as_secs_f64(uint64_t ns) {
   uint64_t secs = ns / 1000000000ull;
   uint32_t nanos = (uint32_t)(ns - secs * 1000000000ull);
-  return (double)secs + (double)nanos / 1e9;
+  const double x = (double)nanos, r = 1.0 / 1e9;
+  const double q0 = x * r;
+  const double q = __builtin_fma(__builtin_fma(-q0, 1e9, x), r, q0);
+  return (double)secs + q;
 }
 
 // f64::max / f64::min (non-NaN operand wins) == IEEE maxNum/minNum

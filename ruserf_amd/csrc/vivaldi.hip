@@ -195,16 +195,18 @@ __device__ __forceinline__ int update_one(double* me, double& err, double& adj, 
     frec[0] = __longlong_as_double((long long)(ns[0] | (ns[1] << 34)));
     frec[1] = __longlong_as_double(
         (long long)((ns[1] >> 30) | (ns[2] << 4) | ((uint64_t)len << 38) | ((uint64_t)head << 40)));
-    // median of the len live samples (as_secs_f64 of each, sorted, index len/2)
-    double t[3];
+    // median of the len live samples: the reference sorts as_secs_f64 of each and takes
+    // index len/2; as_secs_f64 is non-decreasing in the nanoseconds, so the median of the
+    // integers, converted once, is the same value
+    uint64_t t[3];
     uint32_t c = 0;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       uint32_t rel = ((uint32_t)i + Fr - head) % Fr;
-      if ((uint32_t)i < Fr && rel < len) t[c++] = as_secs_f64(ns[i]);
+      if ((uint32_t)i < Fr && rel < len) t[c++] = ns[i];
     }
     for (uint32_t i = 1; i < c; ++i) {
-      double v = t[i];
+      uint64_t v = t[i];
       uint32_t j = i;
       while (j > 0 && t[j - 1] > v) {
         t[j] = t[j - 1];
@@ -212,7 +214,7 @@ __device__ __forceinline__ int update_one(double* me, double& err, double& adj, 
       }
       t[j] = v;
     }
-    rtt_seconds = t[c / 2];
+    rtt_seconds = as_secs_f64(t[c / 2]);
   } else {
     const int FR = FRT;
     uint64_t meta = __double_as_longlong(frec[FR - 1]);
