@@ -423,17 +423,19 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   // the inclusive prefix sum of (overhead + len) is <= limit, so the leading run of picks
   // comes out of one wave scan; the remaining budget is then offered to later (shorter)
   // items one by one, as the reference does.
+  if (limit < 0) return 0;
+  const uint32_t lim = (uint32_t)limit;  // 32-bit budget arithmetic below (used <= lim)
   const uint32_t incl = wave_inclusive_sum_u32(live ? c.overhead + len : 0u);
-  uint64_t pick_m = limit >= 0 ? (ballot(incl <= (uint32_t)limit) & live_m) : 0ull;
-  int64_t used = pick_m ? (int64_t)shfl_u32(incl, 63 - __clzll((long long)pick_m)) : 0;
+  uint64_t pick_m = ballot(incl <= lim) & live_m;
+  uint32_t used = pick_m ? shfl_u32(incl, 63 - __clzll((long long)pick_m)) : 0u;
   for (;;) {
-    const int64_t free_b = limit - used - (int64_t)c.overhead;
+    const int32_t free_b = (int32_t)(lim - used - c.overhead);
     if (free_b <= 0) break;
     const uint64_t cand = ballot(len <= (uint32_t)free_b) & live_m & ~pick_m;
     if (!cand) break;
     const int win = __ffsll((long long)cand) - 1;
     pick_m |= 1ull << win;
-    used += (int64_t)c.overhead + shfl_u32(len, win);
+    used += c.overhead + shfl_u32(len, win);
   }
   if (!pick_m) return used;
   // picks are in ascending lane (= send) order: record rank = picked lanes below
@@ -574,7 +576,10 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
   uint32_t j = 0;
   bool exact = false;
   for (; j < np; ++j) {
-    const int64_t limit = (int64_t)c.limit - (int64_t)shfl_u32(used_v, j);
+    // 32-bit budget arithmetic (a peer's bytes used never exceed the limit): scalar 32-bit
+    // operations instead of 64-bit pairs in the loop the emission spends most of its scalar
+    // issue on
+    const uint32_t limit = c.limit - shfl_u32(used_v, j);
     const uint64_t rem = a_m & ~cons;
     if (!prefix) {  // a skip broke the run's prefix: sums of what is left of it
       incl = wave_inclusive_sum_u32(lane_bit(rem) ? c.overhead + len : 0u);
@@ -582,14 +587,15 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
       prefix = true;
     }
     // (lanes before the consumed prefix wrap to huge sums and fail the compare; masked anyway)
-    uint64_t pick = limit >= 0 ? (ballot(incl - base <= (uint32_t)limit) & rem) : 0ull;
+    uint64_t pick = ballot(incl - base <= limit) & rem;
     const uint32_t top = pick ? shfl_u32(incl, 63 - __clzll((long long)pick)) : base;
-    int64_t used = (int64_t)(top - base);
+    uint32_t used = top - base;
     bool skipped = false;
+    const uint64_t avail = live_m & ~gone;
     for (;;) {
-      const int64_t free_b = limit - used - (int64_t)c.overhead;
+      const int32_t free_b = (int32_t)(limit - used - c.overhead);
       if (free_b <= 0) break;
-      const uint64_t fit = ballot(len <= (uint32_t)free_b) & live_m & ~gone & ~pick;
+      const uint64_t fit = ballot(len <= (uint32_t)free_b) & avail & ~pick;
       if (!fit) break;
       const uint64_t cand = fit & rem;
       if (!cand) {  // the next candidate lies past the class-t0 run (or is a bumped pick)
@@ -598,7 +604,7 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
       }
       const int win = __ffsll((long long)cand) - 1;
       pick |= 1ull << win;
-      used += (int64_t)c.overhead + shfl_u32(len, win);
+      used += c.overhead + shfl_u32(len, win);
       skipped = true;
     }
     if (exact) break;
@@ -617,7 +623,7 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
       if (skipped) prefix = false;
       else base = top;
     }
-    used_v += lane == j ? (uint32_t)used : 0u;
+    used_v += lane == j ? used : 0u;
   }
 #if RSF_EMIT_PROF
   const uint64_t pp1 = __builtin_amdgcn_s_memtime();

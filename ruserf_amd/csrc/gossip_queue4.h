@@ -282,7 +282,7 @@ __device__ __forceinline__ void q4_pick_peers(const GCfg& c, Q4& Q, uint32_t lan
   uint32_t j = 0;
   bool exact = false;
   for (; j < np; ++j) {
-    const int64_t limit = (int64_t)c.limit - (int64_t)shfl_u32(used_v, j);
+    const uint32_t limit = c.limit - shfl_u32(used_v, j);  // (a peer's bytes used never exceed the limit)
     bool rem[kQK], pick[kQK];
 #pragma unroll
     for (uint32_t k = 0; k < kQK; ++k) rem[k] = a[k] && !cons[k];
@@ -294,14 +294,14 @@ __device__ __forceinline__ void q4_pick_peers(const GCfg& c, Q4& Q, uint32_t lan
     uint32_t mx = 0;  // the prefix sum at the last slot of the leading run that fits
 #pragma unroll
     for (uint32_t k = 0; k < kQK; ++k) {
-      pick[k] = limit >= 0 && rem[k] && incl[k] - base <= (uint32_t)limit;
+      pick[k] = rem[k] && incl[k] - base <= limit;
       mx = pick[k] ? incl[k] : mx;
     }
     const uint32_t top = ballot(mx != 0) ? (uint32_t)wave_max_u64(mx) : base;
-    int64_t used = (int64_t)(top - base);
+    uint32_t used = top - base;
     bool skipped = false;
     for (;;) {
-      const int64_t free_b = limit - used - (int64_t)c.overhead;
+      const int32_t free_b = (int32_t)(limit - used - c.overhead);
       if (free_b <= 0) break;
       uint32_t first_fit = kQK, first_cand = kQK;  // this lane's first fitting / candidate slot
 #pragma unroll
@@ -320,7 +320,7 @@ __device__ __forceinline__ void q4_pick_peers(const GCfg& c, Q4& Q, uint32_t lan
       const uint32_t wk = shfl_u32(first_cand, wl);
 #pragma unroll
       for (uint32_t k = 0; k < kQK; ++k) pick[k] = pick[k] || ((int)lane == wl && k == wk);
-      used += (int64_t)c.overhead + shfl_u32(q4_pick(len, wk), wl);
+      used += c.overhead + shfl_u32(q4_pick(len, wk), wl);
       skipped = true;
     }
     if (exact) break;
@@ -345,7 +345,7 @@ __device__ __forceinline__ void q4_pick_peers(const GCfg& c, Q4& Q, uint32_t lan
       if (skipped) prefix = false;
       else base = top;
     }
-    used_v += lane == j ? (uint32_t)used : 0u;
+    used_v += lane == j ? used : 0u;
   }
   bool any = false;
 #pragma unroll
