@@ -54,6 +54,10 @@ if os.path.isdir(f"{v}_fetch"):
                       "method": "2*(FETCH - 0.998*gather) + gather + u8 index read + WRITE"}
 GTAG = os.environ.get("GOSSIP_TAG", "gossip_r01c")
 g = os.path.join(OUT, f"prof_{GTAG}")
+if not os.path.isdir(f"{g}_fetch"):  # keep the committed gossip entry
+    json.dump(res, open(os.path.join(ROOT, "profiles", "traffic.json"), "w"), indent=1)
+    print(json.dumps(res, indent=1))
+    sys.exit(0)
 f_merge = last(f"{g}_fetch/run_counter_collection.csv", "FETCH_SIZE", "merge_kernel")
 w_merge = last(f"{g}_write/run_counter_collection.csv", "WRITE_SIZE", "merge_kernel")
 line = next(json.loads(x) for x in open(f"{g}_trace.log") if x.startswith("{") and '"metric"' in x)
