@@ -588,14 +588,14 @@ static inline void snap_member_event(orc_world* w, uint32_t m, uint32_t ev, uint
   else if (ev == EV_LEAVE || ev == EV_FAILED) *word &= ~(1u << (subj & 31));
 }
 
-static void dlog_put(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key, int cc);
+static void dlog_put(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key, uint64_t flags);
 /* a MemberEvent sent to the application (event_tx): the order-sensitive digest, the
- * snapshotter, and the delivery log (tagged: ltime word = ORC_LOG_MEMBER | type, key =
+ * snapshotter, and the delivery log (flags word ORC_LOG_MEMBER, time word = the type, key =
  * subject), so the log is the member's whole event stream in production order */
 static inline void digest_member_event(orc_world* w, uint32_t m, uint32_t ev, uint32_t subj) {
   w->digest[m] = orc_digest_mix(w->digest[m], DIG_MEMBER | ((uint64_t)ev << 32) | subj);
   snap_member_event(w, m, ev, subj);
-  dlog_put(w, m, ORC_LOG_MEMBER | ev, subj, 0);
+  dlog_put(w, m, ev, subj, ORC_LOG_MEMBER);
 }
 
 /* process_user_event / process_query_event (snapshot.rs:663-684): the largest ltime
@@ -803,14 +803,14 @@ int orc_world_set_delivery_log(orc_world* w, uint32_t per_member) {
 }
 
 /* event_tx.send(UserEvent) (base.rs:831-835) into the member's delivery log */
-static void dlog_put(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key, int cc) {
+static void dlog_put(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key, uint64_t flags) {
   if (!w->dcap) return;
   uint32_t k = w->dcnt[m];
   if (k < w->dcap) {
     uint64_t* e = w->dlog + ((size_t)m * w->dcap + k) * 3;
     e[0] = ltime;
     e[1] = key;
-    e[2] = cc ? 1 : 0;
+    e[2] = flags; /* a word of its own: a user event's ltime is a full u64 off the wire */
   } else {
     w->err[m] |= ORC_E_DLOG;
   }
@@ -840,7 +840,7 @@ int orc_handle_user_event_cc(orc_world* w, uint32_t m, uint64_t ltime, uint64_t 
     w->eb_cnt[slot] = 1;
   }
   w->digest[m] = orc_digest_mix(orc_digest_mix(w->digest[m], DIG_USER ^ key), ltime);
-  dlog_put(w, m, ltime, key, cc);
+  dlog_put(w, m, ltime, key, cc ? ORC_LOG_CC : 0);
   snap_clock(w, m, 0, ltime);
   return ORC_F_REBROADCAST | ORC_F_DELIVER;
 }

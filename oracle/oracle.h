@@ -281,8 +281,9 @@ int orc_handle_user_event(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key
 int orc_handle_user_event_cc(orc_world* w, uint32_t m, uint64_t ltime, uint64_t key, int cc);
 /* Delivery log: per member up to per_member entries per round of its event stream in
  * production order, 3 u64 each: user events (ltime, key, cc); member events
- * (ORC_LOG_MEMBER | MemberEventType, subject, 0) */
-#define ORC_LOG_MEMBER (1ull << 62)
+ * (MemberEventType, subject, ORC_LOG_MEMBER); the third word holds the flags */
+#define ORC_LOG_CC 1ull         /* a user event's cc flag */
+#define ORC_LOG_MEMBER 0x100ull /* a member event */
 #define ORC_MAX_QCAP 256 /* slots per transmit-limited queue (the engine's queue_cap range) */
 int orc_world_set_delivery_log(orc_world* w, uint32_t per_member);
 int orc_handle_query(orc_world* w, uint32_t m, uint64_t ltime, uint32_t id, int no_broadcast);

@@ -98,60 +98,69 @@ extern "C" int rsf_coalesce_user_events(const rsf_user_event* in, uint64_t n, rs
   if (n >= 0x7FFFFFFFull) return rsf::set_error(RSF_ERR_ARG, "batch too large");
   hipStream_t st = (hipStream_t)stream;
   const int ni = (int)n;
-  // buffers: key/key_s/key2/key2_s u64 x4, idx/idx_s/head/seg/start/flag/sel_v/ord u32 x8, lt u64, segmax u64
-  size_t tmp_sort = 0, tmp_scan = 0, tmp_sel = 0, tmp_sort2 = 0;
+  // buffers: key/key_s/key2/key2_s/lt/segmax u64 x6, idx/idx_s/head/seg/start/flag/sel_v/ord u32 x8
   uint64_t *key = nullptr, *key_s = nullptr, *key2 = nullptr, *key2_s = nullptr, *lt = nullptr;
   uint32_t *idx = nullptr, *idx_s = nullptr, *head = nullptr, *seg = nullptr, *start = nullptr, *flag = nullptr,
-           *sel_k_unused = nullptr, *sel_v = nullptr, *ord = nullptr;
-  (void)sel_k_unused;
+           *sel_v = nullptr, *ord = nullptr;
   unsigned long long* segmax = nullptr;
-  uint64_t* sel_k = nullptr;
-  int* d_nsel = nullptr;
-  RSF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_sort, key, key_s, idx, idx_s, ni, 0, 64, st));
-  RSF_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tmp_scan, head, seg, ni, st));
-  RSF_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp_sel, key2, flag, sel_k, d_nsel, ni, st));
-  size_t tmp_sel2 = 0;
-  RSF_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp_sel2, idx_s, flag, sel_v, d_nsel, ni, st));
-  RSF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_sort2, key2, key2_s, sel_v, ord, ni, 0, 64, st));
-  size_t tmp = std::max(std::max(tmp_sort, tmp_scan), std::max(std::max(tmp_sel, tmp_sel2), tmp_sort2));
   const size_t n8 = ((size_t)n * 8 + 255) & ~(size_t)255, n4 = ((size_t)n * 4 + 255) & ~(size_t)255;
-  const size_t total = 6 * n8 + 8 * n4 + 256 + ((tmp + 255) & ~(size_t)255);
   Scratch sc(st);
-  RSF_HIP(hipMallocAsync(&sc.p, total, st));
+  RSF_HIP(hipMallocAsync(&sc.p, 6 * n8 + 8 * n4 + 256, st));
   char* b = (char*)sc.p;
   auto take8 = [&](void* pp) { *(char**)pp = b; b += n8; };
   auto take4 = [&](void* pp) { *(char**)pp = b; b += n4; };
   take8(&key); take8(&key_s); take8(&key2); take8(&key2_s); take8(&lt); take8(&segmax);
   take4(&idx); take4(&idx_s); take4(&head); take4(&seg); take4(&start); take4(&flag); take4(&sel_v); take4(&ord);
-  d_nsel = (int*)b;
-  b += 256;
-  void* t = b;
-  sel_k = key2_s;  // the selected survivor keys land here, then sort back into key2
+  int* d_nsel = (int*)b;
+  uint64_t* sel_k = key2_s;  // the selected survivor keys land here, then sort back into key2
+  // every hipCUB call sized for its own item count and types (rsf::cub_run)
+  rsf::CubTemp tmp;
+  struct Free {
+    rsf::CubTemp& t;
+    ~Free() { t.release(); }
+  } free_tmp{tmp};
   const unsigned g = grid1(n);
   hipLaunchKernelGGL(ce_keys_kernel, dim3(g), dim3(256), 0, st, in, n, key, idx);
-  size_t tb = tmp;
-  RSF_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, key, key_s, idx, idx_s, ni, 0, 64, st));
+  int rc = rsf::cub_run(
+      tmp, st,
+      [&](void* t, size_t& bytes) { return hipcub::DeviceRadixSort::SortPairs(t, bytes, key, key_s, idx, idx_s, ni, 0, 64, st); },
+      "user event sort");
+  if (rc) return rc;
   hipLaunchKernelGGL(ce_heads_kernel, dim3(g), dim3(256), 0, st, in, key_s, idx_s, n, head, lt);
-  tb = tmp;
-  RSF_HIP(hipcub::DeviceScan::InclusiveSum(t, tb, head, seg, ni, st));
+  rc = rsf::cub_run(
+      tmp, st, [&](void* t, size_t& bytes) { return hipcub::DeviceScan::InclusiveSum(t, bytes, head, seg, ni, st); },
+      "user event segment scan");
+  if (rc) return rc;
   RSF_HIP(hipMemsetAsync(segmax, 0, (size_t)n * 8, st));
   hipLaunchKernelGGL(ce_starts_kernel, dim3(g), dim3(256), 0, st, head, seg, n, start);
   hipLaunchKernelGGL(ce_segmax_kernel, dim3(g), dim3(256), 0, st, seg, lt, n, segmax);
   hipLaunchKernelGGL(ce_survivors_kernel, dim3(g), dim3(256), 0, st, key_s, idx_s, seg, start, lt, segmax, n, key2,
                      flag);
   RSF_HIP(hipGetLastError());
-  tb = tmp;
-  RSF_HIP(hipcub::DeviceSelect::Flagged(t, tb, key2, flag, sel_k, d_nsel, ni, st));
-  tb = tmp;
-  RSF_HIP(hipcub::DeviceSelect::Flagged(t, tb, idx_s, flag, sel_v, d_nsel, ni, st));
+  rc = rsf::cub_run(
+      tmp, st,
+      [&](void* t, size_t& bytes) { return hipcub::DeviceSelect::Flagged(t, bytes, key2, flag, sel_k, d_nsel, ni, st); },
+      "user event survivor keys");
+  if (rc) return rc;
+  rc = rsf::cub_run(
+      tmp, st,
+      [&](void* t, size_t& bytes) { return hipcub::DeviceSelect::Flagged(t, bytes, idx_s, flag, sel_v, d_nsel, ni, st); },
+      "user event survivor indices");
+  if (rc) return rc;
   int nsel = 0;
   RSF_HIP(hipMemcpyAsync(&nsel, d_nsel, sizeof(int), hipMemcpyDeviceToHost, st));
   RSF_HIP(hipStreamSynchronize(st));
   if (nsel > 0) {
-    tb = tmp;
-    RSF_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, sel_k, key2, sel_v, ord, nsel, 0, 64, st));
+    rc = rsf::cub_run(
+        tmp, st,
+        [&](void* t, size_t& bytes) {
+          return hipcub::DeviceRadixSort::SortPairs(t, bytes, sel_k, key2, sel_v, ord, nsel, 0, 64, st);
+        },
+        "user event output sort");
+    if (rc) return rc;
     hipLaunchKernelGGL(ce_gather_kernel, dim3(grid1((uint64_t)nsel)), dim3(256), 0, st, in, ord, (uint64_t)nsel, out);
     RSF_HIP(hipGetLastError());
+    RSF_HIP(hipStreamSynchronize(st));
   }
   *n_out = (uint64_t)nsel;
   return RSF_OK;
@@ -190,22 +199,30 @@ __global__ void mc_keys_kernel(const rsf_member_event* __restrict__ in, uint64_t
 // (group << 35 | type << 32 | node) for the output order
 __global__ void mc_flush_kernel(const rsf_member_event* __restrict__ in, const uint64_t* __restrict__ key,
                                 const uint32_t* __restrict__ idx, uint64_t n, uint32_t n_nodes,
-                                uint8_t* __restrict__ last, uint64_t* __restrict__ okey, uint32_t* __restrict__ flag) {
+                                const uint8_t* __restrict__ last, uint64_t* __restrict__ okey, uint32_t* __restrict__ flag) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const bool latest = i + 1 == n || key[i + 1] != key[i];
   uint32_t f = 0;
   if (latest) {
     const rsf_member_event e = in[idx[i]];
-    uint8_t* lp = last + (uint64_t)e.group * n_nodes + e.node;
+    const uint8_t* lp = last + (uint64_t)e.group * n_nodes + e.node;
     const uint8_t prev = *lp;
-    if (!(prev == e.type && e.type != kMevUpdate)) {
-      *lp = (uint8_t)e.type;
-      f = 1;
-    }
+    if (!(prev == e.type && e.type != kMevUpdate)) f = 1;  // recorded by mc_commit_kernel
     okey[i] = ((uint64_t)e.group << 35) | ((uint64_t)e.type << 32) | e.node;
   }
   flag[i] = f;
+}
+
+// last_events[node] = type for the flushed events, once every step of the flush has succeeded
+// (a failed call leaves the table as it was, so the quantum can be flushed again)
+__global__ void mc_commit_kernel(const rsf_member_event* __restrict__ in, const uint32_t* __restrict__ idx,
+                                 const uint32_t* __restrict__ flag, uint64_t n, uint32_t n_nodes,
+                                 uint8_t* __restrict__ last) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !flag[i]) return;
+  const rsf_member_event e = in[idx[i]];
+  last[(uint64_t)e.group * n_nodes + e.node] = (uint8_t)e.type;
 }
 
 __global__ void mc_gather_kernel(const rsf_member_event* __restrict__ in, const uint32_t* __restrict__ order,
@@ -264,12 +281,13 @@ extern "C" int rsf_member_coalescer_flush(rsf_member_coalescer* mc, const rsf_me
   const int ni = (int)n;
   const size_t n8 = ((size_t)n * 8 + 255) & ~(size_t)255, n4 = ((size_t)n * 4 + 255) & ~(size_t)255;
   Scratch sc(st);
-  RSF_HIP(hipMallocAsync(&sc.p, 4 * n8 + 3 * n4 + 256, st));
+  RSF_HIP(hipMallocAsync(&sc.p, 4 * n8 + 4 * n4 + 256, st));
   char* b = (char*)sc.p;
   uint64_t *key = (uint64_t*)b, *key_s = (uint64_t*)(b + n8), *okey = (uint64_t*)(b + 2 * n8),
            *okey_s = (uint64_t*)(b + 3 * n8);
   uint32_t *idx = (uint32_t*)(b + 4 * n8), *idx_s = (uint32_t*)(b + 4 * n8 + n4), *flag = (uint32_t*)(b + 4 * n8 + 2 * n4);
-  unsigned int* dv = (unsigned int*)(b + 4 * n8 + 3 * n4);  // [0] bad input, [1] selected count
+  uint32_t* ord = (uint32_t*)(b + 4 * n8 + 3 * n4);  // the output order (flag stays intact for the commit)
+  unsigned int* dv = (unsigned int*)(b + 4 * n8 + 4 * n4);  // [0] bad input, [1] selected count
   RSF_HIP(hipMemsetAsync(dv, 0, 8, st));
   const unsigned g = grid1(n);
   hipLaunchKernelGGL(mc_keys_kernel, dim3(g), dim3(256), 0, st, in, n, mc->n_groups, mc->n_nodes, key, idx, dv);
@@ -309,7 +327,6 @@ extern "C" int rsf_member_coalescer_flush(rsf_member_coalescer* mc, const rsf_me
   RSF_HIP(hipMemcpyAsync(&nsel, nsel_d, 4, hipMemcpyDeviceToHost, st));
   RSF_HIP(hipStreamSynchronize(st));
   if (nsel > 0) {
-    uint32_t* ord = flag;  // free again
     rc = rsf::cub_run(
         tmp, st,
         [&](void* t, size_t& bytes) {
@@ -319,6 +336,8 @@ extern "C" int rsf_member_coalescer_flush(rsf_member_coalescer* mc, const rsf_me
     if (rc) return rc;
     hipLaunchKernelGGL(mc_gather_kernel, dim3(grid1((uint64_t)nsel)), dim3(256), 0, st, in, (const uint32_t*)ord,
                        (uint64_t)nsel, out);
+    RSF_HIP(hipGetLastError());
+    hipLaunchKernelGGL(mc_commit_kernel, dim3(g), dim3(256), 0, st, in, idx_s, flag, n, mc->n_nodes, mc->last);
     RSF_HIP(hipGetLastError());
     RSF_HIP(hipStreamSynchronize(st));
   }

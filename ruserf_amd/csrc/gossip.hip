@@ -1056,7 +1056,10 @@ __global__ void __launch_bounds__(256) grp_index_kernel(const uint32_t* __restri
   if (RSF_BAD(2, id_s[i] >= n, id_s[i]) || RSF_BAD(3, seg_start && key - lo >= n, key)) return;
   if (wstart) {
     const uint32_t w = key / per;
-    slot[id_s[i]] = (w << kBktWShift) | (((uint32_t)i - wstart[w]) & kBktIdxMask);
+    // a place past the field (an overflowing bucket) saturates to kBktIdxMask, which is >= the
+    // bucket capacity (rsf_gossip_bucket_buffers), so emission skips it instead of wrapping
+    const uint64_t place = (uint64_t)i - wstart[w];
+    slot[id_s[i]] = (w << kBktWShift) | (uint32_t)(place < kBktIdxMask ? place : kBktIdxMask);
     return;
   }
   slot[id_s[i]] = (uint32_t)i;
@@ -2937,7 +2940,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   g->stage_val, g->sort_key, g->sort_val,  g->seg_start,  g->seg_end, g->send_buf,  g->d_counters, g->rec_dec, g->pp_buf,
                   g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
                   g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
-                  g->grp_slot, g->grp_off, g->dec_base, s.dlog, s.dcnt,
+                  g->grp_slot, g->grp_off, g->dec_base, s.dlog, s.dmeta, s.dcnt,
                   g->bkt_send, g->bkt_recv, g->bkt_dec, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn,
                   s.p_ent, s.p_cnt, g->big_base};
   for (void* p : ptrs)
@@ -3245,7 +3248,9 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
   const dim3 egrid(grid1((c.n_loc + RSF_EMIT_PER_WAVE - 1) / RSF_EMIT_PER_WAVE, RSF_EMIT_WPB));
   if (world) {
     // buckets: the shard bounds first, then every group's slot word = (shard, place in bucket)
-    if (ng > kBktIdxMask || world >= (1u << (32 - kBktWShift))) return gerr("too many groups for bucket emission");
+    // only a group's place inside its bucket must fit the slot word's index field
+    if (g->bkt_gcap >= kBktIdxMask || world >= (1u << (32 - kBktWShift)))
+      return gerr("bucket capacity too large for the slot encoding");
     const Buckets bk = send_buckets(g);
     hipLaunchKernelGGL(bucket_bounds_kernel, dim3(1), dim3(64), 0, st, (const uint32_t*)g->grp_key_s, ng, bk.per, world,
                        g->d_wstart, g->bkt_send, bk.stride_u32, bk.gcap, g->d_counters + 58);
@@ -3407,6 +3412,7 @@ int rsf_gossip_bucket_buffers(rsf_gossip* g, uint32_t world, void** send, void**
     // 1/8 more plus 4096 (overflow is flagged, rsf_gossip_bucket_status)
     const uint64_t expect = (c.n_loc * c.fanout + world - 1) / world;
     const uint64_t gcap = std::min<uint64_t>(expect + expect / 8 + 4096, c.n_loc * c.fanout);
+    if (gcap >= kBktIdxMask) return gerr("bucket capacity exceeds the slot word's 26-bit place field");
     g->bkt_gcap = (uint32_t)gcap;
     const Buckets b = bucket_layout(g, world);
     const size_t bytes = (size_t)b.stride_u32 * 4 * world;
@@ -3810,13 +3816,16 @@ int rsf_gossip_set_delivery_log(rsf_gossip* g, uint32_t per_member) {
   RSF_HIP(hipSetDevice(g->device));
   RSF_HIP(hipStreamSynchronize(g->stream));
   if (g->s.dlog) hipFree(g->s.dlog);
+  if (g->s.dmeta) hipFree(g->s.dmeta);
   if (g->s.dcnt) hipFree(g->s.dcnt);
   g->s.dlog = nullptr;
+  g->s.dmeta = nullptr;
   g->s.dcnt = nullptr;
   g->c.dcap = 0;
   if (!per_member) return RSF_OK;
   int rc;
   if ((rc = rsf::dmalloc((void**)&g->s.dlog, (size_t)g->c.n_loc * per_member * 16)) ||
+      (rc = rsf::dmalloc((void**)&g->s.dmeta, (size_t)g->c.n_loc * per_member)) ||
       (rc = rsf::dmalloc((void**)&g->s.dcnt, g->c.n_loc * 4)))
     return rc;
   RSF_HIP(hipMemsetAsync(g->s.dcnt, 0, g->c.n_loc * 4, g->stream));
@@ -3831,9 +3840,11 @@ int rsf_gossip_dump_deliveries(rsf_gossip* g, rsf_delivery* out, uint64_t cap, u
   if (!c.dcap) return RSF_OK;
   std::vector<uint32_t> cnt(c.n_loc);
   std::vector<uint4> log((size_t)c.n_loc * c.dcap);
+  std::vector<uint8_t> meta((size_t)c.n_loc * c.dcap);
   RSF_HIP(hipSetDevice(g->device));
   RSF_HIP(hipMemcpyAsync(cnt.data(), g->s.dcnt, c.n_loc * 4, hipMemcpyDeviceToHost, g->stream));
   RSF_HIP(hipMemcpyAsync(log.data(), g->s.dlog, log.size() * 16, hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipMemcpyAsync(meta.data(), g->s.dmeta, meta.size(), hipMemcpyDeviceToHost, g->stream));
   RSF_HIP(hipStreamSynchronize(g->stream));
   uint64_t o = 0;
   for (uint64_t l = 0; l < c.n_loc; ++l)
@@ -3842,11 +3853,12 @@ int rsf_gossip_dump_deliveries(rsf_gossip* g, rsf_delivery* out, uint64_t cap, u
       const uint4 e = log[l * c.dcap + k];
       const uint64_t lt = ((uint64_t)e.y << 32) | e.x;
       rsf_delivery& d = out[o++];
-      const bool mev = (lt & kLogMemberTag) != 0;
-      d.ltime = lt & ~((1ull << 63) | kLogMemberTag);
+      const uint8_t f = meta[l * c.dcap + k];
+      const bool mev = (f & kLogMember) != 0;
+      d.ltime = lt;
       d.key = ((uint64_t)e.w << 32) | e.z;
       d.member = (uint32_t)(c.lo + l);
-      d.cc = (uint8_t)(lt >> 63);
+      d.cc = (f & kLogCc) ? 1 : 0;
       d.kind = mev ? RSF_DELIVERY_MEMBER_EVENT : RSF_DELIVERY_USER_EVENT;
       d._r[0] = d._r[1] = 0;
     }

@@ -70,7 +70,8 @@ struct GState {
   rsf_rumor* rumors;
   uint32_t* rdec;  // per rumor: its record decoration (subject / kDecQuery / kDecEvent), 4 B
   uint4* rbody;    // per rumor id: the rumor without its key (ltime, subject, type, flags, msg_len), 16 B
-  uint4* dlog;     // [n_loc][dcap] user events delivered to the application: ltime | cc << 63, key
+  uint4* dlog;     // [n_loc][dcap] events delivered to the application: ltime (member event: its type), key
+  uint8_t* dmeta;  // [n_loc][dcap] each entry's flags: kLogCc, kLogMember (a byte of its own: an ltime is a full u64)
   uint32_t* dcnt;  // [n_loc] deliveries since the log was cleared
   // snapshotter per member (rsf_gossip_enable_snapshot; null: off): the alive set as a bitset
   // over subjects, and {last event clock, last query clock, last clock at leave, flags}
@@ -325,11 +326,13 @@ __device__ __forceinline__ void snap_member(const GCfg& c, const GState& s, uint
 }
 
 // one delivery (event_tx.send of a UserEvent, base.rs:831-835) into the member's log slot
+constexpr uint8_t kLogCc = 1, kLogMember = 2;
 __device__ __forceinline__ void dlog_put_raw(const GCfg& c, const GState& s, uint64_t l, uint32_t& err, uint64_t lt,
-                                             uint64_t key) {
+                                             uint64_t key, uint8_t meta) {
   const uint32_t k = s.dcnt[l];
   if (k < c.dcap) {
     s.dlog[l * c.dcap + k] = make_uint4((uint32_t)lt, (uint32_t)(lt >> 32), (uint32_t)key, (uint32_t)(key >> 32));
+    s.dmeta[l * c.dcap + k] = meta;
   } else {
     err |= kErrDlog;
   }
@@ -338,17 +341,16 @@ __device__ __forceinline__ void dlog_put_raw(const GCfg& c, const GState& s, uin
 __device__ __forceinline__ void dlog_put(const GCfg& c, const GState& s, uint64_t l, MRegs& r, uint64_t L,
                                          uint64_t key, bool cc) {
   if (!c.dcap) return;
-  dlog_put_raw(c, s, l, r.err, L | (cc ? (1ull << 63) : 0ull), key);
+  dlog_put_raw(c, s, l, r.err, L, key, cc ? kLogCc : 0);
 }
 // a MemberEvent (event_tx.send of a MemberEvent: handle_node_join / leave / update, the
 // Failed -> Left leave intent, handle_prune, the Reaper) into the same log, so the
 // application's stream keeps member and user events in the order they were produced;
-// bit 62 of the time word tags it (a Lamport time never reaches 2^62), the key is the subject
-constexpr uint64_t kLogMemberTag = 1ull << 62;
+// tagged kLogMember, the time word holds the type, the key the subject
 __device__ __forceinline__ void mlog_put(const GCfg& c, const GState& s, uint64_t l, uint32_t& err, uint32_t ev,
                                          uint32_t subj) {
   if (!c.dcap) return;
-  dlog_put_raw(c, s, l, err, kLogMemberTag | ev, subj);
+  dlog_put_raw(c, s, l, err, ev, subj, kLogMember);
 }
 // the member events of an intent handler's result: Failed -> Left (Leave), then handle_prune (Reap)
 __device__ __forceinline__ void mlog_intent(const GCfg& c, const GState& s, uint64_t l, uint32_t& err, int f,

@@ -388,9 +388,12 @@ int rsf_swim_apply_batch(rsf_swim* w, const rsf_swim_msg* msgs, uint64_t n, uint
   }
   RSF_HIP(hipSetDevice(w->device));
   hipStream_t st = w->stream;
+  // the sort's temporary storage is queried for exactly the call made below (same count and bits)
+  int bits = 1;
+  while (bits < 32 && (w->c.n_loc >> bits)) ++bits;
   size_t sort_bytes = 0;
   RSF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                             (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 32, st));
+                                             (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, bits, st));
   void* p[9];
   const size_t b[9] = {n * sizeof(rsf_swim_msg), n * 4, n * 4, n * 4, n * 4, w->c.n_loc * 4, w->c.n_loc * 4,
                        n * 4, n * 4};
@@ -407,8 +410,6 @@ int rsf_swim_apply_batch(rsf_swim* w, const rsf_swim_msg* msgs, uint64_t n, uint
   RSF_HIP(hipMemcpyAsync(dm, msgs, b[0], hipMemcpyHostToDevice, st));
   hipLaunchKernelGGL(sw_keys_kernel, dim3(grid1(n)), dim3(256), 0, st, dm, n, w->c.lo, key, idx);
   RSF_HIP(hipGetLastError());
-  int bits = 1;
-  while (bits < 32 && (w->c.n_loc >> bits)) ++bits;
   RSF_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, sort_bytes, key, key_s, idx, idx_s, (int)n, 0, bits, st));
   RSF_HIP(hipMemsetAsync(seg_start, 0, b[5], st));
   RSF_HIP(hipMemsetAsync(seg_end, 0, b[6], st));

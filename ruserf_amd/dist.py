@@ -182,6 +182,11 @@ class VivaldiTableRefresh:
         self.lo, self.hi = clients.lo, clients.hi
         self.stride = clients.table_ptr()[1]
         self.stage = None
+        # The gather and the copies below run on torch's current stream: the context's observe
+        # kernels must run on that same stream, or the gather could read or overwrite table rows
+        # observe is still writing (the context defaults to its own non-blocking stream).
+        if torch.cuda.is_available():
+            clients.set_stream(torch.cuda.current_stream().cuda_stream)
 
     def _table(self, ptr):
         t = hbm_tensor(ptr, self.g.n * self.stride, "<f8")

@@ -120,7 +120,8 @@ class MEvent(C.Structure):
     _fields_ = [("group", C.c_uint32), ("node", C.c_uint32), ("type", C.c_uint32), ("member", C.c_uint32)]
 
 
-LOG_MEMBER = 1 << 62  # delivery-log tag of a member event (oracle.h ORC_LOG_MEMBER)
+LOG_CC = 1  # delivery-log flags word (oracle.h ORC_LOG_CC / ORC_LOG_MEMBER)
+LOG_MEMBER = 0x100
 
 # enums (oracle.h)
 OK, ERR_DIM, ERR_COORD, ERR_RTT = 0, 1, 2, 3

@@ -119,3 +119,88 @@ def test_one_rank_rccl_equal_one_context(exchange):
     for k in full:
         assert np.array_equal(got[k], full[k]), k
     one.close()
+
+
+CFG2_N, CFG2_ROUNDS = 2_000_000, 8
+CFG2_SAMPLE = [(0, 64), (CFG2_N // 2 - 32, 64), (CFG2_N - 64, 64)]
+
+
+def _cfg2():
+    """BASELINE configs[2]'s per-GPU shard: 2M members, 4096 tracked subjects, the bench's
+    gossip configuration (bench_gossip.gossip_cfg) and its 1% intent workload."""
+    import bench_gossip as B
+    from ruserf_amd import workload as W
+    cfg = B.gossip_cfg(CFG2_N, CFG2_ROUNDS, 1)
+    subj, acts, ml = W.intents_workload(CFG2_N, B.SUBJECTS, CFG2_ROUNDS, rate=0.01, seed=B.SEED,
+                                        prune_frac=B.PRUNE_FRAC)
+    return cfg, subj, acts, ml
+
+
+def _cfg2_record(eng):
+    """per-member digests, clocks, error bits and prune counts, and the sampled view rows"""
+    m = eng.members()
+    rec = {k: m[k].copy() for k in ["clock", "event_clock", "query_clock", "digest", "err"]}
+    rec["pruned"] = eng.pruned()
+    rec["merged"] = np.array([eng.merged_total()], np.uint64)
+    for i, (r0, cnt) in enumerate(CFG2_SAMPLE):
+        lt, st, kd, tm = eng.view(with_time=True, rows=(r0, cnt))
+        rec[f"view{i}"] = np.stack([lt, st.astype(np.uint64), kd.astype(np.uint64), tm.astype(np.uint64)])
+    return rec
+
+
+def _worker_cfg2(port, q):
+    """The configs[2] shard through ShardedGossip on one RCCL rank (the multi-GPU code path:
+    rumor-block all-reduce, bucket emission, exchange, merge from the buckets)."""
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    torch.cuda.set_stream(torch.cuda.Stream())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    from ruserf_amd import workload as W
+    from ruserf_amd.dist import ShardedGossip
+    cfg, subj, acts, ml = _cfg2()
+    sg = ShardedGossip(cfg, 0, 1, device=0)
+    sg.eng.set_subjects(subj)
+    sg.eng.init_views(*W.initial_views(len(subj)))
+    for t in range(CFG2_ROUNDS):
+        sg.round(t, ml[t], acts[t])
+    torch.cuda.synchronize()
+    rec = _cfg2_record(sg.eng)
+    rec["exchange_ok"] = np.array([sg.buckets and sg.check()])
+    sg.eng.close()
+    dist.destroy_process_group()
+    q.put(rec)
+
+
+def test_configs2_shard_rccl_equal_one_context():
+    """BASELINE configs[2] at its per-GPU shard size (2M members x 4096 subjects, 8 rounds):
+    the multi-GPU code path on one RCCL rank must equal the single-context round -- every
+    member's clocks, digest (of every delivery), error bits and queue prunes, the records
+    merged, and sampled view rows -- with no bucket over capacity (exchange_ok).  The two
+    runs hold ~150 GB each and run one after the other (the rank first, in its own process)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from ruserf_amd import gossip as G
+    from ruserf_amd import workload as W
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29300 + os.getpid() % 1000
+    p = ctx.Process(target=_worker_cfg2, args=(port, q))
+    p.start()
+    got = q.get(timeout=600)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert bool(got.pop("exchange_ok")[0])
+    cfg, subj, acts, ml = _cfg2()
+    one = G.GossipEngine(cfg)
+    one.set_subjects(subj)
+    one.init_views(*W.initial_views(len(subj)))
+    for t in range(CFG2_ROUNDS):
+        one.round(t, ml[t], acts[t])
+    exp = _cfg2_record(one)
+    one.close()
+    assert int(exp["merged"][0]) > CFG2_N  # the rounds carried traffic
+    for k in exp:
+        assert np.array_equal(got[k], exp[k]), k

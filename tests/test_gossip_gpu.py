@@ -50,14 +50,17 @@ def test_intent_rounds_bit_exact(n, s, rounds, rate, qcap, limit):
     L.orc_world_free(C.byref(w))
 
 
-def test_bench_shape_bit_exact():
+@pytest.mark.parametrize("qcap", [64, 256])
+def test_bench_shape_bit_exact(qcap):
     """The bench's configuration (4096 subjects, queue_cap 64, 8 intents of budget per
     target, slot_k 1, 512-slot dedup rings) at 20k members with 5% originating per round:
     the queues saturate as in the bench (every member receives far more new intents than
     it can send), so bounded-queue prunes, full pending lists and merge_big_kernel are all
-    on the path; bit-exact against the oracle after every round."""
+    on the path; bit-exact against the oracle after every round.  queue_cap 256: the same
+    saturated shape through the four-slot-per-lane queues (gossip_queue4.h), whose prune
+    path and full pending lists are then compared as well."""
     n, s, rounds = 20000, 4096, 12
-    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=64, gossip_limit=8 * 24, gossip_overhead=2,
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=qcap, gossip_limit=8 * 24, gossip_overhead=2,
                          max_rumors=1 << 18, event_buffer_size=512, query_buffer_size=512, slot_k=1)
     subj, acts, ml = W.intents_workload(n, s, rounds, rate=0.05, seed=2024)
     views = W.initial_views(s)
@@ -68,6 +71,9 @@ def test_bench_shape_bit_exact():
         H.assert_same(H.engine_state(g), H.world_state(w), f"round {t}")
     st = H.engine_state(g)
     assert int(st["q_pruned"].sum()) > 0  # saturated: the bounded queues dropped items
+    if qcap > 64:  # more than one slot per lane in use
+        r = st["q_rumor"].reshape(n, 3, qcap)
+        assert np.count_nonzero(r[:, 0, :] != 0xFFFFFFFF, axis=1).max() > 64
     g.close()
     L.orc_world_free(C.byref(w))
 
@@ -454,16 +460,16 @@ def _threads():
 
 def _oracle_deliveries(w):
     """the oracle's delivery log as (member, ltime, key, cc, kind) rows, member-major (a member
-    event's ltime word is LOG_MEMBER | type: kind 1, ltime = the type)"""
+    event's flags word holds LOG_MEMBER: kind 1, its ltime word = the type)"""
     n, cap = w.n, w.dcap
     cnt = np.minimum(O.arr(w.dcnt, n, np.uint32), cap)
     log = O.arr(w.dlog, n * cap * 3, np.uint64).reshape(n, cap, 3)
     mask = np.arange(cap)[None, :] < cnt[:, None]
     mem = np.broadcast_to(np.arange(n, dtype=np.uint32)[:, None], (n, cap))[mask]
     e = log[mask]
-    kind = ((e[:, 0] & np.uint64(O.LOG_MEMBER)) != 0).astype(np.uint8)
-    lt = e[:, 0] & ~np.uint64(O.LOG_MEMBER)
-    return mem, lt, e[:, 1], e[:, 2].astype(np.uint8), kind
+    kind = ((e[:, 2] & np.uint64(O.LOG_MEMBER)) != 0).astype(np.uint8)
+    cc = (e[:, 2] & np.uint64(O.LOG_CC)).astype(np.uint8)
+    return mem, e[:, 0], e[:, 1], cc, kind
 
 
 def test_configs3_100k_churn_flood_coalesce():
