@@ -634,11 +634,18 @@ int orc_world_init(orc_world* w, const orc_world_cfg* c) {
       A(q_next_seq, n * 3) || A(eb_ltime, n * c->ebuf) || A(eb_cnt, n * c->ebuf) ||
       A(eb_keys, n * c->ebuf * c->slot_k) || A(qb_ltime, n * c->qbuf) || A(qb_cnt, n * c->qbuf) ||
       A(qb_ids, n * c->qbuf * c->slot_k) || A(rumors, 2 * (size_t)c->cap_rumors) || A(v_time, n * s) ||
-      A(q_pruned, n) || A(q_expired, n)) {
+      A(q_pruned, n) || A(q_expired, n) || A(q_hwm, n * 3)) {
     orc_world_free(w);
     return -1;
   }
 #undef A
+  for (int q = 0; q < 3; ++q) {
+    if (c->qdepth[q] > c->qcap) {
+      orc_world_free(w);
+      return -1;
+    }
+    w->qd[q] = c->qdepth[q] ? c->qdepth[q] : c->qcap;
+  }
   w->cap_rumors = c->cap_rumors;
   w->rbits = 0;
   while ((1u << w->rbits) < c->cap_rumors) w->rbits++;
@@ -661,7 +668,7 @@ void orc_world_free(orc_world* w) {
                   w->refute_ltime, w->v_ltime, w->v_status, w->v_kind, w->q_rumor, w->q_seq,
                   w->q_tx, w->q_len, w->q_next_seq, w->eb_ltime, w->eb_cnt, w->eb_keys,
                   w->qb_ltime, w->qb_cnt, w->qb_ids, w->rumors, w->v_time, w->q_pruned, w->q_expired,
-                  w->dlog, w->dcnt, w->snap_bits, w->snap_sn};
+                  w->dlog, w->dcnt, w->snap_bits, w->snap_sn, w->q_hwm};
   for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) free(ptrs[i]);
   memset(w, 0, sizeof(*w));
 }
@@ -874,21 +881,25 @@ static inline uint64_t tlq_key(uint16_t tx, uint16_t len, uint32_t seq) {
   return ((uint64_t)tx << 48) | ((uint64_t)(0xFFFFu - len) << 32) | (uint64_t)(0xFFFFFFFFu - seq);
 }
 
+/* Slot order is free (the queue's CONTENT is what the model defines): a queue's live items
+ * sit in slots [0, hwm), so every scan stops at the high-water mark. */
 void orc_queue_insert(orc_world* w, uint32_t m, uint32_t q, uint32_t rumor) {
   size_t base = ((size_t)m * 3 + q) * w->qcap;
+  uint32_t* hwm = &w->q_hwm[(size_t)m * 3 + q];
   uint32_t seq = w->q_next_seq[(size_t)m * 3 + q]++;
   uint16_t len = w->rumors[orc_rumor_index(w, rumor)].msg_len;
   uint32_t slot = EMPTY_RUMOR;
-  for (uint32_t i = 0; i < w->qcap; ++i)
+  for (uint32_t i = 0; i < *hwm; ++i)
     if (w->q_rumor[base + i] == EMPTY_RUMOR) {
       slot = i;
       break;
     }
+  if (slot == EMPTY_RUMOR && *hwm < w->qd[q]) slot = (*hwm)++;
   if (slot == EMPTY_RUMOR) { /* full: prune the last item in send order */
     w->q_pruned[m]++;
     w->err[m] |= ORC_E_QUEUE_PRUNE;
     uint64_t kmax = 0;
-    for (uint32_t i = 0; i < w->qcap; ++i) {
+    for (uint32_t i = 0; i < *hwm; ++i) {
       uint64_t k = tlq_key(w->q_tx[base + i], w->q_len[base + i], w->q_seq[base + i]);
       if (slot == EMPTY_RUMOR || k > kmax) {
         kmax = k;
@@ -922,7 +933,8 @@ int orc_rumor_live(const orc_world* w, uint32_t rid) {
 uint32_t orc_queue_expire(orc_world* w, uint32_t m, uint32_t q) {
   size_t base = ((size_t)m * 3 + q) * w->qcap;
   uint32_t cnt = 0;
-  for (uint32_t i = 0; i < w->qcap; ++i) {
+  const uint32_t hwm = w->q_hwm[(size_t)m * 3 + q];
+  for (uint32_t i = 0; i < hwm; ++i) {
     if (w->q_rumor[base + i] == EMPTY_RUMOR || orc_rumor_live(w, w->q_rumor[base + i])) continue;
     w->q_rumor[base + i] = EMPTY_RUMOR;
     w->q_seq[base + i] = 0;
@@ -939,7 +951,9 @@ uint32_t orc_queue_expire(orc_world* w, uint32_t m, uint32_t q) {
 uint32_t orc_queue_get_broadcasts(orc_world* w, uint32_t m, uint32_t q, uint32_t limit,
                                   uint32_t* out, uint32_t max_out, uint32_t* bytes_used) {
   size_t base = ((size_t)m * 3 + q) * w->qcap;
-  uint8_t picked[ORC_MAX_QCAP] = {0}; /* per slot: taken by this call */
+  const uint32_t hwm = w->q_hwm[(size_t)m * 3 + q];
+  uint8_t picked[ORC_MAX_QCAP]; /* per slot: taken by this call */
+  memset(picked, 0, hwm);
   int64_t used = 0;
   uint32_t cnt = 0;
   for (;;) {
@@ -947,7 +961,7 @@ uint32_t orc_queue_get_broadcasts(orc_world* w, uint32_t m, uint32_t q, uint32_t
     if (free_b <= 0) break;
     uint32_t best = EMPTY_RUMOR;
     uint64_t kbest = UINT64_MAX;
-    for (uint32_t i = 0; i < w->qcap; ++i) {
+    for (uint32_t i = 0; i < hwm; ++i) {
       if (w->q_rumor[base + i] == EMPTY_RUMOR || picked[i]) continue;
       if ((int64_t)w->q_len[base + i] > free_b) continue;
       uint64_t k = tlq_key(w->q_tx[base + i], w->q_len[base + i], w->q_seq[base + i]);
@@ -962,7 +976,7 @@ uint32_t orc_queue_get_broadcasts(orc_world* w, uint32_t m, uint32_t q, uint32_t
     used += (int64_t)w->overhead + w->q_len[base + best];
     picked[best] = 1;
   }
-  for (uint32_t i = 0; i < w->qcap; ++i) {
+  for (uint32_t i = 0; i < hwm; ++i) {
     if (!picked[i]) continue;
     if ((uint32_t)w->q_tx[base + i] + 1 >= w->tx_limit) w->q_rumor[base + i] = EMPTY_RUMOR;
     else w->q_tx[base + i]++;
@@ -979,14 +993,15 @@ void orc_check_queues(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue
   for (uint32_t m = 0; m < w->n; ++m)
     for (uint32_t q = 0; q < 3; ++q) {
       size_t base = ((size_t)m * 3 + q) * w->qcap;
+      const uint32_t hwm = w->q_hwm[(size_t)m * 3 + q];
       uint32_t numq = 0;
-      for (uint32_t i = 0; i < w->qcap; ++i) numq += w->q_rumor[base + i] != EMPTY_RUMOR;
+      for (uint32_t i = 0; i < hwm; ++i) numq += w->q_rumor[base + i] != EMPTY_RUMOR;
       st[q] += numq;
       if (numq >= depth_warning) st[3 + q]++;
       while (numq > mx) { /* numq >= max -> prune(max): drop the max item until max remain */
         uint32_t worst = EMPTY_RUMOR;
         uint64_t kmax = 0;
-        for (uint32_t i = 0; i < w->qcap; ++i) {
+        for (uint32_t i = 0; i < hwm; ++i) {
           if (w->q_rumor[base + i] == EMPTY_RUMOR) continue;
           uint64_t k = tlq_key(w->q_tx[base + i], w->q_len[base + i], w->q_seq[base + i]);
           if (worst == EMPTY_RUMOR || k > kmax) {
@@ -1119,7 +1134,10 @@ static void phase_ml(world_job* j) {
 /* 4. emission: each live sender, k peers, broadcast_messages (delegate.rs:307-374) */
 static void phase_emit(world_job* j) {
   orc_world* w = j->w;
-  const uint32_t n = w->n, k = w->fanout, cap_t = 3 * w->qcap;
+  /* records per (sender, peer): every message costs at least overhead + 15 B of the budget
+   * (the shortest of the length model, orc_msg_len), so this bounds one peer's picks */
+  const uint32_t per_peer = w->limit / (w->overhead + 15) + 1;
+  const uint32_t n = w->n, k = w->fanout, cap_t = 3 * w->qcap < per_peer ? 3 * w->qcap : per_peer;
   uint32_t peers[64], buf[3 * ORC_MAX_QCAP];
   j->cap = (size_t)(j->hi - j->lo) * k * cap_t;
   j->rec_recv = (uint32_t*)malloc((j->cap ? j->cap : 1) * sizeof(uint32_t));
@@ -2123,7 +2141,7 @@ int orc_world_restart(orc_world* w, uint32_t m, const uint8_t* file, uint64_t le
     w->q_tx[q] = 0;
     w->q_len[q] = 0;
   }
-  for (uint32_t q = 0; q < 3; ++q) w->q_next_seq[(size_t)m * 3 + q] = 0;
+  for (uint32_t q = 0; q < 3; ++q) w->q_next_seq[(size_t)m * 3 + q] = w->q_hwm[(size_t)m * 3 + q] = 0;
   memset(w->eb_ltime + (size_t)m * w->ebuf, 0, (size_t)w->ebuf * 8);
   memset(w->eb_cnt + (size_t)m * w->ebuf, 0, (size_t)w->ebuf * 4);
   memset(w->eb_keys + (size_t)m * w->ebuf * w->slot_k, 0, (size_t)w->ebuf * w->slot_k * 8);

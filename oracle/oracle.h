@@ -257,12 +257,19 @@ typedef struct {
   uint32_t snap_w;
   int32_t snap_rejoin; /* Options::rejoin_after_leave */
   uint64_t* snap_sn;   /* [n][4] */
+  /* queue capacity per queue (intent, query, event): qd[q] <= qcap, the slot stride.  The
+   * reference's TransmitLimitedQueue is unbounded between QueueChecker ticks; a capacity
+   * deeper than any queue gets between ticks is exactly that (base.rs:720-760). */
+  uint32_t qd[3];
+  uint32_t* q_hwm; /* [n][3] slots [0, hwm) may be live, [hwm, qd) are free (scan bound) */
 } orc_world;
 
 typedef struct {
   uint32_t n, s, qcap, ebuf, qbuf, slot_k, fanout, limit, overhead, retransmit_mult, max_refute;
   uint32_t cap_rumors;
   uint64_t seed;
+  uint32_t qdepth[3]; /* per-queue capacity (intent, query, event); 0 = qcap */
+  uint32_t _pad;
 } orc_world_cfg;
 
 int orc_world_init(orc_world* w, const orc_world_cfg* cfg);
@@ -284,7 +291,7 @@ int orc_handle_user_event_cc(orc_world* w, uint32_t m, uint64_t ltime, uint64_t 
  * (MemberEventType, subject, ORC_LOG_MEMBER); the third word holds the flags */
 #define ORC_LOG_CC 1ull         /* a user event's cc flag */
 #define ORC_LOG_MEMBER 0x100ull /* a member event */
-#define ORC_MAX_QCAP 256 /* slots per transmit-limited queue (the engine's queue_cap range) */
+#define ORC_MAX_QCAP 8192 /* slots per transmit-limited queue (the engine's head + tail depth range) */
 int orc_world_set_delivery_log(orc_world* w, uint32_t per_member);
 int orc_handle_query(orc_world* w, uint32_t m, uint64_t ltime, uint32_t id, int no_broadcast);
 int orc_upsert_intent(orc_world* w, uint32_t m, uint32_t subj, uint8_t kind, uint64_t ltime);

@@ -9,11 +9,19 @@ import oracle_ffi as O
 L = O.lib()
 
 
+def queue_depths(cfg):
+    """each queue's capacity: queue_cap, or the deeper queue_depth (head + HBM tail)"""
+    d = getattr(cfg, "queue_depth", None) or (0, 0, 0)
+    return [int(x) if x else cfg.queue_cap for x in d]
+
+
 def oracle_world(cfg, subj_member, views):
-    wc = O.WorldCfg(n=cfg.n_members, s=cfg.n_subjects, qcap=cfg.queue_cap, ebuf=cfg.event_buffer_size,
+    qd = queue_depths(cfg)
+    wc = O.WorldCfg(n=cfg.n_members, s=cfg.n_subjects, qcap=max(qd), ebuf=cfg.event_buffer_size,
                     qbuf=cfg.query_buffer_size, slot_k=cfg.slot_k, fanout=cfg.fanout, limit=cfg.gossip_limit,
                     overhead=cfg.gossip_overhead, retransmit_mult=cfg.retransmit_mult, max_refute=cfg.max_refute,
                     cap_rumors=cfg.max_rumors, seed=cfg.seed)
+    wc.qdepth[:] = qd
     w = O.World()
     assert L.orc_world_init(C.byref(w), C.byref(wc)) == 0
     n, s = cfg.n_members, cfg.n_subjects

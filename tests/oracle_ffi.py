@@ -85,14 +85,16 @@ class World(C.Structure):
                 ("merges", C.c_uint64), ("sends", C.c_uint64), ("deliveries", C.c_uint64),
                 ("v_time", P32), ("now", C.c_uint32), ("q_pruned", P32), ("q_expired", P32),
                 ("gen", C.c_uint32), ("rbits", C.c_uint32), ("dlog", P64), ("dcnt", P32), ("dcap", C.c_uint32),
-                ("snap_bits", P32), ("snap_w", C.c_uint32), ("snap_rejoin", C.c_int32), ("snap_sn", P64)]
+                ("snap_bits", P32), ("snap_w", C.c_uint32), ("snap_rejoin", C.c_int32), ("snap_sn", P64),
+                ("qd", C.c_uint32 * 3), ("q_hwm", P32)]
 
 
 class WorldCfg(C.Structure):
     _fields_ = [("n", C.c_uint32), ("s", C.c_uint32), ("qcap", C.c_uint32), ("ebuf", C.c_uint32),
                 ("qbuf", C.c_uint32), ("slot_k", C.c_uint32), ("fanout", C.c_uint32),
                 ("limit", C.c_uint32), ("overhead", C.c_uint32), ("retransmit_mult", C.c_uint32),
-                ("max_refute", C.c_uint32), ("cap_rumors", C.c_uint32), ("seed", C.c_uint64)]
+                ("max_refute", C.c_uint32), ("cap_rumors", C.c_uint32), ("seed", C.c_uint64),
+                ("qdepth", C.c_uint32 * 3), ("_pad", C.c_uint32)]
 
 
 class Action(C.Structure):
