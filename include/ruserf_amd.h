@@ -271,7 +271,17 @@ typedef struct rsf_gossip_cfg {
                                   been recycled since expires at its member's next emission */
   uint32_t _reserved;
   uint64_t seed;               /* Philox key of peer selection */
+  /* Deep queues: capacity of the intent / query / event queue (0 = queue_cap).  A depth above
+   * queue_cap (which must then be <= 64) keeps the queue's first queue_cap slots as the
+   * register head emission works on and the rest as an unordered HBM tail of depth - queue_cap
+   * items, up to RSF_MAX_QUEUE_DEPTH.  The reference's TransmitLimitedQueue is unbounded between
+   * QueueChecker ticks (max_queue_depth 4096, core/src/options.rs:512; pruned only by the checker,
+   * core/src/serf/base.rs:720-760): a depth no queue reaches between ticks is that queue exactly;
+   * past it the bounded-queue prune applies (RSF_E_QUEUE_PRUNE, counted). */
+  uint32_t queue_depth[3];
+  uint32_t _reserved2;
 } rsf_gossip_cfg;
+#define RSF_MAX_QUEUE_DEPTH 4160 /* head (<= 64) + tail: max_queue_depth 4096 plus a round's headroom */
 
 /* One rumor (a broadcast message body; SerfBroadcast, core/src/broadcast.rs:153-183). 24 bytes. */
 typedef struct rsf_rumor {
@@ -559,8 +569,17 @@ int rsf_gossip_dump_view(rsf_gossip* g, uint64_t* ltime, uint8_t* status, uint8_
 /* the same for local rows [row0, row0 + rows) only (rows x n_subjects entries) */
 int rsf_gossip_dump_view_rows(rsf_gossip* g, uint64_t row0, uint64_t rows, uint64_t* ltime, uint8_t* status,
                               uint8_t* kind, uint32_t* time);
+/* queues [n_loc][3][D] in send order (live items first, then free slots: rumor 0xFFFFFFFF),
+ * D = the deepest queue's capacity (queue_cap, or max(queue_depth)); next_seq [n_loc][3] */
 int rsf_gossip_dump_queues(rsf_gossip* g, uint32_t* rumor, uint32_t* seq, uint16_t* transmits, uint16_t* len,
                            uint32_t* next_seq);
+/* the same with `width` slots per queue ([n_loc][3][width]: each queue's first width items in
+ * send order); *max_live (optional) = the most items any queue holds (> width: truncated) */
+int rsf_gossip_dump_queues_width(rsf_gossip* g, uint32_t width, uint32_t* rumor, uint32_t* seq, uint16_t* transmits,
+                                 uint16_t* len, uint32_t* next_seq, uint32_t* max_live);
+/* deep queues: members whose emission took the exact whole-queue path (the head alone could
+ * not decide a pick; emit_deep_kernel) since creation, and since the last call */
+int rsf_gossip_deep_stats(rsf_gossip* g, uint64_t* slow_total, uint64_t* slow_since_last);
 int rsf_gossip_dump_buffers(rsf_gossip* g, uint64_t* eb_ltime, uint32_t* eb_cnt, uint64_t* eb_keys,
                             uint64_t* qb_ltime, uint32_t* qb_cnt, uint32_t* qb_ids);
 int rsf_gossip_dump_rumors(rsf_gossip* g, uint32_t first, uint32_t count, rsf_rumor* out);

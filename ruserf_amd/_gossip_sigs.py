@@ -10,7 +10,7 @@ class RsfGossipCfg(C.Structure):
                 ("query_buffer_size", C.c_uint32), ("slot_k", C.c_uint32), ("fanout", C.c_uint32),
                 ("gossip_limit", C.c_uint32), ("gossip_overhead", C.c_uint32), ("retransmit_mult", C.c_uint32),
                 ("max_refute", C.c_uint32), ("max_rumors", C.c_uint32), ("_reserved", C.c_uint32),
-                ("seed", C.c_uint64)]
+                ("seed", C.c_uint64), ("queue_depth", C.c_uint32 * 3), ("_reserved2", C.c_uint32)]
 
 
 def declare(L):
@@ -47,6 +47,8 @@ def declare(L):
     sig("rsf_gossip_reap", [VP, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32])
     sig("rsf_gossip_set_now", [VP, C.c_uint32])
     sig("rsf_gossip_dump_queues", [VP, P32, P32, P16, P16, P32])
+    sig("rsf_gossip_deep_stats", [VP, P64, P64])
+    sig("rsf_gossip_dump_queues_width", [VP, C.c_uint32, P32, P32, P16, P16, P32, P32])
     sig("rsf_gossip_dump_buffers", [VP, P64, P32, P64, P64, P32, P32])
     sig("rsf_gossip_dump_rumors", [VP, C.c_uint32, C.c_uint32, VP])
     sig("rsf_gossip_dump_refutes", [VP, P32, P64])

@@ -118,6 +118,21 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
   return lane63_u64(v);
 }
 #undef RSF_DPP_STEP
+#define RSF_DPP_STEP32(CTRL, RM)                                                               \
+  {                                                                                            \
+    const uint32_t o_ = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, RM, 0xF, false); \
+    v = o_ < v ? o_ : v;                                                                       \
+  }
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  RSF_DPP_STEP32(0xB1, 0xF)
+  RSF_DPP_STEP32(0x4E, 0xF)
+  RSF_DPP_STEP32(0x124, 0xF)
+  RSF_DPP_STEP32(0x128, 0xF)
+  RSF_DPP_STEP32(0x142, 0xA)
+  RSF_DPP_STEP32(0x143, 0xC)
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+#undef RSF_DPP_STEP32
 
 // inclusive prefix max over the wave (lane 0 first); identity 0
 template <int CTRL, int ROWMASK>
@@ -409,14 +424,22 @@ __device__ __forceinline__ void q_rerank(const GCfg& c, QRegs& Q, uint32_t lane,
 #ifndef RSF_EMIT_LAZY
 #define RSF_EMIT_LAZY 1  // emit: one deferred re-rank per queue per emission (q_get_broadcasts_lazy)
 #endif
-template <bool PERMUTE_DEC>
+// DEEP (a tail behind the head, its key / length lower bounds tmin / tminlen): the call is
+// exact only if every pick's key is below tmin and every stop with budget left is one no tail
+// item could fit; otherwise *unsafe is set and the caller abandons the emission (the member
+// then takes emit_deep_kernel's whole-queue path).  Picks are checked before they are bumped.
+template <bool PERMUTE_DEC, bool DEEP = false>
 __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uint32_t lane, int64_t limit,
                                                     uint32_t* stage_val, uint32_t* stage_dec,
                                                     uint64_t out_base, uint32_t& nrec, uint32_t& err, bool& dirty,
-                                                    QLds& row) {
+                                                    QLds& row, uint64_t tmin = ~0ull, uint32_t tminlen = ~0u,
+                                                    bool* unsafe = nullptr) {
   const bool valid = lane < c.qcap;
   const uint64_t live_m = ballot(valid && Q.r != kEmpty);  // a sorted queue: a prefix
-  if (!live_m) return 0;
+  if (!live_m) {
+    if (DEEP && tmin != ~0ull && limit - (int64_t)c.overhead >= (int64_t)tminlen) *unsafe = true;
+    return 0;
+  }
   const bool live = lane_bit(live_m);
   const uint32_t len = Q.tl >> 16;
   // Live items are the sorted prefix.  If every earlier item was taken, item i fits iff
@@ -432,11 +455,20 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
     const int32_t free_b = (int32_t)(lim - used - c.overhead);
     if (free_b <= 0) break;
     const uint64_t cand = ballot(len <= (uint32_t)free_b) & live_m & ~pick_m;
-    if (!cand) break;
+    if (!cand) {
+      if (DEEP && tminlen <= (uint32_t)free_b) *unsafe = true;  // a tail item might fit
+      break;
+    }
     const int win = __ffsll((long long)cand) - 1;
     pick_m |= 1ull << win;
     used += c.overhead + shfl_u32(len, win);
   }
+  if (DEEP && pick_m) {  // the largest pick (the highest lane: the head is sorted) below the tail
+    const int hl = 63 - __clzll((long long)pick_m);
+    const uint32_t tl = shfl_u32(Q.tl, hl);
+    if (tlq_key(tl & 0xFFFF, tl >> 16, shfl_u32(Q.sq, hl)) >= tmin) *unsafe = true;
+  }
+  if (DEEP && *unsafe) return used;
   if (!pick_m) return used;
   // picks are in ascending lane (= send) order: record rank = picked lanes below
   const bool picked = lane_bit(pick_m);
@@ -553,13 +585,18 @@ __device__ __forceinline__ int64_t q_get_broadcasts_lazy(const GCfg& c, QRegs& Q
 // Per-peer state is lane-distributed: lane j (< np) holds peer j's bytes used so far (used_v),
 // records written so far (nrec_v) and the element offset of its group's record slots from
 // ov / od (off_v; ~0 = no output: a bucket over capacity).
-template <bool PERMUTE_DEC>
+// DEEP: as q_get_broadcasts -- abandoned (*unsafe) as soon as the head alone cannot decide.
+template <bool PERMUTE_DEC, bool DEEP = false>
 __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t lane, uint32_t np, uint32_t& used_v,
                                              uint32_t& nrec_v, uint64_t off_v, uint32_t* ov, uint32_t* od,
-                                             uint32_t& err, bool& dirty, QLds& row, uint64_t* ep = nullptr) {
+                                             uint32_t& err, bool& dirty, QLds& row, uint64_t* ep = nullptr,
+                                             uint64_t tmin = ~0ull, uint32_t tminlen = ~0u, bool* unsafe = nullptr) {
   const bool valid = lane < c.qcap;
   const uint64_t live_m = ballot(valid && Q.r != kEmpty);  // a sorted queue: a prefix
-  if (!live_m) return;
+  if (!live_m) {
+    if (DEEP && tmin != ~0ull) *unsafe = true;  // only the tail holds items
+    return;
+  }
 #if RSF_EMIT_PROF
   const uint64_t pp0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -596,7 +633,10 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
       const int32_t free_b = (int32_t)(limit - used - c.overhead);
       if (free_b <= 0) break;
       const uint64_t fit = ballot(len <= (uint32_t)free_b) & avail & ~pick;
-      if (!fit) break;
+      if (!fit) {
+        if (DEEP && tminlen <= (uint32_t)free_b) *unsafe = true;  // a tail item might fit
+        break;
+      }
       const uint64_t cand = fit & rem;
       if (!cand) {  // the next candidate lies past the class-t0 run (or is a bumped pick)
         exact = true;
@@ -608,6 +648,7 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
       skipped = true;
     }
     if (exact) break;
+    if (DEEP && *unsafe) return;
     if (pick) {
       const uint32_t npick = (uint32_t)__popcll(pick);
       const uint32_t nrec = shfl_u32(nrec_v, j);
@@ -630,6 +671,14 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
   ep[0] += pp1 - pp0;  // picks (prefix sums, fit loops)
   if (exact) ep[4] += 1;  // emissions that needed the exact path
 #endif
+  if (DEEP && cons) {  // the largest deferred pick (highest lane) below the tail
+    const int hl = 63 - __clzll((long long)cons);
+    const uint32_t tl = shfl_u32(Q.tl, hl);
+    if (tlq_key(tl & 0xFFFF, tl >> 16, shfl_u32(Q.sq, hl)) >= tmin) {
+      *unsafe = true;
+      return;
+    }
+  }
   if (cons) {
     // the deferred picks: records to their groups, then transmits + 1 or retired
     const bool picked = lane_bit(cons);
@@ -665,8 +714,10 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
     uint32_t nrec = shfl_u32(nrec_v, j);
     const uint64_t off = shfl_u64(off_v, j);
     const bool out = off != ~0ull;
-    const int64_t used = q_get_broadcasts<PERMUTE_DEC>(c, Q, lane, limit, out ? ov : nullptr, out ? od : nullptr,
-                                                       out ? off : 0ull, nrec, err, dirty, row);
+    const int64_t used = q_get_broadcasts<PERMUTE_DEC, DEEP>(c, Q, lane, limit, out ? ov : nullptr, out ? od : nullptr,
+                                                             out ? off : 0ull, nrec, err, dirty, row, tmin, tminlen,
+                                                             unsafe);
+    if (DEEP && *unsafe) return;
     used_v += lane == j ? (uint32_t)used : 0u;
     nrec_v = lane == j ? nrec : nrec_v;
   }
@@ -674,6 +725,27 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
   ep[3] += __builtin_amdgcn_s_memtime() - pp3;  // exact tail
 #endif
 }
+
+// Deep queues: the running tail of one (member, queue) while a wave works on its head.  cnt,
+// minlen, minkey mirror tsum (wave-uniform); spills are written at t[cnt ...] (the row has
+// kTailSlack slots past the capacity) and counted in only by the caller's commit.
+struct Spill {
+  uint4* t = nullptr;
+  uint32_t cnt = 0, minlen = 0xFFFFFFFFu;
+  uint64_t minkey = ~0ull;
+};
+__device__ __forceinline__ Spill spill_of(const GCfg& c, const GState& s, uint64_t l, uint32_t q, uint4 sm) {
+  Spill sp;
+  sp.t = s.tail[q] + l * c.tstride[q];
+  sp.cnt = sm.x;
+  sp.minlen = sm.y;
+  sp.minkey = ((uint64_t)sm.w << 32) | sm.z;
+  return sp;
+}
+__device__ __forceinline__ uint4 spill_sum(const Spill& sp) {
+  return make_uint4(sp.cnt, sp.minlen, (uint32_t)sp.minkey, (uint32_t)(sp.minkey >> 32));
+}
+constexpr uint4 kTSumEmpty = {0u, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
 
 // Batched insert of new items (transmits 0, seqs seq0, seq0 + 1, ... in lane order over
 // `newmask`) into a sorted register-resident queue: the result is the qcap smallest keys of
@@ -686,10 +758,12 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
 // every item is written to its place in the wave's LDS row and read back in order.
 // DEC: the items' record decorations (Q.dec / dec) move with them.
 // Returns the number of live items that did not fit (memberlist Prune of the tail).
-template <bool DEC>
+// SPILL (deep queues): the items that do not fit the head go to the tail instead (sp), and
+// the return value is 0; the caller checks the tail's capacity.
+template <bool DEC, bool SPILL = false>
 __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, uint32_t lane, bool ins, uint32_t rid,
                                                        uint32_t dec, uint32_t len, uint32_t seq0, uint64_t newmask,
-                                                       QLds& row) {
+                                                       QLds& row, Spill* sp = nullptr) {
   const bool valid = lane < c.qcap;
   const uint64_t live_m = ballot(valid && Q.r != kEmpty);
   const bool live = lane_bit(live_m);
@@ -710,6 +784,22 @@ __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, 
     const uint32_t ab = mbcnt_above(same);
     pos_n = lane_bit(same) ? base + ab : pos_n;
     pos_e += lane_bit(etx0_m & ~gt_old_m) ? (uint32_t)__popcll(same) : 0u;
+  }
+  if (SPILL && n_live + n_new > c.qcap) {
+    // positions past the head are the largest keys, in order: they go to the tail, the one at
+    // position qcap being the smallest of them
+    const bool sn = ins && pos_n >= c.qcap, se = live && pos_e >= c.qcap;
+    if (sn) sp->t[sp->cnt + (pos_n - c.qcap)] = make_uint4(rid, myseq, len << 16, DEC ? dec : 0u);
+    if (se) sp->t[sp->cnt + (pos_e - c.qcap)] = make_uint4(Q.r, Q.sq, Q.tl, DEC ? Q.dec : 0u);
+    const uint64_t at_n = ballot(ins && pos_n == c.qcap), at_e = ballot(live && pos_e == c.qcap);
+    const int w = __ffsll((long long)(at_n | at_e)) - 1;
+    const uint32_t tl_w = at_n ? (shfl_u32(len, w) << 16) : shfl_u32(Q.tl, w);
+    const uint32_t sq_w = at_n ? shfl_u32(myseq, w) : shfl_u32(Q.sq, w);
+    const uint64_t kmin = tlq_key(tl_w & 0xFFFF, tl_w >> 16, sq_w);
+    const uint32_t lmin = wave_min_u32(min(sn ? len : 0xFFFFFFFFu, se ? elen : 0xFFFFFFFFu));
+    sp->cnt += n_live + n_new - c.qcap;
+    sp->minkey = kmin < sp->minkey ? kmin : sp->minkey;
+    sp->minlen = lmin < sp->minlen ? lmin : sp->minlen;
   }
   if (ins && pos_n < c.qcap) {
     row.r[pos_n] = rid;
@@ -741,7 +831,7 @@ __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, 
     }
   }
   __builtin_amdgcn_wave_barrier();  // the row is free once every lane has read it
-  return total > c.qcap ? total - c.qcap : 0u;
+  return (!SPILL && total > c.qcap) ? total - c.qcap : 0u;
 }
 
 // A member's pending re-queues (pc: their packed counts, which the caller may hold in
@@ -766,9 +856,9 @@ __device__ __forceinline__ void pend_load(const GState& s, uint64_t l, uint32_t 
     }
   }
 }
-template <bool DEC>
+template <bool DEC, bool SPILL = false>
 __device__ __forceinline__ uint32_t pend_apply(const GCfg& c, QRegs& Q, uint32_t lane, uint32_t q, uint32_t n,
-                                               const PendRegs& p, uint32_t seq0, QLds& row) {
+                                               const PendRegs& p, uint32_t seq0, QLds& row, Spill* sp = nullptr) {
   uint32_t drops = 0, seq = seq0;
 #pragma unroll
   for (uint32_t b = 0; b < 2; ++b) {
@@ -776,8 +866,52 @@ __device__ __forceinline__ uint32_t pend_apply(const GCfg& c, QRegs& Q, uint32_t
     const bool ins = b * kWave + lane < n && (p.lq[b] >> 16) == q;
     const uint64_t m = ballot(ins);
     if (!m) continue;
-    drops += q_insert_batch_lds<DEC>(c, Q, lane, ins, p.rid[b], p.dec[b], p.lq[b] & 0xFFFF, seq, m, row);
+    drops += q_insert_batch_lds<DEC, SPILL>(c, Q, lane, ins, p.rid[b], p.dec[b], p.lq[b] & 0xFFFF, seq, m, row, sp);
     seq += (uint32_t)__popcll(m);
+  }
+  return drops;
+}
+
+// Deep queues: while head + tail hold more than the queue's depth, drop the largest key of the
+// two (the head's is its last live lane; the tail's is found by a pass over it) -- the bounded
+// queue's prune, rare (a queue at its full depth).  One wave; returns the number dropped.
+__device__ __forceinline__ uint32_t deep_prune_wave(const GCfg& c, QRegs& Q, uint32_t lane, uint32_t q, Spill& sp) {
+  uint32_t drops = 0;
+  while (sp.cnt > c.tcap[q]) {
+    const uint64_t live_m = ballot(lane < c.qcap && Q.r != kEmpty);
+    uint64_t hk = 0;
+    int hl = -1;
+    if (live_m) {
+      hl = 63 - __clzll((long long)live_m);
+      const uint32_t tl = shfl_u32(Q.tl, hl);
+      hk = tlq_key(tl & 0xFFFF, tl >> 16, shfl_u32(Q.sq, hl));
+    }
+    uint64_t tk = 0;
+    uint32_t ti = 0;
+    for (uint32_t b = 0; b < sp.cnt; b += kWave) {  // the tail holds items (cnt > tcap >= 1)
+      const bool in = b + lane < sp.cnt;
+      const uint4 e = in ? sp.t[b + lane] : make_uint4(0u, 0u, 0u, 0u);
+      const uint64_t k = in ? tlq_key(e.z & 0xFFFF, e.z >> 16, e.y) : 0ull;
+      const uint64_t m = wave_max_u64(k);
+      const uint64_t at = ballot(in && k == m);
+      if (at && (b == 0 || m > tk)) {
+        tk = m;
+        ti = b + (uint32_t)(__ffsll((long long)at) - 1);
+      }
+    }
+    if (hl >= 0 && hk > tk) {
+      if ((int)lane == hl) {
+        Q.r = kEmpty;
+        Q.sq = 0;
+        Q.tl = 0;
+      }
+    } else {
+      const uint4 last = sp.t[sp.cnt - 1];
+      if (lane == 0) sp.t[ti] = last;
+      __threadfence_block();  // the next pass reads the moved item
+      sp.cnt--;
+    }
+    drops++;
   }
   return drops;
 }
@@ -795,7 +929,14 @@ __device__ __forceinline__ uint32_t pend_flush_wave(const GCfg& c, const GState&
     QRegs Q{kEmpty, 0, 0};
     q_load(c, s, l, q, lane, Q);
     const uint32_t seq0 = s.q_next_seq[l * 3 + q];
-    drops += pend_apply<true>(c, Q, lane, q, n, p, seq0, row);
+    if (c.tcap[q]) {  // deep queue: the head's overflow spills into the tail
+      Spill sp = spill_of(c, s, l, q, s.tsum[l * 3 + q]);
+      pend_apply<true, true>(c, Q, lane, q, n, p, seq0, row, &sp);
+      drops += deep_prune_wave(c, Q, lane, q, sp);
+      if (lane == 0) s.tsum[l * 3 + q] = spill_sum(sp);
+    } else {
+      drops += pend_apply<true>(c, Q, lane, q, n, p, seq0, row);
+    }
     q_store(c, s, l, q, lane, Q, true);
     if (lane == 0) s.q_next_seq[l * 3 + q] = seq0 + nq;
   }
@@ -1152,18 +1293,22 @@ enum : uint32_t { kEhPend = 3, kEhSeq = 4, kEhPruned = 7, kEhErr = 8 };
 struct EmitIn {
   QRegs Q0;
   uint32_t head, gk, gs;
+  uint4 ts;  // deep queues: lane q < 3 holds queue q's tail summary (tsum)
 #if RSF_EMIT_SPEC_PEND
   GState::PendE p0;  // pending entry `lane` (valid when lane < the member's count)
 #endif
 };
+template <bool DEEP = false>
 __device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const uint32_t* __restrict__ grp_key,
                                           const uint32_t* __restrict__ slot, uint64_t l, uint32_t lane, EmitIn& e) {
   e.Q0 = QRegs{kEmpty, 0, 0};
   e.head = kEmpty;
   e.gk = kSentinel;
   e.gs = 0;
+  e.ts = kTSumEmpty;
   if (l >= c.n_loc) return;  // wave-uniform: a wave's last member may lie past the shard
   q_load(c, s, l, 0, lane, e.Q0);
+  if (DEEP && lane < 3) e.ts = s.tsum[l * 3 + lane];
   const uint32_t* hp = nullptr;
   if (lane == 1 || lane == 2) hp = s.q_rumor + (l * 3 + lane) * c.qcap;
   else if (lane == kEhPend) hp = s.p_cnt + l;
@@ -1192,7 +1337,11 @@ __device__ __forceinline__ void bkt_group_keys(const Buckets& bk, uint32_t lane,
   b[bk.keys_off + idx] = gk;
   if (zero_count) b[bk.cnt_off + idx] = 0u;
 }
-template <bool BKT>
+// DEEP (queues with an HBM tail): the emission runs on the heads as below; it is committed
+// only if every pick was decided by the head alone (q_pick_peers' checks against the tails'
+// bounds) and every spill fits its tail -- otherwise nothing is stored (records written to the
+// group slots are rewritten) and the member is listed for emit_deep_kernel.
+template <bool BKT, bool DEEP = false>
 __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_t l, uint32_t lane, EmitIn& e,
                                          uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val,
                                          uint32_t* __restrict__ out_dec, const Buckets& bk, QLds& row) {
@@ -1207,12 +1356,28 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   const uint32_t np = (uint32_t)__popcll(pm);
   const uint32_t pc = shfl_u32(e.head, kEhPend), npend = pend_total(pc);
   if (RSF_BAD2(8, npend > kPend || ((pc >> 24) != 0), pc)) return;
-  const bool ne0 = shfl_u32(Q0.r, 0) != kEmpty || (pc & 0xFF), ne1 = shfl_u32(e.head, 1) != kEmpty || ((pc >> 8) & 0xFF),
-             ne2 = shfl_u32(e.head, 2) != kEmpty || ((pc >> 16) & 0xFF);
+  // deep queues: a queue is non-empty if its tail holds items too
+  const uint32_t tc0 = DEEP ? shfl_u32(e.ts.x, 0) : 0u, tc1 = DEEP ? shfl_u32(e.ts.x, 1) : 0u,
+                 tc2 = DEEP ? shfl_u32(e.ts.x, 2) : 0u;
+  const bool ne0 = shfl_u32(Q0.r, 0) != kEmpty || (pc & 0xFF) || tc0,
+             ne1 = shfl_u32(e.head, 1) != kEmpty || ((pc >> 8) & 0xFF) || tc1,
+             ne2 = shfl_u32(e.head, 2) != kEmpty || ((pc >> 16) & 0xFF) || tc2;
   // no peers: nothing is sent, and the pending re-queues wait for the next emission
   if (np == 0 || !(ne0 || ne1 || ne2)) {
     if (BKT) bkt_group_keys(bk, lane, np, e.gk, e.gs, true);
     return;
+  }
+  Spill sp[3];
+  bool unsafe = false;
+  if (DEEP) {
+#pragma unroll
+    for (uint32_t q = 0; q < 3; ++q)
+      if (c.tcap[q]) {
+        sp[q].t = s.tail[q] + l * c.tstride[q];
+        sp[q].cnt = shfl_u32(e.ts.x, q);
+        sp[q].minlen = shfl_u32(e.ts.y, q);
+        sp[q].minkey = ((uint64_t)shfl_u32(e.ts.w, q) << 32) | shfl_u32(e.ts.z, q);
+      }
   }
   EPROF_T(t1);
   EPROF_ADD(0, t0, t1);
@@ -1251,18 +1416,23 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
     // applied first: in the reference they were queued when the messages arrived
     uint32_t& drops = drops_all;
     if (pc & 0xFF) {
-      drops += pend_apply<true>(c, Q0, lane, 0, npend, pr, shfl_u32(e.head, kEhSeq), row);
+      if (DEEP && c.tcap[0]) pend_apply<true, true>(c, Q0, lane, 0, npend, pr, shfl_u32(e.head, kEhSeq), row, &sp[0]);
+      else drops += pend_apply<true>(c, Q0, lane, 0, npend, pr, shfl_u32(e.head, kEhSeq), row);
       d0 = true;
     }
     if ((pc >> 8) & 0xFF) {
-      drops += pend_apply<false>(c, Q1, lane, 1, npend, pr, shfl_u32(e.head, kEhSeq + 1), row);
+      if (DEEP && c.tcap[1]) pend_apply<false, true>(c, Q1, lane, 1, npend, pr, shfl_u32(e.head, kEhSeq + 1), row, &sp[1]);
+      else drops += pend_apply<false>(c, Q1, lane, 1, npend, pr, shfl_u32(e.head, kEhSeq + 1), row);
       d1 = true;
     }
     if ((pc >> 16) & 0xFF) {
-      drops += pend_apply<false>(c, Q2, lane, 2, npend, pr, shfl_u32(e.head, kEhSeq + 2), row);
+      if (DEEP && c.tcap[2]) pend_apply<false, true>(c, Q2, lane, 2, npend, pr, shfl_u32(e.head, kEhSeq + 2), row, &sp[2]);
+      else drops += pend_apply<false>(c, Q2, lane, 2, npend, pr, shfl_u32(e.head, kEhSeq + 2), row);
       d2 = true;
     }
     if (drops) err |= kErrQueue;
+    // a tail past its capacity needs the bounded queue's exact prune over head and tail
+    if (DEEP) unsafe = sp[0].cnt > c.tcap[0] || sp[1].cnt > c.tcap[1] || sp[2].cnt > c.tcap[2];
     // (the list's bookkeeping -- count, next seqs, prune count -- is written at the end: a store
     // here would make the compiler wait for it before reusing its registers)
   }
@@ -1302,14 +1472,28 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
 #else
     uint64_t* const ep = nullptr;
 #endif
-    if (ne0) q_pick_peers<true>(c, Q0, lane, np, used_v, nrec_v, off, ov, od, err, d0, row, ep);
-    if (ne1) q_pick_peers<false>(c, Q1, lane, np, used_v, nrec_v, off, ov, od, err, d1, row);
-    if (ne2) q_pick_peers<false>(c, Q2, lane, np, used_v, nrec_v, off, ov, od, err, d2, row);
+    if (DEEP) {
+      // a tail's bounds (~0: empty) as of after the spills above
+#define RSF_TB(q) (sp[q].cnt ? sp[q].minkey : ~0ull), (sp[q].cnt ? sp[q].minlen : ~0u)
+      if (ne0 && !unsafe) q_pick_peers<true, true>(c, Q0, lane, np, used_v, nrec_v, off, ov, od, err, d0, row, ep, RSF_TB(0), &unsafe);
+      if (ne1 && !unsafe) q_pick_peers<false, true>(c, Q1, lane, np, used_v, nrec_v, off, ov, od, err, d1, row, nullptr, RSF_TB(1), &unsafe);
+      if (ne2 && !unsafe) q_pick_peers<false, true>(c, Q2, lane, np, used_v, nrec_v, off, ov, od, err, d2, row, nullptr, RSF_TB(2), &unsafe);
+#undef RSF_TB
+      if (unsafe) {  // nothing committed: the whole-queue path redoes this member's emission
+        if (lane == 0) s.deep_ids[atomicAdd(s.deep_n, 1u)] = (uint32_t)l;
+        return;
+      }
+    } else {
+      if (ne0) q_pick_peers<true>(c, Q0, lane, np, used_v, nrec_v, off, ov, od, err, d0, row, ep);
+      if (ne1) q_pick_peers<false>(c, Q1, lane, np, used_v, nrec_v, off, ov, od, err, d1, row);
+      if (ne2) q_pick_peers<false>(c, Q2, lane, np, used_v, nrec_v, off, ov, od, err, d2, row);
+    }
     if (oc && (BKT || nrec_v)) *oc = min(nrec_v, c.cap_t);  // buckets: every group's count
   }
   EPROF_T(t2b);
   EPROF_ADD(3, t2, t2b);
 #else
+  static_assert(!DEEP, "deep queues need the queue-major emission (RSF_EMIT_MULTI)");
 #if RSF_EMIT_LAZY
   uint64_t cons0 = 0, cons1 = 0, cons2 = 0;  // picks whose re-rank is deferred (q_get_broadcasts_lazy)
   uint32_t t00 = 0, t01 = 0, t02 = 0;
@@ -1366,6 +1550,11 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   if (d0) q_store(c, s, l, 0, lane, Q0, true);
   if (d1) q_store(c, s, l, 1, lane, Q1, true);
   if (d2) q_store(c, s, l, 2, lane, Q2, true);
+  if (DEEP && lane < 3) {  // the tails' new counts and bounds (their spilled items are written)
+    const uint32_t tc = lane == 0 ? tc0 : lane == 1 ? tc1 : tc2;
+    const Spill& x = lane == 0 ? sp[0] : lane == 1 ? sp[1] : sp[2];
+    if (c.tcap[lane] && x.cnt != tc) s.tsum[l * 3 + lane] = spill_sum(x);
+  }
   // the member's bookkeeping as ONE lane-distributed store (each lane of `head` writes its own
   // word back where it changed): the applied pending list's count (0) and the queues' next
   // seqs, the prune count, the error flags (a queue prune, a stage overflow; only when new)
@@ -1541,7 +1730,7 @@ __global__ void __launch_bounds__(64) emit4_kernel(GCfg c, GState s, const uint3
 
 // FULL: queue_cap == 64 (one slot per lane of the wave), known at compile time -- every
 // `lane < qcap` test and its branch fold away (the bench configuration)
-template <bool BKT, bool FULL>
+template <bool BKT, bool FULL, bool DEEP = false>
 __global__ void __launch_bounds__(64 * RSF_EMIT_WPB) emit_kernel(GCfg c_in, GState s, const uint32_t* __restrict__ grp_key,
                                                    const uint32_t* __restrict__ slot, uint32_t* __restrict__ cnt_s,
                                                    uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec,
@@ -1555,17 +1744,21 @@ __global__ void __launch_bounds__(64 * RSF_EMIT_WPB) emit_kernel(GCfg c_in, GSta
                       (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)) * RSF_EMIT_PER_WAVE;
   if (l >= c.n_loc) return;
   EmitIn cur, nxt;
-  emit_load(c, s, grp_key, slot, l, lane, cur);
+  emit_load<DEEP>(c, s, grp_key, slot, l, lane, cur);
   if (RSF_EMIT_PER_WAVE == 1) {
-    emit_run<BKT>(c, s, l, lane, cur, cnt_s, out_val, out_dec, bk, row);
+    emit_run<BKT, DEEP>(c, s, l, lane, cur, cnt_s, out_val, out_dec, bk, row);
     return;
   }
   for (uint32_t k = 0; k < RSF_EMIT_PER_WAVE; ++k) {
-    if (k + 1 < RSF_EMIT_PER_WAVE) emit_load(c, s, grp_key, slot, l + k + 1, lane, nxt);
-    if (l + k < c.n_loc) emit_run<BKT>(c, s, l + k, lane, cur, cnt_s, out_val, out_dec, bk, row);
+    if (k + 1 < RSF_EMIT_PER_WAVE) emit_load<DEEP>(c, s, grp_key, slot, l + k + 1, lane, nxt);
+    if (l + k < c.n_loc) emit_run<BKT, DEEP>(c, s, l + k, lane, cur, cnt_s, out_val, out_dec, bk, row);
     cur = nxt;
   }
 }
+
+}  // namespace
+#include "gossip_deep.h"
+namespace {
 
 // Record decoration: what merge_kernel needs to address the view entry (the
 // subject) and to pick the queue, written beside the sorted rumor ids so the
@@ -2363,6 +2556,11 @@ __global__ void init_views_kernel(ViewE* view, uint64_t n_loc, uint32_t S, const
   view[i] = v;
 }
 
+__global__ void tsum_init_kernel(uint4* p, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = kTSumEmpty;
+}
+
 __global__ void iota_u32_kernel(uint32_t* p, uint64_t n) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = (uint32_t)i;
@@ -2480,6 +2678,8 @@ __global__ void __launch_bounds__(256) seg_end_kernel(uint64_t n_loc, const uint
 // drops the items past `max`, the last ones in send order (memberlist
 // TransmitLimitedQueue::prune).  stats[q] = queued, stats[3 + q] = members at or above
 // the warning depth, stats[6 + q] = pruned.
+// Deep queues: numq counts the tail too, and a queue to prune is listed (s.deep_ids) for
+// check_deep_kernel, which keeps the max smallest keys of head and tail.
 __global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uint32_t max_depth, uint32_t warn,
                                                            unsigned long long* __restrict__ stats) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2488,9 +2688,13 @@ __global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uin
   const uint64_t base = t * c.qcap;
   uint32_t n = 0;
   while (n < c.qcap && s.q_rumor[base + n] != kEmpty) n++;
+  if (c.tcap[q]) n += s.tsum[t].x;
   if (n) atomicAdd(stats + q, (unsigned long long)n);
   if (n >= warn) atomicAdd(stats + 3 + q, 1ull);
-  if (n > max_depth) {  // numq >= max -> prune(max): retain max
+  if (n > max_depth && c.tcap[q]) {
+    s.deep_ids[atomicAdd(s.deep_n, 1u)] = (uint32_t)t;
+    atomicAdd(stats + 6 + q, (unsigned long long)(n - max_depth));
+  } else if (n > max_depth) {  // numq >= max -> prune(max): retain max
     for (uint32_t i = max_depth; i < n; ++i) {
       s.q_rumor[base + i] = kEmpty;
       s.q_seq[base + i] = 0;
@@ -2531,9 +2735,9 @@ __global__ void __launch_bounds__(256) expire_kernel(GCfg c, GState s, uint32_t 
   q_load(c, s, l, q, lane, Q);
   const uint32_t age = (gen + G - (Q.r >> c.rbits) % G) % G;
   const uint32_t x = q_expire(c, Q, lane, age >= 2, q == 0);
-  if (!x) return;
-  q_store(c, s, l, q, lane, Q, true);
-  if (x && lane == 0) atomicAdd(s.q_expired + l, x);
+  if (x) q_store(c, s, l, q, lane, Q, true);
+  const uint32_t xt = tail_expire_wave(c, s, l, q, lane, gen, G);  // deep queues: the tail too
+  if ((x + xt) && lane == 0) atomicAdd(s.q_expired + l, x + xt);
 }
 
 // ---- multi-GPU exchange buckets: the sorted groups split by destination shard.
@@ -2691,6 +2895,8 @@ struct rsf_gossip {
            *grp_slot = nullptr, *grp_off = nullptr, *stage_dec = nullptr;
   rsf::CubTemp grp_tmp;  // the group count reduce / scan (each call sized by cub_run)
   unsigned merge_blocks = 1;  // merge_big_kernel's grid: merge_kernel's resident blocks per CU x CUs
+  unsigned deep_blocks = 1;   // emit_deep_kernel / check_deep_kernel grid (resident blocks x CUs)
+  uint64_t deep_last = 0;     // rsf_gossip_deep_stats' previous total
   uint32_t* big_ids = nullptr;  // receivers deferred to merge_big_kernel (count: d_counters[52])
   // RSF_GUARD_ZONES (diagnostic builds): 0xA5-filled zones before and after big_ids and
   // stage_dec and after the sort's storage; rsf_gossip_debug_zones counts changed bytes
@@ -2790,6 +2996,12 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   if (cfg->max_refute == 0 || cfg->max_refute > 4) return gerr("max_refute must be 1..4");
   if (cfg->max_rumors == 0 || (cfg->max_rumors & (cfg->max_rumors - 1)) || cfg->max_rumors > (1u << 30))
     return gerr("max_rumors must be a power of two <= 2^30 (the rumor ring)");
+  for (int q = 0; q < 3; ++q) {
+    const uint32_t d = cfg->queue_depth[q];
+    if (d && d < cfg->queue_cap) return gerr("queue_depth must be 0 or >= queue_cap");
+    if (d > cfg->queue_cap && cfg->queue_cap > kWave) return gerr("deep queues need queue_cap <= 64 (the register head)");
+    if (d > RSF_MAX_QUEUE_DEPTH) return gerr("queue_depth exceeds RSF_MAX_QUEUE_DEPTH");
+  }
   RSF_HIP(hipSetDevice(device));
   rsf_gossip* g = new (std::nothrow) rsf_gossip();
   if (!g) return rsf::set_error(RSF_ERR_NOMEM, "host allocation failed");
@@ -2816,9 +3028,17 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
     c.tx_limit = cfg->retransmit_mult * d;
   }
   c.max_refute = cfg->max_refute;
+  uint32_t max_depth = c.qcap;
+  for (int q = 0; q < 3; ++q) {  // deep queues: the tail behind the register head
+    const uint32_t d = cfg->queue_depth[q];
+    c.tcap[q] = d > c.qcap ? d - c.qcap : 0u;
+    c.tstride[q] = c.tcap[q] ? c.tcap[q] + kTailSlack : 0u;
+    c.deep |= c.tcap[q] ? 1u : 0u;
+    max_depth = std::max(max_depth, c.qcap + c.tcap[q]);
+  }
   {
     uint64_t per = c.limit / (c.overhead + kMinMsgLen);
-    c.cap_t = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(3ull * c.qcap, per));
+    c.cap_t = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(3ull * max_depth, per));
   }
   c.k0 = (uint32_t)cfg->seed;
   c.k1 = (uint32_t)(cfg->seed >> 32);
@@ -2849,6 +3069,11 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
       GA(s.rdec, (size_t)cfg->max_rumors * 2 * 4) || GA(s.rbody, (size_t)cfg->max_rumors * 2 * 16) ||
       GA(s.p_ent, n * kPend * sizeof(GState::PendE)) || GA(s.p_cnt, n * 4))
     return fail(rc);
+  if (c.deep) {  // tails, their summaries, the deferred-member list (also the checker's, 3 per member)
+    for (int q = 0; q < 3; ++q)
+      if (c.tcap[q] && GA(s.tail[q], n * c.tstride[q] * sizeof(uint4))) return fail(rc);
+    if (GA(s.tsum, n * 3 * sizeof(uint4)) || GA(s.deep_ids, n * 3 * 4)) return fail(rc);
+  }
   g->stage_cap = n * c.fanout * c.cap_t;
   if (g->stage_cap >= 0xFFFFFFFFull) return fail(gerr("n_members x fanout x per-target records must fit 32 bits"));
   g->recv_cap = g->stage_cap + g->stage_cap / 2 + 4096;
@@ -2878,12 +3103,19 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
       return fail(rsf::set_error(RSF_ERR_HIP, "occupancy query failed"));
     g->merge_blocks = (unsigned)std::max(1, per_cu * cus);
+    if (c.deep) {
+      int dpc = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpc, emit_deep_kernel<false>, kDeepThreads, 0) != hipSuccess)
+        return fail(rsf::set_error(RSF_ERR_HIP, "occupancy query failed"));
+      g->deep_blocks = (unsigned)std::max(1, dpc * cus);
+    }
   }
   // the hipCUB temporaries are sized per call at their first use (rsf::cub_run)
   hipStream_t st = g->stream;
   bool ok = true;
   auto ms = [&](void* p, int v, size_t b) { ok = ok && hipMemsetAsync(p, v, b, st) == hipSuccess; };
   ms(g->d_counters, 0, 64 * 8);  // status flags and running totals start at zero
+  s.deep_n = reinterpret_cast<uint32_t*>(g->d_counters + 54);  // deferred members (d_counters[55]: their total)
   ms(s.emin, 0, n * 8);
   ms(s.qmin, 0, n * 8);
   ms(s.digest, 0, n * 8);
@@ -2923,6 +3155,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   hipLaunchKernelGGL(fill_u64_kernel, dim3(grid1(n)), dim3(256), 0, st, s.eclock, n, 1ull);
   hipLaunchKernelGGL(fill_u64_kernel, dim3(grid1(n)), dim3(256), 0, st, s.qclock, n, 1ull);
   hipLaunchKernelGGL(iota_u32_kernel, dim3(grid1(g->n_groups)), dim3(256), 0, st, g->grp_id, g->n_groups);
+  if (c.deep) hipLaunchKernelGGL(tsum_init_kernel, dim3(grid1(n * 3)), dim3(256), 0, st, s.tsum, n * 3);
   if (hipStreamSynchronize(st) != hipSuccess) return fail(rsf::set_error(RSF_ERR_HIP, "context init sync failed"));
   *out = g;
   return RSF_OK;
@@ -2942,7 +3175,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
                   g->grp_slot, g->grp_off, g->dec_base, s.dlog, s.dmeta, s.dcnt,
                   g->bkt_send, g->bkt_recv, g->bkt_dec, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn,
-                  s.p_ent, s.p_cnt, g->big_base};
+                  s.p_ent, s.p_cnt, g->big_base, s.tail[0], s.tail[1], s.tail[2], s.tsum, s.deep_ids};
   for (void* p : ptrs)
     if (p) hipFree(p);
   g->scratch.release();
@@ -3226,6 +3459,39 @@ int rsf_gossip_rumor_block(rsf_gossip* g, void** p, uint64_t* bytes) {
 // receiver-ordered record stream (packed into send_buf, n_valid) for the exchange.
 // bucket mode (world > 0): emission straight into the destination shards' buckets
 static Buckets send_buckets(rsf_gossip* g);
+// emission by the queue layout: four slots per lane (65..256), one (64: FULL, or fewer); deep
+// queues then run the members the heads could not decide through emit_deep_kernel
+template <bool BKT>
+static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
+  const GCfg& c = g->c;
+  hipStream_t st = g->stream;
+  const dim3 eb(kWave * RSF_EMIT_WPB);
+  if (c.qcap > kWave) {
+    hipLaunchKernelGGL(emit4_kernel<BKT>, dim3((unsigned)c.n_loc), dim3(kWave), 0, st, c, g->s, g->grp_key, g->grp_slot,
+                       g->grp_cnt, g->stage_val, g->stage_dec, bk);
+  } else if (c.deep) {
+    RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 4, st));
+    if (c.qcap == kWave)
+      hipLaunchKernelGGL((emit_kernel<BKT, true, true>), egrid, eb, 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt,
+                         g->stage_val, g->stage_dec, bk);
+    else
+      hipLaunchKernelGGL((emit_kernel<BKT, false, true>), egrid, eb, 0, st, c, g->s, g->grp_key, g->grp_slot,
+                         g->grp_cnt, g->stage_val, g->stage_dec, bk);
+    RSF_HIP(hipGetLastError());
+    RSF_DBG_SYNC(st, "emit_kernel (deep)");
+    hipLaunchKernelGGL(emit_deep_kernel<BKT>, dim3(g->deep_blocks), dim3(kDeepThreads), 0, st, c, g->s, g->grp_key,
+                       g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, g->d_counters + 55);
+  } else if (c.qcap == kWave) {
+    hipLaunchKernelGGL((emit_kernel<BKT, true>), egrid, eb, 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt,
+                       g->stage_val, g->stage_dec, bk);
+  } else {
+    hipLaunchKernelGGL((emit_kernel<BKT, false>), egrid, eb, 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt,
+                       g->stage_val, g->stage_dec, bk);
+  }
+  RSF_HIP(hipGetLastError());
+  return RSF_OK;
+}
+
 static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t world = 0) {
   const GCfg& c = g->c;
   hipStream_t st = g->stream;
@@ -3259,16 +3525,7 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
     RSF_HIP(hipGetLastError());
     RSF_DBG_SYNC(st, "grp_index_kernel");
     mark(g, 2);
-    if (c.qcap > kWave)
-      hipLaunchKernelGGL(emit4_kernel<true>, dim3((unsigned)c.n_loc), dim3(kWave), 0, st, c, g->s, g->grp_key,
-                         g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk);
-    else if (c.qcap == kWave)
-      hipLaunchKernelGGL((emit_kernel<true, true>), egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key,
-                         g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk);
-    else
-      hipLaunchKernelGGL((emit_kernel<true, false>), egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key,
-                         g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk);
-    RSF_HIP(hipGetLastError());
+    if ((rc = launch_emit<true>(g, egrid, bk))) return rc;
     mark(g, 3);
     return RSF_OK;
   }
@@ -3277,16 +3534,7 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
   RSF_HIP(hipGetLastError());
   RSF_DBG_SYNC(st, "grp_index_kernel");
   mark(g, 2);
-  if (c.qcap > kWave)
-    hipLaunchKernelGGL(emit4_kernel<false>, dim3((unsigned)c.n_loc), dim3(kWave), 0, st, c, g->s, g->grp_key,
-                       g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, Buckets{});
-  else if (c.qcap == kWave)
-    hipLaunchKernelGGL((emit_kernel<false, true>), egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key,
-                       g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, Buckets{});
-  else
-    hipLaunchKernelGGL((emit_kernel<false, false>), egrid, dim3(kWave * RSF_EMIT_WPB), 0, st, c, g->s, g->grp_key,
-                       g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, Buckets{});
-  RSF_HIP(hipGetLastError());
+  if ((rc = launch_emit<false>(g, egrid, Buckets{}))) return rc;
   RSF_DBG_SYNC(st, "emit_kernel");
   if (local) {
     unsigned long long* sum = (unsigned long long*)g->d_counters;
@@ -3766,9 +4014,14 @@ int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t mi
   int rc = flush_pending(g);
   if (rc) return rc;
   RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, g->stream));
+  if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 4, g->stream));
   hipLaunchKernelGGL(check_queues_kernel, dim3(grid1(c.n_loc * 3)), dim3(256), 0, g->stream, c, g->s, max_depth,
                      depth_warning, g->d_counters + 40);
   RSF_HIP(hipGetLastError());
+  if (c.deep) {  // the deep queues over the max: the smallest max keys of head and tail kept
+    hipLaunchKernelGGL(check_deep_kernel, dim3(g->deep_blocks), dim3(kDeepThreads), 0, g->stream, c, g->s, max_depth);
+    RSF_HIP(hipGetLastError());
+  }
   unsigned long long st[9];
   RSF_HIP(hipMemcpyAsync(st, g->d_counters + 40, sizeof(st), hipMemcpyDeviceToHost, g->stream));
   RSF_HIP(hipStreamSynchronize(g->stream));
@@ -3917,9 +4170,71 @@ int rsf_gossip_dump_view(rsf_gossip* g, uint64_t* ltime, uint8_t* status, uint8_
   return rsf_gossip_dump_view_rows(g, 0, g->c.n_loc, ltime, status, kind, time);
 }
 
+// head and tail merged on the host into [n_loc][3][D] in send order
+static int dump_queues_deep(rsf_gossip* g, uint32_t D, uint32_t* rumor, uint32_t* seq, uint16_t* tx, uint16_t* len,
+                            uint32_t* max_live) {
+  const GCfg& c = g->c;
+  const uint64_t n = c.n_loc, hc = n * 3 * c.qcap;
+  uint32_t most = 0;
+  std::vector<uint32_t> hr(hc), hs(hc), ht(hc);
+  std::vector<uint4> sum(n * 3);
+  std::vector<std::vector<uint4>> tail(3);
+  hipStream_t st = g->stream;
+  RSF_HIP(hipMemcpyAsync(hr.data(), g->s.q_rumor, hc * 4, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipMemcpyAsync(hs.data(), g->s.q_seq, hc * 4, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipMemcpyAsync(ht.data(), g->s.q_txlen, hc * 4, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipMemcpyAsync(sum.data(), g->s.tsum, n * 3 * 16, hipMemcpyDeviceToHost, st));
+  for (uint32_t q = 0; q < 3; ++q)
+    if (c.tcap[q]) {
+      tail[q].resize(n * c.tstride[q]);
+      RSF_HIP(hipMemcpyAsync(tail[q].data(), g->s.tail[q], tail[q].size() * 16, hipMemcpyDeviceToHost, st));
+    }
+  RSF_HIP(hipStreamSynchronize(st));
+  std::vector<std::pair<uint64_t, uint32_t>> items;
+  for (uint64_t l = 0; l < n; ++l)
+    for (uint32_t q = 0; q < 3; ++q) {
+      items.clear();
+      const uint64_t hb = (l * 3 + q) * c.qcap;
+      for (uint32_t i = 0; i < c.qcap; ++i)
+        if (hr[hb + i] != kEmpty) items.push_back({tlq_key(ht[hb + i] & 0xFFFF, ht[hb + i] >> 16, hs[hb + i]), hr[hb + i]});
+      if (c.tcap[q])
+        for (uint32_t i = 0; i < sum[l * 3 + q].x; ++i) {
+          const uint4 e = tail[q][l * c.tstride[q] + i];
+          items.push_back({tlq_key(e.z & 0xFFFF, e.z >> 16, e.y), e.x});
+        }
+      std::sort(items.begin(), items.end());
+      most = std::max<uint32_t>(most, (uint32_t)items.size());
+      const uint64_t ob = (l * 3 + q) * D;
+      for (uint32_t i = 0; i < D; ++i) {
+        const bool live = i < items.size();
+        const uint64_t k = live ? items[i].first : 0ull;
+        rumor[ob + i] = live ? items[i].second : kEmpty;
+        seq[ob + i] = live ? 0xFFFFFFFFu - (uint32_t)k : 0u;
+        tx[ob + i] = live ? (uint16_t)(k >> 48) : 0;
+        len[ob + i] = live ? (uint16_t)(0xFFFF - ((k >> 32) & 0xFFFF)) : 0;
+      }
+    }
+  if (max_live) *max_live = most;
+  return RSF_OK;
+}
+
+int rsf_gossip_dump_queues_width(rsf_gossip* g, uint32_t width, uint32_t* rumor, uint32_t* seq, uint16_t* tx,
+                                 uint16_t* len, uint32_t* next_seq, uint32_t* max_live) {
+  if (!g || !rumor || !seq || !tx || !len || !next_seq || !width) return gerr("null argument");
+  RSF_HIP(hipSetDevice(g->device));
+  int rc = flush_pending(g);
+  if (rc) return rc;
+  RSF_HIP(hipMemcpyAsync(next_seq, g->s.q_next_seq, g->c.n_loc * 3 * 4, hipMemcpyDeviceToHost, g->stream));
+  return dump_queues_deep(g, width, rumor, seq, tx, len, max_live);
+}
+
 int rsf_gossip_dump_queues(rsf_gossip* g, uint32_t* rumor, uint32_t* seq, uint16_t* tx, uint16_t* len,
                            uint32_t* next_seq) {
   if (!g || !rumor || !seq || !tx || !len || !next_seq) return gerr("null argument");
+  if (g->c.deep) {
+    const uint32_t D = g->c.qcap + std::max(g->c.tcap[0], std::max(g->c.tcap[1], g->c.tcap[2]));
+    return rsf_gossip_dump_queues_width(g, D, rumor, seq, tx, len, next_seq, nullptr);
+  }
   const uint64_t cnt = g->c.n_loc * 3 * g->c.qcap;
   std::vector<uint32_t> tl(cnt);
   hipStream_t st = g->stream;
@@ -3935,6 +4250,18 @@ int rsf_gossip_dump_queues(rsf_gossip* g, uint32_t* rumor, uint32_t* seq, uint16
     tx[i] = (uint16_t)(tl[i] & 0xFFFF);
     len[i] = (uint16_t)(tl[i] >> 16);
   }
+  return RSF_OK;
+}
+
+int rsf_gossip_deep_stats(rsf_gossip* g, uint64_t* slow_total, uint64_t* slow_since_last) {
+  if (!g) return gerr("null context");
+  unsigned long long t = 0;
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemcpyAsync(&t, g->d_counters + 55, 8, hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  if (slow_total) *slow_total = t;
+  if (slow_since_last) *slow_since_last = t - g->deep_last;
+  g->deep_last = t;
   return RSF_OK;
 }
 
@@ -4190,6 +4517,7 @@ __global__ void __launch_bounds__(256) snap_reset_kernel(GCfg c, GState s, const
     s.q_txlen[l * 3 * c.qcap + j] = 0;
   }
   if (threadIdx.x < 3) s.q_next_seq[l * 3 + threadIdx.x] = 0;
+  if (threadIdx.x < 3 && s.tsum) s.tsum[l * 3 + threadIdx.x] = kTSumEmpty;  // deep queues: empty tails
   if (threadIdx.x == 0) s.p_cnt[l] = 0;  // nothing pending either
   for (uint32_t j = threadIdx.x; j < c.ebuf; j += blockDim.x) {
     s.eb_ltime[l * c.ebuf + j] = 0;

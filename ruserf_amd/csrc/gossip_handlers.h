@@ -38,6 +38,10 @@ struct GCfg {
   uint32_t rbits, rmask;
   uint32_t dcap;  // delivery log entries per member (0: log off)
   uint32_t snap_w, snap_rejoin;  // snapshotter: bitset words per member, rejoin_after_leave
+  // deep queues (qcap <= 64 head + HBM tail): tail capacity per queue (0: none) and the tail
+  // row stride (capacity + room for one emission's spills before its capacity check)
+  uint32_t tcap[3], tstride[3];
+  uint32_t deep;  // any tail
 };
 
 // view entry: members.states[subject] (status, status_time) or recent_intents[subject]
@@ -87,7 +91,18 @@ struct GState {
   // insert.  p_cnt[l] packs the entries per queue: n0 | n1 << 8 | n2 << 16 (sum <= kPend).
   struct PendE { uint32_t rid, dec, lq; } * p_ent;  // [n_loc][kPend], 12-B entries: one contiguous append
   uint32_t* p_cnt;                 // [n_loc]
+  // Deep queues: each queue is its register head (the q_* slots above, sorted) plus an
+  // UNORDERED tail in HBM, tail[q][l * tstride[q] + i] = {rumor, seq, transmits | len << 16,
+  // decoration}, i < tsum[l * 3 + q].x.  tsum = {count, a lower bound of the tail's smallest
+  // message length, a lower bound of its smallest key (lo, hi)}: emission picks from the head
+  // only while a pick's key is below the tail's bound and every stop is decided by a length
+  // the tail cannot fit; any other member takes the exact whole-queue path (emit_deep_kernel).
+  uint4* tail[3];
+  uint4* tsum;       // [n_loc][3]
+  uint32_t* deep_ids;  // [n_loc] members deferred to emit_deep_kernel this round
+  uint32_t* deep_n;    // their count (reset before each emission)
 };
+constexpr uint32_t kTailSlack = 192;  // tail row room past its capacity: one emission's spills (2 x 64) + 64
 constexpr uint32_t kPend = 128;  // pending entries per member (two per lane of a wave)
 // The merge leaves a member at most kPendMerge entries, so the round's originations and
 // refutations (at most 1 + max_refute <= 5 per member) append without applying the list
@@ -429,6 +444,59 @@ __device__ __forceinline__ uint32_t queue_of(uint8_t type) {
 // one; on a full queue the largest item falls off (memberlist Prune), and a new
 // item that would land past the end is itself the pruned one.
 // A full queue loses one live item: counted in q_pruned[l] and flagged (kErrQueue).
+// Deep queues (a tail, tcap[q] > 0): the item that falls off the full head -- its largest, or
+// the new one -- is appended to the tail; past the tail's capacity the largest item of head and
+// tail is pruned (tail_prune_serial).
+__device__ __forceinline__ void tail_append_serial(const GCfg& c, const GState& s, uint64_t l, uint32_t q, uint32_t rid,
+                                                   uint32_t dec, uint32_t seq, uint32_t tl) {
+  uint4* const t = s.tail[q] + l * c.tstride[q];
+  uint4 sm = s.tsum[l * 3 + q];
+  t[sm.x] = make_uint4(rid, seq, tl, dec);
+  sm.x++;
+  sm.y = min(sm.y, tl >> 16);
+  const uint64_t k = tlq_key(tl & 0xFFFF, tl >> 16, seq), mk = ((uint64_t)sm.w << 32) | sm.z;
+  if (k < mk) {
+    sm.z = (uint32_t)k;
+    sm.w = (uint32_t)(k >> 32);
+  }
+  s.tsum[l * 3 + q] = sm;
+}
+// over the queue's depth: drop the largest key of head and tail (the head's is its last live
+// slot; the tail's bounds stay lower bounds)
+__device__ __forceinline__ void tail_prune_serial(const GCfg& c, const GState& s, uint64_t l, uint32_t q, MRegs& r) {
+  uint4 sm = s.tsum[l * 3 + q];
+  if (sm.x <= c.tcap[q]) return;
+  uint4* const t = s.tail[q] + l * c.tstride[q];
+  const uint64_t base = (l * 3 + q) * c.qcap;
+  uint32_t hi = kEmpty, ti = 0;
+  uint64_t hk = 0, tk = 0;
+  for (uint32_t i = 0; i < c.qcap; ++i)
+    if (s.q_rumor[base + i] != kEmpty) {
+      hi = i;
+      const uint32_t x = s.q_txlen[base + i];
+      hk = tlq_key(x & 0xFFFF, x >> 16, s.q_seq[base + i]);
+    }
+  for (uint32_t i = 0; i < sm.x; ++i) {
+    const uint4 e = t[i];
+    const uint64_t x = tlq_key(e.z & 0xFFFF, e.z >> 16, e.y);
+    if (x >= tk) {
+      tk = x;
+      ti = i;
+    }
+  }
+  if (hi != kEmpty && hk > tk) {
+    s.q_rumor[base + hi] = kEmpty;
+    s.q_seq[base + hi] = 0;
+    s.q_txlen[base + hi] = 0;
+  } else {
+    t[ti] = t[sm.x - 1];
+    sm.x--;
+    s.tsum[l * 3 + q] = sm;
+  }
+  s.q_pruned[l] += 1;
+  r.err |= kErrQueue;
+}
+
 __device__ __forceinline__ void queue_insert_item(const GCfg& c, const GState& s, uint64_t l, uint32_t q,
                                                   uint32_t rid, uint32_t dec, uint32_t len, uint32_t seq, MRegs& r) {
   const uint64_t base = (l * 3 + q) * c.qcap;
@@ -438,6 +506,27 @@ __device__ __forceinline__ void queue_insert_item(const GCfg& c, const GState& s
     const uint32_t tl = s.q_txlen[base + cnt];
     if (pos == kEmpty && tlq_key(tl & 0xFFFF, tl >> 16, s.q_seq[base + cnt]) > newkey) pos = cnt;
     cnt++;
+  }
+  if (cnt == c.qcap && c.tcap[q]) {
+    if (pos == kEmpty) {  // the new item is the head's largest: straight to the tail
+      tail_append_serial(c, s, l, q, rid, dec, seq, len << 16);
+    } else {  // the head's largest falls into the tail, the new item shifts in
+      const uint64_t last = base + c.qcap - 1;
+      tail_append_serial(c, s, l, q, s.q_rumor[last], q == 0 ? s.q_dec[l * c.qcap + c.qcap - 1] : 0u, s.q_seq[last],
+                         s.q_txlen[last]);
+      for (uint32_t i = c.qcap - 1; i > pos; --i) {
+        s.q_rumor[base + i] = s.q_rumor[base + i - 1];
+        s.q_seq[base + i] = s.q_seq[base + i - 1];
+        s.q_txlen[base + i] = s.q_txlen[base + i - 1];
+        if (q == 0) s.q_dec[l * c.qcap + i] = s.q_dec[l * c.qcap + i - 1];
+      }
+      if (q == 0) s.q_dec[l * c.qcap + pos] = dec;
+      s.q_rumor[base + pos] = rid;
+      s.q_seq[base + pos] = seq;
+      s.q_txlen[base + pos] = (len << 16);
+    }
+    tail_prune_serial(c, s, l, q, r);
+    return;
   }
   if (cnt == c.qcap) {
     s.q_pruned[l] += 1;

@@ -73,15 +73,25 @@ class GossipConfig:
     max_refute: int = 4
     max_rumors: int = 1 << 20      # rumor ring (a power of two); ids recycle after a full cycle
     seed: int = 0x5EED5EED
+    # deep queues: capacity of the intent / query / event queue (0 = queue_cap); above queue_cap
+    # (<= 64) the queue is a register head of queue_cap slots plus an HBM tail (reference
+    # max_queue_depth 4096, pruned only by the QueueChecker)
+    queue_depth: tuple = None
+
+    def depths(self):
+        d = self.queue_depth or (0, 0, 0)
+        return [int(x) if x else self.queue_cap for x in d]
 
     def to_c(self):
         lo, hi = self.shard if self.shard is not None else (0, self.n_members)
-        return RsfGossipCfg(n_members=self.n_members, shard_lo=lo, shard_hi=hi, n_subjects=self.n_subjects,
-                            queue_cap=self.queue_cap, event_buffer_size=self.event_buffer_size,
-                            query_buffer_size=self.query_buffer_size, slot_k=self.slot_k, fanout=self.fanout,
-                            gossip_limit=self.gossip_limit, gossip_overhead=self.gossip_overhead,
-                            retransmit_mult=self.retransmit_mult, max_refute=self.max_refute,
-                            max_rumors=self.max_rumors, seed=self.seed)
+        c = RsfGossipCfg(n_members=self.n_members, shard_lo=lo, shard_hi=hi, n_subjects=self.n_subjects,
+                         queue_cap=self.queue_cap, event_buffer_size=self.event_buffer_size,
+                         query_buffer_size=self.query_buffer_size, slot_k=self.slot_k, fanout=self.fanout,
+                         gossip_limit=self.gossip_limit, gossip_overhead=self.gossip_overhead,
+                         retransmit_mult=self.retransmit_mult, max_refute=self.max_refute,
+                         max_rumors=self.max_rumors, seed=self.seed)
+        c.queue_depth[:] = [int(x) for x in (self.queue_depth or (0, 0, 0))]
+        return c
 
 
 def _p(a):
@@ -358,15 +368,31 @@ class GossipEngine:
                                             ptr(q, C.c_uint64), ptr(w, C.c_uint64), ptr(p, C.c_uint64)))
         return {"queued": q, "warn": w, "pruned": p}
 
-    def queues(self):
-        n = self.n_loc * 3 * self.cfg.queue_cap
+    def deep_stats(self):
+        """(members that took the exact whole-queue emission since creation, since the last call)"""
+        a, b = C.c_uint64(), C.c_uint64()
+        check(lib().rsf_gossip_deep_stats(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def queues(self, width=None):
+        """[n_loc * 3 * D] per field, D = the deepest queue's capacity, each queue in send order;
+        width: only each queue's first `width` items (then self.max_live = the most any holds)"""
+        w = int(width) if width else max(self.cfg.depths())
+        n = self.n_loc * 3 * w
         r = np.zeros(n, dtype=np.uint32)
         sq = np.zeros(n, dtype=np.uint32)
         tx = np.zeros(n, dtype=np.uint16)
         ln = np.zeros(n, dtype=np.uint16)
         ns = np.zeros(self.n_loc * 3, dtype=np.uint32)
-        check(lib().rsf_gossip_dump_queues(self._h, ptr(r, C.c_uint32), ptr(sq, C.c_uint32), ptr(tx, C.c_uint16),
-                                           ptr(ln, C.c_uint16), ptr(ns, C.c_uint32)))
+        if width:
+            ml = C.c_uint32()
+            check(lib().rsf_gossip_dump_queues_width(self._h, w, ptr(r, C.c_uint32), ptr(sq, C.c_uint32),
+                                                     ptr(tx, C.c_uint16), ptr(ln, C.c_uint16), ptr(ns, C.c_uint32),
+                                                     C.byref(ml)))
+            self.max_live = ml.value
+        else:
+            check(lib().rsf_gossip_dump_queues(self._h, ptr(r, C.c_uint32), ptr(sq, C.c_uint32), ptr(tx, C.c_uint16),
+                                               ptr(ln, C.c_uint16), ptr(ns, C.c_uint32)))
         return r, sq, tx, ln, ns
 
     def buffers(self):

@@ -45,10 +45,20 @@ def oracle_round(w, t, ml, acts, threads=1):
     assert rc == 0
 
 
-def world_state(w, lo=0, hi=None):
+def world_width(w):
+    """slots [0, hwm) of every oracle queue hold all its live items"""
+    return max(1, int(O.arr(w.q_hwm, w.n * 3, np.uint32).max()))
+
+
+def world_state(w, lo=0, hi=None, width=None):
     n, s, q = w.n, w.s, w.qcap
     hi = n if hi is None else hi
     sl = slice(lo, hi)
+    if width is not None:  # deep queues: only the slots that can hold items (width >= the hwm)
+        assert width >= world_width(w)
+        qs = lambda p, t: np.ascontiguousarray(O.arr(p, n * 3 * q, t).reshape(n, 3, q)[sl, :, :width]).reshape(hi - lo, -1)  # noqa: E731
+    else:
+        qs = lambda p, t: O.arr(p, n * 3 * q, t).reshape(n, 3 * q)[sl]  # noqa: E731
     st = {
         "clock": O.arr(w.clock, n, np.uint64)[sl],
         "event_clock": O.arr(w.eclock, n, np.uint64)[sl],
@@ -60,10 +70,10 @@ def world_state(w, lo=0, hi=None):
         "v_status": O.arr(w.v_status, n * s, np.uint8).reshape(n, s)[sl],
         "v_kind": O.arr(w.v_kind, n * s, np.uint8).reshape(n, s)[sl],
         "v_time": O.arr(w.v_time, n * s, np.uint32).reshape(n, s)[sl],
-        "q_rumor": O.arr(w.q_rumor, n * 3 * q, np.uint32).reshape(n, 3 * q)[sl],
-        "q_seq": O.arr(w.q_seq, n * 3 * q, np.uint32).reshape(n, 3 * q)[sl],
-        "q_tx": O.arr(w.q_tx, n * 3 * q, np.uint16).reshape(n, 3 * q)[sl],
-        "q_len": O.arr(w.q_len, n * 3 * q, np.uint16).reshape(n, 3 * q)[sl],
+        "q_rumor": qs(w.q_rumor, np.uint32),
+        "q_seq": qs(w.q_seq, np.uint32),
+        "q_tx": qs(w.q_tx, np.uint16),
+        "q_len": qs(w.q_len, np.uint16),
         "q_next_seq": O.arr(w.q_next_seq, n * 3, np.uint32).reshape(n, 3)[sl],
         "eb_ltime": O.arr(w.eb_ltime, n * w.ebuf, np.uint64).reshape(n, -1)[sl],
         "eb_cnt": O.arr(w.eb_cnt, n * w.ebuf, np.uint32).reshape(n, -1)[sl],
@@ -77,11 +87,13 @@ def world_state(w, lo=0, hi=None):
     return st
 
 
-def engine_state(g):
+def engine_state(g, width=None):
     n, s, q = g.n_loc, g.cfg.n_subjects, g.cfg.queue_cap
     m = g.members()
     lt, stt, kd, vt = g.view(with_time=True)
-    r, sq, tx, ln, ns = g.queues()
+    r, sq, tx, ln, ns = g.queues(width)
+    if width is not None:
+        assert g.max_live <= width, (g.max_live, width)
     ebl, ebc, ebk, qbl, qbc, qbi = g.buffers()
     return {
         "clock": m["clock"], "event_clock": m["event_clock"], "query_clock": m["query_clock"],
@@ -121,6 +133,12 @@ def normalize_queues(st, qcap=None):
             a[np.take_along_axis(empty, order, axis=2)] = 0
         st[k] = a.reshape(n, w)
     return st
+
+
+def deep_states(g, w):
+    """(engine, oracle) states of a deep-queue pair with only the queue slots in use compared"""
+    width = world_width(w)
+    return engine_state(g, width), world_state(w, width=width)
 
 
 def assert_same(a, b, ctx=""):

@@ -1,0 +1,207 @@
+"""Deep transmit-limited queues (queue_depth > queue_cap): a register head plus an unordered
+HBM tail per queue, so a queue holds up to the reference's max_queue_depth (4096,
+core/src/options.rs:512) and is pruned only by the QueueChecker (base.rs:720-760).  Bit-exact
+against the oracle's bounded queue of the same depth (oracle/oracle.c orc_queue_insert /
+orc_queue_get_broadcasts / orc_check_queues): emission decided from the head alone, the
+members whose picks need the tail (emit_deep_kernel), spills, the bounded prune at the full
+depth, ring expiry of tail items, QueueChecker ticks, and the multi-GPU bucket emission."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import gossip_harness as H
+import oracle_ffi as O
+from ruserf_amd import gossip as G
+from ruserf_amd import workload as W
+
+pytestmark = pytest.mark.gpu
+L = O.lib()
+
+
+def pair(cfg, subj_member, views):
+    g = G.GossipEngine(cfg)
+    g.set_subjects(subj_member)
+    g.init_views(*views)
+    w = H.oracle_world(cfg, subj_member, views)
+    return g, w
+
+
+def same(g, w, ctx):
+    e, o = H.deep_states(g, w)
+    H.assert_same(e, o, ctx)
+
+
+def check_both(g, w, mx, mn, warn, ctx):
+    got = g.check_queues(mx, mn, warn)
+    exp = (C.c_uint64 * 9)()
+    L.orc_check_queues(C.byref(w), mx, mn, warn, exp)
+    assert list(got["queued"]) + list(got["warn"]) + list(got["pruned"]) == list(exp), (ctx, mx, mn, warn)
+    same(g, w, f"{ctx} checker {mx}")
+
+
+@pytest.mark.parametrize("rounds", [12])
+def test_deep_bench_shape_bit_exact(rounds):
+    """The bench's saturated shape (20k members, 4096 subjects, 5% originating, 8 intents of
+    budget per target) with the intent queue 4096 deep: nothing is dropped between checker
+    ticks (the queues grow past the 64-slot head), and the state is bit-exact after every
+    round; then a QueueChecker tick at max_queue_depth 128 prunes head and tail together."""
+    n, s = 20000, 4096
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=64, queue_depth=(4096, 0, 0), gossip_limit=8 * 24,
+                         gossip_overhead=2, max_rumors=1 << 18, event_buffer_size=512, query_buffer_size=512,
+                         slot_k=1)
+    subj, acts, ml = W.intents_workload(n, s, rounds, rate=0.05, seed=2024)
+    g, w = pair(cfg, subj, W.initial_views(s))
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t], threads=16)
+        same(g, w, f"round {t}")
+    st = H.engine_state(g, H.world_width(w))
+    assert int(st["q_pruned"].sum()) == 0  # nothing dropped between ticks
+    assert H.world_width(w) > 64  # the queues hold more than the head
+    total, _ = g.deep_stats()
+    assert total > 0  # some emissions needed the tail
+    check_both(g, w, 128, 0, 64, "bench shape")
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
+@pytest.mark.parametrize("qcap,depth,limit,mult", [(16, 100, 400, 4), (64, 200, 260, 1), (8, 40, 600, 2),
+                                                   (32, 64, 1400, 4)])
+def test_deep_churn_flood_prune_ring_bit_exact(qcap, depth, limit, mult):
+    """Intents, user events and queries of many lengths with churn, through heads of 8..64
+    slots and depths small enough to fill: spills, the deferred whole-queue emissions, the
+    bounded prune at the full depth (head or tail losing its largest key), retransmit
+    limits of 1..4 (items retiring out of the head), a rumor ring small enough to wrap (tail
+    items expire), and QueueChecker ticks.  Bit-exact against the oracle after every round."""
+    n, rounds = 1200, 30
+    subj, acts, ml = W.churn_workload(n, rounds, events_per_round=30, queries_per_round=5, seed=depth + qcap)
+    s = len(subj)
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=qcap, queue_depth=(depth, depth, depth),
+                         gossip_limit=limit, gossip_overhead=3, retransmit_mult=mult, max_rumors=512,
+                         event_buffer_size=128, query_buffer_size=128, slot_k=8, max_refute=2)
+    g, w = pair(cfg, subj, W.initial_views(s))
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t])
+        same(g, w, f"round {t}")
+        if t in (9, 19):
+            check_both(g, w, depth // 2, 0, 8, f"round {t}")
+    total, _ = g.deep_stats()
+    assert total > 0
+    assert w.gen >= 2
+    check_both(g, w, 4096, 0, 128, "end")
+    check_both(g, w, 5, 0, 2, "end")
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
+def test_deep_serial_inserts_and_prune():
+    """A member whose peers are all down sends nothing, so its own originations pile up in its
+    pending list; at 128 entries the list is applied one item at a time (pend_push_serial ->
+    queue_insert_item): the full head's largest falls into the tail, and past the depth the
+    largest key of head and tail is pruned (tail_prune_serial).  200 user events of many
+    lengths through a head of 8 and a depth of 40; compared with the oracle's queue at the end
+    (an inspection applies the list, so it would hide the serial path if done every round)."""
+    n, rounds = 3, 200
+    cfg = G.GossipConfig(n_members=n, n_subjects=1, queue_cap=8, queue_depth=(40, 40, 40), fanout=1,
+                         max_rumors=1 << 12, event_buffer_size=512, query_buffer_size=64, slot_k=4)
+    subj = np.array([2], np.uint32)
+    g, w = pair(cfg, subj, W.initial_views(1))
+    alive = np.array([1, 0, 0], np.uint8)
+    g.set_alive(alive)
+    for m in range(n):
+        w.alive[m] = int(alive[m])
+    rng = np.random.default_rng(3)
+    for t in range(rounds):
+        acts = np.zeros(1, G.ACTION_DTYPE)
+        acts["member"], acts["act"] = 0, G.ACT_USER_EVENT
+        acts["name_len"], acts["payload_len"] = rng.integers(1, 30), rng.integers(0, 60)
+        acts["key"] = (int(rng.integers(1, 9)) << 32) | int(rng.integers(1, 99))
+        g.round(t, None, acts)
+        H.oracle_round(w, t, np.zeros(0, G.ML_DTYPE), acts)
+    same(g, w, "end")
+    assert int(g.pruned()[0]) == rounds - 40 and O.arr(w.q_pruned, n, np.uint32)[0] == rounds - 40
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
+def test_configs3_100k_deep_queues_bit_exact():
+    """BASELINE configs[3] (100k members, 1% churn, 100 user events + 10 queries per round)
+    with all three queues 4096 deep: every member's clocks, digest of every delivery, error
+    bits and queue drops bit-exact every round, the full state (queues included) at the end."""
+    n, rounds = 100_000, 9
+    subj, acts, ml = W.churn_workload(n, rounds, events_per_round=100, queries_per_round=10, seed=2024)
+    s = len(subj)
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=64, queue_depth=(4096, 4096, 4096), gossip_limit=1400,
+                         max_rumors=1 << 16, event_buffer_size=512, query_buffer_size=512, slot_k=16)
+    g, w = pair(cfg, subj, W.initial_views(s))
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t], threads=16)
+        m = g.members()
+        for k, ok in [("clock", w.clock), ("event_clock", w.eclock), ("query_clock", w.qclock),
+                      ("digest", w.digest), ("err", w.err)]:
+            exp = O.arr(ok, n, np.uint32 if k == "err" else np.uint64)
+            assert np.array_equal(m[k], exp), (t, k)
+        assert np.array_equal(g.pruned(), O.arr(w.q_pruned, n, np.uint32)), t
+    same(g, w, "final")
+    assert int(g.pruned().sum()) == 0
+    total, _ = g.deep_stats()
+    assert total > 0
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
+def test_deep_two_shards_buckets_equal_one_context():
+    """The multi-GPU bucket emission with deep queues (emit_kernel and emit_deep_kernel writing
+    into the destination buckets): two shard contexts on one GPU, the exchange by hand,
+    equal to one context after every round."""
+    import torch
+    from ruserf_amd.dist import hbm_tensor
+    n, rounds = 4000, 12
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    subj, acts, ml = W.churn_workload(n, rounds, events_per_round=40, queries_per_round=6, seed=9)
+    s = len(subj)
+    base = dict(n_members=n, n_subjects=s, queue_cap=16, queue_depth=(300, 300, 300), gossip_limit=500,
+                max_rumors=1 << 16, event_buffer_size=128, query_buffer_size=128, slot_k=8)
+    views = W.initial_views(s)
+    one = G.GossipEngine(G.GossipConfig(**base))
+    shards = [G.GossipEngine(G.GossipConfig(**base, shard=(0, n // 2))),
+              G.GossipEngine(G.GossipConfig(**base, shard=(n // 2, n)))]
+    for e in [one] + shards:
+        e.set_stream(stream.cuda_stream)
+        e.set_subjects(subj)
+        e.init_views(*views)
+    bufs = [e.bucket_buffers(2) for e in shards]
+    words = bufs[0][2] // 4
+    for t in range(rounds):
+        one.round(t, ml[t], acts[t])
+        for e in shards:
+            e.round_begin(t, ml[t], acts[t])
+        blocks = [hbm_tensor(*e.rumor_block()[:1], e.rumor_block()[1] // 8) for e in shards]
+        total = blocks[0] + blocks[1]
+        for b in blocks:
+            b.copy_(total)
+        for e in shards:
+            e.round_emit_buckets(2)
+        stream.synchronize()
+        for dst, e in enumerate(shards):
+            recv = hbm_tensor(bufs[dst][1], 2 * words, "<i4")
+            for src in range(2):
+                send = hbm_tensor(bufs[src][0], 2 * words, "<i4")
+                recv[src * words:(src + 1) * words].copy_(send[dst * words:(dst + 1) * words])
+        stream.synchronize()
+        for e in shards:
+            e.round_merge_buckets(2)
+        stream.synchronize()
+        assert all(e.bucket_ok() for e in shards)
+        width = 300
+        full = H.normalize_queues(H.engine_state(one, width))
+        halves = [H.normalize_queues(H.engine_state(e, width)) for e in shards]
+        for k in full:
+            assert np.array_equal(np.concatenate([halves[0][k], halves[1][k]]), full[k]), (t, k)
+    assert sum(e.deep_stats()[0] for e in shards) > 0
+    for e in [one] + shards:
+        e.close()
