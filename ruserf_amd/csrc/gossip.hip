@@ -736,7 +736,7 @@ struct Spill {
 };
 __device__ __forceinline__ Spill spill_of(const GCfg& c, const GState& s, uint64_t l, uint32_t q, uint4 sm) {
   Spill sp;
-  sp.t = s.tail[q] + l * c.tstride[q];
+  sp.t = tail_of(s, q) + l * tstride_of(c, q);
   sp.cnt = sm.x;
   sp.minlen = sm.y;
   sp.minkey = ((uint64_t)sm.w << 32) | sm.z;
@@ -877,7 +877,7 @@ __device__ __forceinline__ uint32_t pend_apply(const GCfg& c, QRegs& Q, uint32_t
 // queue's prune, rare (a queue at its full depth).  One wave; returns the number dropped.
 __device__ __forceinline__ uint32_t deep_prune_wave(const GCfg& c, QRegs& Q, uint32_t lane, uint32_t q, Spill& sp) {
   uint32_t drops = 0;
-  while (sp.cnt > c.tcap[q]) {
+  while (sp.cnt > tcap_of(c, q)) {
     const uint64_t live_m = ballot(lane < c.qcap && Q.r != kEmpty);
     uint64_t hk = 0;
     int hl = -1;
@@ -923,13 +923,14 @@ __device__ __forceinline__ uint32_t pend_flush_wave(const GCfg& c, const GState&
   PendRegs p;
   pend_load(s, l, lane, n, p);
   uint32_t drops = 0;
+#pragma unroll
   for (uint32_t q = 0; q < 3; ++q) {
     const uint32_t nq = (pc >> (8 * q)) & 0xFF;
     if (!nq) continue;
     QRegs Q{kEmpty, 0, 0};
     q_load(c, s, l, q, lane, Q);
     const uint32_t seq0 = s.q_next_seq[l * 3 + q];
-    if (c.tcap[q]) {  // deep queue: the head's overflow spills into the tail
+    if (tcap_of(c, q)) {  // deep queue: the head's overflow spills into the tail
       Spill sp = spill_of(c, s, l, q, s.tsum[l * 3 + q]);
       pend_apply<true, true>(c, Q, lane, q, n, p, seq0, row, &sp);
       drops += deep_prune_wave(c, Q, lane, q, sp);
@@ -1367,17 +1368,19 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
     if (BKT) bkt_group_keys(bk, lane, np, e.gk, e.gs, true);
     return;
   }
-  Spill sp[3];
+  // (three named tails, not an array: a dynamically indexed array goes to scratch)
+  Spill sp0, sp1, sp2;
   bool unsafe = false;
   if (DEEP) {
-#pragma unroll
-    for (uint32_t q = 0; q < 3; ++q)
-      if (c.tcap[q]) {
-        sp[q].t = s.tail[q] + l * c.tstride[q];
-        sp[q].cnt = shfl_u32(e.ts.x, q);
-        sp[q].minlen = shfl_u32(e.ts.y, q);
-        sp[q].minkey = ((uint64_t)shfl_u32(e.ts.w, q) << 32) | shfl_u32(e.ts.z, q);
-      }
+    auto get = [&](Spill& x, uint32_t q) {
+      x.t = tail_of(s, q) + l * tstride_of(c, q);
+      x.cnt = shfl_u32(e.ts.x, q);
+      x.minlen = shfl_u32(e.ts.y, q);
+      x.minkey = ((uint64_t)shfl_u32(e.ts.w, q) << 32) | shfl_u32(e.ts.z, q);
+    };
+    if (c.tcap0) get(sp0, 0);
+    if (c.tcap1) get(sp1, 1);
+    if (c.tcap2) get(sp2, 2);
   }
   EPROF_T(t1);
   EPROF_ADD(0, t0, t1);
@@ -1416,23 +1419,23 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
     // applied first: in the reference they were queued when the messages arrived
     uint32_t& drops = drops_all;
     if (pc & 0xFF) {
-      if (DEEP && c.tcap[0]) pend_apply<true, true>(c, Q0, lane, 0, npend, pr, shfl_u32(e.head, kEhSeq), row, &sp[0]);
+      if (DEEP && c.tcap0) pend_apply<true, true>(c, Q0, lane, 0, npend, pr, shfl_u32(e.head, kEhSeq), row, &sp0);
       else drops += pend_apply<true>(c, Q0, lane, 0, npend, pr, shfl_u32(e.head, kEhSeq), row);
       d0 = true;
     }
     if ((pc >> 8) & 0xFF) {
-      if (DEEP && c.tcap[1]) pend_apply<false, true>(c, Q1, lane, 1, npend, pr, shfl_u32(e.head, kEhSeq + 1), row, &sp[1]);
+      if (DEEP && c.tcap1) pend_apply<false, true>(c, Q1, lane, 1, npend, pr, shfl_u32(e.head, kEhSeq + 1), row, &sp1);
       else drops += pend_apply<false>(c, Q1, lane, 1, npend, pr, shfl_u32(e.head, kEhSeq + 1), row);
       d1 = true;
     }
     if ((pc >> 16) & 0xFF) {
-      if (DEEP && c.tcap[2]) pend_apply<false, true>(c, Q2, lane, 2, npend, pr, shfl_u32(e.head, kEhSeq + 2), row, &sp[2]);
+      if (DEEP && c.tcap2) pend_apply<false, true>(c, Q2, lane, 2, npend, pr, shfl_u32(e.head, kEhSeq + 2), row, &sp2);
       else drops += pend_apply<false>(c, Q2, lane, 2, npend, pr, shfl_u32(e.head, kEhSeq + 2), row);
       d2 = true;
     }
     if (drops) err |= kErrQueue;
     // a tail past its capacity needs the bounded queue's exact prune over head and tail
-    if (DEEP) unsafe = sp[0].cnt > c.tcap[0] || sp[1].cnt > c.tcap[1] || sp[2].cnt > c.tcap[2];
+    if (DEEP) unsafe = sp0.cnt > c.tcap0 || sp1.cnt > c.tcap1 || sp2.cnt > c.tcap2;
     // (the list's bookkeeping -- count, next seqs, prune count -- is written at the end: a store
     // here would make the compiler wait for it before reusing its registers)
   }
@@ -1474,7 +1477,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
 #endif
     if (DEEP) {
       // a tail's bounds (~0: empty) as of after the spills above
-#define RSF_TB(q) (sp[q].cnt ? sp[q].minkey : ~0ull), (sp[q].cnt ? sp[q].minlen : ~0u)
+#define RSF_TB(q) (sp##q.cnt ? sp##q.minkey : ~0ull), (sp##q.cnt ? sp##q.minlen : ~0u)
       if (ne0 && !unsafe) q_pick_peers<true, true>(c, Q0, lane, np, used_v, nrec_v, off, ov, od, err, d0, row, ep, RSF_TB(0), &unsafe);
       if (ne1 && !unsafe) q_pick_peers<false, true>(c, Q1, lane, np, used_v, nrec_v, off, ov, od, err, d1, row, nullptr, RSF_TB(1), &unsafe);
       if (ne2 && !unsafe) q_pick_peers<false, true>(c, Q2, lane, np, used_v, nrec_v, off, ov, od, err, d2, row, nullptr, RSF_TB(2), &unsafe);
@@ -1550,10 +1553,12 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   if (d0) q_store(c, s, l, 0, lane, Q0, true);
   if (d1) q_store(c, s, l, 1, lane, Q1, true);
   if (d2) q_store(c, s, l, 2, lane, Q2, true);
-  if (DEEP && lane < 3) {  // the tails' new counts and bounds (their spilled items are written)
-    const uint32_t tc = lane == 0 ? tc0 : lane == 1 ? tc1 : tc2;
-    const Spill& x = lane == 0 ? sp[0] : lane == 1 ? sp[1] : sp[2];
-    if (c.tcap[lane] && x.cnt != tc) s.tsum[l * 3 + lane] = spill_sum(x);
+  if (DEEP) {  // the tails' new counts and bounds (their spilled items are written), lane q for queue q
+    const bool l0 = lane == 0, l1 = lane == 1;
+    const uint32_t tc = l0 ? tc0 : l1 ? tc1 : tc2, tcap = l0 ? c.tcap0 : l1 ? c.tcap1 : c.tcap2;
+    const uint32_t cnt = l0 ? sp0.cnt : l1 ? sp1.cnt : sp2.cnt, mlen = l0 ? sp0.minlen : l1 ? sp1.minlen : sp2.minlen;
+    const uint64_t mkey = l0 ? sp0.minkey : l1 ? sp1.minkey : sp2.minkey;
+    if (lane < 3 && tcap && cnt != tc) s.tsum[l * 3 + lane] = make_uint4(cnt, mlen, (uint32_t)mkey, (uint32_t)(mkey >> 32));
   }
   // the member's bookkeeping as ONE lane-distributed store (each lane of `head` writes its own
   // word back where it changed): the applied pending list's count (0) and the queues' next
@@ -2688,10 +2693,10 @@ __global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uin
   const uint64_t base = t * c.qcap;
   uint32_t n = 0;
   while (n < c.qcap && s.q_rumor[base + n] != kEmpty) n++;
-  if (c.tcap[q]) n += s.tsum[t].x;
+  if (tcap_of(c, q)) n += s.tsum[t].x;
   if (n) atomicAdd(stats + q, (unsigned long long)n);
   if (n >= warn) atomicAdd(stats + 3 + q, 1ull);
-  if (n > max_depth && c.tcap[q]) {
+  if (n > max_depth && tcap_of(c, q)) {
     s.deep_ids[atomicAdd(s.deep_n, 1u)] = (uint32_t)t;
     atomicAdd(stats + 6 + q, (unsigned long long)(n - max_depth));
   } else if (n > max_depth) {  // numq >= max -> prune(max): retain max
@@ -3029,12 +3034,20 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   }
   c.max_refute = cfg->max_refute;
   uint32_t max_depth = c.qcap;
-  for (int q = 0; q < 3; ++q) {  // deep queues: the tail behind the register head
-    const uint32_t d = cfg->queue_depth[q];
-    c.tcap[q] = d > c.qcap ? d - c.qcap : 0u;
-    c.tstride[q] = c.tcap[q] ? c.tcap[q] + kTailSlack : 0u;
-    c.deep |= c.tcap[q] ? 1u : 0u;
-    max_depth = std::max(max_depth, c.qcap + c.tcap[q]);
+  {  // deep queues: the tail behind the register head
+    uint32_t tc[3];
+    for (int q = 0; q < 3; ++q) {
+      const uint32_t d = cfg->queue_depth[q];
+      tc[q] = d > c.qcap ? d - c.qcap : 0u;
+      c.deep |= tc[q] ? 1u : 0u;
+      max_depth = std::max(max_depth, c.qcap + tc[q]);
+    }
+    c.tcap0 = tc[0];
+    c.tcap1 = tc[1];
+    c.tcap2 = tc[2];
+    c.tstride0 = tc[0] ? tc[0] + kTailSlack : 0u;
+    c.tstride1 = tc[1] ? tc[1] + kTailSlack : 0u;
+    c.tstride2 = tc[2] ? tc[2] + kTailSlack : 0u;
   }
   {
     uint64_t per = c.limit / (c.overhead + kMinMsgLen);
@@ -3071,7 +3084,8 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
     return fail(rc);
   if (c.deep) {  // tails, their summaries, the deferred-member list (also the checker's, 3 per member)
     for (int q = 0; q < 3; ++q)
-      if (c.tcap[q] && GA(s.tail[q], n * c.tstride[q] * sizeof(uint4))) return fail(rc);
+      if (tcap_of(c, q) && GA(q == 0 ? s.tail0 : q == 1 ? s.tail1 : s.tail2, n * tstride_of(c, q) * sizeof(uint4)))
+        return fail(rc);
     if (GA(s.tsum, n * 3 * sizeof(uint4)) || GA(s.deep_ids, n * 3 * 4)) return fail(rc);
   }
   g->stage_cap = n * c.fanout * c.cap_t;
@@ -3175,7 +3189,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
                   g->grp_slot, g->grp_off, g->dec_base, s.dlog, s.dmeta, s.dcnt,
                   g->bkt_send, g->bkt_recv, g->bkt_dec, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn,
-                  s.p_ent, s.p_cnt, g->big_base, s.tail[0], s.tail[1], s.tail[2], s.tsum, s.deep_ids};
+                  s.p_ent, s.p_cnt, g->big_base, tail_of(s, 0), tail_of(s, 1), tail_of(s, 2), s.tsum, s.deep_ids};
   for (void* p : ptrs)
     if (p) hipFree(p);
   g->scratch.release();
@@ -4185,9 +4199,9 @@ static int dump_queues_deep(rsf_gossip* g, uint32_t D, uint32_t* rumor, uint32_t
   RSF_HIP(hipMemcpyAsync(ht.data(), g->s.q_txlen, hc * 4, hipMemcpyDeviceToHost, st));
   RSF_HIP(hipMemcpyAsync(sum.data(), g->s.tsum, n * 3 * 16, hipMemcpyDeviceToHost, st));
   for (uint32_t q = 0; q < 3; ++q)
-    if (c.tcap[q]) {
-      tail[q].resize(n * c.tstride[q]);
-      RSF_HIP(hipMemcpyAsync(tail[q].data(), g->s.tail[q], tail[q].size() * 16, hipMemcpyDeviceToHost, st));
+    if (tcap_of(c, q)) {
+      tail[q].resize(n * tstride_of(c, q));
+      RSF_HIP(hipMemcpyAsync(tail[q].data(), tail_of(g->s, q), tail[q].size() * 16, hipMemcpyDeviceToHost, st));
     }
   RSF_HIP(hipStreamSynchronize(st));
   std::vector<std::pair<uint64_t, uint32_t>> items;
@@ -4197,9 +4211,9 @@ static int dump_queues_deep(rsf_gossip* g, uint32_t D, uint32_t* rumor, uint32_t
       const uint64_t hb = (l * 3 + q) * c.qcap;
       for (uint32_t i = 0; i < c.qcap; ++i)
         if (hr[hb + i] != kEmpty) items.push_back({tlq_key(ht[hb + i] & 0xFFFF, ht[hb + i] >> 16, hs[hb + i]), hr[hb + i]});
-      if (c.tcap[q])
+      if (tcap_of(c, q))
         for (uint32_t i = 0; i < sum[l * 3 + q].x; ++i) {
-          const uint4 e = tail[q][l * c.tstride[q] + i];
+          const uint4 e = tail[q][l * tstride_of(c, q) + i];
           items.push_back({tlq_key(e.z & 0xFFFF, e.z >> 16, e.y), e.x});
         }
       std::sort(items.begin(), items.end());
@@ -4232,7 +4246,7 @@ int rsf_gossip_dump_queues(rsf_gossip* g, uint32_t* rumor, uint32_t* seq, uint16
                            uint32_t* next_seq) {
   if (!g || !rumor || !seq || !tx || !len || !next_seq) return gerr("null argument");
   if (g->c.deep) {
-    const uint32_t D = g->c.qcap + std::max(g->c.tcap[0], std::max(g->c.tcap[1], g->c.tcap[2]));
+    const uint32_t D = g->c.qcap + std::max(g->c.tcap0, std::max(g->c.tcap1, g->c.tcap2));
     return rsf_gossip_dump_queues_width(g, D, rumor, seq, tx, len, next_seq, nullptr);
   }
   const uint64_t cnt = g->c.n_loc * 3 * g->c.qcap;

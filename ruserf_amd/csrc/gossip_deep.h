@@ -139,8 +139,8 @@ __device__ uint32_t deep_load_queue(const GCfg& c, const GState& s, uint64_t l, 
   }
   __syncthreads();
   const uint32_t hn = d.hn;
-  const uint32_t tc = c.tcap[q] ? s.tsum[l * 3 + q].x : 0u;
-  const uint4* t = c.tcap[q] ? s.tail[q] + l * c.tstride[q] : nullptr;
+  const uint32_t tc = tcap_of(c, q) ? s.tsum[l * 3 + q].x : 0u;
+  const uint4* t = tcap_of(c, q) ? tail_of(s, q) + l * tstride_of(c, q) : nullptr;
   const uint32_t qdec = q == 1 ? kDecQuery : kDecEvent;
   for (uint32_t i = tid; i < tc; i += kDeepThreads) {
     const uint4 e = t[i];
@@ -179,7 +179,7 @@ __device__ void deep_store_queue(const GCfg& c, const GState& s, uint64_t l, uin
     d.tn = 0;
   }
   __syncthreads();
-  uint4* const t = c.tcap[q] ? s.tail[q] + l * c.tstride[q] : nullptr;
+  uint4* const t = tcap_of(c, q) ? tail_of(s, q) + l * tstride_of(c, q) : nullptr;
   uint64_t tmin = ~0ull;
   uint32_t tlmin = ~0u;
   for (uint32_t i = tid; i < n; i += kDeepThreads) {
@@ -214,7 +214,7 @@ __device__ void deep_store_queue(const GCfg& c, const GState& s, uint64_t l, uin
       if (q == 0) s.q_dec[l * c.qcap + slot] = h ? d.hdec[tid] : 0u;
     }
   }
-  if (tid == 0 && c.tcap[q]) s.tsum[l * 3 + q] = d.tn ? make_uint4(d.tn, tlmin, (uint32_t)tmin, (uint32_t)(tmin >> 32))
+  if (tid == 0 && tcap_of(c, q)) s.tsum[l * 3 + q] = d.tn ? make_uint4(d.tn, tlmin, (uint32_t)tmin, (uint32_t)(tmin >> 32))
                                                       : kTSumEmpty;
   __syncthreads();
 }
@@ -288,7 +288,7 @@ __device__ void deep_emit_member(const GCfg& c, const GState& s, uint64_t l, con
     __syncthreads();
     n += nq;
     // inserting into a bounded queue with no pick in between keeps its depth smallest keys
-    const uint32_t dropped = deep_keep_smallest(d, n, c.qcap + c.tcap[q]);
+    const uint32_t dropped = deep_keep_smallest(d, n, c.qcap + tcap_of(c, q));
     if (tid == 0) d.drops += dropped;
     // get_broadcasts for every peer, queue-major: the smallest fitting unpicked key, repeated
     for (uint32_t j = 0; j < np; ++j) {
@@ -409,10 +409,10 @@ __global__ void __launch_bounds__(kDeepThreads) check_deep_kernel(GCfg c, GState
 // (member, queue), in place, order kept); returns the number dropped; exact new bounds
 __device__ __forceinline__ uint32_t tail_expire_wave(const GCfg& c, const GState& s, uint64_t l, uint32_t q,
                                                      uint32_t lane, uint32_t gen, uint32_t G) {
-  if (!c.tcap[q]) return 0;
+  if (!tcap_of(c, q)) return 0;
   const uint4 sm = s.tsum[l * 3 + q];
   if (!sm.x) return 0;
-  uint4* const t = s.tail[q] + l * c.tstride[q];
+  uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
   uint32_t kept = 0, gone = 0, lmin = ~0u;
   uint64_t kmin = ~0ull;
   for (uint32_t b = 0; b < sm.x; b += kWave) {

@@ -40,7 +40,9 @@ struct GCfg {
   uint32_t snap_w, snap_rejoin;  // snapshotter: bitset words per member, rejoin_after_leave
   // deep queues (qcap <= 64 head + HBM tail): tail capacity per queue (0: none) and the tail
   // row stride (capacity + room for one emission's spills before its capacity check)
-  uint32_t tcap[3], tstride[3];
+  // (named per queue, not arrays: a select between array elements is compiled back into a
+  // dynamic index of a private copy, which goes to scratch or LDS)
+  uint32_t tcap0, tcap1, tcap2, tstride0, tstride1, tstride2;
   uint32_t deep;  // any tail
 };
 
@@ -97,12 +99,16 @@ struct GState {
   // message length, a lower bound of its smallest key (lo, hi)}: emission picks from the head
   // only while a pick's key is below the tail's bound and every stop is decided by a length
   // the tail cannot fit; any other member takes the exact whole-queue path (emit_deep_kernel).
-  uint4* tail[3];
+  uint4 *tail0, *tail1, *tail2;
   uint4* tsum;       // [n_loc][3]
   uint32_t* deep_ids;  // [n_loc] members deferred to emit_deep_kernel this round
   uint32_t* deep_n;    // their count (reset before each emission)
 };
 constexpr uint32_t kTailSlack = 192;  // tail row room past its capacity: one emission's spills (2 x 64) + 64
+// per-queue deep-queue fields by a select on q
+RSF_HD uint32_t tcap_of(const GCfg& c, uint32_t q) { return q == 0 ? c.tcap0 : q == 1 ? c.tcap1 : c.tcap2; }
+RSF_HD uint32_t tstride_of(const GCfg& c, uint32_t q) { return q == 0 ? c.tstride0 : q == 1 ? c.tstride1 : c.tstride2; }
+RSF_HD uint4* tail_of(const GState& s, uint32_t q) { return q == 0 ? s.tail0 : q == 1 ? s.tail1 : s.tail2; }
 constexpr uint32_t kPend = 128;  // pending entries per member (two per lane of a wave)
 // The merge leaves a member at most kPendMerge entries, so the round's originations and
 // refutations (at most 1 + max_refute <= 5 per member) append without applying the list
@@ -449,24 +455,23 @@ __device__ __forceinline__ uint32_t queue_of(uint8_t type) {
 // tail is pruned (tail_prune_serial).
 __device__ __forceinline__ void tail_append_serial(const GCfg& c, const GState& s, uint64_t l, uint32_t q, uint32_t rid,
                                                    uint32_t dec, uint32_t seq, uint32_t tl) {
-  uint4* const t = s.tail[q] + l * c.tstride[q];
-  uint4 sm = s.tsum[l * 3 + q];
-  t[sm.x] = make_uint4(rid, seq, tl, dec);
-  sm.x++;
-  sm.y = min(sm.y, tl >> 16);
+  // (plain scalars, not a uint4 local: HIP's vector type is a union, which keeps a modified
+  // copy out of registers)
+  uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
+  const uint4 sm = s.tsum[l * 3 + q];
+  const uint32_t cnt = sm.x;
+  t[cnt] = make_uint4(rid, seq, tl, dec);
   const uint64_t k = tlq_key(tl & 0xFFFF, tl >> 16, seq), mk = ((uint64_t)sm.w << 32) | sm.z;
-  if (k < mk) {
-    sm.z = (uint32_t)k;
-    sm.w = (uint32_t)(k >> 32);
-  }
-  s.tsum[l * 3 + q] = sm;
+  const uint64_t nk = k < mk ? k : mk;
+  s.tsum[l * 3 + q] = make_uint4(cnt + 1, min(sm.y, tl >> 16), (uint32_t)nk, (uint32_t)(nk >> 32));
 }
 // over the queue's depth: drop the largest key of head and tail (the head's is its last live
-// slot; the tail's bounds stay lower bounds)
-__device__ __forceinline__ void tail_prune_serial(const GCfg& c, const GState& s, uint64_t l, uint32_t q, MRegs& r) {
-  uint4 sm = s.tsum[l * 3 + q];
-  if (sm.x <= c.tcap[q]) return;
-  uint4* const t = s.tail[q] + l * c.tstride[q];
+// slot; the tail's bounds stay lower bounds); true if one was dropped
+__device__ __forceinline__ bool tail_prune_serial(const GCfg& c, const GState& s, uint64_t l, uint32_t q) {
+  const uint4 sm = s.tsum[l * 3 + q];
+  const uint32_t cnt = sm.x;
+  if (cnt <= tcap_of(c, q)) return false;
+  uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
   const uint64_t base = (l * 3 + q) * c.qcap;
   uint32_t hi = kEmpty, ti = 0;
   uint64_t hk = 0, tk = 0;
@@ -476,7 +481,7 @@ __device__ __forceinline__ void tail_prune_serial(const GCfg& c, const GState& s
       const uint32_t x = s.q_txlen[base + i];
       hk = tlq_key(x & 0xFFFF, x >> 16, s.q_seq[base + i]);
     }
-  for (uint32_t i = 0; i < sm.x; ++i) {
+  for (uint32_t i = 0; i < cnt; ++i) {
     const uint4 e = t[i];
     const uint64_t x = tlq_key(e.z & 0xFFFF, e.z >> 16, e.y);
     if (x >= tk) {
@@ -489,12 +494,10 @@ __device__ __forceinline__ void tail_prune_serial(const GCfg& c, const GState& s
     s.q_seq[base + hi] = 0;
     s.q_txlen[base + hi] = 0;
   } else {
-    t[ti] = t[sm.x - 1];
-    sm.x--;
-    s.tsum[l * 3 + q] = sm;
+    t[ti] = t[cnt - 1];
+    s.tsum[l * 3 + q] = make_uint4(cnt - 1, sm.y, sm.z, sm.w);
   }
-  s.q_pruned[l] += 1;
-  r.err |= kErrQueue;
+  return true;
 }
 
 __device__ __forceinline__ void queue_insert_item(const GCfg& c, const GState& s, uint64_t l, uint32_t q,
@@ -507,7 +510,7 @@ __device__ __forceinline__ void queue_insert_item(const GCfg& c, const GState& s
     if (pos == kEmpty && tlq_key(tl & 0xFFFF, tl >> 16, s.q_seq[base + cnt]) > newkey) pos = cnt;
     cnt++;
   }
-  if (cnt == c.qcap && c.tcap[q]) {
+  if (cnt == c.qcap && tcap_of(c, q)) {
     if (pos == kEmpty) {  // the new item is the head's largest: straight to the tail
       tail_append_serial(c, s, l, q, rid, dec, seq, len << 16);
     } else {  // the head's largest falls into the tail, the new item shifts in
@@ -525,7 +528,10 @@ __device__ __forceinline__ void queue_insert_item(const GCfg& c, const GState& s
       s.q_seq[base + pos] = seq;
       s.q_txlen[base + pos] = (len << 16);
     }
-    tail_prune_serial(c, s, l, q, r);
+    if (tail_prune_serial(c, s, l, q)) {
+      s.q_pruned[l] += 1;
+      r.err |= kErrQueue;
+    }
     return;
   }
   if (cnt == c.qcap) {
