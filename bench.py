@@ -224,15 +224,17 @@ def cpu_baseline_vivaldi(seconds_target=8.0):
                       f"{cpu_info()}"}
 
 
-def configs1_point(args, rank, world, queue_cap, settle, warmup, steps):
+def configs1_point(args, rank, world, queue_cap, settle, warmup, steps, queue_depth=0):
     """One more gossip measurement at configs[1]'s 1M members (see main)."""
     from bench_gossip import run_gossip
     a = argparse.Namespace(**vars(args))
     a.members, a.queue_cap, a.settle, a.warmup, a.steps = 1_000_000, queue_cap, settle, warmup, steps
+    a.queue_depth = queue_depth
     torch.cuda.empty_cache()
     r = run_gossip(a, rank, world)
     keep = ["value", "unit", "ms_per_step", "merges_per_s", "records_per_round_per_gpu", "queue_pruned_per_round",
-            "queue_pruned_per_merged_record", "error_members", "cub_canaries_intact", "phases_ms_per_round"]
+            "queue_pruned_per_merged_record", "error_members", "cub_canaries_intact", "phases_ms_per_round",
+            "deep_path_members_per_round"]
     out = {"metric": r["metric"], "steps": steps, "warmup": warmup, **{k: r[k] for k in keep}, "config": r["config"]}
     out["roofline"] = {k: r["roofline"][k] for k in ["bound", "achieved", "peak", "unit", "frac", "kernel",
                                                       "bytes_per_launch", "avg_launch_ms"]}
@@ -316,6 +318,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--queue-cap", type=int, default=64,
                     help="gossip: slots per transmit-limited queue (1..256; the reference's max_queue_depth is 4096)")
+    ap.add_argument("--queue-depth", type=int, default=0,
+                    help="gossip: intent queue depth above --queue-cap (<= 64): a register head plus an HBM tail, "
+                         "pruned only by the QueueChecker (the reference's max_queue_depth is 4096)")
     ap.add_argument("--no-extra-points", action="store_true",
                     help="gossip: skip the configs[1] points (1M members, 64- and 256-slot queues)")
     ap.add_argument("--settle", type=int, default=None,
@@ -384,11 +389,12 @@ def main():
         attach_traffic(workload, res)
         if world == 1 and not args.no_extra_points and args.members != 1_000_000:
             # BASELINE configs[1] on one GPU (1M members, the same workload), at the default
-            # 64-slot queues (saturated: the flood fills every queue each round) and at 256
-            # slots over the first rounds, where no queue overflows -- the rounds of the
-            # reference's queue, unbounded between QueueChecker ticks
+            # 64-slot queues (saturated: the flood fills every queue each round) and with the
+            # reference's queue: 4096 deep (64-slot register head + HBM tail), settled, nothing
+            # dropped between QueueChecker ticks
             res["configs1_points"] = [configs1_point(args, rank, world, 64, None, args.warmup, args.steps),
-                                      configs1_point(args, rank, world, 256, 3, 1, 6)]
+                                      configs1_point(args, rank, world, 64, None, args.warmup, args.steps,
+                                                     queue_depth=4096)]
         if not args.no_vivaldi:
             # the metric's second half, timed in the same invocation (configs[4]: 64M members)
             vargs = argparse.Namespace(**vars(args))

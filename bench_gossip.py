@@ -23,14 +23,18 @@ PRUNE_FRAC = float(os.environ.get("RSF_PRUNE_FRAC", 0.1))
 HBM_PEAK_GBS = 8000.0
 
 
-def gossip_cfg(n_total, rounds_total, world, shard=None, queue_cap=64):
+def gossip_cfg(n_total, rounds_total, world, shard=None, queue_cap=64, queue_depth=0):
+    """queue_depth > queue_cap: the intent queue (the only one this workload fills) is that
+    deep -- register head + HBM tail, pruned only by the QueueChecker as the reference's
+    (max_queue_depth 4096); the query / event queues stay at queue_cap (always empty here)."""
     from ruserf_amd.gossip import GossipConfig
     # rumor ring: a power of two holding >= 64 rounds of rumor blocks (ids recycle after that)
     per_round = SUBJECTS * 4 + int(round(n_total * 0.01))
     ring = 1 << max(10, (per_round * 64 - 1).bit_length())
     return GossipConfig(n_members=n_total, n_subjects=SUBJECTS, shard=shard, queue_cap=queue_cap, event_buffer_size=512,
                         query_buffer_size=512, slot_k=1, fanout=3, gossip_limit=8 * 24, gossip_overhead=2,
-                        retransmit_mult=4, max_refute=4, max_rumors=ring, seed=SEED)
+                        retransmit_mult=4, max_refute=4, max_rumors=ring, seed=SEED,
+                        queue_depth=(queue_depth, 0, 0) if queue_depth > queue_cap else None)
 
 
 # SURVEY §8(d): B_merge = 16 (record read) + 16 (view entry read) + 16 (view entry write)
@@ -67,7 +71,8 @@ def run_gossip(args, rank, world):
     n = per * world
     settle = SETTLE_ROUNDS if args.settle is None else args.settle
     rounds_total = settle + args.warmup + args.steps
-    cfg = gossip_cfg(n, rounds_total, world, queue_cap=args.queue_cap)
+    depth = getattr(args, "queue_depth", 0) or 0
+    cfg = gossip_cfg(n, rounds_total, world, queue_cap=args.queue_cap, queue_depth=depth)
     subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED, prune_frac=PRUNE_FRAC)
     views = W.initial_views(SUBJECTS)
     stream = torch.cuda.current_stream()
@@ -93,6 +98,7 @@ def run_gossip(args, rank, world):
     # as of each member's last emission (no flush): the timed rounds' emissions apply
     # exactly the timed rounds' worth of pending re-queues
     pruned0 = eng.pruned_total(flush=False)
+    deep0 = eng.deep_stats()[0] if depth else 0
     eng.set_profiling(True)
     if sharded:
         sg.set_timing(True)
@@ -113,6 +119,7 @@ def run_gossip(args, rank, world):
     phase_ms, nr = eng.phase_times()
     merged = eng.merged_total() - merged0
     pruned = eng.pruned_total(flush=False) - pruned0
+    deep_members = (eng.deep_stats()[0] - deep0) if depth else None
     st = eng.members()
     from ruserf_amd.gossip import E_QUEUE_PRUNE
     # capacity errors other than the bounded queue's counted prunes (reported separately)
@@ -155,6 +162,7 @@ def run_gossip(args, rank, world):
                                   else "BASELINE configs[1])" if per == 1_000_000 and world == 1 else "custom size)"),
                    "members": n, "members_per_gpu": per, "fanout": 3, "items_per_target": 8,
                    "queue_cap_per_queue": cfg.queue_cap, "subjects": SUBJECTS,
+                   "intent_queue_depth": cfg.depths()[0],
                    "record_slots_per_group": min(3 * cfg.queue_cap, cfg.gossip_limit // (cfg.gossip_overhead + 18)),
                    "settle_rounds": settle, "parallelism": f"members sharded x{world}"
                    + (" (multi-GPU code path forced)" if world == 1 and os.environ.get("RSF_FORCE_SHARDED") == "1"
@@ -168,6 +176,8 @@ def run_gossip(args, rank, world):
         "queue_pruned_per_round": pruned_all / args.steps,
         "queue_pruned_per_merged_record": pruned_all / max(1.0, merged_all),
         "queue_prune_members": qpm_all,
+        # deep queues: members per round whose emission needed the tail (emit_deep_kernel)
+        "deep_path_members_per_round": (deep_members / args.steps) if deep_members is not None else None,
         "phases_ms_per_round": dict(zip(names, avg)),
         # multi-GPU path: device time of the round's collectives (inside the phases above)
         "collectives_ms_per_round": exchange_ms,
