@@ -665,6 +665,11 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
 // (24 KB per block instead of 48), so LDS no longer caps the kernel at 3 waves/SIMD
 #define RSF_VIV_LDS1 0
 #endif
+#ifndef RSF_VIV_OWNDIRECT
+// 1: each lane loads its own row directly (no LDS transpose of the own rows; with RSF_VIV_LDS1
+// the peer rows alone use the wave's 6 KB block)
+#define RSF_VIV_OWNDIRECT 0
+#endif
 #ifndef RSF_VIV_WLATE
 // 1: the adjustment window is folded up to its index as soon as it arrives and its slots after
 // the index are read again after update_vivaldi (cacheable loads, so the second read finds
@@ -725,8 +730,15 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_pipe_kerne
   const double2* src = reinterpret_cast<const double2*>(cur + (p.lo + wbase) * 12);
   const uint32_t last = wrows * 6 - 1;
   double2 own[6];
+#if RSF_VIV_OWNDIRECT
+  // each lane its own row: six 16-B loads at a 96-B stride over the wave's contiguous 6 KB
+  // (the same lines as the coalesced pieces), straight into the registers the update uses
+#pragma unroll
+  for (uint32_t k = 0; k < 6; ++k) own[k] = ld_s(src + min(lane * 6 + k, last));
+#else
 #pragma unroll
   for (uint32_t k = 0; k < 6; ++k) own[k] = ld_s(src + min(lane + 64 * k, last));
+#endif
   double* frec = filt + ((uint64_t)slot * p.shard_n + local) * FR;
   double rec[FR];
   {
@@ -768,8 +780,10 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_pipe_kerne
   double2* so = stage[threadIdx.x / 64][0];
   double2* sp = stage[threadIdx.x / 64][1];
 #endif
+#if !RSF_VIV_OWNDIRECT
 #pragma unroll
   for (uint32_t k = 0; k < 6; ++k) so[lane + 64 * k] = own[k];
+#endif
 #if !RSF_VIV_LDS1
 #pragma unroll
   for (uint32_t ps = 0; ps < 2; ++ps)
@@ -779,6 +793,16 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_pipe_kerne
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   double me[D], other[D], e, a, h, oe, oa, oh;
+#if RSF_VIV_OWNDIRECT
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    me[2 * i] = own[i].x;
+    me[2 * i + 1] = own[i].y;
+  }
+  e = own[4].x;
+  a = own[4].y;
+  h = own[5].x;
+#else
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const double2 t = so[lane * 6 + i];
@@ -788,6 +812,7 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_pipe_kerne
   e = so[lane * 6 + 4].x;
   a = so[lane * 6 + 4].y;
   h = so[lane * 6 + 5].x;
+#endif
 #if RSF_VIV_LDS1
   // the block is free once every lane has read its own row; the peer rows follow
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -366,6 +366,40 @@ def test_queue_prune_counted_and_checker():
     L.orc_world_free(C.byref(w))
 
 
+def test_queue_depth_per_queue_and_checker():
+    """Per-queue capacities (orc_world_cfg.qdepth, the engine's queue_depth): each queue
+    prunes at its own depth, slots past it stay unused, scans stop at the high-water mark,
+    and the QueueChecker counts and prunes head-and-tail queues the same way."""
+    cfg = O.WorldCfg(n=2, s=1, qcap=16, ebuf=512, qbuf=512, slot_k=8, fanout=1, limit=1400, overhead=2,
+                     retransmit_mult=4, max_refute=2, cap_rumors=1024, seed=0x5EED5EED)
+    cfg.qdepth[:] = [4, 16, 8]
+    w = O.World()
+    assert L.orc_world_init(C.byref(w), C.byref(cfg)) == 0
+    assert list(w.qd) == [4, 16, 8]
+    for i in range(30):
+        w.rumors[i].type = 1
+        w.rumors[i].msg_len = 20
+    for q in range(3):
+        for i in range(10):
+            L.orc_queue_insert(C.byref(w), 0, q, 10 * q + i)
+    live = [[w.q_rumor[q * 16 + i] for i in range(16) if w.q_rumor[q * 16 + i] != 0xFFFFFFFF] for q in range(3)]
+    assert sorted(live[0]) == [6, 7, 8, 9]            # depth 4: the newest four kept
+    assert sorted(live[1]) == list(range(10, 20))     # depth 16: nothing dropped
+    assert sorted(live[2]) == list(range(22, 30))     # depth 8
+    assert w.q_pruned[0] == 6 + 2
+    assert [w.q_hwm[q] for q in range(3)] == [4, 10, 8]
+    # a pick frees a slot below the high-water mark; the next insert reuses it
+    out, used = (C.c_uint32 * 8)(), C.c_uint32()
+    w.tx_limit = 1  # every pick retires
+    assert L.orc_queue_get_broadcasts(C.byref(w), 0, 1, 22, out, 8, C.byref(used)) == 1
+    L.orc_queue_insert(C.byref(w), 0, 1, 29)
+    assert w.q_hwm[1] == 10
+    st = (C.c_uint64 * 9)()
+    L.orc_check_queues(C.byref(w), 5, 0, 8, st)
+    assert list(st) == [4, 10, 8, 0, 1, 1, 0, 5, 3]
+    L.orc_world_free(C.byref(w))
+
+
 def test_delegate_merge_remote_state(kats):
     """merge_remote_state (delegate.rs:422-554) through orc_merge_remote_state: the
     reference test's PushPullMessage becomes a sender local_state (status_ltimes ->
