@@ -427,7 +427,7 @@ __device__ __forceinline__ void q_rerank(const GCfg& c, QRegs& Q, uint32_t lane,
 // DEEP (a tail behind the head, its key / length lower bounds tmin / tminlen): the call is
 // exact only if every pick's key is below tmin and every stop with budget left is one no tail
 // item could fit; otherwise *unsafe is set and the caller abandons the emission (the member
-// then takes emit_deep_kernel's whole-queue path).  Picks are checked before they are bumped.
+// then takes emit_deep_wave_kernel's whole-queue path).  Picks are checked before they are bumped.
 template <bool PERMUTE_DEC, bool DEEP = false>
 __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uint32_t lane, int64_t limit,
                                                     uint32_t* stage_val, uint32_t* stage_dec,
@@ -1341,7 +1341,7 @@ __device__ __forceinline__ void bkt_group_keys(const Buckets& bk, uint32_t lane,
 // DEEP (queues with an HBM tail): the emission runs on the heads as below; it is committed
 // only if every pick was decided by the head alone (q_pick_peers' checks against the tails'
 // bounds) and every spill fits its tail -- otherwise nothing is stored (records written to the
-// group slots are rewritten) and the member is listed for emit_deep_kernel.
+// group slots are rewritten) and the member is listed for emit_deep_wave_kernel.
 template <bool BKT, bool DEEP = false>
 __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_t l, uint32_t lane, EmitIn& e,
                                          uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val,
@@ -1483,7 +1483,12 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
       if (ne2 && !unsafe) q_pick_peers<false, true>(c, Q2, lane, np, used_v, nrec_v, off, ov, od, err, d2, row, nullptr, RSF_TB(2), &unsafe);
 #undef RSF_TB
       if (unsafe) {  // nothing committed: the whole-queue path redoes this member's emission
-        if (lane == 0) s.deep_ids[atomicAdd(s.deep_n, 1u)] = (uint32_t)l;
+        // list 0 if every queue's items fit the small LDS capacity, else list 1 (from the back)
+        const uint32_t need = c.qcap + max(max(tc0 + (pc & 0xFF), tc1 + ((pc >> 8) & 0xFF)), tc2 + ((pc >> 16) & 0xFF));
+        if (lane == 0) {
+          if (need <= kDeepSmall) s.deep_ids[atomicAdd(s.deep_n, 1u)] = (uint32_t)l;
+          else s.deep_ids[c.n_loc * 3 - 1 - atomicAdd(s.deep_n + 1, 1u)] = (uint32_t)l;
+        }
         return;
       }
     } else {
@@ -2900,7 +2905,9 @@ struct rsf_gossip {
            *grp_slot = nullptr, *grp_off = nullptr, *stage_dec = nullptr;
   rsf::CubTemp grp_tmp;  // the group count reduce / scan (each call sized by cub_run)
   unsigned merge_blocks = 1;  // merge_big_kernel's grid: merge_kernel's resident blocks per CU x CUs
-  unsigned deep_blocks = 1;   // emit_deep_kernel / check_deep_kernel grid (resident blocks x CUs)
+  unsigned deep_blocks = 1;   // emit_deep_wave_kernel<kDeepSmall> grid (resident waves x CUs)
+  unsigned deep_blocks_big = 1;  // emit_deep_wave_kernel<kDeepBig> grid
+  unsigned deep_check_blocks = 1;  // check_deep_kernel grid
   uint64_t deep_last = 0;     // rsf_gossip_deep_stats' previous total
   uint32_t* big_ids = nullptr;  // receivers deferred to merge_big_kernel (count: d_counters[52])
   // RSF_GUARD_ZONES (diagnostic builds): 0xA5-filled zones before and after big_ids and
@@ -3118,10 +3125,16 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
       return fail(rsf::set_error(RSF_ERR_HIP, "occupancy query failed"));
     g->merge_blocks = (unsigned)std::max(1, per_cu * cus);
     if (c.deep) {
-      int dpc = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpc, emit_deep_kernel<false>, kDeepThreads, 0) != hipSuccess)
+      int dpc = 0, dpb = 0, dpk = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpc, emit_deep_wave_kernel<false, kDeepSmall>, kWave, 0) !=
+              hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpb, emit_deep_wave_kernel<false, kDeepBig>, kWave, 0) !=
+              hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpk, check_deep_kernel, kDeepThreads, 0) != hipSuccess)
         return fail(rsf::set_error(RSF_ERR_HIP, "occupancy query failed"));
       g->deep_blocks = (unsigned)std::max(1, dpc * cus);
+      g->deep_blocks_big = (unsigned)std::max(1, dpb * cus);
+      g->deep_check_blocks = (unsigned)std::max(1, dpk * cus);
     }
   }
   // the hipCUB temporaries are sized per call at their first use (rsf::cub_run)
@@ -3474,7 +3487,7 @@ int rsf_gossip_rumor_block(rsf_gossip* g, void** p, uint64_t* bytes) {
 // bucket mode (world > 0): emission straight into the destination shards' buckets
 static Buckets send_buckets(rsf_gossip* g);
 // emission by the queue layout: four slots per lane (65..256), one (64: FULL, or fewer); deep
-// queues then run the members the heads could not decide through emit_deep_kernel
+// queues then run the members the heads could not decide through emit_deep_wave_kernel
 template <bool BKT>
 static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
   const GCfg& c = g->c;
@@ -3484,7 +3497,7 @@ static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
     hipLaunchKernelGGL(emit4_kernel<BKT>, dim3((unsigned)c.n_loc), dim3(kWave), 0, st, c, g->s, g->grp_key, g->grp_slot,
                        g->grp_cnt, g->stage_val, g->stage_dec, bk);
   } else if (c.deep) {
-    RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 4, st));
+    RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 8, st));
     if (c.qcap == kWave)
       hipLaunchKernelGGL((emit_kernel<BKT, true, true>), egrid, eb, 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt,
                          g->stage_val, g->stage_dec, bk);
@@ -3493,8 +3506,10 @@ static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
                          g->grp_cnt, g->stage_val, g->stage_dec, bk);
     RSF_HIP(hipGetLastError());
     RSF_DBG_SYNC(st, "emit_kernel (deep)");
-    hipLaunchKernelGGL(emit_deep_kernel<BKT>, dim3(g->deep_blocks), dim3(kDeepThreads), 0, st, c, g->s, g->grp_key,
-                       g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, g->d_counters + 55);
+    hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepSmall>), dim3(g->deep_blocks), dim3(kWave), 0, st, c, g->s,
+                       g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 0u, g->d_counters + 55);
+    hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepBig>), dim3(g->deep_blocks_big), dim3(kWave), 0, st, c, g->s,
+                       g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 1u, g->d_counters + 55);
   } else if (c.qcap == kWave) {
     hipLaunchKernelGGL((emit_kernel<BKT, true>), egrid, eb, 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt,
                        g->stage_val, g->stage_dec, bk);
@@ -4028,12 +4043,13 @@ int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t mi
   int rc = flush_pending(g);
   if (rc) return rc;
   RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, g->stream));
-  if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 4, g->stream));
+  if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 8, g->stream));
   hipLaunchKernelGGL(check_queues_kernel, dim3(grid1(c.n_loc * 3)), dim3(256), 0, g->stream, c, g->s, max_depth,
                      depth_warning, g->d_counters + 40);
   RSF_HIP(hipGetLastError());
   if (c.deep) {  // the deep queues over the max: the smallest max keys of head and tail kept
-    hipLaunchKernelGGL(check_deep_kernel, dim3(g->deep_blocks), dim3(kDeepThreads), 0, g->stream, c, g->s, max_depth);
+    hipLaunchKernelGGL(check_deep_kernel, dim3(g->deep_check_blocks), dim3(kDeepThreads), 0, g->stream, c, g->s,
+                       max_depth);
     RSF_HIP(hipGetLastError());
   }
   unsigned long long st[9];

@@ -7,20 +7,15 @@
 // (options.rs:512, base.rs:720-760) -- far more than a register head holds.  emit_run decides a
 // member's picks from the head alone when the tail provably cannot change them (every pick's key
 // below the tail's key bound, every stop one no tail item could fit) and commits; otherwise it
-// stores nothing and lists the member here.  emit_deep_kernel then redoes that member's whole
-// emission exactly, one block per member, with the queue's every item in LDS:
-//   pending re-queues appended (transmits 0, next seqs) -> bounded-queue prune to the depth ->
-//   per peer, queue-major, get_broadcasts = repeated block argmin of the fitting unpicked keys,
-//   then transmits + 1 or retire -> head = the queue_cap smallest keys in order, tail = the rest.
-// The same block routines run the QueueChecker's prune (check_deep_kernel).
+// stores nothing and lists the member for emit_deep_wave_kernel (below), which redoes that
+// member's emission with every item of its queues in LDS.  The block routines first in this file
+// run the QueueChecker's prune (check_deep_kernel).
 #pragma once
 
 namespace {
 
 constexpr uint32_t kDeepThreads = 256;
 constexpr uint32_t kDeepWaves = kDeepThreads / kWave;
-// a queue's items in LDS: head + tail (<= RSF_MAX_QUEUE_DEPTH) + one pending list's new items
-constexpr uint32_t kDeepItems = RSF_MAX_QUEUE_DEPTH + kPend;
 enum : uint8_t { kDeepDead = 0, kDeepLive = 1, kDeepPicked = 2 };
 
 struct DeepLds {
@@ -219,60 +214,211 @@ __device__ void deep_store_queue(const GCfg& c, const GState& s, uint64_t l, uin
   __syncthreads();
 }
 
-// one member's whole emission (emit_run's semantics over every item of every queue)
-template <bool BKT>
-__device__ void deep_emit_member(const GCfg& c, const GState& s, uint64_t l, const uint32_t* __restrict__ grp_key,
-                                 const uint32_t* __restrict__ slot, uint32_t* __restrict__ cnt_s,
-                                 uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec, const Buckets& bk,
-                                 DeepLds& d) {
-  const uint32_t tid = threadIdx.x;
-  const uint32_t pc = s.p_cnt[l], npend = pend_total(pc);
-  if (tid < kWave) {  // the peers (a prefix of the fanout slots): where each one's records go
-    const uint32_t gk = tid < c.fanout ? grp_key[l * c.fanout + tid] : kSentinel;
-    const uint32_t gs = tid < c.fanout ? slot[l * c.fanout + tid] : 0u;
-    const uint64_t pm = ballot(gk != kSentinel);
-    if (tid == 0) {
-      d.np = (uint32_t)__popcll(pm);
-      d.err = 0;
-      d.drops = 0;
-    }
-    if (tid < c.fanout) {
-      uint64_t off = ~0ull;
-      uint32_t* oc = nullptr;
-      if (gk != kSentinel) {
-        if (BKT) {
-          const uint32_t w = gs >> kBktWShift, idx = gs & kBktIdxMask;
-          if (idx < bk.gcap) {
-            off = (uint64_t)w * bk.stride_u32 + bk.vals_off + (uint64_t)idx * c.cap_t;
-            oc = bk.send + (uint64_t)w * bk.stride_u32 + bk.cnt_off + idx;
-          }
-        } else {
-          off = (uint64_t)gs * c.cap_t;
-          oc = cnt_s + gs;
+// ---- one wave per deferred member ------------------------------------------------------
+// The path emit_run defers to (a member whose picks its head could not decide).  Per queue:
+// every item (head, tail, the pending re-queues) into the wave's LDS, the bounded prune to the
+// depth, then the REFILL: the queue_cap smallest keys become the register head (sorted) and the
+// rest the tail with exact bounds, and the ordinary head emission (q_pick_peers with the deep
+// checks) runs again -- with the true smallest keys in the head it almost always decides.  If
+// it still cannot, the picks are made over the LDS items directly (repeated wave argmin of the
+// fitting unpicked keys, as get_broadcasts restated), and head / tail are rebuilt after them.
+// Two capacities: kDeepSmall items (24 KB of LDS, 6 waves per CU) for the common case, the full
+// depth (77 KB) for the rest; emit_run lists a member by the size its largest queue needs.
+constexpr uint32_t kDeepBig = kDeepItems;
+constexpr uint8_t kDeepInHead = 3;
+
+template <uint32_t CAP>
+struct DeepWave {
+  uint64_t key[CAP];
+  uint32_t rid[CAP], dec[CAP];
+  uint8_t st[CAP];
+  GState::PendE pend[kPend];
+  uint32_t hist[256];
+  uint64_t hkey[kWave];
+  uint32_t hrid[kWave], hdec[kWave];
+  QLds row;  // q_pick_peers' re-rank scratch
+};
+
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <uint32_t CAP>
+__device__ __forceinline__ uint32_t w_count(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint8_t state) {
+  uint32_t k = 0;
+  for (uint32_t i = lane; i < n; i += kWave) k += d.st[i] == state ? 1u : 0u;
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(k), 63);
+}
+
+// the k-th smallest (1-based) key among the items in state `state` (distinct keys): 8-bit radix
+// select, one wave
+template <uint32_t CAP>
+__device__ uint64_t w_select_kth(DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint32_t k, uint8_t state) {
+  uint64_t prefix = 0, mask = 0;
+  uint32_t need = k;
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (uint32_t i = lane; i < 256; i += kWave) d.hist[i] = 0;
+    wsync();
+    for (uint32_t i = lane; i < n; i += kWave)
+      if (d.st[i] == state && (d.key[i] & mask) == prefix) atomicAdd(&d.hist[(d.key[i] >> shift) & 0xFF], 1u);
+    wsync();
+    const uint32_t h0 = d.hist[4 * lane], h1 = d.hist[4 * lane + 1], h2 = d.hist[4 * lane + 2], h3 = d.hist[4 * lane + 3];
+    const uint32_t sum = h0 + h1 + h2 + h3, incl = wave_inclusive_sum_u32(sum), excl = incl - sum;
+    const bool here = excl < need && need <= incl;
+    uint32_t b = 0, acc = excl;
+    if (acc + h0 < need) {
+      acc += h0;
+      b = 1;
+      if (acc + h1 < need) {
+        acc += h1;
+        b = 2;
+        if (acc + h2 < need) {
+          acc += h2;
+          b = 3;
         }
       }
-      d.off[tid] = off;
-      d.oc[tid] = oc;
-      d.used[tid] = 0;
-      d.nrec[tid] = 0;
+    }
+    const int w = __ffsll((long long)ballot(here)) - 1;
+    const uint32_t digit = shfl_u32(4 * lane + b, w);
+    need = shfl_u32(need - acc, w);
+    prefix |= (uint64_t)digit << shift;
+    mask |= 0xFFull << shift;
+    wsync();
+  }
+  return prefix;
+}
+
+// head = the qcap smallest live keys, sorted into the lanes of Q (marked kDeepInHead in LDS);
+// returns the bounds of the live items left (the tail): (min key, min length), ~0 if none
+template <uint32_t CAP>
+__device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint32_t q, QRegs& Q,
+                            uint64_t& tmin, uint32_t& tminlen) {
+  const uint32_t na = w_count(d, lane, n, kDeepLive);
+  const uint64_t T = na > c.qcap ? w_select_kth(d, lane, n, c.qcap, kDeepLive) : ~0ull;
+  uint32_t base = 0;
+  uint64_t km = ~0ull;
+  uint32_t lm = ~0u;
+  for (uint32_t b = 0; b < n; b += kWave) {
+    const uint32_t i = b + lane;
+    const bool live = i < n && d.st[i] == kDeepLive;
+    const uint64_t k = live ? d.key[i] : ~0ull;
+    const bool sel = live && k <= T;
+    const uint64_t m = ballot(sel);
+    if (sel) {
+      const uint32_t pos = base + mbcnt(m);
+      d.hkey[pos] = k;
+      d.hrid[pos] = d.rid[i];
+      d.hdec[pos] = d.dec[i];
+      d.st[i] = kDeepInHead;
+    } else if (live) {  // stays in the tail
+      km = k < km ? k : km;
+      lm = min(lm, key_len(k));
+    }
+    base += (uint32_t)__popcll(m);
+  }
+  tmin = wave_min_u64(km);
+  tminlen = wave_min_u32(lm);
+  wsync();
+  const uint32_t hn = base;
+  const bool h = lane < hn;
+  const uint64_t mk = h ? d.hkey[lane] : ~0ull;
+  uint32_t rank = 0;
+  for (uint32_t j = 0; j < hn; ++j) rank += d.hkey[j] < mk ? 1u : 0u;
+  const uint64_t hm = ballot(h);
+  const uint32_t dest = h ? rank : hn + mbcnt(~hm);
+  const int addr = (int)(dest * 4);
+  const uint32_t r = h ? d.hrid[lane] : kEmpty, sq = h ? key_seq(mk) : 0u, tl = h ? key_tl(mk) : 0u,
+                 dc = h ? d.hdec[lane] : (q == 1 ? kDecQuery : kDecEvent);
+  Q.r = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)r);
+  Q.sq = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)sq);
+  Q.tl = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)tl);
+  Q.dec = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)dc);
+  wsync();
+}
+
+// the live items not in the head back to the tail (compacted, any order); returns the count
+template <uint32_t CAP>
+__device__ uint32_t w_store_tail(const GCfg& c, const GState& s, uint64_t l, uint32_t q, const DeepWave<CAP>& d,
+                                 uint32_t lane, uint32_t n) {
+  uint4* const t = tcap_of(c, q) ? tail_of(s, q) + l * tstride_of(c, q) : nullptr;
+  uint32_t base = 0;
+  for (uint32_t b = 0; b < n; b += kWave) {
+    const uint32_t i = b + lane;
+    const bool live = i < n && d.st[i] == kDeepLive;
+    const uint64_t m = ballot(live);
+    if (live) {  // only a deep queue holds more live items than its head
+      const uint64_t k = d.key[i];
+      t[base + mbcnt(m)] = make_uint4(d.rid[i], key_seq(k), key_tl(k), d.dec[i]);
+    }
+    base += (uint32_t)__popcll(m);
+  }
+  return base;
+}
+
+template <bool BKT, uint32_t CAP>
+__device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uint32_t lane,
+                                 const uint32_t* __restrict__ grp_key, const uint32_t* __restrict__ slot,
+                                 uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val,
+                                 uint32_t* __restrict__ out_dec, const Buckets& bk, DeepWave<CAP>& d) {
+  const uint32_t pc = s.p_cnt[l], npend = pend_total(pc);
+  // the peers (a prefix of the fanout slots); lane j < np: peer j's record offset and count word
+  const uint32_t gk = lane < c.fanout ? grp_key[l * c.fanout + lane] : kSentinel;
+  const uint32_t gs = lane < c.fanout ? slot[l * c.fanout + lane] : 0u;
+  const uint32_t np = (uint32_t)__popcll(ballot(gk != kSentinel));
+  uint64_t off_v = ~0ull;
+  uint32_t* oc = nullptr;
+  if (lane < np) {
+    if (BKT) {
+      const uint32_t w = gs >> kBktWShift, idx = gs & kBktIdxMask;
+      if (idx < bk.gcap) {
+        off_v = (uint64_t)w * bk.stride_u32 + bk.vals_off + (uint64_t)idx * c.cap_t;
+        oc = bk.send + (uint64_t)w * bk.stride_u32 + bk.cnt_off + idx;
+      }
+    } else {
+      off_v = (uint64_t)gs * c.cap_t;
+      oc = cnt_s + gs;
     }
   }
-  for (uint32_t i = tid; i < npend; i += kDeepThreads) d.pend[i] = s.p_ent[l * kPend + i];
-  __syncthreads();
-  const uint32_t np = d.np;
+  for (uint32_t i = lane; i < npend; i += kWave) d.pend[i] = s.p_ent[l * kPend + i];
   uint32_t* const ov = BKT ? bk.send : out_val;
   uint32_t* const od = BKT ? nullptr : out_dec;
+  uint32_t used_v = 0, nrec_v = 0, err = 0, drops = 0;
   for (uint32_t q = 0; q < 3; ++q) {
     const uint32_t nq = (pc >> (8 * q)) & 0xFF;
-    uint32_t n = deep_load_queue(c, s, l, q, d);
+    const uint32_t qdec = q == 1 ? kDecQuery : kDecEvent;
+    // every item of the queue into LDS: the head's live prefix, the tail, then the pending
+    // re-queues in list order (transmits 0, the next seqs)
+    QRegs Q{kEmpty, 0, 0};
+    q_load(c, s, l, q, lane, Q);
+    const bool hl = lane < c.qcap && Q.r != kEmpty;
+    const uint32_t hn = (uint32_t)__popcll(ballot(hl));
+    if (hl) {
+      d.key[lane] = tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq);
+      d.rid[lane] = Q.r;
+      d.dec[lane] = Q.dec;
+      d.st[lane] = kDeepLive;
+    }
+    const uint32_t tc = tcap_of(c, q) ? s.tsum[l * 3 + q].x : 0u;
+    if (tc) {
+      const uint4* t = tail_of(s, q) + l * tstride_of(c, q);
+      for (uint32_t i = lane; i < tc; i += kWave) {
+        const uint4 e = t[i];
+        d.key[hn + i] = tlq_key(e.z & 0xFFFF, e.z >> 16, e.y);
+        d.rid[hn + i] = e.x;
+        d.dec[hn + i] = q == 0 ? e.w : qdec;
+        d.st[hn + i] = kDeepLive;
+      }
+    }
+    uint32_t n = hn + tc;
     if (n == 0 && nq == 0) continue;
-    // the pending re-queues of this queue, in list order, transmits 0 and the next seqs
-    if (tid < kWave) {
+    wsync();
+    if (nq) {
       const uint32_t seq0 = s.q_next_seq[l * 3 + q];
-      const uint32_t qdec = q == 1 ? kDecQuery : kDecEvent;
       uint32_t rank0 = 0;
       for (uint32_t b = 0; b < kPend / kWave; ++b) {
-        const uint32_t i = b * kWave + tid;
+        const uint32_t i = b * kWave + lane;
         const bool in = i < npend && (d.pend[i].lq >> 16) == q;
         const uint64_t m = ballot(in);
         if (in) {
@@ -284,103 +430,134 @@ __device__ void deep_emit_member(const GCfg& c, const GState& s, uint64_t l, con
         }
         rank0 += (uint32_t)__popcll(m);
       }
+      n += nq;
+      wsync();
     }
-    __syncthreads();
-    n += nq;
     // inserting into a bounded queue with no pick in between keeps its depth smallest keys
-    const uint32_t dropped = deep_keep_smallest(d, n, c.qcap + tcap_of(c, q));
-    if (tid == 0) d.drops += dropped;
-    // get_broadcasts for every peer, queue-major: the smallest fitting unpicked key, repeated
-    for (uint32_t j = 0; j < np; ++j) {
-      const uint32_t lim = c.limit - d.used[j];
-      uint32_t used = 0, k = 0;
-      for (;;) {
-        const int32_t free_b = (int32_t)(lim - used - c.overhead);
-        if (free_b <= 0) break;
-        uint64_t best = ~0ull;
-        for (uint32_t i = tid; i < n; i += kDeepThreads)
-          if (d.st[i] == kDeepLive) {
-            const uint64_t x = d.key[i];
-            if (key_len(x) <= (uint32_t)free_b && x < best) best = x;
-          }
-        best = blk_min_u64(best, d);
-        if (best == ~0ull) break;
-        for (uint32_t i = tid; i < n; i += kDeepThreads)
-          if (d.st[i] == kDeepLive && d.key[i] == best) d.sel_idx = i;
-        __syncthreads();
-        if (tid == 0) {
-          const uint32_t w = d.sel_idx, pos = d.nrec[j] + k;
-          d.st[w] = kDeepPicked;
-          if (pos < c.cap_t && d.off[j] != ~0ull) {
-            ov[d.off[j] + pos] = d.rid[w];
-            if (od) od[d.off[j] + pos] = d.dec[w];
-          }
-        }
-        k++;
-        used += c.overhead + key_len(best);
-        __syncthreads();
-      }
-      for (uint32_t i = tid; i < n; i += kDeepThreads)  // transmits + 1, or retired at the limit
-        if (d.st[i] == kDeepPicked) {
-          if ((uint32_t)(d.key[i] >> 48) + 1 >= c.tx_limit) {
-            d.st[i] = kDeepDead;
-          } else {
-            d.key[i] += 1ull << 48;
-            d.st[i] = kDeepLive;
-          }
-        }
-      if (tid == 0) {
-        if (d.nrec[j] + k > c.cap_t) d.err |= kErrStage;
-        d.nrec[j] += k;
-        d.used[j] += used;
-      }
-      __syncthreads();
+    const uint32_t depth = c.qcap + tcap_of(c, q);
+    if (n > depth) {
+      const uint64_t T = w_select_kth(d, lane, n, depth, kDeepLive);
+      for (uint32_t i = lane; i < n; i += kWave)
+        if (d.st[i] == kDeepLive && d.key[i] > T) d.st[i] = kDeepDead;
+      drops += n - depth;
+      wsync();
     }
-    deep_store_queue(c, s, l, q, d, n);
-    if (tid < kWave) {  // clear the state flags for the next queue
-      for (uint32_t i = tid; i < n; i += kWave) d.st[i] = kDeepDead;
+    // the refill, then the head's own emission with the deep checks
+    uint64_t tmin;
+    uint32_t tminlen;
+    w_take_head(c, d, lane, n, q, Q, tmin, tminlen);
+    const uint32_t used_0 = used_v, nrec_0 = nrec_v;
+    bool unsafe = false, dirty = false;
+    uint32_t errq = 0;
+    if (q == 0)
+      q_pick_peers<true, true>(c, Q, lane, np, used_v, nrec_v, off_v, ov, od, errq, dirty, d.row, nullptr, tmin, tminlen,
+                               &unsafe);
+    else
+      q_pick_peers<false, true>(c, Q, lane, np, used_v, nrec_v, off_v, ov, od, errq, dirty, d.row, nullptr, tmin,
+                                tminlen, &unsafe);
+    if (!unsafe) {
+      err |= errq;
+      q_store(c, s, l, q, lane, Q, true);
+      const uint32_t cnt = w_store_tail(c, s, l, q, d, lane, n);
+      if (lane == 0 && tcap_of(c, q))
+        s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
+    } else {
+      // the head still cannot decide: get_broadcasts over every item, peer by peer
+      used_v = used_0;
+      nrec_v = nrec_0;
+      for (uint32_t i = lane; i < n; i += kWave)
+        if (d.st[i] == kDeepInHead) d.st[i] = kDeepLive;
+      wsync();
+      for (uint32_t j = 0; j < np; ++j) {
+        const uint32_t lim = c.limit - shfl_u32(used_v, j), nrec = shfl_u32(nrec_v, j);
+        const uint64_t off = shfl_u64(off_v, j);
+        uint32_t used = 0, k = 0;
+        for (;;) {
+          const int32_t free_b = (int32_t)(lim - used - c.overhead);
+          if (free_b <= 0) break;
+          uint64_t best = ~0ull;
+          for (uint32_t i = lane; i < n; i += kWave)
+            if (d.st[i] == kDeepLive) {
+              const uint64_t x = d.key[i];
+              if (key_len(x) <= (uint32_t)free_b && x < best) best = x;
+            }
+          best = wave_min_u64(best);
+          if (best == ~0ull) break;
+          uint32_t wi = kEmpty;
+          for (uint32_t i = lane; i < n; i += kWave)
+            if (d.st[i] == kDeepLive && d.key[i] == best) wi = i;
+          const uint64_t owner = ballot(wi != kEmpty);
+          wi = shfl_u32(wi, __ffsll((long long)owner) - 1);
+          if (lane == 0) {
+            d.st[wi] = kDeepPicked;
+            if (nrec + k < c.cap_t && off != ~0ull) {
+              ov[off + nrec + k] = d.rid[wi];
+              if (od) od[off + nrec + k] = d.dec[wi];
+            }
+          }
+          k++;
+          used += c.overhead + key_len(best);
+          wsync();
+        }
+        for (uint32_t i = lane; i < n; i += kWave)  // transmits + 1, or retired at the limit
+          if (d.st[i] == kDeepPicked) {
+            if ((uint32_t)(d.key[i] >> 48) + 1 >= c.tx_limit) {
+              d.st[i] = kDeepDead;
+            } else {
+              d.key[i] += 1ull << 48;
+              d.st[i] = kDeepLive;
+            }
+          }
+        if (nrec + k > c.cap_t) err |= kErrStage;
+        used_v += lane == j ? used : 0u;
+        nrec_v += lane == j ? k : 0u;
+        wsync();
+      }
+      w_take_head(c, d, lane, n, q, Q, tmin, tminlen);
+      q_store(c, s, l, q, lane, Q, true);
+      const uint32_t cnt = w_store_tail(c, s, l, q, d, lane, n);
+      if (lane == 0 && tcap_of(c, q))
+        s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
     }
-    __syncthreads();
+    for (uint32_t i = lane; i < n; i += kWave) d.st[i] = kDeepDead;  // clean for the next queue
+    wsync();
   }
   // the groups' counts and the member's bookkeeping (emit_run's)
-  if (tid < np) {
-    uint32_t* oc = d.oc[tid];
-    if (oc && (BKT || d.nrec[tid])) *oc = min(d.nrec[tid], c.cap_t);
-  }
-  if (tid == 0) {
+  if (oc && (BKT || nrec_v)) *oc = min(nrec_v, c.cap_t);
+  if (lane == 0) {
     if (npend) {
       s.p_cnt[l] = 0;
       for (uint32_t q = 0; q < 3; ++q) s.q_next_seq[l * 3 + q] += (pc >> (8 * q)) & 0xFF;
     }
-    uint32_t err = d.err;
-    if (d.drops) {
-      s.q_pruned[l] += d.drops;
+    if (drops) {
+      s.q_pruned[l] += drops;
       err |= kErrQueue;
     }
     if (err) s.err[l] |= err;
   }
-  __syncthreads();
 }
 
-// the members emit_run deferred (s.deep_ids, count *s.deep_n): one block each; every block
-// walks the list with a stride of the grid, so each one reaches the end
-template <bool BKT>
-__global__ void __launch_bounds__(kDeepThreads) emit_deep_kernel(GCfg c, GState s, const uint32_t* __restrict__ grp_key,
-                                                                const uint32_t* __restrict__ slot,
-                                                                uint32_t* __restrict__ cnt_s,
-                                                                uint32_t* __restrict__ out_val,
-                                                                uint32_t* __restrict__ out_dec, Buckets bk,
-                                                                unsigned long long* __restrict__ total) {
-  __shared__ DeepLds d;
-  const uint32_t n_list = *s.deep_n;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && n_list) atomicAdd(total, (unsigned long long)n_list);
-  for (uint32_t i = 0; i < kDeepItems; i += kDeepThreads)
-    if (i + threadIdx.x < kDeepItems) d.st[i + threadIdx.x] = kDeepDead;
-  __syncthreads();
+// the members emit_run deferred: list 0 (those that fit kDeepSmall items per queue) from the
+// front of s.deep_ids, list 1 (the rest) from its back; one wave per member, the grid striding
+// over the list so every wave reaches its end
+template <bool BKT, uint32_t CAP>
+__global__ void __launch_bounds__(kWave) emit_deep_wave_kernel(GCfg c, GState s, const uint32_t* __restrict__ grp_key,
+                                                              const uint32_t* __restrict__ slot,
+                                                              uint32_t* __restrict__ cnt_s,
+                                                              uint32_t* __restrict__ out_val,
+                                                              uint32_t* __restrict__ out_dec, Buckets bk, uint32_t list,
+                                                              unsigned long long* __restrict__ total) {
+  __shared__ DeepWave<CAP> d;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n_list = s.deep_n[list];
+  if (blockIdx.x == 0 && lane == 0 && n_list) atomicAdd(total, (unsigned long long)n_list);
+  for (uint32_t i = lane; i < CAP; i += kWave) d.st[i] = kDeepDead;
+  wsync();
+  const uint64_t last = c.n_loc * 3 - 1;
   for (uint32_t it = blockIdx.x; it < n_list; it += gridDim.x) {
-    const uint64_t l = s.deep_ids[it];
-    if (l >= c.n_loc) continue;  // block-uniform
-    deep_emit_member<BKT>(c, s, l, grp_key, slot, cnt_s, out_val, out_dec, bk, d);
+    const uint64_t l = list ? s.deep_ids[last - it] : s.deep_ids[it];
+    if (l >= c.n_loc) continue;  // wave-uniform
+    deep_wave_member<BKT, CAP>(c, s, l, lane, grp_key, slot, cnt_s, out_val, out_dec, bk, d);
   }
 }
 

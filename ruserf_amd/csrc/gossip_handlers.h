@@ -98,11 +98,11 @@ struct GState {
   // decoration}, i < tsum[l * 3 + q].x.  tsum = {count, a lower bound of the tail's smallest
   // message length, a lower bound of its smallest key (lo, hi)}: emission picks from the head
   // only while a pick's key is below the tail's bound and every stop is decided by a length
-  // the tail cannot fit; any other member takes the exact whole-queue path (emit_deep_kernel).
+  // the tail cannot fit; any other member takes the exact whole-queue path (emit_deep_wave_kernel).
   uint4 *tail0, *tail1, *tail2;
   uint4* tsum;       // [n_loc][3]
-  uint32_t* deep_ids;  // [n_loc] members deferred to emit_deep_kernel this round
-  uint32_t* deep_n;    // their count (reset before each emission)
+  uint32_t* deep_ids;  // [n_loc * 3] members deferred to emit_deep_wave_kernel (two lists), or queues to prune
+  uint32_t* deep_n;    // [2] the lists' lengths (reset before each emission)
 };
 constexpr uint32_t kTailSlack = 192;  // tail row room past its capacity: one emission's spills (2 x 64) + 64
 // per-queue deep-queue fields by a select on q
@@ -115,6 +115,10 @@ constexpr uint32_t kPend = 128;  // pending entries per member (two per lane of 
 // serially; a member that emits nothing for many rounds can still fill it (then the
 // serial application runs, slow but exact).
 constexpr uint32_t kPendMerge = kPend - 8;
+// items of one queue the deferred-emission path holds in LDS: the full depth plus a pending
+// list (kDeepItems), and the common case's smaller capacity (kDeepSmall)
+constexpr uint32_t kDeepItems = RSF_MAX_QUEUE_DEPTH + kPend;
+constexpr uint32_t kDeepSmall = 1024 + 64 + kPend;
 RSF_HD uint32_t pend_total(uint32_t pc) { return (pc & 0xFF) + ((pc >> 8) & 0xFF) + ((pc >> 16) & 0xFF); }
 
 // per-member scalar state held in registers while a kernel works on it
