@@ -176,7 +176,7 @@ def run_gossip(args, rank, world):
         "queue_pruned_per_round": pruned_all / args.steps,
         "queue_pruned_per_merged_record": pruned_all / max(1.0, merged_all),
         "queue_prune_members": qpm_all,
-        # deep queues: members per round whose emission needed the tail (emit_deep_kernel)
+        # deep queues: members per round whose emission needed the tail (emit_deep_wave_kernel)
         "deep_path_members_per_round": (deep_members / args.steps) if deep_members is not None else None,
         "phases_ms_per_round": dict(zip(names, avg)),
         # multi-GPU path: device time of the round's collectives (inside the phases above)

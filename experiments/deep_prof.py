@@ -1,0 +1,48 @@
+"""Diagnostic only: why emit_run defers members to the deep path and where the deep wave
+kernel spends its time, at the bench's configs[1] shape with the intent queue 4096 deep
+(needs a library built with -DRSF_DEEP_PROF=1, loaded via RSF_LIB_PATH).
+Usage: deep_prof.py [members] [settle]"""
+import ctypes as C
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+import bench_gossip as B  # noqa: E402
+from ruserf_amd import workload as W  # noqa: E402
+from ruserf_amd._lib import lib  # noqa: E402
+from ruserf_amd.gossip import GossipEngine  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+settle = int(sys.argv[2]) if len(sys.argv) > 2 else B.SETTLE_ROUNDS
+L = lib()
+L.rsf_gossip_deep_prof.restype = C.c_int
+L.rsf_gossip_deep_prof.argtypes = [C.POINTER(C.c_uint64)]
+rounds = settle + 5
+cfg = B.gossip_cfg(n, rounds, 1, queue_depth=4096)
+subj, acts, ml = W.intents_workload(n, B.SUBJECTS, rounds, rate=0.01, seed=B.SEED, prune_frac=B.PRUNE_FRAC)
+eng = GossipEngine(cfg)
+eng.set_subjects(subj)
+eng.init_views(*W.initial_views(B.SUBJECTS))
+buf = (C.c_uint64 * 64)()
+for t in range(settle):
+    eng.round(t, ml[t], acts[t])
+torch.cuda.synchronize()
+assert L.rsf_gossip_deep_prof(buf) == 0, "library not built with RSF_DEEP_PROF=1"
+for t in range(settle, rounds):
+    eng.round(t, ml[t], acts[t])
+torch.cuda.synchronize()
+L.rsf_gossip_deep_prof(buf)
+v = [int(x) for x in buf]
+why = ["empty_head", "pick_len", "pick_key", "exact_empty", "exact_len", "exact_key", "capacity", "-"]
+ph = ["load", "prune", "take_head", "picks", "store", "fallback_picks", "fallback_store", "fallbacks"]
+members = max(1, v[16])
+out = {"rounds": rounds - settle, "deferred_per_round": v[16] / (rounds - settle),
+       "why_per_round": {k: v[i] / (rounds - settle) for i, k in enumerate(why)},
+       "cycles_per_member": v[17] / members,
+       "phase_cycles_per_member": {k: v[8 + i] / members for i, k in enumerate(ph)},
+       "select_passes_per_select": v[18] / max(1, v[19]), "selects_per_member": v[19] / members,
+       "take_head_cycles_per_member": {k: v[20 + i] / members for i, k in enumerate(["count", "select", "gather", "rank_permute"])},
+       "queue_items_hist_by_128": {i * 128: v[32 + i] for i in range(32) if v[32 + i]}}
+print(json.dumps(out))

@@ -578,7 +578,7 @@ int rsf_gossip_dump_queues(rsf_gossip* g, uint32_t* rumor, uint32_t* seq, uint16
 int rsf_gossip_dump_queues_width(rsf_gossip* g, uint32_t width, uint32_t* rumor, uint32_t* seq, uint16_t* transmits,
                                  uint16_t* len, uint32_t* next_seq, uint32_t* max_live);
 /* deep queues: members whose emission took the exact whole-queue path (the head alone could
- * not decide a pick; emit_deep_kernel) since creation, and since the last call */
+ * not decide a pick; emit_deep_wave_kernel) since creation, and since the last call */
 int rsf_gossip_deep_stats(rsf_gossip* g, uint64_t* slow_total, uint64_t* slow_since_last);
 int rsf_gossip_dump_buffers(rsf_gossip* g, uint64_t* eb_ltime, uint32_t* eb_cnt, uint64_t* eb_keys,
                             uint64_t* qb_ltime, uint32_t* qb_cnt, uint32_t* qb_ids);

@@ -48,6 +48,23 @@ constexpr uint32_t kDecQuery = 0xFFFFFFFEu, kDecEvent = 0xFFFFFFFDu, kDecViewMax
 #if RSF_MERGE_PROF || RSF_EMIT_PROF || RSF_CHECKS
 __device__ unsigned long long g_merge_prof[8];
 #endif
+// diagnostic build (experiments/deep_prof.py): why emit_run deferred members to the deep path
+// ([0..7]), the deep wave kernel's per-phase shader-clock totals ([8..15]) and its queue sizes
+// (a histogram by 128 items, [32..63]); read by rsf_gossip_deep_prof
+#ifndef RSF_DEEP_PROF
+#define RSF_DEEP_PROF 0
+#endif
+#if RSF_DEEP_PROF
+__device__ unsigned long long g_deep_prof[64];
+#define RSF_DEEP_WHY(k) \
+  do {                  \
+    if (lane == 0) atomicAdd(&g_deep_prof[(k)], 1ull); \
+  } while (0)
+#else
+#define RSF_DEEP_WHY(k) \
+  do {                  \
+  } while (0)
+#endif
 #if RSF_CHECKS
 #define RSF_BAD(k, cond, val) \
   ((cond) ? (atomicOr(&g_merge_prof[0], 1ull << (k)), g_merge_prof[1 + ((k) % 7)] = (unsigned long long)(val), true) : false)
@@ -437,7 +454,10 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   const bool valid = lane < c.qcap;
   const uint64_t live_m = ballot(valid && Q.r != kEmpty);  // a sorted queue: a prefix
   if (!live_m) {
-    if (DEEP && tmin != ~0ull && limit - (int64_t)c.overhead >= (int64_t)tminlen) *unsafe = true;
+    if (DEEP && tmin != ~0ull && limit - (int64_t)c.overhead >= (int64_t)tminlen) {
+      *unsafe = true;
+      RSF_DEEP_WHY(3);
+    }
     return 0;
   }
   const bool live = lane_bit(live_m);
@@ -456,7 +476,10 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
     if (free_b <= 0) break;
     const uint64_t cand = ballot(len <= (uint32_t)free_b) & live_m & ~pick_m;
     if (!cand) {
-      if (DEEP && tminlen <= (uint32_t)free_b) *unsafe = true;  // a tail item might fit
+      if (DEEP && tminlen <= (uint32_t)free_b) {  // a tail item might fit
+        *unsafe = true;
+        RSF_DEEP_WHY(4);
+      }
       break;
     }
     const int win = __ffsll((long long)cand) - 1;
@@ -466,7 +489,10 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   if (DEEP && pick_m) {  // the largest pick (the highest lane: the head is sorted) below the tail
     const int hl = 63 - __clzll((long long)pick_m);
     const uint32_t tl = shfl_u32(Q.tl, hl);
-    if (tlq_key(tl & 0xFFFF, tl >> 16, shfl_u32(Q.sq, hl)) >= tmin) *unsafe = true;
+    if (tlq_key(tl & 0xFFFF, tl >> 16, shfl_u32(Q.sq, hl)) >= tmin) {
+      *unsafe = true;
+      RSF_DEEP_WHY(5);
+    }
   }
   if (DEEP && *unsafe) return used;
   if (!pick_m) return used;
@@ -594,7 +620,10 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
   const bool valid = lane < c.qcap;
   const uint64_t live_m = ballot(valid && Q.r != kEmpty);  // a sorted queue: a prefix
   if (!live_m) {
-    if (DEEP && tmin != ~0ull) *unsafe = true;  // only the tail holds items
+    if (DEEP && tmin != ~0ull) {  // only the tail holds items
+      *unsafe = true;
+      RSF_DEEP_WHY(0);
+    }
     return;
   }
 #if RSF_EMIT_PROF
@@ -634,7 +663,10 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
       if (free_b <= 0) break;
       const uint64_t fit = ballot(len <= (uint32_t)free_b) & avail & ~pick;
       if (!fit) {
-        if (DEEP && tminlen <= (uint32_t)free_b) *unsafe = true;  // a tail item might fit
+        if (DEEP && tminlen <= (uint32_t)free_b) {  // a tail item might fit
+          *unsafe = true;
+          RSF_DEEP_WHY(1);
+        }
         break;
       }
       const uint64_t cand = fit & rem;
@@ -676,6 +708,7 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
     const uint32_t tl = shfl_u32(Q.tl, hl);
     if (tlq_key(tl & 0xFFFF, tl >> 16, shfl_u32(Q.sq, hl)) >= tmin) {
       *unsafe = true;
+      RSF_DEEP_WHY(2);
       return;
     }
   }
@@ -1436,6 +1469,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
     if (drops) err |= kErrQueue;
     // a tail past its capacity needs the bounded queue's exact prune over head and tail
     if (DEEP) unsafe = sp0.cnt > c.tcap0 || sp1.cnt > c.tcap1 || sp2.cnt > c.tcap2;
+    if (DEEP && unsafe) RSF_DEEP_WHY(6);
     // (the list's bookkeeping -- count, next seqs, prune count -- is written at the end: a store
     // here would make the compiler wait for it before reusing its registers)
   }
@@ -1483,10 +1517,12 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
       if (ne2 && !unsafe) q_pick_peers<false, true>(c, Q2, lane, np, used_v, nrec_v, off, ov, od, err, d2, row, nullptr, RSF_TB(2), &unsafe);
 #undef RSF_TB
       if (unsafe) {  // nothing committed: the whole-queue path redoes this member's emission
-        // list 0 if every queue's items fit the small LDS capacity, else list 1 (from the back)
+        // by the LDS capacity its largest queue needs: list 2 (kDeepTiny; from n_loc), list 0
+        // (kDeepSmall; from the front), list 1 (the full depth; from the back)
         const uint32_t need = c.qcap + max(max(tc0 + (pc & 0xFF), tc1 + ((pc >> 8) & 0xFF)), tc2 + ((pc >> 16) & 0xFF));
         if (lane == 0) {
-          if (need <= kDeepSmall) s.deep_ids[atomicAdd(s.deep_n, 1u)] = (uint32_t)l;
+          if (need <= kDeepTiny) s.deep_ids[c.n_loc + atomicAdd(s.deep_n + 2, 1u)] = (uint32_t)l;
+          else if (need <= kDeepSmall) s.deep_ids[atomicAdd(s.deep_n, 1u)] = (uint32_t)l;
           else s.deep_ids[c.n_loc * 3 - 1 - atomicAdd(s.deep_n + 1, 1u)] = (uint32_t)l;
         }
         return;
@@ -2907,6 +2943,7 @@ struct rsf_gossip {
   unsigned merge_blocks = 1;  // merge_big_kernel's grid: merge_kernel's resident blocks per CU x CUs
   unsigned deep_blocks = 1;   // emit_deep_wave_kernel<kDeepSmall> grid (resident waves x CUs)
   unsigned deep_blocks_big = 1;  // emit_deep_wave_kernel<kDeepBig> grid
+  unsigned deep_blocks_tiny = 1;  // emit_deep_wave_kernel<kDeepTiny> grid
   unsigned deep_check_blocks = 1;  // check_deep_kernel grid
   uint64_t deep_last = 0;     // rsf_gossip_deep_stats' previous total
   uint32_t* big_ids = nullptr;  // receivers deferred to merge_big_kernel (count: d_counters[52])
@@ -3125,15 +3162,18 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
       return fail(rsf::set_error(RSF_ERR_HIP, "occupancy query failed"));
     g->merge_blocks = (unsigned)std::max(1, per_cu * cus);
     if (c.deep) {
-      int dpc = 0, dpb = 0, dpk = 0;
+      int dpc = 0, dpb = 0, dpk = 0, dpt = 1;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpc, emit_deep_wave_kernel<false, kDeepSmall>, kWave, 0) !=
               hipSuccess ||
+          (kDeepTiny && hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                            &dpt, emit_deep_wave_kernel<false, kDeepTiny ? kDeepTiny : kWave>, kWave, 0) != hipSuccess) ||
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpb, emit_deep_wave_kernel<false, kDeepBig>, kWave, 0) !=
               hipSuccess ||
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpk, check_deep_kernel, kDeepThreads, 0) != hipSuccess)
         return fail(rsf::set_error(RSF_ERR_HIP, "occupancy query failed"));
       g->deep_blocks = (unsigned)std::max(1, dpc * cus);
       g->deep_blocks_big = (unsigned)std::max(1, dpb * cus);
+      g->deep_blocks_tiny = (unsigned)std::max(1, dpt * cus);
       g->deep_check_blocks = (unsigned)std::max(1, dpk * cus);
     }
   }
@@ -3142,7 +3182,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   bool ok = true;
   auto ms = [&](void* p, int v, size_t b) { ok = ok && hipMemsetAsync(p, v, b, st) == hipSuccess; };
   ms(g->d_counters, 0, 64 * 8);  // status flags and running totals start at zero
-  s.deep_n = reinterpret_cast<uint32_t*>(g->d_counters + 54);  // deferred members (d_counters[55]: their total)
+  s.deep_n = reinterpret_cast<uint32_t*>(g->d_counters + 53);  // deferred members: 3 lists (words 53-54; [55] their total)
   ms(s.emin, 0, n * 8);
   ms(s.qmin, 0, n * 8);
   ms(s.digest, 0, n * 8);
@@ -3497,7 +3537,7 @@ static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
     hipLaunchKernelGGL(emit4_kernel<BKT>, dim3((unsigned)c.n_loc), dim3(kWave), 0, st, c, g->s, g->grp_key, g->grp_slot,
                        g->grp_cnt, g->stage_val, g->stage_dec, bk);
   } else if (c.deep) {
-    RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 8, st));
+    RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 16, st));
     if (c.qcap == kWave)
       hipLaunchKernelGGL((emit_kernel<BKT, true, true>), egrid, eb, 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt,
                          g->stage_val, g->stage_dec, bk);
@@ -3506,6 +3546,10 @@ static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
                          g->grp_cnt, g->stage_val, g->stage_dec, bk);
     RSF_HIP(hipGetLastError());
     RSF_DBG_SYNC(st, "emit_kernel (deep)");
+    if (kDeepTiny)
+      hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepTiny ? kDeepTiny : kWave>), dim3(g->deep_blocks_tiny),
+                         dim3(kWave), 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec,
+                         bk, 2u, g->d_counters + 55);
     hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepSmall>), dim3(g->deep_blocks), dim3(kWave), 0, st, c, g->s,
                        g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 0u, g->d_counters + 55);
     hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepBig>), dim3(g->deep_blocks_big), dim3(kWave), 0, st, c, g->s,
@@ -3837,6 +3881,22 @@ int rsf_gossip_debug_ptrs(rsf_gossip* g, uint64_t* out, uint32_t n) {
   return (int)k;
 }
 
+// diagnostic only (experiments/deep_prof.py, builds with -DRSF_DEEP_PROF=1): reads and clears
+// the deferral reasons, the deep wave kernel's phase totals and queue-size histogram (64 words);
+// returns -1 in normal builds
+int rsf_gossip_deep_prof(uint64_t* out64) {
+#if RSF_DEEP_PROF
+  RSF_HIP(hipDeviceSynchronize());
+  RSF_HIP(hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_deep_prof), 64 * sizeof(uint64_t)));
+  unsigned long long z[64] = {};
+  RSF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_deep_prof), z, sizeof(z)));
+  return 0;
+#else
+  (void)out64;
+  return -1;
+#endif
+}
+
 // diagnostic only (experiments/merge_prof.py, builds with -DRSF_MERGE_PROF=1): reads and
 // clears merge_kernel's per-phase shader-clock totals; returns -1 in normal builds
 int rsf_gossip_merge_prof(uint64_t* out8) {
@@ -4043,7 +4103,7 @@ int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t mi
   int rc = flush_pending(g);
   if (rc) return rc;
   RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, g->stream));
-  if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 8, g->stream));
+  if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 16, g->stream));
   hipLaunchKernelGGL(check_queues_kernel, dim3(grid1(c.n_loc * 3)), dim3(256), 0, g->stream, c, g->s, max_depth,
                      depth_warning, g->d_counters + 40);
   RSF_HIP(hipGetLastError());

@@ -215,6 +215,10 @@ __device__ void deep_store_queue(const GCfg& c, const GState& s, uint64_t l, uin
 }
 
 // ---- one wave per deferred member ------------------------------------------------------
+#if RSF_DEEP_PROF
+// per-wave totals (one wave per block), added to g_deep_prof once at the kernel's end
+__shared__ unsigned long long s_dprof[64];
+#endif
 // The path emit_run defers to (a member whose picks its head could not decide).  Per queue:
 // every item (head, tail, the pending re-queues) into the wave's LDS, the bounded prune to the
 // depth, then the REFILL: the queue_cap smallest keys become the register head (sorted) and the
@@ -222,8 +226,9 @@ __device__ void deep_store_queue(const GCfg& c, const GState& s, uint64_t l, uin
 // checks) runs again -- with the true smallest keys in the head it almost always decides.  If
 // it still cannot, the picks are made over the LDS items directly (repeated wave argmin of the
 // fitting unpicked keys, as get_broadcasts restated), and head / tail are rebuilt after them.
-// Two capacities: kDeepSmall items (24 KB of LDS, 6 waves per CU) for the common case, the full
-// depth (77 KB) for the rest; emit_run lists a member by the size its largest queue needs.
+// Three capacities: kDeepTiny items (19 KB of LDS) and kDeepSmall (25 KB) for the common cases,
+// the full depth (77 KB) for the rest; emit_run lists a member by the size its largest queue
+// needs.
 constexpr uint32_t kDeepBig = kDeepItems;
 constexpr uint8_t kDeepInHead = 3;
 
@@ -245,47 +250,156 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <uint32_t CAP>
-__device__ __forceinline__ uint32_t w_count(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint8_t state) {
-  uint32_t k = 0;
-  for (uint32_t i = lane; i < n; i += kWave) k += d.st[i] == state ? 1u : 0u;
-  return (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(k), 63);
+__device__ __forceinline__ uint64_t wave_and_u64(uint64_t v) {
+  v &= dpp64<0xB1, 0xF>(v);
+  v &= dpp64<0x4E, 0xF>(v);
+  v &= dpp64<0x124, 0xF>(v);
+  v &= dpp64<0x128, 0xF>(v);
+  v &= dpp64<0x142, 0xA>(v);
+  v &= dpp64<0x143, 0xC>(v);
+  return lane63_u64(v);
+}
+__device__ __forceinline__ uint64_t wave_or_u64(uint64_t v) {
+  v |= dpp64<0xB1, 0xF>(v);
+  v |= dpp64<0x4E, 0xF>(v);
+  v |= dpp64<0x124, 0xF>(v);
+  v |= dpp64<0x128, 0xF>(v);
+  v |= dpp64<0x142, 0xA>(v);
+  v |= dpp64<0x143, 0xC>(v);
+  return lane63_u64(v);
 }
 
-// the k-th smallest (1-based) key among the items in state `state` (distinct keys): 8-bit radix
-// select, one wave
+// The LDS scans below read kDeepU items per lane before using any (one LDS round trip per
+// kDeepU * 64 items instead of one per 64).
+constexpr uint32_t kDeepU = 8;
+
+// kDeepU items per lane from LDS: every load issued (in-range indices) before any is used;
+// v[u]: item b + u * 64 + lane exists and is in state `state`, x[u] its key
 template <uint32_t CAP>
-__device__ uint64_t w_select_kth(DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint32_t k, uint8_t state) {
+__device__ __forceinline__ void w_chunk(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint32_t b, uint8_t state,
+                                        uint64_t (&x)[kDeepU], bool (&v)[kDeepU]) {
+  uint32_t sv[kDeepU];
+#pragma unroll
+  for (uint32_t u = 0; u < kDeepU; ++u) {
+    const uint32_t i = b + u * kWave + lane;
+    const uint32_t ii = i < n ? i : 0u;
+    sv[u] = d.st[ii];
+    x[u] = d.key[ii];
+  }
+#pragma unroll
+  for (uint32_t u = 0; u < kDeepU; ++u) v[u] = (b + u * kWave + lane < n) & (sv[u] == state);
+}
+
+// the items in state `state`: count, smallest and largest key, AND and OR of the keys
+struct WRange {
+  uint32_t cnt;
+  uint64_t lo, hi, an, orr;
+};
+template <uint32_t CAP>
+__device__ WRange w_range(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint8_t state) {
+  uint32_t cnt = 0;
+  uint64_t lo = ~0ull, hi = 0, an = ~0ull, orr = 0;
+  for (uint32_t b = 0; b < n; b += kDeepU * kWave) {
+    uint64_t x[kDeepU];
+    bool v[kDeepU];
+    w_chunk(d, lane, n, b, state, x, v);
+#pragma unroll
+    for (uint32_t u = 0; u < kDeepU; ++u)
+      if (v[u]) {
+        cnt++;
+        lo = x[u] < lo ? x[u] : lo;
+        hi = x[u] > hi ? x[u] : hi;
+        an &= x[u];
+        orr |= x[u];
+      }
+  }
+  WRange r;
+  r.cnt = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(cnt), 63);
+  r.lo = wave_min_u64(lo);
+  r.hi = wave_max_u64(hi);
+  r.an = wave_and_u64(an);
+  r.orr = wave_or_u64(orr);
+  return r;
+}
+
+// the k-th smallest (1-based) key among the items in state `state` (distinct keys; rg their
+// w_range): 8-bit radix select, one wave.  Bytes every candidate key shares (the top bytes, the
+// high byte of the length and of the seq) are taken from rg without a pass; a digit's lanes
+// that agree with the first active lane's digit (the common case: one transmit class, few
+// lengths) are counted by that lane alone; the select stops as soon as the chosen bucket holds
+// one key.
+template <uint32_t CAP>
+__device__ uint64_t w_select_kth(DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint32_t k, uint8_t state,
+                                 const WRange& rg) {
+  if (k <= 1 || rg.lo == rg.hi) return rg.lo;
+  const uint64_t var = rg.an ^ rg.orr;  // the bits that differ between candidates
   uint64_t prefix = 0, mask = 0;
   uint32_t need = k;
+#if RSF_DEEP_PROF
+  if (lane == 0) s_dprof[19] += 1ull;
+#endif
   for (int shift = 56; shift >= 0; shift -= 8) {
+    const uint64_t bm = 0xFFull << shift;
+    if (!(var & bm)) {  // every candidate has this byte
+      prefix |= rg.an & bm;
+      mask |= bm;
+      continue;
+    }
+#if RSF_DEEP_PROF
+    if (lane == 0) s_dprof[18] += 1ull;
+#endif
     for (uint32_t i = lane; i < 256; i += kWave) d.hist[i] = 0;
     wsync();
-    for (uint32_t i = lane; i < n; i += kWave)
-      if (d.st[i] == state && (d.key[i] & mask) == prefix) atomicAdd(&d.hist[(d.key[i] >> shift) & 0xFF], 1u);
+    for (uint32_t b = 0; b < n; b += kDeepU * kWave) {
+      uint64_t x[kDeepU];
+      bool v[kDeepU];
+      w_chunk(d, lane, n, b, state, x, v);
+#pragma unroll
+      for (uint32_t u = 0; u < kDeepU; ++u) {
+        const bool in = v[u] && (x[u] & mask) == prefix;
+        const uint32_t dg = (uint32_t)(x[u] >> shift) & 0xFF;
+        const uint64_t am = ballot(in);
+        if (!am) continue;
+        const int f = __ffsll((long long)am) - 1;
+        const uint32_t d0 = shfl_u32(dg, f);
+        const uint64_t same = ballot(in && dg == d0);
+        if (lane == (uint32_t)f) atomicAdd(&d.hist[d0], (uint32_t)__popcll(same));
+        else if (in && dg != d0) atomicAdd(&d.hist[dg], 1u);
+      }
+    }
     wsync();
     const uint32_t h0 = d.hist[4 * lane], h1 = d.hist[4 * lane + 1], h2 = d.hist[4 * lane + 2], h3 = d.hist[4 * lane + 3];
     const uint32_t sum = h0 + h1 + h2 + h3, incl = wave_inclusive_sum_u32(sum), excl = incl - sum;
     const bool here = excl < need && need <= incl;
-    uint32_t b = 0, acc = excl;
+    uint32_t b = 0, acc = excl, hb = h0;
     if (acc + h0 < need) {
       acc += h0;
       b = 1;
+      hb = h1;
       if (acc + h1 < need) {
         acc += h1;
         b = 2;
+        hb = h2;
         if (acc + h2 < need) {
           acc += h2;
           b = 3;
+          hb = h3;
         }
       }
     }
     const int w = __ffsll((long long)ballot(here)) - 1;
     const uint32_t digit = shfl_u32(4 * lane + b, w);
+    const uint32_t cnt = shfl_u32(hb, w);
     need = shfl_u32(need - acc, w);
     prefix |= (uint64_t)digit << shift;
-    mask |= 0xFFull << shift;
+    mask |= bm;
     wsync();
+    if (cnt == 1 && shift > 0) {  // one key left in the bucket: it is the k-th
+      uint64_t best = ~0ull;
+      for (uint32_t i = lane; i < n; i += kWave)
+        if (d.st[i] == state && (d.key[i] & mask) == prefix) best = d.key[i];
+      return wave_min_u64(best);
+    }
   }
   return prefix;
 }
@@ -295,36 +409,57 @@ __device__ uint64_t w_select_kth(DeepWave<CAP>& d, uint32_t lane, uint32_t n, ui
 template <uint32_t CAP>
 __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint32_t q, QRegs& Q,
                             uint64_t& tmin, uint32_t& tminlen) {
-  const uint32_t na = w_count(d, lane, n, kDeepLive);
-  const uint64_t T = na > c.qcap ? w_select_kth(d, lane, n, c.qcap, kDeepLive) : ~0ull;
+#if RSF_DEEP_PROF
+  uint64_t tt = __builtin_amdgcn_s_memtime();
+#define RSF_TH_T(k)                                                     \
+  do {                                                                  \
+    const uint64_t tn = __builtin_amdgcn_s_memtime();                   \
+    if (lane == 0) s_dprof[(k)] += (unsigned long long)(tn - tt); \
+    tt = tn;                                                            \
+  } while (0)
+#else
+#define RSF_TH_T(k) \
+  do {              \
+  } while (0)
+#endif
+  const WRange rg = w_range(d, lane, n, kDeepLive);
+  RSF_TH_T(20);
+  const uint64_t T = rg.cnt > c.qcap ? w_select_kth(d, lane, n, c.qcap, kDeepLive, rg) : ~0ull;
+  RSF_TH_T(21);
   uint32_t base = 0;
   uint64_t km = ~0ull;
   uint32_t lm = ~0u;
-  for (uint32_t b = 0; b < n; b += kWave) {
-    const uint32_t i = b + lane;
-    const bool live = i < n && d.st[i] == kDeepLive;
-    const uint64_t k = live ? d.key[i] : ~0ull;
-    const bool sel = live && k <= T;
-    const uint64_t m = ballot(sel);
-    if (sel) {
-      const uint32_t pos = base + mbcnt(m);
-      d.hkey[pos] = k;
-      d.hrid[pos] = d.rid[i];
-      d.hdec[pos] = d.dec[i];
-      d.st[i] = kDeepInHead;
-    } else if (live) {  // stays in the tail
-      km = k < km ? k : km;
-      lm = min(lm, key_len(k));
+  for (uint32_t b0 = 0; b0 < n; b0 += kDeepU * kWave) {
+    uint64_t x[kDeepU];
+    bool v[kDeepU];
+    w_chunk(d, lane, n, b0, kDeepLive, x, v);
+#pragma unroll
+    for (uint32_t u = 0; u < kDeepU; ++u) {
+      const uint32_t i = b0 + u * kWave + lane;
+      const bool sel = v[u] && x[u] <= T;
+      const uint64_t m = ballot(sel);
+      if (sel) {
+        const uint32_t pos = base + mbcnt(m);
+        d.hkey[pos] = x[u];
+        d.hrid[pos] = d.rid[i];
+        d.hdec[pos] = d.dec[i];
+        d.st[i] = kDeepInHead;
+      } else if (v[u]) {  // stays in the tail
+        km = x[u] < km ? x[u] : km;
+        lm = min(lm, key_len(x[u]));
+      }
+      base += (uint32_t)__popcll(m);
     }
-    base += (uint32_t)__popcll(m);
   }
   tmin = wave_min_u64(km);
   tminlen = wave_min_u32(lm);
   wsync();
+  RSF_TH_T(22);
   const uint32_t hn = base;
   const bool h = lane < hn;
   const uint64_t mk = h ? d.hkey[lane] : ~0ull;
   uint32_t rank = 0;
+#pragma unroll 8
   for (uint32_t j = 0; j < hn; ++j) rank += d.hkey[j] < mk ? 1u : 0u;
   const uint64_t hm = ballot(h);
   const uint32_t dest = h ? rank : hn + mbcnt(~hm);
@@ -336,6 +471,8 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
   Q.tl = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)tl);
   Q.dec = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)dc);
   wsync();
+  RSF_TH_T(23);
+#undef RSF_TH_T
 }
 
 // the live items not in the head back to the tail (compacted, any order); returns the count
@@ -381,6 +518,28 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
       oc = cnt_s + gs;
     }
   }
+#if RSF_DEEP_PROF
+  uint64_t pt = __builtin_amdgcn_s_memtime();
+  const uint64_t pt_start = pt;
+#define RSF_DEEP_T(k)                                                   \
+  do {                                                                  \
+    const uint64_t pn = __builtin_amdgcn_s_memtime();                   \
+    if (lane == 0) s_dprof[(k)] += (unsigned long long)(pn - pt); \
+    pt = pn;                                                            \
+  } while (0)
+#else
+#define RSF_DEEP_T(k) \
+  do {                \
+  } while (0)
+#endif
+  // lane q < 3: queue q's head non-empty (bit 0) and tail count (<< 1), read up front so empty
+  // queues cost no round trip and the tail loads start at once
+  uint32_t qinfo = 0;
+  if (lane < 3) {
+    const uint32_t r0 = s.q_rumor[(l * 3 + lane) * c.qcap];
+    const uint32_t tcq = tcap_of(c, lane) ? s.tsum[l * 3 + lane].x : 0u;
+    qinfo = (r0 != kEmpty ? 1u : 0u) | (tcq << 1);
+  }
   for (uint32_t i = lane; i < npend; i += kWave) d.pend[i] = s.p_ent[l * kPend + i];
   uint32_t* const ov = BKT ? bk.send : out_val;
   uint32_t* const od = BKT ? nullptr : out_dec;
@@ -388,6 +547,8 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
   for (uint32_t q = 0; q < 3; ++q) {
     const uint32_t nq = (pc >> (8 * q)) & 0xFF;
     const uint32_t qdec = q == 1 ? kDecQuery : kDecEvent;
+    const uint32_t qi = shfl_u32(qinfo, (int)q);
+    if (qi == 0 && nq == 0) continue;  // nothing in head, tail or pending list
     // every item of the queue into LDS: the head's live prefix, the tail, then the pending
     // re-queues in list order (transmits 0, the next seqs)
     QRegs Q{kEmpty, 0, 0};
@@ -400,15 +561,27 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
       d.dec[lane] = Q.dec;
       d.st[lane] = kDeepLive;
     }
-    const uint32_t tc = tcap_of(c, q) ? s.tsum[l * 3 + q].x : 0u;
+    const uint32_t tc = qi >> 1;
     if (tc) {
       const uint4* t = tail_of(s, q) + l * tstride_of(c, q);
-      for (uint32_t i = lane; i < tc; i += kWave) {
-        const uint4 e = t[i];
-        d.key[hn + i] = tlq_key(e.z & 0xFFFF, e.z >> 16, e.y);
-        d.rid[hn + i] = e.x;
-        d.dec[hn + i] = q == 0 ? e.w : qdec;
-        d.st[hn + i] = kDeepLive;
+      constexpr uint32_t U = 8;  // loads in flight per lane before the LDS stores
+      for (uint32_t b = 0; b < tc; b += U * kWave) {
+        uint4 e[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+          const uint32_t i = b + u * kWave + lane;
+          e[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+          const uint32_t i = b + u * kWave + lane;
+          if (i < tc) {
+            d.key[hn + i] = tlq_key(e[u].z & 0xFFFF, e[u].z >> 16, e[u].y);
+            d.rid[hn + i] = e[u].x;
+            d.dec[hn + i] = q == 0 ? e[u].w : qdec;
+            d.st[hn + i] = kDeepLive;
+          }
+        }
       }
     }
     uint32_t n = hn + tc;
@@ -433,10 +606,14 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
       n += nq;
       wsync();
     }
+#if RSF_DEEP_PROF
+    if (lane == 0) s_dprof[32 + min(n / 128u, 31u)] += 1ull;
+#endif
+    RSF_DEEP_T(8);
     // inserting into a bounded queue with no pick in between keeps its depth smallest keys
     const uint32_t depth = c.qcap + tcap_of(c, q);
     if (n > depth) {
-      const uint64_t T = w_select_kth(d, lane, n, depth, kDeepLive);
+      const uint64_t T = w_select_kth(d, lane, n, depth, kDeepLive, w_range(d, lane, n, kDeepLive));
       for (uint32_t i = lane; i < n; i += kWave)
         if (d.st[i] == kDeepLive && d.key[i] > T) d.st[i] = kDeepDead;
       drops += n - depth;
@@ -445,7 +622,9 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
     // the refill, then the head's own emission with the deep checks
     uint64_t tmin;
     uint32_t tminlen;
+    RSF_DEEP_T(9);
     w_take_head(c, d, lane, n, q, Q, tmin, tminlen);
+    RSF_DEEP_T(10);
     const uint32_t used_0 = used_v, nrec_0 = nrec_v;
     bool unsafe = false, dirty = false;
     uint32_t errq = 0;
@@ -455,12 +634,14 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
     else
       q_pick_peers<false, true>(c, Q, lane, np, used_v, nrec_v, off_v, ov, od, errq, dirty, d.row, nullptr, tmin,
                                 tminlen, &unsafe);
+    RSF_DEEP_T(11);
     if (!unsafe) {
       err |= errq;
       q_store(c, s, l, q, lane, Q, true);
       const uint32_t cnt = w_store_tail(c, s, l, q, d, lane, n);
       if (lane == 0 && tcap_of(c, q))
         s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
+      RSF_DEEP_T(12);
     } else {
       // the head still cannot decide: get_broadcasts over every item, peer by peer
       used_v = used_0;
@@ -513,11 +694,16 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
         nrec_v += lane == j ? k : 0u;
         wsync();
       }
+      RSF_DEEP_T(13);
       w_take_head(c, d, lane, n, q, Q, tmin, tminlen);
       q_store(c, s, l, q, lane, Q, true);
       const uint32_t cnt = w_store_tail(c, s, l, q, d, lane, n);
       if (lane == 0 && tcap_of(c, q))
         s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
+      RSF_DEEP_T(14);
+#if RSF_DEEP_PROF
+      if (lane == 0) s_dprof[15] += 1ull;
+#endif
     }
     for (uint32_t i = lane; i < n; i += kWave) d.st[i] = kDeepDead;  // clean for the next queue
     wsync();
@@ -535,6 +721,13 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
     }
     if (err) s.err[l] |= err;
   }
+#if RSF_DEEP_PROF
+  if (lane == 0) {
+    s_dprof[16] += 1ull;
+    s_dprof[17] += (unsigned long long)(__builtin_amdgcn_s_memtime() - pt_start);
+  }
+#endif
+#undef RSF_DEEP_T
 }
 
 // the members emit_run deferred: list 0 (those that fit kDeepSmall items per queue) from the
@@ -549,16 +742,23 @@ __global__ void __launch_bounds__(kWave) emit_deep_wave_kernel(GCfg c, GState s,
                                                               unsigned long long* __restrict__ total) {
   __shared__ DeepWave<CAP> d;
   const uint32_t lane = threadIdx.x;
+#if RSF_DEEP_PROF
+  s_dprof[lane] = 0;
+#endif
   const uint32_t n_list = s.deep_n[list];
   if (blockIdx.x == 0 && lane == 0 && n_list) atomicAdd(total, (unsigned long long)n_list);
   for (uint32_t i = lane; i < CAP; i += kWave) d.st[i] = kDeepDead;
   wsync();
   const uint64_t last = c.n_loc * 3 - 1;
   for (uint32_t it = blockIdx.x; it < n_list; it += gridDim.x) {
-    const uint64_t l = list ? s.deep_ids[last - it] : s.deep_ids[it];
+    const uint64_t l = list == 1 ? s.deep_ids[last - it] : s.deep_ids[(list == 2 ? c.n_loc : 0ull) + it];
     if (l >= c.n_loc) continue;  // wave-uniform
     deep_wave_member<BKT, CAP>(c, s, l, lane, grp_key, slot, cnt_s, out_val, out_dec, bk, d);
   }
+#if RSF_DEEP_PROF
+  wsync();
+  if (s_dprof[lane]) atomicAdd(&g_deep_prof[lane], s_dprof[lane]);
+#endif
 }
 
 // QueueChecker prune of deep queues listed by check_queues_kernel (entries l * 3 + q): keep the

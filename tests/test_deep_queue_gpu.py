@@ -3,7 +3,7 @@ HBM tail per queue, so a queue holds up to the reference's max_queue_depth (4096
 core/src/options.rs:512) and is pruned only by the QueueChecker (base.rs:720-760).  Bit-exact
 against the oracle's bounded queue of the same depth (oracle/oracle.c orc_queue_insert /
 orc_queue_get_broadcasts / orc_check_queues): emission decided from the head alone, the
-members whose picks need the tail (emit_deep_kernel), spills, the bounded prune at the full
+members whose picks need the tail (emit_deep_wave_kernel), spills, the bounded prune at the full
 depth, ring expiry of tail items, QueueChecker ticks, and the multi-GPU bucket emission."""
 import ctypes as C
 
@@ -154,7 +154,7 @@ def test_configs3_100k_deep_queues_bit_exact():
 
 
 def test_deep_two_shards_buckets_equal_one_context():
-    """The multi-GPU bucket emission with deep queues (emit_kernel and emit_deep_kernel writing
+    """The multi-GPU bucket emission with deep queues (emit_kernel and emit_deep_wave_kernel writing
     into the destination buckets): two shard contexts on one GPU, the exchange by hand,
     equal to one context after every round."""
     import torch
