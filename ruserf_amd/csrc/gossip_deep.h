@@ -494,15 +494,39 @@ __device__ uint32_t w_store_tail(const GCfg& c, const GState& s, uint64_t l, uin
   return base;
 }
 
+// A member's first round trip, issued while the wave still works on the member before it:
+// its pending count, its peers' group keys and slots (lane j < fanout), and per queue (lane
+// q < 3) the next seq, whether the head is non-empty (bit 0) and the tail count (<< 1), so
+// empty queues cost nothing and the tail loads start at once.
+struct DeepPre {
+  uint32_t pc, gk, gs, qinfo, qseq;
+};
+__device__ __forceinline__ DeepPre deep_pre(const GCfg& c, const GState& s, uint64_t l, uint32_t lane,
+                                            const uint32_t* __restrict__ grp_key,
+                                            const uint32_t* __restrict__ slot) {
+  DeepPre p{0u, kSentinel, 0u, 0u, 0u};
+  if (l >= c.n_loc) return p;
+  p.pc = s.p_cnt[l];
+  if (lane < c.fanout) {
+    p.gk = grp_key[l * c.fanout + lane];
+    p.gs = slot[l * c.fanout + lane];
+  }
+  if (lane < 3) {
+    p.qseq = s.q_next_seq[l * 3 + lane];
+    const uint32_t r0 = s.q_rumor[(l * 3 + lane) * c.qcap];
+    const uint32_t tcq = tcap_of(c, lane) ? s.tsum[l * 3 + lane].x : 0u;
+    p.qinfo = (r0 != kEmpty ? 1u : 0u) | (tcq << 1);
+  }
+  return p;
+}
+
 template <bool BKT, uint32_t CAP>
-__device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uint32_t lane,
-                                 const uint32_t* __restrict__ grp_key, const uint32_t* __restrict__ slot,
+__device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uint32_t lane, const DeepPre& pre,
                                  uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val,
                                  uint32_t* __restrict__ out_dec, const Buckets& bk, DeepWave<CAP>& d) {
-  const uint32_t pc = s.p_cnt[l], npend = pend_total(pc);
+  const uint32_t pc = pre.pc, npend = pend_total(pc);
   // the peers (a prefix of the fanout slots); lane j < np: peer j's record offset and count word
-  const uint32_t gk = lane < c.fanout ? grp_key[l * c.fanout + lane] : kSentinel;
-  const uint32_t gs = lane < c.fanout ? slot[l * c.fanout + lane] : 0u;
+  const uint32_t gk = pre.gk, gs = pre.gs;
   const uint32_t np = (uint32_t)__popcll(ballot(gk != kSentinel));
   uint64_t off_v = ~0ull;
   uint32_t* oc = nullptr;
@@ -532,14 +556,7 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
   do {                \
   } while (0)
 #endif
-  // lane q < 3: queue q's head non-empty (bit 0) and tail count (<< 1), read up front so empty
-  // queues cost no round trip and the tail loads start at once
-  uint32_t qinfo = 0;
-  if (lane < 3) {
-    const uint32_t r0 = s.q_rumor[(l * 3 + lane) * c.qcap];
-    const uint32_t tcq = tcap_of(c, lane) ? s.tsum[l * 3 + lane].x : 0u;
-    qinfo = (r0 != kEmpty ? 1u : 0u) | (tcq << 1);
-  }
+  const uint32_t qinfo = pre.qinfo, qseq = pre.qseq;
   for (uint32_t i = lane; i < npend; i += kWave) d.pend[i] = s.p_ent[l * kPend + i];
   uint32_t* const ov = BKT ? bk.send : out_val;
   uint32_t* const od = BKT ? nullptr : out_dec;
@@ -588,7 +605,7 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
     if (n == 0 && nq == 0) continue;
     wsync();
     if (nq) {
-      const uint32_t seq0 = s.q_next_seq[l * 3 + q];
+      const uint32_t seq0 = shfl_u32(qseq, (int)q);
       uint32_t rank0 = 0;
       for (uint32_t b = 0; b < kPend / kWave; ++b) {
         const uint32_t i = b * kWave + lane;
@@ -750,10 +767,22 @@ __global__ void __launch_bounds__(kWave) emit_deep_wave_kernel(GCfg c, GState s,
   for (uint32_t i = lane; i < CAP; i += kWave) d.st[i] = kDeepDead;
   wsync();
   const uint64_t last = c.n_loc * 3 - 1;
-  for (uint32_t it = blockIdx.x; it < n_list; it += gridDim.x) {
-    const uint64_t l = list == 1 ? s.deep_ids[last - it] : s.deep_ids[(list == 2 ? c.n_loc : 0ull) + it];
-    if (l >= c.n_loc) continue;  // wave-uniform
-    deep_wave_member<BKT, CAP>(c, s, l, lane, grp_key, slot, cnt_s, out_val, out_dec, bk, d);
+  const uint32_t* const ids = list == 1 ? s.deep_ids + last : s.deep_ids + (list == 2 ? c.n_loc : 0ull);
+  const int64_t dir = list == 1 ? -1 : 1;
+  // software pipeline over the wave's members: the next member's first round trip (deep_pre)
+  // and the id after it are read while this member is worked on
+  const uint32_t G = gridDim.x;
+  uint64_t l = blockIdx.x < n_list ? ids[dir * (int64_t)blockIdx.x] : ~0ull;
+  DeepPre pre = deep_pre(c, s, l, lane, grp_key, slot);
+  uint64_t l_next = blockIdx.x + G < n_list ? ids[dir * (int64_t)(blockIdx.x + G)] : ~0ull;
+  for (uint32_t it = blockIdx.x; it < n_list; it += G) {
+    const DeepPre pre_next = deep_pre(c, s, l_next, lane, grp_key, slot);
+    const uint32_t nn = it + 2 * G;
+    const uint64_t l_after = nn < n_list ? ids[dir * (int64_t)nn] : ~0ull;
+    if (l < c.n_loc) deep_wave_member<BKT, CAP>(c, s, l, lane, pre, cnt_s, out_val, out_dec, bk, d);  // wave-uniform
+    l = l_next;
+    pre = pre_next;
+    l_next = l_after;
   }
 #if RSF_DEEP_PROF
   wsync();
