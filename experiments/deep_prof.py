@@ -42,6 +42,9 @@ out = {"rounds": rounds - settle, "deferred_per_round": v[16] / (rounds - settle
        "why_per_round": {k: v[i] / (rounds - settle) for i, k in enumerate(why)},
        "cycles_per_member": v[17] / members,
        "phase_cycles_per_member": {k: v[8 + i] / members for i, k in enumerate(ph)},
+       "exact_key_split_per_round": {"crossing_pick_in_leading_run": v[24] / (rounds - settle),
+                                     "crossing_pick_is_later_fit": v[25] / (rounds - settle),
+                                     "no_tail_item_fits_before_it": v[26] / (rounds - settle)},
        "select_passes_per_select": v[18] / max(1, v[19]), "selects_per_member": v[19] / members,
        "take_head_cycles_per_member": {k: v[20 + i] / members for i, k in enumerate(["count", "select", "gather", "rank_permute"])},
        "queue_items_hist_by_128": {i * 128: v[32 + i] for i in range(32) if v[32 + i]}}

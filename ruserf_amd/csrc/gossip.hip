@@ -492,6 +492,19 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
     if (tlq_key(tl & 0xFFFF, tl >> 16, shfl_u32(Q.sq, hl)) >= tmin) {
       *unsafe = true;
       RSF_DEEP_WHY(5);
+#if RSF_DEEP_PROF
+      {  // diagnostic: is the first pick past the tail bound in the leading run (24) or a later
+         // fit (25); would "no tail item fits the budget left before it" have decided it (26)
+        const uint64_t below = ballot(live && tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq) < tmin);
+        const uint64_t cross = pick_m & ~below;
+        const int fc = __ffsll((long long)cross) - 1;
+        const uint64_t before = fc > 0 ? (~0ull >> (64 - fc)) : 0ull;
+        RSF_DEEP_WHY((pick_m & before) == before ? 24 : 25);
+        const uint32_t ub = wave_inclusive_sum_u32(lane_bit(pick_m & before) ? c.overhead + len : 0u);
+        const int32_t f0 = (int32_t)lim - (int32_t)shfl_u32(ub, 63) - (int32_t)c.overhead;
+        if (f0 < (int32_t)tminlen) RSF_DEEP_WHY(26);
+      }
+#endif
     }
   }
   if (DEEP && *unsafe) return used;
@@ -1332,7 +1345,7 @@ struct EmitIn {
   GState::PendE p0;  // pending entry `lane` (valid when lane < the member's count)
 #endif
 };
-template <bool DEEP = false>
+template <uint32_t DEEP = 0>
 __device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const uint32_t* __restrict__ grp_key,
                                           const uint32_t* __restrict__ slot, uint64_t l, uint32_t lane, EmitIn& e) {
   e.Q0 = QRegs{kEmpty, 0, 0};
@@ -1375,7 +1388,9 @@ __device__ __forceinline__ void bkt_group_keys(const Buckets& bk, uint32_t lane,
 // only if every pick was decided by the head alone (q_pick_peers' checks against the tails'
 // bounds) and every spill fits its tail -- otherwise nothing is stored (records written to the
 // group slots are rewritten) and the member is listed for emit_deep_wave_kernel.
-template <bool BKT, bool DEEP = false>
+// DEEP: bit q set = queue q may have a tail (1: the intent queue only, 7: all three); the
+// other queues' tail code is compiled away
+template <bool BKT, uint32_t DEEP = 0>
 __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_t l, uint32_t lane, EmitIn& e,
                                          uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val,
                                          uint32_t* __restrict__ out_dec, const Buckets& bk, QLds& row) {
@@ -1391,8 +1406,9 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   const uint32_t pc = shfl_u32(e.head, kEhPend), npend = pend_total(pc);
   if (RSF_BAD2(8, npend > kPend || ((pc >> 24) != 0), pc)) return;
   // deep queues: a queue is non-empty if its tail holds items too
-  const uint32_t tc0 = DEEP ? shfl_u32(e.ts.x, 0) : 0u, tc1 = DEEP ? shfl_u32(e.ts.x, 1) : 0u,
-                 tc2 = DEEP ? shfl_u32(e.ts.x, 2) : 0u;
+  constexpr bool D0 = DEEP & 1, D1 = DEEP & 2, D2 = DEEP & 4;
+  const uint32_t tc0 = D0 ? shfl_u32(e.ts.x, 0) : 0u, tc1 = D1 ? shfl_u32(e.ts.x, 1) : 0u,
+                 tc2 = D2 ? shfl_u32(e.ts.x, 2) : 0u;
   const bool ne0 = shfl_u32(Q0.r, 0) != kEmpty || (pc & 0xFF) || tc0,
              ne1 = shfl_u32(e.head, 1) != kEmpty || ((pc >> 8) & 0xFF) || tc1,
              ne2 = shfl_u32(e.head, 2) != kEmpty || ((pc >> 16) & 0xFF) || tc2;
@@ -1411,9 +1427,9 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
       x.minlen = shfl_u32(e.ts.y, q);
       x.minkey = ((uint64_t)shfl_u32(e.ts.w, q) << 32) | shfl_u32(e.ts.z, q);
     };
-    if (c.tcap0) get(sp0, 0);
-    if (c.tcap1) get(sp1, 1);
-    if (c.tcap2) get(sp2, 2);
+    if (D0 && c.tcap0) get(sp0, 0);
+    if (D1 && c.tcap1) get(sp1, 1);
+    if (D2 && c.tcap2) get(sp2, 2);
   }
   EPROF_T(t1);
   EPROF_ADD(0, t0, t1);
@@ -1452,23 +1468,23 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
     // applied first: in the reference they were queued when the messages arrived
     uint32_t& drops = drops_all;
     if (pc & 0xFF) {
-      if (DEEP && c.tcap0) pend_apply<true, true>(c, Q0, lane, 0, npend, pr, shfl_u32(e.head, kEhSeq), row, &sp0);
+      if (D0 && c.tcap0) pend_apply<true, true>(c, Q0, lane, 0, npend, pr, shfl_u32(e.head, kEhSeq), row, &sp0);
       else drops += pend_apply<true>(c, Q0, lane, 0, npend, pr, shfl_u32(e.head, kEhSeq), row);
       d0 = true;
     }
     if ((pc >> 8) & 0xFF) {
-      if (DEEP && c.tcap1) pend_apply<false, true>(c, Q1, lane, 1, npend, pr, shfl_u32(e.head, kEhSeq + 1), row, &sp1);
+      if (D1 && c.tcap1) pend_apply<false, true>(c, Q1, lane, 1, npend, pr, shfl_u32(e.head, kEhSeq + 1), row, &sp1);
       else drops += pend_apply<false>(c, Q1, lane, 1, npend, pr, shfl_u32(e.head, kEhSeq + 1), row);
       d1 = true;
     }
     if ((pc >> 16) & 0xFF) {
-      if (DEEP && c.tcap2) pend_apply<false, true>(c, Q2, lane, 2, npend, pr, shfl_u32(e.head, kEhSeq + 2), row, &sp2);
+      if (D2 && c.tcap2) pend_apply<false, true>(c, Q2, lane, 2, npend, pr, shfl_u32(e.head, kEhSeq + 2), row, &sp2);
       else drops += pend_apply<false>(c, Q2, lane, 2, npend, pr, shfl_u32(e.head, kEhSeq + 2), row);
       d2 = true;
     }
     if (drops) err |= kErrQueue;
     // a tail past its capacity needs the bounded queue's exact prune over head and tail
-    if (DEEP) unsafe = sp0.cnt > c.tcap0 || sp1.cnt > c.tcap1 || sp2.cnt > c.tcap2;
+    if (DEEP) unsafe = (D0 && sp0.cnt > c.tcap0) || (D1 && sp1.cnt > c.tcap1) || (D2 && sp2.cnt > c.tcap2);
     if (DEEP && unsafe) RSF_DEEP_WHY(6);
     // (the list's bookkeeping -- count, next seqs, prune count -- is written at the end: a store
     // here would make the compiler wait for it before reusing its registers)
@@ -1512,9 +1528,18 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
     if (DEEP) {
       // a tail's bounds (~0: empty) as of after the spills above
 #define RSF_TB(q) (sp##q.cnt ? sp##q.minkey : ~0ull), (sp##q.cnt ? sp##q.minlen : ~0u)
-      if (ne0 && !unsafe) q_pick_peers<true, true>(c, Q0, lane, np, used_v, nrec_v, off, ov, od, err, d0, row, ep, RSF_TB(0), &unsafe);
-      if (ne1 && !unsafe) q_pick_peers<false, true>(c, Q1, lane, np, used_v, nrec_v, off, ov, od, err, d1, row, nullptr, RSF_TB(1), &unsafe);
-      if (ne2 && !unsafe) q_pick_peers<false, true>(c, Q2, lane, np, used_v, nrec_v, off, ov, od, err, d2, row, nullptr, RSF_TB(2), &unsafe);
+      if (ne0 && !unsafe) {
+        if (D0) q_pick_peers<true, true>(c, Q0, lane, np, used_v, nrec_v, off, ov, od, err, d0, row, ep, RSF_TB(0), &unsafe);
+        else q_pick_peers<true>(c, Q0, lane, np, used_v, nrec_v, off, ov, od, err, d0, row, ep);
+      }
+      if (ne1 && !unsafe) {
+        if (D1) q_pick_peers<false, true>(c, Q1, lane, np, used_v, nrec_v, off, ov, od, err, d1, row, nullptr, RSF_TB(1), &unsafe);
+        else q_pick_peers<false>(c, Q1, lane, np, used_v, nrec_v, off, ov, od, err, d1, row);
+      }
+      if (ne2 && !unsafe) {
+        if (D2) q_pick_peers<false, true>(c, Q2, lane, np, used_v, nrec_v, off, ov, od, err, d2, row, nullptr, RSF_TB(2), &unsafe);
+        else q_pick_peers<false>(c, Q2, lane, np, used_v, nrec_v, off, ov, od, err, d2, row);
+      }
 #undef RSF_TB
       if (unsafe) {  // nothing committed: the whole-queue path redoes this member's emission
         // by the LDS capacity its largest queue needs: list 2 (kDeepTiny; from n_loc), list 0
@@ -1596,7 +1621,8 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   if (d2) q_store(c, s, l, 2, lane, Q2, true);
   if (DEEP) {  // the tails' new counts and bounds (their spilled items are written), lane q for queue q
     const bool l0 = lane == 0, l1 = lane == 1;
-    const uint32_t tc = l0 ? tc0 : l1 ? tc1 : tc2, tcap = l0 ? c.tcap0 : l1 ? c.tcap1 : c.tcap2;
+    const uint32_t tc = l0 ? tc0 : l1 ? tc1 : tc2;
+    const uint32_t tcap = l0 ? (D0 ? c.tcap0 : 0u) : l1 ? (D1 ? c.tcap1 : 0u) : (D2 ? c.tcap2 : 0u);
     const uint32_t cnt = l0 ? sp0.cnt : l1 ? sp1.cnt : sp2.cnt, mlen = l0 ? sp0.minlen : l1 ? sp1.minlen : sp2.minlen;
     const uint64_t mkey = l0 ? sp0.minkey : l1 ? sp1.minkey : sp2.minkey;
     if (lane < 3 && tcap && cnt != tc) s.tsum[l * 3 + lane] = make_uint4(cnt, mlen, (uint32_t)mkey, (uint32_t)(mkey >> 32));
@@ -1776,8 +1802,12 @@ __global__ void __launch_bounds__(64) emit4_kernel(GCfg c, GState s, const uint3
 
 // FULL: queue_cap == 64 (one slot per lane of the wave), known at compile time -- every
 // `lane < qcap` test and its branch fold away (the bench configuration)
-template <bool BKT, bool FULL, bool DEEP = false>
-__global__ void __launch_bounds__(64 * RSF_EMIT_WPB) emit_kernel(GCfg c_in, GState s, const uint32_t* __restrict__ grp_key,
+#ifndef RSF_EMIT_DEEP_WPE
+#define RSF_EMIT_DEEP_WPE 8  // deep emission: waves per SIMD the compiler must fit (SGPRs: 101 -> spill to lanes)
+#endif
+template <bool BKT, bool FULL, uint32_t DEEP = 0>
+__global__ void __launch_bounds__(64 * RSF_EMIT_WPB)
+    __attribute__((amdgpu_waves_per_eu(DEEP ? RSF_EMIT_DEEP_WPE : 1, 10))) emit_kernel(GCfg c_in, GState s, const uint32_t* __restrict__ grp_key,
                                                    const uint32_t* __restrict__ slot, uint32_t* __restrict__ cnt_s,
                                                    uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec,
                                                    Buckets bk) {
@@ -3538,12 +3568,20 @@ static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
                        g->grp_cnt, g->stage_val, g->stage_dec, bk);
   } else if (c.deep) {
     RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 16, st));
-    if (c.qcap == kWave)
-      hipLaunchKernelGGL((emit_kernel<BKT, true, true>), egrid, eb, 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt,
-                         g->stage_val, g->stage_dec, bk);
-    else
-      hipLaunchKernelGGL((emit_kernel<BKT, false, true>), egrid, eb, 0, st, c, g->s, g->grp_key, g->grp_slot,
-                         g->grp_cnt, g->stage_val, g->stage_dec, bk);
+    // only the intent queue deep (the common configuration): the other queues' tail code is
+    // compiled out of the emission
+    const bool q0_only = c.tcap1 == 0 && c.tcap2 == 0;
+#define RSF_EMIT_DEEP(FULL, M)                                                                                    \
+  hipLaunchKernelGGL((emit_kernel<BKT, FULL, M>), egrid, eb, 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt, \
+                     g->stage_val, g->stage_dec, bk)
+    if (c.qcap == kWave) {
+      if (q0_only) RSF_EMIT_DEEP(true, 1u);
+      else RSF_EMIT_DEEP(true, 7u);
+    } else {
+      if (q0_only) RSF_EMIT_DEEP(false, 1u);
+      else RSF_EMIT_DEEP(false, 7u);
+    }
+#undef RSF_EMIT_DEEP
     RSF_HIP(hipGetLastError());
     RSF_DBG_SYNC(st, "emit_kernel (deep)");
     if (kDeepTiny)
