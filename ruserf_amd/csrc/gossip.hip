@@ -1802,12 +1802,8 @@ __global__ void __launch_bounds__(64) emit4_kernel(GCfg c, GState s, const uint3
 
 // FULL: queue_cap == 64 (one slot per lane of the wave), known at compile time -- every
 // `lane < qcap` test and its branch fold away (the bench configuration)
-#ifndef RSF_EMIT_DEEP_WPE
-#define RSF_EMIT_DEEP_WPE 8  // deep emission: waves per SIMD the compiler must fit (SGPRs: 101 -> spill to lanes)
-#endif
 template <bool BKT, bool FULL, uint32_t DEEP = 0>
-__global__ void __launch_bounds__(64 * RSF_EMIT_WPB)
-    __attribute__((amdgpu_waves_per_eu(DEEP ? RSF_EMIT_DEEP_WPE : 1, 10))) emit_kernel(GCfg c_in, GState s, const uint32_t* __restrict__ grp_key,
+__global__ void __launch_bounds__(64 * RSF_EMIT_WPB) emit_kernel(GCfg c_in, GState s, const uint32_t* __restrict__ grp_key,
                                                    const uint32_t* __restrict__ slot, uint32_t* __restrict__ cnt_s,
                                                    uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec,
                                                    Buckets bk) {

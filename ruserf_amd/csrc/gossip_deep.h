@@ -557,7 +557,24 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
   } while (0)
 #endif
   const uint32_t qinfo = pre.qinfo, qseq = pre.qseq;
-  for (uint32_t i = lane; i < npend; i += kWave) d.pend[i] = s.p_ent[l * kPend + i];
+  // the pending entries (two per lane) into registers now, into LDS once the first queue's
+  // head and tail loads are in flight too: one round trip for all three
+  static_assert(kPend == 2 * kWave, "two pending entries per lane");
+  // (named scalars: a struct copy here is promoted to an LDS or scratch array)
+  uint32_t pr0 = 0, pd0 = 0, pl0 = 0, pr1 = 0, pd1 = 0, pl1 = 0;
+  if (lane < npend) {
+    const GState::PendE* e = s.p_ent + l * kPend + lane;
+    pr0 = e->rid;
+    pd0 = e->dec;
+    pl0 = e->lq;
+  }
+  if (kWave + lane < npend) {
+    const GState::PendE* e = s.p_ent + l * kPend + kWave + lane;
+    pr1 = e->rid;
+    pd1 = e->dec;
+    pl1 = e->lq;
+  }
+  bool pend_lds = false;
   uint32_t* const ov = BKT ? bk.send : out_val;
   uint32_t* const od = BKT ? nullptr : out_dec;
   uint32_t used_v = 0, nrec_v = 0, err = 0, drops = 0;
@@ -568,8 +585,26 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
     if (qi == 0 && nq == 0) continue;  // nothing in head, tail or pending list
     // every item of the queue into LDS: the head's live prefix, the tail, then the pending
     // re-queues in list order (transmits 0, the next seqs)
+    // issued together: the head, the tail's first kDeepU * 64 items; then the LDS writes
     QRegs Q{kEmpty, 0, 0};
     q_load(c, s, l, q, lane, Q);
+    const uint32_t tc = qi >> 1;
+    const uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
+    uint4 e[kDeepU];
+#pragma unroll
+    for (uint32_t u = 0; u < kDeepU; ++u) {
+      const uint32_t i = u * kWave + lane;
+      e[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
+    }
+    if (!pend_lds) {
+      d.pend[lane].rid = pr0;
+      d.pend[lane].dec = pd0;
+      d.pend[lane].lq = pl0;
+      d.pend[kWave + lane].rid = pr1;
+      d.pend[kWave + lane].dec = pd1;
+      d.pend[kWave + lane].lq = pl1;
+      pend_lds = true;
+    }
     const bool hl = lane < c.qcap && Q.r != kEmpty;
     const uint32_t hn = (uint32_t)__popcll(ballot(hl));
     if (hl) {
@@ -578,27 +613,23 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
       d.dec[lane] = Q.dec;
       d.st[lane] = kDeepLive;
     }
-    const uint32_t tc = qi >> 1;
-    if (tc) {
-      const uint4* t = tail_of(s, q) + l * tstride_of(c, q);
-      constexpr uint32_t U = 8;  // loads in flight per lane before the LDS stores
-      for (uint32_t b = 0; b < tc; b += U * kWave) {
-        uint4 e[U];
+    for (uint32_t b = 0;;) {
 #pragma unroll
-        for (uint32_t u = 0; u < U; ++u) {
-          const uint32_t i = b + u * kWave + lane;
-          e[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
+      for (uint32_t u = 0; u < kDeepU; ++u) {
+        const uint32_t i = b + u * kWave + lane;
+        if (i < tc) {
+          d.key[hn + i] = tlq_key(e[u].z & 0xFFFF, e[u].z >> 16, e[u].y);
+          d.rid[hn + i] = e[u].x;
+          d.dec[hn + i] = q == 0 ? e[u].w : qdec;
+          d.st[hn + i] = kDeepLive;
         }
+      }
+      b += kDeepU * kWave;
+      if (b >= tc) break;
 #pragma unroll
-        for (uint32_t u = 0; u < U; ++u) {
-          const uint32_t i = b + u * kWave + lane;
-          if (i < tc) {
-            d.key[hn + i] = tlq_key(e[u].z & 0xFFFF, e[u].z >> 16, e[u].y);
-            d.rid[hn + i] = e[u].x;
-            d.dec[hn + i] = q == 0 ? e[u].w : qdec;
-            d.st[hn + i] = kDeepLive;
-          }
-        }
+      for (uint32_t u = 0; u < kDeepU; ++u) {  // the next kDeepU * 64 (queues past 512 items)
+        const uint32_t i = b + u * kWave + lane;
+        e[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
       }
     }
     uint32_t n = hn + tc;
