@@ -835,8 +835,10 @@ __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, 
     // positions past the head are the largest keys, in order: they go to the tail, the one at
     // position qcap being the smallest of them
     const bool sn = ins && pos_n >= c.qcap, se = live && pos_e >= c.qcap;
+#if !RSF_DIAG_NO_SPILL_WRITE  // (timing diagnostic only: results differ without the writes)
     if (sn) sp->t[sp->cnt + (pos_n - c.qcap)] = make_uint4(rid, myseq, len << 16, DEC ? dec : 0u);
     if (se) sp->t[sp->cnt + (pos_e - c.qcap)] = make_uint4(Q.r, Q.sq, Q.tl, DEC ? Q.dec : 0u);
+#endif
     const uint64_t at_n = ballot(ins && pos_n == c.qcap), at_e = ballot(live && pos_e == c.qcap);
     const int w = __ffsll((long long)(at_n | at_e)) - 1;
     const uint32_t tl_w = at_n ? (shfl_u32(len, w) << 16) : shfl_u32(Q.tl, w);
@@ -1196,6 +1198,8 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
 // dead sender).  Sender l's records to its j-th peer form GROUP l*fanout + j.
 constexpr uint32_t kPeerBatch = 4;
 __global__ void __launch_bounds__(256) peers_kernel(GCfg c, GState s, uint32_t round, uint32_t* __restrict__ grp_key) {
+  // deep queues: the emission's deferred-member lists start empty (one launch fewer than a memset)
+  if (c.deep && blockIdx.x == 0 && threadIdx.x < 4) s.deep_n[threadIdx.x] = 0u;
   const uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= c.n_loc) return;
   const uint32_t m = (uint32_t)(c.lo + l);
@@ -1527,7 +1531,11 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
 #endif
     if (DEEP) {
       // a tail's bounds (~0: empty) as of after the spills above
+#if RSF_DIAG_NO_DEEP_CHECK  // (timing diagnostic only: picks not checked against the tails)
+#define RSF_TB(q) ~0ull, ~0u
+#else
 #define RSF_TB(q) (sp##q.cnt ? sp##q.minkey : ~0ull), (sp##q.cnt ? sp##q.minlen : ~0u)
+#endif
       if (ne0 && !unsafe) {
         if (D0) q_pick_peers<true, true>(c, Q0, lane, np, used_v, nrec_v, off, ov, od, err, d0, row, ep, RSF_TB(0), &unsafe);
         else q_pick_peers<true>(c, Q0, lane, np, used_v, nrec_v, off, ov, od, err, d0, row, ep);
@@ -3563,7 +3571,7 @@ static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
     hipLaunchKernelGGL(emit4_kernel<BKT>, dim3((unsigned)c.n_loc), dim3(kWave), 0, st, c, g->s, g->grp_key, g->grp_slot,
                        g->grp_cnt, g->stage_val, g->stage_dec, bk);
   } else if (c.deep) {
-    RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 16, st));
+    // (the deferred-member lists were emptied by peers_kernel)
     // only the intent queue deep (the common configuration): the other queues' tail code is
     // compiled out of the emission
     const bool q0_only = c.tcap1 == 0 && c.tcap2 == 0;
