@@ -1810,12 +1810,14 @@ __global__ void __launch_bounds__(64) emit4_kernel(GCfg c, GState s, const uint3
 
 // FULL: queue_cap == 64 (one slot per lane of the wave), known at compile time -- every
 // `lane < qcap` test and its branch fold away (the bench configuration)
-template <bool BKT, bool FULL, uint32_t DEEP = 0>
-__global__ void __launch_bounds__(64 * RSF_EMIT_WPB) emit_kernel(GCfg c_in, GState s, const uint32_t* __restrict__ grp_key,
-                                                   const uint32_t* __restrict__ slot, uint32_t* __restrict__ cnt_s,
-                                                   uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec,
-                                                   Buckets bk) {
-  GCfg c = c_in;
+#ifndef RSF_EMIT_DEEP_SGPR
+#define RSF_EMIT_DEEP_SGPR 0  // > 0: SGPR cap for the deep emission (occupancy 8 needs <= 96 with VCC)
+#endif
+template <bool BKT, bool FULL, uint32_t DEEP>
+__device__ __forceinline__ void emit_body(GCfg c, const GState& s, const uint32_t* __restrict__ grp_key,
+                                          const uint32_t* __restrict__ slot, uint32_t* __restrict__ cnt_s,
+                                          uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec,
+                                          const Buckets& bk) {
   if (FULL) c.qcap = kWave;
   __shared__ QLds rows[RSF_EMIT_WPB];
   const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -1834,6 +1836,25 @@ __global__ void __launch_bounds__(64 * RSF_EMIT_WPB) emit_kernel(GCfg c_in, GSta
     if (l + k < c.n_loc) emit_run<BKT, DEEP>(c, s, l + k, lane, cur, cnt_s, out_val, out_dec, bk, row);
     cur = nxt;
   }
+}
+template <bool BKT, bool FULL>
+__global__ void __launch_bounds__(64 * RSF_EMIT_WPB) emit_kernel(GCfg c, GState s, const uint32_t* __restrict__ grp_key,
+                                                                 const uint32_t* __restrict__ slot,
+                                                                 uint32_t* __restrict__ cnt_s,
+                                                                 uint32_t* __restrict__ out_val,
+                                                                 uint32_t* __restrict__ out_dec, Buckets bk) {
+  emit_body<BKT, FULL, 0>(c, s, grp_key, slot, cnt_s, out_val, out_dec, bk);
+}
+// deep queues (DEEP: the queues with a tail, bit q)
+template <bool BKT, bool FULL, uint32_t DEEP>
+__global__ void __launch_bounds__(64 * RSF_EMIT_WPB)
+#if RSF_EMIT_DEEP_SGPR
+    __attribute__((amdgpu_num_sgpr(RSF_EMIT_DEEP_SGPR)))
+#endif
+    emit_kernel_deep(GCfg c, GState s, const uint32_t* __restrict__ grp_key, const uint32_t* __restrict__ slot,
+                     uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec,
+                     Buckets bk) {
+  emit_body<BKT, FULL, DEEP>(c, s, grp_key, slot, cnt_s, out_val, out_dec, bk);
 }
 
 }  // namespace
@@ -3575,8 +3596,8 @@ static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
     // only the intent queue deep (the common configuration): the other queues' tail code is
     // compiled out of the emission
     const bool q0_only = c.tcap1 == 0 && c.tcap2 == 0;
-#define RSF_EMIT_DEEP(FULL, M)                                                                                    \
-  hipLaunchKernelGGL((emit_kernel<BKT, FULL, M>), egrid, eb, 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt, \
+#define RSF_EMIT_DEEP(FULL, M)                                                                                         \
+  hipLaunchKernelGGL((emit_kernel_deep<BKT, FULL, M>), egrid, eb, 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt, \
                      g->stage_val, g->stage_dec, bk)
     if (c.qcap == kWave) {
       if (q0_only) RSF_EMIT_DEEP(true, 1u);
