@@ -392,9 +392,13 @@ def main():
             # 64-slot queues (saturated: the flood fills every queue each round) and with the
             # reference's queue: 4096 deep (64-slot register head + HBM tail), settled, nothing
             # dropped between QueueChecker ticks
-            res["configs1_points"] = [configs1_point(args, rank, world, 64, None, args.warmup, args.steps),
-                                      configs1_point(args, rank, world, 64, None, args.warmup, args.steps,
-                                                     queue_depth=4096)]
+            pts = [configs1_point(args, rank, world, 64, None, args.warmup, args.steps),
+                   configs1_point(args, rank, world, 64, None, args.warmup, args.steps, queue_depth=4096)]
+            # the deep queues' emission cost against the 64-slot queues', same box, same call
+            e64 = pts[0]["phases_ms_per_round"].get("emit_kernel")
+            edeep = pts[1]["phases_ms_per_round"].get("emit_kernel")
+            pts[1]["emit_ms_vs_q64"] = (edeep / e64) if e64 and edeep else None
+            res["configs1_points"] = pts
         if not args.no_vivaldi:
             # the metric's second half, timed in the same invocation (configs[4]: 64M members)
             vargs = argparse.Namespace(**vars(args))

@@ -1811,7 +1811,7 @@ __global__ void __launch_bounds__(64) emit4_kernel(GCfg c, GState s, const uint3
 // FULL: queue_cap == 64 (one slot per lane of the wave), known at compile time -- every
 // `lane < qcap` test and its branch fold away (the bench configuration)
 #ifndef RSF_EMIT_DEEP_SGPR
-#define RSF_EMIT_DEEP_SGPR 0  // > 0: SGPR cap for the deep emission (occupancy 8 needs <= 96 with VCC)
+#define RSF_EMIT_DEEP_SGPR 94  // SGPR cap for the deep emission: occupancy 8 instead of 7 (11 SGPRs spilled to VGPR lanes; 1.45 -> 1.40 ms at 1M, same box x2); 0: none
 #endif
 template <bool BKT, bool FULL, uint32_t DEEP>
 __device__ __forceinline__ void emit_body(GCfg c, const GState& s, const uint32_t* __restrict__ grp_key,
