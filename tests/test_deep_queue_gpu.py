@@ -205,3 +205,31 @@ def test_deep_two_shards_buckets_equal_one_context():
     assert sum(e.deep_stats()[0] for e in shards) > 0
     for e in [one] + shards:
         e.close()
+
+
+def test_deep_long_queues_all_capacity_classes():
+    """Queues that grow past the deferred path's two smaller LDS capacities (832 and 1 216
+    items): a user-event flood (100 per round) that the retransmit limit retires far slower
+    than it arrives, an event buffer wide enough to accept every event, and a rumor ring that
+    does not wrap, so the event queues of every member grow by tens of items per round.  Members
+    deferred at every size class take emit_deep_wave_kernel<832>, <1216> and <4288>; bit-exact
+    against the oracle every round, with the largest queue past 1 216 items by the end."""
+    n, rounds = 300, 34
+    subj, acts, ml = W.churn_workload(n, rounds, churn=0.01, events_per_round=100, queries_per_round=0, seed=77)
+    s = len(subj)
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=64, queue_depth=(2500, 2500, 2500), gossip_limit=1000,
+                         gossip_overhead=2, retransmit_mult=4, max_rumors=1 << 13, event_buffer_size=4096,
+                         query_buffer_size=64, slot_k=16, max_refute=2)
+    g, w = pair(cfg, subj, W.initial_views(s))
+    deep0 = 0
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t], threads=16)
+        if t % 3 == 2 or t == rounds - 1:
+            same(g, w, f"round {t}")
+    assert H.world_width(w) > 1216  # queues past the two smaller capacity classes
+    total, _ = g.deep_stats()
+    assert total > deep0
+    assert int(g.pruned().sum()) == 0
+    g.close()
+    L.orc_world_free(C.byref(w))
