@@ -292,12 +292,12 @@ __device__ __forceinline__ void w_chunk(const DeepWave<CAP>& d, uint32_t lane, u
 
 // the items in state `state`: count, smallest and largest key, AND and OR of the keys
 struct WRange {
-  uint32_t cnt;
+  uint32_t cnt, cnt_t0;  // cnt_t0: those of transmits 0
   uint64_t lo, hi, an, orr;
 };
 template <uint32_t CAP>
 __device__ WRange w_range(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint8_t state) {
-  uint32_t cnt = 0;
+  uint32_t cnt = 0, c0 = 0;
   uint64_t lo = ~0ull, hi = 0, an = ~0ull, orr = 0;
   for (uint32_t b = 0; b < n; b += kDeepU * kWave) {
     uint64_t x[kDeepU];
@@ -307,6 +307,7 @@ __device__ WRange w_range(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uin
     for (uint32_t u = 0; u < kDeepU; ++u)
       if (v[u]) {
         cnt++;
+        c0 += (x[u] >> 48) == 0 ? 1u : 0u;
         lo = x[u] < lo ? x[u] : lo;
         hi = x[u] > hi ? x[u] : hi;
         an &= x[u];
@@ -315,6 +316,7 @@ __device__ WRange w_range(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uin
   }
   WRange r;
   r.cnt = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(cnt), 63);
+  r.cnt_t0 = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(c0), 63);
   r.lo = wave_min_u64(lo);
   r.hi = wave_max_u64(hi);
   r.an = wave_and_u64(an);
@@ -335,11 +337,15 @@ __device__ uint64_t w_select_kth(DeepWave<CAP>& d, uint32_t lane, uint32_t n, ui
   const uint64_t var = rg.an ^ rg.orr;  // the bits that differ between candidates
   uint64_t prefix = 0, mask = 0;
   uint32_t need = k;
+  // at least k items of transmits 0: the k-th is one of them (the transmit bytes need no pass)
+  const bool t0 = rg.cnt_t0 >= k;
+  if (t0) mask = 0xFFFFull << 48;
 #if RSF_DEEP_PROF
   if (lane == 0) s_dprof[19] += 1ull;
 #endif
   for (int shift = 56; shift >= 0; shift -= 8) {
     const uint64_t bm = 0xFFull << shift;
+    if (t0 && shift >= 48) continue;  // (prefix bytes 0)
     if (!(var & bm)) {  // every candidate has this byte
       prefix |= rg.an & bm;
       mask |= bm;
