@@ -233,3 +233,26 @@ def test_deep_long_queues_all_capacity_classes():
     assert int(g.pruned().sum()) == 0
     g.close()
     L.orc_world_free(C.byref(w))
+
+
+@pytest.mark.parametrize("qcap,depth", [(16, 100), (64, 130)])
+def test_deep_intent_only_prune_bit_exact(qcap, depth):
+    """Only the intent queue deep (queue_depth = (d, 0, 0): the lean variant of the smallest
+    deferred-path class serves it) and small enough to overflow: members whose deferred
+    emission must prune at the depth are passed on to the full-depth kernel.  The saturated
+    intent workload, bit-exact against the oracle after every round, drops counted."""
+    n, s, rounds = 4000, 1024, 14
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=qcap, queue_depth=(depth, 0, 0), gossip_limit=8 * 24,
+                         gossip_overhead=2, max_rumors=1 << 16, event_buffer_size=512, query_buffer_size=512,
+                         slot_k=1)
+    subj, acts, ml = W.intents_workload(n, s, rounds, rate=0.05, seed=5)
+    g, w = pair(cfg, subj, W.initial_views(s))
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t], threads=16)
+        same(g, w, f"round {t}")
+    assert int(g.pruned().sum()) > 0  # the depth was reached
+    total, _ = g.deep_stats()
+    assert total > 0
+    g.close()
+    L.orc_world_free(C.byref(w))
