@@ -551,11 +551,13 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
       const uint64_t m = ballot(sel);
       if (sel) {
         const uint32_t pos = base + mbcnt(m);
-        uint32_t pr, pd;
-        w_payload(d, t, q, hn0, tc0, i, pr, pd);
         d.hkey[pos] = x[u];
-        d.hrid[pos] = pr;
-        d.hdec[pos] = pd;
+        if constexpr (kLean<CAP>) {
+          d.hrid[pos] = i;  // (the item's index: its payload is fetched below, all at once)
+        } else {
+          d.hrid[pos] = d.rid[i];
+          d.hdec[pos] = d.dec[i];
+        }
         d.st[i] = kDeepInHead;
       } else if (v[u]) {  // stays in the tail
         km = x[u] < km ? x[u] : km;
@@ -567,6 +569,15 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
   tmin = wave_min_u64(km);
   tminlen = wave_min_u32(lm);
   wsync();
+  if constexpr (kLean<CAP>) {  // the head items' payloads, one round trip for the whole head
+    if (lane < base) {
+      uint32_t pr, pd;
+      w_payload(d, t, q, hn0, tc0, d.hrid[lane], pr, pd);
+      d.hrid[lane] = pr;
+      d.hdec[lane] = pd;
+    }
+    wsync();
+  }
   RSF_TH_T(22);
   const uint32_t hn = base;
   const bool h = lane < hn;
