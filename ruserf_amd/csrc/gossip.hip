@@ -3218,14 +3218,10 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
     g->merge_blocks = (unsigned)std::max(1, per_cu * cus);
     if (c.deep) {
       int dpc = 0, dpb = 0, dpk = 0, dpt = 1;
-      const bool lean = RSF_DEEP_LEAN && c.tcap1 == 0 && c.tcap2 == 0;  // (see emit_deep_wave_kernel's lean variant)
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpc, emit_deep_wave_kernel<false, kDeepSmall>, kWave, 0) !=
               hipSuccess ||
           (kDeepTiny && hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                            &dpt,
-                            lean ? emit_deep_wave_kernel<false, kDeepTiny ? kDeepTinyLean : kWave>
-                                 : emit_deep_wave_kernel<false, kDeepTiny ? kDeepTiny : kWave>,
-                            kWave, 0) != hipSuccess) ||
+                            &dpt, emit_deep_wave_kernel<false, kDeepTiny ? kDeepTiny : kWave>, kWave, 0) != hipSuccess) ||
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpb, emit_deep_wave_kernel<false, kDeepBig>, kWave, 0) !=
               hipSuccess ||
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpk, check_deep_kernel, kDeepThreads, 0) != hipSuccess)
@@ -3613,13 +3609,7 @@ static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
 #undef RSF_EMIT_DEEP
     RSF_HIP(hipGetLastError());
     RSF_DBG_SYNC(st, "emit_kernel (deep)");
-    // the smallest class first: its lean variant (intent queue the only deep one) passes members it
-    // cannot finish on to list 1, which the full-depth kernel takes last
-    if (kDeepTiny && q0_only && RSF_DEEP_LEAN)
-      hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepTiny ? kDeepTinyLean : kWave>), dim3(g->deep_blocks_tiny),
-                         dim3(kWave), 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec,
-                         bk, 2u, g->d_counters + 55);
-    else if (kDeepTiny)
+    if (kDeepTiny)
       hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepTiny ? kDeepTiny : kWave>), dim3(g->deep_blocks_tiny),
                          dim3(kWave), 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec,
                          bk, 2u, g->d_counters + 55);

@@ -232,63 +232,17 @@ __shared__ unsigned long long s_dprof[64];
 constexpr uint32_t kDeepBig = kDeepItems;
 constexpr uint8_t kDeepInHead = 3;
 
-// LEAN (the smallest class): an item's rumor id and decoration are not held in LDS but read
-// where the item came from -- the old head (hp_*), the tail in HBM (untouched until the store),
-// the pending list (pend, via pidx) -- and the tail is stored by moving only what changed
-// (w_store_lean); a member that needs the bounded prune or the per-pick fallback is passed on to
-// the full-depth kernel instead.  9 B per item instead of 17: 12 waves per CU instead of 8.
-#ifndef RSF_DEEP_LEAN
-#define RSF_DEEP_LEAN 1
-#endif
-// (the lean variant of the smallest class is told apart by its capacity, one item larger;
-// it serves configurations whose only deep queue is the intent queue, the first one a member's
-// emission handles, so a member can still be passed on before anything of it was stored)
-constexpr uint32_t kDeepTinyLean = kDeepTiny + 1;
-template <uint32_t CAP>
-constexpr bool kLean = RSF_DEEP_LEAN && kDeepTiny && CAP == kDeepTinyLean;
-constexpr uint32_t kLeanTgt = 256;  // the lean store's move targets (a tail loses <= 64 to the head)
 template <uint32_t CAP>
 struct DeepWave {
-  static constexpr uint32_t PCAP = kLean<CAP> ? 1 : CAP;  // payload arrays
-  static constexpr uint32_t LCAP = kLean<CAP> ? kWave : 1;
   uint64_t key[CAP];
-  uint32_t rid[PCAP], dec[PCAP];
+  uint32_t rid[CAP], dec[CAP];
   uint8_t st[CAP];
   GState::PendE pend[kPend];
   uint32_t hist[256];
   uint64_t hkey[kWave];
   uint32_t hrid[kWave], hdec[kWave];
   QLds row;  // q_pick_peers' re-rank scratch
-  // lean: the old head's payload, the pending items' list index, the store's move targets
-  uint32_t hp_rid[LCAP], hp_dec[LCAP];
-  uint8_t pidx[kLean<CAP> ? kPend : 1];
-  uint16_t tgt[kLean<CAP> ? kLeanTgt : 1];
 };
-
-// the rumor id and decoration of LDS item i (queue q; hn old head items, then tc tail items,
-// then the pending items)
-template <uint32_t CAP>
-__device__ __forceinline__ void w_payload(const DeepWave<CAP>& d, const uint4* t, uint32_t q, uint32_t hn,
-                                          uint32_t tc, uint32_t i, uint32_t& rid, uint32_t& dec) {
-  if constexpr (kLean<CAP>) {
-    const uint32_t qdec = q == 1 ? kDecQuery : kDecEvent;
-    if (i < hn) {
-      rid = d.hp_rid[i];
-      dec = d.hp_dec[i];
-    } else if (i < hn + tc) {
-      const uint4 e = t[i - hn];
-      rid = e.x;
-      dec = q == 0 ? e.w : qdec;
-    } else {
-      const GState::PendE& e = d.pend[d.pidx[i - hn - tc]];
-      rid = e.rid;
-      dec = q == 0 ? e.dec : qdec;
-    }
-  } else {
-    rid = d.rid[i];
-    dec = d.dec[i];
-  }
-}
 
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -456,70 +410,11 @@ __device__ uint64_t w_select_kth(DeepWave<CAP>& d, uint32_t lane, uint32_t n, ui
   return prefix;
 }
 
-// Lean store of the intent queue's tail (no prune, no per-pick fallback on this path, so tail
-// items are either still live at their place or went to the head): items entering the tail
-// (the old head's that left it, the pending ones) fill the holes the head's new items left,
-// the tail grows at its end or, when it shrinks, its last live items move into the remaining
-// holes.  Reads of moved items (positions >= the new count) never meet a write (< it).
-template <uint32_t CAP>
-__device__ void w_store_lean(const GCfg& c, const GState& s, uint64_t l, uint32_t q, DeepWave<CAP>& d, uint32_t lane,
-                             uint32_t n, uint32_t hn, uint32_t tc, uint64_t tmin, uint32_t tminlen) {
-  uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
-  uint32_t L = 0, I = 0;  // live items: from the tail, entering it
-  for (uint32_t b = 0; b < n; b += kWave) {
-    const uint32_t i = b + lane;
-    const bool live = i < n && d.st[i] == kDeepLive;
-    const bool from_t = i >= hn && i < hn + tc;
-    L += (uint32_t)__popcll(ballot(live && from_t));
-    I += (uint32_t)__popcll(ballot(live && !from_t));
-  }
-  const uint32_t N2 = L + I, span = max(tc, N2);
-  uint32_t T = 0;  // targets: positions < N2 without a live tail item, ascending
-  for (uint32_t b = 0; b < span; b += kWave) {
-    const uint32_t p = b + lane;
-    const bool tg = p < N2 && (p >= tc || d.st[hn + p] != kDeepLive);
-    const uint64_t m = ballot(tg);
-    if (tg) {
-      const uint32_t r = T + mbcnt(m);
-      if (r < kLeanTgt) d.tgt[r] = (uint16_t)p;
-    }
-    T += (uint32_t)__popcll(m);
-  }
-  wsync();
-  uint32_t r0 = 0;  // sources: the entering items, then the live tail items at positions >= N2
-  for (uint32_t b = 0; b < n; b += kWave) {
-    const uint32_t i = b + lane;
-    const bool src = i < n && d.st[i] == kDeepLive && !(i >= hn && i < hn + tc);
-    const uint64_t m = ballot(src);
-    if (src) {
-      const uint32_t r = r0 + mbcnt(m);
-      uint32_t pr, pd;
-      w_payload(d, t, q, hn, tc, i, pr, pd);
-      const uint64_t k = d.key[i];
-      if (r < kLeanTgt) t[d.tgt[r]] = make_uint4(pr, key_seq(k), key_tl(k), pd);
-    }
-    r0 += (uint32_t)__popcll(m);
-  }
-  for (uint32_t b = N2; b < tc; b += kWave) {
-    const uint32_t p = b + lane;
-    const bool src = p < tc && d.st[hn + p] == kDeepLive;
-    const uint64_t m = ballot(src);
-    if (src) {
-      const uint32_t r = r0 + mbcnt(m);
-      const uint4 e = t[p];
-      if (r < kLeanTgt) t[d.tgt[r]] = e;
-    }
-    r0 += (uint32_t)__popcll(m);
-  }
-  if (lane == 0) s.tsum[l * 3 + q] = N2 ? make_uint4(N2, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
-}
-
 // head = the qcap smallest live keys, sorted into the lanes of Q (marked kDeepInHead in LDS);
 // returns the bounds of the live items left (the tail): (min key, min length), ~0 if none
 template <uint32_t CAP>
 __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint32_t q, QRegs& Q,
-                            uint64_t& tmin, uint32_t& tminlen, const uint4* t = nullptr, uint32_t hn0 = 0,
-                            uint32_t tc0 = 0) {
+                            uint64_t& tmin, uint32_t& tminlen) {
 #if RSF_DEEP_PROF
   uint64_t tt = __builtin_amdgcn_s_memtime();
 #define RSF_TH_T(k)                                                     \
@@ -552,12 +447,8 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
       if (sel) {
         const uint32_t pos = base + mbcnt(m);
         d.hkey[pos] = x[u];
-        if constexpr (kLean<CAP>) {
-          d.hrid[pos] = i;  // (the item's index: its payload is fetched below, all at once)
-        } else {
-          d.hrid[pos] = d.rid[i];
-          d.hdec[pos] = d.dec[i];
-        }
+        d.hrid[pos] = d.rid[i];
+        d.hdec[pos] = d.dec[i];
         d.st[i] = kDeepInHead;
       } else if (v[u]) {  // stays in the tail
         km = x[u] < km ? x[u] : km;
@@ -569,15 +460,6 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
   tmin = wave_min_u64(km);
   tminlen = wave_min_u32(lm);
   wsync();
-  if constexpr (kLean<CAP>) {  // the head items' payloads, one round trip for the whole head
-    if (lane < base) {
-      uint32_t pr, pd;
-      w_payload(d, t, q, hn0, tc0, d.hrid[lane], pr, pd);
-      d.hrid[lane] = pr;
-      d.hdec[lane] = pd;
-    }
-    wsync();
-  }
   RSF_TH_T(22);
   const uint32_t hn = base;
   const bool h = lane < hn;
@@ -642,19 +524,6 @@ __device__ __forceinline__ DeepPre deep_pre(const GCfg& c, const GState& s, uint
     p.qinfo = (r0 != kEmpty ? 1u : 0u) | (tcq << 1);
   }
   return p;
-}
-
-// the lean path hands a member to the full-depth kernel (launched after it; list 1 from the
-// back of deep_ids) before anything of the member was stored; its LDS items are cleared
-template <uint32_t CAP>
-__device__ __forceinline__ void deep_pass_on(const GCfg& c, const GState& s, uint64_t l, uint32_t lane,
-                                             DeepWave<CAP>& d, uint32_t n) {
-  if (lane == 0) s.deep_ids[c.n_loc * 3 - 1 - atomicAdd(s.deep_n + 1, 1u)] = (uint32_t)l;
-  for (uint32_t i = lane; i < n; i += kWave) d.st[i] = kDeepDead;
-  wsync();
-#if RSF_DEEP_PROF
-  if (lane == 0) s_dprof[24 + 3] += 1ull;
-#endif
 }
 
 template <bool BKT, uint32_t CAP>
@@ -746,13 +615,8 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
     const uint32_t hn = (uint32_t)__popcll(ballot(hl));
     if (hl) {
       d.key[lane] = tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq);
-      if constexpr (kLean<CAP>) {
-        d.hp_rid[lane] = Q.r;
-        d.hp_dec[lane] = Q.dec;
-      } else {
-        d.rid[lane] = Q.r;
-        d.dec[lane] = Q.dec;
-      }
+      d.rid[lane] = Q.r;
+      d.dec[lane] = Q.dec;
       d.st[lane] = kDeepLive;
     }
     for (uint32_t b = 0;;) {
@@ -761,10 +625,8 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
         const uint32_t i = b + u * kWave + lane;
         if (i < tc) {
           d.key[hn + i] = tlq_key(e[u].z & 0xFFFF, e[u].z >> 16, e[u].y);
-          if constexpr (!kLean<CAP>) {
-            d.rid[hn + i] = e[u].x;
-            d.dec[hn + i] = q == 0 ? e[u].w : qdec;
-          }
+          d.rid[hn + i] = e[u].x;
+          d.dec[hn + i] = q == 0 ? e[u].w : qdec;
           d.st[hn + i] = kDeepLive;
         }
       }
@@ -789,12 +651,8 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
         if (in) {
           const uint32_t r = rank0 + mbcnt(m), j = n + r;
           d.key[j] = tlq_key(0, d.pend[i].lq & 0xFFFF, seq0 + r);
-          if constexpr (kLean<CAP>) {
-            d.pidx[r] = (uint8_t)i;
-          } else {
-            d.rid[j] = d.pend[i].rid;
-            d.dec[j] = q == 0 ? d.pend[i].dec : qdec;
-          }
+          d.rid[j] = d.pend[i].rid;
+          d.dec[j] = q == 0 ? d.pend[i].dec : qdec;
           d.st[j] = kDeepLive;
         }
         rank0 += (uint32_t)__popcll(m);
@@ -808,10 +666,6 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
     RSF_DEEP_T(8);
     // inserting into a bounded queue with no pick in between keeps its depth smallest keys
     const uint32_t depth = c.qcap + tcap_of(c, q);
-    if (kLean<CAP> && n > depth && tcap_of(c, q)) {  // (only queue 0 is deep here: nothing stored yet)
-      deep_pass_on(c, s, l, lane, d, n);
-      return;
-    }
     if (n > depth) {
       const uint64_t T = w_select_kth(d, lane, n, depth, kDeepLive, w_range(d, lane, n, kDeepLive));
       for (uint32_t i = lane; i < n; i += kWave)
@@ -823,7 +677,7 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
     uint64_t tmin;
     uint32_t tminlen;
     RSF_DEEP_T(9);
-    w_take_head(c, d, lane, n, q, Q, tmin, tminlen, tail_of(s, q) + l * tstride_of(c, q), hn, tc);
+    w_take_head(c, d, lane, n, q, Q, tmin, tminlen);
     RSF_DEEP_T(10);
     const uint32_t used_0 = used_v, nrec_0 = nrec_v;
     bool unsafe = false, dirty = false;
@@ -835,22 +689,14 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
       q_pick_peers<false, true>(c, Q, lane, np, used_v, nrec_v, off_v, ov, od, errq, dirty, d.row, nullptr, tmin,
                                 tminlen, &unsafe);
     RSF_DEEP_T(11);
-    if (kLean<CAP> && unsafe) {  // (the per-pick fallback: on the full-depth path)
-      deep_pass_on(c, s, l, lane, d, n);
-      return;
-    }
     if (!unsafe) {
       err |= errq;
       q_store(c, s, l, q, lane, Q, true);
-      if constexpr (kLean<CAP>) {
-        if (tcap_of(c, q)) w_store_lean(c, s, l, q, d, lane, n, hn, tc, tmin, tminlen);
-      } else {
-        const uint32_t cnt = w_store_tail(c, s, l, q, d, lane, n);
-        if (lane == 0 && tcap_of(c, q))
-          s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
-      }
+      const uint32_t cnt = w_store_tail(c, s, l, q, d, lane, n);
+      if (lane == 0 && tcap_of(c, q))
+        s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
       RSF_DEEP_T(12);
-    } else if constexpr (!kLean<CAP>) {
+    } else {
       // the head still cannot decide: get_broadcasts over every item, peer by peer
       used_v = used_0;
       nrec_v = nrec_0;
