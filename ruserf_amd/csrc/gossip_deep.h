@@ -330,10 +330,63 @@ __device__ WRange w_range(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uin
 // that agree with the first active lane's digit (the common case: one transmit class, few
 // lengths) are counted by that lane alone; the select stops as soon as the chosen bucket holds
 // one key.
+// Register variant for the smaller capacities (<= kDeepSmall items: <= 19 keys per lane): the
+// keys stay in registers and the k-th is built one VARYING bit at a time (the bits where the
+// candidates' AND and OR differ), each bit one compare + ballot popcount per key -- no LDS
+// histogram, no atomics.  Non-candidates hold ~0, which never matches a prefix: every
+// candidate key has bit 63 clear (transmits < 2^15), checked by the caller.
+#ifndef RSF_DEEP_SELECT_REG
+#define RSF_DEEP_SELECT_REG 1
+#endif
+template <uint32_t CAP>
+__device__ uint64_t w_select_kth_reg(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint32_t k, uint8_t state,
+                                     const WRange& rg) {
+  constexpr uint32_t R = (CAP + kWave - 1) / kWave;
+  uint64_t kr[R];
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t i = r * kWave + lane;
+    const uint32_t ii = i < n ? i : 0u;
+    const uint8_t st = d.st[ii];
+    const uint64_t x = d.key[ii];
+    kr[r] = (i < n && st == state) ? x : ~0ull;
+  }
+  const uint64_t var = rg.an ^ rg.orr;
+  uint64_t mask = ~var, prefix = rg.an & ~var;  // the bits every candidate shares
+  uint32_t need = k, match = rg.cnt;
+  uint64_t rem = var;
+  while (rem) {
+    const int b = 63 - __clzll((long long)rem);
+    rem &= ~(1ull << b);
+    const uint64_t mb = mask | (1ull << b);
+    uint32_t c0 = 0;  // candidates under the prefix with bit b clear
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) c0 += (uint32_t)__popcll(ballot((kr[r] & mb) == prefix));
+    mask = mb;
+    if (need <= c0) {
+      match = c0;
+    } else {
+      need -= c0;
+      match -= c0;
+      prefix |= 1ull << b;
+    }
+    if (match == 1 && rem) {  // one candidate left under the prefix: it is the k-th
+      uint64_t best = ~0ull;
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r) best = (kr[r] & mask) == prefix ? kr[r] : best;
+      return wave_min_u64(best);
+    }
+  }
+  return prefix;
+}
+
 template <uint32_t CAP>
 __device__ uint64_t w_select_kth(DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint32_t k, uint8_t state,
                                  const WRange& rg) {
   if (k <= 1 || rg.lo == rg.hi) return rg.lo;
+  if constexpr (RSF_DEEP_SELECT_REG && CAP <= kDeepSmall) {
+    if (!(rg.orr >> 63)) return w_select_kth_reg(d, lane, n, k, state, rg);
+  }
   const uint64_t var = rg.an ^ rg.orr;  // the bits that differ between candidates
   uint64_t prefix = 0, mask = 0;
   uint32_t need = k;
