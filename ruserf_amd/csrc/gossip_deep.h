@@ -338,19 +338,8 @@ __device__ WRange w_range(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uin
 #ifndef RSF_DEEP_SELECT_REG
 #define RSF_DEEP_SELECT_REG 1
 #endif
-template <uint32_t CAP>
-__device__ uint64_t w_select_kth_reg(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint32_t k, uint8_t state,
-                                     const WRange& rg) {
-  constexpr uint32_t R = (CAP + kWave - 1) / kWave;
-  uint64_t kr[R];
-#pragma unroll
-  for (uint32_t r = 0; r < R; ++r) {
-    const uint32_t i = r * kWave + lane;
-    const uint32_t ii = i < n ? i : 0u;
-    const uint8_t st = d.st[ii];
-    const uint64_t x = d.key[ii];
-    kr[r] = (i < n && st == state) ? x : ~0ull;
-  }
+template <uint32_t R>
+__device__ uint64_t w_select_kth_keys(const uint64_t (&kr)[R], uint32_t k, const WRange& rg) {
   const uint64_t var = rg.an ^ rg.orr;
   uint64_t mask = ~var, prefix = rg.an & ~var;  // the bits every candidate shares
   uint32_t need = k, match = rg.cnt;
@@ -380,12 +369,50 @@ __device__ uint64_t w_select_kth_reg(const DeepWave<CAP>& d, uint32_t lane, uint
   return prefix;
 }
 
+// the keys of LDS items lane, 64 + lane, ... in state `state` (~0 for the others) and their range
+template <uint32_t CAP, uint32_t R>
+__device__ __forceinline__ WRange w_keys(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint8_t state,
+                                         uint64_t (&kr)[R], uint32_t* vbits = nullptr) {
+  uint32_t cnt = 0, c0 = 0, vb = 0;
+  uint64_t lo = ~0ull, hi = 0, an = ~0ull, orr = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t i = r * kWave + lane;
+    const uint32_t ii = i < n ? i : 0u;
+    const uint8_t st = d.st[ii];
+    const uint64_t x = d.key[ii];
+    const bool v = i < n && st == state;
+    kr[r] = v ? x : ~0ull;
+    vb |= v ? 1u << r : 0u;
+    cnt += v ? 1u : 0u;
+    c0 += (v && (x >> 48) == 0) ? 1u : 0u;
+    lo = v && x < lo ? x : lo;
+    hi = v && x > hi ? x : hi;
+    an &= v ? x : ~0ull;
+    orr |= v ? x : 0ull;
+  }
+  WRange g;
+  g.cnt = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(cnt), 63);
+  g.cnt_t0 = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(c0), 63);
+  g.lo = wave_min_u64(lo);
+  g.hi = wave_max_u64(hi);
+  g.an = wave_and_u64(an);
+  g.orr = wave_or_u64(orr);
+  if (vbits) *vbits = vb;
+  return g;
+}
+
 template <uint32_t CAP>
 __device__ uint64_t w_select_kth(DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint32_t k, uint8_t state,
                                  const WRange& rg) {
   if (k <= 1 || rg.lo == rg.hi) return rg.lo;
   if constexpr (RSF_DEEP_SELECT_REG && CAP <= kDeepSmall) {
-    if (!(rg.orr >> 63)) return w_select_kth_reg(d, lane, n, k, state, rg);
+    if (!(rg.orr >> 63)) {
+      constexpr uint32_t R = (CAP + kWave - 1) / kWave;
+      uint64_t kr[R];
+      w_keys(d, lane, n, state, kr);
+      return w_select_kth_keys(kr, k, rg);
+    }
   }
   const uint64_t var = rg.an ^ rg.orr;  // the bits that differ between candidates
   uint64_t prefix = 0, mask = 0;
@@ -481,13 +508,44 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
   do {              \
   } while (0)
 #endif
+  uint32_t base = 0;
+  uint64_t km = ~0ull;
+  uint32_t lm = ~0u;
+  if constexpr (RSF_DEEP_SELECT_REG && CAP <= kDeepSmall) {
+    // the keys read once into registers: range, select and gather from them
+    constexpr uint32_t R = (CAP + kWave - 1) / kWave;
+    uint64_t kr[R];
+    uint32_t vb;
+    static_assert(R <= 32, "validity bits");
+    const WRange rg = w_keys(d, lane, n, kDeepLive, kr, &vb);
+    RSF_TH_T(20);
+    uint64_t T = ~0ull;
+    if (rg.cnt > c.qcap)
+      T = (rg.orr >> 63) ? w_select_kth(d, lane, n, c.qcap, kDeepLive, rg) : w_select_kth_keys(kr, c.qcap, rg);
+    RSF_TH_T(21);
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint32_t i = r * kWave + lane;
+      const bool v = (vb >> r) & 1u;
+      const bool sel = v && kr[r] <= T;
+      const uint64_t m = ballot(sel);
+      if (sel) {
+        const uint32_t pos = base + mbcnt(m);
+        d.hkey[pos] = kr[r];
+        d.hrid[pos] = d.rid[i];
+        d.hdec[pos] = d.dec[i];
+        d.st[i] = kDeepInHead;
+      } else if (v) {  // stays in the tail
+        km = kr[r] < km ? kr[r] : km;
+        lm = min(lm, key_len(kr[r]));
+      }
+      base += (uint32_t)__popcll(m);
+    }
+  } else {
   const WRange rg = w_range(d, lane, n, kDeepLive);
   RSF_TH_T(20);
   const uint64_t T = rg.cnt > c.qcap ? w_select_kth(d, lane, n, c.qcap, kDeepLive, rg) : ~0ull;
   RSF_TH_T(21);
-  uint32_t base = 0;
-  uint64_t km = ~0ull;
-  uint32_t lm = ~0u;
   for (uint32_t b0 = 0; b0 < n; b0 += kDeepU * kWave) {
     uint64_t x[kDeepU];
     bool v[kDeepU];
@@ -509,6 +567,7 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
       }
       base += (uint32_t)__popcll(m);
     }
+  }
   }
   tmin = wave_min_u64(km);
   tminlen = wave_min_u32(lm);
