@@ -338,9 +338,8 @@ __device__ WRange w_range(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uin
 #ifndef RSF_DEEP_SELECT_REG
 #define RSF_DEEP_SELECT_REG 1
 #endif
-// (rn: the registers that hold items, ceil(n / 64); the rest are skipped by uniform branches)
 template <uint32_t R>
-__device__ uint64_t w_select_kth_keys(const uint64_t (&kr)[R], uint32_t k, const WRange& rg, uint32_t rn = R) {
+__device__ uint64_t w_select_kth_keys(const uint64_t (&kr)[R], uint32_t k, const WRange& rg) {
   const uint64_t var = rg.an ^ rg.orr;
   uint64_t mask = ~var, prefix = rg.an & ~var;  // the bits every candidate shares
   uint32_t need = k, match = rg.cnt;
@@ -351,8 +350,7 @@ __device__ uint64_t w_select_kth_keys(const uint64_t (&kr)[R], uint32_t k, const
     const uint64_t mb = mask | (1ull << b);
     uint32_t c0 = 0;  // candidates under the prefix with bit b clear
 #pragma unroll
-    for (uint32_t r = 0; r < R; ++r)
-      if (r < rn) c0 += (uint32_t)__popcll(ballot((kr[r] & mb) == prefix));
+    for (uint32_t r = 0; r < R; ++r) c0 += (uint32_t)__popcll(ballot((kr[r] & mb) == prefix));
     mask = mb;
     if (need <= c0) {
       match = c0;
@@ -413,7 +411,7 @@ __device__ uint64_t w_select_kth(DeepWave<CAP>& d, uint32_t lane, uint32_t n, ui
       constexpr uint32_t R = (CAP + kWave - 1) / kWave;
       uint64_t kr[R];
       w_keys(d, lane, n, state, kr);
-      return w_select_kth_keys(kr, k, rg, (n + kWave - 1) / kWave);
+      return w_select_kth_keys(kr, k, rg);
     }
   }
   const uint64_t var = rg.an ^ rg.orr;  // the bits that differ between candidates
@@ -523,8 +521,7 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
     RSF_TH_T(20);
     uint64_t T = ~0ull;
     if (rg.cnt > c.qcap)
-      T = (rg.orr >> 63) ? w_select_kth(d, lane, n, c.qcap, kDeepLive, rg)
-                         : w_select_kth_keys(kr, c.qcap, rg, (n + kWave - 1) / kWave);
+      T = (rg.orr >> 63) ? w_select_kth(d, lane, n, c.qcap, kDeepLive, rg) : w_select_kth_keys(kr, c.qcap, rg);
     RSF_TH_T(21);
 #pragma unroll
     for (uint32_t r = 0; r < R; ++r) {
