@@ -835,9 +835,24 @@ __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, 
     // positions past the head are the largest keys, in order: they go to the tail, the one at
     // position qcap being the smallest of them
     const bool sn = ins && pos_n >= c.qcap, se = live && pos_e >= c.qcap;
+#ifndef RSF_SPILL_NT
+#define RSF_SPILL_NT 0  // 1: spills written with non-temporal stores (the tail is read again only by a refill)
+#endif
 #if !RSF_DIAG_NO_SPILL_WRITE  // (timing diagnostic only: results differ without the writes)
-    if (sn) sp->t[sp->cnt + (pos_n - c.qcap)] = make_uint4(rid, myseq, len << 16, DEC ? dec : 0u);
-    if (se) sp->t[sp->cnt + (pos_e - c.qcap)] = make_uint4(Q.r, Q.sq, Q.tl, DEC ? Q.dec : 0u);
+    if constexpr (RSF_SPILL_NT) {
+      typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+      if (sn) {
+        const u4v v = {rid, myseq, len << 16, DEC ? dec : 0u};
+        __builtin_nontemporal_store(v, reinterpret_cast<u4v*>(sp->t + sp->cnt + (pos_n - c.qcap)));
+      }
+      if (se) {
+        const u4v v = {Q.r, Q.sq, Q.tl, DEC ? Q.dec : 0u};
+        __builtin_nontemporal_store(v, reinterpret_cast<u4v*>(sp->t + sp->cnt + (pos_e - c.qcap)));
+      }
+    } else {
+      if (sn) sp->t[sp->cnt + (pos_n - c.qcap)] = make_uint4(rid, myseq, len << 16, DEC ? dec : 0u);
+      if (se) sp->t[sp->cnt + (pos_e - c.qcap)] = make_uint4(Q.r, Q.sq, Q.tl, DEC ? Q.dec : 0u);
+    }
 #endif
     const uint64_t at_n = ballot(ins && pos_n == c.qcap), at_e = ballot(live && pos_e == c.qcap);
     const int w = __ffsll((long long)(at_n | at_e)) - 1;
