@@ -703,8 +703,11 @@ __device__ __forceinline__ void st_s(double2* p, double2 x) {
     *p = x;
   }
 }
+#ifndef RSF_VIV_BLOCK
+#define RSF_VIV_BLOCK 256  // threads per block of the pipe kernel (each wave uses its own LDS rows)
+#endif
 template <int F, int FRT = filt_words(F)>
-__global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_pipe_kernel(
+__global__ void __launch_bounds__(RSF_VIV_BLOCK, RSF_VIV_WAVES) vivaldi_observe_pipe_kernel(
     const double* __restrict__ cur, double* __restrict__ nxt, double* __restrict__ adj_win,
     uint8_t* __restrict__ adj_idx, double* __restrict__ filt, unsigned long long* resets,
     const uint32_t* __restrict__ peer_in, const uint64_t* __restrict__ rtt_in, int32_t* __restrict__ status,
@@ -772,11 +775,11 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_pipe_kerne
     }
   }
 #if RSF_VIV_LDS1
-  __shared__ double2 stage[256 / 64][1][64 * 6];
+  __shared__ double2 stage[RSF_VIV_BLOCK / 64][1][64 * 6];
   double2* so = stage[threadIdx.x / 64][0];
   double2* sp = so;
 #else
-  __shared__ double2 stage[256 / 64][2][64 * 6];
+  __shared__ double2 stage[RSF_VIV_BLOCK / 64][2][64 * 6];
   double2* so = stage[threadIdx.x / 64][0];
   double2* sp = stage[threadIdx.x / 64][1];
 #endif
@@ -1445,7 +1448,9 @@ int rsf_vivaldi_observe(rsf_vivaldi* v, uint32_t slot, const uint32_t* peer, con
   const double* cur = v->table[v->cur];
   double* nxt = v->table[v->cur ^ 1];
   if (RSF_VIV_PIPE && p.dim == 8 && p.F <= 3 && p.W == 20 && p.stride == 12 && RSF_VIV_ROUND_WW == 20)
-    hipLaunchKernelGGL((vivaldi_observe_pipe_kernel<3>), dim3(blocks), dim3(256), 0, v->stream, cur, nxt, v->adj,
+    hipLaunchKernelGGL((vivaldi_observe_pipe_kernel<3>),
+                       dim3((unsigned)((p.shard_n + RSF_VIV_BLOCK - 1) / RSF_VIV_BLOCK)), dim3(RSF_VIV_BLOCK), 0,
+                       v->stream, cur, nxt, v->adj,
                        v->adj_idx, v->filt, v->resets, peer, rtt_ns, status_out, p, slot);
   else if (p.dim == 8 && p.F <= 3 && p.W == 20)
     hipLaunchKernelGGL((vivaldi_observe_kernel<8, 3, RSF_VIV_ROUND_WW>), dim3(blocks), dim3(256), 0, v->stream,
