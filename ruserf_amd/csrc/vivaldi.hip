@@ -704,7 +704,7 @@ __device__ __forceinline__ void st_s(double2* p, double2 x) {
   }
 }
 #ifndef RSF_VIV_BLOCK
-#define RSF_VIV_BLOCK 256  // threads per block of the pipe kernel (each wave uses its own LDS rows)
+#define RSF_VIV_BLOCK 128  // threads per block of the pipe kernel (each wave its own LDS rows); 128: 6.50-6.53 ms at 64M against 6.70 for 256, 6.52 for 64, 7.04 for 512 (same box x2)
 #endif
 template <int F, int FRT = filt_words(F)>
 __global__ void __launch_bounds__(RSF_VIV_BLOCK, RSF_VIV_WAVES) vivaldi_observe_pipe_kernel(
