@@ -32,7 +32,10 @@ using namespace rsf;
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kWavesPerBlock = 4;
+#ifndef RSF_WPB
+#define RSF_WPB 4  // waves per block of the merge and the other wave-per-member kernels
+#endif
+constexpr int kWavesPerBlock = RSF_WPB;
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;
 // record decoration (what merge_kernel needs to address the view entry before the rumor
 // body arrives): the subject slot of an intent, or the queue of a query / user event
