@@ -39,6 +39,17 @@ extern "C" {
 #define RSF_ERR_CODEC_TYPE (-11)   /* unknown MessageType tag, a kind this codec does not carry, or a bad PING_VERSION */
 #define RSF_ERR_CODEC_VARINT (-12) /* varint longer than 10 bytes / overflowing u64 */
 #define RSF_ERR_CODEC_LEN (-13)    /* length field the reference would panic on (< header) or dim > max */
+/* origination size limits (SerfError, core/src/error.rs:292-311): an action's status in
+ * rsf_gossip_action_status; the action did nothing (no clock moved, nothing delivered or queued) */
+#define RSF_ERR_USER_EVENT_LIMIT (-20)     /* UserEventLimitTooLarge: name + payload > max_user_event_size
+                                              (api.rs:258-262); also rsf_gossip_create with
+                                              max_user_event_size > 9 KiB (base.rs:69-70) */
+#define RSF_ERR_USER_EVENT_TOO_LARGE (-21) /* UserEventTooLarge: name + payload > USER_EVENT_SIZE_LIMIT
+                                              9 KiB (api.rs:264-266; serf.rs:42) */
+#define RSF_ERR_RAW_USER_EVENT_TOO_LARGE (-22) /* RawUserEventTooLarge: encoded length > max_user_event_size
+                                                  or > 9 KiB (api.rs:281-287) */
+#define RSF_ERR_QUERY_TOO_LARGE (-23)      /* QueryTooLarge: encoded query > query_size_limit (base.rs:919-921) */
+#define RSF_USER_EVENT_SIZE_LIMIT 9216     /* USER_EVENT_SIZE_LIMIT (core/src/serf.rs:42) */
 
 /* Last error message of the calling thread (static storage, never NULL). */
 const char* rsf_last_error(void);
@@ -269,7 +280,8 @@ typedef struct rsf_gossip_cfg {
   uint32_t max_rumors;         /* rumor ring capacity, a power of two: every round takes a block of
                                   n_subjects * max_refute + n_acts ids; a queue item whose slot has
                                   been recycled since expires at its member's next emission */
-  uint32_t _reserved;
+  uint32_t max_user_event_size; /* Options::max_user_event_size (0 = the default 512, options.rs:526);
+                                   > 9 KiB is RSF_ERR_USER_EVENT_LIMIT at create (base.rs:69-70) */
   uint64_t seed;               /* Philox key of peer selection */
   /* Deep queues: capacity of the intent / query / event queue (0 = queue_cap).  A depth above
    * queue_cap (which must then be <= 64) keeps the queue's first queue_cap slots as the
@@ -279,7 +291,8 @@ typedef struct rsf_gossip_cfg {
    * core/src/serf/base.rs:720-760): a depth no queue reaches between ticks is that queue exactly;
    * past it the bounded-queue prune applies (RSF_E_QUEUE_PRUNE, counted). */
   uint32_t queue_depth[3];
-  uint32_t _reserved2;
+  uint32_t query_size_limit;   /* Options::query_size_limit (0 = the default 1024, options.rs:519); at most
+                                  65534 (the model keeps a message's length in 16 bits) */
 } rsf_gossip_cfg;
 #define RSF_MAX_QUEUE_DEPTH 4160 /* head (<= 64) + tail: max_queue_depth 4096 plus a round's headroom */
 
@@ -297,8 +310,8 @@ typedef struct rsf_rumor {
 #define RSF_ACT_JOIN_SELF 1   /* Serf::join -> broadcast_join(clock.time()) (base.rs:396-412) */
 #define RSF_ACT_LEAVE_SELF 2  /* Serf::leave (api.rs:473-503) */
 #define RSF_ACT_FORCE_LEAVE 3 /* force_leave / remove_failed_node (base.rs:474-500) */
-#define RSF_ACT_USER_EVENT 4  /* Serf::user_event (api.rs:247-315) */
-#define RSF_ACT_QUERY 5       /* query_in (base.rs:869-953) */
+#define RSF_ACT_USER_EVENT 4  /* Serf::user_event (api.rs:247-315): size-checked first (RSF_ERR_USER_EVENT_*) */
+#define RSF_ACT_QUERY 5       /* query_in (base.rs:869-953): size-checked first (RSF_ERR_QUERY_TOO_LARGE) */
 typedef struct rsf_action {
   uint32_t member, act, subject, name_len, payload_len, flags;
   uint64_t key;
@@ -368,6 +381,17 @@ int rsf_gossip_apply_batch(rsf_gossip* g, const rsf_msg* msgs, uint64_t n, int32
  * actions of one round must name distinct members. */
 int rsf_gossip_round(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml, uint32_t n_ml,
                      const rsf_action* acts, uint32_t n_acts);
+/* The result of each action of the last rsf_gossip_round / rsf_gossip_round_begin (host,
+ * n <= that call's n_acts), what the reference's entry point returns: RSF_OK; RSF_SKIPPED
+ * (the member is not in this shard, or its process is down); or the size error of
+ * Serf::user_event (api.rs:255-287: the name + payload checks, then the encoded length,
+ * all before event_clock.increment, api.rs:301) / query_in (base.rs:919-921: the encoded
+ * length, before anything is queued), RSF_ERR_USER_EVENT_* / RSF_ERR_QUERY_TOO_LARGE.  A
+ * rejected action changes nothing: no clock, delivery, queue item or rumor entry (its id
+ * in the round's block stays unused).  The encoded length is the model's (msg_len, without
+ * the type byte), which depends on the clock's varint width, so the check runs on the
+ * device.  Synchronises. */
+int rsf_gossip_action_status(rsf_gossip* g, int32_t* status, uint32_t n);
 
 /* Multi-GPU split of rsf_gossip_round (one context per GPU, members sharded):
  *   begin : phases 1-3 for the shard; writes this round's rumor block, whose
@@ -537,8 +561,10 @@ int rsf_gossip_reconnect(rsf_gossip* g, uint32_t tick, uint32_t* target);
 
 /* ---- QueueChecker (core/src/serf/base.rs:703-760) ---------------------------
  * One checker tick over the three queues of every shard member: max =
- * max_queue_depth, or, when min_queue_depth > 0, max(2 * n_members, min_queue_depth)
- * (get_queue_max); a queue holding >= max items is pruned to max (memberlist
+ * max_queue_depth, or, when min_queue_depth > 0, max(2 * states.len(), min_queue_depth)
+ * per member (get_queue_max, base.rs:748-759; states.len() = the members that node knows:
+ * the N - S untracked ones, itself, its KNOWN subjects); a queue holding >= max items is
+ * pruned to max (memberlist
  * TransmitLimitedQueue::prune drops the last items in send order).  depth_warning
  * is the log threshold.  Host outputs (optional, 3 entries each, per queue
  * intent / query / event): items queued over the shard, members at or above the

@@ -567,6 +567,35 @@ uint32_t orc_msg_len(uint8_t type, uint64_t ltime, uint32_t name_len, uint32_t p
   }
 }
 
+/* Serf::user_event  api.rs:255-287: name + payload against max_user_event_size
+ * (UserEventLimitTooLarge), then USER_EVENT_SIZE_LIMIT (UserEventTooLarge); then the
+ * encoded length (message_encoded_len: the model's length without the type byte) against
+ * both (RawUserEventTooLarge) -- all before event_clock.increment (api.rs:301) */
+int32_t orc_user_event_check(uint32_t max_ue, uint64_t ltime, uint32_t name_len, uint32_t payload_len) {
+  uint64_t before = (uint64_t)name_len + payload_len;
+  if (before > max_ue) return ORC_E_UE_LIMIT;
+  if (before > ORC_USER_EVENT_SIZE_LIMIT) return ORC_E_UE_TOO_LARGE;
+  uint32_t len = orc_msg_len(ORC_MSG_USER_EVENT, ltime, name_len, payload_len) - 1;
+  if (len > max_ue) return ORC_E_UE_RAW;
+  if (len > ORC_USER_EVENT_SIZE_LIMIT) return ORC_E_UE_RAW;
+  return 0;
+}
+
+/* query_in  base.rs:916-921: the encoded query against query_size_limit (QueryTooLarge),
+ * before anything is registered or queued */
+int32_t orc_query_check(uint32_t limit, uint64_t ltime, uint32_t name_len, uint32_t payload_len) {
+  if ((uint64_t)name_len + payload_len > limit) return ORC_E_QUERY_TOO_LARGE; /* encoding holds both */
+  uint32_t len = orc_msg_len(ORC_MSG_QUERY, ltime, name_len, payload_len) - 1;
+  if (len > limit) return ORC_E_QUERY_TOO_LARGE;
+  return 0;
+}
+
+int orc_world_action_status(const orc_world* w, int32_t* out, uint32_t n) {
+  if (n > w->last_n_acts) return -1;
+  if (n) memcpy(out, w->act_status, (size_t)n * sizeof(int32_t));
+  return 0;
+}
+
 uint64_t orc_digest_mix(uint64_t d, uint64_t x) {
   d ^= x;
   d *= 0x100000001B3ull;
@@ -639,6 +668,12 @@ int orc_world_init(orc_world* w, const orc_world_cfg* c) {
     return -1;
   }
 #undef A
+  if (c->max_user_event_size > ORC_USER_EVENT_SIZE_LIMIT || c->query_size_limit > 0xFFFE) { /* base.rs:69-70 */
+    orc_world_free(w);
+    return -1;
+  }
+  w->max_ue = c->max_user_event_size ? c->max_user_event_size : 512;
+  w->query_limit = c->query_size_limit ? c->query_size_limit : 1024;
   for (int q = 0; q < 3; ++q) {
     if (c->qdepth[q] > c->qcap) {
       orc_world_free(w);
@@ -668,7 +703,7 @@ void orc_world_free(orc_world* w) {
                   w->refute_ltime, w->v_ltime, w->v_status, w->v_kind, w->q_rumor, w->q_seq,
                   w->q_tx, w->q_len, w->q_next_seq, w->eb_ltime, w->eb_cnt, w->eb_keys,
                   w->qb_ltime, w->qb_cnt, w->qb_ids, w->rumors, w->v_time, w->q_pruned, w->q_expired,
-                  w->dlog, w->dcnt, w->snap_bits, w->snap_sn, w->q_hwm};
+                  w->dlog, w->dcnt, w->snap_bits, w->snap_sn, w->q_hwm, w->act_status};
   for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) free(ptrs[i]);
   memset(w, 0, sizeof(*w));
 }
@@ -985,12 +1020,28 @@ uint32_t orc_queue_get_broadcasts(orc_world* w, uint32_t m, uint32_t q, uint32_t
   return cnt;
 }
 
+/* members.states.len() of member m (the map holds every member the node knows):
+ * the n - s untracked members (implicitly Alive; the local node is one of them unless
+ * it is a subject), the local node if it is a subject, and the tracked subjects whose
+ * entry is KNOWN (left / failed members stay in the map until reaped, base.rs:519-573) */
+uint64_t orc_states_len(const orc_world* w, uint32_t m) {
+  const size_t row = (size_t)m * w->s;
+  uint64_t known = (uint64_t)(w->n - w->s) + (w->member_subj[m] >= 0 ? 1u : 0u);
+  for (uint32_t subj = 0; subj < w->s; ++subj)
+    if ((int32_t)subj != w->member_subj[m] && w->v_kind[row + subj] == ORC_K_KNOWN) known++;
+  return known;
+}
+
 void orc_check_queues(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
                       uint64_t* stats) {
   uint64_t st[9] = {0};
-  uint64_t mx = max_queue_depth; /* get_queue_max  base.rs:748-759 */
-  if (min_queue_depth > 0) mx = 2ull * w->n > min_queue_depth ? 2ull * w->n : min_queue_depth;
-  for (uint32_t m = 0; m < w->n; ++m)
+  for (uint32_t m = 0; m < w->n; ++m) {
+    /* get_queue_max  base.rs:748-759: each node's checker reads its own members.states */
+    uint64_t mx = max_queue_depth;
+    if (min_queue_depth > 0) {
+      mx = 2ull * orc_states_len(w, m);
+      if (mx < min_queue_depth) mx = min_queue_depth;
+    }
     for (uint32_t q = 0; q < 3; ++q) {
       size_t base = ((size_t)m * 3 + q) * w->qcap;
       const uint32_t hwm = w->q_hwm[(size_t)m * 3 + q];
@@ -1017,6 +1068,7 @@ void orc_check_queues(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue
         st[6 + q]++;
       }
     }
+  }
   if (stats) memcpy(stats, st, sizeof(st));
 }
 
@@ -1248,10 +1300,26 @@ int orc_world_round_mt(orc_world* w, uint32_t round, const orc_ml_event* ml, uin
 
   /* 3. originations (api.rs / base.rs entry points) */
   uint32_t abase = base + w->s * w->max_refute;
+  if (n_acts > w->act_cap) {
+    int32_t* p = (int32_t*)realloc(w->act_status, (size_t)n_acts * sizeof(int32_t));
+    if (!p) return -1;
+    w->act_status = p;
+    w->act_cap = n_acts;
+  }
+  w->last_n_acts = n_acts;
   for (uint32_t a = 0; a < n_acts; ++a) {
     const orc_action* x = &acts[a];
     uint32_t m = x->member, rid = abase + a;
-    if (!w->alive[m]) continue;
+    if (!w->alive[m]) {
+      w->act_status[a] = ORC_SKIPPED;
+      continue;
+    }
+    /* the size checks return before anything moves (api.rs:255-287; base.rs:919-921) */
+    int32_t st = 0;
+    if (x->act == ORC_ACT_USER_EVENT) st = orc_user_event_check(w->max_ue, w->eclock[m], x->name_len, x->payload_len);
+    if (x->act == ORC_ACT_QUERY) st = orc_query_check(w->query_limit, w->qclock[m], x->name_len, x->payload_len);
+    w->act_status[a] = st;
+    if (st) continue;
     switch (x->act) {
       case ORC_ACT_JOIN_SELF: /* Serf::join -> broadcast_join(clock.time()) */
         w->serf_state[m] = ORC_SERF_ALIVE;
@@ -2186,11 +2254,10 @@ uint32_t orc_world_reconnect(orc_world* w, uint32_t tick, uint32_t* target) {
     /* members.states.len(): the n - s untracked members (implicitly Alive; the local node
      * is one of them unless it is a subject), the local node if it is a subject, and the
      * tracked subjects it knows */
-    uint64_t known = (uint64_t)(w->n - w->s) + (w->member_subj[m] >= 0 ? 1u : 0u);
+    const uint64_t known = orc_states_len(w, m);
     uint32_t failed = 0, left = 0;
     for (uint32_t subj = 0; subj < w->s; ++subj) {
       if ((int32_t)subj == w->member_subj[m] || w->v_kind[row + subj] != ORC_K_KNOWN) continue;
-      known++;
       failed += w->v_status[row + subj] == ORC_ST_FAILED;
       left += w->v_status[row + subj] == ORC_ST_LEFT;
     }

@@ -262,6 +262,11 @@ typedef struct {
    * deeper than any queue gets between ticks is exactly that (base.rs:720-760). */
   uint32_t qd[3];
   uint32_t* q_hwm; /* [n][3] slots [0, hwm) may be live, [hwm, qd) are free (scan bound) */
+  /* Options::max_user_event_size / query_size_limit (the origination size checks) */
+  uint32_t max_ue, query_limit;
+  /* the last round's per-action results (orc_world_action_status), act_cap entries */
+  int32_t* act_status;
+  uint32_t act_cap, last_n_acts;
 } orc_world;
 
 typedef struct {
@@ -269,6 +274,8 @@ typedef struct {
   uint32_t cap_rumors;
   uint64_t seed;
   uint32_t qdepth[3]; /* per-queue capacity (intent, query, event); 0 = qcap */
+  uint32_t max_user_event_size; /* Options::max_user_event_size, 0 = 512 (options.rs:526); > 9 KiB fails init */
+  uint32_t query_size_limit;    /* Options::query_size_limit, 0 = 1024 (options.rs:519) */
   uint32_t _pad;
 } orc_world_cfg;
 
@@ -306,14 +313,26 @@ uint32_t orc_queue_expire(orc_world* w, uint32_t m, uint32_t q);
 void orc_queue_insert(orc_world* w, uint32_t m, uint32_t q, uint32_t rumor);
 uint32_t orc_queue_get_broadcasts(orc_world* w, uint32_t m, uint32_t q, uint32_t limit,
                                   uint32_t* out, uint32_t max_out, uint32_t* bytes_used);
+/* members.states.len() of member m: the n - s untracked members, itself, its KNOWN subjects */
+uint64_t orc_states_len(const orc_world* w, uint32_t m);
 /* QueueChecker tick (core/src/serf/base.rs:703-760) over every member's queues: max =
- * max_queue_depth, or max(2n, min_queue_depth) when min_queue_depth > 0; a queue with
+ * max_queue_depth, or max(2 * states.len(), min_queue_depth) of that member when
+ * min_queue_depth > 0; a queue with
  * >= max items is pruned to max (the last items in send order).  stats[9] (optional):
  * per queue queued items, members at/above depth_warning, items pruned. */
 void orc_check_queues(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
                       uint64_t* stats);
 
 uint32_t orc_msg_len(uint8_t type, uint64_t ltime, uint32_t name_len, uint32_t payload_len);
+/* origination size checks: 0 or the status (include/ruserf_amd.h RSF_ERR_USER_EVENT_* = -20..-22,
+ * RSF_ERR_QUERY_TOO_LARGE = -23); ltime = the clock the message would carry */
+enum { ORC_E_UE_LIMIT = -20, ORC_E_UE_TOO_LARGE = -21, ORC_E_UE_RAW = -22, ORC_E_QUERY_TOO_LARGE = -23 };
+#define ORC_USER_EVENT_SIZE_LIMIT 9216u /* USER_EVENT_SIZE_LIMIT, core/src/serf.rs:42 */
+int32_t orc_user_event_check(uint32_t max_ue, uint64_t ltime, uint32_t name_len, uint32_t payload_len);
+int32_t orc_query_check(uint32_t limit, uint64_t ltime, uint32_t name_len, uint32_t payload_len);
+/* the last orc_world_round's action results (0 ok, 4 skipped: member down, or an ORC_E_* size
+ * error); n <= that round's n_acts; returns -1 otherwise */
+int orc_world_action_status(const orc_world* w, int32_t* out, uint32_t n);
 uint64_t orc_digest_mix(uint64_t d, uint64_t x);
 
 /* one origination (workload action) */

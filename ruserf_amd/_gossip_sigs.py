@@ -9,8 +9,8 @@ class RsfGossipCfg(C.Structure):
                 ("n_subjects", C.c_uint32), ("queue_cap", C.c_uint32), ("event_buffer_size", C.c_uint32),
                 ("query_buffer_size", C.c_uint32), ("slot_k", C.c_uint32), ("fanout", C.c_uint32),
                 ("gossip_limit", C.c_uint32), ("gossip_overhead", C.c_uint32), ("retransmit_mult", C.c_uint32),
-                ("max_refute", C.c_uint32), ("max_rumors", C.c_uint32), ("_reserved", C.c_uint32),
-                ("seed", C.c_uint64), ("queue_depth", C.c_uint32 * 3), ("_reserved2", C.c_uint32)]
+                ("max_refute", C.c_uint32), ("max_rumors", C.c_uint32), ("max_user_event_size", C.c_uint32),
+                ("seed", C.c_uint64), ("queue_depth", C.c_uint32 * 3), ("query_size_limit", C.c_uint32)]
 
 
 def declare(L):
@@ -58,6 +58,7 @@ def declare(L):
     sig("rsf_gossip_totals", [VP, P64])
     sig("rsf_gossip_push_pull", [VP, VP, C.c_uint64, C.c_uint32])
     sig("rsf_gossip_push_pull_device", [VP, VP, C.c_uint64, C.c_uint32])
+    sig("rsf_gossip_action_status", [VP, PI32, C.c_uint32])
     sig("rsf_gossip_check_queues", [VP, C.c_uint32, C.c_uint32, C.c_uint32, P64, P64, P64])
     sig("rsf_gossip_dump_pruned", [VP, P32, P32])
     sig("rsf_gossip_flush", [VP])

@@ -938,20 +938,16 @@ __device__ __forceinline__ uint32_t pend_apply(const GCfg& c, QRegs& Q, uint32_t
   return drops;
 }
 
-// Deep queues: while head + tail hold more than the queue's depth, drop the largest key of the
-// two (the head's is its last live lane; the tail's is found by a pass over it) -- the bounded
-// queue's prune, rare (a queue at its full depth).  One wave; returns the number dropped.
+// Deep queues: while the tail holds more than its capacity (head + tail over the queue's
+// depth), drop the largest key of the two -- the bounded queue's prune, rare (a queue at its
+// full depth).  That key is always in the tail: the tail only goes past its capacity by this
+// call's spills, and a spilled item is, by construction, at least every key left in the
+// head (the items whose sorted position among head and new items is >= queue_cap).  So one
+// pass over the tail finds it.  One wave; returns the number dropped.
 __device__ __forceinline__ uint32_t deep_prune_wave(const GCfg& c, QRegs& Q, uint32_t lane, uint32_t q, Spill& sp) {
+  (void)Q;
   uint32_t drops = 0;
   while (sp.cnt > tcap_of(c, q)) {
-    const uint64_t live_m = ballot(lane < c.qcap && Q.r != kEmpty);
-    uint64_t hk = 0;
-    int hl = -1;
-    if (live_m) {
-      hl = 63 - __clzll((long long)live_m);
-      const uint32_t tl = shfl_u32(Q.tl, hl);
-      hk = tlq_key(tl & 0xFFFF, tl >> 16, shfl_u32(Q.sq, hl));
-    }
     uint64_t tk = 0;
     uint32_t ti = 0;
     for (uint32_t b = 0; b < sp.cnt; b += kWave) {  // the tail holds items (cnt > tcap >= 1)
@@ -965,18 +961,10 @@ __device__ __forceinline__ uint32_t deep_prune_wave(const GCfg& c, QRegs& Q, uin
         ti = b + (uint32_t)(__ffsll((long long)at) - 1);
       }
     }
-    if (hl >= 0 && hk > tk) {
-      if ((int)lane == hl) {
-        Q.r = kEmpty;
-        Q.sq = 0;
-        Q.tl = 0;
-      }
-    } else {
-      const uint4 last = sp.t[sp.cnt - 1];
-      if (lane == 0) sp.t[ti] = last;
-      __threadfence_block();  // the next pass reads the moved item
-      sp.cnt--;
-    }
+    const uint4 last = sp.t[sp.cnt - 1];
+    if (lane == 0) sp.t[ti] = last;
+    __threadfence_block();  // the next pass reads the moved item
+    sp.cnt--;
     drops++;
   }
   return drops;
@@ -1138,15 +1126,30 @@ __global__ void __launch_bounds__(256) refute_kernel(GCfg c, GState s, uint32_t 
   store_regs(s, l, r);
 }
 
+// status[a] = the entry point's result (rsf_gossip_action_status): RSF_OK, RSF_SKIPPED (not
+// this shard's member, or its process is down), or a size-limit error, in which case the
+// action does nothing at all (the reference returns before any clock or queue moves).
 __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const rsf_action* __restrict__ acts,
-                                                        uint32_t n_acts, uint32_t abase) {
+                                                        uint32_t n_acts, uint32_t abase, int32_t* __restrict__ status) {
   uint32_t a = blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= n_acts) return;
   rsf_action x = acts[a];
   uint32_t m = x.member;
-  if (m < c.lo || m >= c.lo + c.n_loc || !s.alive[m]) return;
+  if (m < c.lo || m >= c.lo + c.n_loc || !s.alive[m]) {
+    status[a] = RSF_SKIPPED;
+    return;
+  }
   uint64_t l = m - c.lo;
   uint32_t rid = abase + a;
+  if (x.act == RSF_ACT_USER_EVENT || x.act == RSF_ACT_QUERY) {
+    const int32_t e = x.act == RSF_ACT_USER_EVENT
+                          ? user_event_size_check(c.max_ue, s.eclock[l], x.name_len, x.payload_len)
+                          : query_size_check(c.query_limit, s.qclock[l], x.name_len, x.payload_len);
+    status[a] = e;
+    if (e) return;
+  } else {
+    status[a] = RSF_OK;
+  }
   MRegs r;
   load_regs(s, l, r);
   if (RSF_BAD2(13, (x.act == RSF_ACT_JOIN_SELF || x.act == RSF_ACT_LEAVE_SELF) && (uint32_t)r.subj >= c.S, r.subj)) return;
@@ -2799,11 +2802,14 @@ __global__ void __launch_bounds__(256) seg_end_kernel(uint64_t n_loc, const uint
 // the warning depth, stats[6 + q] = pruned.
 // Deep queues: numq counts the tail too, and a queue to prune is listed (s.deep_ids) for
 // check_deep_kernel, which keeps the max smallest keys of head and tail.
+// qmax (non-null when min_queue_depth > 0): each member's own get_queue_max (queue_max_kernel).
 __global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uint32_t max_depth, uint32_t warn,
-                                                           unsigned long long* __restrict__ stats) {
+                                                           unsigned long long* __restrict__ stats,
+                                                           const uint32_t* __restrict__ qmax) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= c.n_loc * 3) return;
   const uint32_t q = (uint32_t)(t % 3);
+  if (qmax) max_depth = qmax[t / 3];
   const uint64_t base = t * c.qcap;
   uint32_t n = 0;
   while (n < c.qcap && s.q_rumor[base + n] != kEmpty) n++;
@@ -2821,6 +2827,29 @@ __global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uin
     }
     atomicAdd(stats + 6 + q, (unsigned long long)(n - max_depth));
   }
+}
+
+// get_queue_max with min_queue_depth > 0 (base.rs:748-759): max(2 * members.states.len(),
+// min_queue_depth), per member, since each node's checker reads its own member map.
+// states.len() is every member the node knows, as the Reconnector counts it
+// (reconnect_kernel): the N - S untracked members, the local node when it is a subject, and
+// the tracked subjects whose entry is KNOWN.  One wave per member; out[l] saturates at 2^32-1.
+__global__ void __launch_bounds__(256) queue_max_kernel(GCfg c, GState s, uint32_t min_depth,
+                                                        uint32_t* __restrict__ out) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint64_t l = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  if (l >= c.n_loc) return;
+  const int32_t own = s.member_subj[l];
+  const ViewE* row = s.view + l * c.S;
+  uint64_t known = (c.N - c.S) + (own >= 0 ? 1u : 0u);
+  for (uint32_t j0 = 0; j0 < c.S; j0 += kWave) {
+    const uint32_t j = j0 + lane;
+    const bool kn = j < c.S && (int32_t)j != own && vkind(row[j].meta) == RSF_KIND_KNOWN;
+    known += (uint32_t)__popcll(ballot(kn));
+  }
+  uint64_t mx = 2 * known;
+  if (mx < min_depth) mx = min_depth;
+  if (lane == 0) out[l] = (uint32_t)(mx < 0xFFFFFFFFull ? mx : 0xFFFFFFFFull);
 }
 
 // Generations alive: gen and gen - 1 (modulo the generation count, even so that the
@@ -2986,7 +3015,8 @@ struct rsf_gossip {
   // per-round device lists
   rsf_ml_event* d_ml = nullptr;
   rsf_action* d_acts = nullptr;
-  uint32_t cap_ml = 0, cap_acts = 0;
+  int32_t* d_act_status = nullptr;  // [cap_acts] originate_kernel's per-action result
+  uint32_t cap_ml = 0, cap_acts = 0, last_n_acts = 0;
   // the round's host lists go to the device from pinned staging (two slots, each reused
   // once the copy issued from it two rounds earlier has completed): a copy from pageable
   // memory would block the host until the stream drained, leaving the GPU idle while the
@@ -3020,6 +3050,7 @@ struct rsf_gossip {
   unsigned deep_check_blocks = 1;  // check_deep_kernel grid
   uint64_t deep_last = 0;     // rsf_gossip_deep_stats' previous total
   uint32_t* big_ids = nullptr;  // receivers deferred to merge_big_kernel (count: d_counters[52])
+  uint32_t* qmax = nullptr;     // [n_loc] per-member get_queue_max (rsf_gossip_check_queues, min_queue_depth > 0)
   // RSF_GUARD_ZONES (diagnostic builds): 0xA5-filled zones before and after big_ids and
   // stage_dec and after the sort's storage; rsf_gossip_debug_zones counts changed bytes
   char *big_base = nullptr, *dec_base = nullptr;
@@ -3076,9 +3107,13 @@ static int ensure_lists(rsf_gossip* g, uint32_t n_ml, uint32_t n_acts) {
   }
   if (n_acts > g->cap_acts) {
     hipFree(g->d_acts);
+    hipFree(g->d_act_status);
     g->d_acts = nullptr;
+    g->d_act_status = nullptr;
+    g->cap_acts = 0;
     uint32_t cap = std::max<uint32_t>(n_acts, 1024);
     if ((rc = dmalloc((void**)&g->d_acts, (size_t)cap * sizeof(rsf_action)))) return rc;
+    if ((rc = dmalloc((void**)&g->d_act_status, (size_t)cap * sizeof(int32_t)))) return rc;
     g->cap_acts = cap;
   }
   return RSF_OK;
@@ -3118,6 +3153,9 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   if (cfg->max_refute == 0 || cfg->max_refute > 4) return gerr("max_refute must be 1..4");
   if (cfg->max_rumors == 0 || (cfg->max_rumors & (cfg->max_rumors - 1)) || cfg->max_rumors > (1u << 30))
     return gerr("max_rumors must be a power of two <= 2^30 (the rumor ring)");
+  if (cfg->max_user_event_size > RSF_USER_EVENT_SIZE_LIMIT)  // Serf::new_in (base.rs:69-70)
+    return rsf::set_error(RSF_ERR_USER_EVENT_LIMIT, "max_user_event_size exceeds USER_EVENT_SIZE_LIMIT (9 KiB)");
+  if (cfg->query_size_limit > 0xFFFE) return gerr("query_size_limit must be <= 65534 (16-bit message lengths)");
   for (int q = 0; q < 3; ++q) {
     const uint32_t d = cfg->queue_depth[q];
     if (d && d < cfg->queue_cap) return gerr("queue_depth must be 0 or >= queue_cap");
@@ -3150,6 +3188,8 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
     c.tx_limit = cfg->retransmit_mult * d;
   }
   c.max_refute = cfg->max_refute;
+  c.max_ue = cfg->max_user_event_size ? cfg->max_user_event_size : 512u;  // options.rs:526
+  c.query_limit = cfg->query_size_limit ? cfg->query_size_limit : 1024u;  // options.rs:519
   uint32_t max_depth = c.qcap;
   {  // deep queues: the tail behind the register head
     uint32_t tc[3];
@@ -3315,7 +3355,8 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
                   g->grp_slot, g->grp_off, g->dec_base, s.dlog, s.dmeta, s.dcnt,
                   g->bkt_send, g->bkt_recv, g->bkt_dec, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn,
-                  s.p_ent, s.p_cnt, g->big_base, tail_of(s, 0), tail_of(s, 1), tail_of(s, 2), s.tsum, s.deep_ids};
+                  s.p_ent, s.p_cnt, g->big_base, tail_of(s, 0), tail_of(s, 1), tail_of(s, 2), s.tsum, s.deep_ids,
+                  g->qmax, g->d_act_status};
   for (void* p : ptrs)
     if (p) hipFree(p);
   g->scratch.release();
@@ -3569,9 +3610,10 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
   if (n_acts) {
     RSF_HIP(hipMemcpyAsync(g->d_acts, pin_acts, b_acts, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(originate_kernel, dim3(grid1(n_acts)), dim3(256), 0, st, c, g->s, g->d_acts, n_acts,
-                       g->round_abase);
+                       g->round_abase, g->d_act_status);
     RSF_DBG_SYNC(st, "originate_kernel");
   }
+  g->last_n_acts = n_acts;
   if (pin_k >= 0) {  // the slot is free again once the stream has passed this point
     RSF_HIP(hipEventRecord(g->pin_ev[pin_k], st));
     g->pin_used[pin_k] = true;
@@ -4176,21 +4218,27 @@ int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t mi
                             uint64_t* num_queued, uint64_t* n_warn, uint64_t* n_pruned) {
   if (!g) return gerr("null context");
   const GCfg& c = g->c;
-  // get_queue_max (base.rs:748-759): members.states.len() is every member the node knows
-  uint64_t mx = max_queue_depth;
-  if (min_queue_depth > 0) mx = std::max<uint64_t>(2 * c.N, min_queue_depth);
-  const uint32_t max_depth = (uint32_t)std::min<uint64_t>(mx, 0xFFFFFFFFull);
+  // get_queue_max (base.rs:748-759): max_queue_depth, or (min_queue_depth > 0) per member
+  // max(2 * members.states.len(), min_queue_depth) -- queue_max_kernel
+  const uint32_t max_depth = max_queue_depth;
   RSF_HIP(hipSetDevice(g->device));
   int rc = flush_pending(g);
   if (rc) return rc;
+  if (min_queue_depth > 0) {
+    if (!g->qmax && (rc = dmalloc((void**)&g->qmax, c.n_loc * 4))) return rc;
+    hipLaunchKernelGGL(queue_max_kernel, dim3(grid1(c.n_loc, 256 / kWave)), dim3(256), 0, g->stream, c, g->s,
+                       min_queue_depth, g->qmax);
+    RSF_HIP(hipGetLastError());
+  }
+  const uint32_t* qmax = min_queue_depth > 0 ? g->qmax : nullptr;
   RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, g->stream));
   if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 16, g->stream));
   hipLaunchKernelGGL(check_queues_kernel, dim3(grid1(c.n_loc * 3)), dim3(256), 0, g->stream, c, g->s, max_depth,
-                     depth_warning, g->d_counters + 40);
+                     depth_warning, g->d_counters + 40, qmax);
   RSF_HIP(hipGetLastError());
   if (c.deep) {  // the deep queues over the max: the smallest max keys of head and tail kept
     hipLaunchKernelGGL(check_deep_kernel, dim3(g->deep_check_blocks), dim3(kDeepThreads), 0, g->stream, c, g->s,
-                       max_depth);
+                       max_depth, qmax);
     RSF_HIP(hipGetLastError());
   }
   unsigned long long st[9];
@@ -4201,6 +4249,16 @@ int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t mi
     if (n_warn) n_warn[q] = st[3 + q];
     if (n_pruned) n_pruned[q] = st[6 + q];
   }
+  return RSF_OK;
+}
+
+int rsf_gossip_action_status(rsf_gossip* g, int32_t* status, uint32_t n) {
+  if (!g || (n && !status)) return gerr("null argument");
+  if (n > g->last_n_acts) return gerr("n exceeds the last round's action count");
+  if (!n) return RSF_OK;
+  RSF_HIP(hipSetDevice(g->device));
+  RSF_HIP(hipMemcpyAsync(status, g->d_act_status, (size_t)n * 4, hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
   return RSF_OK;
 }
 
@@ -4342,6 +4400,7 @@ int rsf_gossip_dump_view(rsf_gossip* g, uint64_t* ltime, uint8_t* status, uint8_
 }
 
 // head and tail merged on the host into [n_loc][3][D] in send order
+// every queue merged from head and tail (tail only on deep contexts), sorted, first D items
 static int dump_queues_deep(rsf_gossip* g, uint32_t D, uint32_t* rumor, uint32_t* seq, uint16_t* tx, uint16_t* len,
                             uint32_t* max_live) {
   const GCfg& c = g->c;
@@ -4354,7 +4413,8 @@ static int dump_queues_deep(rsf_gossip* g, uint32_t D, uint32_t* rumor, uint32_t
   RSF_HIP(hipMemcpyAsync(hr.data(), g->s.q_rumor, hc * 4, hipMemcpyDeviceToHost, st));
   RSF_HIP(hipMemcpyAsync(hs.data(), g->s.q_seq, hc * 4, hipMemcpyDeviceToHost, st));
   RSF_HIP(hipMemcpyAsync(ht.data(), g->s.q_txlen, hc * 4, hipMemcpyDeviceToHost, st));
-  RSF_HIP(hipMemcpyAsync(sum.data(), g->s.tsum, n * 3 * 16, hipMemcpyDeviceToHost, st));
+  // tails and their summaries exist only on deep contexts; otherwise every queue is its head
+  if (c.deep) RSF_HIP(hipMemcpyAsync(sum.data(), g->s.tsum, n * 3 * 16, hipMemcpyDeviceToHost, st));
   for (uint32_t q = 0; q < 3; ++q)
     if (tcap_of(c, q)) {
       tail[q].resize(n * tstride_of(c, q));

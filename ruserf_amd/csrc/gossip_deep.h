@@ -941,7 +941,8 @@ __global__ void __launch_bounds__(kWave) emit_deep_wave_kernel(GCfg c, GState s,
 
 // QueueChecker prune of deep queues listed by check_queues_kernel (entries l * 3 + q): keep the
 // max_depth smallest keys of head and tail
-__global__ void __launch_bounds__(kDeepThreads) check_deep_kernel(GCfg c, GState s, uint32_t max_depth) {
+__global__ void __launch_bounds__(kDeepThreads) check_deep_kernel(GCfg c, GState s, uint32_t max_depth,
+                                                                  const uint32_t* __restrict__ qmax) {
   __shared__ DeepLds d;
   const uint32_t n_list = *s.deep_n;
   for (uint32_t i = 0; i < kDeepItems; i += kDeepThreads)
@@ -953,7 +954,7 @@ __global__ void __launch_bounds__(kDeepThreads) check_deep_kernel(GCfg c, GState
     const uint32_t q = e % 3;
     if (l >= c.n_loc) continue;
     const uint32_t n = deep_load_queue(c, s, l, q, d);
-    deep_keep_smallest(d, n, max_depth);
+    deep_keep_smallest(d, n, qmax ? qmax[l] : max_depth);
     deep_store_queue(c, s, l, q, d, n);
     for (uint32_t i = threadIdx.x; i < n; i += kDeepThreads) d.st[i] = kDeepDead;
     __syncthreads();

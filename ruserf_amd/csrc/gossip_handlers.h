@@ -44,6 +44,7 @@ struct GCfg {
   // dynamic index of a private copy, which goes to scratch or LDS)
   uint32_t tcap0, tcap1, tcap2, tstride0, tstride1, tstride2;
   uint32_t deep;  // any tail
+  uint32_t max_ue, query_limit;  // Options::max_user_event_size / query_size_limit (origination checks)
 };
 
 // view entry: members.states[subject] (status, status_time) or recent_intents[subject]
@@ -186,6 +187,28 @@ RSF_HD uint32_t msg_len(uint8_t type, uint64_t ltime, uint32_t name_len, uint32_
     case RSF_MSG_QUERY: return base + 4 + 28 + 4 + 1 + 8 + (4 + name_len) + (4 + payload_len);
     default: return base;
   }
+}
+
+// Serf::user_event's size checks (api.rs:255-287), all before the event clock moves:
+// name + payload against max_user_event_size, then against USER_EVENT_SIZE_LIMIT, then the
+// encoded length (message_encoded_len: the model's length without the type byte) against
+// both.  0 or the SerfError's status.
+RSF_HD int32_t user_event_size_check(uint32_t max_ue, uint64_t ltime, uint32_t name_len, uint32_t payload_len) {
+  const uint64_t before = (uint64_t)name_len + payload_len;
+  if (before > max_ue) return RSF_ERR_USER_EVENT_LIMIT;
+  if (before > RSF_USER_EVENT_SIZE_LIMIT) return RSF_ERR_USER_EVENT_TOO_LARGE;
+  const uint32_t enc = msg_len(RSF_MSG_USER_EVENT, ltime, name_len, payload_len) - 1;
+  if (enc > max_ue || enc > RSF_USER_EVENT_SIZE_LIMIT) return RSF_ERR_RAW_USER_EVENT_TOO_LARGE;
+  return 0;
+}
+
+// query_in's size check (base.rs:916-921): the encoded query against query_size_limit.  The
+// encoding holds name and payload, so a sum past the limit is rejected before msg_len's
+// 32-bit arithmetic sees it.
+RSF_HD int32_t query_size_check(uint32_t limit, uint64_t ltime, uint32_t name_len, uint32_t payload_len) {
+  if ((uint64_t)name_len + payload_len > limit) return RSF_ERR_QUERY_TOO_LARGE;
+  const uint32_t enc = msg_len(RSF_MSG_QUERY, ltime, name_len, payload_len) - 1;
+  return enc > limit ? RSF_ERR_QUERY_TOO_LARGE : 0;
 }
 
 RSF_HD uint64_t tlq_key(uint32_t tx, uint32_t len, uint32_t seq) {
@@ -474,22 +497,17 @@ __device__ __forceinline__ void tail_append_serial(const GCfg& c, const GState& 
   const uint64_t nk = k < mk ? k : mk;
   s.tsum[l * 3 + q] = make_uint4(cnt + 1, min(sm.y, tl >> 16), (uint32_t)nk, (uint32_t)(nk >> 32));
 }
-// over the queue's depth: drop the largest key of head and tail (the head's is its last live
-// slot; the tail's bounds stay lower bounds); true if one was dropped
+// over the queue's depth: drop the largest key of head and tail; true if one was dropped.
+// That key is in the tail: the tail only exceeds its capacity right after an append, and
+// the appended item (the head's largest, or a new item past it) is at least every key left
+// in the head.  The tail's bounds stay lower bounds.
 __device__ __forceinline__ bool tail_prune_serial(const GCfg& c, const GState& s, uint64_t l, uint32_t q) {
   const uint4 sm = s.tsum[l * 3 + q];
   const uint32_t cnt = sm.x;
   if (cnt <= tcap_of(c, q)) return false;
   uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
-  const uint64_t base = (l * 3 + q) * c.qcap;
-  uint32_t hi = kEmpty, ti = 0;
-  uint64_t hk = 0, tk = 0;
-  for (uint32_t i = 0; i < c.qcap; ++i)
-    if (s.q_rumor[base + i] != kEmpty) {
-      hi = i;
-      const uint32_t x = s.q_txlen[base + i];
-      hk = tlq_key(x & 0xFFFF, x >> 16, s.q_seq[base + i]);
-    }
+  uint32_t ti = 0;
+  uint64_t tk = 0;
   for (uint32_t i = 0; i < cnt; ++i) {
     const uint4 e = t[i];
     const uint64_t x = tlq_key(e.z & 0xFFFF, e.z >> 16, e.y);
@@ -498,14 +516,8 @@ __device__ __forceinline__ bool tail_prune_serial(const GCfg& c, const GState& s
       ti = i;
     }
   }
-  if (hi != kEmpty && hk > tk) {
-    s.q_rumor[base + hi] = kEmpty;
-    s.q_seq[base + hi] = 0;
-    s.q_txlen[base + hi] = 0;
-  } else {
-    t[ti] = t[cnt - 1];
-    s.tsum[l * 3 + q] = make_uint4(cnt - 1, sm.y, sm.z, sm.w);
-  }
+  t[ti] = t[cnt - 1];
+  s.tsum[l * 3 + q] = make_uint4(cnt - 1, sm.y, sm.z, sm.w);
   return true;
 }
 

@@ -183,10 +183,14 @@ class VivaldiTableRefresh:
         self.stride = clients.table_ptr()[1]
         self.stage = None
         # The gather and the copies below run on torch's current stream: the context's observe
-        # kernels must run on that same stream, or the gather could read or overwrite table rows
-        # observe is still writing (the context defaults to its own non-blocking stream).
+        # kernels must be ordered against it, or the gather could read or overwrite table rows
+        # observe is still writing (the context defaults to its own non-blocking stream).  The
+        # context is bound to the current stream here; after_round() orders the refresh against
+        # the bound stream with stream waits whenever the caller's current stream differs.
+        self._bound = None
         if torch.cuda.is_available():
-            clients.set_stream(torch.cuda.current_stream().cuda_stream)
+            self._bound = torch.cuda.current_stream().cuda_stream
+            clients.set_stream(self._bound)
 
     def _table(self, ptr):
         t = hbm_tensor(ptr, self.g.n * self.stride, "<f8")
@@ -199,6 +203,17 @@ class VivaldiTableRefresh:
         other one of the pair after the swap)."""
         if self.world == 1 or (r + 1) % self.R:
             return
+        ctx = None
+        if self._bound is not None and torch.cuda.current_stream().cuda_stream != self._bound:
+            # the caller moved to another stream: wait for the context's observe, and make the
+            # context's next kernels wait for this refresh
+            ctx = torch.cuda.ExternalStream(self._bound)
+            torch.cuda.current_stream().wait_stream(ctx)
+        self._refresh(read_ptr)
+        if ctx is not None:
+            ctx.wait_stream(torch.cuda.current_stream())
+
+    def _refresh(self, read_ptr):
         ptr, _ = self.g.table_ptr()
         full = self._table(ptr)
         lo, hi = self.lo * self.stride, self.hi * self.stride

@@ -39,6 +39,27 @@ E_EVSLOT, E_QSLOT, E_REFUTE, E_STAGE, E_QUEUE_PRUNE = 1, 2, 4, 8, 16
 MAX_QUEUE_DEPTH, MIN_QUEUE_DEPTH, QUEUE_DEPTH_WARNING = 4096, 0, 128
 ACT_JOIN_SELF, ACT_LEAVE_SELF, ACT_FORCE_LEAVE, ACT_USER_EVENT, ACT_QUERY = 1, 2, 3, 4, 5
 ML_JOIN, ML_LEAVE, ML_UPDATE = 1, 2, 3
+# an origination's result (GossipEngine.action_status): ok, skipped (not this shard's member,
+# or its process is down), or the SerfError of the entry point's size checks
+# (core/src/error.rs:292-311; api.rs:255-287, base.rs:919-921)
+ACT_OK, ACT_SKIPPED = 0, 4
+ERR_USER_EVENT_LIMIT, ERR_USER_EVENT_TOO_LARGE, ERR_RAW_USER_EVENT_TOO_LARGE, ERR_QUERY_TOO_LARGE = -20, -21, -22, -23
+USER_EVENT_SIZE_LIMIT = 9 * 1024  # core/src/serf.rs:42
+
+
+def serf_error_text(status, cfg, size=None):
+    """The reference's Display text of an origination error (SerfError, error.rs:294-311).
+    `size` is the value the reference formats into the message where it is not a limit
+    (the encoded length of RawUserEventTooLarge / QueryTooLarge), if the caller has it."""
+    if status == ERR_USER_EVENT_LIMIT:
+        return f"ruserf: user event exceeds configured limit of {cfg.max_user_event_size} bytes before encoding"
+    if status == ERR_USER_EVENT_TOO_LARGE:
+        return f"ruserf: user event exceeds sane limit of {USER_EVENT_SIZE_LIMIT} bytes before encoding"
+    if status == ERR_RAW_USER_EVENT_TOO_LARGE:
+        return f"ruserf: user event exceeds sane limit of {size} bytes after encoding"
+    if status == ERR_QUERY_TOO_LARGE:
+        return f"ruserf: query exceeds limit of {size} bytes"
+    return None
 PP_JOIN, PP_EVENT_JOIN_IGNORE = 1, 2
 
 ACTION_DTYPE = np.dtype([("member", "<u4"), ("act", "<u4"), ("subject", "<u4"), ("name_len", "<u4"),
@@ -77,6 +98,10 @@ class GossipConfig:
     # (<= 64) the queue is a register head of queue_cap slots plus an HBM tail (reference
     # max_queue_depth 4096, pruned only by the QueueChecker)
     queue_depth: tuple = None
+    # Options::max_user_event_size / query_size_limit (options.rs:519, 526): the origination
+    # size checks of Serf::user_event / query_in (api.rs:255-287, base.rs:919-921)
+    max_user_event_size: int = 512
+    query_size_limit: int = 1024
 
     def depths(self):
         d = self.queue_depth or (0, 0, 0)
@@ -89,7 +114,8 @@ class GossipConfig:
                          query_buffer_size=self.query_buffer_size, slot_k=self.slot_k, fanout=self.fanout,
                          gossip_limit=self.gossip_limit, gossip_overhead=self.gossip_overhead,
                          retransmit_mult=self.retransmit_mult, max_refute=self.max_refute,
-                         max_rumors=self.max_rumors, seed=self.seed)
+                         max_rumors=self.max_rumors, seed=self.seed,
+                         max_user_event_size=self.max_user_event_size, query_size_limit=self.query_size_limit)
         c.queue_depth[:] = [int(x) for x in (self.queue_depth or (0, 0, 0))]
         return c
 
@@ -180,11 +206,21 @@ class GossipEngine:
         ml = np.ascontiguousarray(ml if ml is not None else np.zeros(0, ML_DTYPE), dtype=ML_DTYPE)
         acts = np.ascontiguousarray(acts if acts is not None else np.zeros(0, ACTION_DTYPE), dtype=ACTION_DTYPE)
         check(lib().rsf_gossip_round(self._h, t, _p(ml), len(ml), _p(acts), len(acts)))
+        self._n_acts = len(acts)
+
+    def action_status(self):
+        """Each action of the last round / round_begin: ACT_OK, ACT_SKIPPED, or an ERR_* size
+        error (the action then changed nothing).  Synchronises."""
+        n = getattr(self, "_n_acts", 0)
+        out = np.zeros(n, dtype=np.int32)
+        check(lib().rsf_gossip_action_status(self._h, ptr(out, C.c_int32) if n else None, n))
+        return out
 
     def round_begin(self, t, ml=None, acts=None):
         ml = np.ascontiguousarray(ml if ml is not None else np.zeros(0, ML_DTYPE), dtype=ML_DTYPE)
         acts = np.ascontiguousarray(acts if acts is not None else np.zeros(0, ACTION_DTYPE), dtype=ACTION_DTYPE)
         check(lib().rsf_gossip_round_begin(self._h, t, _p(ml), len(ml), _p(acts), len(acts)))
+        self._n_acts = len(acts)
 
     def rumor_block(self):
         p = C.c_void_p()

@@ -62,12 +62,15 @@ def intents_workload(n, s, rounds, rate=0.01, seed=0x5EED5EED, prune_frac=0.1):
 
 
 def churn_workload(n, rounds, churn=0.01, events_per_round=100, queries_per_round=10, names=16,
-                   seed=0x5EED5EED, prune_frac=0.25):
+                   seed=0x5EED5EED, prune_frac=0.25, oversize=0.0):
     """configs[3]: S = churn*n subjects; each fails (memberlist NotifyLeave ->
     Failed, then a force_leave two rounds later, a fraction `prune_frac` of them
     with prune) or leaves gracefully (Serf::leave, then NotifyLeave three rounds
     later) at a random round; plus per round a user-event flood (16 names, 32-byte
-    payloads, cc 50%) and queries."""
+    payloads, cc 50%) and queries.  oversize > 0: that fraction of the events and
+    queries get sizes around the default limits (events: name 1..64 + payload 420..560
+    bytes against max_user_event_size 512; queries: payload 940..1040 against
+    query_size_limit 1024), so some are rejected by the entry points' size checks."""
     rng = np.random.Generator(np.random.Philox(seed))
     s = max(1, int(round(n * churn)))
     subj_member = subjects_for(n, s)
@@ -103,10 +106,16 @@ def churn_workload(n, rounds, churn=0.01, events_per_round=100, queries_per_roun
             rows.append((m, ACT_FORCE_LEAVE, subj, 0, 0, int(pruned[subj]), 0))
         for m in ev:
             name = int(rng.integers(0, names))
-            rows.append((m, ACT_USER_EVENT, 0, 8, 32, int(rng.integers(0, 2)), (name << 32) | payload_id))
+            nl, pl = 8, 32
+            if oversize and rng.random() < oversize:
+                nl, pl = int(rng.integers(1, 65)), int(rng.integers(420, 561))
+            rows.append((m, ACT_USER_EVENT, 0, nl, pl, int(rng.integers(0, 2)), (name << 32) | payload_id))
             payload_id += 1
         for m in qs:
-            rows.append((m, ACT_QUERY, 0, 8, 16, 0, int(rng.integers(0, 1 << 32))))
+            nl, pl = 8, 16
+            if oversize and rng.random() < oversize:
+                nl, pl = 8, int(rng.integers(940, 1041))
+            rows.append((m, ACT_QUERY, 0, nl, pl, 0, int(rng.integers(0, 1 << 32))))
         a = np.array(rows, dtype=ACTION_DTYPE) if rows else np.zeros(0, ACTION_DTYPE)
         a = a[np.argsort(a["member"], kind="stable")]
         acts_all.append(a)

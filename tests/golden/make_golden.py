@@ -192,6 +192,25 @@ def main():
                 "ref": "core/src/coalesce/user.rs:125-200",
                 "events": [["foo", 1, ""], ["foo", 2, ""], ["bar", 2, "test1"], ["bar", 2, "test2"]],
                 "expect_flushed": [["foo", 2, ""], ["bar", 2, "test1"], ["bar", 2, "test2"]]},
+            # origination size limits: Serf::user_event (core/src/serf/api.rs:255-287) and
+            # query_in (core/src/serf/base.rs:916-921) against Options' defaults
+            # (core/src/options.rs:519, 526; test_config leaves both at the default,
+            # core/src/serf/base/tests.rs:27-41)
+            "max_user_event_size": {"ref": "core/src/options.rs:526", "value": 512},
+            "query_size_limit": {"ref": "core/src/options.rs:519", "value": 1024},
+            "user_event_size_limit_const": {"ref": "core/src/serf.rs:42", "value": 9 * 1024},
+            "serf_event_user_size_limit": {
+                "ref": "core/src/serf/base/tests/serf/event.rs:506-525",
+                "name": "this is too large an event", "payload_len": "max_user_event_size",
+                "expect_error_contains": "user event exceeds"},
+            "serf_query_size_limit": {
+                "ref": "core/src/serf/base/tests/serf/event.rs:1070-1085",
+                "name": "this is too large a query", "payload_len": "query_size_limit",
+                "query_size_limit_factor": 1, "expect_error_contains": "query exceeds limit of"},
+            "serf_query_size_limit_increased": {
+                "ref": "core/src/serf/base/tests/serf/event.rs:1087-1100",
+                "name": "this is too large a query", "payload_len": "query_size_limit",
+                "query_size_limit_factor": 2, "expect_ok": True},
         },
     }
     out = os.path.join(HERE, "reference_kats.json")

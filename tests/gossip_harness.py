@@ -20,7 +20,9 @@ def oracle_world(cfg, subj_member, views):
     wc = O.WorldCfg(n=cfg.n_members, s=cfg.n_subjects, qcap=max(qd), ebuf=cfg.event_buffer_size,
                     qbuf=cfg.query_buffer_size, slot_k=cfg.slot_k, fanout=cfg.fanout, limit=cfg.gossip_limit,
                     overhead=cfg.gossip_overhead, retransmit_mult=cfg.retransmit_mult, max_refute=cfg.max_refute,
-                    cap_rumors=cfg.max_rumors, seed=cfg.seed)
+                    cap_rumors=cfg.max_rumors, seed=cfg.seed,
+                    max_user_event_size=getattr(cfg, "max_user_event_size", 512),
+                    query_size_limit=getattr(cfg, "query_size_limit", 1024))
     wc.qdepth[:] = qd
     w = O.World()
     assert L.orc_world_init(C.byref(w), C.byref(wc)) == 0

@@ -86,7 +86,8 @@ class World(C.Structure):
                 ("v_time", P32), ("now", C.c_uint32), ("q_pruned", P32), ("q_expired", P32),
                 ("gen", C.c_uint32), ("rbits", C.c_uint32), ("dlog", P64), ("dcnt", P32), ("dcap", C.c_uint32),
                 ("snap_bits", P32), ("snap_w", C.c_uint32), ("snap_rejoin", C.c_int32), ("snap_sn", P64),
-                ("qd", C.c_uint32 * 3), ("q_hwm", P32)]
+                ("qd", C.c_uint32 * 3), ("q_hwm", P32), ("max_ue", C.c_uint32), ("query_limit", C.c_uint32),
+                ("act_status", PI32), ("act_cap", C.c_uint32), ("last_n_acts", C.c_uint32)]
 
 
 class WorldCfg(C.Structure):
@@ -94,7 +95,8 @@ class WorldCfg(C.Structure):
                 ("qbuf", C.c_uint32), ("slot_k", C.c_uint32), ("fanout", C.c_uint32),
                 ("limit", C.c_uint32), ("overhead", C.c_uint32), ("retransmit_mult", C.c_uint32),
                 ("max_refute", C.c_uint32), ("cap_rumors", C.c_uint32), ("seed", C.c_uint64),
-                ("qdepth", C.c_uint32 * 3), ("_pad", C.c_uint32)]
+                ("qdepth", C.c_uint32 * 3), ("max_user_event_size", C.c_uint32),
+                ("query_size_limit", C.c_uint32), ("_pad", C.c_uint32)]
 
 
 class Action(C.Structure):
@@ -222,6 +224,13 @@ def lib():
     L.orc_pick_peers.restype = C.c_uint32
     L.orc_merge_remote_state.argtypes = [C.POINTER(World), C.c_uint32, C.POINTER(PPState), C.c_int, C.c_int]
     L.orc_push_pull.argtypes = [C.POINTER(World), P32, P32, C.c_uint32, C.c_int, C.c_int]
+    L.orc_states_len.argtypes = [C.POINTER(World), C.c_uint32]
+    L.orc_states_len.restype = C.c_uint64
+    L.orc_world_action_status.argtypes = [C.POINTER(World), PI32, C.c_uint32]
+    L.orc_user_event_check.argtypes = [C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32]
+    L.orc_user_event_check.restype = C.c_int32
+    L.orc_query_check.argtypes = [C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32]
+    L.orc_query_check.restype = C.c_int32
     L.orc_check_queues.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint32, C.c_uint32, P64]
     L.orc_check_queues.restype = None
     L.orc_reap.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]

@@ -71,7 +71,8 @@ def test_deep_bench_shape_bit_exact(rounds):
 def test_deep_churn_flood_prune_ring_bit_exact(qcap, depth, limit, mult):
     """Intents, user events and queries of many lengths with churn, through heads of 8..64
     slots and depths small enough to fill: spills, the deferred whole-queue emissions, the
-    bounded prune at the full depth (head or tail losing its largest key), retransmit
+    bounded prune at the full depth (the largest key of head and tail, which the spills put
+    in the tail: deep_prune_wave / tail_prune_serial), retransmit
     limits of 1..4 (items retiring out of the head), a rumor ring small enough to wrap (tail
     items expire), and QueueChecker ticks.  Bit-exact against the oracle after every round."""
     n, rounds = 1200, 30
@@ -237,9 +238,9 @@ def test_deep_long_queues_all_capacity_classes():
 
 @pytest.mark.parametrize("qcap,depth", [(16, 100), (64, 130)])
 def test_deep_intent_only_prune_bit_exact(qcap, depth):
-    """Only the intent queue deep (queue_depth = (d, 0, 0): the lean variant of the smallest
-    deferred-path class serves it) and small enough to overflow: members whose deferred
-    emission must prune at the depth are passed on to the full-depth kernel.  The saturated
+    """Only the intent queue deep (queue_depth = (d, 0, 0)) and small enough to overflow:
+    the intent-only emission (emit_kernel_deep<..., 1u>, the other queues' tail code compiled
+    away) and the bounded prune at the depth inside emit_deep_wave_kernel.  The saturated
     intent workload, bit-exact against the oracle after every round, drops counted."""
     n, s, rounds = 4000, 1024, 14
     cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=qcap, queue_depth=(depth, 0, 0), gossip_limit=8 * 24,

@@ -215,6 +215,113 @@ def test_churn_and_flood_bit_exact(n, rounds):
     L.orc_world_free(C.byref(w))
 
 
+@pytest.mark.parametrize("limits", [(512, 1024), (300, 1100)])
+def test_churn_flood_oversized_originations_bit_exact(limits):
+    """A churn flood where a fifth of the user events and queries have sizes around the
+    entry points' limits (Serf::user_event, api.rs:255-287; query_in, base.rs:916-921):
+    every action's status (ok / skipped / the SerfError) and the whole state after every
+    round are bit-exact against the oracle; some actions of each kind are rejected and
+    some large ones accepted (that a rejected action moves no clock is asserted directly by
+    test_reference_kats_gpu.py's size-limit tests)."""
+    ue, ql = limits
+    n, rounds = 1500, 14
+    cfg = G.GossipConfig(n_members=n, n_subjects=15, queue_cap=32, gossip_limit=1400, max_rumors=1 << 16,
+                         event_buffer_size=512, query_buffer_size=512, slot_k=8, max_user_event_size=ue,
+                         query_size_limit=ql)
+    subj, acts, ml = W.churn_workload(n, rounds, events_per_round=30, queries_per_round=6, seed=ue + ql,
+                                      oversize=0.2)
+    g, w = pair(cfg, subj, W.initial_views(len(subj)))
+    seen = set()
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t])
+        got = g.action_status()
+        exp = np.zeros(len(acts[t]), np.int32)
+        if len(exp):
+            assert L.orc_world_action_status(C.byref(w), exp.ctypes.data_as(C.POINTER(C.c_int32)), len(exp)) == 0
+        assert np.array_equal(got, exp), f"round {t} action status"
+        seen.update(int(x) for x in got)
+        H.assert_same(H.engine_state(g), H.world_state(w), f"round {t}")
+        a = acts[t]
+        big = (a["act"] == G.ACT_USER_EVENT) & (a["payload_len"] > 32)
+        seen.add(("big_ok", bool(np.any(big & (got == G.ACT_OK)))))
+    assert {G.ERR_USER_EVENT_LIMIT, G.ERR_QUERY_TOO_LARGE, G.ACT_OK} <= seen, seen
+    if ue >= 512:  # names 1..64 + payloads 420..560: some fit the default limit
+        assert ("big_ok", True) in seen
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
+def test_queue_checker_per_member_max_bit_exact():
+    """QueueChecker with min_queue_depth > 0 (get_queue_max, base.rs:748-759): each
+    member's max is 2 * its own members.states.len() -- the untracked members, itself and
+    the subjects it knows -- so members that know different numbers of subjects prune at
+    different depths.  Most members are subjects and start unknown; a random share of the
+    (member, subject) entries is set known, differently per member.  Bit-exact against the
+    oracle (counts and state), then a round on, and again."""
+    n, s, rounds = 80, 76, 10
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=64, gossip_limit=1400, max_rumors=1 << 14,
+                         event_buffer_size=64, query_buffer_size=64, slot_k=4)
+    subj, acts, ml = W.intents_workload(n, s, rounds + 2, rate=0.1, seed=31, prune_frac=0.0)
+    views = (np.zeros(s, np.uint8), np.zeros(s, np.uint8), np.zeros(s, np.uint64))
+    g, w = pair(cfg, subj, views)
+    rng = np.random.default_rng(5)
+    vk = O.arr(w.v_kind, n * s, np.uint8).reshape(n, s)
+    vs = O.arr(w.v_status, n * s, np.uint8).reshape(n, s)
+    for m in range(n):
+        for j in rng.choice(s, size=int(rng.integers(0, 20)), replace=False):
+            g.set_view(m, int(j), G.KIND_KNOWN, G.STATUS_ALIVE, 0)
+            vk[m, j], vs[m, j] = G.KIND_KNOWN, G.STATUS_ALIVE
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t])
+    H.assert_same(H.engine_state(g), H.world_state(w), "before the checker")
+    total_pruned = 0
+    for k, (mx, mn, warn) in enumerate([(4096, 1, 8), (4096, 30, 8)]):
+        got = g.check_queues(mx, mn, warn)
+        exp = (C.c_uint64 * 9)()
+        L.orc_check_queues(C.byref(w), mx, mn, warn, exp)
+        assert list(got["queued"]) + list(got["warn"]) + list(got["pruned"]) == list(exp), (mx, mn, warn)
+        total_pruned += sum(got["pruned"])
+        H.assert_same(H.engine_state(g), H.world_state(w), f"checker {mn}")
+        g.round(rounds + k, ml[rounds + k], acts[rounds + k])
+        H.oracle_round(w, rounds + k, ml[rounds + k], acts[rounds + k])
+        H.assert_same(H.engine_state(g), H.world_state(w), f"round after checker {mn}")
+    assert total_pruned > 0
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
+def test_queues_width_on_plain_queues():
+    """GossipEngine.queues(width) on a context without deep queues (queue_depth None):
+    the first `width` items of every queue, equal to the plain dump truncated, and
+    max_live = the most items any queue holds."""
+    n, s, rounds = 600, 32, 6
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=16, max_rumors=1 << 15, event_buffer_size=32,
+                         query_buffer_size=32, slot_k=2)
+    subj, acts, ml = W.intents_workload(n, s, rounds, rate=0.05, seed=3)
+    g = G.GossipEngine(cfg)
+    g.set_subjects(subj)
+    g.init_views(*W.initial_views(s))
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+    full = [np.asarray(x) for x in g.queues()]
+    for width in (4, 16, 20):
+        part = [np.asarray(x) for x in g.queues(width=width)]
+        w = min(width, 16)
+        live3 = full[0].reshape(n, 3, 16)[:, :, :w] != 0xFFFFFFFF  # free slots' other fields are unspecified
+        for idx, (a, b) in enumerate(zip(full[:4], part[:4])):
+            a3, b3 = a.reshape(n, 3, 16)[:, :, :w], b.reshape(n, 3, width)
+            assert np.array_equal(np.where(live3, a3, 0), np.where(live3, b3[:, :, :w], 0)), idx
+            if width > 16:
+                assert np.all(b3[:, :, 16:] == (0xFFFFFFFF if idx == 0 else 0))
+        assert np.array_equal(live3, part[0].reshape(n, 3, width)[:, :, :w] != 0xFFFFFFFF)
+        assert np.array_equal(full[4], part[4])
+        live = np.count_nonzero(full[0].reshape(n * 3, 16) != 0xFFFFFFFF, axis=1).max()
+        assert g.max_live == live
+    g.close()
+
+
 def test_unknown_subjects_buffer_intents_then_join():
     """Subjects start unknown: intents go to the recent-intent buffer
     (upsert_intent), and a memberlist NotifyJoin consumes it (handle_node_join)."""

@@ -545,3 +545,78 @@ def test_configs0_c1_converges_on_cpu():
     r = bench.c1_leg(with_gpu=False)
     assert r["median_rel_rtt_error_all_pairs"] < 0.1
     assert r["resets"] == 0 and r["cpu_updates_per_s"] > 0
+
+
+# ---------------------------------------------------------------- origination size limits
+def _round_with(w, act, name_len, payload_len, t=0):
+    a = (O.Action * 1)()
+    a[0].member, a[0].act, a[0].name_len, a[0].payload_len, a[0].key = 0, act, name_len, payload_len, 7
+    assert L.orc_world_round(C.byref(w), t, None, 0, a, 1) == 0
+    st = (C.c_int32 * 1)()
+    assert L.orc_world_action_status(C.byref(w), st, 1) == 0
+    return st[0]
+
+
+def test_origination_size_limit_kats(kats):
+    """The reference's size-limit tests against the oracle's restatement of Serf::user_event
+    (api.rs:255-287) and query_in (base.rs:916-921): serf_event_user_size_limit
+    (event.rs:506-525), serf_query_size_limit (:1070-1085) and _increased (:1087-1100).
+    A rejected origination moves no clock and queues nothing."""
+    d = kats["dissemination"]
+    ue_lim, q_lim = d["max_user_event_size"]["value"], d["query_size_limit"]["value"]
+    assert d["user_event_size_limit_const"]["value"] == 9216
+    k = d["serf_event_user_size_limit"]
+    assert L.orc_user_event_check(ue_lim, 1, len(k["name"]), ue_lim) == -20  # UserEventLimitTooLarge
+    assert L.orc_user_event_check(ue_lim, 1, len(k["name"]), ue_lim - len(k["name"])) == -22  # encoded > limit
+    assert L.orc_user_event_check(ue_lim, 1, 8, 32) == 0
+    # the sane limit only binds through the encoded length when the option sits at 9 KiB
+    assert L.orc_user_event_check(9216, 1, 9216 - 8, 8) == -22
+    assert L.orc_user_event_check(9216, 1, 9216, 1) == -20
+    kq = d["serf_query_size_limit"]
+    assert L.orc_query_check(q_lim * kq["query_size_limit_factor"], 1, len(kq["name"]), q_lim) == -23
+    kq2 = d["serf_query_size_limit_increased"]
+    assert L.orc_query_check(q_lim * kq2["query_size_limit_factor"], 1, len(kq2["name"]), q_lim) == 0
+    # the encoded length depends on the clock's varint width: 127 -> 1 byte, 128 -> 2
+    base = L.orc_msg_len(4, 127, 0, 0) - 1  # RSF_MSG_QUERY
+    assert L.orc_query_check(base, 127, 0, 0) == 0 and L.orc_query_check(base, 128, 0, 0) == -23
+
+    # through a round: nothing moves for a rejected event / query, the accepted ones queue
+    w = make_world(n=4, s=1)
+    e0, q0, c0 = w.eclock[0], w.qclock[0], w.clock[0]
+    assert _round_with(w, O.ACT_USER_EVENT, len(k["name"]), ue_lim) == -20
+    assert (w.eclock[0], w.qclock[0], w.clock[0]) == (e0, q0, c0)
+    assert all(w.q_next_seq[i] == 0 for i in range(12)) and all(w.digest[m] == 0 for m in range(4))
+    assert _round_with(w, O.ACT_QUERY, len(kq["name"]), q_lim, t=1) == -23
+    assert all(w.q_next_seq[i] == 0 for i in range(12))
+    L.orc_world_free(C.byref(w))
+    w = make_world(n=4, s=1, query_size_limit=2 * q_lim)
+    assert _round_with(w, O.ACT_QUERY, len(kq2["name"]), q_lim) == 0
+    assert w.q_next_seq[1] == 1  # the origin's query queue took it
+    L.orc_world_free(C.byref(w))
+    bad = O.WorldCfg(n=2, s=1, qcap=8, ebuf=512, qbuf=512, slot_k=8, fanout=1, limit=1400, overhead=2,
+                     retransmit_mult=4, max_refute=2, cap_rumors=1024, max_user_event_size=9217)
+    w = O.World()
+    assert L.orc_world_init(C.byref(w), C.byref(bad)) == -1  # base.rs:69-70
+
+
+def test_states_len_and_per_member_queue_max():
+    """get_queue_max with min_queue_depth > 0 (base.rs:748-759) reads each node's own
+    members.states: 2 * states.len() of that member, so a member that knows fewer tracked
+    subjects prunes at a smaller depth."""
+    w = make_world(n=6, s=5, qcap=32)
+    # member 0 (untracked) knows subjects 0 and 1; member 1 (subject 0) knows nothing else
+    set_known(w, 0, 0, O.ST_ALIVE, 1)
+    set_known(w, 0, 1, O.ST_LEFT, 1)
+    assert L.orc_states_len(C.byref(w), 0) == (6 - 5) + 2
+    assert L.orc_states_len(C.byref(w), 1) == (6 - 5) + 1  # itself
+    for i in range(40):
+        w.rumors[i].type = 1
+        w.rumors[i].msg_len = 20
+    for m in (0, 1):
+        for i in range(20):
+            L.orc_queue_insert(C.byref(w), m, 0, 20 * m + i)
+    st = (C.c_uint64 * 9)()
+    L.orc_check_queues(C.byref(w), 4096, 1, 128, st)
+    live = lambda m: sum(w.q_rumor[m * 3 * 32 + i] != 0xFFFFFFFF for i in range(32))  # noqa: E731
+    assert (live(0), live(1)) == (6, 4) and st[6] == (20 - 6) + (20 - 4)
+    L.orc_world_free(C.byref(w))

@@ -279,3 +279,89 @@ def test_delivery_log_full_width_ltime():
         (big, 7 << 32, 1, G.DELIVERY_USER_EVENT)
     assert (int(d[1]["ltime"]), int(d[1]["key"]), int(d[1]["kind"])) == (1, 1, G.DELIVERY_MEMBER_EVENT)
     g.close()
+
+
+# ------------------------------------------------------------------ origination size limits
+def _originate(g, act, name_len, payload_len, key=7):
+    a = np.zeros(1, G.ACTION_DTYPE)
+    a["member"], a["act"], a["name_len"], a["payload_len"], a["key"] = 0, act, name_len, payload_len, key
+    return a
+
+
+def _sized(k, name):
+    return k[k[name]["payload_len"]]["value"]
+
+
+def _nothing_moved(g, before):
+    """no clock moved, nothing delivered, queued or sent anywhere"""
+    after = g.members()
+    for f in ("clock", "event_clock", "query_clock", "digest"):
+        assert np.array_equal(after[f], before[f]), f
+    assert len(g.deliveries()) == 0
+    rumor, *_x, next_seq = g.queues()
+    assert np.all(rumor == 0xFFFFFFFF) and np.all(next_seq == 0)
+
+
+@pytest.mark.parametrize("payload,expect", [("limit", G.ERR_USER_EVENT_LIMIT), (486, G.ERR_RAW_USER_EVENT_TOO_LARGE),
+                                            (487, G.ERR_USER_EVENT_LIMIT)])
+def test_serf_event_user_size_limit(kats, payload, expect):
+    """Serf::user_event with "this is too large an event" and a payload of
+    max_user_event_size bytes fails with UserEventLimitTooLarge before the event clock
+    moves (event.rs:506-525; api.rs:255-262): status, event clock, deliveries, queues and
+    every member's digest unchanged.  The boundary: name + payload == the limit (26 + 486)
+    passes the first check and fails the encoded-length one (RawUserEventTooLarge,
+    api.rs:281-283); one byte more fails the first."""
+    d = kats["dissemination"]
+    k = d["serf_event_user_size_limit"]
+    limit = _sized(d, "serf_event_user_size_limit")
+    g = engine(max_user_event_size=limit)
+    g.set_delivery_log(8)
+    before = g.members()
+    g.round(0, None, _originate(g, G.ACT_USER_EVENT, len(k["name"]), limit if payload == "limit" else payload))
+    st = int(g.action_status()[0])
+    assert st == expect
+    assert k["expect_error_contains"] in G.serf_error_text(st, g.cfg, size=0)
+    _nothing_moved(g, before)
+    g.close()
+
+
+def test_user_event_within_limit_originates(kats):
+    """A small event passes every check: the event clock moves, the origin delivers it and
+    queues it (the control for the size-limit cases)."""
+    g = engine()
+    g.set_delivery_log(8)
+    g.round(0, None, _originate(g, G.ACT_USER_EVENT, 8, 32))
+    assert g.action_status()[0] == G.ACT_OK
+    assert int(g.members()["event_clock"][0]) == 2 and len(g.deliveries()) >= 1
+    g.close()
+
+
+@pytest.mark.parametrize("case", ["serf_query_size_limit", "serf_query_size_limit_increased"])
+def test_serf_query_size_limit(kats, case):
+    """query_in with "this is too large a query" and a payload of query_size_limit bytes:
+    QueryTooLarge at the default limit (event.rs:1070-1085), accepted at twice the limit
+    (event.rs:1087-1100; base.rs:916-921).  A rejected query queues nothing and moves no
+    clock; an accepted one is handled locally and queued."""
+    d = kats["dissemination"]
+    k = d[case]
+    limit = _sized(d, case)
+    g = engine(query_size_limit=limit * k["query_size_limit_factor"])
+    before = g.members()
+    g.round(0, None, _originate(g, G.ACT_QUERY, len(k["name"]), limit))
+    st = int(g.action_status()[0])
+    if k.get("expect_ok"):
+        assert st == G.ACT_OK
+        *_x, next_seq = g.queues()
+        assert int(next_seq.reshape(-1, 3)[0, 1]) == 1  # the query entered the origin's query queue
+    else:
+        assert st == G.ERR_QUERY_TOO_LARGE
+        assert k["expect_error_contains"] in G.serf_error_text(st, g.cfg, size=0)
+        _nothing_moved(g, before)
+    g.close()
+
+
+def test_user_event_size_limit_at_create():
+    """max_user_event_size above USER_EVENT_SIZE_LIMIT fails at create (base.rs:69-70)."""
+    with pytest.raises(G._lib.EngineError) as e:
+        engine(max_user_event_size=G.USER_EVENT_SIZE_LIMIT + 1)
+    assert e.value.code == G.ERR_USER_EVENT_LIMIT
