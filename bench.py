@@ -230,11 +230,12 @@ def configs1_point(args, rank, world, queue_cap, settle, warmup, steps, queue_de
     a = argparse.Namespace(**vars(args))
     a.members, a.queue_cap, a.settle, a.warmup, a.steps = 1_000_000, queue_cap, settle, warmup, steps
     a.queue_depth = queue_depth
+    a.check_every = 150 if queue_depth else 0
     torch.cuda.empty_cache()
     r = run_gossip(a, rank, world)
     keep = ["value", "unit", "ms_per_step", "merges_per_s", "records_per_round_per_gpu", "queue_pruned_per_round",
             "queue_pruned_per_merged_record", "error_members", "cub_canaries_intact", "phases_ms_per_round",
-            "deep_path_members_per_round"]
+            "deep_path_members_per_round", "queue_regime"]
     out = {"metric": r["metric"], "steps": steps, "warmup": warmup, **{k: r[k] for k in keep}, "config": r["config"]}
     out["roofline"] = {k: r["roofline"][k] for k in ["bound", "achieved", "peak", "unit", "frac", "kernel",
                                                       "bytes_per_launch", "avg_launch_ms"]}
@@ -321,6 +322,9 @@ def main():
     ap.add_argument("--queue-depth", type=int, default=0,
                     help="gossip: intent queue depth above --queue-cap (<= 64): a register head plus an HBM tail, "
                          "pruned only by the QueueChecker (the reference's max_queue_depth is 4096)")
+    ap.add_argument("--check-every", type=int, default=None,
+                    help="gossip: a QueueChecker tick (prune to max_queue_depth 4096) every K rounds inside the round "
+                         "loop, the timed window ending with one (default: 150 with --queue-depth, else none)")
     ap.add_argument("--no-extra-points", action="store_true",
                     help="gossip: skip the configs[1] points (1M members, 64- and 256-slot queues)")
     ap.add_argument("--settle", type=int, default=None,
@@ -331,6 +335,8 @@ def main():
     ap.add_argument("--vivaldi-exchange", choices=["targeted", "allgather"], default="targeted",
                     help="vivaldi, N>1, R=1: fetch only the round's remote peer rows, or all-gather the table")
     args = ap.parse_args()
+    if args.check_every is None:
+        args.check_every = 150 if args.queue_depth else 0
     rank, world, local = env_rank()
     if world != args.gpus and world == 1 and args.gpus > 1:
         print("run multi-GPU through torch.distributed.run (one process per GPU)", file=sys.stderr)

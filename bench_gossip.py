@@ -18,19 +18,29 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 SEED = 0x5EED5EED
 SUBJECTS = 4096
 SETTLE_ROUNDS = 12   # setup: bring the cluster to gossip steady state (queues saturated) before timing
+# the reference's queue regime (deep queues): QueueChecker ticks every queue_check_interval
+# = 30 s (options.rs:512) at memberlist's LAN gossip interval of 200 ms = 150 rounds, each
+# pruning every queue to max_queue_depth 4096 (base.rs:720-760); settled past two ticks
+CHECK_EVERY = 150
+SETTLE_STEADY = 300
+MAX_QUEUE_DEPTH = 4096
+QUEUE_DEPTH_WARNING = 128
 # fraction of force_leaves issued with prune (remove_failed_node_prune); RSF_PRUNE_FRAC overrides
 PRUNE_FRAC = float(os.environ.get("RSF_PRUNE_FRAC", 0.1))
 HBM_PEAK_GBS = 8000.0
 
 
-def gossip_cfg(n_total, rounds_total, world, shard=None, queue_cap=64, queue_depth=0):
+def gossip_cfg(n_total, rounds_total, world, shard=None, queue_cap=64, queue_depth=0, ring_rounds=64):
     """queue_depth > queue_cap: the intent queue (the only one this workload fills) is that
     deep -- register head + HBM tail, pruned only by the QueueChecker as the reference's
-    (max_queue_depth 4096); the query / event queues stay at queue_cap (always empty here)."""
+    (max_queue_depth 4096); the query / event queues stay at queue_cap (always empty here).
+    ring_rounds: the rumor ring holds at least that many rounds of rumor blocks in one
+    generation, so no queued item expires within that many rounds (the reference never
+    expires one: ring_rounds >= the run's rounds makes the model's ring invisible)."""
     from ruserf_amd.gossip import GossipConfig
-    # rumor ring: a power of two holding >= 64 rounds of rumor blocks (ids recycle after that)
+    # rumor ring: a power of two holding >= ring_rounds rounds of rumor blocks (ids recycle after that)
     per_round = SUBJECTS * 4 + int(round(n_total * 0.01))
-    ring = 1 << max(10, (per_round * 64 - 1).bit_length())
+    ring = 1 << max(10, (per_round * max(64, ring_rounds) - 1).bit_length())
     return GossipConfig(n_members=n_total, n_subjects=SUBJECTS, shard=shard, queue_cap=queue_cap, event_buffer_size=512,
                         query_buffer_size=512, slot_k=1, fanout=3, gossip_limit=8 * 24, gossip_overhead=2,
                         retransmit_mult=4, max_refute=4, max_rumors=ring, seed=SEED,
@@ -69,10 +79,20 @@ def run_gossip(args, rank, world):
     from ruserf_amd.gossip import GossipEngine
     per = args.members
     n = per * world
-    settle = SETTLE_ROUNDS if args.settle is None else args.settle
-    rounds_total = settle + args.warmup + args.steps
     depth = getattr(args, "queue_depth", 0) or 0
-    cfg = gossip_cfg(n, rounds_total, world, queue_cap=args.queue_cap, queue_depth=depth)
+    # QueueChecker ticks in the round loop (0: none): every K rounds, counted from round 0, the
+    # timed window placed so that it ENDS with a tick (a tick then weighs 1/steps of the window
+    # instead of 1/K: pessimistic), the ring sized so no queued item expires during the run
+    check_every = getattr(args, "check_every", 0) or 0
+    if check_every:
+        base = SETTLE_STEADY if args.settle is None else args.settle
+        total = -(-(base + args.warmup + args.steps) // check_every) * check_every
+        settle = total - args.warmup - args.steps
+    else:
+        settle = SETTLE_ROUNDS if args.settle is None else args.settle
+    rounds_total = settle + args.warmup + args.steps
+    cfg = gossip_cfg(n, rounds_total, world, queue_cap=args.queue_cap, queue_depth=depth,
+                     ring_rounds=rounds_total if check_every else 64)
     subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED, prune_frac=PRUNE_FRAC)
     views = W.initial_views(SUBJECTS)
     stream = torch.cuda.current_stream()
@@ -87,9 +107,25 @@ def run_gossip(args, rank, world):
         step_fn = lambda t: sg.round(t, ml[t], acts[t])  # noqa: E731
     eng.set_subjects(subj)
     eng.init_views(*views)
+    ticks = {"n": 0, "in_window": 0, "pruned": 0, "last": None}
+
+    def checker(t_, timed):
+        # the QueueChecker tick after round t_ (every check_every rounds); synchronises
+        if not check_every or (t_ + 1) % check_every:
+            return
+        st = eng.check_queues(MAX_QUEUE_DEPTH, 0, QUEUE_DEPTH_WARNING)
+        ticks["n"] += 1
+        ticks["in_window"] += int(timed)
+        ticks["pruned"] += int(st["pruned"][0])
+        ticks["last"] = (t_ + 1, st)
+
+    def step_settle(t_):
+        step_fn(t_)
+        checker(t_, False)
+
     t = 0
     for _ in range(settle + args.warmup):
-        step_fn(t)
+        step_settle(t)
         t += 1
     torch.cuda.synchronize()
     if world > 1:
@@ -99,6 +135,7 @@ def run_gossip(args, rank, world):
     # exactly the timed rounds' worth of pending re-queues
     pruned0 = eng.pruned_total(flush=False)
     deep0 = eng.deep_stats()[0] if depth else 0
+    cls0 = eng.deep_class_stats() if depth else None
     eng.set_profiling(True)
     if sharded:
         sg.set_timing(True)
@@ -108,6 +145,7 @@ def run_gossip(args, rank, world):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step_fn(t)
+        checker(t, True)
         t += 1
     torch.cuda.synchronize()
     if world > 1:
@@ -120,6 +158,28 @@ def run_gossip(args, rank, world):
     merged = eng.merged_total() - merged0
     pruned = eng.pruned_total(flush=False) - pruned0
     deep_members = (eng.deep_stats()[0] - deep0) if depth else None
+    regime = None
+    if check_every:
+        occ = eng.checker_occupancy()
+        h, b = occ["hist"][0].astype(np.int64), occ["bin"]
+        cum = np.cumsum(h)
+        q = lambda f: int((np.searchsorted(cum, f * cum[-1]) + 1) * b)  # noqa: E731  (upper edge of the bin)
+        last_round, last = ticks["last"]
+        regime = {"what": "the reference's queue regime: QueueChecker ticks every check_every rounds "
+                          "(queue_check_interval 30 s / gossip interval 200 ms), each pruning to max_queue_depth; "
+                          "nothing dropped in between (bounded_pruned = 0), no rumor-ring expiry",
+                  "check_every_rounds": check_every, "max_queue_depth": MAX_QUEUE_DEPTH,
+                  "intent_queue_capacity": cfg.depths()[0], "ticks_total": ticks["n"],
+                  "ticks_in_timed_window": ticks["in_window"], "last_tick_after_round": last_round,
+                  "occupancy_at_last_tick": {"mean": float(last["queued"][0]) / per,
+                                             "p50_upper": q(0.5), "p99_upper": q(0.99),
+                                             "max": int(occ["max"][0]), "bin": b},
+                  "pruned_at_last_tick_per_member": float(last["pruned"][0]) / per,
+                  "members_over_warning_at_last_tick": int(last["warn"][0]),
+                  "expired_whole_run": int(eng.expired().sum()),
+                  "deferred_per_round_by_class": dict(zip(["small", "middle", "full"],
+                                                          ((eng.deep_class_stats() - cls0) / args.steps).tolist()))
+                  if depth else None}
     st = eng.members()
     from ruserf_amd.gossip import E_QUEUE_PRUNE
     # capacity errors other than the bounded queue's counted prunes (reported separately)
@@ -174,6 +234,7 @@ def run_gossip(args, rank, world):
         "cub_canaries_intact": canaries_ok,
         # the bounded queue model (queue_cap slots) drops live items when full; counted, not silent
         "queue_pruned_per_round": pruned_all / args.steps,
+        "queue_regime": regime,
         "queue_pruned_per_merged_record": pruned_all / max(1.0, merged_all),
         "queue_prune_members": qpm_all,
         # deep queues: members per round whose emission needed the tail (emit_deep_wave_kernel)

@@ -571,6 +571,11 @@ int rsf_gossip_reconnect(rsf_gossip* g, uint32_t tick, uint32_t* target);
  * warning depth, items pruned.  Synchronises. */
 int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_queue_depth,
                             uint32_t depth_warning, uint64_t* num_queued, uint64_t* n_warn, uint64_t* n_pruned);
+/* Occupancy at the last checker tick, before its prune: hist (host, [3][bins], may be NULL)
+ * counts the shard's members per queue whose item count falls in [b * bin, (b + 1) * bin),
+ * the last bin everything above; max3 (host, 3, may be NULL) = the most items any member's
+ * queue held.  bin / bins (may be NULL) return the histogram's geometry. */
+int rsf_gossip_checker_occupancy(rsf_gossip* g, uint32_t* hist, uint32_t* max3, uint32_t* bin, uint32_t* bins);
 /* Per shard member (host, n_loc each, cumulative; either may be NULL): pruned = live
  * items its bounded queues dropped when full; expired = queue items dropped at
  * emission because their rumor slot was recycled (see max_rumors). */
@@ -606,6 +611,12 @@ int rsf_gossip_dump_queues_width(rsf_gossip* g, uint32_t width, uint32_t* rumor,
 /* deep queues: members whose emission took the exact whole-queue path (the head alone could
  * not decide a pick; emit_deep_wave_kernel) since creation, and since the last call */
 int rsf_gossip_deep_stats(rsf_gossip* g, uint64_t* slow_total, uint64_t* slow_since_last);
+/* the same since creation per LDS capacity class of emit_deep_wave_kernel (host, 3 entries):
+ * [0] the smallest class, [1] the middle one, [2] the full depth.  Synchronises. */
+int rsf_gossip_deep_class_stats(rsf_gossip* g, uint64_t* out3);
+/* items queued per shard member and queue (host, [n_loc][3]: intent, query, event; head + tail),
+ * after applying the pending lists (the QueueChecker's num_queued per node).  Synchronises. */
+int rsf_gossip_queue_lengths(rsf_gossip* g, uint32_t* out);
 int rsf_gossip_dump_buffers(rsf_gossip* g, uint64_t* eb_ltime, uint32_t* eb_cnt, uint64_t* eb_keys,
                             uint64_t* qb_ltime, uint32_t* qb_cnt, uint32_t* qb_ids);
 int rsf_gossip_dump_rumors(rsf_gossip* g, uint32_t first, uint32_t count, rsf_rumor* out);

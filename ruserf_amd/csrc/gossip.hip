@@ -838,25 +838,10 @@ __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, 
     // positions past the head are the largest keys, in order: they go to the tail, the one at
     // position qcap being the smallest of them
     const bool sn = ins && pos_n >= c.qcap, se = live && pos_e >= c.qcap;
-#ifndef RSF_SPILL_NT
-#define RSF_SPILL_NT 0  // 1: spills written with non-temporal stores (the tail is read again only by a refill)
-#endif
-#if !RSF_DIAG_NO_SPILL_WRITE  // (timing diagnostic only: results differ without the writes)
-    if constexpr (RSF_SPILL_NT) {
-      typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-      if (sn) {
-        const u4v v = {rid, myseq, len << 16, DEC ? dec : 0u};
-        __builtin_nontemporal_store(v, reinterpret_cast<u4v*>(sp->t + sp->cnt + (pos_n - c.qcap)));
-      }
-      if (se) {
-        const u4v v = {Q.r, Q.sq, Q.tl, DEC ? Q.dec : 0u};
-        __builtin_nontemporal_store(v, reinterpret_cast<u4v*>(sp->t + sp->cnt + (pos_e - c.qcap)));
-      }
-    } else {
-      if (sn) sp->t[sp->cnt + (pos_n - c.qcap)] = make_uint4(rid, myseq, len << 16, DEC ? dec : 0u);
-      if (se) sp->t[sp->cnt + (pos_e - c.qcap)] = make_uint4(Q.r, Q.sq, Q.tl, DEC ? Q.dec : 0u);
-    }
-#endif
+    // (ordinary stores: non-temporal ones measured 1.37 -> 2.24 ms of emission, later spills
+    // landing in the same partly written sectors)
+    if (sn) sp->t[sp->cnt + (pos_n - c.qcap)] = make_uint4(rid, myseq, len << 16, DEC ? dec : 0u);
+    if (se) sp->t[sp->cnt + (pos_e - c.qcap)] = make_uint4(Q.r, Q.sq, Q.tl, DEC ? Q.dec : 0u);
     const uint64_t at_n = ballot(ins && pos_n == c.qcap), at_e = ballot(live && pos_e == c.qcap);
     const int w = __ffsll((long long)(at_n | at_e)) - 1;
     const uint32_t tl_w = at_n ? (shfl_u32(len, w) << 16) : shfl_u32(Q.tl, w);
@@ -2803,9 +2788,11 @@ __global__ void __launch_bounds__(256) seg_end_kernel(uint64_t n_loc, const uint
 // Deep queues: numq counts the tail too, and a queue to prune is listed (s.deep_ids) for
 // check_deep_kernel, which keeps the max smallest keys of head and tail.
 // qmax (non-null when min_queue_depth > 0): each member's own get_queue_max (queue_max_kernel).
+constexpr uint32_t kOccBin = 64, kOccBins = 160;  // occupancy histogram: 64-item bins up to 10240, then one overflow bin
 __global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uint32_t max_depth, uint32_t warn,
                                                            unsigned long long* __restrict__ stats,
-                                                           const uint32_t* __restrict__ qmax) {
+                                                           const uint32_t* __restrict__ qmax,
+                                                           uint32_t* __restrict__ hist) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= c.n_loc * 3) return;
   const uint32_t q = (uint32_t)(t % 3);
@@ -2814,6 +2801,10 @@ __global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uin
   uint32_t n = 0;
   while (n < c.qcap && s.q_rumor[base + n] != kEmpty) n++;
   if (tcap_of(c, q)) n += s.tsum[t].x;
+  if (hist) {  // occupancy before the prune (rsf_gossip_checker_occupancy)
+    atomicAdd(hist + q * (kOccBins + 1) + min(n / kOccBin, kOccBins), 1u);
+    atomicMax(hist + 3 * (kOccBins + 1) + q, n);
+  }
   if (n) atomicAdd(stats + q, (unsigned long long)n);
   if (n >= warn) atomicAdd(stats + 3 + q, 1ull);
   if (n > max_depth && tcap_of(c, q)) {
@@ -3051,6 +3042,7 @@ struct rsf_gossip {
   uint64_t deep_last = 0;     // rsf_gossip_deep_stats' previous total
   uint32_t* big_ids = nullptr;  // receivers deferred to merge_big_kernel (count: d_counters[52])
   uint32_t* qmax = nullptr;     // [n_loc] per-member get_queue_max (rsf_gossip_check_queues, min_queue_depth > 0)
+  uint32_t* occ_hist = nullptr; // the last checker tick's occupancy histogram + maxima (check_queues_kernel)
   // RSF_GUARD_ZONES (diagnostic builds): 0xA5-filled zones before and after big_ids and
   // stage_dec and after the sort's storage; rsf_gossip_debug_zones counts changed bytes
   char *big_base = nullptr, *dec_base = nullptr;
@@ -3356,7 +3348,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   g->grp_slot, g->grp_off, g->dec_base, s.dlog, s.dmeta, s.dcnt,
                   g->bkt_send, g->bkt_recv, g->bkt_dec, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn,
                   s.p_ent, s.p_cnt, g->big_base, tail_of(s, 0), tail_of(s, 1), tail_of(s, 2), s.tsum, s.deep_ids,
-                  g->qmax, g->d_act_status};
+                  g->qmax, g->d_act_status, g->occ_hist};
   for (void* p : ptrs)
     if (p) hipFree(p);
   g->scratch.release();
@@ -4231,10 +4223,13 @@ int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t mi
     RSF_HIP(hipGetLastError());
   }
   const uint32_t* qmax = min_queue_depth > 0 ? g->qmax : nullptr;
+  const size_t hist_words = 3 * (kOccBins + 1) + 3;
+  if (!g->occ_hist && (rc = dmalloc((void**)&g->occ_hist, hist_words * 4))) return rc;
+  RSF_HIP(hipMemsetAsync(g->occ_hist, 0, hist_words * 4, g->stream));
   RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, g->stream));
   if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 16, g->stream));
   hipLaunchKernelGGL(check_queues_kernel, dim3(grid1(c.n_loc * 3)), dim3(256), 0, g->stream, c, g->s, max_depth,
-                     depth_warning, g->d_counters + 40, qmax);
+                     depth_warning, g->d_counters + 40, qmax, g->occ_hist);
   RSF_HIP(hipGetLastError());
   if (c.deep) {  // the deep queues over the max: the smallest max keys of head and tail kept
     hipLaunchKernelGGL(check_deep_kernel, dim3(g->deep_check_blocks), dim3(kDeepThreads), 0, g->stream, c, g->s,
@@ -4259,6 +4254,22 @@ int rsf_gossip_action_status(rsf_gossip* g, int32_t* status, uint32_t n) {
   RSF_HIP(hipSetDevice(g->device));
   RSF_HIP(hipMemcpyAsync(status, g->d_act_status, (size_t)n * 4, hipMemcpyDeviceToHost, g->stream));
   RSF_HIP(hipStreamSynchronize(g->stream));
+  return RSF_OK;
+}
+
+int rsf_gossip_checker_occupancy(rsf_gossip* g, uint32_t* hist, uint32_t* max3, uint32_t* bin, uint32_t* bins) {
+  if (!g) return gerr("null context");
+  if (bin) *bin = kOccBin;
+  if (bins) *bins = kOccBins + 1;
+  if (!hist && !max3) return RSF_OK;
+  std::vector<uint32_t> h(3 * (kOccBins + 1) + 3, 0u);
+  if (g->occ_hist) {
+    RSF_HIP(hipSetDevice(g->device));
+    RSF_HIP(hipMemcpyAsync(h.data(), g->occ_hist, h.size() * 4, hipMemcpyDeviceToHost, g->stream));
+    RSF_HIP(hipStreamSynchronize(g->stream));
+  }
+  if (hist) std::copy(h.begin(), h.begin() + 3 * (kOccBins + 1), hist);
+  if (max3) std::copy(h.begin() + 3 * (kOccBins + 1), h.end(), max3);
   return RSF_OK;
 }
 
@@ -4493,6 +4504,47 @@ int rsf_gossip_deep_stats(rsf_gossip* g, uint64_t* slow_total, uint64_t* slow_si
   if (slow_total) *slow_total = t;
   if (slow_since_last) *slow_since_last = t - g->deep_last;
   g->deep_last = t;
+  return RSF_OK;
+}
+
+int rsf_gossip_deep_class_stats(rsf_gossip* g, uint64_t* out3) {
+  if (!g || !out3) return gerr("null argument");
+  unsigned long long t[3];
+  RSF_HIP(hipSetDevice(g->device));
+  // lists 0 (kDeepSmall), 1 (the full depth), 2 (kDeepTiny): counters 55 - kDeepClassOff + list
+  RSF_HIP(hipMemcpyAsync(t, g->d_counters + 55 - kDeepClassOff, sizeof(t), hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
+  out3[0] = t[2];
+  out3[1] = t[0];
+  out3[2] = t[1];
+  return RSF_OK;
+}
+
+// per (member, queue): live items of the head (its leading slots) plus the tail's count
+__global__ void __launch_bounds__(256) queue_lengths_kernel(GCfg c, GState s, uint32_t* __restrict__ out) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= c.n_loc * 3) return;
+  const uint64_t base = t * c.qcap;
+  uint32_t n = 0;
+  while (n < c.qcap && s.q_rumor[base + n] != kEmpty) n++;
+  if (tcap_of(c, (uint32_t)(t % 3))) n += s.tsum[t].x;
+  out[t] = n;
+}
+
+int rsf_gossip_queue_lengths(rsf_gossip* g, uint32_t* out) {
+  if (!g || !out) return gerr("null argument");
+  const GCfg& c = g->c;
+  RSF_HIP(hipSetDevice(g->device));
+  int rc = flush_pending(g);
+  if (rc) return rc;
+  void* dv = nullptr;
+  const size_t bytes = c.n_loc * 3 * sizeof(uint32_t);
+  if ((rc = g->scratch.take(&bytes, 1, &dv))) return rc;
+  uint32_t* d = (uint32_t*)dv;
+  hipLaunchKernelGGL(queue_lengths_kernel, dim3(grid1(c.n_loc * 3)), dim3(256), 0, g->stream, c, g->s, d);
+  RSF_HIP(hipGetLastError());
+  RSF_HIP(hipMemcpyAsync(out, d, c.n_loc * 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipStreamSynchronize(g->stream));
   return RSF_OK;
 }
 

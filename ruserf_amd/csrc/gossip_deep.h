@@ -912,7 +912,10 @@ __global__ void __launch_bounds__(kWave) emit_deep_wave_kernel(GCfg c, GState s,
   s_dprof[lane] = 0;
 #endif
   const uint32_t n_list = s.deep_n[list];
-  if (blockIdx.x == 0 && lane == 0 && n_list) atomicAdd(total, (unsigned long long)n_list);
+  if (blockIdx.x == 0 && lane == 0 && n_list) {
+    atomicAdd(total, (unsigned long long)n_list);
+    atomicAdd(total - kDeepClassOff + list, (unsigned long long)n_list);  // per list (rsf_gossip_deep_class_stats)
+  }
   for (uint32_t i = lane; i < CAP; i += kWave) d.st[i] = kDeepDead;
   wsync();
   const uint64_t last = c.n_loc * 3 - 1;

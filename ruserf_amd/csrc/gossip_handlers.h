@@ -105,6 +105,7 @@ struct GState {
   uint32_t* deep_ids;  // [n_loc * 3] members deferred to emit_deep_wave_kernel (two lists), or queues to prune
   uint32_t* deep_n;    // [3] the lists' lengths (reset before each emission)
 };
+constexpr uint32_t kDeepClassOff = 6;  // the per-list deferral counters sit at (total counter) - 6 + list
 constexpr uint32_t kTailSlack = 192;  // tail row room past its capacity: one emission's spills (2 x 64) + 64
 // per-queue deep-queue fields by a select on q
 RSF_HD uint32_t tcap_of(const GCfg& c, uint32_t q) { return q == 0 ? c.tcap0 : q == 1 ? c.tcap1 : c.tcap2; }

@@ -153,11 +153,7 @@ __device__ __forceinline__ bool finite(double x) { return isfinite(x); }
 constexpr RSF_HD int filt_words(uint32_t F) { return F <= 3 ? 2 : 8; }
 constexpr uint64_t kNs34 = (1ull << 34) - 1;
 
-// WLATE (WW > 0): win[0] holds the sequential fold of the window slots BEFORE the index
-// (0.0 + w[0] + ... + w[idx-1], taken by the caller while the slots were in registers); the
-// slots after the index are read again here, after update_vivaldi -- the same fold, in the
-// same order, with the 20-slot window out of registers through the vivaldi update.
-template <int D, int F, int WW, int FRT = filt_words(F), bool NTS = false, bool WLATE = false>
+template <int D, int F, int WW, int FRT = filt_words(F), bool NTS = false>
 __device__ __forceinline__ int update_one(double* me, double& err, double& adj, double& h,
                                           const double* other, double oerr, double oadj, double oh,
                                           uint32_t odim, uint64_t rtt_ns, double* frec,
@@ -284,23 +280,8 @@ __device__ __forceinline__ int update_one(double* me, double& err, double& adj, 
     double sample = rtt_seconds - dist;
     const uint32_t idx = win_idx;
     double sum = 0.0;
-    if constexpr (WLATE) {
-      // the slots after the index, all loads in flight together; the column address passes
-      // through an opaque asm that also reads `sample`, so the loads cannot be hoisted above
-      // the vivaldi update (which would put the window back in registers through it)
-      const double* col = adj_col;
-      asm volatile("" : "+v"(col) : "v"(sample));
-      double tail[WW];
 #pragma unroll
-      for (int i = 0; i < WW; ++i) tail[i] = ((uint32_t)i > idx) ? col[(uint64_t)i * adj_stride] : 0.0;
-      sum = win[0] + sample;
-#pragma unroll
-      for (int i = 0; i < WW; ++i)
-        if ((uint32_t)i > idx) sum = sum + tail[i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < WW; ++i) sum = sum + (((uint32_t)i == idx) ? sample : win[i]);
-    }
+    for (int i = 0; i < WW; ++i) sum = sum + (((uint32_t)i == idx) ? sample : win[i]);
     const uint32_t nidx = (idx + 1 == (uint32_t)WW) ? 0 : idx + 1;
     if constexpr (NTS) {
       __builtin_nontemporal_store(sample, adj_col + (uint64_t)idx * adj_stride);
@@ -660,22 +641,6 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
 #ifndef RSF_VIV_XCD
 #define RSF_VIV_XCD 0  // 1: XCD-contiguous block order (common.h xcd_block)
 #endif
-#ifndef RSF_VIV_LDS1
-// 1: own rows and peer rows pass through ONE 6 KB LDS block per wave, one after the other
-// (24 KB per block instead of 48), so LDS no longer caps the kernel at 3 waves/SIMD
-#define RSF_VIV_LDS1 0
-#endif
-#ifndef RSF_VIV_OWNDIRECT
-// 1: each lane loads its own row directly (no LDS transpose of the own rows; with RSF_VIV_LDS1
-// the peer rows alone use the wave's 6 KB block)
-#define RSF_VIV_OWNDIRECT 0
-#endif
-#ifndef RSF_VIV_WLATE
-// 1: the adjustment window is folded up to its index as soon as it arrives and its slots after
-// the index are read again after update_vivaldi (cacheable loads, so the second read finds
-// them in the cache), keeping 40 VGPRs of window out of the vivaldi update
-#define RSF_VIV_WLATE 0
-#endif
 #ifndef RSF_VIV_NT
 // non-temporal hints (bit 1: member-side loads/stores in the round kernel, 2: its window-slot
 // and window-index stores, 4: the peer gather).  The member-side streams are touched once
@@ -729,19 +694,12 @@ __global__ void __launch_bounds__(RSF_VIV_BLOCK, RSF_VIV_WAVES) vivaldi_observe_
   double win[WW];
 #pragma unroll
   for (int i = 0; i < WW; ++i)
-    win[i] = RSF_VIV_WLATE ? adj_win[(uint64_t)i * p.shard_n + local] : ld_s(adj_win + (uint64_t)i * p.shard_n + local);
+    win[i] = ld_s(adj_win + (uint64_t)i * p.shard_n + local);
   const double2* src = reinterpret_cast<const double2*>(cur + (p.lo + wbase) * 12);
   const uint32_t last = wrows * 6 - 1;
   double2 own[6];
-#if RSF_VIV_OWNDIRECT
-  // each lane its own row: six 16-B loads at a 96-B stride over the wave's contiguous 6 KB
-  // (the same lines as the coalesced pieces), straight into the registers the update uses
-#pragma unroll
-  for (uint32_t k = 0; k < 6; ++k) own[k] = ld_s(src + min(lane * 6 + k, last));
-#else
 #pragma unroll
   for (uint32_t k = 0; k < 6; ++k) own[k] = ld_s(src + min(lane + 64 * k, last));
-#endif
   double* frec = filt + ((uint64_t)slot * p.shard_n + local) * FR;
   double rec[FR];
   {
@@ -774,38 +732,18 @@ __global__ void __launch_bounds__(RSF_VIV_BLOCK, RSF_VIV_WAVES) vivaldi_observe_
       }
     }
   }
-#if RSF_VIV_LDS1
-  __shared__ double2 stage[RSF_VIV_BLOCK / 64][1][64 * 6];
-  double2* so = stage[threadIdx.x / 64][0];
-  double2* sp = so;
-#else
   __shared__ double2 stage[RSF_VIV_BLOCK / 64][2][64 * 6];
   double2* so = stage[threadIdx.x / 64][0];
   double2* sp = stage[threadIdx.x / 64][1];
-#endif
-#if !RSF_VIV_OWNDIRECT
 #pragma unroll
   for (uint32_t k = 0; k < 6; ++k) so[lane + 64 * k] = own[k];
-#endif
-#if !RSF_VIV_LDS1
 #pragma unroll
   for (uint32_t ps = 0; ps < 2; ++ps)
 #pragma unroll
     for (int j = 0; j < 3; ++j) sp[(32 * ps + (lane >> 1)) * 6 + half * 3 + j] = g[ps * 3 + j];
-#endif
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   double me[D], other[D], e, a, h, oe, oa, oh;
-#if RSF_VIV_OWNDIRECT
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    me[2 * i] = own[i].x;
-    me[2 * i + 1] = own[i].y;
-  }
-  e = own[4].x;
-  a = own[4].y;
-  h = own[5].x;
-#else
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const double2 t = so[lane * 6 + i];
@@ -815,18 +753,6 @@ __global__ void __launch_bounds__(RSF_VIV_BLOCK, RSF_VIV_WAVES) vivaldi_observe_
   e = so[lane * 6 + 4].x;
   a = so[lane * 6 + 4].y;
   h = so[lane * 6 + 5].x;
-#endif
-#if RSF_VIV_LDS1
-  // the block is free once every lane has read its own row; the peer rows follow
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (uint32_t ps = 0; ps < 2; ++ps)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) sp[(32 * ps + (lane >> 1)) * 6 + half * 3 + j] = g[ps * 3 + j];
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-#endif
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const double2 u = sp[lane * 6 + i];
@@ -836,21 +762,12 @@ __global__ void __launch_bounds__(RSF_VIV_BLOCK, RSF_VIV_WAVES) vivaldi_observe_
   oe = sp[lane * 6 + 4].x;
   oa = sp[lane * 6 + 4].y;
   oh = sp[lane * 6 + 5].x;
-#if RSF_VIV_WLATE
-  {  // the fold of the slots before the index; the window's registers are free from here
-    double pre = 0.0;
-#pragma unroll
-    for (int i = 0; i < WW; ++i)
-      if ((uint32_t)i < widx) pre = pre + win[i];
-    win[0] = pre;
-  }
-#endif
   int st = RSF_OK;
   if (!active) {
   } else if (peer >= p.n) {
     st = RSF_ERR_ARG;
   } else {
-    st = update_one<D, F, WW, FRT, (RSF_VIV_NT & 2) != 0, RSF_VIV_WLATE != 0>(
+    st = update_one<D, F, WW, FRT, (RSF_VIV_NT & 2) != 0>(
         me, e, a, h, other, oe, oa, oh, p.dim, rtt_ns, rec, adj_win + local, p.shard_n, adj_idx + local, p, m,
         p.round, resets, win, widx);
   }

@@ -431,6 +431,31 @@ class GossipEngine:
                                                ptr(ln, C.c_uint16), ptr(ns, C.c_uint32)))
         return r, sq, tx, ln, ns
 
+    def deep_class_stats(self):
+        """members deferred to the whole-queue emission since creation, per LDS capacity
+        class: (smallest, middle, full depth)"""
+        out = np.zeros(3, dtype=np.uint64)
+        check(lib().rsf_gossip_deep_class_stats(self._h, ptr(out, C.c_uint64)))
+        return out
+
+    def checker_occupancy(self):
+        """The last check_queues tick's occupancy before its prune: {"bin": items per bin,
+        "hist": [3, bins] members per bin per queue (the last bin: everything above),
+        "max": [3] the most items any member's queue held}"""
+        b, nb = C.c_uint32(), C.c_uint32()
+        check(lib().rsf_gossip_checker_occupancy(self._h, None, None, C.byref(b), C.byref(nb)))
+        h = np.zeros(3 * nb.value, dtype=np.uint32)
+        mx = np.zeros(3, dtype=np.uint32)
+        check(lib().rsf_gossip_checker_occupancy(self._h, ptr(h, C.c_uint32), ptr(mx, C.c_uint32), None, None))
+        return {"bin": b.value, "hist": h.reshape(3, nb.value), "max": mx}
+
+    def queue_lengths(self):
+        """[n_loc, 3] items queued per member and queue (intent, query, event), head + tail,
+        after applying the pending lists"""
+        out = np.zeros(self.n_loc * 3, dtype=np.uint32)
+        check(lib().rsf_gossip_queue_lengths(self._h, ptr(out, C.c_uint32)))
+        return out.reshape(self.n_loc, 3)
+
     def buffers(self):
         c = self.cfg
         n = self.n_loc
