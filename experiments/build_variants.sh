@@ -1,6 +1,6 @@
 #!/bin/bash
-# Builds libruserf_amd variants into ab/ (git-ignored, travels to the GPU box) for A/B
-# timing within one gpurun call (load one with RSF_LIB_PATH=$PWD/ab/lib_NAME.so).
+# Builds libruserf_amd variants into $AB (default abx/: git-ignored, travels to the GPU box; delete it after the A/B) for A/B
+# timing within one gpurun call (load one with RSF_LIB_PATH=$PWD/abx/lib_NAME.so).
 # REV=<rev> builds the source as of that git revision instead of the working tree.
 # Only one source file is rebuilt with the extra defines (SRC=gossip by default, or vivaldi);
 # the other objects come from the main build (make -C ruserf_amd/csrc first).
@@ -10,10 +10,10 @@ cd "$(dirname "$0")/.."
 CS=ruserf_amd/csrc
 SRCF=${SRC:-gossip}
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -Wno-unused-value -Wno-unused-result"
-mkdir -p ab
+AB=${AB:-abx}; mkdir -p $AB
 while [ $# -gt 1 ]; do
   name=$1; defs=$2; shift 2
-  d=ab/build_$name; mkdir -p $d
+  d=$AB/build_$name; mkdir -p $d
   src=$CS/$SRCF.hip
   if [ -n "$REV" ]; then
     rm -rf $d/src && mkdir -p $d/src && git archive "$REV" ruserf_amd/csrc include | tar -x -C $d/src
@@ -24,6 +24,6 @@ while [ $# -gt 1 ]; do
   for s in capi vivaldi gossip codec coalesce swim intern; do
     [ "$s" = "$SRCF" ] && objs="$objs $d/$s.o" || objs="$objs $CS/build/$s.o"
   done
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ab/lib_$name.so $objs
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $AB/lib_$name.so $objs
   echo built $name
 done

@@ -20,7 +20,7 @@ L = lib()
 L.rsf_gossip_deep_prof.restype = C.c_int
 L.rsf_gossip_deep_prof.argtypes = [C.POINTER(C.c_uint64)]
 rounds = settle + 5
-cfg = B.gossip_cfg(n, rounds, 1, queue_depth=4096)
+cfg = B.gossip_cfg(n, rounds, 1, queue_depth=4096, ring_rounds=rounds)
 subj, acts, ml = W.intents_workload(n, B.SUBJECTS, rounds, rate=0.01, seed=B.SEED, prune_frac=B.PRUNE_FRAC)
 eng = GossipEngine(cfg)
 eng.set_subjects(subj)
@@ -35,7 +35,7 @@ for t in range(settle, rounds):
 torch.cuda.synchronize()
 L.rsf_gossip_deep_prof(buf)
 v = [int(x) for x in buf]
-why = ["empty_head", "pick_len", "pick_key", "exact_empty", "exact_len", "exact_key", "capacity", "-"]
+why = ["empty_head", "pick_len", "pick_key", "exact_empty", "exact_len", "exact_key", "capacity", "tail_bound_tx0"]
 ph = ["load", "prune", "take_head", "picks", "store", "fallback_picks", "fallback_store", "fallbacks"]
 members = max(1, v[16])
 out = {"rounds": rounds - settle, "deferred_per_round": v[16] / (rounds - settle),
@@ -47,5 +47,7 @@ out = {"rounds": rounds - settle, "deferred_per_round": v[16] / (rounds - settle
                                      "no_tail_item_fits_before_it": v[26] / (rounds - settle)},
        "select_passes_per_select": v[18] / max(1, v[19]), "selects_per_member": v[19] / members,
        "take_head_cycles_per_member": {k: v[20 + i] / members for i, k in enumerate(["count", "select", "gather", "rank_permute"])},
+       "crossing_pick_tx0_per_round": v[27] / (rounds - settle), "crossing_pick_tx_ge1_per_round": v[28] / (rounds - settle),
+       "recent_mode_per_round": v[29] / (rounds - settle), "recent_relisted_per_round": v[30] / (rounds - settle),
        "queue_items_hist_by_128": {i * 128: v[32 + i] for i in range(32) if v[32 + i]}}
 print(json.dumps(out))

@@ -294,7 +294,8 @@ typedef struct rsf_gossip_cfg {
   uint32_t query_size_limit;   /* Options::query_size_limit (0 = the default 1024, options.rs:519); at most
                                   65534 (the model keeps a message's length in 16 bits) */
 } rsf_gossip_cfg;
-#define RSF_MAX_QUEUE_DEPTH 4160 /* head (<= 64) + tail: max_queue_depth 4096 plus a round's headroom */
+#define RSF_MAX_QUEUE_DEPTH 8256 /* head (<= 64) + tail: max_queue_depth 4096 plus what 150 rounds between
+                                    QueueChecker ticks add at the saturated bench workload (~24 a round) */
 
 /* One rumor (a broadcast message body; SerfBroadcast, core/src/broadcast.rs:153-183). 24 bytes. */
 typedef struct rsf_rumor {
@@ -608,6 +609,9 @@ int rsf_gossip_dump_queues(rsf_gossip* g, uint32_t* rumor, uint32_t* seq, uint16
  * send order); *max_live (optional) = the most items any queue holds (> width: truncated) */
 int rsf_gossip_dump_queues_width(rsf_gossip* g, uint32_t width, uint32_t* rumor, uint32_t* seq, uint16_t* transmits,
                                  uint16_t* len, uint32_t* next_seq, uint32_t* max_live);
+/* the same for local rows [row0, row0 + rows) only ([rows][3][width], no next_seq) */
+int rsf_gossip_dump_queues_rows(rsf_gossip* g, uint64_t row0, uint64_t rows, uint32_t width, uint32_t* rumor,
+                                uint32_t* seq, uint16_t* tx, uint16_t* len, uint32_t* max_live);
 /* deep queues: members whose emission took the exact whole-queue path (the head alone could
  * not decide a pick; emit_deep_wave_kernel) since creation, and since the last call */
 int rsf_gossip_deep_stats(rsf_gossip* g, uint64_t* slow_total, uint64_t* slow_since_last);

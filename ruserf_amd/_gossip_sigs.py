@@ -17,7 +17,12 @@ def declare(L):
     i = C.c_int
 
     def sig(name, args):
-        fn = getattr(L, name)
+        # a library built before a function existed (an A/B variant) lacks its symbol: calling
+        # that function then fails loudly; tests/test_capi.py checks the shipped library
+        # exports every declared symbol
+        fn = getattr(L, name, None)
+        if fn is None:
+            return
         fn.restype = i
         fn.argtypes = args
 
@@ -61,6 +66,7 @@ def declare(L):
     sig("rsf_gossip_action_status", [VP, PI32, C.c_uint32])
     sig("rsf_gossip_deep_class_stats", [VP, P64])
     sig("rsf_gossip_queue_lengths", [VP, P32])
+    sig("rsf_gossip_dump_queues_rows", [VP, C.c_uint64, C.c_uint64, C.c_uint32, P32, P32, P16, P16, P32])
     sig("rsf_gossip_checker_occupancy", [VP, P32, P32, P32, P32])
     sig("rsf_gossip_check_queues", [VP, C.c_uint32, C.c_uint32, C.c_uint32, P64, P64, P64])
     sig("rsf_gossip_dump_pruned", [VP, P32, P32])

@@ -503,6 +503,8 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
         const int fc = __ffsll((long long)cross) - 1;
         const uint64_t before = fc > 0 ? (~0ull >> (64 - fc)) : 0ull;
         RSF_DEEP_WHY((pick_m & before) == before ? 24 : 25);
+        RSF_DEEP_WHY((shfl_u32(Q.tl, fc) & 0xFFFF) == 0 ? 27 : 28);  // the crossing pick's transmit class
+        if ((tmin >> 48) == 0) RSF_DEEP_WHY(7);  // the tail's bound is a transmits-0 key
         const uint32_t ub = wave_inclusive_sum_u32(lane_bit(pick_m & before) ? c.overhead + len : 0u);
         const int32_t f0 = (int32_t)lim - (int32_t)shfl_u32(ub, 63) - (int32_t)c.overhead;
         if (f0 < (int32_t)tminlen) RSF_DEEP_WHY(26);
@@ -725,6 +727,7 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
     if (tlq_key(tl & 0xFFFF, tl >> 16, shfl_u32(Q.sq, hl)) >= tmin) {
       *unsafe = true;
       RSF_DEEP_WHY(2);
+      RSF_DEEP_WHY((tl & 0xFFFF) == 0 ? 27 : 28);  // (diagnostic) the crossing pick's transmit class
       return;
     }
   }
@@ -972,8 +975,12 @@ __device__ __forceinline__ uint32_t pend_flush_wave(const GCfg& c, const GState&
     if (tcap_of(c, q)) {  // deep queue: the head's overflow spills into the tail
       Spill sp = spill_of(c, s, l, q, s.tsum[l * 3 + q]);
       pend_apply<true, true>(c, Q, lane, q, n, p, seq0, row, &sp);
-      drops += deep_prune_wave(c, Q, lane, q, sp);
-      if (lane == 0) s.tsum[l * 3 + q] = spill_sum(sp);
+      const uint32_t pd = deep_prune_wave(c, Q, lane, q, sp);
+      drops += pd;
+      if (lane == 0) {
+        s.tsum[l * 3 + q] = spill_sum(sp);
+        if (pd) s.tseal[l * 3 + q].x = 0u;  // the prune moved items inside the tail: no seal
+      }
     } else {
       drops += pend_apply<true>(c, Q, lane, q, n, p, seq0, row);
     }
@@ -1204,8 +1211,6 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
 // dead sender).  Sender l's records to its j-th peer form GROUP l*fanout + j.
 constexpr uint32_t kPeerBatch = 4;
 __global__ void __launch_bounds__(256) peers_kernel(GCfg c, GState s, uint32_t round, uint32_t* __restrict__ grp_key) {
-  // deep queues: the emission's deferred-member lists start empty (one launch fewer than a memset)
-  if (c.deep && blockIdx.x == 0 && threadIdx.x < 4) s.deep_n[threadIdx.x] = 0u;
   const uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= c.n_loc) return;
   const uint32_t m = (uint32_t)(c.lo + l);
@@ -1558,7 +1563,14 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
       if (unsafe) {  // nothing committed: the whole-queue path redoes this member's emission
         // by the LDS capacity its largest queue needs: list 2 (kDeepTiny; from n_loc), list 0
         // (kDeepSmall; from the front), list 1 (the full depth; from the back)
-        const uint32_t need = c.qcap + max(max(tc0 + (pc & 0xFF), tc1 + ((pc >> 8) & 0xFF)), tc2 + ((pc >> 16) & 0xFF));
+        uint32_t need = c.qcap + max(max(tc0 + (pc & 0xFF), tc1 + ((pc >> 8) & 0xFF)), tc2 + ((pc >> 16) & 0xFF));
+        // only the intent queue in use with a sealed tail prefix: the deferred path reads the
+        // tail's recent part only (deep_wave_member's recent mode; it re-lists the member for the
+        // full depth if that cannot decide)
+        if (D0 && c.tcap0 && !ne1 && !ne2 && tc0 + (pc & 0xFF) <= c.tcap0) {
+          const uint32_t m0 = s.tseal[l * 3].x;
+          if (m0 && m0 <= tc0) need = c.qcap + (tc0 - m0) + (pc & 0xFF);
+        }
         if (lane == 0) {
           if (need <= kDeepTiny) s.deep_ids[c.n_loc + atomicAdd(s.deep_n + 2, 1u)] = (uint32_t)l;
           else if (need <= kDeepSmall) s.deep_ids[atomicAdd(s.deep_n, 1u)] = (uint32_t)l;
@@ -3049,6 +3061,14 @@ struct rsf_gossip {
   uint64_t* send_buf = nullptr;
   unsigned long long* d_counters = nullptr;  // [0] n_valid, [1..] shard bounds
   rsf::CubTemp sort_tmp;  // every radix sort of the round (sort_pairs)
+  // Peers ahead: once round t's emission has consumed the groups, round t + 1's peer draw and
+  // group sort (they depend on nothing but liveness and the round number) run on a second
+  // stream, under round t's merge / bucket exchange.  Round t + 1 uses them if nothing changed
+  // liveness in between (ahead_valid), else redraws.  RSF_PEERS_AHEAD=0 turns it off.
+  hipStream_t side = nullptr;
+  hipEvent_t ev_emitted = nullptr, ev_ahead = nullptr;
+  bool ahead_launched = false, ahead_valid = false, ahead_on = true;
+  uint32_t ahead_round = 0;
   int end_bit = 32;
   uint64_t last_sent = 0, last_merged = 0;
   uint32_t cur_round = 0;
@@ -3117,15 +3137,35 @@ static int ensure_lists(rsf_gossip* g, uint32_t n_ml, uint32_t n_acts) {
 constexpr size_t kZone = RSF_GUARD_ZONES ? (2u << 20) : 0;
 // every radix sort sizes its own temporary storage (rsf::cub_run)
 static int sort_pairs(rsf_gossip* g, const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout,
-                      uint64_t n) {
+                      uint64_t n, hipStream_t on = nullptr) {
   const int end_bit = g->end_bit;
-  hipStream_t st = g->stream;
+  hipStream_t st = on ? on : g->stream;
   return rsf::cub_run(
       g->sort_tmp, st,
       [&](void* t, size_t& b) {
         return hipcub::DeviceRadixSort::SortPairs(t, b, kin, kout, vin, vout, (int)n, 0, end_bit, st);
       },
       "group/record radix sort");
+}
+
+// the peers-ahead work in flight (if any) is joined by the context stream and dropped: before
+// anything changes liveness, or uses the group arrays / sort storage another way
+static int ahead_drop(rsf_gossip* g) {
+  if (g->ahead_launched) RSF_HIP(hipStreamWaitEvent(g->stream, g->ev_ahead, 0));
+  g->ahead_launched = g->ahead_valid = false;
+  return RSF_OK;
+}
+
+// peer draw + stable sort of the groups by receiver, on stream `st`
+static int peers_and_sort(rsf_gossip* g, uint32_t round, hipStream_t st) {
+  const GCfg& c = g->c;
+  hipLaunchKernelGGL(peers_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, c, g->s, round, g->grp_key);
+  RSF_HIP(hipGetLastError());
+  RSF_DBG_SYNC(st, "peers_kernel");
+  int rc = sort_pairs(g, g->grp_key, g->grp_key_s, g->grp_id, g->grp_id_s, g->n_groups, st);
+  if (rc) return rc;
+  RSF_DBG_SYNC(st, "group sort");
+  return RSF_OK;
 }
 
 extern "C" {
@@ -3216,6 +3256,14 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   if (hipStreamCreateWithFlags(&g->own, hipStreamNonBlocking) != hipSuccess)
     return fail(rsf::set_error(RSF_ERR_HIP, "hipStreamCreate failed"));
   g->stream = g->own;
+  if (hipStreamCreateWithFlags(&g->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&g->ev_emitted, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&g->ev_ahead, hipEventDisableTiming) != hipSuccess)
+    return fail(rsf::set_error(RSF_ERR_HIP, "hipStreamCreate / hipEventCreate failed"));
+  {
+    const char* e = getenv("RSF_PEERS_AHEAD");
+    g->ahead_on = !(e && e[0] == '0');
+  }
   GState& s = g->s;
   const uint64_t n = c.n_loc, S = c.S;
   int rc;
@@ -3235,7 +3283,8 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
     for (int q = 0; q < 3; ++q)
       if (tcap_of(c, q) && GA(q == 0 ? s.tail0 : q == 1 ? s.tail1 : s.tail2, n * tstride_of(c, q) * sizeof(uint4)))
         return fail(rc);
-    if (GA(s.tsum, n * 3 * sizeof(uint4)) || GA(s.deep_ids, n * 3 * 4)) return fail(rc);
+    if (GA(s.tsum, n * 3 * sizeof(uint4)) || GA(s.tseal, n * 3 * sizeof(uint4)) || GA(s.deep_ids, n * 3 * 4))
+      return fail(rc);
   }
   g->stage_cap = n * c.fanout * c.cap_t;
   if (g->stage_cap >= 0xFFFFFFFFull) return fail(gerr("n_members x fanout x per-target records must fit 32 bits"));
@@ -3327,7 +3376,10 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   hipLaunchKernelGGL(fill_u64_kernel, dim3(grid1(n)), dim3(256), 0, st, s.eclock, n, 1ull);
   hipLaunchKernelGGL(fill_u64_kernel, dim3(grid1(n)), dim3(256), 0, st, s.qclock, n, 1ull);
   hipLaunchKernelGGL(iota_u32_kernel, dim3(grid1(g->n_groups)), dim3(256), 0, st, g->grp_id, g->n_groups);
-  if (c.deep) hipLaunchKernelGGL(tsum_init_kernel, dim3(grid1(n * 3)), dim3(256), 0, st, s.tsum, n * 3);
+  if (c.deep) {  // empty tails, no sealed prefix (m = 0)
+    hipLaunchKernelGGL(tsum_init_kernel, dim3(grid1(n * 3)), dim3(256), 0, st, s.tsum, n * 3);
+    hipLaunchKernelGGL(tsum_init_kernel, dim3(grid1(n * 3)), dim3(256), 0, st, s.tseal, n * 3);
+  }
   if (hipStreamSynchronize(st) != hipSuccess) return fail(rsf::set_error(RSF_ERR_HIP, "context init sync failed"));
   *out = g;
   return RSF_OK;
@@ -3336,6 +3388,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
 int rsf_gossip_destroy(rsf_gossip* g) {
   if (!g) return RSF_OK;
   hipSetDevice(g->device);
+  if (g->side) hipStreamSynchronize(g->side);
   if (g->stream) hipStreamSynchronize(g->stream);
   GState& s = g->s;
   void* ptrs[] = {s.clock,  s.eclock,      s.qclock,       s.emin,        s.qmin,     s.digest,     s.err,
@@ -3348,7 +3401,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   g->grp_slot, g->grp_off, g->dec_base, s.dlog, s.dmeta, s.dcnt,
                   g->bkt_send, g->bkt_recv, g->bkt_dec, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn,
                   s.p_ent, s.p_cnt, g->big_base, tail_of(s, 0), tail_of(s, 1), tail_of(s, 2), s.tsum, s.deep_ids,
-                  g->qmax, g->d_act_status, g->occ_hist};
+                  s.tseal, g->qmax, g->d_act_status, g->occ_hist};
   for (void* p : ptrs)
     if (p) hipFree(p);
   g->scratch.release();
@@ -3363,6 +3416,9 @@ int rsf_gossip_destroy(rsf_gossip* g) {
     for (auto& row : g->ev)
       for (auto& e : row) hipEventDestroy(e);
   if (g->own) hipStreamDestroy(g->own);
+  if (g->side) hipStreamDestroy(g->side);
+  if (g->ev_emitted) hipEventDestroy(g->ev_emitted);
+  if (g->ev_ahead) hipEventDestroy(g->ev_ahead);
   delete g;
   return RSF_OK;
 }
@@ -3376,6 +3432,7 @@ int rsf_gossip_set_stream(rsf_gossip* g, void* st) {
 int rsf_gossip_sync(rsf_gossip* g) {
   if (!g) return gerr("null context");
   RSF_HIP(hipSetDevice(g->device));
+  if (g->ahead_launched) RSF_HIP(hipStreamSynchronize(g->side));
   RSF_HIP(hipStreamSynchronize(g->stream));
   return RSF_OK;
 }
@@ -3436,6 +3493,8 @@ int rsf_gossip_set_view(rsf_gossip* g, uint64_t m, uint32_t subj, uint8_t kind, 
 int rsf_gossip_set_alive(rsf_gossip* g, const uint8_t* alive) {
   if (!g || !alive) return gerr("null argument");
   RSF_HIP(hipSetDevice(g->device));
+  int rc = ahead_drop(g);  // liveness changes: peers drawn ahead are stale
+  if (rc) return rc;
   RSF_HIP(hipMemcpyAsync(g->s.alive, alive, g->c.N, hipMemcpyHostToDevice, g->stream));
   RSF_HIP(hipStreamSynchronize(g->stream));
   return RSF_OK;
@@ -3545,6 +3604,8 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
   RSF_HIP(hipSetDevice(g->device));
   int rc = ensure_lists(g, n_ml, n_acts);
   if (rc) return rc;
+  for (uint32_t e = 0; e < n_ml; ++e)  // liveness changes: peers drawn ahead are stale
+    if (ml[e].set_alive != 2 && (rc = ahead_drop(g))) return rc;
   hipStream_t st = g->stream;
   mark(g, 0);
   g->cur_round = round;
@@ -3680,6 +3741,20 @@ static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
   return RSF_OK;
 }
 
+// after round t's emission (the last reader of grp_key / grp_slot): round t + 1's peers and
+// group sort on the side stream
+static int launch_ahead(rsf_gossip* g, uint32_t round) {
+  if (!g->ahead_on) return RSF_OK;
+  RSF_HIP(hipEventRecord(g->ev_emitted, g->stream));
+  RSF_HIP(hipStreamWaitEvent(g->side, g->ev_emitted, 0));
+  int rc = peers_and_sort(g, round + 1, g->side);
+  if (rc) return rc;
+  RSF_HIP(hipEventRecord(g->ev_ahead, g->side));
+  g->ahead_launched = g->ahead_valid = true;
+  g->ahead_round = round + 1;
+  return RSF_OK;
+}
+
 static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t world = 0) {
   const GCfg& c = g->c;
   hipStream_t st = g->stream;
@@ -3688,12 +3763,13 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
     hipLaunchKernelGGL(dec_fill_kernel, dim3(grid1(g->round_need)), dim3(256), 0, st, (const rsf_rumor*)g->s.rumors,
                        g->s.rdec, g->s.rbody, (uint64_t)(g->round_base & c.rmask), (uint64_t)g->round_need);
   RSF_DBG_SYNC(st, "dec_fill_kernel");
-  hipLaunchKernelGGL(peers_kernel, dim3(grid1(c.n_loc)), dim3(256), 0, st, c, g->s, round, g->grp_key);
-  RSF_HIP(hipGetLastError());
-  RSF_DBG_SYNC(st, "peers_kernel");
-  int rc = sort_pairs(g, g->grp_key, g->grp_key_s, g->grp_id, g->grp_id_s, ng);
-  if (rc) return rc;
-  RSF_DBG_SYNC(st, "group sort");
+  // this round's peers and group order: drawn ahead under the previous round, or now
+  const bool use_ahead = g->ahead_valid && g->ahead_round == round;
+  if (g->ahead_launched) RSF_HIP(hipStreamWaitEvent(st, g->ev_ahead, 0));
+  g->ahead_launched = g->ahead_valid = false;
+  int rc;
+  if (!use_ahead && (rc = peers_and_sort(g, round, st))) return rc;
+  if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 16, st));  // the emission's deferred-member lists
   RSF_HIP(hipMemsetAsync(g->grp_cnt, 0, ng * 4, st));
   if (local) {
     RSF_HIP(hipMemsetAsync(g->seg_start, 0, c.n_loc * 4, st));
@@ -3714,6 +3790,7 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
     RSF_DBG_SYNC(st, "grp_index_kernel");
     mark(g, 2);
     if ((rc = launch_emit<true>(g, egrid, bk))) return rc;
+    if ((rc = launch_ahead(g, round))) return rc;
     mark(g, 3);
     return RSF_OK;
   }
@@ -3724,6 +3801,8 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
   mark(g, 2);
   if ((rc = launch_emit<false>(g, egrid, Buckets{}))) return rc;
   RSF_DBG_SYNC(st, "emit_kernel");
+  // the counts path reads the sorted groups after the emission (grp_expand_kernel): no ahead
+  if (local && (rc = launch_ahead(g, round))) return rc;
   if (local) {
     unsigned long long* sum = (unsigned long long*)g->d_counters;
     const uint32_t* cnt = g->grp_cnt;
@@ -4411,25 +4490,28 @@ int rsf_gossip_dump_view(rsf_gossip* g, uint64_t* ltime, uint8_t* status, uint8_
 }
 
 // head and tail merged on the host into [n_loc][3][D] in send order
-// every queue merged from head and tail (tail only on deep contexts), sorted, first D items
+// every queue of local rows [r0, r0 + n) merged from head and tail (tail only on deep
+// contexts), sorted, first D items; output row 0 = local row r0
 static int dump_queues_deep(rsf_gossip* g, uint32_t D, uint32_t* rumor, uint32_t* seq, uint16_t* tx, uint16_t* len,
-                            uint32_t* max_live) {
+                            uint32_t* max_live, uint64_t r0 = 0, uint64_t rows = ~0ull) {
   const GCfg& c = g->c;
-  const uint64_t n = c.n_loc, hc = n * 3 * c.qcap;
+  const uint64_t n = std::min<uint64_t>(rows, c.n_loc - r0), hc = n * 3 * c.qcap;
   uint32_t most = 0;
   std::vector<uint32_t> hr(hc), hs(hc), ht(hc);
   std::vector<uint4> sum(n * 3);
   std::vector<std::vector<uint4>> tail(3);
   hipStream_t st = g->stream;
-  RSF_HIP(hipMemcpyAsync(hr.data(), g->s.q_rumor, hc * 4, hipMemcpyDeviceToHost, st));
-  RSF_HIP(hipMemcpyAsync(hs.data(), g->s.q_seq, hc * 4, hipMemcpyDeviceToHost, st));
-  RSF_HIP(hipMemcpyAsync(ht.data(), g->s.q_txlen, hc * 4, hipMemcpyDeviceToHost, st));
+  const uint64_t h0 = r0 * 3 * c.qcap;
+  RSF_HIP(hipMemcpyAsync(hr.data(), g->s.q_rumor + h0, hc * 4, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipMemcpyAsync(hs.data(), g->s.q_seq + h0, hc * 4, hipMemcpyDeviceToHost, st));
+  RSF_HIP(hipMemcpyAsync(ht.data(), g->s.q_txlen + h0, hc * 4, hipMemcpyDeviceToHost, st));
   // tails and their summaries exist only on deep contexts; otherwise every queue is its head
-  if (c.deep) RSF_HIP(hipMemcpyAsync(sum.data(), g->s.tsum, n * 3 * 16, hipMemcpyDeviceToHost, st));
+  if (c.deep) RSF_HIP(hipMemcpyAsync(sum.data(), g->s.tsum + r0 * 3, n * 3 * 16, hipMemcpyDeviceToHost, st));
   for (uint32_t q = 0; q < 3; ++q)
     if (tcap_of(c, q)) {
       tail[q].resize(n * tstride_of(c, q));
-      RSF_HIP(hipMemcpyAsync(tail[q].data(), tail_of(g->s, q), tail[q].size() * 16, hipMemcpyDeviceToHost, st));
+      RSF_HIP(hipMemcpyAsync(tail[q].data(), tail_of(g->s, q) + r0 * tstride_of(c, q), tail[q].size() * 16,
+                             hipMemcpyDeviceToHost, st));
     }
   RSF_HIP(hipStreamSynchronize(st));
   std::vector<std::pair<uint64_t, uint32_t>> items;
@@ -4468,6 +4550,15 @@ int rsf_gossip_dump_queues_width(rsf_gossip* g, uint32_t width, uint32_t* rumor,
   if (rc) return rc;
   RSF_HIP(hipMemcpyAsync(next_seq, g->s.q_next_seq, g->c.n_loc * 3 * 4, hipMemcpyDeviceToHost, g->stream));
   return dump_queues_deep(g, width, rumor, seq, tx, len, max_live);
+}
+
+int rsf_gossip_dump_queues_rows(rsf_gossip* g, uint64_t row0, uint64_t rows, uint32_t width, uint32_t* rumor,
+                                uint32_t* seq, uint16_t* tx, uint16_t* len, uint32_t* max_live) {
+  if (!g || !rumor || !seq || !tx || !len || !width || row0 + rows > g->c.n_loc) return gerr("bad argument");
+  RSF_HIP(hipSetDevice(g->device));
+  int rc = flush_pending(g);
+  if (rc) return rc;
+  return dump_queues_deep(g, width, rumor, seq, tx, len, max_live, row0, rows);
 }
 
 int rsf_gossip_dump_queues(rsf_gossip* g, uint32_t* rumor, uint32_t* seq, uint16_t* tx, uint16_t* len,
@@ -4800,7 +4891,10 @@ __global__ void __launch_bounds__(256) snap_reset_kernel(GCfg c, GState s, const
     s.q_txlen[l * 3 * c.qcap + j] = 0;
   }
   if (threadIdx.x < 3) s.q_next_seq[l * 3 + threadIdx.x] = 0;
-  if (threadIdx.x < 3 && s.tsum) s.tsum[l * 3 + threadIdx.x] = kTSumEmpty;  // deep queues: empty tails
+  if (threadIdx.x < 3 && s.tsum) {  // deep queues: empty tails
+    s.tsum[l * 3 + threadIdx.x] = kTSumEmpty;
+    s.tseal[l * 3 + threadIdx.x] = kTSumEmpty;
+  }
   if (threadIdx.x == 0) s.p_cnt[l] = 0;  // nothing pending either
   for (uint32_t j = threadIdx.x; j < c.ebuf; j += blockDim.x) {
     s.eb_ltime[l * c.ebuf + j] = 0;

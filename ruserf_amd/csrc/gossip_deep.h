@@ -209,8 +209,10 @@ __device__ void deep_store_queue(const GCfg& c, const GState& s, uint64_t l, uin
       if (q == 0) s.q_dec[l * c.qcap + slot] = h ? d.hdec[tid] : 0u;
     }
   }
-  if (tid == 0 && tcap_of(c, q)) s.tsum[l * 3 + q] = d.tn ? make_uint4(d.tn, tlmin, (uint32_t)tmin, (uint32_t)(tmin >> 32))
-                                                      : kTSumEmpty;
+  if (tid == 0 && tcap_of(c, q)) {  // exact bounds; the whole tail sealed
+    s.tsum[l * 3 + q] = d.tn ? make_uint4(d.tn, tlmin, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
+    s.tseal[l * 3 + q] = d.tn ? make_uint4(d.tn, (uint32_t)tmin, (uint32_t)(tmin >> 32), 0u) : kTSumEmpty;
+  }
   __syncthreads();
 }
 
@@ -594,10 +596,11 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
 }
 
 // the live items not in the head back to the tail (compacted, any order); returns the count
+// (at tail[t_lo ...]: the recent mode keeps the sealed prefix tail[0, t_lo) in place)
 template <uint32_t CAP>
 __device__ uint32_t w_store_tail(const GCfg& c, const GState& s, uint64_t l, uint32_t q, const DeepWave<CAP>& d,
-                                 uint32_t lane, uint32_t n) {
-  uint4* const t = tcap_of(c, q) ? tail_of(s, q) + l * tstride_of(c, q) : nullptr;
+                                 uint32_t lane, uint32_t n, uint32_t t_lo = 0) {
+  uint4* const t = tcap_of(c, q) ? tail_of(s, q) + l * tstride_of(c, q) + t_lo : nullptr;
   uint32_t base = 0;
   for (uint32_t b = 0; b < n; b += kWave) {
     const uint32_t i = b + lane;
@@ -618,11 +621,13 @@ __device__ uint32_t w_store_tail(const GCfg& c, const GState& s, uint64_t l, uin
 // empty queues cost nothing and the tail loads start at once.
 struct DeepPre {
   uint32_t pc, gk, gs, qinfo, qseq;
+  uint32_t sm, tly;  // lane q < 3: the sealed prefix's count (tseal.x) and the tail's length bound (tsum.y)
+  uint64_t sb;       // lane q < 3: the sealed prefix's key bound
 };
 __device__ __forceinline__ DeepPre deep_pre(const GCfg& c, const GState& s, uint64_t l, uint32_t lane,
                                             const uint32_t* __restrict__ grp_key,
                                             const uint32_t* __restrict__ slot) {
-  DeepPre p{0u, kSentinel, 0u, 0u, 0u};
+  DeepPre p{0u, kSentinel, 0u, 0u, 0u, 0u, ~0u, ~0ull};
   if (l >= c.n_loc) return p;
   p.pc = s.p_cnt[l];
   if (lane < c.fanout) {
@@ -632,8 +637,13 @@ __device__ __forceinline__ DeepPre deep_pre(const GCfg& c, const GState& s, uint
   if (lane < 3) {
     p.qseq = s.q_next_seq[l * 3 + lane];
     const uint32_t r0 = s.q_rumor[(l * 3 + lane) * c.qcap];
-    const uint32_t tcq = tcap_of(c, lane) ? s.tsum[l * 3 + lane].x : 0u;
-    p.qinfo = (r0 != kEmpty ? 1u : 0u) | (tcq << 1);
+    const bool dq = tcap_of(c, lane) != 0;
+    const uint4 ts = dq ? s.tsum[l * 3 + lane] : kTSumEmpty;
+    const uint4 se = dq ? s.tseal[l * 3 + lane] : kTSumEmpty;
+    p.qinfo = (r0 != kEmpty ? 1u : 0u) | (ts.x << 1);
+    p.tly = ts.y;
+    p.sm = se.x;
+    p.sb = ((uint64_t)se.z << 32) | se.y;
   }
   return p;
 }
@@ -707,12 +717,26 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
     QRegs Q{kEmpty, 0, 0};
     q_load(c, s, l, q, lane, Q);
     const uint32_t tc = qi >> 1;
-    const uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
+    // RECENT mode (tseal): only the intent queue in use and a sealed tail prefix: load the
+    // tail's recent part tail[sm, tc) only; valid if the refilled head is full and its largest
+    // key is below the seal's bound (else the member is re-listed for the full depth before
+    // anything is stored -- the intent queue is the first one processed).  The full-depth class
+    // always loads everything.
+    const uint32_t sm = shfl_u32(pre.sm, (int)q);
+    const bool others_empty = q == 0 && shfl_u32(qinfo, 1) == 0 && shfl_u32(qinfo, 2) == 0 && ((pc >> 8) & 0xFFFF) == 0;
+    const bool recent = CAP < kDeepBig && others_empty && sm > 0 && sm <= tc && tc + nq <= tcap_of(c, q);
+    const uint32_t t_lo = recent ? sm : 0u;
+    const uint32_t tn = tc - t_lo;  // tail items loaded
+    if (q == 0 && !recent && c.qcap + tc + nq > CAP) {  // (emit_run listed it by the recent part's need)
+      if (lane == 0) s.deep_ids[c.n_loc * 3 - 1 - atomicAdd(s.deep_n + 1, 1u)] = (uint32_t)l;
+      return;
+    }
+    const uint4* const t = tail_of(s, q) + l * tstride_of(c, q) + t_lo;
     uint4 e[kDeepU];
 #pragma unroll
     for (uint32_t u = 0; u < kDeepU; ++u) {
       const uint32_t i = u * kWave + lane;
-      e[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
+      e[u] = i < tn ? t[i] : make_uint4(0, 0, 0, 0);
     }
     if (!pend_lds) {
       d.pend[lane].rid = pr0;
@@ -735,7 +759,7 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
 #pragma unroll
       for (uint32_t u = 0; u < kDeepU; ++u) {
         const uint32_t i = b + u * kWave + lane;
-        if (i < tc) {
+        if (i < tn) {
           d.key[hn + i] = tlq_key(e[u].z & 0xFFFF, e[u].z >> 16, e[u].y);
           d.rid[hn + i] = e[u].x;
           d.dec[hn + i] = q == 0 ? e[u].w : qdec;
@@ -743,14 +767,14 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
         }
       }
       b += kDeepU * kWave;
-      if (b >= tc) break;
+      if (b >= tn) break;
 #pragma unroll
       for (uint32_t u = 0; u < kDeepU; ++u) {  // the next kDeepU * 64 (queues past 512 items)
         const uint32_t i = b + u * kWave + lane;
-        e[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
+        e[u] = i < tn ? t[i] : make_uint4(0, 0, 0, 0);
       }
     }
-    uint32_t n = hn + tc;
+    uint32_t n = hn + tn;
     if (n == 0 && nq == 0) continue;
     wsync();
     if (nq) {
@@ -791,6 +815,35 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
     RSF_DEEP_T(9);
     w_take_head(c, d, lane, n, q, Q, tmin, tminlen);
     RSF_DEEP_T(10);
+    // recent mode: exact only if the head is full and below every sealed key; the sealed
+    // prefix stays in the tail, so the tail's bounds include the seal's
+    auto relist_full = [&]() {  // nothing stored yet: the full-depth class redoes the member
+      for (uint32_t i = lane; i < n; i += kWave) d.st[i] = kDeepDead;
+      wsync();
+      if (lane == 0) s.deep_ids[c.n_loc * 3 - 1 - atomicAdd(s.deep_n + 1, 1u)] = (uint32_t)l;
+#if RSF_DEEP_PROF
+      if (lane == 0) s_dprof[30] += 1ull;
+#endif
+    };
+    if (recent) {
+      const uint64_t hm = ballot(lane < c.qcap && Q.r != kEmpty);
+      bool ok = (uint32_t)__popcll(hm) == c.qcap;
+      if (ok) {
+        const int hl = 63 - __clzll((long long)hm);
+        const uint32_t tlh = shfl_u32(Q.tl, hl);
+        ok = tlq_key(tlh & 0xFFFF, tlh >> 16, shfl_u32(Q.sq, hl)) < shfl_u64(pre.sb, (int)q);
+      }
+      if (!ok) {
+        relist_full();
+        return;
+      }
+      const uint64_t sb = shfl_u64(pre.sb, (int)q);
+      tmin = sb < tmin ? sb : tmin;
+      tminlen = min(tminlen, shfl_u32(pre.tly, (int)q));
+#if RSF_DEEP_PROF
+      if (lane == 0) s_dprof[29] += 1ull;
+#endif
+    }
     const uint32_t used_0 = used_v, nrec_0 = nrec_v;
     bool unsafe = false, dirty = false;
     uint32_t errq = 0;
@@ -801,12 +854,21 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
       q_pick_peers<false, true>(c, Q, lane, np, used_v, nrec_v, off_v, ov, od, errq, dirty, d.row, nullptr, tmin,
                                 tminlen, &unsafe);
     RSF_DEEP_T(11);
+    if (unsafe && recent) {
+      relist_full();
+      return;
+    }
     if (!unsafe) {
       err |= errq;
       q_store(c, s, l, q, lane, Q, true);
-      const uint32_t cnt = w_store_tail(c, s, l, q, d, lane, n);
-      if (lane == 0 && tcap_of(c, q))
-        s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
+      const uint32_t cnt = t_lo + w_store_tail(c, s, l, q, d, lane, n, t_lo);
+      if (lane == 0 && tcap_of(c, q)) {
+        // the tail from here on is sealed: every item's key >= tmin (exact over the items this
+        // refill wrote, the seal's bound over the prefix it kept)
+        const uint4 sum = cnt ? make_uint4(cnt, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
+        s.tsum[l * 3 + q] = sum;
+        s.tseal[l * 3 + q] = cnt ? make_uint4(cnt, (uint32_t)tmin, (uint32_t)(tmin >> 32), 0u) : kTSumEmpty;
+      }
       RSF_DEEP_T(12);
     } else {
       // the head still cannot decide: get_broadcasts over every item, peer by peer
@@ -864,8 +926,10 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
       w_take_head(c, d, lane, n, q, Q, tmin, tminlen);
       q_store(c, s, l, q, lane, Q, true);
       const uint32_t cnt = w_store_tail(c, s, l, q, d, lane, n);
-      if (lane == 0 && tcap_of(c, q))
+      if (lane == 0 && tcap_of(c, q)) {
         s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
+        s.tseal[l * 3 + q] = cnt ? make_uint4(cnt, (uint32_t)tmin, (uint32_t)(tmin >> 32), 0u) : kTSumEmpty;
+      }
       RSF_DEEP_T(14);
 #if RSF_DEEP_PROF
       if (lane == 0) s_dprof[15] += 1ull;
@@ -989,8 +1053,10 @@ __device__ __forceinline__ uint32_t tail_expire_wave(const GCfg& c, const GState
     kept += (uint32_t)__popcll(km);
     gone += (uint32_t)__popcll(ballot(stale));
   }
-  if (gone && lane == 0)
+  if (gone && lane == 0) {  // exact bounds over what is kept; the whole tail sealed
     s.tsum[l * 3 + q] = kept ? make_uint4(kept, lmin, (uint32_t)kmin, (uint32_t)(kmin >> 32)) : kTSumEmpty;
+    s.tseal[l * 3 + q] = kept ? make_uint4(kept, (uint32_t)kmin, (uint32_t)(kmin >> 32), 0u) : kTSumEmpty;
+  }
   return gone;
 }
 

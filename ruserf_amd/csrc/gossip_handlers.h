@@ -102,6 +102,14 @@ struct GState {
   // the tail cannot fit; any other member takes the exact whole-queue path (emit_deep_wave_kernel).
   uint4 *tail0, *tail1, *tail2;
   uint4* tsum;       // [n_loc][3]
+  // Sealed tail prefix (a hint for the deferred path): tseal[l * 3 + q] = {m, B lo, B hi, -}:
+  // every item of tail[0, m) has a key >= B.  The deferred path then refills the head from the
+  // head, the pending list and only the RECENT part tail[m, count) -- the items spilled since
+  // the last refill -- whenever the qcap-th smallest of those is below B (no sealed item can
+  // precede it), instead of reading the whole tail; each refill seals what it leaves.  Spills
+  // append past m and keep it valid; any writer that moves items inside [0, m) reseals (exact)
+  // or sets m = 0.
+  uint4* tseal;      // [n_loc][3]
   uint32_t* deep_ids;  // [n_loc * 3] members deferred to emit_deep_wave_kernel (two lists), or queues to prune
   uint32_t* deep_n;    // [3] the lists' lengths (reset before each emission)
 };
@@ -519,6 +527,7 @@ __device__ __forceinline__ bool tail_prune_serial(const GCfg& c, const GState& s
   }
   t[ti] = t[cnt - 1];
   s.tsum[l * 3 + q] = make_uint4(cnt - 1, sm.y, sm.z, sm.w);
+  s.tseal[l * 3 + q].x = 0u;  // an item moved into the sealed prefix: no seal
   return true;
 }
 

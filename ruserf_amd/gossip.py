@@ -456,6 +456,18 @@ class GossipEngine:
         check(lib().rsf_gossip_queue_lengths(self._h, ptr(out, C.c_uint32)))
         return out.reshape(self.n_loc, 3)
 
+    def queues_rows(self, row0, rows, width):
+        """queues of local rows [row0, row0 + rows), each queue's first `width` items in send
+        order: (rumor, seq, transmits, len) arrays shaped [rows, 3, width]"""
+        n = rows * 3 * width
+        r, sq = np.zeros(n, dtype=np.uint32), np.zeros(n, dtype=np.uint32)
+        tx, ln = np.zeros(n, dtype=np.uint16), np.zeros(n, dtype=np.uint16)
+        ml = C.c_uint32()
+        check(lib().rsf_gossip_dump_queues_rows(self._h, row0, rows, width, ptr(r, C.c_uint32), ptr(sq, C.c_uint32),
+                                                ptr(tx, C.c_uint16), ptr(ln, C.c_uint16), C.byref(ml)))
+        self.max_live = ml.value
+        return tuple(a.reshape(rows, 3, width) for a in (r, sq, tx, ln))
+
     def buffers(self):
         c = self.cfg
         n = self.n_loc
