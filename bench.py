@@ -40,6 +40,9 @@ SEED = 0x5EED5EED
 # writes self 88 + window slot 8 + window index 4 + filter sample 8 + filter meta 4  (D=8, W=20, F=3)
 VIVALDI_BYTES = 492
 HBM_PEAK_GBS = 8000.0
+# the gossip headline runs the reference's queue regime: the intent queue deep enough that
+# nothing is dropped between QueueChecker ticks (4096 after a tick + ~24 a round x 150 rounds)
+DEFAULT_QUEUE_DEPTH = 8704
 
 
 class CudaArray:
@@ -224,19 +227,20 @@ def cpu_baseline_vivaldi(seconds_target=8.0):
                       f"{cpu_info()}"}
 
 
-def configs1_point(args, rank, world, queue_cap, settle, warmup, steps, queue_depth=0):
-    """One more gossip measurement at configs[1]'s 1M members (see main)."""
+def model_point(args, rank, world, members):
+    """One more gossip measurement with the bounded 64-slot queues (see main)."""
     from bench_gossip import run_gossip
     a = argparse.Namespace(**vars(args))
-    a.members, a.queue_cap, a.settle, a.warmup, a.steps = 1_000_000, queue_cap, settle, warmup, steps
-    a.queue_depth = queue_depth
-    a.check_every = 150 if queue_depth else 0
+    a.members, a.queue_cap, a.settle = members, 64, None
+    a.queue_depth, a.check_every = 0, 0
     torch.cuda.empty_cache()
     r = run_gossip(a, rank, world)
     keep = ["value", "unit", "ms_per_step", "merges_per_s", "records_per_round_per_gpu", "queue_pruned_per_round",
-            "queue_pruned_per_merged_record", "error_members", "cub_canaries_intact", "phases_ms_per_round",
-            "deep_path_members_per_round", "queue_regime"]
-    out = {"metric": r["metric"], "steps": steps, "warmup": warmup, **{k: r[k] for k in keep}, "config": r["config"]}
+            "queue_pruned_per_merged_record", "error_members", "cub_canaries_intact", "phases_ms_per_round"]
+    out = {"metric": r["metric"], "steps": args.steps, "warmup": args.warmup, **{k: r[k] for k in keep},
+           "config": r["config"],
+           "what": "model point: queues bounded at 64 slots, pruned on insert (the reference's queues are "
+                   "unbounded between QueueChecker ticks); not the reference's regime"}
     out["roofline"] = {k: r["roofline"][k] for k in ["bound", "achieved", "peak", "unit", "frac", "kernel",
                                                       "bytes_per_launch", "avg_launch_ms"]}
     return out
@@ -319,9 +323,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--queue-cap", type=int, default=64,
                     help="gossip: slots per transmit-limited queue (1..256; the reference's max_queue_depth is 4096)")
-    ap.add_argument("--queue-depth", type=int, default=0,
+    ap.add_argument("--queue-depth", type=int, default=None,
                     help="gossip: intent queue depth above --queue-cap (<= 64): a register head plus an HBM tail, "
-                         "pruned only by the QueueChecker (the reference's max_queue_depth is 4096)")
+                         "pruned only by the QueueChecker every --check-every rounds (the reference's regime; default "
+                         "8192: max_queue_depth 4096 plus what 150 rounds add between ticks); 0: the bounded "
+                         "--queue-cap model")
     ap.add_argument("--check-every", type=int, default=None,
                     help="gossip: a QueueChecker tick (prune to max_queue_depth 4096) every K rounds inside the round "
                          "loop, the timed window ending with one (default: 150 with --queue-depth, else none)")
@@ -335,6 +341,8 @@ def main():
     ap.add_argument("--vivaldi-exchange", choices=["targeted", "allgather"], default="targeted",
                     help="vivaldi, N>1, R=1: fetch only the round's remote peer rows, or all-gather the table")
     args = ap.parse_args()
+    if args.queue_depth is None:
+        args.queue_depth = DEFAULT_QUEUE_DEPTH if args.queue_cap <= 64 else 0
     if args.check_every is None:
         args.check_every = 150 if args.queue_depth else 0
     rank, world, local = env_rank()
@@ -387,24 +395,23 @@ def main():
             cpu = cpu_baseline_pushpull(args)
     else:
         from bench_gossip import run_gossip, cpu_baseline_gossip
-        args.members = args.members or 2_000_000
+        # BASELINE configs[1] (1M members on one MI355X; configs[2]'s 16M do not fit one GPU)
+        # in the reference's queue regime; per GPU under torch.distributed (weak scaling)
+        args.members = args.members or 1_000_000
         res = run_gossip(args, rank, world)
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline_gossip(args)
         attach_traffic(workload, res)
-        if world == 1 and not args.no_extra_points and args.members != 1_000_000:
-            # BASELINE configs[1] on one GPU (1M members, the same workload), at the default
-            # 64-slot queues (saturated: the flood fills every queue each round) and with the
-            # reference's queue: 4096 deep (64-slot register head + HBM tail), settled, nothing
-            # dropped between QueueChecker ticks
-            pts = [configs1_point(args, rank, world, 64, None, args.warmup, args.steps),
-                   configs1_point(args, rank, world, 64, None, args.warmup, args.steps, queue_depth=4096)]
-            # the deep queues' emission cost against the 64-slot queues', same box, same call
+        if world == 1 and not args.no_extra_points:
+            # labelled model points, same box, same call: the bounded 64-slot queue (prunes on
+            # insert, which the reference never does) at configs[1] and at configs[2]'s 2M shard
+            pts = [model_point(args, rank, world, 1_000_000), model_point(args, rank, world, 2_000_000)]
             e64 = pts[0]["phases_ms_per_round"].get("emit_kernel")
-            edeep = pts[1]["phases_ms_per_round"].get("emit_kernel")
-            pts[1]["emit_ms_vs_q64"] = (edeep / e64) if e64 and edeep else None
-            res["configs1_points"] = pts
+            edeep = res["phases_ms_per_round"].get("emit_kernel")
+            if res.get("queue_regime") and e64 and edeep:
+                res["queue_regime"]["emit_ms_vs_q64_same_call"] = edeep / e64
+            res["model_points_q64"] = pts
         if not args.no_vivaldi:
             # the metric's second half, timed in the same invocation (configs[4]: 64M members)
             vargs = argparse.Namespace(**vars(args))

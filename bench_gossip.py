@@ -177,7 +177,7 @@ def run_gossip(args, rank, world):
                   "pruned_at_last_tick_per_member": float(last["pruned"][0]) / per,
                   "members_over_warning_at_last_tick": int(last["warn"][0]),
                   "expired_whole_run": int(eng.expired().sum()),
-                  "deferred_per_round_by_class": dict(zip(["small", "middle", "full"],
+                  "deferred_per_round_by_class": dict(zip(["tiny", "small", "middle", "full"],
                                                           ((eng.deep_class_stats() - cls0) / args.steps).tolist()))
                   if depth else None}
     st = eng.members()
@@ -217,9 +217,13 @@ def run_gossip(args, rank, world):
         "ms_per_step": wall / args.steps * 1e3, "dtype": "u64",
         "config": {"workload": f"gossip rounds, {n} members ({per}/GPU), fanout k=3, {SUBJECTS} tracked subjects, "
                                f"1% of members originate a join/leave intent per round, member-state merge + "
-                               f"Lamport clocks ("
-                               + ("BASELINE configs[2] shard: 2M members/GPU, 16M at 8 GPUs)" if per == 2_000_000
-                                  else "BASELINE configs[1])" if per == 1_000_000 and world == 1 else "custom size)"),
+                               f"Lamport clocks, "
+                               + (f"the reference's queue regime (intent queue {cfg.depths()[0]} deep, QueueChecker "
+                                  f"prune to {MAX_QUEUE_DEPTH} every {check_every} rounds, settled {settle} rounds) "
+                                  if check_every else f"bounded {cfg.queue_cap}-slot queues (model point) ")
+                               + ("(BASELINE configs[2] shard: 2M members/GPU, 16M at 8 GPUs)" if per == 2_000_000
+                                  else "(BASELINE configs[1]: 1M members on one MI355X)" if per == 1_000_000 and world == 1
+                                  else "(1M members per GPU, weak scaling)" if per == 1_000_000 else "(custom size)"),
                    "members": n, "members_per_gpu": per, "fanout": 3, "items_per_target": 8,
                    "queue_cap_per_queue": cfg.queue_cap, "subjects": SUBJECTS,
                    "intent_queue_depth": cfg.depths()[0],

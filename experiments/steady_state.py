@@ -50,9 +50,12 @@ for t in range(rounds):
                "deferred_per_round": [(int(a) - int(b)) / every for a, b in zip(cls, cls0)],
                "bounded_pruned": pr - pr0, "expired": ex - ex0}
         if tick:
+            torch.cuda.synchronize()
+            tt = time.perf_counter()
             st = eng.check_queues(4096, 0, 128)
+            tick_ms = (time.perf_counter() - tt) * 1e3
             rec["tick"] = {"queued": int(st["queued"][0]), "pruned": int(st["pruned"][0]),
-                           "warn_members": int(st["warn"][0])}
+                           "warn_members": int(st["warn"][0]), "ms": round(tick_ms, 2)}
         print(json.dumps(rec), flush=True)
         cls0, pr0, ex0 = cls, pr, ex
         torch.cuda.synchronize()

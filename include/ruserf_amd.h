@@ -294,7 +294,7 @@ typedef struct rsf_gossip_cfg {
   uint32_t query_size_limit;   /* Options::query_size_limit (0 = the default 1024, options.rs:519); at most
                                   65534 (the model keeps a message's length in 16 bits) */
 } rsf_gossip_cfg;
-#define RSF_MAX_QUEUE_DEPTH 8256 /* head (<= 64) + tail: max_queue_depth 4096 plus what 150 rounds between
+#define RSF_MAX_QUEUE_DEPTH 8768 /* head (<= 64) + tail: max_queue_depth 4096 plus what 150 rounds between
                                     QueueChecker ticks add at the saturated bench workload (~24 a round) */
 
 /* One rumor (a broadcast message body; SerfBroadcast, core/src/broadcast.rs:153-183). 24 bytes. */
@@ -615,9 +615,10 @@ int rsf_gossip_dump_queues_rows(rsf_gossip* g, uint64_t row0, uint64_t rows, uin
 /* deep queues: members whose emission took the exact whole-queue path (the head alone could
  * not decide a pick; emit_deep_wave_kernel) since creation, and since the last call */
 int rsf_gossip_deep_stats(rsf_gossip* g, uint64_t* slow_total, uint64_t* slow_since_last);
-/* the same since creation per LDS capacity class of emit_deep_wave_kernel (host, 3 entries):
- * [0] the smallest class, [1] the middle one, [2] the full depth.  Synchronises. */
-int rsf_gossip_deep_class_stats(rsf_gossip* g, uint64_t* out3);
+/* the same since creation per LDS capacity class of emit_deep_wave_kernel (host, 4 entries):
+ * [0] the smallest class, [1] the small one, [2] the middle one, [3] the full depth (members the
+ * smaller classes re-list to it count twice).  Synchronises. */
+int rsf_gossip_deep_class_stats(rsf_gossip* g, uint64_t* out4);
 /* items queued per shard member and queue (host, [n_loc][3]: intent, query, event; head + tail),
  * after applying the pending lists (the QueueChecker's num_queued per node).  Synchronises. */
 int rsf_gossip_queue_lengths(rsf_gossip* g, uint32_t* out);

@@ -298,7 +298,7 @@ int orc_handle_user_event_cc(orc_world* w, uint32_t m, uint64_t ltime, uint64_t 
  * (MemberEventType, subject, ORC_LOG_MEMBER); the third word holds the flags */
 #define ORC_LOG_CC 1ull         /* a user event's cc flag */
 #define ORC_LOG_MEMBER 0x100ull /* a member event */
-#define ORC_MAX_QCAP 8320 /* slots per transmit-limited queue (the engine's head + tail depth range) */
+#define ORC_MAX_QCAP 8832 /* slots per transmit-limited queue (the engine's head + tail depth range) */
 int orc_world_set_delivery_log(orc_world* w, uint32_t per_member);
 int orc_handle_query(orc_world* w, uint32_t m, uint64_t ltime, uint32_t id, int no_broadcast);
 int orc_upsert_intent(orc_world* w, uint32_t m, uint32_t subj, uint8_t kind, uint64_t ltime);

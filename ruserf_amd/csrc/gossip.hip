@@ -1562,7 +1562,8 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
 #undef RSF_TB
       if (unsafe) {  // nothing committed: the whole-queue path redoes this member's emission
         // by the LDS capacity its largest queue needs: list 2 (kDeepTiny; from n_loc), list 0
-        // (kDeepSmall; from the front), list 1 (the full depth; from the back)
+        // (kDeepSmall; from the front), list 3 (kDeepMid; from 3 n_loc), list 1 (the full depth;
+        // from 3 n_loc - 1 down)
         uint32_t need = c.qcap + max(max(tc0 + (pc & 0xFF), tc1 + ((pc >> 8) & 0xFF)), tc2 + ((pc >> 16) & 0xFF));
         // only the intent queue in use with a sealed tail prefix: the deferred path reads the
         // tail's recent part only (deep_wave_member's recent mode; it re-lists the member for the
@@ -1574,6 +1575,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
         if (lane == 0) {
           if (need <= kDeepTiny) s.deep_ids[c.n_loc + atomicAdd(s.deep_n + 2, 1u)] = (uint32_t)l;
           else if (need <= kDeepSmall) s.deep_ids[atomicAdd(s.deep_n, 1u)] = (uint32_t)l;
+          else if (need <= kDeepMid) s.deep_ids[c.n_loc * 3 + atomicAdd(s.deep_n + 3, 1u)] = (uint32_t)l;
           else s.deep_ids[c.n_loc * 3 - 1 - atomicAdd(s.deep_n + 1, 1u)] = (uint32_t)l;
         }
         return;
@@ -2798,7 +2800,7 @@ __global__ void __launch_bounds__(256) seg_end_kernel(uint64_t n_loc, const uint
 // TransmitLimitedQueue::prune).  stats[q] = queued, stats[3 + q] = members at or above
 // the warning depth, stats[6 + q] = pruned.
 // Deep queues: numq counts the tail too, and a queue to prune is listed (s.deep_ids) for
-// check_deep_kernel, which keeps the max smallest keys of head and tail.
+// check_stream_kernel, which keeps the max smallest keys of head and tail.
 // qmax (non-null when min_queue_depth > 0): each member's own get_queue_max (queue_max_kernel).
 constexpr uint32_t kOccBin = 64, kOccBins = 160;  // occupancy histogram: 64-item bins up to 10240, then one overflow bin
 __global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uint32_t max_depth, uint32_t warn,
@@ -3050,7 +3052,8 @@ struct rsf_gossip {
   unsigned deep_blocks = 1;   // emit_deep_wave_kernel<kDeepSmall> grid (resident waves x CUs)
   unsigned deep_blocks_big = 1;  // emit_deep_wave_kernel<kDeepBig> grid
   unsigned deep_blocks_tiny = 1;  // emit_deep_wave_kernel<kDeepTiny> grid
-  unsigned deep_check_blocks = 1;  // check_deep_kernel grid
+  unsigned deep_blocks_mid = 1;   // emit_deep_wave_kernel<kDeepMid> grid
+  unsigned deep_check_blocks = 1;  // check_stream_kernel grid
   uint64_t deep_last = 0;     // rsf_gossip_deep_stats' previous total
   uint32_t* big_ids = nullptr;  // receivers deferred to merge_big_kernel (count: d_counters[52])
   uint32_t* qmax = nullptr;     // [n_loc] per-member get_queue_max (rsf_gossip_check_queues, min_queue_depth > 0)
@@ -3283,7 +3286,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
     for (int q = 0; q < 3; ++q)
       if (tcap_of(c, q) && GA(q == 0 ? s.tail0 : q == 1 ? s.tail1 : s.tail2, n * tstride_of(c, q) * sizeof(uint4)))
         return fail(rc);
-    if (GA(s.tsum, n * 3 * sizeof(uint4)) || GA(s.tseal, n * 3 * sizeof(uint4)) || GA(s.deep_ids, n * 3 * 4))
+    if (GA(s.tsum, n * 3 * sizeof(uint4)) || GA(s.tseal, n * 3 * sizeof(uint4)) || GA(s.deep_ids, n * 4 * 4))
       return fail(rc);
   }
   g->stage_cap = n * c.fanout * c.cap_t;
@@ -3316,18 +3319,21 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
       return fail(rsf::set_error(RSF_ERR_HIP, "occupancy query failed"));
     g->merge_blocks = (unsigned)std::max(1, per_cu * cus);
     if (c.deep) {
-      int dpc = 0, dpb = 0, dpk = 0, dpt = 1;
+      int dpc = 0, dpb = 0, dpk = 0, dpt = 0, dpm = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpc, emit_deep_wave_kernel<false, kDeepSmall>, kWave, 0) !=
               hipSuccess ||
-          (kDeepTiny && hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                            &dpt, emit_deep_wave_kernel<false, kDeepTiny ? kDeepTiny : kWave>, kWave, 0) != hipSuccess) ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpt, emit_deep_wave_kernel<false, kDeepTiny>, kWave, 0) !=
+              hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpm, emit_deep_wave_kernel<false, kDeepMid>, kWave, 0) !=
+              hipSuccess ||
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpb, emit_deep_wave_kernel<false, kDeepBig>, kWave, 0) !=
               hipSuccess ||
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpk, check_deep_kernel, kDeepThreads, 0) != hipSuccess)
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpk, check_stream_kernel, kDeepThreads, 0) != hipSuccess)
         return fail(rsf::set_error(RSF_ERR_HIP, "occupancy query failed"));
       g->deep_blocks = (unsigned)std::max(1, dpc * cus);
       g->deep_blocks_big = (unsigned)std::max(1, dpb * cus);
       g->deep_blocks_tiny = (unsigned)std::max(1, dpt * cus);
+      g->deep_blocks_mid = (unsigned)std::max(1, dpm * cus);
       g->deep_check_blocks = (unsigned)std::max(1, dpk * cus);
     }
   }
@@ -3722,12 +3728,13 @@ static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
 #undef RSF_EMIT_DEEP
     RSF_HIP(hipGetLastError());
     RSF_DBG_SYNC(st, "emit_kernel (deep)");
-    if (kDeepTiny)
-      hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepTiny ? kDeepTiny : kWave>), dim3(g->deep_blocks_tiny),
-                         dim3(kWave), 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec,
-                         bk, 2u, g->d_counters + 55);
+    // by capacity, the full depth last (the smaller classes re-list members to it)
+    hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepTiny>), dim3(g->deep_blocks_tiny), dim3(kWave), 0, st, c, g->s,
+                       g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 2u, g->d_counters + 55);
     hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepSmall>), dim3(g->deep_blocks), dim3(kWave), 0, st, c, g->s,
                        g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 0u, g->d_counters + 55);
+    hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepMid>), dim3(g->deep_blocks_mid), dim3(kWave), 0, st, c, g->s,
+                       g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 3u, g->d_counters + 55);
     hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepBig>), dim3(g->deep_blocks_big), dim3(kWave), 0, st, c, g->s,
                        g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 1u, g->d_counters + 55);
   } else if (c.qcap == kWave) {
@@ -4311,7 +4318,7 @@ int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t mi
                      depth_warning, g->d_counters + 40, qmax, g->occ_hist);
   RSF_HIP(hipGetLastError());
   if (c.deep) {  // the deep queues over the max: the smallest max keys of head and tail kept
-    hipLaunchKernelGGL(check_deep_kernel, dim3(g->deep_check_blocks), dim3(kDeepThreads), 0, g->stream, c, g->s,
+    hipLaunchKernelGGL(check_stream_kernel, dim3(g->deep_check_blocks), dim3(kDeepThreads), 0, g->stream, c, g->s,
                        max_depth, qmax);
     RSF_HIP(hipGetLastError());
   }
@@ -4598,16 +4605,18 @@ int rsf_gossip_deep_stats(rsf_gossip* g, uint64_t* slow_total, uint64_t* slow_si
   return RSF_OK;
 }
 
-int rsf_gossip_deep_class_stats(rsf_gossip* g, uint64_t* out3) {
-  if (!g || !out3) return gerr("null argument");
-  unsigned long long t[3];
+int rsf_gossip_deep_class_stats(rsf_gossip* g, uint64_t* out4) {
+  if (!g || !out4) return gerr("null argument");
+  unsigned long long t[8];
   RSF_HIP(hipSetDevice(g->device));
-  // lists 0 (kDeepSmall), 1 (the full depth), 2 (kDeepTiny): counters 55 - kDeepClassOff + list
+  // lists 0 (kDeepSmall), 1 (the full depth), 2 (kDeepTiny) at counters 55 - kDeepClassOff + list,
+  // list 3 (kDeepMid) at 56
   RSF_HIP(hipMemcpyAsync(t, g->d_counters + 55 - kDeepClassOff, sizeof(t), hipMemcpyDeviceToHost, g->stream));
   RSF_HIP(hipStreamSynchronize(g->stream));
-  out3[0] = t[2];
-  out3[1] = t[0];
-  out3[2] = t[1];
+  out4[0] = t[2];
+  out4[1] = t[0];
+  out4[2] = t[7];
+  out4[3] = t[1];
   return RSF_OK;
 }
 

@@ -9,213 +9,34 @@
 // below the tail's key bound, every stop one no tail item could fit) and commits; otherwise it
 // stores nothing and lists the member for emit_deep_wave_kernel (below), which redoes that
 // member's emission with every item of its queues in LDS.  The block routines first in this file
-// run the QueueChecker's prune (check_deep_kernel).
+// run the QueueChecker's prune (check_stream_kernel).
 #pragma once
 
 namespace {
 
 constexpr uint32_t kDeepThreads = 256;
+// tail items a refill leaves unsealed past the head (w_store_tail, check_stream_kernel)
+constexpr uint32_t kDeepReserve = 128;
+// items per thread / lane in flight in the tail loads and LDS scans
+constexpr uint32_t kDeepU = 8;
 constexpr uint32_t kDeepWaves = kDeepThreads / kWave;
 enum : uint8_t { kDeepDead = 0, kDeepLive = 1, kDeepPicked = 2 };
-
-struct DeepLds {
-  uint64_t key[kDeepItems];
-  uint32_t rid[kDeepItems];
-  uint32_t dec[kDeepItems];
-  uint8_t st[kDeepItems];
-  GState::PendE pend[kPend];
-  uint32_t hist[256];
-  uint64_t hkey[kWave];
-  uint32_t hrid[kWave], hdec[kWave];
-  uint64_t w64[kDeepWaves];
-  uint32_t w32[kDeepWaves];
-  uint64_t off[8];
-  uint32_t* oc[8];
-  uint32_t used[8], nrec[8];
-  uint32_t sel_digit, sel_need, sel_idx, hn, tn, np, err, drops;
-};
 
 __device__ __forceinline__ uint32_t key_len(uint64_t k) { return 0xFFFFu - (uint32_t)((k >> 32) & 0xFFFF); }
 __device__ __forceinline__ uint32_t key_seq(uint64_t k) { return 0xFFFFFFFFu - (uint32_t)k; }
 __device__ __forceinline__ uint32_t key_tl(uint64_t k) { return (uint32_t)(k >> 48) | (key_len(k) << 16); }
 
-// block-wide reductions (every thread calls; the result is block-uniform)
-__device__ __forceinline__ uint64_t blk_min_u64(uint64_t v, DeepLds& d) {
-  v = wave_min_u64(v);
-  __syncthreads();
-  if ((threadIdx.x & (kWave - 1)) == 0) d.w64[threadIdx.x / kWave] = v;
-  __syncthreads();
-  uint64_t m = d.w64[0];
+// wave AND / OR by butterfly shuffles (every lane gets the result)
+__device__ __forceinline__ uint64_t wave_and_u64_blk(uint64_t v) {
 #pragma unroll
-  for (uint32_t w = 1; w < kDeepWaves; ++w) m = d.w64[w] < m ? d.w64[w] : m;
-  return m;
+  for (int o = 32; o > 0; o >>= 1) v &= (uint64_t)__shfl_xor((long long)v, o);
+  return v;
 }
-__device__ __forceinline__ uint32_t blk_min_u32(uint32_t v, DeepLds& d) {
-  v = wave_min_u32(v);
-  __syncthreads();
-  if ((threadIdx.x & (kWave - 1)) == 0) d.w32[threadIdx.x / kWave] = v;
-  __syncthreads();
-  uint32_t m = d.w32[0];
+__device__ __forceinline__ uint64_t wave_or_u64_blk(uint64_t v) {
 #pragma unroll
-  for (uint32_t w = 1; w < kDeepWaves; ++w) m = min(m, d.w32[w]);
-  return m;
+  for (int o = 32; o > 0; o >>= 1) v |= (uint64_t)__shfl_xor((long long)v, o);
+  return v;
 }
-__device__ __forceinline__ uint32_t blk_sum_u32(uint32_t v, DeepLds& d) {
-  v = wave_inclusive_sum_u32(v);
-  v = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-  __syncthreads();
-  if ((threadIdx.x & (kWave - 1)) == 0) d.w32[threadIdx.x / kWave] = v;
-  __syncthreads();
-  uint32_t m = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < kDeepWaves; ++w) m += d.w32[w];
-  return m;
-}
-
-// The k-th smallest (1-based) key of the live items [0, n) -- keys are distinct -- by an 8-bit
-// radix select: per digit a histogram of the candidates still matching the decided prefix,
-// then the digit where the running count reaches k.
-__device__ uint64_t blk_select_kth(DeepLds& d, uint32_t n, uint32_t k) {
-  const uint32_t tid = threadIdx.x;
-  uint64_t prefix = 0, mask = 0;
-  uint32_t need = k;
-  for (int shift = 56; shift >= 0; shift -= 8) {
-    __syncthreads();
-    for (uint32_t i = tid; i < 256; i += kDeepThreads) d.hist[i] = 0;
-    __syncthreads();
-    for (uint32_t i = tid; i < n; i += kDeepThreads)
-      if (d.st[i] != kDeepDead && (d.key[i] & mask) == prefix) atomicAdd(&d.hist[(d.key[i] >> shift) & 0xFF], 1u);
-    __syncthreads();
-    if (tid < kWave) {  // running counts over the 256 bins, four per lane
-      const uint32_t h0 = d.hist[4 * tid], h1 = d.hist[4 * tid + 1], h2 = d.hist[4 * tid + 2], h3 = d.hist[4 * tid + 3];
-      const uint32_t sum = h0 + h1 + h2 + h3, incl = wave_inclusive_sum_u32(sum), excl = incl - sum;
-      if (excl < need && need <= incl) {
-        uint32_t b = 0, acc = excl;
-        if (acc + h0 < need) {
-          acc += h0;
-          b = 1;
-          if (acc + h1 < need) {
-            acc += h1;
-            b = 2;
-            if (acc + h2 < need) {
-              acc += h2;
-              b = 3;
-            }
-          }
-        }
-        d.sel_digit = 4 * tid + b;
-        d.sel_need = need - acc;
-      }
-    }
-    __syncthreads();
-    prefix |= (uint64_t)d.sel_digit << shift;
-    mask |= 0xFFull << shift;
-    need = d.sel_need;
-  }
-  return prefix;
-}
-
-// the queue's live items into LDS: the head's live prefix at [0, hn), the tail after it;
-// returns n = hn + tail count (block-uniform)
-__device__ uint32_t deep_load_queue(const GCfg& c, const GState& s, uint64_t l, uint32_t q, DeepLds& d) {
-  const uint32_t tid = threadIdx.x;
-  if (tid < kWave) {
-    QRegs Q{kEmpty, 0, 0};
-    q_load(c, s, l, q, tid, Q);
-    const bool live = tid < c.qcap && Q.r != kEmpty;
-    if (live) {
-      d.key[tid] = tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq);
-      d.rid[tid] = Q.r;
-      d.dec[tid] = Q.dec;
-      d.st[tid] = kDeepLive;
-    }
-    const uint64_t m = ballot(live);
-    if (tid == 0) d.hn = (uint32_t)__popcll(m);
-  }
-  __syncthreads();
-  const uint32_t hn = d.hn;
-  const uint32_t tc = tcap_of(c, q) ? s.tsum[l * 3 + q].x : 0u;
-  const uint4* t = tcap_of(c, q) ? tail_of(s, q) + l * tstride_of(c, q) : nullptr;
-  const uint32_t qdec = q == 1 ? kDecQuery : kDecEvent;
-  for (uint32_t i = tid; i < tc; i += kDeepThreads) {
-    const uint4 e = t[i];
-    d.key[hn + i] = tlq_key(e.z & 0xFFFF, e.z >> 16, e.y);
-    d.rid[hn + i] = e.x;
-    d.dec[hn + i] = q == 0 ? e.w : qdec;
-    d.st[hn + i] = kDeepLive;
-  }
-  __syncthreads();
-  return hn + tc;
-}
-
-// keep the `keep` smallest live keys (the bounded queue's prune); returns how many it dropped
-__device__ uint32_t deep_keep_smallest(DeepLds& d, uint32_t n, uint32_t keep) {
-  uint32_t live = 0;
-  for (uint32_t i = threadIdx.x; i < n; i += kDeepThreads) live += d.st[i] != kDeepDead;
-  live = blk_sum_u32(live, d);
-  if (live <= keep) return 0;
-  const uint64_t T = keep ? blk_select_kth(d, n, keep) : 0ull;
-  for (uint32_t i = threadIdx.x; i < n; i += kDeepThreads)
-    if (d.st[i] != kDeepDead && (keep == 0 || d.key[i] > T)) d.st[i] = kDeepDead;
-  __syncthreads();
-  return live - keep;
-}
-
-// the queue back to HBM: head = the qcap smallest live keys in send order (free slots after
-// them), tail = every other live item (any order) with its exact bounds
-__device__ void deep_store_queue(const GCfg& c, const GState& s, uint64_t l, uint32_t q, DeepLds& d, uint32_t n) {
-  const uint32_t tid = threadIdx.x;
-  uint32_t live = 0;
-  for (uint32_t i = tid; i < n; i += kDeepThreads) live += d.st[i] != kDeepDead;
-  live = blk_sum_u32(live, d);
-  const uint64_t T = live > c.qcap ? blk_select_kth(d, n, c.qcap) : ~0ull;
-  if (tid == 0) {
-    d.hn = 0;
-    d.tn = 0;
-  }
-  __syncthreads();
-  uint4* const t = tcap_of(c, q) ? tail_of(s, q) + l * tstride_of(c, q) : nullptr;
-  uint64_t tmin = ~0ull;
-  uint32_t tlmin = ~0u;
-  for (uint32_t i = tid; i < n; i += kDeepThreads) {
-    if (d.st[i] == kDeepDead) continue;
-    const uint64_t k = d.key[i];
-    if (k <= T) {
-      const uint32_t h = atomicAdd(&d.hn, 1u);
-      d.hkey[h] = k;
-      d.hrid[h] = d.rid[i];
-      d.hdec[h] = d.dec[i];
-    } else {  // only a deep queue holds more live items than its head
-      const uint32_t j = atomicAdd(&d.tn, 1u);
-      t[j] = make_uint4(d.rid[i], key_seq(k), key_tl(k), d.dec[i]);
-      tmin = k < tmin ? k : tmin;
-      tlmin = min(tlmin, key_len(k));
-    }
-  }
-  tmin = blk_min_u64(tmin, d);
-  tlmin = blk_min_u32(tlmin, d);
-  if (tid < kWave) {  // wave 0: the head in key order (rank = smaller keys among the head's)
-    const uint32_t hn = d.hn;
-    const uint64_t mk = tid < hn ? d.hkey[tid] : ~0ull;
-    uint32_t rank = 0;
-    for (uint32_t j = 0; j < hn; ++j) rank += d.hkey[j] < mk ? 1u : 0u;
-    if (tid < c.qcap) {
-      const uint32_t slot = tid < hn ? rank : tid;
-      const uint64_t i = (l * 3 + q) * c.qcap + slot;
-      const bool h = tid < hn;
-      s.q_rumor[i] = h ? d.hrid[tid] : kEmpty;
-      s.q_seq[i] = h ? key_seq(mk) : 0u;
-      s.q_txlen[i] = h ? key_tl(mk) : 0u;
-      if (q == 0) s.q_dec[l * c.qcap + slot] = h ? d.hdec[tid] : 0u;
-    }
-  }
-  if (tid == 0 && tcap_of(c, q)) {  // exact bounds; the whole tail sealed
-    s.tsum[l * 3 + q] = d.tn ? make_uint4(d.tn, tlmin, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
-    s.tseal[l * 3 + q] = d.tn ? make_uint4(d.tn, (uint32_t)tmin, (uint32_t)(tmin >> 32), 0u) : kTSumEmpty;
-  }
-  __syncthreads();
-}
-
 // ---- one wave per deferred member ------------------------------------------------------
 #if RSF_DEEP_PROF
 // per-wave totals (one wave per block), added to g_deep_prof once at the kernel's end
@@ -273,7 +94,6 @@ __device__ __forceinline__ uint64_t wave_or_u64(uint64_t v) {
 
 // The LDS scans below read kDeepU items per lane before using any (one LDS round trip per
 // kDeepU * 64 items instead of one per 64).
-constexpr uint32_t kDeepU = 8;
 
 // kDeepU items per lane from LDS: every load issued (in-range indices) before any is used;
 // v[u]: item b + u * 64 + lane exists and is in state `state`, x[u] its key
@@ -408,7 +228,9 @@ template <uint32_t CAP>
 __device__ uint64_t w_select_kth(DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint32_t k, uint8_t state,
                                  const WRange& rg) {
   if (k <= 1 || rg.lo == rg.hi) return rg.lo;
-  if constexpr (RSF_DEEP_SELECT_REG && CAP <= kDeepSmall) {
+  // (the smallest class only: at kDeepSmall the second register-resident key set beside
+  // w_take_head's spills to scratch)
+  if constexpr (RSF_DEEP_SELECT_REG && CAP <= kDeepTiny) {
     if (!(rg.orr >> 63)) {
       constexpr uint32_t R = (CAP + kWave - 1) / kWave;
       uint64_t kr[R];
@@ -595,24 +417,70 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
 #undef RSF_TH_T
 }
 
-// the live items not in the head back to the tail (compacted, any order); returns the count
-// (at tail[t_lo ...]: the recent mode keeps the sealed prefix tail[0, t_lo) in place)
+// the live items not in the head back to the tail (compacted) at tail[t_lo ...], in two
+// groups: first every item above the kDeepReserve-th smallest of them (they join the sealed
+// prefix), then the kDeepReserve smallest (the RESERVE: left in the recent part, so the next
+// refill -- which usually needs exactly the items just past the head, e.g. a backlog of
+// transmits-0 items -- finds them without the sealed prefix).  Returns the count; *nb = the
+// sealed group's size, *bmin = its smallest key (~0 if none).
 template <uint32_t CAP>
-__device__ uint32_t w_store_tail(const GCfg& c, const GState& s, uint64_t l, uint32_t q, const DeepWave<CAP>& d,
-                                 uint32_t lane, uint32_t n, uint32_t t_lo = 0) {
+__device__ uint32_t w_store_tail(const GCfg& c, const GState& s, uint64_t l, uint32_t q, DeepWave<CAP>& d,
+                                 uint32_t lane, uint32_t n, uint32_t t_lo, uint32_t* nb, uint64_t* bmin) {
   uint4* const t = tcap_of(c, q) ? tail_of(s, q) + l * tstride_of(c, q) + t_lo : nullptr;
+  const WRange rg = w_range(d, lane, n, kDeepLive);
+  // R: the reserve's largest key (every live item when there are no more than the reserve)
+  const uint64_t R = rg.cnt > kDeepReserve ? w_select_kth(d, lane, n, kDeepReserve, kDeepLive, rg) : ~0ull;
   uint32_t base = 0;
-  for (uint32_t b = 0; b < n; b += kWave) {
-    const uint32_t i = b + lane;
-    const bool live = i < n && d.st[i] == kDeepLive;
-    const uint64_t m = ballot(live);
-    if (live) {  // only a deep queue holds more live items than its head
-      const uint64_t k = d.key[i];
-      t[base + mbcnt(m)] = make_uint4(d.rid[i], key_seq(k), key_tl(k), d.dec[i]);
+  uint64_t bm = ~0ull;
+  for (uint32_t pass = 0; pass < 2; ++pass) {  // 0: the sealed group (> R), 1: the reserve (<= R)
+    if (pass == 1) {
+      *nb = base;
+      *bmin = wave_min_u64(bm);
     }
-    base += (uint32_t)__popcll(m);
+    for (uint32_t b = 0; b < n; b += kWave) {
+      const uint32_t i = b + lane;
+      const uint64_t k = i < n ? d.key[i] : 0ull;
+      const bool live = i < n && d.st[i] == kDeepLive && ((k > R) == (pass == 0));
+      const uint64_t m = ballot(live);
+      if (live) {  // only a deep queue holds more live items than its head
+        t[base + mbcnt(m)] = make_uint4(d.rid[i], key_seq(k), key_tl(k), d.dec[i]);
+        if (pass == 0) bm = k < bm ? k : bm;
+      }
+      base += (uint32_t)__popcll(m);
+    }
   }
   return base;
+}
+
+// the sealed prefix tail[0, sm) into LDS after the n items there (live): the recent mode could
+// not decide, the member continues with every item; returns the new item count
+template <uint32_t CAP>
+__device__ uint32_t w_load_sealed(const GCfg& c, const GState& s, uint64_t l, uint32_t q, DeepWave<CAP>& d,
+                                  uint32_t lane, uint32_t n, uint32_t sm) {
+  const uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
+  const uint32_t qdec = q == 1 ? kDecQuery : kDecEvent;
+  for (uint32_t i = lane; i < n; i += kWave)
+    if (d.st[i] == kDeepInHead) d.st[i] = kDeepLive;
+  for (uint32_t b = 0; b < sm; b += kDeepU * kWave) {
+    uint4 e[kDeepU];
+#pragma unroll
+    for (uint32_t u = 0; u < kDeepU; ++u) {
+      const uint32_t i = b + u * kWave + lane;
+      e[u] = i < sm ? t[i] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kDeepU; ++u) {
+      const uint32_t i = b + u * kWave + lane;
+      if (i < sm) {
+        d.key[n + i] = tlq_key(e[u].z & 0xFFFF, e[u].z >> 16, e[u].y);
+        d.rid[n + i] = e[u].x;
+        d.dec[n + i] = q == 0 ? e[u].w : qdec;
+        d.st[n + i] = kDeepLive;
+      }
+    }
+  }
+  wsync();
+  return n + sm;
 }
 
 // A member's first round trip, issued while the wave still works on the member before it:
@@ -621,13 +489,12 @@ __device__ uint32_t w_store_tail(const GCfg& c, const GState& s, uint64_t l, uin
 // empty queues cost nothing and the tail loads start at once.
 struct DeepPre {
   uint32_t pc, gk, gs, qinfo, qseq;
-  uint32_t sm, tly;  // lane q < 3: the sealed prefix's count (tseal.x) and the tail's length bound (tsum.y)
-  uint64_t sb;       // lane q < 3: the sealed prefix's key bound
+  uint32_t sm;  // lane q < 3: the sealed prefix's count (tseal.x)
 };
 __device__ __forceinline__ DeepPre deep_pre(const GCfg& c, const GState& s, uint64_t l, uint32_t lane,
                                             const uint32_t* __restrict__ grp_key,
                                             const uint32_t* __restrict__ slot) {
-  DeepPre p{0u, kSentinel, 0u, 0u, 0u, 0u, ~0u, ~0ull};
+  DeepPre p{0u, kSentinel, 0u, 0u, 0u, 0u};
   if (l >= c.n_loc) return p;
   p.pc = s.p_cnt[l];
   if (lane < c.fanout) {
@@ -638,14 +505,24 @@ __device__ __forceinline__ DeepPre deep_pre(const GCfg& c, const GState& s, uint
     p.qseq = s.q_next_seq[l * 3 + lane];
     const uint32_t r0 = s.q_rumor[(l * 3 + lane) * c.qcap];
     const bool dq = tcap_of(c, lane) != 0;
-    const uint4 ts = dq ? s.tsum[l * 3 + lane] : kTSumEmpty;
-    const uint4 se = dq ? s.tseal[l * 3 + lane] : kTSumEmpty;
-    p.qinfo = (r0 != kEmpty ? 1u : 0u) | (ts.x << 1);
-    p.tly = ts.y;
-    p.sm = se.x;
-    p.sb = ((uint64_t)se.z << 32) | se.y;
+    const uint32_t tcq = dq ? s.tsum[l * 3 + lane].x : 0u;
+    p.qinfo = (r0 != kEmpty ? 1u : 0u) | (tcq << 1);
+    p.sm = dq ? s.tseal[l * 3 + lane].x : 0u;
   }
   return p;
+}
+
+// recent mode could not decide: nothing of the member is stored yet, the full-depth class
+// (launched after this one) redoes it; the wave's LDS items are cleared for the next member
+template <uint32_t CAP>
+__device__ __forceinline__ void deep_relist_full(const GCfg& c, const GState& s, uint64_t l, uint32_t lane, uint32_t n,
+                                                 DeepWave<CAP>& d) {
+  for (uint32_t i = lane; i < n; i += kWave) d.st[i] = kDeepDead;
+  wsync();
+  if (lane == 0) s.deep_ids[c.n_loc * 3 - 1 - atomicAdd(s.deep_n + 1, 1u)] = (uint32_t)l;
+#if RSF_DEEP_PROF
+  if (lane == 0) s_dprof[30] += 1ull;
+#endif
 }
 
 template <bool BKT, uint32_t CAP>
@@ -724,10 +601,12 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
     // always loads everything.
     const uint32_t sm = shfl_u32(pre.sm, (int)q);
     const bool others_empty = q == 0 && shfl_u32(qinfo, 1) == 0 && shfl_u32(qinfo, 2) == 0 && ((pc >> 8) & 0xFFFF) == 0;
-    const bool recent = CAP < kDeepBig && others_empty && sm > 0 && sm <= tc && tc + nq <= tcap_of(c, q);
-    const uint32_t t_lo = recent ? sm : 0u;
+    bool recent = others_empty && sm > 0 && sm <= tc && tc + nq <= tcap_of(c, q);
+    uint32_t t_lo = recent ? sm : 0u;
     const uint32_t tn = tc - t_lo;  // tail items loaded
-    if (q == 0 && !recent && c.qcap + tc + nq > CAP) {  // (emit_run listed it by the recent part's need)
+    // the full depth fits this class: a recent mode that cannot decide continues in place
+    const bool fits_all = c.qcap + tc + nq <= CAP;
+    if (q == 0 && !recent && !fits_all) {  // (emit_run listed it by the recent part's need)
       if (lane == 0) s.deep_ids[c.n_loc * 3 - 1 - atomicAdd(s.deep_n + 1, 1u)] = (uint32_t)l;
       return;
     }
@@ -817,29 +696,35 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
     RSF_DEEP_T(10);
     // recent mode: exact only if the head is full and below every sealed key; the sealed
     // prefix stays in the tail, so the tail's bounds include the seal's
-    auto relist_full = [&]() {  // nothing stored yet: the full-depth class redoes the member
-      for (uint32_t i = lane; i < n; i += kWave) d.st[i] = kDeepDead;
-      wsync();
-      if (lane == 0) s.deep_ids[c.n_loc * 3 - 1 - atomicAdd(s.deep_n + 1, 1u)] = (uint32_t)l;
-#if RSF_DEEP_PROF
-      if (lane == 0) s_dprof[30] += 1ull;
-#endif
-    };
+    uint64_t sb = ~0ull;  // the kept sealed prefix's key bound (recent mode)
     if (recent) {
+      const uint4 se = s.tseal[l * 3 + q];
+      sb = ((uint64_t)se.z << 32) | se.y;
       const uint64_t hm = ballot(lane < c.qcap && Q.r != kEmpty);
       bool ok = (uint32_t)__popcll(hm) == c.qcap;
       if (ok) {
         const int hl = 63 - __clzll((long long)hm);
         const uint32_t tlh = shfl_u32(Q.tl, hl);
-        ok = tlq_key(tlh & 0xFFFF, tlh >> 16, shfl_u32(Q.sq, hl)) < shfl_u64(pre.sb, (int)q);
+        ok = tlq_key(tlh & 0xFFFF, tlh >> 16, shfl_u32(Q.sq, hl)) < sb;
       }
-      if (!ok) {
-        relist_full();
+      if (!ok && !fits_all) {
+        deep_relist_full(c, s, l, lane, n, d);
         return;
       }
-      const uint64_t sb = shfl_u64(pre.sb, (int)q);
+      if (!ok) {  // every item after all: the sealed prefix joins, the refill is redone
+#if RSF_DEEP_PROF
+        if (lane == 0) s_dprof[30] += 1ull;
+#endif
+        n = w_load_sealed(c, s, l, q, d, lane, n, t_lo);
+        recent = false;
+        t_lo = 0;
+        sb = ~0ull;
+        w_take_head(c, d, lane, n, q, Q, tmin, tminlen);
+      }
+    }
+    if (recent) {
       tmin = sb < tmin ? sb : tmin;
-      tminlen = min(tminlen, shfl_u32(pre.tly, (int)q));
+      tminlen = min(tminlen, s.tsum[l * 3 + q].y);  // (a bound over the whole tail: covers the sealed part)
 #if RSF_DEEP_PROF
       if (lane == 0) s_dprof[29] += 1ull;
 #endif
@@ -855,19 +740,28 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
                                 tminlen, &unsafe);
     RSF_DEEP_T(11);
     if (unsafe && recent) {
-      relist_full();
-      return;
+      if (!fits_all) {
+        deep_relist_full(c, s, l, lane, n, d);
+        return;
+      }
+      // the head cannot decide even now: every item (the sealed prefix joins) for the fallback
+      n = w_load_sealed(c, s, l, q, d, lane, n, t_lo);
+      recent = false;
+      t_lo = 0;
+      sb = ~0ull;
     }
     if (!unsafe) {
       err |= errq;
       q_store(c, s, l, q, lane, Q, true);
-      const uint32_t cnt = t_lo + w_store_tail(c, s, l, q, d, lane, n, t_lo);
+      uint32_t nb = 0;
+      uint64_t bmin = ~0ull;
+      const uint32_t cnt = t_lo + w_store_tail(c, s, l, q, d, lane, n, t_lo, &nb, &bmin);
       if (lane == 0 && tcap_of(c, q)) {
-        // the tail from here on is sealed: every item's key >= tmin (exact over the items this
-        // refill wrote, the seal's bound over the prefix it kept)
-        const uint4 sum = cnt ? make_uint4(cnt, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
-        s.tsum[l * 3 + q] = sum;
-        s.tseal[l * 3 + q] = cnt ? make_uint4(cnt, (uint32_t)tmin, (uint32_t)(tmin >> 32), 0u) : kTSumEmpty;
+        s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
+        // sealed: the kept prefix and the group written above the reserve (key bound: the
+        // smaller of their bounds); the reserve stays in the recent part
+        const uint64_t b = bmin < sb ? bmin : sb;
+        s.tseal[l * 3 + q] = t_lo + nb ? make_uint4(t_lo + nb, (uint32_t)b, (uint32_t)(b >> 32), 0u) : kTSumEmpty;
       }
       RSF_DEEP_T(12);
     } else {
@@ -925,10 +819,12 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
       RSF_DEEP_T(13);
       w_take_head(c, d, lane, n, q, Q, tmin, tminlen);
       q_store(c, s, l, q, lane, Q, true);
-      const uint32_t cnt = w_store_tail(c, s, l, q, d, lane, n);
+      uint32_t nb = 0;
+      uint64_t bmin = ~0ull;
+      const uint32_t cnt = w_store_tail(c, s, l, q, d, lane, n, 0u, &nb, &bmin);
       if (lane == 0 && tcap_of(c, q)) {
         s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
-        s.tseal[l * 3 + q] = cnt ? make_uint4(cnt, (uint32_t)tmin, (uint32_t)(tmin >> 32), 0u) : kTSumEmpty;
+        s.tseal[l * 3 + q] = nb ? make_uint4(nb, (uint32_t)bmin, (uint32_t)(bmin >> 32), 0u) : kTSumEmpty;
       }
       RSF_DEEP_T(14);
 #if RSF_DEEP_PROF
@@ -978,12 +874,13 @@ __global__ void __launch_bounds__(kWave) emit_deep_wave_kernel(GCfg c, GState s,
   const uint32_t n_list = s.deep_n[list];
   if (blockIdx.x == 0 && lane == 0 && n_list) {
     atomicAdd(total, (unsigned long long)n_list);
-    atomicAdd(total - kDeepClassOff + list, (unsigned long long)n_list);  // per list (rsf_gossip_deep_class_stats)
+    atomicAdd(list == 3 ? total + 1 : total - kDeepClassOff + list, (unsigned long long)n_list);  // per list
   }
   for (uint32_t i = lane; i < CAP; i += kWave) d.st[i] = kDeepDead;
   wsync();
   const uint64_t last = c.n_loc * 3 - 1;
-  const uint32_t* const ids = list == 1 ? s.deep_ids + last : s.deep_ids + (list == 2 ? c.n_loc : 0ull);
+  const uint32_t* const ids = list == 1 ? s.deep_ids + last
+                                        : s.deep_ids + (list == 2 ? c.n_loc : list == 3 ? c.n_loc * 3 : 0ull);
   const int64_t dir = list == 1 ? -1 : 1;
   // software pipeline over the wave's members: the next member's first round trip (deep_pre)
   // and the id after it are read while this member is worked on
@@ -1006,24 +903,302 @@ __global__ void __launch_bounds__(kWave) emit_deep_wave_kernel(GCfg c, GState s,
 #endif
 }
 
-// QueueChecker prune of deep queues listed by check_queues_kernel (entries l * 3 + q): keep the
-// max_depth smallest keys of head and tail
-__global__ void __launch_bounds__(kDeepThreads) check_deep_kernel(GCfg c, GState s, uint32_t max_depth,
-                                                                  const uint32_t* __restrict__ qmax) {
-  __shared__ DeepLds d;
-  const uint32_t n_list = *s.deep_n;
-  for (uint32_t i = 0; i < kDeepItems; i += kDeepThreads)
-    if (i + threadIdx.x < kDeepItems) d.st[i + threadIdx.x] = kDeepDead;
+// ---- the QueueChecker's prune streaming from HBM (check_stream_kernel) -------------------
+// A queue's items indexed i < qcap: head slot i (live if its rumor is set), i >= qcap: tail
+// item i - qcap.  Nothing is staged in LDS but a histogram and the items that change place, so
+// a CU holds eight of these blocks instead of one LDS-bound block; the passes after the first
+// re-read the queue from the caches (a member's queue is ~130 KB at the reference's regime).
+struct StreamQ {
+  const uint32_t *hr, *hs, *ht;  // head slots: rumor, seq, transmits | len << 16
+  const uint4* t;                // tail
+  uint32_t qcap, tc;
+};
+__device__ __forceinline__ bool sq_key(const StreamQ& Q, uint32_t i, uint64_t& k) {
+  if (i < Q.qcap) {
+    if (Q.hr[i] == kEmpty) return false;
+    const uint32_t tl = Q.ht[i];
+    k = tlq_key(tl & 0xFFFF, tl >> 16, Q.hs[i]);
+    return true;
+  }
+  const uint4 e = Q.t[i - Q.qcap];
+  k = tlq_key(e.z & 0xFFFF, e.z >> 16, e.y);
+  return true;
+}
+
+struct StreamLds {
+  uint32_t hist[256];
+  uint64_t w64[kDeepWaves], w64b[kDeepWaves];
+  uint32_t sel_digit, sel_need, sel_cnt, nb, nr, nh;
+  uint4 hitem[kWave];         // the new head's items (<= qcap)
+  uint64_t hkey[kWave];
+  uint4 ritem[kDeepReserve];  // the reserve (written after the sealed group)
+};
+
+// block-uniform minimum (every thread calls)
+__device__ __forceinline__ uint64_t blk_min_u64(uint64_t v, StreamLds& d) {
+  v = wave_min_u64(v);
   __syncthreads();
+  if ((threadIdx.x & (kWave - 1)) == 0) d.w64[threadIdx.x / kWave] = v;
+  __syncthreads();
+  uint64_t m = d.w64[0];
+#pragma unroll
+  for (uint32_t w = 1; w < kDeepWaves; ++w) m = d.w64[w] < m ? d.w64[w] : m;
+  return m;
+}
+
+// the k-th smallest live key (1 <= k <= live count) by a radix select over the streamed keys;
+// bytes every live key shares (from the caller's AND / OR) take no pass; a digit's lanes that
+// agree with the wave's first active lane are counted by that lane alone (a saturated queue's
+// keys share their transmit and high seq bytes: one LDS address would take thousands of
+// atomics); the select stops once the chosen bucket holds one key
+__device__ uint64_t stream_select_kth(const StreamQ& Q, StreamLds& d, uint32_t k, uint64_t an, uint64_t orr) {
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), n = Q.qcap + Q.tc;
+  const uint64_t var = an ^ orr;
+  uint64_t prefix = 0, mask = 0;
+  uint32_t need = k;
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    const uint64_t bm = 0xFFull << shift;
+    if (!(var & bm)) {
+      prefix |= an & bm;
+      mask |= bm;
+      continue;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < 256; i += kDeepThreads) d.hist[i] = 0;
+    __syncthreads();
+    for (uint32_t b = 0; b < n; b += kDeepU * kDeepThreads) {
+      uint64_t x[kDeepU];
+      bool v[kDeepU];
+#pragma unroll
+      for (uint32_t u = 0; u < kDeepU; ++u) {
+        const uint32_t i = b + u * kDeepThreads + tid;
+        x[u] = 0;
+        v[u] = i < n && sq_key(Q, i, x[u]);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kDeepU; ++u) {
+        const bool in = v[u] && (x[u] & mask) == prefix;
+        const uint32_t dg = in ? (uint32_t)(x[u] >> shift) & 0xFF : 0u;
+        const uint64_t am = ballot(in);
+        if (!am) continue;
+        const int f = __ffsll((long long)am) - 1;
+        const uint32_t d0 = shfl_u32(dg, f);
+        const uint64_t same = ballot(in && dg == d0);
+        if (lane == (uint32_t)f) atomicAdd(&d.hist[d0], (uint32_t)__popcll(same));
+        else if (in && dg != d0) atomicAdd(&d.hist[dg], 1u);
+      }
+    }
+    __syncthreads();
+    if (tid < kWave) {  // running counts over the 256 bins, four per lane
+      const uint32_t h0 = d.hist[4 * tid], h1 = d.hist[4 * tid + 1], h2 = d.hist[4 * tid + 2], h3 = d.hist[4 * tid + 3];
+      const uint32_t sum = h0 + h1 + h2 + h3, incl = wave_inclusive_sum_u32(sum), excl = incl - sum;
+      if (excl < need && need <= incl) {
+        uint32_t b = 0, acc = excl, hb = h0;
+        if (acc + h0 < need) {
+          acc += h0;
+          b = 1;
+          hb = h1;
+          if (acc + h1 < need) {
+            acc += h1;
+            b = 2;
+            hb = h2;
+            if (acc + h2 < need) {
+              acc += h2;
+              b = 3;
+              hb = h3;
+            }
+          }
+        }
+        d.sel_digit = 4 * tid + b;
+        d.sel_need = need - acc;
+        d.sel_cnt = hb;
+      }
+    }
+    __syncthreads();
+    prefix |= (uint64_t)d.sel_digit << shift;
+    mask |= bm;
+    need = d.sel_need;
+    if (d.sel_cnt == 1 && shift > 0) {  // one key left under the prefix: it is the k-th
+      uint64_t best = ~0ull;
+      for (uint32_t i = tid; i < n; i += kDeepThreads) {
+        uint64_t x = 0;
+        if (sq_key(Q, i, x) && (x & mask) == prefix) best = x;
+      }
+      return blk_min_u64(best, d);
+    }
+  }
+  return prefix;
+}
+
+// QueueChecker prune of the deep queues check_queues_kernel listed (entries l * 3 + q): keep the
+// `max` smallest keys (each member's own max with qmax), the head refilled with the qcap
+// smallest of them, the tail = the rest in the two groups w_store_tail writes (sealed above the
+// reserve), exact bounds.  The tail is compacted in place in index order (an item is written at
+// or below the position it was read from, after every thread has read its chunk); the items
+// leaving the old head are written after the tail's.
+__global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GState s, uint32_t max_depth,
+                                                                    const uint32_t* __restrict__ qmax) {
+  __shared__ StreamLds d;
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
+  const uint32_t n_list = *s.deep_n;
   for (uint32_t it = blockIdx.x; it < n_list; it += gridDim.x) {
     const uint32_t e = s.deep_ids[it];
     const uint64_t l = e / 3;
     const uint32_t q = e % 3;
-    if (l >= c.n_loc) continue;
-    const uint32_t n = deep_load_queue(c, s, l, q, d);
-    deep_keep_smallest(d, n, qmax ? qmax[l] : max_depth);
-    deep_store_queue(c, s, l, q, d, n);
-    for (uint32_t i = threadIdx.x; i < n; i += kDeepThreads) d.st[i] = kDeepDead;
+    if (l >= c.n_loc || !tcap_of(c, q)) continue;
+    const uint32_t keep = qmax ? qmax[l] : max_depth;
+    const uint64_t hb = (l * 3 + q) * c.qcap;
+    const StreamQ Q{s.q_rumor + hb, s.q_seq + hb, s.q_txlen + hb, tail_of(s, q) + l * tstride_of(c, q), c.qcap,
+                    s.tsum[l * 3 + q].x};
+    const uint32_t n = c.qcap + Q.tc;
+    // live count, AND / OR of the live keys
+    uint64_t an = ~0ull, orr = 0;
+    uint32_t live = 0;
+    for (uint32_t i = tid; i < n; i += kDeepThreads) {
+      uint64_t x = 0;
+      if (sq_key(Q, i, x)) {
+        an &= x;
+        orr |= x;
+        live++;
+      }
+    }
+    an = wave_and_u64_blk(an);
+    orr = wave_or_u64_blk(orr);
+    live = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(live), 63);
+    __syncthreads();
+    if (lane == 0) {
+      d.w64[tid / kWave] = an;
+      d.w64b[tid / kWave] = orr;
+      d.hist[tid / kWave] = live;
+    }
+    __syncthreads();
+    an = d.w64[0];
+    orr = d.w64b[0];
+    live = d.hist[0];
+#pragma unroll
+    for (uint32_t w = 1; w < kDeepWaves; ++w) {
+      an &= d.w64[w];
+      orr |= d.w64b[w];
+      live += d.hist[w];
+    }
+    if (live <= keep) continue;  // (listed by the same count: cannot happen)
+    const uint64_t T = keep ? stream_select_kth(Q, d, keep, an, orr) : 0ull;  // the largest key kept
+    const uint64_t Th = keep > c.qcap ? stream_select_kth(Q, d, c.qcap, an, orr) : T;  // the new head's largest
+    const uint64_t TR = keep > c.qcap + kDeepReserve ? stream_select_kth(Q, d, c.qcap + kDeepReserve, an, orr) : T;
+    __syncthreads();
+    if (tid == 0) {
+      d.nb = 0;
+      d.nr = 0;
+      d.nh = 0;
+    }
+    __syncthreads();
+    uint64_t bmin = ~0ull, tmin = ~0ull;
+    uint32_t tlmin = ~0u;
+    uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
+    // the tail in index order: the sealed group (TR < key <= T) compacted in place, the reserve
+    // (Th < key <= TR) and the new head's items (key <= Th) staged in LDS
+    for (uint32_t b = 0; b < Q.tc; b += kDeepThreads) {
+      const uint32_t i = b + tid;
+      const bool in = i < Q.tc;
+      uint4 x = make_uint4(0, 0, 0, 0);
+      uint64_t k = ~0ull;
+      if (in) {
+        x = t[i];
+        k = tlq_key(x.z & 0xFFFF, x.z >> 16, x.y);
+      }
+      const bool sealed = in && k > TR && k <= T, res = in && k > Th && k <= TR, head = in && k <= Th;
+      const uint64_t sm = ballot(sealed);
+      if (lane == 0) d.hist[tid / kWave] = (uint32_t)__popcll(sm);
+      __syncthreads();  // every thread has read its item: the chunk's positions may be rewritten
+      uint32_t before = 0, tot = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < kDeepWaves; ++w) {
+        const uint32_t cw = d.hist[w];
+        before += w < tid / kWave ? cw : 0u;
+        tot += cw;
+      }
+      const uint32_t nb0 = d.nb;
+      if (sealed) {
+        t[nb0 + before + mbcnt(sm)] = x;
+        bmin = k < bmin ? k : bmin;
+        tlmin = min(tlmin, key_len(k));
+      }
+      if (res) {
+        d.ritem[atomicAdd(&d.nr, 1u)] = x;
+        tmin = k < tmin ? k : tmin;
+        tlmin = min(tlmin, key_len(k));
+      }
+      if (head) {
+        const uint32_t j = atomicAdd(&d.nh, 1u);
+        d.hitem[j] = make_uint4(x.x, x.y, x.z, q == 0 ? x.w : 0u);
+        d.hkey[j] = k;
+      }
+      __syncthreads();
+      if (tid == 0) d.nb = nb0 + tot;
+      __syncthreads();
+    }
+    // the old head's items: to the new head, the reserve, or the sealed group (appended)
+    if (tid < kWave) {
+      const bool live_h = tid < c.qcap && Q.hr[tid] != kEmpty;
+      uint4 x = make_uint4(0, 0, 0, 0);
+      uint64_t k = ~0ull;
+      if (live_h) {
+        x = make_uint4(Q.hr[tid], Q.hs[tid], Q.ht[tid], q == 0 ? s.q_dec[l * c.qcap + tid] : 0u);
+        k = tlq_key(x.z & 0xFFFF, x.z >> 16, x.y);
+      }
+      const bool sealed = live_h && k > TR && k <= T, res = live_h && k > Th && k <= TR, head = live_h && k <= Th;
+      const uint64_t sm = ballot(sealed);
+      const uint32_t nb0 = d.nb;
+      if (sealed) {
+        t[nb0 + mbcnt(sm)] = x;
+        bmin = k < bmin ? k : bmin;
+        tlmin = min(tlmin, key_len(k));
+      }
+      if (res) {
+        d.ritem[atomicAdd(&d.nr, 1u)] = x;
+        tmin = k < tmin ? k : tmin;
+        tlmin = min(tlmin, key_len(k));
+      }
+      if (head) {
+        const uint32_t j = atomicAdd(&d.nh, 1u);
+        d.hitem[j] = x;
+        d.hkey[j] = k;
+      }
+      wsync();
+      if (lane == 0) d.nb = nb0 + (uint32_t)__popcll(sm);
+    }
+    __syncthreads();
+    const uint32_t nb = d.nb, nr = d.nr, nh = d.nh;
+    for (uint32_t j = tid; j < nr; j += kDeepThreads) t[nb + j] = d.ritem[j];  // the reserve after them
+    // the new head in key order (rank among the staged keys), free slots after it
+    if (tid < kWave) {
+      const uint64_t mk = tid < nh ? d.hkey[tid] : ~0ull;
+      uint32_t rank = 0;
+      for (uint32_t j = 0; j < nh; ++j) rank += d.hkey[j] < mk ? 1u : 0u;
+      if (tid < c.qcap) {
+        const bool h = tid < nh;
+        const uint32_t slot = h ? rank : tid;
+        const uint4 x = h ? d.hitem[tid] : make_uint4(kEmpty, 0u, 0u, 0u);
+        s.q_rumor[hb + slot] = x.x;
+        s.q_seq[hb + slot] = x.y;
+        s.q_txlen[hb + slot] = x.z;
+        if (q == 0) s.q_dec[l * c.qcap + slot] = x.w;
+      }
+    }
+    bmin = blk_min_u64(bmin, d);
+    tmin = blk_min_u64(tmin, d);
+    tmin = bmin < tmin ? bmin : tmin;
+    uint32_t lm = wave_min_u32(tlmin);
+    __syncthreads();
+    if (lane == 0) d.hist[tid / kWave] = lm;
+    __syncthreads();
+    if (tid == 0) {
+      for (uint32_t w = 1; w < kDeepWaves; ++w) lm = min(lm, d.hist[w]);
+      lm = min(lm, d.hist[0]);
+      const uint32_t cnt = nb + nr;
+      s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, lm, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
+      s.tseal[l * 3 + q] = nb ? make_uint4(nb, (uint32_t)bmin, (uint32_t)(bmin >> 32), 0u) : kTSumEmpty;
+    }
     __syncthreads();
   }
 }

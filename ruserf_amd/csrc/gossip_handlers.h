@@ -111,7 +111,7 @@ struct GState {
   // or sets m = 0.
   uint4* tseal;      // [n_loc][3]
   uint32_t* deep_ids;  // [n_loc * 3] members deferred to emit_deep_wave_kernel (two lists), or queues to prune
-  uint32_t* deep_n;    // [3] the lists' lengths (reset before each emission)
+  uint32_t* deep_n;    // [4] the lists' lengths (reset before each emission)
 };
 constexpr uint32_t kDeepClassOff = 6;  // the per-list deferral counters sit at (total counter) - 6 + list
 constexpr uint32_t kTailSlack = 192;  // tail row room past its capacity: one emission's spills (2 x 64) + 64
@@ -126,14 +126,13 @@ constexpr uint32_t kPend = 128;  // pending entries per member (two per lane of 
 // serial application runs, slow but exact).
 constexpr uint32_t kPendMerge = kPend - 8;
 // items of one queue the deferred-emission path holds in LDS: the full depth plus a pending
-// list (kDeepItems), and two smaller capacities for the common cases (kDeepSmall, kDeepTiny;
-// RSF_DEEP_TINY=0 drops the smallest class)
-#ifndef RSF_DEEP_TINY
-#define RSF_DEEP_TINY 1
-#endif
+// list (kDeepItems, 1 wave per CU), and three smaller capacities for the common cases -- with a
+// sealed tail prefix the path reads only the head, the reserve, the items spilled since the last
+// refill and the pending list (kDeepTiny 8, kDeepSmall 6, kDeepMid 3 waves per CU)
 constexpr uint32_t kDeepItems = RSF_MAX_QUEUE_DEPTH + kPend;
+constexpr uint32_t kDeepTiny = 640 + 64 + kPend;
 constexpr uint32_t kDeepSmall = 1024 + 64 + kPend;
-constexpr uint32_t kDeepTiny = RSF_DEEP_TINY ? 640 + 64 + kPend : 0u;
+constexpr uint32_t kDeepMid = 2240 + 64 + kPend;
 RSF_HD uint32_t pend_total(uint32_t pc) { return (pc & 0xFF) + ((pc >> 8) & 0xFF) + ((pc >> 16) & 0xFF); }
 
 // per-member scalar state held in registers while a kernel works on it

@@ -433,8 +433,8 @@ class GossipEngine:
 
     def deep_class_stats(self):
         """members deferred to the whole-queue emission since creation, per LDS capacity
-        class: (smallest, middle, full depth)"""
-        out = np.zeros(3, dtype=np.uint64)
+        class: (tiny, small, middle, full depth)"""
+        out = np.zeros(4, dtype=np.uint64)
         check(lib().rsf_gossip_deep_class_stats(self._h, ptr(out, C.c_uint64)))
         return out
 

@@ -66,6 +66,45 @@ def test_deep_bench_shape_bit_exact(rounds):
     L.orc_world_free(C.byref(w))
 
 
+def test_deep_steady_state_ticks_bit_exact():
+    """The reference's queue regime over many rounds at the bench's saturated shape (4096
+    subjects, 8 intents of budget per target, 5% originating; 8k members): the intent queue
+    8192 deep grows ~24 items a round, QueueChecker ticks every 25 rounds prune it to 1 100
+    (the second and third ticks prune), and the ring is sized so nothing expires.
+    The deferred path runs its recent mode (the tail's sealed prefix stays in HBM), re-lists
+    members whose recent part cannot decide, and the full-depth class (tails past 1 216
+    items) -- every one of them bit-exact against the oracle, compared every 5 rounds and
+    after every tick."""
+    n, s, rounds, every, mx = 8000, 4096, 80, 25, 1100
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=64, queue_depth=(8192, 0, 0), gossip_limit=8 * 24,
+                         gossip_overhead=2, max_rumors=1 << 20, event_buffer_size=512, query_buffer_size=512,
+                         slot_k=1)
+    subj, acts, ml = W.intents_workload(n, s, rounds, rate=0.05, seed=77)
+    g, w = pair(cfg, subj, W.initial_views(s))
+    pruned_at_ticks = 0
+    cls0 = g.deep_class_stats()
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t], threads=16)
+        if (t + 1) % 5 == 0:
+            same(g, w, f"round {t}")
+        if (t + 1) % every == 0:
+            got = g.check_queues(mx, 0, 128)
+            exp = (C.c_uint64 * 9)()
+            L.orc_check_queues(C.byref(w), mx, 0, 128, exp)
+            assert list(got["queued"]) + list(got["warn"]) + list(got["pruned"]) == list(exp), t
+            pruned_at_ticks += int(got["pruned"][0])
+            same(g, w, f"tick after round {t}")
+    st = H.engine_state(g, H.world_width(w))
+    assert int(st["q_pruned"].sum()) == 0  # nothing dropped between ticks
+    assert int(st["q_expired"].sum()) == 0  # the ring never wrapped onto a queued item
+    assert pruned_at_ticks > 0
+    cls = g.deep_class_stats() - cls0
+    assert cls[0] > 0 and cls[3] > 0, cls  # the recent mode's smallest class and the full depth both ran
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
 @pytest.mark.parametrize("qcap,depth,limit,mult", [(16, 100, 400, 4), (64, 200, 260, 1), (8, 40, 600, 2),
                                                    (32, 64, 1400, 4)])
 def test_deep_churn_flood_prune_ring_bit_exact(qcap, depth, limit, mult):
