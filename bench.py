@@ -394,14 +394,14 @@ def main():
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline_pushpull(args)
     else:
-        from bench_gossip import run_gossip, cpu_baseline_gossip
+        from bench_gossip import run_gossip, cpu_baseline_gossip, cpu_baseline_gossip_deep
         # BASELINE configs[1] (1M members on one MI355X; configs[2]'s 16M do not fit one GPU)
         # in the reference's queue regime; per GPU under torch.distributed (weak scaling)
         args.members = args.members or 1_000_000
         res = run_gossip(args, rank, world)
         cpu = None
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline_gossip(args)
+            cpu = cpu_baseline_gossip_deep(args) if args.queue_depth else cpu_baseline_gossip(args)
         attach_traffic(workload, res)
         if world == 1 and not args.no_extra_points:
             # labelled model points, same box, same call: the bounded 64-slot queue (prunes on

@@ -22,7 +22,7 @@ SETTLE_ROUNDS = 12   # setup: bring the cluster to gossip steady state (queues s
 # = 30 s (options.rs:512) at memberlist's LAN gossip interval of 200 ms = 150 rounds, each
 # pruning every queue to max_queue_depth 4096 (base.rs:720-760); settled past two ticks
 CHECK_EVERY = 150
-SETTLE_STEADY = 300
+SETTLE_STEADY = 330
 MAX_QUEUE_DEPTH = 4096
 QUEUE_DEPTH_WARNING = 128
 # fraction of force_leaves issued with prune (remove_failed_node_prune); RSF_PRUNE_FRAC overrides
@@ -80,16 +80,13 @@ def run_gossip(args, rank, world):
     per = args.members
     n = per * world
     depth = getattr(args, "queue_depth", 0) or 0
-    # QueueChecker ticks in the round loop (0: none): every K rounds, counted from round 0, the
-    # timed window placed so that it ENDS with a tick (a tick then weighs 1/steps of the window
-    # instead of 1/K: pessimistic), the ring sized so no queued item expires during the run
+    # QueueChecker ticks in the round loop (0: none), staggered: each member's checker runs on
+    # its own timer (base.rs:703-735), member m ticking after the rounds t with
+    # (t + 1) % K == m % K, so every round carries 1/K of the ticks (the prune included in the
+    # timed steps at its true rate) and the queues cycle between max_queue_depth and what K
+    # rounds add; the ring sized so no queued item expires during the run
     check_every = getattr(args, "check_every", 0) or 0
-    if check_every:
-        base = SETTLE_STEADY if args.settle is None else args.settle
-        total = -(-(base + args.warmup + args.steps) // check_every) * check_every
-        settle = total - args.warmup - args.steps
-    else:
-        settle = SETTLE_ROUNDS if args.settle is None else args.settle
+    settle = (SETTLE_STEADY if check_every else SETTLE_ROUNDS) if args.settle is None else args.settle
     rounds_total = settle + args.warmup + args.steps
     cfg = gossip_cfg(n, rounds_total, world, queue_cap=args.queue_cap, queue_depth=depth,
                      ring_rounds=rounds_total if check_every else 64)
@@ -107,21 +104,15 @@ def run_gossip(args, rank, world):
         step_fn = lambda t: sg.round(t, ml[t], acts[t])  # noqa: E731
     eng.set_subjects(subj)
     eng.init_views(*views)
-    ticks = {"n": 0, "in_window": 0, "pruned": 0, "last": None}
 
-    def checker(t_, timed):
-        # the QueueChecker tick after round t_ (every check_every rounds); synchronises
-        if not check_every or (t_ + 1) % check_every:
-            return
-        st = eng.check_queues(MAX_QUEUE_DEPTH, 0, QUEUE_DEPTH_WARNING)
-        ticks["n"] += 1
-        ticks["in_window"] += int(timed)
-        ticks["pruned"] += int(st["pruned"][0])
-        ticks["last"] = (t_ + 1, st)
+    def checker(t_):
+        # the staggered QueueChecker ticks due after round t_ (asynchronous)
+        if check_every:
+            eng.check_queues_phase(check_every, (t_ + 1) % check_every, MAX_QUEUE_DEPTH, 0, QUEUE_DEPTH_WARNING)
 
     def step_settle(t_):
         step_fn(t_)
-        checker(t_, False)
+        checker(t_)
 
     t = 0
     for _ in range(settle + args.warmup):
@@ -136,6 +127,8 @@ def run_gossip(args, rank, world):
     pruned0 = eng.pruned_total(flush=False)
     deep0 = eng.deep_stats()[0] if depth else 0
     cls0 = eng.deep_class_stats() if depth else None
+    if check_every:
+        eng.checker_stats(reset=True)
     eng.set_profiling(True)
     if sharded:
         sg.set_timing(True)
@@ -145,7 +138,7 @@ def run_gossip(args, rank, world):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step_fn(t)
-        checker(t, True)
+        checker(t)
         t += 1
     torch.cuda.synchronize()
     if world > 1:
@@ -161,21 +154,29 @@ def run_gossip(args, rank, world):
     regime = None
     if check_every:
         occ = eng.checker_occupancy()
+        cst = eng.checker_stats()
         h, b = occ["hist"][0].astype(np.int64), occ["bin"]
         cum = np.cumsum(h)
         q = lambda f: int((np.searchsorted(cum, f * cum[-1]) + 1) * b)  # noqa: E731  (upper edge of the bin)
-        last_round, last = ticks["last"]
-        regime = {"what": "the reference's queue regime: QueueChecker ticks every check_every rounds "
-                          "(queue_check_interval 30 s / gossip interval 200 ms), each pruning to max_queue_depth; "
-                          "nothing dropped in between (bounded_pruned = 0), no rumor-ring expiry",
+        ticked = int(cum[-1])
+        ql = eng.queue_lengths()[:, 0].astype(np.int64)
+        regime = {"what": "the reference's queue regime: each member's QueueChecker ticks every check_every rounds "
+                          "(queue_check_interval 30 s / gossip interval 200 ms) on its own phase (member id mod "
+                          "check_every), pruning its queues to max_queue_depth; nothing dropped in between "
+                          "(bounded_pruned = 0), no rumor-ring expiry",
                   "check_every_rounds": check_every, "max_queue_depth": MAX_QUEUE_DEPTH,
-                  "intent_queue_capacity": cfg.depths()[0], "ticks_total": ticks["n"],
-                  "ticks_in_timed_window": ticks["in_window"], "last_tick_after_round": last_round,
-                  "occupancy_at_last_tick": {"mean": float(last["queued"][0]) / per,
-                                             "p50_upper": q(0.5), "p99_upper": q(0.99),
-                                             "max": int(occ["max"][0]), "bin": b},
-                  "pruned_at_last_tick_per_member": float(last["pruned"][0]) / per,
-                  "members_over_warning_at_last_tick": int(last["warn"][0]),
+                  "intent_queue_capacity": cfg.depths()[0], "settle_rounds": settle,
+                  "ticks_in_timed_window": ticked,
+                  "intent_queue_items_after_window": {"mean": float(ql.mean()), "p50": int(np.percentile(ql, 50)),
+                                                      "p99": int(np.percentile(ql, 99)), "max": int(ql.max()),
+                                                      "min": int(ql.min())},
+                  "occupancy_at_ticks_in_window": {"members_ticked": ticked,
+                                                   "mean": float(cst["queued"][0]) / max(1, ticked),
+                                                   "p50_upper": q(0.5), "p99_upper": q(0.99),
+                                                   "max": int(occ["max"][0]), "bin": b},
+                  "pruned_per_tick": float(cst["pruned"][0]) / max(1, ticked),
+                  "pruned_per_round": float(cst["pruned"][0]) / args.steps,
+                  "members_over_warning_in_window": int(cst["warn"][0]),
                   "expired_whole_run": int(eng.expired().sum()),
                   "deferred_per_round_by_class": dict(zip(["tiny", "small", "middle", "full"],
                                                           ((eng.deep_class_stats() - cls0) / args.steps).tolist()))
@@ -218,8 +219,9 @@ def run_gossip(args, rank, world):
         "config": {"workload": f"gossip rounds, {n} members ({per}/GPU), fanout k=3, {SUBJECTS} tracked subjects, "
                                f"1% of members originate a join/leave intent per round, member-state merge + "
                                f"Lamport clocks, "
-                               + (f"the reference's queue regime (intent queue {cfg.depths()[0]} deep, QueueChecker "
-                                  f"prune to {MAX_QUEUE_DEPTH} every {check_every} rounds, settled {settle} rounds) "
+                               + (f"the reference's queue regime (intent queue {cfg.depths()[0]} deep, each member's "
+                                  f"QueueChecker pruning to {MAX_QUEUE_DEPTH} every {check_every} rounds on its own "
+                                  f"phase, inside the timed rounds; settled {settle} rounds) "
                                   if check_every else f"bounded {cfg.queue_cap}-slot queues (model point) ")
                                + ("(BASELINE configs[2] shard: 2M members/GPU, 16M at 8 GPUs)" if per == 2_000_000
                                   else "(BASELINE configs[1]: 1M members on one MI355X)" if per == 1_000_000 and world == 1
@@ -260,6 +262,55 @@ def run_gossip(args, rank, world):
     }
 
 
+def cpu_baseline_gossip_deep(args, seconds_target=10.0, n=20_000, settle=60):
+    """The oracle's round in the same queue regime as the line (the intent queue as deep as
+    the engine's, no prune between ticks) on a bounded sample: n members settled `settle`
+    rounds (queues ~24 items a round deep by then), then timed on all the box's threads
+    and on one.  The oracle's queue is a sorted array (insert O(depth)), as memberlist's
+    TransmitLimitedQueue is a btree of O(log depth): the CPU figure is the restatement's."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import gossip_harness as H  # test infrastructure: checker / CPU baseline only
+    from bench import cpu_info, cpu_threads
+    from ruserf_amd import workload as W
+    th = cpu_threads()
+    rounds_total = settle + 40
+    cfg = gossip_cfg(n, rounds_total, 1, queue_cap=64, queue_depth=args.queue_depth, ring_rounds=rounds_total)
+    subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED, prune_frac=PRUNE_FRAC)
+    w = H.oracle_world(cfg, subj, W.initial_views(SUBJECTS))
+    t = 0
+
+    def rnd(threads):
+        H.oracle_round(w, t, ml[t], acts[t], threads=threads)
+        H.L.orc_check_queues_phase(C.byref(w), MAX_QUEUE_DEPTH, 0, QUEUE_DEPTH_WARNING, CHECK_EVERY,
+                                   (t + 1) % CHECK_EVERY, None)
+    for _ in range(settle):
+        rnd(th)
+        t += 1
+
+    def timed(threads, budget, max_rounds):
+        nonlocal t
+        done, spent = 0, 0.0
+        while spent < budget and done < max_rounds and t < rounds_total:
+            t0 = time.perf_counter()
+            rnd(threads)
+            spent += time.perf_counter() - t0
+            done += 1
+            t += 1
+        return done, spent
+    done_mt, spent_mt = timed(th, seconds_target, 20)
+    done_1, spent_1 = timed(1, seconds_target / 2, 3)
+    width = H.world_width(w)
+    H.L.orc_world_free(C.byref(w))
+    return {"value": n * done_mt / spent_mt, "unit": "node-rounds/s", "cores": th, "kind": "port",
+            "value_1thread": n * done_1 / spent_1,
+            "cpu_model": cpu_info(),
+            "sample": f"oracle gossip rounds (orc_world_round_mt), {n} members, {SUBJECTS} subjects, the same workload "
+                      f"and queue depth ({cfg.depths()[0]}), settled {settle} rounds (deepest queue {width} items), the staggered checker ticks "
+                      f"included; "
+                      f"{done_mt} rounds on {th} threads ({spent_mt:.1f}s), {done_1} rounds on 1 thread "
+                      f"({spent_1:.1f}s); {cpu_info()}"}
+
+
 def cpu_baseline_gossip(args, seconds_target=10.0, n=200_000):
     """The oracle's round (the C restatement of the same path) on a bounded sample:
     n members, the same subject count and workload, settled, then timed with all the
@@ -284,7 +335,7 @@ def cpu_baseline_gossip(args, seconds_target=10.0, n=200_000):
         done, spent = 0, 0.0
         while spent < budget and done < max_rounds and t < rounds_total:
             t0 = time.perf_counter()
-            H.oracle_round(w, t, ml[t], acts[t], threads=threads)
+            rnd(threads)
             spent += time.perf_counter() - t0
             done += 1
             t += 1

@@ -4,7 +4,9 @@ so nothing expires, and a queue depth (register head + HBM tail) as deep as the 
 Every `every` rounds it prints one JSON line: ms per round over the window, intent-queue
 occupancy (mean / p50 / p99 / max over members), deferred members per round per LDS class,
 bounded-queue drops (between ticks; the reference drops none) and ring expiries.
-Usage: steady_state.py [members] [rounds] [check_every] [depth] [every]"""
+With mode "stagger" each member ticks on its own phase (member id mod check_every) after every
+round instead (rsf_gossip_check_queues_phase), inside the timed windows.
+Usage: steady_state.py [members] [rounds] [check_every] [depth] [every] [sync|stagger]"""
 import json
 import sys
 import time
@@ -22,9 +24,10 @@ rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 450
 check_every = int(sys.argv[3]) if len(sys.argv) > 3 else 150
 depth = int(sys.argv[4]) if len(sys.argv) > 4 else 4096
 every = int(sys.argv[5]) if len(sys.argv) > 5 else 10
+stagger = len(sys.argv) > 6 and sys.argv[6] == "stagger"
 cfg = B.gossip_cfg(n, rounds, 1, queue_depth=depth, ring_rounds=rounds)
 print(json.dumps({"members": n, "rounds": rounds, "check_every": check_every, "depth": cfg.depths()[0],
-                  "max_rumors": cfg.max_rumors}), flush=True)
+                  "max_rumors": cfg.max_rumors, "stagger": stagger}), flush=True)
 subj, acts, ml = W.intents_workload(n, B.SUBJECTS, rounds, rate=0.01, seed=B.SEED, prune_frac=B.PRUNE_FRAC)
 torch.cuda.set_stream(torch.cuda.Stream())
 eng = GossipEngine(cfg)
@@ -36,7 +39,9 @@ pr0, ex0 = 0, 0
 t0 = time.perf_counter()
 for t in range(rounds):
     eng.round(t, ml[t], acts[t])
-    tick = check_every and (t + 1) % check_every == 0
+    if stagger:
+        eng.check_queues_phase(check_every, (t + 1) % check_every, 4096, 0, 128)
+    tick = not stagger and check_every and (t + 1) % check_every == 0
     if (t + 1) % every == 0 or tick:
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / every * 1e3
@@ -49,6 +54,9 @@ for t in range(rounds):
                        "p99": int(np.percentile(ql, 99)), "max": int(ql.max())},
                "deferred_per_round": [(int(a) - int(b)) / every for a, b in zip(cls, cls0)],
                "bounded_pruned": pr - pr0, "expired": ex - ex0}
+        if stagger:
+            cs = eng.checker_stats(reset=True)
+            rec["ticks"] = {"pruned_per_round": int(cs["pruned"][0]) / every}
         if tick:
             torch.cuda.synchronize()
             tt = time.perf_counter()

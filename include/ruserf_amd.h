@@ -572,7 +572,21 @@ int rsf_gossip_reconnect(rsf_gossip* g, uint32_t tick, uint32_t* target);
  * warning depth, items pruned.  Synchronises. */
 int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_queue_depth,
                             uint32_t depth_warning, uint64_t* num_queued, uint64_t* n_warn, uint64_t* n_pruned);
-/* Occupancy at the last checker tick, before its prune: hist (host, [3][bins], may be NULL)
+/* Staggered ticks: each node's QueueChecker runs on its own interval timer
+ * (base.rs:703-735), so the nodes' ticks need not coincide.  This runs the same tick at the
+ * shard members whose global id is phase mod period only; called after every round with
+ * phase = (round + 1) mod period, every member ticks once per period rounds and each round
+ * carries 1/period of the ticks.  Asynchronous: the counts accumulate (with the occupancy
+ * histogram) until rsf_gossip_checker_stats resets them; rsf_gossip_check_queues resets
+ * them at its start.  Errors: period 0 or phase >= period. */
+int rsf_gossip_check_queues_phase(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_queue_depth,
+                                  uint32_t depth_warning, uint32_t period, uint32_t phase);
+/* The checker counts since the last reset (host, 3 entries each, may be NULL; as
+ * rsf_gossip_check_queues reports them); reset != 0 zeroes them and the occupancy
+ * histogram afterwards.  Synchronises. */
+int rsf_gossip_checker_stats(rsf_gossip* g, uint64_t* num_queued, uint64_t* n_warn, uint64_t* n_pruned, int reset);
+/* Occupancy at the checker ticks since the last reset (rsf_gossip_check_queues, or
+ * rsf_gossip_checker_stats with reset), before their prunes: hist (host, [3][bins], may be NULL)
  * counts the shard's members per queue whose item count falls in [b * bin, (b + 1) * bin),
  * the last bin everything above; max3 (host, 3, may be NULL) = the most items any member's
  * queue held.  bin / bins (may be NULL) return the histogram's geometry. */

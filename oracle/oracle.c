@@ -1032,10 +1032,19 @@ uint64_t orc_states_len(const orc_world* w, uint32_t m) {
   return known;
 }
 
-void orc_check_queues(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
-                      uint64_t* stats) {
+static int u64_cmp(const void* a, const void* b) {
+  const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+  return x < y ? -1 : x > y;
+}
+
+void orc_check_queues_phase(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue_depth,
+                            uint32_t depth_warning, uint32_t period, uint32_t phase, uint64_t* stats) {
   uint64_t st[9] = {0};
+  uint64_t* keys = NULL;
+  size_t kcap = 0;
+  if (!period) period = 1;
   for (uint32_t m = 0; m < w->n; ++m) {
+    if (m % period != phase) continue; /* this node's checker is not due this round */
     /* get_queue_max  base.rs:748-759: each node's checker reads its own members.states */
     uint64_t mx = max_queue_depth;
     if (min_queue_depth > 0) {
@@ -1049,27 +1058,36 @@ void orc_check_queues(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue
       for (uint32_t i = 0; i < hwm; ++i) numq += w->q_rumor[base + i] != EMPTY_RUMOR;
       st[q] += numq;
       if (numq >= depth_warning) st[3 + q]++;
-      while (numq > mx) { /* numq >= max -> prune(max): drop the max item until max remain */
-        uint32_t worst = EMPTY_RUMOR;
-        uint64_t kmax = 0;
-        for (uint32_t i = 0; i < hwm; ++i) {
-          if (w->q_rumor[base + i] == EMPTY_RUMOR) continue;
-          uint64_t k = tlq_key(w->q_tx[base + i], w->q_len[base + i], w->q_seq[base + i]);
-          if (worst == EMPTY_RUMOR || k > kmax) {
-            kmax = k;
-            worst = i;
-          }
-        }
-        w->q_rumor[base + worst] = EMPTY_RUMOR;
-        w->q_seq[base + worst] = 0;
-        w->q_tx[base + worst] = 0;
-        w->q_len[base + worst] = 0;
-        numq--;
-        st[6 + q]++;
+      if (numq <= mx) continue;
+      /* numq >= max -> prune(max): the items past the max-th in send order go, the largest
+       * first (the keys are distinct: seq is unique within a queue), so the max smallest stay */
+      if (numq > kcap) {
+        kcap = numq;
+        keys = (uint64_t*)realloc(keys, kcap * sizeof(uint64_t));
       }
+      uint32_t k = 0;
+      for (uint32_t i = 0; i < hwm; ++i)
+        if (w->q_rumor[base + i] != EMPTY_RUMOR) keys[k++] = tlq_key(w->q_tx[base + i], w->q_len[base + i], w->q_seq[base + i]);
+      qsort(keys, k, sizeof(uint64_t), u64_cmp);
+      const uint64_t T = mx ? keys[mx - 1] : 0;
+      for (uint32_t i = 0; i < hwm; ++i) {
+        if (w->q_rumor[base + i] == EMPTY_RUMOR) continue;
+        if (mx && tlq_key(w->q_tx[base + i], w->q_len[base + i], w->q_seq[base + i]) <= T) continue;
+        w->q_rumor[base + i] = EMPTY_RUMOR;
+        w->q_seq[base + i] = 0;
+        w->q_tx[base + i] = 0;
+        w->q_len[base + i] = 0;
+      }
+      st[6 + q] += numq - mx;
     }
   }
+  free(keys);
   if (stats) memcpy(stats, st, sizeof(st));
+}
+
+void orc_check_queues(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
+                      uint64_t* stats) {
+  orc_check_queues_phase(w, max_queue_depth, min_queue_depth, depth_warning, 1, 0, stats);
 }
 
 /* kRandomNodes model: k distinct live peers != m, Philox-drawn (memberlist util.go; unpinned) */

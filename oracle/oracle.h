@@ -322,6 +322,10 @@ uint64_t orc_states_len(const orc_world* w, uint32_t m);
  * per queue queued items, members at/above depth_warning, items pruned. */
 void orc_check_queues(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
                       uint64_t* stats);
+/* The same tick at the members whose id is phase mod period only (each node's QueueChecker
+ * runs on its own timer, base.rs:703-735: staggered ticks, one phase per round). */
+void orc_check_queues_phase(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue_depth,
+                            uint32_t depth_warning, uint32_t period, uint32_t phase, uint64_t* stats);
 
 uint32_t orc_msg_len(uint8_t type, uint64_t ltime, uint32_t name_len, uint32_t payload_len);
 /* origination size checks: 0 or the status (include/ruserf_amd.h RSF_ERR_USER_EVENT_* = -20..-22,

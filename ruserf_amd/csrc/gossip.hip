@@ -1006,11 +1006,12 @@ __device__ __forceinline__ uint32_t pend_flush_any(const GCfg& c, const GState& 
 static_assert(sizeof(QLds4) >= sizeof(QLds), "a QLds4 row holds a QLds");
 
 // every member's pending re-queues applied (before anything but emission reads the queues)
-__global__ void __launch_bounds__(256) pend_flush_kernel(GCfg c, GState s) {
+// period > 1: only the members whose global id is phase mod period (a staggered checker tick)
+__global__ void __launch_bounds__(256) pend_flush_kernel(GCfg c, GState s, uint32_t period, uint32_t phase) {
   __shared__ QLds4 rows[kWavesPerBlock];
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  if (l >= c.n_loc) return;
+  if (l >= c.n_loc || (c.lo + l) % period != phase) return;
   const uint32_t pc = s.p_cnt[l];
   if (!pc) return;
   if (pend_flush_any(c, s, l, lane, pc, rows[threadIdx.x / kWave]) && lane == 0) s.err[l] |= kErrQueue;
@@ -2806,9 +2807,10 @@ constexpr uint32_t kOccBin = 64, kOccBins = 160;  // occupancy histogram: 64-ite
 __global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uint32_t max_depth, uint32_t warn,
                                                            unsigned long long* __restrict__ stats,
                                                            const uint32_t* __restrict__ qmax,
-                                                           uint32_t* __restrict__ hist) {
+                                                           uint32_t* __restrict__ hist, uint32_t period,
+                                                           uint32_t phase) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= c.n_loc * 3) return;
+  if (t >= c.n_loc * 3 || (c.lo + t / 3) % period != phase) return;
   const uint32_t q = (uint32_t)(t % 3);
   if (qmax) max_depth = qmax[t / 3];
   const uint64_t base = t * c.qcap;
@@ -2840,10 +2842,10 @@ __global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uin
 // (reconnect_kernel): the N - S untracked members, the local node when it is a subject, and
 // the tracked subjects whose entry is KNOWN.  One wave per member; out[l] saturates at 2^32-1.
 __global__ void __launch_bounds__(256) queue_max_kernel(GCfg c, GState s, uint32_t min_depth,
-                                                        uint32_t* __restrict__ out) {
+                                                        uint32_t* __restrict__ out, uint32_t period, uint32_t phase) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint64_t l = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
-  if (l >= c.n_loc) return;
+  if (l >= c.n_loc || (c.lo + l) % period != phase) return;
   const int32_t own = s.member_subj[l];
   const ViewE* row = s.view + l * c.S;
   uint64_t known = (c.N - c.S) + (own >= 0 ? 1u : 0u);
@@ -3104,9 +3106,9 @@ static void mark(rsf_gossip* g, int k) {
 
 // Every member's pending re-queues applied to its queues: before anything other than
 // emission reads the queues, the queue-prune counters or the error flags.
-static int flush_pending(rsf_gossip* g) {
+static int flush_pending(rsf_gossip* g, uint32_t period = 1, uint32_t phase = 0) {
   hipLaunchKernelGGL(pend_flush_kernel, dim3(grid1(g->c.n_loc, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0,
-                     g->stream, g->c, g->s);
+                     g->stream, g->c, g->s, period, phase);
   RSF_HIP(hipGetLastError());
   return RSF_OK;
 }
@@ -4292,36 +4294,46 @@ int rsf_gossip_set_now(rsf_gossip* g, uint32_t now) {
   return RSF_OK;
 }
 
-int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
-                            uint64_t* num_queued, uint64_t* n_warn, uint64_t* n_pruned) {
-  if (!g) return gerr("null context");
+// one checker tick at the members whose global id is phase mod period (period 1: all), on
+// the engine's stream; reset: the stats block and the occupancy histogram start from zero
+static int check_launch(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
+                        uint32_t period, uint32_t phase, bool reset) {
   const GCfg& c = g->c;
   // get_queue_max (base.rs:748-759): max_queue_depth, or (min_queue_depth > 0) per member
   // max(2 * members.states.len(), min_queue_depth) -- queue_max_kernel
   const uint32_t max_depth = max_queue_depth;
   RSF_HIP(hipSetDevice(g->device));
-  int rc = flush_pending(g);
+  int rc = flush_pending(g, period, phase);
   if (rc) return rc;
   if (min_queue_depth > 0) {
     if (!g->qmax && (rc = dmalloc((void**)&g->qmax, c.n_loc * 4))) return rc;
     hipLaunchKernelGGL(queue_max_kernel, dim3(grid1(c.n_loc, 256 / kWave)), dim3(256), 0, g->stream, c, g->s,
-                       min_queue_depth, g->qmax);
+                       min_queue_depth, g->qmax, period, phase);
     RSF_HIP(hipGetLastError());
   }
   const uint32_t* qmax = min_queue_depth > 0 ? g->qmax : nullptr;
   const size_t hist_words = 3 * (kOccBins + 1) + 3;
-  if (!g->occ_hist && (rc = dmalloc((void**)&g->occ_hist, hist_words * 4))) return rc;
-  RSF_HIP(hipMemsetAsync(g->occ_hist, 0, hist_words * 4, g->stream));
-  RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, g->stream));
+  if (!g->occ_hist) {
+    if ((rc = dmalloc((void**)&g->occ_hist, hist_words * 4))) return rc;
+    reset = true;
+  }
+  if (reset) {
+    RSF_HIP(hipMemsetAsync(g->occ_hist, 0, hist_words * 4, g->stream));
+    RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, g->stream));
+  }
   if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 16, g->stream));
   hipLaunchKernelGGL(check_queues_kernel, dim3(grid1(c.n_loc * 3)), dim3(256), 0, g->stream, c, g->s, max_depth,
-                     depth_warning, g->d_counters + 40, qmax, g->occ_hist);
+                     depth_warning, g->d_counters + 40, qmax, g->occ_hist, period, phase);
   RSF_HIP(hipGetLastError());
   if (c.deep) {  // the deep queues over the max: the smallest max keys of head and tail kept
     hipLaunchKernelGGL(check_stream_kernel, dim3(g->deep_check_blocks), dim3(kDeepThreads), 0, g->stream, c, g->s,
                        max_depth, qmax);
     RSF_HIP(hipGetLastError());
   }
+  return RSF_OK;
+}
+
+static int check_stats(rsf_gossip* g, uint64_t* num_queued, uint64_t* n_warn, uint64_t* n_pruned) {
   unsigned long long st[9];
   RSF_HIP(hipMemcpyAsync(st, g->d_counters + 40, sizeof(st), hipMemcpyDeviceToHost, g->stream));
   RSF_HIP(hipStreamSynchronize(g->stream));
@@ -4331,6 +4343,41 @@ int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t mi
     if (n_pruned) n_pruned[q] = st[6 + q];
   }
   return RSF_OK;
+}
+
+int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
+                            uint64_t* num_queued, uint64_t* n_warn, uint64_t* n_pruned) {
+  if (!g) return gerr("null context");
+  int rc = check_launch(g, max_queue_depth, min_queue_depth, depth_warning, 1, 0, true);
+  return rc ? rc : check_stats(g, num_queued, n_warn, n_pruned);
+}
+
+int rsf_gossip_check_queues_phase(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_queue_depth,
+                                  uint32_t depth_warning, uint32_t period, uint32_t phase) {
+  if (!g) return gerr("null context");
+  if (!period || phase >= period) return gerr("phase must be below a non-zero period");
+  return check_launch(g, max_queue_depth, min_queue_depth, depth_warning, period, phase, false);
+}
+
+int rsf_gossip_checker_stats(rsf_gossip* g, uint64_t* num_queued, uint64_t* n_warn, uint64_t* n_pruned, int reset) {
+  if (!g) return gerr("null context");
+  RSF_HIP(hipSetDevice(g->device));
+  const bool have = g->occ_hist != nullptr;
+  int rc = RSF_OK;
+  if (have) {
+    rc = check_stats(g, num_queued, n_warn, n_pruned);
+  } else {
+    for (int q = 0; q < 3; ++q) {
+      if (num_queued) num_queued[q] = 0;
+      if (n_warn) n_warn[q] = 0;
+      if (n_pruned) n_pruned[q] = 0;
+    }
+  }
+  if (!rc && reset && have) {
+    RSF_HIP(hipMemsetAsync(g->occ_hist, 0, (3 * (kOccBins + 1) + 3) * 4, g->stream));
+    RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, g->stream));
+  }
+  return rc;
 }
 
 int rsf_gossip_action_status(rsf_gossip* g, int32_t* status, uint32_t n) {

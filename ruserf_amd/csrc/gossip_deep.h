@@ -903,39 +903,25 @@ __global__ void __launch_bounds__(kWave) emit_deep_wave_kernel(GCfg c, GState s,
 #endif
 }
 
-// ---- the QueueChecker's prune streaming from HBM (check_stream_kernel) -------------------
-// A queue's items indexed i < qcap: head slot i (live if its rumor is set), i >= qcap: tail
-// item i - qcap.  Nothing is staged in LDS but a histogram and the items that change place, so
-// a CU holds eight of these blocks instead of one LDS-bound block; the passes after the first
-// re-read the queue from the caches (a member's queue is ~130 KB at the reference's regime).
-struct StreamQ {
-  const uint32_t *hr, *hs, *ht;  // head slots: rumor, seq, transmits | len << 16
-  const uint4* t;                // tail
-  uint32_t qcap, tc;
-};
-__device__ __forceinline__ bool sq_key(const StreamQ& Q, uint32_t i, uint64_t& k) {
-  if (i < Q.qcap) {
-    if (Q.hr[i] == kEmpty) return false;
-    const uint32_t tl = Q.ht[i];
-    k = tlq_key(tl & 0xFFFF, tl >> 16, Q.hs[i]);
-    return true;
-  }
-  const uint4 e = Q.t[i - Q.qcap];
-  k = tlq_key(e.z & 0xFFFF, e.z >> 16, e.y);
-  return true;
-}
-
-struct StreamLds {
-  uint32_t hist[256];
+// ---- the QueueChecker's prune (check_stream_kernel) --------------------------------------
+// One block per listed (member, queue).  Pass 1 streams head and tail once and keeps only the
+// 8-B keys in LDS (live head keys first, then the tail's in index order); the three selects
+// (the max-th key, the new head's qcap-th, the reserve's (qcap + R)-th) run together over the
+// LDS keys, one histogram each per radix pass; pass 2 streams the tail again and compacts it
+// in place, eight loads in flight per thread.  Two blocks per CU (the keys of a full queue are
+// 70 KB).
+struct CheckLds {
+  uint32_t hist[3][256];
   uint64_t w64[kDeepWaves], w64b[kDeepWaves];
-  uint32_t sel_digit, sel_need, sel_cnt, nb, nr, nh;
+  uint32_t wcnt[kDeepU][kDeepWaves];
+  uint32_t sel_digit[3], sel_need[3], nb, nr, nh, hn;
   uint4 hitem[kWave];         // the new head's items (<= qcap)
   uint64_t hkey[kWave];
   uint4 ritem[kDeepReserve];  // the reserve (written after the sealed group)
 };
 
 // block-uniform minimum (every thread calls)
-__device__ __forceinline__ uint64_t blk_min_u64(uint64_t v, StreamLds& d) {
+__device__ __forceinline__ uint64_t blk_min_u64(uint64_t v, CheckLds& d) {
   v = wave_min_u64(v);
   __syncthreads();
   if ((threadIdx.x & (kWave - 1)) == 0) d.w64[threadIdx.x / kWave] = v;
@@ -946,100 +932,95 @@ __device__ __forceinline__ uint64_t blk_min_u64(uint64_t v, StreamLds& d) {
   return m;
 }
 
-// the k-th smallest live key (1 <= k <= live count) by a radix select over the streamed keys;
-// bytes every live key shares (from the caller's AND / OR) take no pass; a digit's lanes that
-// agree with the wave's first active lane are counted by that lane alone (a saturated queue's
-// keys share their transmit and high seq bytes: one LDS address would take thousands of
-// atomics); the select stops once the chosen bucket holds one key
-__device__ uint64_t stream_select_kth(const StreamQ& Q, StreamLds& d, uint32_t k, uint64_t an, uint64_t orr) {
-  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), n = Q.qcap + Q.tc;
+// the ks[j]-th smallest of the n LDS keys for each active j (1 <= ks[j] <= n), by a radix
+// select over the bytes where the keys differ (from the caller's AND / OR), the three selects
+// sharing each pass over the keys.  A digit's lanes that agree with the wave's first active
+// lane are counted by that lane alone (a saturated queue's keys share their transmit byte: one
+// LDS address would take thousands of atomics).
+__device__ void lds_select3(const uint64_t* __restrict__ keys, uint32_t n, CheckLds& d, const uint32_t ks[3],
+                            const bool act[3], uint64_t an, uint64_t orr, uint64_t out[3]) {
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   const uint64_t var = an ^ orr;
-  uint64_t prefix = 0, mask = 0;
-  uint32_t need = k;
+  uint64_t prefix[3] = {0, 0, 0}, mask = 0;
+  uint32_t need[3] = {ks[0], ks[1], ks[2]};
   for (int shift = 56; shift >= 0; shift -= 8) {
     const uint64_t bm = 0xFFull << shift;
     if (!(var & bm)) {
-      prefix |= an & bm;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) prefix[j] |= an & bm;
       mask |= bm;
       continue;
     }
     __syncthreads();
-    for (uint32_t i = tid; i < 256; i += kDeepThreads) d.hist[i] = 0;
+    for (uint32_t i = tid; i < 3 * 256; i += kDeepThreads) (&d.hist[0][0])[i] = 0;
     __syncthreads();
-    for (uint32_t b = 0; b < n; b += kDeepU * kDeepThreads) {
-      uint64_t x[kDeepU];
-      bool v[kDeepU];
+    for (uint32_t i0 = 0; i0 < n; i0 += kDeepThreads) {
+      const uint32_t i = i0 + tid;
+      const bool v = i < n;
+      const uint64_t x = v ? keys[i] : 0ull;
+      const uint32_t dg = (uint32_t)(x >> shift) & 0xFF;
 #pragma unroll
-      for (uint32_t u = 0; u < kDeepU; ++u) {
-        const uint32_t i = b + u * kDeepThreads + tid;
-        x[u] = 0;
-        v[u] = i < n && sq_key(Q, i, x[u]);
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < kDeepU; ++u) {
-        const bool in = v[u] && (x[u] & mask) == prefix;
-        const uint32_t dg = in ? (uint32_t)(x[u] >> shift) & 0xFF : 0u;
+      for (int j = 0; j < 3; ++j) {
+        if (!act[j]) continue;
+        const bool in = v && (x & mask) == prefix[j];
         const uint64_t am = ballot(in);
         if (!am) continue;
         const int f = __ffsll((long long)am) - 1;
         const uint32_t d0 = shfl_u32(dg, f);
         const uint64_t same = ballot(in && dg == d0);
-        if (lane == (uint32_t)f) atomicAdd(&d.hist[d0], (uint32_t)__popcll(same));
-        else if (in && dg != d0) atomicAdd(&d.hist[dg], 1u);
+        if (lane == (uint32_t)f) atomicAdd(&d.hist[j][d0], (uint32_t)__popcll(same));
+        else if (in && dg != d0) atomicAdd(&d.hist[j][dg], 1u);
       }
     }
     __syncthreads();
-    if (tid < kWave) {  // running counts over the 256 bins, four per lane
-      const uint32_t h0 = d.hist[4 * tid], h1 = d.hist[4 * tid + 1], h2 = d.hist[4 * tid + 2], h3 = d.hist[4 * tid + 3];
+    const bool aw = w == 0 ? act[0] : w == 1 ? act[1] : w == 2 ? act[2] : false;
+    if (aw) {  // wave j picks select j's digit: running counts, four bins per lane
+      const uint32_t* h = d.hist[w];
+      const uint32_t h0 = h[4 * lane], h1 = h[4 * lane + 1], h2 = h[4 * lane + 2], h3 = h[4 * lane + 3];
       const uint32_t sum = h0 + h1 + h2 + h3, incl = wave_inclusive_sum_u32(sum), excl = incl - sum;
-      if (excl < need && need <= incl) {
-        uint32_t b = 0, acc = excl, hb = h0;
-        if (acc + h0 < need) {
+      const uint32_t nd = w == 0 ? need[0] : w == 1 ? need[1] : need[2];
+      if (excl < nd && nd <= incl) {
+        uint32_t b = 0, acc = excl;
+        if (acc + h0 < nd) {
           acc += h0;
           b = 1;
-          hb = h1;
-          if (acc + h1 < need) {
+          if (acc + h1 < nd) {
             acc += h1;
             b = 2;
-            hb = h2;
-            if (acc + h2 < need) {
+            if (acc + h2 < nd) {
               acc += h2;
               b = 3;
-              hb = h3;
             }
           }
         }
-        d.sel_digit = 4 * tid + b;
-        d.sel_need = need - acc;
-        d.sel_cnt = hb;
+        d.sel_digit[w] = 4 * lane + b;
+        d.sel_need[w] = nd - acc;
       }
     }
     __syncthreads();
-    prefix |= (uint64_t)d.sel_digit << shift;
-    mask |= bm;
-    need = d.sel_need;
-    if (d.sel_cnt == 1 && shift > 0) {  // one key left under the prefix: it is the k-th
-      uint64_t best = ~0ull;
-      for (uint32_t i = tid; i < n; i += kDeepThreads) {
-        uint64_t x = 0;
-        if (sq_key(Q, i, x) && (x & mask) == prefix) best = x;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      if (act[j]) {
+        prefix[j] |= (uint64_t)d.sel_digit[j] << shift;
+        need[j] = d.sel_need[j];
       }
-      return blk_min_u64(best, d);
-    }
+    mask |= bm;
   }
-  return prefix;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) out[j] = prefix[j];
 }
 
 // QueueChecker prune of the deep queues check_queues_kernel listed (entries l * 3 + q): keep the
 // `max` smallest keys (each member's own max with qmax), the head refilled with the qcap
 // smallest of them, the tail = the rest in the two groups w_store_tail writes (sealed above the
 // reserve), exact bounds.  The tail is compacted in place in index order (an item is written at
-// or below the position it was read from, after every thread has read its chunk); the items
+// or below the position it was read from, after every thread has read its batch); the items
 // leaving the old head are written after the tail's.
 __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GState s, uint32_t max_depth,
                                                                     const uint32_t* __restrict__ qmax) {
-  __shared__ StreamLds d;
-  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
+  __shared__ CheckLds d;
+  __shared__ uint64_t keys[kDeepItems];
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   const uint32_t n_list = *s.deep_n;
   for (uint32_t it = blockIdx.x; it < n_list; it += gridDim.x) {
     const uint32_t e = s.deep_ids[it];
@@ -1048,102 +1029,138 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
     if (l >= c.n_loc || !tcap_of(c, q)) continue;
     const uint32_t keep = qmax ? qmax[l] : max_depth;
     const uint64_t hb = (l * 3 + q) * c.qcap;
-    const StreamQ Q{s.q_rumor + hb, s.q_seq + hb, s.q_txlen + hb, tail_of(s, q) + l * tstride_of(c, q), c.qcap,
-                    s.tsum[l * 3 + q].x};
-    const uint32_t n = c.qcap + Q.tc;
-    // live count, AND / OR of the live keys
+    const uint32_t tc = s.tsum[l * 3 + q].x;
+    if (c.qcap + tc > kDeepItems) continue;  // (the tail's capacity is below it: cannot happen)
+    uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
+    // pass 1: the keys into LDS, AND / OR of them
     uint64_t an = ~0ull, orr = 0;
-    uint32_t live = 0;
-    for (uint32_t i = tid; i < n; i += kDeepThreads) {
-      uint64_t x = 0;
-      if (sq_key(Q, i, x)) {
-        an &= x;
-        orr |= x;
-        live++;
+    if (w == 0) {
+      const bool live_h = lane < c.qcap && s.q_rumor[hb + lane] != kEmpty;
+      const uint64_t lm = ballot(live_h);
+      if (live_h) {
+        const uint32_t tl = s.q_txlen[hb + lane];
+        const uint64_t k = tlq_key(tl & 0xFFFF, tl >> 16, s.q_seq[hb + lane]);
+        keys[mbcnt(lm)] = k;
+        an = k;
+        orr = k;
+      }
+      if (lane == 0) d.hn = (uint32_t)__popcll(lm);
+    }
+    __syncthreads();
+    const uint32_t hn = d.hn, n = hn + tc;
+    for (uint32_t b = 0; b < tc; b += kDeepU * kDeepThreads) {
+      uint4 x[kDeepU];
+#pragma unroll
+      for (uint32_t u = 0; u < kDeepU; ++u) {
+        const uint32_t i = b + u * kDeepThreads + tid;
+        x[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kDeepU; ++u) {
+        const uint32_t i = b + u * kDeepThreads + tid;
+        if (i < tc) {
+          const uint64_t k = tlq_key(x[u].z & 0xFFFF, x[u].z >> 16, x[u].y);
+          keys[hn + i] = k;
+          an &= k;
+          orr |= k;
+        }
       }
     }
     an = wave_and_u64_blk(an);
     orr = wave_or_u64_blk(orr);
-    live = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(live), 63);
     __syncthreads();
     if (lane == 0) {
-      d.w64[tid / kWave] = an;
-      d.w64b[tid / kWave] = orr;
-      d.hist[tid / kWave] = live;
+      d.w64[w] = an;
+      d.w64b[w] = orr;
     }
-    __syncthreads();
-    an = d.w64[0];
-    orr = d.w64b[0];
-    live = d.hist[0];
-#pragma unroll
-    for (uint32_t w = 1; w < kDeepWaves; ++w) {
-      an &= d.w64[w];
-      orr |= d.w64b[w];
-      live += d.hist[w];
-    }
-    if (live <= keep) continue;  // (listed by the same count: cannot happen)
-    const uint64_t T = keep ? stream_select_kth(Q, d, keep, an, orr) : 0ull;  // the largest key kept
-    const uint64_t Th = keep > c.qcap ? stream_select_kth(Q, d, c.qcap, an, orr) : T;  // the new head's largest
-    const uint64_t TR = keep > c.qcap + kDeepReserve ? stream_select_kth(Q, d, c.qcap + kDeepReserve, an, orr) : T;
-    __syncthreads();
     if (tid == 0) {
       d.nb = 0;
       d.nr = 0;
       d.nh = 0;
     }
     __syncthreads();
+    an = d.w64[0];
+    orr = d.w64b[0];
+#pragma unroll
+    for (uint32_t v = 1; v < kDeepWaves; ++v) {
+      an &= d.w64[v];
+      orr |= d.w64b[v];
+    }
+    if (n <= keep) continue;  // (listed by the same count: cannot happen)
+    // the largest key kept, the new head's largest, the reserve's largest
+    const uint32_t ks[3] = {keep, c.qcap, c.qcap + kDeepReserve};
+    const bool act[3] = {keep > 0, keep > c.qcap, keep > c.qcap + kDeepReserve};
+    uint64_t sel[3];
+    lds_select3(keys, n, d, ks, act, an, orr, sel);
+    const uint64_t T = act[0] ? sel[0] : 0ull;
+    const uint64_t Th = act[1] ? sel[1] : T;
+    const uint64_t TR = act[2] ? sel[2] : T;
+    const bool any = act[0];
     uint64_t bmin = ~0ull, tmin = ~0ull;
     uint32_t tlmin = ~0u;
-    uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
-    // the tail in index order: the sealed group (TR < key <= T) compacted in place, the reserve
-    // (Th < key <= TR) and the new head's items (key <= Th) staged in LDS
-    for (uint32_t b = 0; b < Q.tc; b += kDeepThreads) {
-      const uint32_t i = b + tid;
-      const bool in = i < Q.tc;
-      uint4 x = make_uint4(0, 0, 0, 0);
-      uint64_t k = ~0ull;
-      if (in) {
-        x = t[i];
-        k = tlq_key(x.z & 0xFFFF, x.z >> 16, x.y);
-      }
-      const bool sealed = in && k > TR && k <= T, res = in && k > Th && k <= TR, head = in && k <= Th;
-      const uint64_t sm = ballot(sealed);
-      if (lane == 0) d.hist[tid / kWave] = (uint32_t)__popcll(sm);
-      __syncthreads();  // every thread has read its item: the chunk's positions may be rewritten
-      uint32_t before = 0, tot = 0;
+    // pass 2, the tail in index order: the sealed group (TR < key <= T) compacted in place, the
+    // reserve (Th < key <= TR) and the new head's items (key <= Th) staged in LDS
+    for (uint32_t b = 0; b < tc; b += kDeepU * kDeepThreads) {
+      uint4 x[kDeepU];
 #pragma unroll
-      for (uint32_t w = 0; w < kDeepWaves; ++w) {
-        const uint32_t cw = d.hist[w];
-        before += w < tid / kWave ? cw : 0u;
-        tot += cw;
+      for (uint32_t u = 0; u < kDeepU; ++u) {
+        const uint32_t i = b + u * kDeepThreads + tid;
+        x[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
       }
-      const uint32_t nb0 = d.nb;
-      if (sealed) {
-        t[nb0 + before + mbcnt(sm)] = x;
-        bmin = k < bmin ? k : bmin;
-        tlmin = min(tlmin, key_len(k));
+      uint64_t sm[kDeepU];
+#pragma unroll
+      for (uint32_t u = 0; u < kDeepU; ++u) {
+        const uint32_t i = b + u * kDeepThreads + tid;
+        const uint64_t k = i < tc ? keys[hn + i] : ~0ull;
+        const bool in = any && i < tc;
+        sm[u] = ballot(in && k > TR && k <= T);
+        if (lane == 0) d.wcnt[u][w] = (uint32_t)__popcll(sm[u]);
       }
-      if (res) {
-        d.ritem[atomicAdd(&d.nr, 1u)] = x;
-        tmin = k < tmin ? k : tmin;
-        tlmin = min(tlmin, key_len(k));
-      }
-      if (head) {
-        const uint32_t j = atomicAdd(&d.nh, 1u);
-        d.hitem[j] = make_uint4(x.x, x.y, x.z, q == 0 ? x.w : 0u);
-        d.hkey[j] = k;
+      __syncthreads();  // every thread has read its batch: the batch's positions may be rewritten
+      uint32_t base = d.nb, tot = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < kDeepU; ++u)
+#pragma unroll
+        for (uint32_t v = 0; v < kDeepWaves; ++v) tot += d.wcnt[u][v];
+#pragma unroll
+      for (uint32_t u = 0; u < kDeepU; ++u) {
+        const uint32_t i = b + u * kDeepThreads + tid;
+        uint32_t before = 0;
+#pragma unroll
+        for (uint32_t v = 0; v < kDeepWaves; ++v) before += v < w ? d.wcnt[u][v] : 0u;
+        const uint64_t k = i < tc ? keys[hn + i] : ~0ull;
+        const bool in = any && i < tc;
+        const bool sealed = in && k > TR && k <= T, res = in && k > Th && k <= TR, head = in && k <= Th;
+        if (sealed) {
+          t[base + before + mbcnt(sm[u])] = x[u];
+          bmin = k < bmin ? k : bmin;
+          tlmin = min(tlmin, key_len(k));
+        }
+        if (res) {
+          d.ritem[atomicAdd(&d.nr, 1u)] = x[u];
+          tmin = k < tmin ? k : tmin;
+          tlmin = min(tlmin, key_len(k));
+        }
+        if (head) {
+          const uint32_t j = atomicAdd(&d.nh, 1u);
+          d.hitem[j] = make_uint4(x[u].x, x[u].y, x[u].z, q == 0 ? x[u].w : 0u);
+          d.hkey[j] = k;
+        }
+#pragma unroll
+        for (uint32_t v = 0; v < kDeepWaves; ++v) base += d.wcnt[u][v];
       }
       __syncthreads();
-      if (tid == 0) d.nb = nb0 + tot;
+      if (tid == 0) d.nb += tot;
       __syncthreads();
     }
     // the old head's items: to the new head, the reserve, or the sealed group (appended)
     if (tid < kWave) {
-      const bool live_h = tid < c.qcap && Q.hr[tid] != kEmpty;
+      const bool live_h = any && tid < c.qcap && s.q_rumor[hb + tid] != kEmpty;
       uint4 x = make_uint4(0, 0, 0, 0);
       uint64_t k = ~0ull;
       if (live_h) {
-        x = make_uint4(Q.hr[tid], Q.hs[tid], Q.ht[tid], q == 0 ? s.q_dec[l * c.qcap + tid] : 0u);
+        x = make_uint4(s.q_rumor[hb + tid], s.q_seq[hb + tid], s.q_txlen[hb + tid],
+                       q == 0 ? s.q_dec[l * c.qcap + tid] : 0u);
         k = tlq_key(x.z & 0xFFFF, x.z >> 16, x.y);
       }
       const bool sealed = live_h && k > TR && k <= T, res = live_h && k > Th && k <= TR, head = live_h && k <= Th;
@@ -1190,11 +1207,10 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
     tmin = bmin < tmin ? bmin : tmin;
     uint32_t lm = wave_min_u32(tlmin);
     __syncthreads();
-    if (lane == 0) d.hist[tid / kWave] = lm;
+    if (lane == 0) d.wcnt[0][w] = lm;
     __syncthreads();
     if (tid == 0) {
-      for (uint32_t w = 1; w < kDeepWaves; ++w) lm = min(lm, d.hist[w]);
-      lm = min(lm, d.hist[0]);
+      for (uint32_t v = 0; v < kDeepWaves; ++v) lm = min(lm, d.wcnt[0][v]);
       const uint32_t cnt = nb + nr;
       s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, lm, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
       s.tseal[l * 3 + q] = nb ? make_uint4(nb, (uint32_t)bmin, (uint32_t)(bmin >> 32), 0u) : kTSumEmpty;

@@ -404,6 +404,21 @@ class GossipEngine:
                                             ptr(q, C.c_uint64), ptr(w, C.c_uint64), ptr(p, C.c_uint64)))
         return {"queued": q, "warn": w, "pruned": p}
 
+    def check_queues_phase(self, period, phase, max_queue_depth=MAX_QUEUE_DEPTH, min_queue_depth=MIN_QUEUE_DEPTH,
+                           depth_warning=QUEUE_DEPTH_WARNING):
+        """A staggered QueueChecker tick: the same tick at the members whose global id is
+        phase mod period only (each node's checker runs on its own timer).  Asynchronous;
+        the counts accumulate until checker_stats(reset=True)."""
+        check(lib().rsf_gossip_check_queues_phase(self._h, max_queue_depth, min_queue_depth, depth_warning,
+                                                  int(period), int(phase)))
+
+    def checker_stats(self, reset=False):
+        """{queued, warn, pruned} accumulated by the checker ticks since the last reset"""
+        q, w, p = (np.zeros(3, dtype=np.uint64) for _ in range(3))
+        check(lib().rsf_gossip_checker_stats(self._h, ptr(q, C.c_uint64), ptr(w, C.c_uint64), ptr(p, C.c_uint64),
+                                             int(bool(reset))))
+        return {"queued": q, "warn": w, "pruned": p}
+
     def deep_stats(self):
         """(members that took the exact whole-queue emission since creation, since the last call)"""
         a, b = C.c_uint64(), C.c_uint64()

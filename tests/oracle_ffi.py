@@ -233,6 +233,9 @@ def lib():
     L.orc_query_check.restype = C.c_int32
     L.orc_check_queues.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint32, C.c_uint32, P64]
     L.orc_check_queues.restype = None
+    L.orc_check_queues_phase.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                         C.c_uint32, P64]
+    L.orc_check_queues_phase.restype = None
     L.orc_reap.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
     L.orc_varint_len.argtypes = [C.c_uint64]
     L.orc_varint_len.restype = C.c_uint32

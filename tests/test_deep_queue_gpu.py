@@ -105,6 +105,67 @@ def test_deep_steady_state_ticks_bit_exact():
     L.orc_world_free(C.byref(w))
 
 
+def test_deep_staggered_ticks_bit_exact():
+    """Staggered QueueChecker ticks (rsf_gossip_check_queues_phase: each node's checker on
+    its own timer, one phase of 25 after every round) in the reference's queue regime at the
+    bench's saturated shape: every member's intent queue is pruned to 1 100 once per 25
+    rounds, at its own round, by the streaming prune; bit-exact against the oracle's phased
+    tick (orc_check_queues_phase), compared every 5 rounds, and the accumulated counts equal."""
+    n, s, rounds, period, mx = 8000, 4096, 80, 25, 1100
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=64, queue_depth=(8192, 0, 0), gossip_limit=8 * 24,
+                         gossip_overhead=2, max_rumors=1 << 20, event_buffer_size=512, query_buffer_size=512,
+                         slot_k=1)
+    subj, acts, ml = W.intents_workload(n, s, rounds, rate=0.05, seed=78)
+    g, w = pair(cfg, subj, W.initial_views(s))
+    exp_tot = np.zeros(9, dtype=np.uint64)
+    g.checker_stats(reset=True)
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t], threads=16)
+        g.check_queues_phase(period, (t + 1) % period, mx, 0, 128)
+        exp = (C.c_uint64 * 9)()
+        L.orc_check_queues_phase(C.byref(w), mx, 0, 128, period, (t + 1) % period, exp)
+        exp_tot += np.array(list(exp), dtype=np.uint64)
+        if (t + 1) % 5 == 0:
+            same(g, w, f"round {t}")
+    got = g.checker_stats(reset=True)
+    assert list(got["queued"]) + list(got["warn"]) + list(got["pruned"]) == list(exp_tot)
+    assert int(exp_tot[6]) > 0
+    assert list(g.checker_stats()["queued"]) == [0, 0, 0]  # reset
+    st = H.engine_state(g, H.world_width(w))
+    assert int(st["q_pruned"].sum()) == 0 and int(st["q_expired"].sum()) == 0
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
+@pytest.mark.parametrize("qcap,depth", [(16, 100), (32, 0)])
+def test_staggered_ticks_churn_bit_exact(qcap, depth):
+    """Phased ticks over all three queues with churn, deep (head + tail) and bounded queues:
+    each round's phase of 4 prunes to a max small enough to bite; bit-exact every round."""
+    n, rounds, period = 1200, 20, 4
+    subj, acts, ml = W.churn_workload(n, rounds, events_per_round=30, queries_per_round=5, seed=qcap + depth)
+    s = len(subj)
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=qcap, queue_depth=(depth, depth, depth),
+                         gossip_limit=400, gossip_overhead=3, retransmit_mult=4, max_rumors=512,
+                         event_buffer_size=128, query_buffer_size=128, slot_k=8, max_refute=2)
+    g, w = pair(cfg, subj, W.initial_views(s))
+    mx = max(4, (depth or qcap) // 3)
+    pruned = 0
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t])
+        g.check_queues_phase(period, t % period, mx, 0, 8)
+        exp = (C.c_uint64 * 9)()
+        L.orc_check_queues_phase(C.byref(w), mx, 0, 8, period, t % period, exp)
+        pruned += sum(exp[6:9])
+        same(g, w, f"round {t}")
+    assert pruned > 0
+    with pytest.raises(Exception):
+        g.check_queues_phase(4, 4)
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
 @pytest.mark.parametrize("qcap,depth,limit,mult", [(16, 100, 400, 4), (64, 200, 260, 1), (8, 40, 600, 2),
                                                    (32, 64, 1400, 4)])
 def test_deep_churn_flood_prune_ring_bit_exact(qcap, depth, limit, mult):

@@ -366,6 +366,40 @@ def test_queue_prune_counted_and_checker():
     L.orc_world_free(C.byref(w))
 
 
+def test_checker_phases_compose_to_one_tick():
+    """Staggered ticks (orc_check_queues_phase: each node's checker on its own timer,
+    base.rs:703-735): the phases 0..p-1 of one period, with nothing in between, are one
+    tick over every member -- the same queues kept and the same counts; a phase's tick
+    touches only its own members."""
+    def world():
+        w = make_world(n=7, s=1, qcap=16)
+        r = 0
+        for m in range(7):
+            for i in range(5 + 2 * m):
+                w.rumors[r].type = 1
+                w.rumors[r].msg_len = 20 + (i % 3)
+                L.orc_queue_insert(C.byref(w), m, 0, r)
+                r += 1
+        return w
+    a, b = world(), world()
+    full = (C.c_uint64 * 9)()
+    L.orc_check_queues(C.byref(a), 6, 0, 8, full)
+    tot = np.zeros(9, dtype=np.uint64)
+    for ph in range(3):
+        before = [b.q_rumor[i] for i in range(7 * 3 * 16)]
+        st = (C.c_uint64 * 9)()
+        L.orc_check_queues_phase(C.byref(b), 6, 0, 8, 3, ph, st)
+        tot += np.array(list(st), dtype=np.uint64)
+        for m in range(7):
+            if m % 3 != ph:  # other phases' members untouched
+                assert [b.q_rumor[i] for i in range(m * 48, m * 48 + 48)] == before[m * 48:m * 48 + 48]
+    assert list(tot) == list(full)
+    assert [a.q_rumor[i] for i in range(7 * 3 * 16)] == [b.q_rumor[i] for i in range(7 * 3 * 16)]
+    assert int(full[6]) == sum(max(0, min(5 + 2 * m, 16) - 6) for m in range(7))  # (16 slots: one dropped on insert)
+    L.orc_world_free(C.byref(a))
+    L.orc_world_free(C.byref(b))
+
+
 def test_queue_depth_per_queue_and_checker():
     """Per-queue capacities (orc_world_cfg.qdepth, the engine's queue_depth): each queue
     prunes at its own depth, slots past it stay unused, scans stop at the high-water mark,
