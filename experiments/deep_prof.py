@@ -25,7 +25,7 @@ subj, acts, ml = W.intents_workload(n, B.SUBJECTS, rounds, rate=0.01, seed=B.SEE
 eng = GossipEngine(cfg)
 eng.set_subjects(subj)
 eng.init_views(*W.initial_views(B.SUBJECTS))
-buf = (C.c_uint64 * 64)()
+buf = (C.c_uint64 * 80)()
 for t in range(settle):
     eng.round(t, ml[t], acts[t])
 torch.cuda.synchronize()

@@ -58,7 +58,7 @@ __device__ unsigned long long g_merge_prof[8];
 #define RSF_DEEP_PROF 0
 #endif
 #if RSF_DEEP_PROF
-__device__ unsigned long long g_deep_prof[64];
+__device__ unsigned long long g_deep_prof[80];
 #define RSF_DEEP_WHY(k) \
   do {                  \
     if (lane == 0) atomicAdd(&g_deep_prof[(k)], 1ull); \
@@ -1006,12 +1006,22 @@ __device__ __forceinline__ uint32_t pend_flush_any(const GCfg& c, const GState& 
 static_assert(sizeof(QLds4) >= sizeof(QLds), "a QLds4 row holds a QLds");
 
 // every member's pending re-queues applied (before anything but emission reads the queues)
-// period > 1: only the members whose global id is phase mod period (a staggered checker tick)
+// period > 1: only the members whose global id is phase mod period (a staggered checker tick);
+// the grids run over those members only: local ids phase_first + i * period
+__host__ __device__ inline uint64_t phase_first(const GCfg& c, uint32_t period, uint32_t phase) {
+  return (phase + period - (uint32_t)(c.lo % period)) % period;
+}
+__host__ __device__ inline uint64_t phase_count(const GCfg& c, uint32_t period, uint32_t phase) {
+  const uint64_t l0 = phase_first(c, period, phase);
+  return c.n_loc > l0 ? (c.n_loc - l0 + period - 1) / period : 0;
+}
 __global__ void __launch_bounds__(256) pend_flush_kernel(GCfg c, GState s, uint32_t period, uint32_t phase) {
   __shared__ QLds4 rows[kWavesPerBlock];
   const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  if (l >= c.n_loc || (c.lo + l) % period != phase) return;
+  const uint64_t l = phase_first(c, period, phase) +
+                     ((uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)) *
+                         period;
+  if (l >= c.n_loc) return;
   const uint32_t pc = s.p_cnt[l];
   if (!pc) return;
   if (pend_flush_any(c, s, l, lane, pc, rows[threadIdx.x / kWave]) && lane == 0) s.err[l] |= kErrQueue;
@@ -2809,9 +2819,11 @@ __global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uin
                                                            const uint32_t* __restrict__ qmax,
                                                            uint32_t* __restrict__ hist, uint32_t period,
                                                            uint32_t phase) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= c.n_loc * 3 || (c.lo + t / 3) % period != phase) return;
-  const uint32_t q = (uint32_t)(t % 3);
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t l = phase_first(c, period, phase) + (i / 3) * period;
+  if (l >= c.n_loc) return;
+  const uint32_t q = (uint32_t)(i % 3);
+  const uint64_t t = l * 3 + q;
   if (qmax) max_depth = qmax[t / 3];
   const uint64_t base = t * c.qcap;
   uint32_t n = 0;
@@ -2844,8 +2856,8 @@ __global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uin
 __global__ void __launch_bounds__(256) queue_max_kernel(GCfg c, GState s, uint32_t min_depth,
                                                         uint32_t* __restrict__ out, uint32_t period, uint32_t phase) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint64_t l = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
-  if (l >= c.n_loc || (c.lo + l) % period != phase) return;
+  const uint64_t l = phase_first(c, period, phase) + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave * period;
+  if (l >= c.n_loc) return;
   const int32_t own = s.member_subj[l];
   const ViewE* row = s.view + l * c.S;
   uint64_t known = (c.N - c.S) + (own >= 0 ? 1u : 0u);
@@ -3107,7 +3119,9 @@ static void mark(rsf_gossip* g, int k) {
 // Every member's pending re-queues applied to its queues: before anything other than
 // emission reads the queues, the queue-prune counters or the error flags.
 static int flush_pending(rsf_gossip* g, uint32_t period = 1, uint32_t phase = 0) {
-  hipLaunchKernelGGL(pend_flush_kernel, dim3(grid1(g->c.n_loc, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0,
+  const uint64_t cnt = phase_count(g->c, period, phase);
+  if (!cnt) return RSF_OK;
+  hipLaunchKernelGGL(pend_flush_kernel, dim3(grid1(cnt, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0,
                      g->stream, g->c, g->s, period, phase);
   RSF_HIP(hipGetLastError());
   return RSF_OK;
@@ -4090,8 +4104,8 @@ int rsf_gossip_debug_ptrs(rsf_gossip* g, uint64_t* out, uint32_t n) {
 int rsf_gossip_deep_prof(uint64_t* out64) {
 #if RSF_DEEP_PROF
   RSF_HIP(hipDeviceSynchronize());
-  RSF_HIP(hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_deep_prof), 64 * sizeof(uint64_t)));
-  unsigned long long z[64] = {};
+  RSF_HIP(hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_deep_prof), 80 * sizeof(uint64_t)));
+  unsigned long long z[80] = {};
   RSF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_deep_prof), z, sizeof(z)));
   return 0;
 #else
@@ -4307,8 +4321,8 @@ static int check_launch(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_qu
   if (rc) return rc;
   if (min_queue_depth > 0) {
     if (!g->qmax && (rc = dmalloc((void**)&g->qmax, c.n_loc * 4))) return rc;
-    hipLaunchKernelGGL(queue_max_kernel, dim3(grid1(c.n_loc, 256 / kWave)), dim3(256), 0, g->stream, c, g->s,
-                       min_queue_depth, g->qmax, period, phase);
+    hipLaunchKernelGGL(queue_max_kernel, dim3(grid1(std::max<uint64_t>(1, phase_count(c, period, phase)), 256 / kWave)),
+                       dim3(256), 0, g->stream, c, g->s, min_queue_depth, g->qmax, period, phase);
     RSF_HIP(hipGetLastError());
   }
   const uint32_t* qmax = min_queue_depth > 0 ? g->qmax : nullptr;
@@ -4322,8 +4336,9 @@ static int check_launch(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_qu
     RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, g->stream));
   }
   if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 16, g->stream));
-  hipLaunchKernelGGL(check_queues_kernel, dim3(grid1(c.n_loc * 3)), dim3(256), 0, g->stream, c, g->s, max_depth,
-                     depth_warning, g->d_counters + 40, qmax, g->occ_hist, period, phase);
+  hipLaunchKernelGGL(check_queues_kernel, dim3(grid1(std::max<uint64_t>(1, phase_count(c, period, phase)) * 3)),
+                     dim3(256), 0, g->stream, c, g->s, max_depth, depth_warning, g->d_counters + 40, qmax, g->occ_hist,
+                     period, phase);
   RSF_HIP(hipGetLastError());
   if (c.deep) {  // the deep queues over the max: the smallest max keys of head and tail kept
     hipLaunchKernelGGL(check_stream_kernel, dim3(g->deep_check_blocks), dim3(kDeepThreads), 0, g->stream, c, g->s,

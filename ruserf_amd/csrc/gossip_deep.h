@@ -939,6 +939,7 @@ __device__ __forceinline__ uint64_t blk_min_u64(uint64_t v, CheckLds& d) {
 // LDS address would take thousands of atomics).
 __device__ void lds_select3(const uint64_t* __restrict__ keys, uint32_t n, CheckLds& d, const uint32_t ks[3],
                             const bool act[3], uint64_t an, uint64_t orr, uint64_t out[3]) {
+  constexpr uint32_t U = 4;
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   const uint64_t var = an ^ orr;
   uint64_t prefix[3] = {0, 0, 0}, mask = 0;
@@ -951,31 +952,43 @@ __device__ void lds_select3(const uint64_t* __restrict__ keys, uint32_t n, Check
       mask |= bm;
       continue;
     }
+    // selects whose prefixes agree share one histogram (always at the first varying byte)
+    const uint32_t al1 = act[1] && !(act[0] && prefix[1] == prefix[0]) ? 1u : 0u;
+    const uint32_t al2 = act[2] && !(act[0] && prefix[2] == prefix[0]) ? (act[1] && prefix[2] == prefix[1] ? al1 : 2u) : 0u;
+    const bool own[3] = {act[0], al1 == 1, al2 == 2};
     __syncthreads();
     for (uint32_t i = tid; i < 3 * 256; i += kDeepThreads) (&d.hist[0][0])[i] = 0;
     __syncthreads();
-    for (uint32_t i0 = 0; i0 < n; i0 += kDeepThreads) {
-      const uint32_t i = i0 + tid;
-      const bool v = i < n;
-      const uint64_t x = v ? keys[i] : 0ull;
-      const uint32_t dg = (uint32_t)(x >> shift) & 0xFF;
+    for (uint32_t i0 = 0; i0 < n; i0 += U * kDeepThreads) {
+      uint64_t x[U];
+      bool v[U];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        if (!act[j]) continue;
-        const bool in = v && (x & mask) == prefix[j];
-        const uint64_t am = ballot(in);
-        if (!am) continue;
-        const int f = __ffsll((long long)am) - 1;
-        const uint32_t d0 = shfl_u32(dg, f);
-        const uint64_t same = ballot(in && dg == d0);
-        if (lane == (uint32_t)f) atomicAdd(&d.hist[j][d0], (uint32_t)__popcll(same));
-        else if (in && dg != d0) atomicAdd(&d.hist[j][dg], 1u);
+      for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t i = i0 + u * kDeepThreads + tid;
+        v[u] = i < n;
+        x[u] = v[u] ? keys[i] : 0ull;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t dg = (uint32_t)(x[u] >> shift) & 0xFF;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          if (!own[j]) continue;
+          const bool in = v[u] && (x[u] & mask) == prefix[j];
+          const uint64_t am = ballot(in);
+          if (!am) continue;
+          const int f = __ffsll((long long)am) - 1;
+          const uint32_t d0 = shfl_u32(dg, f);
+          const uint64_t same = ballot(in && dg == d0);
+          if (lane == (uint32_t)f) atomicAdd(&d.hist[j][d0], (uint32_t)__popcll(same));
+          else if (in && dg != d0) atomicAdd(&d.hist[j][dg], 1u);
+        }
       }
     }
     __syncthreads();
     const bool aw = w == 0 ? act[0] : w == 1 ? act[1] : w == 2 ? act[2] : false;
     if (aw) {  // wave j picks select j's digit: running counts, four bins per lane
-      const uint32_t* h = d.hist[w];
+      const uint32_t* h = d.hist[w == 0 ? 0u : w == 1 ? al1 : al2];
       const uint32_t h0 = h[4 * lane], h1 = h[4 * lane + 1], h2 = h[4 * lane + 2], h3 = h[4 * lane + 3];
       const uint32_t sum = h0 + h1 + h2 + h3, incl = wave_inclusive_sum_u32(sum), excl = incl - sum;
       const uint32_t nd = w == 0 ? need[0] : w == 1 ? need[1] : need[2];
@@ -1022,7 +1035,14 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
   __shared__ uint64_t keys[kDeepItems];
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   const uint32_t n_list = *s.deep_n;
+#if RSF_DEEP_PROF
+  uint64_t pf[5] = {0, 0, 0, 0, 0}, pc = 0;
+#define RSF_CK(i) const uint64_t ck##i = clock64()
+#else
+#define RSF_CK(i)
+#endif
   for (uint32_t it = blockIdx.x; it < n_list; it += gridDim.x) {
+    RSF_CK(0);
     const uint32_t e = s.deep_ids[it];
     const uint64_t l = e / 3;
     const uint32_t q = e % 3;
@@ -1087,6 +1107,7 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
       orr |= d.w64b[v];
     }
     if (n <= keep) continue;  // (listed by the same count: cannot happen)
+    RSF_CK(1);
     // the largest key kept, the new head's largest, the reserve's largest
     const uint32_t ks[3] = {keep, c.qcap, c.qcap + kDeepReserve};
     const bool act[3] = {keep > 0, keep > c.qcap, keep > c.qcap + kDeepReserve};
@@ -1096,6 +1117,7 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
     const uint64_t Th = act[1] ? sel[1] : T;
     const uint64_t TR = act[2] ? sel[2] : T;
     const bool any = act[0];
+    RSF_CK(2);
     uint64_t bmin = ~0ull, tmin = ~0ull;
     uint32_t tlmin = ~0u;
     // pass 2, the tail in index order: the sealed group (TR < key <= T) compacted in place, the
@@ -1153,6 +1175,7 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
       if (tid == 0) d.nb += tot;
       __syncthreads();
     }
+    RSF_CK(3);
     // the old head's items: to the new head, the reserve, or the sealed group (appended)
     if (tid < kWave) {
       const bool live_h = any && tid < c.qcap && s.q_rumor[hb + tid] != kEmpty;
@@ -1216,7 +1239,23 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
       s.tseal[l * 3 + q] = nb ? make_uint4(nb, (uint32_t)bmin, (uint32_t)(bmin >> 32), 0u) : kTSumEmpty;
     }
     __syncthreads();
+#if RSF_DEEP_PROF
+    const uint64_t ck4 = clock64();
+    pf[0] += ck1 - ck0;
+    pf[1] += ck2 - ck1;
+    pf[2] += ck3 - ck2;
+    pf[3] += ck4 - ck3;
+    pf[4] += n;
+    pc++;
+#endif
   }
+#if RSF_DEEP_PROF
+  if (tid == 0) {
+    for (int i = 0; i < 5; ++i) atomicAdd(&g_deep_prof[64 + i], pf[i]);
+    atomicAdd(&g_deep_prof[69], pc);
+  }
+#endif
+#undef RSF_CK
 }
 
 // ring wrap: a deep queue's tail drops its items of the recycled generation (one wave per
