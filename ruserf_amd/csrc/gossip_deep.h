@@ -937,8 +937,10 @@ __device__ __forceinline__ uint64_t blk_min_u64(uint64_t v, CheckLds& d) {
 // sharing each pass over the keys.  A digit's lanes that agree with the wave's first active
 // lane are counted by that lane alone (a saturated queue's keys share their transmit byte: one
 // LDS address would take thousands of atomics).
+// pre48: d.hist[0] already holds every key's byte 6 (bits 48..55; the caller's pass 1 counted
+// them, valid when byte 7 is the same in every key), so that byte takes no pass here
 __device__ void lds_select3(const uint64_t* __restrict__ keys, uint32_t n, CheckLds& d, const uint32_t ks[3],
-                            const bool act[3], uint64_t an, uint64_t orr, uint64_t out[3]) {
+                            const bool act[3], uint64_t an, uint64_t orr, bool pre48, uint64_t out[3]) {
   constexpr uint32_t U = 4;
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   const uint64_t var = an ^ orr;
@@ -956,10 +958,11 @@ __device__ void lds_select3(const uint64_t* __restrict__ keys, uint32_t n, Check
     const uint32_t al1 = act[1] && !(act[0] && prefix[1] == prefix[0]) ? 1u : 0u;
     const uint32_t al2 = act[2] && !(act[0] && prefix[2] == prefix[0]) ? (act[1] && prefix[2] == prefix[1] ? al1 : 2u) : 0u;
     const bool own[3] = {act[0], al1 == 1, al2 == 2};
+    const bool counted = pre48 && shift == 48;  // (all three prefixes agree there: al1 = al2 = 0)
     __syncthreads();
-    for (uint32_t i = tid; i < 3 * 256; i += kDeepThreads) (&d.hist[0][0])[i] = 0;
+    for (uint32_t i = counted ? 3 * 256 : tid; i < 3 * 256; i += kDeepThreads) (&d.hist[0][0])[i] = 0;
     __syncthreads();
-    for (uint32_t i0 = 0; i0 < n; i0 += U * kDeepThreads) {
+    for (uint32_t i0 = 0; i0 < (counted ? 0u : n); i0 += U * kDeepThreads) {
       uint64_t x[U];
       bool v[U];
 #pragma unroll
@@ -1052,7 +1055,11 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
     const uint32_t tc = s.tsum[l * 3 + q].x;
     if (c.qcap + tc > kDeepItems) continue;  // (the tail's capacity is below it: cannot happen)
     uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
-    // pass 1: the keys into LDS, AND / OR of them
+    // pass 1: the keys into LDS, AND / OR of them, and (transmit counts below 256: byte 7 is
+    // zero in every key) the histogram of byte 6 -- the first radix pass of the selects
+    const bool fuse = c.tx_limit < 256;
+    for (uint32_t i = tid; i < 256; i += kDeepThreads) d.hist[0][i] = 0;
+    __syncthreads();
     uint64_t an = ~0ull, orr = 0;
     if (w == 0) {
       const bool live_h = lane < c.qcap && s.q_rumor[hb + lane] != kEmpty;
@@ -1063,26 +1070,40 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
         keys[mbcnt(lm)] = k;
         an = k;
         orr = k;
+        if (fuse) atomicAdd(&d.hist[0][(uint32_t)(k >> 48) & 0xFF], 1u);
       }
       if (lane == 0) d.hn = (uint32_t)__popcll(lm);
     }
     __syncthreads();
     const uint32_t hn = d.hn, n = hn + tc;
-    for (uint32_t b = 0; b < tc; b += kDeepU * kDeepThreads) {
-      uint4 x[kDeepU];
+    constexpr uint32_t U1 = 16;
+    for (uint32_t b = 0; b < tc; b += U1 * kDeepThreads) {
+      uint4 x[U1];
 #pragma unroll
-      for (uint32_t u = 0; u < kDeepU; ++u) {
+      for (uint32_t u = 0; u < U1; ++u) {
         const uint32_t i = b + u * kDeepThreads + tid;
         x[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
-      for (uint32_t u = 0; u < kDeepU; ++u) {
+      for (uint32_t u = 0; u < U1; ++u) {
         const uint32_t i = b + u * kDeepThreads + tid;
-        if (i < tc) {
-          const uint64_t k = tlq_key(x[u].z & 0xFFFF, x[u].z >> 16, x[u].y);
+        const bool in = i < tc;
+        const uint64_t k = tlq_key(x[u].z & 0xFFFF, x[u].z >> 16, x[u].y);
+        if (in) {
           keys[hn + i] = k;
           an &= k;
           orr |= k;
+        }
+        if (fuse) {  // one atomic for the lanes that agree with the first active lane
+          const uint32_t dg = (uint32_t)(k >> 48) & 0xFF;
+          const uint64_t am = ballot(in);
+          if (am) {
+            const int f = __ffsll((long long)am) - 1;
+            const uint32_t d0 = shfl_u32(dg, f);
+            const uint64_t same = ballot(in && dg == d0);
+            if (lane == (uint32_t)f) atomicAdd(&d.hist[0][d0], (uint32_t)__popcll(same));
+            else if (in && dg != d0) atomicAdd(&d.hist[0][dg], 1u);
+          }
         }
       }
     }
@@ -1112,7 +1133,7 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
     const uint32_t ks[3] = {keep, c.qcap, c.qcap + kDeepReserve};
     const bool act[3] = {keep > 0, keep > c.qcap, keep > c.qcap + kDeepReserve};
     uint64_t sel[3];
-    lds_select3(keys, n, d, ks, act, an, orr, sel);
+    lds_select3(keys, n, d, ks, act, an, orr, fuse, sel);
     const uint64_t T = act[0] ? sel[0] : 0ull;
     const uint64_t Th = act[1] ? sel[1] : T;
     const uint64_t TR = act[2] ? sel[2] : T;
