@@ -2814,37 +2814,54 @@ __global__ void __launch_bounds__(256) seg_end_kernel(uint64_t n_loc, const uint
 // check_stream_kernel, which keeps the max smallest keys of head and tail.
 // qmax (non-null when min_queue_depth > 0): each member's own get_queue_max (queue_max_kernel).
 constexpr uint32_t kOccBin = 64, kOccBins = 160;  // occupancy histogram: 64-item bins up to 10240, then one overflow bin
+// One wave per member (lane = head slot; 65..256-slot queues in chunks of 64): a queue's
+// head count is its leading run of live slots, one ballot per chunk.
 __global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uint32_t max_depth, uint32_t warn,
                                                            unsigned long long* __restrict__ stats,
                                                            const uint32_t* __restrict__ qmax,
                                                            uint32_t* __restrict__ hist, uint32_t period,
                                                            uint32_t phase) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t l = phase_first(c, period, phase) + (i / 3) * period;
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint64_t l = phase_first(c, period, phase) + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave * period;
   if (l >= c.n_loc) return;
-  const uint32_t q = (uint32_t)(i % 3);
-  const uint64_t t = l * 3 + q;
-  if (qmax) max_depth = qmax[t / 3];
-  const uint64_t base = t * c.qcap;
-  uint32_t n = 0;
-  while (n < c.qcap && s.q_rumor[base + n] != kEmpty) n++;
-  if (tcap_of(c, q)) n += s.tsum[t].x;
-  if (hist) {  // occupancy before the prune (rsf_gossip_checker_occupancy)
-    atomicAdd(hist + q * (kOccBins + 1) + min(n / kOccBin, kOccBins), 1u);
-    atomicMax(hist + 3 * (kOccBins + 1) + q, n);
+  if (qmax) max_depth = qmax[l];
+  uint32_t nq[3];
+#pragma unroll
+  for (uint32_t q = 0; q < 3; ++q) {
+    const uint64_t base = (l * 3 + q) * c.qcap;
+    uint32_t n = 0;
+    for (uint32_t j = 0; j < c.qcap; j += kWave) {
+      const bool live = j + lane < c.qcap && s.q_rumor[base + j + lane] != kEmpty;
+      const uint64_t m = ballot(live);
+      const uint32_t run = m == ~0ull ? kWave : (uint32_t)__builtin_ctzll(~m);
+      n = j + run;
+      if (run < kWave) break;
+    }
+    if (tcap_of(c, q)) n += s.tsum[l * 3 + q].x;
+    nq[q] = n;
   }
-  if (n) atomicAdd(stats + q, (unsigned long long)n);
-  if (n >= warn) atomicAdd(stats + 3 + q, 1ull);
-  if (n > max_depth && tcap_of(c, q)) {
-    s.deep_ids[atomicAdd(s.deep_n, 1u)] = (uint32_t)t;
-    atomicAdd(stats + 6 + q, (unsigned long long)(n - max_depth));
-  } else if (n > max_depth) {  // numq >= max -> prune(max): retain max
-    for (uint32_t i = max_depth; i < n; ++i) {
+  if (lane < 3) {
+    const uint32_t q = lane, n = q == 0 ? nq[0] : q == 1 ? nq[1] : nq[2];
+    if (hist) {  // occupancy before the prune (rsf_gossip_checker_occupancy)
+      atomicAdd(hist + q * (kOccBins + 1) + min(n / kOccBin, kOccBins), 1u);
+      atomicMax(hist + 3 * (kOccBins + 1) + q, n);
+    }
+    if (n) atomicAdd(stats + q, (unsigned long long)n);
+    if (n >= warn) atomicAdd(stats + 3 + q, 1ull);
+    if (n > max_depth) {
+      if (tcap_of(c, q)) s.deep_ids[atomicAdd(s.deep_n, 1u)] = (uint32_t)(l * 3 + q);
+      atomicAdd(stats + 6 + q, (unsigned long long)(n - max_depth));
+    }
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < 3; ++q) {
+    if (tcap_of(c, q) || nq[q] <= max_depth) continue;  // numq >= max -> prune(max): retain max
+    const uint64_t base = (l * 3 + q) * c.qcap;
+    for (uint32_t i = max_depth + lane; i < nq[q]; i += kWave) {
       s.q_rumor[base + i] = kEmpty;
       s.q_seq[base + i] = 0;
       s.q_txlen[base + i] = 0;
     }
-    atomicAdd(stats + 6 + q, (unsigned long long)(n - max_depth));
   }
 }
 
@@ -3084,6 +3101,10 @@ struct rsf_gossip {
   // liveness in between (ahead_valid), else redraws.  RSF_PEERS_AHEAD=0 turns it off.
   hipStream_t side = nullptr;
   hipEvent_t ev_emitted = nullptr, ev_ahead = nullptr;
+  // deep queues: the full-depth class and the middle class run on their own stream, beside the
+  // tiny and small classes (ev_lists: the lists are complete; ev_deep_side: that stream is done)
+  hipStream_t deep_side = nullptr;
+  hipEvent_t ev_lists = nullptr, ev_deep_side = nullptr;
   bool ahead_launched = false, ahead_valid = false, ahead_on = true;
   uint32_t ahead_round = 0;
   int end_bit = 32;
@@ -3279,6 +3300,10 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
       hipEventCreateWithFlags(&g->ev_emitted, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&g->ev_ahead, hipEventDisableTiming) != hipSuccess)
     return fail(rsf::set_error(RSF_ERR_HIP, "hipStreamCreate / hipEventCreate failed"));
+  if (c.deep && (hipStreamCreateWithFlags(&g->deep_side, hipStreamNonBlocking) != hipSuccess ||
+                 hipEventCreateWithFlags(&g->ev_lists, hipEventDisableTiming) != hipSuccess ||
+                 hipEventCreateWithFlags(&g->ev_deep_side, hipEventDisableTiming) != hipSuccess))
+    return fail(rsf::set_error(RSF_ERR_HIP, "hipStreamCreate / hipEventCreate failed"));
   {
     const char* e = getenv("RSF_PEERS_AHEAD");
     g->ahead_on = !(e && e[0] == '0');
@@ -3302,7 +3327,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
     for (int q = 0; q < 3; ++q)
       if (tcap_of(c, q) && GA(q == 0 ? s.tail0 : q == 1 ? s.tail1 : s.tail2, n * tstride_of(c, q) * sizeof(uint4)))
         return fail(rc);
-    if (GA(s.tsum, n * 3 * sizeof(uint4)) || GA(s.tseal, n * 3 * sizeof(uint4)) || GA(s.deep_ids, n * 4 * 4))
+    if (GA(s.tsum, n * 3 * sizeof(uint4)) || GA(s.tseal, n * 3 * sizeof(uint4)) || GA(s.deep_ids, n * 5 * 4))
       return fail(rc);
   }
   g->stage_cap = n * c.fanout * c.cap_t;
@@ -3311,7 +3336,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   const uint64_t pipe = std::max(g->stage_cap, g->recv_cap);
   if (GA(g->stage_key, pipe * 4) || GA(g->stage_val, pipe * 4) || GA(g->sort_key, pipe * 4) ||
       GA(g->sort_val, pipe * 4) || GA(g->seg_start, n * 4) || GA(g->seg_end, n * 4) || GA(g->send_buf, pipe * 8) || GA(g->rec_dec, pipe * 4) ||
-      GA(g->d_counters, 64 * 8))
+      GA(g->d_counters, 72 * 8))
     return fail(rc);
   g->n_groups = n * c.fanout;
   if (GA(g->grp_key, g->n_groups * 4) || GA(g->grp_cnt, g->n_groups * 4) || GA(g->grp_key_s, g->n_groups * 4) ||
@@ -3357,8 +3382,9 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   hipStream_t st = g->stream;
   bool ok = true;
   auto ms = [&](void* p, int v, size_t b) { ok = ok && hipMemsetAsync(p, v, b, st) == hipSuccess; };
-  ms(g->d_counters, 0, 64 * 8);  // status flags and running totals start at zero
-  s.deep_n = reinterpret_cast<uint32_t*>(g->d_counters + 53);  // deferred members: 3 lists (words 53-54; [55] their total)
+  ms(g->d_counters, 0, 72 * 8);  // status flags and running totals start at zero
+  // deferred members: the counts of lists 0..4 (words 64-66; [55] their total)
+  s.deep_n = reinterpret_cast<uint32_t*>(g->d_counters + 64);
   ms(s.emin, 0, n * 8);
   ms(s.qmin, 0, n * 8);
   ms(s.digest, 0, n * 8);
@@ -3440,6 +3466,10 @@ int rsf_gossip_destroy(rsf_gossip* g) {
   if (g->own) hipStreamDestroy(g->own);
   if (g->side) hipStreamDestroy(g->side);
   if (g->ev_emitted) hipEventDestroy(g->ev_emitted);
+  if (g->deep_side) hipStreamSynchronize(g->deep_side);
+  if (g->deep_side) hipStreamDestroy(g->deep_side);
+  if (g->ev_lists) hipEventDestroy(g->ev_lists);
+  if (g->ev_deep_side) hipEventDestroy(g->ev_deep_side);
   if (g->ev_ahead) hipEventDestroy(g->ev_ahead);
   delete g;
   return RSF_OK;
@@ -3744,15 +3774,24 @@ static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
 #undef RSF_EMIT_DEEP
     RSF_HIP(hipGetLastError());
     RSF_DBG_SYNC(st, "emit_kernel (deep)");
-    // by capacity, the full depth last (the smaller classes re-list members to it)
+    // the classes work on disjoint members: the full depth (list 1) and the middle class on
+    // the deep side stream beside the tiny and small classes; the members the smaller classes
+    // re-list (list 4) go through the full depth last, after every class has run
+    hipStream_t sd = g->deep_side;
+    RSF_HIP(hipEventRecord(g->ev_lists, st));
+    RSF_HIP(hipStreamWaitEvent(sd, g->ev_lists, 0));
+    hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepBig>), dim3(g->deep_blocks_big), dim3(kWave), 0, sd, c, g->s,
+                       g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 1u, g->d_counters + 55);
+    hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepMid>), dim3(g->deep_blocks_mid), dim3(kWave), 0, sd, c, g->s,
+                       g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 3u, g->d_counters + 55);
+    RSF_HIP(hipEventRecord(g->ev_deep_side, sd));
     hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepTiny>), dim3(g->deep_blocks_tiny), dim3(kWave), 0, st, c, g->s,
                        g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 2u, g->d_counters + 55);
     hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepSmall>), dim3(g->deep_blocks), dim3(kWave), 0, st, c, g->s,
                        g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 0u, g->d_counters + 55);
-    hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepMid>), dim3(g->deep_blocks_mid), dim3(kWave), 0, st, c, g->s,
-                       g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 3u, g->d_counters + 55);
+    RSF_HIP(hipStreamWaitEvent(st, g->ev_deep_side, 0));
     hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepBig>), dim3(g->deep_blocks_big), dim3(kWave), 0, st, c, g->s,
-                       g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 1u, g->d_counters + 55);
+                       g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 4u, g->d_counters + 55);
   } else if (c.qcap == kWave) {
     hipLaunchKernelGGL((emit_kernel<BKT, true>), egrid, eb, 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt,
                        g->stage_val, g->stage_dec, bk);
@@ -3792,7 +3831,7 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
   g->ahead_launched = g->ahead_valid = false;
   int rc;
   if (!use_ahead && (rc = peers_and_sort(g, round, st))) return rc;
-  if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 16, st));  // the emission's deferred-member lists
+  if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, kDeepLists * 4, st));  // the emission's deferred-member lists
   RSF_HIP(hipMemsetAsync(g->grp_cnt, 0, ng * 4, st));
   if (local) {
     RSF_HIP(hipMemsetAsync(g->seg_start, 0, c.n_loc * 4, st));
@@ -4335,8 +4374,8 @@ static int check_launch(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_qu
     RSF_HIP(hipMemsetAsync(g->occ_hist, 0, hist_words * 4, g->stream));
     RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, g->stream));
   }
-  if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, 16, g->stream));
-  hipLaunchKernelGGL(check_queues_kernel, dim3(grid1(std::max<uint64_t>(1, phase_count(c, period, phase)) * 3)),
+  if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, kDeepLists * 4, g->stream));
+  hipLaunchKernelGGL(check_queues_kernel, dim3(grid1(std::max<uint64_t>(1, phase_count(c, period, phase)), 256 / kWave)),
                      dim3(256), 0, g->stream, c, g->s, max_depth, depth_warning, g->d_counters + 40, qmax, g->occ_hist,
                      period, phase);
   RSF_HIP(hipGetLastError());

@@ -519,7 +519,7 @@ __device__ __forceinline__ void deep_relist_full(const GCfg& c, const GState& s,
                                                  DeepWave<CAP>& d) {
   for (uint32_t i = lane; i < n; i += kWave) d.st[i] = kDeepDead;
   wsync();
-  if (lane == 0) s.deep_ids[c.n_loc * 3 - 1 - atomicAdd(s.deep_n + 1, 1u)] = (uint32_t)l;
+  if (lane == 0) s.deep_ids[c.n_loc * 4 + atomicAdd(s.deep_n + 4, 1u)] = (uint32_t)l;  // list 4
 #if RSF_DEEP_PROF
   if (lane == 0) s_dprof[30] += 1ull;
 #endif
@@ -607,7 +607,7 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
     // the full depth fits this class: a recent mode that cannot decide continues in place
     const bool fits_all = c.qcap + tc + nq <= CAP;
     if (q == 0 && !recent && !fits_all) {  // (emit_run listed it by the recent part's need)
-      if (lane == 0) s.deep_ids[c.n_loc * 3 - 1 - atomicAdd(s.deep_n + 1, 1u)] = (uint32_t)l;
+      if (lane == 0) s.deep_ids[c.n_loc * 4 + atomicAdd(s.deep_n + 4, 1u)] = (uint32_t)l;  // list 4
       return;
     }
     const uint4* const t = tail_of(s, q) + l * tstride_of(c, q) + t_lo;
@@ -874,13 +874,15 @@ __global__ void __launch_bounds__(kWave) emit_deep_wave_kernel(GCfg c, GState s,
   const uint32_t n_list = s.deep_n[list];
   if (blockIdx.x == 0 && lane == 0 && n_list) {
     atomicAdd(total, (unsigned long long)n_list);
-    atomicAdd(list == 3 ? total + 1 : total - kDeepClassOff + list, (unsigned long long)n_list);  // per list
+    // per class (the re-listed members count with the full depth)
+    atomicAdd(list == 3 ? total + 1 : total - kDeepClassOff + (list == 4 ? 1u : list), (unsigned long long)n_list);
   }
   for (uint32_t i = lane; i < CAP; i += kWave) d.st[i] = kDeepDead;
   wsync();
   const uint64_t last = c.n_loc * 3 - 1;
-  const uint32_t* const ids = list == 1 ? s.deep_ids + last
-                                        : s.deep_ids + (list == 2 ? c.n_loc : list == 3 ? c.n_loc * 3 : 0ull);
+  const uint32_t* const ids =
+      list == 1 ? s.deep_ids + last
+                : s.deep_ids + (list == 2 ? c.n_loc : list == 3 ? c.n_loc * 3 : list == 4 ? c.n_loc * 4 : 0ull);
   const int64_t dir = list == 1 ? -1 : 1;
   // software pipeline over the wave's members: the next member's first round trip (deep_pre)
   // and the id after it are read while this member is worked on

@@ -111,8 +111,10 @@ struct GState {
   // or sets m = 0.
   uint4* tseal;      // [n_loc][3]
   uint32_t* deep_ids;  // [n_loc * 3] members deferred to emit_deep_wave_kernel (two lists), or queues to prune
-  uint32_t* deep_n;    // [4] the lists' lengths (reset before each emission)
+  uint32_t* deep_n;    // [kDeepLists] the lists' lengths (reset before each emission)
 };
+// deferred-member lists: 0 small, 1 full depth, 2 tiny, 3 middle, 4 re-listed to the full depth
+constexpr uint32_t kDeepLists = 5;
 constexpr uint32_t kDeepClassOff = 6;  // the per-list deferral counters sit at (total counter) - 6 + list
 constexpr uint32_t kTailSlack = 192;  // tail row room past its capacity: one emission's spills (2 x 64) + 64
 // per-queue deep-queue fields by a select on q
