@@ -81,10 +81,10 @@ def run_gossip(args, rank, world):
     n = per * world
     depth = getattr(args, "queue_depth", 0) or 0
     # QueueChecker ticks in the round loop (0: none), staggered: each member's checker runs on
-    # its own timer (base.rs:703-735), member m ticking after the rounds t with
-    # (t + 1) % K == m % K, so every round carries 1/K of the ticks (the prune included in the
-    # timed steps at its true rate) and the queues cycle between max_queue_depth and what K
-    # rounds add; the ring sized so no queued item expires during the run
+    # its own timer (base.rs:703-735), member m ticking in the rounds r with r % K == m % K,
+    # so every round carries 1/K of the ticks (the prune included in the timed steps at its
+    # true rate) and the queues cycle between max_queue_depth and what K rounds add; the ring
+    # sized so no queued item expires during the run
     check_every = getattr(args, "check_every", 0) or 0
     settle = (SETTLE_STEADY if check_every else SETTLE_ROUNDS) if args.settle is None else args.settle
     rounds_total = settle + args.warmup + args.steps
@@ -104,15 +104,13 @@ def run_gossip(args, rank, world):
         step_fn = lambda t: sg.round(t, ml[t], acts[t])  # noqa: E731
     eng.set_subjects(subj)
     eng.init_views(*views)
-
-    def checker(t_):
-        # the staggered QueueChecker ticks due after round t_ (asynchronous)
-        if check_every:
-            eng.check_queues_phase(check_every, (t_ + 1) % check_every, MAX_QUEUE_DEPTH, 0, QUEUE_DEPTH_WARNING)
+    if check_every:
+        # the staggered ticks inside the rounds: round r ticks the members with id = r mod K,
+        # between its emission and its merge, on a second stream beside the merge
+        eng.set_checker(check_every, MAX_QUEUE_DEPTH, 0, QUEUE_DEPTH_WARNING)
 
     def step_settle(t_):
         step_fn(t_)
-        checker(t_)
 
     t = 0
     for _ in range(settle + args.warmup):
@@ -138,7 +136,6 @@ def run_gossip(args, rank, world):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step_fn(t)
-        checker(t)
         t += 1
     torch.cuda.synchronize()
     if world > 1:
@@ -279,10 +276,10 @@ def cpu_baseline_gossip_deep(args, seconds_target=10.0, n=20_000, settle=60):
     w = H.oracle_world(cfg, subj, W.initial_views(SUBJECTS))
     t = 0
 
+    H.L.orc_world_set_checker(C.byref(w), MAX_QUEUE_DEPTH, 0, QUEUE_DEPTH_WARNING, CHECK_EVERY)
+
     def rnd(threads):
         H.oracle_round(w, t, ml[t], acts[t], threads=threads)
-        H.L.orc_check_queues_phase(C.byref(w), MAX_QUEUE_DEPTH, 0, QUEUE_DEPTH_WARNING, CHECK_EVERY,
-                                   (t + 1) % CHECK_EVERY, None)
     for _ in range(settle):
         rnd(th)
         t += 1
@@ -297,7 +294,7 @@ def cpu_baseline_gossip_deep(args, seconds_target=10.0, n=20_000, settle=60):
             done += 1
             t += 1
         return done, spent
-    done_mt, spent_mt = timed(th, seconds_target, 20)
+    done_mt, spent_mt = timed(th, seconds_target, 36)
     done_1, spent_1 = timed(1, seconds_target / 2, 3)
     width = H.world_width(w)
     H.L.orc_world_free(C.byref(w))

@@ -6,7 +6,8 @@ occupancy (mean / p50 / p99 / max over members), deferred members per round per 
 bounded-queue drops (between ticks; the reference drops none) and ring expiries.
 With mode "stagger" each member ticks on its own phase (member id mod check_every) after every
 round instead (rsf_gossip_check_queues_phase), inside the timed windows.
-Usage: steady_state.py [members] [rounds] [check_every] [depth] [every] [sync|stagger]"""
+Mode "inround": the same staggered ticks inside the rounds (rsf_gossip_set_checker).
+Usage: steady_state.py [members] [rounds] [check_every] [depth] [every] [sync|stagger|inround]"""
 import json
 import sys
 import time
@@ -25,15 +26,18 @@ check_every = int(sys.argv[3]) if len(sys.argv) > 3 else 150
 depth = int(sys.argv[4]) if len(sys.argv) > 4 else 4096
 every = int(sys.argv[5]) if len(sys.argv) > 5 else 10
 stagger = len(sys.argv) > 6 and sys.argv[6] == "stagger"
+inround = len(sys.argv) > 6 and sys.argv[6] == "inround"
 cfg = B.gossip_cfg(n, rounds, 1, queue_depth=depth, ring_rounds=rounds)
 print(json.dumps({"members": n, "rounds": rounds, "check_every": check_every, "depth": cfg.depths()[0],
-                  "max_rumors": cfg.max_rumors, "stagger": stagger}), flush=True)
+                  "max_rumors": cfg.max_rumors, "stagger": stagger, "inround": inround}), flush=True)
 subj, acts, ml = W.intents_workload(n, B.SUBJECTS, rounds, rate=0.01, seed=B.SEED, prune_frac=B.PRUNE_FRAC)
 torch.cuda.set_stream(torch.cuda.Stream())
 eng = GossipEngine(cfg)
 eng.set_stream(torch.cuda.current_stream().cuda_stream)
 eng.set_subjects(subj)
 eng.init_views(*W.initial_views(B.SUBJECTS))
+if inround:
+    eng.set_checker(check_every, 4096, 0, 128)
 cls0 = eng.deep_class_stats()
 pr0, ex0 = 0, 0
 t0 = time.perf_counter()
@@ -41,7 +45,7 @@ for t in range(rounds):
     eng.round(t, ml[t], acts[t])
     if stagger:
         eng.check_queues_phase(check_every, (t + 1) % check_every, 4096, 0, 128)
-    tick = not stagger and check_every and (t + 1) % check_every == 0
+    tick = not (stagger or inround) and check_every and (t + 1) % check_every == 0
     if (t + 1) % every == 0 or tick:
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / every * 1e3
@@ -54,7 +58,7 @@ for t in range(rounds):
                        "p99": int(np.percentile(ql, 99)), "max": int(ql.max())},
                "deferred_per_round": [(int(a) - int(b)) / every for a, b in zip(cls, cls0)],
                "bounded_pruned": pr - pr0, "expired": ex - ex0}
-        if stagger:
+        if stagger or inround:
             cs = eng.checker_stats(reset=True)
             rec["ticks"] = {"pruned_per_round": int(cs["pruned"][0]) / every}
         if tick:

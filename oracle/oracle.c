@@ -1090,6 +1090,15 @@ void orc_check_queues(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue
   orc_check_queues_phase(w, max_queue_depth, min_queue_depth, depth_warning, 1, 0, stats);
 }
 
+void orc_world_set_checker(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
+                           uint32_t period) {
+  w->chk_period = period;
+  w->chk_max = max_queue_depth;
+  w->chk_min = min_queue_depth;
+  w->chk_warn = depth_warning;
+  memset(w->chk_stats, 0, sizeof(w->chk_stats));
+}
+
 /* kRandomNodes model: k distinct live peers != m, Philox-drawn (memberlist util.go; unpinned) */
 uint32_t orc_pick_peers(uint64_t seed, uint32_t n, const uint8_t* alive, uint32_t m, uint32_t round,
                         uint32_t k, uint32_t* out) {
@@ -1391,6 +1400,14 @@ int orc_world_round_mt(orc_world* w, uint32_t round, const orc_ml_event* ml, uin
     fail |= jobs[i].fail;
     nrec += jobs[i].nrec;
     w->sends += jobs[i].sends;
+  }
+
+  /* 4b. the staggered QueueChecker ticks due this round (each node's checker on its own
+   *     timer, base.rs:703-735), between the emission and the merge */
+  if (!fail && w->chk_period) {
+    uint64_t st[9];
+    orc_check_queues_phase(w, w->chk_max, w->chk_min, w->chk_warn, w->chk_period, round % w->chk_period, st);
+    for (int i = 0; i < 9; ++i) w->chk_stats[i] += st[i];
   }
 
   /* 5. merge in canonical (sender, position) order per receiver: stable

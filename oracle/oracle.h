@@ -267,6 +267,11 @@ typedef struct {
   /* the last round's per-action results (orc_world_action_status), act_cap entries */
   int32_t* act_status;
   uint32_t act_cap, last_n_acts;
+  /* in-round staggered QueueChecker (orc_world_set_checker): in round r, after the emission
+   * and before the merge, the tick of the members with id mod chk_period == r mod chk_period;
+   * chk_stats accumulates its counts (orc_check_queues' layout).  chk_period 0: off. */
+  uint32_t chk_period, chk_max, chk_min, chk_warn;
+  uint64_t chk_stats[9];
 } orc_world;
 
 typedef struct {
@@ -326,6 +331,8 @@ void orc_check_queues(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue
  * runs on its own timer, base.rs:703-735: staggered ticks, one phase per round). */
 void orc_check_queues_phase(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue_depth,
                             uint32_t depth_warning, uint32_t period, uint32_t phase, uint64_t* stats);
+void orc_world_set_checker(orc_world* w, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
+                           uint32_t period);
 
 uint32_t orc_msg_len(uint8_t type, uint64_t ltime, uint32_t name_len, uint32_t payload_len);
 /* origination size checks: 0 or the status (include/ruserf_amd.h RSF_ERR_USER_EVENT_* = -20..-22,

@@ -71,6 +71,7 @@ def declare(L):
     sig("rsf_gossip_check_queues", [VP, C.c_uint32, C.c_uint32, C.c_uint32, P64, P64, P64])
     sig("rsf_gossip_check_queues_phase", [VP, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32])
     sig("rsf_gossip_checker_stats", [VP, P64, P64, P64, i])
+    sig("rsf_gossip_set_checker", [VP, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32])
     sig("rsf_gossip_dump_pruned", [VP, P32, P32])
     sig("rsf_gossip_flush", [VP])
     sig("rsf_gossip_pruned_total", [VP, C.c_int, C.POINTER(C.c_uint64)])

@@ -3105,6 +3105,12 @@ struct rsf_gossip {
   // tiny and small classes (ev_lists: the lists are complete; ev_deep_side: that stream is done)
   hipStream_t deep_side = nullptr;
   hipEvent_t ev_lists = nullptr, ev_deep_side = nullptr;
+  // in-round checker ticks (rsf_gossip_set_checker): period 0 = off; they run on chk_stream
+  // (the deep side stream, or chk_own) beside the merge, joined back by join_check
+  uint32_t chk_period = 0, chk_max = 0, chk_min = 0, chk_warn = 0;
+  hipStream_t chk_stream = nullptr, chk_own = nullptr;
+  hipEvent_t ev_chk_fork = nullptr, ev_chk = nullptr;
+  bool chk_pending = false;
   bool ahead_launched = false, ahead_valid = false, ahead_on = true;
   uint32_t ahead_round = 0;
   int end_bit = 32;
@@ -3139,7 +3145,17 @@ static void mark(rsf_gossip* g, int k) {
 
 // Every member's pending re-queues applied to its queues: before anything other than
 // emission reads the queues, the queue-prune counters or the error flags.
+// the engine's stream waits for an in-round checker tick still running on its own stream
+static int join_check(rsf_gossip* g) {
+  if (!g->chk_pending) return RSF_OK;
+  g->chk_pending = false;
+  RSF_HIP(hipStreamWaitEvent(g->stream, g->ev_chk, 0));
+  return RSF_OK;
+}
+
 static int flush_pending(rsf_gossip* g, uint32_t period = 1, uint32_t phase = 0) {
+  int jrc = join_check(g);
+  if (jrc) return jrc;
   const uint64_t cnt = phase_count(g->c, period, phase);
   if (!cnt) return RSF_OK;
   hipLaunchKernelGGL(pend_flush_kernel, dim3(grid1(cnt, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0,
@@ -3300,6 +3316,9 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
       hipEventCreateWithFlags(&g->ev_emitted, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&g->ev_ahead, hipEventDisableTiming) != hipSuccess)
     return fail(rsf::set_error(RSF_ERR_HIP, "hipStreamCreate / hipEventCreate failed"));
+  if (hipEventCreateWithFlags(&g->ev_chk_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&g->ev_chk, hipEventDisableTiming) != hipSuccess)
+    return fail(rsf::set_error(RSF_ERR_HIP, "hipEventCreate failed"));
   if (c.deep && (hipStreamCreateWithFlags(&g->deep_side, hipStreamNonBlocking) != hipSuccess ||
                  hipEventCreateWithFlags(&g->ev_lists, hipEventDisableTiming) != hipSuccess ||
                  hipEventCreateWithFlags(&g->ev_deep_side, hipEventDisableTiming) != hipSuccess))
@@ -3470,6 +3489,10 @@ int rsf_gossip_destroy(rsf_gossip* g) {
   if (g->deep_side) hipStreamDestroy(g->deep_side);
   if (g->ev_lists) hipEventDestroy(g->ev_lists);
   if (g->ev_deep_side) hipEventDestroy(g->ev_deep_side);
+  if (g->chk_own) hipStreamSynchronize(g->chk_own);
+  if (g->chk_own) hipStreamDestroy(g->chk_own);
+  if (g->ev_chk_fork) hipEventDestroy(g->ev_chk_fork);
+  if (g->ev_chk) hipEventDestroy(g->ev_chk);
   if (g->ev_ahead) hipEventDestroy(g->ev_ahead);
   delete g;
   return RSF_OK;
@@ -3484,6 +3507,8 @@ int rsf_gossip_set_stream(rsf_gossip* g, void* st) {
 int rsf_gossip_sync(rsf_gossip* g) {
   if (!g) return gerr("null context");
   RSF_HIP(hipSetDevice(g->device));
+  int jrc = join_check(g);
+  if (jrc) return jrc;
   if (g->ahead_launched) RSF_HIP(hipStreamSynchronize(g->side));
   RSF_HIP(hipStreamSynchronize(g->stream));
   return RSF_OK;
@@ -3635,6 +3660,11 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
                            const rsf_action* acts, uint32_t n_acts) {
   if (!g || (n_ml && !ml) || (n_acts && !acts)) return gerr("null argument");
   const GCfg& c = g->c;
+  {  // an in-round checker tick of the previous round, if its merge call did not join it
+    RSF_HIP(hipSetDevice(g->device));
+    int jrc = join_check(g);
+    if (jrc) return jrc;
+  }
   for (uint32_t e = 0; e < n_ml; ++e)
     if (ml[e].subject >= c.S || (ml[e].kind != RSF_ML_JOIN && ml[e].kind != RSF_ML_LEAVE && ml[e].kind != RSF_ML_UPDATE) || ml[e].set_alive > 2)
       return gerr("bad memberlist event");
@@ -3817,6 +3847,7 @@ static int launch_ahead(rsf_gossip* g, uint32_t round) {
   return RSF_OK;
 }
 
+static int check_in_round(rsf_gossip* g, uint32_t round);
 static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t world = 0) {
   const GCfg& c = g->c;
   hipStream_t st = g->stream;
@@ -3853,6 +3884,7 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
     mark(g, 2);
     if ((rc = launch_emit<true>(g, egrid, bk))) return rc;
     if ((rc = launch_ahead(g, round))) return rc;
+    if ((rc = check_in_round(g, round))) return rc;
     mark(g, 3);
     return RSF_OK;
   }
@@ -3865,6 +3897,7 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
   RSF_DBG_SYNC(st, "emit_kernel");
   // the counts path reads the sorted groups after the emission (grp_expand_kernel): no ahead
   if (local && (rc = launch_ahead(g, round))) return rc;
+  if ((rc = check_in_round(g, round))) return rc;
   if (local) {
     unsigned long long* sum = (unsigned long long*)g->d_counters;
     const uint32_t* cnt = g->grp_cnt;
@@ -3971,7 +4004,8 @@ int rsf_gossip_round(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml, uint
   g->merged_from_stage = true;
   g->merged_from_buckets = false;
   hipLaunchKernelGGL(accumulate_kernel, dim3(1), dim3(64), 0, g->stream, g->d_counters, 0u);
-  return launch_merge(g, nullptr, true);
+  if ((rc = launch_merge(g, nullptr, true))) return rc;
+  return join_check(g);
 }
 
 int rsf_gossip_bucket_buffers(rsf_gossip* g, uint32_t world, void** send, void** recv, uint64_t* bucket_bytes) {
@@ -4042,7 +4076,7 @@ int rsf_gossip_round_merge_buckets(rsf_gossip* g, uint32_t world) {
   int rc = merge_launch<true>(g, nullptr, nullptr, g->d_rstart, g->d_rend, nullptr, c.cap_t, bk);
   if (rc) return rc;
   mark(g, 4);
-  return RSF_OK;
+  return join_check(g);
 }
 
 int rsf_gossip_bucket_status(rsf_gossip* g, int* ok) {
@@ -4349,8 +4383,11 @@ int rsf_gossip_set_now(rsf_gossip* g, uint32_t now) {
 
 // one checker tick at the members whose global id is phase mod period (period 1: all), on
 // the engine's stream; reset: the stats block and the occupancy histogram start from zero
+// rs: the stream the count and the prune run on (the flush and queue_max_kernel, which read
+// pending lists and views, always run on the engine's stream first); another stream than the
+// engine's is joined back by join_check
 static int check_launch(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
-                        uint32_t period, uint32_t phase, bool reset) {
+                        uint32_t period, uint32_t phase, bool reset, hipStream_t rs) {
   const GCfg& c = g->c;
   // get_queue_max (base.rs:748-759): max_queue_depth, or (min_queue_depth > 0) per member
   // max(2 * members.states.len(), min_queue_depth) -- queue_max_kernel
@@ -4370,21 +4407,39 @@ static int check_launch(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_qu
     if ((rc = dmalloc((void**)&g->occ_hist, hist_words * 4))) return rc;
     reset = true;
   }
-  if (reset) {
-    RSF_HIP(hipMemsetAsync(g->occ_hist, 0, hist_words * 4, g->stream));
-    RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, g->stream));
+  const bool fork = rs != g->stream;
+  if (fork) {
+    RSF_HIP(hipEventRecord(g->ev_chk_fork, g->stream));
+    RSF_HIP(hipStreamWaitEvent(rs, g->ev_chk_fork, 0));
   }
-  if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, kDeepLists * 4, g->stream));
+  if (reset) {
+    RSF_HIP(hipMemsetAsync(g->occ_hist, 0, hist_words * 4, rs));
+    RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, rs));
+  }
+  if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, kDeepLists * 4, rs));
   hipLaunchKernelGGL(check_queues_kernel, dim3(grid1(std::max<uint64_t>(1, phase_count(c, period, phase)), 256 / kWave)),
-                     dim3(256), 0, g->stream, c, g->s, max_depth, depth_warning, g->d_counters + 40, qmax, g->occ_hist,
-                     period, phase);
+                     dim3(256), 0, rs, c, g->s, max_depth, depth_warning, g->d_counters + 40, qmax, g->occ_hist, period,
+                     phase);
   RSF_HIP(hipGetLastError());
   if (c.deep) {  // the deep queues over the max: the smallest max keys of head and tail kept
-    hipLaunchKernelGGL(check_stream_kernel, dim3(g->deep_check_blocks), dim3(kDeepThreads), 0, g->stream, c, g->s,
-                       max_depth, qmax);
+    hipLaunchKernelGGL(check_stream_kernel, dim3(g->deep_check_blocks), dim3(kDeepThreads), 0, rs, c, g->s, max_depth,
+                       qmax);
     RSF_HIP(hipGetLastError());
   }
+  if (fork) {
+    RSF_HIP(hipEventRecord(g->ev_chk, rs));
+    g->chk_pending = true;
+  }
   return RSF_OK;
+}
+
+// the in-round checker ticks (rsf_gossip_set_checker): after round `round`'s emission, on the
+// checker stream, beside the merge -- the merge touches no queue, and every pending list of
+// the ticking members was applied by the emission or by the flush before the fork
+static int check_in_round(rsf_gossip* g, uint32_t round) {
+  if (!g->chk_period) return RSF_OK;
+  return check_launch(g, g->chk_max, g->chk_min, g->chk_warn, g->chk_period, round % g->chk_period, false,
+                      g->chk_stream);
 }
 
 static int check_stats(rsf_gossip* g, uint64_t* num_queued, uint64_t* n_warn, uint64_t* n_pruned) {
@@ -4402,7 +4457,7 @@ static int check_stats(rsf_gossip* g, uint64_t* num_queued, uint64_t* n_warn, ui
 int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
                             uint64_t* num_queued, uint64_t* n_warn, uint64_t* n_pruned) {
   if (!g) return gerr("null context");
-  int rc = check_launch(g, max_queue_depth, min_queue_depth, depth_warning, 1, 0, true);
+  int rc = check_launch(g, max_queue_depth, min_queue_depth, depth_warning, 1, 0, true, g->stream);
   return rc ? rc : check_stats(g, num_queued, n_warn, n_pruned);
 }
 
@@ -4410,12 +4465,35 @@ int rsf_gossip_check_queues_phase(rsf_gossip* g, uint32_t max_queue_depth, uint3
                                   uint32_t depth_warning, uint32_t period, uint32_t phase) {
   if (!g) return gerr("null context");
   if (!period || phase >= period) return gerr("phase must be below a non-zero period");
-  return check_launch(g, max_queue_depth, min_queue_depth, depth_warning, period, phase, false);
+  return check_launch(g, max_queue_depth, min_queue_depth, depth_warning, period, phase, false, g->stream);
+}
+
+int rsf_gossip_set_checker(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
+                           uint32_t period) {
+  if (!g) return gerr("null context");
+  RSF_HIP(hipSetDevice(g->device));
+  int rc = join_check(g);
+  if (rc) return rc;
+  if (period && !g->chk_stream) {
+    if (g->deep_side) {
+      g->chk_stream = g->deep_side;  // idle once the emission is done
+    } else {
+      RSF_HIP(hipStreamCreateWithFlags(&g->chk_own, hipStreamNonBlocking));
+      g->chk_stream = g->chk_own;
+    }
+  }
+  g->chk_period = period;
+  g->chk_max = max_queue_depth;
+  g->chk_min = min_queue_depth;
+  g->chk_warn = depth_warning;
+  return rsf_gossip_checker_stats(g, nullptr, nullptr, nullptr, 1);
 }
 
 int rsf_gossip_checker_stats(rsf_gossip* g, uint64_t* num_queued, uint64_t* n_warn, uint64_t* n_pruned, int reset) {
   if (!g) return gerr("null context");
   RSF_HIP(hipSetDevice(g->device));
+  int jrc = join_check(g);
+  if (jrc) return jrc;
   const bool have = g->occ_hist != nullptr;
   int rc = RSF_OK;
   if (have) {
@@ -4446,6 +4524,9 @@ int rsf_gossip_action_status(rsf_gossip* g, int32_t* status, uint32_t n) {
 
 int rsf_gossip_checker_occupancy(rsf_gossip* g, uint32_t* hist, uint32_t* max3, uint32_t* bin, uint32_t* bins) {
   if (!g) return gerr("null context");
+  RSF_HIP(hipSetDevice(g->device));
+  int jrc = join_check(g);
+  if (jrc) return jrc;
   if (bin) *bin = kOccBin;
   if (bins) *bins = kOccBins + 1;
   if (!hist && !max3) return RSF_OK;

@@ -87,7 +87,9 @@ class World(C.Structure):
                 ("gen", C.c_uint32), ("rbits", C.c_uint32), ("dlog", P64), ("dcnt", P32), ("dcap", C.c_uint32),
                 ("snap_bits", P32), ("snap_w", C.c_uint32), ("snap_rejoin", C.c_int32), ("snap_sn", P64),
                 ("qd", C.c_uint32 * 3), ("q_hwm", P32), ("max_ue", C.c_uint32), ("query_limit", C.c_uint32),
-                ("act_status", PI32), ("act_cap", C.c_uint32), ("last_n_acts", C.c_uint32)]
+                ("act_status", PI32), ("act_cap", C.c_uint32), ("last_n_acts", C.c_uint32),
+                ("chk_period", C.c_uint32), ("chk_max", C.c_uint32), ("chk_min", C.c_uint32),
+                ("chk_warn", C.c_uint32), ("chk_stats", C.c_uint64 * 9)]
 
 
 class WorldCfg(C.Structure):
@@ -236,6 +238,8 @@ def lib():
     L.orc_check_queues_phase.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                          C.c_uint32, P64]
     L.orc_check_queues_phase.restype = None
+    L.orc_world_set_checker.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
+    L.orc_world_set_checker.restype = None
     L.orc_reap.argtypes = [C.POINTER(World), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
     L.orc_varint_len.argtypes = [C.c_uint64]
     L.orc_varint_len.restype = C.c_uint32

@@ -138,6 +138,63 @@ def test_deep_staggered_ticks_bit_exact():
     L.orc_world_free(C.byref(w))
 
 
+def test_deep_in_round_checker_bit_exact():
+    """In-round staggered ticks (rsf_gossip_set_checker: every round r ticks the members with
+    id = r mod 25 between its emission and its merge, on a second stream beside the merge)
+    in the reference's queue regime at the bench's saturated shape; bit-exact against the
+    oracle's tick at the same point (orc_world_set_checker), compared every 5 rounds, the
+    accumulated counts equal."""
+    n, s, rounds, period, mx = 8000, 4096, 80, 25, 1100
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=64, queue_depth=(8192, 0, 0), gossip_limit=8 * 24,
+                         gossip_overhead=2, max_rumors=1 << 20, event_buffer_size=512, query_buffer_size=512,
+                         slot_k=1)
+    subj, acts, ml = W.intents_workload(n, s, rounds, rate=0.05, seed=79)
+    g, w = pair(cfg, subj, W.initial_views(s))
+    g.set_checker(period, mx, 0, 128)
+    L.orc_world_set_checker(C.byref(w), mx, 0, 128, period)
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t], threads=16)
+        if (t + 1) % 5 == 0:
+            same(g, w, f"round {t}")
+    got = g.checker_stats()
+    assert list(got["queued"]) + list(got["warn"]) + list(got["pruned"]) == list(w.chk_stats)
+    assert int(w.chk_stats[6]) > 0
+    st = H.engine_state(g, H.world_width(w))
+    assert int(st["q_pruned"].sum()) == 0 and int(st["q_expired"].sum()) == 0
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
+@pytest.mark.parametrize("qcap,depth,mn", [(16, 100, 0), (32, 0, 0), (16, 100, 5)])
+def test_in_round_checker_churn_bit_exact(qcap, depth, mn):
+    """In-round ticks over all three queues with churn (members going down keep their pending
+    re-queues: the tick's flush applies them before the fork), deep and bounded queues, and
+    the per-member max (min_queue_depth > 0: queue_max_kernel reads the views before the
+    merge changes them); bit-exact every round."""
+    n, rounds, period = 1200, 20, 4
+    subj, acts, ml = W.churn_workload(n, rounds, events_per_round=30, queries_per_round=5, seed=qcap + depth + mn)
+    s = len(subj)
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=qcap, queue_depth=(depth, depth, depth),
+                         gossip_limit=400, gossip_overhead=3, retransmit_mult=4, max_rumors=512,
+                         event_buffer_size=128, query_buffer_size=128, slot_k=8, max_refute=2)
+    g, w = pair(cfg, subj, W.initial_views(s))
+    mx = max(4, (depth or qcap) // 3)
+    g.set_checker(period, mx, mn, 8)
+    L.orc_world_set_checker(C.byref(w), mx, mn, 8, period)
+    for t in range(rounds):
+        g.round(t, ml[t], acts[t])
+        H.oracle_round(w, t, ml[t], acts[t])
+        same(g, w, f"round {t}")
+    got = g.checker_stats()
+    assert list(got["queued"]) + list(got["warn"]) + list(got["pruned"]) == list(w.chk_stats)
+    if not mn:
+        assert int(sum(w.chk_stats[6:9])) > 0
+    g.set_checker(0)
+    g.close()
+    L.orc_world_free(C.byref(w))
+
+
 @pytest.mark.parametrize("qcap,depth", [(16, 100), (32, 0)])
 def test_staggered_ticks_churn_bit_exact(qcap, depth):
     """Phased ticks over all three queues with churn, deep (head + tail) and bounded queues:
