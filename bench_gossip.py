@@ -106,7 +106,7 @@ def run_gossip(args, rank, world):
     eng.init_views(*views)
     if check_every:
         # the staggered ticks inside the rounds: round r ticks the members with id = r mod K,
-        # between its emission and its merge, on a second stream beside the merge
+        # between its emission and its merge
         eng.set_checker(check_every, MAX_QUEUE_DEPTH, 0, QUEUE_DEPTH_WARNING)
 
     def step_settle(t_):

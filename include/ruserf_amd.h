@@ -583,9 +583,8 @@ int rsf_gossip_check_queues_phase(rsf_gossip* g, uint32_t max_queue_depth, uint3
                                   uint32_t depth_warning, uint32_t period, uint32_t phase);
 /* In-round staggered ticks (period > 0; 0 turns them off): from the next round on, every
  * round r runs the tick of the members whose global id is r mod period, after the round's
- * emission and before its merge, on a second HIP stream beside the merge (the merge touches
- * no queue).  The oracle's orc_world_set_checker places its tick at the same point.  Resets
- * the counts (rsf_gossip_checker_stats). */
+ * emission and before its merge.  The oracle's orc_world_set_checker places its tick at the
+ * same point.  Resets the counts (rsf_gossip_checker_stats). */
 int rsf_gossip_set_checker(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
                            uint32_t period);
 /* The checker counts since the last reset (host, 3 entries each, may be NULL; as

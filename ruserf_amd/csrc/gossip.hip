@@ -3101,16 +3101,8 @@ struct rsf_gossip {
   // liveness in between (ahead_valid), else redraws.  RSF_PEERS_AHEAD=0 turns it off.
   hipStream_t side = nullptr;
   hipEvent_t ev_emitted = nullptr, ev_ahead = nullptr;
-  // deep queues: the full-depth class and the middle class run on their own stream, beside the
-  // tiny and small classes (ev_lists: the lists are complete; ev_deep_side: that stream is done)
-  hipStream_t deep_side = nullptr;
-  hipEvent_t ev_lists = nullptr, ev_deep_side = nullptr;
-  // in-round checker ticks (rsf_gossip_set_checker): period 0 = off; they run on chk_stream
-  // (the deep side stream, or chk_own) beside the merge, joined back by join_check
+  // in-round checker ticks (rsf_gossip_set_checker): period 0 = off
   uint32_t chk_period = 0, chk_max = 0, chk_min = 0, chk_warn = 0;
-  hipStream_t chk_stream = nullptr, chk_own = nullptr;
-  hipEvent_t ev_chk_fork = nullptr, ev_chk = nullptr;
-  bool chk_pending = false;
   bool ahead_launched = false, ahead_valid = false, ahead_on = true;
   uint32_t ahead_round = 0;
   int end_bit = 32;
@@ -3145,17 +3137,7 @@ static void mark(rsf_gossip* g, int k) {
 
 // Every member's pending re-queues applied to its queues: before anything other than
 // emission reads the queues, the queue-prune counters or the error flags.
-// the engine's stream waits for an in-round checker tick still running on its own stream
-static int join_check(rsf_gossip* g) {
-  if (!g->chk_pending) return RSF_OK;
-  g->chk_pending = false;
-  RSF_HIP(hipStreamWaitEvent(g->stream, g->ev_chk, 0));
-  return RSF_OK;
-}
-
 static int flush_pending(rsf_gossip* g, uint32_t period = 1, uint32_t phase = 0) {
-  int jrc = join_check(g);
-  if (jrc) return jrc;
   const uint64_t cnt = phase_count(g->c, period, phase);
   if (!cnt) return RSF_OK;
   hipLaunchKernelGGL(pend_flush_kernel, dim3(grid1(cnt, kWavesPerBlock)), dim3(kWave * kWavesPerBlock), 0,
@@ -3315,13 +3297,6 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   if (hipStreamCreateWithFlags(&g->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&g->ev_emitted, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&g->ev_ahead, hipEventDisableTiming) != hipSuccess)
-    return fail(rsf::set_error(RSF_ERR_HIP, "hipStreamCreate / hipEventCreate failed"));
-  if (hipEventCreateWithFlags(&g->ev_chk_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&g->ev_chk, hipEventDisableTiming) != hipSuccess)
-    return fail(rsf::set_error(RSF_ERR_HIP, "hipEventCreate failed"));
-  if (c.deep && (hipStreamCreateWithFlags(&g->deep_side, hipStreamNonBlocking) != hipSuccess ||
-                 hipEventCreateWithFlags(&g->ev_lists, hipEventDisableTiming) != hipSuccess ||
-                 hipEventCreateWithFlags(&g->ev_deep_side, hipEventDisableTiming) != hipSuccess))
     return fail(rsf::set_error(RSF_ERR_HIP, "hipStreamCreate / hipEventCreate failed"));
   {
     const char* e = getenv("RSF_PEERS_AHEAD");
@@ -3485,14 +3460,6 @@ int rsf_gossip_destroy(rsf_gossip* g) {
   if (g->own) hipStreamDestroy(g->own);
   if (g->side) hipStreamDestroy(g->side);
   if (g->ev_emitted) hipEventDestroy(g->ev_emitted);
-  if (g->deep_side) hipStreamSynchronize(g->deep_side);
-  if (g->deep_side) hipStreamDestroy(g->deep_side);
-  if (g->ev_lists) hipEventDestroy(g->ev_lists);
-  if (g->ev_deep_side) hipEventDestroy(g->ev_deep_side);
-  if (g->chk_own) hipStreamSynchronize(g->chk_own);
-  if (g->chk_own) hipStreamDestroy(g->chk_own);
-  if (g->ev_chk_fork) hipEventDestroy(g->ev_chk_fork);
-  if (g->ev_chk) hipEventDestroy(g->ev_chk);
   if (g->ev_ahead) hipEventDestroy(g->ev_ahead);
   delete g;
   return RSF_OK;
@@ -3507,8 +3474,6 @@ int rsf_gossip_set_stream(rsf_gossip* g, void* st) {
 int rsf_gossip_sync(rsf_gossip* g) {
   if (!g) return gerr("null context");
   RSF_HIP(hipSetDevice(g->device));
-  int jrc = join_check(g);
-  if (jrc) return jrc;
   if (g->ahead_launched) RSF_HIP(hipStreamSynchronize(g->side));
   RSF_HIP(hipStreamSynchronize(g->stream));
   return RSF_OK;
@@ -3660,11 +3625,6 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
                            const rsf_action* acts, uint32_t n_acts) {
   if (!g || (n_ml && !ml) || (n_acts && !acts)) return gerr("null argument");
   const GCfg& c = g->c;
-  {  // an in-round checker tick of the previous round, if its merge call did not join it
-    RSF_HIP(hipSetDevice(g->device));
-    int jrc = join_check(g);
-    if (jrc) return jrc;
-  }
   for (uint32_t e = 0; e < n_ml; ++e)
     if (ml[e].subject >= c.S || (ml[e].kind != RSF_ML_JOIN && ml[e].kind != RSF_ML_LEAVE && ml[e].kind != RSF_ML_UPDATE) || ml[e].set_alive > 2)
       return gerr("bad memberlist event");
@@ -3804,22 +3764,17 @@ static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
 #undef RSF_EMIT_DEEP
     RSF_HIP(hipGetLastError());
     RSF_DBG_SYNC(st, "emit_kernel (deep)");
-    // the classes work on disjoint members: the full depth (list 1) and the middle class on
-    // the deep side stream beside the tiny and small classes; the members the smaller classes
-    // re-list (list 4) go through the full depth last, after every class has run
-    hipStream_t sd = g->deep_side;
-    RSF_HIP(hipEventRecord(g->ev_lists, st));
-    RSF_HIP(hipStreamWaitEvent(sd, g->ev_lists, 0));
-    hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepBig>), dim3(g->deep_blocks_big), dim3(kWave), 0, sd, c, g->s,
-                       g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 1u, g->d_counters + 55);
-    hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepMid>), dim3(g->deep_blocks_mid), dim3(kWave), 0, sd, c, g->s,
-                       g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 3u, g->d_counters + 55);
-    RSF_HIP(hipEventRecord(g->ev_deep_side, sd));
+    // by capacity; the members the smaller classes re-list (list 4) go through the full depth
+    // last.  (Run beside each other on two streams, the classes were slower: a full-depth
+    // wave holds most of its CU's LDS, so the small classes' waves could not share the CU.)
     hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepTiny>), dim3(g->deep_blocks_tiny), dim3(kWave), 0, st, c, g->s,
                        g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 2u, g->d_counters + 55);
     hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepSmall>), dim3(g->deep_blocks), dim3(kWave), 0, st, c, g->s,
                        g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 0u, g->d_counters + 55);
-    RSF_HIP(hipStreamWaitEvent(st, g->ev_deep_side, 0));
+    hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepMid>), dim3(g->deep_blocks_mid), dim3(kWave), 0, st, c, g->s,
+                       g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 3u, g->d_counters + 55);
+    hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepBig>), dim3(g->deep_blocks_big), dim3(kWave), 0, st, c, g->s,
+                       g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 1u, g->d_counters + 55);
     hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepBig>), dim3(g->deep_blocks_big), dim3(kWave), 0, st, c, g->s,
                        g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 4u, g->d_counters + 55);
   } else if (c.qcap == kWave) {
@@ -4004,8 +3959,7 @@ int rsf_gossip_round(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml, uint
   g->merged_from_stage = true;
   g->merged_from_buckets = false;
   hipLaunchKernelGGL(accumulate_kernel, dim3(1), dim3(64), 0, g->stream, g->d_counters, 0u);
-  if ((rc = launch_merge(g, nullptr, true))) return rc;
-  return join_check(g);
+  return launch_merge(g, nullptr, true);
 }
 
 int rsf_gossip_bucket_buffers(rsf_gossip* g, uint32_t world, void** send, void** recv, uint64_t* bucket_bytes) {
@@ -4076,7 +4030,7 @@ int rsf_gossip_round_merge_buckets(rsf_gossip* g, uint32_t world) {
   int rc = merge_launch<true>(g, nullptr, nullptr, g->d_rstart, g->d_rend, nullptr, c.cap_t, bk);
   if (rc) return rc;
   mark(g, 4);
-  return join_check(g);
+  return RSF_OK;
 }
 
 int rsf_gossip_bucket_status(rsf_gossip* g, int* ok) {
@@ -4383,11 +4337,9 @@ int rsf_gossip_set_now(rsf_gossip* g, uint32_t now) {
 
 // one checker tick at the members whose global id is phase mod period (period 1: all), on
 // the engine's stream; reset: the stats block and the occupancy histogram start from zero
-// rs: the stream the count and the prune run on (the flush and queue_max_kernel, which read
-// pending lists and views, always run on the engine's stream first); another stream than the
-// engine's is joined back by join_check
 static int check_launch(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
-                        uint32_t period, uint32_t phase, bool reset, hipStream_t rs) {
+                        uint32_t period, uint32_t phase, bool reset) {
+  hipStream_t rs = g->stream;
   const GCfg& c = g->c;
   // get_queue_max (base.rs:748-759): max_queue_depth, or (min_queue_depth > 0) per member
   // max(2 * members.states.len(), min_queue_depth) -- queue_max_kernel
@@ -4407,11 +4359,6 @@ static int check_launch(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_qu
     if ((rc = dmalloc((void**)&g->occ_hist, hist_words * 4))) return rc;
     reset = true;
   }
-  const bool fork = rs != g->stream;
-  if (fork) {
-    RSF_HIP(hipEventRecord(g->ev_chk_fork, g->stream));
-    RSF_HIP(hipStreamWaitEvent(rs, g->ev_chk_fork, 0));
-  }
   if (reset) {
     RSF_HIP(hipMemsetAsync(g->occ_hist, 0, hist_words * 4, rs));
     RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, rs));
@@ -4426,20 +4373,15 @@ static int check_launch(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_qu
                        qmax);
     RSF_HIP(hipGetLastError());
   }
-  if (fork) {
-    RSF_HIP(hipEventRecord(g->ev_chk, rs));
-    g->chk_pending = true;
-  }
   return RSF_OK;
 }
 
-// the in-round checker ticks (rsf_gossip_set_checker): after round `round`'s emission, on the
-// checker stream, beside the merge -- the merge touches no queue, and every pending list of
-// the ticking members was applied by the emission or by the flush before the fork
+// the in-round checker ticks (rsf_gossip_set_checker): after round `round`'s emission, before
+// its merge.  (Run on a second stream beside the merge, the prune and the merge each took
+// longer and the round did not shorten: the prune's blocks hold most of a CU's LDS.)
 static int check_in_round(rsf_gossip* g, uint32_t round) {
   if (!g->chk_period) return RSF_OK;
-  return check_launch(g, g->chk_max, g->chk_min, g->chk_warn, g->chk_period, round % g->chk_period, false,
-                      g->chk_stream);
+  return check_launch(g, g->chk_max, g->chk_min, g->chk_warn, g->chk_period, round % g->chk_period, false);
 }
 
 static int check_stats(rsf_gossip* g, uint64_t* num_queued, uint64_t* n_warn, uint64_t* n_pruned) {
@@ -4457,7 +4399,7 @@ static int check_stats(rsf_gossip* g, uint64_t* num_queued, uint64_t* n_warn, ui
 int rsf_gossip_check_queues(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
                             uint64_t* num_queued, uint64_t* n_warn, uint64_t* n_pruned) {
   if (!g) return gerr("null context");
-  int rc = check_launch(g, max_queue_depth, min_queue_depth, depth_warning, 1, 0, true, g->stream);
+  int rc = check_launch(g, max_queue_depth, min_queue_depth, depth_warning, 1, 0, true);
   return rc ? rc : check_stats(g, num_queued, n_warn, n_pruned);
 }
 
@@ -4465,23 +4407,13 @@ int rsf_gossip_check_queues_phase(rsf_gossip* g, uint32_t max_queue_depth, uint3
                                   uint32_t depth_warning, uint32_t period, uint32_t phase) {
   if (!g) return gerr("null context");
   if (!period || phase >= period) return gerr("phase must be below a non-zero period");
-  return check_launch(g, max_queue_depth, min_queue_depth, depth_warning, period, phase, false, g->stream);
+  return check_launch(g, max_queue_depth, min_queue_depth, depth_warning, period, phase, false);
 }
 
 int rsf_gossip_set_checker(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_queue_depth, uint32_t depth_warning,
                            uint32_t period) {
   if (!g) return gerr("null context");
   RSF_HIP(hipSetDevice(g->device));
-  int rc = join_check(g);
-  if (rc) return rc;
-  if (period && !g->chk_stream) {
-    if (g->deep_side) {
-      g->chk_stream = g->deep_side;  // idle once the emission is done
-    } else {
-      RSF_HIP(hipStreamCreateWithFlags(&g->chk_own, hipStreamNonBlocking));
-      g->chk_stream = g->chk_own;
-    }
-  }
   g->chk_period = period;
   g->chk_max = max_queue_depth;
   g->chk_min = min_queue_depth;
@@ -4492,8 +4424,6 @@ int rsf_gossip_set_checker(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min
 int rsf_gossip_checker_stats(rsf_gossip* g, uint64_t* num_queued, uint64_t* n_warn, uint64_t* n_pruned, int reset) {
   if (!g) return gerr("null context");
   RSF_HIP(hipSetDevice(g->device));
-  int jrc = join_check(g);
-  if (jrc) return jrc;
   const bool have = g->occ_hist != nullptr;
   int rc = RSF_OK;
   if (have) {
@@ -4524,9 +4454,6 @@ int rsf_gossip_action_status(rsf_gossip* g, int32_t* status, uint32_t n) {
 
 int rsf_gossip_checker_occupancy(rsf_gossip* g, uint32_t* hist, uint32_t* max3, uint32_t* bin, uint32_t* bins) {
   if (!g) return gerr("null context");
-  RSF_HIP(hipSetDevice(g->device));
-  int jrc = join_check(g);
-  if (jrc) return jrc;
   if (bin) *bin = kOccBin;
   if (bins) *bins = kOccBins + 1;
   if (!hist && !max3) return RSF_OK;

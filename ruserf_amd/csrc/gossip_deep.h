@@ -1131,20 +1131,18 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
     }
     if (n <= keep) continue;  // (listed by the same count: cannot happen)
     RSF_CK(1);
-    // the largest key kept, the new head's largest, the reserve's largest
-    const uint32_t ks[3] = {keep, c.qcap, c.qcap + kDeepReserve};
-    const bool act[3] = {keep > 0, keep > c.qcap, keep > c.qcap + kDeepReserve};
+    // the largest key kept
+    const uint32_t ks[3] = {keep, 0u, 0u};
+    const bool act[3] = {keep > 0, false, false};
     uint64_t sel[3];
     lds_select3(keys, n, d, ks, act, an, orr, fuse, sel);
     const uint64_t T = act[0] ? sel[0] : 0ull;
-    const uint64_t Th = act[1] ? sel[1] : T;
-    const uint64_t TR = act[2] ? sel[2] : T;
     const bool any = act[0];
     RSF_CK(2);
-    uint64_t bmin = ~0ull, tmin = ~0ull;
-    uint32_t tlmin = ~0u;
-    // pass 2, the tail in index order: the sealed group (TR < key <= T) compacted in place, the
-    // reserve (Th < key <= TR) and the new head's items (key <= Th) staged in LDS
+    // pass 2: the tail's kept items (key <= T) compacted in place in index order, so the sealed
+    // prefix stays a prefix (its bound still holds) and the unsealed items follow it
+    const uint32_t m = min(s.tseal[l * 3 + q].x, tc);
+    uint32_t kept_sealed = 0;
     for (uint32_t b = 0; b < tc; b += kDeepU * kDeepThreads) {
       uint4 x[kDeepU];
 #pragma unroll
@@ -1152,14 +1150,14 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
         const uint32_t i = b + u * kDeepThreads + tid;
         x[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
       }
-      uint64_t sm[kDeepU];
+      uint64_t km[kDeepU];
 #pragma unroll
       for (uint32_t u = 0; u < kDeepU; ++u) {
         const uint32_t i = b + u * kDeepThreads + tid;
-        const uint64_t k = i < tc ? keys[hn + i] : ~0ull;
-        const bool in = any && i < tc;
-        sm[u] = ballot(in && k > TR && k <= T);
-        if (lane == 0) d.wcnt[u][w] = (uint32_t)__popcll(sm[u]);
+        const bool kp = any && i < tc && keys[hn + i] <= T;
+        km[u] = ballot(kp);
+        if (lane == 0) d.wcnt[u][w] = (uint32_t)__popcll(km[u]);
+        kept_sealed += kp && i < m ? 1u : 0u;
       }
       __syncthreads();  // every thread has read its batch: the batch's positions may be rewritten
       uint32_t base = d.nb, tot = 0;
@@ -1169,28 +1167,10 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
         for (uint32_t v = 0; v < kDeepWaves; ++v) tot += d.wcnt[u][v];
 #pragma unroll
       for (uint32_t u = 0; u < kDeepU; ++u) {
-        const uint32_t i = b + u * kDeepThreads + tid;
         uint32_t before = 0;
 #pragma unroll
         for (uint32_t v = 0; v < kDeepWaves; ++v) before += v < w ? d.wcnt[u][v] : 0u;
-        const uint64_t k = i < tc ? keys[hn + i] : ~0ull;
-        const bool in = any && i < tc;
-        const bool sealed = in && k > TR && k <= T, res = in && k > Th && k <= TR, head = in && k <= Th;
-        if (sealed) {
-          t[base + before + mbcnt(sm[u])] = x[u];
-          bmin = k < bmin ? k : bmin;
-          tlmin = min(tlmin, key_len(k));
-        }
-        if (res) {
-          d.ritem[atomicAdd(&d.nr, 1u)] = x[u];
-          tmin = k < tmin ? k : tmin;
-          tlmin = min(tlmin, key_len(k));
-        }
-        if (head) {
-          const uint32_t j = atomicAdd(&d.nh, 1u);
-          d.hitem[j] = make_uint4(x[u].x, x[u].y, x[u].z, q == 0 ? x[u].w : 0u);
-          d.hkey[j] = k;
-        }
+        if ((km[u] >> lane) & 1ull) t[base + before + mbcnt(km[u])] = x[u];
 #pragma unroll
         for (uint32_t v = 0; v < kDeepWaves; ++v) base += d.wcnt[u][v];
       }
@@ -1198,68 +1178,25 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
       if (tid == 0) d.nb += tot;
       __syncthreads();
     }
-    RSF_CK(3);
-    // the old head's items: to the new head, the reserve, or the sealed group (appended)
-    if (tid < kWave) {
-      const bool live_h = any && tid < c.qcap && s.q_rumor[hb + tid] != kEmpty;
-      uint4 x = make_uint4(0, 0, 0, 0);
-      uint64_t k = ~0ull;
-      if (live_h) {
-        x = make_uint4(s.q_rumor[hb + tid], s.q_seq[hb + tid], s.q_txlen[hb + tid],
-                       q == 0 ? s.q_dec[l * c.qcap + tid] : 0u);
-        k = tlq_key(x.z & 0xFFFF, x.z >> 16, x.y);
-      }
-      const bool sealed = live_h && k > TR && k <= T, res = live_h && k > Th && k <= TR, head = live_h && k <= Th;
-      const uint64_t sm = ballot(sealed);
-      const uint32_t nb0 = d.nb;
-      if (sealed) {
-        t[nb0 + mbcnt(sm)] = x;
-        bmin = k < bmin ? k : bmin;
-        tlmin = min(tlmin, key_len(k));
-      }
-      if (res) {
-        d.ritem[atomicAdd(&d.nr, 1u)] = x;
-        tmin = k < tmin ? k : tmin;
-        tlmin = min(tlmin, key_len(k));
-      }
-      if (head) {
-        const uint32_t j = atomicAdd(&d.nh, 1u);
-        d.hitem[j] = x;
-        d.hkey[j] = k;
-      }
-      wsync();
-      if (lane == 0) d.nb = nb0 + (uint32_t)__popcll(sm);
+    // the head is sorted: the items past T are a suffix of its slots
+    if (tid < c.qcap && s.q_rumor[hb + tid] != kEmpty &&
+        (!any || tlq_key(s.q_txlen[hb + tid] & 0xFFFF, s.q_txlen[hb + tid] >> 16, s.q_seq[hb + tid]) > T)) {
+      s.q_rumor[hb + tid] = kEmpty;
+      s.q_seq[hb + tid] = 0;
+      s.q_txlen[hb + tid] = 0;
     }
+    kept_sealed = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(kept_sealed), 63);
     __syncthreads();
-    const uint32_t nb = d.nb, nr = d.nr, nh = d.nh;
-    for (uint32_t j = tid; j < nr; j += kDeepThreads) t[nb + j] = d.ritem[j];  // the reserve after them
-    // the new head in key order (rank among the staged keys), free slots after it
-    if (tid < kWave) {
-      const uint64_t mk = tid < nh ? d.hkey[tid] : ~0ull;
-      uint32_t rank = 0;
-      for (uint32_t j = 0; j < nh; ++j) rank += d.hkey[j] < mk ? 1u : 0u;
-      if (tid < c.qcap) {
-        const bool h = tid < nh;
-        const uint32_t slot = h ? rank : tid;
-        const uint4 x = h ? d.hitem[tid] : make_uint4(kEmpty, 0u, 0u, 0u);
-        s.q_rumor[hb + slot] = x.x;
-        s.q_seq[hb + slot] = x.y;
-        s.q_txlen[hb + slot] = x.z;
-        if (q == 0) s.q_dec[l * c.qcap + slot] = x.w;
-      }
-    }
-    bmin = blk_min_u64(bmin, d);
-    tmin = blk_min_u64(tmin, d);
-    tmin = bmin < tmin ? bmin : tmin;
-    uint32_t lm = wave_min_u32(tlmin);
-    __syncthreads();
-    if (lane == 0) d.wcnt[0][w] = lm;
+    if (lane == 0) d.wcnt[0][w] = kept_sealed;
     __syncthreads();
     if (tid == 0) {
-      for (uint32_t v = 0; v < kDeepWaves; ++v) lm = min(lm, d.wcnt[0][v]);
-      const uint32_t cnt = nb + nr;
-      s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, lm, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
-      s.tseal[l * 3 + q] = nb ? make_uint4(nb, (uint32_t)bmin, (uint32_t)(bmin >> 32), 0u) : kTSumEmpty;
+      uint32_t ms = 0;
+      for (uint32_t v = 0; v < kDeepWaves; ++v) ms += d.wcnt[0][v];
+      const uint32_t cnt = d.nb;
+      const uint4 old = s.tsum[l * 3 + q], os = s.tseal[l * 3 + q];
+      // the bounds stay valid lower bounds (only items left)
+      s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, old.y, old.z, old.w) : kTSumEmpty;
+      s.tseal[l * 3 + q] = ms ? make_uint4(ms, os.y, os.z, os.w) : kTSumEmpty;
     }
     __syncthreads();
 #if RSF_DEEP_PROF

@@ -415,8 +415,8 @@ class GossipEngine:
     def set_checker(self, period, max_queue_depth=MAX_QUEUE_DEPTH, min_queue_depth=MIN_QUEUE_DEPTH,
                     depth_warning=QUEUE_DEPTH_WARNING):
         """In-round staggered QueueChecker ticks: every round r then ticks the members whose
-        global id is r mod period, between the round's emission and its merge, on a second
-        stream beside the merge (period 0: off).  Resets the checker counts."""
+        global id is r mod period, between the round's emission and its merge (period 0:
+        off).  Resets the checker counts."""
         check(lib().rsf_gossip_set_checker(self._h, max_queue_depth, min_queue_depth, depth_warning, int(period)))
 
     def checker_stats(self, reset=False):
