@@ -2814,54 +2814,72 @@ __global__ void __launch_bounds__(256) seg_end_kernel(uint64_t n_loc, const uint
 // check_stream_kernel, which keeps the max smallest keys of head and tail.
 // qmax (non-null when min_queue_depth > 0): each member's own get_queue_max (queue_max_kernel).
 constexpr uint32_t kOccBin = 64, kOccBins = 160;  // occupancy histogram: 64-item bins up to 10240, then one overflow bin
-// One wave per member (lane = head slot; 65..256-slot queues in chunks of 64): a queue's
-// head count is its leading run of live slots, one ballot per chunk.
+// One wave per member (lane = head slot; 65..256-slot queues in chunks of 64), a grid-stride
+// loop over the phase's members: a queue's head count is its leading run of live slots, one
+// ballot per chunk.  The counts and the occupancy histogram are summed per block in LDS and
+// added to HBM once per block (one global atomic per member on the same few addresses took
+// 0.25 ms for 6.7k members).
 __global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uint32_t max_depth, uint32_t warn,
                                                            unsigned long long* __restrict__ stats,
                                                            const uint32_t* __restrict__ qmax,
                                                            uint32_t* __restrict__ hist, uint32_t period,
                                                            uint32_t phase) {
+  __shared__ unsigned long long bst[9];
+  __shared__ uint32_t bh[3 * (kOccBins + 1) + 3];
   const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint64_t l = phase_first(c, period, phase) + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave * period;
-  if (l >= c.n_loc) return;
-  if (qmax) max_depth = qmax[l];
-  uint32_t nq[3];
+  for (uint32_t i = threadIdx.x; i < 3 * (kOccBins + 1) + 3; i += blockDim.x) bh[i] = 0;
+  if (threadIdx.x < 9) bst[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t l0 = phase_first(c, period, phase);
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / kWave);
+  for (uint64_t wi = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;; wi += nw) {
+    const uint64_t l = l0 + wi * period;
+    if (l >= c.n_loc) break;
+    const uint32_t mx = qmax ? qmax[l] : max_depth;
+    uint32_t nq[3];
 #pragma unroll
-  for (uint32_t q = 0; q < 3; ++q) {
-    const uint64_t base = (l * 3 + q) * c.qcap;
-    uint32_t n = 0;
-    for (uint32_t j = 0; j < c.qcap; j += kWave) {
-      const bool live = j + lane < c.qcap && s.q_rumor[base + j + lane] != kEmpty;
-      const uint64_t m = ballot(live);
-      const uint32_t run = m == ~0ull ? kWave : (uint32_t)__builtin_ctzll(~m);
-      n = j + run;
-      if (run < kWave) break;
+    for (uint32_t q = 0; q < 3; ++q) {
+      const uint64_t base = (l * 3 + q) * c.qcap;
+      uint32_t n = 0;
+      for (uint32_t j = 0; j < c.qcap; j += kWave) {
+        const bool live = j + lane < c.qcap && s.q_rumor[base + j + lane] != kEmpty;
+        const uint64_t m = ballot(live);
+        const uint32_t run = m == ~0ull ? kWave : (uint32_t)__builtin_ctzll(~m);
+        n = j + run;
+        if (run < kWave) break;
+      }
+      if (tcap_of(c, q)) n += s.tsum[l * 3 + q].x;
+      nq[q] = n;
     }
-    if (tcap_of(c, q)) n += s.tsum[l * 3 + q].x;
-    nq[q] = n;
-  }
-  if (lane < 3) {
-    const uint32_t q = lane, n = q == 0 ? nq[0] : q == 1 ? nq[1] : nq[2];
-    if (hist) {  // occupancy before the prune (rsf_gossip_checker_occupancy)
-      atomicAdd(hist + q * (kOccBins + 1) + min(n / kOccBin, kOccBins), 1u);
-      atomicMax(hist + 3 * (kOccBins + 1) + q, n);
+    if (lane < 3) {
+      const uint32_t q = lane, n = q == 0 ? nq[0] : q == 1 ? nq[1] : nq[2];
+      atomicAdd(&bh[q * (kOccBins + 1) + min(n / kOccBin, kOccBins)], 1u);  // occupancy before the prune
+      atomicMax(&bh[3 * (kOccBins + 1) + q], n);
+      if (n) atomicAdd(&bst[q], (unsigned long long)n);
+      if (n >= warn) atomicAdd(&bst[3 + q], 1ull);
+      if (n > mx) {
+        if (tcap_of(c, q)) s.deep_ids[atomicAdd(s.deep_n, 1u)] = (uint32_t)(l * 3 + q);
+        atomicAdd(&bst[6 + q], (unsigned long long)(n - mx));
+      }
     }
-    if (n) atomicAdd(stats + q, (unsigned long long)n);
-    if (n >= warn) atomicAdd(stats + 3 + q, 1ull);
-    if (n > max_depth) {
-      if (tcap_of(c, q)) s.deep_ids[atomicAdd(s.deep_n, 1u)] = (uint32_t)(l * 3 + q);
-      atomicAdd(stats + 6 + q, (unsigned long long)(n - max_depth));
-    }
-  }
 #pragma unroll
-  for (uint32_t q = 0; q < 3; ++q) {
-    if (tcap_of(c, q) || nq[q] <= max_depth) continue;  // numq >= max -> prune(max): retain max
-    const uint64_t base = (l * 3 + q) * c.qcap;
-    for (uint32_t i = max_depth + lane; i < nq[q]; i += kWave) {
-      s.q_rumor[base + i] = kEmpty;
-      s.q_seq[base + i] = 0;
-      s.q_txlen[base + i] = 0;
+    for (uint32_t q = 0; q < 3; ++q) {
+      if (tcap_of(c, q) || nq[q] <= mx) continue;  // numq >= max -> prune(max): retain max
+      const uint64_t base = (l * 3 + q) * c.qcap;
+      for (uint32_t i = mx + lane; i < nq[q]; i += kWave) {
+        s.q_rumor[base + i] = kEmpty;
+        s.q_seq[base + i] = 0;
+        s.q_txlen[base + i] = 0;
+      }
     }
+  }
+  __syncthreads();
+  if (threadIdx.x < 9 && bst[threadIdx.x]) atomicAdd(stats + threadIdx.x, bst[threadIdx.x]);
+  if (hist) {
+    for (uint32_t i = threadIdx.x; i < 3 * (kOccBins + 1); i += blockDim.x)
+      if (bh[i]) atomicAdd(hist + i, bh[i]);
+    if (threadIdx.x < 3 && bh[3 * (kOccBins + 1) + threadIdx.x])
+      atomicMax(hist + 3 * (kOccBins + 1) + threadIdx.x, bh[3 * (kOccBins + 1) + threadIdx.x]);
   }
 }
 
@@ -3838,8 +3856,10 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
     RSF_DBG_SYNC(st, "grp_index_kernel");
     mark(g, 2);
     if ((rc = launch_emit<true>(g, egrid, bk))) return rc;
-    if ((rc = launch_ahead(g, round))) return rc;
+    // the tick before the next round's peers start on the side stream: the prune's blocks
+    // hold most of a CU's LDS and would only trade places with the sort's
     if ((rc = check_in_round(g, round))) return rc;
+    if ((rc = launch_ahead(g, round))) return rc;
     mark(g, 3);
     return RSF_OK;
   }
@@ -3851,8 +3871,8 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
   if ((rc = launch_emit<false>(g, egrid, Buckets{}))) return rc;
   RSF_DBG_SYNC(st, "emit_kernel");
   // the counts path reads the sorted groups after the emission (grp_expand_kernel): no ahead
-  if (local && (rc = launch_ahead(g, round))) return rc;
   if ((rc = check_in_round(g, round))) return rc;
+  if (local && (rc = launch_ahead(g, round))) return rc;
   if (local) {
     unsigned long long* sum = (unsigned long long*)g->d_counters;
     const uint32_t* cnt = g->grp_cnt;
@@ -4364,7 +4384,9 @@ static int check_launch(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_qu
     RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, rs));
   }
   if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, kDeepLists * 4, rs));
-  hipLaunchKernelGGL(check_queues_kernel, dim3(grid1(std::max<uint64_t>(1, phase_count(c, period, phase)), 256 / kWave)),
+  hipLaunchKernelGGL(check_queues_kernel,
+                     dim3((unsigned)std::min<uint64_t>(1024, grid1(std::max<uint64_t>(1, phase_count(c, period, phase)),
+                                                                   256 / kWave))),
                      dim3(256), 0, rs, c, g->s, max_depth, depth_warning, g->d_counters + 40, qmax, g->occ_hist, period,
                      phase);
   RSF_HIP(hipGetLastError());
