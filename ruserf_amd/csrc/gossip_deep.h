@@ -902,6 +902,11 @@ __global__ void __launch_bounds__(kWave) emit_deep_wave_kernel(GCfg c, GState s,
 #if RSF_DEEP_PROF
   wsync();
   if (s_dprof[lane]) atomicAdd(&g_deep_prof[lane], s_dprof[lane]);
+  if (lane == 0) {  // per class: [70 + c] cycles, [74 + c] members (c: tiny, small, middle, full)
+    constexpr uint32_t cls = CAP == kDeepTiny ? 0u : CAP == kDeepSmall ? 1u : CAP == kDeepMid ? 2u : 3u;
+    atomicAdd(&g_deep_prof[70 + cls], s_dprof[17]);
+    atomicAdd(&g_deep_prof[74 + cls], s_dprof[16]);
+  }
 #endif
 }
 
@@ -1178,6 +1183,7 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
       if (tid == 0) d.nb += tot;
       __syncthreads();
     }
+    RSF_CK(3);
     // the head is sorted: the items past T are a suffix of its slots
     if (tid < c.qcap && s.q_rumor[hb + tid] != kEmpty &&
         (!any || tlq_key(s.q_txlen[hb + tid] & 0xFFFF, s.q_txlen[hb + tid] >> 16, s.q_seq[hb + tid]) > T)) {
