@@ -259,7 +259,7 @@ def run_gossip(args, rank, world):
     }
 
 
-def cpu_baseline_gossip_deep(args, seconds_target=10.0, n=20_000, settle=60):
+def cpu_baseline_gossip_deep(args, seconds_target=12.0, n=40_000, settle=60):
     """The oracle's round in the same queue regime as the line (the intent queue as deep as
     the engine's, no prune between ticks) on a bounded sample: n members settled `settle`
     rounds (queues ~24 items a round deep by then), then timed on all the box's threads
@@ -270,7 +270,7 @@ def cpu_baseline_gossip_deep(args, seconds_target=10.0, n=20_000, settle=60):
     from bench import cpu_info, cpu_threads
     from ruserf_amd import workload as W
     th = cpu_threads()
-    rounds_total = settle + 40
+    rounds_total = settle + 72
     cfg = gossip_cfg(n, rounds_total, 1, queue_cap=64, queue_depth=args.queue_depth, ring_rounds=rounds_total)
     subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED, prune_frac=PRUNE_FRAC)
     w = H.oracle_world(cfg, subj, W.initial_views(SUBJECTS))
@@ -294,7 +294,7 @@ def cpu_baseline_gossip_deep(args, seconds_target=10.0, n=20_000, settle=60):
             done += 1
             t += 1
         return done, spent
-    done_mt, spent_mt = timed(th, seconds_target, 36)
+    done_mt, spent_mt = timed(th, seconds_target, 64)
     done_1, spent_1 = timed(1, seconds_target / 2, 3)
     width = H.world_width(w)
     H.L.orc_world_free(C.byref(w))

@@ -315,10 +315,12 @@ __device__ uint64_t w_select_kth(DeepWave<CAP>& d, uint32_t lane, uint32_t n, ui
 }
 
 // head = the qcap smallest live keys, sorted into the lanes of Q (marked kDeepInHead in LDS);
-// returns the bounds of the live items left (the tail): (min key, min length), ~0 if none
+// returns the bounds of the live items left (the tail): (min key, min length), ~0 if none, and
+// for w_store_tail the reserve's largest key rres (the (qcap + kDeepReserve)-th smallest: the
+// head's picks leave the other items' keys as they are; ~0 when every item left is reserve)
 template <uint32_t CAP>
 __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint32_t q, QRegs& Q,
-                            uint64_t& tmin, uint32_t& tminlen) {
+                            uint64_t& tmin, uint32_t& tminlen, uint64_t& rres) {
 #if RSF_DEEP_PROF
   uint64_t tt = __builtin_amdgcn_s_memtime();
 #define RSF_TH_T(k)                                                     \
@@ -344,8 +346,17 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
     const WRange rg = w_keys(d, lane, n, kDeepLive, kr, &vb);
     RSF_TH_T(20);
     uint64_t T = ~0ull;
-    if (rg.cnt > c.qcap)
-      T = (rg.orr >> 63) ? w_select_kth(d, lane, n, c.qcap, kDeepLive, rg) : w_select_kth_keys(kr, c.qcap, rg);
+    rres = ~0ull;
+    // the head's largest, then the reserve's: one select routine in a loop (two inlined copies
+    // spill to scratch)
+#pragma unroll 1
+    for (uint32_t j = 0; j < 2; ++j) {
+      const uint32_t k = j ? c.qcap + kDeepReserve : c.qcap;
+      if (rg.cnt <= k) break;
+      const uint64_t x = (rg.orr >> 63) ? w_select_kth(d, lane, n, k, kDeepLive, rg) : w_select_kth_keys(kr, k, rg);
+      if (j) rres = x;
+      else T = x;
+    }
     RSF_TH_T(21);
 #pragma unroll
     for (uint32_t r = 0; r < R; ++r) {
@@ -368,7 +379,16 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
   } else {
   const WRange rg = w_range(d, lane, n, kDeepLive);
   RSF_TH_T(20);
-  const uint64_t T = rg.cnt > c.qcap ? w_select_kth(d, lane, n, c.qcap, kDeepLive, rg) : ~0ull;
+  uint64_t T = ~0ull;
+  rres = ~0ull;
+#pragma unroll 1
+  for (uint32_t j = 0; j < 2; ++j) {
+    const uint32_t k = j ? c.qcap + kDeepReserve : c.qcap;
+    if (rg.cnt <= k) break;
+    const uint64_t x = w_select_kth(d, lane, n, k, kDeepLive, rg);
+    if (j) rres = x;
+    else T = x;
+  }
   RSF_TH_T(21);
   for (uint32_t b0 = 0; b0 < n; b0 += kDeepU * kWave) {
     uint64_t x[kDeepU];
@@ -425,31 +445,32 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
 // sealed group's size, *bmin = its smallest key (~0 if none).
 template <uint32_t CAP>
 __device__ uint32_t w_store_tail(const GCfg& c, const GState& s, uint64_t l, uint32_t q, DeepWave<CAP>& d,
-                                 uint32_t lane, uint32_t n, uint32_t t_lo, uint32_t* nb, uint64_t* bmin) {
+                                 uint32_t lane, uint32_t n, uint32_t t_lo, uint64_t R, uint32_t* nb, uint64_t* bmin) {
   uint4* const t = tcap_of(c, q) ? tail_of(s, q) + l * tstride_of(c, q) + t_lo : nullptr;
-  const WRange rg = w_range(d, lane, n, kDeepLive);
-  // R: the reserve's largest key (every live item when there are no more than the reserve)
-  const uint64_t R = rg.cnt > kDeepReserve ? w_select_kth(d, lane, n, kDeepReserve, kDeepLive, rg) : ~0ull;
-  uint32_t base = 0;
-  uint64_t bm = ~0ull;
-  for (uint32_t pass = 0; pass < 2; ++pass) {  // 0: the sealed group (> R), 1: the reserve (<= R)
-    if (pass == 1) {
-      *nb = base;
-      *bmin = wave_min_u64(bm);
-    }
-    for (uint32_t b = 0; b < n; b += kWave) {
-      const uint32_t i = b + lane;
-      const uint64_t k = i < n ? d.key[i] : 0ull;
-      const bool live = i < n && d.st[i] == kDeepLive && ((k > R) == (pass == 0));
-      const uint64_t m = ballot(live);
-      if (live) {  // only a deep queue holds more live items than its head
-        t[base + mbcnt(m)] = make_uint4(d.rid[i], key_seq(k), key_tl(k), d.dec[i]);
-        if (pass == 0) bm = k < bm ? k : bm;
-      }
-      base += (uint32_t)__popcll(m);
-    }
+  // the sealed group's size first (one count pass: the reserve is R's items and below)
+  uint32_t ns = 0;
+  for (uint32_t b = 0; b < n; b += kWave) {
+    const uint32_t i = b + lane;
+    ns += (uint32_t)__popcll(ballot(i < n && d.st[i] == kDeepLive && d.key[i] > R));
   }
-  return base;
+  // one pass writes both groups: sealed (> R) at [0, ns), the reserve (<= R) from ns on
+  uint32_t bs = 0, br = ns;
+  uint64_t bm = ~0ull;
+  for (uint32_t b = 0; b < n; b += kWave) {
+    const uint32_t i = b + lane;
+    const uint64_t k = i < n ? d.key[i] : 0ull;
+    const bool live = i < n && d.st[i] == kDeepLive;
+    const bool sealed = live && k > R, res = live && k <= R;
+    const uint64_t ms = ballot(sealed), mr = ballot(res);
+    if (live)  // only a deep queue holds more live items than its head
+      t[sealed ? bs + mbcnt(ms) : br + mbcnt(mr)] = make_uint4(d.rid[i], key_seq(k), key_tl(k), d.dec[i]);
+    if (sealed) bm = k < bm ? k : bm;
+    bs += (uint32_t)__popcll(ms);
+    br += (uint32_t)__popcll(mr);
+  }
+  *nb = ns;
+  *bmin = wave_min_u64(bm);
+  return br;
 }
 
 // the sealed prefix tail[0, sm) into LDS after the n items there (live): the recent mode could
@@ -689,10 +710,10 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
       wsync();
     }
     // the refill, then the head's own emission with the deep checks
-    uint64_t tmin;
+    uint64_t tmin, rres;
     uint32_t tminlen;
     RSF_DEEP_T(9);
-    w_take_head(c, d, lane, n, q, Q, tmin, tminlen);
+    w_take_head(c, d, lane, n, q, Q, tmin, tminlen, rres);
     RSF_DEEP_T(10);
     // recent mode: exact only if the head is full and below every sealed key; the sealed
     // prefix stays in the tail, so the tail's bounds include the seal's
@@ -719,7 +740,7 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
         recent = false;
         t_lo = 0;
         sb = ~0ull;
-        w_take_head(c, d, lane, n, q, Q, tmin, tminlen);
+        w_take_head(c, d, lane, n, q, Q, tmin, tminlen, rres);
       }
     }
     if (recent) {
@@ -755,7 +776,7 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
       q_store(c, s, l, q, lane, Q, true);
       uint32_t nb = 0;
       uint64_t bmin = ~0ull;
-      const uint32_t cnt = t_lo + w_store_tail(c, s, l, q, d, lane, n, t_lo, &nb, &bmin);
+      const uint32_t cnt = t_lo + w_store_tail(c, s, l, q, d, lane, n, t_lo, rres, &nb, &bmin);
       if (lane == 0 && tcap_of(c, q)) {
         s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
         // sealed: the kept prefix and the group written above the reserve (key bound: the
@@ -817,11 +838,11 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
         wsync();
       }
       RSF_DEEP_T(13);
-      w_take_head(c, d, lane, n, q, Q, tmin, tminlen);
+      w_take_head(c, d, lane, n, q, Q, tmin, tminlen, rres);
       q_store(c, s, l, q, lane, Q, true);
       uint32_t nb = 0;
       uint64_t bmin = ~0ull;
-      const uint32_t cnt = w_store_tail(c, s, l, q, d, lane, n, 0u, &nb, &bmin);
+      const uint32_t cnt = w_store_tail(c, s, l, q, d, lane, n, 0u, rres, &nb, &bmin);
       if (lane == 0 && tcap_of(c, q)) {
         s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
         s.tseal[l * 3 + q] = nb ? make_uint4(nb, (uint32_t)bmin, (uint32_t)(bmin >> 32), 0u) : kTSumEmpty;
