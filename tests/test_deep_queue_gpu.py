@@ -311,10 +311,12 @@ def test_configs3_100k_deep_queues_bit_exact():
     L.orc_world_free(C.byref(w))
 
 
-def test_deep_two_shards_buckets_equal_one_context():
+@pytest.mark.parametrize("checker", [False, True])
+def test_deep_two_shards_buckets_equal_one_context(checker):
     """The multi-GPU bucket emission with deep queues (emit_kernel and emit_deep_wave_kernel writing
     into the destination buckets): two shard contexts on one GPU, the exchange by hand,
-    equal to one context after every round."""
+    equal to one context after every round; with `checker`, the in-round staggered ticks too
+    (phases by global member id, so each shard ticks its own members of that phase)."""
     import torch
     from ruserf_amd.dist import hbm_tensor
     n, rounds = 4000, 12
@@ -332,6 +334,8 @@ def test_deep_two_shards_buckets_equal_one_context():
         e.set_stream(stream.cuda_stream)
         e.set_subjects(subj)
         e.init_views(*views)
+        if checker:
+            e.set_checker(3, 40, 0, 8)
     bufs = [e.bucket_buffers(2) for e in shards]
     words = bufs[0][2] // 4
     for t in range(rounds):
@@ -361,6 +365,11 @@ def test_deep_two_shards_buckets_equal_one_context():
         for k in full:
             assert np.array_equal(np.concatenate([halves[0][k], halves[1][k]]), full[k]), (t, k)
     assert sum(e.deep_stats()[0] for e in shards) > 0
+    if checker:
+        got = [e.checker_stats() for e in [one] + shards]
+        for key in ("queued", "warn", "pruned"):
+            assert np.array_equal(got[0][key], got[1][key] + got[2][key]), key
+        assert int(got[0]["pruned"].sum()) > 0
     for e in [one] + shards:
         e.close()
 
