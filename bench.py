@@ -154,9 +154,15 @@ def run_vivaldi(args, rank, world):
         if targeted:
             sv.fetch(peer[r].data_ptr())
 
+    def presend(r):
+        # round r + 1's requests go out while round r's observe runs
+        if targeted and r + 1 < rounds:
+            sv.presend(peer[r + 1].data_ptr())
+
     for _ in range(args.warmup):
         fetch(step[0])
         observe(step[0])
+        presend(step[0])
         refresh(step[0])
         step[0] += 1
     torch.cuda.synchronize()
@@ -170,6 +176,7 @@ def run_vivaldi(args, rank, world):
         evs[i][0].record(stream)
         observe(step[0])
         evs[i][1].record(stream)
+        presend(step[0])
         refresh(step[0])
         step[0] += 1
     torch.cuda.synchronize()

@@ -146,20 +146,57 @@ class ShardedVivaldi:
         self.rep_send = hbm_tensor(b["rep_send"], world * b["rep_bucket_bytes"] // 8, "<f8")
         self.rep_recv = hbm_tensor(b["rep_recv"], world * b["rep_bucket_bytes"] // 8, "<f8")
         self.stage = _staged(group, self.req_send.device)
+        self._side = None        # the stream the next round's requests go out on
+        self._sent = None        # the peer-id pointer whose requests are already out
+        self._ev_applied = None  # this round's apply done (it reads the request buckets)
+        self._ev_sent = None
 
     def fetch(self, peer_ptr):
         """Bring the rows of this round's remote peers into the current table."""
         g, w = self.g, self.world
-        g.exchange_requests(w, peer_ptr)
-        all_to_all(self.req_recv, self.req_send, self.stage, self.group)
+        main = torch.cuda.current_stream()
+        if self._sent is not None and self._sent == peer_ptr:
+            main.wait_event(self._ev_sent)  # requests built and exchanged during the last observe
+        else:
+            g.exchange_requests(w, peer_ptr)
+            all_to_all(self.req_recv, self.req_send, self.stage, self.group)
+        self._sent = None
         g.exchange_serve(w)
         all_to_all(self.rep_recv, self.rep_send, self.stage, self.group)
         g.exchange_apply(w)
+        if self._ev_applied is None:
+            self._ev_applied = torch.cuda.Event()
+        self._ev_applied.record(main)
 
-    def round(self, r, peer_ptr, rtt_ptr, status_ptr=None, slots=16):
+    def presend(self, next_peer_ptr):
+        """The next round's requests, built and exchanged on a side stream while this round's
+        observe runs (its peer ids are known ahead: the probe schedule), so the next fetch
+        starts at the serve.  Call after this round's fetch, with the context on torch's
+        current stream."""
+        if self.world == 1 or self._ev_applied is None:
+            return
+        main = torch.cuda.current_stream()
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=main.device)
+            self._ev_sent = torch.cuda.Event()
+        side = self._side
+        side.wait_event(self._ev_applied)
+        self.g.set_stream(side.cuda_stream)
+        try:
+            with torch.cuda.stream(side):
+                self.g.exchange_requests(self.world, next_peer_ptr)
+                all_to_all(self.req_recv, self.req_send, self.stage, self.group)
+        finally:
+            self.g.set_stream(main.cuda_stream)
+        self._ev_sent.record(side)
+        self._sent = next_peer_ptr
+
+    def round(self, r, peer_ptr, rtt_ptr, status_ptr=None, slots=16, next_peer_ptr=None):
         if self.world > 1:
             self.fetch(peer_ptr)
         self.g.observe(r % slots, peer_ptr, rtt_ptr, status_ptr, r)
+        if next_peer_ptr is not None:
+            self.presend(next_peer_ptr)
 
     def check(self):
         """True if no request bucket overflowed and every request reached its owner."""

@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 N, ROUNDS, SEED = 24_000, 14, 0x5EED
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, presend=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
@@ -28,14 +28,17 @@ def _worker(rank, world, port, q):
     g.set_stream(torch.cuda.current_stream().cuda_stream)
     sv = ShardedVivaldi(g, rank, world)
     assert sv.stage
-    peer = torch.empty(per, dtype=torch.int32, device="cuda")
-    rtt = torch.empty(per, dtype=torch.int64, device="cuda")
+    # every round's probes up front (the next round's requests can go out during a round)
+    peer = torch.empty((ROUNDS, per), dtype=torch.int32, device="cuda")
+    rtt = torch.empty((ROUNDS, per), dtype=torch.int64, device="cuda")
     remote = 0
     for r in range(ROUNDS):
-        g.gen_probes(r, peer.data_ptr(), rtt.data_ptr())
-        p = peer.cpu().numpy()
+        g.gen_probes(r, peer[r].data_ptr(), rtt[r].data_ptr())
+        p = peer[r].cpu().numpy()
         remote += int(np.count_nonzero((p < lo) | (p >= hi)))
-        sv.round(r, peer.data_ptr(), rtt.data_ptr())
+    for r in range(ROUNDS):
+        nxt = peer[r + 1].data_ptr() if presend and r + 1 < ROUNDS else None
+        sv.round(r, peer[r].data_ptr(), rtt[r].data_ptr(), next_peer_ptr=nxt)
     torch.cuda.synchronize()
     ok = sv.check()
     rows = g.get_rows(lo, per)
@@ -45,13 +48,15 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_sharded_vivaldi_equals_one_context(world):
+@pytest.mark.parametrize("world,presend", [(2, False), (2, True)])
+def test_sharded_vivaldi_equals_one_context(world, presend):
+    """presend: round r + 1's requests built and exchanged on a side stream during round r
+    (ShardedVivaldi.presend); the result is the same bit for bit."""
     from ruserf_amd import CoordinateClients, CoordinateOptions
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29600 + os.getpid() % 1000
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    port = 29600 + os.getpid() % 1000 + (7 if presend else 0)
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, presend)) for r in range(world)]
     for p in procs:
         p.start()
     got = {}
