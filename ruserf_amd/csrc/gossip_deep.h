@@ -938,10 +938,17 @@ __global__ void __launch_bounds__(kWave) emit_deep_wave_kernel(GCfg c, GState s,
 // LDS keys, one histogram each per radix pass; pass 2 streams the tail again and compacts it
 // in place, eight loads in flight per thread.  Two blocks per CU (the keys of a full queue are
 // 70 KB).
+#ifndef RSF_CHK_U1
+#define RSF_CHK_U1 16  // check_stream_kernel's pass 1: 16-B loads in flight per thread
+#endif
+#ifndef RSF_CHK_U2
+#define RSF_CHK_U2 8  // its pass 2 (the compaction): items per thread per batch
+#endif
+constexpr uint32_t kChkU2 = RSF_CHK_U2;
 struct CheckLds {
   uint32_t hist[3][256];
   uint64_t w64[kDeepWaves], w64b[kDeepWaves];
-  uint32_t wcnt[kDeepU][kDeepWaves];
+  uint32_t wcnt[kChkU2][kDeepWaves];
   uint32_t sel_digit[3], sel_need[3], nb, nr, nh, hn;
   uint4 hitem[kWave];         // the new head's items (<= qcap)
   uint64_t hkey[kWave];
@@ -1104,7 +1111,7 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
     }
     __syncthreads();
     const uint32_t hn = d.hn, n = hn + tc;
-    constexpr uint32_t U1 = 16;
+    constexpr uint32_t U1 = RSF_CHK_U1;
     for (uint32_t b = 0; b < tc; b += U1 * kDeepThreads) {
       uint4 x[U1];
 #pragma unroll
@@ -1169,16 +1176,16 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
     // prefix stays a prefix (its bound still holds) and the unsealed items follow it
     const uint32_t m = min(s.tseal[l * 3 + q].x, tc);
     uint32_t kept_sealed = 0;
-    for (uint32_t b = 0; b < tc; b += kDeepU * kDeepThreads) {
-      uint4 x[kDeepU];
+    for (uint32_t b = 0; b < tc; b += kChkU2 * kDeepThreads) {
+      uint4 x[kChkU2];
 #pragma unroll
-      for (uint32_t u = 0; u < kDeepU; ++u) {
+      for (uint32_t u = 0; u < kChkU2; ++u) {
         const uint32_t i = b + u * kDeepThreads + tid;
         x[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
       }
-      uint64_t km[kDeepU];
+      uint64_t km[kChkU2];
 #pragma unroll
-      for (uint32_t u = 0; u < kDeepU; ++u) {
+      for (uint32_t u = 0; u < kChkU2; ++u) {
         const uint32_t i = b + u * kDeepThreads + tid;
         const bool kp = any && i < tc && keys[hn + i] <= T;
         km[u] = ballot(kp);
@@ -1188,11 +1195,11 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
       __syncthreads();  // every thread has read its batch: the batch's positions may be rewritten
       uint32_t base = d.nb, tot = 0;
 #pragma unroll
-      for (uint32_t u = 0; u < kDeepU; ++u)
+      for (uint32_t u = 0; u < kChkU2; ++u)
 #pragma unroll
         for (uint32_t v = 0; v < kDeepWaves; ++v) tot += d.wcnt[u][v];
 #pragma unroll
-      for (uint32_t u = 0; u < kDeepU; ++u) {
+      for (uint32_t u = 0; u < kChkU2; ++u) {
         uint32_t before = 0;
 #pragma unroll
         for (uint32_t v = 0; v < kDeepWaves; ++v) before += v < w ? d.wcnt[u][v] : 0u;
