@@ -546,6 +546,9 @@ __device__ __forceinline__ void deep_relist_full(const GCfg& c, const GState& s,
 #endif
 }
 
+#ifndef RSF_DEEP_PULL
+#define RSF_DEEP_PULL 1  // 0: re-list to the full depth instead (A/B)
+#endif
 // recent mode with a full head whose largest key Y is not below the sealed prefix's bound:
 // only the sealed items below Y can join the head.  Stream tail[0, m) and append those to LDS
 // after the n items there (live); each one's place goes to d.pend[j].rid (free in recent mode
@@ -796,7 +799,7 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
         ok = Y < sb;
       }
       bool redo = false;  // one refill call site for both cases below (another copy spills)
-      if (!ok && full) {
+      if (RSF_DEEP_PULL && !ok && full) {
         // only the sealed items below the head's largest key can join it: pull those in
         const uint32_t got = w_pull_sealed(c, s, l, q, d, lane, n, t_lo, Y);
         if (got != ~0u) {
