@@ -125,7 +125,6 @@ def run_gossip(args, rank, world):
     pruned0 = eng.pruned_total(flush=False)
     deep0 = eng.deep_stats()[0] if depth else 0
     cls0 = eng.deep_class_stats() if depth else None
-    pulls0 = eng.deep_pulls() if depth else 0
     if check_every:
         eng.checker_stats(reset=True)
     eng.set_profiling(True)
@@ -178,8 +177,7 @@ def run_gossip(args, rank, world):
                   "expired_whole_run": int(eng.expired().sum()),
                   "deferred_per_round_by_class": dict(zip(["tiny", "small", "middle", "full"],
                                                           ((eng.deep_class_stats() - cls0) / args.steps).tolist()))
-                  if depth else None,
-                  "sealed_pulls_per_round": (eng.deep_pulls() - pulls0) / args.steps if depth else None}
+                  if depth else None}
     st = eng.members()
     from ruserf_amd.gossip import E_QUEUE_PRUNE
     # capacity errors other than the bounded queue's counted prunes (reported separately)

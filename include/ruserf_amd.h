@@ -639,10 +639,6 @@ int rsf_gossip_deep_stats(rsf_gossip* g, uint64_t* slow_total, uint64_t* slow_si
  * [0] the smallest class, [1] the small one, [2] the middle one, [3] the full depth (members the
  * smaller classes re-list to it count twice).  Synchronises. */
 int rsf_gossip_deep_class_stats(rsf_gossip* g, uint64_t* out4);
-/* Deferred emissions whose recent mode pulled sealed items into the head (the head's largest
- * key was not below the sealed prefix's bound; only the sealed items below it were read in,
- * DESIGN.md §5.5), since creation.  Synchronises. */
-int rsf_gossip_deep_pulls(rsf_gossip* g, uint64_t* total);
 /* items queued per shard member and queue (host, [n_loc][3]: intent, query, event; head + tail),
  * after applying the pending lists (the QueueChecker's num_queued per node).  Synchronises. */
 int rsf_gossip_queue_lengths(rsf_gossip* g, uint32_t* out);

@@ -3397,7 +3397,6 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   ms(g->d_counters, 0, 72 * 8);  // status flags and running totals start at zero
   // deferred members: the counts of lists 0..4 (words 64-66; [55] their total)
   s.deep_n = reinterpret_cast<uint32_t*>(g->d_counters + 64);
-  s.deep_pulls = g->d_counters + 61;  // running total (rsf_gossip_deep_pulls)
   ms(s.emin, 0, n * 8);
   ms(s.qmin, 0, n * 8);
   ms(s.digest, 0, n * 8);
@@ -4734,16 +4733,6 @@ int rsf_gossip_deep_stats(rsf_gossip* g, uint64_t* slow_total, uint64_t* slow_si
   if (slow_total) *slow_total = t;
   if (slow_since_last) *slow_since_last = t - g->deep_last;
   g->deep_last = t;
-  return RSF_OK;
-}
-
-int rsf_gossip_deep_pulls(rsf_gossip* g, uint64_t* total) {
-  if (!g || !total) return gerr("null argument");
-  unsigned long long t = 0;
-  RSF_HIP(hipSetDevice(g->device));
-  RSF_HIP(hipMemcpyAsync(&t, g->d_counters + 61, 8, hipMemcpyDeviceToHost, g->stream));
-  RSF_HIP(hipStreamSynchronize(g->stream));
-  *total = t;
   return RSF_OK;
 }
 

@@ -546,72 +546,6 @@ __device__ __forceinline__ void deep_relist_full(const GCfg& c, const GState& s,
 #endif
 }
 
-#ifndef RSF_DEEP_PULL
-#define RSF_DEEP_PULL 1  // 0: re-list to the full depth instead (A/B)
-#endif
-// recent mode with a full head whose largest key Y is not below the sealed prefix's bound:
-// only the sealed items below Y can join the head.  Stream tail[0, m) and append those to LDS
-// after the n items there (live); each one's place goes to d.pend[j].rid (free in recent mode
-// once the pending entries are items: only the intent queue has any).  Reads only: HBM
-// changes at the commit (w_fill_sealed), so a member re-listed after this is intact.
-// Returns the count pulled, or ~0u (more than the place list or LDS holds; the LDS slots
-// past n are then left live for the caller to clear).
-template <uint32_t CAP>
-__device__ uint32_t w_pull_sealed(const GCfg& c, const GState& s, uint64_t l, uint32_t q, DeepWave<CAP>& d,
-                                  uint32_t lane, uint32_t n, uint32_t m, uint64_t Y) {
-  const uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
-  const uint32_t room = min(kPend, CAP - n);
-  uint32_t got = 0;
-  for (uint32_t b = 0; b < m; b += kDeepU * kWave) {
-    uint4 e[kDeepU];
-#pragma unroll
-    for (uint32_t u = 0; u < kDeepU; ++u) {
-      const uint32_t i = b + u * kWave + lane;
-      e[u] = i < m ? t[i] : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < kDeepU; ++u) {
-      const uint32_t i = b + u * kWave + lane;
-      const uint64_t k = tlq_key(e[u].z & 0xFFFF, e[u].z >> 16, e[u].y);
-      const bool take = i < m && k < Y;
-      const uint64_t tm = ballot(take);
-      const uint32_t j = got + mbcnt(tm);
-      if (take && j < room) {
-        d.key[n + j] = k;
-        d.rid[n + j] = e[u].x;
-        d.dec[n + j] = q == 0 ? e[u].w : (q == 1 ? kDecQuery : kDecEvent);
-        d.st[n + j] = kDeepLive;
-        d.pend[j].rid = i;  // ascending: streamed in index order
-      }
-      got += (uint32_t)__popcll(tm);
-    }
-  }
-  wsync();
-  return got > room ? ~0u : got;
-}
-
-// the commit of a pull: the sealed prefix tail[0, m) loses its `got` pulled items (places in
-// d.pend[j].rid, ascending); its last `got` places' other items move into the pulled places
-// below m - got (the prefix's order is free), so it becomes tail[0, m - got)
-template <uint32_t CAP>
-__device__ void w_fill_sealed(const GCfg& c, const GState& s, uint64_t l, uint32_t q, DeepWave<CAP>& d,
-                              uint32_t lane, uint32_t m, uint32_t got) {
-  uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
-  const uint32_t m1 = m - got;
-  uint32_t movers = 0;
-  for (uint32_t b = 0; b < got; b += kWave) {
-    const uint32_t pos = m1 + b + lane;
-    bool pulled = false;
-    for (uint32_t j = 0; j < got; ++j) pulled |= d.pend[j].rid == pos;
-    const bool mover = b + lane < got && !pulled;
-    const uint64_t mm = ballot(mover);
-    // the r-th mover fills the r-th smallest pulled place (the places below m1 come first)
-    if (mover) t[d.pend[movers + mbcnt(mm)].rid] = t[pos];
-    movers += (uint32_t)__popcll(mm);
-  }
-  wsync();
-}
-
 template <bool BKT, uint32_t CAP>
 __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uint32_t lane, const DeepPre& pre,
                                  uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val,
@@ -784,41 +718,23 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
     // recent mode: exact only if the head is full and below every sealed key; the sealed
     // prefix stays in the tail, so the tail's bounds include the seal's
     uint64_t sb = ~0ull;  // the kept sealed prefix's key bound (recent mode)
-    uint32_t pull_m = 0, pulled = 0;  // a pull: the prefix's length before it, the items pulled
     if (recent) {
       const uint4 se = s.tseal[l * 3 + q];
       sb = ((uint64_t)se.z << 32) | se.y;
       const uint64_t hm = ballot(lane < c.qcap && Q.r != kEmpty);
       const bool full = (uint32_t)__popcll(hm) == c.qcap;
       bool ok = full;
-      uint64_t Y = 0;
       if (full) {
         const int hl = 63 - __clzll((long long)hm);
         const uint32_t tlh = shfl_u32(Q.tl, hl);
-        Y = tlq_key(tlh & 0xFFFF, tlh >> 16, shfl_u32(Q.sq, hl));
-        ok = Y < sb;
+        ok = tlq_key(tlh & 0xFFFF, tlh >> 16, shfl_u32(Q.sq, hl)) < sb;
       }
-      bool redo = false;  // one refill call site for both cases below (another copy spills)
-      if (RSF_DEEP_PULL && !ok && full) {
-        // only the sealed items below the head's largest key can join it: pull those in
-        const uint32_t got = w_pull_sealed(c, s, l, q, d, lane, n, t_lo, Y);
-        if (got != ~0u) {
-          n += got;
-          pull_m = t_lo;
-          pulled = got;
-          t_lo -= got;
-          sb = Y + 1;  // every item left in the prefix is above Y; the new head's largest is at most Y
-          redo = true;
-        } else {  // too many: the slots the pull filled are cleared, the whole-queue ways follow
-          for (uint32_t i = n + lane; i < n + min(kPend, CAP - n); i += kWave) d.st[i] = kDeepDead;
-          wsync();
-        }
-      }
-      if (!ok && !redo && !fits_all) {
+      bool redo = false;  // one refill call site (another inlined copy spills)
+      if (!ok && !fits_all) {
         deep_relist_full(c, s, l, lane, n, d);
         return;
       }
-      if (!ok && !redo) {  // every item after all: the sealed prefix joins, the refill is redone
+      if (!ok) {  // every item after all: the sealed prefix joins, the refill is redone
 #if RSF_DEEP_PROF
         if (lane == 0) s_dprof[30] += 1ull;
 #endif
@@ -866,10 +782,6 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
     if (!unsafe) {
       err |= errq;
       q_store(c, s, l, q, lane, Q, true);
-      if (pulled) {  // the pulled items leave the sealed prefix (before the store reuses its end)
-        w_fill_sealed(c, s, l, q, d, lane, pull_m, pulled);
-        if (lane == 0) atomicAdd(s.deep_pulls, 1ull);
-      }
       uint32_t nb = 0;
       uint64_t bmin = ~0ull;
       const uint32_t cnt = t_lo + w_store_tail(c, s, l, q, d, lane, n, t_lo, rres, &nb, &bmin);

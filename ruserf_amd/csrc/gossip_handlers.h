@@ -112,7 +112,6 @@ struct GState {
   uint4* tseal;      // [n_loc][3]
   uint32_t* deep_ids;  // [n_loc * 3] members deferred to emit_deep_wave_kernel (two lists), or queues to prune
   uint32_t* deep_n;    // [kDeepLists] the lists' lengths (reset before each emission)
-  unsigned long long* deep_pulls;  // recent-mode refills that pulled sealed items in (w_pull_sealed)
 };
 // deferred-member lists: 0 small, 1 full depth, 2 tiny, 3 middle, 4 re-listed to the full depth
 constexpr uint32_t kDeepLists = 5;

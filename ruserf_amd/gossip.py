@@ -453,12 +453,6 @@ class GossipEngine:
                                                ptr(ln, C.c_uint16), ptr(ns, C.c_uint32)))
         return r, sq, tx, ln, ns
 
-    def deep_pulls(self):
-        """deferred emissions whose recent mode pulled sealed items into the head, since creation"""
-        v = np.zeros(1, dtype=np.uint64)
-        check(lib().rsf_gossip_deep_pulls(self._h, ptr(v, C.c_uint64)))
-        return int(v[0])
-
     def deep_class_stats(self):
         """members deferred to the whole-queue emission since creation, per LDS capacity
         class: (tiny, small, middle, full depth)"""
