@@ -3782,9 +3782,10 @@ static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
 #undef RSF_EMIT_DEEP
     RSF_HIP(hipGetLastError());
     RSF_DBG_SYNC(st, "emit_kernel (deep)");
-    // by capacity; the members the smaller classes re-list (list 4) go through the full depth
-    // last.  (Run beside each other on two streams, the classes were slower: a full-depth
-    // wave holds most of its CU's LDS, so the small classes' waves could not share the CU.)
+    // by capacity; the full depth last, with the members the smaller classes re-list (list 4)
+    // after its own in the same launch.  (Run beside each other on two streams, the classes
+    // were slower: a full-depth wave holds most of its CU's LDS, so the small classes' waves
+    // could not share the CU.)
     hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepTiny>), dim3(g->deep_blocks_tiny), dim3(kWave), 0, st, c, g->s,
                        g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 2u, g->d_counters + 55);
     hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepSmall>), dim3(g->deep_blocks), dim3(kWave), 0, st, c, g->s,
@@ -3793,8 +3794,6 @@ static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
                        g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 3u, g->d_counters + 55);
     hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepBig>), dim3(g->deep_blocks_big), dim3(kWave), 0, st, c, g->s,
                        g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 1u, g->d_counters + 55);
-    hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepBig>), dim3(g->deep_blocks_big), dim3(kWave), 0, st, c, g->s,
-                       g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 4u, g->d_counters + 55);
   } else if (c.qcap == kWave) {
     hipLaunchKernelGGL((emit_kernel<BKT, true>), egrid, eb, 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt,
                        g->stage_val, g->stage_dec, bk);

@@ -900,29 +900,34 @@ __global__ void __launch_bounds__(kWave) emit_deep_wave_kernel(GCfg c, GState s,
 #if RSF_DEEP_PROF
   s_dprof[lane] = 0;
 #endif
-  const uint32_t n_list = s.deep_n[list];
+  // list 1 (the full depth) also takes list 4 (the members the smaller classes re-listed),
+  // after its own: one launch, one tail
+  const uint32_t n_own = s.deep_n[list], n_re = list == 1 ? s.deep_n[4] : 0u, n_list = n_own + n_re;
   if (blockIdx.x == 0 && lane == 0 && n_list) {
     atomicAdd(total, (unsigned long long)n_list);
     // per class (the re-listed members count with the full depth)
-    atomicAdd(list == 3 ? total + 1 : total - kDeepClassOff + (list == 4 ? 1u : list), (unsigned long long)n_list);
+    atomicAdd(list == 3 ? total + 1 : total - kDeepClassOff + list, (unsigned long long)n_list);
   }
   for (uint32_t i = lane; i < CAP; i += kWave) d.st[i] = kDeepDead;
   wsync();
   const uint64_t last = c.n_loc * 3 - 1;
-  const uint32_t* const ids =
-      list == 1 ? s.deep_ids + last
-                : s.deep_ids + (list == 2 ? c.n_loc : list == 3 ? c.n_loc * 3 : list == 4 ? c.n_loc * 4 : 0ull);
+  const uint32_t* const ids = list == 1 ? s.deep_ids + last
+                                        : s.deep_ids + (list == 2 ? c.n_loc : list == 3 ? c.n_loc * 3 : 0ull);
+  const uint32_t* const re = s.deep_ids + c.n_loc * 4;
   const int64_t dir = list == 1 ? -1 : 1;
+  auto id_at = [&](uint32_t i) -> uint64_t {
+    if (i >= n_list) return ~0ull;
+    return i < n_own ? ids[dir * (int64_t)i] : re[i - n_own];
+  };
   // software pipeline over the wave's members: the next member's first round trip (deep_pre)
   // and the id after it are read while this member is worked on
   const uint32_t G = gridDim.x;
-  uint64_t l = blockIdx.x < n_list ? ids[dir * (int64_t)blockIdx.x] : ~0ull;
+  uint64_t l = id_at(blockIdx.x);
   DeepPre pre = deep_pre(c, s, l, lane, grp_key, slot);
-  uint64_t l_next = blockIdx.x + G < n_list ? ids[dir * (int64_t)(blockIdx.x + G)] : ~0ull;
+  uint64_t l_next = id_at(blockIdx.x + G);
   for (uint32_t it = blockIdx.x; it < n_list; it += G) {
     const DeepPre pre_next = deep_pre(c, s, l_next, lane, grp_key, slot);
-    const uint32_t nn = it + 2 * G;
-    const uint64_t l_after = nn < n_list ? ids[dir * (int64_t)nn] : ~0ull;
+    const uint64_t l_after = id_at(it + 2 * G);
     if (l < c.n_loc) deep_wave_member<BKT, CAP>(c, s, l, lane, pre, cnt_s, out_val, out_dec, bk, d);  // wave-uniform
     l = l_next;
     pre = pre_next;
