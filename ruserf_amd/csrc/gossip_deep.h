@@ -160,6 +160,9 @@ __device__ WRange w_range(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uin
 #ifndef RSF_DEEP_SELECT_REG
 #define RSF_DEEP_SELECT_REG 1
 #endif
+#ifndef RSF_DEEP_REG_CAP
+#define RSF_DEEP_REG_CAP kDeepSmall  // the refill's keys in registers up to this class (at 2 432: 256 VGPRs and 204 B of scratch)
+#endif
 template <uint32_t R>
 __device__ uint64_t w_select_kth_keys(const uint64_t (&kr)[R], uint32_t k, const WRange& rg) {
   const uint64_t var = rg.an ^ rg.orr;
@@ -194,8 +197,9 @@ __device__ uint64_t w_select_kth_keys(const uint64_t (&kr)[R], uint32_t k, const
 // the keys of LDS items lane, 64 + lane, ... in state `state` (~0 for the others) and their range
 template <uint32_t CAP, uint32_t R>
 __device__ __forceinline__ WRange w_keys(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint8_t state,
-                                         uint64_t (&kr)[R], uint32_t* vbits = nullptr) {
-  uint32_t cnt = 0, c0 = 0, vb = 0;
+                                         uint64_t (&kr)[R], uint64_t* vbits = nullptr) {
+  uint32_t cnt = 0, c0 = 0;
+  uint64_t vb = 0;
   uint64_t lo = ~0ull, hi = 0, an = ~0ull, orr = 0;
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
@@ -205,7 +209,7 @@ __device__ __forceinline__ WRange w_keys(const DeepWave<CAP>& d, uint32_t lane, 
     const uint64_t x = d.key[ii];
     const bool v = i < n && st == state;
     kr[r] = v ? x : ~0ull;
-    vb |= v ? 1u << r : 0u;
+    vb |= v ? 1ull << r : 0ull;
     cnt += v ? 1u : 0u;
     c0 += (v && (x >> 48) == 0) ? 1u : 0u;
     lo = v && x < lo ? x : lo;
@@ -337,12 +341,12 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
   uint32_t base = 0;
   uint64_t km = ~0ull;
   uint32_t lm = ~0u;
-  if constexpr (RSF_DEEP_SELECT_REG && CAP <= kDeepSmall) {
+  if constexpr (RSF_DEEP_SELECT_REG && CAP <= RSF_DEEP_REG_CAP) {
     // the keys read once into registers: range, select and gather from them
     constexpr uint32_t R = (CAP + kWave - 1) / kWave;
     uint64_t kr[R];
-    uint32_t vb;
-    static_assert(R <= 32, "validity bits");
+    uint64_t vb;
+    static_assert(R <= 64, "validity bits");
     const WRange rg = w_keys(d, lane, n, kDeepLive, kr, &vb);
     RSF_TH_T(20);
     uint64_t T = ~0ull;
@@ -361,7 +365,7 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
 #pragma unroll
     for (uint32_t r = 0; r < R; ++r) {
       const uint32_t i = r * kWave + lane;
-      const bool v = (vb >> r) & 1u;
+      const bool v = (vb >> r) & 1ull;
       const bool sel = v && kr[r] <= T;
       const uint64_t m = ballot(sel);
       if (sel) {
@@ -1178,39 +1182,101 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
     if (n <= keep) continue;  // (listed by the same count: cannot happen)
     RSF_CK(1);
     // the largest key kept
-    const uint32_t ks[3] = {keep, 0u, 0u};
+    const uint32_t kk[3] = {keep, 0u, 0u};
     const bool act[3] = {keep > 0, false, false};
     uint64_t sel[3];
-    lds_select3(keys, n, d, ks, act, an, orr, fuse, sel);
+    lds_select3(keys, n, d, kk, act, an, orr, fuse, sel);
     const uint64_t T = act[0] ? sel[0] : 0ull;
     const bool any = act[0];
     RSF_CK(2);
-    // pass 2: the tail's kept items (key <= T) compacted in place in index order, so the sealed
-    // prefix stays a prefix (its bound still holds) and the unsealed items follow it
+    // pass 2, the kept items (key <= T) only: the sealed prefix [0, m) keeps its kept items in
+    // its first ks places (the kept ones past ks move into the dropped places below ks; the
+    // prefix's order is free and its bound still holds), then the unsealed part's kept items
+    // follow from ks on in index order.  Only [ks, tc) is read and only what moves is written.
     const uint32_t m = min(s.tseal[l * 3 + q].x, tc);
-    uint32_t kept_sealed = 0;
-    for (uint32_t b = 0; b < tc; b += kChkU2 * kDeepThreads) {
+    uint32_t ks = 0, ku = 0;
+    {
+      uint32_t a0 = 0, a1 = 0;
+      for (uint32_t i = tid; i < tc; i += kDeepThreads)
+        if (any && keys[hn + i] <= T) (i < m ? a0 : a1)++;
+      a0 = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(a0), 63);
+      a1 = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(a1), 63);
+      __syncthreads();
+      if (lane == 0) {
+        d.wcnt[0][w] = a0;
+        d.wcnt[1][w] = a1;
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t v = 0; v < kDeepWaves; ++v) {
+        ks += d.wcnt[0][v];
+        ku += d.wcnt[1][v];
+      }
+    }
+    // the dropped places below ks, ascending, into LDS over the keys already read (u32 r sits
+    // in the u64 key slot r / 2, a place below ks that this or an earlier chunk has read)
+    uint32_t* const hole = reinterpret_cast<uint32_t*>(keys);
+    uint32_t nh_ = 0;
+    for (uint32_t c0 = 0; c0 < ks; c0 += kDeepThreads) {
+      const uint32_t i = c0 + tid;
+      const bool hl = i < ks && !(keys[hn + i] <= T);
+      const uint64_t hm = ballot(hl);
+      __syncthreads();  // every key of the chunk read; wcnt free
+      if (lane == 0) d.wcnt[0][w] = (uint32_t)__popcll(hm);
+      __syncthreads();
+      uint32_t before = 0, tot = 0;
+#pragma unroll
+      for (uint32_t v = 0; v < kDeepWaves; ++v) {
+        before += v < w ? d.wcnt[0][v] : 0u;
+        tot += d.wcnt[0][v];
+      }
+      if (hl) hole[nh_ + before + mbcnt(hm)] = i;
+      nh_ += tot;
+    }
+    __syncthreads();
+    // the kept items of [ks, m) into the holes (sources and holes disjoint: all loads in flight)
+    uint32_t moved = 0;
+    for (uint32_t b = ks; b < m; b += kChkU2 * kDeepThreads) {
       uint4 x[kChkU2];
+      uint64_t km[kChkU2];
 #pragma unroll
       for (uint32_t u = 0; u < kChkU2; ++u) {
         const uint32_t i = b + u * kDeepThreads + tid;
-        x[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
+        const bool mv = any && i < m && keys[hn + i] <= T;
+        x[u] = mv ? t[i] : make_uint4(0, 0, 0, 0);
+        km[u] = ballot(mv);
+        if (lane == 0) d.wcnt[u][w] = (uint32_t)__popcll(km[u]);
       }
+      __syncthreads();
+      uint32_t base = moved;
+#pragma unroll
+      for (uint32_t u = 0; u < kChkU2; ++u) {
+        uint32_t before = 0;
+#pragma unroll
+        for (uint32_t v = 0; v < kDeepWaves; ++v) before += v < w ? d.wcnt[u][v] : 0u;
+        if ((km[u] >> lane) & 1ull) t[hole[base + before + mbcnt(km[u])]] = x[u];
+#pragma unroll
+        for (uint32_t v = 0; v < kDeepWaves; ++v) base += d.wcnt[u][v];
+      }
+      moved = base;
+      __syncthreads();
+    }
+    // the unsealed part's kept items to ks + their rank (at or below where each is read; the
+    // places [ks, m) they may land on were read above)
+    uint32_t put = ks;
+    for (uint32_t b = m; b < tc; b += kChkU2 * kDeepThreads) {
+      uint4 x[kChkU2];
       uint64_t km[kChkU2];
 #pragma unroll
       for (uint32_t u = 0; u < kChkU2; ++u) {
         const uint32_t i = b + u * kDeepThreads + tid;
         const bool kp = any && i < tc && keys[hn + i] <= T;
+        x[u] = kp ? t[i] : make_uint4(0, 0, 0, 0);
         km[u] = ballot(kp);
         if (lane == 0) d.wcnt[u][w] = (uint32_t)__popcll(km[u]);
-        kept_sealed += kp && i < m ? 1u : 0u;
       }
-      __syncthreads();  // every thread has read its batch: the batch's positions may be rewritten
-      uint32_t base = d.nb, tot = 0;
-#pragma unroll
-      for (uint32_t u = 0; u < kChkU2; ++u)
-#pragma unroll
-        for (uint32_t v = 0; v < kDeepWaves; ++v) tot += d.wcnt[u][v];
+      __syncthreads();  // every thread has read its batch: the batch's places may be rewritten
+      uint32_t base = put;
 #pragma unroll
       for (uint32_t u = 0; u < kChkU2; ++u) {
         uint32_t before = 0;
@@ -1220,8 +1286,7 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
 #pragma unroll
         for (uint32_t v = 0; v < kDeepWaves; ++v) base += d.wcnt[u][v];
       }
-      __syncthreads();
-      if (tid == 0) d.nb += tot;
+      put = base;
       __syncthreads();
     }
     RSF_CK(3);
@@ -1232,14 +1297,8 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
       s.q_seq[hb + tid] = 0;
       s.q_txlen[hb + tid] = 0;
     }
-    kept_sealed = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(kept_sealed), 63);
-    __syncthreads();
-    if (lane == 0) d.wcnt[0][w] = kept_sealed;
-    __syncthreads();
     if (tid == 0) {
-      uint32_t ms = 0;
-      for (uint32_t v = 0; v < kDeepWaves; ++v) ms += d.wcnt[0][v];
-      const uint32_t cnt = d.nb;
+      const uint32_t ms = ks, cnt = ks + ku;
       const uint4 old = s.tsum[l * 3 + q], os = s.tseal[l * 3 + q];
       // the bounds stay valid lower bounds (only items left)
       s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, old.y, old.z, old.w) : kTSumEmpty;
