@@ -1189,94 +1189,32 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
     const uint64_t T = act[0] ? sel[0] : 0ull;
     const bool any = act[0];
     RSF_CK(2);
-    // pass 2, the kept items (key <= T) only: the sealed prefix [0, m) keeps its kept items in
-    // its first ks places (the kept ones past ks move into the dropped places below ks; the
-    // prefix's order is free and its bound still holds), then the unsealed part's kept items
-    // follow from ks on in index order.  Only [ks, tc) is read and only what moves is written.
+    // pass 2: the tail's kept items (key <= T) compacted in place in index order, so the sealed
+    // prefix stays a prefix (its bound still holds) and the unsealed items follow it
     const uint32_t m = min(s.tseal[l * 3 + q].x, tc);
-    uint32_t ks = 0, ku = 0;
-    {
-      uint32_t a0 = 0, a1 = 0;
-      for (uint32_t i = tid; i < tc; i += kDeepThreads)
-        if (any && keys[hn + i] <= T) (i < m ? a0 : a1)++;
-      a0 = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(a0), 63);
-      a1 = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(a1), 63);
-      __syncthreads();
-      if (lane == 0) {
-        d.wcnt[0][w] = a0;
-        d.wcnt[1][w] = a1;
-      }
-      __syncthreads();
-#pragma unroll
-      for (uint32_t v = 0; v < kDeepWaves; ++v) {
-        ks += d.wcnt[0][v];
-        ku += d.wcnt[1][v];
-      }
-    }
-    // the dropped places below ks, ascending, into LDS over the keys already read (u32 r sits
-    // in the u64 key slot r / 2, a place below ks that this or an earlier chunk has read)
-    uint32_t* const hole = reinterpret_cast<uint32_t*>(keys);
-    uint32_t nh_ = 0;
-    for (uint32_t c0 = 0; c0 < ks; c0 += kDeepThreads) {
-      const uint32_t i = c0 + tid;
-      const bool hl = i < ks && !(keys[hn + i] <= T);
-      const uint64_t hm = ballot(hl);
-      __syncthreads();  // every key of the chunk read; wcnt free
-      if (lane == 0) d.wcnt[0][w] = (uint32_t)__popcll(hm);
-      __syncthreads();
-      uint32_t before = 0, tot = 0;
-#pragma unroll
-      for (uint32_t v = 0; v < kDeepWaves; ++v) {
-        before += v < w ? d.wcnt[0][v] : 0u;
-        tot += d.wcnt[0][v];
-      }
-      if (hl) hole[nh_ + before + mbcnt(hm)] = i;
-      nh_ += tot;
-    }
-    __syncthreads();
-    // the kept items of [ks, m) into the holes (sources and holes disjoint: all loads in flight)
-    uint32_t moved = 0;
-    for (uint32_t b = ks; b < m; b += kChkU2 * kDeepThreads) {
+    uint32_t kept_sealed = 0;
+    for (uint32_t b = 0; b < tc; b += kChkU2 * kDeepThreads) {
       uint4 x[kChkU2];
-      uint64_t km[kChkU2];
 #pragma unroll
       for (uint32_t u = 0; u < kChkU2; ++u) {
         const uint32_t i = b + u * kDeepThreads + tid;
-        const bool mv = any && i < m && keys[hn + i] <= T;
-        x[u] = mv ? t[i] : make_uint4(0, 0, 0, 0);
-        km[u] = ballot(mv);
-        if (lane == 0) d.wcnt[u][w] = (uint32_t)__popcll(km[u]);
+        x[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
       }
-      __syncthreads();
-      uint32_t base = moved;
-#pragma unroll
-      for (uint32_t u = 0; u < kChkU2; ++u) {
-        uint32_t before = 0;
-#pragma unroll
-        for (uint32_t v = 0; v < kDeepWaves; ++v) before += v < w ? d.wcnt[u][v] : 0u;
-        if ((km[u] >> lane) & 1ull) t[hole[base + before + mbcnt(km[u])]] = x[u];
-#pragma unroll
-        for (uint32_t v = 0; v < kDeepWaves; ++v) base += d.wcnt[u][v];
-      }
-      moved = base;
-      __syncthreads();
-    }
-    // the unsealed part's kept items to ks + their rank (at or below where each is read; the
-    // places [ks, m) they may land on were read above)
-    uint32_t put = ks;
-    for (uint32_t b = m; b < tc; b += kChkU2 * kDeepThreads) {
-      uint4 x[kChkU2];
       uint64_t km[kChkU2];
 #pragma unroll
       for (uint32_t u = 0; u < kChkU2; ++u) {
         const uint32_t i = b + u * kDeepThreads + tid;
         const bool kp = any && i < tc && keys[hn + i] <= T;
-        x[u] = kp ? t[i] : make_uint4(0, 0, 0, 0);
         km[u] = ballot(kp);
         if (lane == 0) d.wcnt[u][w] = (uint32_t)__popcll(km[u]);
+        kept_sealed += kp && i < m ? 1u : 0u;
       }
-      __syncthreads();  // every thread has read its batch: the batch's places may be rewritten
-      uint32_t base = put;
+      __syncthreads();  // every thread has read its batch: the batch's positions may be rewritten
+      uint32_t base = d.nb, tot = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < kChkU2; ++u)
+#pragma unroll
+        for (uint32_t v = 0; v < kDeepWaves; ++v) tot += d.wcnt[u][v];
 #pragma unroll
       for (uint32_t u = 0; u < kChkU2; ++u) {
         uint32_t before = 0;
@@ -1286,7 +1224,8 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
 #pragma unroll
         for (uint32_t v = 0; v < kDeepWaves; ++v) base += d.wcnt[u][v];
       }
-      put = base;
+      __syncthreads();
+      if (tid == 0) d.nb += tot;
       __syncthreads();
     }
     RSF_CK(3);
@@ -1297,8 +1236,14 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
       s.q_seq[hb + tid] = 0;
       s.q_txlen[hb + tid] = 0;
     }
+    kept_sealed = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(kept_sealed), 63);
+    __syncthreads();
+    if (lane == 0) d.wcnt[0][w] = kept_sealed;
+    __syncthreads();
     if (tid == 0) {
-      const uint32_t ms = ks, cnt = ks + ku;
+      uint32_t ms = 0;
+      for (uint32_t v = 0; v < kDeepWaves; ++v) ms += d.wcnt[0][v];
+      const uint32_t cnt = d.nb;
       const uint4 old = s.tsum[l * 3 + q], os = s.tseal[l * 3 + q];
       // the bounds stay valid lower bounds (only items left)
       s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, old.y, old.z, old.w) : kTSumEmpty;
