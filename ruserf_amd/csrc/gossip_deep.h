@@ -160,9 +160,6 @@ __device__ WRange w_range(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uin
 #ifndef RSF_DEEP_SELECT_REG
 #define RSF_DEEP_SELECT_REG 1
 #endif
-#ifndef RSF_DEEP_REG_CAP
-#define RSF_DEEP_REG_CAP kDeepSmall  // the refill's keys in registers up to this class (at 2 432: 256 VGPRs and 204 B of scratch)
-#endif
 template <uint32_t R>
 __device__ uint64_t w_select_kth_keys(const uint64_t (&kr)[R], uint32_t k, const WRange& rg) {
   const uint64_t var = rg.an ^ rg.orr;
@@ -197,9 +194,8 @@ __device__ uint64_t w_select_kth_keys(const uint64_t (&kr)[R], uint32_t k, const
 // the keys of LDS items lane, 64 + lane, ... in state `state` (~0 for the others) and their range
 template <uint32_t CAP, uint32_t R>
 __device__ __forceinline__ WRange w_keys(const DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint8_t state,
-                                         uint64_t (&kr)[R], uint64_t* vbits = nullptr) {
-  uint32_t cnt = 0, c0 = 0;
-  uint64_t vb = 0;
+                                         uint64_t (&kr)[R], uint32_t* vbits = nullptr) {
+  uint32_t cnt = 0, c0 = 0, vb = 0;
   uint64_t lo = ~0ull, hi = 0, an = ~0ull, orr = 0;
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
@@ -209,7 +205,7 @@ __device__ __forceinline__ WRange w_keys(const DeepWave<CAP>& d, uint32_t lane, 
     const uint64_t x = d.key[ii];
     const bool v = i < n && st == state;
     kr[r] = v ? x : ~0ull;
-    vb |= v ? 1ull << r : 0ull;
+    vb |= v ? 1u << r : 0u;
     cnt += v ? 1u : 0u;
     c0 += (v && (x >> 48) == 0) ? 1u : 0u;
     lo = v && x < lo ? x : lo;
@@ -341,12 +337,14 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
   uint32_t base = 0;
   uint64_t km = ~0ull;
   uint32_t lm = ~0u;
-  if constexpr (RSF_DEEP_SELECT_REG && CAP <= RSF_DEEP_REG_CAP) {
+  // (keys in registers up to kDeepSmall: at kDeepMid, 38 keys per lane, the wave needs 256
+  // VGPRs and spills 204 B to scratch)
+  if constexpr (RSF_DEEP_SELECT_REG && CAP <= kDeepSmall) {
     // the keys read once into registers: range, select and gather from them
     constexpr uint32_t R = (CAP + kWave - 1) / kWave;
     uint64_t kr[R];
-    uint64_t vb;
-    static_assert(R <= 64, "validity bits");
+    uint32_t vb;
+    static_assert(R <= 32, "validity bits");
     const WRange rg = w_keys(d, lane, n, kDeepLive, kr, &vb);
     RSF_TH_T(20);
     uint64_t T = ~0ull;
@@ -365,7 +363,7 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
 #pragma unroll
     for (uint32_t r = 0; r < R; ++r) {
       const uint32_t i = r * kWave + lane;
-      const bool v = (vb >> r) & 1ull;
+      const bool v = (vb >> r) & 1u;
       const bool sel = v && kr[r] <= T;
       const uint64_t m = ballot(sel);
       if (sel) {
