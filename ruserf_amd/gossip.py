@@ -461,7 +461,7 @@ class GossipEngine:
         return out
 
     def checker_occupancy(self):
-        """The last check_queues tick's occupancy before its prune: {"bin": items per bin,
+        """The checker ticks' occupancy since the last reset, before their prunes: {"bin": items per bin,
         "hist": [3, bins] members per bin per queue (the last bin: everything above),
         "max": [3] the most items any member's queue held}"""
         b, nb = C.c_uint32(), C.c_uint32()

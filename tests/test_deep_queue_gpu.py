@@ -422,3 +422,49 @@ def test_deep_intent_only_prune_bit_exact(qcap, depth):
     assert total > 0
     g.close()
     L.orc_world_free(C.byref(w))
+
+
+def test_configs1_reference_regime_properties():
+    """BASELINE configs[1] (1M members, 4096 tracked subjects) in the bench's reference regime:
+    the intent queue 8704 deep, in-round staggered ticks to 4096 every 150 rounds, the ring
+    sized so nothing expires, 320 rounds (every member ticked at least once past 4096 items).
+    Too large for the oracle, so size-independent properties: nothing dropped between ticks
+    and nothing expired; no capacity error; the members that ticked in the last round hold
+    at most 4096 items and every queue at most its depth; each tick pruned to exactly the max
+    (pruned = queued - 4096 x members over it, from the checker's own counts); the items
+    queued stay under the retransmit limit; the hipCUB temporaries intact."""
+    n, s, rounds, period, mx = 1_000_000, 4096, 320, 150, 4096
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=64, queue_depth=(8704, 0, 0), gossip_limit=8 * 24,
+                         gossip_overhead=2, max_rumors=1 << 23, event_buffer_size=512, query_buffer_size=512,
+                         slot_k=1)
+    subj, acts, ml = W.intents_workload(n, s, rounds, rate=0.01, seed=0x5EED, prune_frac=0.1)
+    g = G.GossipEngine(cfg)
+    g.set_subjects(subj)
+    g.init_views(*W.initial_views(s))
+    g.set_checker(period, mx, 0, 128)
+    for t in range(rounds - 1):
+        g.round(t, ml[t], acts[t])
+    g.checker_stats(reset=True)
+    t = rounds - 1
+    g.round(t, ml[t], acts[t])
+    st = g.checker_stats()
+    occ = g.checker_occupancy()
+    ticked = int(occ["hist"][0].sum())
+    assert ticked == len(range(t % period, n, period))
+    over = int(st["warn"][0])  # every ticked member is over the warning depth (128)
+    assert over == ticked and int(st["pruned"][0]) > 0
+    # no ticked queue below the max: each was pruned to exactly the max
+    assert int(occ["hist"][0][:mx // occ["bin"]].sum()) == 0
+    assert int(st["pruned"][0]) == int(st["queued"][0]) - mx * ticked
+    ql = g.queue_lengths()[:, 0].astype(np.int64)
+    assert np.all(ql[t % period::period] <= mx)
+    assert int(ql.max()) <= cfg.depths()[0]
+    assert int(g.pruned().sum()) == 0 and int(g.expired().sum()) == 0
+    m = g.members()
+    assert np.all((m["err"] & ~np.uint32(G.E_QUEUE_PRUNE)) == 0) and np.all(m["err"] == 0)
+    rows = (0, 64)
+    r, sq, tx, ln = g.queues_rows(rows[0], rows[1], cfg.depths()[0])
+    limit = O.lib().orc_retransmit_limit(4, n)
+    assert np.all(tx[r != 0xFFFFFFFF] < limit)
+    assert all(g.cub_canaries())
+    g.close()
