@@ -429,10 +429,11 @@ def test_configs1_reference_regime_properties():
     the intent queue 8704 deep, in-round staggered ticks to 4096 every 150 rounds, the ring
     sized so nothing expires, 320 rounds (every member ticked at least once past 4096 items).
     Too large for the oracle, so size-independent properties: nothing dropped between ticks
-    and nothing expired; no capacity error; the members that ticked in the last round hold
-    at most 4096 items and every queue at most its depth; each tick pruned to exactly the max
-    (pruned = queued - 4096 x members over it, from the checker's own counts); the items
-    queued stay under the retransmit limit; the hipCUB temporaries intact."""
+    and nothing expired; no capacity error; each tick of the last round pruned to exactly the
+    max (pruned = queued - 4096 x members ticked, from the checker's own counts, none below
+    it); those members hold at most the max plus the round's re-queues, every queue at most
+    its depth; the items queued stay under the retransmit limit; the hipCUB temporaries
+    intact."""
     n, s, rounds, period, mx = 1_000_000, 4096, 320, 150, 4096
     cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=64, queue_depth=(8704, 0, 0), gossip_limit=8 * 24,
                          gossip_overhead=2, max_rumors=1 << 23, event_buffer_size=512, query_buffer_size=512,
@@ -456,8 +457,11 @@ def test_configs1_reference_regime_properties():
     # no ticked queue below the max: each was pruned to exactly the max
     assert int(occ["hist"][0][:mx // occ["bin"]].sum()) == 0
     assert int(st["pruned"][0]) == int(st["queued"][0]) - mx * ticked
+    # (read after the round's merge, whose re-queues the read applies first: at most one
+    # pending list of 128 entries on top of the pruned 4096)
     ql = g.queue_lengths()[:, 0].astype(np.int64)
-    assert np.all(ql[t % period::period] <= mx)
+    assert np.all(ql[t % period::period] <= mx + 128)
+    assert np.median(ql) > mx + 128  # the others are not
     assert int(ql.max()) <= cfg.depths()[0]
     assert int(g.pruned().sum()) == 0 and int(g.expired().sum()) == 0
     m = g.members()
