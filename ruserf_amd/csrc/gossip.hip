@@ -1312,7 +1312,7 @@ __global__ void __launch_bounds__(256) grp_index_kernel(const uint32_t* __restri
 // the wire instead of 80.
 constexpr uint32_t kMaxRuns = 8;
 #ifndef RSF_BUCKET_DEC_MODE
-#define RSF_BUCKET_DEC_MODE 2  // receive-side decorations: see bucket_index_kernel
+#define RSF_BUCKET_DEC_MODE 0  // receive-side decorations: see bucket_index_kernel
 #endif
 struct Buckets {
   const uint32_t* base;  // receive buffer (RUNS merge); emission writes through `send`
@@ -2971,11 +2971,14 @@ __global__ void bucket_bounds_kernel(const uint32_t* __restrict__ key_s, uint64_
 // unsorted bucket is flagged.  Grid-stride over a bounded grid: one atomic per block (an
 // atomic per 256 groups on one address serialised into ~0.25 ms at 6M groups).
 // RSF_BUCKET_DEC_MODE: where the receive side gets its records' decorations --
-//   0  bucket_dec_kernel rebuilds them into `decs` (one thread per record slot: 0.32 ms per
-//      round at 2M members, most of it launching and indexing 61M mostly idle threads)
+//   0  bucket_dec_kernel rebuilds them into `decs` (one thread per record slot).  The default:
+//      in the reference regime at 1M members (a rumor table of 2 x 8M ids, 64 MB of
+//      decorations) the merge's own lookups cost more (5.19 vs 5.31 ms per round, same box)
 //   1  this pass rebuilds them (one thread per group: measured slower still, 6.24 vs 6.11
-//      ms per round, the per-group loops diverge)
-//   2  the merge looks each one up from the rumor id it has just read (no pass, no array)
+//      ms per round at 2M, the per-group loops diverge)
+//   2  the merge looks each one up from the rumor id it has just read (no pass, no array;
+//      round 4's choice at 2M members with 64-slot queues, where the table is small: the
+//      decoration pass cost 0.32 ms there, most of it launching and indexing 61M threads)
 constexpr unsigned kBucketIndexBlocks = RSF_BUCKET_DEC_MODE == 1 ? 4096 : 1024;
 __global__ void __launch_bounds__(256) bucket_index_kernel(Buckets bk, uint64_t lo, uint64_t n_loc,
                                                            uint32_t* __restrict__ rstart, uint32_t* __restrict__ rend,
