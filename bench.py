@@ -10,10 +10,12 @@ line's `vivaldi` object with its own ms_per_step, roofline and cpu_baseline.
 
 One step = one pass of the hot path over one batch of synthetic input:
   gossip  : one gossip round over the shard's members -> metric "node-rounds/s".
-            Default 2M members per GPU: BASELINE's metric is quoted at 16M members
-            (configs[2], 16M over 8 GPUs); SURVEY §8(d) C3 weak-scales it at 2M/GPU
-            over 1/2/4/8 GPUs, so N=1 runs one 2M shard.  configs[1] (1M on one GPU)
-            is `--members 1000000`.
+            Default 1M members per GPU (BASELINE configs[1] at N=1) in the reference's
+            queue regime: the intent queue DEFAULT_QUEUE_DEPTH (8 704) deep, each member's
+            QueueChecker pruning it to 4 096 every 150 rounds on its own phase inside the
+            timed rounds.  configs[2]'s 2M-per-GPU shard is `--members 2000000`; the line
+            also carries labelled points at 2M (the same regime) and with bounded 64-slot
+            queues (model points).
   vivaldi : one Vivaldi round (every member probes one neighbour and runs
             CoordinateClient::update) (configs[4]) -> "Vivaldi updates/s"
 Multi-GPU: one process per GPU (torch.distributed over RCCL), members sharded
@@ -333,15 +335,16 @@ def main():
     ap.add_argument("--queue-depth", type=int, default=None,
                     help="gossip: intent queue depth above --queue-cap (<= 64): a register head plus an HBM tail, "
                          "pruned only by the QueueChecker every --check-every rounds (the reference's regime; default "
-                         "8192: max_queue_depth 4096 plus what 150 rounds add between ticks); 0: the bounded "
-                         "--queue-cap model")
+                         "8704: max_queue_depth 4096 plus what 150 rounds add between ticks, with margin); 0: the "
+                         "bounded --queue-cap model")
     ap.add_argument("--check-every", type=int, default=None,
                     help="gossip: a QueueChecker tick (prune to max_queue_depth 4096) every K rounds inside the round "
                          "loop, the timed window ending with one (default: 150 with --queue-depth, else none)")
     ap.add_argument("--no-extra-points", action="store_true",
                     help="gossip: skip the configs[1] points (1M members, 64- and 256-slot queues)")
     ap.add_argument("--settle", type=int, default=None,
-                    help="gossip: untimed rounds before warmup (default 12: queues saturated)")
+                    help="gossip: untimed rounds before warmup (default 330 in the queue regime: queues at their "
+                         "steady state past two checker ticks; 12 with bounded queues: saturated)")
     ap.add_argument("--no-vivaldi", action="store_true", help="gossip: skip the Vivaldi leg of the line")
     ap.add_argument("--refresh-every", type=int, default=1,
                     help="vivaldi, N>1: all-gather the coordinate table after every R-th round (C5: 1 and 8)")

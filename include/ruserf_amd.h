@@ -262,6 +262,8 @@ int rsf_vivaldi_true_rtt_ns(rsf_vivaldi* v, uint32_t a, uint32_t b, uint64_t* ns
 #define RSF_E_STAGE 8           /* a (sender, peer) message held more than cap_t records */
 #define RSF_E_QUEUE_PRUNE 16    /* a transmit-limited queue was full: a live item was dropped */
 #define RSF_E_DELIVERY_LOG 32   /* the delivery log of a member was full (deliveries happened, unlogged) */
+#define RSF_E_DEEP_INVARIANT 64 /* a deep queue broke an engine invariant (a tail past the checker's LDS
+                                   capacity): the QueueChecker could not prune it (never set in a valid run) */
 
 typedef struct rsf_gossip_cfg {
   uint64_t n_members;          /* N (global) */
@@ -639,6 +641,14 @@ int rsf_gossip_deep_stats(rsf_gossip* g, uint64_t* slow_total, uint64_t* slow_si
  * [0] the smallest class, [1] the small one, [2] the middle one, [3] the full depth (members the
  * smaller classes re-list to it count twice).  Synchronises. */
 int rsf_gossip_deep_class_stats(rsf_gossip* g, uint64_t* out4);
+/* the full-depth class's members since creation: the items their queues held in its LDS (sum
+ * and the largest; head, tail and pending list).  Diagnostics of the deferred path (engine
+ * state, no reference counterpart).  Synchronises. */
+int rsf_gossip_deep_full_items(rsf_gossip* g, uint64_t* sum, uint64_t* max);
+/* queue q's HBM tail per shard member (host, [n_loc] each, either may be NULL): its item count
+ * and the length of its sealed prefix, as the engine holds them (the pending
+ * lists are NOT applied first).  Engine state, no reference counterpart.  Synchronises. */
+int rsf_gossip_dump_tails(rsf_gossip* g, uint32_t q, uint32_t* count, uint32_t* sealed);
 /* items queued per shard member and queue (host, [n_loc][3]: intent, query, event; head + tail),
  * after applying the pending lists (the QueueChecker's num_queued per node).  Synchronises. */
 int rsf_gossip_queue_lengths(rsf_gossip* g, uint32_t* out);

@@ -663,7 +663,7 @@ int orc_world_init(orc_world* w, const orc_world_cfg* c) {
       A(q_next_seq, n * 3) || A(eb_ltime, n * c->ebuf) || A(eb_cnt, n * c->ebuf) ||
       A(eb_keys, n * c->ebuf * c->slot_k) || A(qb_ltime, n * c->qbuf) || A(qb_cnt, n * c->qbuf) ||
       A(qb_ids, n * c->qbuf * c->slot_k) || A(rumors, 2 * (size_t)c->cap_rumors) || A(v_time, n * s) ||
-      A(q_pruned, n) || A(q_expired, n) || A(q_hwm, n * 3)) {
+      A(q_pruned, n) || A(q_expired, n) || A(q_hwm, n * 3) || A(q_hole, n * 3)) {
     orc_world_free(w);
     return -1;
   }
@@ -703,7 +703,7 @@ void orc_world_free(orc_world* w) {
                   w->refute_ltime, w->v_ltime, w->v_status, w->v_kind, w->q_rumor, w->q_seq,
                   w->q_tx, w->q_len, w->q_next_seq, w->eb_ltime, w->eb_cnt, w->eb_keys,
                   w->qb_ltime, w->qb_cnt, w->qb_ids, w->rumors, w->v_time, w->q_pruned, w->q_expired,
-                  w->dlog, w->dcnt, w->snap_bits, w->snap_sn, w->q_hwm, w->act_status};
+                  w->dlog, w->dcnt, w->snap_bits, w->snap_sn, w->q_hwm, w->act_status, w->q_hole};
   for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) free(ptrs[i]);
   memset(w, 0, sizeof(*w));
 }
@@ -921,15 +921,18 @@ static inline uint64_t tlq_key(uint16_t tx, uint16_t len, uint32_t seq) {
 void orc_queue_insert(orc_world* w, uint32_t m, uint32_t q, uint32_t rumor) {
   size_t base = ((size_t)m * 3 + q) * w->qcap;
   uint32_t* hwm = &w->q_hwm[(size_t)m * 3 + q];
+  uint32_t* hole = &w->q_hole[(size_t)m * 3 + q];
   uint32_t seq = w->q_next_seq[(size_t)m * 3 + q]++;
   uint16_t len = w->rumors[orc_rumor_index(w, rumor)].msg_len;
   uint32_t slot = EMPTY_RUMOR;
-  for (uint32_t i = 0; i < *hwm; ++i)
+  /* the first free slot (no slot below *hole is free) */
+  for (uint32_t i = *hole; i < *hwm; ++i)
     if (w->q_rumor[base + i] == EMPTY_RUMOR) {
       slot = i;
       break;
     }
   if (slot == EMPTY_RUMOR && *hwm < w->qd[q]) slot = (*hwm)++;
+  if (slot != EMPTY_RUMOR) *hole = slot + 1;
   if (slot == EMPTY_RUMOR) { /* full: prune the last item in send order */
     w->q_pruned[m]++;
     w->err[m] |= ORC_E_QUEUE_PRUNE;
@@ -975,6 +978,7 @@ uint32_t orc_queue_expire(orc_world* w, uint32_t m, uint32_t q) {
     w->q_seq[base + i] = 0;
     w->q_tx[base + i] = 0;
     w->q_len[base + i] = 0;
+    if (i < w->q_hole[(size_t)m * 3 + q]) w->q_hole[(size_t)m * 3 + q] = i;
     cnt++;
   }
   return cnt;
@@ -987,34 +991,48 @@ uint32_t orc_queue_get_broadcasts(orc_world* w, uint32_t m, uint32_t q, uint32_t
                                   uint32_t* out, uint32_t max_out, uint32_t* bytes_used) {
   size_t base = ((size_t)m * 3 + q) * w->qcap;
   const uint32_t hwm = w->q_hwm[(size_t)m * 3 + q];
-  uint8_t picked[ORC_MAX_QCAP]; /* per slot: taken by this call */
-  memset(picked, 0, hwm);
   int64_t used = 0;
   uint32_t cnt = 0;
+  /* The live items' keys are gathered once (the oracle's speed only); each pick is then the
+   * smallest key among the unpicked items that fit the budget left (keys are distinct: seq is
+   * unique in a queue).  A picked item's key becomes UINT64_MAX. */
+  uint64_t kk[ORC_MAX_QCAP];
+  uint32_t ki[ORC_MAX_QCAP];
+  uint32_t picked[ORC_MAX_QCAP];
+  uint32_t kn = 0, np = 0;
+  for (uint32_t i = 0; i < hwm; ++i) {
+    if (w->q_rumor[base + i] == EMPTY_RUMOR) continue;
+    kk[kn] = tlq_key(w->q_tx[base + i], w->q_len[base + i], w->q_seq[base + i]);
+    ki[kn++] = i;
+  }
   for (;;) {
     int64_t free_b = (int64_t)limit - used - (int64_t)w->overhead;
     if (free_b <= 0) break;
     uint32_t best = EMPTY_RUMOR;
     uint64_t kbest = UINT64_MAX;
-    for (uint32_t i = 0; i < hwm; ++i) {
-      if (w->q_rumor[base + i] == EMPTY_RUMOR || picked[i]) continue;
-      if ((int64_t)w->q_len[base + i] > free_b) continue;
-      uint64_t k = tlq_key(w->q_tx[base + i], w->q_len[base + i], w->q_seq[base + i]);
-      if (k < kbest) {
-        kbest = k;
-        best = i;
-      }
+    for (uint32_t j = 0; j < kn; ++j) {
+      if (kk[j] >= kbest) continue;
+      /* the key's length field: 0xFFFF - len */
+      if ((int64_t)(0xFFFFu - (uint32_t)((kk[j] >> 32) & 0xFFFFu)) > free_b) continue;
+      kbest = kk[j];
+      best = j;
     }
     if (best == EMPTY_RUMOR) break;
-    if (cnt < max_out) out[cnt] = w->q_rumor[base + best];
+    const uint32_t i = ki[best];
+    kk[best] = UINT64_MAX;
+    if (cnt < max_out) out[cnt] = w->q_rumor[base + i];
     cnt++;
-    used += (int64_t)w->overhead + w->q_len[base + best];
-    picked[best] = 1;
+    used += (int64_t)w->overhead + w->q_len[base + i];
+    picked[np++] = i;
   }
-  for (uint32_t i = 0; i < hwm; ++i) {
-    if (!picked[i]) continue;
-    if ((uint32_t)w->q_tx[base + i] + 1 >= w->tx_limit) w->q_rumor[base + i] = EMPTY_RUMOR;
-    else w->q_tx[base + i]++;
+  for (uint32_t j = 0; j < np; ++j) {
+    const uint32_t i = picked[j];
+    if ((uint32_t)w->q_tx[base + i] + 1 >= w->tx_limit) {
+      w->q_rumor[base + i] = EMPTY_RUMOR;
+      if (i < w->q_hole[(size_t)m * 3 + q]) w->q_hole[(size_t)m * 3 + q] = i;
+    } else {
+      w->q_tx[base + i]++;
+    }
   }
   *bytes_used = (uint32_t)used;
   return cnt;
@@ -1073,6 +1091,7 @@ void orc_check_queues_phase(orc_world* w, uint32_t max_queue_depth, uint32_t min
       for (uint32_t i = 0; i < hwm; ++i) {
         if (w->q_rumor[base + i] == EMPTY_RUMOR) continue;
         if (mx && tlq_key(w->q_tx[base + i], w->q_len[base + i], w->q_seq[base + i]) <= T) continue;
+        if (i < w->q_hole[(size_t)m * 3 + q]) w->q_hole[(size_t)m * 3 + q] = i;
         w->q_rumor[base + i] = EMPTY_RUMOR;
         w->q_seq[base + i] = 0;
         w->q_tx[base + i] = 0;
@@ -2244,7 +2263,7 @@ int orc_world_restart(orc_world* w, uint32_t m, const uint8_t* file, uint64_t le
     w->q_tx[q] = 0;
     w->q_len[q] = 0;
   }
-  for (uint32_t q = 0; q < 3; ++q) w->q_next_seq[(size_t)m * 3 + q] = w->q_hwm[(size_t)m * 3 + q] = 0;
+  for (uint32_t q = 0; q < 3; ++q) w->q_next_seq[(size_t)m * 3 + q] = w->q_hwm[(size_t)m * 3 + q] = w->q_hole[(size_t)m * 3 + q] = 0;
   memset(w->eb_ltime + (size_t)m * w->ebuf, 0, (size_t)w->ebuf * 8);
   memset(w->eb_cnt + (size_t)m * w->ebuf, 0, (size_t)w->ebuf * 4);
   memset(w->eb_keys + (size_t)m * w->ebuf * w->slot_k, 0, (size_t)w->ebuf * w->slot_k * 8);

@@ -272,6 +272,9 @@ typedef struct {
    * chk_stats accumulates its counts (orc_check_queues' layout).  chk_period 0: off. */
   uint32_t chk_period, chk_max, chk_min, chk_warn;
   uint64_t chk_stats[9];
+  /* [n][3] no slot below it is free (a scan-start hint for orc_queue_insert's first-free-slot
+   * search; every writer that frees a slot lowers it).  The oracle's speed only. */
+  uint32_t* q_hole;
 } orc_world;
 
 typedef struct {

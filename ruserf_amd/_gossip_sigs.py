@@ -65,6 +65,8 @@ def declare(L):
     sig("rsf_gossip_push_pull_device", [VP, VP, C.c_uint64, C.c_uint32])
     sig("rsf_gossip_action_status", [VP, PI32, C.c_uint32])
     sig("rsf_gossip_deep_class_stats", [VP, P64])
+    sig("rsf_gossip_deep_full_items", [VP, P64, P64])
+    sig("rsf_gossip_dump_tails", [VP, C.c_uint32, P32, P32])
     sig("rsf_gossip_queue_lengths", [VP, P32])
     sig("rsf_gossip_dump_queues_rows", [VP, C.c_uint64, C.c_uint64, C.c_uint32, P32, P32, P16, P16, P32])
     sig("rsf_gossip_checker_occupancy", [VP, P32, P32, P32, P32])

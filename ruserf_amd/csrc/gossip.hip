@@ -438,12 +438,6 @@ __device__ __forceinline__ void q_rerank(const GCfg& c, QRegs& Q, uint32_t lane,
 #ifndef RSF_EMIT_NT
 #define RSF_EMIT_NT 0  // emit: records written non-temporally
 #endif
-#ifndef RSF_EMIT_MULTI
-#define RSF_EMIT_MULTI 1  // emit: all peers' picks per queue in one pass (q_pick_peers); 0: per peer (q_get_broadcasts_lazy)
-#endif
-#ifndef RSF_EMIT_LAZY
-#define RSF_EMIT_LAZY 1  // emit: one deferred re-rank per queue per emission (q_get_broadcasts_lazy)
-#endif
 // DEEP (a tail behind the head, its key / length lower bounds tmin / tminlen): the call is
 // exact only if every pick's key is below tmin and every stop with budget left is one no tail
 // item could fit; otherwise *unsafe is set and the caller abandons the emission (the member
@@ -539,86 +533,11 @@ __device__ __forceinline__ int64_t q_get_broadcasts(const GCfg& c, QRegs& Q, uin
   return used;
 }
 
-// get_broadcasts with the re-rank deferred.  Between the fanout peers' calls of one
-// emission a queue is left in VIRTUAL order: the items picked so far (`cons`, all from the
-// queue's lowest transmit class t0) are bumped or retired in place but not moved.  The
-// actual send order is then [unpicked items of class t0, in lane order] followed by the
-// merge of everything else, so a call whose picks all come from that leading run -- the
-// prefix that fits, then later shorter items, as long as the next candidate is still of
-// class t0 -- picks exactly what the reference would.  When the next candidate could lie
-// past the run (its order there is not known without the merge), the deferred re-rank is
-// done and the exact q_get_broadcasts runs.  The caller materialises (q_materialize) after
-// the last peer.  Three re-ranks per emission become one in the common case.
-template <bool PERMUTE_DEC>
-__device__ __forceinline__ void q_materialize(const GCfg& c, QRegs& Q, uint32_t lane, uint64_t& cons, QLds& row) {
-  if (!cons) return;
-  const uint64_t live_m = ballot(lane < c.qcap && Q.r != kEmpty);
-  q_rerank<PERMUTE_DEC>(c, Q, lane, cons & live_m, live_m & ~cons, row);
-  cons = 0;
-}
-template <bool PERMUTE_DEC>
-__device__ __forceinline__ int64_t q_get_broadcasts_lazy(const GCfg& c, QRegs& Q, uint32_t lane, int64_t limit,
-                                                         uint32_t* stage_val, uint32_t* stage_dec, uint64_t out_base,
-                                                         uint32_t& nrec, uint32_t& err, bool& dirty, QLds& row,
-                                                         uint64_t& cons, uint32_t& t0) {
-  const bool valid = lane < c.qcap;
-  const uint64_t live_m = ballot(valid && Q.r != kEmpty);
-  if (!live_m) return 0;
-  if (!cons) t0 = shfl_u32(Q.tl, 0) & 0xFFFF;  // materialised: lane 0 holds the smallest key
-  const uint32_t len = Q.tl >> 16;
-  const uint64_t a_m = ballot(valid && Q.r != kEmpty && (Q.tl & 0xFFFF) == t0) & ~cons;
-  const bool in_a = lane_bit(a_m);
-  const uint32_t incl = wave_inclusive_sum_u32(in_a ? c.overhead + len : 0u);
-  uint64_t pick_m = limit >= 0 ? (ballot((int64_t)incl <= limit) & a_m) : 0ull;
-  int64_t used = pick_m ? (int64_t)shfl_u32(incl, 63 - __clzll((long long)pick_m)) : 0;
-  bool exact = false;
-  for (;;) {
-    const int64_t free_b = limit - used - (int64_t)c.overhead;
-    if (free_b <= 0) break;
-    const uint64_t fit = ballot((int64_t)len <= free_b) & live_m & ~pick_m;
-    if (!fit) break;
-    const uint64_t cand = fit & a_m;
-    if (!cand) {  // the next candidate lies past the class-t0 run
-      exact = true;
-      break;
-    }
-    const int win = __ffsll((long long)cand) - 1;
-    pick_m |= 1ull << win;
-    used += (int64_t)c.overhead + shfl_u32(len, win);
-  }
-  if (exact) {
-    q_materialize<PERMUTE_DEC>(c, Q, lane, cons, row);
-    return q_get_broadcasts<PERMUTE_DEC>(c, Q, lane, limit, stage_val, stage_dec, out_base, nrec, err, dirty, row);
-  }
-  if (!pick_m) return used;
-  const bool picked = lane_bit(pick_m);
-  const uint32_t npick = (uint32_t)__popcll(pick_m);
-  const uint32_t rank = mbcnt(pick_m);
-  if (picked && nrec + rank < c.cap_t && stage_val) {
-#if RSF_EMIT_NT
-    __builtin_nontemporal_store(Q.r, stage_val + out_base + nrec + rank);
-    if (stage_dec) __builtin_nontemporal_store(Q.dec, stage_dec + out_base + nrec + rank);
-#else
-    stage_val[out_base + nrec + rank] = Q.r;
-    if (stage_dec) stage_dec[out_base + nrec + rank] = Q.dec;
-#endif
-  }
-  if (nrec + npick > c.cap_t) err |= kErrStage;
-  nrec += npick;
-  dirty = true;
-  const bool retire = picked && (Q.tl & 0xFFFF) + 1 >= c.tx_limit;
-  if (retire) Q.r = kEmpty;
-  else if (picked) Q.tl = Q.tl + 1;
-  cons |= pick_m;
-  return used;
-}
-
 // All the fanout peers' get_broadcasts calls on ONE queue in one pass (queue-major emission).
 // A peer's picks from queue q depend only on q's state after the earlier peers' picks from q
 // and on what the peer's earlier queues left of its byte budget, so running queue 0 for every
 // peer, then queue 1, then queue 2 picks exactly what the reference's peer-major
-// broadcast_messages loop picks.  Within a queue this is q_get_broadcasts_lazy's rule for
-// every peer: while all picks come from the queue's lowest transmit class t0 (the leading run
+// broadcast_messages loop picks.  Within a queue, for every peer: while all picks come from the queue's lowest transmit class t0 (the leading run
 // of the sorted queue), the send order is [unpicked class-t0 items in lane order] followed by
 // everything else, so ONE prefix sum of the run's costs serves every peer (each peer's prefix
 // is a further stretch of the same sums), the picked items are bumped in place and the re-rank
@@ -1148,14 +1067,20 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
     const int32_t e = x.act == RSF_ACT_USER_EVENT
                           ? user_event_size_check(c.max_ue, s.eclock[l], x.name_len, x.payload_len)
                           : query_size_check(c.query_limit, s.qclock[l], x.name_len, x.payload_len);
-    status[a] = e;
-    if (e) return;
-  } else {
-    status[a] = RSF_OK;
+    if (e) {
+      status[a] = e;
+      return;
+    }
   }
   MRegs r;
   load_regs(s, l, r);
-  if (RSF_BAD2(13, (x.act == RSF_ACT_JOIN_SELF || x.act == RSF_ACT_LEAVE_SELF) && (uint32_t)r.subj >= c.S, r.subj)) return;
+  // join / leave of the member itself: only a tracked subject has a view entry about itself
+  // (rsf_gossip_round_begin rejects the call on the host; this keeps the status truthful)
+  if ((x.act == RSF_ACT_JOIN_SELF || x.act == RSF_ACT_LEAVE_SELF) && (uint32_t)r.subj >= c.S) {
+    status[a] = RSF_ERR_ARG;
+    return;
+  }
+  status[a] = RSF_OK;
   uint64_t ref = 0;
   switch (x.act) {
     case RSF_ACT_JOIN_SELF:
@@ -1360,16 +1285,10 @@ __device__ unsigned long long g_eprof2[512 * 8];  // q_pick_peers' own split
 // word per lane (`head`): lanes 1, 2 the query / event queue heads, kEhPend the pending
 // re-queue counts, kEhSeq + q the queues' next insertion seqs, kEhPruned, kEhErr
 enum : uint32_t { kEhPend = 3, kEhSeq = 4, kEhPruned = 7, kEhErr = 8 };
-#ifndef RSF_EMIT_SPEC_PEND
-#define RSF_EMIT_SPEC_PEND 0  // K > 0: the first K pending entries loaded in the first round trip, unconditionally (K = 64 measured +0.15 ms at 2M: the extra bytes cost more than the round trip)
-#endif
 struct EmitIn {
   QRegs Q0;
   uint32_t head, gk, gs;
   uint4 ts;  // deep queues: lane q < 3 holds queue q's tail summary (tsum)
-#if RSF_EMIT_SPEC_PEND
-  GState::PendE p0;  // pending entry `lane` (valid when lane < the member's count)
-#endif
 };
 template <uint32_t DEEP = 0>
 __device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const uint32_t* __restrict__ grp_key,
@@ -1391,12 +1310,6 @@ __device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const 
   if (hp) e.head = *hp;
   e.gk = lane < c.fanout ? grp_key[l * c.fanout + lane] : kSentinel;
   e.gs = lane < c.fanout ? slot[l * c.fanout + lane] : 0u;
-#if RSF_EMIT_SPEC_PEND
-  // the pending list's first half does not depend on the count: issued with the first round
-  // trip instead of a second one after it (entries past the count are ignored)
-  e.p0 = GState::PendE{0u, 0u, 0u};
-  if (lane < RSF_EMIT_SPEC_PEND) e.p0 = s.p_ent[l * kPend + lane];
-#endif
 }
 // buckets: lanes < np write their group's receiver key (and, when nothing will be emitted,
 // its zero count) into the destination bucket -- the bucket headers come from emission
@@ -1463,18 +1376,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   uint32_t err = 0;
   // the pending re-queues (merge_kernel's and the originations' since the last emission)
   PendRegs pr;
-#if RSF_EMIT_SPEC_PEND
-  if (npend <= RSF_EMIT_SPEC_PEND) {
-    pr.rid[0] = lane < npend ? e.p0.rid : 0u;
-    pr.dec[0] = lane < npend ? e.p0.dec : 0u;
-    pr.lq[0] = lane < npend ? e.p0.lq : 0u;
-    pr.rid[1] = pr.dec[1] = pr.lq[1] = 0;
-  } else {
-    pend_load(s, l, lane, npend, pr);
-  }
-#else
   pend_load(s, l, lane, npend, pr);
-#endif
   // buckets: each peer's destination shard and that bucket's first group (same round trip)
   uint32_t wdst = 0;  // (bucket mode: the slot word holds the shard and the bucket place)
   if (BKT && lane < np) {
@@ -1519,7 +1421,6 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
 #if RSF_EMIT_PROF
   EPROF_ADD(2, t1b, t2);
 #endif
-#if RSF_EMIT_MULTI
   {
     // queue-major: every peer's picks from the intent queue, then the query queue, then the
     // event queue (q_pick_peers).  Lane j < np holds peer j's group: where its records go
@@ -1553,11 +1454,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
 #endif
     if (DEEP) {
       // a tail's bounds (~0: empty) as of after the spills above
-#if RSF_DIAG_NO_DEEP_CHECK  // (timing diagnostic only: picks not checked against the tails)
-#define RSF_TB(q) ~0ull, ~0u
-#else
 #define RSF_TB(q) (sp##q.cnt ? sp##q.minkey : ~0ull), (sp##q.cnt ? sp##q.minlen : ~0u)
-#endif
       if (ne0 && !unsafe) {
         if (D0) q_pick_peers<true, true>(c, Q0, lane, np, used_v, nrec_v, off, ov, od, err, d0, row, ep, RSF_TB(0), &unsafe);
         else q_pick_peers<true>(c, Q0, lane, np, used_v, nrec_v, off, ov, od, err, d0, row, ep);
@@ -1600,59 +1497,6 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   }
   EPROF_T(t2b);
   EPROF_ADD(3, t2, t2b);
-#else
-  static_assert(!DEEP, "deep queues need the queue-major emission (RSF_EMIT_MULTI)");
-#if RSF_EMIT_LAZY
-  uint64_t cons0 = 0, cons1 = 0, cons2 = 0;  // picks whose re-rank is deferred (q_get_broadcasts_lazy)
-  uint32_t t00 = 0, t01 = 0, t02 = 0;
-#endif
-  for (uint32_t j = 0; j < np; ++j) {
-    const uint32_t gslot = shfl_u32(e.gs, j);
-    if (RSF_BAD2(7, !BKT && gslot >= c.n_loc * c.fanout, gslot)) return;
-    uint64_t out_base = (uint64_t)gslot * c.cap_t;
-    uint32_t* ov = out_val;
-    uint32_t* od = out_dec;
-    uint32_t* oc = cnt_s + gslot;
-    if (BKT) {  // the group's place in its destination's bucket
-      const uint32_t w = gslot >> kBktWShift, idx = gslot & kBktIdxMask;
-      uint32_t* b = bk.send + (uint64_t)w * bk.stride_u32;
-      if (idx < bk.gcap) {
-        ov = b + bk.vals_off;
-        od = nullptr;  // decorations are rebuilt on the receive side
-        oc = b + bk.cnt_off + idx;
-        out_base = (uint64_t)idx * c.cap_t;
-      } else {
-        ov = od = oc = nullptr;  // over the bucket capacity: flagged by the bounds kernel
-      }
-    }
-    uint32_t nrec = 0;
-    int64_t used = 0;
-#if RSF_EMIT_LAZY
-    // (a queue that was empty before the pending list and got nothing from it stays empty)
-    if (ne0)
-      used += q_get_broadcasts_lazy<true>(c, Q0, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d0, row,
-                                          cons0, t00);
-    if (ne1)
-      used += q_get_broadcasts_lazy<false>(c, Q1, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d1, row,
-                                           cons1, t01);
-    if (ne2)
-      used += q_get_broadcasts_lazy<false>(c, Q2, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d2, row,
-                                           cons2, t02);
-#else
-    used += q_get_broadcasts<true>(c, Q0, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d0, row);
-    used += q_get_broadcasts<false>(c, Q1, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d1, row);
-    used += q_get_broadcasts<false>(c, Q2, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d2, row);
-#endif
-    if (lane == 0 && oc && (BKT || nrec)) *oc = min(nrec, c.cap_t);  // buckets: every group's count
-  }
-  EPROF_T(t2b);
-  EPROF_ADD(3, t2, t2b);
-#if RSF_EMIT_LAZY
-  q_materialize<true>(c, Q0, lane, cons0, row);
-  q_materialize<false>(c, Q1, lane, cons1, row);
-  q_materialize<false>(c, Q2, lane, cons2, row);
-#endif
-#endif  // RSF_EMIT_MULTI
   EPROF_T(t3);
   EPROF_ADD(4, t2b, t3);
   if (d0) q_store(c, s, l, 0, lane, Q0, true);
@@ -1765,7 +1609,6 @@ __device__ __forceinline__ void emit_run4(const GCfg& c, const GState& s, const 
       err |= kErrQueue;
     }
   }
-#if RSF_EMIT_MULTI
   {
     // queue-major, as emit_run: every peer's picks from each queue in one pass (q4_pick_peers)
     uint64_t off = ~0ull;
@@ -1794,33 +1637,6 @@ __device__ __forceinline__ void emit_run4(const GCfg& c, const GState& s, const 
     if (ne2) q4_pick_peers<false>(c, Q2, lane, np, used_v, nrec_v, off, ov, od, err, d2, row);
     if (oc && (BKT || nrec_v)) *oc = min(nrec_v, c.cap_t);
   }
-#else
-  for (uint32_t j = 0; j < np; ++j) {
-    const uint32_t gslot = shfl_u32(gs, j);
-    uint64_t out_base = (uint64_t)gslot * c.cap_t;
-    uint32_t* ov = out_val;
-    uint32_t* od = out_dec;
-    uint32_t* oc = cnt_s + gslot;
-    if (BKT) {
-      const uint32_t w = gslot >> kBktWShift, idx = gslot & kBktIdxMask;
-      uint32_t* b = bk.send + (uint64_t)w * bk.stride_u32;
-      if (idx < bk.gcap) {
-        ov = b + bk.vals_off;
-        od = nullptr;
-        oc = b + bk.cnt_off + idx;
-        out_base = (uint64_t)idx * c.cap_t;
-      } else {
-        ov = od = oc = nullptr;
-      }
-    }
-    uint32_t nrec = 0;
-    int64_t used = 0;
-    used += q4_get_broadcasts<true>(c, Q0, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d0, row);
-    used += q4_get_broadcasts<false>(c, Q1, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d1, row);
-    used += q4_get_broadcasts<false>(c, Q2, lane, (int64_t)c.limit - used, ov, od, out_base, nrec, err, d2, row);
-    if (lane == 0 && oc && (BKT || nrec)) *oc = min(nrec, c.cap_t);
-  }
-#endif
   if (d0) q4_store(c, s, l, 0, lane, Q0);
   if (d1) q4_store(c, s, l, 1, lane, Q1);
   if (d2) q4_store(c, s, l, 2, lane, Q2);
@@ -1981,16 +1797,9 @@ __global__ void __launch_bounds__(256) grp_expand_kernel(const uint32_t* __restr
 //   * digest contributions (member events, deliveries), refutations and
 //     re-queues are then applied serially in record order.
 // User events / queries (dedup rings in HBM) run serially in lane 0.
-#ifndef RSF_MERGE_NT
-#define RSF_MERGE_NT 0  // merge: records (ids, decorations, group counts) read non-temporally
-#endif
 // the merge's record streams are read once per round
 __device__ __forceinline__ uint32_t rec_ld(const uint32_t* p) {
-#if RSF_MERGE_NT
-  return __builtin_nontemporal_load(p);
-#else
   return *p;
-#endif
 }
 #ifndef RSF_MERGE_WAVES
 #define RSF_MERGE_WAVES 7  // min waves/SIMD for merge_kernel (register cap; 7 measured fastest with 8 receivers per wave, 8 before)
@@ -3068,6 +2877,7 @@ struct rsf_gossip {
   // rumor ring: cursor (next free slot) and generation; the round's block is slots
   // [round_slot, round_slot + round_need), its ids round_base + i (gen << rbits | slot)
   uint32_t n_rumors = 0, max_rumors = 0, gen = 0;
+  std::vector<uint32_t> subj_sorted;  // the tracked subjects' members, sorted (action checks)
   uint32_t round_slot = 0, round_base = 0, round_abase = 0, round_need = 0;
   // per-round device lists
   rsf_ml_event* d_ml = nullptr;
@@ -3511,6 +3321,8 @@ int rsf_gossip_set_subjects(rsf_gossip* g, const uint32_t* subj_member) {
     if (seen[m]++) return gerr("a member is the subject of two slots");
     if (m >= c.lo && m < c.lo + c.n_loc) ms[m - c.lo] = (int32_t)s;
   }
+  g->subj_sorted.assign(subj_member, subj_member + c.S);
+  std::sort(g->subj_sorted.begin(), g->subj_sorted.end());
   RSF_HIP(hipSetDevice(g->device));
   RSF_HIP(hipMemcpyAsync(g->s.subj_member, subj_member, c.S * 4, hipMemcpyHostToDevice, g->stream));
   RSF_HIP(hipMemcpyAsync(g->s.member_subj, ms.data(), c.n_loc * 4, hipMemcpyHostToDevice, g->stream));
@@ -3657,6 +3469,9 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
       const rsf_action& x = acts[a];
       if (x.member >= c.N || x.act < RSF_ACT_JOIN_SELF || x.act > RSF_ACT_QUERY) return gerr("bad action");
       if (x.act == RSF_ACT_FORCE_LEAVE && x.subject >= c.S) return gerr("force_leave subject out of range");
+      if ((x.act == RSF_ACT_JOIN_SELF || x.act == RSF_ACT_LEAVE_SELF) &&
+          !std::binary_search(g->subj_sorted.begin(), g->subj_sorted.end(), x.member))
+        return gerr("join / leave of a member that is not a tracked subject");
       ms.push_back(x.member);
     }
     std::sort(ms.begin(), ms.end());
@@ -3815,9 +3630,12 @@ static int launch_ahead(rsf_gossip* g, uint32_t round) {
   RSF_HIP(hipEventRecord(g->ev_emitted, g->stream));
   RSF_HIP(hipStreamWaitEvent(g->side, g->ev_emitted, 0));
   int rc = peers_and_sort(g, round + 1, g->side);
-  if (rc) return rc;
+  // (also on an error: work already queued on the side stream may still write the group keys,
+  // so the main stream must wait for it before their next use -- ahead_drop does)
   RSF_HIP(hipEventRecord(g->ev_ahead, g->side));
-  g->ahead_launched = g->ahead_valid = true;
+  g->ahead_launched = true;
+  g->ahead_valid = rc == RSF_OK;
+  if (rc) return rc;
   g->ahead_round = round + 1;
   return RSF_OK;
 }
@@ -4750,6 +4568,38 @@ int rsf_gossip_deep_class_stats(rsf_gossip* g, uint64_t* out4) {
   out4[1] = t[0];
   out4[2] = t[7];
   out4[3] = t[1];
+  return RSF_OK;
+}
+
+int rsf_gossip_deep_full_items(rsf_gossip* g, uint64_t* sum, uint64_t* max) {
+  if (!g || !sum || !max) return gerr("null argument");
+  unsigned long long t[2] = {0, 0};
+  RSF_HIP(hipSetDevice(g->device));
+  if (g->c.deep) {
+    RSF_HIP(hipMemcpyAsync(t, g->s.deep_n + kDeepFullItems, sizeof(t), hipMemcpyDeviceToHost, g->stream));
+    RSF_HIP(hipStreamSynchronize(g->stream));
+  }
+  *sum = t[0];
+  *max = t[1];
+  return RSF_OK;
+}
+
+int rsf_gossip_dump_tails(rsf_gossip* g, uint32_t q, uint32_t* count, uint32_t* sealed) {
+  if (!g || q > 2) return gerr("bad argument");
+  const GCfg& c = g->c;
+  const uint64_t n = c.n_loc;
+  RSF_HIP(hipSetDevice(g->device));
+  std::vector<uint4> ts(n * 3), tz(n * 3);
+  if (c.deep) {
+    RSF_HIP(hipMemcpyAsync(ts.data(), g->s.tsum, n * 3 * sizeof(uint4), hipMemcpyDeviceToHost, g->stream));
+    RSF_HIP(hipMemcpyAsync(tz.data(), g->s.tseal, n * 3 * sizeof(uint4), hipMemcpyDeviceToHost, g->stream));
+    RSF_HIP(hipStreamSynchronize(g->stream));
+  }
+  const bool dq = c.deep && tcap_of(c, q);
+  for (uint64_t l = 0; l < n; ++l) {
+    if (count) count[l] = dq ? ts[l * 3 + q].x : 0u;
+    if (sealed) sealed[l] = dq ? std::min(tz[l * 3 + q].x, ts[l * 3 + q].x) : 0u;
+  }
   return RSF_OK;
 }
 

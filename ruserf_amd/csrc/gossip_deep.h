@@ -862,6 +862,11 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
       if (lane == 0) s_dprof[15] += 1ull;
 #endif
     }
+    if (CAP == kDeepBig && lane == 0) {  // the full-depth class: items it held (rsf_gossip_deep_full_items)
+      unsigned long long* const fi = reinterpret_cast<unsigned long long*>(s.deep_n + kDeepFullItems);
+      atomicAdd(fi, (unsigned long long)n);
+      atomicMax(fi + 1, (unsigned long long)n);
+    }
     for (uint32_t i = lane; i < n; i += kWave) d.st[i] = kDeepDead;  // clean for the next queue
     wsync();
   }
@@ -948,11 +953,9 @@ __global__ void __launch_bounds__(kWave) emit_deep_wave_kernel(GCfg c, GState s,
 
 // ---- the QueueChecker's prune (check_stream_kernel) --------------------------------------
 // One block per listed (member, queue).  Pass 1 streams head and tail once and keeps only the
-// 8-B keys in LDS (live head keys first, then the tail's in index order); the three selects
-// (the max-th key, the new head's qcap-th, the reserve's (qcap + R)-th) run together over the
-// LDS keys, one histogram each per radix pass; pass 2 streams the tail again and compacts it
-// in place, eight loads in flight per thread.  Two blocks per CU (the keys of a full queue are
-// 70 KB).
+// 8-B keys in LDS (live head keys first, then the tail's in index order); one select over the
+// LDS keys finds the max-th key; pass 2 streams the tail again and compacts it in place.  Two
+// blocks per CU (the keys of a full queue are 70 KB).
 #ifndef RSF_CHK_U1
 #define RSF_CHK_U1 32  // check_stream_kernel's pass 1: 16-B loads in flight per thread (16: 99.2 ms per 1M-member tick, 32: 97.3)
 #endif
@@ -964,10 +967,7 @@ struct CheckLds {
   uint32_t hist[3][256];
   uint64_t w64[kDeepWaves], w64b[kDeepWaves];
   uint32_t wcnt[kChkU2][kDeepWaves];
-  uint32_t sel_digit[3], sel_need[3], nb, nr, nh, hn;
-  uint4 hitem[kWave];         // the new head's items (<= qcap)
-  uint64_t hkey[kWave];
-  uint4 ritem[kDeepReserve];  // the reserve (written after the sealed group)
+  uint32_t sel_digit[3], sel_need[3], nb, hn;
 };
 
 // block-uniform minimum (every thread calls)
@@ -1077,11 +1077,18 @@ __device__ void lds_select3(const uint64_t* __restrict__ keys, uint32_t n, Check
 }
 
 // QueueChecker prune of the deep queues check_queues_kernel listed (entries l * 3 + q): keep the
-// `max` smallest keys (each member's own max with qmax), the head refilled with the qcap
-// smallest of them, the tail = the rest in the two groups w_store_tail writes (sealed above the
-// reserve), exact bounds.  The tail is compacted in place in index order (an item is written at
-// or below the position it was read from, after every thread has read its batch); the items
-// leaving the old head are written after the tail's.
+// `max` smallest keys of head and tail (each member's own max with qmax) and drop the rest.
+// One 256-thread block per (member, queue):
+//   pass 1 streams the head and the tail once and keeps only their 8-B keys in LDS (plus, with
+//          transmit counts below 256, the histogram of the keys' first varying byte);
+//   one radix select over the LDS keys finds the max-th smallest key T;
+//   pass 2 compacts the tail's kept items (key <= T) in place in index order (each batch is read
+//          whole before any of its positions is rewritten; an item moves only downwards), so a
+//          sealed prefix stays a prefix with its bound intact and only its length changes; the
+//          head is sorted, so its items past T are a suffix of its slots and are cleared.
+// No refill: the head may be left part-full with a non-empty tail.  That is a valid state --
+// emission then cannot decide from the head and the member takes the deferred whole-queue path,
+// which refills the head with the queue's smallest keys (emit_deep_wave_kernel).
 __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GState s, uint32_t max_depth,
                                                                     const uint32_t* __restrict__ qmax) {
   __shared__ CheckLds d;
@@ -1103,7 +1110,10 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
     const uint32_t keep = qmax ? qmax[l] : max_depth;
     const uint64_t hb = (l * 3 + q) * c.qcap;
     const uint32_t tc = s.tsum[l * 3 + q].x;
-    if (c.qcap + tc > kDeepItems) continue;  // (the tail's capacity is below it: cannot happen)
+    if (c.qcap + tc > kDeepItems) {  // (the tail's capacity is below it: an engine invariant broke)
+      if (tid == 0) atomicOr(s.err + l, (uint32_t)RSF_E_DEEP_INVARIANT);
+      continue;
+    }
     uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
     // pass 1: the keys into LDS, AND / OR of them, and (transmit counts below 256: byte 7 is
     // zero in every key) the histogram of byte 6 -- the first radix pass of the selects
@@ -1164,11 +1174,7 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
       d.w64[w] = an;
       d.w64b[w] = orr;
     }
-    if (tid == 0) {
-      d.nb = 0;
-      d.nr = 0;
-      d.nh = 0;
-    }
+    if (tid == 0) d.nb = 0;
     __syncthreads();
     an = d.w64[0];
     orr = d.w64b[0];

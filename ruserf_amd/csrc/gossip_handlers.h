@@ -116,6 +116,9 @@ struct GState {
 // deferred-member lists: 0 small, 1 full depth, 2 tiny, 3 middle, 4 re-listed to the full depth
 constexpr uint32_t kDeepLists = 5;
 constexpr uint32_t kDeepClassOff = 6;  // the per-list deferral counters sit at (total counter) - 6 + list
+// past the lists' counts (u32 words of deep_n): two u64 counters of the full-depth class, the
+// items its members held (sum, max) since creation
+constexpr uint32_t kDeepFullItems = 8;
 constexpr uint32_t kTailSlack = 192;  // tail row room past its capacity: one emission's spills (2 x 64) + 64
 // per-queue deep-queue fields by a select on q
 RSF_HD uint32_t tcap_of(const GCfg& c, uint32_t q) { return q == 0 ? c.tcap0 : q == 1 ? c.tcap1 : c.tcap2; }

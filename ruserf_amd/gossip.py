@@ -34,7 +34,7 @@ STATUS_NONE, STATUS_ALIVE, STATUS_LEAVING, STATUS_LEFT, STATUS_FAILED = 0, 1, 2,
 MSG_LEAVE, MSG_JOIN, MSG_USER_EVENT, MSG_QUERY = 0, 1, 3, 4
 F_REBROADCAST, F_REFUTE, F_PRUNE, F_DELIVER, F_MEMBER_EVENT = 1, 2, 4, 8, 16
 # per-member error bits (members()["err"])
-E_EVSLOT, E_QSLOT, E_REFUTE, E_STAGE, E_QUEUE_PRUNE = 1, 2, 4, 8, 16
+E_EVSLOT, E_QSLOT, E_REFUTE, E_STAGE, E_QUEUE_PRUNE, E_DELIVERY_LOG, E_DEEP_INVARIANT = 1, 2, 4, 8, 16, 32, 64
 # QueueOptions defaults (core/src/options.rs:494-530)
 MAX_QUEUE_DEPTH, MIN_QUEUE_DEPTH, QUEUE_DEPTH_WARNING = 4096, 0, 128
 ACT_JOIN_SELF, ACT_LEAVE_SELF, ACT_FORCE_LEAVE, ACT_USER_EVENT, ACT_QUERY = 1, 2, 3, 4, 5
@@ -459,6 +459,20 @@ class GossipEngine:
         out = np.zeros(4, dtype=np.uint64)
         check(lib().rsf_gossip_deep_class_stats(self._h, ptr(out, C.c_uint64)))
         return out
+
+    def deep_full_items(self):
+        """(sum, max) of the items the full-depth deferred class held per member since creation"""
+        a, b = C.c_uint64(), C.c_uint64()
+        check(lib().rsf_gossip_deep_full_items(self._h, C.byref(a), C.byref(b)))
+        return int(a.value), int(b.value)
+
+    def tails(self, q=0):
+        """queue q's HBM tail per member as the engine holds it (pending lists not applied):
+        (item counts, sealed-prefix lengths), each [n_loc]"""
+        cnt = np.zeros(self.n_loc, dtype=np.uint32)
+        sealed = np.zeros(self.n_loc, dtype=np.uint32)
+        check(lib().rsf_gossip_dump_tails(self._h, q, ptr(cnt, C.c_uint32), ptr(sealed, C.c_uint32)))
+        return cnt, sealed
 
     def checker_occupancy(self):
         """The checker ticks' occupancy since the last reset, before their prunes: {"bin": items per bin,

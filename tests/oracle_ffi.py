@@ -89,7 +89,7 @@ class World(C.Structure):
                 ("qd", C.c_uint32 * 3), ("q_hwm", P32), ("max_ue", C.c_uint32), ("query_limit", C.c_uint32),
                 ("act_status", PI32), ("act_cap", C.c_uint32), ("last_n_acts", C.c_uint32),
                 ("chk_period", C.c_uint32), ("chk_max", C.c_uint32), ("chk_min", C.c_uint32),
-                ("chk_warn", C.c_uint32), ("chk_stats", C.c_uint64 * 9)]
+                ("chk_warn", C.c_uint32), ("chk_stats", C.c_uint64 * 9), ("q_hole", P32)]
 
 
 class WorldCfg(C.Structure):
