@@ -701,13 +701,23 @@ __device__ __forceinline__ void q_pick_peers(const GCfg& c, QRegs& Q, uint32_t l
 // minlen, minkey mirror tsum (wave-uniform); spills are written at t[cnt ...] (the row has
 // kTailSlack slots past the capacity) and counted in only by the caller's commit.
 struct Spill {
-  uint4* t = nullptr;
+  uint4* t = nullptr;      // the query / event queues' 16-B items
+  uint64_t* t8 = nullptr;  // the intent queue's packed items (tail_pack)
   uint32_t cnt = 0, minlen = 0xFFFFFFFFu;
   uint64_t minkey = ~0ull;
 };
+__device__ __forceinline__ void spill_row(const GCfg& c, const GState& s, uint64_t l, uint32_t q, Spill& sp) {
+  if (q == 0) sp.t8 = tail8(s, c, l);
+  else sp.t = tail16(s, q) + l * tstride_of(c, q);
+}
+__device__ __forceinline__ void spill_put(const GCfg& c, const Spill& sp, uint32_t i, uint32_t rid, uint32_t seq,
+                                          uint32_t tl, uint32_t dec) {
+  if (sp.t8) sp.t8[i] = tail_pack(c, rid, seq, tl);
+  else sp.t[i] = make_uint4(rid, seq, tl, dec);
+}
 __device__ __forceinline__ Spill spill_of(const GCfg& c, const GState& s, uint64_t l, uint32_t q, uint4 sm) {
   Spill sp;
-  sp.t = tail_of(s, q) + l * tstride_of(c, q);
+  spill_row(c, s, l, q, sp);
   sp.cnt = sm.x;
   sp.minlen = sm.y;
   sp.minkey = ((uint64_t)sm.w << 32) | sm.z;
@@ -762,8 +772,8 @@ __device__ __forceinline__ uint32_t q_insert_batch_lds(const GCfg& c, QRegs& Q, 
     const bool sn = ins && pos_n >= c.qcap, se = live && pos_e >= c.qcap;
     // (ordinary stores: non-temporal ones measured 1.37 -> 2.24 ms of emission, later spills
     // landing in the same partly written sectors)
-    if (sn) sp->t[sp->cnt + (pos_n - c.qcap)] = make_uint4(rid, myseq, len << 16, DEC ? dec : 0u);
-    if (se) sp->t[sp->cnt + (pos_e - c.qcap)] = make_uint4(Q.r, Q.sq, Q.tl, DEC ? Q.dec : 0u);
+    if (sn) spill_put(c, *sp, sp->cnt + (pos_n - c.qcap), rid, myseq, len << 16, DEC ? dec : 0u);
+    if (se) spill_put(c, *sp, sp->cnt + (pos_e - c.qcap), Q.r, Q.sq, Q.tl, DEC ? Q.dec : 0u);
     const uint64_t at_n = ballot(ins && pos_n == c.qcap), at_e = ballot(live && pos_e == c.qcap);
     const int w = __ffsll((long long)(at_n | at_e)) - 1;
     const uint32_t tl_w = at_n ? (shfl_u32(len, w) << 16) : shfl_u32(Q.tl, w);
@@ -851,7 +861,9 @@ __device__ __forceinline__ uint32_t pend_apply(const GCfg& c, QRegs& Q, uint32_t
 // call's spills, and a spilled item is, by construction, at least every key left in the
 // head (the items whose sorted position among head and new items is >= queue_cap).  So one
 // pass over the tail finds it.  One wave; returns the number dropped.
-__device__ __forceinline__ uint32_t deep_prune_wave(const GCfg& c, QRegs& Q, uint32_t lane, uint32_t q, Spill& sp) {
+// nseq: the queue's next seq after the spills (every tail item is older)
+__device__ __forceinline__ uint32_t deep_prune_wave(const GCfg& c, QRegs& Q, uint32_t lane, uint32_t q, Spill& sp,
+                                                    uint32_t nseq) {
   (void)Q;
   uint32_t drops = 0;
   while (sp.cnt > tcap_of(c, q)) {
@@ -859,8 +871,15 @@ __device__ __forceinline__ uint32_t deep_prune_wave(const GCfg& c, QRegs& Q, uin
     uint32_t ti = 0;
     for (uint32_t b = 0; b < sp.cnt; b += kWave) {  // the tail holds items (cnt > tcap >= 1)
       const bool in = b + lane < sp.cnt;
-      const uint4 e = in ? sp.t[b + lane] : make_uint4(0u, 0u, 0u, 0u);
-      const uint64_t k = in ? tlq_key(e.z & 0xFFFF, e.z >> 16, e.y) : 0ull;
+      uint64_t k = 0ull;
+      if (sp.t8) {
+        const uint64_t x = in ? sp.t8[b + lane] : 0ull;
+        const uint32_t tl = tail_tl(x);
+        k = in ? tlq_key(tl & 0xFFFF, tl >> 16, tail_seq(x, nseq)) : 0ull;
+      } else {
+        const uint4 e = in ? sp.t[b + lane] : make_uint4(0u, 0u, 0u, 0u);
+        k = in ? tlq_key(e.z & 0xFFFF, e.z >> 16, e.y) : 0ull;
+      }
       const uint64_t m = wave_max_u64(k);
       const uint64_t at = ballot(in && k == m);
       if (at && (b == 0 || m > tk)) {
@@ -868,8 +887,13 @@ __device__ __forceinline__ uint32_t deep_prune_wave(const GCfg& c, QRegs& Q, uin
         ti = b + (uint32_t)(__ffsll((long long)at) - 1);
       }
     }
-    const uint4 last = sp.t[sp.cnt - 1];
-    if (lane == 0) sp.t[ti] = last;
+    if (sp.t8) {
+      const uint64_t last = sp.t8[sp.cnt - 1];
+      if (lane == 0) sp.t8[ti] = last;
+    } else {
+      const uint4 last = sp.t[sp.cnt - 1];
+      if (lane == 0) sp.t[ti] = last;
+    }
     __threadfence_block();  // the next pass reads the moved item
     sp.cnt--;
     drops++;
@@ -894,7 +918,7 @@ __device__ __forceinline__ uint32_t pend_flush_wave(const GCfg& c, const GState&
     if (tcap_of(c, q)) {  // deep queue: the head's overflow spills into the tail
       Spill sp = spill_of(c, s, l, q, s.tsum[l * 3 + q]);
       pend_apply<true, true>(c, Q, lane, q, n, p, seq0, row, &sp);
-      const uint32_t pd = deep_prune_wave(c, Q, lane, q, sp);
+      const uint32_t pd = deep_prune_wave(c, Q, lane, q, sp, seq0 + nq);
       drops += pd;
       if (lane == 0) {
         s.tsum[l * 3 + q] = spill_sum(sp);
@@ -964,7 +988,7 @@ __global__ void __launch_bounds__(256) ml_kernel(GCfg c, GState s, const rsf_ml_
       touched = true;
     }
     if (al && m != sm) {
-      ViewE* v = s.view + l * c.S + subj;
+      ViewS* v = s.view + l * c.S + subj;
       if (ml[e].kind == RSF_ML_JOIN) {
         h_node_join(v, r, subj);
         snap_member(c, s, l, subj, true);
@@ -1361,7 +1385,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   bool unsafe = false;
   if (DEEP) {
     auto get = [&](Spill& x, uint32_t q) {
-      x.t = tail_of(s, q) + l * tstride_of(c, q);
+      spill_row(c, s, l, q, x);
       x.cnt = shfl_u32(e.ts.x, q);
       x.minlen = shfl_u32(e.ts.y, q);
       x.minkey = ((uint64_t)shfl_u32(e.ts.w, q) << 32) | shfl_u32(e.ts.z, q);
@@ -1923,7 +1947,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
   r.err = shfl_u32(su, kSuErr);
   r.serf_state = (uint8_t)shfl_u32(su, kSuSerf);
   r.subj = (int32_t)shfl_u32(su, kSuSubj);
-  ViewE* vrow = s.view + l * c.S;
+  ViewS* vrow = s.view + l * c.S;
   MPROF_T(t_setup);
   MPROF_ADD(0, t_start, t_setup);
   const uint64_t vs = (uint64_t)st * stride;
@@ -2227,7 +2251,7 @@ __global__ void __launch_bounds__(256) merge_big_kernel(GCfg c, GState s, const 
 // local state before it merges the remote one, so every sender's state is copied
 // to a slab first (streaming, one block per pair), then merged.
 struct PPSlab {
-  ViewE* view;        // [pair][S]
+  ViewS* view;        // [pair][S]
   uint64_t* eb_ltime; // [pair][ebuf]
   uint32_t* eb_cnt;   // [pair][ebuf]
   uint64_t* eb_keys;  // [pair][ebuf * slot_k]
@@ -2238,8 +2262,8 @@ __global__ void __launch_bounds__(256) pp_snapshot_kernel(GCfg c, GState s, cons
                                                           PPSlab sl) {
   const uint64_t p = blockIdx.x;
   const uint64_t l = pairs[p].sender - c.lo;
-  const uint4* vsrc = reinterpret_cast<const uint4*>(s.view + l * c.S);
-  uint4* vdst = reinterpret_cast<uint4*>(sl.view + p * c.S);
+  const ViewS* vsrc = s.view + l * c.S;
+  ViewS* vdst = sl.view + p * c.S;
   for (uint32_t i = threadIdx.x; i < c.S; i += blockDim.x) vdst[i] = vsrc[i];
   for (uint32_t i = threadIdx.x; i < c.ebuf; i += blockDim.x) {
     sl.eb_ltime[p * c.ebuf + i] = s.eb_ltime[l * c.ebuf + i];
@@ -2278,8 +2302,8 @@ __global__ void __launch_bounds__(256) pp_merge_kernel(GCfg c, GState s, const r
   if (pel > 0) witness(r.eclock, pel - 1);
   if (pql > 0) witness(r.qclock, pql - 1);
   // ---- status_ltimes / left_members
-  const ViewE* sv = sl.view + p * c.S;
-  ViewE* vrow = s.view + l * c.S;
+  const ViewS* sv = sl.view + p * c.S;
+  ViewS* vrow = s.view + l * c.S;
   uint64_t c_leave = r.clock, c_join = r.clock;
   for (uint32_t base = 0; base < c.S; base += kWave) {
     const uint32_t subj = base + lane;
@@ -2411,7 +2435,7 @@ __global__ void __launch_bounds__(256) reap_kernel(GCfg c, GState s, uint32_t no
   const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   if (l >= c.n_loc) return;
   if (!s.alive[c.lo + l]) return;
-  ViewE* vrow = s.view + l * c.S;
+  ViewS* vrow = s.view + l * c.S;
   uint64_t dig = s.digest[l];
   const uint64_t d0 = dig;
   uint32_t lerr = 0;  // delivery-log overflow
@@ -2422,7 +2446,8 @@ __global__ void __launch_bounds__(256) reap_kernel(GCfg c, GState s, uint32_t no
       const uint32_t subj = base + lane;
       ViewE v{};
       if (subj < c.S) v = vrow[subj];
-      const uint32_t kind = vkind(v.meta), st = vstatus(v.meta), age = now - v.t;
+      // (stamps are kept mod 2^27: the age is exact below 2^27 rounds)
+      const uint32_t kind = vkind(v.meta), st = vstatus(v.meta), age = (now - v.t) & kViewTMask;
       const bool known = subj < c.S && kind == RSF_KIND_KNOWN;
       const bool failed = known && st == RSF_STATUS_FAILED && age > rc_to;   // leave_time.elapsed() > timeout
       const bool left = known && st == RSF_STATUS_LEFT && age > ts_to;
@@ -2455,7 +2480,7 @@ __global__ void __launch_bounds__(256) apply_kernel(GCfg c, GState s, const rsf_
   if (st >= en) return;
   MRegs r;
   load_regs(s, l, r);
-  ViewE* vrow = s.view + l * c.S;
+  ViewS* vrow = s.view + l * c.S;
   for (uint32_t i = st; i < en; ++i) {
     uint32_t k = order[i];
     rsf_msg x = msgs[k];
@@ -2485,7 +2510,7 @@ __global__ void keys_from_msgs_kernel(const rsf_msg* __restrict__ msgs, uint64_t
   idx[i] = (uint32_t)i;
 }
 
-__global__ void init_views_kernel(ViewE* view, uint64_t n_loc, uint32_t S, const uint8_t* kind,
+__global__ void init_views_kernel(ViewS* view, uint64_t n_loc, uint32_t S, const uint8_t* kind,
                                   const uint8_t* status, const uint64_t* ltime) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_loc * S) return;
@@ -2703,11 +2728,11 @@ __global__ void __launch_bounds__(256) queue_max_kernel(GCfg c, GState s, uint32
   const uint64_t l = phase_first(c, period, phase) + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave * period;
   if (l >= c.n_loc) return;
   const int32_t own = s.member_subj[l];
-  const ViewE* row = s.view + l * c.S;
+  const ViewS* row = s.view + l * c.S;
   uint64_t known = (c.N - c.S) + (own >= 0 ? 1u : 0u);
   for (uint32_t j0 = 0; j0 < c.S; j0 += kWave) {
     const uint32_t j = j0 + lane;
-    const bool kn = j < c.S && (int32_t)j != own && vkind(row[j].meta) == RSF_KIND_KNOWN;
+    const bool kn = j < c.S && (int32_t)j != own && vkind(ViewE(row[j]).meta) == RSF_KIND_KNOWN;
     known += (uint32_t)__popcll(ballot(kn));
   }
   uint64_t mx = 2 * known;
@@ -2717,7 +2742,6 @@ __global__ void __launch_bounds__(256) queue_max_kernel(GCfg c, GState s, uint32
 
 // Generations alive: gen and gen - 1 (modulo the generation count, even so that the
 // parity alternates across the wrap).
-__host__ __device__ inline uint32_t rumor_generations(const GCfg& c) { return (uint32_t)((1ull << (32 - c.rbits)) - 2); }
 
 // At the start of generation `gen` (the ring wrapped): every queue drops its items of
 // generation gen - 2, whose table half this generation overwrites.  One wave per
@@ -3117,11 +3141,17 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   c.rbits = 0;
   while ((1u << c.rbits) < cfg->max_rumors) c.rbits++;
   c.rmask = (cfg->max_rumors << 1) - 1;
+  c.gen = 0;
   g->end_bit = bits_for(N);
   auto fail = [&](int code) {
     rsf_gossip_destroy(g);
     return code;
   };
+  // the intent queue's packed tail items (tail_pack): the ring slot and parity in 27 bits,
+  // transmits in 6
+  if (c.tcap0 && c.rbits > 26) return fail(gerr("a deep intent queue needs max_rumors <= 2^26 (packed tail items)"));
+  if (c.tcap0 && c.tx_limit > 64)
+    return fail(gerr("a deep intent queue needs a retransmit limit <= 64 (packed tail items)"));
   if (hipStreamCreateWithFlags(&g->own, hipStreamNonBlocking) != hipSuccess)
     return fail(rsf::set_error(RSF_ERR_HIP, "hipStreamCreate failed"));
   g->stream = g->own;
@@ -3140,7 +3170,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   if (GA(s.clock, n * 8) || GA(s.eclock, n * 8) || GA(s.qclock, n * 8) || GA(s.emin, n * 8) || GA(s.qmin, n * 8) ||
       GA(s.digest, n * 8) || GA(s.err, n * 4) || GA(s.alive, N) || GA(s.serf_state, n) || GA(s.member_subj, n * 4) ||
       GA(s.subj_member, S * 4) || GA(s.refute_cnt, S * 4) || GA(s.refute_ltime, S * c.max_refute * 8) ||
-      GA(s.view, n * S * sizeof(ViewE)) || GA(s.q_rumor, n * 3 * c.qcap * 4) || GA(s.q_seq, n * 3 * c.qcap * 4) ||
+      GA(s.view, n * S * sizeof(ViewS)) || GA(s.q_rumor, n * 3 * c.qcap * 4) || GA(s.q_seq, n * 3 * c.qcap * 4) ||
       GA(s.q_txlen, n * 3 * c.qcap * 4) || GA(s.q_dec, n * c.qcap * 4) || GA(s.q_next_seq, n * 3 * 4) || GA(s.q_pruned, n * 4) || GA(s.q_expired, n * 4) || GA(s.eb_ltime, n * c.ebuf * 8) ||
       GA(s.eb_cnt, n * c.ebuf * 4) || GA(s.eb_keys, n * c.ebuf * c.slot_k * 8) || GA(s.qb_ltime, n * c.qbuf * 8) ||
       GA(s.qb_cnt, n * c.qbuf * 4) || GA(s.qb_ids, n * c.qbuf * c.slot_k * 4) ||
@@ -3150,7 +3180,8 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
     return fail(rc);
   if (c.deep) {  // tails, their summaries, the deferred-member list (also the checker's, 3 per member)
     for (int q = 0; q < 3; ++q)
-      if (tcap_of(c, q) && GA(q == 0 ? s.tail0 : q == 1 ? s.tail1 : s.tail2, n * tstride_of(c, q) * sizeof(uint4)))
+      if (tcap_of(c, q) && (q == 0 ? GA(s.tail0, n * c.tstride0 * sizeof(uint64_t))
+                                   : GA(q == 1 ? s.tail1 : s.tail2, n * tstride_of(c, q) * sizeof(uint4))))
         return fail(rc);
     if (GA(s.tsum, n * 3 * sizeof(uint4)) || GA(s.tseal, n * 3 * sizeof(uint4)) || GA(s.deep_ids, n * 5 * 4))
       return fail(rc);
@@ -3220,7 +3251,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   ms(s.subj_member, 0, S * 4);
   ms(s.refute_cnt, 0, S * 4);
   ms(s.refute_ltime, 0, S * c.max_refute * 8);
-  ms(s.view, 0, n * S * sizeof(ViewE));
+  ms(s.view, 0, n * S * sizeof(ViewS));
   ms(s.q_rumor, 0xFF, n * 3 * c.qcap * 4);
   ms(s.q_seq, 0, n * 3 * c.qcap * 4);
   ms(s.q_txlen, 0, n * 3 * c.qcap * 4);
@@ -3273,7 +3304,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
                   g->grp_slot, g->grp_off, g->dec_base, s.dlog, s.dmeta, s.dcnt,
                   g->bkt_send, g->bkt_recv, g->bkt_dec, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn,
-                  s.p_ent, s.p_cnt, g->big_base, tail_of(s, 0), tail_of(s, 1), tail_of(s, 2), s.tsum, s.deep_ids,
+                  s.p_ent, s.p_cnt, g->big_base, s.tail0, s.tail1, s.tail2, s.tsum, s.deep_ids,
                   s.tseal, g->qmax, g->d_act_status, g->occ_hist};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -3355,10 +3386,12 @@ int rsf_gossip_set_view(rsf_gossip* g, uint64_t m, uint32_t subj, uint8_t kind, 
   const GCfg& c = g->c;
   if (m < c.lo || m >= c.lo + c.n_loc || subj >= c.S) return gerr("member/subject out of range");
   if (kind > RSF_KIND_KNOWN || status > RSF_STATUS_FAILED) return gerr("bad view kind/status");
-  ViewE v;
-  v.ltime = ltime;
-  v.meta = status | ((uint32_t)kind << 8);
-  v.t = 0;
+  ViewE e;
+  e.ltime = ltime;
+  e.meta = status | ((uint32_t)kind << 8);
+  e.t = 0;
+  ViewS v;
+  v = e;
   RSF_HIP(hipSetDevice(g->device));
   RSF_HIP(hipMemcpyAsync(g->s.view + (m - c.lo) * c.S + subj, &v, sizeof(v), hipMemcpyHostToDevice, g->stream));
   RSF_HIP(hipStreamSynchronize(g->stream));
@@ -3491,6 +3524,7 @@ int rsf_gossip_round_begin(rsf_gossip* g, uint32_t round, const rsf_ml_event* ml
   if ((uint64_t)g->n_rumors + need > g->max_rumors) {  // the block restarts the ring, next generation
     g->n_rumors = 0;
     g->gen = (g->gen + 1) % rumor_generations(c);
+    g->c.gen = g->gen;
     // this generation reuses the half of the table of generation gen - 2: queued ids of
     // that generation expire now, before anything reads or re-queues them
     if ((rc = flush_pending(g))) return rc;
@@ -4095,7 +4129,7 @@ int rsf_gossip_round_merge_runs(rsf_gossip* g, const uint64_t* recv, const uint6
 }
 
 static size_t pp_bytes_per_pair(const GCfg& c) {
-  return (size_t)c.S * sizeof(ViewE) + (size_t)c.ebuf * 12 + (size_t)c.ebuf * c.slot_k * 8 + 32;
+  return (size_t)c.S * sizeof(ViewS) + (size_t)c.ebuf * 12 + (size_t)c.ebuf * c.slot_k * 8 + 32;
 }
 
 int rsf_gossip_push_pull_device(rsf_gossip* g, const rsf_pp_pair* pairs, uint64_t n, uint32_t flags) {
@@ -4117,8 +4151,8 @@ int rsf_gossip_push_pull_device(rsf_gossip* g, const rsf_pp_pair* pairs, uint64_
   // slab regions, each 16-byte aligned
   char* b = (char*)g->pp_buf;
   PPSlab sl;
-  sl.view = (ViewE*)b;
-  b += (size_t)c.S * sizeof(ViewE) * n;
+  sl.view = (ViewS*)b;
+  b += (size_t)c.S * sizeof(ViewS) * n;
   sl.eb_keys = (uint64_t*)b;
   b += (size_t)c.ebuf * c.slot_k * 8 * n;
   sl.eb_ltime = (uint64_t*)b;
@@ -4429,15 +4463,16 @@ int rsf_gossip_dump_view_rows(rsf_gossip* g, uint64_t row0, uint64_t rows, uint6
   if (!g || !ltime || !status || !kind) return gerr("null argument");
   if (row0 > g->c.n_loc || rows > g->c.n_loc - row0) return gerr("rows outside the shard");
   const uint64_t cnt = rows * g->c.S;
-  std::vector<ViewE> v(cnt);
+  std::vector<ViewS> vs(cnt);
   RSF_HIP(hipSetDevice(g->device));
-  RSF_HIP(hipMemcpyAsync(v.data(), g->s.view + row0 * g->c.S, cnt * sizeof(ViewE), hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipMemcpyAsync(vs.data(), g->s.view + row0 * g->c.S, cnt * sizeof(ViewS), hipMemcpyDeviceToHost, g->stream));
   RSF_HIP(hipStreamSynchronize(g->stream));
   for (uint64_t i = 0; i < cnt; ++i) {
-    ltime[i] = v[i].ltime;
-    status[i] = (uint8_t)(v[i].meta & 0xFF);
-    kind[i] = (uint8_t)((v[i].meta >> 8) & 0xFF);
-    if (time) time[i] = v[i].t;
+    const ViewE v = vs[i];
+    ltime[i] = v.ltime;
+    status[i] = (uint8_t)(v.meta & 0xFF);
+    kind[i] = (uint8_t)((v.meta >> 8) & 0xFF);
+    if (time) time[i] = v.t;  // (mod 2^27)
   }
   return RSF_OK;
 }
@@ -4458,6 +4493,8 @@ static int dump_queues_deep(rsf_gossip* g, uint32_t D, uint32_t* rumor, uint32_t
   std::vector<uint32_t> hr(hc), hs(hc), ht(hc);
   std::vector<uint4> sum(n * 3);
   std::vector<std::vector<uint4>> tail(3);
+  std::vector<uint64_t> tail0;  // the intent queue's packed items
+  std::vector<uint32_t> nseq(n * 3);
   hipStream_t st = g->stream;
   const uint64_t h0 = r0 * 3 * c.qcap;
   RSF_HIP(hipMemcpyAsync(hr.data(), g->s.q_rumor + h0, hc * 4, hipMemcpyDeviceToHost, st));
@@ -4467,10 +4504,16 @@ static int dump_queues_deep(rsf_gossip* g, uint32_t D, uint32_t* rumor, uint32_t
   if (c.deep) RSF_HIP(hipMemcpyAsync(sum.data(), g->s.tsum + r0 * 3, n * 3 * 16, hipMemcpyDeviceToHost, st));
   for (uint32_t q = 0; q < 3; ++q)
     if (tcap_of(c, q)) {
-      tail[q].resize(n * tstride_of(c, q));
-      RSF_HIP(hipMemcpyAsync(tail[q].data(), tail_of(g->s, q) + r0 * tstride_of(c, q), tail[q].size() * 16,
-                             hipMemcpyDeviceToHost, st));
+      if (q == 0) {
+        tail0.resize(n * c.tstride0);
+        RSF_HIP(hipMemcpyAsync(tail0.data(), g->s.tail0 + r0 * c.tstride0, tail0.size() * 8, hipMemcpyDeviceToHost, st));
+      } else {
+        tail[q].resize(n * tstride_of(c, q));
+        RSF_HIP(hipMemcpyAsync(tail[q].data(), tail16(g->s, q) + r0 * tstride_of(c, q), tail[q].size() * 16,
+                               hipMemcpyDeviceToHost, st));
+      }
     }
+  RSF_HIP(hipMemcpyAsync(nseq.data(), g->s.q_next_seq + r0 * 3, n * 3 * 4, hipMemcpyDeviceToHost, st));
   RSF_HIP(hipStreamSynchronize(st));
   std::vector<std::pair<uint64_t, uint32_t>> items;
   for (uint64_t l = 0; l < n; ++l)
@@ -4481,7 +4524,8 @@ static int dump_queues_deep(rsf_gossip* g, uint32_t D, uint32_t* rumor, uint32_t
         if (hr[hb + i] != kEmpty) items.push_back({tlq_key(ht[hb + i] & 0xFFFF, ht[hb + i] >> 16, hs[hb + i]), hr[hb + i]});
       if (tcap_of(c, q))
         for (uint32_t i = 0; i < sum[l * 3 + q].x; ++i) {
-          const uint4 e = tail[q][l * tstride_of(c, q) + i];
+          const uint4 e = q == 0 ? tail_unpack(c, tail0[l * c.tstride0 + i], nseq[l * 3])
+                                 : tail[q][l * tstride_of(c, q) + i];
           items.push_back({tlq_key(e.z & 0xFFFF, e.z >> 16, e.y), e.x});
         }
       std::sort(items.begin(), items.end());
@@ -4750,7 +4794,7 @@ __global__ void __launch_bounds__(256) snap_init_kernel(GCfg c, GState s) {
   for (uint32_t b = 0; b < 32; ++b) {
     const uint32_t j = k * 32 + b;
     if (j >= c.S) break;
-    const uint32_t meta = s.view[l * c.S + j].meta;
+    const uint32_t meta = ViewE(s.view[l * c.S + j]).meta;
     const uint32_t st = vstatus(meta);
     if (vkind(meta) == RSF_KIND_KNOWN && (st == RSF_STATUS_ALIVE || st == RSF_STATUS_LEAVING)) bits |= 1u << b;
   }
@@ -4959,13 +5003,13 @@ __global__ void __launch_bounds__(256) reconnect_kernel(GCfg c, GState s, uint32
   if (target && lane == 0) target[l] = kEmpty;
   if (!s.alive[m]) return;
   const int32_t own = s.member_subj[l];
-  const ViewE* row = s.view + l * c.S;
+  const ViewS* row = s.view + l * c.S;
   uint32_t failed = 0, left = 0;
   uint64_t known = (c.N - c.S) + (own >= 0 ? 1u : 0u);  // members.states: see above
   for (uint32_t j0 = 0; j0 < c.S; j0 += kWave) {
     const uint32_t j = j0 + lane;
     uint32_t meta = 0;
-    if (j < c.S && (int32_t)j != own) meta = row[j].meta;
+    if (j < c.S && (int32_t)j != own) meta = ViewE(row[j]).meta;
     const bool kn = vkind(meta) == RSF_KIND_KNOWN;
     known += (uint32_t)__popcll(ballot(kn));
     failed += (uint32_t)__popcll(ballot(kn && vstatus(meta) == RSF_STATUS_FAILED));
@@ -4983,7 +5027,7 @@ __global__ void __launch_bounds__(256) reconnect_kernel(GCfg c, GState s, uint32
   for (uint32_t j0 = 0; j0 < c.S && tj == kEmpty; j0 += kWave) {
     const uint32_t j = j0 + lane;
     uint32_t meta = 0;
-    if (j < c.S && (int32_t)j != own) meta = row[j].meta;
+    if (j < c.S && (int32_t)j != own) meta = ViewE(row[j]).meta;
     const bool fa = vkind(meta) == RSF_KIND_KNOWN && vstatus(meta) == RSF_STATUS_FAILED;
     const unsigned long long mask = ballot(fa);
     const uint32_t cnt = (uint32_t)__popcll(mask);

@@ -314,12 +314,17 @@ __device__ uint64_t w_select_kth(DeepWave<CAP>& d, uint32_t lane, uint32_t n, ui
   return prefix;
 }
 
+// intent items that came from the packed tail enter the head with their rumor's decoration
+__device__ __forceinline__ void head_dec_fix(const GCfg& c, const GState& s, QRegs& Q) {
+  if (Q.dec == kDecLookup) Q.dec = s.rdec[Q.r & c.rmask];
+}
+
 // head = the qcap smallest live keys, sorted into the lanes of Q (marked kDeepInHead in LDS);
 // returns the bounds of the live items left (the tail): (min key, min length), ~0 if none, and
 // for w_store_tail the reserve's largest key rres (the (qcap + kDeepReserve)-th smallest: the
 // head's picks leave the other items' keys as they are; ~0 when every item left is reserve)
 template <uint32_t CAP>
-__device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint32_t q, QRegs& Q,
+__device__ __forceinline__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint32_t n, uint32_t q, QRegs& Q,
                             uint64_t& tmin, uint32_t& tminlen, uint64_t& rres) {
 #if RSF_DEEP_PROF
   uint64_t tt = __builtin_amdgcn_s_memtime();
@@ -439,6 +444,33 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
 #undef RSF_TH_T
 }
 
+// U * 64 tail items [b + u * 64 + lane] of (l, q) in the unpacked 16-B form, all loads issued
+// before any is used; indices at or past `end` give zeros.  The intent queue's packed items
+// (q == 0) come back with decoration kDecLookup.
+template <uint32_t U>
+__device__ __forceinline__ void tail_chunk(const GCfg& c, const GState& s, uint64_t l, uint32_t q, uint32_t b,
+                                           uint32_t end, uint32_t lane, uint32_t nseq, uint4 (&e)[U]) {
+  if (q == 0) {
+    const uint64_t* const t = tail8(s, c, l);
+    uint64_t x[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t i = b + u * kWave + lane;
+      x[u] = i < end ? t[i] : 0ull;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u)
+      e[u] = b + u * kWave + lane < end ? tail_unpack(c, x[u], nseq) : make_uint4(0, 0, 0, 0);
+  } else {
+    const uint4* const t = tail16(s, q) + l * tstride_of(c, q);
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t i = b + u * kWave + lane;
+      e[u] = i < end ? t[i] : make_uint4(0, 0, 0, 0);
+    }
+  }
+}
+
 // the live items not in the head back to the tail (compacted) at tail[t_lo ...], in two
 // groups: first every item above the kDeepReserve-th smallest of them (they join the sealed
 // prefix), then the kDeepReserve smallest (the RESERVE: left in the recent part, so the next
@@ -446,9 +478,11 @@ __device__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uint32_t lane, uint
 // transmits-0 items -- finds them without the sealed prefix).  Returns the count; *nb = the
 // sealed group's size, *bmin = its smallest key (~0 if none).
 template <uint32_t CAP>
-__device__ uint32_t w_store_tail(const GCfg& c, const GState& s, uint64_t l, uint32_t q, DeepWave<CAP>& d,
+__device__ __forceinline__ uint32_t w_store_tail(const GCfg& c, const GState& s, uint64_t l, uint32_t q, DeepWave<CAP>& d,
                                  uint32_t lane, uint32_t n, uint32_t t_lo, uint64_t R, uint32_t* nb, uint64_t* bmin) {
-  uint4* const t = tcap_of(c, q) ? tail_of(s, q) + l * tstride_of(c, q) + t_lo : nullptr;
+  // (q == 0: the intent queue's packed items; only a deep queue holds more live items than its head)
+  uint4* const t = q && tcap_of(c, q) ? tail16(s, q) + l * tstride_of(c, q) + t_lo : nullptr;
+  uint64_t* const t8 = q == 0 && c.tcap0 ? tail8(s, c, l) + t_lo : nullptr;
   // the sealed group's size first (one count pass: the reserve is R's items and below)
   uint32_t ns = 0;
   for (uint32_t b = 0; b < n; b += kWave) {
@@ -464,8 +498,11 @@ __device__ uint32_t w_store_tail(const GCfg& c, const GState& s, uint64_t l, uin
     const bool live = i < n && d.st[i] == kDeepLive;
     const bool sealed = live && k > R, res = live && k <= R;
     const uint64_t ms = ballot(sealed), mr = ballot(res);
-    if (live)  // only a deep queue holds more live items than its head
-      t[sealed ? bs + mbcnt(ms) : br + mbcnt(mr)] = make_uint4(d.rid[i], key_seq(k), key_tl(k), d.dec[i]);
+    if (live) {
+      const uint32_t at = sealed ? bs + mbcnt(ms) : br + mbcnt(mr);
+      if (q == 0) t8[at] = tail_pack(c, d.rid[i], key_seq(k), key_tl(k));
+      else t[at] = make_uint4(d.rid[i], key_seq(k), key_tl(k), d.dec[i]);
+    }
     if (sealed) bm = k < bm ? k : bm;
     bs += (uint32_t)__popcll(ms);
     br += (uint32_t)__popcll(mr);
@@ -477,27 +514,23 @@ __device__ uint32_t w_store_tail(const GCfg& c, const GState& s, uint64_t l, uin
 
 // the sealed prefix tail[0, sm) into LDS after the n items there (live): the recent mode could
 // not decide, the member continues with every item; returns the new item count
+// nseq: the queue's next seq before this emission (every tail item is older)
 template <uint32_t CAP>
-__device__ uint32_t w_load_sealed(const GCfg& c, const GState& s, uint64_t l, uint32_t q, DeepWave<CAP>& d,
-                                  uint32_t lane, uint32_t n, uint32_t sm) {
-  const uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
+__device__ __forceinline__ uint32_t w_load_sealed(const GCfg& c, const GState& s, uint64_t l, uint32_t q, DeepWave<CAP>& d,
+                                  uint32_t lane, uint32_t n, uint32_t sm, uint32_t nseq) {
   const uint32_t qdec = q == 1 ? kDecQuery : kDecEvent;
   for (uint32_t i = lane; i < n; i += kWave)
     if (d.st[i] == kDeepInHead) d.st[i] = kDeepLive;
   for (uint32_t b = 0; b < sm; b += kDeepU * kWave) {
     uint4 e[kDeepU];
-#pragma unroll
-    for (uint32_t u = 0; u < kDeepU; ++u) {
-      const uint32_t i = b + u * kWave + lane;
-      e[u] = i < sm ? t[i] : make_uint4(0, 0, 0, 0);
-    }
+    tail_chunk<kDeepU>(c, s, l, q, b, sm, lane, nseq, e);
 #pragma unroll
     for (uint32_t u = 0; u < kDeepU; ++u) {
       const uint32_t i = b + u * kWave + lane;
       if (i < sm) {
         d.key[n + i] = tlq_key(e[u].z & 0xFFFF, e[u].z >> 16, e[u].y);
         d.rid[n + i] = e[u].x;
-        d.dec[n + i] = q == 0 ? e[u].w : qdec;
+        d.dec[n + i] = q == 0 ? kDecLookup : qdec;
         d.st[n + i] = kDeepLive;
       }
     }
@@ -549,7 +582,7 @@ __device__ __forceinline__ void deep_relist_full(const GCfg& c, const GState& s,
 }
 
 template <bool BKT, uint32_t CAP>
-__device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uint32_t lane, const DeepPre& pre,
+__device__ __forceinline__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uint32_t lane, const DeepPre& pre,
                                  uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val,
                                  uint32_t* __restrict__ out_dec, const Buckets& bk, DeepWave<CAP>& d) {
   const uint32_t pc = pre.pc, npend = pend_total(pc);
@@ -633,13 +666,9 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
       if (lane == 0) s.deep_ids[c.n_loc * 4 + atomicAdd(s.deep_n + 4, 1u)] = (uint32_t)l;  // list 4
       return;
     }
-    const uint4* const t = tail_of(s, q) + l * tstride_of(c, q) + t_lo;
+    const uint32_t nseq = shfl_u32(qseq, (int)q);  // (every tail item is older)
     uint4 e[kDeepU];
-#pragma unroll
-    for (uint32_t u = 0; u < kDeepU; ++u) {
-      const uint32_t i = u * kWave + lane;
-      e[u] = i < tn ? t[i] : make_uint4(0, 0, 0, 0);
-    }
+    tail_chunk<kDeepU>(c, s, l, q, t_lo, tc, lane, nseq, e);
     if (!pend_lds) {
       d.pend[lane].rid = pr0;
       d.pend[lane].dec = pd0;
@@ -664,17 +693,13 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
         if (i < tn) {
           d.key[hn + i] = tlq_key(e[u].z & 0xFFFF, e[u].z >> 16, e[u].y);
           d.rid[hn + i] = e[u].x;
-          d.dec[hn + i] = q == 0 ? e[u].w : qdec;
+          d.dec[hn + i] = q == 0 ? kDecLookup : qdec;
           d.st[hn + i] = kDeepLive;
         }
       }
       b += kDeepU * kWave;
       if (b >= tn) break;
-#pragma unroll
-      for (uint32_t u = 0; u < kDeepU; ++u) {  // the next kDeepU * 64 (queues past 512 items)
-        const uint32_t i = b + u * kWave + lane;
-        e[u] = i < tn ? t[i] : make_uint4(0, 0, 0, 0);
-      }
+      tail_chunk<kDeepU>(c, s, l, q, t_lo + b, tc, lane, nseq, e);  // the next kDeepU * 64 (queues past 512 items)
     }
     uint32_t n = hn + tn;
     if (n == 0 && nq == 0) continue;
@@ -716,6 +741,7 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
     uint32_t tminlen;
     RSF_DEEP_T(9);
     w_take_head(c, d, lane, n, q, Q, tmin, tminlen, rres);
+    head_dec_fix(c, s, Q);
     RSF_DEEP_T(10);
     // recent mode: exact only if the head is full and below every sealed key; the sealed
     // prefix stays in the tail, so the tail's bounds include the seal's
@@ -740,7 +766,7 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
 #if RSF_DEEP_PROF
         if (lane == 0) s_dprof[30] += 1ull;
 #endif
-        n = w_load_sealed(c, s, l, q, d, lane, n, t_lo);
+        n = w_load_sealed(c, s, l, q, d, lane, n, t_lo, shfl_u32(qseq, (int)q));
         recent = false;
         t_lo = 0;
         sb = ~0ull;
@@ -751,6 +777,7 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
           if (d.st[i] == kDeepInHead) d.st[i] = kDeepLive;
         wsync();
         w_take_head(c, d, lane, n, q, Q, tmin, tminlen, rres);
+        head_dec_fix(c, s, Q);
       }
     }
     if (recent) {
@@ -776,7 +803,7 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
         return;
       }
       // the head cannot decide even now: every item (the sealed prefix joins) for the fallback
-      n = w_load_sealed(c, s, l, q, d, lane, n, t_lo);
+      n = w_load_sealed(c, s, l, q, d, lane, n, t_lo, shfl_u32(qseq, (int)q));
       recent = false;
       t_lo = 0;
       sb = ~0ull;
@@ -826,7 +853,7 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
             d.st[wi] = kDeepPicked;
             if (nrec + k < c.cap_t && off != ~0ull) {
               ov[off + nrec + k] = d.rid[wi];
-              if (od) od[off + nrec + k] = d.dec[wi];
+              if (od) od[off + nrec + k] = d.dec[wi] == kDecLookup ? s.rdec[d.rid[wi] & c.rmask] : d.dec[wi];
             }
           }
           k++;
@@ -849,6 +876,7 @@ __device__ void deep_wave_member(const GCfg& c, const GState& s, uint64_t l, uin
       }
       RSF_DEEP_T(13);
       w_take_head(c, d, lane, n, q, Q, tmin, tminlen, rres);
+      head_dec_fix(c, s, Q);
       q_store(c, s, l, q, lane, Q, true);
       uint32_t nb = 0;
       uint64_t bmin = ~0ull;
@@ -1114,7 +1142,10 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
       if (tid == 0) atomicOr(s.err + l, (uint32_t)RSF_E_DEEP_INVARIANT);
       continue;
     }
-    uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
+    // the intent queue's packed items (q == 0) or the 16-B items of the others
+    uint4* const t = q ? tail16(s, q) + l * tstride_of(c, q) : nullptr;
+    uint64_t* const t8 = q ? nullptr : tail8(s, c, l);
+    const uint32_t nseq = s.q_next_seq[l * 3 + q];  // (every tail item is older)
     // pass 1: the keys into LDS, AND / OR of them, and (transmit counts below 256: byte 7 is
     // zero in every key) the histogram of byte 6 -- the first radix pass of the selects
     const bool fuse = c.tx_limit < 256;
@@ -1137,33 +1168,54 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
     __syncthreads();
     const uint32_t hn = d.hn, n = hn + tc;
     constexpr uint32_t U1 = RSF_CHK_U1;
-    for (uint32_t b = 0; b < tc; b += U1 * kDeepThreads) {
-      uint4 x[U1];
-#pragma unroll
-      for (uint32_t u = 0; u < U1; ++u) {
-        const uint32_t i = b + u * kDeepThreads + tid;
-        x[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
+    auto put = [&](uint32_t i, bool in, uint64_t k) {
+      if (in) {
+        keys[hn + i] = k;
+        an &= k;
+        orr |= k;
       }
-#pragma unroll
-      for (uint32_t u = 0; u < U1; ++u) {
-        const uint32_t i = b + u * kDeepThreads + tid;
-        const bool in = i < tc;
-        const uint64_t k = tlq_key(x[u].z & 0xFFFF, x[u].z >> 16, x[u].y);
-        if (in) {
-          keys[hn + i] = k;
-          an &= k;
-          orr |= k;
+      if (fuse) {  // one atomic for the lanes that agree with the first active lane
+        const uint32_t dg = (uint32_t)(k >> 48) & 0xFF;
+        const uint64_t am = ballot(in);
+        if (am) {
+          const int f = __ffsll((long long)am) - 1;
+          const uint32_t d0 = shfl_u32(dg, f);
+          const uint64_t same = ballot(in && dg == d0);
+          if (lane == (uint32_t)f) atomicAdd(&d.hist[0][d0], (uint32_t)__popcll(same));
+          else if (in && dg != d0) atomicAdd(&d.hist[0][dg], 1u);
         }
-        if (fuse) {  // one atomic for the lanes that agree with the first active lane
-          const uint32_t dg = (uint32_t)(k >> 48) & 0xFF;
-          const uint64_t am = ballot(in);
-          if (am) {
-            const int f = __ffsll((long long)am) - 1;
-            const uint32_t d0 = shfl_u32(dg, f);
-            const uint64_t same = ballot(in && dg == d0);
-            if (lane == (uint32_t)f) atomicAdd(&d.hist[0][d0], (uint32_t)__popcll(same));
-            else if (in && dg != d0) atomicAdd(&d.hist[0][dg], 1u);
-          }
+      }
+    };
+    if (t8) {
+      bool old_item = false;  // an item near the end of the packed seq window
+      for (uint32_t b = 0; b < tc; b += U1 * kDeepThreads) {
+        uint64_t x[U1];
+#pragma unroll
+        for (uint32_t u = 0; u < U1; ++u) {
+          const uint32_t i = b + u * kDeepThreads + tid;
+          x[u] = i < tc ? t8[i] : 0ull;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U1; ++u) {
+          const uint32_t i = b + u * kDeepThreads + tid;
+          const uint32_t tl = tail_tl(x[u]);
+          old_item |= i < tc && tail_age_over(x[u], nseq);
+          put(i, i < tc, tlq_key(tl & 0xFFFF, tl >> 16, tail_seq(x[u], nseq)));
+        }
+      }
+      if (old_item) atomicOr(s.err + l, (uint32_t)RSF_E_DEEP_INVARIANT);
+    } else {
+      for (uint32_t b = 0; b < tc; b += U1 * kDeepThreads) {
+        uint4 x[U1];
+#pragma unroll
+        for (uint32_t u = 0; u < U1; ++u) {
+          const uint32_t i = b + u * kDeepThreads + tid;
+          x[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U1; ++u) {
+          const uint32_t i = b + u * kDeepThreads + tid;
+          put(i, i < tc, tlq_key(x[u].z & 0xFFFF, x[u].z >> 16, x[u].y));
         }
       }
     }
@@ -1198,11 +1250,17 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
     const uint32_t m = min(s.tseal[l * 3 + q].x, tc);
     uint32_t kept_sealed = 0;
     for (uint32_t b = 0; b < tc; b += kChkU2 * kDeepThreads) {
+      // (the items move as they are: 8 B packed or 16 B; the keys come from pass 1)
       uint4 x[kChkU2];
 #pragma unroll
       for (uint32_t u = 0; u < kChkU2; ++u) {
         const uint32_t i = b + u * kDeepThreads + tid;
-        x[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
+        if (t8) {
+          const uint64_t v = i < tc ? t8[i] : 0ull;
+          x[u] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u);
+        } else {
+          x[u] = i < tc ? t[i] : make_uint4(0, 0, 0, 0);
+        }
       }
       uint64_t km[kChkU2];
 #pragma unroll
@@ -1224,7 +1282,11 @@ __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GSta
         uint32_t before = 0;
 #pragma unroll
         for (uint32_t v = 0; v < kDeepWaves; ++v) before += v < w ? d.wcnt[u][v] : 0u;
-        if ((km[u] >> lane) & 1ull) t[base + before + mbcnt(km[u])] = x[u];
+        if ((km[u] >> lane) & 1ull) {
+          const uint32_t at = base + before + mbcnt(km[u]);
+          if (t8) t8[at] = ((uint64_t)x[u].y << 32) | x[u].x;
+          else t[at] = x[u];
+        }
 #pragma unroll
         for (uint32_t v = 0; v < kDeepWaves; ++v) base += d.wcnt[u][v];
       }
@@ -1280,17 +1342,35 @@ __device__ __forceinline__ uint32_t tail_expire_wave(const GCfg& c, const GState
   if (!tcap_of(c, q)) return 0;
   const uint4 sm = s.tsum[l * 3 + q];
   if (!sm.x) return 0;
-  uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
+  uint4* const t = q ? tail16(s, q) + l * tstride_of(c, q) : nullptr;
+  uint64_t* const t8 = q ? nullptr : tail8(s, c, l);
+  const uint32_t nseq = s.q_next_seq[l * 3 + q];
+  // packed items hold the generation's parity only: rebuilt against the previous generation
+  // (gen - 1), the newest any queued item can have before this wrap, an item is of gen - 1 or
+  // of gen - 2 -- the stale one
+  const uint32_t gprev = gen == 0 ? G - 1 : gen - 1;
   uint32_t kept = 0, gone = 0, lmin = ~0u;
   uint64_t kmin = ~0ull;
+  bool old_item = false;
   for (uint32_t b = 0; b < sm.x; b += kWave) {
     const bool in = b + lane < sm.x;
-    const uint4 e = in ? t[b + lane] : make_uint4(kEmpty, 0u, 0u, 0u);
+    uint4 e;
+    uint64_t x = 0ull;
+    if (t8) {
+      x = in ? t8[b + lane] : 0ull;
+      e = make_uint4(tail_rid(c, x, gprev), tail_seq(x, nseq), tail_tl(x), 0u);
+      old_item |= in && tail_age_over(x, nseq);
+    } else {
+      e = in ? t[b + lane] : make_uint4(kEmpty, 0u, 0u, 0u);
+    }
     const bool stale = in && (gen + G - (e.x >> c.rbits) % G) % G >= 2;
     const bool keep = in && !stale;
     const uint64_t km = ballot(keep);
     __threadfence_block();  // every lane has read its item before any is overwritten
-    if (keep) t[kept + mbcnt(km)] = e;
+    if (keep) {
+      if (t8) t8[kept + mbcnt(km)] = x;
+      else t[kept + mbcnt(km)] = e;
+    }
     const uint64_t k = keep ? tlq_key(e.z & 0xFFFF, e.z >> 16, e.y) : ~0ull;
     const uint64_t mk = wave_min_u64(k);
     kmin = mk < kmin ? mk : kmin;
@@ -1298,6 +1378,7 @@ __device__ __forceinline__ uint32_t tail_expire_wave(const GCfg& c, const GState
     kept += (uint32_t)__popcll(km);
     gone += (uint32_t)__popcll(ballot(stale));
   }
+  if (ballot(old_item) && lane == 0) atomicOr(s.err + l, (uint32_t)RSF_E_DEEP_INVARIANT);
   if (gone && lane == 0) {  // exact bounds over what is kept; the whole tail sealed
     s.tsum[l * 3 + q] = kept ? make_uint4(kept, lmin, (uint32_t)kmin, (uint32_t)(kmin >> 32)) : kTSumEmpty;
     s.tseal[l * 3 + q] = kept ? make_uint4(kept, (uint32_t)kmin, (uint32_t)(kmin >> 32), 0u) : kTSumEmpty;

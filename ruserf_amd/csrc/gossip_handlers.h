@@ -45,14 +45,39 @@ struct GCfg {
   uint32_t tcap0, tcap1, tcap2, tstride0, tstride1, tstride2;
   uint32_t deep;  // any tail
   uint32_t max_ue, query_limit;  // Options::max_user_event_size / query_size_limit (origination checks)
+  uint32_t gen;  // the rumor ring's current generation (rebuilds the intent tail's packed rumor ids)
 };
 
-// view entry: members.states[subject] (status, status_time) or recent_intents[subject]
-struct __align__(16) ViewE {
+// view entry: members.states[subject] (status, status_time) or recent_intents[subject] --
+// the register form the handlers work on
+struct ViewE {
   uint64_t ltime;
   uint32_t meta;  // status | kind << 8
   uint32_t t;     // leave_time of a Failed/Left member, wall time of a buffered intent (base.rs:1355, 1364, 1813)
 };
+// ... and its 12-B form in HBM: the Lamport time whole, and one word for the time stamp (27 bits),
+// the status (3 bits) and the kind (2 bits).  Time stamps are kept mod 2^27 (rounds): the
+// reaper's ages (now - stamp) are exact while below 2^27 rounds, and the dumps return the
+// stamp mod 2^27.
+constexpr uint32_t kViewTBits = 27;
+constexpr uint32_t kViewTMask = (1u << kViewTBits) - 1;
+struct ViewS {
+  uint32_t lo, hi, mt;
+  RSF_HD operator ViewE() const {
+    ViewE v;
+    v.ltime = ((uint64_t)hi << 32) | lo;
+    v.meta = ((mt >> 27) & 7u) | ((mt >> 30) << 8);
+    v.t = mt & kViewTMask;
+    return v;
+  }
+  RSF_HD ViewS& operator=(const ViewE& v) {
+    lo = (uint32_t)v.ltime;
+    hi = (uint32_t)(v.ltime >> 32);
+    mt = (v.t & kViewTMask) | ((v.meta & 7u) << 27) | (((v.meta >> 8) & 3u) << 30);
+    return *this;
+  }
+};
+static_assert(sizeof(ViewS) == 12, "12-B view entries");
 
 struct GState {
   uint64_t *clock, *eclock, *qclock, *emin, *qmin, *digest;
@@ -63,7 +88,7 @@ struct GState {
   uint32_t* subj_member;  // [S]
   uint32_t* refute_cnt;   // [S]
   uint64_t* refute_ltime; // [S][max_refute]
-  ViewE* view;            // [n_loc][S]
+  ViewS* view;            // [n_loc][S], 12-B entries
   uint32_t *q_rumor, *q_seq, *q_txlen, *q_next_seq;  // [n_loc][3][qcap], next_seq [n_loc][3]
   uint32_t* q_dec;        // [n_loc][qcap] intent queue: each item's record decoration (subject slot)
   uint32_t* q_pruned;     // [n_loc] live queue items dropped by a full queue (memberlist Prune), cumulative
@@ -95,12 +120,16 @@ struct GState {
   struct PendE { uint32_t rid, dec, lq; } * p_ent;  // [n_loc][kPend], 12-B entries: one contiguous append
   uint32_t* p_cnt;                 // [n_loc]
   // Deep queues: each queue is its register head (the q_* slots above, sorted) plus an
-  // UNORDERED tail in HBM, tail[q][l * tstride[q] + i] = {rumor, seq, transmits | len << 16,
-  // decoration}, i < tsum[l * 3 + q].x.  tsum = {count, a lower bound of the tail's smallest
+  // UNORDERED tail in HBM, tail[q][l * tstride[q] + i], i < tsum[l * 3 + q].x: for the query and
+  // event queues 16-B items {rumor, seq, transmits | len << 16, decoration}; for the intent queue
+  // 8-B packed items (tail_pack below: the rumor's ring slot and generation parity, transmits,
+  // length and the seq's low bits; the decoration is the rumor's, s.rdec).  tsum = {count, a
+  // lower bound of the tail's smallest
   // message length, a lower bound of its smallest key (lo, hi)}: emission picks from the head
   // only while a pick's key is below the tail's bound and every stop is decided by a length
   // the tail cannot fit; any other member takes the exact whole-queue path (emit_deep_wave_kernel).
-  uint4 *tail0, *tail1, *tail2;
+  uint64_t* tail0;  // the intent queue's tail: packed 8-B items
+  uint4 *tail1, *tail2;
   uint4* tsum;       // [n_loc][3]
   // Sealed tail prefix (a hint for the deferred path): tseal[l * 3 + q] = {m, B lo, B hi, -}:
   // every item of tail[0, m) has a key >= B.  The deferred path then refills the head from the
@@ -123,7 +152,45 @@ constexpr uint32_t kTailSlack = 192;  // tail row room past its capacity: one em
 // per-queue deep-queue fields by a select on q
 RSF_HD uint32_t tcap_of(const GCfg& c, uint32_t q) { return q == 0 ? c.tcap0 : q == 1 ? c.tcap1 : c.tcap2; }
 RSF_HD uint32_t tstride_of(const GCfg& c, uint32_t q) { return q == 0 ? c.tstride0 : q == 1 ? c.tstride1 : c.tstride2; }
-RSF_HD uint4* tail_of(const GState& s, uint32_t q) { return q == 0 ? s.tail0 : q == 1 ? s.tail1 : s.tail2; }
+// the query / event queues' 16-B tails (q = 1, 2); the intent queue's is s.tail0 (tail8)
+RSF_HD uint4* tail16(const GState& s, uint32_t q) { return q == 1 ? s.tail1 : s.tail2; }
+RSF_HD uint64_t* tail8(const GState& s, const GCfg& c, uint64_t l) { return s.tail0 + l * c.tstride0; }
+RSF_HD uint32_t rumor_generations(const GCfg& c) { return (uint32_t)((1ull << (32 - c.rbits)) - 2); }
+
+// The intent queue's packed tail item (8 B), low bits first:
+//   seq mod 2^25 | transmits (6 bits) << 25 | length (6 bits) << 31 | (rumor & rmask) << 37.
+// Intent messages are at most 28 bytes long (msg_len), transmits stay below the retransmit
+// limit (<= 64, checked at create), and rumor & rmask is the ring slot plus the generation's
+// parity (rbits + 1 <= 27 bits, checked at create).  Unpacking rebuilds
+//   * the rumor id from the parity: only the current generation and the one before hold live
+//     items (the ring's wrap expires the older one first, expire_kernel), so the id's
+//     generation is `gen` if the parities agree, else gen - 1;
+//   * the seq from the queue's next seq: every queued item is older, and an item whose age
+//     (next seq - seq) reaches 2^24 insertions is flagged (RSF_E_DEEP_INVARIANT) by the
+//     QueueChecker's and the ring expiry's passes, long before the 2^25 window could alias;
+//   * the decoration, which is the rumor's (s.rdec), only when the item enters the head.
+constexpr uint32_t kTailSeqBits = 25;
+constexpr uint32_t kTailSeqMask = (1u << kTailSeqBits) - 1;
+constexpr uint32_t kTailAgeFlag = 1u << 24;
+constexpr uint32_t kDecLookup = 0xFFFFFFFCu;  // a decoration still to be read from s.rdec
+RSF_HD uint64_t tail_pack(const GCfg& c, uint32_t rid, uint32_t seq, uint32_t tl) {
+  return (uint64_t)(seq & kTailSeqMask) | ((uint64_t)(tl & 0x3F) << 25) | ((uint64_t)((tl >> 16) & 0x3F) << 31) |
+         ((uint64_t)(rid & c.rmask) << 37);
+}
+RSF_HD uint32_t tail_seq(uint64_t x, uint32_t nseq) { return nseq - ((nseq - (uint32_t)x) & kTailSeqMask); }
+RSF_HD uint32_t tail_tl(uint64_t x) { return ((uint32_t)(x >> 25) & 0x3F) | (((uint32_t)(x >> 31) & 0x3F) << 16); }
+// gen: the generation the rebuild is relative to (the newest whose items may be queued)
+RSF_HD uint32_t tail_rid(const GCfg& c, uint64_t x, uint32_t gen) {
+  const uint32_t sl = (uint32_t)(x >> 37);
+  const uint32_t par = (sl >> c.rbits) & 1u;
+  const uint32_t g = par == (gen & 1u) ? gen : (gen == 0 ? rumor_generations(c) - 1 : gen - 1);
+  return (g << c.rbits) | (sl & ((1u << c.rbits) - 1));
+}
+// the unpacked form of the 16-B items (decoration kDecLookup)
+RSF_HD uint4 tail_unpack(const GCfg& c, uint64_t x, uint32_t nseq) {
+  return make_uint4(tail_rid(c, x, c.gen), tail_seq(x, nseq), tail_tl(x), kDecLookup);
+}
+RSF_HD bool tail_age_over(uint64_t x, uint32_t nseq) { return ((nseq - (uint32_t)x) & kTailSeqMask) >= kTailAgeFlag; }
 constexpr uint32_t kPend = 128;  // pending entries per member (two per lane of a wave)
 // The merge leaves a member at most kPendMerge entries, so the round's originations and
 // refutations (at most 1 + max_refute <= 5 per member) append without applying the list
@@ -233,7 +300,7 @@ __device__ __forceinline__ uint32_t vkind(uint32_t meta) { return (meta >> 8) & 
 __device__ __forceinline__ uint32_t vmeta(uint32_t status, uint32_t kind) { return status | (kind << 8); }
 
 // upsert_intent (base.rs:1797-1828)
-__device__ __forceinline__ bool upsert_intent(ViewE* e, uint32_t kind, uint64_t L, uint32_t now) {
+__device__ __forceinline__ bool upsert_intent(ViewS* e, uint32_t kind, uint64_t L, uint32_t now) {
   ViewE v = *e;
   if (vkind(v.meta) == RSF_KIND_UNKNOWN || L > v.ltime) {
     v.ltime = L;
@@ -269,7 +336,7 @@ __device__ __forceinline__ int hv_join_intent(ViewE& v, MRegs& r, uint64_t L, ui
   }
   return upsert_intent_v(v, RSF_KIND_INTENT_JOIN, L, now) ? RSF_F_REBROADCAST : 0;
 }
-__device__ __forceinline__ int h_join_intent(ViewE* e, MRegs& r, uint64_t L, uint32_t now) {
+__device__ __forceinline__ int h_join_intent(ViewS* e, MRegs& r, uint64_t L, uint32_t now) {
   ViewE v = *e;
   int f = hv_join_intent(v, r, L, now);
   *e = v;
@@ -317,7 +384,7 @@ __device__ __forceinline__ int hv_leave_intent(ViewE& v, MRegs& r, uint32_t subj
   }
   return f;
 }
-__device__ __forceinline__ int h_leave_intent(ViewE* e, MRegs& r, uint32_t subj, uint64_t L, bool prune,
+__device__ __forceinline__ int h_leave_intent(ViewS* e, MRegs& r, uint32_t subj, uint64_t L, bool prune,
                                               uint64_t& refute, uint32_t now) {
   ViewE v = *e;
   int f = hv_leave_intent(v, r, subj, L, prune, refute, now);
@@ -326,7 +393,7 @@ __device__ __forceinline__ int h_leave_intent(ViewE* e, MRegs& r, uint32_t subj,
 }
 
 // handle_node_join (base.rs:1167-1298)
-__device__ __forceinline__ int h_node_join(ViewE* e, MRegs& r, uint32_t subj) {
+__device__ __forceinline__ int h_node_join(ViewS* e, MRegs& r, uint32_t subj) {
   ViewE v = *e;
   uint32_t kind = vkind(v.meta);
   v.t = 0;  // leave_time: None (base.rs:1226, 1265)
@@ -349,14 +416,14 @@ __device__ __forceinline__ int h_node_join(ViewE* e, MRegs& r, uint32_t subj) {
 }
 
 // handle_node_update (base.rs:1532-1583): a member with state gets the Update event
-__device__ __forceinline__ int h_node_update(const ViewE* e, MRegs& r, uint32_t subj) {
-  if (vkind(e->meta) != RSF_KIND_KNOWN) return 0;
+__device__ __forceinline__ int h_node_update(const ViewS* e, MRegs& r, uint32_t subj) {
+  if (vkind(ViewE(*e).meta) != RSF_KIND_KNOWN) return 0;
   r.digest = digest_mix(r.digest, kDigMember | ((uint64_t)kEvUpdate << 32) | subj);
   return RSF_F_MEMBER_EVENT;
 }
 
 // handle_node_leave (base.rs:1339-1407)
-__device__ __forceinline__ int h_node_leave(ViewE* e, MRegs& r, uint32_t subj, uint32_t now) {
+__device__ __forceinline__ int h_node_leave(ViewS* e, MRegs& r, uint32_t subj, uint32_t now) {
   ViewE v = *e;
   if (vkind(v.meta) != RSF_KIND_KNOWN) return 0;
   uint32_t st = vstatus(v.meta), ev;
@@ -502,10 +569,10 @@ __device__ __forceinline__ void tail_append_serial(const GCfg& c, const GState& 
                                                    uint32_t dec, uint32_t seq, uint32_t tl) {
   // (plain scalars, not a uint4 local: HIP's vector type is a union, which keeps a modified
   // copy out of registers)
-  uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
   const uint4 sm = s.tsum[l * 3 + q];
   const uint32_t cnt = sm.x;
-  t[cnt] = make_uint4(rid, seq, tl, dec);
+  if (q == 0) tail8(s, c, l)[cnt] = tail_pack(c, rid, seq, tl);
+  else (tail16(s, q) + l * tstride_of(c, q))[cnt] = make_uint4(rid, seq, tl, dec);
   const uint64_t k = tlq_key(tl & 0xFFFF, tl >> 16, seq), mk = ((uint64_t)sm.w << 32) | sm.z;
   const uint64_t nk = k < mk ? k : mk;
   s.tsum[l * 3 + q] = make_uint4(cnt + 1, min(sm.y, tl >> 16), (uint32_t)nk, (uint32_t)(nk >> 32));
@@ -518,18 +585,33 @@ __device__ __forceinline__ bool tail_prune_serial(const GCfg& c, const GState& s
   const uint4 sm = s.tsum[l * 3 + q];
   const uint32_t cnt = sm.x;
   if (cnt <= tcap_of(c, q)) return false;
-  uint4* const t = tail_of(s, q) + l * tstride_of(c, q);
   uint32_t ti = 0;
   uint64_t tk = 0;
-  for (uint32_t i = 0; i < cnt; ++i) {
-    const uint4 e = t[i];
-    const uint64_t x = tlq_key(e.z & 0xFFFF, e.z >> 16, e.y);
-    if (x >= tk) {
-      tk = x;
-      ti = i;
+  if (q == 0) {
+    uint64_t* const t = tail8(s, c, l);
+    const uint32_t nseq = s.q_next_seq[l * 3];  // (every tail item is older)
+    for (uint32_t i = 0; i < cnt; ++i) {
+      const uint64_t e = t[i];
+      const uint32_t tl = tail_tl(e);
+      const uint64_t x = tlq_key(tl & 0xFFFF, tl >> 16, tail_seq(e, nseq));
+      if (x >= tk) {
+        tk = x;
+        ti = i;
+      }
     }
+    t[ti] = t[cnt - 1];
+  } else {
+    uint4* const t = tail16(s, q) + l * tstride_of(c, q);
+    for (uint32_t i = 0; i < cnt; ++i) {
+      const uint4 e = t[i];
+      const uint64_t x = tlq_key(e.z & 0xFFFF, e.z >> 16, e.y);
+      if (x >= tk) {
+        tk = x;
+        ti = i;
+      }
+    }
+    t[ti] = t[cnt - 1];
   }
-  t[ti] = t[cnt - 1];
   s.tsum[l * 3 + q] = make_uint4(cnt - 1, sm.y, sm.z, sm.w);
   s.tseal[l * 3 + q].x = 0u;  // an item moved into the sealed prefix: no seal
   return true;
