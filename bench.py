@@ -255,6 +255,26 @@ def model_point(args, rank, world, members):
     return out
 
 
+def regime_point(args, rank, world, members):
+    """configs[2]'s per-GPU shard (2M members) in the same reference queue regime as the line,
+    same box, same call: a labelled point beside the configs[1] headline."""
+    from bench_gossip import run_gossip
+    a = argparse.Namespace(**vars(args))
+    a.members = members
+    torch.cuda.empty_cache()
+    r = run_gossip(a, rank, world)
+    keep = ["value", "unit", "ms_per_step", "merges_per_s", "records_per_round_per_gpu", "queue_pruned_per_round",
+            "error_members", "cub_canaries_intact", "phases_ms_per_round", "queue_regime",
+            "deep_path_members_per_round"]
+    out = {"metric": r["metric"], "steps": args.steps, "warmup": args.warmup, **{k: r[k] for k in keep},
+           "config": r["config"],
+           "what": "BASELINE configs[2]'s per-GPU shard (2M members; 16M over 8 GPUs) in the reference's queue "
+                   "regime, one GPU (the multi-GPU exchange is not in this point)"}
+    out["roofline"] = {k: r["roofline"][k] for k in ["bound", "achieved", "peak", "unit", "frac", "kernel",
+                                                      "bytes_per_launch", "avg_launch_ms"]}
+    return out
+
+
 def c1_leg(rounds=1000, n=1000, with_gpu=True):
     """BASELINE configs[0] / SURVEY §8(d) C1: Vivaldi over a 1k-node synthetic RTT matrix on
     the CPU path -- the oracle (the C restatement of CoordinateClient::update; the Rust
@@ -346,6 +366,9 @@ def main():
                     help="gossip: untimed rounds before warmup (default 330 in the queue regime: queues at their "
                          "steady state past two checker ticks; 12 with bounded queues: saturated)")
     ap.add_argument("--no-vivaldi", action="store_true", help="gossip: skip the Vivaldi leg of the line")
+    ap.add_argument("--ring-rounds", type=int, default=None,
+                    help="gossip: rounds of rumor blocks the rumor ring holds per generation (default: the whole "
+                         "run in the queue regime, so nothing expires)")
     ap.add_argument("--refresh-every", type=int, default=1,
                     help="vivaldi, N>1: all-gather the coordinate table after every R-th round (C5: 1 and 8)")
     ap.add_argument("--vivaldi-exchange", choices=["targeted", "allgather"], default="targeted",
@@ -416,6 +439,8 @@ def main():
         if world == 1 and not args.no_extra_points:
             # labelled model points, same box, same call: the bounded 64-slot queue (prunes on
             # insert, which the reference never does) at configs[1] and at configs[2]'s 2M shard
+            if args.queue_depth and args.members == 1_000_000:
+                res["configs2_shard_regime"] = regime_point(args, rank, world, 2_000_000)
             pts = [model_point(args, rank, world, 1_000_000), model_point(args, rank, world, 2_000_000)]
             e64 = pts[0]["phases_ms_per_round"].get("emit_kernel")
             edeep = res["phases_ms_per_round"].get("emit_kernel")

@@ -5,7 +5,10 @@ and a flood of 100 user events (cc 50%) + 10 queries per round, event/query buff
 
 Two passes over the same seeded workload (the engine is deterministic, so both
 passes compute identical rounds):
-  timed    : --warmup + --steps rounds, the round only -> node-rounds/s
+  timed    : --warmup + --steps rounds, the round only -> node-rounds/s (by default in the
+             reference's queue regime: --queue-depth for all three queues, the in-round
+             staggered QueueChecker every --check-every rounds, no ring expiry; with
+             --queue-depth 0 the bounded 64-slot model)
   delivery : the same rounds plus a dissemination tail with the delivery log on
              (UserEvents handed to the application, base.rs:831-835): for every
              user event originated in the timed window, how many live members
@@ -28,22 +31,35 @@ EVENTS, QUERIES = int(os.environ.get("RSF_CHURN_EVENTS", 100)), int(os.environ.g
 TAIL = 24  # dissemination rounds after the timed window (delivery pass)
 
 
-def churn_cfg(n, s):
+MAX_QUEUE_DEPTH, QUEUE_DEPTH_WARNING = 4096, 128  # options.rs:512 (max_queue_depth), the checker's warning
+
+
+def churn_cfg(n, s, depth=0, rounds_total=64):
+    """depth > 64: the reference's queue regime -- all three queues that deep (register head +
+    HBM tail), pruned only by the staggered QueueChecker, and the rumor ring sized so nothing
+    expires in `rounds_total` rounds; 0: the bounded 64-slot model with a 2^16-slot ring."""
     from ruserf_amd.gossip import GossipConfig
+    ring = 1 << 16
+    if depth:
+        per_round = s * 4 + EVENTS + QUERIES
+        ring = 1 << max(16, (per_round * rounds_total - 1).bit_length())
     return GossipConfig(n_members=n, n_subjects=s, queue_cap=64, event_buffer_size=512, query_buffer_size=512,
                         slot_k=16, fanout=3, gossip_limit=1400, gossip_overhead=2, retransmit_mult=4, max_refute=4,
-                        max_rumors=1 << 16, seed=SEED)
+                        max_rumors=ring, seed=SEED, queue_depth=(depth, depth, depth) if depth else None)
 
 
-def _engine(n, rounds_total):
+def _engine(n, rounds_total, depth=0, check_every=0):
     from ruserf_amd import workload as W
     from ruserf_amd.gossip import GossipEngine
     subj, acts, ml = W.churn_workload(n, rounds_total, events_per_round=EVENTS, queries_per_round=QUERIES,
                                       seed=SEED)
-    eng = GossipEngine(churn_cfg(n, len(subj)), device=torch.cuda.current_device())
+    eng = GossipEngine(churn_cfg(n, len(subj), depth, rounds_total), device=torch.cuda.current_device())
     eng.set_stream(torch.cuda.current_stream().cuda_stream)
     eng.set_subjects(subj)
     eng.init_views(*W.initial_views(len(subj)))
+    if depth and check_every:
+        # each member's QueueChecker on its own phase (member id mod check_every), in the rounds
+        eng.set_checker(check_every, MAX_QUEUE_DEPTH, 0, QUEUE_DEPTH_WARNING)
     return eng, subj, acts, ml
 
 
@@ -53,8 +69,10 @@ def run_churn(args, rank, world):
     n = args.members or N_DEFAULT
     timed_rounds = args.warmup + args.steps
     rounds_total = timed_rounds + TAIL
+    depth = getattr(args, "queue_depth", 0) or 0
+    check_every = (getattr(args, "check_every", 0) or 0) if depth else 0
     # ---- timed pass
-    eng, subj, acts, ml = _engine(n, rounds_total)
+    eng, subj, acts, ml = _engine(n, rounds_total, depth, check_every)
     for t in range(args.warmup):
         eng.round(t, ml[t], acts[t])
     torch.cuda.synchronize()
@@ -72,13 +90,25 @@ def run_churn(args, rank, world):
     phase_ms, nr = eng.phase_times()
     merged = eng.merged_total() - merged0
     eng.set_profiling(False)
+    regime = None
+    if depth:
+        ql = eng.queue_lengths().astype(np.int64)
+        regime = {"what": "the reference's queue regime: all three queues " + str(depth) + " deep, pruned only by "
+                          "each member's QueueChecker (every " + str(check_every) + " rounds on its own phase, to "
+                          + str(MAX_QUEUE_DEPTH) + "), no rumor-ring expiry",
+                  "queue_items_after_window": {q: {"mean": float(ql[:, i].mean()), "max": int(ql[:, i].max())}
+                                               for i, q in enumerate(["intent", "query", "event"])},
+                  "bounded_pruned_total": int(eng.pruned().astype(np.uint64).sum()),
+                  "expired_total": int(eng.expired().astype(np.uint64).sum()),
+                  "deferred_per_round_by_class": dict(zip(["tiny", "small", "middle", "full"],
+                                                          (eng.deep_class_stats() / max(1, timed_rounds)).tolist()))}
     eng.close()
     if world > 1:  # independent replicas (configs[3] is a one-GPU cluster)
         t_ = torch.tensor([wall], dtype=torch.float64, device="cuda")
         torch.distributed.all_reduce(t_, op=torch.distributed.ReduceOp.MAX)
         wall = float(t_[0])
     # ---- delivery pass (untimed), the same rounds with the delivery log
-    eng, subj, acts, ml = _engine(n, rounds_total)
+    eng, subj, acts, ml = _engine(n, rounds_total, depth, check_every)
     eng.set_delivery_log(768)
     # member events: one MemberEventCoalescer per member over its stream, a quantum per round
     mcoal = MemberEventCoalescer(n, len(subj))
@@ -153,9 +183,13 @@ def run_churn(args, rank, world):
         "scaling": "weak",
         "config": {"workload": f"BASELINE configs[3]: {n} members, 1% churn ({len(subj)} subjects fail or leave, "
                                f"25% of failures force-left with prune), {EVENTS} user events (cc 50%) + {QUERIES} "
-                               f"queries per round, event/query buffers 512, retransmit mult 4, fanout 3",
-                   "members": n, "members_per_gpu": n, "parallelism": "one cluster per GPU"
-                   + (f" ({world} independent replicas)" if world > 1 else "")},
+                               f"queries per round, event/query buffers 512, retransmit mult 4, fanout 3, "
+                               + (f"the reference's queue regime (queues {depth} deep, staggered checker every "
+                                  f"{check_every} rounds to {MAX_QUEUE_DEPTH})" if depth else
+                                  "bounded 64-slot queues (model point)"),
+                   "members": n, "members_per_gpu": n, "queue_depth": depth or 64,
+                   "parallelism": "one cluster per GPU" + (f" ({world} independent replicas)" if world > 1 else "")},
+        "queue_regime": regime,
         "phases_ms_per_round": dict(zip(names, avg)),
         "merges_per_s": merged / wall, "records_per_round_per_gpu": records,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -190,7 +224,11 @@ def cpu_baseline_churn(args, seconds_target=10.0):
     rounds_total = args.warmup + args.steps + TAIL
     subj, acts, ml = W.churn_workload(n, rounds_total, events_per_round=EVENTS, queries_per_round=QUERIES,
                                       seed=SEED)
-    w = H.oracle_world(churn_cfg(n, len(subj)), subj, W.initial_views(len(subj)))
+    depth = getattr(args, "queue_depth", 0) or 0
+    check_every = (getattr(args, "check_every", 0) or 0) if depth else 0
+    w = H.oracle_world(churn_cfg(n, len(subj), depth, rounds_total), subj, W.initial_views(len(subj)))
+    if depth and check_every:
+        H.L.orc_world_set_checker(C.byref(w), MAX_QUEUE_DEPTH, 0, QUEUE_DEPTH_WARNING, check_every)
     t = 0
     for _ in range(args.warmup):
         H.oracle_round(w, t, ml[t], acts[t], threads=th)
@@ -205,4 +243,4 @@ def cpu_baseline_churn(args, seconds_target=10.0):
     H.L.orc_world_free(C.byref(w))
     return {"value": n * done / spent, "unit": "node-rounds/s", "cores": th, "kind": "port",
             "sample": f"oracle configs[3] rounds {args.warmup}..{t - 1} ({done} rounds, {spent:.1f}s) of the same "
-                      f"workload on {th} threads; {cpu_info()}"}
+                      f"workload and queue configuration (depth {depth or 64}) on {th} threads; {cpu_info()}"}

@@ -30,7 +30,8 @@ PRUNE_FRAC = float(os.environ.get("RSF_PRUNE_FRAC", 0.1))
 HBM_PEAK_GBS = 8000.0
 
 
-def gossip_cfg(n_total, rounds_total, world, shard=None, queue_cap=64, queue_depth=0, ring_rounds=64):
+def gossip_cfg(n_total, rounds_total, world, shard=None, queue_cap=64, queue_depth=0, ring_rounds=64,
+               retransmit_mult=4):
     """queue_depth > queue_cap: the intent queue (the only one this workload fills) is that
     deep -- register head + HBM tail, pruned only by the QueueChecker as the reference's
     (max_queue_depth 4096); the query / event queues stay at queue_cap (always empty here).
@@ -43,7 +44,7 @@ def gossip_cfg(n_total, rounds_total, world, shard=None, queue_cap=64, queue_dep
     ring = 1 << max(10, (per_round * max(64, ring_rounds) - 1).bit_length())
     return GossipConfig(n_members=n_total, n_subjects=SUBJECTS, shard=shard, queue_cap=queue_cap, event_buffer_size=512,
                         query_buffer_size=512, slot_k=1, fanout=3, gossip_limit=8 * 24, gossip_overhead=2,
-                        retransmit_mult=4, max_refute=4, max_rumors=ring, seed=SEED,
+                        retransmit_mult=retransmit_mult, max_refute=4, max_rumors=ring, seed=SEED,
                         queue_depth=(queue_depth, 0, 0) if queue_depth > queue_cap else None)
 
 
@@ -88,8 +89,11 @@ def run_gossip(args, rank, world):
     check_every = getattr(args, "check_every", 0) or 0
     settle = (SETTLE_STEADY if check_every else SETTLE_ROUNDS) if args.settle is None else args.settle
     rounds_total = settle + args.warmup + args.steps
-    cfg = gossip_cfg(n, rounds_total, world, queue_cap=args.queue_cap, queue_depth=depth,
-                     ring_rounds=rounds_total if check_every else 64)
+    # the rumor ring: sized for the whole run in the queue regime (no queued item expires, as in
+    # the reference); --ring-rounds overrides it (an A/B of the merge's rumor-body gather against
+    # a ring small enough for the MALL -- items then expire, counted in expired_whole_run)
+    ring_rounds = getattr(args, "ring_rounds", None) or (rounds_total if check_every else 64)
+    cfg = gossip_cfg(n, rounds_total, world, queue_cap=args.queue_cap, queue_depth=depth, ring_rounds=ring_rounds)
     subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED, prune_frac=PRUNE_FRAC)
     views = W.initial_views(SUBJECTS)
     stream = torch.cuda.current_stream()
@@ -175,6 +179,7 @@ def run_gossip(args, rank, world):
                   "pruned_per_round": float(cst["pruned"][0]) / args.steps,
                   "members_over_warning_in_window": int(cst["warn"][0]),
                   "expired_whole_run": int(eng.expired().sum()),
+                  "rumor_ring_slots": int(cfg.max_rumors), "ring_rounds": int(ring_rounds),
                   "deferred_per_round_by_class": dict(zip(["tiny", "small", "middle", "full"],
                                                           ((eng.deep_class_stats() - cls0) / args.steps).tolist()))
                   if depth else None}
@@ -259,30 +264,40 @@ def run_gossip(args, rank, world):
     }
 
 
-def cpu_baseline_gossip_deep(args, seconds_target=12.0, n=40_000, settle=60):
-    """The oracle's round in the same queue regime as the line (the intent queue as deep as
-    the engine's, no prune between ticks) on a bounded sample: n members settled `settle`
-    rounds (queues ~24 items a round deep by then), then timed on all the box's threads
-    and on one.  The oracle's queue is a sorted array (insert O(depth)), as memberlist's
-    TransmitLimitedQueue is a btree of O(log depth): the CPU figure is the restatement's."""
+def cpu_baseline_gossip_deep(args, seconds_target=12.0, n=5_000):
+    """The oracle's round in the line's queue regime and at its occupancy, on a bounded sample:
+    n members, the intent queue as deep as the engine's, the staggered QueueChecker (every
+    CHECK_EVERY rounds to MAX_QUEUE_DEPTH) and the ring sized so nothing expires, settled
+    SETTLE_STEADY rounds -- as the GPU line -- so the queues hold 4-6k items; then timed on all
+    the box's threads and on one.  The retransmit limit is the line's (28 = 4 x 7 digits at
+    1M members): at n members the multiplier is scaled to give the same limit.  The oracle's
+    queue is an array scanned per pick (memberlist's TransmitLimitedQueue is a btree); the CPU
+    figure is the restatement's."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import gossip_harness as H  # test infrastructure: checker / CPU baseline only
     from bench import cpu_info, cpu_threads
     from ruserf_amd import workload as W
     th = cpu_threads()
+    settle = SETTLE_STEADY
     rounds_total = settle + 72
-    cfg = gossip_cfg(n, rounds_total, 1, queue_cap=64, queue_depth=args.queue_depth, ring_rounds=rounds_total)
+    L = H.L
+    digits = lambda x: len(str(int(x)))  # noqa: E731  (ceil(log10(x + 1)) for x >= 1)
+    limit = 4 * digits(max(1, args.members))
+    mult = max(1, round(limit / digits(n)))
+    cfg = gossip_cfg(n, rounds_total, 1, queue_cap=64, queue_depth=args.queue_depth, ring_rounds=rounds_total,
+                     retransmit_mult=mult)
     subj, acts, ml = W.intents_workload(n, SUBJECTS, rounds_total, rate=0.01, seed=SEED, prune_frac=PRUNE_FRAC)
     w = H.oracle_world(cfg, subj, W.initial_views(SUBJECTS))
     t = 0
-
-    H.L.orc_world_set_checker(C.byref(w), MAX_QUEUE_DEPTH, 0, QUEUE_DEPTH_WARNING, CHECK_EVERY)
+    L.orc_world_set_checker(C.byref(w), MAX_QUEUE_DEPTH, 0, QUEUE_DEPTH_WARNING, CHECK_EVERY)
 
     def rnd(threads):
         H.oracle_round(w, t, ml[t], acts[t], threads=threads)
+    t_settle = time.perf_counter()
     for _ in range(settle):
         rnd(th)
         t += 1
+    t_settle = time.perf_counter() - t_settle
 
     def timed(threads, budget, max_rounds):
         nonlocal t
@@ -294,16 +309,19 @@ def cpu_baseline_gossip_deep(args, seconds_target=12.0, n=40_000, settle=60):
             done += 1
             t += 1
         return done, spent
-    done_mt, spent_mt = timed(th, seconds_target, 64)
-    done_1, spent_1 = timed(1, seconds_target / 2, 3)
-    width = H.world_width(w)
-    H.L.orc_world_free(C.byref(w))
+    done_mt, spent_mt = timed(th, seconds_target, 60)
+    done_1, spent_1 = timed(1, seconds_target / 2, 10)
+    hw = H.world_width(w)
+    ql = (H.O.arr(w.q_rumor, n * 3 * w.qcap, np.uint32).reshape(n, 3, w.qcap)[:, 0, :hw] != 0xFFFFFFFF).sum(axis=1)
+    L.orc_world_free(C.byref(w))
     return {"value": n * done_mt / spent_mt, "unit": "node-rounds/s", "cores": th, "kind": "port",
             "value_1thread": n * done_1 / spent_1,
             "cpu_model": cpu_info(),
-            "sample": f"oracle gossip rounds (orc_world_round_mt), {n} members, {SUBJECTS} subjects, the same workload "
-                      f"and queue depth ({cfg.depths()[0]}), settled {settle} rounds (deepest queue {width} items), the staggered checker ticks "
-                      f"included; "
+            "queue_items": {"mean": float(ql.mean()), "p99": int(np.percentile(ql, 99)), "max": int(ql.max())},
+            "sample": f"oracle gossip rounds (orc_world_round_mt), {n} members, {SUBJECTS} subjects, the line's workload, "
+                      f"queue regime and depth ({cfg.depths()[0]}; staggered checker every {CHECK_EVERY} rounds to "
+                      f"{MAX_QUEUE_DEPTH}; retransmit limit {limit}), settled {settle} rounds ({t_settle:.0f}s, not "
+                      f"timed) to intent queues of mean {ql.mean():.0f} / p99 {np.percentile(ql, 99):.0f} items; "
                       f"{done_mt} rounds on {th} threads ({spent_mt:.1f}s), {done_1} rounds on 1 thread "
                       f"({spent_1:.1f}s); {cpu_info()}"}
 

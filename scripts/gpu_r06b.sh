@@ -7,3 +7,5 @@ bash $S pytest_gpu 1100 python -u -m pytest tests -m gpu -v -s --timeout 1500 --
 bash scripts/ab.sh abx 2 gossip old default || exit 1
 bash $S bench_2m 600 python -u bench.py --workload gossip --members 2000000 --steps 20 --warmup 3 --no-cpu-baseline --no-vivaldi --no-extra-points
 grep -h "passed\|failed" gpurun_out/pytest_gpu.log | tail -2
+bash $S bench_churn 600 python -u bench.py --workload churn --steps 20 --warmup 3 --no-cpu-baseline
+grep -h '^{' gpurun_out/bench_churn.log | cut -c1-600

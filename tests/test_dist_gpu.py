@@ -122,18 +122,32 @@ def test_one_rank_rccl_equal_one_context(exchange):
 
 
 CFG2_N, CFG2_ROUNDS = 2_000_000, 8
+CFG2_REGIME_ROUNDS = 330  # the bench's settle: queues at their steady state, the second checker pass pruning
 CFG2_SAMPLE = [(0, 64), (CFG2_N // 2 - 32, 64), (CFG2_N - 64, 64)]
 
 
-def _cfg2():
+def _cfg2(regime=False):
     """BASELINE configs[2]'s per-GPU shard: 2M members, 4096 tracked subjects, the bench's
-    gossip configuration (bench_gossip.gossip_cfg) and its 1% intent workload."""
+    gossip configuration (bench_gossip.gossip_cfg) and its 1% intent workload.  regime: the
+    bench's reference queue regime (intent queue DEFAULT_QUEUE_DEPTH deep, the staggered
+    checker, the ring sized so nothing expires) over CFG2_REGIME_ROUNDS rounds."""
+    import bench as BB
     import bench_gossip as B
     from ruserf_amd import workload as W
-    cfg = B.gossip_cfg(CFG2_N, CFG2_ROUNDS, 1)
-    subj, acts, ml = W.intents_workload(CFG2_N, B.SUBJECTS, CFG2_ROUNDS, rate=0.01, seed=B.SEED,
+    rounds = CFG2_REGIME_ROUNDS if regime else CFG2_ROUNDS
+    if regime:
+        cfg = B.gossip_cfg(CFG2_N, rounds, 1, queue_depth=BB.DEFAULT_QUEUE_DEPTH, ring_rounds=rounds)
+    else:
+        cfg = B.gossip_cfg(CFG2_N, rounds, 1)
+    subj, acts, ml = W.intents_workload(CFG2_N, B.SUBJECTS, rounds, rate=0.01, seed=B.SEED,
                                         prune_frac=B.PRUNE_FRAC)
     return cfg, subj, acts, ml
+
+
+def _cfg2_checker(eng, regime):
+    import bench_gossip as B
+    if regime:
+        eng.set_checker(B.CHECK_EVERY, B.MAX_QUEUE_DEPTH, 0, B.QUEUE_DEPTH_WARNING)
 
 
 def _cfg2_record(eng):
@@ -141,6 +155,7 @@ def _cfg2_record(eng):
     m = eng.members()
     rec = {k: m[k].copy() for k in ["clock", "event_clock", "query_clock", "digest", "err"]}
     rec["pruned"] = eng.pruned()
+    rec["expired"] = eng.expired()
     rec["merged"] = np.array([eng.merged_total()], np.uint64)
     for i, (r0, cnt) in enumerate(CFG2_SAMPLE):
         lt, st, kd, tm = eng.view(with_time=True, rows=(r0, cnt))
@@ -148,7 +163,7 @@ def _cfg2_record(eng):
     return rec
 
 
-def _worker_cfg2(port, q):
+def _worker_cfg2(port, q, regime=False):
     """The configs[2] shard through ShardedGossip on one RCCL rank (the multi-GPU code path:
     rumor-block all-reduce, bucket emission, exchange, merge from the buckets)."""
     import sys
@@ -160,18 +175,64 @@ def _worker_cfg2(port, q):
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     from ruserf_amd import workload as W
     from ruserf_amd.dist import ShardedGossip
-    cfg, subj, acts, ml = _cfg2()
+    cfg, subj, acts, ml = _cfg2(regime)
     sg = ShardedGossip(cfg, 0, 1, device=0)
     sg.eng.set_subjects(subj)
     sg.eng.init_views(*W.initial_views(len(subj)))
-    for t in range(CFG2_ROUNDS):
+    _cfg2_checker(sg.eng, regime)
+    for t in range(len(acts)):
         sg.round(t, ml[t], acts[t])
     torch.cuda.synchronize()
     rec = _cfg2_record(sg.eng)
+    if regime:
+        rec["queue_lengths"] = sg.eng.queue_lengths()[:, 0].copy()
+        rec["checker"] = np.array(sum((list(v) for v in sg.eng.checker_stats().values()), []), np.uint64)
     rec["exchange_ok"] = np.array([sg.buckets and sg.check()])
     sg.eng.close()
     dist.destroy_process_group()
     q.put(rec)
+
+
+def test_configs2_shard_regime_rccl_equal_one_context():
+    """BASELINE configs[2]'s per-GPU shard (2M members x 4096 subjects) in the bench's reference
+    queue regime -- the intent queue 8 704 deep (packed 8-B tail items, 12-B view entries: the
+    regime fits one MI355X at 2M members), each member's QueueChecker pruning to 4096 every
+    150 rounds on its own phase, 330 rounds so the second pass prunes queues of 4-8k items --
+    through the multi-GPU code path on one RCCL rank, equal to the single-context round: every
+    member's clocks, digest, error bits, prunes and expiries, its intent queue length, the
+    checker's counts, the records merged and sampled view rows; nothing dropped between ticks,
+    nothing expired.  (The rank runs first, in its own process, then the single context.)"""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from ruserf_amd import gossip as G
+    from ruserf_amd import workload as W
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + os.getpid() % 200
+    p = ctx.Process(target=_worker_cfg2, args=(port, q, True))
+    p.start()
+    got = q.get(timeout=900)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert bool(got.pop("exchange_ok")[0])
+    cfg, subj, acts, ml = _cfg2(True)
+    one = G.GossipEngine(cfg)
+    one.set_subjects(subj)
+    one.init_views(*W.initial_views(len(subj)))
+    _cfg2_checker(one, True)
+    for t in range(len(acts)):
+        one.round(t, ml[t], acts[t])
+    exp = _cfg2_record(one)
+    exp["queue_lengths"] = one.queue_lengths()[:, 0].copy()
+    exp["checker"] = np.array(sum((list(v) for v in one.checker_stats().values()), []), np.uint64)
+    one.close()
+    for k in exp:
+        assert np.array_equal(got[k], exp[k]), k
+    ql = exp["queue_lengths"].astype(np.int64)
+    assert ql.mean() > 4096 and int(ql.max()) > 7000, (ql.mean(), ql.max())  # the regime's occupancy
+    assert int(exp["pruned"].sum()) == 0 and int(exp["expired"].sum()) == 0
+    assert np.all(exp["err"] == 0)
+    assert int(exp["checker"][6]) > 0  # the ticks pruned
 
 
 def test_configs2_shard_rccl_equal_one_context():
