@@ -988,7 +988,7 @@ __global__ void __launch_bounds__(256) ml_kernel(GCfg c, GState s, const rsf_ml_
       touched = true;
     }
     if (al && m != sm) {
-      ViewS* v = s.view + l * c.S + subj;
+      ViewS* v = vent(s, c, l, subj);
       if (ml[e].kind == RSF_ML_JOIN) {
         h_node_join(v, r, subj);
         snap_member(c, s, l, subj, true);
@@ -1049,7 +1049,7 @@ __device__ __forceinline__ void broadcast_join(const GCfg& c, const GState& s, u
                                                uint32_t rid) {
   uint32_t subj = (uint32_t)r.subj;
   witness(r.clock, L);
-  h_join_intent(s.view + l * c.S + subj, r, L, c.now);
+  h_join_intent(vent(s, c, l, subj), r, L, c.now);
   uint32_t len = msg_len(RSF_MSG_JOIN, L, 0, 0);
   put_rumor(c, s, rid, RSF_MSG_JOIN, 0, subj, L, 0, len);
   pend_push_serial(c, s, l, kQIntent, rid, subj, len, r);
@@ -1124,7 +1124,7 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
       }
       r.clock++;
       uint32_t subj = (uint32_t)r.subj;
-      mlog_intent(c, s, l, r.err, h_leave_intent(s.view + l * c.S + subj, r, subj, lt, false, ref, c.now), subj);
+      mlog_intent(c, s, l, r.err, h_leave_intent(vent(s, c, l, subj), r, subj, lt, false, ref, c.now), subj);
       uint32_t len = msg_len(RSF_MSG_LEAVE, lt, 0, 0);
       put_rumor(c, s, rid, RSF_MSG_LEAVE, 0, subj, lt, 0, len);
       pend_push_serial(c, s, l, kQIntent, rid, subj, len, r);
@@ -1133,7 +1133,7 @@ __global__ void __launch_bounds__(256) originate_kernel(GCfg c, GState s, const 
     case RSF_ACT_FORCE_LEAVE: {
       uint64_t lt = r.clock;
       bool prune = x.flags & 1;
-      int f = h_leave_intent(s.view + l * c.S + x.subject, r, x.subject, lt, prune, ref, c.now);
+      int f = h_leave_intent(vent(s, c, l, x.subject), r, x.subject, lt, prune, ref, c.now);
       mlog_intent(c, s, l, r.err, f, x.subject);
       if (f & RSF_F_REFUTE) push_refute(c, s, r, ref);
       uint32_t len = msg_len(RSF_MSG_LEAVE, lt, 0, 0);
@@ -1947,7 +1947,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
   r.err = shfl_u32(su, kSuErr);
   r.serf_state = (uint8_t)shfl_u32(su, kSuSerf);
   r.subj = (int32_t)shfl_u32(su, kSuSubj);
-  ViewS* vrow = s.view + l * c.S;
+  ViewS* vrow = vrow_of(s, c, l);
   MPROF_T(t_setup);
   MPROF_ADD(0, t_start, t_setup);
   const uint64_t vs = (uint64_t)st * stride;
@@ -2018,7 +2018,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
       ru = rumor_from_body(b, key);
     }
     ViewE pre{};
-    if (is_view) pre = vrow[dsub];  // issued beside the rumor-body load (a non-temporal load measured far slower)
+    if (is_view) pre = *view_at(vrow, dsub);  // issued beside the rumor-body load (a non-temporal load measured far slower)
     const uint32_t my_subj = is_view ? dsub : 0xFFFFFFFFu;
     // chains: previous / next record of the same subject in this chunk
     int prev = -1, next = -1;
@@ -2106,7 +2106,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
       }
       if (!ballot(!done)) break;
     }
-    if (next < 0 && is_view && dirty) vrow[my_subj] = v;  // last link writes the subject back
+    if (next < 0 && is_view && dirty) *view_at(vrow, my_subj) = v;  // last link writes the subject back
     if (chunk_max > r.clock) r.clock = chunk_max;
     MPROF_T(t_c2);
     MPROF_ADD(2, t_c1, t_c2);
@@ -2262,9 +2262,9 @@ __global__ void __launch_bounds__(256) pp_snapshot_kernel(GCfg c, GState s, cons
                                                           PPSlab sl) {
   const uint64_t p = blockIdx.x;
   const uint64_t l = pairs[p].sender - c.lo;
-  const ViewS* vsrc = s.view + l * c.S;
-  ViewS* vdst = sl.view + p * c.S;
-  for (uint32_t i = threadIdx.x; i < c.S; i += blockDim.x) vdst[i] = vsrc[i];
+  const uint4* vsrc = reinterpret_cast<const uint4*>(vrow_of(s, c, l));
+  uint4* vdst = reinterpret_cast<uint4*>(view_row(sl.view, c.vrow, p));
+  for (uint32_t i = threadIdx.x; i < c.vrow / 16; i += blockDim.x) vdst[i] = vsrc[i];
   for (uint32_t i = threadIdx.x; i < c.ebuf; i += blockDim.x) {
     sl.eb_ltime[p * c.ebuf + i] = s.eb_ltime[l * c.ebuf + i];
     sl.eb_cnt[p * c.ebuf + i] = s.eb_cnt[l * c.ebuf + i];
@@ -2302,19 +2302,19 @@ __global__ void __launch_bounds__(256) pp_merge_kernel(GCfg c, GState s, const r
   if (pel > 0) witness(r.eclock, pel - 1);
   if (pql > 0) witness(r.qclock, pql - 1);
   // ---- status_ltimes / left_members
-  const ViewS* sv = sl.view + p * c.S;
-  ViewS* vrow = s.view + l * c.S;
+  const ViewS* sv = view_row(sl.view, c.vrow, p);
+  ViewS* vrow = vrow_of(s, c, l);
   uint64_t c_leave = r.clock, c_join = r.clock;
   for (uint32_t base = 0; base < c.S; base += kWave) {
     const uint32_t subj = base + lane;
     const bool valid = subj < c.S;
     ViewE se{};
-    if (valid) se = sv[subj];
+    if (valid) se = *view_at(sv, subj);
     const bool known = valid && vkind(se.meta) == RSF_KIND_KNOWN;
     const bool left = known && vstatus(se.meta) == RSF_STATUS_LEFT;
     const bool join = known && !left;
     ViewE v{};
-    if (known) v = vrow[subj];
+    if (known) v = *view_at(vrow, subj);
     const uint64_t L = left ? se.ltime + 1 : se.ltime;
     const uint64_t incl = wave_inclusive_max_u64(left ? L + 1 : 0);
     const uint64_t excl = wave_shr1_u64(incl);
@@ -2329,7 +2329,7 @@ __global__ void __launch_bounds__(256) pp_merge_kernel(GCfg c, GState s, const r
       const uint32_t t0 = v.t;
       if (left) f = hv_leave_intent(v, rr, subj, L, false, ref, c.now);
       else f = hv_join_intent(v, rr, L, c.now);
-      if (v.ltime != lt0 || v.meta != mt0 || v.t != t0) vrow[subj] = v;
+      if (v.ltime != lt0 || v.meta != mt0 || v.t != t0) *view_at(vrow, subj) = v;
     }
     const uint64_t lmax = lane63_u64(incl);
     if (lmax > c_leave) c_leave = lmax;
@@ -2435,7 +2435,7 @@ __global__ void __launch_bounds__(256) reap_kernel(GCfg c, GState s, uint32_t no
   const uint64_t l = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   if (l >= c.n_loc) return;
   if (!s.alive[c.lo + l]) return;
-  ViewS* vrow = s.view + l * c.S;
+  ViewS* vrow = vrow_of(s, c, l);
   uint64_t dig = s.digest[l];
   const uint64_t d0 = dig;
   uint32_t lerr = 0;  // delivery-log overflow
@@ -2445,7 +2445,7 @@ __global__ void __launch_bounds__(256) reap_kernel(GCfg c, GState s, uint32_t no
     for (uint32_t base = 0; base < c.S; base += kWave) {
       const uint32_t subj = base + lane;
       ViewE v{};
-      if (subj < c.S) v = vrow[subj];
+      if (subj < c.S) v = *view_at(vrow, subj);
       // (stamps are kept mod 2^27: the age is exact below 2^27 rounds)
       const uint32_t kind = vkind(v.meta), st = vstatus(v.meta), age = (now - v.t) & kViewTMask;
       const bool known = subj < c.S && kind == RSF_KIND_KNOWN;
@@ -2453,7 +2453,7 @@ __global__ void __launch_bounds__(256) reap_kernel(GCfg c, GState s, uint32_t no
       const bool left = known && st == RSF_STATUS_LEFT && age > ts_to;
       const bool intent = subj < c.S && (kind == RSF_KIND_INTENT_JOIN || kind == RSF_KIND_INTENT_LEAVE) && age > in_to;
       const bool reap = pass == 0 ? failed : left;
-      if (reap || (pass == 0 && intent)) vrow[subj] = ViewE{0ull, 0u, 0u};  // erase_node / reap_intents
+      if (reap || (pass == 0 && intent)) *view_at(vrow, subj) = ViewE{0ull, 0u, 0u};  // erase_node / reap_intents
       if (pass == 0) any_left = any_left || ballot(left) != 0;
       uint64_t mm = ballot(reap);
       while (mm) {  // Reap member events, slot order
@@ -2480,16 +2480,16 @@ __global__ void __launch_bounds__(256) apply_kernel(GCfg c, GState s, const rsf_
   if (st >= en) return;
   MRegs r;
   load_regs(s, l, r);
-  ViewS* vrow = s.view + l * c.S;
+  ViewS* vrow = vrow_of(s, c, l);
   for (uint32_t i = st; i < en; ++i) {
     uint32_t k = order[i];
     rsf_msg x = msgs[k];
     uint64_t ref = 0;
     int f = 0;
     switch (x.type) {
-      case RSF_MSG_JOIN: f = h_join_intent(vrow + x.subject, r, x.ltime, c.now); break;
+      case RSF_MSG_JOIN: f = h_join_intent(view_at(vrow, x.subject), r, x.ltime, c.now); break;
       case RSF_MSG_LEAVE:
-        f = h_leave_intent(vrow + x.subject, r, x.subject, x.ltime, x.flags & 1, ref, c.now);
+        f = h_leave_intent(view_at(vrow, x.subject), r, x.subject, x.ltime, x.flags & 1, ref, c.now);
         mlog_intent(c, s, l, r.err, f, x.subject);
         break;
       case RSF_MSG_USER_EVENT: f = h_user_event(c, s, l, r, x.ltime, x.key, x.flags & 1); break;
@@ -2510,7 +2510,7 @@ __global__ void keys_from_msgs_kernel(const rsf_msg* __restrict__ msgs, uint64_t
   idx[i] = (uint32_t)i;
 }
 
-__global__ void init_views_kernel(ViewS* view, uint64_t n_loc, uint32_t S, const uint8_t* kind,
+__global__ void init_views_kernel(ViewS* view, uint64_t vrow, uint64_t n_loc, uint32_t S, const uint8_t* kind,
                                   const uint8_t* status, const uint64_t* ltime) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_loc * S) return;
@@ -2519,7 +2519,7 @@ __global__ void init_views_kernel(ViewS* view, uint64_t n_loc, uint32_t S, const
   v.ltime = ltime[subj];
   v.meta = vmeta(status[subj], kind[subj]);
   v.t = 0;
-  view[i] = v;
+  *view_at(view_row(view, vrow, i / S), subj) = v;
 }
 
 __global__ void tsum_init_kernel(uint4* p, uint64_t n) {
@@ -2728,11 +2728,11 @@ __global__ void __launch_bounds__(256) queue_max_kernel(GCfg c, GState s, uint32
   const uint64_t l = phase_first(c, period, phase) + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave * period;
   if (l >= c.n_loc) return;
   const int32_t own = s.member_subj[l];
-  const ViewS* row = s.view + l * c.S;
+  const ViewS* row = vrow_of(s, c, l);
   uint64_t known = (c.N - c.S) + (own >= 0 ? 1u : 0u);
   for (uint32_t j0 = 0; j0 < c.S; j0 += kWave) {
     const uint32_t j = j0 + lane;
-    const bool kn = j < c.S && (int32_t)j != own && vkind(ViewE(row[j]).meta) == RSF_KIND_KNOWN;
+    const bool kn = j < c.S && (int32_t)j != own && vkind(ViewE(*view_at(row, j)).meta) == RSF_KIND_KNOWN;
     known += (uint32_t)__popcll(ballot(kn));
   }
   uint64_t mx = 2 * known;
@@ -3096,6 +3096,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   c.lo = cfg->shard_lo;
   c.n_loc = cfg->shard_hi - cfg->shard_lo;
   c.S = cfg->n_subjects;
+  c.vrow = view_row_bytes(c.S);
   c.qcap = cfg->queue_cap;
   c.ebuf = cfg->event_buffer_size;
   c.qbuf = cfg->query_buffer_size;
@@ -3170,7 +3171,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   if (GA(s.clock, n * 8) || GA(s.eclock, n * 8) || GA(s.qclock, n * 8) || GA(s.emin, n * 8) || GA(s.qmin, n * 8) ||
       GA(s.digest, n * 8) || GA(s.err, n * 4) || GA(s.alive, N) || GA(s.serf_state, n) || GA(s.member_subj, n * 4) ||
       GA(s.subj_member, S * 4) || GA(s.refute_cnt, S * 4) || GA(s.refute_ltime, S * c.max_refute * 8) ||
-      GA(s.view, n * S * sizeof(ViewS)) || GA(s.q_rumor, n * 3 * c.qcap * 4) || GA(s.q_seq, n * 3 * c.qcap * 4) ||
+      GA(s.view, n * c.vrow) || GA(s.q_rumor, n * 3 * c.qcap * 4) || GA(s.q_seq, n * 3 * c.qcap * 4) ||
       GA(s.q_txlen, n * 3 * c.qcap * 4) || GA(s.q_dec, n * c.qcap * 4) || GA(s.q_next_seq, n * 3 * 4) || GA(s.q_pruned, n * 4) || GA(s.q_expired, n * 4) || GA(s.eb_ltime, n * c.ebuf * 8) ||
       GA(s.eb_cnt, n * c.ebuf * 4) || GA(s.eb_keys, n * c.ebuf * c.slot_k * 8) || GA(s.qb_ltime, n * c.qbuf * 8) ||
       GA(s.qb_cnt, n * c.qbuf * 4) || GA(s.qb_ids, n * c.qbuf * c.slot_k * 4) ||
@@ -3251,7 +3252,7 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
   ms(s.subj_member, 0, S * 4);
   ms(s.refute_cnt, 0, S * 4);
   ms(s.refute_ltime, 0, S * c.max_refute * 8);
-  ms(s.view, 0, n * S * sizeof(ViewS));
+  ms(s.view, 0, n * c.vrow);
   ms(s.q_rumor, 0xFF, n * 3 * c.qcap * 4);
   ms(s.q_seq, 0, n * 3 * c.qcap * 4);
   ms(s.q_txlen, 0, n * 3 * c.qcap * 4);
@@ -3374,7 +3375,7 @@ int rsf_gossip_init_views(rsf_gossip* g, const uint8_t* kind, const uint8_t* sta
   RSF_HIP(hipMemcpyAsync(d[0], kind, c.S, hipMemcpyHostToDevice, g->stream));
   RSF_HIP(hipMemcpyAsync(d[1], status, c.S, hipMemcpyHostToDevice, g->stream));
   RSF_HIP(hipMemcpyAsync(d[2], ltime, (size_t)c.S * 8, hipMemcpyHostToDevice, g->stream));
-  hipLaunchKernelGGL(init_views_kernel, dim3(grid1(c.n_loc * c.S)), dim3(256), 0, g->stream, g->s.view, c.n_loc, c.S,
+  hipLaunchKernelGGL(init_views_kernel, dim3(grid1(c.n_loc * c.S)), dim3(256), 0, g->stream, g->s.view, c.vrow, c.n_loc, c.S,
                      (const uint8_t*)d[0], (const uint8_t*)d[1], (const uint64_t*)d[2]);
   RSF_HIP(hipGetLastError());
   RSF_HIP(hipStreamSynchronize(g->stream));
@@ -3393,7 +3394,7 @@ int rsf_gossip_set_view(rsf_gossip* g, uint64_t m, uint32_t subj, uint8_t kind, 
   ViewS v;
   v = e;
   RSF_HIP(hipSetDevice(g->device));
-  RSF_HIP(hipMemcpyAsync(g->s.view + (m - c.lo) * c.S + subj, &v, sizeof(v), hipMemcpyHostToDevice, g->stream));
+  RSF_HIP(hipMemcpyAsync(vent(g->s, c, m - c.lo, subj), &v, sizeof(v), hipMemcpyHostToDevice, g->stream));
   RSF_HIP(hipStreamSynchronize(g->stream));
   return RSF_OK;
 }
@@ -4129,7 +4130,7 @@ int rsf_gossip_round_merge_runs(rsf_gossip* g, const uint64_t* recv, const uint6
 }
 
 static size_t pp_bytes_per_pair(const GCfg& c) {
-  return (size_t)c.S * sizeof(ViewS) + (size_t)c.ebuf * 12 + (size_t)c.ebuf * c.slot_k * 8 + 32;
+  return (size_t)c.vrow + (size_t)c.ebuf * 12 + (size_t)c.ebuf * c.slot_k * 8 + 32;
 }
 
 int rsf_gossip_push_pull_device(rsf_gossip* g, const rsf_pp_pair* pairs, uint64_t n, uint32_t flags) {
@@ -4152,7 +4153,7 @@ int rsf_gossip_push_pull_device(rsf_gossip* g, const rsf_pp_pair* pairs, uint64_
   char* b = (char*)g->pp_buf;
   PPSlab sl;
   sl.view = (ViewS*)b;
-  b += (size_t)c.S * sizeof(ViewS) * n;
+  b += (size_t)c.vrow * n;
   sl.eb_keys = (uint64_t*)b;
   b += (size_t)c.ebuf * c.slot_k * 8 * n;
   sl.eb_ltime = (uint64_t*)b;
@@ -4463,12 +4464,14 @@ int rsf_gossip_dump_view_rows(rsf_gossip* g, uint64_t row0, uint64_t rows, uint6
   if (!g || !ltime || !status || !kind) return gerr("null argument");
   if (row0 > g->c.n_loc || rows > g->c.n_loc - row0) return gerr("rows outside the shard");
   const uint64_t cnt = rows * g->c.S;
-  std::vector<ViewS> vs(cnt);
+  const GCfg& c = g->c;
+  std::vector<uint4> raw(rows * c.vrow / 16);
   RSF_HIP(hipSetDevice(g->device));
-  RSF_HIP(hipMemcpyAsync(vs.data(), g->s.view + row0 * g->c.S, cnt * sizeof(ViewS), hipMemcpyDeviceToHost, g->stream));
+  RSF_HIP(hipMemcpyAsync(raw.data(), vrow_of(g->s, c, row0), rows * c.vrow, hipMemcpyDeviceToHost, g->stream));
   RSF_HIP(hipStreamSynchronize(g->stream));
+  ViewS* const base = reinterpret_cast<ViewS*>(raw.data());
   for (uint64_t i = 0; i < cnt; ++i) {
-    const ViewE v = vs[i];
+    const ViewE v = *view_at(view_row(base, c.vrow, i / c.S), (uint32_t)(i % c.S));
     ltime[i] = v.ltime;
     status[i] = (uint8_t)(v.meta & 0xFF);
     kind[i] = (uint8_t)((v.meta >> 8) & 0xFF);
@@ -4794,7 +4797,7 @@ __global__ void __launch_bounds__(256) snap_init_kernel(GCfg c, GState s) {
   for (uint32_t b = 0; b < 32; ++b) {
     const uint32_t j = k * 32 + b;
     if (j >= c.S) break;
-    const uint32_t meta = ViewE(s.view[l * c.S + j]).meta;
+    const uint32_t meta = ViewE(*vent(s, c, l, j)).meta;
     const uint32_t st = vstatus(meta);
     if (vkind(meta) == RSF_KIND_KNOWN && (st == RSF_STATUS_ALIVE || st == RSF_STATUS_LEAVING)) bits |= 1u << b;
   }
@@ -4920,7 +4923,7 @@ __global__ void __launch_bounds__(256) snap_reset_kernel(GCfg c, GState s, const
   const uint32_t i = blockIdx.x;
   if (res[i] < 0) return;
   const uint64_t l = members[i] - c.lo;
-  for (uint32_t j = threadIdx.x; j < c.S; j += blockDim.x) s.view[l * c.S + j] = ViewE{0ull, 0u, 0u};
+  for (uint32_t j = threadIdx.x; j < c.S; j += blockDim.x) *vent(s, c, l, j) = ViewE{0ull, 0u, 0u};
   for (uint32_t j = threadIdx.x; j < 3 * c.qcap; j += blockDim.x) {
     s.q_rumor[l * 3 * c.qcap + j] = kEmpty;
     s.q_seq[l * 3 * c.qcap + j] = 0;
@@ -4980,7 +4983,7 @@ __global__ void __launch_bounds__(256) snap_restart_kernel(GCfg c, GState s, con
   if (joined)
     for (uint32_t j = 0; j < c.S; ++j)
       if ((int32_t)j != r.subj && s.alive[s.subj_member[j]]) {
-        h_node_join(s.view + l * c.S + j, r, j);
+        h_node_join(vent(s, c, l, j), r, j);
         snap_member(c, s, l, j, true);
         mlog_put(c, s, l, r.err, kEvJoin, j);
       }
@@ -5003,13 +5006,13 @@ __global__ void __launch_bounds__(256) reconnect_kernel(GCfg c, GState s, uint32
   if (target && lane == 0) target[l] = kEmpty;
   if (!s.alive[m]) return;
   const int32_t own = s.member_subj[l];
-  const ViewS* row = s.view + l * c.S;
+  const ViewS* row = vrow_of(s, c, l);
   uint32_t failed = 0, left = 0;
   uint64_t known = (c.N - c.S) + (own >= 0 ? 1u : 0u);  // members.states: see above
   for (uint32_t j0 = 0; j0 < c.S; j0 += kWave) {
     const uint32_t j = j0 + lane;
     uint32_t meta = 0;
-    if (j < c.S && (int32_t)j != own) meta = ViewE(row[j]).meta;
+    if (j < c.S && (int32_t)j != own) meta = ViewE(*view_at(row, j)).meta;
     const bool kn = vkind(meta) == RSF_KIND_KNOWN;
     known += (uint32_t)__popcll(ballot(kn));
     failed += (uint32_t)__popcll(ballot(kn && vstatus(meta) == RSF_STATUS_FAILED));
@@ -5027,7 +5030,7 @@ __global__ void __launch_bounds__(256) reconnect_kernel(GCfg c, GState s, uint32
   for (uint32_t j0 = 0; j0 < c.S && tj == kEmpty; j0 += kWave) {
     const uint32_t j = j0 + lane;
     uint32_t meta = 0;
-    if (j < c.S && (int32_t)j != own) meta = ViewE(row[j]).meta;
+    if (j < c.S && (int32_t)j != own) meta = ViewE(*view_at(row, j)).meta;
     const bool fa = vkind(meta) == RSF_KIND_KNOWN && vstatus(meta) == RSF_STATUS_FAILED;
     const unsigned long long mask = ballot(fa);
     const uint32_t cnt = (uint32_t)__popcll(mask);
@@ -5044,7 +5047,7 @@ __global__ void __launch_bounds__(256) reconnect_kernel(GCfg c, GState s, uint32
   if (!s.alive[s.subj_member[tj]]) return;
   MRegs r;
   load_regs(s, l, r);
-  h_node_join(s.view + l * c.S + tj, r, tj);
+  h_node_join(vent(s, c, l, tj), r, tj);
   snap_member(c, s, l, tj, true);
   mlog_put(c, s, l, r.err, kEvJoin, tj);
   store_regs(s, l, r);

@@ -46,6 +46,7 @@ struct GCfg {
   uint32_t deep;  // any tail
   uint32_t max_ue, query_limit;  // Options::max_user_event_size / query_size_limit (origination checks)
   uint32_t gen;  // the rumor ring's current generation (rebuilds the intent tail's packed rumor ids)
+  uint64_t vrow;  // bytes of a member's view row (view_row_bytes(S))
 };
 
 // view entry: members.states[subject] (status, status_time) or recent_intents[subject] --
@@ -78,6 +79,22 @@ struct ViewS {
   }
 };
 static_assert(sizeof(ViewS) == 12, "12-B view entries");
+// A member's row: five entries to each 64-B sector (60 B + 4 B of padding), so no entry
+// straddles a sector (a random entry is one sector read and one written back, as with 16-B
+// entries) at 12.8 B per entry.
+constexpr uint32_t kViewPerSector = 5;
+RSF_HD uint64_t view_row_bytes(uint32_t S) { return (uint64_t)((S + kViewPerSector - 1) / kViewPerSector) * 64u; }
+RSF_HD ViewS* view_at(ViewS* row, uint32_t subj) {
+  return reinterpret_cast<ViewS*>(reinterpret_cast<char*>(row) + (uint64_t)(subj / kViewPerSector) * 64u +
+                                  (subj % kViewPerSector) * 12u);
+}
+RSF_HD const ViewS* view_at(const ViewS* row, uint32_t subj) {
+  return reinterpret_cast<const ViewS*>(reinterpret_cast<const char*>(row) + (uint64_t)(subj / kViewPerSector) * 64u +
+                                        (subj % kViewPerSector) * 12u);
+}
+RSF_HD ViewS* view_row(ViewS* base, uint64_t row_bytes, uint64_t l) {
+  return reinterpret_cast<ViewS*>(reinterpret_cast<char*>(base) + l * row_bytes);
+}
 
 struct GState {
   uint64_t *clock, *eclock, *qclock, *emin, *qmin, *digest;
@@ -88,7 +105,7 @@ struct GState {
   uint32_t* subj_member;  // [S]
   uint32_t* refute_cnt;   // [S]
   uint64_t* refute_ltime; // [S][max_refute]
-  ViewS* view;            // [n_loc][S], 12-B entries
+  ViewS* view;            // [n_loc] rows of vrow bytes: S 12-B entries, five to a 64-B sector
   uint32_t *q_rumor, *q_seq, *q_txlen, *q_next_seq;  // [n_loc][3][qcap], next_seq [n_loc][3]
   uint32_t* q_dec;        // [n_loc][qcap] intent queue: each item's record decoration (subject slot)
   uint32_t* q_pruned;     // [n_loc] live queue items dropped by a full queue (memberlist Prune), cumulative
@@ -206,6 +223,9 @@ constexpr uint32_t kDeepTiny = 640 + 64 + kPend;
 constexpr uint32_t kDeepSmall = 1024 + 64 + kPend;
 constexpr uint32_t kDeepMid = 2240 + 64 + kPend;
 RSF_HD uint32_t pend_total(uint32_t pc) { return (pc & 0xFF) + ((pc >> 8) & 0xFF) + ((pc >> 16) & 0xFF); }
+
+RSF_HD ViewS* vrow_of(const GState& s, const GCfg& c, uint64_t l) { return view_row(s.view, c.vrow, l); }
+RSF_HD ViewS* vent(const GState& s, const GCfg& c, uint64_t l, uint32_t subj) { return view_at(vrow_of(s, c, l), subj); }
 
 // per-member scalar state held in registers while a kernel works on it
 struct MRegs {
