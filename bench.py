@@ -127,6 +127,7 @@ def run_vivaldi(args, rank, world):
     if targeted:
         from ruserf_amd.dist import ShardedVivaldi
         sv = ShardedVivaldi(g, rank, world)
+        sv.time_chunks = True
 
     refresher = None
     if world > 1 and not targeted:
@@ -148,17 +149,22 @@ def run_vivaldi(args, rank, world):
 
     read_ptr = [None]  # the table a round reads (the other one after it)
 
+    chunks = max(1, getattr(args, "vivaldi_chunks", 1)) if targeted else 1
+
     def observe(r):
         read_ptr[0] = g.table_ptr()[0]
-        g.observe(r % 16, peer[r].data_ptr(), rtt[r].data_ptr(), None, r)
+        if chunks > 1:  # the exchange of chunk i + 1 beside the observe of chunk i (round_chunked)
+            sv.round_chunked(r, peer[r].data_ptr(), rtt[r].data_ptr(), chunks=chunks)
+        else:
+            g.observe(r % 16, peer[r].data_ptr(), rtt[r].data_ptr(), None, r)
 
     def fetch(r):
-        if targeted:
+        if targeted and chunks == 1:
             sv.fetch(peer[r].data_ptr())
 
     def presend(r):
         # round r + 1's requests go out while round r's observe runs
-        if targeted and r + 1 < rounds:
+        if targeted and chunks == 1 and r + 1 < rounds:
             sv.presend(peer[r + 1].data_ptr())
 
     for _ in range(args.warmup):
@@ -185,6 +191,8 @@ def run_vivaldi(args, rank, world):
     barrier(world)
     wall = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in evs]
+    if chunks > 1:  # the observe kernels' own time: the chunks' launches summed per round
+        kernel_ms = [sum(a.elapsed_time(b) for a, b in rnd) for rnd in sv.chunk_events[-args.steps:]]
     wall = max_over_ranks(wall, world)
     if targeted and not sv.check():
         raise RuntimeError("vivaldi exchange: a request bucket overflowed")
@@ -201,7 +209,8 @@ def run_vivaldi(args, rank, world):
                                f"probe inputs (peer, rtt) pre-generated in HBM",
                    "members": n, "members_per_gpu": per, "parallelism": f"members sharded x{world}",
                    "table_refresh_every_rounds": R,
-                   "exchange": ("targeted peer rows" if targeted else f"table all-gather every {R} rounds")
+                   "exchange": ((f"targeted peer rows, the round pipelined in {chunks} member chunks" if chunks > 1
+                                 else "targeted peer rows") if targeted else f"table all-gather every {R} rounds")
                    if world > 1 else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -373,6 +382,9 @@ def main():
                     help="vivaldi, N>1: all-gather the coordinate table after every R-th round (C5: 1 and 8)")
     ap.add_argument("--vivaldi-exchange", choices=["targeted", "allgather"], default="targeted",
                     help="vivaldi, N>1, R=1: fetch only the round's remote peer rows, or all-gather the table")
+    ap.add_argument("--vivaldi-chunks", type=int, default=4,
+                    help="vivaldi, N>1, targeted: the round pipelined in this many member chunks (chunk i observed "
+                         "while chunk i+1's rows are exchanged); 1: the exchange before the whole observe")
     args = ap.parse_args()
     if args.queue_depth is None:
         args.queue_depth = DEFAULT_QUEUE_DEPTH if args.queue_cap <= 64 else 0

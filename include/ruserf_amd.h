@@ -163,6 +163,14 @@ int rsf_vivaldi_round(rsf_vivaldi* v, uint32_t round);
 int rsf_vivaldi_gen_probes(rsf_vivaldi* v, uint32_t round, uint32_t* peer_out, uint64_t* rtt_ns_out);
 int rsf_vivaldi_observe(rsf_vivaldi* v, uint32_t slot, const uint32_t* peer, const uint64_t* rtt_ns,
                         int32_t* status_out, uint32_t round);
+/* rsf_vivaldi_observe over the shard members lo+first .. lo+first+count-1 only (first a
+ * multiple of 64; the arrays are still indexed by shard member), WITHOUT flipping the tables:
+ * a round pipelined by member chunks (each chunk observed as soon as its peers' rows are in
+ * the current table) calls it once per chunk, then rsf_vivaldi_flip.  Chunks of one round must
+ * not overlap.  Asynchronous. */
+int rsf_vivaldi_observe_range(rsf_vivaldi* v, uint32_t slot, const uint32_t* peer, const uint64_t* rtt_ns,
+                              int32_t* status_out, uint32_t round, uint64_t first, uint64_t count);
+int rsf_vivaldi_flip(rsf_vivaldi* v);
 
 /* memberlist's probe loop feeding the coordinates (memberlist is not
  * vendored: parity unpinned).  rsf_vivaldi_probe: member lo+i probes neighbour slot
@@ -215,6 +223,10 @@ typedef struct rsf_vivaldi_xbufs {
 } rsf_vivaldi_xbufs;
 int rsf_vivaldi_exchange_buffers(rsf_vivaldi* v, uint32_t world, rsf_vivaldi_xbufs* out);
 int rsf_vivaldi_exchange_requests(rsf_vivaldi* v, uint32_t world, const uint32_t* peer);
+/* the requests of shard members lo+first .. lo+first+count-1 only (peer indexed by shard member):
+ * one chunk of a pipelined round, whose serve / apply follow as above */
+int rsf_vivaldi_exchange_requests_range(rsf_vivaldi* v, uint32_t world, const uint32_t* peer, uint64_t first,
+                                        uint64_t count);
 int rsf_vivaldi_exchange_serve(rsf_vivaldi* v, uint32_t world);
 int rsf_vivaldi_exchange_apply(rsf_vivaldi* v, uint32_t world);
 int rsf_vivaldi_exchange_status(rsf_vivaldi* v, int* ok);

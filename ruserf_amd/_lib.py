@@ -103,12 +103,15 @@ def lib():
     _sig(L, "rsf_vivaldi_round", i, [VP, C.c_uint32])
     _sig(L, "rsf_vivaldi_gen_probes", i, [VP, C.c_uint32, VP, VP])
     _sig(L, "rsf_vivaldi_observe", i, [VP, C.c_uint32, VP, VP, VP, C.c_uint32])
+    _sig(L, "rsf_vivaldi_observe_range", i, [VP, C.c_uint32, VP, VP, VP, C.c_uint32, C.c_uint64, C.c_uint64])
+    _sig(L, "rsf_vivaldi_flip", i, [VP])
     _sig(L, "rsf_vivaldi_table", i, [VP, C.POINTER(VP), P64])
     _sig(L, "rsf_vivaldi_true_rtt_ns", i, [VP, C.c_uint32, C.c_uint32, P64])
     _sig(L, "rsf_vivaldi_probe", i, [VP, C.c_uint32, VP, VP, VP, VP])
     _sig(L, "rsf_vivaldi_probe_acks", i, [VP, VP, VP, VP, VP, C.c_uint64])
     _sig(L, "rsf_vivaldi_exchange_buffers", i, [VP, C.c_uint32, C.POINTER(RsfVivaldiXbufs)])
     _sig(L, "rsf_vivaldi_exchange_requests", i, [VP, C.c_uint32, VP])
+    _sig(L, "rsf_vivaldi_exchange_requests_range", i, [VP, C.c_uint32, VP, C.c_uint64, C.c_uint64])
     _sig(L, "rsf_vivaldi_exchange_serve", i, [VP, C.c_uint32])
     _sig(L, "rsf_vivaldi_exchange_apply", i, [VP, C.c_uint32])
     _sig(L, "rsf_vivaldi_exchange_status", i, [VP, C.POINTER(C.c_int)])

@@ -238,6 +238,15 @@ class CoordinateClients:
         check(lib().rsf_vivaldi_observe(self._h, slot, C.c_void_p(peer_ptr), C.c_void_p(rtt_ptr),
                                         C.c_void_p(status_ptr) if status_ptr else None, round_))
 
+    def observe_range(self, slot, peer_ptr, rtt_ptr, first, count, status_ptr=None, round_=0):
+        """observe() over shard members [first, first + count) only, without flipping the
+        tables (one chunk of a pipelined round; flip() after the last chunk)"""
+        check(lib().rsf_vivaldi_observe_range(self._h, slot, C.c_void_p(peer_ptr), C.c_void_p(rtt_ptr),
+                                              C.c_void_p(status_ptr) if status_ptr else None, round_, first, count))
+
+    def flip(self):
+        check(lib().rsf_vivaldi_flip(self._h))
+
     # ---- memberlist's probe loop (see ruserf_amd.probe.ProbeLoop)
     def probe(self, r, up_ptr, peer_ptr, rtt_ptr, acked_ptr):
         """Probes of round r with process liveness up[N] (device pointers, asynchronous)."""
@@ -277,8 +286,12 @@ class CoordinateClients:
         check(lib().rsf_vivaldi_exchange_buffers(self._h, world, C.byref(x)))
         return {k: getattr(x, k) for k, _ in RsfVivaldiXbufs._fields_}
 
-    def exchange_requests(self, world, peer_ptr):
-        check(lib().rsf_vivaldi_exchange_requests(self._h, world, C.c_void_p(peer_ptr)))
+    def exchange_requests(self, world, peer_ptr, first=None, count=None):
+        """the round's requests; with first / count those of shard members [first, first + count)"""
+        if first is None:
+            check(lib().rsf_vivaldi_exchange_requests(self._h, world, C.c_void_p(peer_ptr)))
+        else:
+            check(lib().rsf_vivaldi_exchange_requests_range(self._h, world, C.c_void_p(peer_ptr), first, count))
 
     def exchange_serve(self, world):
         check(lib().rsf_vivaldi_exchange_serve(self._h, world))

@@ -52,6 +52,10 @@ struct VivParams {
   uint32_t k0, k1;   // Philox key (seed)
   uint32_t round;
   double error_max, ce, cc, height_min, rho;
+  // the observe kernels' members: shard-local [first, end) (the whole shard unless a caller
+  // pipelines the round by chunks, rsf_vivaldi_observe_range); per-member arrays keep their
+  // shard_n strides
+  uint64_t first, end;
 };
 
 // --------------------------------------------------------------------------
@@ -479,10 +483,10 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
   // D == 8: the peer rows are gathered two lanes per row (below), so every lane of the
   // wave stays to take part; a lane past the shard end only helps with the gather.
   constexpr bool kCoop = RSF_VIV_COOP && (D == 8) && !(ABL & 1);
-  const uint64_t local0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = local0 < p.shard_n;
+  const uint64_t local0 = p.first + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = local0 < p.end;
   if (!kCoop && !active) return;
-  const uint64_t local = active ? local0 : p.shard_n - 1;  // inactive lanes read a valid member, store nothing
+  const uint64_t local = active ? local0 : p.end - 1;  // inactive lanes read a valid member, store nothing
   const uint32_t m = (uint32_t)(p.lo + local);
   const int FR = FRT;
   // ---- every independent load first: probe input, window index + window, own row, filter record
@@ -508,7 +512,7 @@ __global__ void __launch_bounds__(256, RSF_VIV_WAVES) vivaldi_observe_kernel(
   double2* sw = stage[kCoop ? threadIdx.x / 64 : 0];
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wbase = local0 - lane;  // the wave's first (shard-local) member
-  const uint32_t wrows = wbase >= p.shard_n ? 0u : (uint32_t)min((uint64_t)64, p.shard_n - wbase);
+  const uint32_t wrows = wbase >= p.end ? 0u : (uint32_t)min((uint64_t)64, p.end - wbase);
   if (ABL & 8) {
 #pragma unroll
     for (int i = 0; i < D; ++i) me[i] = 0.001 * (double)(m & 7);
@@ -680,12 +684,12 @@ __global__ void __launch_bounds__(RSF_VIV_BLOCK, RSF_VIV_WAVES) vivaldi_observe_
   constexpr int D = 8, WW = 20, FR = FRT;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t bid = RSF_VIV_XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-  const uint64_t local0 = (uint64_t)bid * blockDim.x + threadIdx.x;
+  const uint64_t local0 = p.first + (uint64_t)bid * blockDim.x + threadIdx.x;
   const uint64_t wbase = local0 - lane;  // the wave's first shard-local member
-  if (wbase >= p.shard_n) return;        // wave-uniform: no lane of this wave has a member
-  const uint32_t wrows = (uint32_t)min((uint64_t)64, p.shard_n - wbase);
+  if (wbase >= p.end) return;            // wave-uniform: no lane of this wave has a member
+  const uint32_t wrows = (uint32_t)min((uint64_t)64, p.end - wbase);
   const bool active = lane < wrows;
-  const uint64_t local = active ? local0 : p.shard_n - 1;  // inactive lanes read a valid member, store nothing
+  const uint64_t local = active ? local0 : p.end - 1;  // inactive lanes read a valid member, store nothing
   const uint32_t m = (uint32_t)(p.lo + local);
   // ---- round trip 1: probe input first, then every member-side stream
   const uint32_t peer = ld_s(peer_in + local);
@@ -958,12 +962,13 @@ static int set_err_args(const char* m) { return rsf::set_error(RSF_ERR_ARG, m); 
 // ---- targeted peer-row exchange: each shard asks the owners for the rows
 // of this round's remote peers only, instead of all-gathering the whole table.
 // requests: one thread per shard member whose peer lives on another shard
-__global__ void __launch_bounds__(256) xreq_pack_kernel(const uint32_t* __restrict__ peer, uint64_t lo, uint64_t shard_n,
-                                                        uint64_t per, uint32_t* __restrict__ req, uint64_t req_words,
-                                                        uint32_t cap, uint32_t* __restrict__ cnt,
+// peer: the requesting members' peer ids (count of them)
+__global__ void __launch_bounds__(256) xreq_pack_kernel(const uint32_t* __restrict__ peer, uint64_t count, uint64_t lo,
+                                                        uint64_t shard_n, uint64_t per, uint32_t* __restrict__ req,
+                                                        uint64_t req_words, uint32_t cap, uint32_t* __restrict__ cnt,
                                                         unsigned long long* __restrict__ flags) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= shard_n) return;
+  if (i >= count) return;
   const uint32_t p = peer[i];
   if ((uint64_t)p - lo < shard_n) return;  // own shard: the row is local
   const uint32_t w = (uint32_t)(p / per);
@@ -1354,19 +1359,24 @@ int rsf_vivaldi_probe_acks(rsf_vivaldi* v, const uint32_t* peer, const uint8_t* 
 #ifndef RSF_VIV_ROUND_WW
 #define RSF_VIV_ROUND_WW 20  // 0: runtime-sized window loop for the default config too
 #endif
-int rsf_vivaldi_observe(rsf_vivaldi* v, uint32_t slot, const uint32_t* peer, const uint64_t* rtt_ns,
-                        int32_t* status_out, uint32_t round) {
+int rsf_vivaldi_observe_range(rsf_vivaldi* v, uint32_t slot, const uint32_t* peer, const uint64_t* rtt_ns,
+                              int32_t* status_out, uint32_t round, uint64_t first, uint64_t count) {
   if (!v || !peer || !rtt_ns) return set_err_args("null argument");
   if (slot >= v->p.peers) return set_err_args("peer_slot out of range");
+  if (first > v->p.shard_n || count > v->p.shard_n - first) return set_err_args("members outside the shard");
+  if (first % 64) return set_err_args("a range must start at a multiple of 64 (one wave's members)");
+  if (!count) return RSF_OK;
   RSF_HIP(hipSetDevice(v->device));
   VivParams p = v->p;
   p.round = round;
-  unsigned blocks = (unsigned)((p.shard_n + 255) / 256);
+  p.first = first;
+  p.end = first + count;
+  unsigned blocks = (unsigned)((count + 255) / 256);
   const double* cur = v->table[v->cur];
   double* nxt = v->table[v->cur ^ 1];
   if (RSF_VIV_PIPE && p.dim == 8 && p.F <= 3 && p.W == 20 && p.stride == 12 && RSF_VIV_ROUND_WW == 20)
     hipLaunchKernelGGL((vivaldi_observe_pipe_kernel<3>),
-                       dim3((unsigned)((p.shard_n + RSF_VIV_BLOCK - 1) / RSF_VIV_BLOCK)), dim3(RSF_VIV_BLOCK), 0,
+                       dim3((unsigned)((count + RSF_VIV_BLOCK - 1) / RSF_VIV_BLOCK)), dim3(RSF_VIV_BLOCK), 0,
                        v->stream, cur, nxt, v->adj,
                        v->adj_idx, v->filt, v->resets, peer, rtt_ns, status_out, p, slot);
   else if (p.dim == 8 && p.F <= 3 && p.W == 20)
@@ -1378,6 +1388,19 @@ int rsf_vivaldi_observe(rsf_vivaldi* v, uint32_t slot, const uint32_t* peer, con
                                        cur, nxt, v->adj, v->adj_idx, v->filt, v->resets, peer, rtt_ns, status_out,
                                        p, slot));
   RSF_HIP(hipGetLastError());
+  return RSF_OK;
+}
+
+int rsf_vivaldi_flip(rsf_vivaldi* v) {
+  if (!v) return set_err_args("null argument");
+  v->cur ^= 1;
+  return RSF_OK;
+}
+
+int rsf_vivaldi_observe(rsf_vivaldi* v, uint32_t slot, const uint32_t* peer, const uint64_t* rtt_ns,
+                        int32_t* status_out, uint32_t round) {
+  const int rc = rsf_vivaldi_observe_range(v, slot, peer, rtt_ns, status_out, round, 0, v ? v->p.shard_n : 0);
+  if (rc) return rc;
   v->cur ^= 1;
   return RSF_OK;
 }
@@ -1402,6 +1425,8 @@ int rsf_vivaldi_round_ablate(rsf_vivaldi* v, uint32_t round, uint32_t mask) {
   if (!v || v->p.dim != 8 || v->p.F > 3 || v->p.W != 20) return set_err_args("ablation needs D=8 F=3 W=20");
   VivParams p = v->p;
   p.round = round;
+  p.first = 0;
+  p.end = p.shard_n;
   const uint32_t slot = round % p.peers;
   unsigned blocks = (unsigned)((p.shard_n + 255) / 256);
   const double* cur = v->table[v->cur];
@@ -1463,17 +1488,24 @@ int rsf_vivaldi_exchange_buffers(rsf_vivaldi* v, uint32_t world, rsf_vivaldi_xbu
   return RSF_OK;
 }
 
-int rsf_vivaldi_exchange_requests(rsf_vivaldi* v, uint32_t world, const uint32_t* peer) {
+int rsf_vivaldi_exchange_requests_range(rsf_vivaldi* v, uint32_t world, const uint32_t* peer, uint64_t first,
+                                        uint64_t count) {
   if (!v || !peer || world != v->xw) return set_err_args("call rsf_vivaldi_exchange_buffers(world) first");
   const VivParams& p = v->p;
+  if (first > p.shard_n || count > p.shard_n - first) return set_err_args("members outside the shard");
   RSF_HIP(hipSetDevice(v->device));
   RSF_HIP(hipMemsetAsync(v->xcnt, 0, 4 * world, v->stream));
-  hipLaunchKernelGGL(xreq_pack_kernel, dim3((unsigned)((p.shard_n + 255) / 256)), dim3(256), 0, v->stream, peer, p.lo,
-                     p.shard_n, p.shard_n, v->req_send, v->req_words, v->xcap, v->xcnt, v->xflags);
+  if (count)
+    hipLaunchKernelGGL(xreq_pack_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, v->stream, peer + first,
+                       count, p.lo, p.shard_n, p.shard_n, v->req_send, v->req_words, v->xcap, v->xcnt, v->xflags);
   hipLaunchKernelGGL(xreq_header_kernel, dim3((world + 63) / 64), dim3(64), 0, v->stream, v->req_send, v->req_words,
                      (const uint32_t*)v->xcnt, world, v->xcap);
   RSF_HIP(hipGetLastError());
   return RSF_OK;
+}
+
+int rsf_vivaldi_exchange_requests(rsf_vivaldi* v, uint32_t world, const uint32_t* peer) {
+  return rsf_vivaldi_exchange_requests_range(v, world, peer, 0, v ? v->p.shard_n : 0);
 }
 
 int rsf_vivaldi_exchange_serve(rsf_vivaldi* v, uint32_t world) {

@@ -150,6 +150,8 @@ class ShardedVivaldi:
         self._sent = None        # the peer-id pointer whose requests are already out
         self._ev_applied = None  # this round's apply done (it reads the request buckets)
         self._ev_sent = None
+        self.time_chunks = False  # round_chunked: time each chunk's observe (chunk_events)
+        self.chunk_events = []
 
     def fetch(self, peer_ptr):
         """Bring the rows of this round's remote peers into the current table."""
@@ -191,12 +193,68 @@ class ShardedVivaldi:
         self._ev_sent.record(side)
         self._sent = next_peer_ptr
 
-    def round(self, r, peer_ptr, rtt_ptr, status_ptr=None, slots=16, next_peer_ptr=None):
+    def round(self, r, peer_ptr, rtt_ptr, status_ptr=None, slots=16, next_peer_ptr=None, chunks=1):
+        if self.world > 1 and chunks > 1:
+            return self.round_chunked(r, peer_ptr, rtt_ptr, status_ptr, slots, chunks)
         if self.world > 1:
             self.fetch(peer_ptr)
         self.g.observe(r % slots, peer_ptr, rtt_ptr, status_ptr, r)
         if next_peer_ptr is not None:
             self.presend(next_peer_ptr)
+
+    def round_chunked(self, r, peer_ptr, rtt_ptr, status_ptr=None, slots=16, chunks=4):
+        """The round pipelined by member chunks: chunk i is observed while chunk i + 1's remote
+        peer rows are requested, served, replied and applied on a side stream, so the exchange
+        hides behind the observe instead of preceding it.  Exact: every row served or applied
+        is the owner's end-of-previous-round row (coordinate.rs:462-499 reads the peer's last
+        coordinate) -- the owners' observe writes the other table, and a remote row applied
+        twice (a peer of two chunks) is the same bytes.  Each rank runs the same number of
+        chunks, so the all-to-alls pair up across ranks."""
+        g, w = self.g, self.world
+        main = torch.cuda.current_stream()
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=main.device)
+            self._ev_sent = torch.cuda.Event()
+        side = self._side
+        n = g.hi - g.lo
+        step = -(-n // chunks)
+        step = -(-step // 64) * 64  # chunks start at multiples of 64 (one wave's members)
+        bounds = [(a, min(n, a + step)) for a in range(0, n, step)]
+        bounds += [(n, n)] * (chunks - len(bounds))  # every rank joins every chunk's collectives
+        ev_in = torch.cuda.Event()
+        ev_in.record(main)  # the previous round's observe (and anything else queued) first
+        side.wait_event(ev_in)
+        done = []
+        g.set_stream(side.cuda_stream)
+        try:
+            with torch.cuda.stream(side):
+                for a, b in bounds:
+                    g.exchange_requests(w, peer_ptr, a, b - a)
+                    all_to_all(self.req_recv, self.req_send, self.stage, self.group)
+                    g.exchange_serve(w)
+                    all_to_all(self.rep_recv, self.rep_send, self.stage, self.group)
+                    g.exchange_apply(w)
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    done.append(ev)
+        finally:
+            g.set_stream(main.cuda_stream)
+        timed = []
+        for (a, b), ev in zip(bounds, done):
+            main.wait_event(ev)
+            if self.time_chunks:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(main)
+            g.observe_range(r % slots, peer_ptr, rtt_ptr, a, b - a, status_ptr, r)
+            if self.time_chunks:
+                e1.record(main)
+                timed.append((e0, e1))
+        g.flip()
+        self.chunk_events.append(timed)
+        # the side stream's next use (the next round's requests) must follow this round's observe
+        self._ev_applied = torch.cuda.Event()
+        self._ev_applied.record(main)
+        side.wait_event(self._ev_applied)
 
     def check(self):
         """True if no request bucket overflowed and every request reached its owner."""

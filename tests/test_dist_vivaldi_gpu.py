@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 N, ROUNDS, SEED = 24_000, 14, 0x5EED
 
 
-def _worker(rank, world, port, q, presend=False):
+def _worker(rank, world, port, q, presend=False, chunks=1):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
@@ -38,7 +38,7 @@ def _worker(rank, world, port, q, presend=False):
         remote += int(np.count_nonzero((p < lo) | (p >= hi)))
     for r in range(ROUNDS):
         nxt = peer[r + 1].data_ptr() if presend and r + 1 < ROUNDS else None
-        sv.round(r, peer[r].data_ptr(), rtt[r].data_ptr(), next_peer_ptr=nxt)
+        sv.round(r, peer[r].data_ptr(), rtt[r].data_ptr(), next_peer_ptr=nxt, chunks=chunks)
     torch.cuda.synchronize()
     ok = sv.check()
     rows = g.get_rows(lo, per)
@@ -48,15 +48,17 @@ def _worker(rank, world, port, q, presend=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,presend", [(2, False), (2, True)])
-def test_sharded_vivaldi_equals_one_context(world, presend):
+@pytest.mark.parametrize("world,presend,chunks", [(2, False, 1), (2, True, 1), (2, False, 4), (2, False, 7)])
+def test_sharded_vivaldi_equals_one_context(world, presend, chunks):
     """presend: round r + 1's requests built and exchanged on a side stream during round r
-    (ShardedVivaldi.presend); the result is the same bit for bit."""
+    (ShardedVivaldi.presend); chunks > 1: the round pipelined by member chunks, chunk i
+    observed while chunk i + 1's rows are exchanged on a side stream (round_chunked; 7 chunks
+    leave the last one short).  The result is the same bit for bit."""
     from ruserf_amd import CoordinateClients, CoordinateOptions
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29600 + os.getpid() % 1000 + (7 if presend else 0)
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, presend)) for r in range(world)]
+    port = 29600 + os.getpid() % 1000 + (7 if presend else 0) + 13 * chunks
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, presend, chunks)) for r in range(world)]
     for p in procs:
         p.start()
     got = {}
