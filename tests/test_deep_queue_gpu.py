@@ -472,3 +472,52 @@ def test_configs1_reference_regime_properties():
     assert np.all(tx[r != 0xFFFFFFFF] < limit)
     assert all(g.cub_canaries())
     g.close()
+
+
+def test_packed_intent_tail_config_limits():
+    """The intent queue's packed 8-B tail items hold the rumor's ring slot and
+    generation parity in 27 bits and transmits in 6: a deep intent queue with more than 2^26
+    ring slots per generation or a retransmit limit above 64 is refused at create, and the
+    same configurations with a bounded (or query/event-only deep) queue are accepted."""
+    base = dict(n_members=64, n_subjects=4, queue_cap=16, event_buffer_size=16, query_buffer_size=16, slot_k=2)
+    with pytest.raises(Exception):
+        G.GossipEngine(G.GossipConfig(**base, queue_depth=(100, 0, 0), max_rumors=1 << 27))
+    with pytest.raises(Exception):
+        G.GossipEngine(G.GossipConfig(**base, queue_depth=(100, 0, 0), retransmit_mult=33, max_rumors=1 << 10))
+    for cfg in [G.GossipConfig(**base, max_rumors=1 << 27),
+                G.GossipConfig(**base, queue_depth=(0, 100, 100), retransmit_mult=33, max_rumors=1 << 10),
+                G.GossipConfig(**base, queue_depth=(100, 0, 0), max_rumors=1 << 26)]:
+        G.GossipEngine(cfg).close()
+
+
+def test_view_time_stamps_mod_2_27_reaper_ages():
+    """View time stamps are kept mod 2^27 rounds (12-B view entries): a Left
+    member stamped just below 2^27 and reaped just above it ages by the true difference, so the
+    Reaper's tombstone decision equals the oracle's (which keeps the whole u32)."""
+    n, s = 8, 2
+    subj = np.array([6, 7], np.uint32)
+    for timeout, reaped in [(25, True), (35, False)]:
+        cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=8, max_rumors=1024, event_buffer_size=64,
+                             query_buffer_size=64, slot_k=2)
+        g, w = pair(cfg, subj, W.initial_views(s))
+        stamp, now = (1 << 27) - 10, (1 << 27) + 20  # true age 30 rounds
+        for m in range(n):  # every member knows subject 0 as Leaving
+            g.set_view(m, 0, G.KIND_KNOWN, G.STATUS_LEAVING, 3)
+        O.arr(w.v_kind, n * s, np.uint8).reshape(n, s)[:, 0] = G.KIND_KNOWN
+        O.arr(w.v_status, n * s, np.uint8).reshape(n, s)[:, 0] = G.STATUS_LEAVING
+        O.arr(w.v_ltime, n * s, np.uint64).reshape(n, s)[:, 0] = 3
+        # memberlist NotifyLeave of subject 0 at round `stamp`: Leaving -> Left, leave_time = stamp
+        ml = np.zeros(1, G.ML_DTYPE)
+        ml["subject"], ml["kind"], ml["set_alive"] = 0, G.ML_LEAVE, 2  # (liveness unchanged)
+        g.round(stamp, ml, None)
+        H.oracle_round(w, stamp, ml, np.zeros(0, G.ACTION_DTYPE))
+        _, st, kd, tm = g.view(with_time=True)
+        assert int(st.reshape(n, s)[1, 0]) == G.STATUS_LEFT and int(tm.reshape(n, s)[1, 0]) == stamp % (1 << 27)
+        g.reap(now, 1 << 30, timeout, 1 << 30)
+        assert L.orc_reap(C.byref(w), now, 1 << 30, timeout, 1 << 30) == 0
+        _, st, kd, tm = g.view(with_time=True)
+        exp_kind = O.arr(w.v_kind, n * s, np.uint8).reshape(n, s)
+        assert np.array_equal(kd.reshape(n, s), exp_kind)
+        assert (int(exp_kind[1, 0]) == G.KIND_UNKNOWN) == reaped, (timeout, exp_kind[1, 0])
+        g.close()
+        L.orc_world_free(C.byref(w))
