@@ -49,21 +49,25 @@ __shared__ unsigned long long s_dprof[64];
 // checks) runs again -- with the true smallest keys in the head it almost always decides.  If
 // it still cannot, the picks are made over the LDS items directly (repeated wave argmin of the
 // fitting unpicked keys, as get_broadcasts restated), and head / tail are rebuilt after them.
-// Three capacities: kDeepTiny items (19 KB of LDS) and kDeepSmall (25 KB) for the common cases,
-// the full depth (77 KB) for the rest; emit_run lists a member by the size its largest queue
+// Capacities: kDeepTiny items (15 KB of LDS), kDeepSmall (20 KB) and kDeepMid (35 KB) for the common cases,
+// the full depth (117 KB) for the rest; emit_run lists a member by the size its largest queue
 // needs.
 constexpr uint32_t kDeepBig = kDeepItems;
 constexpr uint8_t kDeepInHead = 3;
 
+// No per-item decoration: an item's decoration is a function of its queue and rumor (the
+// intent queue's is the rumor's record decoration, s.rdec; the query / event queues' a
+// constant), so it is read when the item enters the head (head_dec) or is picked by the
+// per-peer fallback -- 4 B per item less LDS (the middle class 4 waves per CU instead of 3).
 template <uint32_t CAP>
 struct DeepWave {
   uint64_t key[CAP];
-  uint32_t rid[CAP], dec[CAP];
+  uint32_t rid[CAP];
   uint8_t st[CAP];
   GState::PendE pend[kPend];
   uint32_t hist[256];
   uint64_t hkey[kWave];
-  uint32_t hrid[kWave], hdec[kWave];
+  uint32_t hrid[kWave];
   QLds row;  // q_pick_peers' re-rank scratch
 };
 
@@ -314,9 +318,10 @@ __device__ uint64_t w_select_kth(DeepWave<CAP>& d, uint32_t lane, uint32_t n, ui
   return prefix;
 }
 
-// intent items that came from the packed tail enter the head with their rumor's decoration
+// the intent queue's head items get their rumor's record decoration (w_take_head leaves
+// kDecLookup; the query / event queues' decorations are constants)
 __device__ __forceinline__ void head_dec_fix(const GCfg& c, const GState& s, QRegs& Q) {
-  if (Q.dec == kDecLookup) Q.dec = s.rdec[Q.r & c.rmask];
+  if (Q.dec == kDecLookup && Q.r != kEmpty) Q.dec = s.rdec[Q.r & c.rmask];
 }
 
 // head = the qcap smallest live keys, sorted into the lanes of Q (marked kDeepInHead in LDS);
@@ -375,7 +380,6 @@ __device__ __forceinline__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uin
         const uint32_t pos = base + mbcnt(m);
         d.hkey[pos] = kr[r];
         d.hrid[pos] = d.rid[i];
-        d.hdec[pos] = d.dec[i];
         d.st[i] = kDeepInHead;
       } else if (v) {  // stays in the tail
         km = kr[r] < km ? kr[r] : km;
@@ -410,7 +414,6 @@ __device__ __forceinline__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uin
         const uint32_t pos = base + mbcnt(m);
         d.hkey[pos] = x[u];
         d.hrid[pos] = d.rid[i];
-        d.hdec[pos] = d.dec[i];
         d.st[i] = kDeepInHead;
       } else if (v[u]) {  // stays in the tail
         km = x[u] < km ? x[u] : km;
@@ -434,7 +437,7 @@ __device__ __forceinline__ void w_take_head(const GCfg& c, DeepWave<CAP>& d, uin
   const uint32_t dest = h ? rank : hn + mbcnt(~hm);
   const int addr = (int)(dest * 4);
   const uint32_t r = h ? d.hrid[lane] : kEmpty, sq = h ? key_seq(mk) : 0u, tl = h ? key_tl(mk) : 0u,
-                 dc = h ? d.hdec[lane] : (q == 1 ? kDecQuery : kDecEvent);
+                 dc = q == 0 ? kDecLookup : (q == 1 ? kDecQuery : kDecEvent);  // (head_dec fills the intents')
   Q.r = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)r);
   Q.sq = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)sq);
   Q.tl = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)tl);
@@ -501,7 +504,7 @@ __device__ __forceinline__ uint32_t w_store_tail(const GCfg& c, const GState& s,
     if (live) {
       const uint32_t at = sealed ? bs + mbcnt(ms) : br + mbcnt(mr);
       if (q == 0) t8[at] = tail_pack(c, d.rid[i], key_seq(k), key_tl(k));
-      else t[at] = make_uint4(d.rid[i], key_seq(k), key_tl(k), d.dec[i]);
+      else t[at] = make_uint4(d.rid[i], key_seq(k), key_tl(k), q == 1 ? kDecQuery : kDecEvent);
     }
     if (sealed) bm = k < bm ? k : bm;
     bs += (uint32_t)__popcll(ms);
@@ -518,7 +521,6 @@ __device__ __forceinline__ uint32_t w_store_tail(const GCfg& c, const GState& s,
 template <uint32_t CAP>
 __device__ __forceinline__ uint32_t w_load_sealed(const GCfg& c, const GState& s, uint64_t l, uint32_t q, DeepWave<CAP>& d,
                                   uint32_t lane, uint32_t n, uint32_t sm, uint32_t nseq) {
-  const uint32_t qdec = q == 1 ? kDecQuery : kDecEvent;
   for (uint32_t i = lane; i < n; i += kWave)
     if (d.st[i] == kDeepInHead) d.st[i] = kDeepLive;
   for (uint32_t b = 0; b < sm; b += kDeepU * kWave) {
@@ -530,7 +532,6 @@ __device__ __forceinline__ uint32_t w_load_sealed(const GCfg& c, const GState& s
       if (i < sm) {
         d.key[n + i] = tlq_key(e[u].z & 0xFFFF, e[u].z >> 16, e[u].y);
         d.rid[n + i] = e[u].x;
-        d.dec[n + i] = q == 0 ? kDecLookup : qdec;
         d.st[n + i] = kDeepLive;
       }
     }
@@ -641,7 +642,6 @@ __device__ __forceinline__ void deep_wave_member(const GCfg& c, const GState& s,
   uint32_t used_v = 0, nrec_v = 0, err = 0, drops = 0;
   for (uint32_t q = 0; q < 3; ++q) {
     const uint32_t nq = (pc >> (8 * q)) & 0xFF;
-    const uint32_t qdec = q == 1 ? kDecQuery : kDecEvent;
     const uint32_t qi = shfl_u32(qinfo, (int)q);
     if (qi == 0 && nq == 0) continue;  // nothing in head, tail or pending list
     // every item of the queue into LDS: the head's live prefix, the tail, then the pending
@@ -683,7 +683,6 @@ __device__ __forceinline__ void deep_wave_member(const GCfg& c, const GState& s,
     if (hl) {
       d.key[lane] = tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq);
       d.rid[lane] = Q.r;
-      d.dec[lane] = Q.dec;
       d.st[lane] = kDeepLive;
     }
     for (uint32_t b = 0;;) {
@@ -693,7 +692,6 @@ __device__ __forceinline__ void deep_wave_member(const GCfg& c, const GState& s,
         if (i < tn) {
           d.key[hn + i] = tlq_key(e[u].z & 0xFFFF, e[u].z >> 16, e[u].y);
           d.rid[hn + i] = e[u].x;
-          d.dec[hn + i] = q == 0 ? kDecLookup : qdec;
           d.st[hn + i] = kDeepLive;
         }
       }
@@ -715,7 +713,6 @@ __device__ __forceinline__ void deep_wave_member(const GCfg& c, const GState& s,
           const uint32_t r = rank0 + mbcnt(m), j = n + r;
           d.key[j] = tlq_key(0, d.pend[i].lq & 0xFFFF, seq0 + r);
           d.rid[j] = d.pend[i].rid;
-          d.dec[j] = q == 0 ? d.pend[i].dec : qdec;
           d.st[j] = kDeepLive;
         }
         rank0 += (uint32_t)__popcll(m);
@@ -853,7 +850,7 @@ __device__ __forceinline__ void deep_wave_member(const GCfg& c, const GState& s,
             d.st[wi] = kDeepPicked;
             if (nrec + k < c.cap_t && off != ~0ull) {
               ov[off + nrec + k] = d.rid[wi];
-              if (od) od[off + nrec + k] = d.dec[wi] == kDecLookup ? s.rdec[d.rid[wi] & c.rmask] : d.dec[wi];
+              if (od) od[off + nrec + k] = q == 0 ? s.rdec[d.rid[wi] & c.rmask] : (q == 1 ? kDecQuery : kDecEvent);
             }
           }
           k++;

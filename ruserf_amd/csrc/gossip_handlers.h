@@ -217,7 +217,7 @@ constexpr uint32_t kPendMerge = kPend - 8;
 // items of one queue the deferred-emission path holds in LDS: the full depth plus a pending
 // list (kDeepItems, 1 wave per CU), and three smaller capacities for the common cases -- with a
 // sealed tail prefix the path reads only the head, the reserve, the items spilled since the last
-// refill and the pending list (kDeepTiny 8, kDeepSmall 6, kDeepMid 3 waves per CU)
+// refill and the pending list (kDeepTiny and kDeepSmall 8 waves per CU, kDeepMid 4; no per-item decoration in LDS)
 constexpr uint32_t kDeepItems = RSF_MAX_QUEUE_DEPTH + kPend;
 constexpr uint32_t kDeepTiny = 640 + 64 + kPend;
 constexpr uint32_t kDeepSmall = 1024 + 64 + kPend;
