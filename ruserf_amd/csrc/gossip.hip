@@ -2853,17 +2853,34 @@ __global__ void __launch_bounds__(256) bucket_index_kernel(Buckets bk, uint64_t 
   }
 }
 // receive side: every record slot of a received group gets its decoration from the
-// replicated rumor table (slots past the group's count are never read by the merge)
+// replicated rumor table (slots past the group's count are never read by the merge).
+// Grid (slot blocks, run): 32-bit slot arithmetic within a run (the host checks gcap * cap_t
+// < 2^32), and a block past the run's groups leaves at once -- one thread per slot of a
+// 64-bit flattened grid spent most of its time in two 64-bit divisions (0.25 ms per round at
+// 1M members)
 __global__ void __launch_bounds__(256) bucket_dec_kernel(Buckets bk, uint32_t cap_t, const uint32_t* __restrict__ rdec,
                                                          uint32_t rmask, uint32_t* __restrict__ decs) {
-  const uint64_t per = (uint64_t)bk.gcap * cap_t;
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t r = (uint32_t)(t / per);
-  if (r >= bk.n_runs) return;
-  const uint64_t i = t - (uint64_t)r * per, grp = i / cap_t;
+  const uint32_t r = blockIdx.y;
   const uint32_t* b = bk.run(r);
-  if (grp >= b[0] || (uint32_t)(i - grp * cap_t) >= b[bk.cnt_off + grp]) return;
-  decs[t] = rdec[b[bk.vals_off + i] & rmask];
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;  // record slot within run r
+  if (i >= b[0] * cap_t) return;
+  const uint32_t grp = i / cap_t;
+  if (i - grp * cap_t >= b[bk.cnt_off + grp]) return;
+  decs[(uint64_t)r * bk.gcap * cap_t + i] = rdec[b[bk.vals_off + i] & rmask];
+}
+
+// several device buffers cleared by one launch (each hipMemsetAsync is a launch of its own,
+// ~5 us on the stream however small the buffer): up to kZeroSpans spans of 4-B words
+constexpr int kZeroSpans = 4;
+struct ZeroSpans {
+  uint32_t* p[kZeroSpans];
+  uint64_t words[kZeroSpans];
+};
+__global__ void __launch_bounds__(256) zero_spans_kernel(ZeroSpans z) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+#pragma unroll
+  for (int k = 0; k < kZeroSpans; ++k)
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < z.words[k]; i += stride) z.p[k][i] = 0u;
 }
 
 // counters[60] (records merged since creation) += counters[from] (this round's)
@@ -3690,11 +3707,23 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
   g->ahead_launched = g->ahead_valid = false;
   int rc;
   if (!use_ahead && (rc = peers_and_sort(g, round, st))) return rc;
-  if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, kDeepLists * 4, st));  // the emission's deferred-member lists
-  RSF_HIP(hipMemsetAsync(g->grp_cnt, 0, ng * 4, st));
-  if (local) {
-    RSF_HIP(hipMemsetAsync(g->seg_start, 0, c.n_loc * 4, st));
-    RSF_HIP(hipMemsetAsync(g->seg_end, 0, c.n_loc * 4, st));
+  {
+    // the emission's deferred-member lists, the group counts (buckets carry their own), the
+    // segment bounds of the single-context merge: one launch
+    ZeroSpans z{};
+    int k = 0;
+    if (c.deep) z.p[k] = g->s.deep_n, z.words[k++] = kDeepLists;
+    if (!world) z.p[k] = g->grp_cnt, z.words[k++] = ng;
+    if (local) {
+      z.p[k] = g->seg_start, z.words[k++] = c.n_loc;
+      z.p[k] = g->seg_end, z.words[k++] = c.n_loc;
+    }
+    uint64_t most = 0;
+    for (int i = 0; i < k; ++i) most = std::max(most, z.words[i]);
+    if (most) {
+      hipLaunchKernelGGL(zero_spans_kernel, dim3((unsigned)std::min<uint64_t>(grid1(most), 2048)), dim3(256), 0, st, z);
+      RSF_HIP(hipGetLastError());
+    }
   }
   const dim3 egrid(grid1((c.n_loc + RSF_EMIT_PER_WAVE - 1) / RSF_EMIT_PER_WAVE, RSF_EMIT_WPB));
   if (world) {
@@ -3853,6 +3882,7 @@ int rsf_gossip_bucket_buffers(rsf_gossip* g, uint32_t world, void** send, void**
     const uint64_t expect = (c.n_loc * c.fanout + world - 1) / world;
     const uint64_t gcap = std::min<uint64_t>(expect + expect / 8 + 4096, c.n_loc * c.fanout);
     if (gcap >= kBktIdxMask) return gerr("bucket capacity exceeds the slot word's 26-bit place field");
+    if (gcap * (c.cap_t + 2) + 64 >= (1ull << 32)) return gerr("a bucket's record slots exceed 32-bit indexing");
     g->bkt_gcap = (uint32_t)gcap;
     const Buckets b = bucket_layout(g, world);
     const size_t bytes = (size_t)b.stride_u32 * 4 * world;
@@ -3897,8 +3927,8 @@ int rsf_gossip_round_merge_buckets(rsf_gossip* g, uint32_t world) {
                      g->d_counters + 58, c.cap_t, (const uint32_t*)g->s.rdec, c.rmask,
                      RSF_BUCKET_DEC_MODE == 1 ? g->bkt_dec : nullptr);
   if (RSF_BUCKET_DEC_MODE == 0)
-    hipLaunchKernelGGL(bucket_dec_kernel, dim3(grid1((uint64_t)world * bk.gcap * c.cap_t)), dim3(256), 0, st, bk,
-                       c.cap_t, (const uint32_t*)g->s.rdec, c.rmask, g->bkt_dec);
+    hipLaunchKernelGGL(bucket_dec_kernel, dim3((unsigned)grid1((uint64_t)bk.gcap * c.cap_t), world), dim3(256), 0, st,
+                       bk, c.cap_t, (const uint32_t*)g->s.rdec, c.rmask, g->bkt_dec);
   hipLaunchKernelGGL(accumulate_kernel, dim3(1), dim3(64), 0, st, g->d_counters, 57u);
   if (g->profiling && g->prof_rounds < rsf_gossip::kMaxProfRounds)
     hipEventRecord(g->ev[g->prof_rounds][3], g->stream);  // exchange time lands in the sort slot
