@@ -1251,26 +1251,24 @@ __global__ void __launch_bounds__(256) grp_index_kernel(const uint32_t* __restri
 #endif
 
 // Multi-GPU exchange buckets (rsf_gossip_round_emit_buckets): one bucket per destination
-// shard, u32 layout [n_groups, 3 x pad | keys[gcap] | cnt[gcap] | vals[gcap * cap_t]]; the
-// groups of a bucket are sorted by receiver.  On the receive side the world's buckets arrive
+// shard, u32 layout [n_groups, 3 x pad | keys[gcap] | cnt[gcap] | vals[gcap * cap_t] |
+// decs[gcap * cap_t]]; the groups of a bucket are sorted by receiver.  On the receive side the world's buckets arrive
 // back to back in source-rank order = runs.  The bucket a shard addresses to itself never
 // travels: the receive side reads run `self_run` from the send buffer (the receive buffer's
 // slot for it is left as it is), so the exchange moves (world - 1) buckets per rank.
-// Record decorations do not travel either: every shard holds the whole rumor table, so the
-// receive side looks them up from the rumor ids (rdec, L2-resident) -- 44 B per group on
-// the wire instead of 80.
+// Record decorations travel with the rumor ids (80 B per group of 9 slots instead of 44):
+// emission has them in registers, while rebuilding them on the receive side from the
+// replicated rumor table cost a random 64-B sector per record -- 0.24 ms per round at 1M
+// members in the reference regime, whose picks span millions of rumor ids (the merge looking
+// them up itself, a separate pass per slot or per group: all slower).
 constexpr uint32_t kMaxRuns = 8;
-#ifndef RSF_BUCKET_DEC_MODE
-#define RSF_BUCKET_DEC_MODE 0  // receive-side decorations: see bucket_index_kernel
-#endif
 struct Buckets {
   const uint32_t* base;  // receive buffer (RUNS merge); emission writes through `send`
   uint32_t* send;        // send buffer (emission into buckets)
   const uint32_t* wstart;  // emission: per destination shard, its first group in sorted order
   uint64_t per;            // members per shard
   uint64_t stride_u32;   // one bucket
-  const uint32_t* decs;  // RSF_BUCKET_DEC_MODE < 2: the records' decorations, [run][gcap * cap_t]
-  uint32_t keys_off, cnt_off, vals_off, gcap, n_runs, self_run;
+  uint32_t keys_off, cnt_off, vals_off, decs_off, gcap, n_runs, self_run;
   // run r's bucket on the receive side
   __device__ __forceinline__ const uint32_t* run(uint32_t r) const {
     return (r == self_run ? (const uint32_t*)send : base) + (uint64_t)r * stride_u32;
@@ -1468,7 +1466,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
     }
     if (BKT) {
       ov = bk.send;
-      od = nullptr;  // decorations are rebuilt on the receive side
+      od = bk.send + (bk.decs_off - bk.vals_off);  // (off addresses the vals: the decs sit a fixed distance on)
     }
     uint32_t used_v = 0, nrec_v = 0;
 #if RSF_EMIT_PROF
@@ -1653,7 +1651,7 @@ __device__ __forceinline__ void emit_run4(const GCfg& c, const GState& s, const 
     }
     if (BKT) {
       ov = bk.send;
-      od = nullptr;
+      od = bk.send + (bk.decs_off - bk.vals_off);
     }
     uint32_t used_v = 0, nrec_v = 0;
     if (ne0) q4_pick_peers<true>(c, Q0, lane, np, used_v, nrec_v, off, ov, od, err, d0, row);
@@ -1981,11 +1979,7 @@ __device__ __forceinline__ void merge_one(const GCfg& c, const GState& s, const 
       const uint32_t* b = bk.run(r);
       if (in) {
         rid0 = rec_ld(b + bk.vals_off + g * stride + gk);
-#if RSF_BUCKET_DEC_MODE < 2
-        dsub0 = rec_ld(bk.decs + (uint64_t)r * bk.gcap * stride + g * stride + gk);
-#else
-        dsub0 = s.rdec[rid0 & c.rmask];  // decorations do not travel (see Buckets)
-#endif
+        dsub0 = rec_ld(b + bk.decs_off + g * stride + gk);
         gc = rec_ld(b + bk.cnt_off + g);
       }
     } else {
@@ -2803,22 +2797,11 @@ __global__ void bucket_bounds_kernel(const uint32_t* __restrict__ key_s, uint64_
 // merged (group counts) summed for the statistics; a receiver outside the shard or an
 // unsorted bucket is flagged.  Grid-stride over a bounded grid: one atomic per block (an
 // atomic per 256 groups on one address serialised into ~0.25 ms at 6M groups).
-// RSF_BUCKET_DEC_MODE: where the receive side gets its records' decorations --
-//   0  bucket_dec_kernel rebuilds them into `decs` (one thread per record slot).  The default:
-//      in the reference regime at 1M members (a rumor table of 2 x 8M ids, 64 MB of
-//      decorations) the merge's own lookups cost more (5.19 vs 5.31 ms per round, same box)
-//   1  this pass rebuilds them (one thread per group: measured slower still, 6.24 vs 6.11
-//      ms per round at 2M, the per-group loops diverge)
-//   2  the merge looks each one up from the rumor id it has just read (no pass, no array;
-//      round 4's choice at 2M members with 64-slot queues, where the table is small: the
-//      decoration pass cost 0.32 ms there, most of it launching and indexing 61M threads)
-constexpr unsigned kBucketIndexBlocks = RSF_BUCKET_DEC_MODE == 1 ? 4096 : 1024;
+constexpr unsigned kBucketIndexBlocks = 1024;
 __global__ void __launch_bounds__(256) bucket_index_kernel(Buckets bk, uint64_t lo, uint64_t n_loc,
                                                            uint32_t* __restrict__ rstart, uint32_t* __restrict__ rend,
                                                            unsigned long long* __restrict__ merged,
-                                                           unsigned long long* __restrict__ flags, uint32_t cap_t,
-                                                           const uint32_t* __restrict__ rdec, uint32_t rmask,
-                                                           uint32_t* __restrict__ decs) {
+                                                           unsigned long long* __restrict__ flags) {
   const uint64_t n = (uint64_t)bk.n_runs * bk.gcap;
   uint64_t sum = 0;
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
@@ -2836,12 +2819,6 @@ __global__ void __launch_bounds__(256) bucket_index_kernel(Buckets bk, uint64_t 
     sum += cnt;
     if (i == 0 || b[bk.keys_off + i - 1] != key) rstart[(uint64_t)r * n_loc + l] = i;
     if (i + 1 == ng || b[bk.keys_off + i + 1] != key) rend[(uint64_t)r * n_loc + l] = i + 1;
-    if (decs) {
-      const uint32_t* v = b + bk.vals_off + (uint64_t)i * cap_t;
-      uint32_t* d = decs + ((uint64_t)r * bk.gcap + i) * cap_t;
-      const uint32_t k_end = cnt < cap_t ? cnt : cap_t;
-      for (uint32_t k = 0; k < k_end; ++k) d[k] = rdec[v[k] & rmask];
-    }
   }
   __shared__ uint64_t part[4];
   for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
@@ -2852,23 +2829,6 @@ __global__ void __launch_bounds__(256) bucket_index_kernel(Buckets bk, uint64_t 
     if (tot) atomicAdd(merged, tot);
   }
 }
-// receive side: every record slot of a received group gets its decoration from the
-// replicated rumor table (slots past the group's count are never read by the merge).
-// Grid (slot blocks, run): 32-bit slot arithmetic within a run (the host checks gcap * cap_t
-// < 2^32), and a block past the run's groups leaves at once -- one thread per slot of a
-// 64-bit flattened grid spent most of its time in two 64-bit divisions (0.25 ms per round at
-// 1M members)
-__global__ void __launch_bounds__(256) bucket_dec_kernel(Buckets bk, uint32_t cap_t, const uint32_t* __restrict__ rdec,
-                                                         uint32_t rmask, uint32_t* __restrict__ decs) {
-  const uint32_t r = blockIdx.y;
-  const uint32_t* b = bk.run(r);
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;  // record slot within run r
-  if (i >= b[0] * cap_t) return;
-  const uint32_t grp = i / cap_t;
-  if (i - grp * cap_t >= b[bk.cnt_off + grp]) return;
-  decs[(uint64_t)r * bk.gcap * cap_t + i] = rdec[b[bk.vals_off + i] & rmask];
-}
-
 // several device buffers cleared by one launch (each hipMemsetAsync is a launch of its own,
 // ~5 us on the stream however small the buffer): up to kZeroSpans spans of 4-B words
 constexpr int kZeroSpans = 4;
@@ -2982,7 +2942,7 @@ struct rsf_gossip {
   uint32_t cur_round = 0;
   bool merged_from_stage = true, merged_from_buckets = false;
   // bucket exchange: send / receive buffers (world buckets each), group ranges per run
-  uint32_t *bkt_send = nullptr, *bkt_recv = nullptr, *bkt_dec = nullptr, *d_rstart = nullptr, *d_rend = nullptr, *d_wstart = nullptr;
+  uint32_t *bkt_send = nullptr, *bkt_recv = nullptr, *d_rstart = nullptr, *d_rend = nullptr, *d_wstart = nullptr;
   uint32_t bkt_world = 0, bkt_gcap = 0;
   uint64_t total_merged_host = 0;  // multi-GPU merges (n_recv known on host)
   // run-merge tables of rsf_gossip_round_merge_runs: [run_cap][n_loc] u32 x3, [n_loc] u32
@@ -3321,7 +3281,7 @@ int rsf_gossip_destroy(rsf_gossip* g) {
                   g->run_start, g->run_end, g->run_base, g->run_total, g->d_run_off,
                   g->grp_key, g->grp_cnt, g->grp_key_s, g->grp_id, g->grp_id_s,
                   g->grp_slot, g->grp_off, g->dec_base, s.dlog, s.dmeta, s.dcnt,
-                  g->bkt_send, g->bkt_recv, g->bkt_dec, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn,
+                  g->bkt_send, g->bkt_recv, g->d_rstart, g->d_rend, g->d_wstart, s.snap_bits, s.snap_sn,
                   s.p_ent, s.p_cnt, g->big_base, s.tail0, s.tail1, s.tail2, s.tsum, s.deep_ids,
                   s.tseal, g->qmax, g->d_act_status, g->occ_hist};
   for (void* p : ptrs)
@@ -3824,7 +3784,8 @@ static Buckets bucket_layout(const rsf_gossip* g, uint32_t world) {
   b.keys_off = 4;
   b.cnt_off = b.keys_off + b.gcap;
   b.vals_off = b.cnt_off + b.gcap;
-  b.stride_u32 = ((uint64_t)b.vals_off + (uint64_t)b.gcap * c.cap_t + 63) & ~63ull;  // 256-B aligned buckets
+  b.decs_off = b.vals_off + b.gcap * c.cap_t;
+  b.stride_u32 = ((uint64_t)b.decs_off + (uint64_t)b.gcap * c.cap_t + 63) & ~63ull;  // 256-B aligned buckets
   b.per = world ? c.N / world : c.N;
   b.n_runs = world;
   b.self_run = (uint32_t)(c.lo / b.per);
@@ -3835,7 +3796,6 @@ static Buckets send_buckets(rsf_gossip* g) {
   b.send = g->bkt_send;
   b.wstart = g->d_wstart;
   b.base = g->bkt_recv;
-  b.decs = g->bkt_dec;
   return b;
 }
 
@@ -3873,22 +3833,21 @@ int rsf_gossip_bucket_buffers(rsf_gossip* g, uint32_t world, void** send, void**
   if (world != g->bkt_world) {
     RSF_HIP(hipSetDevice(g->device));
     RSF_HIP(hipStreamSynchronize(g->stream));
-    for (void* p : {(void*)g->bkt_send, (void*)g->bkt_recv, (void*)g->bkt_dec, (void*)g->d_rstart, (void*)g->d_rend})
+    for (void* p : {(void*)g->bkt_send, (void*)g->bkt_recv, (void*)g->d_rstart, (void*)g->d_rend})
       if (p) hipFree(p);
-    g->bkt_send = g->bkt_recv = g->bkt_dec = g->d_rstart = g->d_rend = nullptr;
+    g->bkt_send = g->bkt_recv = g->d_rstart = g->d_rend = nullptr;
     g->bkt_world = 0;
     // groups per destination: n_loc * fanout / world for uniform peers; the capacity holds
     // 1/8 more plus 4096 (overflow is flagged, rsf_gossip_bucket_status)
     const uint64_t expect = (c.n_loc * c.fanout + world - 1) / world;
     const uint64_t gcap = std::min<uint64_t>(expect + expect / 8 + 4096, c.n_loc * c.fanout);
     if (gcap >= kBktIdxMask) return gerr("bucket capacity exceeds the slot word's 26-bit place field");
-    if (gcap * (c.cap_t + 2) + 64 >= (1ull << 32)) return gerr("a bucket's record slots exceed 32-bit indexing");
+    if (gcap * (2 * c.cap_t + 2) + 64 >= (1ull << 32)) return gerr("a bucket exceeds 32-bit word offsets");
     g->bkt_gcap = (uint32_t)gcap;
     const Buckets b = bucket_layout(g, world);
     const size_t bytes = (size_t)b.stride_u32 * 4 * world;
     int rc;
     if ((rc = rsf::dmalloc((void**)&g->bkt_send, bytes)) || (rc = rsf::dmalloc((void**)&g->bkt_recv, bytes)) ||
-        (RSF_BUCKET_DEC_MODE < 2 && (rc = rsf::dmalloc((void**)&g->bkt_dec, (size_t)world * gcap * c.cap_t * 4))) ||
         (rc = rsf::dmalloc((void**)&g->d_rstart, (size_t)world * c.n_loc * 4)) ||
         (rc = rsf::dmalloc((void**)&g->d_rend, (size_t)world * c.n_loc * 4)))
       return rc;
@@ -3919,16 +3878,17 @@ int rsf_gossip_round_merge_buckets(rsf_gossip* g, uint32_t world) {
   RSF_HIP(hipSetDevice(g->device));
   hipStream_t st = g->stream;
   const Buckets bk = send_buckets(g);
-  RSF_HIP(hipMemsetAsync(g->d_rstart, 0, (size_t)world * c.n_loc * 4, st));
-  RSF_HIP(hipMemsetAsync(g->d_rend, 0, (size_t)world * c.n_loc * 4, st));
-  RSF_HIP(hipMemsetAsync(g->d_counters + 57, 0, 8, st));
+  {  // the runs' receiver ranges and the records-merged counter: one launch
+    ZeroSpans z{};
+    z.p[0] = g->d_rstart, z.words[0] = (uint64_t)world * c.n_loc;
+    z.p[1] = g->d_rend, z.words[1] = (uint64_t)world * c.n_loc;
+    z.p[2] = reinterpret_cast<uint32_t*>(g->d_counters + 57), z.words[2] = 2;
+    hipLaunchKernelGGL(zero_spans_kernel, dim3((unsigned)std::min<uint64_t>(grid1(z.words[0]), 2048)), dim3(256), 0, st, z);
+    RSF_HIP(hipGetLastError());
+  }
   hipLaunchKernelGGL(bucket_index_kernel, dim3(std::min<uint64_t>(grid1((uint64_t)world * bk.gcap), kBucketIndexBlocks)),
                      dim3(256), 0, st, bk, c.lo, c.n_loc, g->d_rstart, g->d_rend, g->d_counters + 57,
-                     g->d_counters + 58, c.cap_t, (const uint32_t*)g->s.rdec, c.rmask,
-                     RSF_BUCKET_DEC_MODE == 1 ? g->bkt_dec : nullptr);
-  if (RSF_BUCKET_DEC_MODE == 0)
-    hipLaunchKernelGGL(bucket_dec_kernel, dim3((unsigned)grid1((uint64_t)bk.gcap * c.cap_t), world), dim3(256), 0, st,
-                       bk, c.cap_t, (const uint32_t*)g->s.rdec, c.rmask, g->bkt_dec);
+                     g->d_counters + 58);
   hipLaunchKernelGGL(accumulate_kernel, dim3(1), dim3(64), 0, st, g->d_counters, 57u);
   if (g->profiling && g->prof_rounds < rsf_gossip::kMaxProfRounds)
     hipEventRecord(g->ev[g->prof_rounds][3], g->stream);  // exchange time lands in the sort slot

@@ -638,7 +638,7 @@ __device__ __forceinline__ void deep_wave_member(const GCfg& c, const GState& s,
   }
   bool pend_lds = false;
   uint32_t* const ov = BKT ? bk.send : out_val;
-  uint32_t* const od = BKT ? nullptr : out_dec;
+  uint32_t* const od = BKT ? bk.send + (bk.decs_off - bk.vals_off) : out_dec;
   uint32_t used_v = 0, nrec_v = 0, err = 0, drops = 0;
   for (uint32_t q = 0; q < 3; ++q) {
     const uint32_t nq = (pc >> (8 * q)) & 0xFF;
