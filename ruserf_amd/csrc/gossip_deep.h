@@ -976,6 +976,555 @@ __global__ void __launch_bounds__(kWave) emit_deep_wave_kernel(GCfg c, GState s,
 #endif
 }
 
+// ---- the full-depth class: one 256-thread block per member ----------------------------------
+// The members whose queues need the full depth (a few hundred per round in the reference
+// regime: the re-listed ones and the largest queues) ran one wave each at one wave per CU (the
+// class holds 117 KB of LDS), each pass over their 5-9k items a long one-wave loop.  Here the
+// block's four waves share the streaming work -- the tail load, the key range, the radix
+// selects, the head gather and the tail store -- while the head's register work (q_load, the
+// picks, q_store and the rare per-peer fallback) stays with wave 0.  Always the whole queue (no
+// recent mode): the same items result; the tail's slot order and seal may differ from the
+// one-wave path's (neither is observable: the tail is unordered, its seal only a bound).
+constexpr uint32_t kDeepBlkWaves = 4, kDeepBlkThreads = kDeepBlkWaves * kWave;
+struct DeepBlk {
+  uint64_t r64[kDeepBlkWaves][4];  // per-wave partials of the block reductions
+  uint32_t r32[kDeepBlkWaves][4];
+  uint64_t hk[kDeepBlkWaves][kWave];  // the head gather: each wave's items, in its range's order
+  uint32_t hr[kDeepBlkWaves][kWave];
+  uint32_t u[8];  // wave 0's broadcasts: [0..2] select digit / need / bucket count, [4] hn, [5] unsafe
+};
+__device__ __forceinline__ uint64_t b_min_u64(uint64_t v, DeepBlk& x, uint32_t tid) {
+  v = wave_min_u64(v);
+  if ((tid & (kWave - 1)) == 0) x.r64[tid / kWave][3] = v;
+  __syncthreads();
+  uint64_t m = x.r64[0][3];
+#pragma unroll
+  for (uint32_t w = 1; w < kDeepBlkWaves; ++w) m = x.r64[w][3] < m ? x.r64[w][3] : m;
+  __syncthreads();
+  return m;
+}
+// items [lo, hi) of wave w's contiguous range (a multiple of 64 per wave): deterministic
+// compaction orders without a block scan per 64 items
+__device__ __forceinline__ void b_wave_range(uint32_t n, uint32_t w, uint32_t& lo, uint32_t& hi) {
+  const uint32_t per = ((n + kDeepBlkThreads - 1) / kDeepBlkThreads) * kWave;
+  lo = min(n, w * per);
+  hi = min(n, lo + per);
+}
+template <uint32_t CAP>
+__device__ WRange b_range(const DeepWave<CAP>& d, DeepBlk& x, uint32_t tid, uint32_t n, uint8_t state) {
+  uint32_t cnt = 0, c0 = 0;
+  uint64_t lo = ~0ull, hi = 0, an = ~0ull, orr = 0;
+  for (uint32_t b = 0; b < n; b += kDeepU * kDeepBlkThreads) {
+    uint64_t xk[kDeepU];
+    uint32_t sv[kDeepU];
+#pragma unroll
+    for (uint32_t u = 0; u < kDeepU; ++u) {
+      const uint32_t i = b + u * kDeepBlkThreads + tid, ii = i < n ? i : 0u;
+      sv[u] = d.st[ii];
+      xk[u] = d.key[ii];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kDeepU; ++u)
+      if (b + u * kDeepBlkThreads + tid < n && sv[u] == state) {
+        cnt++;
+        c0 += (xk[u] >> 48) == 0 ? 1u : 0u;
+        lo = xk[u] < lo ? xk[u] : lo;
+        hi = xk[u] > hi ? xk[u] : hi;
+        an &= xk[u];
+        orr |= xk[u];
+      }
+  }
+  const uint32_t w = tid / kWave;
+  cnt = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(cnt), 63);
+  c0 = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_sum_u32(c0), 63);
+  lo = wave_min_u64(lo);
+  hi = wave_max_u64(hi);
+  an = wave_and_u64(an);
+  orr = wave_or_u64(orr);
+  if ((tid & (kWave - 1)) == 0) {
+    x.r64[w][0] = lo;
+    x.r64[w][1] = hi;
+    x.r64[w][2] = an;
+    x.r64[w][3] = orr;
+    x.r32[w][0] = cnt;
+    x.r32[w][1] = c0;
+  }
+  __syncthreads();
+  WRange r{0u, 0u, ~0ull, 0ull, ~0ull, 0ull};
+#pragma unroll
+  for (uint32_t v = 0; v < kDeepBlkWaves; ++v) {
+    r.cnt += x.r32[v][0];
+    r.cnt_t0 += x.r32[v][1];
+    r.lo = x.r64[v][0] < r.lo ? x.r64[v][0] : r.lo;
+    r.hi = x.r64[v][1] > r.hi ? x.r64[v][1] : r.hi;
+    r.an &= x.r64[v][2];
+    r.orr |= x.r64[v][3];
+  }
+  __syncthreads();
+  return r;
+}
+// w_select_kth's LDS radix select, the key passes shared by the block's waves
+template <uint32_t CAP>
+__device__ uint64_t b_select_kth(DeepWave<CAP>& d, DeepBlk& x, uint32_t tid, uint32_t n, uint32_t k, uint8_t state,
+                                 const WRange& rg) {
+  if (k <= 1 || rg.lo == rg.hi) return rg.lo;
+  const uint32_t lane = tid & (kWave - 1), w = tid / kWave;
+  const uint64_t var = rg.an ^ rg.orr;
+  uint64_t prefix = 0, mask = 0;
+  uint32_t need = k;
+  const bool t0 = rg.cnt_t0 >= k;
+  if (t0) mask = 0xFFFFull << 48;
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    const uint64_t bm = 0xFFull << shift;
+    if (t0 && shift >= 48) continue;
+    if (!(var & bm)) {
+      prefix |= rg.an & bm;
+      mask |= bm;
+      continue;
+    }
+    d.hist[tid] = 0;  // (256 threads, 256 bins)
+    __syncthreads();
+    for (uint32_t b = 0; b < n; b += kDeepU * kDeepBlkThreads) {
+      uint64_t xk[kDeepU];
+      uint32_t sv[kDeepU];
+#pragma unroll
+      for (uint32_t u = 0; u < kDeepU; ++u) {
+        const uint32_t i = b + u * kDeepBlkThreads + tid, ii = i < n ? i : 0u;
+        sv[u] = d.st[ii];
+        xk[u] = d.key[ii];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kDeepU; ++u) {
+        const bool in = b + u * kDeepBlkThreads + tid < n && sv[u] == state && (xk[u] & mask) == prefix;
+        const uint32_t dg = (uint32_t)(xk[u] >> shift) & 0xFF;
+        const uint64_t am = ballot(in);
+        if (!am) continue;
+        const int f = __ffsll((long long)am) - 1;
+        const uint32_t d0 = shfl_u32(dg, f);
+        const uint64_t same = ballot(in && dg == d0);
+        if (lane == (uint32_t)f) atomicAdd(&d.hist[d0], (uint32_t)__popcll(same));
+        else if (in && dg != d0) atomicAdd(&d.hist[dg], 1u);
+      }
+    }
+    __syncthreads();
+    if (w == 0) {  // the digit holding the need-th key: running counts, four bins per lane
+      const uint32_t h0 = d.hist[4 * lane], h1 = d.hist[4 * lane + 1], h2 = d.hist[4 * lane + 2], h3 = d.hist[4 * lane + 3];
+      const uint32_t sum = h0 + h1 + h2 + h3, incl = wave_inclusive_sum_u32(sum), excl = incl - sum;
+      if (excl < need && need <= incl) {
+        uint32_t b = 0, acc = excl, hb = h0;
+        if (acc + h0 < need) {
+          acc += h0;
+          b = 1;
+          hb = h1;
+          if (acc + h1 < need) {
+            acc += h1;
+            b = 2;
+            hb = h2;
+            if (acc + h2 < need) {
+              acc += h2;
+              b = 3;
+              hb = h3;
+            }
+          }
+        }
+        x.u[0] = 4 * lane + b;
+        x.u[1] = need - acc;
+        x.u[2] = hb;
+      }
+    }
+    __syncthreads();
+    const uint32_t digit = x.u[0], cnt = x.u[2];
+    need = x.u[1];
+    prefix |= (uint64_t)digit << shift;
+    mask |= bm;
+    if (cnt == 1 && shift > 0) {  // one key left in the bucket: it is the k-th
+      uint64_t best = ~0ull;
+      for (uint32_t i = tid; i < n; i += kDeepBlkThreads)
+        if (d.st[i] == state && (d.key[i] & mask) == prefix) best = d.key[i];
+      return b_min_u64(best, x, tid);
+    }
+  }
+  return prefix;
+}
+// w_take_head with the block: the range, the two selects and the gather shared; wave 0 ranks
+// the head's keys and permutes them into its register head Q.  tmin / tminlen / rres are
+// block-uniform.
+template <uint32_t CAP>
+__device__ __forceinline__ void b_take_head(const GCfg& c, DeepWave<CAP>& d, DeepBlk& x, uint32_t tid, uint32_t n,
+                                            uint32_t q, QRegs& Q, uint64_t& tmin, uint32_t& tminlen, uint64_t& rres) {
+  const uint32_t lane = tid & (kWave - 1), w = tid / kWave;
+  const WRange rg = b_range(d, x, tid, n, kDeepLive);
+  uint64_t T = ~0ull;
+  rres = ~0ull;
+#pragma unroll 1
+  for (uint32_t j = 0; j < 2; ++j) {
+    const uint32_t k = j ? c.qcap + kDeepReserve : c.qcap;
+    if (rg.cnt <= k) break;
+    const uint64_t v = b_select_kth(d, x, tid, n, k, kDeepLive, rg);
+    if (j) rres = v;
+    else T = v;
+  }
+  // the head's items (at most qcap <= 64: keys are distinct) gathered per wave range
+  uint32_t lo, hi, base = 0;
+  b_wave_range(n, w, lo, hi);
+  uint64_t km = ~0ull;
+  uint32_t lm = ~0u;
+  for (uint32_t b = lo; b < hi; b += kWave) {
+    const uint32_t i = b + lane;
+    const bool v = i < hi && d.st[i] == kDeepLive;
+    const uint64_t k = v ? d.key[i] : ~0ull;
+    const bool sel = v && k <= T;
+    const uint64_t m = ballot(sel);
+    if (sel) {
+      const uint32_t pos = base + mbcnt(m);
+      x.hk[w][pos] = k;
+      x.hr[w][pos] = d.rid[i];
+      d.st[i] = kDeepInHead;
+    } else if (v) {  // stays in the tail
+      km = k < km ? k : km;
+      lm = min(lm, key_len(k));
+    }
+    base += (uint32_t)__popcll(m);
+  }
+  if (lane == 0) x.r32[w][2] = base;
+  tmin = b_min_u64(km, x, tid);  // (its barriers publish the gather)
+  tminlen = (uint32_t)b_min_u64(lm, x, tid);
+  if (w == 0) {
+    uint32_t hn = 0, src_w = 0, src_i = lane;
+#pragma unroll
+    for (uint32_t v = 0; v < kDeepBlkWaves; ++v) {
+      const uint32_t cv = x.r32[v][2];
+      if (lane >= hn && lane < hn + cv) {
+        src_w = v;
+        src_i = lane - hn;
+      }
+      hn += cv;
+    }
+    const bool h = lane < hn;
+    const uint64_t mk = h ? x.hk[src_w][src_i] : ~0ull;
+    const uint32_t hr = h ? x.hr[src_w][src_i] : kEmpty;
+    d.hkey[lane] = mk;
+    wsync();
+    uint32_t rank = 0;
+#pragma unroll 8
+    for (uint32_t j = 0; j < hn; ++j) rank += d.hkey[j] < mk ? 1u : 0u;
+    const uint64_t hm = ballot(h);
+    const uint32_t dest = h ? rank : hn + mbcnt(~hm);
+    const int addr = (int)(dest * 4);
+    const uint32_t sq = h ? key_seq(mk) : 0u, tl = h ? key_tl(mk) : 0u,
+                   dc = q == 0 ? kDecLookup : (q == 1 ? kDecQuery : kDecEvent);
+    Q.r = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)hr);
+    Q.sq = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)sq);
+    Q.tl = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)tl);
+    Q.dec = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)dc);
+    wsync();
+  }
+}
+// w_store_tail with the block (t_lo = 0): per wave range, a count pass, one block scan, a write
+// pass -- the sealed group (keys > R) at [0, ns), the reserve after it.  Block-uniform result.
+template <uint32_t CAP>
+__device__ __forceinline__ uint32_t b_store_tail(const GCfg& c, const GState& s, uint64_t l, uint32_t q,
+                                                 DeepWave<CAP>& d, DeepBlk& x, uint32_t tid, uint32_t n, uint64_t R,
+                                                 uint32_t* nb, uint64_t* bmin) {
+  const uint32_t lane = tid & (kWave - 1), w = tid / kWave;
+  uint4* const t = q && tcap_of(c, q) ? tail16(s, q) + l * tstride_of(c, q) : nullptr;
+  uint64_t* const t8 = q == 0 && c.tcap0 ? tail8(s, c, l) : nullptr;
+  uint32_t lo, hi;
+  b_wave_range(n, w, lo, hi);
+  uint32_t ns = 0, nr = 0;
+  for (uint32_t b = lo; b < hi; b += kWave) {
+    const uint32_t i = b + lane;
+    const bool live = i < hi && d.st[i] == kDeepLive;
+    const bool sealed = live && d.key[i] > R;
+    ns += (uint32_t)__popcll(ballot(sealed));
+    nr += (uint32_t)__popcll(ballot(live && !sealed));
+  }
+  if (lane == 0) {
+    x.r32[w][0] = ns;
+    x.r32[w][1] = nr;
+  }
+  __syncthreads();
+  uint32_t ns_all = 0, so = 0, ro = 0, total = 0;
+#pragma unroll
+  for (uint32_t v = 0; v < kDeepBlkWaves; ++v) {
+    ns_all += x.r32[v][0];
+    total += x.r32[v][0] + x.r32[v][1];
+    so += v < w ? x.r32[v][0] : 0u;
+    ro += v < w ? x.r32[v][1] : 0u;
+  }
+  __syncthreads();
+  uint32_t bs = so, br = ns_all + ro;
+  uint64_t bm = ~0ull;
+  for (uint32_t b = lo; b < hi; b += kWave) {
+    const uint32_t i = b + lane;
+    const uint64_t k = i < hi ? d.key[i] : 0ull;
+    const bool live = i < hi && d.st[i] == kDeepLive;
+    const bool sealed = live && k > R, res = live && k <= R;
+    const uint64_t ms = ballot(sealed), mr = ballot(res);
+    if (live) {
+      const uint32_t at = sealed ? bs + mbcnt(ms) : br + mbcnt(mr);
+      if (q == 0) t8[at] = tail_pack(c, d.rid[i], key_seq(k), key_tl(k));
+      else t[at] = make_uint4(d.rid[i], key_seq(k), key_tl(k), q == 1 ? kDecQuery : kDecEvent);
+    }
+    if (sealed) bm = k < bm ? k : bm;
+    bs += (uint32_t)__popcll(ms);
+    br += (uint32_t)__popcll(mr);
+  }
+  *nb = ns_all;
+  *bmin = b_min_u64(bm, x, tid);
+  return total;
+}
+
+template <bool BKT>
+__device__ __forceinline__ void deep_block_member(const GCfg& c, const GState& s, uint64_t l, uint32_t tid,
+                                                  const DeepPre& pre, uint32_t* __restrict__ cnt_s,
+                                                  uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec,
+                                                  const Buckets& bk, DeepWave<kDeepBig>& d, DeepBlk& x) {
+  const uint32_t lane = tid & (kWave - 1), w = tid / kWave;
+  const uint32_t pc = pre.pc, npend = pend_total(pc);
+  const uint32_t gk = pre.gk, gs = pre.gs;
+  const uint32_t np = (uint32_t)__popcll(ballot(gk != kSentinel));
+  uint64_t off_v = ~0ull;
+  uint32_t* oc = nullptr;
+  if (lane < np) {
+    if (BKT) {
+      const uint32_t wd = gs >> kBktWShift, idx = gs & kBktIdxMask;
+      if (idx < bk.gcap) {
+        off_v = (uint64_t)wd * bk.stride_u32 + bk.vals_off + (uint64_t)idx * c.cap_t;
+        oc = bk.send + (uint64_t)wd * bk.stride_u32 + bk.cnt_off + idx;
+      }
+    } else {
+      off_v = (uint64_t)gs * c.cap_t;
+      oc = cnt_s + gs;
+    }
+  }
+  const uint32_t qinfo = pre.qinfo, qseq = pre.qseq;
+  static_assert(kPend <= kDeepBlkThreads, "one pending entry per thread");
+  if (tid < npend) d.pend[tid] = s.p_ent[l * kPend + tid];
+  uint32_t* const ov = BKT ? bk.send : out_val;
+  uint32_t* const od = BKT ? bk.send + (bk.decs_off - bk.vals_off) : out_dec;
+  uint32_t used_v = 0, nrec_v = 0, err = 0, drops = 0;  // (wave 0's)
+  __syncthreads();
+  for (uint32_t q = 0; q < 3; ++q) {
+    const uint32_t nq = (pc >> (8 * q)) & 0xFF;
+    const uint32_t qi = shfl_u32(qinfo, (int)q);
+    if (qi == 0 && nq == 0) continue;  // (block-uniform: every wave read the same first round trip)
+    const uint32_t tc = qi >> 1, nseq = shfl_u32(qseq, (int)q);
+    if (c.qcap + tc + nq > kDeepBig) {  // (the tail's capacity is below it: an engine invariant broke)
+      if (tid == 0) atomicOr(s.err + l, (uint32_t)RSF_E_DEEP_INVARIANT);
+      continue;
+    }
+    QRegs Q{kEmpty, 0, 0};
+    if (w == 0) {
+      q_load(c, s, l, q, lane, Q);
+      const bool hl = lane < c.qcap && Q.r != kEmpty;
+      const uint64_t hm = ballot(hl);
+      if (hl) {
+        d.key[lane] = tlq_key(Q.tl & 0xFFFF, Q.tl >> 16, Q.sq);
+        d.rid[lane] = Q.r;
+        d.st[lane] = kDeepLive;
+      }
+      if (lane == 0) x.u[4] = (uint32_t)__popcll(hm);
+    }
+    __syncthreads();
+    const uint32_t hn = x.u[4];
+    // the whole tail, every thread kDeepU items in flight
+    for (uint32_t b = 0; b < tc; b += kDeepU * kDeepBlkThreads) {
+      uint4 e[kDeepU];
+      if (q == 0) {
+        const uint64_t* const t8 = tail8(s, c, l);
+        uint64_t v[kDeepU];
+#pragma unroll
+        for (uint32_t u = 0; u < kDeepU; ++u) {
+          const uint32_t i = b + u * kDeepBlkThreads + tid;
+          v[u] = i < tc ? t8[i] : 0ull;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kDeepU; ++u) e[u] = tail_unpack(c, v[u], nseq);
+      } else {
+        const uint4* const t16 = tail16(s, q) + l * tstride_of(c, q);
+#pragma unroll
+        for (uint32_t u = 0; u < kDeepU; ++u) {
+          const uint32_t i = b + u * kDeepBlkThreads + tid;
+          e[u] = i < tc ? t16[i] : make_uint4(0, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kDeepU; ++u) {
+        const uint32_t i = b + u * kDeepBlkThreads + tid;
+        if (i < tc) {
+          d.key[hn + i] = tlq_key(e[u].z & 0xFFFF, e[u].z >> 16, e[u].y);
+          d.rid[hn + i] = e[u].x;
+          d.st[hn + i] = kDeepLive;
+        }
+      }
+    }
+    uint32_t n = hn + tc;
+    if (n == 0 && nq == 0) continue;
+    if (nq && w == 0) {  // the pending re-queues after them, in list order (transmits 0, the next seqs)
+      uint32_t rank0 = 0;
+      for (uint32_t b = 0; b < kPend / kWave; ++b) {
+        const uint32_t i = b * kWave + lane;
+        const bool in = i < npend && (d.pend[i].lq >> 16) == q;
+        const uint64_t m = ballot(in);
+        if (in) {
+          const uint32_t r = rank0 + mbcnt(m), j = n + r;
+          d.key[j] = tlq_key(0, d.pend[i].lq & 0xFFFF, nseq + r);
+          d.rid[j] = d.pend[i].rid;
+          d.st[j] = kDeepLive;
+        }
+        rank0 += (uint32_t)__popcll(m);
+      }
+    }
+    n += nq;
+    __syncthreads();
+    // the bounded prune to the depth (inserts with no pick in between keep the smallest keys)
+    const uint32_t depth = c.qcap + tcap_of(c, q);
+    if (n > depth) {
+      const uint64_t T = b_select_kth(d, x, tid, n, depth, kDeepLive, b_range(d, x, tid, n, kDeepLive));
+      for (uint32_t i = tid; i < n; i += kDeepBlkThreads)
+        if (d.st[i] == kDeepLive && d.key[i] > T) d.st[i] = kDeepDead;
+      drops += n - depth;
+      __syncthreads();
+    }
+    uint64_t tmin, rres;
+    uint32_t tminlen;
+    b_take_head(c, d, x, tid, n, q, Q, tmin, tminlen, rres);
+    const uint32_t used_0 = used_v, nrec_0 = nrec_v;
+    uint32_t errq = 0;
+    if (w == 0) {
+      head_dec_fix(c, s, Q);
+      bool unsafe = false, dirty = false;
+      if (q == 0)
+        q_pick_peers<true, true>(c, Q, lane, np, used_v, nrec_v, off_v, ov, od, errq, dirty, d.row, nullptr, tmin,
+                                 tminlen, &unsafe);
+      else
+        q_pick_peers<false, true>(c, Q, lane, np, used_v, nrec_v, off_v, ov, od, errq, dirty, d.row, nullptr, tmin,
+                                  tminlen, &unsafe);
+      if (lane == 0) x.u[5] = unsafe ? 1u : 0u;
+    }
+    __syncthreads();
+    const bool unsafe = x.u[5] != 0;
+    if (unsafe) {
+      // the head still cannot decide: get_broadcasts over every item, peer by peer (wave 0; rare)
+      if (w == 0) {
+        used_v = used_0;
+        nrec_v = nrec_0;
+        for (uint32_t i = lane; i < n; i += kWave)
+          if (d.st[i] == kDeepInHead) d.st[i] = kDeepLive;
+        wsync();
+        for (uint32_t j = 0; j < np; ++j) {
+          const uint32_t lim = c.limit - shfl_u32(used_v, j), nrec = shfl_u32(nrec_v, j);
+          const uint64_t off = shfl_u64(off_v, j);
+          uint32_t used = 0, k = 0;
+          for (;;) {
+            const int32_t free_b = (int32_t)(lim - used - c.overhead);
+            if (free_b <= 0) break;
+            uint64_t best = ~0ull;
+            for (uint32_t i = lane; i < n; i += kWave)
+              if (d.st[i] == kDeepLive) {
+                const uint64_t kx = d.key[i];
+                if (key_len(kx) <= (uint32_t)free_b && kx < best) best = kx;
+              }
+            best = wave_min_u64(best);
+            if (best == ~0ull) break;
+            uint32_t wi = kEmpty;
+            for (uint32_t i = lane; i < n; i += kWave)
+              if (d.st[i] == kDeepLive && d.key[i] == best) wi = i;
+            const uint64_t owner = ballot(wi != kEmpty);
+            wi = shfl_u32(wi, __ffsll((long long)owner) - 1);
+            if (lane == 0) {
+              d.st[wi] = kDeepPicked;
+              if (nrec + k < c.cap_t && off != ~0ull) {
+                ov[off + nrec + k] = d.rid[wi];
+                if (od) od[off + nrec + k] = q == 0 ? s.rdec[d.rid[wi] & c.rmask] : (q == 1 ? kDecQuery : kDecEvent);
+              }
+            }
+            k++;
+            used += c.overhead + key_len(best);
+            wsync();
+          }
+          for (uint32_t i = lane; i < n; i += kWave)  // transmits + 1, or retired at the limit
+            if (d.st[i] == kDeepPicked) {
+              if ((uint32_t)(d.key[i] >> 48) + 1 >= c.tx_limit) {
+                d.st[i] = kDeepDead;
+              } else {
+                d.key[i] += 1ull << 48;
+                d.st[i] = kDeepLive;
+              }
+            }
+          if (nrec + k > c.cap_t) err |= kErrStage;
+          used_v += lane == j ? used : 0u;
+          nrec_v += lane == j ? k : 0u;
+          wsync();
+        }
+      }
+      __syncthreads();
+      b_take_head(c, d, x, tid, n, q, Q, tmin, tminlen, rres);
+      if (w == 0) head_dec_fix(c, s, Q);
+    } else if (w == 0) {
+      err |= errq;
+    }
+    if (w == 0) q_store(c, s, l, q, lane, Q, true);
+    uint32_t nb = 0;
+    uint64_t bmin = ~0ull;
+    const uint32_t cnt = b_store_tail(c, s, l, q, d, x, tid, n, rres, &nb, &bmin);
+    if (tid == 0) {
+      if (tcap_of(c, q)) {
+        s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
+        s.tseal[l * 3 + q] = nb ? make_uint4(nb, (uint32_t)bmin, (uint32_t)(bmin >> 32), 0u) : kTSumEmpty;
+      }
+      unsigned long long* const fi = reinterpret_cast<unsigned long long*>(s.deep_n + kDeepFullItems);
+      atomicAdd(fi, (unsigned long long)n);  // the items the full-depth class held (rsf_gossip_deep_full_items)
+      atomicMax(fi + 1, (unsigned long long)n);
+    }
+    for (uint32_t i = tid; i < n; i += kDeepBlkThreads) d.st[i] = kDeepDead;  // clean for the next queue
+    __syncthreads();
+  }
+  if (w == 0) {  // the groups' counts and the member's bookkeeping (emit_run's)
+    if (oc && (BKT || nrec_v)) *oc = min(nrec_v, c.cap_t);
+    if (lane == 0) {
+      if (npend) {
+        s.p_cnt[l] = 0;
+        for (uint32_t q = 0; q < 3; ++q) s.q_next_seq[l * 3 + q] += (pc >> (8 * q)) & 0xFF;
+      }
+      if (drops) {
+        s.q_pruned[l] += drops;
+        err |= kErrQueue;
+      }
+      if (err) s.err[l] |= err;
+    }
+  }
+  __syncthreads();
+}
+
+// list 1 (the full depth, from the back of s.deep_ids) and list 4 (the members the smaller
+// classes re-listed) with one block per member, the grid striding over both
+template <bool BKT>
+__global__ void __launch_bounds__(kDeepBlkThreads) emit_deep_block_kernel(
+    GCfg c, GState s, const uint32_t* __restrict__ grp_key, const uint32_t* __restrict__ slot,
+    uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec, Buckets bk,
+    unsigned long long* __restrict__ total) {
+  __shared__ DeepWave<kDeepBig> d;
+  __shared__ DeepBlk x;
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
+  const uint32_t n_own = s.deep_n[1], n_re = s.deep_n[4], n_list = n_own + n_re;
+  if (blockIdx.x == 0 && tid == 0 && n_list) {
+    atomicAdd(total, (unsigned long long)n_list);
+    atomicAdd(total - kDeepClassOff + 1, (unsigned long long)n_list);  // (the full depth's class counter)
+  }
+  for (uint32_t i = tid; i < kDeepBig; i += kDeepBlkThreads) d.st[i] = kDeepDead;
+  __syncthreads();
+  const uint32_t* const ids = s.deep_ids + (c.n_loc * 3 - 1);
+  const uint32_t* const re = s.deep_ids + c.n_loc * 4;
+  for (uint32_t it = blockIdx.x; it < n_list; it += gridDim.x) {
+    const uint64_t l = it < n_own ? ids[-(int64_t)it] : re[it - n_own];
+    if (l >= c.n_loc) continue;  // (block-uniform)
+    const DeepPre pre = deep_pre(c, s, l, lane, grp_key, slot);  // (every wave reads the same)
+    deep_block_member<BKT>(c, s, l, tid, pre, cnt_s, out_val, out_dec, bk, d, x);
+  }
+}
+
 // ---- the QueueChecker's prune (check_stream_kernel) --------------------------------------
 // One block per listed (member, queue).  Pass 1 streams head and tail once and keeps only the
 // 8-B keys in LDS (live head keys first, then the tail's in index order); one select over the
