@@ -976,22 +976,21 @@ __global__ void __launch_bounds__(kWave) emit_deep_wave_kernel(GCfg c, GState s,
 #endif
 }
 
-// ---- the full-depth class: one 256-thread block per member ----------------------------------
-// The members whose queues need the full depth (a few hundred per round in the reference
-// regime: the re-listed ones and the largest queues) ran one wave each at one wave per CU (the
-// class holds 117 KB of LDS), each pass over their 5-9k items a long one-wave loop.  Here the
-// block's four waves share the streaming work -- the tail load, the key range, the radix
-// selects, the head gather and the tail store -- while the head's register work (q_load, the
-// picks, q_store and the rare per-peer fallback) stays with wave 0.  Always the whole queue (no
-// recent mode): the same items result; the tail's slot order and seal may differ from the
-// one-wave path's (neither is observable: the tail is unordered, its seal only a bound).
+// ---- the larger classes: one 256-thread block per member -------------------------------------
+// The members whose queues need the middle or the full depth ran one wave each at four waves
+// (middle) or one wave (full depth: 117 KB of LDS) per CU, each pass over their 1.2-9k items a
+// long one-wave loop.  Here the block's four waves share the streaming work -- the tail load,
+// the key range, the radix selects, the head gather and the tail store -- while the head's
+// register work (q_load, the picks, q_store and the rare per-peer fallback) stays with wave 0.
+// The same decisions as deep_wave_member (recent mode, re-listing); the tail's slot order may
+// differ from the one-wave path's (it is unordered: nothing reads its order).
 constexpr uint32_t kDeepBlkWaves = 4, kDeepBlkThreads = kDeepBlkWaves * kWave;
 struct DeepBlk {
   uint64_t r64[kDeepBlkWaves][4];  // per-wave partials of the block reductions
   uint32_t r32[kDeepBlkWaves][4];
   uint64_t hk[kDeepBlkWaves][kWave];  // the head gather: each wave's items, in its range's order
   uint32_t hr[kDeepBlkWaves][kWave];
-  uint32_t u[8];  // wave 0's broadcasts: [0..2] select digit / need / bucket count, [4] hn, [5] unsafe
+  uint32_t u[8];  // wave 0's broadcasts: [0..2] select digit / need / bucket count, [4] hn, [5] unsafe, [6] recent ok
 };
 __device__ __forceinline__ uint64_t b_min_u64(uint64_t v, DeepBlk& x, uint32_t tid) {
   v = wave_min_u64(v);
@@ -1220,15 +1219,15 @@ __device__ __forceinline__ void b_take_head(const GCfg& c, DeepWave<CAP>& d, Dee
     wsync();
   }
 }
-// w_store_tail with the block (t_lo = 0): per wave range, a count pass, one block scan, a write
-// pass -- the sealed group (keys > R) at [0, ns), the reserve after it.  Block-uniform result.
+// w_store_tail with the block, at tail[t_lo ...]: per wave range, a count pass, one block scan, a
+// write pass -- the sealed group (keys > R) first, the reserve after it.  Block-uniform result.
 template <uint32_t CAP>
 __device__ __forceinline__ uint32_t b_store_tail(const GCfg& c, const GState& s, uint64_t l, uint32_t q,
-                                                 DeepWave<CAP>& d, DeepBlk& x, uint32_t tid, uint32_t n, uint64_t R,
-                                                 uint32_t* nb, uint64_t* bmin) {
+                                                 DeepWave<CAP>& d, DeepBlk& x, uint32_t tid, uint32_t n, uint32_t t_lo,
+                                                 uint64_t R, uint32_t* nb, uint64_t* bmin) {
   const uint32_t lane = tid & (kWave - 1), w = tid / kWave;
-  uint4* const t = q && tcap_of(c, q) ? tail16(s, q) + l * tstride_of(c, q) : nullptr;
-  uint64_t* const t8 = q == 0 && c.tcap0 ? tail8(s, c, l) : nullptr;
+  uint4* const t = q && tcap_of(c, q) ? tail16(s, q) + l * tstride_of(c, q) + t_lo : nullptr;
+  uint64_t* const t8 = q == 0 && c.tcap0 ? tail8(s, c, l) + t_lo : nullptr;
   uint32_t lo, hi;
   b_wave_range(n, w, lo, hi);
   uint32_t ns = 0, nr = 0;
@@ -1275,11 +1274,69 @@ __device__ __forceinline__ uint32_t b_store_tail(const GCfg& c, const GState& s,
   return total;
 }
 
-template <bool BKT>
+// tail[t_lo, t_hi) of (l, q) into LDS items [at, ...) (live), every thread kDeepU items in flight
+template <uint32_t CAP>
+__device__ __forceinline__ void b_tail_load(const GCfg& c, const GState& s, uint64_t l, uint32_t q, DeepWave<CAP>& d,
+                                            uint32_t tid, uint32_t t_lo, uint32_t t_hi, uint32_t at, uint32_t nseq) {
+  const uint32_t tn = t_hi - t_lo;
+  for (uint32_t b = 0; b < tn; b += kDeepU * kDeepBlkThreads) {
+    uint4 e[kDeepU];
+    if (q == 0) {
+      const uint64_t* const t8 = tail8(s, c, l) + t_lo;
+      uint64_t v[kDeepU];
+#pragma unroll
+      for (uint32_t u = 0; u < kDeepU; ++u) {
+        const uint32_t i = b + u * kDeepBlkThreads + tid;
+        v[u] = i < tn ? t8[i] : 0ull;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kDeepU; ++u) e[u] = tail_unpack(c, v[u], nseq);
+    } else {
+      const uint4* const t16 = tail16(s, q) + l * tstride_of(c, q) + t_lo;
+#pragma unroll
+      for (uint32_t u = 0; u < kDeepU; ++u) {
+        const uint32_t i = b + u * kDeepBlkThreads + tid;
+        e[u] = i < tn ? t16[i] : make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kDeepU; ++u) {
+      const uint32_t i = b + u * kDeepBlkThreads + tid;
+      if (i < tn) {
+        d.key[at + i] = tlq_key(e[u].z & 0xFFFF, e[u].z >> 16, e[u].y);
+        d.rid[at + i] = e[u].x;
+        d.st[at + i] = kDeepLive;
+      }
+    }
+  }
+}
+// the sealed prefix tail[0, sm) into LDS after the n items there (w_load_sealed with the block);
+// returns the new item count
+template <uint32_t CAP>
+__device__ __forceinline__ uint32_t b_load_sealed(const GCfg& c, const GState& s, uint64_t l, uint32_t q,
+                                                  DeepWave<CAP>& d, uint32_t tid, uint32_t n, uint32_t sm,
+                                                  uint32_t nseq) {
+  for (uint32_t i = tid; i < n; i += kDeepBlkThreads)
+    if (d.st[i] == kDeepInHead) d.st[i] = kDeepLive;
+  b_tail_load(c, s, l, q, d, tid, 0u, sm, n, nseq);
+  __syncthreads();
+  return n + sm;
+}
+// recent mode could not decide and the class cannot hold the whole queue: nothing of the member
+// is stored yet; the LDS items are cleared and the member re-listed for the full depth (list 4)
+template <uint32_t CAP>
+__device__ __forceinline__ void b_relist_full(const GCfg& c, const GState& s, uint64_t l, uint32_t tid, uint32_t n,
+                                              DeepWave<CAP>& d) {
+  for (uint32_t i = tid; i < n; i += kDeepBlkThreads) d.st[i] = kDeepDead;
+  if (tid == 0) s.deep_ids[c.n_loc * 4 + atomicAdd(s.deep_n + 4, 1u)] = (uint32_t)l;
+  __syncthreads();
+}
+
+template <bool BKT, uint32_t CAP>
 __device__ __forceinline__ void deep_block_member(const GCfg& c, const GState& s, uint64_t l, uint32_t tid,
                                                   const DeepPre& pre, uint32_t* __restrict__ cnt_s,
                                                   uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec,
-                                                  const Buckets& bk, DeepWave<kDeepBig>& d, DeepBlk& x) {
+                                                  const Buckets& bk, DeepWave<CAP>& d, DeepBlk& x) {
   const uint32_t lane = tid & (kWave - 1), w = tid / kWave;
   const uint32_t pc = pre.pc, npend = pend_total(pc);
   const uint32_t gk = pre.gk, gs = pre.gs;
@@ -1310,8 +1367,19 @@ __device__ __forceinline__ void deep_block_member(const GCfg& c, const GState& s
     const uint32_t qi = shfl_u32(qinfo, (int)q);
     if (qi == 0 && nq == 0) continue;  // (block-uniform: every wave read the same first round trip)
     const uint32_t tc = qi >> 1, nseq = shfl_u32(qseq, (int)q);
-    if (c.qcap + tc + nq > kDeepBig) {  // (the tail's capacity is below it: an engine invariant broke)
-      if (tid == 0) atomicOr(s.err + l, (uint32_t)RSF_E_DEEP_INVARIANT);
+    // RECENT mode as deep_wave_member's: only the intent queue in use and a sealed tail prefix
+    const uint32_t sm = shfl_u32(pre.sm, (int)q);
+    const bool others_empty = q == 0 && shfl_u32(qinfo, 1) == 0 && shfl_u32(qinfo, 2) == 0 && ((pc >> 8) & 0xFFFF) == 0;
+    bool recent = others_empty && sm > 0 && sm <= tc && tc + nq <= tcap_of(c, q);
+    uint32_t t_lo = recent ? sm : 0u;
+    const bool fits_all = c.qcap + tc + nq <= CAP;
+    if (!recent && !fits_all) {
+      if (q == 0 && CAP < kDeepBig) {  // (emit_run listed it by the recent part's need)
+        if (tid == 0) s.deep_ids[c.n_loc * 4 + atomicAdd(s.deep_n + 4, 1u)] = (uint32_t)l;  // list 4
+        __syncthreads();
+        return;
+      }
+      if (tid == 0) atomicOr(s.err + l, (uint32_t)RSF_E_DEEP_INVARIANT);  // (the tail's capacity is below it)
       continue;
     }
     QRegs Q{kEmpty, 0, 0};
@@ -1328,38 +1396,9 @@ __device__ __forceinline__ void deep_block_member(const GCfg& c, const GState& s
     }
     __syncthreads();
     const uint32_t hn = x.u[4];
-    // the whole tail, every thread kDeepU items in flight
-    for (uint32_t b = 0; b < tc; b += kDeepU * kDeepBlkThreads) {
-      uint4 e[kDeepU];
-      if (q == 0) {
-        const uint64_t* const t8 = tail8(s, c, l);
-        uint64_t v[kDeepU];
-#pragma unroll
-        for (uint32_t u = 0; u < kDeepU; ++u) {
-          const uint32_t i = b + u * kDeepBlkThreads + tid;
-          v[u] = i < tc ? t8[i] : 0ull;
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kDeepU; ++u) e[u] = tail_unpack(c, v[u], nseq);
-      } else {
-        const uint4* const t16 = tail16(s, q) + l * tstride_of(c, q);
-#pragma unroll
-        for (uint32_t u = 0; u < kDeepU; ++u) {
-          const uint32_t i = b + u * kDeepBlkThreads + tid;
-          e[u] = i < tc ? t16[i] : make_uint4(0, 0, 0, 0);
-        }
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < kDeepU; ++u) {
-        const uint32_t i = b + u * kDeepBlkThreads + tid;
-        if (i < tc) {
-          d.key[hn + i] = tlq_key(e[u].z & 0xFFFF, e[u].z >> 16, e[u].y);
-          d.rid[hn + i] = e[u].x;
-          d.st[hn + i] = kDeepLive;
-        }
-      }
-    }
-    uint32_t n = hn + tc;
+    b_tail_load(c, s, l, q, d, tid, t_lo, tc, hn, nseq);
+    const uint32_t tn = tc - t_lo;
+    uint32_t n = hn + tn;
     if (n == 0 && nq == 0) continue;
     if (nq && w == 0) {  // the pending re-queues after them, in list order (transmits 0, the next seqs)
       uint32_t rank0 = 0;
@@ -1390,6 +1429,40 @@ __device__ __forceinline__ void deep_block_member(const GCfg& c, const GState& s
     uint64_t tmin, rres;
     uint32_t tminlen;
     b_take_head(c, d, x, tid, n, q, Q, tmin, tminlen, rres);
+    // recent mode: exact only if the head is full and below every sealed key; the sealed prefix
+    // stays in the tail, so the tail's bounds include the seal's
+    uint64_t sb = ~0ull;
+    if (recent) {
+      const uint4 se = s.tseal[l * 3 + q];
+      sb = ((uint64_t)se.z << 32) | se.y;
+      if (w == 0) {
+        const uint64_t hm = ballot(lane < c.qcap && Q.r != kEmpty);
+        bool ok = (uint32_t)__popcll(hm) == c.qcap;
+        if (ok) {
+          const int hl = 63 - __clzll((long long)hm);
+          const uint32_t tlh = shfl_u32(Q.tl, hl);
+          ok = tlq_key(tlh & 0xFFFF, tlh >> 16, shfl_u32(Q.sq, hl)) < sb;
+        }
+        if (lane == 0) x.u[6] = ok ? 1u : 0u;
+      }
+      __syncthreads();
+      if (!x.u[6]) {
+        if (!fits_all) {
+          b_relist_full(c, s, l, tid, n, d);
+          return;
+        }
+        // every item after all: the sealed prefix joins, the refill is redone
+        n = b_load_sealed(c, s, l, q, d, tid, n, t_lo, nseq);
+        recent = false;
+        t_lo = 0;
+        sb = ~0ull;
+        b_take_head(c, d, x, tid, n, q, Q, tmin, tminlen, rres);
+      }
+    }
+    if (recent) {
+      tmin = sb < tmin ? sb : tmin;
+      tminlen = min(tminlen, s.tsum[l * 3 + q].y);  // (a bound over the whole tail: covers the sealed part)
+    }
     const uint32_t used_0 = used_v, nrec_0 = nrec_v;
     uint32_t errq = 0;
     if (w == 0) {
@@ -1405,6 +1478,17 @@ __device__ __forceinline__ void deep_block_member(const GCfg& c, const GState& s
     }
     __syncthreads();
     const bool unsafe = x.u[5] != 0;
+    if (unsafe && recent) {
+      if (!fits_all) {
+        b_relist_full(c, s, l, tid, n, d);
+        return;
+      }
+      // the head cannot decide even now: every item (the sealed prefix joins) for the fallback
+      n = b_load_sealed(c, s, l, q, d, tid, n, t_lo, nseq);
+      recent = false;
+      t_lo = 0;
+      sb = ~0ull;
+    }
     if (unsafe) {
       // the head still cannot decide: get_broadcasts over every item, peer by peer (wave 0; rare)
       if (w == 0) {
@@ -1468,15 +1552,19 @@ __device__ __forceinline__ void deep_block_member(const GCfg& c, const GState& s
     if (w == 0) q_store(c, s, l, q, lane, Q, true);
     uint32_t nb = 0;
     uint64_t bmin = ~0ull;
-    const uint32_t cnt = b_store_tail(c, s, l, q, d, x, tid, n, rres, &nb, &bmin);
+    const uint32_t cnt = t_lo + b_store_tail(c, s, l, q, d, x, tid, n, t_lo, rres, &nb, &bmin);
     if (tid == 0) {
       if (tcap_of(c, q)) {
         s.tsum[l * 3 + q] = cnt ? make_uint4(cnt, tminlen, (uint32_t)tmin, (uint32_t)(tmin >> 32)) : kTSumEmpty;
-        s.tseal[l * 3 + q] = nb ? make_uint4(nb, (uint32_t)bmin, (uint32_t)(bmin >> 32), 0u) : kTSumEmpty;
+        // sealed: the kept prefix (recent mode) and the group written above the reserve
+        const uint64_t b = bmin < sb ? bmin : sb;
+        s.tseal[l * 3 + q] = t_lo + nb ? make_uint4(t_lo + nb, (uint32_t)b, (uint32_t)(b >> 32), 0u) : kTSumEmpty;
       }
-      unsigned long long* const fi = reinterpret_cast<unsigned long long*>(s.deep_n + kDeepFullItems);
-      atomicAdd(fi, (unsigned long long)n);  // the items the full-depth class held (rsf_gossip_deep_full_items)
-      atomicMax(fi + 1, (unsigned long long)n);
+      if (CAP == kDeepBig) {  // the items the full-depth class held (rsf_gossip_deep_full_items)
+        unsigned long long* const fi = reinterpret_cast<unsigned long long*>(s.deep_n + kDeepFullItems);
+        atomicAdd(fi, (unsigned long long)n);
+        atomicMax(fi + 1, (unsigned long long)n);
+      }
     }
     for (uint32_t i = tid; i < n; i += kDeepBlkThreads) d.st[i] = kDeepDead;  // clean for the next queue
     __syncthreads();
@@ -1498,30 +1586,32 @@ __device__ __forceinline__ void deep_block_member(const GCfg& c, const GState& s
   __syncthreads();
 }
 
-// list 1 (the full depth, from the back of s.deep_ids) and list 4 (the members the smaller
-// classes re-listed) with one block per member, the grid striding over both
-template <bool BKT>
+// emit_deep_wave_kernel's lists with one block per member: list 3 (the middle class), or list 1
+// (the full depth, from the back of s.deep_ids) followed by list 4 (the members the smaller
+// classes re-listed); the grid strides over them
+template <bool BKT, uint32_t CAP>
 __global__ void __launch_bounds__(kDeepBlkThreads) emit_deep_block_kernel(
     GCfg c, GState s, const uint32_t* __restrict__ grp_key, const uint32_t* __restrict__ slot,
     uint32_t* __restrict__ cnt_s, uint32_t* __restrict__ out_val, uint32_t* __restrict__ out_dec, Buckets bk,
-    unsigned long long* __restrict__ total) {
-  __shared__ DeepWave<kDeepBig> d;
+    uint32_t list, unsigned long long* __restrict__ total) {
+  __shared__ DeepWave<CAP> d;
   __shared__ DeepBlk x;
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
-  const uint32_t n_own = s.deep_n[1], n_re = s.deep_n[4], n_list = n_own + n_re;
+  const uint32_t n_own = s.deep_n[list], n_re = list == 1 ? s.deep_n[4] : 0u, n_list = n_own + n_re;
   if (blockIdx.x == 0 && tid == 0 && n_list) {
     atomicAdd(total, (unsigned long long)n_list);
-    atomicAdd(total - kDeepClassOff + 1, (unsigned long long)n_list);  // (the full depth's class counter)
+    atomicAdd(list == 3 ? total + 1 : total - kDeepClassOff + list, (unsigned long long)n_list);  // per class
   }
-  for (uint32_t i = tid; i < kDeepBig; i += kDeepBlkThreads) d.st[i] = kDeepDead;
+  for (uint32_t i = tid; i < CAP; i += kDeepBlkThreads) d.st[i] = kDeepDead;
   __syncthreads();
-  const uint32_t* const ids = s.deep_ids + (c.n_loc * 3 - 1);
+  const uint32_t* const ids = list == 1 ? s.deep_ids + (c.n_loc * 3 - 1) : s.deep_ids + c.n_loc * 3;
+  const int64_t dir = list == 1 ? -1 : 1;
   const uint32_t* const re = s.deep_ids + c.n_loc * 4;
   for (uint32_t it = blockIdx.x; it < n_list; it += gridDim.x) {
-    const uint64_t l = it < n_own ? ids[-(int64_t)it] : re[it - n_own];
+    const uint64_t l = it < n_own ? ids[dir * (int64_t)it] : re[it - n_own];
     if (l >= c.n_loc) continue;  // (block-uniform)
     const DeepPre pre = deep_pre(c, s, l, lane, grp_key, slot);  // (every wave reads the same)
-    deep_block_member<BKT>(c, s, l, tid, pre, cnt_s, out_val, out_dec, bk, d, x);
+    deep_block_member<BKT, CAP>(c, s, l, tid, pre, cnt_s, out_val, out_dec, bk, d, x);
   }
 }
 
