@@ -1262,12 +1262,6 @@ __global__ void __launch_bounds__(256) grp_index_kernel(const uint32_t* __restri
 // members in the reference regime, whose picks span millions of rumor ids (the merge looking
 // them up itself, a separate pass per slot or per group: all slower).
 constexpr uint32_t kMaxRuns = 8;
-#ifndef RSF_DEEP_FULL_BLOCK
-#define RSF_DEEP_FULL_BLOCK 1  // the full-depth class: one 256-thread block per member (0: one wave, emit_deep_wave_kernel)
-#endif
-#ifndef RSF_DEEP_MID_BLOCK
-#define RSF_DEEP_MID_BLOCK 1  // the middle class likewise
-#endif
 struct Buckets {
   const uint32_t* base;  // receive buffer (RUNS merge); emission writes through `send`
   uint32_t* send;        // send buffer (emission into buckets)
@@ -3201,24 +3195,15 @@ int rsf_gossip_create(rsf_gossip** out, const rsf_gossip_cfg* cfg, int device) {
     g->merge_blocks = (unsigned)std::max(1, per_cu * cus);
     if (c.deep) {
       int dpc = 0, dpb = 0, dpk = 0, dpt = 0, dpm = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpc, emit_deep_wave_kernel<false, kDeepSmall>, kWave, 0) !=
+      if (
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpc, emit_deep_wave_kernel<false, kDeepSmall>, kWave, 0) !=
               hipSuccess ||
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpt, emit_deep_wave_kernel<false, kDeepTiny>, kWave, 0) !=
               hipSuccess ||
-#if RSF_DEEP_MID_BLOCK
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpm, emit_deep_block_kernel<false, kDeepMid>, kDeepBlkThreads, 0) !=
               hipSuccess ||
-#else
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpm, emit_deep_wave_kernel<false, kDeepMid>, kWave, 0) !=
-              hipSuccess ||
-#endif
-#if RSF_DEEP_FULL_BLOCK
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpb, emit_deep_block_kernel<false, kDeepBig>, kDeepBlkThreads, 0) !=
               hipSuccess ||
-#else
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpb, emit_deep_wave_kernel<false, kDeepBig>, kWave, 0) !=
-              hipSuccess ||
-#endif
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&dpk, check_stream_kernel, kDeepThreads, 0) != hipSuccess)
         return fail(rsf::set_error(RSF_ERR_HIP, "occupancy query failed"));
       g->deep_blocks = (unsigned)std::max(1, dpc * cus);
@@ -3636,20 +3621,10 @@ static int launch_emit(rsf_gossip* g, dim3 egrid, const Buckets& bk) {
                        g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 2u, g->d_counters + 55);
     hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepSmall>), dim3(g->deep_blocks), dim3(kWave), 0, st, c, g->s,
                        g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 0u, g->d_counters + 55);
-#if RSF_DEEP_MID_BLOCK
     hipLaunchKernelGGL((emit_deep_block_kernel<BKT, kDeepMid>), dim3(g->deep_blocks_mid), dim3(kDeepBlkThreads), 0, st, c,
                        g->s, g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 3u, g->d_counters + 55);
-#else
-    hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepMid>), dim3(g->deep_blocks_mid), dim3(kWave), 0, st, c, g->s,
-                       g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 3u, g->d_counters + 55);
-#endif
-#if RSF_DEEP_FULL_BLOCK
     hipLaunchKernelGGL((emit_deep_block_kernel<BKT, kDeepBig>), dim3(g->deep_blocks_big), dim3(kDeepBlkThreads), 0, st, c,
                        g->s, g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 1u, g->d_counters + 55);
-#else
-    hipLaunchKernelGGL((emit_deep_wave_kernel<BKT, kDeepBig>), dim3(g->deep_blocks_big), dim3(kWave), 0, st, c, g->s,
-                       g->grp_key, g->grp_slot, g->grp_cnt, g->stage_val, g->stage_dec, bk, 1u, g->d_counters + 55);
-#endif
   } else if (c.qcap == kWave) {
     hipLaunchKernelGGL((emit_kernel<BKT, true>), egrid, eb, 0, st, c, g->s, g->grp_key, g->grp_slot, g->grp_cnt,
                        g->stage_val, g->stage_dec, bk);

@@ -1586,9 +1586,9 @@ __device__ __forceinline__ void deep_block_member(const GCfg& c, const GState& s
   __syncthreads();
 }
 
-// emit_deep_wave_kernel's lists with one block per member: list 3 (the middle class), or list 1
-// (the full depth, from the back of s.deep_ids) followed by list 4 (the members the smaller
-// classes re-listed); the grid strides over them
+// emit_deep_wave_kernel's lists with one block per member: list 2 / 0 / 3 (the tiny / small /
+// middle class), or list 1 (the full depth, from the back of s.deep_ids) followed by list 4 (the
+// members the smaller classes re-listed); the grid strides over them
 template <bool BKT, uint32_t CAP>
 __global__ void __launch_bounds__(kDeepBlkThreads) emit_deep_block_kernel(
     GCfg c, GState s, const uint32_t* __restrict__ grp_key, const uint32_t* __restrict__ slot,
@@ -1604,7 +1604,8 @@ __global__ void __launch_bounds__(kDeepBlkThreads) emit_deep_block_kernel(
   }
   for (uint32_t i = tid; i < CAP; i += kDeepBlkThreads) d.st[i] = kDeepDead;
   __syncthreads();
-  const uint32_t* const ids = list == 1 ? s.deep_ids + (c.n_loc * 3 - 1) : s.deep_ids + c.n_loc * 3;
+  const uint32_t* const ids = list == 1 ? s.deep_ids + (c.n_loc * 3 - 1)
+                                        : s.deep_ids + (list == 2 ? c.n_loc : list == 3 ? c.n_loc * 3 : 0ull);
   const int64_t dir = list == 1 ? -1 : 1;
   const uint32_t* const re = s.deep_ids + c.n_loc * 4;
   for (uint32_t it = blockIdx.x; it < n_list; it += gridDim.x) {
