@@ -437,8 +437,7 @@ int rsf_gossip_check_runs(rsf_gossip* g, int* ok);
  * world size) and returns the send and receive buffers, `world` buckets of bucket_bytes
  * each, device memory.  round_emit_buckets emits straight into the send buckets (each
  * holds its shard's (sender, peer) groups sorted by receiver: a header with the group
- * count, the receivers, record counts and rumor ids; the record decorations are looked
- * up on the receive side from the replicated rumor table).  The caller moves bucket w of
+ * count, the receivers, record counts, rumor ids and the records' decorations).  The caller moves bucket w of
  * every rank r to slot r of rank w's receive buffer (source-rank order), for every w other
  * than r itself -- a shard's own bucket is read from its send buffer, so its receive slot is
  * never read and need not be filled (grouped point-to-point sends/receives, or an

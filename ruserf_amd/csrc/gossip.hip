@@ -2685,10 +2685,10 @@ __global__ void __launch_bounds__(256) check_queues_kernel(GCfg c, GState s, uin
       atomicMax(&bh[3 * (kOccBins + 1) + q], n);
       if (n) atomicAdd(&bst[q], (unsigned long long)n);
       if (n >= warn) atomicAdd(&bst[3 + q], 1ull);
-      if (n > mx) {
-        if (tcap_of(c, q)) s.deep_ids[atomicAdd(s.deep_n, 1u)] = (uint32_t)(l * 3 + q);
-        atomicAdd(&bst[6 + q], (unsigned long long)(n - mx));
-      }
+      if (n > mx) atomicAdd(&bst[6 + q], (unsigned long long)(n - mx));
+      // the deep queues' entries for check_stream_kernel at fixed places (kEmpty: under the
+      // max): one atomic per listed queue on a single counter took most of this kernel's time
+      if (tcap_of(c, q)) s.deep_ids[wi * deep_queues(c) + deep_rank(c, q)] = n > mx ? (uint32_t)(l * 3 + q) : kEmpty;
     }
 #pragma unroll
     for (uint32_t q = 0; q < 3; ++q) {
@@ -4229,7 +4229,6 @@ static int check_launch(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_qu
     RSF_HIP(hipMemsetAsync(g->occ_hist, 0, hist_words * 4, rs));
     RSF_HIP(hipMemsetAsync(g->d_counters + 40, 0, 9 * 8, rs));
   }
-  if (c.deep) RSF_HIP(hipMemsetAsync(g->s.deep_n, 0, kDeepLists * 4, rs));
   hipLaunchKernelGGL(check_queues_kernel,
                      dim3((unsigned)std::min<uint64_t>(1024, grid1(std::max<uint64_t>(1, phase_count(c, period, phase)),
                                                                    256 / kWave))),
@@ -4237,8 +4236,9 @@ static int check_launch(rsf_gossip* g, uint32_t max_queue_depth, uint32_t min_qu
                      phase);
   RSF_HIP(hipGetLastError());
   if (c.deep) {  // the deep queues over the max: the smallest max keys of head and tail kept
+    const uint64_t n_list = phase_count(c, period, phase) * deep_queues(c);
     hipLaunchKernelGGL(check_stream_kernel, dim3(g->deep_check_blocks), dim3(kDeepThreads), 0, rs, c, g->s, max_depth,
-                       qmax);
+                       qmax, (uint32_t)n_list);
     RSF_HIP(hipGetLastError());
   }
   return RSF_OK;

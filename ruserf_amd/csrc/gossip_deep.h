@@ -1755,20 +1755,23 @@ __device__ void lds_select3(const uint64_t* __restrict__ keys, uint32_t n, Check
 // emission then cannot decide from the head and the member takes the deferred whole-queue path,
 // which refills the head with the queue's smallest keys (emit_deep_wave_kernel).
 __global__ void __launch_bounds__(kDeepThreads) check_stream_kernel(GCfg c, GState s, uint32_t max_depth,
-                                                                    const uint32_t* __restrict__ qmax) {
+                                                                    const uint32_t* __restrict__ qmax, uint32_t n_list) {
   __shared__ CheckLds d;
   __shared__ uint64_t keys[kDeepItems];
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
-  const uint32_t n_list = *s.deep_n;
 #if RSF_DEEP_PROF
   uint64_t pf[5] = {0, 0, 0, 0, 0}, pc = 0;
 #define RSF_CK(i) const uint64_t ck##i = clock64()
 #else
 #define RSF_CK(i)
 #endif
+  // check_queues_kernel's entries at fixed places, kEmpty for a queue under its max; the next
+  // entry is read while this one is worked on
+  uint32_t e_next = blockIdx.x < n_list ? s.deep_ids[blockIdx.x] : kEmpty;
   for (uint32_t it = blockIdx.x; it < n_list; it += gridDim.x) {
     RSF_CK(0);
-    const uint32_t e = s.deep_ids[it];
+    const uint32_t e = e_next;
+    e_next = it + gridDim.x < n_list ? s.deep_ids[it + gridDim.x] : kEmpty;
     const uint64_t l = e / 3;
     const uint32_t q = e % 3;
     if (l >= c.n_loc || !tcap_of(c, q)) continue;

@@ -168,6 +168,11 @@ constexpr uint32_t kDeepFullItems = 8;
 constexpr uint32_t kTailSlack = 192;  // tail row room past its capacity: one emission's spills (2 x 64) + 64
 // per-queue deep-queue fields by a select on q
 RSF_HD uint32_t tcap_of(const GCfg& c, uint32_t q) { return q == 0 ? c.tcap0 : q == 1 ? c.tcap1 : c.tcap2; }
+// the deep queues (those with a tail): how many, and queue q's place among them
+RSF_HD uint32_t deep_queues(const GCfg& c) { return (c.tcap0 ? 1u : 0u) + (c.tcap1 ? 1u : 0u) + (c.tcap2 ? 1u : 0u); }
+RSF_HD uint32_t deep_rank(const GCfg& c, uint32_t q) {
+  return (q > 0 && c.tcap0 ? 1u : 0u) + (q > 1 && c.tcap1 ? 1u : 0u);
+}
 RSF_HD uint32_t tstride_of(const GCfg& c, uint32_t q) { return q == 0 ? c.tstride0 : q == 1 ? c.tstride1 : c.tstride2; }
 // the query / event queues' 16-B tails (q = 1, 2); the intent queue's is s.tail0 (tail8)
 RSF_HD uint4* tail16(const GState& s, uint32_t q) { return q == 1 ? s.tail1 : s.tail2; }

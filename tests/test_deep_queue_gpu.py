@@ -312,8 +312,8 @@ def test_configs3_100k_deep_queues_bit_exact():
 
 @pytest.mark.parametrize("checker", [False, True])
 def test_deep_two_shards_buckets_equal_one_context(checker):
-    """The multi-GPU bucket emission with deep queues (emit_kernel and emit_deep_wave_kernel writing
-    into the destination buckets): two shard contexts on one GPU, the exchange by hand,
+    """The multi-GPU bucket emission with deep queues (emit_kernel_deep and the deferred classes
+    writing into the destination buckets): two shard contexts on one GPU, the exchange by hand,
     equal to one context after every round; with `checker`, the in-round staggered ticks too
     (phases by global member id, so each shard ticks its own members of that phase)."""
     import torch
@@ -373,21 +373,24 @@ def test_deep_two_shards_buckets_equal_one_context(checker):
         e.close()
 
 
-def test_deep_long_queues_all_capacity_classes():
+@pytest.mark.parametrize("depth,rounds", [(2500, 34), (1400, 40), (2600, 90)])
+def test_deep_long_queues_all_capacity_classes(depth, rounds):
     """Queues that grow past the deferred path's two smaller LDS capacities (832 and 1 216
     items): a user-event flood (100 per round) that the retransmit limit retires far slower
     than it arrives, an event buffer wide enough to accept every event, and a rumor ring that
     does not wrap, so the event queues of every member grow by tens of items per round.  Members
-    deferred at every size class take emit_deep_wave_kernel<832>, <1216> and <4288>; bit-exact
-    against the oracle every round, with the largest queue past 1 216 items by the end."""
-    n, rounds = 300, 34
+    deferred at every size class take emit_deep_wave_kernel<832>, <1216> and the block classes
+    (emit_deep_block_kernel<2432> and the full depth); bit-exact against the oracle every third
+    round, with the largest queue past 1 216 items by the end.  Depth 2 500: nothing pruned;
+    1 400 and 2 600: the event queues reach their depth inside the middle class and the full
+    depth, so the block classes' bounded prune runs (drops counted, equal to the oracle's)."""
+    n = 300
     subj, acts, ml = W.churn_workload(n, rounds, churn=0.01, events_per_round=100, queries_per_round=0, seed=77)
     s = len(subj)
-    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=64, queue_depth=(2500, 2500, 2500), gossip_limit=1000,
-                         gossip_overhead=2, retransmit_mult=4, max_rumors=1 << 13, event_buffer_size=4096,
+    cfg = G.GossipConfig(n_members=n, n_subjects=s, queue_cap=64, queue_depth=(depth, depth, depth), gossip_limit=1000,
+                         gossip_overhead=2, retransmit_mult=4, max_rumors=1 << 17, event_buffer_size=10000,
                          query_buffer_size=64, slot_k=16, max_refute=2)
     g, w = pair(cfg, subj, W.initial_views(s))
-    deep0 = 0
     for t in range(rounds):
         g.round(t, ml[t], acts[t])
         H.oracle_round(w, t, ml[t], acts[t], threads=16)
@@ -395,8 +398,15 @@ def test_deep_long_queues_all_capacity_classes():
             same(g, w, f"round {t}")
     assert H.world_width(w) > 1216  # queues past the two smaller capacity classes
     total, _ = g.deep_stats()
-    assert total > deep0
-    assert int(g.pruned().sum()) == 0
+    assert total > 0
+    cls = g.deep_class_stats()
+    assert cls[2] > 0, cls  # the middle class ran
+    if depth == 2500:
+        assert int(g.pruned().sum()) == 0
+    else:
+        assert int(g.pruned().sum()) > 0  # the bounded prune at the depth ran
+    if depth == 2600:
+        assert cls[3] > 0, cls  # the full depth ran
     g.close()
     L.orc_world_free(C.byref(w))
 
