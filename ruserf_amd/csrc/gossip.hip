@@ -1211,7 +1211,9 @@ __global__ void __launch_bounds__(256) grp_index_kernel(const uint32_t* __restri
                                                         const uint32_t* __restrict__ id_s, uint64_t n, uint64_t lo,
                                                         uint32_t* __restrict__ slot, uint32_t* __restrict__ seg_start,
                                                         uint32_t* __restrict__ seg_end,
-                                                        const uint32_t* __restrict__ wstart = nullptr, uint32_t per = 0) {
+                                                        const uint32_t* __restrict__ wstart = nullptr, uint32_t per = 0,
+                                                        uint32_t* __restrict__ bkt_keys = nullptr, uint64_t bstride = 0,
+                                                        uint32_t gcap = 0) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t key = key_s[i];
@@ -1223,6 +1225,9 @@ __global__ void __launch_bounds__(256) grp_index_kernel(const uint32_t* __restri
     // bucket capacity (rsf_gossip_bucket_buffers), so emission skips it instead of wrapping
     const uint64_t place = (uint64_t)i - wstart[w];
     slot[id_s[i]] = (w << kBktWShift) | (uint32_t)(place < kBktIdxMask ? place : kBktIdxMask);
+    // the bucket's receiver keys, in sorted order: coalesced here instead of scattered from
+    // the emission (one 4-B write per group into a random sector)
+    if (place < gcap) bkt_keys[(uint64_t)w * bstride + place] = key;
     return;
   }
   slot[id_s[i]] = (uint32_t)i;
@@ -1333,17 +1338,13 @@ __device__ __forceinline__ void emit_load(const GCfg& c, const GState& s, const 
   e.gk = lane < c.fanout ? grp_key[l * c.fanout + lane] : kSentinel;
   e.gs = lane < c.fanout ? slot[l * c.fanout + lane] : 0u;
 }
-// buckets: lanes < np write their group's receiver key (and, when nothing will be emitted,
-// its zero count) into the destination bucket -- the bucket headers come from emission
-// itself, no separate pass over the sorted groups
-__device__ __forceinline__ void bkt_group_keys(const Buckets& bk, uint32_t lane, uint32_t np, uint32_t gk, uint32_t gs,
-                                               bool zero_count) {
+// buckets: when nothing will be emitted, lanes < np write their group's zero count into the
+// destination bucket (the groups' receiver keys are written by grp_index_kernel, in sorted order)
+__device__ __forceinline__ void bkt_zero_counts(const Buckets& bk, uint32_t lane, uint32_t np, uint32_t gs) {
   if (lane >= np) return;
   const uint32_t w = gs >> kBktWShift, idx = gs & kBktIdxMask;  // pre-encoded by grp_index_kernel
   if (idx >= bk.gcap) return;  // over the bucket capacity: flagged by the bounds kernel
-  uint32_t* b = bk.send + (uint64_t)w * bk.stride_u32;
-  b[bk.keys_off + idx] = gk;
-  if (zero_count) b[bk.cnt_off + idx] = 0u;
+  bk.send[(uint64_t)w * bk.stride_u32 + bk.cnt_off + idx] = 0u;
 }
 // DEEP (queues with an HBM tail): the emission runs on the heads as below; it is committed
 // only if every pick was decided by the head alone (q_pick_peers' checks against the tails'
@@ -1375,7 +1376,7 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
              ne2 = shfl_u32(e.head, 2) != kEmpty || ((pc >> 16) & 0xFF) || tc2;
   // no peers: nothing is sent, and the pending re-queues wait for the next emission
   if (np == 0 || !(ne0 || ne1 || ne2)) {
-    if (BKT) bkt_group_keys(bk, lane, np, e.gk, e.gs, true);
+    if (BKT) bkt_zero_counts(bk, lane, np, e.gs);
     return;
   }
   // (three named tails, not an array: a dynamically indexed array goes to scratch)
@@ -1399,13 +1400,9 @@ __device__ __forceinline__ void emit_run(const GCfg& c, const GState& s, uint64_
   // the pending re-queues (merge_kernel's and the originations' since the last emission)
   PendRegs pr;
   pend_load(s, l, lane, npend, pr);
-  // buckets: each peer's destination shard and that bucket's first group (same round trip)
-  uint32_t wdst = 0;  // (bucket mode: the slot word holds the shard and the bucket place)
-  if (BKT && lane < np) {
-    wdst = e.gs >> kBktWShift;
-    const uint32_t idx = e.gs & kBktIdxMask;
-    if (idx < bk.gcap) bk.send[(uint64_t)wdst * bk.stride_u32 + bk.keys_off + idx] = e.gk;
-  }
+  // buckets: each peer's destination shard (the slot word holds the shard and the bucket place)
+  uint32_t wdst = 0;
+  if (BKT && lane < np) wdst = e.gs >> kBktWShift;
   if (ne1) q_load(c, s, l, 1, lane, Q1);
   if (ne2) q_load(c, s, l, 2, lane, Q2);
 #if RSF_EMIT_PROF
@@ -1582,7 +1579,7 @@ __device__ __forceinline__ void emit_run4(const GCfg& c, const GState& s, const 
   const bool ne0 = shfl_u32(head, 0) != kEmpty || (pc & 0xFF), ne1 = shfl_u32(head, 1) != kEmpty || ((pc >> 8) & 0xFF),
              ne2 = shfl_u32(head, 2) != kEmpty || ((pc >> 16) & 0xFF);
   if (np == 0 || !(ne0 || ne1 || ne2)) {
-    if (BKT) bkt_group_keys(bk, lane, np, gk, gs, true);
+    if (BKT) bkt_zero_counts(bk, lane, np, gs);
     return;
   }
   bool d0 = false, d1 = false, d2 = false;
@@ -1590,11 +1587,7 @@ __device__ __forceinline__ void emit_run4(const GCfg& c, const GState& s, const 
   PendRegs pr;
   pend_load(s, l, lane, npend, pr);
   uint32_t wdst = 0;
-  if (BKT && lane < np) {
-    wdst = gs >> kBktWShift;
-    const uint32_t idx = gs & kBktIdxMask;
-    if (idx < bk.gcap) bk.send[(uint64_t)wdst * bk.stride_u32 + bk.keys_off + idx] = gk;
-  }
+  if (BKT && lane < np) wdst = gs >> kBktWShift;
   Q4 Q0, Q1, Q2;
 #pragma unroll
   for (uint32_t k = 0; k < kQK; ++k) {
@@ -2802,10 +2795,12 @@ __global__ void __launch_bounds__(256) bucket_index_kernel(Buckets bk, uint64_t 
                                                            uint32_t* __restrict__ rstart, uint32_t* __restrict__ rend,
                                                            unsigned long long* __restrict__ merged,
                                                            unsigned long long* __restrict__ flags) {
-  const uint64_t n = (uint64_t)bk.n_runs * bk.gcap;
+  // 32-bit indices: n_runs <= 8 buckets of < 2^26 groups (checked at rsf_gossip_bucket_buffers);
+  // the 64-bit division per group was most of this kernel's time
+  const uint32_t n = bk.n_runs * bk.gcap;
   uint64_t sum = 0;
-  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t r = (uint32_t)(t / bk.gcap), i = (uint32_t)(t % bk.gcap);
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    const uint32_t r = t / bk.gcap, i = t - r * bk.gcap;
     const uint32_t* b = bk.run(r);
     const uint32_t ng = b[0];
     if (i >= ng) continue;
@@ -3696,7 +3691,8 @@ static int emit_and_sort(rsf_gossip* g, uint32_t round, bool local, uint32_t wor
     hipLaunchKernelGGL(bucket_bounds_kernel, dim3(1), dim3(64), 0, st, (const uint32_t*)g->grp_key_s, ng, bk.per, world,
                        g->d_wstart, g->bkt_send, bk.stride_u32, bk.gcap, g->d_counters + 58);
     hipLaunchKernelGGL(grp_index_kernel, dim3(grid1(ng)), dim3(256), 0, st, g->grp_key_s, g->grp_id_s, ng, c.lo,
-                       g->grp_slot, nullptr, nullptr, (const uint32_t*)g->d_wstart, (uint32_t)bk.per);
+                       g->grp_slot, nullptr, nullptr, (const uint32_t*)g->d_wstart, (uint32_t)bk.per,
+                       g->bkt_send + bk.keys_off, bk.stride_u32, bk.gcap);
     RSF_HIP(hipGetLastError());
     RSF_DBG_SYNC(st, "grp_index_kernel");
     mark(g, 2);
