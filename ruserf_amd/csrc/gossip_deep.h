@@ -917,9 +917,10 @@ __device__ __forceinline__ void deep_wave_member(const GCfg& c, const GState& s,
 #undef RSF_DEEP_T
 }
 
-// the members emit_run deferred: list 0 (those that fit kDeepSmall items per queue) from the
-// front of s.deep_ids, list 1 (the rest) from its back; one wave per member, the grid striding
-// over the list so every wave reaches its end
+// the members emit_run deferred to the two smaller classes, one wave per member: list 2 (those
+// that fit kDeepTiny items) and list 0 (kDeepSmall), the grid striding over the list so every
+// wave reaches its end.  (The middle class and the full depth run one block per member,
+// emit_deep_block_kernel below; this kernel still takes any list, as it did before them.)
 template <bool BKT, uint32_t CAP>
 __global__ void __launch_bounds__(kWave) emit_deep_wave_kernel(GCfg c, GState s, const uint32_t* __restrict__ grp_key,
                                                               const uint32_t* __restrict__ slot,
