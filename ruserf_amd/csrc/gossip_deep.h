@@ -16,9 +16,15 @@ namespace {
 
 constexpr uint32_t kDeepThreads = 256;
 // tail items a refill leaves unsealed past the head (w_store_tail, check_stream_kernel)
-constexpr uint32_t kDeepReserve = 128;
+#ifndef RSF_DEEP_RESERVE
+#define RSF_DEEP_RESERVE 128  // 64 and 256 measured slower (profiles/r06/ab_tunables/)
+#endif
+constexpr uint32_t kDeepReserve = RSF_DEEP_RESERVE;
 // items per thread / lane in flight in the tail loads and LDS scans
-constexpr uint32_t kDeepU = 8;
+#ifndef RSF_DEEP_U
+#define RSF_DEEP_U 4  // 4 and 6: emission phase -0.035 ms against 8 and 2, same box x3 (profiles/r06/ab_deep_u/)
+#endif
+constexpr uint32_t kDeepU = RSF_DEEP_U;
 constexpr uint32_t kDeepWaves = kDeepThreads / kWave;
 enum : uint8_t { kDeepDead = 0, kDeepLive = 1, kDeepPicked = 2 };
 
@@ -697,7 +703,7 @@ __device__ __forceinline__ void deep_wave_member(const GCfg& c, const GState& s,
       }
       b += kDeepU * kWave;
       if (b >= tn) break;
-      tail_chunk<kDeepU>(c, s, l, q, t_lo + b, tc, lane, nseq, e);  // the next kDeepU * 64 (queues past 512 items)
+      tail_chunk<kDeepU>(c, s, l, q, t_lo + b, tc, lane, nseq, e);  // the next kDeepU * 64 (queues past kDeepU * 64 items)
     }
     uint32_t n = hn + tn;
     if (n == 0 && nq == 0) continue;
